@@ -1,0 +1,421 @@
+// attention.hip — paged GQA attention for the LLM worker (K4/K5 of SURVEY §2.6).
+//
+// KV cache layout (written by rope_kv.hip): [num_blocks][Hkv][block_size][D] bf16.
+//
+// decode  (one query token per sequence): memory-bound split-K over context partitions. A 256-thread
+//   workgroup owns (sequence, kv-head, partition); D/8 lanes cover one cached position with 16-byte
+//   loads, so a wave streams 64*16 B of K (then V) per step; all G = Hq/Hkv query heads of the kv
+//   head are scored from the same K/V bytes (GQA packing: K/V are read once per kv head, not per q
+//   head). Online softmax in the log2 domain; partitions merge in attn_decode_reduce.
+// prefill (varlen, causal, paged context incl. cached prefix): flash-attention forward on MFMA
+//   16x16x32 bf16. A workgroup holds 16 query rows x up to 8 query heads of one kv head (one wave per
+//   head) so every K/V tile staged in LDS is reused by all heads of the group. K is stored
+//   XOR-swizzled for conflict-free ds_read_b128 B-fragments; V is read with ds_read_b64_tr_b16
+//   (hardware transpose) from a region-swizzled image; P goes register -> LDS -> A-fragment.
+#include "mx_common.h"
+
+#define LOG2E 1.4426950408889634f
+
+// ------------------------------------------------------------------------------------------------
+template <int D, int G>
+__global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restrict__ q, int q_stride,
+                                                          const bf16_t* __restrict__ kc,
+                                                          const bf16_t* __restrict__ vc,
+                                                          const int* __restrict__ block_tables, int bt_stride,
+                                                          const int* __restrict__ seq_lens, int Hkv, int bs,
+                                                          float scale, int part_size, int n_parts,
+                                                          bf16_t* __restrict__ out, int out_stride,
+                                                          float2* __restrict__ part_ml, float* __restrict__ part_o) {
+    constexpr int LPP = D / 8;        // lanes per position
+    constexpr int PPW = 64 / LPP;     // positions per wave step
+    constexpr int PPB = 4 * PPW;      // positions per workgroup step
+    __shared__ float sm_m[4][G], sm_l[4][G];
+    __shared__ float sm_o[4][G][D];
+    const int kvh = blockIdx.x, b = blockIdx.y, part = blockIdx.z;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int pg = lane / LPP, dl = lane % LPP;
+    const int L = seq_lens[b];
+    const int p0 = part * part_size;
+    const int p1 = min(L, p0 + part_size);
+    const int Hq = Hkv * G;
+
+    float qf[G][8];
+    const float qs = scale * LOG2E;
+#pragma unroll
+    for (int h = 0; h < G; ++h) {
+        const uint4 raw = *(const uint4*)(q + (size_t)b * q_stride + (size_t)(kvh * G + h) * D + dl * 8);
+        const uint32_t w[4] = {raw.x, raw.y, raw.z, raw.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            qf[h][2 * j] = __uint_as_float(w[j] << 16) * qs;
+            qf[h][2 * j + 1] = __uint_as_float(w[j] & 0xFFFF0000u) * qs;
+        }
+    }
+    float m[G], l[G], o[G][8];
+#pragma unroll
+    for (int h = 0; h < G; ++h) {
+        m[h] = -INFINITY;
+        l[h] = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[h][j] = 0.f;
+    }
+    const int* bt = block_tables + (size_t)b * bt_stride;
+    for (int base = p0; base < p1; base += PPB) {
+        const int p = base + wave * PPW + pg;
+        const bool valid = p < p1;
+        float kf[8], vf[8];
+        if (valid) {
+            const int blk = bt[p / bs], off = p % bs;
+            const size_t eo = (((size_t)blk * Hkv + kvh) * bs + off) * D + dl * 8;
+            const uint4 kr = *(const uint4*)(kc + eo);
+            const uint4 vr = *(const uint4*)(vc + eo);
+            const uint32_t kw[4] = {kr.x, kr.y, kr.z, kr.w}, vw[4] = {vr.x, vr.y, vr.z, vr.w};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                kf[2 * j] = __uint_as_float(kw[j] << 16);
+                kf[2 * j + 1] = __uint_as_float(kw[j] & 0xFFFF0000u);
+                vf[2 * j] = __uint_as_float(vw[j] << 16);
+                vf[2 * j + 1] = __uint_as_float(vw[j] & 0xFFFF0000u);
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) kf[j] = vf[j] = 0.f;
+        }
+#pragma unroll
+        for (int h = 0; h < G; ++h) {
+            float s = 0.f;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) s = fmaf(qf[h][j], kf[j], s);
+            s = group_sum<LPP>(s);
+            if (valid) {
+                const float mn = fmaxf(m[h], s);
+                const float a = exp2f(m[h] - mn);  // m = -inf -> 0
+                const float pr = exp2f(s - mn);
+                l[h] = l[h] * a + pr;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) o[h][j] = fmaf(pr, vf[j], o[h][j] * a);
+                m[h] = mn;
+            }
+        }
+    }
+    // merge the PPW position groups of the wave (xor over lane offsets LPP, 2LPP, ...)
+#pragma unroll
+    for (int off = LPP; off < 64; off <<= 1) {
+#pragma unroll
+        for (int h = 0; h < G; ++h) {
+            const float m2 = __shfl_xor(m[h], off, 64), l2 = __shfl_xor(l[h], off, 64);
+            const float mn = fmaxf(m[h], m2);
+            const float a1 = mn == -INFINITY ? 0.f : exp2f(m[h] - mn);
+            const float a2 = mn == -INFINITY ? 0.f : exp2f(m2 - mn);
+            l[h] = l[h] * a1 + l2 * a2;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float o2 = __shfl_xor(o[h][j], off, 64);
+                o[h][j] = o[h][j] * a1 + o2 * a2;
+            }
+            m[h] = mn;
+        }
+    }
+    if (pg == 0) {
+#pragma unroll
+        for (int h = 0; h < G; ++h) {
+            if (dl == 0) { sm_m[wave][h] = m[h]; sm_l[wave][h] = l[h]; }
+#pragma unroll
+            for (int j = 0; j < 8; ++j) sm_o[wave][h][dl * 8 + j] = o[h][j];
+        }
+    }
+    __syncthreads();
+    // combine the 4 waves: thread -> (h, d)
+    for (int idx = threadIdx.x; idx < G * D; idx += 256) {
+        const int h = idx / D, d = idx % D;
+        float mx = -INFINITY;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) mx = fmaxf(mx, sm_m[w][h]);
+        float ls = 0.f, os = 0.f;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            const float a = mx == -INFINITY ? 0.f : exp2f(sm_m[w][h] - mx);
+            ls += sm_l[w][h] * a;
+            os += sm_o[w][h][d] * a;
+        }
+        const int hq = kvh * G + h;
+        if (n_parts == 1) {
+            out[(size_t)b * out_stride + (size_t)hq * D + d] = f32_to_bf16(ls > 0.f ? os / ls : 0.f);
+        } else {
+            const size_t pi = ((size_t)b * Hq + hq) * n_parts + part;
+            if (d == 0) part_ml[pi] = make_float2(mx, ls);
+            part_o[pi * D + d] = os;
+        }
+    }
+}
+
+__global__ __launch_bounds__(128) void attn_decode_reduce_kernel(const float2* __restrict__ part_ml,
+                                                                  const float* __restrict__ part_o, int n_parts,
+                                                                  int Hq, int D, const int* __restrict__ seq_lens,
+                                                                  int part_size, bf16_t* __restrict__ out,
+                                                                  int out_stride) {
+    const int bh = blockIdx.x;
+    const int b = bh / Hq, h = bh % Hq;
+    const int np = min(n_parts, (seq_lens[b] + part_size - 1) / part_size);
+    float mx = -INFINITY;
+    for (int p = 0; p < np; ++p) mx = fmaxf(mx, part_ml[(size_t)bh * n_parts + p].x);
+    for (int d = threadIdx.x; d < D; d += blockDim.x) {
+        float ls = 0.f, os = 0.f;
+        for (int p = 0; p < np; ++p) {
+            const float2 ml = part_ml[(size_t)bh * n_parts + p];
+            const float a = mx == -INFINITY ? 0.f : exp2f(ml.x - mx);
+            ls += ml.y * a;
+            os += part_o[((size_t)bh * n_parts + p) * D + d] * a;
+        }
+        out[(size_t)b * out_stride + (size_t)h * D + d] = f32_to_bf16(ls > 0.f ? os / ls : 0.f);
+    }
+}
+
+template <int D, int G>
+static int launch_decode(const bf16_t* q, int q_stride, const bf16_t* kc, const bf16_t* vc, const int* bt,
+                         int bt_stride, const int* seq_lens, int B, int Hkv, int bs, float scale, int part_size,
+                         int n_parts, bf16_t* out, int out_stride, float2* part_ml, float* part_o,
+                         hipStream_t st) {
+    dim3 grid(Hkv, B, n_parts);
+    attn_decode_kernel<D, G><<<grid, 256, 0, st>>>(q, q_stride, kc, vc, bt, bt_stride, seq_lens, Hkv, bs, scale,
+                                                   part_size, n_parts, out, out_stride, part_ml, part_o);
+    if (n_parts > 1)
+        attn_decode_reduce_kernel<<<B * Hkv * G, 128, 0, st>>>(part_ml, part_o, n_parts, Hkv * G, D, seq_lens,
+                                                               part_size, out, out_stride);
+    MXK_CHECK_LAUNCH();
+}
+
+extern "C" int mxk_attn_decode(const bf16_t* q, int q_stride, const bf16_t* kc, const bf16_t* vc, const int* bt,
+                               int bt_stride, const int* seq_lens, int B, int Hq, int Hkv, int D, int bs,
+                               float scale, int part_size, int n_parts, bf16_t* out, int out_stride,
+                               float2* part_ml, float* part_o, hipStream_t st) {
+    if (B <= 0) return 0;
+    if (Hq % Hkv) return (int)hipErrorInvalidValue;
+    const int G = Hq / Hkv;
+    if (n_parts > 1 && (!part_ml || !part_o)) return (int)hipErrorInvalidValue;
+#define DEC(D_, G_) \
+    if (D == D_ && G == G_) return launch_decode<D_, G_>(q, q_stride, kc, vc, bt, bt_stride, seq_lens, B, Hkv, bs, scale, part_size, n_parts, out, out_stride, part_ml, part_o, st);
+    DEC(128, 1) DEC(128, 2) DEC(128, 3) DEC(128, 4) DEC(128, 5) DEC(128, 6) DEC(128, 7) DEC(128, 8)
+    DEC(64, 1) DEC(64, 2) DEC(64, 4) DEC(64, 8) DEC(256, 1) DEC(256, 2) DEC(256, 4) DEC(256, 8)
+#undef DEC
+    return (int)hipErrorInvalidValue;
+}
+
+// ------------------------------------------------------------------------------------------------
+// prefill: MFMA flash attention over the paged cache.
+// K image: row p (64 per tile) holds D/8 16-byte chunks; chunk c lives at slot c ^ fk(p).
+template <int D>
+MX_DEV int k_lds_off(int p, int c) {
+    const int r = p & 15;
+    int f;
+    if constexpr (D == 128) f = r ^ (((r + 4) >> 3) & 1);
+    else f = ((r >> 1) & 7) ^ (((r + 4) >> 3) & 1);
+    return p * (D * 2) + ((c ^ (f & (D / 8 - 1))) << 4);
+}
+// V image: row p holds D/16 32-byte regions (16 dims each); region nt lives at nt ^ sv(p).
+template <int D>
+MX_DEV int v_lds_off(int p, int nt) {
+    int sv;
+    if constexpr (D == 128) sv = (p & 3) | (((p >> 3) & 1) << 2);
+    else sv = ((p >> 1) & 1) | (((p >> 3) & 1) << 1);
+    return p * (D * 2) + ((nt ^ sv) << 5);
+}
+
+template <int D, int GW>
+__global__ __launch_bounds__(512) void attn_prefill_kernel(const bf16_t* __restrict__ q,
+                                                           const bf16_t* __restrict__ kc,
+                                                           const bf16_t* __restrict__ vc,
+                                                           const int* __restrict__ block_tables, int bt_stride,
+                                                           const int* __restrict__ tile_seq,
+                                                           const int* __restrict__ tile_q0,
+                                                           const int* __restrict__ cu_q,
+                                                           const int* __restrict__ ctx_lens, int Hq, int Hkv,
+                                                           int G, int bs, float scale, bf16_t* __restrict__ out) {
+    constexpr int NW = GW >= 3 ? GW : 4;      // waves per workgroup
+    constexpr int RT = NW / GW;               // 16-row query tiles per workgroup
+    constexpr int KT = 64;                    // keys per tile
+    constexpr int KBYTES = KT * D * 2;
+    constexpr int PSTRIDE = (KT + 8) * 2;     // bytes per P row (padded)
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    char* k_lds = smem;
+    char* v_lds = smem + KBYTES;
+    char* p_lds = smem + 2 * KBYTES;
+    const int NT = NW * 64;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int g = lane >> 4, col = lane & 15;
+    const int tile = blockIdx.x;
+    const int s = tile_seq[tile], q0 = tile_q0[tile];
+    const int hq = blockIdx.y * GW + (wave % GW);
+    const int kvh = (blockIdx.y * GW) / G;
+    const int rt = wave / GW;
+    const int qbeg = cu_q[s], qlen = cu_q[s + 1] - qbeg;
+    const int ctx = ctx_lens[s];
+    const int pos_off = ctx - qlen;  // position of query 0
+    const int* bt = block_tables + (size_t)s * bt_stride;
+    const int row_q0 = q0 + rt * 16;        // first query index of this wave
+    const int wg_rows = RT * 16;
+    const int kv_end = min(ctx, pos_off + min(qlen, q0 + wg_rows));
+    const float qs = scale * LOG2E;
+
+    // Q fragments: lane row = col, dims 32ks + 8g
+    bf16x8 qf[D / 32];
+    {
+        const int qi = row_q0 + col;
+#pragma unroll
+        for (int ks = 0; ks < D / 32; ++ks) {
+            if (qi < qlen) qf[ks] = *(const bf16x8*)(q + ((size_t)(qbeg + qi) * Hq + hq) * D + 32 * ks + 8 * g);
+            else qf[ks] = (bf16x8){};
+        }
+    }
+    f32x4 oacc[D / 16];
+#pragma unroll
+    for (int i = 0; i < D / 16; ++i) oacc[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    float mrow[4], lrow[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { mrow[i] = -INFINITY; lrow[i] = 0.f; }
+    char* pw = p_lds + wave * 16 * PSTRIDE;
+
+    for (int kt0 = 0; kt0 < kv_end; kt0 += KT) {
+        // ---- stage K and V tiles (64 keys x D) ----
+        constexpr int CH = KT * D / 8;  // 16-byte chunks per tile
+        for (int id = threadIdx.x; id < CH; id += NT) {
+            const int p = id / (D / 8), c = id % (D / 8);
+            const int pos = kt0 + p;
+            uint4 kv = make_uint4(0, 0, 0, 0), vv = make_uint4(0, 0, 0, 0);
+            if (pos < kv_end) {
+                const int blk = bt[pos / bs], off = pos % bs;
+                const size_t eo = (((size_t)blk * Hkv + kvh) * bs + off) * D + c * 8;
+                kv = *(const uint4*)(kc + eo);
+                vv = *(const uint4*)(vc + eo);
+            }
+            *(uint4*)(k_lds + k_lds_off<D>(p, c)) = kv;
+            *(uint4*)(v_lds + v_lds_off<D>(p, c >> 1) + 16 * (c & 1)) = vv;
+        }
+        __syncthreads();
+        // ---- S = Q K^T : 16 rows x 64 keys ----
+        f32x4 sacc[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            sacc[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int ks = 0; ks < D / 32; ++ks) {
+                const bf16x8 kf = *(const bf16x8*)(k_lds + k_lds_off<D>(16 * t + col, 4 * ks + g));
+                sacc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qf[ks], kf, sacc[t], 0, 0, 0);
+            }
+        }
+        // ---- mask + online softmax (rows 4g+i, keys 16t+col) ----
+        float rmax[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int qi = row_q0 + 4 * g + i;
+            const int qpos = pos_off + qi;
+            float mx = -INFINITY;
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const int kp = kt0 + 16 * t + col;
+                float v = sacc[t][i] * qs;
+                if (kp > qpos || kp >= ctx || qi >= qlen) v = -INFINITY;
+                sacc[t][i] = v;
+                mx = fmaxf(mx, v);
+            }
+            rmax[i] = group_max<16>(mx);
+        }
+        float alpha[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const float mn = fmaxf(mrow[i], rmax[i]);
+            alpha[i] = mn == -INFINITY ? 1.f : exp2f(mrow[i] - mn);
+            float rs = 0.f;
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const float pv = mn == -INFINITY ? 0.f : exp2f(sacc[t][i] - mn);
+                sacc[t][i] = pv;
+                rs += pv;
+            }
+            rs = group_sum<16>(rs);
+            lrow[i] = lrow[i] * alpha[i] + rs;
+            mrow[i] = mn;
+        }
+#pragma unroll
+        for (int nt = 0; nt < D / 16; ++nt)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) oacc[nt][i] *= alpha[i];
+        // ---- P -> LDS (bf16) ----
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                *(bf16_t*)(pw + (4 * g + i) * PSTRIDE + (16 * t + col) * 2) = f32_to_bf16(sacc[t][i]);
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): P visible to the wave (same wave reads)
+        __builtin_amdgcn_wave_barrier();
+        // ---- O += P V ----
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            const bf16x8 pa = *(const bf16x8*)(pw + col * PSTRIDE + (32 * ks + 8 * g) * 2);
+            const int r0 = 32 * ks + 8 * g;
+            const int q4 = col >> 2, p4 = col & 3;
+#pragma unroll
+            for (int nt = 0; nt < D / 16; ++nt) {
+                const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                    (MX_LDS s16x4*)(v_lds + v_lds_off<D>(r0 + q4, nt) + 8 * p4));
+                const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                    (MX_LDS s16x4*)(v_lds + v_lds_off<D>(r0 + 4 + q4, nt) + 8 * p4));
+                bf16x8 vb;
+                vb[0] = __builtin_bit_cast(__bf16, lo[0]); vb[1] = __builtin_bit_cast(__bf16, lo[1]);
+                vb[2] = __builtin_bit_cast(__bf16, lo[2]); vb[3] = __builtin_bit_cast(__bf16, lo[3]);
+                vb[4] = __builtin_bit_cast(__bf16, hi[0]); vb[5] = __builtin_bit_cast(__bf16, hi[1]);
+                vb[6] = __builtin_bit_cast(__bf16, hi[2]); vb[7] = __builtin_bit_cast(__bf16, hi[3]);
+                oacc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, vb, oacc[nt], 0, 0, 0);
+            }
+        }
+        __syncthreads();
+    }
+    // ---- write O / l ----
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int qi = row_q0 + 4 * g + i;
+        if (qi >= qlen) continue;
+        const float inv = lrow[i] > 0.f ? 1.f / lrow[i] : 0.f;
+#pragma unroll
+        for (int nt = 0; nt < D / 16; ++nt)
+            out[((size_t)(qbeg + qi) * Hq + hq) * D + 16 * nt + col] = f32_to_bf16(oacc[nt][i] * inv);
+    }
+}
+
+template <int D, int GW>
+static int launch_prefill(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, const int* bt, int bt_stride,
+                          const int* tile_seq, const int* tile_q0, int n_tiles, const int* cu_q,
+                          const int* ctx_lens, int Hq, int Hkv, int bs, float scale, bf16_t* out,
+                          hipStream_t st) {
+    constexpr int NW = GW >= 3 ? GW : 4;
+    const size_t lds = 2 * 64 * D * 2 + NW * 16 * (64 + 8) * 2;
+    dim3 grid(n_tiles, Hq / GW);
+    attn_prefill_kernel<D, GW><<<grid, NW * 64, lds, st>>>(q, kc, vc, bt, bt_stride, tile_seq, tile_q0, cu_q,
+                                                            ctx_lens, Hq, Hkv, Hq / Hkv, bs, scale, out);
+    MXK_CHECK_LAUNCH();
+}
+
+// rows per workgroup for the host-side tile map: 16 * (NW / GW)
+extern "C" int mxk_attn_prefill_rows(int Hq, int Hkv) {
+    const int G = Hq / Hkv;
+    const int GW = G <= 8 ? G : 8;
+    const int NW = GW >= 3 ? GW : 4;
+    return 16 * (NW / GW);
+}
+
+extern "C" int mxk_attn_prefill(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, const int* bt, int bt_stride,
+                                const int* tile_seq, const int* tile_q0, int n_tiles, const int* cu_q,
+                                const int* ctx_lens, int Hq, int Hkv, int D, int bs, float scale, bf16_t* out,
+                                hipStream_t st) {
+    if (n_tiles <= 0) return 0;
+    if (Hq % Hkv) return (int)hipErrorInvalidValue;
+    const int G = Hq / Hkv;
+    const int GW = G <= 8 ? G : 8;
+    if (G > 8 && G % 8) return (int)hipErrorInvalidValue;
+#define PF(D_, GW_) \
+    if (D == D_ && GW == GW_) return launch_prefill<D_, GW_>(q, kc, vc, bt, bt_stride, tile_seq, tile_q0, n_tiles, cu_q, ctx_lens, Hq, Hkv, bs, scale, out, st);
+    PF(128, 1) PF(128, 2) PF(128, 3) PF(128, 4) PF(128, 5) PF(128, 6) PF(128, 7) PF(128, 8)
+    PF(64, 1) PF(64, 2) PF(64, 4) PF(64, 8)
+#undef PF
+    return (int)hipErrorInvalidValue;
+}

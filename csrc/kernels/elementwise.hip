@@ -1,0 +1,132 @@
+// elementwise.hip — small fused element-wise kernels (K11/K12 of SURVEY §2.6) used outside the
+// fused GEMM epilogues: SwiGLU/GeGLU on separate gate/up buffers, GELU, residual adds, fp32<->bf16
+// casts and embedding-row gathers for dense (f32/f16/bf16) tables. All loads are 16-byte vectors.
+#include "mx_common.h"
+
+// y[m, f] = act(g[m, f]) * u[m, f]; g/u bf16 with row stride ld_in, out bf16
+template <int ACT>
+__global__ __launch_bounds__(256) void glu_kernel(const bf16_t* __restrict__ g, const bf16_t* __restrict__ u,
+                                                  int ld_in, bf16_t* __restrict__ y, int ld_out, int F) {
+    const int m = blockIdx.y;
+    const int f = (blockIdx.x * 256 + threadIdx.x) * 8;
+    if (f >= F) return;
+    const uint4 gr = *(const uint4*)(g + (size_t)m * ld_in + f);
+    const uint4 ur = *(const uint4*)(u + (size_t)m * ld_in + f);
+    const uint32_t gw[4] = {gr.x, gr.y, gr.z, gr.w}, uw[4] = {ur.x, ur.y, ur.z, ur.w};
+    uint32_t o[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        float g0 = __uint_as_float(gw[j] << 16), g1 = __uint_as_float(gw[j] & 0xFFFF0000u);
+        float u0 = __uint_as_float(uw[j] << 16), u1 = __uint_as_float(uw[j] & 0xFFFF0000u);
+        float a0, a1;
+        if (ACT == 0) { a0 = silu_f(g0); a1 = silu_f(g1); }
+        else if (ACT == 1) { a0 = gelu_tanh_f(g0); a1 = gelu_tanh_f(g1); }
+        else { a0 = gelu_erf_f(g0); a1 = gelu_erf_f(g1); }
+        o[j] = pack_bf16x2(a0 * u0, a1 * u1);
+    }
+    *(uint4*)(y + (size_t)m * ld_out + f) = make_uint4(o[0], o[1], o[2], o[3]);
+}
+
+extern "C" int mxk_glu(int act, const bf16_t* g, const bf16_t* u, int ld_in, bf16_t* y, int ld_out, int M, int F,
+                       hipStream_t st) {
+    if (M <= 0) return 0;
+    if (F % 8) return (int)hipErrorInvalidValue;
+    dim3 grid((F / 8 + 255) / 256, M);
+    if (act == 0) glu_kernel<0><<<grid, 256, 0, st>>>(g, u, ld_in, y, ld_out, F);
+    else if (act == 1) glu_kernel<1><<<grid, 256, 0, st>>>(g, u, ld_in, y, ld_out, F);
+    else glu_kernel<2><<<grid, 256, 0, st>>>(g, u, ld_in, y, ld_out, F);
+    MXK_CHECK_LAUNCH();
+}
+
+// in-place activation on fp32 (act: 0 silu, 1 gelu-tanh, 2 gelu-erf, 3 relu)
+__global__ __launch_bounds__(256) void act_f32_kernel(float* __restrict__ x, size_t n, int act) {
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+        float v = x[i];
+        if (act == 0) v = silu_f(v);
+        else if (act == 1) v = gelu_tanh_f(v);
+        else if (act == 2) v = gelu_erf_f(v);
+        else v = fmaxf(v, 0.f);
+        x[i] = v;
+    }
+}
+
+extern "C" int mxk_act_f32(float* x, size_t n, int act, hipStream_t st) {
+    if (!n) return 0;
+    const int grid = (int)min((size_t)4096, (n + 255) / 256);
+    act_f32_kernel<<<grid, 256, 0, st>>>(x, n, act);
+    MXK_CHECK_LAUNCH();
+}
+
+// fp32 -> bf16 cast of a [rows, cols] view with strides
+__global__ __launch_bounds__(256) void cast_f32_bf16_kernel(const float* __restrict__ x, int ldx,
+                                                            bf16_t* __restrict__ y, int ldy, int cols) {
+    const int r = blockIdx.y;
+    for (int c = (blockIdx.x * 256 + threadIdx.x) * 4; c < cols; c += gridDim.x * 256 * 4) {
+        const float4 v = *(const float4*)(x + (size_t)r * ldx + c);
+        uint2 p;
+        p.x = pack_bf16x2(v.x, v.y);
+        p.y = pack_bf16x2(v.z, v.w);
+        *(uint2*)(y + (size_t)r * ldy + c) = p;
+    }
+}
+
+extern "C" int mxk_cast_f32_bf16(const float* x, int ldx, bf16_t* y, int ldy, int rows, int cols, hipStream_t st) {
+    if (rows <= 0) return 0;
+    if (cols % 4) return (int)hipErrorInvalidValue;
+    dim3 grid(min(64, (cols / 4 + 255) / 256), rows);
+    cast_f32_bf16_kernel<<<grid, 256, 0, st>>>(x, ldx, y, ldy, cols);
+    MXK_CHECK_LAUNCH();
+}
+
+// gather rows of a dense table: dtype 0 f32, 1 f16, 2 bf16 -> fp32 out (the residual stream)
+__global__ __launch_bounds__(256) void gather_rows_kernel(const void* __restrict__ tab, int dtype,
+                                                          const int* __restrict__ ids, int H, float scale,
+                                                          float* __restrict__ out) {
+    const int r = blockIdx.x;
+    const size_t base = (size_t)ids[r] * H;
+    for (int c = threadIdx.x; c < H; c += 256) {
+        float v;
+        if (dtype == 0) v = ((const float*)tab)[base + c];
+        else if (dtype == 1) v = half_to_f32(((const uint16_t*)tab)[base + c]);
+        else v = bf16_to_f32(((const uint16_t*)tab)[base + c]);
+        out[(size_t)r * H + c] = v * scale;
+    }
+}
+
+extern "C" int mxk_gather_rows(const void* tab, int dtype, const int* ids, int n, int H, float scale, float* out,
+                               hipStream_t st) {
+    if (n <= 0) return 0;
+    gather_rows_kernel<<<n, 256, 0, st>>>(tab, dtype, ids, H, scale, out);
+    MXK_CHECK_LAUNCH();
+}
+
+// scale fp32 rows in place (embedding scale for Gemma-style models) and add bias vectors
+__global__ __launch_bounds__(256) void add_bias_f32_kernel(float* __restrict__ x, int ld, const float* __restrict__ b,
+                                                           int cols) {
+    const int r = blockIdx.y;
+    for (int c = blockIdx.x * 256 + threadIdx.x; c < cols; c += gridDim.x * 256) x[(size_t)r * ld + c] += b[c];
+}
+
+extern "C" int mxk_add_bias_f32(float* x, int ld, const float* b, int rows, int cols, hipStream_t st) {
+    if (rows <= 0) return 0;
+    dim3 grid(min(64, (cols + 255) / 256), rows);
+    add_bias_f32_kernel<<<grid, 256, 0, st>>>(x, ld, b, cols);
+    MXK_CHECK_LAUNCH();
+}
+
+// gather selected rows of an fp32 matrix (last-token-of-each-sequence selection before the LM head)
+__global__ __launch_bounds__(256) void select_rows_f32_kernel(const float* __restrict__ x, int ld,
+                                                              const int* __restrict__ idx, int cols,
+                                                              float* __restrict__ y, int ldy) {
+    const int r = blockIdx.x;
+    const float* src = x + (size_t)idx[r] * ld;
+    for (int c = threadIdx.x * 4; c < cols; c += 1024) *(float4*)(y + (size_t)r * ldy + c) = *(const float4*)(src + c);
+}
+
+extern "C" int mxk_select_rows_f32(const float* x, int ld, const int* idx, int n, int cols, float* y, int ldy,
+                                   hipStream_t st) {
+    if (n <= 0) return 0;
+    if (cols % 4) return (int)hipErrorInvalidValue;
+    select_rows_f32_kernel<<<n, 256, 0, st>>>(x, ld, idx, cols, y, ldy);
+    MXK_CHECK_LAUNCH();
+}

@@ -1,0 +1,148 @@
+// mx_common.h — shared device helpers for the localai_tfp_amd CDNA4 (gfx950) kernels.
+//
+// Conventions used by every kernel in this directory:
+//   * wave64 only: every lane index is `threadIdx.x & 63`, every reduction is over 64 lanes.
+//   * activations in HBM are bf16 (uint16_t bit patterns) or fp32; accumulation is always fp32.
+//   * every launcher is `extern "C" int mxk_*(..., hipStream_t)` and returns the hipError_t of the
+//     launch so the Python side can raise loudly; launchers never allocate or synchronise, so all of
+//     them are safe inside hipGraph stream capture.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef uint16_t bf16_t;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4v __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+#define MX_DEV __device__ __forceinline__
+#define MX_LDS __attribute__((address_space(3)))
+
+MX_DEV float bf16_to_f32(bf16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
+
+// round-to-nearest-even; NaN stays NaN (the plain cast lowers to v_cvt_pk_bf16_f32 on gfx950).
+MX_DEV bf16_t f32_to_bf16(float f) {
+    __bf16 b = (__bf16)f;
+    return __builtin_bit_cast(bf16_t, b);
+}
+
+MX_DEV uint32_t pack_bf16x2(float lo, float hi) {
+    bf16x2v v = {(__bf16)lo, (__bf16)hi};
+    return __builtin_bit_cast(uint32_t, v);
+}
+
+MX_DEV float half_to_f32(uint16_t h) { return (float)__builtin_bit_cast(_Float16, h); }
+
+MX_DEV float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+MX_DEV float wave_max(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+// sum over groups of `W` consecutive lanes (W power of two <= 64)
+template <int W>
+MX_DEV float group_sum(float v) {
+#pragma unroll
+    for (int o = W / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+template <int W>
+MX_DEV float group_max(float v) {
+#pragma unroll
+    for (int o = W / 2; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+MX_DEV int wave_sum_i(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// block-wide sum for blockDim.x == NT (multiple of 64); `red` must hold NT/64 floats.
+template <int NT>
+MX_DEV float block_sum(float v, float* red) {
+    v = wave_sum(v);
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    if (l == 0) red[w] = v;
+    __syncthreads();
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < NT / 64; ++i) t += red[i];
+    __syncthreads();
+    return t;
+}
+template <int NT>
+MX_DEV float block_max(float v, float* red) {
+    v = wave_max(v);
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    if (l == 0) red[w] = v;
+    __syncthreads();
+    float t = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < NT / 64; ++i) t = fmaxf(t, red[i]);
+    __syncthreads();
+    return t;
+}
+
+MX_DEV float silu_f(float x) { return x / (1.f + __expf(-x)); }
+MX_DEV float gelu_tanh_f(float x) {
+    const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+    return 0.5f * x * (1.f + tanhf(k0 * (x + k1 * x * x * x)));
+}
+MX_DEV float gelu_erf_f(float x) { return 0.5f * x * (1.f + erff(x * 0.7071067811865476f)); }
+
+#define MXK_CHECK_LAUNCH() return (int)hipGetLastError()
+
+// ---- GGML block formats (byte layouts identical to GGUF on disk) ----
+// Q4_K: 256 elements, 144 B: half d, half dmin, u8 scales[12], u8 qs[128]
+// Q6_K: repacked at load time to a 16B-aligned 208 B block + a separate fp16 d plane (see quant.py)
+// Q8_0: repacked to an int8 plane [N][K] + fp16 d plane [N][K/32]
+enum MxQuantType : int {
+    MXQ_Q4_K = 12,
+    MXQ_Q6_K = 14,
+    MXQ_Q8_0 = 8,
+    MXQ_Q5_K = 13,
+    MXQ_Q4_0 = 2,
+};
+
+// Q4_K 6-bit packed (scale, min) for sub-block j (0..7) out of the 12 scale bytes.
+MX_DEV void q4k_scale_min(const uint8_t* q, int j, int& sc, int& m) {
+    if (j < 4) {
+        sc = q[j] & 63;
+        m = q[j + 4] & 63;
+    } else {
+        sc = (q[j + 4] & 0xF) | ((q[j - 4] >> 6) << 4);
+        m = (q[j + 4] >> 4) | ((q[j] >> 6) << 4);
+    }
+}
+
+// Same decode from the three 32-bit words of the scale array (no byte-addressed loads).
+MX_DEV void q4k_scale_min_w(uint32_t w0, uint32_t w1, uint32_t w2, int j, int& sc, int& m) {
+    auto byte = [&](int i) -> int {
+        uint32_t w = i < 4 ? w0 : (i < 8 ? w1 : w2);
+        return (w >> (8 * (i & 3))) & 0xFF;
+    };
+    if (j < 4) {
+        sc = byte(j) & 63;
+        m = byte(j + 4) & 63;
+    } else {
+        sc = (byte(j + 4) & 0xF) | ((byte(j - 4) >> 6) << 4);
+        m = (byte(j + 4) >> 4) | ((byte(j) >> 6) << 4);
+    }
+}
+
+// sign-extend four packed 6-bit unsigned values (0..63, stored one per byte) after subtracting 32.
+MX_DEV uint32_t q6_bias_bytes(uint32_t q) {
+    uint32_t t = q ^ 0x20202020u;          // flips bit5: (q-32) in 6-bit two's complement
+    uint32_t s = t & 0x20202020u;          // sign bits
+    return t | (s << 1) | (s << 2);        // extend to bits 6,7
+}

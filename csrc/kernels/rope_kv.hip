@@ -1,0 +1,100 @@
+// rope_kv.hip — fused bias + RoPE + paged KV-cache append (K8 + K10 of SURVEY §2.6).
+//
+// Consumes the fp32 QKV projection of T tokens ([T, (Hq + 2*Hkv) * D], written by the qgemm/qgemv
+// F32 epilogue), applies the optional QKV bias (Qwen2), rotates Q and K, writes Q as bf16 for the
+// attention kernel and scatters K/V into the paged cache:
+//   cache layout  [num_blocks][Hkv][block_size][D] bf16 — a kv-head's block is one contiguous
+//   block_size*D*2-byte run, so decode attention streams it with 16-byte loads.
+// Rotation: theta_i = pos * inv_freq[i] (the host folds freq_base, linear/llama3/YaRN scaling into
+// inv_freq and the YaRN magnitude correction into attn_factor; grpc-server.cpp:2419-2439 is the
+// reference's parameter surface). Modes: NORM (adjacent pairs, llama) and NEOX (half split).
+#include "mx_common.h"
+
+template <bool NEOX, bool HAS_BIAS>
+__global__ __launch_bounds__(256) void rope_kv_kernel(const float* __restrict__ qkv, const float* __restrict__ bias,
+                                                      const int* __restrict__ pos, const int* __restrict__ slots,
+                                                      const float* __restrict__ inv_freq, float attn_factor,
+                                                      int Hq, int Hkv, int D, int rot_dim, bf16_t* __restrict__ qo,
+                                                      bf16_t* __restrict__ kc, bf16_t* __restrict__ vc,
+                                                      int block_size) {
+    __shared__ float cs[256], sn[256];
+    const int t = blockIdx.x;
+    const int p = pos[t];
+    const int half = rot_dim / 2;
+    for (int i = threadIdx.x; i < half; i += 256) {
+        float s, c;
+        sincosf((float)p * inv_freq[i], &s, &c);
+        cs[i] = c * attn_factor;
+        sn[i] = s * attn_factor;
+    }
+    __syncthreads();
+    const int W = (Hq + 2 * Hkv) * D;
+    const float* row = qkv + (size_t)t * W;
+    const int slot = slots[t];
+    const int blk = slot >= 0 ? slot / block_size : 0, off = slot >= 0 ? slot % block_size : 0;
+    // rotate q and k heads: one thread per output element; dims >= rot_dim pass through.
+    const int nh = Hq + Hkv;
+    const int total = nh * D;
+    for (int idx = threadIdx.x; idx < total; idx += 256) {
+        const int h = idx / D, d = idx % D;
+        float x = row[h * D + d];
+        if (HAS_BIAS) x += bias[h * D + d];
+        float y = x;
+        if (d < rot_dim) {
+            int pd, fi;
+            bool first;
+            if (NEOX) { first = d < half; pd = first ? d + half : d - half; fi = first ? d : d - half; }
+            else { first = (d & 1) == 0; pd = first ? d + 1 : d - 1; fi = d >> 1; }
+            float xp = row[h * D + pd];
+            if (HAS_BIAS) xp += bias[h * D + pd];
+            const float c = cs[fi], s = sn[fi];
+            y = first ? (x * c - xp * s) : (xp * s + x * c);
+        }
+        if (h < Hq) {
+            qo[((size_t)t * Hq + h) * D + d] = f32_to_bf16(y);
+        } else if (slot >= 0) {
+            const int kh = h - Hq;
+            kc[(((size_t)blk * Hkv + kh) * block_size + off) * D + d] = f32_to_bf16(y);
+        }
+    }
+    if (slot >= 0) {
+        const float* vr = row + (Hq + Hkv) * D;
+        for (int idx = threadIdx.x; idx < Hkv * D; idx += 256) {
+            const int kh = idx / D, d = idx % D;
+            float v = vr[idx];
+            if (HAS_BIAS) v += bias[(Hq + Hkv) * D + idx];
+            vc[(((size_t)blk * Hkv + kh) * block_size + off) * D + d] = f32_to_bf16(v);
+        }
+    }
+}
+
+extern "C" int mxk_rope_kv(const float* qkv, const float* bias, const int* pos, const int* slots,
+                           const float* inv_freq, float attn_factor, int T, int Hq, int Hkv, int D, int rot_dim,
+                           int neox, bf16_t* qo, bf16_t* kc, bf16_t* vc, int block_size, hipStream_t st) {
+    if (T <= 0) return 0;
+    if (rot_dim > 512 || (rot_dim & 1) || D & 1) return (int)hipErrorInvalidValue;
+#define RK(N_, B_) rope_kv_kernel<N_, B_><<<T, 256, 0, st>>>(qkv, bias, pos, slots, inv_freq, attn_factor, Hq, Hkv, D, rot_dim, qo, kc, vc, block_size)
+    if (neox) { if (bias) RK(true, true); else RK(true, false); }
+    else { if (bias) RK(false, true); else RK(false, false); }
+#undef RK
+    MXK_CHECK_LAUNCH();
+}
+
+// Copy whole KV blocks (prefix-cache copy-on-write / beam fork): dst[i] <- src[i] for all layers
+// handled by the caller (one launch per layer cache tensor).
+__global__ __launch_bounds__(256) void copy_blocks_kernel(bf16_t* __restrict__ cache, const int* __restrict__ src,
+                                                          const int* __restrict__ dst, int block_elems) {
+    const int b = blockIdx.y;
+    const size_t so = (size_t)src[b] * block_elems, dO = (size_t)dst[b] * block_elems;
+    for (int i = (blockIdx.x * 256 + threadIdx.x) * 8; i < block_elems; i += gridDim.x * 256 * 8)
+        *(uint4*)(cache + dO + i) = *(const uint4*)(cache + so + i);
+}
+
+extern "C" int mxk_copy_blocks(bf16_t* cache, const int* src, const int* dst, int n, int block_elems,
+                               hipStream_t st) {
+    if (n <= 0) return 0;
+    if (block_elems % 8) return (int)hipErrorInvalidValue;
+    dim3 grid(min(64, (block_elems / 8 + 255) / 256), n);
+    copy_blocks_kernel<<<grid, 256, 0, st>>>(cache, src, dst, block_elems);
+    MXK_CHECK_LAUNCH();
+}

@@ -1,0 +1,260 @@
+// sampling.hip — fused on-GPU token sampler (K13 of SURVEY §2.6).
+//
+// The reference samples on the CPU over the full 128k-vocab logits of every slot every step
+// (grpc-server.cpp:2038 common_sampler_sample). Here one 1024-thread workgroup per sequence does the
+// whole chain on the device with no sort:
+//   sparse penalties/bias (repeat, presence, frequency, logit_bias: host passes unique (tok, count,
+//   bias) triples per row)  ->  grammar allow-mask  ->  temperature  ->  top-k / top-p / min-p /
+//   typical-p / mirostat-v2 truncation, each as a threshold found by bisection on the value axis
+//   ->  Gumbel-max draw over the kept set (exactly a categorical sample of the renormalised
+//   distribution), or argmax when greedy.
+// Output: token id and its log-probability under the final (truncated, tempered) distribution.
+#include "mx_common.h"
+
+struct SampleParams {
+    float temperature;  // <= 0 -> greedy
+    int top_k;          // <= 0 -> off
+    float top_p;        // >= 1 -> off
+    float min_p;        // <= 0 -> off
+    float typical_p;    // >= 1 -> off
+    float mirostat_tau;  // mirostat v2 truncation mu (already 2*tau on first step); <= 0 -> off
+    float repeat_penalty;
+    float presence_penalty;
+    float frequency_penalty;
+    int pen_offset;  // into the sparse penalty arrays
+    int pen_count;
+    unsigned long long seed;
+};
+
+MX_DEV uint32_t mix32(uint64_t x) {
+    x ^= x >> 33; x *= 0xff51afd7ed558ccdULL;
+    x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ULL;
+    x ^= x >> 33;
+    return (uint32_t)x;
+}
+MX_DEV float gumbel(uint64_t seed, uint32_t i) {
+    const uint32_t r = mix32(seed * 0x9E3779B97F4A7C15ULL + i);
+    const float u = ((float)(r >> 8) + 0.5f) * (1.f / 16777216.f);
+    return -__logf(-__logf(u));
+}
+
+constexpr int SNT = 1024;
+
+MX_DEV float bsum(float v, float* red) {
+    v = wave_sum(v);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < SNT / 64; ++i) t += red[i];
+    __syncthreads();
+    return t;
+}
+MX_DEV float bmax(float v, float* red) {
+    v = wave_max(v);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    float t = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < SNT / 64; ++i) t = fmaxf(t, red[i]);
+    __syncthreads();
+    return t;
+}
+
+__global__ __launch_bounds__(SNT) void sample_kernel(float* __restrict__ logits, int ld, int V,
+                                                     const SampleParams* __restrict__ params,
+                                                     const int* __restrict__ pen_tok,
+                                                     const int* __restrict__ pen_cnt,
+                                                     const float* __restrict__ pen_bias,
+                                                     const uint32_t* __restrict__ allow_mask, int mask_ld,
+                                                     int* __restrict__ out_tok, float* __restrict__ out_logp) {
+    __shared__ float red[SNT / 64];
+    __shared__ float rv[SNT / 64];
+    __shared__ int ri[SNT / 64];
+    const int row = blockIdx.x;
+    const SampleParams P = params[row];
+    float* x = logits + (size_t)row * ld;
+    // 1. sparse penalties + logit bias (unique tokens per row -> no write conflicts)
+    for (int i = threadIdx.x; i < P.pen_count; i += SNT) {
+        const int t = pen_tok[P.pen_offset + i];
+        if (t < 0 || t >= V) continue;
+        const int c = pen_cnt[P.pen_offset + i];
+        float v = x[t];
+        if (c > 0) {
+            if (P.repeat_penalty != 1.f) v = v > 0.f ? v / P.repeat_penalty : v * P.repeat_penalty;
+            v -= P.frequency_penalty * (float)c + P.presence_penalty;
+        }
+        v += pen_bias[P.pen_offset + i];
+        x[t] = v;
+    }
+    __syncthreads();
+    const bool greedy = P.temperature <= 0.f;
+    const float itemp = greedy ? 1.f : 1.f / P.temperature;
+    const uint32_t* am = allow_mask ? allow_mask + (size_t)row * mask_ld : nullptr;
+    auto val = [&](int i) -> float {
+        float v = x[i];
+        if (am && !((am[i >> 5] >> (i & 31)) & 1u)) return -INFINITY;
+        return v * itemp;
+    };
+    // 2. max and log-sum-exp of the tempered distribution
+    float mx = -INFINITY;
+    for (int i = threadIdx.x; i < V; i += SNT) mx = fmaxf(mx, val(i));
+    mx = bmax(mx, red);
+    float thr = -INFINITY;  // keep tokens with val >= thr
+    if (!greedy) {
+        // top-k: largest thr with count(val >= thr) >= k, by bisection on [mx - 64, mx]
+        if (P.top_k > 0 && P.top_k < V) {
+            float lo = mx - 80.f, hi = mx;
+            for (int it = 0; it < 28; ++it) {
+                const float mid = 0.5f * (lo + hi);
+                float c = 0.f;
+                for (int i = threadIdx.x; i < V; i += SNT) c += val(i) >= mid ? 1.f : 0.f;
+                c = bsum(c, red);
+                if (c >= (float)P.top_k) lo = mid; else hi = mid;
+            }
+            thr = fmaxf(thr, lo);
+        }
+        float Z = 0.f;
+        for (int i = threadIdx.x; i < V; i += SNT) { const float v = val(i); Z += v >= thr ? __expf(v - mx) : 0.f; }
+        Z = bsum(Z, red);
+        // min-p: keep p >= min_p * p_max  <=>  val >= mx + log(min_p)
+        if (P.min_p > 0.f && P.min_p <= 1.f) thr = fmaxf(thr, mx + __logf(P.min_p));
+        // top-p: largest thr with mass(val >= thr) >= top_p * Z
+        if (P.top_p < 1.f && P.top_p > 0.f) {
+            float lo = fmaxf(thr, mx - 80.f), hi = mx;
+            for (int it = 0; it < 28; ++it) {
+                const float mid = 0.5f * (lo + hi);
+                float s = 0.f;
+                for (int i = threadIdx.x; i < V; i += SNT) { const float v = val(i); s += v >= mid ? __expf(v - mx) : 0.f; }
+                s = bsum(s, red);
+                if (s >= P.top_p * Z) lo = mid; else hi = mid;
+            }
+            thr = fmaxf(thr, lo);
+        }
+        // typical-p: keep tokens whose surprise is closest to the entropy, cumulative mass >= typical_p
+        if (P.typical_p < 1.f && P.typical_p > 0.f) {
+            const float lZ = __logf(Z);
+            float H = 0.f;
+            for (int i = threadIdx.x; i < V; i += SNT) {
+                const float v = val(i);
+                if (v >= thr) { const float lp = v - mx - lZ; H -= __expf(lp) * lp; }
+            }
+            H = bsum(H, red);
+            // bisection on eps: keep |(-lp) - H| <= eps
+            float lo = 0.f, hi = 80.f;
+            for (int it = 0; it < 28; ++it) {
+                const float mid = 0.5f * (lo + hi);
+                float s = 0.f;
+                for (int i = threadIdx.x; i < V; i += SNT) {
+                    const float v = val(i);
+                    if (v >= thr) { const float lp = v - mx - lZ; s += fabsf(-lp - H) <= mid ? __expf(lp) : 0.f; }
+                }
+                s = bsum(s, red);
+                if (s >= P.typical_p) hi = mid; else lo = mid;
+            }
+            // encode the typical band into the value test below via a second bound: keep v with
+            // |-(v - mx - lZ) - H| <= hi.  (applied in the draw loop)
+            thr = fmaxf(thr, -INFINITY);
+            // stash in shared for the draw
+            if (threadIdx.x == 0) { rv[0] = hi; rv[1] = H; rv[2] = lZ; }
+            __syncthreads();
+        }
+        // mirostat v2: keep tokens with surprise -log2 p <= mu
+        if (P.mirostat_tau > 0.f) {
+            const float lZ = __logf(Z);
+            // -log2(p) <= mu  <=>  v >= mx + lZ - mu*ln2
+            thr = fmaxf(thr, mx + lZ - P.mirostat_tau * 0.69314718f);
+            thr = fminf(thr, mx);  // always keep the argmax
+        }
+    }
+    const bool typ = !greedy && P.typical_p < 1.f && P.typical_p > 0.f;
+    float tb = 0.f, tH = 0.f, tlZ = 0.f;
+    if (typ) { tb = rv[0]; tH = rv[1]; tlZ = rv[2]; }
+    __syncthreads();
+    // 3. draw: argmax of v (+ Gumbel noise) over the kept set
+    float best = -INFINITY;
+    int bi = 0x7fffffff;
+    for (int i = threadIdx.x; i < V; i += SNT) {
+        const float v = val(i);
+        if (v < thr || v == -INFINITY) continue;
+        if (typ && fabsf(-(v - mx - tlZ) - tH) > tb && v < mx) continue;
+        const float sc = greedy ? v : v + gumbel(P.seed, (uint32_t)i);
+        if (sc > best || (sc == best && i < bi)) { best = sc; bi = i; }
+    }
+    // block argmax
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const float ob = __shfl_xor(best, o, 64);
+        const int oi = __shfl_xor(bi, o, 64);
+        if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+    }
+    if ((threadIdx.x & 63) == 0) { rv[threadIdx.x >> 6] = best; ri[threadIdx.x >> 6] = bi; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float b = rv[0];
+        int id = ri[0];
+        for (int w = 1; w < SNT / 64; ++w)
+            if (rv[w] > b || (rv[w] == b && ri[w] < id)) { b = rv[w]; id = ri[w]; }
+        if (id == 0x7fffffff) id = 0;
+        out_tok[row] = id;
+        rv[0] = (float)id;
+    }
+    __syncthreads();
+    if (out_logp) {
+        // log-prob of the chosen token under the tempered, truncated distribution
+        const int id = (int)rv[0];
+        float Z = 0.f;
+        for (int i = threadIdx.x; i < V; i += SNT) {
+            const float v = val(i);
+            if (v >= thr && v != -INFINITY) Z += __expf(v - mx);
+        }
+        Z = bsum(Z, red);
+        if (threadIdx.x == 0) out_logp[row] = val(id) - mx - __logf(fmaxf(Z, 1e-30f));
+    }
+}
+
+extern "C" int mxk_sample(float* logits, int ld, int B, int V, const SampleParams* params, const int* pen_tok,
+                          const int* pen_cnt, const float* pen_bias, const uint32_t* allow_mask, int mask_ld,
+                          int* out_tok, float* out_logp, hipStream_t st) {
+    if (B <= 0) return 0;
+    sample_kernel<<<B, SNT, 0, st>>>(logits, ld, V, params, pen_tok, pen_cnt, pen_bias, allow_mask, mask_ld, out_tok,
+                                     out_logp);
+    MXK_CHECK_LAUNCH();
+}
+
+extern "C" int mxk_sample_params_size() { return (int)sizeof(SampleParams); }
+
+// greedy argmax over rows (fast path used by the decode graph when every row is greedy)
+__global__ __launch_bounds__(1024) void argmax_kernel(const float* __restrict__ x, int ld, int V,
+                                                      int* __restrict__ out) {
+    __shared__ float rv[16];
+    __shared__ int ri[16];
+    const float* r = x + (size_t)blockIdx.x * ld;
+    float best = -INFINITY;
+    int bi = 0x7fffffff;
+    for (int i = threadIdx.x; i < V; i += 1024) {
+        const float v = r[i];
+        if (v > best) { best = v; bi = i; }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const float ob = __shfl_xor(best, o, 64);
+        const int oi = __shfl_xor(bi, o, 64);
+        if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+    }
+    if ((threadIdx.x & 63) == 0) { rv[threadIdx.x >> 6] = best; ri[threadIdx.x >> 6] = bi; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float b = rv[0];
+        int id = ri[0];
+        for (int w = 1; w < 16; ++w)
+            if (rv[w] > b || (rv[w] == b && ri[w] < id)) { b = rv[w]; id = ri[w]; }
+        out[blockIdx.x] = id == 0x7fffffff ? 0 : id;
+    }
+}
+
+extern "C" int mxk_argmax(const float* x, int ld, int B, int V, int* out, hipStream_t st) {
+    if (B <= 0) return 0;
+    argmax_kernel<<<B, 1024, 0, st>>>(x, ld, V, out);
+    MXK_CHECK_LAUNCH();
+}

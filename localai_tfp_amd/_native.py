@@ -1,0 +1,147 @@
+"""ctypes bindings for the in-tree native libraries (``_lib/libmxk.so``, ``_lib/libmxrt.so``).
+
+Every GPU op in :mod:`localai_tfp_amd.ops` goes through :func:`kcall`. On a machine with a GPU the
+kernel library is REQUIRED: if it is missing or fails to load, :func:`kernels` raises instead of
+falling back to eager PyTorch, so a GPU test can never pass on a silent fallback. The plain
+PyTorch implementations in ``ops`` are only used for CPU tensors (CI / CPU plumbing path).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+from pathlib import Path
+
+_LIBDIR = Path(__file__).resolve().parent / "_lib"
+_lock = threading.Lock()
+_kernels = None
+_runtime = None
+
+P = C.c_void_p
+I = C.c_int
+F = C.c_float
+SZ = C.c_size_t
+U64 = C.c_uint64
+
+# name -> argtypes (restype is always c_int = hipError_t of the launch)
+KERNEL_SIGS = {
+    "mxk_rmsnorm": [P, I, P, I, P, P, P, I, P, P, I, I, F, P],
+    "mxk_quant_q8": [P, I, P, P, I, I, P],
+    "mxk_layernorm": [P, I, P, I, P, P, P, P, P, I, I, I, F, P],
+    "mxk_groupnorm_nhwc": [P, P, P, P, I, I, I, I, F, I, P],
+    "mxk_qgemm_mfma": [I, I, I, I, P, I, P, P, I, I, I, I, P, I, P],
+    "mxk_qgemv": [I, I, P, P, P, P, I, I, I, P, I, P],
+    "mxk_dequant_rows": [I, P, P, P, I, I, P, P, I, P],
+    "mxk_rope_kv": [P, P, P, P, P, F, I, I, I, I, I, I, P, P, P, I, P],
+    "mxk_copy_blocks": [P, P, P, I, I, P],
+    "mxk_attn_decode": [P, I, P, P, P, I, P, I, I, I, I, I, F, I, I, P, I, P, P, P],
+    "mxk_attn_prefill": [P, P, P, P, I, P, P, I, P, P, I, I, I, I, F, P, P],
+    "mxk_attn_prefill_rows": [I, I],
+    "mxk_sample": [P, I, I, I, P, P, P, P, P, I, P, P, P],
+    "mxk_sample_params_size": [],
+    "mxk_argmax": [P, I, I, I, P, P],
+    "mxk_glu": [I, P, P, I, P, I, I, I, P],
+    "mxk_act_f32": [P, SZ, I, P],
+    "mxk_cast_f32_bf16": [P, I, P, I, I, I, P],
+    "mxk_gather_rows": [P, I, P, I, I, F, P, P],
+    "mxk_add_bias_f32": [P, I, P, I, I, P],
+    "mxk_select_rows_f32": [P, I, P, I, I, P, I, P],
+    "mxk_bf16_gemm": [P, I, P, I, P, I, I, I, I, I, P],
+    "mxk_conv2d_nhwc": [P, P, P, P, I, I, I, I, I, I, I, I, I, I, P],
+    "mxk_cosine_topk": [P, P, I, I, I, I, P, P, P],
+}
+
+HIP_ERRORS = {1: "hipErrorInvalidValue", 2: "hipErrorOutOfMemory", 98: "hipErrorInvalidDeviceFunction",
+              209: "hipErrorNoBinaryForGpu", 700: "hipErrorIllegalAddress", 719: "hipErrorLaunchFailure"}
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+def _load(name: str):
+    path = _LIBDIR / name
+    if not path.exists():
+        raise NativeError(
+            f"{path} is missing: build it with `python -m localai_tfp_amd._build` "
+            "(or __graft_entry__.build())")
+    return C.CDLL(str(path), mode=C.RTLD_GLOBAL)
+
+
+def kernels():
+    """Load libmxk.so (HIP kernels). Raises NativeError if it cannot be loaded."""
+    global _kernels
+    if _kernels is None:
+        with _lock:
+            if _kernels is None:
+                lib = _load("libmxk.so")
+                for n, sig in KERNEL_SIGS.items():
+                    fn = getattr(lib, n, None)
+                    if fn is None:
+                        continue
+                    fn.argtypes = sig
+                    fn.restype = C.c_int
+                _kernels = lib
+    return _kernels
+
+
+def runtime():
+    """Load libmxrt.so (host runtime: GGUF parser, block allocator, grammar, store)."""
+    global _runtime
+    if _runtime is None:
+        with _lock:
+            if _runtime is None:
+                _runtime = _load("libmxrt.so")
+                from . import _rt_sigs
+                _rt_sigs.bind(_runtime)
+    return _runtime
+
+
+def have_kernels() -> bool:
+    try:
+        kernels()
+        return True
+    except Exception:
+        return False
+
+
+def kcall(name: str, *args):
+    fn = getattr(kernels(), name, None)
+    if fn is None:
+        raise NativeError(f"{name} not exported by libmxk.so (stale build?)")
+    rc = fn(*args)
+    if rc != 0:
+        raise NativeError(f"{name} failed: {HIP_ERRORS.get(rc, rc)} ({rc})")
+    return rc
+
+
+def stream_ptr(device=None) -> int:
+    import torch
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def ptr(t) -> int | None:
+    """data pointer of a tensor (None passes through as a null pointer)."""
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def loaded_library_paths():
+    """Paths of the native libraries loaded into this process (for diagnostics / tests)."""
+    out = []
+    for lib in (_kernels, _runtime):
+        if lib is not None:
+            out.append(lib._name)
+    return out
+
+
+def gpu_required() -> bool:
+    """True when a GPU is present: then native kernels are mandatory (no eager fallback)."""
+    if os.environ.get("MX_ALLOW_CPU_ONLY"):
+        return False
+    try:
+        import torch
+        return torch.cuda.is_available()
+    except Exception:
+        return False

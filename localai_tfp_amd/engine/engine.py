@@ -1,0 +1,469 @@
+"""LLM serving engine: the MI355X worker's replacement for the reference's llama.cpp slot server
+(backend/cpp/llama/grpc-server.cpp). One engine drives one model replica (one GPU, or one TP group).
+
+Loop (one iteration = one `step()`, cf. `llama_server_queue::start_loop` + `update_slots`,
+utils.hpp:255, grpc-server.cpp:1639):
+    schedule  -> paged continuous batch (decode rows first, then prefill chunks)
+    forward   -> decode-only steps replay a captured hipGraph per batch-size bucket
+    sample    -> fused on-GPU sampler (greedy rows: argmax kernel inside the graph)
+    process   -> stop tokens / stop strings / length, incremental detokenisation, timings
+
+Requests arrive from any thread through `submit()`; each gets a `RequestHandle` whose queue
+receives `StepOutput`s (the reference's task/result queues, utils.hpp:192-409).
+"""
+from __future__ import annotations
+
+import logging
+import queue
+import threading
+import time
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from ..models.llama import ForwardBatch, LlamaModel, Workspace
+from ..ops.sampling import SamplerBatch
+from .kv_cache import KVCache, make_block_manager
+from .scheduler import Scheduler, SchedulerOutput
+from .sequence import Request, Sequence, Status, StepOutput
+
+log = logging.getLogger("localai_tfp_amd.engine")
+
+
+@dataclass
+class EngineConfig:
+    max_num_seqs: int = 256
+    max_batched_tokens: int = 2048
+    max_model_len: int = 8192
+    block_size: int = 16
+    num_blocks: int | None = None  # None -> size from free HBM
+    kv_mem_fraction: float = 0.85
+    enable_prefix_cache: bool = True
+    use_graphs: bool = True
+    graph_buckets: tuple = (1, 2, 4, 8, 16, 32, 48, 64, 96, 128, 160, 192, 224, 256)
+    attn_part_size: int = 512
+    prefill_bf16_cache: bool = False
+
+
+class RequestHandle:
+    def __init__(self, rid: int):
+        self.rid = rid
+        self.q: queue.Queue[StepOutput] = queue.Queue()
+        self.done = False
+
+    def __iter__(self):
+        while True:
+            o = self.q.get()
+            yield o
+            if o.finished:
+                return
+
+
+class DecodeGraph:
+    """Static-input hipGraph of one decode step (forward + greedy argmax) for a batch bucket."""
+
+    def __init__(self, engine: "LLMEngine", B: int):
+        e = engine
+        dev = e.device
+        self.B = B
+        self.maxb = e.max_blocks_per_seq
+        self.tokens = torch.zeros(B, dtype=torch.int32, device=dev)
+        self.positions = torch.zeros(B, dtype=torch.int32, device=dev)
+        self.slots = torch.full((B,), -1, dtype=torch.int32, device=dev)
+        self.bt = torch.zeros((B, self.maxb), dtype=torch.int32, device=dev)
+        self.lens = torch.ones(B, dtype=torch.int32, device=dev)
+        self.lidx = torch.arange(B, dtype=torch.int32, device=dev)
+        self.argmax = torch.zeros(B, dtype=torch.int32, device=dev)
+        self.fb = ForwardBatch(self.tokens, self.positions, self.slots, self.lidx, n_decode=B,
+                               dec_block_tables=self.bt, dec_seq_lens=self.lens, dec_max_len=e.cfg.max_model_len)
+        self.graph = None
+        self.logits = None
+
+    def capture(self, engine: "LLMEngine"):
+        from .. import _native as N
+        s = torch.cuda.Stream(device=engine.device)
+        s.wait_stream(torch.cuda.current_stream(engine.device))
+        with torch.cuda.stream(s):
+            for _ in range(2):  # warm-up (allocations, lazy init) outside capture
+                lg = engine.model.forward(self.fb, engine.kv, engine.ws)
+                N.kcall("mxk_argmax", lg.data_ptr(), lg.stride(0), self.B, lg.shape[1], self.argmax.data_ptr(),
+                        N.stream_ptr())
+        torch.cuda.current_stream(engine.device).wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            self.logits = engine.model.forward(self.fb, engine.kv, engine.ws)
+            N.kcall("mxk_argmax", self.logits.data_ptr(), self.logits.stride(0), self.B, self.logits.shape[1],
+                    self.argmax.data_ptr(), N.stream_ptr())
+        self.graph = g
+
+    def run(self, tokens, positions, slots, bt, lens, n: int):
+        self.tokens[:n].copy_(tokens, non_blocking=True)
+        self.positions[:n].copy_(positions, non_blocking=True)
+        self.slots[:n].copy_(slots, non_blocking=True)
+        self.bt[:n, : bt.shape[1]].copy_(bt, non_blocking=True)
+        self.lens[:n].copy_(lens, non_blocking=True)
+        if n < self.B:
+            self.slots[n:].fill_(-1)
+            self.lens[n:].fill_(1)
+            self.bt[n:].zero_()
+        self.graph.replay()
+        return self.logits[:n], self.argmax[:n]
+
+
+class LLMEngine:
+    def __init__(self, model: LlamaModel, tokenizer, cfg: EngineConfig | None = None):
+        self.model = model
+        self.tok = tokenizer
+        self.cfg = cfg or EngineConfig()
+        self.device = model.device
+        mc = model.cfg
+        c = self.cfg
+        c.max_model_len = min(c.max_model_len, max(mc.ctx_train, 256)) if c.max_model_len else mc.ctx_train
+        self.max_blocks_per_seq = (c.max_model_len + c.block_size - 1) // c.block_size
+        nb = c.num_blocks or KVCache.auto_num_blocks(mc.n_layers, model.n_kv, c.block_size, mc.head_dim, self.device,
+                                                     c.kv_mem_fraction)
+        self.kv = KVCache(mc.n_layers, nb, model.n_kv, c.block_size, mc.head_dim, self.device)
+        self.bm = make_block_manager(nb, c.block_size, c.enable_prefix_cache)
+        self.sched = Scheduler(self.bm, c.block_size, c.max_num_seqs, c.max_batched_tokens, c.max_model_len)
+        max_parts = max(1, -(-c.max_model_len // c.attn_part_size))
+        self.ws = Workspace(mc, max(c.max_batched_tokens, c.max_num_seqs), c.max_num_seqs, self.device,
+                            model.tp_size, max_parts)
+        self.sampler = SamplerBatch(self.device)
+        self.handles: dict[int, RequestHandle] = {}
+        self.seqs: dict[int, Sequence] = {}
+        self._inbox: queue.Queue = queue.Queue()
+        self._cv = threading.Condition()
+        self._thread: threading.Thread | None = None
+        self._stop = False
+        self.graphs: dict[int, DecodeGraph] = {}
+        self.use_graphs = c.use_graphs and self.device.type == "cuda"
+        self.eos_ids = set(getattr(tokenizer, "eos_token_ids", []) or [])
+        self.stats = dict(steps=0, decode_tokens=0, prefill_tokens=0, graph_steps=0, preemptions=0,
+                          busy_s=0.0, prompt_tokens_total=0, gen_tokens_total=0, cached_tokens_total=0)
+        self.last_metrics = {}
+        if c.prefill_bf16_cache and self.device.type == "cuda":
+            model.enable_prefill_bf16_cache()
+
+    # ------------------------------------------------------------------ request API
+    def submit(self, req: Request) -> RequestHandle:
+        h = RequestHandle(req.rid)
+        self.handles[req.rid] = h
+        self._inbox.put(("add", req))
+        with self._cv:
+            self._cv.notify()
+        return h
+
+    def abort(self, rid: int):
+        self._inbox.put(("abort", rid))
+        with self._cv:
+            self._cv.notify()
+
+    def _drain_inbox(self):
+        while True:
+            try:
+                kind, x = self._inbox.get_nowait()
+            except queue.Empty:
+                return
+            if kind == "add":
+                req: Request = x
+                max_prompt = self.cfg.max_model_len - 1
+                if len(req.prompt_ids) > max_prompt:
+                    # reference truncation rule (grpc-server.cpp:1793-1814): keep the head (n_keep)
+                    # and the back half of what remains
+                    ids = req.prompt_ids
+                    n_keep = min(getattr(req, "n_keep", 0) or 0, max_prompt // 2)
+                    erased = len(ids) - max_prompt
+                    req.prompt_ids = ids[:n_keep] + ids[n_keep + erased:]
+                if not req.prompt_ids:
+                    req.prompt_ids = [getattr(self.tok, "bos_token_id", 0) or 0]
+                s = Sequence(req, self.tok)
+                self.seqs[req.rid] = s
+                self.sched.add(s)
+            else:
+                s = self.sched.abort(x)
+                if s is not None:
+                    self._finish(s, "abort")
+
+    # ------------------------------------------------------------------ loop
+    def start(self):
+        if self._thread is None:
+            self._thread = threading.Thread(target=self._loop, name="llm-engine", daemon=True)
+            self._thread.start()
+
+    def shutdown(self):
+        self._stop = True
+        with self._cv:
+            self._cv.notify_all()
+        if self._thread:
+            self._thread.join(timeout=10)
+
+    def _loop(self):
+        if self.device.type == "cuda":
+            torch.cuda.set_device(self.device)
+        while not self._stop:
+            self._drain_inbox()
+            if not self.sched.has_work():
+                with self._cv:
+                    self._cv.wait(timeout=0.05)
+                continue
+            try:
+                self.step()
+            except Exception as ex:  # fail every in-flight request loudly, keep the worker alive
+                log.exception("engine step failed")
+                for s in list(self.sched.running) + list(self.sched.waiting):
+                    self.sched.abort(s.rid)
+                    self._finish(s, f"error:{type(ex).__name__}: {ex}")
+
+    def run_until_done(self, max_steps: int = 1 << 30):
+        """Synchronous driver (tests / bench): step until every submitted request finished."""
+        self._drain_inbox()
+        n = 0
+        while self.sched.has_work() and n < max_steps:
+            self.step()
+            self._drain_inbox()
+            n += 1
+        return n
+
+    # ------------------------------------------------------------------ one iteration
+    def step(self):
+        t0 = time.perf_counter()
+        so = self.sched.schedule()
+        for s in so.preempted:
+            if s.status == Status.FINISHED:
+                self._finish(s, s.finish_reason or "error")
+            else:
+                self.stats["preemptions"] += 1
+        if so.empty:
+            return
+        toks, lps = self._forward_and_sample(so)
+        self.sched.commit(so)
+        self._process(so, toks, lps)
+        dt = time.perf_counter() - t0
+        st = self.stats
+        st["steps"] += 1
+        st["decode_tokens"] += len(so.decode)
+        st["prefill_tokens"] += sum(p.n for p in so.prefill)
+        st["busy_s"] += dt
+
+    def _graph_for(self, n: int) -> DecodeGraph | None:
+        if not self.use_graphs:
+            return None
+        b = next((x for x in self.cfg.graph_buckets if x >= n and x <= self.cfg.max_num_seqs), None)
+        if b is None:
+            return None
+        g = self.graphs.get(b)
+        if g is None:
+            g = DecodeGraph(self, b)
+            try:
+                g.capture(self)
+            except Exception:
+                log.exception("hipGraph capture failed for bucket %d; running eager", b)
+                self.use_graphs = False
+                return None
+            self.graphs[b] = g
+        return g
+
+    def _forward_and_sample(self, so: SchedulerOutput):
+        dev = self.device
+        bs = self.cfg.block_size
+        dec = so.decode
+        pf = so.prefill
+        nd = len(dec)
+        T = so.num_tokens
+        tokens = np.empty(T, np.int32)
+        positions = np.empty(T, np.int32)
+        slots = np.empty(T, np.int32)
+        i = 0
+        for it in dec:
+            s = it.seq
+            p = s.num_computed
+            tokens[i] = s.output_ids[-1] if s.output_ids else s.prompt_ids[-1]
+            positions[i] = p
+            slots[i] = s.blocks[p // bs] * bs + p % bs
+            i += 1
+        for it in pf:
+            s = it.seq
+            ids = s.all_ids
+            r = np.arange(it.start, it.start + it.n)
+            tokens[i:i + it.n] = ids[it.start:it.start + it.n]
+            positions[i:i + it.n] = r
+            blk = np.asarray(s.blocks, np.int32)
+            slots[i:i + it.n] = blk[r // bs] * bs + r % bs
+            i += it.n
+        sample_items = [it for it in dec] + [it for it in pf if it.sample]
+        # rows whose logits are needed: decode rows + last row of finishing prefills
+        lidx = list(range(nd))
+        off = nd
+        for it in pf:
+            if it.sample:
+                lidx.append(off + it.n - 1)
+            off += it.n
+        params = [it.seq.params for it in sample_items]
+        greedy_only = all(p.greedy and not p.logit_bias and p.repeat_penalty == 1.0 and not p.presence_penalty
+                          and not p.frequency_penalty for p in params) and not any(it.seq.grammar for it in sample_items)
+        # ---- decode-only fast path: graph replay ----
+        if not pf and nd and self.use_graphs:
+            g = self._graph_for(nd)
+            if g is not None:
+                maxb = max(len(it.seq.blocks) for it in dec)
+                bt = np.zeros((nd, maxb), np.int32)
+                lens = np.empty(nd, np.int32)
+                for k, it in enumerate(dec):
+                    bt[k, :len(it.seq.blocks)] = it.seq.blocks
+                    lens[k] = it.seq.num_computed + 1
+                h = torch.from_numpy(np.concatenate([tokens, positions, slots, lens, bt.reshape(-1)])).pin_memory()
+                d = h.to(dev, non_blocking=True)
+                logits, am = g.run(d[:nd], d[nd:2 * nd], d[2 * nd:3 * nd], d[4 * nd:].view(nd, maxb), d[3 * nd:4 * nd], nd)
+                self.stats["graph_steps"] += 1
+                if greedy_only:
+                    return am.cpu().tolist(), None
+                return self._sample(logits, sample_items)
+        # ---- eager path ----
+        fb = self._build_fb(so, tokens, positions, slots, lidx)
+        logits = self.model.forward(fb, self.kv, self.ws)
+        if not sample_items:
+            return [], None
+        return self._sample(logits, sample_items)
+
+    def _build_fb(self, so, tokens, positions, slots, lidx) -> ForwardBatch:
+        dev = self.device
+        dec, pf = so.decode, so.prefill
+        nd = len(dec)
+        arrs = {"tokens": tokens, "positions": positions, "slots": slots, "lidx": np.asarray(lidx, np.int32)}
+        if nd:
+            maxb = max(len(it.seq.blocks) for it in dec)
+            bt = np.zeros((nd, maxb), np.int32)
+            lens = np.empty(nd, np.int32)
+            for k, it in enumerate(dec):
+                bt[k, :len(it.seq.blocks)] = it.seq.blocks
+                lens[k] = it.seq.num_computed + 1
+            arrs["dec_bt"] = bt
+            arrs["dec_lens"] = lens
+        if pf:
+            maxb = max(len(it.seq.blocks) for it in pf)
+            bt = np.zeros((len(pf), maxb), np.int32)
+            cu = np.zeros(len(pf) + 1, np.int32)
+            ctx = np.empty(len(pf), np.int32)
+            for k, it in enumerate(pf):
+                bt[k, :len(it.seq.blocks)] = it.seq.blocks
+                cu[k + 1] = cu[k] + it.n
+                ctx[k] = it.start + it.n
+            arrs["pf_bt"] = bt
+            arrs["pf_cu"] = cu
+            arrs["pf_ctx"] = ctx
+        t = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev, non_blocking=True) for k, v in arrs.items()}
+        fb = ForwardBatch(t["tokens"], t["positions"], t["slots"], t["lidx"], n_decode=nd)
+        if nd:
+            fb.dec_block_tables, fb.dec_seq_lens = t["dec_bt"], t["dec_lens"]
+            fb.dec_max_len = int(arrs["dec_lens"].max())
+        if pf:
+            fb.pf_block_tables, fb.pf_cu_q, fb.pf_ctx_lens = t["pf_bt"], t["pf_cu"], t["pf_ctx"]
+            fb.pf_q_lens_host = [it.n for it in pf]
+            fb.pf_ctx_lens_host = [it.start + it.n for it in pf]
+        return fb
+
+    def _sample(self, logits, items):
+        params = [it.seq.params for it in items]
+        hist = [it.seq.all_ids for it in items]
+        steps = [len(it.seq.output_ids) for it in items]
+        mask = None
+        if any(it.seq.grammar for it in items):
+            mask = self._grammar_mask(items, logits.shape[1])
+        mus = [it.seq.mirostat_mu for it in items] if any(p.mirostat == 2 for p in params) else None
+        tok, lp = self.sampler.sample(logits, params, hist, steps, mask, mus)
+        return tok.cpu().tolist(), (lp.cpu().tolist() if lp is not None else None)
+
+    def _grammar_mask(self, items, V):
+        words = (V + 31) // 32
+        m = np.full((len(items), words), 0xFFFFFFFF, np.uint32)
+        for k, it in enumerate(items):
+            g = it.seq.grammar
+            if g is not None:
+                m[k] = g.allowed_mask(V)
+        t = torch.from_numpy(m.view(np.int32))
+        return t.to(self.device) if self.device.type == "cuda" else t
+
+    # ------------------------------------------------------------------ post-processing
+    def _process(self, so: SchedulerOutput, toks, lps):
+        now = time.perf_counter()
+        items = [it for it in so.decode] + [it for it in so.prefill if it.sample]
+        for k, it in enumerate(items):
+            s = it.seq
+            if s.status == Status.FINISHED:
+                continue
+            t = int(toks[k])
+            lp = lps[k] if lps is not None else None
+            if s.t_first_token is None:
+                s.t_first_token = now
+            if s.grammar is not None:
+                s.grammar.accept(t)
+            if s.params.mirostat == 2 and lp is not None:
+                # mu <- mu - eta * (surprise - tau)  (surprise in bits)
+                s.mirostat_mu -= s.params.mirostat_eta * (-lp / 0.6931471805599453 - s.params.mirostat_tau)
+            s.append_token(t, lp)
+            reason = None
+            if (t in self.eos_ids or t in s.req.stop_token_ids) and not s.params.ignore_eos:
+                reason = "stop"
+                s.output_ids.pop()  # EOS is not part of the visible output
+                s._pending_ids.pop() if s._pending_ids else None
+            elif len(s.output_ids) >= s.req.max_tokens:
+                reason = "length"
+            elif s.total_len >= self.cfg.max_model_len:
+                reason = "length"
+            elif s.grammar is not None and s.grammar.is_done():
+                reason = "stop"
+            text, hit = s.flush_text(final=reason is not None)
+            if hit:
+                reason = "stop"
+            if reason:
+                self.sched.finish(s, reason)
+            self._emit(s, text, reason)
+
+    def _emit(self, s: Sequence, text: str, reason: str | None):
+        h = self.handles.get(s.rid)
+        ids, lp = s.take_pending()
+        o = StepOutput(s.rid, text, ids, lp, reason is not None, reason)
+        if reason is not None:
+            self._fill_usage(s, o)
+            self.handles.pop(s.rid, None)
+            self.seqs.pop(s.rid, None)
+            st = self.stats
+            st["prompt_tokens_total"] += len(s.prompt_ids)
+            st["gen_tokens_total"] += len(s.output_ids)
+            st["cached_tokens_total"] += s.num_cached
+        if h is not None:
+            h.q.put(o)
+
+    def _fill_usage(self, s: Sequence, o: StepOutput):
+        o.prompt_tokens = len(s.prompt_ids)
+        o.completion_tokens = len(s.output_ids)
+        o.cached_tokens = s.num_cached
+        t_first = s.t_first_token or time.perf_counter()
+        o.ttft_ms = (t_first - s.t_arrival) * 1e3
+        o.t_prompt_ms = (t_first - (s.t_first_sched or s.t_arrival)) * 1e3
+        o.t_gen_ms = ((s.t_finish or time.perf_counter()) - t_first) * 1e3
+        self.last_metrics = dict(tokens_per_second=(o.completion_tokens / max(o.t_gen_ms, 1e-3) * 1e3),
+                                 tokens_generated=o.completion_tokens, prompt_tokens_processed=o.prompt_tokens)
+
+    def _finish(self, s: Sequence, reason: str):
+        if s.status != Status.FINISHED:
+            self.sched.finish(s, reason)
+        s.finish_reason = reason
+        self._emit(s, "", reason)
+
+    # ------------------------------------------------------------------ convenience
+    def generate(self, prompt_ids, params=None, max_tokens=32, stop=None) -> StepOutput:
+        from ..ops.sampling import SamplingParams
+        req = Request(list(prompt_ids), params or SamplingParams(temperature=0.0), max_tokens, stop or [])
+        h = self.submit(req)
+        if self._thread is None:
+            self.run_until_done()
+        text, ids = "", []
+        last = None
+        for o in h:
+            text += o.text
+            ids += o.token_ids
+            last = o
+        last.text, last.token_ids = text, ids
+        return last

@@ -1,0 +1,333 @@
+"""Llama-family decoder (llama / llama3 / mistral / qwen2 / tinyllama ...) on the MI355X kernels.
+
+This is the compute graph llama.cpp builds inside `llama_decode` for the reference worker
+(grpc-server.cpp:2002), re-expressed as a fixed sequence of fused HIP kernels per layer:
+
+    rmsnorm(h) -> {bf16 | q8}            (norm.hip)
+    QKV  = x W_qkv^T  -> fp32            (qgemm.hip, fused Q|K|V weight, split-K atomics)
+    rope + KV append (paged)             (rope_kv.hip)
+    attention: decode rows | prefill rows (attention.hip, paged GQA)
+    h += attn W_o^T                       (qgemm.hip EPI_ADD_F32 straight into the residual)
+    rmsnorm(h)
+    act = silu(x W_g^T) * (x W_u^T)       (qgemm.hip EPI_SWIGLU on 16-row interleaved gate|up)
+    h += act W_d^T
+    logits = rmsnorm(h[last]) W_out^T     (only rows that need sampling)
+
+Decode batches of <= 4 tokens take the int8-dot GEMV path (norm kernels emit q8 directly);
+larger batches the dequant-MFMA path. Tensor parallelism (parallel/tp.py) shards heads / FFN
+columns and all-reduces the residual after the row-parallel projections.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+from ..formats.gguf import QType
+from ..ops import core as K
+from ..ops.linear import (EPI_ADD_F32, EPI_BF16, EPI_F32, EPI_SWIGLU, QWeight, concat_rows, interleave_gate_up,
+                          qmatmul)
+from .config import LlamaConfig
+
+GEMV_MAX_M = 4
+
+
+@dataclass
+class LlamaLayer:
+    attn_norm: torch.Tensor
+    ffn_norm: torch.Tensor
+    qkv_parts: list  # [QWeight] Q|K|V fused where the quant types agree (Q4_K_M: v may be Q6_K)
+    bqkv: torch.Tensor | None
+    wo: QWeight
+    wgu: QWeight | None  # interleaved gate|up
+    wg: QWeight | None
+    wu: QWeight | None
+    wd: QWeight
+
+
+@dataclass
+class ForwardBatch:
+    """Flattened scheduler step. Decode tokens (one per sequence) come first, then prefill chunks."""
+    tokens: torch.Tensor  # int32 [T]
+    positions: torch.Tensor  # int32 [T]
+    slots: torch.Tensor  # int32 [T] flat cache slot (-1 = don't store)
+    logits_idx: torch.Tensor  # int32 [S_out] rows of T whose logits are needed
+    n_decode: int = 0
+    dec_block_tables: torch.Tensor | None = None  # [n_decode, maxb]
+    dec_seq_lens: torch.Tensor | None = None  # [n_decode] context length incl. the new token
+    dec_max_len: int = 0
+    pf_block_tables: torch.Tensor | None = None  # [S_p, maxb]
+    pf_cu_q: torch.Tensor | None = None  # [S_p + 1] offsets relative to the first prefill token
+    pf_ctx_lens: torch.Tensor | None = None  # [S_p]
+    pf_q_lens_host: list = field(default_factory=list)
+    pf_ctx_lens_host: list = field(default_factory=list)
+    want_hidden: bool = False  # embeddings: return normalised hidden rows instead of logits
+
+    @property
+    def T(self) -> int:
+        return int(self.tokens.shape[0])
+
+
+class Workspace:
+    """Per-engine scratch buffers sized for the largest step; forward() only takes views, so the
+    same storage is reused step to step and hipGraph capture sees static addresses."""
+
+    def __init__(self, cfg: LlamaConfig, max_tokens: int, max_seqs: int, device, tp_size: int = 1,
+                 max_parts: int = 64):
+        dev = torch.device(device)
+        H, F = cfg.hidden, cfg.ffn // tp_size
+        qd, kvd = cfg.q_dim // tp_size, cfg.kv_dim // tp_size
+        T = max_tokens
+        self.max_tokens, self.max_seqs = T, max_seqs
+        self.h = torch.empty((T, H), dtype=torch.float32, device=dev)
+        self.xb = torch.empty((T, max(H, F, qd)), dtype=torch.bfloat16, device=dev)
+        kmax = max(H, F, qd)
+        self.xq = torch.empty((T * kmax,), dtype=torch.int8, device=dev)
+        self.xds = torch.empty((T * kmax // 32 * 2,), dtype=torch.float32, device=dev)
+        self.qkv = torch.empty((T, qd + 2 * kvd), dtype=torch.float32, device=dev)
+        self.q = torch.empty((T, qd), dtype=torch.bfloat16, device=dev)
+        self.attn = torch.empty((T, qd), dtype=torch.bfloat16, device=dev)
+        self.act = torch.empty((T, F), dtype=torch.bfloat16, device=dev)
+        self.act2 = torch.empty((T, F), dtype=torch.bfloat16, device=dev) if dev.type == "cpu" else None
+        self.hs = torch.empty((max_seqs, H), dtype=torch.float32, device=dev)
+        self.logits = torch.empty((max_seqs, cfg.vocab), dtype=torch.float32, device=dev)
+        nh = cfg.n_heads // tp_size
+        self.part_ml = torch.empty((max_seqs * nh * max_parts, 2), dtype=torch.float32, device=dev)
+        self.part_o = torch.empty((max_seqs * nh * max_parts, cfg.head_dim), dtype=torch.float32, device=dev)
+
+    def q8(self, M: int, K_: int):
+        return self.xq[: M * K_].view(M, K_), self.xds[: M * K_ // 16].view(M, K_ // 32, 2)
+
+
+class LlamaModel:
+    def __init__(self, cfg: LlamaConfig, device="cpu", tp_rank: int = 0, tp_size: int = 1, tp_group=None):
+        self.cfg = cfg
+        self.device = torch.device(device)
+        self.tp_rank, self.tp_size, self.tp_group = tp_rank, tp_size, tp_group
+        self.layers: list[LlamaLayer] = []
+        self.tok_embd: QWeight | torch.Tensor | None = None
+        self.out_norm: torch.Tensor | None = None
+        self.lm_head: QWeight | None = None
+        rot = cfg.rope_dim
+        inv, af = K.rope_inv_freq(rot, cfg.rope_base, cfg.rope_scale, cfg.rope_scaling, cfg.rope_orig_ctx,
+                                  llama3=cfg.rope_llama3, freq_factors=cfg.extra.get("rope_freqs"))
+        self.inv_freq = inv.to(self.device)
+        self.attn_factor = af
+        self.scale = 1.0 / math.sqrt(cfg.head_dim)
+        self.n_heads = cfg.n_heads // tp_size
+        self.n_kv = max(1, cfg.n_kv_heads // tp_size)
+
+    # ------------------------------------------------------------------ loading
+    @classmethod
+    def load(cls, cfg: LlamaConfig, get_tensor, device="cpu", tp_rank=0, tp_size=1, tp_group=None,
+             fuse: bool = True, progress=None) -> "LlamaModel":
+        """get_tensor(name) -> (raw ndarray, qtype, ggml_shape) or None."""
+        from ..parallel import tp as TP
+        m = cls(cfg, device, tp_rank, tp_size, tp_group)
+        dev = m.device
+
+        def f32(name):
+            t = get_tensor(name)
+            if t is None:
+                return None
+            raw, qt, shape = t
+            from ..ops.quant import dequantize
+            return torch.from_numpy(np.ascontiguousarray(dequantize(raw, qt, shape)).reshape(-1).copy()).to(dev)
+
+        def qw(name, split=None):
+            t = get_tensor(name)
+            if t is None:
+                return None
+            raw, qt, shape = t
+            K_, N_ = int(shape[0]), int(np.prod(shape[1:]))
+            raw = np.asarray(raw).view(np.uint8).reshape(N_, -1)  # ggml bytes, one row per output
+            if tp_size > 1 and split is not None:
+                raw, N_, K_ = TP.shard_raw(raw, qt, N_, K_, split, tp_rank, tp_size, cfg)
+            return QWeight.from_ggml(raw, qt, N_, K_, dev, name)
+
+        hd = cfg.head_dim
+        for i in range(cfg.n_layers):
+            p = f"blk.{i}."
+            wq = qw(p + "attn_q.weight", ("col_heads", cfg.n_heads, hd))
+            wk = qw(p + "attn_k.weight", ("col_heads", cfg.n_kv_heads, hd))
+            wv = qw(p + "attn_v.weight", ("col_heads", cfg.n_kv_heads, hd))
+            bias = None
+            if cfg.qkv_bias:
+                bq, bk, bv = f32(p + "attn_q.bias"), f32(p + "attn_k.bias"), f32(p + "attn_v.bias")
+                if bq is not None:
+                    if tp_size > 1:
+                        bq, bk, bv = (TP.shard_vec(b, hd * n, tp_rank, tp_size) for b, n in
+                                      ((bq, cfg.n_heads), (bk, cfg.n_kv_heads), (bv, cfg.n_kv_heads)))
+                    bias = torch.cat([bq, bk, bv]).float().contiguous()
+            parts = [[wq]]
+            for w in (wk, wv):
+                if fuse and w.qtype == parts[-1][-1].qtype and w.K == parts[-1][-1].K:
+                    parts[-1].append(w)
+                else:
+                    parts.append([w])
+            qkv_parts = [g[0] if len(g) == 1 else concat_rows(g, p + "attn_qkv") for g in parts]
+            wg = qw(p + "ffn_gate.weight", ("col", cfg.ffn))
+            wu = qw(p + "ffn_up.weight", ("col", cfg.ffn))
+            wgu = interleave_gate_up(wg, wu, p + "ffn_gate_up") if fuse else None
+            layer = LlamaLayer(
+                attn_norm=f32(p + "attn_norm.weight").float(),
+                ffn_norm=f32(p + "ffn_norm.weight").float(),
+                qkv_parts=qkv_parts, bqkv=bias,
+                wo=qw(p + "attn_output.weight", ("row", cfg.q_dim)),
+                wgu=wgu, wg=None if wgu is not None else wg, wu=None if wgu is not None else wu,
+                wd=qw(p + "ffn_down.weight", ("row", cfg.ffn)),
+            )
+            m.layers.append(layer)
+            if progress:
+                progress(i + 1, cfg.n_layers)
+        emb = get_tensor("token_embd.weight")
+        raw, qt, shape = emb
+        m.tok_embd = QWeight.from_ggml(np.asarray(raw).view(np.uint8).reshape(int(shape[1]), -1), qt,
+                                       int(shape[1]), int(shape[0]), dev, "token_embd")
+        m.out_norm = f32("output_norm.weight").float()
+        head = get_tensor("output.weight")
+        if head is None:
+            m.lm_head = m.tok_embd
+            cfg.tie_embeddings = True
+        else:
+            m.lm_head = qw("output.weight")
+        return m
+
+    def weight_bytes(self) -> int:
+        n = 0
+        for L in self.layers:
+            for w in (*L.qkv_parts, L.wo, L.wgu, L.wg, L.wu, L.wd):
+                if w is not None:
+                    n += w.nbytes()
+        n += self.lm_head.nbytes()
+        if self.tok_embd is not self.lm_head:
+            n += self.tok_embd.nbytes()
+        return n
+
+    def enable_prefill_bf16_cache(self):
+        for L in self.layers:
+            for w in (*L.qkv_parts, L.wo, L.wgu, L.wg, L.wu, L.wd):
+                if w is not None:
+                    w.build_bf16_cache()
+
+    # ------------------------------------------------------------------ forward
+    def embed(self, tokens: torch.Tensor, out: torch.Tensor):
+        E = self.tok_embd
+        if E.device.type == "cpu" or not E.is_quant:
+            if E.device.type == "cpu":
+                out.copy_(E.dense_f32()[tokens.long()] * self.cfg.embed_scale)
+            else:
+                K.gather_rows(E.data, tokens, out, self.cfg.embed_scale)
+            return out
+        from .. import _native as N
+        N.kcall("mxk_dequant_rows", int(E.qtype), E.data.data_ptr(), N.ptr(E.dplane), tokens.data_ptr(),
+                tokens.numel(), E.K, None, out.data_ptr(), out.stride(0), N.stream_ptr())
+        if self.cfg.embed_scale != 1.0:
+            out.mul_(self.cfg.embed_scale)
+        return out
+
+    def _allreduce(self, t: torch.Tensor):
+        if self.tp_size > 1:
+            from ..parallel import tp as TP
+            TP.all_reduce_(t, self.tp_group)
+
+    def forward(self, fb: ForwardBatch, kv, ws: Workspace) -> torch.Tensor:
+        cfg = self.cfg
+        T = fb.T
+        H = cfg.hidden
+        D = cfg.head_dim
+        Hq, Hkv = self.n_heads, self.n_kv
+        qd, kvd = Hq * D, Hkv * D
+        F = self.layers[0].wd.K if self.layers else 0
+        eps = cfg.rms_eps
+        gemv = T <= GEMV_MAX_M and self.device.type == "cuda"
+        nd = fb.n_decode
+        h = ws.h[:T]
+        self.embed(fb.tokens, h)
+        xb = ws.xb[:T, :H]
+        for li, L in enumerate(self.layers):
+            kc, vc = kv.layer(li)
+            # ---- attention block ----
+            if gemv:
+                xq, xds = ws.q8(T, H)
+                K.rmsnorm(h, L.attn_norm, eps, out_q8=(xq, xds))
+            else:
+                K.rmsnorm(h, L.attn_norm, eps, out_bf16=xb)
+                xq = xds = None
+            qkv = ws.qkv[:T]
+            if not gemv:
+                qkv.zero_()
+            off = 0
+            for w in L.qkv_parts:
+                sl = qkv[:, off:off + w.N] if len(L.qkv_parts) > 1 else qkv
+                if gemv:
+                    qmatmul(w, None, EPI_F32, sl, xq=xq, xds=xds)
+                else:
+                    qmatmul(w, xb, EPI_F32, sl, out_zeroed=True)
+                off += w.N
+            q = ws.q[:T]
+            K.rope_kv(qkv, L.bqkv, fb.positions, fb.slots, self.inv_freq, self.attn_factor, Hq, Hkv, D,
+                      cfg.rope_dim, cfg.neox, q.view(T, Hq, D), kc, vc, kv.block_size)
+            attn = ws.attn[:T]
+            if nd:
+                K.attn_decode(q[:nd].view(nd, Hq, D), kc, vc, fb.dec_block_tables, fb.dec_seq_lens, self.scale,
+                              attn[:nd].view(nd, Hq, D), max_seq_len=fb.dec_max_len or None,
+                              workspace=(ws.part_ml, ws.part_o))
+            if T > nd:
+                K.attn_prefill(q[nd:].view(T - nd, Hq, D), kc, vc, fb.pf_block_tables, fb.pf_cu_q, fb.pf_ctx_lens,
+                               self.scale, attn[nd:].view(T - nd, Hq, D), fb.pf_q_lens_host, fb.pf_ctx_lens_host)
+            if self.tp_size > 1 and self.tp_rank != 0:
+                h.zero_()
+            if gemv:
+                aq, ads = ws.q8(T, qd)
+                K.quant_q8(attn, aq, ads)
+                qmatmul(L.wo, None, EPI_ADD_F32, h, xq=aq, xds=ads)
+            else:
+                qmatmul(L.wo, attn, EPI_ADD_F32, h)
+            self._allreduce(h)
+            # ---- FFN block ----
+            if gemv:
+                xq, xds = ws.q8(T, H)
+                K.rmsnorm(h, L.ffn_norm, eps, out_q8=(xq, xds))
+            else:
+                K.rmsnorm(h, L.ffn_norm, eps, out_bf16=xb)
+            act = ws.act[:T]
+            if L.wgu is not None:
+                if gemv:
+                    qmatmul(L.wgu, None, EPI_SWIGLU, act, xq=xq, xds=xds)
+                else:
+                    qmatmul(L.wgu, xb, EPI_SWIGLU, act)
+            else:
+                g_out = torch.empty((T, F), dtype=torch.bfloat16, device=h.device)
+                u_out = torch.empty((T, F), dtype=torch.bfloat16, device=h.device)
+                xin = xb if not gemv else None
+                qmatmul(L.wg, xin, EPI_BF16, g_out, xq=xq, xds=xds)
+                qmatmul(L.wu, xin, EPI_BF16, u_out, xq=xq, xds=xds)
+                K.glu(g_out, u_out, act, "silu")
+            if self.tp_size > 1 and self.tp_rank != 0:
+                h.zero_()
+            if gemv:
+                aq, ads = ws.q8(T, F)
+                K.quant_q8(act, aq, ads)
+                qmatmul(L.wd, None, EPI_ADD_F32, h, xq=aq, xds=ads)
+            else:
+                qmatmul(L.wd, act, EPI_ADD_F32, h)
+            self._allreduce(h)
+        # ---- head ----
+        S = fb.logits_idx.numel()
+        hs = ws.hs[:S]
+        K.select_rows(h, fb.logits_idx, hs)
+        if fb.want_hidden:
+            return hs * torch.rsqrt(hs.pow(2).mean(-1, keepdim=True) + eps) * self.out_norm
+        logits = ws.logits[:S]
+        if S <= GEMV_MAX_M and self.device.type == "cuda" and self.lm_head.is_quant:
+            xq, xds = ws.q8(S, H)
+            K.rmsnorm(hs, self.out_norm, eps, out_q8=(xq, xds))
+            qmatmul(self.lm_head, None, EPI_F32, logits, xq=xq, xds=xds)
+        else:
+            xbs = ws.xb[:S, :H]
+            K.rmsnorm(hs, self.out_norm, eps, out_bf16=xbs)
+            qmatmul(self.lm_head, xbs, EPI_F32, logits)
+        return logits

@@ -1,0 +1,113 @@
+"""Synthetic random-init checkpoints of real architectures (no network to fetch weights).
+
+``llama_tensor_plan`` reproduces llama.cpp's Q4_K_M type recipe (llama_tensor_get_type): Q4_K
+everywhere, Q6_K for output.weight and for attn_v / ffn_down on the "more bits" layers
+(i < n/8, i >= 7n/8, or (i - n/8) % 3 == 2), F32 norms. ``synthetic_source`` returns a
+``get_tensor`` callable producing random blocks in the quantised domain (valid fp16 scales,
+uniform codes, element std ~0.02) — same bytes-per-weight and kernels as a real Q4_K_M file.
+``write_synthetic_gguf`` streams such a model (plus a tokenizer) to disk for the end-to-end tests.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from ..formats.gguf import GGUFWriter, QType, tensor_nbytes
+from ..ops.quant import random_quantized
+from .config import LlamaConfig
+
+
+def _more_bits(i: int, n: int) -> bool:
+    return i < n // 8 or i >= 7 * n // 8 or (i - n // 8) % 3 == 2
+
+
+def llama_tensor_plan(cfg: LlamaConfig, ftype: str = "Q4_K_M"):
+    """[(name, ggml_shape, qtype)] for a Llama-architecture GGUF."""
+    H, F, V = cfg.hidden, cfg.ffn, cfg.vocab
+    qd, kvd = cfg.q_dim, cfg.kv_dim
+    base = {"Q4_K_M": QType.Q4_K, "Q6_K": QType.Q6_K, "Q8_0": QType.Q8_0, "F16": QType.F16}[ftype]
+    hi = QType.Q6_K if ftype == "Q4_K_M" else base
+    out = [("token_embd.weight", (H, V), base)]
+    L = cfg.n_layers
+    for i in range(L):
+        p = f"blk.{i}."
+        mb = _more_bits(i, L)
+        out += [
+            (p + "attn_norm.weight", (H,), QType.F32),
+            (p + "attn_q.weight", (H, qd), base),
+            (p + "attn_k.weight", (H, kvd), base),
+            (p + "attn_v.weight", (H, kvd), hi if mb else base),
+            (p + "attn_output.weight", (qd, H), base),
+            (p + "ffn_norm.weight", (H,), QType.F32),
+            (p + "ffn_gate.weight", (H, F), base),
+            (p + "ffn_up.weight", (H, F), base),
+            (p + "ffn_down.weight", (F, H), hi if mb else base),
+        ]
+        if cfg.qkv_bias:
+            out += [(p + "attn_q.bias", (qd,), QType.F32), (p + "attn_k.bias", (kvd,), QType.F32),
+                    (p + "attn_v.bias", (kvd,), QType.F32)]
+    out.append(("output_norm.weight", (H,), QType.F32))
+    if not cfg.tie_embeddings:
+        out.append(("output.weight", (H, V), QType.Q6_K if ftype == "Q4_K_M" else base))
+    return out
+
+
+def _gen(rng, name, shape, qt, cfg):
+    n = int(np.prod(shape))
+    if qt == QType.F32:
+        if name.endswith("norm.weight"):
+            return (1.0 + 0.05 * rng.standard_normal(n, dtype=np.float32)).astype(np.float32).view(np.uint8)
+        return (0.02 * rng.standard_normal(n, dtype=np.float32)).view(np.uint8)
+    std = 0.02
+    if name.startswith("token_embd"):
+        std = 1.0 / np.sqrt(cfg.hidden) * 4
+    return random_quantized(rng, qt, n // shape[0], shape[0], std=std)
+
+
+def synthetic_source(cfg: LlamaConfig, ftype: str = "Q4_K_M", seed: int = 0):
+    plan = {n: (s, q) for n, s, q in llama_tensor_plan(cfg, ftype)}
+    order = {n: i for i, n in enumerate(plan)}
+
+    def get_tensor(name):
+        if name not in plan:
+            return None
+        shape, qt = plan[name]
+        rng = np.random.default_rng(seed * 100003 + order[name])
+        return _gen(rng, name, shape, qt, cfg), int(qt), shape
+
+    get_tensor.plan = plan
+    return get_tensor
+
+
+def gguf_metadata(cfg: LlamaConfig, ftype: str = "Q4_K_M") -> dict:
+    a = cfg.arch
+    md = {
+        "general.architecture": a,
+        "general.name": cfg.name,
+        "general.file_type": {"Q4_K_M": 15, "Q6_K": 18, "Q8_0": 7, "F16": 1}[ftype],
+        f"{a}.block_count": cfg.n_layers,
+        f"{a}.context_length": cfg.ctx_train,
+        f"{a}.embedding_length": cfg.hidden,
+        f"{a}.feed_forward_length": cfg.ffn,
+        f"{a}.attention.head_count": cfg.n_heads,
+        f"{a}.attention.head_count_kv": cfg.n_kv_heads,
+        f"{a}.attention.layer_norm_rms_epsilon": float(cfg.rms_eps),
+        f"{a}.rope.freq_base": float(cfg.rope_base),
+        f"{a}.rope.dimension_count": cfg.rope_dim,
+        f"{a}.vocab_size": cfg.vocab,
+    }
+    if cfg.head_dim * cfg.n_heads != cfg.hidden:
+        md[f"{a}.attention.key_length"] = cfg.head_dim
+        md[f"{a}.attention.value_length"] = cfg.head_dim
+    return md
+
+
+def write_synthetic_gguf(path, cfg: LlamaConfig, ftype: str = "Q4_K_M", seed: int = 0, tokenizer_md: dict | None = None):
+    src = synthetic_source(cfg, ftype, seed)
+    w = GGUFWriter(path)
+    for k, v in gguf_metadata(cfg, ftype).items():
+        w.add(k, v)
+    for k, v in (tokenizer_md or {}).items():
+        w.add(k, v)
+    for name, (shape, qt) in src.plan.items():
+        w.add_tensor(name, (lambda n=name: src(n)[0].tobytes()), shape=shape, qtype=qt)
+    return w.write()

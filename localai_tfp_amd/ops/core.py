@@ -1,0 +1,329 @@
+"""Device ops: each function runs the HIP kernel on CUDA (ROCm) tensors and an fp32 PyTorch
+reference on CPU tensors. The CPU path is the numerics oracle for tests (HIP vs plain fp32) and
+the plumbing path the engine uses when no GPU is present; on a GPU box the native library is
+mandatory (``_native.kernels`` raises when it is missing).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn.functional as F
+
+from .. import _native as N
+
+# ------------------------------------------------------------------------------------------------
+# norms
+
+
+def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, *, out_bf16: torch.Tensor | None = None,
+            out_q8: tuple | None = None, residual_bf16: torch.Tensor | None = None):
+    """y = x / rms(x) * w for fp32 rows x [M, H]; optionally x += residual_bf16 first (written back).
+    Writes bf16 rows and/or q8 blocks (xq int8 [M, H], xds fp32 [M, H/32, 2])."""
+    M, H = x.shape
+    if M == 0:
+        return
+    if not x.is_cuda:
+        if residual_bf16 is not None:
+            x.add_(residual_bf16.float())
+        y = x * torch.rsqrt(x.pow(2).mean(-1, keepdim=True) + eps) * w
+        if out_bf16 is not None:
+            out_bf16.copy_(y)
+        if out_q8 is not None:
+            _quant_q8_ref(y, *out_q8)
+        return
+    xq, xds = out_q8 if out_q8 is not None else (None, None)
+    N.kcall("mxk_rmsnorm", x.data_ptr(), x.stride(0), N.ptr(residual_bf16),
+            residual_bf16.stride(0) if residual_bf16 is not None else 0,
+            x.data_ptr() if residual_bf16 is not None else None, w.data_ptr(), N.ptr(out_bf16),
+            out_bf16.stride(0) if out_bf16 is not None else 0, N.ptr(xq), N.ptr(xds), M, H, float(eps),
+            N.stream_ptr())
+
+
+def _quant_q8_ref(y: torch.Tensor, xq: torch.Tensor, xds: torch.Tensor):
+    M, K = y.shape
+    b = y.float().reshape(M, K // 32, 32)
+    d = b.abs().amax(-1) / 127.0
+    idd = torch.where(d > 0, 1.0 / d.clamp_min(1e-30), torch.zeros_like(d))
+    q = torch.round(b * idd[..., None]).clamp(-127, 127)
+    xq.copy_(q.reshape(M, K).to(torch.int8))
+    ds = xds.view(M, K // 32, 2)
+    ds[..., 0] = d
+    ds[..., 1] = d * q.sum(-1)
+
+
+def quant_q8(x: torch.Tensor, xq: torch.Tensor, xds: torch.Tensor):
+    M, K = x.shape
+    if M == 0:
+        return
+    if not x.is_cuda:
+        return _quant_q8_ref(x, xq, xds)
+    N.kcall("mxk_quant_q8", x.data_ptr(), x.stride(0), xq.data_ptr(), xds.data_ptr(), M, K, N.stream_ptr())
+
+
+def layernorm(x: torch.Tensor, g: torch.Tensor | None, b: torch.Tensor | None, eps: float,
+              out: torch.Tensor, residual: torch.Tensor | None = None, xsum: torch.Tensor | None = None):
+    """fp32 x [M, H] (+ residual) -> layernorm -> out (bf16 or fp32)."""
+    M, H = x.shape
+    if M == 0:
+        return out
+    if not x.is_cuda:
+        v = x + residual if residual is not None else x
+        if xsum is not None:
+            xsum.copy_(v)
+        out.copy_(F.layer_norm(v, (H,), g, b, eps))
+        return out
+    ob = out if out.dtype == torch.bfloat16 else None
+    of = out if out.dtype == torch.float32 else None
+    N.kcall("mxk_layernorm", x.data_ptr(), x.stride(0), N.ptr(residual), residual.stride(0) if residual is not None else 0,
+            N.ptr(xsum), N.ptr(g), N.ptr(b), N.ptr(ob), N.ptr(of), out.stride(0), M, H, float(eps), N.stream_ptr())
+    return out
+
+
+def groupnorm_nhwc(x: torch.Tensor, g: torch.Tensor, b: torch.Tensor, groups: int, eps: float, silu: bool,
+                   out: torch.Tensor | None = None):
+    """x fp32 [N, H, W, C] (channels-last)."""
+    n, h, w, c = x.shape
+    out = torch.empty_like(x) if out is None else out
+    if not x.is_cuda:
+        y = F.group_norm(x.permute(0, 3, 1, 2), groups, g, b, eps)
+        if silu:
+            y = F.silu(y)
+        out.copy_(y.permute(0, 2, 3, 1))
+        return out
+    N.kcall("mxk_groupnorm_nhwc", x.data_ptr(), out.data_ptr(), g.data_ptr(), b.data_ptr(), n, h * w, c, groups,
+            float(eps), int(silu), N.stream_ptr())
+    return out
+
+
+# ------------------------------------------------------------------------------------------------
+# rotary embeddings
+
+
+def rope_inv_freq(rot_dim: int, base: float = 10000.0, scale: float = 1.0, scaling: str = "none",
+                  orig_ctx: int = 0, ext_factor: float = -1.0, beta_fast: float = 32.0, beta_slow: float = 1.0,
+                  llama3: dict | None = None, freq_factors=None):
+    """inv_freq table [rot_dim/2] and attention magnitude factor for the rope_kv kernel.
+    Supports none/linear scaling, llama3.1 frequency smoothing, YaRN ramp (ext_factor) and
+    per-frequency factors (GGUF rope_freqs)."""
+    i = torch.arange(0, rot_dim, 2, dtype=torch.float64)
+    inv = 1.0 / (base ** (i / rot_dim))
+    attn_factor = 1.0
+    if freq_factors is not None:
+        inv = inv / torch.as_tensor(freq_factors, dtype=torch.float64)[: inv.numel()]
+    if llama3:
+        factor = llama3.get("factor", 8.0)
+        lo, hi = llama3.get("low_freq_factor", 1.0), llama3.get("high_freq_factor", 4.0)
+        old = llama3.get("original_max_position_embeddings", 8192)
+        wl = 2 * math.pi / inv
+        lo_wl, hi_wl = old / lo, old / hi
+        smooth = (old / wl - lo) / (hi - lo)
+        scaled = torch.where(wl > lo_wl, inv / factor, inv)
+        mid = (wl <= lo_wl) & (wl >= hi_wl)
+        scaled = torch.where(mid, (1 - smooth) * inv / factor + smooth * inv, scaled)
+        inv = scaled
+    elif scaling == "linear" and scale not in (0.0, 1.0):
+        inv = inv * scale
+    elif scaling == "yarn" and scale not in (0.0, 1.0):
+        # scale = freq_scale (= 1/factor) as in llama.cpp
+        factor = 1.0 / scale
+        orig = orig_ctx or 4096
+
+        def corr_dim(nrot):
+            return rot_dim * math.log(orig / (nrot * 2 * math.pi)) / (2 * math.log(base))
+
+        low = max(math.floor(corr_dim(beta_fast)), 0)
+        high = min(math.ceil(corr_dim(beta_slow)), rot_dim - 1)
+        ramp = ((i / 2 - low) / max(high - low, 1e-3)).clamp(0, 1)
+        ext = 1.0 if ext_factor < 0 else ext_factor
+        mask = (1 - ramp) * ext
+        inv = inv / factor * (1 - mask) + inv * mask
+        attn_factor = 0.1 * math.log(factor) + 1.0
+    return inv.float(), float(attn_factor)
+
+
+def rope_kv(qkv: torch.Tensor, bias: torch.Tensor | None, positions: torch.Tensor, slots: torch.Tensor,
+            inv_freq: torch.Tensor, attn_factor: float, Hq: int, Hkv: int, D: int, rot_dim: int, neox: bool,
+            q_out: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, block_size: int):
+    """qkv fp32 [T, (Hq+2Hkv)*D] -> q_out bf16 [T, Hq, D]; K/V scattered into the paged cache
+    [num_blocks, Hkv, block_size, D] at `slots` (flat block*bs+offset; -1 skips)."""
+    T = qkv.shape[0]
+    if T == 0:
+        return
+    if not qkv.is_cuda:
+        x = qkv.float()
+        if bias is not None:
+            x = x + bias
+        q = x[:, : Hq * D].reshape(T, Hq, D)
+        k = x[:, Hq * D:(Hq + Hkv) * D].reshape(T, Hkv, D)
+        v = x[:, (Hq + Hkv) * D:].reshape(T, Hkv, D)
+        ang = positions.double()[:, None] * inv_freq.double()[None, :]
+        cos = (torch.cos(ang) * attn_factor).float()
+        sin = (torch.sin(ang) * attn_factor).float()
+
+        def rot(t):
+            t = t.clone()
+            r = t[..., :rot_dim]
+            if neox:
+                a, b = r[..., : rot_dim // 2], r[..., rot_dim // 2:]
+                c, s = cos[:, None, :], sin[:, None, :]
+                t[..., :rot_dim] = torch.cat([a * c - b * s, a * s + b * c], -1)
+            else:
+                a, b = r[..., 0::2], r[..., 1::2]
+                c, s = cos[:, None, :], sin[:, None, :]
+                out = torch.empty_like(r)
+                out[..., 0::2] = a * c - b * s
+                out[..., 1::2] = a * s + b * c
+                t[..., :rot_dim] = out
+            return t
+
+        q_out.copy_(rot(q).to(q_out.dtype))
+        kr = rot(k)
+        for t in range(T):
+            s = int(slots[t])
+            if s < 0:
+                continue
+            blk, off = divmod(s, block_size)
+            k_cache[blk, :, off, :] = kr[t].to(k_cache.dtype)
+            v_cache[blk, :, off, :] = v[t].to(v_cache.dtype)
+        return
+    N.kcall("mxk_rope_kv", qkv.data_ptr(), N.ptr(bias), positions.data_ptr(), slots.data_ptr(), inv_freq.data_ptr(),
+            float(attn_factor), T, Hq, Hkv, D, rot_dim, int(neox), q_out.data_ptr(), k_cache.data_ptr(),
+            v_cache.data_ptr(), block_size, N.stream_ptr())
+
+
+# ------------------------------------------------------------------------------------------------
+# attention
+
+
+def _attn_ref_one(q, k_cache, v_cache, table, ctx: int, qpos0: int, scale: float, block_size: int):
+    """q [t, Hq, D] for query positions qpos0..qpos0+t-1 of one sequence; causal over ctx keys."""
+    t, Hq, D = q.shape
+    Hkv = k_cache.shape[1]
+    nb = (ctx + block_size - 1) // block_size
+    blocks = table[:nb].long()
+    k = k_cache[blocks].permute(1, 0, 2, 3).reshape(Hkv, nb * block_size, D)[:, :ctx].float()
+    v = v_cache[blocks].permute(1, 0, 2, 3).reshape(Hkv, nb * block_size, D)[:, :ctx].float()
+    G = Hq // Hkv
+    k = k.repeat_interleave(G, 0)
+    v = v.repeat_interleave(G, 0)
+    s = torch.einsum("thd,hkd->htk", q.float(), k) * scale
+    qp = torch.arange(qpos0, qpos0 + t)[:, None]
+    kp = torch.arange(ctx)[None, :]
+    s = s.masked_fill((kp > qp)[None], float("-inf"))
+    p = torch.softmax(s, -1)
+    return torch.einsum("htk,hkd->thd", p, v)
+
+
+def attn_decode(q: torch.Tensor, k_cache, v_cache, block_tables: torch.Tensor, seq_lens: torch.Tensor,
+                scale: float, out: torch.Tensor, part_size: int = 512, n_parts: int | None = None,
+                workspace: tuple | None = None, max_seq_len: int | None = None):
+    """q bf16 [B, Hq, D] (one query token per sequence, at position seq_len-1)."""
+    B, Hq, D = q.shape
+    if B == 0:
+        return out
+    Hkv, bs = k_cache.shape[1], k_cache.shape[2]
+    if not q.is_cuda:
+        for b in range(B):
+            L = int(seq_lens[b])
+            out[b] = _attn_ref_one(q[b:b + 1], k_cache, v_cache, block_tables[b], L, L - 1, scale, bs)[0].to(out.dtype)
+        return out
+    if n_parts is None:
+        ml = max_seq_len if max_seq_len is not None else int(seq_lens.max())
+        n_parts = max(1, -(-ml // part_size))
+    if n_parts > 1:
+        if workspace is None:
+            ml_t = torch.empty((B * Hq * n_parts, 2), dtype=torch.float32, device=q.device)
+            po = torch.empty((B * Hq * n_parts, D), dtype=torch.float32, device=q.device)
+        else:
+            ml_t, po = workspace
+    else:
+        ml_t = po = None
+    N.kcall("mxk_attn_decode", q.data_ptr(), q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
+            block_tables.data_ptr(), block_tables.stride(0), seq_lens.data_ptr(), B, Hq, Hkv, D, bs, float(scale),
+            part_size, n_parts, out.data_ptr(), out.stride(0), N.ptr(ml_t), N.ptr(po), N.stream_ptr())
+    return out
+
+
+def prefill_tiles(q_lens, rows_per_tile: int):
+    seqs, q0s = [], []
+    for s, ql in enumerate(q_lens):
+        for q0 in range(0, int(ql), rows_per_tile):
+            seqs.append(s)
+            q0s.append(q0)
+    return seqs, q0s
+
+
+def attn_prefill(q: torch.Tensor, k_cache, v_cache, block_tables: torch.Tensor, cu_q: torch.Tensor,
+                 ctx_lens: torch.Tensor, scale: float, out: torch.Tensor, q_lens_host=None, ctx_lens_host=None):
+    """q bf16 [T, Hq, D] for S sequences (cu_q [S+1]); keys 0..ctx_len-1 from the paged cache."""
+    T, Hq, D = q.shape
+    if T == 0:
+        return out
+    Hkv, bs = k_cache.shape[1], k_cache.shape[2]
+    cu = cu_q.tolist() if q_lens_host is None else None
+    if q_lens_host is None:
+        q_lens_host = [cu[i + 1] - cu[i] for i in range(len(cu) - 1)]
+    if ctx_lens_host is None:
+        ctx_lens_host = ctx_lens.tolist()
+    if not q.is_cuda:
+        off = 0
+        for s, ql in enumerate(q_lens_host):
+            ctx = int(ctx_lens_host[s])
+            out[off:off + ql] = _attn_ref_one(q[off:off + ql], k_cache, v_cache, block_tables[s], ctx, ctx - ql,
+                                              scale, bs).to(out.dtype)
+            off += ql
+        return out
+    rows = N.kernels().mxk_attn_prefill_rows(Hq, Hkv)
+    seqs, q0s = prefill_tiles(q_lens_host, rows)
+    tiles = torch.tensor([seqs, q0s], dtype=torch.int32).to(q.device, non_blocking=True)
+    N.kcall("mxk_attn_prefill", q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), block_tables.data_ptr(),
+            block_tables.stride(0), tiles[0].data_ptr(), tiles[1].data_ptr(), len(seqs), cu_q.data_ptr(),
+            ctx_lens.data_ptr(), Hq, Hkv, D, bs, float(scale), out.data_ptr(), N.stream_ptr())
+    return out
+
+
+# ------------------------------------------------------------------------------------------------
+# activations / misc
+
+
+def glu(gate: torch.Tensor, up: torch.Tensor, out: torch.Tensor, act: str = "silu"):
+    a = {"silu": 0, "gelu": 1, "gelu_tanh": 1, "gelu_erf": 2}[act]
+    if not gate.is_cuda:
+        g = gate.float()
+        y = F.silu(g) if a == 0 else F.gelu(g, approximate="tanh" if a == 1 else "none")
+        out.copy_(y * up.float())
+        return out
+    M, Fd = gate.shape
+    N.kcall("mxk_glu", a, gate.data_ptr(), up.data_ptr(), gate.stride(0), out.data_ptr(), out.stride(0), M, Fd,
+            N.stream_ptr())
+    return out
+
+
+def gather_rows(table: torch.Tensor, ids: torch.Tensor, out: torch.Tensor, scale: float = 1.0):
+    """dense embedding gather -> fp32 rows"""
+    if not table.is_cuda:
+        out.copy_(table[ids.long()].float() * scale)
+        return out
+    dt = {torch.float32: 0, torch.float16: 1, torch.bfloat16: 2}[table.dtype]
+    N.kcall("mxk_gather_rows", table.data_ptr(), dt, ids.data_ptr(), ids.numel(), table.shape[1], float(scale),
+            out.data_ptr(), N.stream_ptr())
+    return out
+
+
+def select_rows(x: torch.Tensor, idx: torch.Tensor, out: torch.Tensor):
+    if not x.is_cuda:
+        out.copy_(x[idx.long()])
+        return out
+    N.kcall("mxk_select_rows_f32", x.data_ptr(), x.stride(0), idx.data_ptr(), idx.numel(), x.shape[1], out.data_ptr(),
+            out.stride(0), N.stream_ptr())
+    return out
+
+
+def cast_bf16(x: torch.Tensor, out: torch.Tensor):
+    if not x.is_cuda:
+        out.copy_(x)
+        return out
+    N.kcall("mxk_cast_f32_bf16", x.data_ptr(), x.stride(0), out.data_ptr(), out.stride(0), x.shape[0], x.shape[1],
+            N.stream_ptr())
+    return out

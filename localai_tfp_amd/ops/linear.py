@@ -1,0 +1,230 @@
+"""Quantised linear layers: GPU weight container + M-dependent kernel dispatch.
+
+``QWeight`` owns one [N, K] projection in a GPU-native layout (ops/quant.py). ``qmatmul`` picks:
+
+* M <= 4 and q8 activations available  -> ``mxk_qgemv``   (int8 dot4, HBM-bound decode)
+* otherwise                             -> ``mxk_qgemm_mfma`` (dequant-to-bf16 MFMA), with the
+  workgroup shape (WM x 16 rows, WN x 16 cols per wave) and split-K chosen so the grid covers the
+  256 CUs: split-K partials go through fp32 atomics into either the residual stream (o_proj,
+  down_proj: EPI_ADD_F32) or a zeroed fp32 buffer (QKV).
+* dense (F16/BF16/F32 or non-native quant types densified at load) -> hipBLASLt via torch.matmul.
+
+On CPU tensors everything runs as an fp32 PyTorch reference (dequantised weights), which is the
+numerics oracle for the HIP kernels.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from .. import _native as N
+from ..formats.gguf import QType
+from . import quant as Q
+
+EPI_F32, EPI_BF16, EPI_ADD_F32, EPI_SWIGLU = 0, 1, 2, 3
+CU_COUNT = 256
+
+
+class QWeight:
+    """A [N, K] weight. ``qtype`` is a ggml QType for native quant layouts, or "dense"."""
+
+    def __init__(self, N_: int, K: int, qtype, data: torch.Tensor, dplane: torch.Tensor | None = None,
+                 raw_ggml: np.ndarray | None = None, raw_qtype: int | None = None, name: str = ""):
+        self.N, self.K = int(N_), int(K)
+        self.qtype = qtype
+        self.data = data
+        self.dplane = dplane
+        self.name = name
+        self._raw = raw_ggml  # kept only for CPU reference dequantisation
+        self._raw_qtype = raw_qtype
+        self._dense_f32: torch.Tensor | None = None
+        self.bf16_cache: torch.Tensor | None = None
+
+    # ---------------------------------------------------------------- construction
+    @classmethod
+    def from_ggml(cls, raw: np.ndarray, qtype: int, N_: int, K: int, device="cpu", name: str = "",
+                  dense_dtype=torch.bfloat16):
+        qt = QType(qtype)
+        dev = torch.device(device)
+        if dev.type == "cpu":
+            # CPU: keep the ggml bytes, dequantise lazily for the reference path
+            return cls(N_, K, int(qt) if qt in Q.GPU_NATIVE else "dense",
+                       torch.empty(0), None, np.asarray(raw), int(qt), name)
+        if qt in Q.GPU_NATIVE and K % 256 == 0:
+            data, dpl = Q.repack_for_gpu(raw, qt, N_, K)
+            t = torch.from_numpy(np.ascontiguousarray(data)).to(dev)
+            d = torch.from_numpy(np.ascontiguousarray(dpl).view(np.int16)).to(dev) if dpl is not None else None
+            return cls(N_, K, int(qt), t, d, None, int(qt), name)
+        dense = Q.dequantize(raw, qt, (K, N_))
+        t = torch.from_numpy(dense).to(dev, dense_dtype)
+        return cls(N_, K, "dense", t, None, None, int(qt), name)
+
+    @classmethod
+    def dense(cls, w: torch.Tensor, name: str = ""):
+        return cls(w.shape[0], w.shape[1], "dense", w.contiguous(), None, None, None, name)
+
+    @property
+    def is_quant(self) -> bool:
+        return self.qtype != "dense"
+
+    @property
+    def device(self):
+        return self.data.device if self.data.numel() else torch.device("cpu")
+
+    def nbytes(self) -> int:
+        n = self.data.numel() * self.data.element_size()
+        if self.dplane is not None:
+            n += self.dplane.numel() * 2
+        return n
+
+    # ---------------------------------------------------------------- reference / caches
+    def dense_f32(self) -> torch.Tensor:
+        """fp32 [N, K] (CPU reference or debugging)."""
+        if self._dense_f32 is not None:
+            return self._dense_f32
+        if self._raw is not None:
+            w = torch.from_numpy(Q.dequantize(self._raw, self._raw_qtype, (self.K, self.N)).copy())
+        elif self.qtype == "dense":
+            w = self.data.float()
+        else:
+            w = self.dequant_gpu(torch.float32)
+        if w.device.type == "cpu":
+            self._dense_f32 = w
+        return w
+
+    def dequant_gpu(self, dtype=torch.bfloat16, rows: torch.Tensor | None = None) -> torch.Tensor:
+        assert self.is_quant and self.data.is_cuda
+        n = self.N if rows is None else rows.numel()
+        out = torch.empty((n, self.K), dtype=dtype, device=self.data.device)
+        ob = out if dtype == torch.bfloat16 else None
+        of = out if dtype == torch.float32 else None
+        N.kcall("mxk_dequant_rows", int(self.qtype), self.data.data_ptr(), N.ptr(self.dplane),
+                N.ptr(rows), n, self.K, N.ptr(ob), N.ptr(of), self.K, N.stream_ptr())
+        return out
+
+    def build_bf16_cache(self):
+        """Optional dense bf16 copy for large-M prefill through hipBLASLt (288 GB HBM makes the
+        2 B/param copy affordable; opt-in via engine config `prefill_bf16_cache`)."""
+        if self.is_quant and self.data.is_cuda and self.bf16_cache is None:
+            self.bf16_cache = self.dequant_gpu(torch.bfloat16)
+        return self.bf16_cache
+
+
+def concat_rows(ws: list[QWeight], name: str = "") -> QWeight | None:
+    """Fuse projections sharing K and qtype along N (e.g. Q|K|V). None if not fusable."""
+    if not ws or any(w.qtype != ws[0].qtype or w.K != ws[0].K for w in ws):
+        return None
+    if ws[0].device.type == "cpu":
+        if any(w._raw is None for w in ws):
+            return None
+        raw = np.concatenate([np.asarray(w._raw).reshape(w.N, -1) for w in ws], 0)
+        return QWeight(sum(w.N for w in ws), ws[0].K, ws[0].qtype, torch.empty(0), None, raw,
+                       ws[0]._raw_qtype, name)
+    data = torch.cat([w.data for w in ws], 0)
+    dpl = torch.cat([w.dplane for w in ws], 0) if ws[0].dplane is not None else None
+    return QWeight(sum(w.N for w in ws), ws[0].K, ws[0].qtype, data, dpl, None, ws[0]._raw_qtype, name)
+
+
+def interleave_gate_up(gate: QWeight, up: QWeight, name: str = "") -> QWeight | None:
+    """Gate/up rows interleaved in 16-row groups for the fused SwiGLU epilogue."""
+    if gate.qtype != up.qtype or gate.K != up.K or gate.N != up.N or gate.N % 16:
+        return None
+    if gate.device.type == "cpu":
+        if gate._raw is None:
+            return None
+        raw = Q.interleave_rows16(np.asarray(gate._raw).reshape(gate.N, -1), np.asarray(up._raw).reshape(up.N, -1))
+        return QWeight(2 * gate.N, gate.K, gate.qtype, torch.empty(0), None, raw, gate._raw_qtype, name)
+
+    def il(a, b):
+        g = a.shape[0] // 16
+        return torch.stack([a.reshape(g, 16, -1), b.reshape(g, 16, -1)], 1).reshape(2 * a.shape[0], -1)
+
+    data = il(gate.data, up.data)
+    dpl = il(gate.dplane, up.dplane) if gate.dplane is not None else None
+    return QWeight(2 * gate.N, gate.K, gate.qtype, data, dpl, None, gate._raw_qtype, name)
+
+
+# ------------------------------------------------------------------------------------------------
+def _mfma_shape(M: int, N_: int, nblk: int, can_split: bool, qtype: int):
+    if M <= 16:
+        wm = 1
+    elif M <= 32:
+        wm = 2
+    elif M <= 64:
+        wm = 4
+    else:
+        wm = 8
+    wn = 2
+    cols = -(-N_ // (64 * wn))
+    mt = -(-M // (16 * wm))
+    splits = 1
+    if can_split:
+        target = 2 * CU_COUNT
+        while cols * mt * splits < target and splits * 2 <= nblk // 2:
+            splits *= 2
+    return wm, wn, splits
+
+
+def qmatmul(W: QWeight, x: torch.Tensor | None, epi: int, out: torch.Tensor, *, xq: torch.Tensor | None = None,
+            xds: torch.Tensor | None = None, out_zeroed: bool = False):
+    """out (+)= x @ W^T with the given epilogue.
+
+    x:   bf16 [M, K] (MFMA / dense path) — may be None when (xq, xds) given and M <= 4
+    epi: EPI_F32 (store fp32) | EPI_BF16 | EPI_ADD_F32 (out += ; fp32) | EPI_SWIGLU (bf16 [M, N/2])
+    out_zeroed: for EPI_F32, caller guarantees `out` is zero so split-K may accumulate atomically.
+    """
+    M = (x if x is not None else xq).shape[0]
+    if M == 0:
+        return out
+    dev = (x if x is not None else xq).device
+    if dev.type == "cpu":
+        return _qmatmul_ref(W, x if x is not None else _deq_q8(xq, xds), epi, out)
+    if not W.is_quant:
+        y = torch.matmul(x, W.data.t()) if x.dtype == W.data.dtype else torch.matmul(x.to(W.data.dtype), W.data.t())
+        return _apply_epi_dense(y, epi, out)
+    if M <= 4 and xq is not None:
+        N.kcall("mxk_qgemv", int(W.qtype), epi, xq.data_ptr(), xds.data_ptr(), W.data.data_ptr(), N.ptr(W.dplane),
+                M, W.N, W.K, out.data_ptr(), out.stride(0), N.stream_ptr())
+        return out
+    if x is None:
+        raise ValueError("qmatmul: MFMA path needs bf16 activations")
+    if W.bf16_cache is not None and M >= 256:
+        y = torch.matmul(x, W.bf16_cache.t())
+        return _apply_epi_dense(y, epi, out)
+    nblk = W.K // 256
+    can_split = epi == EPI_ADD_F32 or (epi == EPI_F32 and out_zeroed)
+    wm, wn, splits = _mfma_shape(M, W.N, nblk, can_split, int(W.qtype))
+    e = epi
+    if epi == EPI_F32 and splits > 1:
+        e = EPI_ADD_F32
+    N.kcall("mxk_qgemm_mfma", int(W.qtype), e, wm, wn, x.data_ptr(), x.stride(0), W.data.data_ptr(),
+            N.ptr(W.dplane), M, W.N, W.K, splits, out.data_ptr(), out.stride(0), N.stream_ptr())
+    return out
+
+
+def _apply_epi_dense(y: torch.Tensor, epi: int, out: torch.Tensor):
+    if epi == EPI_F32:
+        out.copy_(y)
+    elif epi == EPI_BF16:
+        out.copy_(y)
+    elif epi == EPI_ADD_F32:
+        out.add_(y.float())
+    else:
+        yf = y.float()
+        Nn = yf.shape[1]
+        g = Nn // 32
+        v = yf.reshape(-1, g, 2, 16)
+        gate, up = v[:, :, 0, :].reshape(-1, Nn // 2), v[:, :, 1, :].reshape(-1, Nn // 2)
+        out.copy_(torch.nn.functional.silu(gate) * up)
+    return out
+
+
+def _qmatmul_ref(W: QWeight, x: torch.Tensor, epi: int, out: torch.Tensor):
+    y = x.float() @ W.dense_f32().t()
+    return _apply_epi_dense(y, epi, out)
+
+
+def _deq_q8(xq: torch.Tensor, xds: torch.Tensor) -> torch.Tensor:
+    M, K = xq.shape
+    d = xds.reshape(M, K // 32, 2)[:, :, 0]
+    return (xq.float().reshape(M, K // 32, 32) * d[:, :, None]).reshape(M, K)

@@ -1,0 +1,180 @@
+"""Batched token sampling (GPU: csrc/kernels/sampling.hip; CPU: PyTorch reference).
+
+Sampling parameters follow llama.cpp's chain as driven by the reference worker
+(grpc-server.cpp:690-964 `launch_slot_with_data`: temperature, top_k, top_p, min_p, typical_p,
+repeat/presence/frequency penalties over the last `repeat_last_n` tokens, logit_bias, mirostat,
+seed). Penalties and logit bias are passed sparsely per row as unique (token, count, bias).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+from .. import _native as N
+
+SAMPLE_DTYPE = np.dtype([
+    ("temperature", np.float32), ("top_k", np.int32), ("top_p", np.float32), ("min_p", np.float32),
+    ("typical_p", np.float32), ("mirostat_tau", np.float32), ("repeat_penalty", np.float32),
+    ("presence_penalty", np.float32), ("frequency_penalty", np.float32), ("pen_offset", np.int32),
+    ("pen_count", np.int32), ("seed", np.uint64)], align=True)
+
+
+@dataclass
+class SamplingParams:
+    temperature: float = 0.8
+    top_k: int = 40
+    top_p: float = 0.95
+    min_p: float = 0.05
+    typical_p: float = 1.0
+    repeat_penalty: float = 1.0
+    repeat_last_n: int = 64
+    presence_penalty: float = 0.0
+    frequency_penalty: float = 0.0
+    mirostat: int = 0
+    mirostat_tau: float = 5.0
+    mirostat_eta: float = 0.1
+    seed: int = -1
+    logit_bias: dict = field(default_factory=dict)
+    ignore_eos: bool = False
+    n_probs: int = 0
+
+    @property
+    def greedy(self) -> bool:
+        return self.temperature <= 0.0 or self.top_k == 1
+
+
+def _check_size():
+    sz = N.kernels().mxk_sample_params_size()
+    if sz != SAMPLE_DTYPE.itemsize:
+        raise N.NativeError(f"SampleParams ABI mismatch: C {sz} B vs numpy {SAMPLE_DTYPE.itemsize} B")
+
+
+class SamplerBatch:
+    """Host-side packing of per-row parameters + sparse penalty lists into device buffers."""
+
+    def __init__(self, device):
+        self.device = torch.device(device)
+        self._checked = False
+
+    def pack(self, params: list[SamplingParams], histories: list[list[int]], steps: list[int],
+             mirostat_mu: list[float] | None = None):
+        B = len(params)
+        arr = np.zeros(B, SAMPLE_DTYPE)
+        toks, cnts, bias = [], [], []
+        for i, p in enumerate(params):
+            arr[i]["temperature"] = 0.0 if p.greedy else p.temperature
+            arr[i]["top_k"] = p.top_k
+            arr[i]["top_p"] = p.top_p
+            arr[i]["min_p"] = p.min_p
+            arr[i]["typical_p"] = p.typical_p
+            arr[i]["mirostat_tau"] = (mirostat_mu[i] if mirostat_mu else 2 * p.mirostat_tau) if p.mirostat == 2 else 0.0
+            arr[i]["repeat_penalty"] = p.repeat_penalty
+            arr[i]["presence_penalty"] = p.presence_penalty
+            arr[i]["frequency_penalty"] = p.frequency_penalty
+            seed = p.seed if p.seed is not None and p.seed >= 0 else 0x5DEECE66D
+            arr[i]["seed"] = (int(seed) * 1000003 + int(steps[i])) & 0xFFFFFFFFFFFFFFFF
+            d: dict[int, list] = {}
+            if p.repeat_penalty != 1.0 or p.presence_penalty or p.frequency_penalty:
+                hist = histories[i][-p.repeat_last_n:] if p.repeat_last_n > 0 else histories[i]
+                for t in hist:
+                    e = d.setdefault(int(t), [0, 0.0])
+                    e[0] += 1
+            for t, b in (p.logit_bias or {}).items():
+                e = d.setdefault(int(t), [0, 0.0])
+                e[1] += float(b)
+            arr[i]["pen_offset"] = len(toks)
+            arr[i]["pen_count"] = len(d)
+            for t, (c, b) in d.items():
+                toks.append(t)
+                cnts.append(c)
+                bias.append(b)
+        return arr, np.asarray(toks or [0], np.int32), np.asarray(cnts or [0], np.int32), np.asarray(bias or [0.0], np.float32)
+
+    def sample(self, logits: torch.Tensor, params: list[SamplingParams], histories: list[list[int]],
+               steps: list[int], allow_mask: torch.Tensor | None = None, mirostat_mu=None):
+        """logits fp32 [B, V] (modified in place) -> (tokens int32 [B], logprobs fp32 [B]) on device."""
+        B, V = logits.shape
+        if not logits.is_cuda:
+            return sample_ref(logits, params, histories, steps, allow_mask)
+        if not self._checked:
+            _check_size()
+            self._checked = True
+        if all(p.greedy and not p.logit_bias and p.repeat_penalty == 1.0 and not p.presence_penalty
+               and not p.frequency_penalty for p in params) and allow_mask is None:
+            tok = torch.empty(B, dtype=torch.int32, device=logits.device)
+            N.kcall("mxk_argmax", logits.data_ptr(), logits.stride(0), B, V, tok.data_ptr(), N.stream_ptr())
+            return tok, None
+        arr, toks, cnts, bias = self.pack(params, histories, steps, mirostat_mu)
+        dev = logits.device
+        pbuf = torch.from_numpy(arr.view(np.uint8)).to(dev, non_blocking=True)
+        t_t = torch.from_numpy(toks).to(dev, non_blocking=True)
+        c_t = torch.from_numpy(cnts).to(dev, non_blocking=True)
+        b_t = torch.from_numpy(bias).to(dev, non_blocking=True)
+        tok = torch.empty(B, dtype=torch.int32, device=dev)
+        lp = torch.empty(B, dtype=torch.float32, device=dev)
+        N.kcall("mxk_sample", logits.data_ptr(), logits.stride(0), B, V, pbuf.data_ptr(), t_t.data_ptr(),
+                c_t.data_ptr(), b_t.data_ptr(), N.ptr(allow_mask), allow_mask.stride(0) if allow_mask is not None else 0,
+                tok.data_ptr(), lp.data_ptr(), N.stream_ptr())
+        return tok, lp
+
+
+def sample_ref(logits: torch.Tensor, params, histories, steps, allow_mask=None):
+    """PyTorch reference of the same chain (CPU engine path)."""
+    B, V = logits.shape
+    toks = torch.empty(B, dtype=torch.int32)
+    lps = torch.empty(B, dtype=torch.float32)
+    for i, p in enumerate(params):
+        x = logits[i].float().clone()
+        counts: dict[int, int] = {}
+        if p.repeat_penalty != 1.0 or p.presence_penalty or p.frequency_penalty:
+            hist = histories[i][-p.repeat_last_n:] if p.repeat_last_n > 0 else histories[i]
+            for t in hist:
+                counts[int(t)] = counts.get(int(t), 0) + 1
+        for t, c in counts.items():
+            if 0 <= t < V:
+                v = x[t]
+                if p.repeat_penalty != 1.0:
+                    v = v / p.repeat_penalty if v > 0 else v * p.repeat_penalty
+                x[t] = v - p.frequency_penalty * c - p.presence_penalty
+        for t, b in (p.logit_bias or {}).items():
+            if 0 <= int(t) < V:
+                x[int(t)] += float(b)
+        if allow_mask is not None:
+            m = allow_mask[i]
+            bits = ((m[:, None] >> torch.arange(32, dtype=torch.int32)) & 1).reshape(-1)[:V].bool()
+            x = torch.where(bits, x, torch.full_like(x, float("-inf")))
+        if p.greedy:
+            t = int(torch.argmax(x))
+            toks[i] = t
+            lps[i] = 0.0
+            continue
+        x = x / p.temperature
+        keep = torch.isfinite(x)
+        if p.top_k > 0 and p.top_k < V:
+            kth = torch.topk(x, p.top_k).values[-1]
+            keep &= x >= kth
+        mx = x.max()
+        if p.min_p > 0:
+            keep &= x >= mx + np.log(p.min_p)
+        if 0 < p.top_p < 1:
+            xs = torch.where(keep, x, torch.full_like(x, float("-inf")))
+            pr = torch.softmax(xs, -1)
+            sp, si = torch.sort(pr, descending=True)
+            cum = torch.cumsum(sp, 0)
+            n_keep = int((cum < p.top_p).sum()) + 1
+            k2 = torch.zeros_like(keep)
+            k2[si[:n_keep]] = True
+            keep &= k2
+        if p.mirostat == 2:
+            xs = torch.where(keep, x, torch.full_like(x, float("-inf")))
+            lp = torch.log_softmax(xs, -1) / np.log(2)
+            keep &= (-lp <= 2 * p.mirostat_tau) | (x == mx)
+        xs = torch.where(keep, x, torch.full_like(x, float("-inf")))
+        pr = torch.softmax(xs, -1)
+        g = torch.Generator().manual_seed(((p.seed if p.seed >= 0 else 0x5DEECE66D) * 1000003 + steps[i]) & 0x7FFFFFFF)
+        t = int(torch.multinomial(pr, 1, generator=g))
+        toks[i] = t
+        lps[i] = float(torch.log(pr[t].clamp_min(1e-30)))
+    return toks, lps

@@ -1,0 +1,271 @@
+"""HIP kernel numerics vs plain PyTorch fp32 references of the same op (run on MI355X)."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from localai_tfp_amd import _native as N
+from localai_tfp_amd.formats.gguf import QType
+from localai_tfp_amd.ops import core as K
+from localai_tfp_amd.ops import quant as Q
+from localai_tfp_amd.ops.linear import EPI_ADD_F32, EPI_BF16, EPI_F32, EPI_SWIGLU, QWeight, qmatmul
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def rel(a, b):
+    a, b = a.float().cpu(), b.float().cpu()
+    return float((a - b).norm() / (b.norm() + 1e-12))
+
+
+def make_w(qt, n, k, seed=0):
+    rng = np.random.default_rng(seed)
+    x = rng.standard_normal((n, k), dtype=np.float32) * 0.05
+    raw = Q.QUANTIZERS[QType(qt)](x)
+    dense = Q.dequantize(raw, qt, (k, n))
+    return raw.reshape(n, -1), torch.from_numpy(dense)
+
+
+def test_native_loaded():
+    lib = N.kernels()
+    assert lib is not None
+    assert any("libmxk.so" in p for p in N.loaded_library_paths())
+
+
+@pytest.mark.parametrize("H", [4096, 2048, 5120, 320])
+def test_rmsnorm(H):
+    torch.manual_seed(0)
+    M = 7
+    x = torch.randn(M, H, device=DEV) * 3
+    w = torch.rand(H, device=DEV) + 0.5
+    ob = torch.empty(M, H, dtype=torch.bfloat16, device=DEV)
+    xq = torch.empty(M, H, dtype=torch.int8, device=DEV)
+    xds = torch.empty(M, H // 32, 2, device=DEV)
+    K.rmsnorm(x, w, 1e-5, out_bf16=ob, out_q8=(xq, xds))
+    ref = (x.cpu() * torch.rsqrt(x.cpu().pow(2).mean(-1, keepdim=True) + 1e-5) * w.cpu())
+    assert rel(ob, ref) < 5e-3
+    deq = xq.float().cpu().reshape(M, H // 32, 32) * xds.cpu()[:, :, :1]
+    assert rel(deq.reshape(M, H), ref) < 1.5e-2
+    s = xds.cpu()[:, :, 1]
+    assert torch.allclose(s, xds.cpu()[:, :, 0] * xq.cpu().float().reshape(M, H // 32, 32).sum(-1), rtol=1e-4, atol=1e-4)
+
+
+def test_quant_q8():
+    x = (torch.randn(5, 14336, device=DEV) * 2).bfloat16()
+    xq = torch.empty(5, 14336, dtype=torch.int8, device=DEV)
+    xds = torch.empty(5, 14336 // 32, 2, device=DEV)
+    K.quant_q8(x, xq, xds)
+    xq_r = torch.empty(5, 14336, dtype=torch.int8)
+    xds_r = torch.empty(5, 14336 // 32, 2)
+    K.quant_q8(x.cpu(), xq_r, xds_r)
+    assert (xq.cpu().int() - xq_r.int()).abs().max() <= 1
+    assert torch.allclose(xds.cpu()[..., 0], xds_r[..., 0], rtol=1e-5)
+
+
+@pytest.mark.parametrize("qt", [QType.Q4_K, QType.Q6_K, QType.Q8_0])
+def test_dequant_rows(qt):
+    raw, dense = make_w(qt, 48, 1024, seed=int(qt))
+    W = QWeight.from_ggml(raw, qt, 48, 1024, DEV)
+    out = W.dequant_gpu(torch.float32)
+    assert torch.allclose(out.cpu(), dense, atol=1e-6, rtol=1e-3)
+    rows = torch.tensor([3, 0, 47, 3], dtype=torch.int32, device=DEV)
+    sel = W.dequant_gpu(torch.float32, rows)
+    assert torch.allclose(sel.cpu(), dense[[3, 0, 47, 3]], atol=1e-6, rtol=1e-3)
+
+
+@pytest.mark.parametrize("qt", [QType.Q4_K, QType.Q6_K, QType.Q8_0])
+@pytest.mark.parametrize("M", [1, 2, 3, 4])
+def test_qgemv(qt, M):
+    n, k = 512, 4096
+    raw, dense = make_w(qt, n, k, seed=M)
+    W = QWeight.from_ggml(raw, qt, n, k, DEV)
+    x = torch.randn(M, k, device=DEV)
+    xq = torch.empty(M, k, dtype=torch.int8, device=DEV)
+    xds = torch.empty(M, k // 32, 2, device=DEV)
+    K.quant_q8(x.bfloat16(), xq, xds)
+    xd = xq.float().cpu().reshape(M, k // 32, 32) * xds.cpu()[:, :, :1]
+    ref = xd.reshape(M, k) @ dense.t()
+    out = torch.empty(M, n, device=DEV)
+    qmatmul(W, None, EPI_F32, out, xq=xq, xds=xds)
+    assert rel(out, ref) < 2e-3
+    acc = torch.randn(M, n, device=DEV)
+    acc0 = acc.clone()
+    qmatmul(W, None, EPI_ADD_F32, acc, xq=xq, xds=xds)
+    assert rel(acc - acc0, ref) < 2e-3
+    sw = torch.empty(M, n // 2, dtype=torch.bfloat16, device=DEV)
+    qmatmul(W, None, EPI_SWIGLU, sw, xq=xq, xds=xds)
+    g = ref.reshape(M, n // 32, 2, 16)
+    ref_sw = torch.nn.functional.silu(g[:, :, 0].reshape(M, -1)) * g[:, :, 1].reshape(M, -1)
+    assert rel(sw, ref_sw) < 1e-2
+
+
+@pytest.mark.parametrize("qt", [QType.Q4_K, QType.Q6_K, QType.Q8_0])
+@pytest.mark.parametrize("M", [5, 16, 33, 64, 100, 257])
+def test_qgemm_mfma(qt, M):
+    n, k = 384, 2048
+    raw, dense = make_w(qt, n, k, seed=M + 7)
+    W = QWeight.from_ggml(raw, qt, n, k, DEV)
+    x = torch.randn(M, k, device=DEV).bfloat16()
+    ref = x.float().cpu() @ dense.t()
+    out = torch.empty(M, n, device=DEV)
+    qmatmul(W, x, EPI_F32, out)
+    assert rel(out, ref) < 1e-2
+    z = torch.zeros(M, n, device=DEV)
+    qmatmul(W, x, EPI_F32, z, out_zeroed=True)  # may split-K through atomics
+    assert rel(z, ref) < 1e-2
+    acc = torch.randn(M, n, device=DEV)
+    acc0 = acc.clone()
+    qmatmul(W, x, EPI_ADD_F32, acc)
+    assert rel(acc - acc0, ref) < 1e-2
+    ob = torch.empty(M, n, dtype=torch.bfloat16, device=DEV)
+    qmatmul(W, x, EPI_BF16, ob)
+    assert rel(ob, ref) < 1.5e-2
+    sw = torch.empty(M, n // 2, dtype=torch.bfloat16, device=DEV)
+    qmatmul(W, x, EPI_SWIGLU, sw)
+    g = ref.reshape(M, n // 32, 2, 16)
+    ref_sw = torch.nn.functional.silu(g[:, :, 0].reshape(M, -1)) * g[:, :, 1].reshape(M, -1)
+    assert rel(sw, ref_sw) < 2e-2
+
+
+def test_qgemm_strided_out_and_lda():
+    qt = QType.Q4_K
+    raw, dense = make_w(qt, 256, 1024, seed=3)
+    W = QWeight.from_ggml(raw, qt, 256, 1024, DEV)
+    xb = torch.randn(20, 2048, device=DEV).bfloat16()
+    x = xb[:, :1024]
+    big = torch.zeros(20, 600, device=DEV)
+    qmatmul(W, x, EPI_F32, big[:, 100:356])
+    ref = x.float().cpu() @ dense.t()
+    assert rel(big[:, 100:356], ref) < 1e-2
+    assert float(big[:, :100].abs().sum()) == 0.0
+
+
+def _rope_setup(T, Hq, Hkv, D, nb, bs, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    qkv = torch.randn(T, (Hq + 2 * Hkv) * D, generator=g)
+    pos = torch.randint(0, 3000, (T,), generator=g, dtype=torch.int32)
+    slots = torch.randperm(nb * bs, generator=g)[:T].to(torch.int32)
+    slots[0] = -1
+    return qkv, pos, slots
+
+
+@pytest.mark.parametrize("neox", [False, True])
+@pytest.mark.parametrize("D,rot", [(128, 128), (64, 64), (128, 64)])
+def test_rope_kv(neox, D, rot):
+    T, Hq, Hkv, nb, bs = 9, 8, 2, 8, 16
+    qkv, pos, slots = _rope_setup(T, Hq, Hkv, D, nb, bs)
+    bias = torch.randn((Hq + 2 * Hkv) * D) * 0.1
+    inv, af = K.rope_inv_freq(rot, 500000.0)
+    outs = []
+    for dev in ("cpu", DEV):
+        q = torch.empty(T, Hq, D, dtype=torch.bfloat16, device=dev)
+        kc = torch.zeros(nb, Hkv, bs, D, dtype=torch.bfloat16, device=dev)
+        vc = torch.zeros_like(kc)
+        K.rope_kv(qkv.to(dev), bias.to(dev), pos.to(dev), slots.to(dev), inv.to(dev), af, Hq, Hkv, D, rot, neox, q, kc, vc, bs)
+        outs.append((q.cpu(), kc.cpu(), vc.cpu()))
+    for a, b in zip(*outs):
+        assert rel(b, a) < 1e-2
+
+
+def _paged_kv(nb, Hkv, bs, D, seed):
+    g = torch.Generator().manual_seed(seed)
+    kc = (torch.randn(nb, Hkv, bs, D, generator=g)).bfloat16()
+    vc = (torch.randn(nb, Hkv, bs, D, generator=g)).bfloat16()
+    return kc, vc
+
+
+@pytest.mark.parametrize("Hq,Hkv,D", [(32, 8, 128), (8, 8, 128), (28, 4, 128), (32, 8, 64), (64, 8, 128)])
+@pytest.mark.parametrize("lens", [[1, 17, 300], [1200, 5, 2049]])
+def test_attn_decode(Hq, Hkv, D, lens):
+    bs, nb = 16, 512
+    kc, vc = _paged_kv(nb, Hkv, bs, D, 1)
+    B = len(lens)
+    maxb = max((l + bs - 1) // bs for l in lens)
+    bt = torch.zeros(B, maxb, dtype=torch.int32)
+    perm = torch.randperm(nb - 1)[: B * maxb] + 1
+    for b in range(B):
+        bt[b] = perm[b * maxb:(b + 1) * maxb].int()
+    seq = torch.tensor(lens, dtype=torch.int32)
+    q = torch.randn(B, Hq, D).bfloat16()
+    scale = 1 / math.sqrt(D)
+    ref = torch.empty(B, Hq, D)
+    K.attn_decode(q, kc, vc, bt, seq, scale, ref)
+    for part in (512, 128):
+        out = torch.empty(B, Hq, D, dtype=torch.bfloat16, device=DEV)
+        K.attn_decode(q.to(DEV), kc.to(DEV), vc.to(DEV), bt.to(DEV), seq.to(DEV), scale, out, part_size=part)
+        assert rel(out, ref) < 1e-2, part
+
+
+@pytest.mark.parametrize("Hq,Hkv,D", [(32, 8, 128), (8, 8, 128), (16, 8, 128), (28, 4, 128), (32, 8, 64), (64, 8, 128)])
+def test_attn_prefill(Hq, Hkv, D):
+    bs, nb = 16, 256
+    kc, vc = _paged_kv(nb, Hkv, bs, D, 2)
+    q_lens = [37, 1, 130, 64]
+    ctx = [37, 20, 300, 64]  # seq 1 and 2 have cached prefixes
+    S = len(q_lens)
+    maxb = max((c + bs - 1) // bs for c in ctx)
+    bt = torch.zeros(S, maxb, dtype=torch.int32)
+    perm = torch.randperm(nb - 1)[: S * maxb] + 1
+    for s in range(S):
+        bt[s] = perm[s * maxb:(s + 1) * maxb].int()
+    cu = torch.tensor([0] + list(np.cumsum(q_lens)), dtype=torch.int32)
+    T = int(cu[-1])
+    q = torch.randn(T, Hq, D).bfloat16()
+    ctx_t = torch.tensor(ctx, dtype=torch.int32)
+    scale = 1 / math.sqrt(D)
+    ref = torch.empty(T, Hq, D)
+    K.attn_prefill(q, kc, vc, bt, cu, ctx_t, scale, ref, q_lens, ctx)
+    out = torch.empty(T, Hq, D, dtype=torch.bfloat16, device=DEV)
+    K.attn_prefill(q.to(DEV), kc.to(DEV), vc.to(DEV), bt.to(DEV), cu.to(DEV), ctx_t.to(DEV), scale, out, q_lens, ctx)
+    assert rel(out, ref) < 1.5e-2
+
+
+def test_sampling_greedy_and_topk():
+    from localai_tfp_amd.ops.sampling import SamplerBatch, SamplingParams
+    torch.manual_seed(0)
+    V = 128256
+    logits = torch.randn(6, V, device=DEV) * 3
+    am = logits.argmax(-1).cpu()
+    sb = SamplerBatch(DEV)
+    ps = [SamplingParams(temperature=0.0)] * 3 + [SamplingParams(temperature=0.7, top_k=1)] * 3
+    tok, _ = sb.sample(logits.clone(), ps, [[]] * 6, [0] * 6)
+    assert torch.equal(tok.cpu().long(), am)
+    # top-k=5: samples must be inside the top-5 set
+    p5 = [SamplingParams(temperature=1.0, top_k=5, top_p=1.0, min_p=0.0, seed=i) for i in range(6)]
+    top5 = logits.topk(5, -1).indices.cpu()
+    for step in range(20):
+        tok, lp = sb.sample(logits.clone(), p5, [[]] * 6, [step] * 6)
+        for r in range(6):
+            assert int(tok[r]) in top5[r].tolist()
+        assert torch.all(lp.cpu() <= 0)
+
+
+def test_sampling_distribution():
+    from localai_tfp_amd.ops.sampling import SamplerBatch, SamplingParams
+    V = 1000
+    logits = torch.full((1, V), -30.0, device=DEV)
+    logits[0, :4] = torch.log(torch.tensor([0.1, 0.2, 0.3, 0.4], device=DEV))
+    sb = SamplerBatch(DEV)
+    cnt = np.zeros(4)
+    for s in range(2000):
+        tok, _ = sb.sample(logits.clone(), [SamplingParams(temperature=1.0, top_k=0, top_p=1.0, min_p=0.0, seed=s)], [[]], [0])
+        cnt[int(tok[0])] += 1
+    freq = cnt / cnt.sum()
+    assert np.allclose(freq, [0.1, 0.2, 0.3, 0.4], atol=0.04), freq
+
+
+def test_penalties_and_bias():
+    from localai_tfp_amd.ops.sampling import SamplerBatch, SamplingParams
+    V = 5000
+    logits = torch.zeros(1, V, device=DEV)
+    logits[0, 10] = 5.0
+    logits[0, 11] = 4.0
+    sb = SamplerBatch(DEV)
+    p = SamplingParams(temperature=0.0, repeat_penalty=2.0, repeat_last_n=8)
+    tok, _ = sb.sample(logits.clone(), [p], [[10]], [0])
+    assert int(tok[0]) == 11  # 5/2 < 4
+    p2 = SamplingParams(temperature=0.0, logit_bias={42: 100.0})
+    tok, _ = sb.sample(logits.clone(), [p2], [[]], [0])
+    assert int(tok[0]) == 42

@@ -1,0 +1,102 @@
+"""End-to-end GPU checks: the HIP model forward against the fp32 CPU reference of the same
+architecture/weights, and the engine (graphs on/off, prefix cache) on a small Llama."""
+import numpy as np
+import pytest
+import torch
+
+from localai_tfp_amd.engine.engine import EngineConfig, LLMEngine
+from localai_tfp_amd.models.config import tiny_config
+from localai_tfp_amd.models.llama import ForwardBatch, LlamaModel, Workspace
+from localai_tfp_amd.engine.kv_cache import KVCache
+from localai_tfp_amd.models.synthetic import synthetic_source
+from localai_tfp_amd.ops.sampling import SamplingParams
+from localai_tfp_amd.tokenizer import ByteTokenizer
+
+pytestmark = pytest.mark.gpu
+
+
+def _cfg():
+    return tiny_config(hidden=512, ffn=1024, n_heads=8, n_kv_heads=2, head_dim=64, rope_dim=64, vocab=1024,
+                       n_layers=4)
+
+
+def _run(model, dev, prompt, forced):
+    cfg = model.cfg
+    bs = 16
+    kv = KVCache(cfg.n_layers, 64, model.n_kv, bs, cfg.head_dim, dev)
+    ws = Workspace(cfg, 256, 8, dev)
+    blocks = list(range(1, 1 + (len(prompt) + len(forced) + bs) // bs + 1))
+    bt = torch.tensor([blocks], dtype=torch.int32, device=dev)
+    P = len(prompt)
+    pos = torch.arange(P, dtype=torch.int32)
+    slots = torch.tensor([blocks[p // bs] * bs + p % bs for p in range(P)], dtype=torch.int32)
+    fb = ForwardBatch(torch.tensor(prompt, dtype=torch.int32, device=dev), pos.to(dev), slots.to(dev),
+                      torch.tensor([P - 1], dtype=torch.int32, device=dev), n_decode=0, pf_block_tables=bt,
+                      pf_cu_q=torch.tensor([0, P], dtype=torch.int32, device=dev),
+                      pf_ctx_lens=torch.tensor([P], dtype=torch.int32, device=dev), pf_q_lens_host=[P],
+                      pf_ctx_lens_host=[P])
+    outs = [model.forward(fb, kv, ws).float().cpu().clone()]
+    for i, t in enumerate(forced):
+        p = P + i
+        fb = ForwardBatch(torch.tensor([t], dtype=torch.int32, device=dev),
+                          torch.tensor([p], dtype=torch.int32, device=dev),
+                          torch.tensor([blocks[p // bs] * bs + p % bs], dtype=torch.int32, device=dev),
+                          torch.tensor([0], dtype=torch.int32, device=dev), n_decode=1, dec_block_tables=bt,
+                          dec_seq_lens=torch.tensor([p + 1], dtype=torch.int32, device=dev), dec_max_len=p + 1)
+        outs.append(model.forward(fb, kv, ws).float().cpu().clone())
+    return outs
+
+
+def test_forward_matches_cpu_reference():
+    cfg = _cfg()
+    src = synthetic_source(cfg, "Q4_K_M", seed=5)
+    m_cpu = LlamaModel.load(cfg, src, "cpu")
+    m_gpu = LlamaModel.load(cfg, src, "cuda")
+    prompt = list(np.random.default_rng(0).integers(0, cfg.vocab, 40))
+    forced = [5, 99, 700, 3]
+    a = _run(m_cpu, "cpu", prompt, forced)
+    b = _run(m_gpu, "cuda", prompt, forced)
+    for x, y in zip(a, b):
+        r = float((x - y).norm() / x.norm())
+        assert r < 6e-2, r
+
+
+def test_engine_graph_vs_eager_and_prefix_cache():
+    cfg = _cfg()
+    src = synthetic_source(cfg, "Q4_K_M", seed=6)
+    model = LlamaModel.load(cfg, src, "cuda")
+    tok = ByteTokenizer(cfg.vocab)
+    prompt = tok.encode("The quick brown fox jumps over the lazy dog. " * 3)
+    outs = []
+    for graphs in (False, True):
+        e = LLMEngine(model, tok, EngineConfig(num_blocks=512, max_num_seqs=16, max_batched_tokens=512,
+                                               max_model_len=1024, use_graphs=graphs))
+        o = e.generate(prompt, SamplingParams(temperature=0.0), max_tokens=24)
+        o2 = e.generate(prompt, SamplingParams(temperature=0.0), max_tokens=24)
+        assert o2.cached_tokens > 0
+        # the cached run recomputes only the prompt tail (possibly on the q8 GEMV path): require the
+        # greedy streams to agree on their first tokens
+        assert o2.token_ids[:4] == o.token_ids[:4]
+        outs.append(o.token_ids)
+    # graph replay may differ only through non-deterministic split-K atomics; require the prefix
+    # of the greedy stream to agree
+    agree = sum(1 for x, y in zip(*outs) if x == y)
+    assert agree >= 8, outs
+
+
+def test_engine_concurrent_batch():
+    cfg = _cfg()
+    model = LlamaModel.load(cfg, synthetic_source(cfg, "Q4_K_M", seed=7), "cuda")
+    tok = ByteTokenizer(cfg.vocab)
+    e = LLMEngine(model, tok, EngineConfig(num_blocks=1024, max_num_seqs=32, max_batched_tokens=256,
+                                           max_model_len=1024))
+    from localai_tfp_amd.engine.sequence import Request
+    hs = []
+    for i in range(40):
+        p = SamplingParams(temperature=0.8, top_k=40, top_p=0.9, seed=i, ignore_eos=True)
+        hs.append(e.submit(Request(tok.encode(f"request number {i} " * (1 + i % 5)), p, max_tokens=10 + i % 7)))
+    e.run_until_done()
+    for i, h in enumerate(hs):
+        outs = list(h)
+        assert outs[-1].finished and outs[-1].finish_reason == "length"
+        assert sum(len(o.token_ids) for o in outs) == 10 + i % 7
