@@ -60,42 +60,60 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restri
         for (int j = 0; j < 8; ++j) o[h][j] = 0.f;
     }
     const int* bt = block_tables + (size_t)b * bt_stride;
-    for (int base = p0; base < p1; base += PPB) {
-        const int p = base + wave * PPW + pg;
-        const bool valid = p < p1;
-        float kf[8], vf[8];
-        if (valid) {
-            const int blk = bt[p / bs], off = p % bs;
-            const size_t eo = (((size_t)blk * Hkv + kvh) * bs + off) * D + dl * 8;
-            const uint4 kr = *(const uint4*)(kc + eo);
-            const uint4 vr = *(const uint4*)(vc + eo);
-            const uint32_t kw[4] = {kr.x, kr.y, kr.z, kr.w}, vw[4] = {vr.x, vr.y, vr.z, vr.w};
+    // U positions per lane group per iteration: all 2U 16-byte K/V loads are issued before any of
+    // them is consumed (memory-level parallelism), then one online-softmax update covers U keys.
+    constexpr int U = 4;
+    for (int base = p0; base < p1; base += PPB * U) {
+        uint4 kr[U], vr[U];
+        bool valid[U];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                kf[2 * j] = __uint_as_float(kw[j] << 16);
-                kf[2 * j + 1] = __uint_as_float(kw[j] & 0xFFFF0000u);
-                vf[2 * j] = __uint_as_float(vw[j] << 16);
-                vf[2 * j + 1] = __uint_as_float(vw[j] & 0xFFFF0000u);
+        for (int u = 0; u < U; ++u) {
+            const int p = base + u * PPB + wave * PPW + pg;
+            valid[u] = p < p1;
+            if (valid[u]) {
+                const int blk = bt[p / bs], off = p % bs;
+                const size_t eo = (((size_t)blk * Hkv + kvh) * bs + off) * D + dl * 8;
+                kr[u] = *(const uint4*)(kc + eo);
+                vr[u] = *(const uint4*)(vc + eo);
+            } else {
+                kr[u] = vr[u] = make_uint4(0, 0, 0, 0);
             }
-        } else {
-#pragma unroll
-            for (int j = 0; j < 8; ++j) kf[j] = vf[j] = 0.f;
         }
 #pragma unroll
         for (int h = 0; h < G; ++h) {
-            float s = 0.f;
+            float s[U];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) s = fmaf(qf[h][j], kf[j], s);
-            s = group_sum<LPP>(s);
-            if (valid) {
-                const float mn = fmaxf(m[h], s);
-                const float a = exp2f(m[h] - mn);  // m = -inf -> 0
-                const float pr = exp2f(s - mn);
-                l[h] = l[h] * a + pr;
+            for (int u = 0; u < U; ++u) {
+                const uint32_t kw[4] = {kr[u].x, kr[u].y, kr[u].z, kr[u].w};
+                float acc = 0.f;
 #pragma unroll
-                for (int j = 0; j < 8; ++j) o[h][j] = fmaf(pr, vf[j], o[h][j] * a);
-                m[h] = mn;
+                for (int j = 0; j < 4; ++j) {
+                    acc = fmaf(qf[h][2 * j], __uint_as_float(kw[j] << 16), acc);
+                    acc = fmaf(qf[h][2 * j + 1], __uint_as_float(kw[j] & 0xFFFF0000u), acc);
+                }
+                s[u] = group_sum<LPP>(acc);
+                if (!valid[u]) s[u] = -INFINITY;
             }
+            float mx = m[h];
+#pragma unroll
+            for (int u = 0; u < U; ++u) mx = fmaxf(mx, s[u]);
+            if (mx == -INFINITY) continue;  // nothing valid for this lane group yet
+            const float a = exp2f(m[h] - mx);
+            l[h] *= a;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) o[h][j] *= a;
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const float pr = exp2f(s[u] - mx);  // invalid -> exp2(-inf) = 0
+                l[h] += pr;
+                const uint32_t vw[4] = {vr[u].x, vr[u].y, vr[u].z, vr[u].w};
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    o[h][2 * j] = fmaf(pr, __uint_as_float(vw[j] << 16), o[h][2 * j]);
+                    o[h][2 * j + 1] = fmaf(pr, __uint_as_float(vw[j] & 0xFFFF0000u), o[h][2 * j + 1]);
+                }
+            }
+            m[h] = mx;
         }
     }
     // merge the PPW position groups of the wave (xor over lane offsets LPP, 2LPP, ...)
@@ -221,7 +239,7 @@ MX_DEV int v_lds_off(int p, int nt) {
     return p * (D * 2) + ((nt ^ sv) << 5);
 }
 
-template <int D, int GW>
+template <int D, int GW, int VT>
 __global__ __launch_bounds__(512) void attn_prefill_kernel(const bf16_t* __restrict__ q,
                                                            const bf16_t* __restrict__ kc,
                                                            const bf16_t* __restrict__ vc,
@@ -236,10 +254,12 @@ __global__ __launch_bounds__(512) void attn_prefill_kernel(const bf16_t* __restr
     constexpr int KT = 64;                    // keys per tile
     constexpr int KBYTES = KT * D * 2;
     constexpr int PSTRIDE = (KT + 8) * 2;     // bytes per P row (padded)
+    constexpr int VTSTRIDE = (KT + 8) * 2;    // VT=1: bytes per transposed V row (one dim)
+    constexpr int VBYTES = VT ? D * VTSTRIDE : KBYTES;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     char* k_lds = smem;
     char* v_lds = smem + KBYTES;
-    char* p_lds = smem + 2 * KBYTES;
+    char* p_lds = smem + KBYTES + VBYTES;
     const int NT = NW * 64;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int g = lane >> 4, col = lane & 15;
@@ -289,7 +309,14 @@ __global__ __launch_bounds__(512) void attn_prefill_kernel(const bf16_t* __restr
                 vv = *(const uint4*)(vc + eo);
             }
             *(uint4*)(k_lds + k_lds_off<D>(p, c)) = kv;
-            *(uint4*)(v_lds + v_lds_off<D>(p, c >> 1) + 16 * (c & 1)) = vv;
+            if constexpr (VT == 0) {
+                *(uint4*)(v_lds + v_lds_off<D>(p, c >> 1) + 16 * (c & 1)) = vv;
+            } else {
+                const uint32_t w[4] = {vv.x, vv.y, vv.z, vv.w};
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+                    *(bf16_t*)(v_lds + (8 * c + j) * VTSTRIDE + 2 * p) = (bf16_t)(w[j >> 1] >> (16 * (j & 1)));
+            }
         }
         __syncthreads();
         // ---- S = Q K^T : 16 rows x 64 keys ----
@@ -356,15 +383,20 @@ __global__ __launch_bounds__(512) void attn_prefill_kernel(const bf16_t* __restr
             const int q4 = col >> 2, p4 = col & 3;
 #pragma unroll
             for (int nt = 0; nt < D / 16; ++nt) {
-                const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                    (MX_LDS s16x4*)(v_lds + v_lds_off<D>(r0 + q4, nt) + 8 * p4));
-                const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                    (MX_LDS s16x4*)(v_lds + v_lds_off<D>(r0 + 4 + q4, nt) + 8 * p4));
                 bf16x8 vb;
-                vb[0] = __builtin_bit_cast(__bf16, lo[0]); vb[1] = __builtin_bit_cast(__bf16, lo[1]);
-                vb[2] = __builtin_bit_cast(__bf16, lo[2]); vb[3] = __builtin_bit_cast(__bf16, lo[3]);
-                vb[4] = __builtin_bit_cast(__bf16, hi[0]); vb[5] = __builtin_bit_cast(__bf16, hi[1]);
-                vb[6] = __builtin_bit_cast(__bf16, hi[2]); vb[7] = __builtin_bit_cast(__bf16, hi[3]);
+                if constexpr (VT == 0) {
+                    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                        (MX_LDS s16x4*)(v_lds + v_lds_off<D>(r0 + q4, nt) + 8 * p4));
+                    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                        (MX_LDS s16x4*)(v_lds + v_lds_off<D>(r0 + 4 + q4, nt) + 8 * p4));
+                    // whole-vector reinterpretation: per-element bf16 bit_casts of the v4i16 result were
+                    // miscompiled (hipcc dropped elements 2,3 of each transposed read)
+                    const u32x2 l2 = __builtin_bit_cast(u32x2, lo), h2 = __builtin_bit_cast(u32x2, hi);
+                    const u32x4 w4 = {l2[0], l2[1], h2[0], h2[1]};
+                    vb = __builtin_bit_cast(bf16x8, w4);
+                } else {
+                    vb = *(const bf16x8*)(v_lds + (16 * nt + col) * VTSTRIDE + r0 * 2);
+                }
                 oacc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, vb, oacc[nt], 0, 0, 0);
             }
         }
@@ -385,13 +417,19 @@ __global__ __launch_bounds__(512) void attn_prefill_kernel(const bf16_t* __restr
 template <int D, int GW>
 static int launch_prefill(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, const int* bt, int bt_stride,
                           const int* tile_seq, const int* tile_q0, int n_tiles, const int* cu_q,
-                          const int* ctx_lens, int Hq, int Hkv, int bs, float scale, bf16_t* out,
+                          const int* ctx_lens, int Hq, int Hkv, int bs, float scale, bf16_t* out, int vmode,
                           hipStream_t st) {
     constexpr int NW = GW >= 3 ? GW : 4;
-    const size_t lds = 2 * 64 * D * 2 + NW * 16 * (64 + 8) * 2;
     dim3 grid(n_tiles, Hq / GW);
-    attn_prefill_kernel<D, GW><<<grid, NW * 64, lds, st>>>(q, kc, vc, bt, bt_stride, tile_seq, tile_q0, cu_q,
-                                                            ctx_lens, Hq, Hkv, Hq / Hkv, bs, scale, out);
+    if (vmode == 0) {
+        const size_t lds = 2 * 64 * D * 2 + NW * 16 * (64 + 8) * 2;
+        attn_prefill_kernel<D, GW, 0><<<grid, NW * 64, lds, st>>>(q, kc, vc, bt, bt_stride, tile_seq, tile_q0, cu_q,
+                                                                   ctx_lens, Hq, Hkv, Hq / Hkv, bs, scale, out);
+    } else {
+        const size_t lds = 64 * D * 2 + D * (64 + 8) * 2 + NW * 16 * (64 + 8) * 2;
+        attn_prefill_kernel<D, GW, 1><<<grid, NW * 64, lds, st>>>(q, kc, vc, bt, bt_stride, tile_seq, tile_q0, cu_q,
+                                                                   ctx_lens, Hq, Hkv, Hq / Hkv, bs, scale, out);
+    }
     MXK_CHECK_LAUNCH();
 }
 
@@ -406,16 +444,34 @@ extern "C" int mxk_attn_prefill_rows(int Hq, int Hkv) {
 extern "C" int mxk_attn_prefill(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, const int* bt, int bt_stride,
                                 const int* tile_seq, const int* tile_q0, int n_tiles, const int* cu_q,
                                 const int* ctx_lens, int Hq, int Hkv, int D, int bs, float scale, bf16_t* out,
-                                hipStream_t st) {
+                                int vmode, hipStream_t st) {
     if (n_tiles <= 0) return 0;
     if (Hq % Hkv) return (int)hipErrorInvalidValue;
     const int G = Hq / Hkv;
     const int GW = G <= 8 ? G : 8;
     if (G > 8 && G % 8) return (int)hipErrorInvalidValue;
 #define PF(D_, GW_) \
-    if (D == D_ && GW == GW_) return launch_prefill<D_, GW_>(q, kc, vc, bt, bt_stride, tile_seq, tile_q0, n_tiles, cu_q, ctx_lens, Hq, Hkv, bs, scale, out, st);
+    if (D == D_ && GW == GW_) return launch_prefill<D_, GW_>(q, kc, vc, bt, bt_stride, tile_seq, tile_q0, n_tiles, cu_q, ctx_lens, Hq, Hkv, bs, scale, out, vmode, st);
     PF(128, 1) PF(128, 2) PF(128, 3) PF(128, 4) PF(128, 5) PF(128, 6) PF(128, 7) PF(128, 8)
     PF(64, 1) PF(64, 2) PF(64, 4) PF(64, 8)
 #undef PF
     return (int)hipErrorInvalidValue;
+}
+
+// debug probe: semantics of ds_read_b64_tr_b16 on this device. LDS holds value r*16+c at row r
+// (16 rows), column c (16 cols), 32-byte rows; lane l supplies row (l&15)>>2 (+4*(l>>4)),
+// columns 4*(l&3). out[l*4 + e] = element e returned to lane l.
+__global__ void probe_tr16_kernel(short* out) {
+    __shared__ __attribute__((aligned(16))) short lds[16 * 16];
+    for (int i = threadIdx.x; i < 256; i += 64) lds[i] = (short)i;
+    __syncthreads();
+    const int l = threadIdx.x;
+    const int row = ((l & 15) >> 2) + 4 * (l >> 4);
+    const int colg = 4 * (l & 3);
+    s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((MX_LDS s16x4*)(lds + row * 16 + colg));
+    for (int e = 0; e < 4; ++e) out[l * 4 + e] = v[e];
+}
+extern "C" int mxk_probe_tr16(short* out, hipStream_t st) {
+    probe_tr16_kernel<<<1, 64, 0, st>>>(out);
+    MXK_CHECK_LAUNCH();
 }

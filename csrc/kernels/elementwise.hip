@@ -38,6 +38,36 @@ extern "C" int mxk_glu(int act, const bf16_t* g, const bf16_t* u, int ld_in, bf1
     MXK_CHECK_LAUNCH();
 }
 
+// SwiGLU over a gate|up product whose columns are interleaved in 16-column groups (the layout of
+// the fused gate_up weight): y[m, 32*(f/16) + f%16] = gate, y[m, 32*(f/16) + 16 + f%16] = up.
+__global__ __launch_bounds__(256) void swiglu_il16_kernel(const bf16_t* __restrict__ y, int ldy,
+                                                          bf16_t* __restrict__ out, int ldo, int F) {
+    const int m = blockIdx.y;
+    const int f = (blockIdx.x * 256 + threadIdx.x) * 8;  // 8 features: half of a 16-group
+    if (f >= F) return;
+    const int grp = f >> 4, sub = f & 15;
+    const bf16_t* base = y + (size_t)m * ldy + grp * 32 + sub;
+    const uint4 gr = *(const uint4*)base;
+    const uint4 ur = *(const uint4*)(base + 16);
+    const uint32_t gw[4] = {gr.x, gr.y, gr.z, gr.w}, uw[4] = {ur.x, ur.y, ur.z, ur.w};
+    uint32_t o[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const float g0 = __uint_as_float(gw[j] << 16), g1 = __uint_as_float(gw[j] & 0xFFFF0000u);
+        const float u0 = __uint_as_float(uw[j] << 16), u1 = __uint_as_float(uw[j] & 0xFFFF0000u);
+        o[j] = pack_bf16x2(silu_f(g0) * u0, silu_f(g1) * u1);
+    }
+    *(uint4*)(out + (size_t)m * ldo + f) = make_uint4(o[0], o[1], o[2], o[3]);
+}
+
+extern "C" int mxk_swiglu_il16(const bf16_t* y, int ldy, bf16_t* out, int ldo, int M, int F, hipStream_t st) {
+    if (M <= 0) return 0;
+    if (F % 16) return (int)hipErrorInvalidValue;
+    dim3 grid((F / 8 + 255) / 256, M);
+    swiglu_il16_kernel<<<grid, 256, 0, st>>>(y, ldy, out, ldo, F);
+    MXK_CHECK_LAUNCH();
+}
+
 // in-place activation on fp32 (act: 0 silu, 1 gelu-tanh, 2 gelu-erf, 3 relu)
 __global__ __launch_bounds__(256) void act_f32_kernel(float* __restrict__ x, size_t n, int act) {
     for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {

@@ -78,6 +78,16 @@ struct WFrag<MXQ_Q8_0> {
 template <int QT>
 struct Deq;
 
+template <int KS, class D, class F>
+MX_DEV bf16x8 to_bf16x8(const D& d, const F& f) {
+    float v[8];
+    d.template vals<KS>(f, v);
+    bf16x8 r;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = (__bf16)v[j];
+    return r;
+}
+
 template <>
 struct Deq<MXQ_Q4_K> {
     float s[2], m[2];
@@ -90,19 +100,19 @@ struct Deq<MXQ_Q4_K> {
         s[1] = d * sc; m[1] = dm * mn;
     }
     template <int KS>
-    MX_DEV bf16x8 frag(const WFrag<MXQ_Q4_K>& f) const {
+    MX_DEV void vals(const WFrag<MXQ_Q4_K>& f, float (&v)[8]) const {
         constexpr int hi = KS >> 2;
         uint32_t w0 = f.q(2 * (KS & 3)), w1 = f.q(2 * (KS & 3) + 1);
         w0 = (w0 >> (4 * hi)) & 0x0F0F0F0Fu;
         w1 = (w1 >> (4 * hi)) & 0x0F0F0F0Fu;
         const float sc = s[hi], mn = -m[hi];
-        bf16x8 r;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) r[j] = (__bf16)fmaf(sc, (float)((w0 >> (8 * j)) & 0xFF), mn);
+        for (int j = 0; j < 4; ++j) v[j] = fmaf(sc, (float)((w0 >> (8 * j)) & 0xFF), mn);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) r[4 + j] = (__bf16)fmaf(sc, (float)((w1 >> (8 * j)) & 0xFF), mn);
-        return r;
+        for (int j = 0; j < 4; ++j) v[4 + j] = fmaf(sc, (float)((w1 >> (8 * j)) & 0xFF), mn);
     }
+    template <int KS>
+    MX_DEV bf16x8 frag(const WFrag<MXQ_Q4_K>& f) const { return to_bf16x8<KS>(*this, f); }
 };
 
 template <>
@@ -114,20 +124,20 @@ struct Deq<MXQ_Q6_K> {
         for (int i = 0; i < 4; ++i) s[i] = d * (float)(int8_t)((f.sc >> (8 * i)) & 0xFF);
     }
     template <int KS>
-    MX_DEV bf16x8 frag(const WFrag<MXQ_Q6_K>& f) const {
+    MX_DEV void vals(const WFrag<MXQ_Q6_K>& f, float (&v)[8]) const {
         constexpr int hi = KS >> 2, qsh = 2 * (KS >> 1);
         uint32_t w0 = (f.ql(2 * (KS & 3)) >> (4 * hi)) & 0x0F0F0F0Fu;
         uint32_t w1 = (f.ql(2 * (KS & 3) + 1) >> (4 * hi)) & 0x0F0F0F0Fu;
         w0 |= ((f.hh[2 * (KS & 1)] >> qsh) & 0x03030303u) << 4;
         w1 |= ((f.hh[2 * (KS & 1) + 1] >> qsh) & 0x03030303u) << 4;
         const float sc = s[KS >> 1], off = -32.f * sc;
-        bf16x8 r;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) r[j] = (__bf16)fmaf(sc, (float)((w0 >> (8 * j)) & 0xFF), off);
+        for (int j = 0; j < 4; ++j) v[j] = fmaf(sc, (float)((w0 >> (8 * j)) & 0xFF), off);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) r[4 + j] = (__bf16)fmaf(sc, (float)((w1 >> (8 * j)) & 0xFF), off);
-        return r;
+        for (int j = 0; j < 4; ++j) v[4 + j] = fmaf(sc, (float)((w1 >> (8 * j)) & 0xFF), off);
     }
+    template <int KS>
+    MX_DEV bf16x8 frag(const WFrag<MXQ_Q6_K>& f) const { return to_bf16x8<KS>(*this, f); }
 };
 
 template <>
@@ -138,16 +148,16 @@ struct Deq<MXQ_Q8_0> {
         s[1] = half_to_f32(f.d >> 16);
     }
     template <int KS>
-    MX_DEV bf16x8 frag(const WFrag<MXQ_Q8_0>& f) const {
+    MX_DEV void vals(const WFrag<MXQ_Q8_0>& f, float (&v)[8]) const {
         const uint32_t w0 = f.word(2 * KS), w1 = f.word(2 * KS + 1);
         const float sc = s[KS >> 2];
-        bf16x8 r;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) r[j] = (__bf16)(sc * (float)(int8_t)((w0 >> (8 * j)) & 0xFF));
+        for (int j = 0; j < 4; ++j) v[j] = sc * (float)(int8_t)((w0 >> (8 * j)) & 0xFF);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) r[4 + j] = (__bf16)(sc * (float)(int8_t)((w1 >> (8 * j)) & 0xFF));
-        return r;
+        for (int j = 0; j < 4; ++j) v[4 + j] = sc * (float)(int8_t)((w1 >> (8 * j)) & 0xFF);
     }
+    template <int KS>
+    MX_DEV bf16x8 frag(const WFrag<MXQ_Q8_0>& f) const { return to_bf16x8<KS>(*this, f); }
 };
 
 // LDS image of the activation tile: row r (0..BM-1) holds the 256 k of one super-block as 32
@@ -439,29 +449,26 @@ __global__ __launch_bounds__(256) void dequant_rows_kernel(const uint8_t* __rest
     Deq<QT> dq;
     dq.prep(f, g);
     // lane writes elements 64g + 4c .. +3  => k-step ks = c>>1, j in (c&1)*4 .. +3
-    bf16x8 v;
+    float v[8];
     switch (c >> 1) {
-        case 0: v = dq.template frag<0>(f); break;
-        case 1: v = dq.template frag<1>(f); break;
-        case 2: v = dq.template frag<2>(f); break;
-        case 3: v = dq.template frag<3>(f); break;
-        case 4: v = dq.template frag<4>(f); break;
-        case 5: v = dq.template frag<5>(f); break;
-        case 6: v = dq.template frag<6>(f); break;
-        default: v = dq.template frag<7>(f); break;
+        case 0: dq.template vals<0>(f, v); break;
+        case 1: dq.template vals<1>(f, v); break;
+        case 2: dq.template vals<2>(f, v); break;
+        case 3: dq.template vals<3>(f, v); break;
+        case 4: dq.template vals<4>(f, v); break;
+        case 5: dq.template vals<5>(f, v); break;
+        case 6: dq.template vals<6>(f, v); break;
+        default: dq.template vals<7>(f, v); break;
     }
     const int e0 = kb * 256 + 64 * g + 4 * c;
     const int jo = (c & 1) * 4;
     if (ob) {
         uint2 p;
-        p.x = (uint32_t)__builtin_bit_cast(uint16_t, v[jo]) | ((uint32_t)__builtin_bit_cast(uint16_t, v[jo + 1]) << 16);
-        p.y = (uint32_t)__builtin_bit_cast(uint16_t, v[jo + 2]) | ((uint32_t)__builtin_bit_cast(uint16_t, v[jo + 3]) << 16);
+        p.x = pack_bf16x2(v[jo], v[jo + 1]);
+        p.y = pack_bf16x2(v[jo + 2], v[jo + 3]);
         *(uint2*)(ob + (size_t)orow * ldo + e0) = p;
     }
-    if (of) {
-        float4 p = make_float4((float)v[jo], (float)v[jo + 1], (float)v[jo + 2], (float)v[jo + 3]);
-        *(float4*)(of + (size_t)orow * ldo + e0) = p;
-    }
+    if (of) *(float4*)(of + (size_t)orow * ldo + e0) = make_float4(v[jo], v[jo + 1], v[jo + 2], v[jo + 3]);
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -42,8 +42,8 @@ class EngineConfig:
     enable_prefix_cache: bool = True
     use_graphs: bool = True
     graph_buckets: tuple = (1, 2, 4, 8, 16, 32, 48, 64, 96, 128, 160, 192, 224, 256)
-    attn_part_size: int = 512
-    prefill_bf16_cache: bool = False
+    attn_part_size: int = 256  # must match ops.core.attn_decode's default
+    prefill_bf16_cache: bool = True  # dense bf16 copy of the linear weights for M>=128 prefill (GPU)
 
 
 class RequestHandle:

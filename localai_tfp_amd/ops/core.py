@@ -216,7 +216,7 @@ def _attn_ref_one(q, k_cache, v_cache, table, ctx: int, qpos0: int, scale: float
 
 
 def attn_decode(q: torch.Tensor, k_cache, v_cache, block_tables: torch.Tensor, seq_lens: torch.Tensor,
-                scale: float, out: torch.Tensor, part_size: int = 512, n_parts: int | None = None,
+                scale: float, out: torch.Tensor, part_size: int = 256, n_parts: int | None = None,
                 workspace: tuple | None = None, max_seq_len: int | None = None):
     """q bf16 [B, Hq, D] (one query token per sequence, at position seq_len-1)."""
     B, Hq, D = q.shape
@@ -254,8 +254,12 @@ def prefill_tiles(q_lens, rows_per_tile: int):
     return seqs, q0s
 
 
+ATTN_VMODE = int(__import__("os").environ.get("MX_ATTN_VMODE", "0"))
+
+
 def attn_prefill(q: torch.Tensor, k_cache, v_cache, block_tables: torch.Tensor, cu_q: torch.Tensor,
-                 ctx_lens: torch.Tensor, scale: float, out: torch.Tensor, q_lens_host=None, ctx_lens_host=None):
+                 ctx_lens: torch.Tensor, scale: float, out: torch.Tensor, q_lens_host=None, ctx_lens_host=None,
+                 vmode: int | None = None):
     """q bf16 [T, Hq, D] for S sequences (cu_q [S+1]); keys 0..ctx_len-1 from the paged cache."""
     T, Hq, D = q.shape
     if T == 0:
@@ -279,7 +283,8 @@ def attn_prefill(q: torch.Tensor, k_cache, v_cache, block_tables: torch.Tensor, 
     tiles = torch.tensor([seqs, q0s], dtype=torch.int32).to(q.device, non_blocking=True)
     N.kcall("mxk_attn_prefill", q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), block_tables.data_ptr(),
             block_tables.stride(0), tiles[0].data_ptr(), tiles[1].data_ptr(), len(seqs), cu_q.data_ptr(),
-            ctx_lens.data_ptr(), Hq, Hkv, D, bs, float(scale), out.data_ptr(), N.stream_ptr())
+            ctx_lens.data_ptr(), Hq, Hkv, D, bs, float(scale), out.data_ptr(),
+            ATTN_VMODE if vmode is None else int(vmode), N.stream_ptr())
     return out
 
 

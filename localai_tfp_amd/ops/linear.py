@@ -23,6 +23,8 @@ from . import quant as Q
 
 EPI_F32, EPI_BF16, EPI_ADD_F32, EPI_SWIGLU = 0, 1, 2, 3
 CU_COUNT = 256
+# prefill rows at or above this go through the dense bf16 weight cache (hipBLASLt) when enabled
+BF16_CACHE_MIN_M = int(__import__("os").environ.get("MX_BF16_CACHE_MIN_M", "128"))
 
 
 class QWeight:
@@ -188,8 +190,12 @@ def qmatmul(W: QWeight, x: torch.Tensor | None, epi: int, out: torch.Tensor, *, 
         return out
     if x is None:
         raise ValueError("qmatmul: MFMA path needs bf16 activations")
-    if W.bf16_cache is not None and M >= 256:
+    if W.bf16_cache is not None and M >= BF16_CACHE_MIN_M:
         y = torch.matmul(x, W.bf16_cache.t())
+        if epi == EPI_SWIGLU:
+            N.kcall("mxk_swiglu_il16", y.data_ptr(), y.stride(0), out.data_ptr(), out.stride(0), M, W.N // 2,
+                    N.stream_ptr())
+            return out
         return _apply_epi_dense(y, epi, out)
     nblk = W.K // 256
     can_split = epi == EPI_ADD_F32 or (epi == EPI_F32 and out_zeroed)

@@ -65,7 +65,7 @@ def dq_q4_0(raw):
     qs = b[:, 2:18]
     lo = (qs & 0xF).astype(np.int8) - 8
     hi = (qs >> 4).astype(np.int8) - 8
-    return (np.concatenate([lo, hi], 1).astype(np.float32) * d).reshape(-1)
+    return (np.concatenate([lo, hi], 1).astype(np.float32) * d[:, None]).reshape(-1)
 
 
 def dq_q4_1(raw):
@@ -74,7 +74,7 @@ def dq_q4_1(raw):
     m = _f16(b[:, 2:4].copy())
     qs = b[:, 4:20]
     q = np.concatenate([qs & 0xF, qs >> 4], 1).astype(np.float32)
-    return (q * d + m).reshape(-1)
+    return (q * d[:, None] + m[:, None]).reshape(-1)
 
 
 def _q5_high(qh_bytes):
@@ -91,7 +91,7 @@ def dq_q5_0(raw):
     lo = (qs & 0xF) | (hb[:, :16] << 4)
     hi = (qs >> 4) | (hb[:, 16:] << 4)
     q = np.concatenate([lo, hi], 1).astype(np.float32) - 16
-    return (q * d).reshape(-1)
+    return (q * d[:, None]).reshape(-1)
 
 
 def dq_q5_1(raw):
@@ -103,14 +103,14 @@ def dq_q5_1(raw):
     lo = (qs & 0xF) | (hb[:, :16] << 4)
     hi = (qs >> 4) | (hb[:, 16:] << 4)
     q = np.concatenate([lo, hi], 1).astype(np.float32)
-    return (q * d + m).reshape(-1)
+    return (q * d[:, None] + m[:, None]).reshape(-1)
 
 
 def dq_q8_0(raw):
     b = _blocks(raw, QType.Q8_0)
     d = _f16(b[:, 0:2].copy())
     q = b[:, 2:34].view(np.int8).astype(np.float32)
-    return (q * d).reshape(-1)
+    return (q * d[:, None]).reshape(-1)
 
 
 def dq_q2_k(raw):

@@ -198,8 +198,19 @@ def test_attn_decode(Hq, Hkv, D, lens):
         assert rel(out, ref) < 1e-2, part
 
 
+def test_probe_tr16_semantics():
+    out = torch.zeros(256, dtype=torch.int16, device=DEV)
+    N.kcall("mxk_probe_tr16", out.data_ptr(), N.stream_ptr())
+    got = out.cpu().view(64, 4).tolist()
+    # expected (guide §5.5 T10): lane i of a 16-lane group receives column i of the group's 4 rows
+    exp = [[(4 * (l >> 4) + e) * 16 + (l & 15) for e in range(4)] for l in range(64)]
+    print("tr16 lanes 0..7:", got[:8])
+    assert got == exp
+
+
+@pytest.mark.parametrize("vmode", [0, 1])
 @pytest.mark.parametrize("Hq,Hkv,D", [(32, 8, 128), (8, 8, 128), (16, 8, 128), (28, 4, 128), (32, 8, 64), (64, 8, 128)])
-def test_attn_prefill(Hq, Hkv, D):
+def test_attn_prefill(Hq, Hkv, D, vmode):
     bs, nb = 16, 256
     kc, vc = _paged_kv(nb, Hkv, bs, D, 2)
     q_lens = [37, 1, 130, 64]
@@ -218,8 +229,14 @@ def test_attn_prefill(Hq, Hkv, D):
     ref = torch.empty(T, Hq, D)
     K.attn_prefill(q, kc, vc, bt, cu, ctx_t, scale, ref, q_lens, ctx)
     out = torch.empty(T, Hq, D, dtype=torch.bfloat16, device=DEV)
-    K.attn_prefill(q.to(DEV), kc.to(DEV), vc.to(DEV), bt.to(DEV), cu.to(DEV), ctx_t.to(DEV), scale, out, q_lens, ctx)
-    assert rel(out, ref) < 1.5e-2
+    K.attn_prefill(q.to(DEV), kc.to(DEV), vc.to(DEV), bt.to(DEV), cu.to(DEV), ctx_t.to(DEV), scale, out, q_lens, ctx,
+                   vmode=vmode)
+    errs = []
+    off = 0
+    for s, ql in enumerate(q_lens):
+        errs.append(round(rel(out[off:off + ql], ref[off:off + ql]), 4))
+        off += ql
+    assert rel(out, ref) < 1.5e-2, errs
 
 
 def test_sampling_greedy_and_topk():

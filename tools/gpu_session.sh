@@ -13,5 +13,14 @@ if [ -n "${BENCH_ARGS+x}" ]; then
   timeout -k 10 ${BENCH_TIMEOUT:-600} python bench.py $BENCH_ARGS > gpurun_out/bench.log 2>&1
   rc=$?
   echo "bench rc=$rc"; tail -3 gpurun_out/bench.log
+  [ $rc -ne 0 ] && exit $rc
+fi
+if [ -n "${PROF_ARGS+x}" ]; then
+  cd /tmp && export TMPDIR=/tmp
+  timeout -k 10 ${PROF_TIMEOUT:-600} rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" $PROF_ARGS > "$GRAFT_REPO_ROOT/gpurun_out/prof.log" 2>&1
+  rc=$?
+  cd "$GRAFT_REPO_ROOT"
+  echo "prof rc=$rc"; tail -3 gpurun_out/prof.log
+  find gpurun_out/prof -name "*stats*" | head
   exit $rc
 fi
