@@ -38,6 +38,9 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restri
     const int p0 = part * part_size;
     const int p1 = min(L, p0 + part_size);
     const int Hq = Hkv * G;
+    // partitions past the end of this sequence do nothing (the reduce kernel reads only the
+    // ceil(L / part_size) live ones); graphs launch a fixed partition count for max_model_len.
+    if (p0 >= L && part > 0) return;
 
     float qf[G][8];
     const float qs = scale * LOG2E;

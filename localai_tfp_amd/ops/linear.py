@@ -191,7 +191,15 @@ def qmatmul(W: QWeight, x: torch.Tensor | None, epi: int, out: torch.Tensor, *, 
     if x is None:
         raise ValueError("qmatmul: MFMA path needs bf16 activations")
     if W.bf16_cache is not None and M >= BF16_CACHE_MIN_M:
-        y = torch.matmul(x, W.bf16_cache.t())
+        wt = W.bf16_cache.t()
+        if epi in (EPI_ADD_F32, EPI_F32) and out.is_contiguous() and _fp32_out_ok():
+            # hipBLASLt bf16 x bf16 -> fp32 with the residual add fused as beta = 1
+            if epi == EPI_ADD_F32:
+                torch.addmm(out, x, wt, out_dtype=torch.float32, out=out)
+            else:
+                torch.mm(x, wt, out_dtype=torch.float32, out=out)
+            return out
+        y = torch.matmul(x, wt)
         if epi == EPI_SWIGLU:
             N.kcall("mxk_swiglu_il16", y.data_ptr(), y.stride(0), out.data_ptr(), out.stride(0), M, W.N // 2,
                     N.stream_ptr())
@@ -206,6 +214,26 @@ def qmatmul(W: QWeight, x: torch.Tensor | None, epi: int, out: torch.Tensor, *, 
     N.kcall("mxk_qgemm_mfma", int(W.qtype), e, wm, wn, x.data_ptr(), x.stride(0), W.data.data_ptr(),
             N.ptr(W.dplane), M, W.N, W.K, splits, out.data_ptr(), out.stride(0), N.stream_ptr())
     return out
+
+
+_FP32_OUT = None
+
+
+def _fp32_out_ok() -> bool:
+    """Does this torch build expose mm/addmm with out_dtype=float32 for bf16 inputs (ROCm)?"""
+    global _FP32_OUT
+    if _FP32_OUT is None:
+        try:
+            a = torch.ones(16, 32, dtype=torch.bfloat16, device="cuda")
+            b = torch.ones(32, 16, dtype=torch.bfloat16, device="cuda")
+            o = torch.ones(16, 16, dtype=torch.float32, device="cuda")
+            torch.addmm(o, a, b, out_dtype=torch.float32, out=o)
+            o2 = torch.empty(16, 16, dtype=torch.float32, device="cuda")
+            torch.mm(a, b, out_dtype=torch.float32, out=o2)
+            _FP32_OUT = bool(torch.allclose(o, torch.full_like(o, 33.0))) and bool(torch.allclose(o2, torch.full_like(o2, 32.0)))
+        except Exception:
+            _FP32_OUT = False
+    return _FP32_OUT
 
 
 def _apply_epi_dense(y: torch.Tensor, epi: int, out: torch.Tensor):
