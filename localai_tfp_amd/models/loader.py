@@ -1,0 +1,80 @@
+"""Model acquisition for the LLM worker: GGUF files (llama.cpp's format, what the reference's
+llama-cpp backend loads) or `synthetic:<arch>` random-init checkpoints of a named architecture
+(bench / tests — there is no network to fetch real weights)."""
+from __future__ import annotations
+
+import logging
+import os
+
+import numpy as np
+
+from ..formats.gguf import GGUFReader
+from . import config as C
+from .config import LlamaConfig
+from .llama import LlamaModel
+
+log = logging.getLogger("localai_tfp_amd.models")
+
+SYNTHETIC = {"llama3-8b": C.LLAMA3_8B, "llama3-70b": C.LLAMA3_70B, "llama32-1b": C.LLAMA32_1B,
+             "tiny": C.tiny_config()}
+SUPPORTED_ARCHS = {"llama", "mistral", "qwen2", "qwen3", "granite", "internlm2", "deci", "exaone", "olmo", "minicpm",
+                   "smollm", "codellama"}
+
+
+def gguf_source(reader: GGUFReader):
+    def get_tensor(name):
+        ti = reader.tensors.get(name)
+        if ti is None:
+            return None
+        return reader.tensor_bytes(name), ti.qtype, ti.shape
+    return get_tensor
+
+
+def load_llm(model: str, device="cpu", tp_rank: int = 0, tp_size: int = 1, tp_group=None, overrides: dict | None = None):
+    """-> (LlamaModel, tokenizer, LlamaConfig, metadata dict)"""
+    from ..tokenizer import ByteTokenizer, from_gguf
+    ov = overrides or {}
+    if model.startswith("synthetic:"):
+        from .synthetic import synthetic_source
+        key = model.split(":", 1)[1]
+        cfg = SYNTHETIC[key]
+        import copy
+        cfg = copy.deepcopy(cfg)
+        _apply_overrides(cfg, ov)
+        m = LlamaModel.load(cfg, synthetic_source(cfg, "Q4_K_M", seed=1), device, tp_rank, tp_size, tp_group)
+        return m, ByteTokenizer(cfg.vocab), cfg, {}
+    if not os.path.isfile(model):
+        raise FileNotFoundError(model)
+    r = GGUFReader(model)
+    md = dict(r.metadata)
+    arch = str(md.get("general.architecture", "llama"))
+    if arch not in SUPPORTED_ARCHS:
+        log.warning("architecture %r not in the tested set; trying the Llama graph", arch)
+    cfg = LlamaConfig.from_gguf_metadata(md)
+    if f"{arch}.rope.scaling.type" not in md and "rope_freqs.weight" in r.tensors:
+        from ..ops.quant import dequantize
+        ti = r.tensors["rope_freqs.weight"]
+        cfg.extra["rope_freqs"] = dequantize(r.tensor_bytes("rope_freqs.weight"), ti.qtype, ti.shape).tolist()
+    _apply_overrides(cfg, ov)
+    m = LlamaModel.load(cfg, gguf_source(r), device, tp_rank, tp_size, tp_group)
+    try:
+        tok = from_gguf(md)
+    except Exception as ex:
+        log.warning("no usable tokenizer in %s (%s); byte-level fallback", model, ex)
+        tok = ByteTokenizer(cfg.vocab)
+    return m, tok, cfg, md
+
+
+def _apply_overrides(cfg: LlamaConfig, ov: dict):
+    if ov.get("rope_freq_base"):
+        cfg.rope_base = float(ov["rope_freq_base"])
+    if ov.get("rope_freq_scale"):
+        cfg.rope_scale = float(ov["rope_freq_scale"])
+        if cfg.rope_scaling == "none":
+            cfg.rope_scaling = "linear"
+    if ov.get("rope_scaling"):
+        cfg.rope_scaling = str(ov["rope_scaling"])
+    if ov.get("rms_norm_eps"):
+        cfg.rms_eps = float(ov["rms_norm_eps"])
+    if ov.get("context_size"):
+        cfg.ctx_train = max(cfg.ctx_train, int(ov["context_size"])) if ov.get("extend_context") else cfg.ctx_train

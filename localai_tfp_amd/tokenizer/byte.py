@@ -67,3 +67,13 @@ class ByteTokenizer:
 
     def token_to_piece(self, t: int) -> str:
         return self.decode([t], skip_special=False)
+
+
+def _byte_token_bytes(self) -> list[bytes]:
+    out = [bytes([i]) for i in range(256)]
+    out += [b""] * len(self.specials)
+    out += [f"<t{i}>".encode() for i in range(len(out), self.vocab_size)]
+    return out
+
+
+ByteTokenizer.token_bytes = _byte_token_bytes

@@ -55,6 +55,28 @@ class _Base:
     def token_to_piece(self, t: int) -> str:
         return self.decode([t], skip_special=False)
 
+    def token_bytes(self) -> list[bytes]:
+        """Raw bytes each token id emits (b"" for control tokens) — for grammar masking."""
+        if getattr(self, "_tb", None) is None:
+            self._tb = [b"" if self.token_type[i] in (TT_CONTROL, TT_UNKNOWN, TT_UNUSED) else self._piece_bytes(i)
+                        for i in range(self.vocab_size)]
+        return self._tb
+
+
+def _bytes_to_unicode():
+    bs = list(range(ord("!"), ord("~") + 1)) + list(range(ord("¡"), ord("¬") + 1)) + list(range(ord("®"), ord("ÿ") + 1))
+    cs = bs[:]
+    n = 0
+    for b in range(256):
+        if b not in bs:
+            bs.append(b)
+            cs.append(256 + n)
+            n += 1
+    return {chr(c): b for b, c in zip(bs, cs)}
+
+
+_U2B = _bytes_to_unicode()
+
 
 class BPETokenizer(_Base):
     def __init__(self, md: dict):
@@ -93,6 +115,15 @@ class BPETokenizer(_Base):
 
     def decode(self, ids, skip_special: bool = True) -> str:
         return self._tk.decode([int(i) for i in ids], skip_special_tokens=skip_special)
+
+    def _piece_bytes(self, i: int) -> bytes:
+        t = self.tokens[i]
+        if self.token_type[i] == TT_USER:
+            return t.encode()
+        try:
+            return bytes(_U2B[c] for c in t)
+        except KeyError:
+            return t.encode()
 
 
 def _bpe_has_ignore():
@@ -189,6 +220,12 @@ class SPMTokenizer(_Base):
         if add_special and self.add_eos and self.eos_token_id is not None:
             ids.append(int(self.eos_token_id))
         return ids
+
+    def _piece_bytes(self, i: int) -> bytes:
+        piece = self.tokens[i]
+        if self.token_type[i] == TT_BYTE or re.fullmatch(r"<0x[0-9A-Fa-f]{2}>", piece):
+            return bytes([int(piece[3:5], 16)])
+        return piece.replace("▁", " ").encode()
 
     def decode(self, ids, skip_special: bool = True) -> str:
         buf = bytearray()
