@@ -321,7 +321,9 @@ class LLMEngine:
                 return self._sample(logits, sample_items)
         # ---- eager path ----
         fb = self._build_fb(so, tokens, positions, slots, lidx)
+        fb.keep_hidden = any(it.seq.req.embedding for it in sample_items)
         logits = self.model.forward(fb, self.kv, self.ws)
+        self._hidden = self.model.last_hidden if fb.keep_hidden else None
         if not sample_items:
             return [], None
         return self._sample(logits, sample_items)
@@ -392,10 +394,24 @@ class LLMEngine:
             s = it.seq
             if s.status == Status.FINISHED:
                 continue
-            t = int(toks[k])
-            lp = lps[k] if lps is not None else None
             if s.t_first_token is None:
                 s.t_first_token = now
+            if s.req.embedding:
+                # last-token pooling over the final-normed hidden state, L2-normalised
+                # (grpc-server.cpp:1357-1414 send_embedding with pooling != NONE)
+                v = self._hidden[k]
+                v = (v / v.norm().clamp_min(1e-12)).cpu().tolist()
+                self.sched.finish(s, "stop")
+                h = self.handles.get(s.rid)
+                o = StepOutput(s.rid, finished=True, finish_reason="stop", embedding=v)
+                self._fill_usage(s, o, metrics=False)
+                self.handles.pop(s.rid, None)
+                self.seqs.pop(s.rid, None)
+                if h is not None:
+                    h.q.put(o)
+                continue
+            t = int(toks[k])
+            lp = lps[k] if lps is not None else None
             if s.grammar is not None:
                 s.grammar.accept(t)
             if s.params.mirostat == 2 and lp is not None:
@@ -435,7 +451,7 @@ class LLMEngine:
         if h is not None:
             h.q.put(o)
 
-    def _fill_usage(self, s: Sequence, o: StepOutput):
+    def _fill_usage(self, s: Sequence, o: StepOutput, metrics: bool = True):
         o.prompt_tokens = len(s.prompt_ids)
         o.completion_tokens = len(s.output_ids)
         o.cached_tokens = s.num_cached
@@ -443,8 +459,10 @@ class LLMEngine:
         o.ttft_ms = (t_first - s.t_arrival) * 1e3
         o.t_prompt_ms = (t_first - (s.t_first_sched or s.t_arrival)) * 1e3
         o.t_gen_ms = ((s.t_finish or time.perf_counter()) - t_first) * 1e3
-        self.last_metrics = dict(tokens_per_second=(o.completion_tokens / max(o.t_gen_ms, 1e-3) * 1e3),
-                                 tokens_generated=o.completion_tokens, prompt_tokens_processed=o.prompt_tokens)
+        if metrics:
+            self.last_metrics = dict(tokens_per_second=(o.completion_tokens / max(o.t_gen_ms, 1e-3) * 1e3),
+                                     tokens_generated=o.completion_tokens,
+                                     prompt_tokens_processed=o.prompt_tokens)
 
     def _finish(self, s: Sequence, reason: str):
         if s.status != Status.FINISHED:

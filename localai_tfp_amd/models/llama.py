@@ -64,6 +64,7 @@ class ForwardBatch:
     pf_q_lens_host: list = field(default_factory=list)
     pf_ctx_lens_host: list = field(default_factory=list)
     want_hidden: bool = False  # embeddings: return normalised hidden rows instead of logits
+    keep_hidden: bool = False  # also stash the final-normed hidden rows in model.last_hidden
 
     @property
     def T(self) -> int:
@@ -319,8 +320,11 @@ class LlamaModel:
         S = fb.logits_idx.numel()
         hs = ws.hs[:S]
         K.select_rows(h, fb.logits_idx, hs)
-        if fb.want_hidden:
-            return hs * torch.rsqrt(hs.pow(2).mean(-1, keepdim=True) + eps) * self.out_norm
+        if fb.want_hidden or fb.keep_hidden:
+            hn = hs.float() * torch.rsqrt(hs.float().pow(2).mean(-1, keepdim=True) + eps) * self.out_norm
+            if fb.want_hidden:
+                return hn
+            self.last_hidden = hn
         logits = ws.logits[:S]
         if S <= GEMV_MAX_M and self.device.type == "cuda" and self.lm_head.is_quant:
             xq, xds = ws.q8(S, H)

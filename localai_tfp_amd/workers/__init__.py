@@ -1,0 +1,44 @@
+"""gRPC backend workers (one process per model instance, one GPU per process).
+
+Registry of backend names -> worker modules, with the reference's aliases
+(pkg/model/initializers.go:24-41)."""
+WORKERS = {
+    "llama-cpp": "localai_tfp_amd.workers.llm",
+    "mx-llm": "localai_tfp_amd.workers.llm",
+    "vllm": "localai_tfp_amd.workers.llm",
+    "transformers": "localai_tfp_amd.workers.llm",
+    "exllama2": "localai_tfp_amd.workers.llm",
+    "bert-embeddings": "localai_tfp_amd.workers.bert",
+    "sentencetransformers": "localai_tfp_amd.workers.bert",
+    "rerankers": "localai_tfp_amd.workers.bert",
+    "whisper": "localai_tfp_amd.workers.whisper",
+    "faster-whisper": "localai_tfp_amd.workers.whisper",
+    "stablediffusion-ggml": "localai_tfp_amd.workers.diffusion",
+    "diffusers": "localai_tfp_amd.workers.diffusion",
+    "local-store": "localai_tfp_amd.workers.store",
+    "silero-vad": "localai_tfp_amd.workers.vad",
+    "piper": "localai_tfp_amd.workers.tts",
+    "bark": "localai_tfp_amd.workers.tts",
+    "bark-cpp": "localai_tfp_amd.workers.tts",
+    "coqui": "localai_tfp_amd.workers.tts",
+    "kokoro": "localai_tfp_amd.workers.tts",
+}
+
+ALIASES = {
+    "llama": "llama-cpp",
+    "llama.cpp": "llama-cpp",
+    "go-llama": "llama-cpp",
+    "sentencetransformers": "transformers",
+    "stablediffusion": "stablediffusion-ggml",
+    "tinydream": "stablediffusion-ggml",
+    "huggingface-embeddings": "bert-embeddings",
+    "whisper-ggml": "whisper",
+}
+
+# auto-detection order when a model config names no backend (initializers.go:137-179)
+AUTODETECT_ORDER = ["llama-cpp", "bert-embeddings", "whisper", "stablediffusion-ggml", "piper", "silero-vad"]
+
+
+def resolve(name: str) -> str:
+    n = (name or "").strip().lower()
+    return ALIASES.get(n, n)

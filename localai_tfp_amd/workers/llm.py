@@ -1,0 +1,314 @@
+"""LLM worker: the backend.Backend gRPC service over :class:`engine.LLMEngine`.
+
+Behavioural parity target: the reference's llama.cpp gRPC server
+(backend/cpp/llama/grpc-server.cpp):
+  * LoadModel  - ModelOptions -> engine/model settings (params_parse :2324-2455, LoadModel :2467-2487)
+  * Predict / PredictStream - PredictOptions -> sampling request (parse_options :2164-2229), replies
+    carrying message / tokens / prompt_tokens / timings (:2488-2576)
+  * Embedding  - final-token pooled, L2-normalised hidden state (:2579-2601, send_embedding :1357-1414)
+  * TokenizeString (:2603-2613), GetMetrics (:2615-2638); Status (not implemented there) reports
+    engine state + HBM use here.
+
+Differences by design: the engine is a paged-KV continuous-batching scheduler with hipGraph decode
+(no per-slot context split, no `n_parallel`), `Messages` + `UseTokenizerTemplate` are honoured
+(the reference ignores them), grammars are enforced by the native GBNF matcher
+(csrc/runtime/grammar.cpp) with optional lazy trigger words (ModelOptions.GrammarTriggers).
+"""
+from __future__ import annotations
+
+import json
+import logging
+import os
+import threading
+import time
+
+import grpc
+
+from ..engine.engine import EngineConfig, LLMEngine
+from ..engine.sequence import Request
+from ..grpc import pb
+from ..grpc.server import BackendServicer, worker_main
+from ..ops.sampling import SamplingParams
+
+log = logging.getLogger("localai_tfp_amd.workers.llm")
+
+
+def parse_options(opts) -> dict:
+    """ModelOptions.Options: ["key:value", "flag", ...] -> dict (grpc-server.cpp:2403-2430)."""
+    out = {}
+    for o in opts:
+        k, _, v = o.partition(":")
+        out[k.strip()] = v.strip() if v else True
+    return out
+
+
+def sampling_from_predict(r) -> SamplingParams:
+    p = SamplingParams()
+    p.temperature = float(r.Temperature)
+    p.top_k = int(r.TopK) if r.TopK > 0 else 0
+    p.top_p = float(r.TopP) if 0 < r.TopP <= 1 else 1.0
+    p.typical_p = float(r.TypicalP) if 0 < r.TypicalP < 1 else 1.0
+    p.min_p = 0.0
+    p.repeat_penalty = float(r.Penalty) if r.Penalty > 0 else 1.0
+    p.repeat_last_n = int(r.Repeat) if r.Repeat != 0 else 64
+    p.presence_penalty = float(r.PresencePenalty)
+    p.frequency_penalty = float(r.FrequencyPenalty)
+    p.mirostat = int(r.Mirostat)
+    if r.MirostatTAU:
+        p.mirostat_tau = float(r.MirostatTAU)
+    if r.MirostatETA:
+        p.mirostat_eta = float(r.MirostatETA)
+    p.seed = int(r.Seed) if r.Seed not in (0, -1) else -1
+    p.ignore_eos = bool(r.IgnoreEOS)
+    if r.LogitBias:
+        try:
+            lb = json.loads(r.LogitBias)
+            p.logit_bias = {int(k): float(v) for k, v in lb.items()}
+        except (ValueError, AttributeError):
+            log.warning("ignoring malformed LogitBias %r", r.LogitBias[:80])
+    return p
+
+
+class LazyGrammar:
+    """Grammar enforced only after a trigger word shows up in the output (lazy grammars,
+    grpc-server.cpp:2437-2451). Before the trigger every token is allowed."""
+
+    def __init__(self, make_matcher, triggers: list[str], token_bytes):
+        self.make, self.triggers, self.tb = make_matcher, triggers, token_bytes
+        self.m = None
+        self.buf = b""
+        self._dead = False
+
+    def allowed_mask(self, V):
+        if self.m is None:
+            import numpy as np
+            return np.full((V + 31) // 32, 0xFFFFFFFF, np.uint32)
+        return self.m.allowed_mask(V)
+
+    def accept(self, t: int) -> bool:
+        if self.m is not None:
+            return self.m.accept(t)
+        self.buf += self.tb[t] if t < len(self.tb) else b""
+        for w in self.triggers:
+            i = self.buf.find(w.encode())
+            if i >= 0:
+                self.m = self.make()
+                self._dead = not self.m.accept_bytes(self.buf[i:])
+                return True
+        return True
+
+    def is_done(self) -> bool:
+        return self.m is not None and (self._dead or self.m.is_done())
+
+
+class LLMServicer(BackendServicer):
+    def __init__(self, device: str | None = None):
+        super().__init__()
+        self.engine: LLMEngine | None = None
+        self.tok = None
+        self.model_opts = None
+        self.device = device
+        self._vocab = None
+        self._tb = None
+        self._grammars: dict[str, object] = {}
+        self._glock = threading.Lock()
+        self.triggers: list[str] = []
+        self.embeddings_enabled = False
+        self.state = pb.STATE_UNINITIALIZED
+
+    # ---------------------------------------------------------------- load
+    def LoadModel(self, request, context):
+        import torch
+        from ..models.loader import load_llm
+        try:
+            t0 = time.perf_counter()
+            opts = parse_options(request.Options)
+            path = request.ModelFile or request.Model
+            if path and not path.startswith("synthetic:") and not os.path.isabs(path) and request.ModelPath:
+                path = os.path.join(request.ModelPath, path)
+            if self.device is None:
+                if torch.cuda.is_available():
+                    mg = request.MainGPU.strip()
+                    self.device = f"cuda:{int(mg)}" if mg.isdigit() else "cuda:0"
+                else:
+                    self.device = "cpu"
+            if request.LoraAdapter or len(request.LoraAdapters):
+                log.warning("LoRA adapters are not supported by this worker yet; ignoring")
+            ov = {"rope_freq_base": request.RopeFreqBase, "rope_freq_scale": request.RopeFreqScale,
+                  "rope_scaling": request.RopeScaling, "rms_norm_eps": request.RMSNormEps}
+            model, tok, mcfg, _ = load_llm(path, self.device, overrides=ov)
+            ec = EngineConfig()
+            if request.ContextSize > 0:
+                ec.max_model_len = int(request.ContextSize)
+            if request.NBatch > 0:
+                ec.max_batched_tokens = max(int(request.NBatch), 64)
+            par = int(os.environ.get("LLAMACPP_PARALLEL", "0") or 0) or int(opts.get("parallel", 0) or 0)
+            if par > 0:
+                ec.max_num_seqs = par
+            if "gpu_memory_utilization" in opts or request.GPUMemoryUtilization > 0:
+                ec.kv_mem_fraction = float(opts.get("gpu_memory_utilization", request.GPUMemoryUtilization))
+            if opts.get("no_prefix_cache") or opts.get("cache_prompt") == "false":
+                ec.enable_prefix_cache = False
+            if request.EnforceEager or opts.get("enforce_eager"):
+                ec.use_graphs = False
+            if self.device == "cpu":
+                ec.num_blocks = ec.num_blocks or 512
+            self.engine = LLMEngine(model, tok, ec)
+            self.engine.start()
+            self.tok = tok
+            self.model_opts = request
+            self.embeddings_enabled = bool(request.Embeddings)
+            self.triggers = [t.word for t in request.GrammarTriggers if t.word]
+            self.state = pb.STATE_READY
+            msg = f"loaded {path} in {time.perf_counter() - t0:.1f}s on {self.device}"
+            log.info(msg)
+            return pb.Result(message=msg, success=True)
+        except Exception as ex:
+            log.exception("LoadModel failed")
+            self.state = pb.STATE_ERROR
+            return pb.Result(message=f"failed to load model: {ex}", success=False)
+
+    # ---------------------------------------------------------------- helpers
+    def _need_engine(self, context):
+        if self.engine is None:
+            context.abort(grpc.StatusCode.FAILED_PRECONDITION, "model not loaded")
+
+    def _prompt_ids(self, r) -> list[int]:
+        if r.UseTokenizerTemplate and len(r.Messages) and getattr(self.tok, "chat_template", None):
+            from ..templates.chat import render_chat
+            msgs = [{"role": m.role, "content": m.content} for m in r.Messages]
+            text = render_chat(msgs, self.tok, add_generation_prompt=True)
+            return self.tok.encode(text, add_special=False)
+        if len(r.EmbeddingTokens) and not r.Prompt:
+            return list(r.EmbeddingTokens)
+        return self.tok.encode(r.Prompt, add_special=True)
+
+    def _grammar(self, gbnf: str):
+        from ..runtime_native import GrammarMatcher, NativeGrammar, NativeVocab
+        with self._glock:
+            if self._vocab is None:
+                self._tb = self.tok.token_bytes()
+                self._vocab = NativeVocab(self._tb)
+            g = self._grammars.get(gbnf)
+            if g is None:
+                g = NativeGrammar(gbnf)
+                if len(self._grammars) > 64:
+                    self._grammars.clear()
+                self._grammars[gbnf] = g
+        eos = self.tok.eos_token_id if self.tok.eos_token_id is not None else -1
+        vocab, tb = self._vocab, self._tb
+
+        def make():
+            return GrammarMatcher(g, vocab, tb, eos)
+        if self.triggers:
+            return lambda: LazyGrammar(make, self.triggers, tb)
+        return make
+
+    def _request(self, r) -> Request:
+        ids = self._prompt_ids(r)
+        mt = int(r.Tokens)
+        max_tokens = mt if mt > 0 else self.engine.cfg.max_model_len
+        req = Request(ids, sampling_from_predict(r), max_tokens, [s for s in r.StopPrompts if s])
+        req.cache_prompt = True
+        req.n_keep = int(r.NKeep) if r.NKeep > 0 else 0
+        if r.Grammar:
+            req.grammar = self._grammar(r.Grammar)
+        if len(r.Images) or len(r.Videos) or len(r.Audios):
+            log.warning("multimodal inputs are not supported by the LLM worker; ignoring %d images",
+                        len(r.Images))
+        return req
+
+    @staticmethod
+    def _reply(o, text: bytes | str = b"") -> object:
+        if isinstance(text, str):
+            text = text.encode("utf-8")
+        return pb.Reply(message=text, tokens=o.completion_tokens, prompt_tokens=o.prompt_tokens,
+                        timing_prompt_processing=o.t_prompt_ms, timing_token_generation=o.t_gen_ms)
+
+    # ---------------------------------------------------------------- RPCs
+    def Predict(self, request, context):
+        self._need_engine(context)
+        req = self._request(request)
+        h = self.engine.submit(req)
+        context.add_callback(lambda: self.engine.abort(req.rid) if not h.done else None)
+        parts = []
+        last = None
+        for o in h:
+            parts.append(o.text)
+            last = o
+        h.done = True
+        if last.finish_reason and last.finish_reason.startswith("error"):
+            context.abort(grpc.StatusCode.INTERNAL, last.finish_reason)
+        return self._reply(last, "".join(parts))
+
+    def PredictStream(self, request, context):
+        self._need_engine(context)
+        req = self._request(request)
+        h = self.engine.submit(req)
+        context.add_callback(lambda: self.engine.abort(req.rid) if not h.done else None)
+        for o in h:
+            if o.finished:
+                h.done = True
+                if o.finish_reason and o.finish_reason.startswith("error"):
+                    context.abort(grpc.StatusCode.INTERNAL, o.finish_reason)
+                yield self._reply(o, o.text)
+                return
+            if o.text:
+                yield pb.Reply(message=o.text.encode("utf-8"), tokens=0, prompt_tokens=0)
+
+    def Embedding(self, request, context):
+        self._need_engine(context)
+        if len(request.EmbeddingTokens):
+            ids = list(request.EmbeddingTokens)
+        else:
+            ids = self.tok.encode(request.Embeddings or request.Prompt, add_special=True)
+        req = Request(ids, SamplingParams(temperature=0.0), 1)
+        req.embedding = True
+        req.cache_prompt = False
+        h = self.engine.submit(req)
+        last = None
+        for o in h:
+            last = o
+        if last is None or last.embedding is None:
+            context.abort(grpc.StatusCode.INTERNAL, f"embedding failed: {last.finish_reason if last else '?'}")
+        return pb.EmbeddingResult(embeddings=last.embedding)
+
+    def TokenizeString(self, request, context):
+        self._need_engine(context)
+        ids = self.tok.encode(request.Prompt, add_special=False)
+        return pb.TokenizationResponse(length=len(ids), tokens=ids)
+
+    def GetMetrics(self, request, context):
+        m = self.engine.last_metrics if self.engine else {}
+        return pb.MetricsResponse(slot_id=0, prompt_json_for_slot="",
+                                  tokens_per_second=float(m.get("tokens_per_second", 0.0)),
+                                  tokens_generated=int(m.get("tokens_generated", 0)),
+                                  prompt_tokens_processed=int(m.get("prompt_tokens_processed", 0)))
+
+    def Status(self, request, context):
+        st = super().Status(request, context)
+        if self.engine is None:
+            st.state = self.state
+            return st
+        e = self.engine
+        busy = e.sched.has_work()
+        st.state = pb.STATE_BUSY if busy else self.state
+        try:
+            import torch
+            if e.device.type == "cuda":
+                st.memory.breakdown["gpu_allocated"] = int(torch.cuda.memory_allocated(e.device))
+                st.memory.breakdown["kv_cache"] = int(e.kv.k.numel() * e.kv.k.element_size() * 2)
+                st.memory.breakdown["weights"] = int(e.model.weight_bytes())
+        except Exception:
+            pass
+        for k in ("prompt_tokens_total", "gen_tokens_total", "cached_tokens_total", "preemptions"):
+            st.memory.breakdown[k] = int(e.stats.get(k, 0))
+        return st
+
+
+def main(argv=None):
+    worker_main(LLMServicer, argv)
+
+
+if __name__ == "__main__":
+    main()
