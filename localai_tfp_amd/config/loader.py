@@ -29,6 +29,7 @@ class ModelConfigLoader:
         self.model_path = str(model_path)
         self.ctx_size, self.threads, self.f16, self.debug = ctx_size, threads, f16, debug
         self._configs: dict[str, ModelConfig] = {}
+        self._implicit: dict[str, ModelConfig] = {}
         self._lock = threading.RLock()
 
     # ---------------------------------------------------------------- loading
@@ -91,12 +92,18 @@ class ModelConfigLoader:
                 self.load_config_file(cand)
                 with self._lock:
                     c = self._configs.get(name)
+        if c is not None:
+            return c.copy()  # defaults were applied when the file was read
+        # implicit config for a bare model file; cached so the GGUF header is parsed once, not per request
+        with self._lock:
+            c = self._implicit.get(name)
         if c is None:
             c = ModelConfig(name=name)
             c.parameters.model = name
-        c = c.copy()
-        self._defaults(c)
-        return c
+            self._defaults(c)
+            with self._lock:
+                self._implicit[name] = c
+        return c.copy()
 
     # ---------------------------------------------------------------- queries
     def get(self, name: str) -> ModelConfig | None:

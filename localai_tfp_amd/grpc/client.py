@@ -104,3 +104,47 @@ class BackendClient:
                 return lambda req, timeout=None: self.stream(name, req, timeout)
             return lambda req, timeout=None: self.call(name, req, timeout)
         raise AttributeError(name)
+
+
+class AsyncBackendClient:
+    """grpc.aio twin of :class:`BackendClient` for the gateway's event loop (one channel per
+    backend address and loop; streaming token replies never block a worker thread)."""
+
+    def __init__(self, address: str, sync: BackendClient | None = None):
+        import grpc.aio
+        self.address = address
+        self.sync = sync  # shares busy/last-used bookkeeping with the sync client (WatchDog)
+        self._chan = grpc.aio.insecure_channel(address, options=[("grpc.max_send_message_length", MAX_MSG),
+                                                                 ("grpc.max_receive_message_length", MAX_MSG)])
+        self._stubs = {}
+        for name, (_, req, resp, stream) in METHODS.items():
+            path = f"/{FULL_SERVICE}/{name}"
+            rs = getattr(pb, resp).FromString
+            qs = getattr(pb, req).SerializeToString
+            self._stubs[name] = (self._chan.unary_stream(path, request_serializer=qs, response_deserializer=rs)
+                                 if stream else
+                                 self._chan.unary_unary(path, request_serializer=qs, response_deserializer=rs))
+
+    async def call(self, name: str, request, timeout: float | None = None):
+        if self.sync:
+            self.sync._enter()
+        try:
+            return await self._stubs[name](request, timeout=timeout)
+        finally:
+            if self.sync:
+                self.sync._exit()
+
+    async def stream(self, name: str, request, timeout: float | None = None):
+        if self.sync:
+            self.sync._enter()
+        call = self._stubs[name](request, timeout=timeout)
+        try:
+            async for r in call:
+                yield r
+        finally:
+            call.cancel()  # no-op when finished; aborts the backend request if the client went away
+            if self.sync:
+                self.sync._exit()
+
+    async def close(self):
+        await self._chan.close()
