@@ -1,23 +1,34 @@
 #!/usr/bin/env python3
-"""Headline benchmark: output tokens/s + p50 TTFT of chat-completion serving, Llama-3-8B-Instruct
-Q4_K_M, one engine replica per GPU (BASELINE.json config #2; N GPUs = data-parallel replicas).
+"""Headline benchmark: output tokens/s + p50 TTFT of /v1/chat/completions serving, Llama-3-8B-Instruct
+Q4_K_M, one serving replica per GPU (BASELINE.json config #2; N GPUs = N data-parallel replicas).
 
 Contract (driver): `python bench.py --gpus N --steps K --warmup W`; for N > 1 it is launched with
-torch.distributed.run, one rank per GPU (RCCL). Each rank builds a random-init Llama-3-8B with the
-exact Q4_K_M tensor types of a real checkpoint (models/synthetic.py; no network for weights) and
-serves a closed-loop load of `--concurrency` chat requests (prompt `--prompt-len` tokens rendered
-through the Llama-3 chat template, `--gen-len` output tokens, ignore_eos). A "step" is one engine
-iteration (continuous batching: decode rows + chunked prefill). W untimed steps (graph capture,
-warm caches), then exactly K timed steps bracketed by barrier + device sync. Output tokens counted
-are those produced inside the timed window; TTFT is measured per request from submission to its
-first token (requests whose first token lands in the window). Rank 0 prints one JSON line.
+torch.distributed.run, one rank per GPU (RCCL). Each rank:
+  * builds a random-init Llama-3-8B with the exact Q4_K_M tensor types of a real checkpoint
+    (models/synthetic.py; no network for weights) and its LLM engine (paged KV, continuous batching,
+    hipGraph decode) inside an LLM gRPC worker (workers/llm.py, grpc.aio server) in this process;
+  * (`--path http`, default) starts the HTTP gateway (`python -m localai_tfp_amd run`, FastAPI) in a
+    child process, pointed at the worker as an external gRPC backend, and a closed-loop load generator
+    (tools/loadgen.py) in another child: `--concurrency` users streaming chat completions
+    (prompt `--prompt-len` tokens after the Llama-3 chat template, `--gen-len` tokens, ignore_eos);
+  * (`--path engine`) drives the engine directly in-process (kernel/scheduler-only number).
+A "step" is one engine iteration (continuous batching: decode rows + chunked prefill). The engine
+thread itself brackets the window: at step W it does device sync + barrier and records t0, at step
+W+K again sync + barrier and t1, so exactly K steps are timed on every rank. Output tokens = tokens
+the engine generated for HTTP requests inside the window; TTFT = client-side time from sending the
+request to the first content chunk, over requests whose first token arrived inside the window.
+value = sum over ranks of tokens / max over ranks of window. Rank 0 prints one JSON line.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import signal
+import subprocess
 import sys
+import tempfile
+import threading
 import time
 
 import numpy as np
@@ -27,21 +38,46 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "output tokens/sec + p50 TTFT, /v1/chat/completions Llama-3-8B Q4_K at 1/2/4/8 MI355X"
+TEMPLATE_OVERHEAD = 24  # Llama-3 chat template tokens around one user message (ByteTokenizer)
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=300)
-    ap.add_argument("--warmup", type=int, default=60)
+    ap.add_argument("--steps", type=int, default=400)
+    ap.add_argument("--warmup", type=int, default=200)
     ap.add_argument("--model", default="llama3-8b", choices=["llama3-8b", "llama3-70b", "llama32-1b"])
+    ap.add_argument("--path", default="http", choices=["http", "engine"])
     ap.add_argument("--concurrency", type=int, default=128)
     ap.add_argument("--prompt-len", type=int, default=256)
     ap.add_argument("--gen-len", type=int, default=256)
     ap.add_argument("--max-batched-tokens", type=int, default=2048)
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--profile-steps", type=int, default=0)
+    ap.add_argument("--timeout", type=float, default=900.0, help="abort if the window is not reached")
     return ap.parse_args()
+
+
+def free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def wait_http(url: str, timeout: float, proc=None):
+    import urllib.request
+    t0 = time.time()
+    while time.time() - t0 < timeout:
+        if proc is not None and proc.poll() is not None:
+            raise RuntimeError(f"gateway exited with {proc.returncode}")
+        try:
+            with urllib.request.urlopen(url, timeout=2) as r:
+                if r.status == 200:
+                    return
+        except Exception:
+            time.sleep(0.25)
+    raise TimeoutError(url)
 
 
 def main():
@@ -61,12 +97,9 @@ def main():
     from localai_tfp_amd import _build
     _build.build_all()
     from localai_tfp_amd.engine.engine import EngineConfig, LLMEngine
-    from localai_tfp_amd.engine.sequence import Request
     from localai_tfp_amd.models import config as C
     from localai_tfp_amd.models.llama import LlamaModel
     from localai_tfp_amd.models.synthetic import synthetic_source
-    from localai_tfp_amd.ops.sampling import SamplingParams
-    from localai_tfp_amd.templates.chat import render_chat
     from localai_tfp_amd.tokenizer import ByteTokenizer
 
     cfg = {"llama3-8b": C.LLAMA3_8B, "llama3-70b": C.LLAMA3_70B, "llama32-1b": C.LLAMA32_1B}[args.model]
@@ -78,30 +111,194 @@ def main():
     tok = ByteTokenizer(cfg.vocab)
     ecfg = EngineConfig(max_num_seqs=args.concurrency, max_batched_tokens=args.max_batched_tokens,
                         max_model_len=max(4096, args.prompt_len + args.gen_len + 64), use_graphs=not args.no_graphs)
+    if dev.type == "cpu":
+        ecfg.num_blocks = 2048
     eng = LLMEngine(model, tok, ecfg)
+    t0 = time.time()
+    n_graphs = eng.precapture_graphs()
+    t_capture = time.time() - t0
 
-    rng = np.random.default_rng(1234 + rank)
-    words = ["the", "model", "serves", "tokens", "fast", "on", "MI355X", "with", "paged", "attention", "and",
-             "hipGraph", "decode", "kernels", "for", "every", "request", "in", "the", "batch"]
+    if args.path == "http":
+        res = run_http(args, eng, tok, cfg, dev, dist)
+    else:
+        res = run_engine(args, eng, tok, dev, dist)
+    t_el, tokens, ttfts, extra = res
+
+    p50 = float(np.percentile(ttfts, 50)) if len(ttfts) else float("nan")
+    p99 = float(np.percentile(ttfts, 99)) if len(ttfts) else float("nan")
+    t_max, tok_sum, p50_all, p99_all = t_el, float(tokens), p50, p99
+    if dist:
+        tt = torch.tensor([t_el, float(tokens), p50, p99], device=dev, dtype=torch.float64)
+        mx = tt.clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        sm = tt.clone()
+        dist.all_reduce(sm, op=dist.ReduceOp.SUM)
+        t_max, tok_sum = float(mx[0]), float(sm[1])
+        p50_all, p99_all = float(sm[2] / world), float(mx[3])
+    value = tok_sum / t_max
+    if rank == 0:
+        st = eng.stats
+        out = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "output tokens/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(t_max / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic (random-init Llama-3-8B weights in real Q4_K_M block formats; synthetic chat prompts)",
+            "p50_ttft_ms": round(p50_all, 2),
+            "p99_ttft_ms": round(p99_all, 2),
+            "config": {
+                "model": cfg.name + " Q4_K_M", "global_batch": args.concurrency * world,
+                "seq_len": args.prompt_len + args.gen_len, "prompt_len": args.prompt_len, "gen_len": args.gen_len,
+                "concurrency_per_gpu": args.concurrency, "parallelism": f"dp{world}",
+                "path": ("HTTP /v1/chat/completions (SSE) -> gateway -> gRPC -> engine" if args.path == "http"
+                         else "engine in-process (gateway/gRPC excluded)"),
+                "load_s": round(t_load, 1), "graph_capture_s": round(t_capture, 1), "graphs": n_graphs,
+                "graph_steps": st["graph_steps"], "total_steps": st["steps"],
+                "weights_gb": round(model.weight_bytes() / 1e9, 2), "kv_blocks": eng.kv.num_blocks, **extra,
+            },
+        }
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+class Window:
+    """Engine-thread hook: sync + barrier at step W and W+K; exactly K steps timed."""
+
+    def __init__(self, eng, warmup, steps, dev, dist):
+        self.eng, self.W, self.K, self.dev, self.dist = eng, warmup, steps, dev, dist
+        self.t0 = self.t1 = None
+        self.tok0 = self.tok1 = 0
+        self.done = threading.Event()
+
+    def _sync(self):
+        if self.dev.type == "cuda":
+            torch.cuda.synchronize(self.dev)
+        if self.dist:
+            self.dist.barrier()
+
+    def __call__(self, i):
+        if i == self.W and self.t0 is None:
+            self._sync()
+            self.t0 = time.monotonic()
+            self.tok0 = self.eng.stats["out_tokens"]
+        elif i == self.W + self.K and self.t1 is None:
+            self._sync()
+            self.t1 = time.monotonic()
+            self.tok1 = self.eng.stats["out_tokens"]
+            self.done.set()
+
+
+def run_http(args, eng, tok, cfg, dev, dist):
+    import yaml
+    from localai_tfp_amd.grpc.server import AioServer
+    from localai_tfp_amd.workers.llm import LLMServicer
+
+    svc = LLMServicer(device=str(dev))
+    svc.attach(eng, tok)
+    win = Window(eng, args.warmup, args.steps, dev, dist)
+    eng.on_step = win
+    eng.start()
+    server = AioServer(svc, "127.0.0.1:0", max_workers=16)
+    work = tempfile.mkdtemp(prefix="mxbench")
+    models = os.path.join(work, "models")
+    os.makedirs(models)
+    with open(os.path.join(models, "llama-3-8b-instruct.yaml"), "w") as f:
+        yaml.safe_dump({"name": "llama-3-8b-instruct", "backend": "llama-cpp",
+                        "context_size": eng.cfg.max_model_len,
+                        "parameters": {"model": f"synthetic:{args.model}", "temperature": 0.0},
+                        "template": {"use_tokenizer_template": True},
+                        "known_usecases": ["chat"]}, f)
+    port = free_port()
+    env = dict(os.environ)
+    env["LOCALAI_GPUS"] = "none"          # the gateway never touches the GPU
+    env.pop("RANK", None), env.pop("WORLD_SIZE", None), env.pop("LOCAL_RANK", None)
+    gw_log = open(os.path.join(work, "gateway.log"), "w")
+    gw = subprocess.Popen([sys.executable, "-m", "localai_tfp_amd", "run", "--models-path", models,
+                           "--address", f"127.0.0.1:{port}", "--disable-webui", "--log-level", "warning",
+                           "--localai-config-dir", os.path.join(work, "cfg"),
+                           "--generated-content-path", os.path.join(work, "gen"),
+                           "--upload-path", os.path.join(work, "up"),
+                           "--external-grpc-backends", f"llama-cpp:127.0.0.1:{server.port}"],
+                          env=env, cwd=ROOT, stdout=gw_log, stderr=subprocess.STDOUT, start_new_session=True)
+    lg = None
+    try:
+        wait_http(f"http://127.0.0.1:{port}/readyz", 120, gw)
+        rec_path = os.path.join(work, "loadgen.json")
+        lg = subprocess.Popen([sys.executable, "-m", "localai_tfp_amd.tools.loadgen",
+                               "--url", f"http://127.0.0.1:{port}", "--model", "llama-3-8b-instruct",
+                               "--concurrency", str(args.concurrency),
+                               "--prompt-chars", str(max(1, args.prompt_len - TEMPLATE_OVERHEAD)),
+                               "--gen-len", str(args.gen_len), "--seed", str(int(os.environ.get("RANK", "0"))),
+                               "--out", rec_path], env=env, cwd=ROOT, start_new_session=True)
+        t_start = time.time()
+        last = -1
+        while not win.done.wait(30):
+            n = eng.stats["steps"]
+            print(f"[bench rank {os.environ.get('RANK', '0')}] steps={n} out_tokens={eng.stats['out_tokens']}",
+                  file=sys.stderr, flush=True)
+            if lg.poll() is not None or gw.poll() is not None:
+                raise RuntimeError("load generator or gateway exited early; see " + work)
+            if time.time() - t_start > args.timeout or (n == last and n > 0):
+                raise TimeoutError(f"window not reached (steps={n}); see {work}")
+            last = n
+    finally:
+        if lg is not None and lg.poll() is None:
+            lg.send_signal(signal.SIGTERM)
+            try:
+                lg.wait(timeout=60)
+            except subprocess.TimeoutExpired:
+                lg.kill()
+        eng.on_step = None
+        eng.shutdown()
+        gw.terminate()
+        try:
+            gw.wait(timeout=20)
+        except subprocess.TimeoutExpired:
+            gw.kill()
+        server.stop()
+    recs = []
+    try:
+        with open(rec_path) as f:
+            recs = json.load(f)
+    except (OSError, ValueError):
+        pass
+    t0, t1 = win.t0, win.t1
+    ttfts = [(r["t_first"] - r["t_send"]) * 1e3 for r in recs if r.get("t_first") and t0 <= r["t_first"] <= t1]
+    done = [r for r in recs if r.get("ok") and t0 <= r["t_end"] <= t1]
+    client_tps = sum(r["tokens"] for r in done) / (t1 - t0) if done else 0.0
+    errors = sum(1 for r in recs if r.get("error") not in (None, "CancelledError"))
+    extra = {"client_completed_requests": len(done), "client_tokens_per_s_completed": round(client_tps, 1),
+             "http_errors": errors, "ttft_samples": len(ttfts)}
+    return t1 - t0, win.tok1 - win.tok0, ttfts, extra
+
+
+def run_engine(args, eng, tok, dev, dist):
+    from localai_tfp_amd.engine.sequence import Request
+    from localai_tfp_amd.ops.sampling import SamplingParams
+    from localai_tfp_amd.templates.chat import render_chat
+    rng = np.random.default_rng(1234 + int(os.environ.get("RANK", "0")))
+    words = ["the", "model", "serves", "tokens", "fast", "on", "MI355X", "with", "paged", "attention"]
 
     def make_prompt():
-        # chat request -> Llama-3 template -> byte tokens, trimmed/padded to prompt_len
-        body = " ".join(rng.choice(words, size=args.prompt_len))
-        ids = tok.encode(render_chat([{"role": "user", "content": body}], tok))
-        ids = ids[: args.prompt_len]
-        return ids
+        body = " ".join(rng.choice(words, size=args.prompt_len))[: max(1, args.prompt_len - TEMPLATE_OVERHEAD)]
+        return tok.encode(render_chat([{"role": "user", "content": body}], tok))
 
     sp = SamplingParams(temperature=0.0, top_k=1, ignore_eos=True)
-    inflight = {}
-    ttfts_all = []
-    stats = {"tokens": 0}
-    timed = {"on": False}
     handles = {}
+    ttfts = []
+    timed = {"on": False}
 
     def submit():
         req = Request(make_prompt(), sp, max_tokens=args.gen_len)
-        h = eng.submit(req)
-        handles[req.rid] = (h, time.perf_counter())
+        handles[req.rid] = (eng.submit(req), time.monotonic())
 
     for _ in range(args.concurrency):
         submit()
@@ -111,12 +308,10 @@ def main():
         for rid, (h, t_sub) in list(handles.items()):
             while not h.q.empty():
                 o = h.q.get_nowait()
-                if timed["on"]:
-                    stats["tokens"] += len(o.token_ids)
                 if o.token_ids and not getattr(h, "_first", False):
                     h._first = True
                     if timed["on"]:
-                        ttfts_all.append((time.perf_counter() - t_sub) * 1e3)
+                        ttfts.append((time.monotonic() - t_sub) * 1e3)
                 if o.finished:
                     done.append(rid)
         for rid in done:
@@ -135,68 +330,16 @@ def main():
     if dist:
         dist.barrier()
     timed["on"] = True
-    t_start = time.perf_counter()
-    prof = None
-    if args.profile_steps:
-        prof = torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CPU, torch.profiler.ProfilerActivity.CUDA])
-        prof.start()
-    for i in range(args.steps):
+    tok0 = eng.stats["out_tokens"]
+    t_start = time.monotonic()
+    for _ in range(args.steps):
         step()
     if dev.type == "cuda":
         torch.cuda.synchronize()
     if dist:
         dist.barrier()
-    t_el = time.perf_counter() - t_start
-    if prof:
-        prof.stop()
-        if rank == 0:
-            print(prof.key_averages().table(sort_by="cuda_time_total", row_limit=30), file=sys.stderr)
-    tokens = stats["tokens"]
-    p50 = float(np.percentile(ttfts_all, 50)) if ttfts_all else float("nan")
-    p99 = float(np.percentile(ttfts_all, 99)) if ttfts_all else float("nan")
-    t_max = t_el
-    tok_sum = tokens
-    p50_all = p50
-    if dist:
-        tt = torch.tensor([t_el, float(tokens), p50], device=dev, dtype=torch.float64)
-        mx = tt.clone()
-        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-        sm = tt.clone()
-        dist.all_reduce(sm, op=dist.ReduceOp.SUM)
-        t_max = float(mx[0])
-        tok_sum = float(sm[1])
-        p50_all = float(sm[2] / world)
-    value = tok_sum / t_max
-    if rank == 0:
-        st = eng.stats
-        out = {
-            "metric": METRIC,
-            "value": round(value, 2),
-            "unit": "output tokens/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(t_max / args.steps * 1e3, 3),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "bf16",
-            "data": "synthetic (random-init Llama-3-8B weights in real Q4_K_M block formats; synthetic chat prompts)",
-            "p50_ttft_ms": round(p50_all, 2),
-            "p99_ttft_ms": round(p99, 2),
-            "config": {
-                "model": cfg.name + " Q4_K_M", "global_batch": args.concurrency * world,
-                "seq_len": args.prompt_len + args.gen_len, "prompt_len": args.prompt_len, "gen_len": args.gen_len,
-                "concurrency_per_gpu": args.concurrency, "parallelism": f"dp{world}",
-                "path": "engine (scheduler+kernels, in-process; gateway/gRPC excluded)",
-                "load_s": round(t_load, 1), "graph_steps": st["graph_steps"], "total_steps": st["steps"],
-                "weights_gb": round(model.weight_bytes() / 1e9, 2), "kv_blocks": eng.kv.num_blocks,
-            },
-        }
-        print(json.dumps(out), flush=True)
-    eng.shutdown()
-    if dist:
-        dist.destroy_process_group()
+    t_el = time.monotonic() - t_start
+    return t_el, eng.stats["out_tokens"] - tok0, ttfts, {}
 
 
 if __name__ == "__main__":

@@ -47,10 +47,20 @@ class EngineConfig:
 
 
 class RequestHandle:
-    def __init__(self, rid: int):
+    """Per-request output channel. By default a thread-safe queue; `sink` (e.g. an asyncio
+    loop.call_soon_threadsafe bound to an asyncio.Queue) receives outputs instead."""
+
+    def __init__(self, rid: int, sink=None):
         self.rid = rid
         self.q: queue.Queue[StepOutput] = queue.Queue()
+        self.sink = sink
         self.done = False
+
+    def put(self, o: StepOutput):
+        if self.sink is not None:
+            self.sink(o)
+        else:
+            self.q.put(o)
 
     def __iter__(self):
         while True:
@@ -140,14 +150,16 @@ class LLMEngine:
         self.use_graphs = c.use_graphs and self.device.type == "cuda"
         self.eos_ids = set(getattr(tokenizer, "eos_token_ids", []) or [])
         self.stats = dict(steps=0, decode_tokens=0, prefill_tokens=0, graph_steps=0, preemptions=0,
-                          busy_s=0.0, prompt_tokens_total=0, gen_tokens_total=0, cached_tokens_total=0)
+                          busy_s=0.0, prompt_tokens_total=0, gen_tokens_total=0, cached_tokens_total=0,
+                          out_tokens=0)
         self.last_metrics = {}
+        self.on_step = None  # optional hook called with the step index before each loop step (bench)
         if c.prefill_bf16_cache and self.device.type == "cuda":
             model.enable_prefill_bf16_cache()
 
     # ------------------------------------------------------------------ request API
-    def submit(self, req: Request) -> RequestHandle:
-        h = RequestHandle(req.rid)
+    def submit(self, req: Request, sink=None) -> RequestHandle:
+        h = RequestHandle(req.rid, sink)
         self.handles[req.rid] = h
         self._inbox.put(("add", req))
         with self._cv:
@@ -186,6 +198,16 @@ class LLMEngine:
                     self._finish(s, "abort")
 
     # ------------------------------------------------------------------ loop
+    def precapture_graphs(self):
+        """Capture every decode bucket up front (vLLM-style) so no capture lands mid-serving."""
+        if not self.use_graphs:
+            return 0
+        n = 0
+        for b in self.cfg.graph_buckets:
+            if b <= self.cfg.max_num_seqs and self._graph_for(b) is not None:
+                n += 1
+        return n
+
     def start(self):
         if self._thread is None:
             self._thread = threading.Thread(target=self._loop, name="llm-engine", daemon=True)
@@ -208,6 +230,8 @@ class LLMEngine:
                     self._cv.wait(timeout=0.05)
                 continue
             try:
+                if self.on_step is not None:
+                    self.on_step(self.stats["steps"])
                 self.step()
             except Exception as ex:  # fail every in-flight request loudly, keep the worker alive
                 log.exception("engine step failed")
@@ -408,7 +432,7 @@ class LLMEngine:
                 self.handles.pop(s.rid, None)
                 self.seqs.pop(s.rid, None)
                 if h is not None:
-                    h.q.put(o)
+                    h.put(o)
                 continue
             t = int(toks[k])
             lp = lps[k] if lps is not None else None
@@ -418,6 +442,7 @@ class LLMEngine:
                 # mu <- mu - eta * (surprise - tau)  (surprise in bits)
                 s.mirostat_mu -= s.params.mirostat_eta * (-lp / 0.6931471805599453 - s.params.mirostat_tau)
             s.append_token(t, lp)
+            self.stats["out_tokens"] += 1
             reason = None
             if (t in self.eos_ids or t in s.req.stop_token_ids) and not s.params.ignore_eos:
                 reason = "stop"
@@ -449,7 +474,7 @@ class LLMEngine:
             st["gen_tokens_total"] += len(s.output_ids)
             st["cached_tokens_total"] += s.num_cached
         if h is not None:
-            h.q.put(o)
+            h.put(o)
 
     def _fill_usage(self, s: Sequence, o: StepOutput, metrics: bool = True):
         o.prompt_tokens = len(s.prompt_ids)

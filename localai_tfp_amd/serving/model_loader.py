@@ -96,7 +96,7 @@ class Replica:
             eng = getattr(self.servicer, "engine", None)
             if eng is not None and hasattr(eng, "shutdown"):
                 eng.shutdown()
-            self.server.stop(0)
+            self.server.stop()
         if self.proc is not None and self.proc.poll() is None:
             self.proc.terminate()
             try:
@@ -369,7 +369,7 @@ class ModelLoader:
 
     def _start_inproc(self, backend: str, parallel: bool, gpus) -> Replica:
         import importlib
-        from ..grpc.server import make_server
+        from ..grpc.server import AioServer
         mod = importlib.import_module(_module_for(backend))
         servicer_cls = next(getattr(mod, n) for n in dir(mod) if n.endswith("Servicer") and n != "BackendServicer")
         dev = None
@@ -379,9 +379,8 @@ class ModelLoader:
             svc = servicer_cls(device=dev)
         except TypeError:
             svc = servicer_cls()
-        server, port = make_server(svc, "127.0.0.1:0", max_workers=64)
-        server.start()
-        addr = f"127.0.0.1:{port}"
+        server = AioServer(svc, "127.0.0.1:0")
+        addr = f"127.0.0.1:{server.port}"
         return Replica(addr, BackendClient(addr, parallel=parallel), None, tuple(gpus), server, svc)
 
     def _spawn(self, backend: str, ext: str | None, parallel: bool, gpus, tp: int) -> Replica:

@@ -1,0 +1,105 @@
+"""Closed-loop HTTP load generator for /v1/chat/completions (SSE streaming).
+
+`--concurrency` virtual users each send a chat request, consume the SSE stream, record
+(t_send, t_first_content, t_end, completion_tokens) with time.monotonic() (system-wide clock on
+Linux, so the numbers line up with the server process), and immediately send the next request.
+Runs until SIGTERM/SIGINT or `--duration`, then writes all records as JSON to `--out`.
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import json
+import random
+import signal
+import time
+
+WORDS = ["the", "model", "serves", "tokens", "fast", "on", "MI355X", "with", "paged", "attention", "and",
+         "hipGraph", "decode", "kernels", "for", "every", "request", "in", "batch", "xGMI"]
+
+
+async def one(session, url, body, rec, stop):
+    t0 = time.monotonic()
+    r = {"t_send": t0, "t_first": None, "t_end": None, "tokens": 0, "ok": False}
+    try:
+        async with session.post(url, json=body) as resp:
+            buf = b""
+            async for chunk in resp.content.iter_any():
+                buf += chunk
+                while b"\n\n" in buf:
+                    ev, buf = buf.split(b"\n\n", 1)
+                    if not ev.startswith(b"data: "):
+                        continue
+                    payload = ev[6:]
+                    if payload == b"[DONE]":
+                        r["ok"] = True
+                        continue
+                    j = json.loads(payload)
+                    ch = (j.get("choices") or [{}])
+                    d = ch[0].get("delta") or {} if ch else {}
+                    if d.get("content") and r["t_first"] is None:
+                        r["t_first"] = time.monotonic()
+                    u = j.get("usage")
+                    if u:
+                        r["tokens"] = u.get("completion_tokens", r["tokens"])
+    except (asyncio.CancelledError, Exception) as ex:  # noqa: BLE001 - record and move on
+        r["error"] = type(ex).__name__
+    r["t_end"] = time.monotonic()
+    rec.append(r)
+
+
+async def user(session, url, mk_body, rec, stop: asyncio.Event):
+    while not stop.is_set():
+        await one(session, url, mk_body(), rec, stop)
+
+
+async def run(a):
+    import aiohttp
+    rng = random.Random(a.seed)
+    url = a.url.rstrip("/") + "/v1/chat/completions"
+
+    def mk_body():
+        n_words = max(1, a.prompt_chars // 6)
+        content = " ".join(rng.choice(WORDS) for _ in range(n_words))[: a.prompt_chars]
+        return {"model": a.model, "stream": True, "max_tokens": a.gen_len, "temperature": a.temperature,
+                "ignore_eos": True, "messages": [{"role": "user", "content": content}]}
+    rec: list = []
+    stop = asyncio.Event()
+    loop = asyncio.get_running_loop()
+    for s in (signal.SIGTERM, signal.SIGINT):
+        loop.add_signal_handler(s, stop.set)
+    conn = aiohttp.TCPConnector(limit=0, force_close=False)
+    timeout = aiohttp.ClientTimeout(total=None, sock_read=600)
+    async with aiohttp.ClientSession(connector=conn, timeout=timeout) as session:
+        tasks = [asyncio.ensure_future(user(session, url, mk_body, rec, stop)) for _ in range(a.concurrency)]
+        if a.duration:
+            try:
+                await asyncio.wait_for(stop.wait(), a.duration)
+            except asyncio.TimeoutError:
+                stop.set()
+        else:
+            await stop.wait()
+        for t in tasks:
+            t.cancel()
+        await asyncio.gather(*tasks, return_exceptions=True)
+    with open(a.out, "w") as f:
+        json.dump(rec, f)
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--url", required=True)
+    ap.add_argument("--model", required=True)
+    ap.add_argument("--concurrency", type=int, default=64)
+    ap.add_argument("--prompt-chars", type=int, default=220)
+    ap.add_argument("--gen-len", type=int, default=256)
+    ap.add_argument("--temperature", type=float, default=0.0)
+    ap.add_argument("--duration", type=float, default=0.0)
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--out", required=True)
+    a = ap.parse_args(argv)
+    asyncio.run(run(a))
+
+
+if __name__ == "__main__":
+    main()

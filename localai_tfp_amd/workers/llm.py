@@ -117,9 +117,18 @@ class LLMServicer(BackendServicer):
         self.state = pb.STATE_UNINITIALIZED
 
     # ---------------------------------------------------------------- load
+    def attach(self, engine: LLMEngine, tok):
+        """Serve an engine built in-process (bench / embedding the worker in another program);
+        subsequent LoadModel calls are acknowledged without reloading."""
+        self.engine, self.tok = engine, tok
+        self.preloaded = True
+        self.state = pb.STATE_READY
+
     def LoadModel(self, request, context):
         import torch
         from ..models.loader import load_llm
+        if getattr(self, "preloaded", False):
+            return pb.Result(message="preloaded", success=True)
         try:
             t0 = time.perf_counter()
             opts = parse_options(request.Options)
@@ -154,6 +163,8 @@ class LLMServicer(BackendServicer):
             if self.device == "cpu":
                 ec.num_blocks = ec.num_blocks or 512
             self.engine = LLMEngine(model, tok, ec)
+            if not opts.get("lazy_graphs"):
+                self.engine.precapture_graphs()
             self.engine.start()
             self.tok = tok
             self.model_opts = request
@@ -226,35 +237,59 @@ class LLMServicer(BackendServicer):
                         timing_prompt_processing=o.t_prompt_ms, timing_token_generation=o.t_gen_ms)
 
     # ---------------------------------------------------------------- RPCs
-    def Predict(self, request, context):
-        self._need_engine(context)
-        req = self._request(request)
-        h = self.engine.submit(req)
-        context.add_callback(lambda: self.engine.abort(req.rid) if not h.done else None)
-        parts = []
-        last = None
-        for o in h:
-            parts.append(o.text)
-            last = o
-        h.done = True
-        if last.finish_reason and last.finish_reason.startswith("error"):
-            context.abort(grpc.StatusCode.INTERNAL, last.finish_reason)
-        return self._reply(last, "".join(parts))
+    def _submit_async(self, req):
+        """Submit with an asyncio sink: the engine thread hands outputs to this loop directly."""
+        import asyncio
+        loop = asyncio.get_running_loop()
+        q: asyncio.Queue = asyncio.Queue()
+        h = self.engine.submit(req, sink=lambda o: loop.call_soon_threadsafe(q.put_nowait, o))
+        return h, q
 
-    def PredictStream(self, request, context):
-        self._need_engine(context)
+    async def Predict(self, request, context):
+        if self.engine is None:
+            await context.abort(grpc.StatusCode.FAILED_PRECONDITION, "model not loaded")
         req = self._request(request)
-        h = self.engine.submit(req)
-        context.add_callback(lambda: self.engine.abort(req.rid) if not h.done else None)
-        for o in h:
-            if o.finished:
-                h.done = True
-                if o.finish_reason and o.finish_reason.startswith("error"):
-                    context.abort(grpc.StatusCode.INTERNAL, o.finish_reason)
-                yield self._reply(o, o.text)
-                return
-            if o.text:
-                yield pb.Reply(message=o.text.encode("utf-8"), tokens=0, prompt_tokens=0)
+        h, q = self._submit_async(req)
+        parts = []
+        try:
+            while True:
+                o = await q.get()
+                parts.append(o.text)
+                if o.finished:
+                    h.done = True
+                    break
+        finally:
+            if not h.done:
+                self.engine.abort(req.rid)
+        if o.finish_reason and o.finish_reason.startswith("error"):
+            await context.abort(grpc.StatusCode.INTERNAL, o.finish_reason)
+        return self._reply(o, "".join(parts))
+
+    async def PredictStream(self, request, context):
+        """One Reply per engine output; when the client lags, queued outputs are coalesced into a
+        single Reply (fewer messages under load, same byte stream)."""
+        if self.engine is None:
+            await context.abort(grpc.StatusCode.FAILED_PRECONDITION, "model not loaded")
+        req = self._request(request)
+        h, q = self._submit_async(req)
+        try:
+            while True:
+                o = await q.get()
+                text = o.text
+                while not o.finished and not q.empty():
+                    o = q.get_nowait()
+                    text += o.text
+                if o.finished:
+                    h.done = True
+                    if o.finish_reason and o.finish_reason.startswith("error"):
+                        await context.abort(grpc.StatusCode.INTERNAL, o.finish_reason)
+                    yield self._reply(o, text)
+                    return
+                if text:
+                    yield pb.Reply(message=text.encode("utf-8"))
+        finally:
+            if not h.done:  # client went away: free the sequence's KV blocks now
+                self.engine.abort(req.rid)
 
     def Embedding(self, request, context):
         self._need_engine(context)

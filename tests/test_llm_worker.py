@@ -7,23 +7,22 @@ import pytest
 
 from localai_tfp_amd.grpc import pb
 from localai_tfp_amd.grpc.client import BackendClient
-from localai_tfp_amd.grpc.server import make_server
+from localai_tfp_amd.grpc.server import AioServer
 from localai_tfp_amd.workers.llm import LLMServicer
 
 
 @pytest.fixture(scope="module")
 def client():
     svc = LLMServicer(device="cpu")
-    server, port = make_server(svc, "127.0.0.1:0", max_workers=8)
-    server.start()
-    c = BackendClient(f"127.0.0.1:{port}")
+    server = AioServer(svc, "127.0.0.1:0", max_workers=8)
+    c = BackendClient(f"127.0.0.1:{server.port}")
     assert c.health()
     r = c.load_model(pb.ModelOptions(Model="synthetic:tiny", ContextSize=512, Embeddings=True))
     assert r.success, r.message
     yield c
     c.close()
     svc.engine.shutdown()
-    server.stop(0)
+    server.stop()
 
 
 def opts(**kw):
