@@ -201,6 +201,7 @@ def run_http(args, eng, tok, cfg, dev, dist):
     from localai_tfp_amd.grpc.server import AioServer
     from localai_tfp_amd.workers.llm import LLMServicer
 
+    sys.setswitchinterval(0.0005)  # same as workers/llm.py main(): engine thread + gRPC loop share the GIL
     svc = LLMServicer(device=str(dev))
     svc.attach(eng, tok)
     win = Window(eng, args.warmup, args.steps, dev, dist)

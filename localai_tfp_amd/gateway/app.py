@@ -37,16 +37,80 @@ def _error(status: int, msg: str, typ: str = "invalid_request_error") -> JSONRes
     return JSONResponse({"error": {"code": status, "message": msg, "type": typ}}, status_code=status)
 
 
+class GatewayMiddleware:
+    """Pure-ASGI middleware (auth + latency metrics + machine tag). Starlette's BaseHTTPMiddleware
+    pushes every streamed body chunk through an anyio memory stream, which dominated the gateway's
+    CPU profile under SSE load; this one only wraps `send` when it has to."""
+
+    def __init__(self, app, state, exempt, health_paths):
+        self.app, self.state, self.exempt, self.health = app, state, exempt, health_paths
+        c = state.cfg
+        self.cfg = c
+        self.metrics = API_LATENCY if (not c.disable_metrics_endpoint and API_LATENCY is not None) else None
+        self.tag = c.machine_tag.encode() if c.machine_tag else None
+
+    def _authorized(self, scope) -> bool:
+        keys = self.state.all_api_keys
+        path = scope["path"]
+        if not keys or path in self.health:
+            return True
+        c = self.cfg
+        if scope["method"] == "GET" and (c.disable_api_key_requirement_for_http_get or
+                                         any(r.match(path) for r in self.exempt)):
+            return True
+        hdr = {k: v for k, v in scope["headers"] if k in (b"authorization", b"x-api-key", b"xi-api-key")}
+        auth = hdr.get(b"authorization", b"").decode("latin-1")
+        if auth.lower().startswith("bearer "):
+            tok = auth[7:]
+        else:
+            tok = (hdr.get(b"x-api-key") or hdr.get(b"xi-api-key") or b"").decode("latin-1")
+        if c.use_subtle_key_comparison:
+            return any(hmac.compare_digest(tok.encode(), k.encode()) for k in keys)
+        return tok in keys
+
+    async def __call__(self, scope, receive, send):
+        if scope["type"] != "http":
+            return await self.app(scope, receive, send)
+        if not self._authorized(scope):
+            resp = PlainTextResponse("", status_code=401) if self.cfg.opaque_errors else \
+                _error(401, "An authentication key is required", "invalid_request_error")
+            return await resp(scope, receive, send)
+        if self.tag is not None:
+            inner_send = send
+
+            async def send(msg, _s=inner_send):
+                if msg["type"] == "http.response.start":
+                    msg = dict(msg)
+                    msg["headers"] = list(msg.get("headers", [])) + [(b"machine-tag", self.tag)]
+                await _s(msg)
+        if self.metrics is None or scope["path"] == "/metrics":
+            return await self.app(scope, receive, send)
+        t0 = time.perf_counter()
+        try:
+            await self.app(scope, receive, send)
+        finally:
+            self.metrics.labels(scope["method"], scope["path"]).observe(time.perf_counter() - t0)
+
+
 def create_app(cfg: ApplicationConfig | None = None, inproc: bool | None = None, startup: bool = True) -> FastAPI:
     state = Application(cfg, inproc)
     c = state.cfg
     @contextlib.asynccontextmanager
     async def lifespan(_app):
+        import os
+        prof = None
+        if os.environ.get("LOCALAI_CPROFILE"):  # diagnostics: profile the serving process
+            import cProfile
+            prof = cProfile.Profile()
+            prof.enable()
         if startup:
             import asyncio
             await asyncio.get_running_loop().run_in_executor(None, state.startup)
         yield
         state.shutdown()
+        if prof is not None:
+            prof.disable()
+            prof.dump_stats(os.environ["LOCALAI_CPROFILE"])
 
     app = FastAPI(title="LocalAI (MI355X-native)", version=c.version, docs_url="/swagger/index.html",
                   openapi_url="/swagger/doc.json", lifespan=lifespan)
@@ -70,42 +134,7 @@ def create_app(cfg: ApplicationConfig | None = None, inproc: bool | None = None,
     exempt = [re.compile(p) for p in c.http_get_exempted_endpoints]
     health_paths = {"/healthz", "/readyz"}
 
-    @app.middleware("http")
-    async def auth_mw(request: Request, call_next):
-        keys = state.all_api_keys
-        path = request.url.path
-        if keys and path not in health_paths:
-            if not (request.method == "GET" and (c.disable_api_key_requirement_for_http_get or
-                                                 any(r.match(path) for r in exempt))):
-                auth = request.headers.get("authorization", "")
-                tok = auth[7:] if auth.lower().startswith("bearer ") else (
-                    request.headers.get("x-api-key") or request.headers.get("xi-api-key") or "")
-                if c.use_subtle_key_comparison:
-                    ok = any(hmac.compare_digest(tok.encode(), k.encode()) for k in keys)
-                else:
-                    ok = tok in keys
-                if not ok:
-                    if c.opaque_errors:
-                        return PlainTextResponse("", status_code=401)
-                    return _error(401, "An authentication key is required", "invalid_request_error")
-        return await call_next(request)
-
-    if not c.disable_metrics_endpoint and API_LATENCY is not None:
-        @app.middleware("http")
-        async def metrics_mw(request: Request, call_next):
-            t0 = time.perf_counter()
-            resp = await call_next(request)
-            path = request.url.path
-            if path != "/metrics":
-                API_LATENCY.labels(request.method, path).observe(time.perf_counter() - t0)
-            return resp
-
-    if c.machine_tag:
-        @app.middleware("http")
-        async def tag_mw(request: Request, call_next):
-            resp = await call_next(request)
-            resp.headers["Machine-Tag"] = c.machine_tag
-            return resp
+    app.add_middleware(GatewayMiddleware, state=state, exempt=exempt, health_paths=health_paths)
 
     if c.cors:
         from fastapi.middleware.cors import CORSMiddleware

@@ -142,6 +142,29 @@ class Inference:
         text = r.message.decode("utf-8", errors="replace")
         return LLMResponse(prefix + text if prefix else text, usage)
 
+    async def predict_stream(self, cfg, prompt: str, messages=None, images=(), videos=(), audios=(),
+                             correlation_id: str = ""):
+        """Async generator of (text, usage) pieces straight off the gRPC stream (no queue hop);
+        `usage` is the same mutable TokenUsage updated as counts arrive."""
+        m = await self.model(cfg)
+        opts = self._predict_opts(cfg, prompt, messages, images, videos, audios)
+        opts.CorrelationId = correlation_id
+        usage = TokenUsage()
+        if cfg.template.reply_prefix:
+            yield cfg.template.reply_prefix, usage
+        dec = codecs.getincrementaldecoder("utf-8")(errors="replace")
+        async for r in m.apick().stream("PredictStream", opts):
+            if r.tokens or r.prompt_tokens:
+                usage.prompt, usage.completion = r.prompt_tokens, r.tokens
+                usage.timing_prompt_processing = r.timing_prompt_processing
+                usage.timing_token_generation = r.timing_token_generation
+            text = dec.decode(r.message) if r.message else ""
+            if text:
+                yield text, usage
+        tail = dec.decode(b"", final=True)
+        if tail:
+            yield tail, usage
+
     async def embeddings(self, cfg, text: str | None = None, tokens: list | None = None) -> list[float]:
         m = await self.model(cfg)
         o = predict_options(cfg, self.app.cfg.models_path)

@@ -14,7 +14,7 @@ import time
 import uuid
 
 from fastapi import APIRouter, Request
-from fastapi.responses import JSONResponse, StreamingResponse
+from fastapi.responses import JSONResponse, Response
 
 from .. import functions as F
 from ..config.model_config import FLAG_CHAT, FLAG_COMPLETION, FLAG_EDIT, FLAG_EMBEDDINGS
@@ -153,11 +153,10 @@ async def chat(request: Request):
     if req.stream:
         include_usage = bool(req.stream_options.get("include_usage"))
         if not should_use_fn:
-            return StreamingResponse(_chat_stream(a, req, cfg, prompt, base, extra_usage, include_usage),
-                                     media_type="text/event-stream",
-                                     headers={**SSE_HEADERS, "X-Correlation-ID": cid})
-        return StreamingResponse(_chat_stream_tools(a, req, cfg, prompt, base, no_action, extra_usage),
-                                 media_type="text/event-stream", headers={**SSE_HEADERS, "X-Correlation-ID": cid})
+            return SSEResponse(_chat_stream(a, req, cfg, prompt, base, extra_usage, include_usage),
+                               {"X-Correlation-ID": cid})
+        return SSEResponse(_chat_stream_tools(a, req, cfg, prompt, base, no_action, extra_usage),
+                           {"X-Correlation-ID": cid})
 
     text_to_return = [""]
 
@@ -196,48 +195,90 @@ async def chat(request: Request):
                          "usage": usage.openai(extra_usage)}, headers={"X-Correlation-ID": cid})
 
 
-async def _chat_stream(a, req, cfg, prompt, base, extra_usage, include_usage):
-    import asyncio
-    q: asyncio.Queue = asyncio.Queue()
-    usage_box = [TokenUsage()]
+class SSEResponse(Response):
+    """Raw ASGI text/event-stream response: one `send` per chunk, client disconnect cancels the
+    producer (frees the backend sequence through the gRPC cancel). Starlette's StreamingResponse
+    adds an anyio task group + checkpoints per chunk, which showed up in the gateway profile."""
 
-    async def on_token(s, usage):
-        usage_box[0] = usage
-        await q.put(s)
+    def __init__(self, gen, headers: dict | None = None):  # noqa: super().__init__ deliberately skipped
+        self.gen = gen
+        self.background = None
+        self.status_code = 200
+        self.raw_headers = [(b"content-type", b"text/event-stream"), (b"cache-control", b"no-cache"),
+                        (b"connection", b"keep-alive"), (b"x-accel-buffering", b"no")]
+        for k, v in (headers or {}).items():
+            if k.lower() not in ("cache-control", "connection", "x-accel-buffering"):
+                self.raw_headers.append((k.lower().encode(), str(v).encode()))
 
-    async def run():
+    async def __call__(self, scope, receive, send):
+        import asyncio
+        me = asyncio.current_task()
+        gone = [False]
+
+        async def watch():
+            while True:
+                msg = await receive()
+                if msg["type"] == "http.disconnect":
+                    gone[0] = True
+                    me.cancel()
+                    return
+        watcher = asyncio.ensure_future(watch())
         try:
-            await compute_choices(a, req, prompt, cfg, lambda s, c: None, on_token)
-        except Exception as ex:  # surface as an error chunk
-            await q.put(ex)
+            await send({"type": "http.response.start", "status": 200, "headers": self.raw_headers})
+            async for chunk in self.gen:
+                await send({"type": "http.response.body", "body": chunk, "more_body": True})
+            await send({"type": "http.response.body", "body": b"", "more_body": False})
+        except asyncio.CancelledError:
+            if not gone[0]:
+                raise
         finally:
-            await q.put(None)
+            watcher.cancel()
+            await self.gen.aclose()
 
+
+class _ChunkFmt:
+    """Pre-serialised chat.completion.chunk envelope: per token only the content string (and the
+    usage object when it changes) is JSON-encoded."""
+
+    def __init__(self, base: dict, obj: str, extra_usage: bool):
+        head = _dumps({**base, "object": obj})[:-1]
+        self.pre = ("data: " + head + ',"choices":[{"index":0,"finish_reason":null,"delta":{"content":').encode()
+        self.extra = extra_usage
+        self._u = None
+        self._ub = b""
+
+    def usage(self, u: TokenUsage) -> bytes:
+        key = (u.prompt, u.completion, u.timing_prompt_processing, u.timing_token_generation)
+        if key != self._u:
+            self._u = key
+            self._ub = _dumps(u.openai(self.extra)).encode()
+        return self._ub
+
+    def content(self, text: str, u: TokenUsage) -> bytes:
+        return self.pre + _dumps(text).encode() + b'}}],"usage":' + self.usage(u) + b"}\n\n"
+
+
+async def _chat_stream(a, req, cfg, prompt, base, extra_usage, include_usage):
+    fmt = _ChunkFmt(base, "chat.completion.chunk", extra_usage)
+    usage = TokenUsage()
     yield sse({**base, "object": "chat.completion.chunk",
                "choices": [{"index": 0, "finish_reason": None, "delta": {"role": "assistant", "content": ""}}]})
-    task = asyncio.ensure_future(run())
+    imgs, vids, auds = _media(req)
     try:
-        while True:
-            item = await q.get()
-            if item is None:
-                break
-            if isinstance(item, Exception):
-                yield sse({"error": {"message": str(item), "type": "server_error"}})
-                break
-            yield sse({**base, "object": "chat.completion.chunk",
-                       "choices": [{"index": 0, "finish_reason": None, "delta": {"content": item}}],
-                       "usage": usage_box[0].openai(extra_usage)})
-        final = {**base, "object": "chat.completion.chunk",
-                 "choices": [{"index": 0, "finish_reason": "stop", "delta": {"content": ""}}],
-                 "usage": usage_box[0].openai(extra_usage)}
-        yield sse(final)
-        if include_usage:
-            yield sse({**base, "object": "chat.completion.chunk", "choices": [],
-                       "usage": usage_box[0].openai(extra_usage)})
-        yield SSE_DONE
-    finally:
-        if not task.done():
-            task.cancel()
+        for _ in range(req.n or 1):
+            async for text, u in a.inference.predict_stream(cfg, prompt, req.messages, imgs, vids, auds,
+                                                            req.correlation_id):
+                usage = u
+                yield fmt.content(text, u)
+    except Exception as ex:  # surface as an error event, then terminate the stream cleanly
+        log.error("chat stream failed: %s", ex)
+        yield sse({"error": {"message": str(ex), "type": "server_error"}})
+    yield sse({**base, "object": "chat.completion.chunk",
+               "choices": [{"index": 0, "finish_reason": "stop", "delta": {"content": ""}}],
+               "usage": usage.openai(extra_usage)})
+    if include_usage:
+        yield sse({**base, "object": "chat.completion.chunk", "choices": [], "usage": usage.openai(extra_usage)})
+    yield SSE_DONE
 
 
 async def _chat_stream_tools(a, req, cfg, prompt, base, no_action, extra_usage):
@@ -316,8 +357,7 @@ async def completion(request: Request):
         if len(prompts) > 1:
             raise RequestError("cannot handle more than 1 `PromptStrings` when Streaming")
         prompt = tmpl(prompts[0])
-        return StreamingResponse(_completion_stream(a, req, cfg, prompt, base, extra_usage),
-                                 media_type="text/event-stream", headers={**SSE_HEADERS, "X-Correlation-ID": cid})
+        return SSEResponse(_completion_stream(a, req, cfg, prompt, base, extra_usage), {"X-Correlation-ID": cid})
     all_choices = []
     total = TokenUsage()
     for k, p in enumerate(prompts):
@@ -333,39 +373,20 @@ async def completion(request: Request):
 
 
 async def _completion_stream(a, req, cfg, prompt, base, extra_usage):
-    import asyncio
-    q: asyncio.Queue = asyncio.Queue()
-    ub = [TokenUsage()]
-
-    async def on_token(s, u):
-        ub[0] = u
-        await q.put(s)
-
-    async def run():
-        try:
-            await compute_choices(a, req, prompt, cfg, lambda s, c: None, on_token)
-        except Exception as ex:
-            await q.put(ex)
-        finally:
-            await q.put(None)
-    task = asyncio.ensure_future(run())
+    head = _dumps({**base, "object": "text_completion"})[:-1]
+    pre = ("data: " + head + ',"choices":[{"index":0,"finish_reason":null,"text":').encode()
+    fmt = _ChunkFmt(base, "text_completion", extra_usage)
+    usage = TokenUsage()
     try:
-        while True:
-            item = await q.get()
-            if item is None:
-                break
-            if isinstance(item, Exception):
-                yield sse({"error": {"message": str(item), "type": "server_error"}})
-                break
-            yield sse({**base, "object": "text_completion",
-                       "choices": [{"index": 0, "finish_reason": None, "text": item}],
-                       "usage": ub[0].openai(extra_usage)})
-        yield sse({**base, "object": "text_completion",
-                   "choices": [{"index": 0, "finish_reason": "stop"}], "usage": ub[0].openai(extra_usage)})
-        yield SSE_DONE
-    finally:
-        if not task.done():
-            task.cancel()
+        async for text, u in a.inference.predict_stream(cfg, prompt, req.messages, (), (), (), req.correlation_id):
+            usage = u
+            yield pre + _dumps(text).encode() + b'}],"usage":' + fmt.usage(u) + b"}\n\n"
+    except Exception as ex:
+        log.error("completion stream failed: %s", ex)
+        yield sse({"error": {"message": str(ex), "type": "server_error"}})
+    yield sse({**base, "object": "text_completion", "choices": [{"index": 0, "finish_reason": "stop"}],
+               "usage": usage.openai(extra_usage)})
+    yield SSE_DONE
 
 
 @router.post("/v1/edits")

@@ -20,7 +20,7 @@ WORDS = ["the", "model", "serves", "tokens", "fast", "on", "MI355X", "with", "pa
 
 async def one(session, url, body, rec, stop):
     t0 = time.monotonic()
-    r = {"t_send": t0, "t_first": None, "t_end": None, "tokens": 0, "ok": False}
+    r = {"t_send": t0, "t_first": None, "t_end": None, "tokens": 0, "chunks": 0, "ok": False}
     try:
         async with session.post(url, json=body) as resp:
             buf = b""
@@ -37,8 +37,10 @@ async def one(session, url, body, rec, stop):
                     j = json.loads(payload)
                     ch = (j.get("choices") or [{}])
                     d = ch[0].get("delta") or {} if ch else {}
-                    if d.get("content") and r["t_first"] is None:
-                        r["t_first"] = time.monotonic()
+                    if d.get("content"):
+                        r["chunks"] += 1
+                        if r["t_first"] is None:
+                            r["t_first"] = time.monotonic()
                     u = j.get("usage")
                     if u:
                         r["tokens"] = u.get("completion_tokens", r["tokens"])

@@ -342,6 +342,10 @@ class LLMServicer(BackendServicer):
 
 
 def main(argv=None):
+    import sys
+    # the engine thread and the gRPC event loop share the GIL: hand it over quickly so a decode
+    # step never waits a full default 5 ms switch interval behind stream bookkeeping
+    sys.setswitchinterval(0.0005)
     worker_main(LLMServicer, argv)
 
 
