@@ -70,6 +70,16 @@ class RequestHandle:
                 return
 
 
+class BatchedSink:
+    """Collects the outputs of one engine step for handles submitted with a `batch_key` and hands
+    them over in ONE cross-thread call (e.g. one loop.call_soon_threadsafe per step instead of one
+    per token: 128 self-pipe writes per decode step otherwise)."""
+
+    def __init__(self, deliver):
+        self.deliver = deliver  # deliver(list[(key, StepOutput)]) — called from the engine thread
+        self.buf: list = []
+
+
 class DecodeGraph:
     """Static-input hipGraph of one decode step (forward + greedy argmax) for a batch bucket."""
 
@@ -154,12 +164,16 @@ class LLMEngine:
                           out_tokens=0)
         self.last_metrics = {}
         self.on_step = None  # optional hook called with the step index before each loop step (bench)
+        self.batch_sink: BatchedSink | None = None
         if c.prefill_bf16_cache and self.device.type == "cuda":
             model.enable_prefill_bf16_cache()
 
     # ------------------------------------------------------------------ request API
-    def submit(self, req: Request, sink=None) -> RequestHandle:
+    def submit(self, req: Request, sink=None, batch_key=None) -> RequestHandle:
+        """`sink`: per-output callback; `batch_key` (with `self.batch_sink` set): outputs are
+        gathered per step and delivered together as (batch_key, output) pairs."""
         h = RequestHandle(req.rid, sink)
+        h.batch_key = batch_key
         self.handles[req.rid] = h
         self._inbox.put(("add", req))
         with self._cv:
@@ -220,11 +234,18 @@ class LLMEngine:
         if self._thread:
             self._thread.join(timeout=10)
 
+    def flush_outputs(self):
+        bs = self.batch_sink
+        if bs is not None and bs.buf:
+            items, bs.buf = bs.buf, []
+            bs.deliver(items)
+
     def _loop(self):
         if self.device.type == "cuda":
             torch.cuda.set_device(self.device)
         while not self._stop:
             self._drain_inbox()
+            self.flush_outputs()
             if not self.sched.has_work():
                 with self._cv:
                     self._cv.wait(timeout=0.05)
@@ -238,6 +259,7 @@ class LLMEngine:
                 for s in list(self.sched.running) + list(self.sched.waiting):
                     self.sched.abort(s.rid)
                     self._finish(s, f"error:{type(ex).__name__}: {ex}")
+            self.flush_outputs()
 
     def run_until_done(self, max_steps: int = 1 << 30):
         """Synchronous driver (tests / bench): step until every submitted request finished."""
@@ -432,7 +454,10 @@ class LLMEngine:
                 self.handles.pop(s.rid, None)
                 self.seqs.pop(s.rid, None)
                 if h is not None:
-                    h.put(o)
+                    if h.batch_key is not None and self.batch_sink is not None:
+                        self.batch_sink.buf.append((h.batch_key, o))
+                    else:
+                        h.put(o)
                 continue
             t = int(toks[k])
             lp = lps[k] if lps is not None else None
@@ -474,7 +499,10 @@ class LLMEngine:
             st["gen_tokens_total"] += len(s.output_ids)
             st["cached_tokens_total"] += s.num_cached
         if h is not None:
-            h.put(o)
+            if h.batch_key is not None and self.batch_sink is not None:
+                self.batch_sink.buf.append((h.batch_key, o))
+            else:
+                h.put(o)
 
     def _fill_usage(self, s: Sequence, o: StepOutput, metrics: bool = True):
         o.prompt_tokens = len(s.prompt_ids)

@@ -238,11 +238,21 @@ class LLMServicer(BackendServicer):
 
     # ---------------------------------------------------------------- RPCs
     def _submit_async(self, req):
-        """Submit with an asyncio sink: the engine thread hands outputs to this loop directly."""
+        """Submit with an asyncio queue as the batch key: the engine delivers each step's outputs
+        for all streams in one call_soon_threadsafe (engine.BatchedSink)."""
         import asyncio
+        from ..engine.engine import BatchedSink
         loop = asyncio.get_running_loop()
+        eng = self.engine
+        if eng.batch_sink is None or getattr(eng.batch_sink, "loop", None) is not loop:
+            def dispatch(items):
+                for q, o in items:
+                    q.put_nowait(o)
+            bs = BatchedSink(lambda items: loop.call_soon_threadsafe(dispatch, items))
+            bs.loop = loop
+            eng.batch_sink = bs
         q: asyncio.Queue = asyncio.Queue()
-        h = self.engine.submit(req, sink=lambda o: loop.call_soon_threadsafe(q.put_nowait, o))
+        h = eng.submit(req, batch_key=q)
         return h, q
 
     async def Predict(self, request, context):
