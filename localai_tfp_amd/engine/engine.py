@@ -132,7 +132,8 @@ class DecodeGraph:
 
 
 class LLMEngine:
-    def __init__(self, model: LlamaModel, tokenizer, cfg: EngineConfig | None = None):
+    def __init__(self, model: LlamaModel, tokenizer, cfg: EngineConfig | None = None, tp=None):
+        self.tp = tp  # parallel.tp_engine.TPLink (leader or follower side) when tensor parallel
         self.model = model
         self.tok = tokenizer
         self.cfg = cfg or EngineConfig()
@@ -143,6 +144,8 @@ class LLMEngine:
         self.max_blocks_per_seq = (c.max_model_len + c.block_size - 1) // c.block_size
         nb = c.num_blocks or KVCache.auto_num_blocks(mc.n_layers, model.n_kv, c.block_size, mc.head_dim, self.device,
                                                      c.kv_mem_fraction)
+        if self.tp is not None:  # every rank must hold the same block ids
+            nb = self.tp.allreduce_min(nb)
         self.kv = KVCache(mc.n_layers, nb, model.n_kv, c.block_size, mc.head_dim, self.device)
         self.bm = make_block_manager(nb, c.block_size, c.enable_prefix_cache)
         self.sched = Scheduler(self.bm, c.block_size, c.max_num_seqs, c.max_batched_tokens, c.max_model_len)
@@ -216,6 +219,8 @@ class LLMEngine:
         """Capture every decode bucket up front (vLLM-style) so no capture lands mid-serving."""
         if not self.use_graphs:
             return 0
+        if self.tp is not None and self.tp.is_leader:
+            self.tp.send_plan("capture")  # followers capture the same buckets in the same order
         n = 0
         for b in self.cfg.graph_buckets:
             if b <= self.cfg.max_num_seqs and self._graph_for(b) is not None:
@@ -233,6 +238,9 @@ class LLMEngine:
             self._cv.notify_all()
         if self._thread:
             self._thread.join(timeout=10)
+        if self.tp is not None and self.tp.is_leader and not getattr(self, "_tp_stopped", False):
+            self._tp_stopped = True
+            self.tp.send_plan(None)  # followers leave follow()
 
     def flush_outputs(self):
         bs = self.batch_sink
@@ -310,11 +318,12 @@ class LLMEngine:
             self.graphs[b] = g
         return g
 
-    def _forward_and_sample(self, so: SchedulerOutput):
-        dev = self.device
+    # ------------------------------------------------------------------ step plan / execution
+    def _plan(self, so: SchedulerOutput) -> dict:
+        """Host-side description of one forward step (plain numpy; broadcast verbatim to tensor-
+        parallel followers, which replay it with engine.follow())."""
         bs = self.cfg.block_size
-        dec = so.decode
-        pf = so.prefill
+        dec, pf = so.decode, so.prefill
         nd = len(dec)
         T = so.num_tokens
         tokens = np.empty(T, np.int32)
@@ -337,7 +346,6 @@ class LLMEngine:
             blk = np.asarray(s.blocks, np.int32)
             slots[i:i + it.n] = blk[r // bs] * bs + r % bs
             i += it.n
-        sample_items = [it for it in dec] + [it for it in pf if it.sample]
         # rows whose logits are needed: decode rows + last row of finishing prefills
         lidx = list(range(nd))
         off = nd
@@ -345,40 +353,8 @@ class LLMEngine:
             if it.sample:
                 lidx.append(off + it.n - 1)
             off += it.n
-        params = [it.seq.params for it in sample_items]
-        greedy_only = all(p.greedy and not p.logit_bias and p.repeat_penalty == 1.0 and not p.presence_penalty
-                          and not p.frequency_penalty for p in params) and not any(it.seq.grammar for it in sample_items)
-        # ---- decode-only fast path: graph replay ----
-        if not pf and nd and self.use_graphs:
-            g = self._graph_for(nd)
-            if g is not None:
-                maxb = max(len(it.seq.blocks) for it in dec)
-                bt = np.zeros((nd, maxb), np.int32)
-                lens = np.empty(nd, np.int32)
-                for k, it in enumerate(dec):
-                    bt[k, :len(it.seq.blocks)] = it.seq.blocks
-                    lens[k] = it.seq.num_computed + 1
-                h = torch.from_numpy(np.concatenate([tokens, positions, slots, lens, bt.reshape(-1)])).pin_memory()
-                d = h.to(dev, non_blocking=True)
-                logits, am = g.run(d[:nd], d[nd:2 * nd], d[2 * nd:3 * nd], d[4 * nd:].view(nd, maxb), d[3 * nd:4 * nd], nd)
-                self.stats["graph_steps"] += 1
-                if greedy_only:
-                    return am.cpu().tolist(), None
-                return self._sample(logits, sample_items)
-        # ---- eager path ----
-        fb = self._build_fb(so, tokens, positions, slots, lidx)
-        fb.keep_hidden = any(it.seq.req.embedding for it in sample_items)
-        logits = self.model.forward(fb, self.kv, self.ws)
-        self._hidden = self.model.last_hidden if fb.keep_hidden else None
-        if not sample_items:
-            return [], None
-        return self._sample(logits, sample_items)
-
-    def _build_fb(self, so, tokens, positions, slots, lidx) -> ForwardBatch:
-        dev = self.device
-        dec, pf = so.decode, so.prefill
-        nd = len(dec)
-        arrs = {"tokens": tokens, "positions": positions, "slots": slots, "lidx": np.asarray(lidx, np.int32)}
+        plan = {"nd": nd, "tokens": tokens, "positions": positions, "slots": slots,
+                "lidx": np.asarray(lidx, np.int32), "keep_hidden": False}
         if nd:
             maxb = max(len(it.seq.blocks) for it in dec)
             bt = np.zeros((nd, maxb), np.int32)
@@ -386,8 +362,7 @@ class LLMEngine:
             for k, it in enumerate(dec):
                 bt[k, :len(it.seq.blocks)] = it.seq.blocks
                 lens[k] = it.seq.num_computed + 1
-            arrs["dec_bt"] = bt
-            arrs["dec_lens"] = lens
+            plan["dec_bt"], plan["dec_lens"] = bt, lens
         if pf:
             maxb = max(len(it.seq.blocks) for it in pf)
             bt = np.zeros((len(pf), maxb), np.int32)
@@ -397,19 +372,77 @@ class LLMEngine:
                 bt[k, :len(it.seq.blocks)] = it.seq.blocks
                 cu[k + 1] = cu[k] + it.n
                 ctx[k] = it.start + it.n
-            arrs["pf_bt"] = bt
-            arrs["pf_cu"] = cu
-            arrs["pf_ctx"] = ctx
-        t = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev, non_blocking=True) for k, v in arrs.items()}
+            plan["pf_bt"], plan["pf_cu"], plan["pf_ctx"] = bt, cu, ctx
+            plan["keep_hidden"] = any(it.seq.req.embedding for it in pf if it.sample)
+        plan["graph"] = bool(not pf and nd and self.use_graphs and self._graph_for(nd) is not None)
+        return plan
+
+    def _execute(self, plan: dict):
+        """Run the step's forward on this rank. Returns (logits, argmax-or-None)."""
+        dev = self.device
+        nd = plan["nd"]
+        if plan["graph"]:
+            g = self._graph_for(nd)
+            bt = plan["dec_bt"]
+            maxb = bt.shape[1]
+            h = torch.from_numpy(np.concatenate([plan["tokens"], plan["positions"], plan["slots"], plan["dec_lens"],
+                                                 bt.reshape(-1)])).pin_memory()
+            d = h.to(dev, non_blocking=True)
+            logits, am = g.run(d[:nd], d[nd:2 * nd], d[2 * nd:3 * nd], d[4 * nd:].view(nd, maxb),
+                               d[3 * nd:4 * nd], nd)
+            self.stats["graph_steps"] += 1
+            return logits, am
+        fb = self._build_fb(plan)
+        logits = self.model.forward(fb, self.kv, self.ws)
+        self._hidden = self.model.last_hidden if fb.keep_hidden else None
+        return logits, None
+
+    def _forward_and_sample(self, so: SchedulerOutput):
+        plan = self._plan(so)
+        if self.tp is not None:
+            self.tp.send_plan(plan)
+        logits, am = self._execute(plan)
+        sample_items = [it for it in so.decode] + [it for it in so.prefill if it.sample]
+        if not sample_items:
+            return [], None
+        params = [it.seq.params for it in sample_items]
+        greedy_only = all(p.greedy and not p.logit_bias and p.repeat_penalty == 1.0 and not p.presence_penalty
+                          and not p.frequency_penalty for p in params) and not any(it.seq.grammar for it in sample_items)
+        if am is not None and greedy_only:
+            return am.cpu().tolist(), None
+        return self._sample(logits, sample_items)
+
+    def _build_fb(self, plan: dict) -> ForwardBatch:
+        dev = self.device
+        nd = plan["nd"]
+        keys = ["tokens", "positions", "slots", "lidx", "dec_bt", "dec_lens", "pf_bt", "pf_cu", "pf_ctx"]
+        t = {k: torch.from_numpy(np.ascontiguousarray(plan[k])).to(dev, non_blocking=True) for k in keys if k in plan}
         fb = ForwardBatch(t["tokens"], t["positions"], t["slots"], t["lidx"], n_decode=nd)
         if nd:
             fb.dec_block_tables, fb.dec_seq_lens = t["dec_bt"], t["dec_lens"]
-            fb.dec_max_len = int(arrs["dec_lens"].max())
-        if pf:
+            fb.dec_max_len = int(plan["dec_lens"].max())
+        if "pf_cu" in plan:
             fb.pf_block_tables, fb.pf_cu_q, fb.pf_ctx_lens = t["pf_bt"], t["pf_cu"], t["pf_ctx"]
-            fb.pf_q_lens_host = [it.n for it in pf]
-            fb.pf_ctx_lens_host = [it.start + it.n for it in pf]
+            cu = plan["pf_cu"]
+            fb.pf_q_lens_host = [int(cu[k + 1] - cu[k]) for k in range(len(cu) - 1)]
+            fb.pf_ctx_lens_host = [int(x) for x in plan["pf_ctx"]]
+        fb.keep_hidden = bool(plan.get("keep_hidden"))
         return fb
+
+    # ------------------------------------------------------------------ tensor-parallel follower
+    def follow(self):
+        """Follower-rank loop: replay the leader's step plans (forward only; the leader samples).
+        Returns when the leader sends a stop message."""
+        if self.device.type == "cuda":
+            torch.cuda.set_device(self.device)
+        while True:
+            msg = self.tp.recv_plan()
+            if msg is None:
+                return
+            if msg == "capture":
+                self.precapture_graphs()
+                continue
+            self._execute(msg)
 
     def _sample(self, logits, items):
         params = [it.seq.params for it in items]

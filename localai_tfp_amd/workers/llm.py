@@ -102,8 +102,9 @@ class LazyGrammar:
 
 
 class LLMServicer(BackendServicer):
-    def __init__(self, device: str | None = None):
+    def __init__(self, device: str | None = None, tp=None):
         super().__init__()
+        self.tp = tp  # parallel.tp_engine.TPLink on the leader rank of a tensor-parallel worker
         self.engine: LLMEngine | None = None
         self.tok = None
         self.model_opts = None
@@ -145,7 +146,6 @@ class LLMServicer(BackendServicer):
                 log.warning("LoRA adapters are not supported by this worker yet; ignoring")
             ov = {"rope_freq_base": request.RopeFreqBase, "rope_freq_scale": request.RopeFreqScale,
                   "rope_scaling": request.RopeScaling, "rms_norm_eps": request.RMSNormEps}
-            model, tok, mcfg, _ = load_llm(path, self.device, overrides=ov)
             ec = EngineConfig()
             if request.ContextSize > 0:
                 ec.max_model_len = int(request.ContextSize)
@@ -162,7 +162,16 @@ class LLMServicer(BackendServicer):
                 ec.use_graphs = False
             if self.device == "cpu":
                 ec.num_blocks = ec.num_blocks or 512
-            self.engine = LLMEngine(model, tok, ec)
+            if self.engine is not None:  # reload: stop the old engine (and the followers' replay)
+                self.engine.shutdown()
+                self.engine = None
+            if self.tp is not None:
+                import dataclasses
+                self.tp.send_control("load", (path, ov, dataclasses.asdict(ec)))
+                model, tok, mcfg, _ = load_llm(path, self.device, self.tp.rank, self.tp.world, None, ov)
+            else:
+                model, tok, mcfg, _ = load_llm(path, self.device, overrides=ov)
+            self.engine = LLMEngine(model, tok, ec, tp=self.tp)
             if not opts.get("lazy_graphs"):
                 self.engine.precapture_graphs()
             self.engine.start()
@@ -356,6 +365,16 @@ def main(argv=None):
     # the engine thread and the gRPC event loop share the GIL: hand it over quickly so a decode
     # step never waits a full default 5 ms switch interval behind stream bookkeeping
     sys.setswitchinterval(0.0005)
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        # tensor-parallel worker under torch.distributed.run: rank 0 serves gRPC, others follow
+        from ..parallel.tp_engine import follower_main, init_from_env
+        link, dev = init_from_env()
+        if link.rank != 0:
+            follower_main(link, dev)
+            return
+        worker_main(lambda: LLMServicer(device=str(dev), tp=link), argv)
+        link.send_control("stop")
+        return
     worker_main(LLMServicer, argv)
 
 
