@@ -161,6 +161,8 @@ def main():
                          else "engine in-process (gateway/gRPC excluded)"),
                 "load_s": round(t_load, 1), "graph_capture_s": round(t_capture, 1), "graphs": n_graphs,
                 "graph_steps": st["graph_steps"], "total_steps": st["steps"],
+                "host_ms_per_step": {k[:-2]: round(st[k] / max(1, st["steps"]) * 1e3, 3)
+                                     for k in ("sched_s", "plan_s", "fwd_s", "wait_s", "process_s")},
                 "weights_gb": round(model.weight_bytes() / 1e9, 2), "kv_blocks": eng.kv.num_blocks, **extra,
             },
         }

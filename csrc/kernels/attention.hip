@@ -17,7 +17,7 @@
 #define LOG2E 1.4426950408889634f
 
 // ------------------------------------------------------------------------------------------------
-template <int D, int G>
+template <int D, int G, bool F16>
 __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restrict__ q, int q_stride,
                                                           const bf16_t* __restrict__ kc,
                                                           const bf16_t* __restrict__ vc,
@@ -161,7 +161,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restri
         }
         const int hq = kvh * G + h;
         if (n_parts == 1) {
-            out[(size_t)b * out_stride + (size_t)hq * D + d] = f32_to_bf16(ls > 0.f ? os / ls : 0.f);
+            out[(size_t)b * out_stride + (size_t)hq * D + d] = f32_to_act<F16>(ls > 0.f ? os / ls : 0.f);
         } else {
             const size_t pi = ((size_t)b * Hq + hq) * n_parts + part;
             if (d == 0) part_ml[pi] = make_float2(mx, ls);
@@ -170,6 +170,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restri
     }
 }
 
+template <bool F16>
 __global__ __launch_bounds__(128) void attn_decode_reduce_kernel(const float2* __restrict__ part_ml,
                                                                   const float* __restrict__ part_o, int n_parts,
                                                                   int Hq, int D, const int* __restrict__ seq_lens,
@@ -188,7 +189,7 @@ __global__ __launch_bounds__(128) void attn_decode_reduce_kernel(const float2* _
             ls += ml.y * a;
             os += part_o[((size_t)bh * n_parts + p) * D + d] * a;
         }
-        out[(size_t)b * out_stride + (size_t)h * D + d] = f32_to_bf16(ls > 0.f ? os / ls : 0.f);
+        out[(size_t)b * out_stride + (size_t)h * D + d] = f32_to_act<F16>(ls > 0.f ? os / ls : 0.f);
     }
 }
 
@@ -198,11 +199,13 @@ static int launch_decode(const bf16_t* q, int q_stride, const bf16_t* kc, const 
                          int n_parts, bf16_t* out, int out_stride, float2* part_ml, float* part_o,
                          hipStream_t st) {
     dim3 grid(Hkv, B, n_parts);
-    attn_decode_kernel<D, G><<<grid, 256, 0, st>>>(q, q_stride, kc, vc, bt, bt_stride, seq_lens, Hkv, bs, scale,
-                                                   part_size, n_parts, out, out_stride, part_ml, part_o);
-    if (n_parts > 1)
-        attn_decode_reduce_kernel<<<B * Hkv * G, 128, 0, st>>>(part_ml, part_o, n_parts, Hkv * G, D, seq_lens,
-                                                               part_size, out, out_stride);
+    MX_ACT_DISPATCH({
+        attn_decode_kernel<D, G, F16><<<grid, 256, 0, st>>>(q, q_stride, kc, vc, bt, bt_stride, seq_lens, Hkv, bs,
+                                                            scale, part_size, n_parts, out, out_stride, part_ml, part_o);
+        if (n_parts > 1)
+            attn_decode_reduce_kernel<F16><<<B * Hkv * G, 128, 0, st>>>(part_ml, part_o, n_parts, Hkv * G, D, seq_lens,
+                                                                        part_size, out, out_stride);
+    });
     MXK_CHECK_LAUNCH();
 }
 
@@ -242,7 +245,7 @@ MX_DEV int v_lds_off(int p, int nt) {
     return p * (D * 2) + ((nt ^ sv) << 5);
 }
 
-template <int D, int GW, int VT>
+template <int D, int GW, int VT, bool F16>
 __global__ __launch_bounds__(512) void attn_prefill_kernel(const bf16_t* __restrict__ q,
                                                            const bf16_t* __restrict__ kc,
                                                            const bf16_t* __restrict__ vc,
@@ -413,7 +416,7 @@ __global__ __launch_bounds__(512) void attn_prefill_kernel(const bf16_t* __restr
         const float inv = lrow[i] > 0.f ? 1.f / lrow[i] : 0.f;
 #pragma unroll
         for (int nt = 0; nt < D / 16; ++nt)
-            out[((size_t)(qbeg + qi) * Hq + hq) * D + 16 * nt + col] = f32_to_bf16(oacc[nt][i] * inv);
+            out[((size_t)(qbeg + qi) * Hq + hq) * D + 16 * nt + col] = f32_to_act<F16>(oacc[nt][i] * inv);
     }
 }
 
@@ -424,15 +427,17 @@ static int launch_prefill(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, c
                           hipStream_t st) {
     constexpr int NW = GW >= 3 ? GW : 4;
     dim3 grid(n_tiles, Hq / GW);
-    if (vmode == 0) {
-        const size_t lds = 2 * 64 * D * 2 + NW * 16 * (64 + 8) * 2;
-        attn_prefill_kernel<D, GW, 0><<<grid, NW * 64, lds, st>>>(q, kc, vc, bt, bt_stride, tile_seq, tile_q0, cu_q,
-                                                                   ctx_lens, Hq, Hkv, Hq / Hkv, bs, scale, out);
-    } else {
-        const size_t lds = 64 * D * 2 + D * (64 + 8) * 2 + NW * 16 * (64 + 8) * 2;
-        attn_prefill_kernel<D, GW, 1><<<grid, NW * 64, lds, st>>>(q, kc, vc, bt, bt_stride, tile_seq, tile_q0, cu_q,
-                                                                   ctx_lens, Hq, Hkv, Hq / Hkv, bs, scale, out);
-    }
+    MX_ACT_DISPATCH({
+        if (vmode == 0) {
+            const size_t lds = 2 * 64 * D * 2 + NW * 16 * (64 + 8) * 2;
+            attn_prefill_kernel<D, GW, 0, F16><<<grid, NW * 64, lds, st>>>(
+                q, kc, vc, bt, bt_stride, tile_seq, tile_q0, cu_q, ctx_lens, Hq, Hkv, Hq / Hkv, bs, scale, out);
+        } else {
+            const size_t lds = 64 * D * 2 + D * (64 + 8) * 2 + NW * 16 * (64 + 8) * 2;
+            attn_prefill_kernel<D, GW, 1, F16><<<grid, NW * 64, lds, st>>>(
+                q, kc, vc, bt, bt_stride, tile_seq, tile_q0, cu_q, ctx_lens, Hq, Hkv, Hq / Hkv, bs, scale, out);
+        }
+    });
     MXK_CHECK_LAUNCH();
 }
 

@@ -3,8 +3,17 @@
 // casts and embedding-row gathers for dense (f32/f16/bf16) tables. All loads are 16-byte vectors.
 #include "mx_common.h"
 
+// library-wide 16-bit activation format (see mx_common.h): 0 bf16, 1 f16
+int g_mx_act_f16 = 0;
+extern "C" int mxk_set_act_f16(int on) {
+    const int prev = g_mx_act_f16;
+    g_mx_act_f16 = on ? 1 : 0;
+    return prev;
+}
+extern "C" int mxk_get_act_f16() { return g_mx_act_f16; }
+
 // y[m, f] = act(g[m, f]) * u[m, f]; g/u bf16 with row stride ld_in, out bf16
-template <int ACT>
+template <int ACT, bool F16>
 __global__ __launch_bounds__(256) void glu_kernel(const bf16_t* __restrict__ g, const bf16_t* __restrict__ u,
                                                   int ld_in, bf16_t* __restrict__ y, int ld_out, int F) {
     const int m = blockIdx.y;
@@ -16,13 +25,14 @@ __global__ __launch_bounds__(256) void glu_kernel(const bf16_t* __restrict__ g, 
     uint32_t o[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-        float g0 = __uint_as_float(gw[j] << 16), g1 = __uint_as_float(gw[j] & 0xFFFF0000u);
-        float u0 = __uint_as_float(uw[j] << 16), u1 = __uint_as_float(uw[j] & 0xFFFF0000u);
+        float g0, g1, u0, u1;
+        unpack_act2<F16>(gw[j], g0, g1);
+        unpack_act2<F16>(uw[j], u0, u1);
         float a0, a1;
         if (ACT == 0) { a0 = silu_f(g0); a1 = silu_f(g1); }
         else if (ACT == 1) { a0 = gelu_tanh_f(g0); a1 = gelu_tanh_f(g1); }
         else { a0 = gelu_erf_f(g0); a1 = gelu_erf_f(g1); }
-        o[j] = pack_bf16x2(a0 * u0, a1 * u1);
+        o[j] = pack_act2<F16>(a0 * u0, a1 * u1);
     }
     *(uint4*)(y + (size_t)m * ld_out + f) = make_uint4(o[0], o[1], o[2], o[3]);
 }
@@ -32,14 +42,17 @@ extern "C" int mxk_glu(int act, const bf16_t* g, const bf16_t* u, int ld_in, bf1
     if (M <= 0) return 0;
     if (F % 8) return (int)hipErrorInvalidValue;
     dim3 grid((F / 8 + 255) / 256, M);
-    if (act == 0) glu_kernel<0><<<grid, 256, 0, st>>>(g, u, ld_in, y, ld_out, F);
-    else if (act == 1) glu_kernel<1><<<grid, 256, 0, st>>>(g, u, ld_in, y, ld_out, F);
-    else glu_kernel<2><<<grid, 256, 0, st>>>(g, u, ld_in, y, ld_out, F);
+    MX_ACT_DISPATCH({
+        if (act == 0) glu_kernel<0, F16><<<grid, 256, 0, st>>>(g, u, ld_in, y, ld_out, F);
+        else if (act == 1) glu_kernel<1, F16><<<grid, 256, 0, st>>>(g, u, ld_in, y, ld_out, F);
+        else glu_kernel<2, F16><<<grid, 256, 0, st>>>(g, u, ld_in, y, ld_out, F);
+    });
     MXK_CHECK_LAUNCH();
 }
 
 // SwiGLU over a gate|up product whose columns are interleaved in 16-column groups (the layout of
 // the fused gate_up weight): y[m, 32*(f/16) + f%16] = gate, y[m, 32*(f/16) + 16 + f%16] = up.
+template <bool F16>
 __global__ __launch_bounds__(256) void swiglu_il16_kernel(const bf16_t* __restrict__ y, int ldy,
                                                           bf16_t* __restrict__ out, int ldo, int F) {
     const int m = blockIdx.y;
@@ -53,9 +66,10 @@ __global__ __launch_bounds__(256) void swiglu_il16_kernel(const bf16_t* __restri
     uint32_t o[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-        const float g0 = __uint_as_float(gw[j] << 16), g1 = __uint_as_float(gw[j] & 0xFFFF0000u);
-        const float u0 = __uint_as_float(uw[j] << 16), u1 = __uint_as_float(uw[j] & 0xFFFF0000u);
-        o[j] = pack_bf16x2(silu_f(g0) * u0, silu_f(g1) * u1);
+        float g0, g1, u0, u1;
+        unpack_act2<F16>(gw[j], g0, g1);
+        unpack_act2<F16>(uw[j], u0, u1);
+        o[j] = pack_act2<F16>(silu_f(g0) * u0, silu_f(g1) * u1);
     }
     *(uint4*)(out + (size_t)m * ldo + f) = make_uint4(o[0], o[1], o[2], o[3]);
 }
@@ -64,7 +78,7 @@ extern "C" int mxk_swiglu_il16(const bf16_t* y, int ldy, bf16_t* out, int ldo, i
     if (M <= 0) return 0;
     if (F % 16) return (int)hipErrorInvalidValue;
     dim3 grid((F / 8 + 255) / 256, M);
-    swiglu_il16_kernel<<<grid, 256, 0, st>>>(y, ldy, out, ldo, F);
+    MX_ACT_DISPATCH(swiglu_il16_kernel<F16><<<grid, 256, 0, st>>>(y, ldy, out, ldo, F));
     MXK_CHECK_LAUNCH();
 }
 
@@ -87,15 +101,16 @@ extern "C" int mxk_act_f32(float* x, size_t n, int act, hipStream_t st) {
     MXK_CHECK_LAUNCH();
 }
 
-// fp32 -> bf16 cast of a [rows, cols] view with strides
+// fp32 -> act16 (bf16 or f16, library mode) cast of a [rows, cols] view with strides
+template <bool F16>
 __global__ __launch_bounds__(256) void cast_f32_bf16_kernel(const float* __restrict__ x, int ldx,
                                                             bf16_t* __restrict__ y, int ldy, int cols) {
     const int r = blockIdx.y;
     for (int c = (blockIdx.x * 256 + threadIdx.x) * 4; c < cols; c += gridDim.x * 256 * 4) {
         const float4 v = *(const float4*)(x + (size_t)r * ldx + c);
         uint2 p;
-        p.x = pack_bf16x2(v.x, v.y);
-        p.y = pack_bf16x2(v.z, v.w);
+        p.x = pack_act2<F16>(v.x, v.y);
+        p.y = pack_act2<F16>(v.z, v.w);
         *(uint2*)(y + (size_t)r * ldy + c) = p;
     }
 }
@@ -104,7 +119,7 @@ extern "C" int mxk_cast_f32_bf16(const float* x, int ldx, bf16_t* y, int ldy, in
     if (rows <= 0) return 0;
     if (cols % 4) return (int)hipErrorInvalidValue;
     dim3 grid(min(64, (cols / 4 + 255) / 256), rows);
-    cast_f32_bf16_kernel<<<grid, 256, 0, st>>>(x, ldx, y, ldy, cols);
+    MX_ACT_DISPATCH(cast_f32_bf16_kernel<F16><<<grid, 256, 0, st>>>(x, ldx, y, ldy, cols));
     MXK_CHECK_LAUNCH();
 }
 

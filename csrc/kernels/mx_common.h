@@ -38,6 +38,58 @@ MX_DEV uint32_t pack_bf16x2(float lo, float hi) {
 
 MX_DEV float half_to_f32(uint16_t h) { return (float)__builtin_bit_cast(_Float16, h); }
 
+// ---- 16-bit activation format -------------------------------------------------------------------
+// GEMM operands produced by norms / attention / SwiGLU are either bf16 or f16 ("act16"). f16 lets
+// the quantised-weight GEMM dequantise with packed f16 math (2 values per VALU op, see qgemm16.hip)
+// and keeps 3 more mantissa bits than bf16 (llama.cpp's GPU GEMMs also run dequantised weights in
+// f16). The format is a library-wide mode (mxk_set_act_f16); kernels are templated on it.
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+extern int g_mx_act_f16;  // host-side mode, read by launchers (defined in elementwise.hip)
+
+template <bool F16>
+MX_DEV uint16_t f32_to_act(float f) {
+    if constexpr (F16) return __builtin_bit_cast(uint16_t, (_Float16)f);
+    else return f32_to_bf16(f);
+}
+template <bool F16>
+MX_DEV float act_to_f32(uint16_t v) {
+    if constexpr (F16) return half_to_f32(v);
+    else return bf16_to_f32(v);
+}
+template <bool F16>
+MX_DEV uint32_t pack_act2(float lo, float hi) {
+    if constexpr (F16) {
+        f16x2 v = {(_Float16)lo, (_Float16)hi};
+        return __builtin_bit_cast(uint32_t, v);
+    } else {
+        return pack_bf16x2(lo, hi);
+    }
+}
+// unpack 2 activations from one dword
+template <bool F16>
+MX_DEV void unpack_act2(uint32_t w, float& lo, float& hi) {
+    if constexpr (F16) {
+        f16x2 v = __builtin_bit_cast(f16x2, w);
+        lo = (float)v[0];
+        hi = (float)v[1];
+    } else {
+        lo = __uint_as_float(w << 16);
+        hi = __uint_as_float(w & 0xFFFF0000u);
+    }
+}
+// dispatch helper: MX_ACT_DISPATCH(expr) instantiates `expr` with a constexpr bool F16.
+#define MX_ACT_DISPATCH(...)                     \
+    do {                                         \
+        if (g_mx_act_f16) {                      \
+            constexpr bool F16 = true;           \
+            __VA_ARGS__;                         \
+        } else {                                 \
+            constexpr bool F16 = false;          \
+            __VA_ARGS__;                         \
+        }                                        \
+    } while (0)
+
 MX_DEV float wave_sum(float v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -9,7 +9,7 @@
 // One 256-thread workgroup per row; float4 loads; the sum of squares never leaves registers/LDS.
 #include "mx_common.h"
 
-template <bool WANT_BF16, bool WANT_Q8, bool HAS_RES>
+template <bool WANT_BF16, bool WANT_Q8, bool HAS_RES, bool F16>
 __global__ __launch_bounds__(256) void rmsnorm_kernel(const float* __restrict__ x, int ldx,
                                                       const bf16_t* __restrict__ res, int ldr,
                                                       float* __restrict__ xout, const float* __restrict__ w,
@@ -48,8 +48,8 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(const float* __restrict__ 
             float a0 = v[i].x * rs * g.x, a1 = v[i].y * rs * g.y, a2 = v[i].z * rs * g.z, a3 = v[i].w * rs * g.w;
             if (WANT_BF16) {
                 uint2 p;
-                p.x = pack_bf16x2(a0, a1);
-                p.y = pack_bf16x2(a2, a3);
+                p.x = pack_act2<F16>(a0, a1);
+                p.y = pack_act2<F16>(a2, a3);
                 *(uint2*)(ob + (size_t)row * ldo + c) = p;
             }
             if (WANT_Q8) {
@@ -71,7 +71,7 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(const float* __restrict__ 
 }
 
 // generic (any H multiple of 32) slow path: one thread per element pair, used for odd model sizes.
-template <bool WANT_BF16, bool WANT_Q8>
+template <bool WANT_BF16, bool WANT_Q8, bool F16>
 __global__ __launch_bounds__(256) void rmsnorm_generic_kernel(const float* __restrict__ x, int ldx,
                                                               const float* __restrict__ w, bf16_t* __restrict__ ob,
                                                               int ldo, int8_t* __restrict__ oq,
@@ -87,7 +87,7 @@ __global__ __launch_bounds__(256) void rmsnorm_generic_kernel(const float* __res
     for (int b = threadIdx.x / 32; b < (H + 31) / 32; b += 8) {
         const int c = b * 32 + (threadIdx.x & 31);
         float a = c < H ? xr[c] * rs * w[c] : 0.f;
-        if (WANT_BF16 && c < H) ob[(size_t)row * ldo + c] = f32_to_bf16(a);
+        if (WANT_BF16 && c < H) ob[(size_t)row * ldo + c] = f32_to_act<F16>(a);
         if (WANT_Q8) {
             float am = group_max<32>(fabsf(a));
             float d = am / 127.f;
@@ -107,22 +107,29 @@ extern "C" int mxk_rmsnorm(const float* x, int ldx, const bf16_t* res, int ldr, 
     const bool wb = ob != nullptr, wq = oq != nullptr, hr = res != nullptr;
     if (H % 1024 == 0 && H <= 8192) {
 #define RMS_L(B, Q, R) \
-    rmsnorm_kernel<B, Q, R><<<rows, 256, 0, st>>>(x, ldx, res, ldr, xout, w, ob, ldo, oq, ods, H, eps)
-        if (hr) {
-            if (wb && wq) RMS_L(true, true, true);
-            else if (wb) RMS_L(true, false, true);
-            else RMS_L(false, true, true);
-        } else {
-            if (wb && wq) RMS_L(true, true, false);
-            else if (wb) RMS_L(true, false, false);
-            else RMS_L(false, true, false);
-        }
+    rmsnorm_kernel<B, Q, R, F16><<<rows, 256, 0, st>>>(x, ldx, res, ldr, xout, w, ob, ldo, oq, ods, H, eps)
+        MX_ACT_DISPATCH({
+            if (hr) {
+                if (wb && wq) RMS_L(true, true, true);
+                else if (wb) RMS_L(true, false, true);
+                else RMS_L(false, true, true);
+            } else {
+                if (wb && wq) RMS_L(true, true, false);
+                else if (wb) RMS_L(true, false, false);
+                else RMS_L(false, true, false);
+            }
+        });
 #undef RMS_L
     } else {
         if (hr) return (int)hipErrorInvalidValue;  // residual fusion only on the fast path
-        if (wb && wq) rmsnorm_generic_kernel<true, true><<<rows, 256, 0, st>>>(x, ldx, w, ob, ldo, oq, ods, H, eps);
-        else if (wb) rmsnorm_generic_kernel<true, false><<<rows, 256, 0, st>>>(x, ldx, w, ob, ldo, oq, ods, H, eps);
-        else rmsnorm_generic_kernel<false, true><<<rows, 256, 0, st>>>(x, ldx, w, ob, ldo, oq, ods, H, eps);
+        MX_ACT_DISPATCH({
+            if (wb && wq)
+                rmsnorm_generic_kernel<true, true, F16><<<rows, 256, 0, st>>>(x, ldx, w, ob, ldo, oq, ods, H, eps);
+            else if (wb)
+                rmsnorm_generic_kernel<true, false, F16><<<rows, 256, 0, st>>>(x, ldx, w, ob, ldo, oq, ods, H, eps);
+            else
+                rmsnorm_generic_kernel<false, true, F16><<<rows, 256, 0, st>>>(x, ldx, w, ob, ldo, oq, ods, H, eps);
+        });
     }
     MXK_CHECK_LAUNCH();
 }
@@ -130,6 +137,7 @@ extern "C" int mxk_rmsnorm(const float* x, int ldx, const bf16_t* res, int ldr, 
 // ---------------------------------------------------------------------------------------------
 // quantise bf16 rows to q8 blocks (for the GEMV path after attention / SwiGLU). One wave per
 // 64 x 32-element block group: lane l handles 8 elements; 4 lanes per block.
+template <bool F16>
 __global__ __launch_bounds__(256) void quant_q8_kernel(const bf16_t* __restrict__ x, int ldx, int8_t* __restrict__ oq,
                                                        float2* __restrict__ ods, int K) {
     const int row = blockIdx.y;
@@ -137,10 +145,10 @@ __global__ __launch_bounds__(256) void quant_q8_kernel(const bf16_t* __restrict_
     if (e0 >= K) return;  // K multiple of 32 -> whole 4-lane groups exit together
     uint4 raw = *(const uint4*)(x + (size_t)row * ldx + e0);
     float a[8];
-    a[0] = __uint_as_float(raw.x << 16); a[1] = __uint_as_float(raw.x & 0xFFFF0000u);
-    a[2] = __uint_as_float(raw.y << 16); a[3] = __uint_as_float(raw.y & 0xFFFF0000u);
-    a[4] = __uint_as_float(raw.z << 16); a[5] = __uint_as_float(raw.z & 0xFFFF0000u);
-    a[6] = __uint_as_float(raw.w << 16); a[7] = __uint_as_float(raw.w & 0xFFFF0000u);
+    unpack_act2<F16>(raw.x, a[0], a[1]);
+    unpack_act2<F16>(raw.y, a[2], a[3]);
+    unpack_act2<F16>(raw.z, a[4], a[5]);
+    unpack_act2<F16>(raw.w, a[6], a[7]);
     float am = 0.f;
 #pragma unroll
     for (int i = 0; i < 8; ++i) am = fmaxf(am, fabsf(a[i]));
@@ -161,13 +169,14 @@ extern "C" int mxk_quant_q8(const bf16_t* x, int ldx, int8_t* oq, float2* ods, i
     if (rows <= 0) return 0;
     if (K % 32) return (int)hipErrorInvalidValue;
     dim3 grid((K / 8 + 255) / 256, rows);
-    quant_q8_kernel<<<grid, 256, 0, st>>>(x, ldx, oq, ods, K);
+    MX_ACT_DISPATCH(quant_q8_kernel<F16><<<grid, 256, 0, st>>>(x, ldx, oq, ods, K));
     MXK_CHECK_LAUNCH();
 }
 
 // ---------------------------------------------------------------------------------------------
 // LayerNorm (BERT / Whisper / CLIP): bf16 or fp32 in, bf16 out, fp32 gamma/beta. Optional fused
 // residual add (x + r) written back to `xsum` (fp32) when non-null.
+template <bool F16>
 __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict__ x, int ldx,
                                                         const float* __restrict__ r, int ldr,
                                                         float* __restrict__ xsum, const float* __restrict__ g,
@@ -192,7 +201,7 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
         if (r) v += r[(size_t)row * ldr + c];
         if (xsum) xsum[(size_t)row * ldx + c] = v;
         float y = (v - mean) * rs * (g ? g[c] : 1.f) + (b ? b[c] : 0.f);
-        if (ob) ob[(size_t)row * ldo + c] = f32_to_bf16(y);
+        if (ob) ob[(size_t)row * ldo + c] = f32_to_act<F16>(y);
         if (of) of[(size_t)row * ldo + c] = y;
     }
 }
@@ -201,7 +210,7 @@ extern "C" int mxk_layernorm(const float* x, int ldx, const float* r, int ldr, f
                              const float* b, bf16_t* ob, float* of, int ldo, int rows, int H, float eps,
                              hipStream_t st) {
     if (rows <= 0) return 0;
-    layernorm_kernel<<<rows, 256, 0, st>>>(x, ldx, r, ldr, xsum, g, b, ob, of, ldo, H, eps);
+    MX_ACT_DISPATCH(layernorm_kernel<F16><<<rows, 256, 0, st>>>(x, ldx, r, ldr, xsum, g, b, ob, of, ldo, H, eps));
     MXK_CHECK_LAUNCH();
 }
 

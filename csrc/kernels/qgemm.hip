@@ -367,7 +367,7 @@ struct Dot<MXQ_Q8_0> {
     }
 };
 
-template <int QT, int MM, int EPI>
+template <int QT, int MM, int EPI, bool F16>
 __global__ __launch_bounds__(256) void qgemv_dot4_kernel(const int8_t* __restrict__ xq,
                                                          const float2* __restrict__ xds,
                                                          const uint8_t* __restrict__ W,
@@ -412,13 +412,13 @@ __global__ __launch_bounds__(256) void qgemv_dot4_kernel(const int8_t* __restric
         const float a1 = wave_sum(acc1[m]);
         if (lane == 0) {
             if constexpr (EPI == EPI_SWIGLU) {
-                ((bf16_t*)Cv)[(size_t)m * ldc + slot] = f32_to_bf16(silu_f(a0) * a1);
+                ((bf16_t*)Cv)[(size_t)m * ldc + slot] = f32_to_act<F16>(silu_f(a0) * a1);
             } else if constexpr (EPI == EPI_F32) {
                 ((float*)Cv)[(size_t)m * ldc + r0] = a0;
                 if (v1) ((float*)Cv)[(size_t)m * ldc + r1] = a1;
             } else if constexpr (EPI == EPI_BF16) {
-                ((bf16_t*)Cv)[(size_t)m * ldc + r0] = f32_to_bf16(a0);
-                if (v1) ((bf16_t*)Cv)[(size_t)m * ldc + r1] = f32_to_bf16(a1);
+                ((bf16_t*)Cv)[(size_t)m * ldc + r0] = f32_to_act<F16>(a0);
+                if (v1) ((bf16_t*)Cv)[(size_t)m * ldc + r1] = f32_to_act<F16>(a1);
             } else {
                 ((float*)Cv)[(size_t)m * ldc + r0] += a0;
                 if (v1) ((float*)Cv)[(size_t)m * ldc + r1] += a1;
@@ -430,7 +430,7 @@ __global__ __launch_bounds__(256) void qgemv_dot4_kernel(const int8_t* __restric
 // ---------------------------------------------------------------------------------------------
 // dequantise whole rows to bf16 (embedding lookup K9, and the optional bf16 weight cache used by
 // large-M prefill through hipBLASLt). rows[i] selects the source row (nullptr -> identity).
-template <int QT>
+template <int QT, bool F16>
 __global__ __launch_bounds__(256) void dequant_rows_kernel(const uint8_t* __restrict__ W,
                                                            const uint16_t* __restrict__ WD,
                                                            const int* __restrict__ rows, int K,
@@ -464,8 +464,8 @@ __global__ __launch_bounds__(256) void dequant_rows_kernel(const uint8_t* __rest
     const int jo = (c & 1) * 4;
     if (ob) {
         uint2 p;
-        p.x = pack_bf16x2(v[jo], v[jo + 1]);
-        p.y = pack_bf16x2(v[jo + 2], v[jo + 3]);
+        p.x = pack_act2<F16>(v[jo], v[jo + 1]);
+        p.y = pack_act2<F16>(v[jo + 2], v[jo + 3]);
         *(uint2*)(ob + (size_t)orow * ldo + e0) = p;
     }
     if (of) *(float4*)(of + (size_t)orow * ldo + e0) = make_float4(v[jo], v[jo + 1], v[jo + 2], v[jo + 3]);
@@ -525,7 +525,7 @@ static int launch_gemv(const int8_t* xq, const float2* xds, const uint8_t* W, co
                        int K, void* C, int ldc, hipStream_t st) {
     const int slots = EPI == EPI_SWIGLU ? N / 2 : (N + 1) / 2;
     dim3 grid((slots + 3) / 4);
-    qgemv_dot4_kernel<QT, MM, EPI><<<grid, 256, 0, st>>>(xq, xds, W, WD, M, N, K, C, ldc);
+    MX_ACT_DISPATCH(qgemv_dot4_kernel<QT, MM, EPI, F16><<<grid, 256, 0, st>>>(xq, xds, W, WD, M, N, K, C, ldc));
     MXK_CHECK_LAUNCH();
 }
 
@@ -560,11 +560,15 @@ extern "C" int mxk_dequant_rows(int qtype, const uint8_t* W, const uint16_t* WD,
     if (nrows <= 0) return 0;
     if (K % 256) return (int)hipErrorInvalidValue;
     dim3 grid((K / 256 + 3) / 4, nrows);
-    switch (qtype) {
-        case MXQ_Q4_K: dequant_rows_kernel<MXQ_Q4_K><<<grid, 256, 0, st>>>(W, WD, rows, K, ob, of, ldo); break;
-        case MXQ_Q6_K: dequant_rows_kernel<MXQ_Q6_K><<<grid, 256, 0, st>>>(W, WD, rows, K, ob, of, ldo); break;
-        case MXQ_Q8_0: dequant_rows_kernel<MXQ_Q8_0><<<grid, 256, 0, st>>>(W, WD, rows, K, ob, of, ldo); break;
-        default: return (int)hipErrorInvalidValue;
-    }
+    int rc = 0;
+    MX_ACT_DISPATCH({
+        switch (qtype) {
+            case MXQ_Q4_K: dequant_rows_kernel<MXQ_Q4_K, F16><<<grid, 256, 0, st>>>(W, WD, rows, K, ob, of, ldo); break;
+            case MXQ_Q6_K: dequant_rows_kernel<MXQ_Q6_K, F16><<<grid, 256, 0, st>>>(W, WD, rows, K, ob, of, ldo); break;
+            case MXQ_Q8_0: dequant_rows_kernel<MXQ_Q8_0, F16><<<grid, 256, 0, st>>>(W, WD, rows, K, ob, of, ldo); break;
+            default: rc = (int)hipErrorInvalidValue;
+        }
+    });
+    if (rc) return rc;
     MXK_CHECK_LAUNCH();
 }

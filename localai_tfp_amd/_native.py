@@ -30,6 +30,9 @@ KERNEL_SIGS = {
     "mxk_layernorm": [P, I, P, I, P, P, P, P, P, I, I, I, F, P],
     "mxk_groupnorm_nhwc": [P, P, P, P, I, I, I, I, F, I, P],
     "mxk_qgemm_mfma": [I, I, I, I, P, I, P, P, I, I, I, I, P, I, P],
+    "mxk_qgemm16": [I, I, I, I, P, I, P, P, I, I, I, I, P, I, P],
+    "mxk_set_act_f16": [I],
+    "mxk_get_act_f16": [],
     "mxk_qgemv": [I, I, P, P, P, P, I, I, I, P, I, P],
     "mxk_dequant_rows": [I, P, P, P, I, I, P, P, I, P],
     "mxk_rope_kv": [P, P, P, P, P, F, I, I, I, I, I, I, P, P, P, I, P],
@@ -105,6 +108,21 @@ def have_kernels() -> bool:
         return True
     except Exception:
         return False
+
+
+_act_f16_mode = None
+
+
+def ensure_act(dtype) -> None:
+    """Put the kernel library's 16-bit activation format (bf16 | f16) in line with a tensor dtype
+    before a launch that reads or writes 16-bit activations (mxk_set_act_f16; kernels are templated
+    on it). Cached on the Python side, so steady-state calls cost one comparison."""
+    global _act_f16_mode
+    import torch
+    want = dtype == torch.float16
+    if want != _act_f16_mode:
+        kernels().mxk_set_act_f16(int(want))
+        _act_f16_mode = want
 
 
 def kcall(name: str, *args):

@@ -164,7 +164,7 @@ class LLMEngine:
         self.eos_ids = set(getattr(tokenizer, "eos_token_ids", []) or [])
         self.stats = dict(steps=0, decode_tokens=0, prefill_tokens=0, graph_steps=0, preemptions=0,
                           busy_s=0.0, prompt_tokens_total=0, gen_tokens_total=0, cached_tokens_total=0,
-                          out_tokens=0)
+                          out_tokens=0, sched_s=0.0, plan_s=0.0, fwd_s=0.0, wait_s=0.0, process_s=0.0)
         self.last_metrics = {}
         self.on_step = None  # optional hook called with the step index before each loop step (bench)
         self.batch_sink: BatchedSink | None = None
@@ -290,11 +290,17 @@ class LLMEngine:
                 self.stats["preemptions"] += 1
         if so.empty:
             return
+        t1 = time.perf_counter()
         toks, lps = self._forward_and_sample(so)
+        t2 = time.perf_counter()
         self.sched.commit(so)
         self._process(so, toks, lps)
-        dt = time.perf_counter() - t0
+        t3 = time.perf_counter()
+        dt = t3 - t0
         st = self.stats
+        st["sched_s"] += t1 - t0
+        st["fwd_s"] += t2 - t1
+        st["process_s"] += t3 - t2
         st["steps"] += 1
         st["decode_tokens"] += len(so.decode)
         st["prefill_tokens"] += sum(p.n for p in so.prefill)
@@ -398,7 +404,9 @@ class LLMEngine:
         return logits, None
 
     def _forward_and_sample(self, so: SchedulerOutput):
+        t0 = time.perf_counter()
         plan = self._plan(so)
+        self.stats["plan_s"] += time.perf_counter() - t0
         if self.tp is not None:
             self.tp.send_plan(plan)
         logits, am = self._execute(plan)
@@ -409,7 +417,10 @@ class LLMEngine:
         greedy_only = all(p.greedy and not p.logit_bias and p.repeat_penalty == 1.0 and not p.presence_penalty
                           and not p.frequency_penalty for p in params) and not any(it.seq.grammar for it in sample_items)
         if am is not None and greedy_only:
-            return am.cpu().tolist(), None
+            t0 = time.perf_counter()
+            out = am.cpu().tolist()
+            self.stats["wait_s"] += time.perf_counter() - t0
+            return out, None
         return self._sample(logits, sample_items)
 
     def _build_fb(self, plan: dict) -> ForwardBatch:

@@ -27,7 +27,7 @@ import torch
 
 from ..formats.gguf import QType
 from ..ops import core as K
-from ..ops.linear import (EPI_ADD_F32, EPI_BF16, EPI_F32, EPI_SWIGLU, QWeight, concat_rows, interleave_gate_up,
+from ..ops.linear import (ACT_DTYPE, EPI_ADD_F32, EPI_BF16, EPI_F32, EPI_SWIGLU, QWeight, concat_rows, interleave_gate_up,
                           qmatmul)
 from .config import LlamaConfig
 
@@ -83,15 +83,16 @@ class Workspace:
         T = max_tokens
         self.max_tokens, self.max_seqs = T, max_seqs
         self.h = torch.empty((T, H), dtype=torch.float32, device=dev)
-        self.xb = torch.empty((T, max(H, F, qd)), dtype=torch.bfloat16, device=dev)
+        act = ACT_DTYPE  # 16-bit GEMM operands (f16 by default, ops/linear.py)
+        self.xb = torch.empty((T, max(H, F, qd)), dtype=act, device=dev)
         kmax = max(H, F, qd)
         self.xq = torch.empty((T * kmax,), dtype=torch.int8, device=dev)
         self.xds = torch.empty((T * kmax // 32 * 2,), dtype=torch.float32, device=dev)
         self.qkv = torch.empty((T, qd + 2 * kvd), dtype=torch.float32, device=dev)
         self.q = torch.empty((T, qd), dtype=torch.bfloat16, device=dev)
-        self.attn = torch.empty((T, qd), dtype=torch.bfloat16, device=dev)
-        self.act = torch.empty((T, F), dtype=torch.bfloat16, device=dev)
-        self.act2 = torch.empty((T, F), dtype=torch.bfloat16, device=dev) if dev.type == "cpu" else None
+        self.attn = torch.empty((T, qd), dtype=act, device=dev)
+        self.act = torch.empty((T, F), dtype=act, device=dev)
+        self.act2 = torch.empty((T, F), dtype=act, device=dev) if dev.type == "cpu" else None
         self.hs = torch.empty((max_seqs, H), dtype=torch.float32, device=dev)
         self.logits = torch.empty((max_seqs, cfg.vocab), dtype=torch.float32, device=dev)
         nh = cfg.n_heads // tp_size
@@ -208,10 +209,13 @@ class LlamaModel:
         return n
 
     def enable_prefill_bf16_cache(self):
+        """Dense 16-bit copies of the projections (+ LM head) for the hipBLASLt large-M path."""
         for L in self.layers:
             for w in (*L.qkv_parts, L.wo, L.wgu, L.wg, L.wu, L.wd):
                 if w is not None:
                     w.build_bf16_cache()
+        if isinstance(self.lm_head, QWeight) and self.lm_head.is_quant:
+            self.lm_head.build_bf16_cache()
 
     # ------------------------------------------------------------------ forward
     def embed(self, tokens: torch.Tensor, out: torch.Tensor):
@@ -301,8 +305,8 @@ class LlamaModel:
                 else:
                     qmatmul(L.wgu, xb, EPI_SWIGLU, act)
             else:
-                g_out = torch.empty((T, F), dtype=torch.bfloat16, device=h.device)
-                u_out = torch.empty((T, F), dtype=torch.bfloat16, device=h.device)
+                g_out = torch.empty((T, F), dtype=ACT_DTYPE, device=h.device)
+                u_out = torch.empty((T, F), dtype=ACT_DTYPE, device=h.device)
                 xin = xb if not gemv else None
                 qmatmul(L.wg, xin, EPI_BF16, g_out, xq=xq, xds=xds)
                 qmatmul(L.wu, xin, EPI_BF16, u_out, xq=xq, xds=xds)

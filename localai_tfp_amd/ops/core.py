@@ -33,6 +33,8 @@ def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, *, out_bf16: torch.Ten
             _quant_q8_ref(y, *out_q8)
         return
     xq, xds = out_q8 if out_q8 is not None else (None, None)
+    if out_bf16 is not None:
+        N.ensure_act(out_bf16.dtype)
     N.kcall("mxk_rmsnorm", x.data_ptr(), x.stride(0), N.ptr(residual_bf16),
             residual_bf16.stride(0) if residual_bf16 is not None else 0,
             x.data_ptr() if residual_bf16 is not None else None, w.data_ptr(), N.ptr(out_bf16),
@@ -58,6 +60,7 @@ def quant_q8(x: torch.Tensor, xq: torch.Tensor, xds: torch.Tensor):
         return
     if not x.is_cuda:
         return _quant_q8_ref(x, xq, xds)
+    N.ensure_act(x.dtype)
     N.kcall("mxk_quant_q8", x.data_ptr(), x.stride(0), xq.data_ptr(), xds.data_ptr(), M, K, N.stream_ptr())
 
 
@@ -73,8 +76,10 @@ def layernorm(x: torch.Tensor, g: torch.Tensor | None, b: torch.Tensor | None, e
             xsum.copy_(v)
         out.copy_(F.layer_norm(v, (H,), g, b, eps))
         return out
-    ob = out if out.dtype == torch.bfloat16 else None
+    ob = out if out.dtype in (torch.bfloat16, torch.float16) else None
     of = out if out.dtype == torch.float32 else None
+    if ob is not None:
+        N.ensure_act(ob.dtype)
     N.kcall("mxk_layernorm", x.data_ptr(), x.stride(0), N.ptr(residual), residual.stride(0) if residual is not None else 0,
             N.ptr(xsum), N.ptr(g), N.ptr(b), N.ptr(ob), N.ptr(of), out.stride(0), M, H, float(eps), N.stream_ptr())
     return out
@@ -239,6 +244,7 @@ def attn_decode(q: torch.Tensor, k_cache, v_cache, block_tables: torch.Tensor, s
             ml_t, po = workspace
     else:
         ml_t = po = None
+    N.ensure_act(out.dtype)
     N.kcall("mxk_attn_decode", q.data_ptr(), q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
             block_tables.data_ptr(), block_tables.stride(0), seq_lens.data_ptr(), B, Hq, Hkv, D, bs, float(scale),
             part_size, n_parts, out.data_ptr(), out.stride(0), N.ptr(ml_t), N.ptr(po), N.stream_ptr())
@@ -281,6 +287,7 @@ def attn_prefill(q: torch.Tensor, k_cache, v_cache, block_tables: torch.Tensor, 
     rows = N.kernels().mxk_attn_prefill_rows(Hq, Hkv)
     seqs, q0s = prefill_tiles(q_lens_host, rows)
     tiles = torch.tensor([seqs, q0s], dtype=torch.int32).to(q.device, non_blocking=True)
+    N.ensure_act(out.dtype)
     N.kcall("mxk_attn_prefill", q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), block_tables.data_ptr(),
             block_tables.stride(0), tiles[0].data_ptr(), tiles[1].data_ptr(), len(seqs), cu_q.data_ptr(),
             ctx_lens.data_ptr(), Hq, Hkv, D, bs, float(scale), out.data_ptr(),
@@ -300,6 +307,7 @@ def glu(gate: torch.Tensor, up: torch.Tensor, out: torch.Tensor, act: str = "sil
         out.copy_(y * up.float())
         return out
     M, Fd = gate.shape
+    N.ensure_act(out.dtype)
     N.kcall("mxk_glu", a, gate.data_ptr(), up.data_ptr(), gate.stride(0), out.data_ptr(), out.stride(0), M, Fd,
             N.stream_ptr())
     return out
@@ -325,10 +333,16 @@ def select_rows(x: torch.Tensor, idx: torch.Tensor, out: torch.Tensor):
     return out
 
 
+def cast_act(x: torch.Tensor, out: torch.Tensor):
+    """fp32 -> 16-bit activation (bf16 or f16, by out.dtype)."""
+    return cast_bf16(x, out)
+
+
 def cast_bf16(x: torch.Tensor, out: torch.Tensor):
     if not x.is_cuda:
         out.copy_(x)
         return out
+    N.ensure_act(out.dtype)
     N.kcall("mxk_cast_f32_bf16", x.data_ptr(), x.stride(0), out.data_ptr(), out.stride(0), x.shape[0], x.shape[1],
             N.stream_ptr())
     return out

@@ -22,9 +22,15 @@ from ..formats.gguf import QType
 from . import quant as Q
 
 EPI_F32, EPI_BF16, EPI_ADD_F32, EPI_SWIGLU = 0, 1, 2, 3
+EPI_ACT = EPI_BF16  # "16-bit activation out" (bf16 or f16 by the output tensor's dtype)
 CU_COUNT = 256
-# prefill rows at or above this go through the dense bf16 weight cache (hipBLASLt) when enabled
-BF16_CACHE_MIN_M = int(__import__("os").environ.get("MX_BF16_CACHE_MIN_M", "128"))
+_os = __import__("os")
+# 16-bit activation format of the model graphs: f16 by default (packed-f16 dequant GEMM, qgemm16.hip);
+# MX_ACT=bf16 selects the bf16 kernels.
+ACT_DTYPE = torch.bfloat16 if _os.environ.get("MX_ACT", "f16").lower() == "bf16" else torch.float16
+# rows at or above this go through the dense 16-bit weight cache (hipBLASLt) when it is enabled;
+# below it the quantised MFMA kernels (decode batches) — tuned with tools/bench_qgemm.py.
+BF16_CACHE_MIN_M = int(_os.environ.get("MX_BF16_CACHE_MIN_M", "0")) or None
 
 
 class QWeight:
@@ -98,17 +104,19 @@ class QWeight:
         assert self.is_quant and self.data.is_cuda
         n = self.N if rows is None else rows.numel()
         out = torch.empty((n, self.K), dtype=dtype, device=self.data.device)
-        ob = out if dtype == torch.bfloat16 else None
+        ob = out if dtype in (torch.bfloat16, torch.float16) else None
         of = out if dtype == torch.float32 else None
+        if ob is not None:
+            N.ensure_act(dtype)
         N.kcall("mxk_dequant_rows", int(self.qtype), self.data.data_ptr(), N.ptr(self.dplane),
                 N.ptr(rows), n, self.K, N.ptr(ob), N.ptr(of), self.K, N.stream_ptr())
         return out
 
-    def build_bf16_cache(self):
-        """Optional dense bf16 copy for large-M prefill through hipBLASLt (288 GB HBM makes the
-        2 B/param copy affordable; opt-in via engine config `prefill_bf16_cache`)."""
+    def build_bf16_cache(self, dtype=None):
+        """Optional dense 16-bit (ACT_DTYPE) copy for large-M prefill through hipBLASLt (288 GB HBM
+        makes the 2 B/param copy affordable; engine config `prefill_bf16_cache`)."""
         if self.is_quant and self.data.is_cuda and self.bf16_cache is None:
-            self.bf16_cache = self.dequant_gpu(torch.bfloat16)
+            self.bf16_cache = self.dequant_gpu(dtype or ACT_DTYPE)
         return self.bf16_cache
 
 
@@ -185,14 +193,17 @@ def qmatmul(W: QWeight, x: torch.Tensor | None, epi: int, out: torch.Tensor, *, 
         y = torch.matmul(x, W.data.t()) if x.dtype == W.data.dtype else torch.matmul(x.to(W.data.dtype), W.data.t())
         return _apply_epi_dense(y, epi, out)
     if M <= 4 and xq is not None:
+        if epi in (EPI_BF16, EPI_SWIGLU):
+            N.ensure_act(out.dtype)
         N.kcall("mxk_qgemv", int(W.qtype), epi, xq.data_ptr(), xds.data_ptr(), W.data.data_ptr(), N.ptr(W.dplane),
                 M, W.N, W.K, out.data_ptr(), out.stride(0), N.stream_ptr())
         return out
     if x is None:
-        raise ValueError("qmatmul: MFMA path needs bf16 activations")
-    if W.bf16_cache is not None and M >= BF16_CACHE_MIN_M:
+        raise ValueError("qmatmul: MFMA path needs 16-bit activations")
+    can_split = epi == EPI_ADD_F32 or (epi == EPI_F32 and out_zeroed)
+    if W.bf16_cache is not None and M >= dense_min_m(x.dtype, epi, can_split) and W.bf16_cache.dtype == x.dtype:
         wt = W.bf16_cache.t()
-        if epi in (EPI_ADD_F32, EPI_F32) and out.is_contiguous() and _fp32_out_ok():
+        if epi in (EPI_ADD_F32, EPI_F32) and out.is_contiguous() and _fp32_out_ok(x.dtype):
             # hipBLASLt bf16 x bf16 -> fp32 with the residual add fused as beta = 1
             if epi == EPI_ADD_F32:
                 torch.addmm(out, x, wt, out_dtype=torch.float32, out=out)
@@ -201,39 +212,77 @@ def qmatmul(W: QWeight, x: torch.Tensor | None, epi: int, out: torch.Tensor, *, 
             return out
         y = torch.matmul(x, wt)
         if epi == EPI_SWIGLU:
+            N.ensure_act(out.dtype)
             N.kcall("mxk_swiglu_il16", y.data_ptr(), y.stride(0), out.data_ptr(), out.stride(0), M, W.N // 2,
                     N.stream_ptr())
             return out
         return _apply_epi_dense(y, epi, out)
     nblk = W.K // 256
-    can_split = epi == EPI_ADD_F32 or (epi == EPI_F32 and out_zeroed)
-    wm, wn, splits = _mfma_shape(M, W.N, nblk, can_split, int(W.qtype))
+    f16 = x.dtype == torch.float16
+    wm, wn, splits = (_mfma16_shape if f16 else _mfma_shape)(M, W.N, nblk, can_split, int(W.qtype))
     e = epi
     if epi == EPI_F32 and splits > 1:
         e = EPI_ADD_F32
-    N.kcall("mxk_qgemm_mfma", int(W.qtype), e, wm, wn, x.data_ptr(), x.stride(0), W.data.data_ptr(),
-            N.ptr(W.dplane), M, W.N, W.K, splits, out.data_ptr(), out.stride(0), N.stream_ptr())
+    if e in (EPI_BF16, EPI_SWIGLU) and out.dtype != x.dtype:
+        raise ValueError(f"qmatmul: {out.dtype} output with {x.dtype} activations")
+    N.kcall("mxk_qgemm16" if f16 else "mxk_qgemm_mfma", int(W.qtype), e, wm, wn, x.data_ptr(), x.stride(0),
+            W.data.data_ptr(), N.ptr(W.dplane), M, W.N, W.K, splits, out.data_ptr(), out.stride(0), N.stream_ptr())
     return out
 
 
-_FP32_OUT = None
+def dense_min_m(dtype, epi: int = EPI_ADD_F32, can_split: bool = True) -> int:
+    """Smallest M routed to the dense weight cache (hipBLASLt). From tools/bench_qgemm.py +
+    tools/tune_qgemm16.py on MI355X (Llama-3-8B shapes): the bf16 dequant-MFMA kernel loses to the
+    dense path from M=128; the packed-f16 kernel with split-K wins for the residual-accumulating /
+    split-able projections up to M=256 (qkv 19.6 vs 20.5 us, o_proj 15.4 vs 19.6, down 42 vs 58.5 at
+    M=128) but loses the SwiGLU gate|up (no split-K) from M~96 and the LM head from M~48."""
+    if BF16_CACHE_MIN_M:
+        return BF16_CACHE_MIN_M
+    if dtype != torch.float16:
+        return 128
+    if epi == EPI_SWIGLU:
+        return 96
+    if not can_split:
+        return 48
+    return 320
 
 
-def _fp32_out_ok() -> bool:
-    """Does this torch build expose mm/addmm with out_dtype=float32 for bf16 inputs (ROCm)?"""
-    global _FP32_OUT
-    if _FP32_OUT is None:
+def _mfma16_shape(M: int, N_: int, nblk: int, can_split: bool, qtype: int):
+    """qgemm16 tile / split-K choice (tools/tune_qgemm16.py): 64-row tiles (WM=4, 2 waves/SIMD);
+    split-able outputs take WN=1 (64 columns per workgroup) and 2-8 K splits — fp32 atomics are
+    cheap at few splits but their count scales with M x N x splits."""
+    wm = 1 if M <= 16 else 2 if M <= 32 else 4
+    if not can_split:
+        return wm, 2, 1
+    wn = 1 if wm == 4 else 2
+    if M <= 64:
+        splits = 8 if nblk >= 32 else 4
+    elif M <= 128:
+        splits = 4 if nblk >= 32 else 2
+    else:
+        splits = 2
+    splits = max(1, min(splits, nblk // 2))
+    return wm, wn, splits
+
+
+_FP32_OUT: dict = {}
+
+
+def _fp32_out_ok(dtype=torch.bfloat16) -> bool:
+    """Does this torch build expose mm/addmm with out_dtype=float32 for 16-bit inputs (ROCm)?"""
+    if dtype not in _FP32_OUT:
         try:
-            a = torch.ones(16, 32, dtype=torch.bfloat16, device="cuda")
-            b = torch.ones(32, 16, dtype=torch.bfloat16, device="cuda")
+            a = torch.ones(16, 32, dtype=dtype, device="cuda")
+            b = torch.ones(32, 16, dtype=dtype, device="cuda")
             o = torch.ones(16, 16, dtype=torch.float32, device="cuda")
             torch.addmm(o, a, b, out_dtype=torch.float32, out=o)
             o2 = torch.empty(16, 16, dtype=torch.float32, device="cuda")
             torch.mm(a, b, out_dtype=torch.float32, out=o2)
-            _FP32_OUT = bool(torch.allclose(o, torch.full_like(o, 33.0))) and bool(torch.allclose(o2, torch.full_like(o2, 32.0)))
+            _FP32_OUT[dtype] = bool(torch.allclose(o, torch.full_like(o, 33.0))) and \
+                bool(torch.allclose(o2, torch.full_like(o2, 32.0)))
         except Exception:
-            _FP32_OUT = False
-    return _FP32_OUT
+            _FP32_OUT[dtype] = False
+    return _FP32_OUT[dtype]
 
 
 def _apply_epi_dense(y: torch.Tensor, epi: int, out: torch.Tensor):

@@ -286,3 +286,91 @@ def test_penalties_and_bias():
     p2 = SamplingParams(temperature=0.0, logit_bias={42: 100.0})
     tok, _ = sb.sample(logits.clone(), [p2], [[]], [0])
     assert int(tok[0]) == 42
+
+
+# ------------------------------------------------------------------------------------------------
+# f16 activation path (qgemm16.hip packed-f16 dequant; f16 outputs of the producers)
+
+@pytest.mark.parametrize("qt", [QType.Q4_K, QType.Q6_K, QType.Q8_0])
+@pytest.mark.parametrize("M", [5, 16, 33, 64, 100, 128, 257])
+def test_qgemm16(qt, M):
+    n, k = 384, 2048
+    raw, dense = make_w(qt, n, k, seed=M + 11)
+    W = QWeight.from_ggml(raw, qt, n, k, DEV)
+    x = torch.randn(M, k, device=DEV).half()
+    ref = x.float().cpu() @ dense.t()
+    out = torch.empty(M, n, device=DEV)
+    qmatmul(W, x, EPI_F32, out)
+    assert rel(out, ref) < 5e-3
+    z = torch.zeros(M, n, device=DEV)
+    qmatmul(W, x, EPI_F32, z, out_zeroed=True)
+    assert rel(z, ref) < 5e-3
+    acc = torch.randn(M, n, device=DEV)
+    acc0 = acc.clone()
+    qmatmul(W, x, EPI_ADD_F32, acc)
+    assert rel(acc - acc0, ref) < 5e-3
+    ob = torch.empty(M, n, dtype=torch.float16, device=DEV)
+    qmatmul(W, x, EPI_BF16, ob)
+    assert rel(ob, ref) < 5e-3
+    sw = torch.empty(M, n // 2, dtype=torch.float16, device=DEV)
+    qmatmul(W, x, EPI_SWIGLU, sw)
+    g = ref.reshape(M, n // 32, 2, 16)
+    ref_sw = torch.nn.functional.silu(g[:, :, 0].reshape(M, -1)) * g[:, :, 1].reshape(M, -1)
+    assert rel(sw, ref_sw) < 1e-2
+
+
+def test_f16_producers():
+    M, H = 7, 4096
+    x = torch.randn(M, H, device=DEV) * 3
+    w = torch.rand(H, device=DEV) + 0.5
+    ref = (x * torch.rsqrt(x.pow(2).mean(-1, keepdim=True) + 1e-5) * w).cpu()
+    for dt in (torch.float16, torch.bfloat16, torch.float16):  # mode switches back and forth
+        ob = torch.empty(M, H, dtype=dt, device=DEV)
+        K.rmsnorm(x.clone(), w, 1e-5, out_bf16=ob)
+        assert rel(ob, ref) < (2e-3 if dt == torch.float16 else 1e-2)
+    # quant_q8 reads f16
+    xh = ref.to(DEV).half()
+    xq = torch.empty(M, H, dtype=torch.int8, device=DEV)
+    xds = torch.empty(M, H // 32, 2, device=DEV)
+    K.quant_q8(xh, xq, xds)
+    deq = xq.float().view(M, H // 32, 32) * xds[..., :1]
+    assert rel(deq.view(M, H), ref) < 1e-2
+    # swiglu / glu / cast in f16
+    g = torch.randn(M, 256, device=DEV).half()
+    u = torch.randn(M, 256, device=DEV).half()
+    o = torch.empty(M, 256, dtype=torch.float16, device=DEV)
+    K.glu(g, u, o)
+    assert rel(o, (torch.nn.functional.silu(g.float()) * u.float()).cpu()) < 5e-3
+    c = torch.empty(M, H, dtype=torch.float16, device=DEV)
+    K.cast_act(x, c)
+    assert rel(c, x.cpu()) < 1e-3
+
+
+def test_dense_cache_f16():
+    qt = QType.Q4_K
+    raw, dense = make_w(qt, 512, 1024, seed=5)
+    W = QWeight.from_ggml(raw, qt, 512, 1024, DEV)
+    W.build_bf16_cache(torch.float16)
+    assert W.bf16_cache.dtype == torch.float16
+    assert rel(W.bf16_cache, dense) < 1e-3
+    x = torch.randn(600, 1024, device=DEV).half()
+    out = torch.zeros(600, 512, device=DEV)
+    qmatmul(W, x, EPI_ADD_F32, out)  # M=600 -> hipBLASLt f16 path
+    assert rel(out, x.float().cpu() @ dense.t()) < 5e-3
+
+
+@pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
+def test_attn_outputs_act16(dt):
+    Hq, Hkv, D, bs, nb = 32, 8, 128, 16, 64
+    kc, vc = _paged_kv(nb, Hkv, bs, D, 3)
+    lens = [40, 300]
+    B = len(lens)
+    maxb = max((l + bs - 1) // bs for l in lens)
+    bt = (torch.randperm(nb - 1)[: B * maxb] + 1).int().view(B, maxb)
+    seq = torch.tensor(lens, dtype=torch.int32)
+    q = torch.randn(B, Hq, D).bfloat16()
+    ref = torch.empty(B, Hq, D)
+    K.attn_decode(q, kc, vc, bt, seq, 0.088, ref)
+    out = torch.empty(B, Hq, D, dtype=dt, device=DEV)
+    K.attn_decode(q.to(DEV), kc.to(DEV), vc.to(DEV), bt.to(DEV), seq.to(DEV), 0.088, out, part_size=128)
+    assert rel(out, ref) < 1e-2
