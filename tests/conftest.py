@@ -23,6 +23,9 @@ def _has_gpu():
 
 def pytest_collection_modifyitems(config, items):
     if _has_gpu():
+        # make sure the in-tree kernels match the sources (hash-checked, a no-op when fresh)
+        from localai_tfp_amd import _build
+        _build.build_all()
         return
     skip = pytest.mark.skip(reason="no GPU in this environment")
     for it in items:
