@@ -72,12 +72,20 @@ class RequestHandle:
 
 class BatchedSink:
     """Collects the outputs of one engine step for handles submitted with a `batch_key` and hands
-    them over in ONE cross-thread call (e.g. one loop.call_soon_threadsafe per step instead of one
-    per token: 128 self-pipe writes per decode step otherwise)."""
+    them over per consumer channel in ONE call (`key.channel.deliver([(key, output), ...])`, from the
+    engine thread): one loop.call_soon_threadsafe per step for the gRPC event loop, one sendall per
+    step per mxstream connection — instead of one cross-thread wakeup per token."""
 
-    def __init__(self, deliver):
-        self.deliver = deliver  # deliver(list[(key, StepOutput)]) — called from the engine thread
+    def __init__(self, deliver=None):
         self.buf: list = []
+
+    def flush(self):
+        items, self.buf = self.buf, []
+        by: dict = {}
+        for k, o in items:
+            by.setdefault(k.channel, []).append((k, o))
+        for ch, its in by.items():
+            ch.deliver(its)
 
 
 class DecodeGraph:
@@ -245,8 +253,7 @@ class LLMEngine:
     def flush_outputs(self):
         bs = self.batch_sink
         if bs is not None and bs.buf:
-            items, bs.buf = bs.buf, []
-            bs.deliver(items)
+            bs.flush()
 
     def _loop(self):
         if self.device.type == "cuda":

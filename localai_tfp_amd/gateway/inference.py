@@ -153,7 +153,24 @@ class Inference:
         if cfg.template.reply_prefix:
             yield cfg.template.reply_prefix, usage
         dec = codecs.getincrementaldecoder("utf-8")(errors="replace")
-        async for r in m.apick().stream("PredictStream", opts):
+        rep = m.pick_replica()
+        mx = rep.mxclient()
+        if mx is not None:  # batched token channel to our own workers (serving/mxstream.py)
+            from ..serving.mxstream import F_ERROR
+            async for flags, tok, ptok, tp, tg, data in mx.stream(opts):
+                if flags & F_ERROR:
+                    raise RuntimeError(data.decode("utf-8", "replace"))
+                if tok or ptok:
+                    usage.prompt, usage.completion = ptok, tok
+                    usage.timing_prompt_processing, usage.timing_token_generation = tp, tg
+                text = dec.decode(data) if data else ""
+                if text:
+                    yield text, usage
+            tail = dec.decode(b"", final=True)
+            if tail:
+                yield tail, usage
+            return
+        async for r in rep.aclient().stream("PredictStream", opts):
             if r.tokens or r.prompt_tokens:
                 usage.prompt, usage.completion = r.prompt_tokens, r.tokens
                 usage.timing_prompt_processing = r.timing_prompt_processing

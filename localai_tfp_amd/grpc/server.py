@@ -236,6 +236,7 @@ class AioServer:
             self.port = self.server.add_insecure_port(self.addr)
             if self.port == 0:
                 raise RuntimeError(f"could not bind {self.addr}")
+            servicer.bound_addr = f"{self.addr.rsplit(':', 1)[0]}:{self.port}"
             await self.server.start()
         try:
             self.loop.run_until_complete(start())

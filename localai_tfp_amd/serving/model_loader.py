@@ -65,6 +65,20 @@ class Replica:
         self.server, self.servicer = server, servicer
         self.log_tail: collections.deque[str] = collections.deque(maxlen=200)
         self._aclients: dict[int, object] = {}
+        self.mx_path = ""  # mxstream socket advertised by the worker's LoadModel reply
+        self._mxclients: dict[int, object] = {}
+
+    def mxclient(self):
+        """Batched token channel (serving/mxstream.py) bound to the running loop, or None."""
+        if not self.mx_path:
+            return None
+        import asyncio
+        from .mxstream import StreamClient
+        key = id(asyncio.get_running_loop())
+        c = self._mxclients.get(key)
+        if c is None:
+            c = self._mxclients[key] = StreamClient(self.mx_path)
+        return c
 
     def aclient(self):
         """Async client bound to the running event loop (gateway request path)."""
@@ -353,6 +367,10 @@ class ModelLoader:
                 res = r.client.load_model(opts)
                 if not res.success:
                     raise BackendLoadError(res.message or "LoadModel failed")
+                for part in (res.message or "").split(";"):
+                    k, _, v = part.strip().partition("=")
+                    if k == "mxstream" and v and os.path.exists(v):
+                        r.mx_path = v
                 if self.watchdog:
                     self.watchdog.add(r.address, name)
                     r.client.watchdog = self.watchdog

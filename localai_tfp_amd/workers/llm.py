@@ -101,6 +101,26 @@ class LazyGrammar:
         return self.m is not None and (self._dead or self.m.is_done())
 
 
+class _LoopChannel:
+    def __init__(self, loop):
+        self.loop = loop
+
+    @staticmethod
+    def _dispatch(items):
+        for k, o in items:
+            k.q.put_nowait(o)
+
+    def deliver(self, items):
+        self.loop.call_soon_threadsafe(self._dispatch, items)
+
+
+class _QKey:
+    __slots__ = ("channel", "q")
+
+    def __init__(self, channel, q):
+        self.channel, self.q = channel, q
+
+
 class LLMServicer(BackendServicer):
     def __init__(self, device: str | None = None, tp=None):
         super().__init__()
@@ -114,6 +134,8 @@ class LLMServicer(BackendServicer):
         self._grammars: dict[str, object] = {}
         self._glock = threading.Lock()
         self.triggers: list[str] = []
+        self._channels: dict = {}
+        self.mxstream = None  # serving.mxstream.StreamServer once a model is loaded
         self.embeddings_enabled = False
         self.state = pb.STATE_UNINITIALIZED
 
@@ -125,11 +147,27 @@ class LLMServicer(BackendServicer):
         self.preloaded = True
         self.state = pb.STATE_READY
 
+    def _start_mxstream(self) -> str:
+        """Batched token channel for this framework's gateway (serving/mxstream.py); the address
+        is advertised in the LoadModel result as `mxstream=<path>`."""
+        if os.environ.get("MX_STREAM", "1") == "0" or self.engine is None:
+            return ""
+        if self.mxstream is None:
+            from ..serving.mxstream import StreamServer, socket_path_for
+            addr = getattr(self, "bound_addr", "") or f"pid{os.getpid()}:0"
+            try:
+                self.mxstream = StreamServer(self, socket_path_for(addr))
+            except OSError as ex:
+                log.warning("mxstream disabled: %s", ex)
+                return ""
+        return self.mxstream.path
+
     def LoadModel(self, request, context):
         import torch
         from ..models.loader import load_llm
         if getattr(self, "preloaded", False):
-            return pb.Result(message="preloaded", success=True)
+            mx = self._start_mxstream()
+            return pb.Result(message="preloaded" + (f"; mxstream={mx}" if mx else ""), success=True)
         try:
             t0 = time.perf_counter()
             opts = parse_options(request.Options)
@@ -181,6 +219,9 @@ class LLMServicer(BackendServicer):
             self.triggers = [t.word for t in request.GrammarTriggers if t.word]
             self.state = pb.STATE_READY
             msg = f"loaded {path} in {time.perf_counter() - t0:.1f}s on {self.device}"
+            mx = self._start_mxstream()
+            if mx:
+                msg += f"; mxstream={mx}"
             log.info(msg)
             return pb.Result(message=msg, success=True)
         except Exception as ex:
@@ -247,21 +288,19 @@ class LLMServicer(BackendServicer):
 
     # ---------------------------------------------------------------- RPCs
     def _submit_async(self, req):
-        """Submit with an asyncio queue as the batch key: the engine delivers each step's outputs
-        for all streams in one call_soon_threadsafe (engine.BatchedSink)."""
+        """Submit with an asyncio queue behind a per-loop channel: the engine delivers each step's
+        outputs for all streams of this loop in one call_soon_threadsafe (engine.BatchedSink)."""
         import asyncio
         from ..engine.engine import BatchedSink
         loop = asyncio.get_running_loop()
         eng = self.engine
-        if eng.batch_sink is None or getattr(eng.batch_sink, "loop", None) is not loop:
-            def dispatch(items):
-                for q, o in items:
-                    q.put_nowait(o)
-            bs = BatchedSink(lambda items: loop.call_soon_threadsafe(dispatch, items))
-            bs.loop = loop
-            eng.batch_sink = bs
+        if eng.batch_sink is None:
+            eng.batch_sink = BatchedSink()
+        ch = self._channels.get(id(loop))
+        if ch is None:
+            ch = self._channels[id(loop)] = _LoopChannel(loop)
         q: asyncio.Queue = asyncio.Queue()
-        h = eng.submit(req, batch_key=q)
+        h = eng.submit(req, batch_key=_QKey(ch, q))
         return h, q
 
     async def Predict(self, request, context):

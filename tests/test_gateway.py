@@ -71,6 +71,25 @@ def test_chat_stream_sse_framing(env):
     nonstream = c.post("/v1/chat/completions", json={**body, "stream": False}).json()
     assert text == nonstream["choices"][0]["message"]["content"]
     assert chunks[-1]["usage"]["completion_tokens"] == 8
+    # streamed through the batched worker channel (serving/mxstream.py), not per-token gRPC
+    rep = env[1].loader.get("tiny").replicas[0]
+    assert rep.mx_path and rep._mxclients
+
+
+def test_grpc_stream_path_matches_mxstream(env, monkeypatch):
+    c, a = env
+    body = {"model": "tiny", "stream": True, "messages": [{"role": "user", "content": "again"}]}
+    with c.stream("POST", "/v1/chat/completions", json=body) as r:
+        raw_mx = "".join(r.iter_text())
+    rep = a.loader.get("tiny").replicas[0]
+    monkeypatch.setattr(rep, "mx_path", "")
+    with c.stream("POST", "/v1/chat/completions", json=body) as r:
+        raw_grpc = "".join(r.iter_text())
+
+    def text(raw):
+        return "".join((json.loads(e[6:])["choices"][0].get("delta") or {}).get("content") or ""
+                       for e in raw.split("\n\n") if e.startswith("data: {"))
+    assert text(raw_mx) == text(raw_grpc) and text(raw_mx)
 
 
 def test_chat_go_template_and_stop(env):
