@@ -136,6 +136,9 @@ def main():
         t_max, tok_sum = float(mx[0]), float(sm[1])
         p50_all, p99_all = float(sm[2] / world), float(mx[3])
     value = tok_sum / t_max
+    from localai_tfp_amd.ops.linear import ACT_DTYPE
+    # 16-bit MFMA operands (Q4_K_M weights dequantised in-register), fp32 accumulation everywhere
+    act_name = "fp16" if ACT_DTYPE == torch.float16 else "bf16"
     if rank == 0:
         st = eng.stats
         out = {
@@ -149,7 +152,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16",
+            "dtype": act_name,
             "data": "synthetic (random-init Llama-3-8B weights in real Q4_K_M block formats; synthetic chat prompts)",
             "p50_ttft_ms": round(p50_all, 2),
             "p99_ttft_ms": round(p99_all, 2),
