@@ -160,7 +160,7 @@ def main():
                 "model": cfg.name + " Q4_K_M", "global_batch": args.concurrency * world,
                 "seq_len": args.prompt_len + args.gen_len, "prompt_len": args.prompt_len, "gen_len": args.gen_len,
                 "concurrency_per_gpu": args.concurrency, "parallelism": f"dp{world}",
-                "path": ("HTTP /v1/chat/completions (SSE) -> gateway -> gRPC -> engine" if args.path == "http"
+                "path": ("HTTP /v1/chat/completions (SSE) -> FastAPI gateway -> mxstream (batched gRPC-side channel) -> LLM worker engine" if args.path == "http"
                          else "engine in-process (gateway/gRPC excluded)"),
                 "load_s": round(t_load, 1), "graph_capture_s": round(t_capture, 1), "graphs": n_graphs,
                 "graph_steps": st["graph_steps"], "total_steps": st["steps"],
