@@ -295,6 +295,57 @@ def attn_prefill(q: torch.Tensor, k_cache, v_cache, block_tables: torch.Tensor, 
     return out
 
 
+def attn_dense(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, out: torch.Tensor, B: int, Sq: int, Sk: int,
+               Hq: int, Hkv: int, D: int, scale: float, causal: bool = False,
+               qlen: torch.Tensor | None = None, klen: torch.Tensor | None = None):
+    """Flash attention over dense token-major 16-bit tensors (attention_dense.hip).
+
+    q/out: [B*Sq, >= Hq*D] (row stride = .stride(0)); k/v: [B*Sk, >= Hkv*D]. Head dims other than
+    64/128 are zero-padded to the next supported size (exact: padded dims add 0 to q.k and produce
+    0 output columns that are dropped). klen/qlen: optional int32 [B] valid lengths (padding)."""
+    if B == 0 or Sq == 0:
+        return out
+    if not q.is_cuda:
+        qf = q[:, :Hq * D].float().view(B, Sq, Hq, D).transpose(1, 2)
+        kf = k[:, :Hkv * D].float().view(B, Sk, Hkv, D).transpose(1, 2)
+        vf = v[:, :Hkv * D].float().view(B, Sk, Hkv, D).transpose(1, 2)
+        if Hq != Hkv:
+            kf = kf.repeat_interleave(Hq // Hkv, 1)
+            vf = vf.repeat_interleave(Hq // Hkv, 1)
+        s = torch.einsum("bhqd,bhkd->bhqk", qf, kf) * scale
+        kp = torch.arange(Sk)
+        mask = torch.zeros(B, 1, Sq, Sk, dtype=torch.bool)
+        if causal:
+            mask |= (kp[None, :] > (torch.arange(Sq)[:, None] + (Sk - Sq)))[None, None]
+        if klen is not None:
+            mask |= (kp[None, None, None, :] >= klen.view(B, 1, 1, 1).cpu())
+        s = s.masked_fill(mask, float("-inf"))
+        p = torch.softmax(s, -1).nan_to_num(0.0)
+        o = torch.einsum("bhqk,bhkd->bqhd", p, vf).reshape(B * Sq, Hq * D)
+        if qlen is not None:
+            for b in range(B):
+                o[b * Sq + int(qlen[b]):(b + 1) * Sq] = 0
+        out[:, :Hq * D].copy_(o)
+        return out
+    Dp = 64 if D <= 64 else 128
+    if Dp != D:
+        def pad(t, H):
+            x = t[:, :H * D].reshape(t.shape[0], H, D)
+            return torch.nn.functional.pad(x, (0, Dp - D)).reshape(t.shape[0], H * Dp)
+        qp, kp_, vp = pad(q, Hq), pad(k, Hkv), pad(v, Hkv)
+        op = torch.empty((out.shape[0], Hq * Dp), dtype=out.dtype, device=out.device)
+        attn_dense(qp, kp_, vp, op, B, Sq, Sk, Hq, Hkv, Dp, scale, causal, qlen, klen)
+        out[:, :Hq * D].copy_(op.view(-1, Hq, Dp)[..., :D].reshape(-1, Hq * D))
+        return out
+    if not (q.dtype == k.dtype == v.dtype == out.dtype):
+        raise ValueError("attn_dense: q/k/v/out must share one 16-bit dtype")
+    N.ensure_act(out.dtype)
+    N.kcall("mxk_attn_dense", q.data_ptr(), q.stride(0), k.data_ptr(), k.stride(0), v.data_ptr(), v.stride(0),
+            out.data_ptr(), out.stride(0), B, Sq, Sk, Hq, Hkv, D, N.ptr(qlen), N.ptr(klen), int(causal),
+            float(scale), N.stream_ptr())
+    return out
+
+
 # ------------------------------------------------------------------------------------------------
 # activations / misc
 

@@ -374,3 +374,20 @@ def test_attn_outputs_act16(dt):
     out = torch.empty(B, Hq, D, dtype=dt, device=DEV)
     K.attn_decode(q.to(DEV), kc.to(DEV), vc.to(DEV), bt.to(DEV), seq.to(DEV), 0.088, out, part_size=128)
     assert rel(out, ref) < 1e-2
+
+
+@pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("D,Hq,Hkv", [(64, 8, 8), (128, 8, 2), (40, 8, 8), (80, 4, 4)])
+@pytest.mark.parametrize("causal", [False, True])
+def test_attn_dense(dt, D, Hq, Hkv, causal):
+    B, Sq, Sk = 2, 77, 150 if not causal else 77
+    g = torch.Generator().manual_seed(D + Hq)
+    q = torch.randn(B * Sq, Hq * D, generator=g).to(dt)
+    k = torch.randn(B * Sk, Hkv * D, generator=g).to(dt)
+    v = torch.randn(B * Sk, Hkv * D, generator=g).to(dt)
+    klen = torch.tensor([Sk, Sk - 13], dtype=torch.int32)
+    ref = torch.empty(B * Sq, Hq * D)
+    K.attn_dense(q, k, v, ref, B, Sq, Sk, Hq, Hkv, D, 0.125, causal, klen=klen)
+    out = torch.empty(B * Sq, Hq * D, dtype=dt, device=DEV)
+    K.attn_dense(q.to(DEV), k.to(DEV), v.to(DEV), out, B, Sq, Sk, Hq, Hkv, D, 0.125, causal, klen=klen.to(DEV))
+    assert rel(out, ref) < 1.5e-2
