@@ -241,7 +241,7 @@ def guess_backend(cfg, model_path: str) -> list[str]:
     full = os.path.join(model_path, m)
     low = m.lower()
     if low.startswith("synthetic:"):
-        return ["llama-cpp"]
+        return ["bert-embeddings"] if low.startswith("synthetic:bert") else ["llama-cpp"]
     if low.endswith(".onnx"):
         return ["piper", "silero-vad"]
     if low.endswith(".gguf") and os.path.isfile(full):
