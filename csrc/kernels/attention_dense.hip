@@ -48,7 +48,8 @@ __global__ __launch_bounds__(256) void attn_dense_kernel(const uint16_t* __restr
                                                          const uint16_t* __restrict__ v, int v_stride,
                                                          uint16_t* __restrict__ o, int o_stride, int Sq, int Sk,
                                                          int Hq, int Hkv, const int* __restrict__ qlen_b,
-                                                         const int* __restrict__ klen_b, int causal, float scale) {
+                                                         const int* __restrict__ klen_b, int causal, float scale,
+                                                         int kv_rows) {
     constexpr int KT = 64;
     constexpr int KBYTES = KT * D * 2;
     constexpr int PSTRIDE = (KT + 8) * 2;
@@ -67,8 +68,8 @@ __global__ __launch_bounds__(256) void attn_dense_kernel(const uint16_t* __restr
     int kv_end = klen;
     if (causal) kv_end = min(kv_end, blockIdx.x * 64 + 64 + shift);
     const float qs = scale * LOG2E_D;
-    const uint16_t* kb = k + (size_t)b * Sk * k_stride + (size_t)kvh * D;
-    const uint16_t* vb_ = v + (size_t)b * Sk * v_stride + (size_t)kvh * D;
+    const uint16_t* kb = k + (size_t)b * kv_rows * k_stride + (size_t)kvh * D;
+    const uint16_t* vb_ = v + (size_t)b * kv_rows * v_stride + (size_t)kvh * D;
 
     u32x4 qf[D / 32];
     {
@@ -183,21 +184,25 @@ __global__ __launch_bounds__(256) void attn_dense_kernel(const uint16_t* __restr
 }
 
 // q/k/v/o: 16-bit (act16 mode) token-major with row strides in elements; B batches of Sq queries /
-// Sk keys; Hq query heads, Hkv key/value heads (Hq % Hkv == 0); D in {64, 128}.
+// Sk keys; Hq query heads, Hkv key/value heads (Hq % Hkv == 0); D in {64, 128}. K/V rows of batch b
+// start at row b * kv_rows (kv_rows = 0 -> Sk): a fixed-capacity KV cache [B, cap, H*D] is read in
+// place with Sk = valid length (causal offset Sk - Sq) or Sk = cap with per-batch klen.
 extern "C" int mxk_attn_dense(const uint16_t* q, int q_stride, const uint16_t* k, int k_stride, const uint16_t* v,
                               int v_stride, uint16_t* o, int o_stride, int B, int Sq, int Sk, int Hq, int Hkv, int D,
-                              const int* qlen, const int* klen, int causal, float scale, hipStream_t st) {
+                              const int* qlen, const int* klen, int causal, float scale, int kv_rows,
+                              hipStream_t st) {
     if (B <= 0 || Sq <= 0) return 0;
+    if (kv_rows <= 0) kv_rows = Sk;
     if (Hq % Hkv || (D != 64 && D != 128)) return (int)hipErrorInvalidValue;
     if ((q_stride | k_stride | v_stride) & 7) return (int)hipErrorInvalidValue;
     dim3 grid((Sq + 63) / 64, Hq, B);
     MX_ACT_DISPATCH({
         if (D == 128)
             attn_dense_kernel<128, F16><<<grid, 256, 0, st>>>(q, q_stride, k, k_stride, v, v_stride, o, o_stride, Sq, Sk,
-                                                             Hq, Hkv, qlen, klen, causal, scale);
+                                                             Hq, Hkv, qlen, klen, causal, scale, kv_rows);
         else
             attn_dense_kernel<64, F16><<<grid, 256, 0, st>>>(q, q_stride, k, k_stride, v, v_stride, o, o_stride, Sq, Sk,
-                                                            Hq, Hkv, qlen, klen, causal, scale);
+                                                            Hq, Hkv, qlen, klen, causal, scale, kv_rows);
     });
     MXK_CHECK_LAUNCH();
 }

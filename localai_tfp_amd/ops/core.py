@@ -297,18 +297,21 @@ def attn_prefill(q: torch.Tensor, k_cache, v_cache, block_tables: torch.Tensor, 
 
 def attn_dense(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, out: torch.Tensor, B: int, Sq: int, Sk: int,
                Hq: int, Hkv: int, D: int, scale: float, causal: bool = False,
-               qlen: torch.Tensor | None = None, klen: torch.Tensor | None = None):
+               qlen: torch.Tensor | None = None, klen: torch.Tensor | None = None, kv_rows: int = 0):
     """Flash attention over dense token-major 16-bit tensors (attention_dense.hip).
 
-    q/out: [B*Sq, >= Hq*D] (row stride = .stride(0)); k/v: [B*Sk, >= Hkv*D]. Head dims other than
-    64/128 are zero-padded to the next supported size (exact: padded dims add 0 to q.k and produce
-    0 output columns that are dropped). klen/qlen: optional int32 [B] valid lengths (padding)."""
+    q/out: [B*Sq, >= Hq*D] (row stride = .stride(0)); k/v: [B*kv_rows, >= Hkv*D] of which the first
+    Sk rows per batch are read (kv_rows = 0 -> Sk; a fixed-capacity KV cache passes its capacity).
+    Head dims other than 64/128 are zero-padded to the next supported size (exact: padded dims add
+    0 to q.k and produce 0 output columns that are dropped). klen/qlen: optional int32 [B] valid
+    lengths (padding)."""
     if B == 0 or Sq == 0:
         return out
+    R = kv_rows or Sk
     if not q.is_cuda:
         qf = q[:, :Hq * D].float().view(B, Sq, Hq, D).transpose(1, 2)
-        kf = k[:, :Hkv * D].float().view(B, Sk, Hkv, D).transpose(1, 2)
-        vf = v[:, :Hkv * D].float().view(B, Sk, Hkv, D).transpose(1, 2)
+        kf = k[:B * R, :Hkv * D].float().view(B, R, Hkv, D)[:, :Sk].transpose(1, 2)
+        vf = v[:B * R, :Hkv * D].float().view(B, R, Hkv, D)[:, :Sk].transpose(1, 2)
         if Hq != Hkv:
             kf = kf.repeat_interleave(Hq // Hkv, 1)
             vf = vf.repeat_interleave(Hq // Hkv, 1)
@@ -332,9 +335,9 @@ def attn_dense(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, out: torch.Ten
         def pad(t, H):
             x = t[:, :H * D].reshape(t.shape[0], H, D)
             return torch.nn.functional.pad(x, (0, Dp - D)).reshape(t.shape[0], H * Dp)
-        qp, kp_, vp = pad(q, Hq), pad(k, Hkv), pad(v, Hkv)
+        qp, kp_, vp = pad(q, Hq), pad(k[:B * R], Hkv), pad(v[:B * R], Hkv)
         op = torch.empty((out.shape[0], Hq * Dp), dtype=out.dtype, device=out.device)
-        attn_dense(qp, kp_, vp, op, B, Sq, Sk, Hq, Hkv, Dp, scale, causal, qlen, klen)
+        attn_dense(qp, kp_, vp, op, B, Sq, Sk, Hq, Hkv, Dp, scale, causal, qlen, klen, R)
         out[:, :Hq * D].copy_(op.view(-1, Hq, Dp)[..., :D].reshape(-1, Hq * D))
         return out
     if not (q.dtype == k.dtype == v.dtype == out.dtype):
@@ -342,7 +345,7 @@ def attn_dense(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, out: torch.Ten
     N.ensure_act(out.dtype)
     N.kcall("mxk_attn_dense", q.data_ptr(), q.stride(0), k.data_ptr(), k.stride(0), v.data_ptr(), v.stride(0),
             out.data_ptr(), out.stride(0), B, Sq, Sk, Hq, Hkv, D, N.ptr(qlen), N.ptr(klen), int(causal),
-            float(scale), N.stream_ptr())
+            float(scale), int(R), N.stream_ptr())
     return out
 
 

@@ -391,3 +391,27 @@ def test_attn_dense(dt, D, Hq, Hkv, causal):
     out = torch.empty(B * Sq, Hq * D, dtype=dt, device=DEV)
     K.attn_dense(q.to(DEV), k.to(DEV), v.to(DEV), out, B, Sq, Sk, Hq, Hkv, D, 0.125, causal, klen=klen.to(DEV))
     assert rel(out, ref) < 1.5e-2
+
+
+@pytest.mark.parametrize("causal", [False, True])
+def test_attn_dense_kv_capacity(causal):
+    """Fixed-capacity KV cache read in place (kv_rows): Whisper decoder self-attention layout."""
+    B, Sq, Sk, cap, H, D = 3, 5 if causal else 1, 37, 64, 8, 64
+    dt = torch.float16
+    g = torch.Generator().manual_seed(11)
+    q = torch.randn(B * Sq, H * D, generator=g).to(dt)
+    k = torch.randn(B * cap, H * D, generator=g).to(dt)
+    v = torch.randn(B * cap, H * D, generator=g).to(dt)
+    klen = torch.tensor([Sk, Sk - 3, 9], dtype=torch.int32)
+    ref = torch.empty(B * Sq, H * D)
+    kw = dict(klen=None if causal else klen, kv_rows=cap)
+    K.attn_dense(q, k, v, ref, B, Sq, Sk, H, H, D, 0.125, causal, **kw)
+    kref = k.view(B, cap, -1)[:, :Sk].reshape(B * Sk, -1)
+    vref = v.view(B, cap, -1)[:, :Sk].reshape(B * Sk, -1)
+    ref2 = torch.empty(B * Sq, H * D)
+    K.attn_dense(q, kref, vref, ref2, B, Sq, Sk, H, H, D, 0.125, causal, klen=None if causal else klen)
+    assert torch.allclose(ref, ref2)
+    out = torch.empty(B * Sq, H * D, dtype=dt, device=DEV)
+    kw = dict(klen=None if causal else klen.to(DEV), kv_rows=cap)
+    K.attn_dense(q.to(DEV), k.to(DEV), v.to(DEV), out, B, Sq, Sk, H, H, D, 0.125, causal, **kw)
+    assert rel(out, ref) < 1.5e-2
