@@ -1,0 +1,219 @@
+// diffusion.hip — normalisation / modulation kernels for the diffusion models (SD3 MMDiT, SD UNet,
+// VAE) and other adaLN transformers:
+//
+//  * layernorm_mod:  y = LN(x) * (1 + scale[b]) + shift[b]   (adaLN-Zero / AdaLayerNormContinuous)
+//                    fp32 residual stream in, act16 out; per-sample modulation rows from the
+//                    conditioning GEMM (fp32 or act16), two-pass variance from registers.
+//  * gate_add:       x[b, s, :] += gate[b, :] * y[b, s, :]  (gated residual, act16 y, fp32 x)
+//  * GroupNorm NHWC: a wide stats pass (grid over spatial chunks x samples, per-group partials
+//                    reduced in LDS, fp64 atomics into [N, G, 2]) + an elementwise apply pass with
+//                    optional fused SiLU, act16 in / act16 out. The old one-workgroup-per-group
+//                    kernel left most of the 256 CUs idle at VAE resolutions (HW up to 1M).
+#include "mx_common.h"
+
+// ---------------------------------------------------------------------------------------------
+// LayerNorm + modulation
+template <bool F16, int PER>
+__global__ __launch_bounds__(256) void layernorm_mod_kernel(const float* __restrict__ x, int ldx,
+                                                            const float* __restrict__ scale,
+                                                            const float* __restrict__ shift, int ldm,
+                                                            int rows_per_b, uint16_t* __restrict__ out, int ldo,
+                                                            int H, float eps) {
+    __shared__ float red[4];
+    const int row = blockIdx.x;
+    const int b = row / rows_per_b;
+    const float* xr = x + (size_t)row * ldx;
+    float v[PER];
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+        const int c = threadIdx.x + 256 * i;
+        v[i] = c < H ? xr[c] : 0.f;
+        s += v[i];
+    }
+    s = block_sum<256>(s, red);
+    const float mean = s / H;
+    float ss = 0.f;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+        const int c = threadIdx.x + 256 * i;
+        const float d = c < H ? v[i] - mean : 0.f;
+        ss += d * d;
+    }
+    ss = block_sum<256>(ss, red);
+    const float rs = rsqrtf(ss / H + eps);
+    const float* sc = scale ? scale + (size_t)b * ldm : nullptr;
+    const float* sh = shift ? shift + (size_t)b * ldm : nullptr;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+        const int c = threadIdx.x + 256 * i;
+        if (c < H) {
+            float y = (v[i] - mean) * rs;
+            if (sc) y *= 1.f + sc[c];
+            if (sh) y += sh[c];
+            out[(size_t)row * ldo + c] = f32_to_act<F16>(y);
+        }
+    }
+}
+
+extern "C" int mxk_layernorm_mod(const float* x, int ldx, const float* scale, const float* shift, int ldm,
+                                 int rows_per_b, uint16_t* out, int ldo, int rows, int H, float eps, hipStream_t st) {
+    if (rows <= 0) return 0;
+    if (H > 256 * 16 || rows_per_b <= 0) return (int)hipErrorInvalidValue;
+#define LNM(P) layernorm_mod_kernel<F16, P><<<rows, 256, 0, st>>>(x, ldx, scale, shift, ldm, rows_per_b, out, ldo, H, eps)
+    MX_ACT_DISPATCH({
+        if (H <= 1024) LNM(4);
+        else if (H <= 2048) LNM(8);
+        else LNM(16);
+    });
+#undef LNM
+    MXK_CHECK_LAUNCH();
+}
+
+// ---------------------------------------------------------------------------------------------
+// gated residual: x (fp32) += gate[b] * y (act16), 8 columns per thread
+template <bool F16>
+__global__ __launch_bounds__(256) void gate_add_kernel(float* __restrict__ x, int ldx, const uint16_t* __restrict__ y,
+                                                       int ldy, const float* __restrict__ gate, int ldg,
+                                                       int rows_per_b, int rows, int H) {
+    const int cpr = H / 8;
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= (size_t)rows * cpr) return;
+    const int row = (int)(i / cpr), c = (int)(i % cpr) * 8;
+    const int b = row / rows_per_b;
+    const uint4 yv = *(const uint4*)(y + (size_t)row * ldy + c);
+    const uint32_t yw[4] = {yv.x, yv.y, yv.z, yv.w};
+    float* xr = x + (size_t)row * ldx + c;
+    float4 a = *(float4*)xr, bq = *(float4*)(xr + 4);
+    float xs[8] = {a.x, a.y, a.z, a.w, bq.x, bq.y, bq.z, bq.w};
+    const float* g = gate ? gate + (size_t)b * ldg + c : nullptr;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        float lo, hi;
+        unpack_act2<F16>(yw[k], lo, hi);
+        xs[2 * k] += (g ? g[2 * k] : 1.f) * lo;
+        xs[2 * k + 1] += (g ? g[2 * k + 1] : 1.f) * hi;
+    }
+    *(float4*)xr = make_float4(xs[0], xs[1], xs[2], xs[3]);
+    *(float4*)(xr + 4) = make_float4(xs[4], xs[5], xs[6], xs[7]);
+}
+
+extern "C" int mxk_gate_add(float* x, int ldx, const uint16_t* y, int ldy, const float* gate, int ldg, int rows_per_b,
+                            int rows, int H, hipStream_t st) {
+    if (rows <= 0) return 0;
+    if (H % 8 || ldx % 4 || ldy % 8) return (int)hipErrorInvalidValue;
+    const size_t n = (size_t)rows * (H / 8);
+    MX_ACT_DISPATCH(gate_add_kernel<F16><<<(unsigned)((n + 255) / 256), 256, 0, st>>>(x, ldx, y, ldy, gate, ldg,
+                                                                                      rows_per_b, rows, H));
+    MXK_CHECK_LAUNCH();
+}
+
+// ---------------------------------------------------------------------------------------------
+// GroupNorm over NHWC act16
+constexpr int GN_MAXG = 32;
+
+template <bool F16>
+__global__ __launch_bounds__(256) void gn_stats_kernel(const uint16_t* __restrict__ x, int HW, int C, int G,
+                                                       int rows_per_block, double* __restrict__ stats) {
+    __shared__ float gs[GN_MAXG], gss[GN_MAXG];
+    const int n = blockIdx.y;
+    const int cpr = C / 8;                 // 8-channel chunks per pixel row
+    const int rpi = 256 / cpr;             // pixel rows per iteration (cpr <= 256)
+    const int t = threadIdx.x;
+    if (t < GN_MAXG) { gs[t] = 0.f; gss[t] = 0.f; }
+    __syncthreads();
+    const int p0 = blockIdx.x * rows_per_block;
+    const int p1 = min(HW, p0 + rows_per_block);
+    float s[8] = {0, 0, 0, 0, 0, 0, 0, 0}, ss[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const int cc = t % cpr, pr = t / cpr;
+    if (pr < rpi) {
+        const uint16_t* xb = x + (size_t)n * HW * C + cc * 8;
+        for (int p = p0 + pr; p < p1; p += rpi) {
+            const uint4 v = *(const uint4*)(xb + (size_t)p * C);
+            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                float lo, hi;
+                unpack_act2<F16>(w[k], lo, hi);
+                s[2 * k] += lo;
+                ss[2 * k] += lo * lo;
+                s[2 * k + 1] += hi;
+                ss[2 * k + 1] += hi * hi;
+            }
+        }
+        const int cg = C / G;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int g = (cc * 8 + k) / cg;
+            atomicAdd(&gs[g], s[k]);
+            atomicAdd(&gss[g], ss[k]);
+        }
+    }
+    __syncthreads();
+    if (t < G) {
+        atomicAdd(&stats[((size_t)n * G + t) * 2], (double)gs[t]);
+        atomicAdd(&stats[((size_t)n * G + t) * 2 + 1], (double)gss[t]);
+    }
+}
+
+template <bool F16, bool SILU>
+__global__ __launch_bounds__(256) void gn_apply_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y,
+                                                       const float* __restrict__ gamma,
+                                                       const float* __restrict__ beta,
+                                                       const double* __restrict__ stats, int HW, int C, int G,
+                                                       float eps, size_t total8) {
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= total8) return;
+    const int cpr = C / 8;
+    const int c0 = (int)(i % cpr) * 8;
+    const int n = (int)(i / ((size_t)HW * cpr));
+    const int cg = C / G;
+    const double cnt = (double)HW * cg;
+    const uint4 v = *(const uint4*)(x + i * 8);
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    uint32_t o[4];
+    int gprev = -1;
+    float mean = 0.f, rs = 0.f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        float e[2];
+        unpack_act2<F16>(w[k], e[0], e[1]);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int c = c0 + 2 * k + j;
+            const int g = c / cg;
+            if (g != gprev) {
+                const double m = stats[((size_t)n * G + g) * 2] / cnt;
+                const double var = fmax(stats[((size_t)n * G + g) * 2 + 1] / cnt - m * m, 0.0);
+                mean = (float)m;
+                rs = rsqrtf((float)var + eps);
+                gprev = g;
+            }
+            float r = (e[j] - mean) * rs * gamma[c] + beta[c];
+            if (SILU) r = silu_f(r);
+            e[j] = r;
+        }
+        o[k] = pack_act2<F16>(e[0], e[1]);
+    }
+    *(uint4*)(y + i * 8) = make_uint4(o[0], o[1], o[2], o[3]);
+}
+
+// x, y: act16 [N, HW, C] (NHWC / channels_last), y may alias x. workspace: N*G*2 doubles.
+extern "C" int mxk_groupnorm16(const uint16_t* x, uint16_t* y, const float* gamma, const float* beta, int N, int HW,
+                               int C, int G, float eps, int silu, double* ws, hipStream_t st) {
+    if (N <= 0 || HW <= 0) return 0;
+    if (C % 8 || C % G || G > GN_MAXG || C / 8 > 256) return (int)hipErrorInvalidValue;
+    hipMemsetAsync(ws, 0, sizeof(double) * N * G * 2, st);
+    const int rpi = 256 / (C / 8);
+    int rows_per_block = max(rpi * 8, (HW + 255) / 256);          // >= 8 iterations, <= 256 blocks per sample
+    rows_per_block = (rows_per_block + rpi - 1) / rpi * rpi;
+    dim3 g1((HW + rows_per_block - 1) / rows_per_block, N);
+    const size_t total8 = (size_t)N * HW * (C / 8);
+    const unsigned g2 = (unsigned)((total8 + 255) / 256);
+    MX_ACT_DISPATCH({
+        gn_stats_kernel<F16><<<g1, 256, 0, st>>>(x, HW, C, G, rows_per_block, ws);
+        if (silu) gn_apply_kernel<F16, true><<<g2, 256, 0, st>>>(x, y, gamma, beta, ws, HW, C, G, eps, total8);
+        else gn_apply_kernel<F16, false><<<g2, 256, 0, st>>>(x, y, gamma, beta, ws, HW, C, G, eps, total8);
+    });
+    MXK_CHECK_LAUNCH();
+}

@@ -29,6 +29,9 @@ KERNEL_SIGS = {
     "mxk_quant_q8": [P, I, P, P, I, I, P],
     "mxk_layernorm": [P, I, P, I, P, P, P, P, P, I, I, I, F, P],
     "mxk_groupnorm_nhwc": [P, P, P, P, I, I, I, I, F, I, P],
+    "mxk_layernorm_mod": [P, I, P, P, I, I, P, I, I, I, F, P],
+    "mxk_gate_add": [P, I, P, I, P, I, I, I, I, P],
+    "mxk_groupnorm16": [P, P, P, P, I, I, I, I, F, I, P, P],
     "mxk_qgemm_mfma": [I, I, I, I, P, I, P, P, I, I, I, I, P, I, P],
     "mxk_qgemm16": [I, I, I, I, P, I, P, P, I, I, I, I, P, I, P],
     "mxk_set_act_f16": [I],
@@ -52,9 +55,6 @@ KERNEL_SIGS = {
     "mxk_gather_rows": [P, I, P, I, I, F, P, P],
     "mxk_add_bias_f32": [P, I, P, I, I, P],
     "mxk_select_rows_f32": [P, I, P, I, I, P, I, P],
-    "mxk_bf16_gemm": [P, I, P, I, P, I, I, I, I, I, P],
-    "mxk_conv2d_nhwc": [P, P, P, P, I, I, I, I, I, I, I, I, I, I, P],
-    "mxk_cosine_topk": [P, P, I, I, I, I, P, P, P],
 }
 
 HIP_ERRORS = {1: "hipErrorInvalidValue", 2: "hipErrorOutOfMemory", 98: "hipErrorInvalidDeviceFunction",

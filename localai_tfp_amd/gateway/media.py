@@ -5,6 +5,7 @@ localai/tts.go:25 (also served at /v1/audio/speech), localai/video.go:67, static
 core/http/app.go:168-170; backend side core/backend/image.go, transcript.go, tts.go, video.go."""
 from __future__ import annotations
 
+import asyncio
 import base64
 import os
 import shutil
@@ -74,24 +75,29 @@ async def images(request: Request):
         except ValueError:
             raise RequestError("invalid value for 'size'")
         b64 = cfg.response_format == "b64_json"
-        out = []
         base_url = str(request.base_url).rstrip("/")
+        jobs = []
         for prompt in cfg.prompt_strings:
             for _ in range(req.n or 1):
                 pos, _, neg = prompt.partition("|")
                 step = req.step or cfg.step or 15
                 img_dir = os.path.join(a.cfg.generated_content_dir, "images")
                 dst = os.path.join(img_dir if not b64 else a.cfg.generated_content_dir, f"b64{uuid.uuid4().hex}.png")
-                await a.inference.image(cfg, height=h, width=w, mode=req.mode, step=step,
-                                        seed=cfg.resolved_seed(), positive_prompt=pos, negative_prompt=neg,
-                                        dst=dst, src=src, EnableParameters=cfg.diffusers.enable_parameters,
-                                        CLIPSkip=cfg.diffusers.clip_skip)
-                if b64:
-                    with open(dst, "rb") as f:
-                        out.append({"b64_json": base64.b64encode(f.read()).decode()})
-                    os.remove(dst)
-                else:
-                    out.append({"url": f"{base_url}/generated-images/{os.path.basename(dst)}"})
+                jobs.append((dst, a.inference.image(
+                    cfg, height=h, width=w, mode=req.mode, step=step, seed=cfg.resolved_seed(),
+                    positive_prompt=pos, negative_prompt=neg, dst=dst, src=src,
+                    EnableParameters=cfg.diffusers.enable_parameters, CLIPSkip=cfg.diffusers.clip_skip)))
+        # the reference renders the N images one after another (image.go:158-226); here they are
+        # issued together so data-parallel replicas (one per GPU) render them concurrently
+        await asyncio.gather(*(j for _, j in jobs))
+        out = []
+        for dst, _ in jobs:
+            if b64:
+                with open(dst, "rb") as f:
+                    out.append({"b64_json": base64.b64encode(f.read()).decode()})
+                os.remove(dst)
+            else:
+                out.append({"url": f"{base_url}/generated-images/{os.path.basename(dst)}"})
         return {"id": str(uuid.uuid4()), "created": int(time.time()), "data": out,
                 "usage": {"prompt_tokens": 0, "completion_tokens": 0, "total_tokens": 0}}
     finally:

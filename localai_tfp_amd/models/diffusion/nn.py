@@ -1,0 +1,120 @@
+"""Shared building blocks of the diffusion stack (text encoders, MMDiT, VAE, UNet).
+
+Parameters live in `torch.nn.Module`s named like the public Hugging Face / diffusers checkpoints so a
+`state_dict` loads directly from safetensors; the forward passes run on this library's kernels:
+hipBLASLt GEMMs (F.linear / addmm with fp32 accumulate into residual streams), attention on the
+MFMA flash kernel (attention_dense.hip, head dim <= 128; larger heads — only the VAE mid-block's
+single 512-wide head — use PyTorch SDPA), adaLN / gated residual / GroupNorm kernels
+(diffusion.hip), and MIOpen convolutions in channels_last (NHWC) layout.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+from ...ops import core as K
+from ...ops.linear import _fp32_out_ok
+
+
+def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, B: int, Sq: int, Sk: int, H: int, D: int,
+              scale: float | None = None, causal: bool = False, klen=None) -> torch.Tensor:
+    """q: [B*Sq, H*D] rows (any row stride), k/v: [B*Sk, H*D] -> [B*Sq, H*D] (q dtype)."""
+    scale = scale if scale is not None else 1.0 / math.sqrt(D)
+    if q.is_cuda and D <= 128:
+        out = torch.empty(B * Sq, H * D, dtype=q.dtype, device=q.device)
+        return K.attn_dense(q, k, v, out, B, Sq, Sk, H, H, D, scale, causal, klen=klen)
+    qh = q.reshape(B, Sq, H, D).transpose(1, 2)
+    kh = k.reshape(B, Sk, H, D).transpose(1, 2)
+    vh = v.reshape(B, Sk, H, D).transpose(1, 2)
+    mask = None
+    if klen is not None:
+        mask = (torch.arange(Sk, device=q.device)[None, :] < klen.to(q.device).view(B, 1))[:, None, None, :]
+    o = F.scaled_dot_product_attention(qh, kh, vh, attn_mask=mask, is_causal=causal and mask is None, scale=scale)
+    return o.transpose(1, 2).reshape(B * Sq, H * D)
+
+
+def linear_acc(x: torch.Tensor, lin: nn.Linear, acc: torch.Tensor) -> torch.Tensor:
+    """acc (fp32) += lin(x): the residual add runs as GEMM beta = 1 where the build supports fp32 out."""
+    if x.is_cuda and x.dtype != torch.float32 and _fp32_out_ok(x.dtype) and acc.is_contiguous():
+        if lin.bias is not None:
+            acc.add_(lin.bias)
+        torch.addmm(acc, x, lin.weight.t(), out_dtype=torch.float32, out=acc)
+        return acc
+    acc.add_(F.linear(x, lin.weight, lin.bias).float())
+    return acc
+
+
+def linear_f32(x: torch.Tensor, lin: nn.Linear) -> torch.Tensor:
+    if x.is_cuda and x.dtype != torch.float32 and _fp32_out_ok(x.dtype):
+        out = torch.empty(x.shape[0], lin.out_features, dtype=torch.float32, device=x.device)
+        if lin.bias is not None:
+            out.copy_(lin.bias.float().expand_as(out))
+            torch.addmm(out, x, lin.weight.t(), out_dtype=torch.float32, out=out)
+        else:
+            torch.mm(x, lin.weight.t(), out_dtype=torch.float32, out=out)
+        return out
+    return F.linear(x, lin.weight, lin.bias).float()
+
+
+def layernorm16(x: torch.Tensor, w, b, eps: float, dtype) -> torch.Tensor:
+    out = torch.empty(x.shape, dtype=dtype, device=x.device)
+    K.layernorm(x, w, b, eps, out)
+    return out
+
+
+def timestep_embedding(t: torch.Tensor, dim: int, flip_sin_to_cos: bool = True, shift: float = 0.0,
+                       max_period: float = 10000.0) -> torch.Tensor:
+    """Sinusoidal timestep features (diffusers `Timesteps`)."""
+    half = dim // 2
+    ex = -math.log(max_period) * torch.arange(half, dtype=torch.float32, device=t.device) / (half - shift)
+    a = t.float()[:, None] * torch.exp(ex)[None, :]
+    emb = torch.cat([torch.sin(a), torch.cos(a)], -1)
+    if flip_sin_to_cos:
+        emb = torch.cat([emb[:, half:], emb[:, :half]], -1)
+    return emb
+
+
+class GroupNorm(nn.GroupNorm):
+    """GroupNorm (+ fused SiLU) on NHWC 16-bit activations (diffusion.hip); fp32 parameters."""
+
+    def run(self, x: torch.Tensor, silu: bool = False) -> torch.Tensor:
+        return K.groupnorm16(x, self.weight, self.bias, self.num_groups, self.eps, silu)
+
+
+def conv(x: torch.Tensor, m: nn.Conv2d) -> torch.Tensor:
+    return F.conv2d(x, m.weight, m.bias, m.stride, m.padding)
+
+
+def cast_module(m: nn.Module, device, dtype) -> nn.Module:
+    """Weights to `dtype` on `device`; norm parameters stay fp32 (the norm kernels read fp32)."""
+    m.to(device)
+    for mod in m.modules():
+        keep32 = isinstance(mod, (nn.LayerNorm, nn.GroupNorm)) or type(mod).__name__.endswith("RMSNorm")
+        for p in mod.parameters(recurse=False):
+            p.data = p.data.float() if keep32 else p.data.to(dtype)
+        for n, bf in mod.named_buffers(recurse=False):
+            setattr(mod, n, bf.float())
+    for mod in m.modules():
+        if isinstance(mod, nn.Conv2d) and torch.device(device).type == "cuda":
+            mod.weight.data = mod.weight.data.contiguous(memory_format=torch.channels_last)
+    return m
+
+
+def init_synthetic(m: nn.Module, seed: int = 0, std: float = 0.02):
+    """Random-init weights in place (benchmarks / tests; no checkpoint download). Norm weights 1,
+    biases 0, other tensors N(0, std) scaled by fan-in for linears/convs."""
+    g = torch.Generator(device=next(m.parameters()).device).manual_seed(seed)
+    with torch.no_grad():
+        for name, p in m.named_parameters():
+            if name.endswith("bias"):
+                p.zero_()
+            elif p.dim() == 1:
+                p.fill_(1.0)
+            else:
+                fan_in = p[0].numel() if p.dim() > 1 else 1
+                s = std if "embed" in name and p.dim() == 2 and "linear" not in name else 1.0 / math.sqrt(fan_in)
+                p.normal_(0.0, s, generator=g)
+    return m

@@ -101,6 +101,76 @@ def groupnorm_nhwc(x: torch.Tensor, g: torch.Tensor, b: torch.Tensor, groups: in
     return out
 
 
+def layernorm_mod(x: torch.Tensor, scale: torch.Tensor | None, shift: torch.Tensor | None, rows_per_b: int,
+                  out: torch.Tensor, eps: float = 1e-6):
+    """adaLN: out = LN(x) * (1 + scale[b]) + shift[b], b = row // rows_per_b (diffusion.hip).
+    x fp32 [M, H]; scale/shift fp32 [B, >=H] row views (any row stride); out act16 [M, H]."""
+    M, H = x.shape
+    if M == 0:
+        return out
+    if not x.is_cuda:
+        y = F.layer_norm(x, (H,), eps=eps).view(-1, rows_per_b, H)
+        if scale is not None:
+            y = y * (1 + scale[:, None, :H])
+        if shift is not None:
+            y = y + shift[:, None, :H]
+        out.copy_(y.reshape(M, H))
+        return out
+    N.ensure_act(out.dtype)
+    ld = (scale if scale is not None else shift).stride(0) if (scale is not None or shift is not None) else 0
+    if scale is not None and shift is not None and scale.stride(0) != shift.stride(0):
+        raise ValueError("layernorm_mod: scale/shift must share a row stride")
+    N.kcall("mxk_layernorm_mod", x.data_ptr(), x.stride(0), N.ptr(scale), N.ptr(shift), ld, rows_per_b,
+            out.data_ptr(), out.stride(0), M, H, float(eps), N.stream_ptr())
+    return out
+
+
+def gate_add(x: torch.Tensor, y: torch.Tensor, gate: torch.Tensor | None, rows_per_b: int):
+    """x (fp32 [M, H]) += gate[b] * y (act16 [M, H]); gate fp32 [B, >=H] row view or None (= 1)."""
+    M, H = x.shape
+    if M == 0:
+        return x
+    if not x.is_cuda:
+        yy = y.float().view(-1, rows_per_b, H)
+        if gate is not None:
+            yy = yy * gate[:, None, :H]
+        x.add_(yy.reshape(M, H))
+        return x
+    N.ensure_act(y.dtype)
+    N.kcall("mxk_gate_add", x.data_ptr(), x.stride(0), y.data_ptr(), y.stride(0), N.ptr(gate),
+            gate.stride(0) if gate is not None else 0, rows_per_b, M, H, N.stream_ptr())
+    return x
+
+
+_GN_WS: dict = {}
+
+
+def groupnorm16(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, groups: int, eps: float, silu: bool,
+                out: torch.Tensor | None = None) -> torch.Tensor:
+    """GroupNorm (+SiLU) over an NCHW-shaped, channels_last 16-bit tensor (diffusion.hip); CPU: fp32."""
+    n, c, h, w = x.shape
+    if not x.is_cuda:
+        y = F.group_norm(x.float(), groups, gamma, beta, eps)
+        y = F.silu(y) if silu else y
+        y = y.to(x.dtype)
+        if out is not None:
+            out.copy_(y)
+            return out
+        return y
+    if not x.is_contiguous(memory_format=torch.channels_last):
+        x = x.contiguous(memory_format=torch.channels_last)
+    if out is None:
+        out = torch.empty_like(x, memory_format=torch.channels_last)
+    key = (x.device, n * groups)
+    ws = _GN_WS.get(key)
+    if ws is None:
+        ws = _GN_WS[key] = torch.empty(n * groups * 2, dtype=torch.float64, device=x.device)
+    N.ensure_act(x.dtype)
+    N.kcall("mxk_groupnorm16", x.data_ptr(), out.data_ptr(), gamma.data_ptr(), beta.data_ptr(), n, h * w, c, groups,
+            float(eps), int(silu), ws.data_ptr(), N.stream_ptr())
+    return out
+
+
 # ------------------------------------------------------------------------------------------------
 # rotary embeddings
 

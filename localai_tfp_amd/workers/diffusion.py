@@ -1,0 +1,90 @@
+"""Image generation worker: the reference's `stablediffusion-ggml` (sd.cpp, gosd.cpp/gosd.go) and
+`diffusers` backends behind one GenerateImage RPC.
+
+LoadModel: a diffusers-layout SD3 directory, or `synthetic:sd3-medium | sd3-medium-no-t5 | sd3-test`
+(random-init weights). ModelOptions.Options ("key:value", as gosd.cpp:56-162 parses them):
+  sampler:<euler|euler_a|heun|dpm2|dpm++2s_a|dpm++2m|dpm++2mv2|ipndm|ipndm_v|lcm|ddim_trailing|tcd>
+  scheduler:<default|discrete|karras|exponential|ays|gits>
+  cfg_scale:<float>   (ModelOptions.CFGScale also honoured)
+  t5:<true|false>     (drop the T5-XXL encoder; SD3 runs with zero T5 features)
+  strength:<float>    (img2img denoise strength)
+GenerateImage: positive / negative prompt, width, height, step, seed, dst (PNG), src (img2img).
+One image per call; data parallelism = one worker replica per GPU (model config `data_parallel`),
+with the gateway spreading concurrent requests across replicas.
+"""
+from __future__ import annotations
+
+import logging
+import os
+
+from ..grpc import pb
+from ..grpc.server import BackendServicer, worker_main
+
+log = logging.getLogger("localai_tfp_amd.workers.diffusion")
+
+
+class DiffusionServicer(BackendServicer):
+    locking = True  # one generation at a time per GPU (gosd.go SingleThread)
+
+    def __init__(self, device: str | None = None):
+        super().__init__()
+        self.device = device
+        self.pipe = None
+        self.defaults = {}
+
+    def LoadModel(self, request, context):
+        import torch
+        from ..models.diffusion.pipeline import SD3Pipeline
+        try:
+            if self.device is None:
+                self.device = "cuda:0" if torch.cuda.is_available() else "cpu"
+            opts = {}
+            for kv in request.Options:
+                k, _, v = kv.partition(":")
+                opts[k.strip()] = v.strip()
+            use_t5 = opts.get("t5", "true").lower() not in ("0", "false", "no")
+            path = request.ModelFile or request.Model
+            if path.startswith("synthetic:"):
+                name = path.split(":", 1)[1]
+                if not use_t5 and name == "sd3-medium":
+                    name = "sd3-medium-no-t5"
+                self.pipe = SD3Pipeline.synthetic(name, self.device)
+            else:
+                if not os.path.isabs(path) and request.ModelPath:
+                    path = os.path.join(request.ModelPath, path)
+                if not os.path.isdir(path):
+                    raise ValueError(f"{path}: expected a diffusers-layout model directory")
+                self.pipe = SD3Pipeline.from_diffusers(path, self.device, use_t5=use_t5)
+            self.defaults = dict(sampler=opts.get("sampler", "euler"), schedule=opts.get("scheduler", "default"),
+                                 cfg_scale=float(opts.get("cfg_scale", request.CFGScale or 7.0)),
+                                 strength=float(opts.get("strength", 0.75)))
+            return pb.Result(message="loaded", success=True)
+        except Exception as ex:
+            log.exception("LoadModel failed")
+            return pb.Result(message=f"failed to load model: {ex}", success=False)
+
+    def GenerateImage(self, request, context):
+        from ..models.diffusion.pipeline import GenParams, load_image, save_png
+        if self.pipe is None:
+            return pb.Result(message="model not loaded", success=False)
+        try:
+            w = request.width or 512
+            h = request.height or 512
+            gp = GenParams(width=w, height=h, steps=request.step or 20, seed=request.seed,
+                           negative=request.negative_prompt, **self.defaults)
+            gp.extra["clip_skip"] = request.CLIPSkip
+            init = load_image(request.src, w, h) if request.src else None
+            img = self.pipe.generate(request.positive_prompt, gp, init)
+            save_png(img, request.dst)
+            return pb.Result(message="ok", success=True)
+        except Exception as ex:
+            log.exception("GenerateImage failed")
+            return pb.Result(message=f"generation failed: {ex}", success=False)
+
+
+def main(argv=None):
+    worker_main(DiffusionServicer, argv)
+
+
+if __name__ == "__main__":
+    main()
