@@ -1,0 +1,185 @@
+// qgemm32.hip — quantised-weight GEMM on 32x32x16 f16 MFMA tiles for decode / mixed batches
+// (M ~ 64..256), the shape class that dominates continuous-batching decode steps.
+//
+//   C[M, N] (+)= A[M, K] · W[N, K]^T,   A f16 (act16 mode), W in Q4_K / Q6_K(repacked) / Q8_0(repacked)
+//
+// Why 32x32 tiles: with 16x16x32 tiles (qgemm16.hip) one dequantised B fragment (8 weights per lane,
+// ~16 packed-f16 VALU ops) feeds WM 16-cycle MFMAs, and at WM = 4 the dequantisation VALU plus the
+// MFMA-held issue slots exceed the MFMA time (VALU-bound). A 32x32x16 MFMA consumes the same
+// 8 weights per lane for twice the FLOPs (32 cycles), so one fragment feeds WM x 32 cycles of matrix
+// work and the dequantisation hides in the free issue slots; the A operand is read from LDS at half
+// the bytes per FLOP.
+//
+// Virtual-k: lane group h = lane >> 5 owns elements [128h, 128h + 128) of every 256-element
+// super-block (two "quarters" 2h, 2h+1 in the qgemm16 layouts, so the W16 decoders are reused);
+// MFMA k-step ks (0..15) consumes elements 128h + 8ks + j on both operands. A k-block's A tile
+// (BM x 256 f16) is staged once per workgroup into an XOR-swizzled LDS image (16-B chunk c of row r at
+// chunk c ^ (r & 7): the 8 rows a ds_read_b128 lane group touches hit distinct banks) and shared by
+// the 4 waves, which split N (32 columns each). Split-K over grid.y accumulates with fp32 atomics.
+#include "qdeq16.h"
+
+MX_DEV int a32_lds_off(int r, int c) { return r * 512 + ((c ^ (r & 7)) << 4); }
+
+template <int QT, int WM, int EPI>
+__global__ __launch_bounds__(256, 1) void qgemm32_kernel(const uint16_t* __restrict__ A, int lda,
+                                                          const uint8_t* __restrict__ W,
+                                                          const uint16_t* __restrict__ WD, int M, int N, int K,
+                                                          int kb_per_split, void* __restrict__ Cv, int ldc) {
+    constexpr int BM = WM * 32;
+    constexpr int A_BYTES = BM * 512;
+    constexpr int A_PASSES = BM * 32 / 256;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int h = lane >> 5, col = lane & 31;
+    const int nblk = K >> 8;
+    const int n_base = (blockIdx.x * 4 + wave) * 32;
+    const int m_base = blockIdx.z * BM;
+    const int kb0 = blockIdx.y * kb_per_split;
+    const int kb1 = min(kb0 + kb_per_split, nblk);
+    if (kb0 >= kb1) return;
+
+    f32x16 acc[WM];
+#pragma unroll
+    for (int i = 0; i < WM; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
+
+    u32x4 areg[A_PASSES];
+    auto load_a = [&](int kb) {
+#pragma unroll
+        for (int p = 0; p < A_PASSES; ++p) {
+            const int id = p * 256 + threadIdx.x;
+            const int r = id >> 5, c = id & 31;
+            const int m = min(m_base + r, M - 1);  // rows past M compute garbage that is never stored
+            areg[p] = *(const u32x4*)(A + (size_t)m * lda + (size_t)kb * 256 + c * 8);
+        }
+    };
+    auto store_a = [&](int buf) {
+#pragma unroll
+        for (int p = 0; p < A_PASSES; ++p) {
+            const int id = p * 256 + threadIdx.x;
+            *(u32x4*)(smem + buf * A_BYTES + a32_lds_off(id >> 5, id & 31)) = areg[p];
+        }
+    };
+    const int n = n_base + col;
+    const bool nvalid = n < N;
+    W16<QT> wq[2], wn[2];
+    auto load_w = [&](W16<QT>(&f)[2], int kb) {
+        if (nvalid) {
+            f[0].load(W, WD, n, kb, nblk, 2 * h);
+            f[1].load(W, WD, n, kb, nblk, 2 * h + 1);
+        } else {
+            f[0].zero();
+            f[1].zero();
+        }
+    };
+
+    load_a(kb0);
+    load_w(wq, kb0);
+    store_a(0);
+    __syncthreads();
+    int buf = 0;
+    for (int kb = kb0; kb < kb1; ++kb) {
+        const bool more = kb + 1 < kb1;
+        if (more) {
+            load_a(kb + 1);
+            load_w(wn, kb + 1);
+        }
+        wq[0].prep(2 * h);
+        wq[1].prep(2 * h + 1);
+        const char* abuf = smem + buf * A_BYTES;
+#define Q32_KSTEP(KS)                                                                                      \
+    {                                                                                                      \
+        const f16x8 bfr = wq[(KS) >> 3].template frag<(KS) & 7>();                                         \
+        _Pragma("unroll") for (int i = 0; i < WM; ++i) {                                                   \
+            const f16x8 af = *(const f16x8*)(abuf + a32_lds_off(i * 32 + col, 16 * h + (KS)));            \
+            acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af, bfr, acc[i], 0, 0, 0);                     \
+        }                                                                                                  \
+    }
+        Q32_KSTEP(0) Q32_KSTEP(1) Q32_KSTEP(2) Q32_KSTEP(3) Q32_KSTEP(4) Q32_KSTEP(5) Q32_KSTEP(6) Q32_KSTEP(7)
+        Q32_KSTEP(8) Q32_KSTEP(9) Q32_KSTEP(10) Q32_KSTEP(11) Q32_KSTEP(12) Q32_KSTEP(13) Q32_KSTEP(14)
+        Q32_KSTEP(15)
+#undef Q32_KSTEP
+        if (more) {
+            store_a(buf ^ 1);
+            wq[0] = wn[0];
+            wq[1] = wn[1];
+        }
+        __syncthreads();
+        buf ^= 1;
+    }
+
+    // epilogue: 32x32 C/D layout: col = lane & 31, row = 8*(r>>2) + 4*(lane>>5) + (r&3)
+    if constexpr (EPI == E16_SWIGLU) {
+        // W rows interleaved in 16-row groups: tile columns 0..15 gate, 16..31 up of the same features
+#pragma unroll
+        for (int i = 0; i < WM; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float v = acc[i][r];
+                const float up = __shfl_xor(v, 16);
+                const int m = m_base + i * 32 + 8 * (r >> 2) + 4 * h + (r & 3);
+                if (col < 16 && nvalid && m < M)
+                    ((uint16_t*)Cv)[(size_t)m * ldc + (n_base >> 1) + col] = f32_to_act<true>(silu_f(v) * up);
+            }
+        return;
+    }
+    if (!nvalid) return;
+#pragma unroll
+    for (int i = 0; i < WM; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int m = m_base + i * 32 + 8 * (r >> 2) + 4 * h + (r & 3);
+            if (m >= M) continue;
+            const float v = acc[i][r];
+            if constexpr (EPI == E16_F32) ((float*)Cv)[(size_t)m * ldc + n] = v;
+            else if constexpr (EPI == E16_ACT) ((uint16_t*)Cv)[(size_t)m * ldc + n] = f32_to_act<true>(v);
+            else atomicAdd(((float*)Cv) + (size_t)m * ldc + n, v);
+        }
+}
+
+template <int QT, int WM, int EPI>
+static int launch32(const uint16_t* A, int lda, const uint8_t* W, const uint16_t* WD, int M, int N, int K, int splits,
+                    void* C, int ldc, hipStream_t st) {
+    const int nblk = K / 256;
+    const int kbs = (nblk + splits - 1) / splits;
+    dim3 grid((N + 127) / 128, splits, (M + WM * 32 - 1) / (WM * 32));
+    const size_t lds = 2 * WM * 32 * 512;
+    qgemm32_kernel<QT, WM, EPI><<<grid, 256, lds, st>>>(A, lda, W, WD, M, N, K, kbs, C, ldc);
+    MXK_CHECK_LAUNCH();
+}
+
+template <int QT, int EPI>
+static int dispatch32(int wm, const uint16_t* A, int lda, const uint8_t* W, const uint16_t* WD, int M, int N, int K,
+                      int splits, void* C, int ldc, hipStream_t st) {
+    switch (wm) {
+        case 1: return launch32<QT, 1, EPI>(A, lda, W, WD, M, N, K, splits, C, ldc, st);
+        case 2: return launch32<QT, 2, EPI>(A, lda, W, WD, M, N, K, splits, C, ldc, st);
+        case 4: return launch32<QT, 4, EPI>(A, lda, W, WD, M, N, K, splits, C, ldc, st);
+    }
+    return (int)hipErrorInvalidValue;
+}
+
+// A must be f16 (act16 mode f16). epi as mxk_qgemm16: 0 fp32 store, 1 act16 store, 2 fp32 atomic
+// accumulate (split-K allowed), 3 SwiGLU over 16-row interleaved gate/up -> act16.
+extern "C" int mxk_qgemm32(int qtype, int epi, int wm, const uint16_t* A, int lda, const uint8_t* W,
+                           const uint16_t* WD, int M, int N, int K, int splits, void* C, int ldc, hipStream_t st) {
+    if (M <= 0) return 0;
+    if (K % 256 || (lda & 7)) return (int)hipErrorInvalidValue;
+    if (epi != E16_ADD_F32 && splits != 1) return (int)hipErrorInvalidValue;
+    if (epi == E16_SWIGLU && (N & 31)) return (int)hipErrorInvalidValue;
+#define Q32_EPI(QT_)                                                                                       \
+    switch (epi) {                                                                                         \
+        case E16_F32: return dispatch32<QT_, E16_F32>(wm, A, lda, W, WD, M, N, K, splits, C, ldc, st);         \
+        case E16_ACT: return dispatch32<QT_, E16_ACT>(wm, A, lda, W, WD, M, N, K, splits, C, ldc, st);         \
+        case E16_ADD_F32: return dispatch32<QT_, E16_ADD_F32>(wm, A, lda, W, WD, M, N, K, splits, C, ldc, st); \
+        case E16_SWIGLU: return dispatch32<QT_, E16_SWIGLU>(wm, A, lda, W, WD, M, N, K, splits, C, ldc, st);   \
+    }
+    switch (qtype) {
+        case MXQ_Q4_K: Q32_EPI(MXQ_Q4_K) break;
+        case MXQ_Q6_K: Q32_EPI(MXQ_Q6_K) break;
+        case MXQ_Q8_0: Q32_EPI(MXQ_Q8_0) break;
+    }
+#undef Q32_EPI
+    return (int)hipErrorInvalidValue;
+}

@@ -319,6 +319,38 @@ def test_qgemm16(qt, M):
     assert rel(sw, ref_sw) < 1e-2
 
 
+@pytest.mark.parametrize("qt", [QType.Q4_K, QType.Q6_K, QType.Q8_0])
+@pytest.mark.parametrize("M,wm,splits", [(48, 2, 1), (77, 4, 2), (128, 4, 1), (128, 2, 4), (200, 4, 2), (33, 1, 1)])
+def test_qgemm32(qt, M, wm, splits, monkeypatch):
+    """qgemm32.hip (32x32x16 f16 MFMA tiles) for every epilogue and tile / split-K choice."""
+    from localai_tfp_amd.ops import linear as L
+    monkeypatch.setattr(L, "Q32_MIN_M", 1)
+    monkeypatch.setattr(L, "Q32_FORCE", (wm, splits))
+    n, k = 512, 2048
+    raw, dense = make_w(qt, n, k, seed=M + 3 * wm)
+    W = QWeight.from_ggml(raw, qt, n, k, DEV)
+    x = torch.randn(M, k, device=DEV).half()
+    ref = x.float().cpu() @ dense.t()
+    out = torch.empty(M, n, device=DEV)
+    qmatmul(W, x, EPI_F32, out)
+    assert rel(out, ref) < 5e-3
+    z = torch.zeros(M, n, device=DEV)
+    qmatmul(W, x, EPI_F32, z, out_zeroed=True)
+    assert rel(z, ref) < 5e-3
+    acc = torch.randn(M, n, device=DEV)
+    acc0 = acc.clone()
+    qmatmul(W, x, EPI_ADD_F32, acc)
+    assert rel(acc - acc0, ref) < 5e-3
+    ob = torch.empty(M, n, dtype=torch.float16, device=DEV)
+    qmatmul(W, x, EPI_BF16, ob)
+    assert rel(ob, ref) < 5e-3
+    sw = torch.empty(M, n // 2, dtype=torch.float16, device=DEV)
+    qmatmul(W, x, EPI_SWIGLU, sw)
+    g = ref.reshape(M, n // 32, 2, 16)
+    ref_sw = torch.nn.functional.silu(g[:, :, 0].reshape(M, -1)) * g[:, :, 1].reshape(M, -1)
+    assert rel(sw, ref_sw) < 1e-2
+
+
 def test_f16_producers():
     M, H = 7, 4096
     x = torch.randn(M, H, device=DEV) * 3
