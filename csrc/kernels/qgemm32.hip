@@ -20,7 +20,7 @@
 
 MX_DEV int a32_lds_off(int r, int c) { return r * 512 + ((c ^ (r & 7)) << 4); }
 
-template <int QT, int WM, int EPI>
+template <int QT, int WM, int WN, int EPI>
 __global__ __launch_bounds__(256, 1) void qgemm32_kernel(const uint16_t* __restrict__ A, int lda,
                                                           const uint8_t* __restrict__ W,
                                                           const uint16_t* __restrict__ WD, int M, int N, int K,
@@ -32,17 +32,19 @@ __global__ __launch_bounds__(256, 1) void qgemm32_kernel(const uint16_t* __restr
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int h = lane >> 5, col = lane & 31;
     const int nblk = K >> 8;
-    const int n_base = (blockIdx.x * 4 + wave) * 32;
+    const int n_base = (blockIdx.x * 4 + wave) * 32 * WN;
     const int m_base = blockIdx.z * BM;
     const int kb0 = blockIdx.y * kb_per_split;
     const int kb1 = min(kb0 + kb_per_split, nblk);
     if (kb0 >= kb1) return;
 
-    f32x16 acc[WM];
+    f32x16 acc[WM][WN];
 #pragma unroll
     for (int i = 0; i < WM; ++i)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
+        for (int t = 0; t < WN; ++t)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][t][r] = 0.f;
 
     u32x4 areg[A_PASSES];
     auto load_a = [&](int kb) {
@@ -61,16 +63,18 @@ __global__ __launch_bounds__(256, 1) void qgemm32_kernel(const uint16_t* __restr
             *(u32x4*)(smem + buf * A_BYTES + a32_lds_off(id >> 5, id & 31)) = areg[p];
         }
     };
-    const int n = n_base + col;
-    const bool nvalid = n < N;
-    W16<QT> wq[2], wn[2];
-    auto load_w = [&](W16<QT>(&f)[2], int kb) {
-        if (nvalid) {
-            f[0].load(W, WD, n, kb, nblk, 2 * h);
-            f[1].load(W, WD, n, kb, nblk, 2 * h + 1);
-        } else {
-            f[0].zero();
-            f[1].zero();
+    W16<QT> wq[WN][2], wn[WN][2];
+    auto load_w = [&](W16<QT>(&f)[WN][2], int kb) {
+#pragma unroll
+        for (int t = 0; t < WN; ++t) {
+            const int n = n_base + 32 * t + col;
+            if (n < N) {
+                f[t][0].load(W, WD, n, kb, nblk, 2 * h);
+                f[t][1].load(W, WD, n, kb, nblk, 2 * h + 1);
+            } else {
+                f[t][0].zero();
+                f[t][1].zero();
+            }
         }
     };
 
@@ -85,15 +89,20 @@ __global__ __launch_bounds__(256, 1) void qgemm32_kernel(const uint16_t* __restr
             load_a(kb + 1);
             load_w(wn, kb + 1);
         }
-        wq[0].prep(2 * h);
-        wq[1].prep(2 * h + 1);
+#pragma unroll
+        for (int t = 0; t < WN; ++t) {
+            wq[t][0].prep(2 * h);
+            wq[t][1].prep(2 * h + 1);
+        }
         const char* abuf = smem + buf * A_BYTES;
 #define Q32_KSTEP(KS)                                                                                      \
     {                                                                                                      \
-        const f16x8 bfr = wq[(KS) >> 3].template frag<(KS) & 7>();                                         \
+        f16x8 bfr[WN];                                                                                     \
+        _Pragma("unroll") for (int t = 0; t < WN; ++t) bfr[t] = wq[t][(KS) >> 3].template frag<(KS) & 7>(); \
         _Pragma("unroll") for (int i = 0; i < WM; ++i) {                                                   \
             const f16x8 af = *(const f16x8*)(abuf + a32_lds_off(i * 32 + col, 16 * h + (KS)));            \
-            acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af, bfr, acc[i], 0, 0, 0);                     \
+            _Pragma("unroll") for (int t = 0; t < WN; ++t) acc[i][t] =                                     \
+                __builtin_amdgcn_mfma_f32_32x32x16_f16(af, bfr[t], acc[i][t], 0, 0, 0);                    \
         }                                                                                                  \
     }
         Q32_KSTEP(0) Q32_KSTEP(1) Q32_KSTEP(2) Q32_KSTEP(3) Q32_KSTEP(4) Q32_KSTEP(5) Q32_KSTEP(6) Q32_KSTEP(7)
@@ -102,67 +111,75 @@ __global__ __launch_bounds__(256, 1) void qgemm32_kernel(const uint16_t* __restr
 #undef Q32_KSTEP
         if (more) {
             store_a(buf ^ 1);
-            wq[0] = wn[0];
-            wq[1] = wn[1];
+#pragma unroll
+            for (int t = 0; t < WN; ++t) {
+                wq[t][0] = wn[t][0];
+                wq[t][1] = wn[t][1];
+            }
         }
         __syncthreads();
         buf ^= 1;
     }
 
     // epilogue: 32x32 C/D layout: col = lane & 31, row = 8*(r>>2) + 4*(lane>>5) + (r&3)
-    if constexpr (EPI == E16_SWIGLU) {
-        // W rows interleaved in 16-row groups: tile columns 0..15 gate, 16..31 up of the same features
+#pragma unroll
+    for (int t = 0; t < WN; ++t) {
+        const int nt = n_base + 32 * t;
+        const int n = nt + col;
+        if constexpr (EPI == E16_SWIGLU) {
+            // W rows interleaved in 16-row groups: tile columns 0..15 gate, 16..31 up of the same features
+#pragma unroll
+            for (int i = 0; i < WM; ++i)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const float v = acc[i][t][r];
+                    const float up = __shfl_xor(v, 16);
+                    const int m = m_base + i * 32 + 8 * (r >> 2) + 4 * h + (r & 3);
+                    if (col < 16 && n < N && m < M)
+                        ((uint16_t*)Cv)[(size_t)m * ldc + (nt >> 1) + col] = f32_to_act<true>(silu_f(v) * up);
+                }
+            continue;
+        }
+        if (n >= N) continue;
 #pragma unroll
         for (int i = 0; i < WM; ++i)
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                const float v = acc[i][r];
-                const float up = __shfl_xor(v, 16);
                 const int m = m_base + i * 32 + 8 * (r >> 2) + 4 * h + (r & 3);
-                if (col < 16 && nvalid && m < M)
-                    ((uint16_t*)Cv)[(size_t)m * ldc + (n_base >> 1) + col] = f32_to_act<true>(silu_f(v) * up);
+                if (m >= M) continue;
+                const float v = acc[i][t][r];
+                if constexpr (EPI == E16_F32) ((float*)Cv)[(size_t)m * ldc + n] = v;
+                else if constexpr (EPI == E16_ACT) ((uint16_t*)Cv)[(size_t)m * ldc + n] = f32_to_act<true>(v);
+                else atomicAdd(((float*)Cv) + (size_t)m * ldc + n, v);
             }
-        return;
     }
-    if (!nvalid) return;
-#pragma unroll
-    for (int i = 0; i < WM; ++i)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int m = m_base + i * 32 + 8 * (r >> 2) + 4 * h + (r & 3);
-            if (m >= M) continue;
-            const float v = acc[i][r];
-            if constexpr (EPI == E16_F32) ((float*)Cv)[(size_t)m * ldc + n] = v;
-            else if constexpr (EPI == E16_ACT) ((uint16_t*)Cv)[(size_t)m * ldc + n] = f32_to_act<true>(v);
-            else atomicAdd(((float*)Cv) + (size_t)m * ldc + n, v);
-        }
 }
 
-template <int QT, int WM, int EPI>
+template <int QT, int WM, int WN, int EPI>
 static int launch32(const uint16_t* A, int lda, const uint8_t* W, const uint16_t* WD, int M, int N, int K, int splits,
                     void* C, int ldc, hipStream_t st) {
     const int nblk = K / 256;
     const int kbs = (nblk + splits - 1) / splits;
-    dim3 grid((N + 127) / 128, splits, (M + WM * 32 - 1) / (WM * 32));
+    dim3 grid((N + 128 * WN - 1) / (128 * WN), splits, (M + WM * 32 - 1) / (WM * 32));
     const size_t lds = 2 * WM * 32 * 512;
-    qgemm32_kernel<QT, WM, EPI><<<grid, 256, lds, st>>>(A, lda, W, WD, M, N, K, kbs, C, ldc);
+    qgemm32_kernel<QT, WM, WN, EPI><<<grid, 256, lds, st>>>(A, lda, W, WD, M, N, K, kbs, C, ldc);
     MXK_CHECK_LAUNCH();
 }
 
 template <int QT, int EPI>
-static int dispatch32(int wm, const uint16_t* A, int lda, const uint8_t* W, const uint16_t* WD, int M, int N, int K,
-                      int splits, void* C, int ldc, hipStream_t st) {
-    switch (wm) {
-        case 1: return launch32<QT, 1, EPI>(A, lda, W, WD, M, N, K, splits, C, ldc, st);
-        case 2: return launch32<QT, 2, EPI>(A, lda, W, WD, M, N, K, splits, C, ldc, st);
-        case 4: return launch32<QT, 4, EPI>(A, lda, W, WD, M, N, K, splits, C, ldc, st);
-    }
+static int dispatch32(int wm, int wn, const uint16_t* A, int lda, const uint8_t* W, const uint16_t* WD, int M,
+                      int N, int K, int splits, void* C, int ldc, hipStream_t st) {
+    if (QT != MXQ_Q4_K && wm * wn > 4) wn = 1;  // Q6_K / Q8_0 fragments need more registers (spills)
+#define Q32_CASE(WM_, WN_) \
+    if (wm == WM_ && wn == WN_) return launch32<QT, WM_, WN_, EPI>(A, lda, W, WD, M, N, K, splits, C, ldc, st);
+    Q32_CASE(1, 1) Q32_CASE(2, 1) Q32_CASE(4, 1) Q32_CASE(1, 2) Q32_CASE(2, 2) Q32_CASE(4, 2)
+#undef Q32_CASE
     return (int)hipErrorInvalidValue;
 }
 
 // A must be f16 (act16 mode f16). epi as mxk_qgemm16: 0 fp32 store, 1 act16 store, 2 fp32 atomic
 // accumulate (split-K allowed), 3 SwiGLU over 16-row interleaved gate/up -> act16.
-extern "C" int mxk_qgemm32(int qtype, int epi, int wm, const uint16_t* A, int lda, const uint8_t* W,
+extern "C" int mxk_qgemm32(int qtype, int epi, int wm, int wn, const uint16_t* A, int lda, const uint8_t* W,
                            const uint16_t* WD, int M, int N, int K, int splits, void* C, int ldc, hipStream_t st) {
     if (M <= 0) return 0;
     if (K % 256 || (lda & 7)) return (int)hipErrorInvalidValue;
@@ -170,10 +187,10 @@ extern "C" int mxk_qgemm32(int qtype, int epi, int wm, const uint16_t* A, int ld
     if (epi == E16_SWIGLU && (N & 31)) return (int)hipErrorInvalidValue;
 #define Q32_EPI(QT_)                                                                                       \
     switch (epi) {                                                                                         \
-        case E16_F32: return dispatch32<QT_, E16_F32>(wm, A, lda, W, WD, M, N, K, splits, C, ldc, st);         \
-        case E16_ACT: return dispatch32<QT_, E16_ACT>(wm, A, lda, W, WD, M, N, K, splits, C, ldc, st);         \
-        case E16_ADD_F32: return dispatch32<QT_, E16_ADD_F32>(wm, A, lda, W, WD, M, N, K, splits, C, ldc, st); \
-        case E16_SWIGLU: return dispatch32<QT_, E16_SWIGLU>(wm, A, lda, W, WD, M, N, K, splits, C, ldc, st);   \
+        case E16_F32: return dispatch32<QT_, E16_F32>(wm, wn, A, lda, W, WD, M, N, K, splits, C, ldc, st);         \
+        case E16_ACT: return dispatch32<QT_, E16_ACT>(wm, wn, A, lda, W, WD, M, N, K, splits, C, ldc, st);         \
+        case E16_ADD_F32: return dispatch32<QT_, E16_ADD_F32>(wm, wn, A, lda, W, WD, M, N, K, splits, C, ldc, st); \
+        case E16_SWIGLU: return dispatch32<QT_, E16_SWIGLU>(wm, wn, A, lda, W, WD, M, N, K, splits, C, ldc, st);   \
     }
     switch (qtype) {
         case MXQ_Q4_K: Q32_EPI(MXQ_Q4_K) break;

@@ -34,7 +34,7 @@ KERNEL_SIGS = {
     "mxk_groupnorm16": [P, P, P, P, I, I, I, I, F, I, P, P],
     "mxk_qgemm_mfma": [I, I, I, I, P, I, P, P, I, I, I, I, P, I, P],
     "mxk_qgemm16": [I, I, I, I, P, I, P, P, I, I, I, I, P, I, P],
-    "mxk_qgemm32": [I, I, I, P, I, P, P, I, I, I, I, P, I, P],
+    "mxk_qgemm32": [I, I, I, I, P, I, P, P, I, I, I, I, P, I, P],
     "mxk_set_act_f16": [I],
     "mxk_attn_dense": [P, I, P, I, P, I, P, I, I, I, I, I, I, I, P, P, I, F, I, P],
     "mxk_get_act_f16": [],

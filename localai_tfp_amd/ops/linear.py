@@ -222,13 +222,13 @@ def qmatmul(W: QWeight, x: torch.Tensor | None, epi: int, out: torch.Tensor, *, 
     nblk = W.K // 256
     f16 = x.dtype == torch.float16
     if f16 and M >= Q32_MIN_M:
-        wm, splits = _mfma32_shape(M, W.N, nblk, can_split)
+        wm, wn, splits = _mfma32_shape(M, W.N, nblk, can_split)
         e = EPI_ADD_F32 if (epi == EPI_F32 and splits > 1) else epi
         if e in (EPI_BF16, EPI_SWIGLU) and out.dtype != x.dtype:
             raise ValueError(f"qmatmul: {out.dtype} output with {x.dtype} activations")
         if e in (EPI_BF16, EPI_SWIGLU):
             N.ensure_act(out.dtype)
-        N.kcall("mxk_qgemm32", int(W.qtype), e, wm, x.data_ptr(), x.stride(0), W.data.data_ptr(), N.ptr(W.dplane),
+        N.kcall("mxk_qgemm32", int(W.qtype), e, wm, wn, x.data_ptr(), x.stride(0), W.data.data_ptr(), N.ptr(W.dplane),
                 M, W.N, W.K, splits, out.data_ptr(), out.stride(0), N.stream_ptr())
         return out
     wm, wn, splits = (_mfma16_shape if f16 else _mfma_shape)(M, W.N, nblk, can_split, int(W.qtype))
@@ -260,23 +260,24 @@ def dense_min_m(dtype, epi: int = EPI_ADD_F32, can_split: bool = True) -> int:
 
 
 Q32_MIN_M = int(os.environ.get("MX_Q32_MIN_M", "48"))
-Q32_FORCE: tuple | None = None  # (wm, splits) override for tuning (tools/tune_qgemm32.py)
+Q32_FORCE: tuple | None = None  # (wm, wn, splits) override for tuning (tools/tune_qgemm32.py)
 
 
 def _mfma32_shape(M: int, N_: int, nblk: int, can_split: bool):
     """qgemm32 tile / split-K choice: 32*wm-row tiles, 128 columns per workgroup, K splits (fp32
     atomics) only for split-able outputs until the grid covers the CUs."""
     if Q32_FORCE is not None:
-        wm, splits = Q32_FORCE
-        return wm, (splits if can_split else 1)
+        wm, wn, splits = Q32_FORCE
+        return wm, wn, (splits if can_split else 1)
     wm = 1 if M <= 32 else 2 if M <= 64 else 4
-    cols = -(-N_ // 128)
+    wn = 2 if N_ >= 8192 else 1
+    cols = -(-N_ // (128 * wn))
     mt = -(-M // (32 * wm))
     splits = 1
     if can_split:
         while cols * mt * splits < CU_COUNT and splits * 2 <= max(1, nblk // 4):
             splits *= 2
-    return wm, splits
+    return wm, wn, splits
 
 
 def _mfma16_shape(M: int, N_: int, nblk: int, can_split: bool, qtype: int):

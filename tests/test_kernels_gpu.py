@@ -320,12 +320,13 @@ def test_qgemm16(qt, M):
 
 
 @pytest.mark.parametrize("qt", [QType.Q4_K, QType.Q6_K, QType.Q8_0])
-@pytest.mark.parametrize("M,wm,splits", [(48, 2, 1), (77, 4, 2), (128, 4, 1), (128, 2, 4), (200, 4, 2), (33, 1, 1)])
-def test_qgemm32(qt, M, wm, splits, monkeypatch):
+@pytest.mark.parametrize("M,wm,wn,splits", [(48, 2, 1, 1), (77, 4, 2, 2), (128, 4, 1, 1), (128, 2, 2, 4),
+                                             (200, 4, 2, 2), (33, 1, 1, 1)])
+def test_qgemm32(qt, M, wm, wn, splits, monkeypatch):
     """qgemm32.hip (32x32x16 f16 MFMA tiles) for every epilogue and tile / split-K choice."""
     from localai_tfp_amd.ops import linear as L
     monkeypatch.setattr(L, "Q32_MIN_M", 1)
-    monkeypatch.setattr(L, "Q32_FORCE", (wm, splits))
+    monkeypatch.setattr(L, "Q32_FORCE", (wm, wn, splits))
     n, k = 512, 2048
     raw, dense = make_w(qt, n, k, seed=M + 3 * wm)
     W = QWeight.from_ggml(raw, qt, n, k, DEV)

@@ -54,15 +54,16 @@ def main():
             res["q16_us"] = round(bench(lambda: L.qmatmul(W, x, epi, out, out_zeroed=True)), 2)
             L.Q32_MIN_M = 1
             best = None
-            for wm in (1, 2, 4):
-                for sp in (1, 2, 4, 8):
-                    L.Q32_FORCE = (wm, sp)
-                    us = bench(lambda: L.qmatmul(W, x, epi, out, out_zeroed=True))
-                    if best is None or us < best[0]:
-                        best = (us, wm, sp)
+            for wm in (2, 4):
+                for wn in (1, 2):
+                    for sp in ((1, 2, 4, 8) if epi in (L.EPI_F32, L.EPI_ADD_F32) else (1,)):
+                        L.Q32_FORCE = (wm, wn, sp)
+                        us = bench(lambda: L.qmatmul(W, x, epi, out, out_zeroed=True))
+                        if best is None or us < best[0]:
+                            best = (us, wm, sp, wn)
             L.Q32_FORCE = None
             res["q32_auto_us"] = round(bench(lambda: L.qmatmul(W, x, epi, out, out_zeroed=True)), 2)
-            res["q32_best_us"], res["q32_wm"], res["q32_splits"] = round(best[0], 2), best[1], best[2]
+            res["q32_best_us"], res["q32_wm"], res["q32_splits"], res["q32_wn"] = round(best[0], 2), best[1], best[2], best[3]
             W.bf16_cache = cache
             L.BF16_CACHE_MIN_M = 1
             res["dense_us"] = round(bench(lambda: L.qmatmul(W, x, epi, out, out_zeroed=True)), 2)
