@@ -27,7 +27,6 @@ __global__ __launch_bounds__(256, 1) void qgemm32_kernel(const uint16_t* __restr
                                                           int kb_per_split, void* __restrict__ Cv, int ldc) {
     constexpr int BM = WM * 32;
     constexpr int A_BYTES = BM * 512;
-    constexpr int A_PASSES = BM * 32 / 256;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int h = lane >> 5, col = lane & 31;
@@ -46,21 +45,19 @@ __global__ __launch_bounds__(256, 1) void qgemm32_kernel(const uint16_t* __restr
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][t][r] = 0.f;
 
-    u32x4 areg[A_PASSES];
-    auto load_a = [&](int kb) {
+    // A staging: global -> LDS directly (global_load_lds, 16 B per lane). The LDS image is lane-linear
+    // per wave-instruction, so the XOR swizzle is applied to the SOURCE address: LDS chunk p (row
+    // p / 32, physical chunk p % 32) receives logical chunk (p % 32) ^ (row & 7).
+    constexpr int G_PER_WAVE = BM / 8;  // 1 KB wave-instructions per wave per k-block
+    auto stage_a = [&](int kb, int buf) {
+        char* base = smem + buf * A_BYTES + wave * G_PER_WAVE * 1024;
 #pragma unroll
-        for (int p = 0; p < A_PASSES; ++p) {
-            const int id = p * 256 + threadIdx.x;
-            const int r = id >> 5, c = id & 31;
+        for (int j = 0; j < G_PER_WAVE; ++j) {
+            const int p = (wave * G_PER_WAVE + j) * 64 + lane;
+            const int r = p >> 5, c = (p & 31) ^ (r & 7);
             const int m = min(m_base + r, M - 1);  // rows past M compute garbage that is never stored
-            areg[p] = *(const u32x4*)(A + (size_t)m * lda + (size_t)kb * 256 + c * 8);
-        }
-    };
-    auto store_a = [&](int buf) {
-#pragma unroll
-        for (int p = 0; p < A_PASSES; ++p) {
-            const int id = p * 256 + threadIdx.x;
-            *(u32x4*)(smem + buf * A_BYTES + a32_lds_off(id >> 5, id & 31)) = areg[p];
+            __builtin_amdgcn_global_load_lds((const void*)(A + (size_t)m * lda + (size_t)kb * 256 + c * 8),
+                                             (__attribute__((address_space(3))) void*)(base + j * 1024), 16, 0, 0);
         }
     };
     W16<QT> wq[WN][2], wn[WN][2];
@@ -78,47 +75,50 @@ __global__ __launch_bounds__(256, 1) void qgemm32_kernel(const uint16_t* __restr
         }
     };
 
-    load_a(kb0);
-    load_w(wq, kb0);
-    store_a(0);
-    __syncthreads();
-    int buf = 0;
-    for (int kb = kb0; kb < kb1; ++kb) {
+    // k-block body; the two W register sets swap roles statically (loop unrolled by 2) so no
+    // register copy ties the next block's loads to the middle of this block's compute.
+    auto body = [&](W16<QT>(&cur)[WN][2], W16<QT>(&nxt)[WN][2], int kb, int buf) {
         const bool more = kb + 1 < kb1;
         if (more) {
-            load_a(kb + 1);
-            load_w(wn, kb + 1);
+            stage_a(kb + 1, buf ^ 1);
+            load_w(nxt, kb + 1);
         }
 #pragma unroll
         for (int t = 0; t < WN; ++t) {
-            wq[t][0].prep(2 * h);
-            wq[t][1].prep(2 * h + 1);
+            cur[t][0].prep(2 * h);
+            cur[t][1].prep(2 * h + 1);
         }
         const char* abuf = smem + buf * A_BYTES;
-#define Q32_KSTEP(KS)                                                                                      \
-    {                                                                                                      \
-        f16x8 bfr[WN];                                                                                     \
-        _Pragma("unroll") for (int t = 0; t < WN; ++t) bfr[t] = wq[t][(KS) >> 3].template frag<(KS) & 7>(); \
-        _Pragma("unroll") for (int i = 0; i < WM; ++i) {                                                   \
-            const f16x8 af = *(const f16x8*)(abuf + a32_lds_off(i * 32 + col, 16 * h + (KS)));            \
-            _Pragma("unroll") for (int t = 0; t < WN; ++t) acc[i][t] =                                     \
-                __builtin_amdgcn_mfma_f32_32x32x16_f16(af, bfr[t], acc[i][t], 0, 0, 0);                    \
-        }                                                                                                  \
-    }
-        Q32_KSTEP(0) Q32_KSTEP(1) Q32_KSTEP(2) Q32_KSTEP(3) Q32_KSTEP(4) Q32_KSTEP(5) Q32_KSTEP(6) Q32_KSTEP(7)
-        Q32_KSTEP(8) Q32_KSTEP(9) Q32_KSTEP(10) Q32_KSTEP(11) Q32_KSTEP(12) Q32_KSTEP(13) Q32_KSTEP(14)
-        Q32_KSTEP(15)
-#undef Q32_KSTEP
-        if (more) {
-            store_a(buf ^ 1);
+        // A fragments double-buffered in registers: the reads for step ks+1 are in flight while
+        // step ks's MFMAs run (otherwise every MFMA waits a full LDS latency).
+        f16x8 af0[WM], af1[WM];
 #pragma unroll
-            for (int t = 0; t < WN; ++t) {
-                wq[t][0] = wn[t][0];
-                wq[t][1] = wn[t][1];
-            }
-        }
-        __syncthreads();
-        buf ^= 1;
+        for (int i = 0; i < WM; ++i) af0[i] = *(const f16x8*)(abuf + a32_lds_off(i * 32 + col, 16 * h));
+#define Q32_KSTEP(KS, CUR, NXT)                                                                            \
+    {                                                                                                      \
+        if ((KS) < 15) {                                                                                   \
+            _Pragma("unroll") for (int i = 0; i < WM; ++i) NXT[i] =                                        \
+                *(const f16x8*)(abuf + a32_lds_off(i * 32 + col, 16 * h + (KS) + 1));                     \
+        }                                                                                                  \
+        f16x8 bfr[WN];                                                                                     \
+        _Pragma("unroll") for (int t = 0; t < WN; ++t) bfr[t] = cur[t][(KS) >> 3].template frag<(KS) & 7>(); \
+        _Pragma("unroll") for (int i = 0; i < WM; ++i)                                                     \
+            _Pragma("unroll") for (int t = 0; t < WN; ++t) acc[i][t] =                                     \
+                __builtin_amdgcn_mfma_f32_32x32x16_f16(CUR[i], bfr[t], acc[i][t], 0, 0, 0);                \
+    }
+        Q32_KSTEP(0, af0, af1) Q32_KSTEP(1, af1, af0) Q32_KSTEP(2, af0, af1) Q32_KSTEP(3, af1, af0)
+        Q32_KSTEP(4, af0, af1) Q32_KSTEP(5, af1, af0) Q32_KSTEP(6, af0, af1) Q32_KSTEP(7, af1, af0)
+        Q32_KSTEP(8, af0, af1) Q32_KSTEP(9, af1, af0) Q32_KSTEP(10, af0, af1) Q32_KSTEP(11, af1, af0)
+        Q32_KSTEP(12, af0, af1) Q32_KSTEP(13, af1, af0) Q32_KSTEP(14, af0, af1) Q32_KSTEP(15, af1, af0)
+#undef Q32_KSTEP
+        __syncthreads();  // drains the k+1 global_load_lds / W loads (vmcnt(0)) and orders LDS reuse
+    };
+    stage_a(kb0, 0);
+    load_w(wq, kb0);
+    __syncthreads();
+    for (int kb = kb0; kb < kb1; kb += 2) {
+        body(wq, wn, kb, 0);
+        if (kb + 1 < kb1) body(wn, wq, kb + 1, 1);
     }
 
     // epilogue: 32x32 C/D layout: col = lane & 31, row = 8*(r>>2) + 4*(lane>>5) + (r&3)
@@ -162,7 +162,8 @@ static int launch32(const uint16_t* A, int lda, const uint8_t* W, const uint16_t
     const int kbs = (nblk + splits - 1) / splits;
     dim3 grid((N + 128 * WN - 1) / (128 * WN), splits, (M + WM * 32 - 1) / (WM * 32));
     const size_t lds = 2 * WM * 32 * 512;
-    qgemm32_kernel<QT, WM, WN, EPI><<<grid, 256, lds, st>>>(A, lda, W, WD, M, N, K, kbs, C, ldc);
+    if constexpr (QT != MXQ_Q4_K && WM * WN > 4) return (int)hipErrorInvalidValue;  // register-bound
+    else qgemm32_kernel<QT, WM, WN, EPI><<<grid, 256, lds, st>>>(A, lda, W, WD, M, N, K, kbs, C, ldc);
     MXK_CHECK_LAUNCH();
 }
 
