@@ -60,7 +60,8 @@ __global__ __launch_bounds__(256, 1) void qgemm32_kernel(const uint16_t* __restr
                                              (__attribute__((address_space(3))) void*)(base + j * 1024), 16, 0, 0);
         }
     };
-    W16<QT> wq[WN][2], wn[WN][2];
+    constexpr int WPF = 2;
+    W16<QT> w0[WN][2], w1[WN][2], w2[WN][2];
     auto load_w = [&](W16<QT>(&f)[WN][2], int kb) {
 #pragma unroll
         for (int t = 0; t < WN; ++t) {
@@ -78,11 +79,8 @@ __global__ __launch_bounds__(256, 1) void qgemm32_kernel(const uint16_t* __restr
     // k-block body; the two W register sets swap roles statically (loop unrolled by 2) so no
     // register copy ties the next block's loads to the middle of this block's compute.
     auto body = [&](W16<QT>(&cur)[WN][2], W16<QT>(&nxt)[WN][2], int kb, int buf) {
-        const bool more = kb + 1 < kb1;
-        if (more) {
-            stage_a(kb + 1, buf ^ 1);
-            load_w(nxt, kb + 1);
-        }
+        if (kb + 1 < kb1) stage_a(kb + 1, buf ^ 1);
+        if (kb + WPF < kb1) load_w(nxt, kb + WPF);  // W register ring: WPF blocks ahead
 #pragma unroll
         for (int t = 0; t < WN; ++t) {
             cur[t][0].prep(2 * h);
@@ -114,11 +112,15 @@ __global__ __launch_bounds__(256, 1) void qgemm32_kernel(const uint16_t* __restr
         __syncthreads();  // drains the k+1 global_load_lds / W loads (vmcnt(0)) and orders LDS reuse
     };
     stage_a(kb0, 0);
-    load_w(wq, kb0);
+    load_w(w0, kb0);
+    if (kb0 + 1 < kb1) load_w(w1, kb0 + 1);
     __syncthreads();
-    for (int kb = kb0; kb < kb1; kb += 2) {
-        body(wq, wn, kb, 0);
-        if (kb + 1 < kb1) body(wn, wq, kb + 1, 1);
+    // the three W register sets rotate statically (loop unrolled x3): block kb computes from one set
+    // while the loads of kb+1 (issued a block earlier) and kb+2 (issued now) are in flight
+    for (int kb = kb0; kb < kb1; kb += 3) {
+        body(w0, w2, kb, (kb - kb0) & 1);
+        if (kb + 1 < kb1) body(w1, w0, kb + 1, (kb + 1 - kb0) & 1);
+        if (kb + 2 < kb1) body(w2, w1, kb + 2, (kb + 2 - kb0) & 1);
     }
 
     // epilogue: 32x32 C/D layout: col = lane & 31, row = 8*(r>>2) + 4*(lane>>5) + (r&3)

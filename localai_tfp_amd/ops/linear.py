@@ -270,7 +270,7 @@ def _mfma32_shape(M: int, N_: int, nblk: int, can_split: bool):
         wm, wn, splits = Q32_FORCE
         return wm, wn, (splits if can_split else 1)
     wm = 1 if M <= 32 else 2 if M <= 64 else 4
-    wn = 2 if N_ >= 8192 else 1
+    wn = 1
     cols = -(-N_ // (128 * wn))
     mt = -(-M // (32 * wm))
     splits = 1
