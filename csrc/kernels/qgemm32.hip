@@ -18,7 +18,7 @@
 // the 4 waves, which split N (32 columns each). Split-K over grid.y accumulates with fp32 atomics.
 #include "qdeq16.h"
 
-MX_DEV int a32_lds_off(int r, int c) { return r * 512 + ((c ^ (r & 7)) << 4); }
+MX_DEV int a32_lds_off(int r, int c) { return r * 512 + ((c ^ (r & 15)) << 4); }
 
 template <int QT, int WM, int WN, int EPI>
 __global__ __launch_bounds__(256, 1) void qgemm32_kernel(const uint16_t* __restrict__ A, int lda,
@@ -54,7 +54,7 @@ __global__ __launch_bounds__(256, 1) void qgemm32_kernel(const uint16_t* __restr
 #pragma unroll
         for (int j = 0; j < G_PER_WAVE; ++j) {
             const int p = (wave * G_PER_WAVE + j) * 64 + lane;
-            const int r = p >> 5, c = (p & 31) ^ (r & 7);
+            const int r = p >> 5, c = (p & 31) ^ (r & 15);
             const int m = min(m_base + r, M - 1);  // rows past M compute garbage that is never stored
             __builtin_amdgcn_global_load_lds((const void*)(A + (size_t)m * lda + (size_t)kb * 256 + c * 8),
                                              (__attribute__((address_space(3))) void*)(base + j * 1024), 16, 0, 0);
