@@ -49,19 +49,24 @@ __global__ __launch_bounds__(256, 1) void qgemm32_kernel(const uint16_t* __restr
     // per wave-instruction, so the XOR swizzle is applied to the SOURCE address: LDS chunk p (row
     // p / 32, physical chunk p % 32) receives logical chunk (p % 32) ^ (row & 7).
     constexpr int G_PER_WAVE = BM / 8;  // 1 KB wave-instructions per wave per k-block
+    uint32_t aoff[G_PER_WAVE];          // per-lane source element offsets (k-block 0), computed once
+#pragma unroll
+    for (int j = 0; j < G_PER_WAVE; ++j) {
+        const int p = (wave * G_PER_WAVE + j) * 64 + lane;
+        const int r = p >> 5, c = (p & 31) ^ (r & 15);
+        const int m = min(m_base + r, M - 1);  // rows past M compute garbage that is never stored
+        aoff[j] = (uint32_t)(m * lda + c * 8);
+    }
     auto stage_a = [&](int kb, int buf) {
         char* base = smem + buf * A_BYTES + wave * G_PER_WAVE * 1024;
+        const uint16_t* ak = A + (size_t)kb * 256;
 #pragma unroll
-        for (int j = 0; j < G_PER_WAVE; ++j) {
-            const int p = (wave * G_PER_WAVE + j) * 64 + lane;
-            const int r = p >> 5, c = (p & 31) ^ (r & 15);
-            const int m = min(m_base + r, M - 1);  // rows past M compute garbage that is never stored
-            __builtin_amdgcn_global_load_lds((const void*)(A + (size_t)m * lda + (size_t)kb * 256 + c * 8),
+        for (int j = 0; j < G_PER_WAVE; ++j)
+            __builtin_amdgcn_global_load_lds((const void*)(ak + aoff[j]),
                                              (__attribute__((address_space(3))) void*)(base + j * 1024), 16, 0, 0);
-        }
     };
-    constexpr int WPF = 2;
-    W16<QT> w0[WN][2], w1[WN][2], w2[WN][2];
+    constexpr int WPF = 1;
+    W16<QT> w0[WN][2], w1[WN][2];
     auto load_w = [&](W16<QT>(&f)[WN][2], int kb) {
 #pragma unroll
         for (int t = 0; t < WN; ++t) {
@@ -113,14 +118,19 @@ __global__ __launch_bounds__(256, 1) void qgemm32_kernel(const uint16_t* __restr
     };
     stage_a(kb0, 0);
     load_w(w0, kb0);
-    if (kb0 + 1 < kb1) load_w(w1, kb0 + 1);
     __syncthreads();
-    // the three W register sets rotate statically (loop unrolled x3): block kb computes from one set
-    // while the loads of kb+1 (issued a block earlier) and kb+2 (issued now) are in flight
-    for (int kb = kb0; kb < kb1; kb += 3) {
-        body(w0, w2, kb, (kb - kb0) & 1);
-        if (kb + 1 < kb1) body(w1, w0, kb + 1, (kb + 1 - kb0) & 1);
-        if (kb + 2 < kb1) body(w2, w1, kb + 2, (kb + 2 - kb0) & 1);
+    int buf = 0;
+    for (int kb = kb0; kb < kb1; ++kb) {
+        body(w0, w1, kb, buf);
+        // keep the register hand-over after the block's MFMAs: hoisted, it would wait (vmcnt) for the
+        // next block's loads in the middle of this block's compute
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int t = 0; t < WN; ++t) {
+            w0[t][0] = w1[t][0];
+            w0[t][1] = w1[t][1];
+        }
+        buf ^= 1;
     }
 
     // epilogue: 32x32 C/D layout: col = lane & 31, row = 8*(r>>2) + 4*(lane>>5) + (r&3)
