@@ -21,7 +21,7 @@
 MX_DEV int a32_lds_off(int r, int c) { return r * 512 + ((c ^ (r & 15)) << 4); }
 
 template <int QT, int WM, int WN, int EPI>
-__global__ __launch_bounds__(256, 1) void qgemm32_kernel(const uint16_t* __restrict__ A, int lda,
+__global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) void qgemm32_kernel(const uint16_t* __restrict__ A, int lda,
                                                           const uint8_t* __restrict__ W,
                                                           const uint16_t* __restrict__ WD, int M, int N, int K,
                                                           int kb_per_split, void* __restrict__ Cv, int ldc) {
@@ -92,27 +92,39 @@ __global__ __launch_bounds__(256, 1) void qgemm32_kernel(const uint16_t* __restr
             cur[t][1].prep(2 * h + 1);
         }
         const char* abuf = smem + buf * A_BYTES;
-        // A fragments double-buffered in registers: the reads for step ks+1 are in flight while
-        // step ks's MFMAs run (otherwise every MFMA waits a full LDS latency).
-        f16x8 af0[WM], af1[WM];
+        // Software pipeline over the 16 k-steps: step ks issues the LDS reads of A(ks+1) and the
+        // dequantisation of B(ks+1) between its own WM x WN MFMAs (sched_group_barrier pins the
+        // interleave; left alone the scheduler sinks the reads next to their use and every MFMA
+        // waits a full LDS latency).
+        f16x8 a0[WM], a1[WM], b0[WN], b1[WN];
 #pragma unroll
-        for (int i = 0; i < WM; ++i) af0[i] = *(const f16x8*)(abuf + a32_lds_off(i * 32 + col, 16 * h));
-#define Q32_KSTEP(KS, CUR, NXT)                                                                            \
+        for (int i = 0; i < WM; ++i) a0[i] = *(const f16x8*)(abuf + a32_lds_off(i * 32 + col, 16 * h));
+#pragma unroll
+        for (int t = 0; t < WN; ++t) b0[t] = cur[t][0].template frag<0>();
+#define Q32_KSTEP(KS, AC, BC, AN, BN)                                                                      \
     {                                                                                                      \
-        if ((KS) < 15) {                                                                                   \
-            _Pragma("unroll") for (int i = 0; i < WM; ++i) NXT[i] =                                        \
+        if constexpr ((KS) < 15) {                                                                         \
+            _Pragma("unroll") for (int i = 0; i < WM; ++i) AN[i] =                                         \
                 *(const f16x8*)(abuf + a32_lds_off(i * 32 + col, 16 * h + (KS) + 1));                     \
+            _Pragma("unroll") for (int t = 0; t < WN; ++t) BN[t] =                                         \
+                cur[t][((KS) + 1) >> 3].template frag<((KS) + 1) & 7>();                                   \
         }                                                                                                  \
-        f16x8 bfr[WN];                                                                                     \
-        _Pragma("unroll") for (int t = 0; t < WN; ++t) bfr[t] = cur[t][(KS) >> 3].template frag<(KS) & 7>(); \
         _Pragma("unroll") for (int i = 0; i < WM; ++i)                                                     \
             _Pragma("unroll") for (int t = 0; t < WN; ++t) acc[i][t] =                                     \
-                __builtin_amdgcn_mfma_f32_32x32x16_f16(CUR[i], bfr[t], acc[i][t], 0, 0, 0);                \
+                __builtin_amdgcn_mfma_f32_32x32x16_f16(AC[i], BC[t], acc[i][t], 0, 0, 0);                  \
+        if constexpr ((KS) < 15) __builtin_amdgcn_sched_group_barrier(0x100, WM, 0);                      \
+        _Pragma("unroll") for (int i = 0; i < WM * WN; ++i) {                                              \
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                                             \
+            if constexpr ((KS) < 15)                                                                       \
+                __builtin_amdgcn_sched_group_barrier(0x002, (16 * WN + WM * WN - 1) / (WM * WN), 0);       \
+        }                                                                                                  \
     }
-        Q32_KSTEP(0, af0, af1) Q32_KSTEP(1, af1, af0) Q32_KSTEP(2, af0, af1) Q32_KSTEP(3, af1, af0)
-        Q32_KSTEP(4, af0, af1) Q32_KSTEP(5, af1, af0) Q32_KSTEP(6, af0, af1) Q32_KSTEP(7, af1, af0)
-        Q32_KSTEP(8, af0, af1) Q32_KSTEP(9, af1, af0) Q32_KSTEP(10, af0, af1) Q32_KSTEP(11, af1, af0)
-        Q32_KSTEP(12, af0, af1) Q32_KSTEP(13, af1, af0) Q32_KSTEP(14, af0, af1) Q32_KSTEP(15, af1, af0)
+        Q32_KSTEP(0, a0, b0, a1, b1) Q32_KSTEP(1, a1, b1, a0, b0) Q32_KSTEP(2, a0, b0, a1, b1)
+        Q32_KSTEP(3, a1, b1, a0, b0) Q32_KSTEP(4, a0, b0, a1, b1) Q32_KSTEP(5, a1, b1, a0, b0)
+        Q32_KSTEP(6, a0, b0, a1, b1) Q32_KSTEP(7, a1, b1, a0, b0) Q32_KSTEP(8, a0, b0, a1, b1)
+        Q32_KSTEP(9, a1, b1, a0, b0) Q32_KSTEP(10, a0, b0, a1, b1) Q32_KSTEP(11, a1, b1, a0, b0)
+        Q32_KSTEP(12, a0, b0, a1, b1) Q32_KSTEP(13, a1, b1, a0, b0) Q32_KSTEP(14, a0, b0, a1, b1)
+        Q32_KSTEP(15, a1, b1, a0, b0)
 #undef Q32_KSTEP
         __syncthreads();  // drains the k+1 global_load_lds / W loads (vmcnt(0)) and orders LDS reuse
     };
