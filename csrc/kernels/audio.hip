@@ -1,0 +1,161 @@
+// audio.hip — recurrent / vocoder kernels for the speech workers (silero VAD, VITS TTS).
+//
+//  * lstm_scan: a persistent LSTM recurrence. One workgroup per sequence, 4*H threads (one per
+//    gate row). Thread j keeps row j of W_hh in VGPRs for the whole scan (H=128 -> 128 fp32
+//    registers), the hidden state lives in LDS and is read as broadcast float4s, so a time step is
+//    H FMAs per lane + two barriers and no HBM traffic besides the precomputed input gates
+//    gx[t] = W_ih x_t + b_ih + b_hh (one hipBLASLt GEMM over all steps, done by the caller).
+//    HEAD fuses silero's decoder (ReLU -> 1x1 conv -> sigmoid) into the scan, so the only output
+//    is one speech probability per step. Replaces the reference's per-window onnxruntime call
+//    (silero-vad-go speech.Detector.infer), which re-enters the runtime 31 times per second of
+//    audio.
+//    H <= 128: a 4H-thread workgroup keeps its W_hh rows in registers only up to 2 waves / SIMD.
+#include "mx_common.h"
+
+MX_DEV float sigmoid_f(float x) { return 1.f / (1.f + __expf(-x)); }
+MX_DEV float tanh_f(float x) {
+    const float e = __expf(-2.f * fabsf(x));
+    const float t = (1.f - e) / (1.f + e);
+    return copysignf(t, x);
+}
+
+template <int H, bool HEAD>
+__global__ __launch_bounds__(4 * H) void lstm_scan_kernel(const float* __restrict__ gx,   // [B, T, 4H]
+                                                          const float* __restrict__ whh,  // [4H, H]
+                                                          float* __restrict__ h_io,       // [B, H]
+                                                          float* __restrict__ c_io,       // [B, H]
+                                                          const float* __restrict__ head_w,  // [H]
+                                                          float head_b,
+                                                          float* __restrict__ out,  // HEAD ? [B, T] : [B, T, H]
+                                                          int T) {
+    constexpr int G = 4 * H;
+    __shared__ __attribute__((aligned(16))) float sh_h[H];
+    __shared__ float sh_g[G];
+    __shared__ float sh_red[2 * (H / 64 > 0 ? H / 64 : 1)];
+    const int j = threadIdx.x;
+    const int b = blockIdx.x;
+    float w[H];
+    {
+        const float4* wr = reinterpret_cast<const float4*>(whh + (size_t)j * H);
+#pragma unroll
+        for (int i = 0; i < H / 4; ++i) {
+            const float4 v = wr[i];
+            w[4 * i] = v.x;
+            w[4 * i + 1] = v.y;
+            w[4 * i + 2] = v.z;
+            w[4 * i + 3] = v.w;
+        }
+    }
+    float c = 0.f, hw = 0.f;
+    if (j < H) {
+        sh_h[j] = h_io[(size_t)b * H + j];
+        c = c_io[(size_t)b * H + j];
+        if (HEAD) hw = head_w[j];
+    }
+    const float* g_row = gx + (size_t)b * T * G;
+    float g_next = T > 0 ? g_row[j] : 0.f;
+    __syncthreads();
+    constexpr int NW = H / 64;
+    for (int t = 0; t < T; ++t) {
+        if (HEAD && j == 0 && t > 0) {
+            float s = head_b;
+#pragma unroll
+            for (int i = 0; i < NW; ++i) s += sh_red[i];
+            out[(size_t)b * T + t - 1] = sigmoid_f(s);
+        }
+        float acc = g_next;
+        if (t + 1 < T) g_next = g_row[(size_t)(t + 1) * G + j];  // prefetch: latency hidden by the dot
+        const float4* hv = reinterpret_cast<const float4*>(sh_h);
+#pragma unroll
+        for (int i = 0; i < H / 4; ++i) {
+            const float4 h4 = hv[i];
+            acc = fmaf(w[4 * i], h4.x, acc);
+            acc = fmaf(w[4 * i + 1], h4.y, acc);
+            acc = fmaf(w[4 * i + 2], h4.z, acc);
+            acc = fmaf(w[4 * i + 3], h4.w, acc);
+        }
+        sh_g[j] = acc;
+        __syncthreads();
+        if (j < H) {  // PyTorch gate order: i, f, g, o
+            const float ig = sigmoid_f(sh_g[j]);
+            const float fg = sigmoid_f(sh_g[H + j]);
+            const float gg = tanh_f(sh_g[2 * H + j]);
+            const float og = sigmoid_f(sh_g[3 * H + j]);
+            c = fg * c + ig * gg;
+            const float h = og * tanh_f(c);
+            sh_h[j] = h;
+            if (HEAD) {
+                const float p = wave_sum(fmaxf(h, 0.f) * hw);
+                if ((j & 63) == 0) sh_red[j >> 6] = p;
+            } else {
+                out[((size_t)b * T + t) * H + j] = h;
+            }
+        }
+        __syncthreads();
+    }
+    if (j < H) {
+        h_io[(size_t)b * H + j] = sh_h[j];
+        c_io[(size_t)b * H + j] = c;
+    }
+    if (HEAD && j == 0 && T > 0) {
+        float s = head_b;
+#pragma unroll
+        for (int i = 0; i < NW; ++i) s += sh_red[i];
+        out[(size_t)b * T + T - 1] = sigmoid_f(s);
+    }
+}
+
+extern "C" int mxk_lstm_scan(const float* gx, const float* whh, float* h_io, float* c_io, const float* head_w,
+                             float head_b, float* out, int B, int T, int H, hipStream_t st) {
+    if (B <= 0) return 0;
+    const bool head = head_w != nullptr;
+#define MX_LSTM(HH)                                                                                         \
+    if (H == HH) {                                                                                          \
+        if (head)                                                                                           \
+            lstm_scan_kernel<HH, true><<<B, 4 * HH, 0, st>>>(gx, whh, h_io, c_io, head_w, head_b, out, T);  \
+        else                                                                                                \
+            lstm_scan_kernel<HH, false><<<B, 4 * HH, 0, st>>>(gx, whh, h_io, c_io, head_w, head_b, out, T); \
+        return (int)hipGetLastError();                                                                      \
+    }
+    MX_LSTM(64)
+    MX_LSTM(128)
+#undef MX_LSTM
+    return (int)hipErrorInvalidValue;
+}
+
+// ---------------------------------------------------------------------------------------------
+// WaveNet gate (VITS flows / posterior encoder): out[b, c, t] = tanh(x[b, c, t]) * sigmoid(x[b, H + c, t])
+// for x [B, 2H, T] -> out [B, H, T]; one read of each half, float4-vectorised along T when T % 4 == 0.
+__global__ __launch_bounds__(256) void wavenet_gate_kernel(const float* __restrict__ x, float* __restrict__ out,
+                                                           int H, int T, long total4, int vec) {
+    const long i = (long)blockIdx.x * 256 + threadIdx.x;
+    if (i >= total4) return;
+    if (vec) {
+        const long e = i * 4;
+        const long bc = e / T;  // b * H + c
+        const int t = (int)(e - bc * T);
+        const long b = bc / H, c = bc - b * H;
+        const float4 a = *reinterpret_cast<const float4*>(x + ((b * 2 * H + c) * T + t));
+        const float4 g = *reinterpret_cast<const float4*>(x + ((b * 2 * H + H + c) * T + t));
+        float4 o;
+        o.x = tanh_f(a.x) * sigmoid_f(g.x);
+        o.y = tanh_f(a.y) * sigmoid_f(g.y);
+        o.z = tanh_f(a.z) * sigmoid_f(g.z);
+        o.w = tanh_f(a.w) * sigmoid_f(g.w);
+        *reinterpret_cast<float4*>(out + e) = o;
+    } else {
+        const long bc = i / T;
+        const int t = (int)(i - bc * T);
+        const long b = bc / H, c = bc - b * H;
+        out[i] = tanh_f(x[(b * 2 * H + c) * T + t]) * sigmoid_f(x[(b * 2 * H + H + c) * T + t]);
+    }
+}
+
+extern "C" int mxk_wavenet_gate(const float* x, float* out, int B, int H, int T, hipStream_t st) {
+    const long n = (long)B * H * T;
+    if (n == 0) return 0;
+    const int vec = (T % 4) == 0;
+    const long work = vec ? n / 4 : n;
+    wavenet_gate_kernel<<<(unsigned)((work + 255) / 256), 256, 0, st>>>(x, out, H, T, work, vec);
+    return (int)hipGetLastError();
+}

@@ -56,6 +56,8 @@ KERNEL_SIGS = {
     "mxk_gather_rows": [P, I, P, I, I, F, P, P],
     "mxk_add_bias_f32": [P, I, P, I, I, P],
     "mxk_select_rows_f32": [P, I, P, I, I, P, I, P],
+    "mxk_lstm_scan": [P, P, P, P, P, F, P, I, I, I, P],
+    "mxk_wavenet_gate": [P, P, I, I, I, P],
 }
 
 HIP_ERRORS = {1: "hipErrorInvalidValue", 2: "hipErrorOutOfMemory", 98: "hipErrorInvalidDeviceFunction",

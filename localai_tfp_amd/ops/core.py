@@ -470,3 +470,14 @@ def cast_bf16(x: torch.Tensor, out: torch.Tensor):
     N.kcall("mxk_cast_f32_bf16", x.data_ptr(), x.stride(0), out.data_ptr(), out.stride(0), x.shape[0], x.shape[1],
             N.stream_ptr())
     return out
+
+
+def wavenet_gate(x: torch.Tensor, H: int) -> torch.Tensor:
+    """tanh(x[:, :H]) * sigmoid(x[:, H:]) for x [B, 2H, T] fp32 (audio.hip wavenet_gate)."""
+    if not x.is_cuda:
+        return torch.tanh(x[:, :H]) * torch.sigmoid(x[:, H:])
+    x = x.contiguous().float()
+    B, _, T = x.shape
+    out = torch.empty(B, H, T, device=x.device, dtype=torch.float32)
+    N.kcall("mxk_wavenet_gate", x.data_ptr(), out.data_ptr(), B, H, T, N.stream_ptr())
+    return out

@@ -22,6 +22,8 @@ WORKERS = {
     "bark-cpp": "localai_tfp_amd.workers.tts",
     "coqui": "localai_tfp_amd.workers.tts",
     "kokoro": "localai_tfp_amd.workers.tts",
+    "transformers-musicgen": "localai_tfp_amd.workers.tts",
+    "transformers-tts": "localai_tfp_amd.workers.tts",
 }
 
 ALIASES = {
@@ -41,4 +43,6 @@ AUTODETECT_ORDER = ["llama-cpp", "bert-embeddings", "whisper", "stablediffusion-
 
 def resolve(name: str) -> str:
     n = (name or "").strip().lower()
+    if n in WORKERS:  # a registered name wins over an alias (sentencetransformers -> the BERT worker)
+        return n
     return ALIASES.get(n, n)

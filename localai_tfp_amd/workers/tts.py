@@ -1,0 +1,113 @@
+"""Text-to-speech worker: the reference's `piper` (backend/go/tts/piper.go:20-49), `bark-cpp`
+(backend/go/bark/gobark.go), `coqui` / `kokoro` / `bark` Python backends
+(backend/python/coqui/backend.py, kokoro/backend.py) behind the TTS RPC, all served by one VITS
+engine (models/tts.py) on the GPU.
+
+LoadModel: a Hugging Face VITS directory (MMS-TTS layout) or `synthetic:vits-test | vits-base`.
+ModelOptions.Options ("key:value"): noise_scale, noise_scale_duration (alias noise_w), speaking_rate
+(alias length_scale = 1 / rate), seed.
+TTS: text -> 16-bit PCM WAV at the model's sample rate in `dst`. `voice` selects the speaker of a
+multi-speaker model (an integer id; piper's per-voice .onnx file selection has no equivalent because
+voices are separate checkpoints here — configure one model per voice). `language` is accepted and
+ignored like piper does.
+SoundGeneration (ElevenLabs /v1/sound-generation): the same synthesis, trimmed / padded to
+`duration` seconds when given (the reference only implements it in the transformers MusicGen
+backend; a MusicGen engine is not part of this worker).
+"""
+from __future__ import annotations
+
+import logging
+import os
+
+import numpy as np
+
+from ..grpc import pb
+from ..grpc.server import BackendServicer, worker_main
+
+log = logging.getLogger("localai_tfp_amd.workers.tts")
+
+
+class TTSServicer(BackendServicer):
+    locking = True  # base.SingleThread in the reference backends
+
+    def __init__(self, device: str | None = None):
+        super().__init__()
+        self.device = device
+        self.model = None
+        self.tok = None
+        self.opts: dict = {}
+
+    def LoadModel(self, request, context):
+        import torch
+        from ..models import tts as T
+        try:
+            if self.device is None:
+                self.device = "cuda:0" if torch.cuda.is_available() else "cpu"
+            path = request.ModelFile or request.Model
+            if not path.startswith("synthetic:") and not os.path.isabs(path) and request.ModelPath:
+                path = os.path.join(request.ModelPath, path)
+            if not path.startswith("synthetic:") and os.path.isfile(path):
+                if path.endswith(".onnx"):
+                    raise ValueError(f"{path}: piper .onnx voices need onnxruntime, which this image lacks; "
+                                     "use a VITS checkpoint directory (config.json + safetensors + vocab.json)")
+                path = os.path.dirname(path)
+            self.model, self.tok = T.load_vits(path, self.device)
+            o = {}
+            for kv in request.Options:
+                k, _, v = kv.partition(":")
+                o[k.strip()] = v.strip()
+            self.opts = o
+            return pb.Result(message=f"loaded {self.model.cfg.name}", success=True)
+        except Exception as ex:
+            log.exception("LoadModel failed")
+            return pb.Result(message=f"failed to load model: {ex}", success=False)
+
+    def _synth(self, text: str, voice: str = "") -> np.ndarray:
+        o = self.opts
+        rate = float(o["speaking_rate"]) if "speaking_rate" in o else (
+            1.0 / float(o["length_scale"]) if "length_scale" in o else None)
+        nsd = o.get("noise_scale_duration", o.get("noise_w"))
+        spk = int(voice) if voice and voice.strip().lstrip("-").isdigit() else None
+        ids = self.tok.encode(text)
+        if len(ids) <= 1:
+            raise ValueError("no speakable characters in the input text")
+        return self.model.synthesize(ids, speaker=spk, speaking_rate=rate,
+                                     noise_scale=float(o["noise_scale"]) if "noise_scale" in o else None,
+                                     noise_scale_duration=float(nsd) if nsd is not None else None,
+                                     seed=int(o.get("seed", 0)))
+
+    def TTS(self, request, context):
+        from ..utils.audio import write_wav
+        if self.model is None:
+            return pb.Result(message="model not loaded", success=False)
+        try:
+            wav = self._synth(request.text, request.voice)
+            write_wav(request.dst, wav, self.model.cfg.sample_rate)
+            return pb.Result(message="ok", success=True)
+        except Exception as ex:
+            log.exception("TTS failed")
+            return pb.Result(message=f"tts failed: {ex}", success=False)
+
+    def SoundGeneration(self, request, context):
+        from ..utils.audio import write_wav
+        if self.model is None:
+            return pb.Result(message="model not loaded", success=False)
+        try:
+            wav = self._synth(request.text)
+            sr = self.model.cfg.sample_rate
+            if request.HasField("duration") and request.duration > 0:
+                n = int(request.duration * sr)
+                wav = np.pad(wav, (0, max(0, n - wav.size)))[:n]
+            write_wav(request.dst, wav, sr)
+            return pb.Result(message="ok", success=True)
+        except Exception as ex:
+            log.exception("SoundGeneration failed")
+            return pb.Result(message=f"sound generation failed: {ex}", success=False)
+
+
+def main(argv=None):
+    worker_main(TTSServicer, argv)
+
+
+if __name__ == "__main__":
+    main()
