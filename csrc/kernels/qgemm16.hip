@@ -26,11 +26,26 @@ MX_DEV int a16_lds_off(int r, int c) {
     return r * 512 + ((c ^ (rr ^ ((rr + 4) & 8))) << 4);
 }
 
-template <int QT, int WM, int WN, int EPI>
+// Grouped mode (GR, mixture-of-experts): rows of A are token-expert pairs sorted by expert
+// (moe.hip moe_sort); expert e owns sorted rows [off[e], off[e+1]) and weight rows [e*N, (e+1)*N)
+// of one stacked [E*N, K] matrix. blockIdx.z walks a compacted tile list: tile_start[e] is the
+// prefix sum of ceil(rows_e / BM) (computed on the device by moe_sort for this BM), so a launch
+// sized for the worst case (ceil(P/BM) + E tiles) needs no host round-trip and stays inside a
+// captured hipGraph; surplus workgroups exit at once. `a_rows` (optional) gathers A rows through
+// an index (pair -> token row), so the router's input is never copied per expert.
+struct MoeGroups {
+    const int* a_rows;      // [P] A row of sorted pair p, or null (A already in sorted order)
+    const int* off;         // [E+1] sorted-row offsets per expert
+    const int* tile_start;  // [E+1] tile prefix sums for this BM
+    int E;
+};
+
+template <int QT, int WM, int WN, int EPI, bool GR = false>
 __global__ __launch_bounds__(256, (WM >= 8 ? 1 : 2)) void qgemm16_kernel(const uint16_t* __restrict__ A, int lda,
                                                          const uint8_t* __restrict__ W,
                                                          const uint16_t* __restrict__ WD, int M, int N, int K,
-                                                         int kb_per_split, void* __restrict__ Cv, int ldc) {
+                                                         int kb_per_split, void* __restrict__ Cv, int ldc,
+                                                         MoeGroups grp = {}) {
     constexpr int BM = WM * 16;
     constexpr int A_BYTES = BM * 512;
     constexpr int A_PASSES = BM * 32 / 256;
@@ -39,7 +54,21 @@ __global__ __launch_bounds__(256, (WM >= 8 ? 1 : 2)) void qgemm16_kernel(const u
     const int g = lane >> 4, col = lane & 15;
     const int nblk = K >> 8;
     const int n_base = (blockIdx.x * 4 + wave) * (WN * 16);
-    const int m_base = blockIdx.z * BM;
+    int m_base = blockIdx.z * BM;
+    int m_end = M, n_row0 = 0;
+    if constexpr (GR) {
+        const int z = blockIdx.z;
+        if (z >= grp.tile_start[grp.E]) return;
+        int lo = 0, hi = grp.E;  // largest e with tile_start[e] <= z (empty experts have equal starts)
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (grp.tile_start[mid] <= z) lo = mid;
+            else hi = mid;
+        }
+        m_base = grp.off[lo] + (z - grp.tile_start[lo]) * BM;
+        m_end = grp.off[lo + 1];
+        n_row0 = lo * N;
+    }
     const int kb0 = blockIdx.y * kb_per_split;
     const int kb1 = min(kb0 + kb_per_split, nblk);
     if (kb0 >= kb1) return;
@@ -57,7 +86,8 @@ __global__ __launch_bounds__(256, (WM >= 8 ? 1 : 2)) void qgemm16_kernel(const u
             const int id = p * 256 + threadIdx.x;
             const int r = id >> 5, c = id & 31;
             const int m = m_base + r;
-            if (m < M) areg[p] = *(const u32x4*)(A + (size_t)m * lda + (size_t)kb * 256 + c * 8);
+            const int ar = (GR && grp.a_rows) ? (m < m_end ? grp.a_rows[m] : 0) : m;
+            if (m < m_end) areg[p] = *(const u32x4*)(A + (size_t)ar * lda + (size_t)kb * 256 + c * 8);
             else areg[p] = (u32x4){0, 0, 0, 0};
         }
     };
@@ -73,7 +103,7 @@ __global__ __launch_bounds__(256, (WM >= 8 ? 1 : 2)) void qgemm16_kernel(const u
 #pragma unroll
         for (int t = 0; t < WN; ++t) {
             const int n = n_base + t * 16 + col;
-            if (n < N) f[t].load(W, WD, n, kb, nblk, g);
+            if (n < N) f[t].load(W, WD, n_row0 + n, kb, nblk, g);
             else f[t].zero();
         }
     };
@@ -125,7 +155,7 @@ __global__ __launch_bounds__(256, (WM >= 8 ? 1 : 2)) void qgemm16_kernel(const u
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                     const int m = m_base + i * 16 + 4 * g + e;
-                    if (m < M) {
+                    if (m < m_end) {
                         const float gv = acc[i][t][e], uv = acc[i][t + 1][e];
                         ((uint16_t*)Cv)[(size_t)m * ldc + feat] = f32_to_act<true>(silu_f(gv) * uv);
                     }
@@ -136,7 +166,7 @@ __global__ __launch_bounds__(256, (WM >= 8 ? 1 : 2)) void qgemm16_kernel(const u
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                     const int m = m_base + i * 16 + 4 * g + e;
-                    if (m >= M) continue;
+                    if (m >= m_end) continue;
                     const float v = acc[i][t][e];
                     if constexpr (EPI == E16_F32) ((float*)Cv)[(size_t)m * ldc + n] = v;
                     else if constexpr (EPI == E16_ACT) ((uint16_t*)Cv)[(size_t)m * ldc + n] = f32_to_act<true>(v);
@@ -192,5 +222,48 @@ extern "C" int mxk_qgemm16(int qtype, int epi, int wm, int wn, const uint16_t* A
         case MXQ_Q8_0: Q16_EPI(MXQ_Q8_0) break;
     }
 #undef Q16_EPI
+    return (int)hipErrorInvalidValue;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Grouped (MoE) entry: P sorted token-expert rows, per-expert N x K weights stacked in W.
+// epi: E16_SWIGLU (gate|up interleaved per expert, act16 out [P, N/2]) or E16_F32 / E16_ACT.
+template <int QT, int EPI>
+static int launch16g(int wm, const uint16_t* A, int lda, const int* a_rows, const uint8_t* W, const uint16_t* WD,
+                     const int* off, const int* tile_start, int E, int P, int N, int K, void* C, int ldc,
+                     hipStream_t st) {
+    const int BM = wm * 16;
+    const int max_tiles = (P + BM - 1) / BM + (E < P ? E : P);
+    dim3 grid((N + 127) / 128, 1, max_tiles);
+    MoeGroups g{a_rows, off, tile_start, E};
+    const size_t lds = 2 * BM * 512;
+#define Q16G(WM_)                                                                                     \
+    if (wm == WM_) {                                                                                  \
+        qgemm16_kernel<QT, WM_, 2, EPI, true><<<grid, 256, lds, st>>>(A, lda, W, WD, P, N, K, K / 256, C, ldc, g); \
+        MXK_CHECK_LAUNCH();                                                                           \
+    }
+    Q16G(1) Q16G(2) Q16G(4)
+#undef Q16G
+    return (int)hipErrorInvalidValue;
+}
+
+extern "C" int mxk_moe_qgemm16(int qtype, int epi, int wm, const uint16_t* A, int lda, const int* a_rows,
+                               const uint8_t* W, const uint16_t* WD, const int* off, const int* tile_start, int E,
+                               int P, int N, int K, void* C, int ldc, hipStream_t st) {
+    if (P <= 0) return 0;
+    if (K % 256 || N % 32) return (int)hipErrorInvalidValue;
+#define Q16G_EPI(QT_)                                                                                               \
+    switch (epi) {                                                                                                  \
+        case E16_F32: return launch16g<QT_, E16_F32>(wm, A, lda, a_rows, W, WD, off, tile_start, E, P, N, K, C, ldc, st); \
+        case E16_ACT: return launch16g<QT_, E16_ACT>(wm, A, lda, a_rows, W, WD, off, tile_start, E, P, N, K, C, ldc, st); \
+        case E16_SWIGLU:                                                                                            \
+            return launch16g<QT_, E16_SWIGLU>(wm, A, lda, a_rows, W, WD, off, tile_start, E, P, N, K, C, ldc, st);  \
+    }
+    switch (qtype) {
+        case MXQ_Q4_K: Q16G_EPI(MXQ_Q4_K) break;
+        case MXQ_Q6_K: Q16G_EPI(MXQ_Q6_K) break;
+        case MXQ_Q8_0: Q16G_EPI(MXQ_Q8_0) break;
+    }
+#undef Q16G_EPI
     return (int)hipErrorInvalidValue;
 }

@@ -8,16 +8,20 @@
 // Rotation: theta_i = pos * inv_freq[i] (the host folds freq_base, linear/llama3/YaRN scaling into
 // inv_freq and the YaRN magnitude correction into attn_factor; grpc-server.cpp:2419-2439 is the
 // reference's parameter surface). Modes: NORM (adjacent pairs, llama) and NEOX (half split).
+// QKN (Qwen3): per-head RMSNorm of every q and k head (weights qn / kn over head_dim) applied
+// after the bias and before the rotation — one wave per head computes the head's rms into LDS,
+// so the normalisation costs one extra read of the row instead of a separate kernel.
 #include "mx_common.h"
 
-template <bool NEOX, bool HAS_BIAS>
+template <bool NEOX, bool HAS_BIAS, bool QKN>
 __global__ __launch_bounds__(256) void rope_kv_kernel(const float* __restrict__ qkv, const float* __restrict__ bias,
                                                       const int* __restrict__ pos, const int* __restrict__ slots,
                                                       const float* __restrict__ inv_freq, float attn_factor,
                                                       int Hq, int Hkv, int D, int rot_dim, bf16_t* __restrict__ qo,
                                                       bf16_t* __restrict__ kc, bf16_t* __restrict__ vc,
-                                                      int block_size) {
-    __shared__ float cs[256], sn[256];
+                                                      int block_size, const float* __restrict__ qn,
+                                                      const float* __restrict__ kn, float eps) {
+    __shared__ float cs[256], sn[256], rsh[QKN ? 256 : 1];
     const int t = blockIdx.x;
     const int p = pos[t];
     const int half = rot_dim / 2;
@@ -27,9 +31,22 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(const float* __restrict__ 
         cs[i] = c * attn_factor;
         sn[i] = s * attn_factor;
     }
-    __syncthreads();
     const int W = (Hq + 2 * Hkv) * D;
     const float* row = qkv + (size_t)t * W;
+    if constexpr (QKN) {
+        const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+        for (int h = wave; h < Hq + Hkv; h += 4) {
+            float ss = 0.f;
+            for (int d = lane; d < D; d += 64) {
+                float x = row[h * D + d];
+                if (HAS_BIAS) x += bias[h * D + d];
+                ss += x * x;
+            }
+            ss = wave_sum(ss);
+            if (lane == 0) rsh[h] = rsqrtf(ss / D + eps);
+        }
+    }
+    __syncthreads();
     const int slot = slots[t];
     const int blk = slot >= 0 ? slot / block_size : 0, off = slot >= 0 ? slot % block_size : 0;
     // rotate q and k heads: one thread per output element; dims >= rot_dim pass through.
@@ -39,6 +56,13 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(const float* __restrict__ 
         const int h = idx / D, d = idx % D;
         float x = row[h * D + d];
         if (HAS_BIAS) x += bias[h * D + d];
+        float nscale = 1.f;
+        const float* nw = nullptr;
+        if constexpr (QKN) {
+            nscale = rsh[h];
+            nw = h < Hq ? qn : kn;
+            x *= nscale * nw[d];
+        }
         float y = x;
         if (d < rot_dim) {
             int pd, fi;
@@ -47,6 +71,7 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(const float* __restrict__ 
             else { first = (d & 1) == 0; pd = first ? d + 1 : d - 1; fi = d >> 1; }
             float xp = row[h * D + pd];
             if (HAS_BIAS) xp += bias[h * D + pd];
+            if constexpr (QKN) xp *= nscale * nw[pd];
             const float c = cs[fi], s = sn[fi];
             y = first ? (x * c - xp * s) : (xp * s + x * c);
         }
@@ -70,12 +95,17 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(const float* __restrict__ 
 
 extern "C" int mxk_rope_kv(const float* qkv, const float* bias, const int* pos, const int* slots,
                            const float* inv_freq, float attn_factor, int T, int Hq, int Hkv, int D, int rot_dim,
-                           int neox, bf16_t* qo, bf16_t* kc, bf16_t* vc, int block_size, hipStream_t st) {
+                           int neox, bf16_t* qo, bf16_t* kc, bf16_t* vc, int block_size, const float* qn,
+                           const float* kn, float eps, hipStream_t st) {
     if (T <= 0) return 0;
     if (rot_dim > 512 || (rot_dim & 1) || D & 1) return (int)hipErrorInvalidValue;
-#define RK(N_, B_) rope_kv_kernel<N_, B_><<<T, 256, 0, st>>>(qkv, bias, pos, slots, inv_freq, attn_factor, Hq, Hkv, D, rot_dim, qo, kc, vc, block_size)
-    if (neox) { if (bias) RK(true, true); else RK(true, false); }
-    else { if (bias) RK(false, true); else RK(false, false); }
+    const bool qkn = qn != nullptr && kn != nullptr;
+    if (qkn && Hq + Hkv > 256) return (int)hipErrorInvalidValue;
+#define RK(N_, B_, Q_) rope_kv_kernel<N_, B_, Q_><<<T, 256, 0, st>>>(qkv, bias, pos, slots, inv_freq, attn_factor, Hq, Hkv, D, rot_dim, qo, kc, vc, block_size, qn, kn, eps)
+#define RKQ(N_, B_) { if (qkn) RK(N_, B_, true); else RK(N_, B_, false); }
+    if (neox) { if (bias) RKQ(true, true) else RKQ(true, false) }
+    else { if (bias) RKQ(false, true) else RKQ(false, false) }
+#undef RKQ
 #undef RK
     MXK_CHECK_LAUNCH();
 }

@@ -40,7 +40,7 @@ KERNEL_SIGS = {
     "mxk_get_act_f16": [],
     "mxk_qgemv": [I, I, P, P, P, P, I, I, I, P, I, P],
     "mxk_dequant_rows": [I, P, P, P, I, I, P, P, I, P],
-    "mxk_rope_kv": [P, P, P, P, P, F, I, I, I, I, I, I, P, P, P, I, P],
+    "mxk_rope_kv": [P, P, P, P, P, F, I, I, I, I, I, I, P, P, P, I, P, P, F, P],
     "mxk_copy_blocks": [P, P, P, I, I, P],
     "mxk_attn_decode": [P, I, P, P, P, I, P, I, I, I, I, I, F, I, I, P, I, P, P, P],
     "mxk_attn_prefill": [P, P, P, P, I, P, P, I, P, P, I, I, I, I, F, P, I, P],
@@ -58,6 +58,10 @@ KERNEL_SIGS = {
     "mxk_select_rows_f32": [P, I, P, I, I, P, I, P],
     "mxk_lstm_scan": [P, P, P, P, P, F, P, I, I, I, P],
     "mxk_wavenet_gate": [P, P, I, I, I, P],
+    "mxk_moe_route": [P, I, I, I, I, I, P, P, P],
+    "mxk_moe_sort": [P, I, I, I, I, P, P, P, P, P],
+    "mxk_moe_combine": [P, I, P, P, I, I, I, P, I, I, P],
+    "mxk_moe_qgemm16": [I, I, I, P, I, P, P, P, P, P, I, I, I, I, P, I, P],
 }
 
 HIP_ERRORS = {1: "hipErrorInvalidValue", 2: "hipErrorOutOfMemory", 98: "hipErrorInvalidDeviceFunction",

@@ -4,7 +4,7 @@ from __future__ import annotations
 from dataclasses import dataclass, field
 
 # llama.cpp rope type per architecture: NORM (adjacent pairs) vs NEOX (half split)
-NEOX_ARCHS = {"qwen2", "qwen2moe", "qwen3", "phi2", "phi3", "gemma", "gemma2", "gemma3", "starcoder2",
+NEOX_ARCHS = {"qwen2", "qwen2moe", "qwen3", "qwen3moe", "phi2", "phi3", "gemma", "gemma2", "gemma3", "starcoder2",
               "falcon", "gptneox", "stablelm", "olmo2", "bert", "nomic-bert", "jina-bert-v2"}
 BIAS_QKV_ARCHS = {"qwen2", "qwen2moe"}
 
@@ -30,6 +30,13 @@ class LlamaConfig:
     tie_embeddings: bool = False
     qkv_bias: bool = False
     embed_scale: float = 1.0
+    # mixture of experts (Mixtral = llama arch with experts, qwen2moe, qwen3moe)
+    n_expert: int = 0
+    n_expert_used: int = 0
+    expert_ffn: int = 0
+    expert_shared_ffn: int = 0
+    moe_renorm: bool = True  # renormalise the top-k router weights (Mixtral, Qwen3-MoE; not Qwen2-MoE)
+    qk_norm: bool = False  # per-head RMSNorm of q and k before RoPE (Qwen3)
     name: str = "llama"
     extra: dict = field(default_factory=dict)
 
@@ -47,7 +54,11 @@ class LlamaConfig:
 
     def n_params(self) -> int:
         h, f, L = self.hidden, self.ffn, self.n_layers
-        per = h * (self.q_dim + 2 * self.kv_dim) + self.q_dim * h + 3 * h * f + 2 * h
+        if self.n_expert:
+            ffn_p = self.n_expert * (3 * h * self.expert_ffn + h) + 3 * h * self.expert_shared_ffn
+        else:
+            ffn_p = 3 * h * f
+        per = h * (self.q_dim + 2 * self.kv_dim) + self.q_dim * h + ffn_p + 2 * h
         emb = self.vocab * h * (1 if self.tie_embeddings else 2)
         return L * per + emb + h
 
@@ -94,6 +105,14 @@ class LlamaConfig:
         )
         if arch in ("gemma", "gemma2", "gemma3"):
             cfg.embed_scale = hidden ** 0.5
+        ne = int(g("expert_count", 0) or 0)
+        if ne:
+            cfg.n_expert = ne
+            cfg.n_expert_used = int(g("expert_used_count", 2))
+            cfg.expert_ffn = int(g("expert_feed_forward_length", 0) or 0) or cfg.ffn
+            cfg.expert_shared_ffn = int(g("expert_shared_feed_forward_length", 0) or 0)
+            cfg.moe_renorm = bool(g("expert_weights_norm", arch != "qwen2moe"))
+        cfg.qk_norm = arch in ("qwen3", "qwen3moe")
         return cfg
 
 
@@ -102,6 +121,17 @@ LLAMA3_70B = LlamaConfig(name="Llama-3-70B-Instruct", n_layers=80, hidden=8192, 
                          n_kv_heads=8)
 LLAMA32_1B = LlamaConfig(name="Llama-3.2-1B", n_layers=16, hidden=2048, ffn=8192, n_heads=32, n_kv_heads=8,
                          head_dim=64, rope_dim=64, tie_embeddings=True)
+
+
+QWEN3_30B_A3B = LlamaConfig(arch="qwen3moe", name="Qwen3-30B-A3B", n_layers=48, hidden=2048, ffn=6144,
+                            n_heads=32, n_kv_heads=4, head_dim=128, rope_dim=128, vocab=151936, ctx_train=40960,
+                            rope_base=1000000.0, rms_eps=1e-6, n_expert=128, n_expert_used=8, expert_ffn=768,
+                            qk_norm=True)
+MIXTRAL_8X7B = LlamaConfig(name="Mixtral-8x7B-Instruct", n_layers=32, hidden=4096, ffn=14336, n_heads=32,
+                           n_kv_heads=8, vocab=32000, ctx_train=32768, rope_base=1000000.0, n_expert=8,
+                           n_expert_used=2, expert_ffn=14336)
+QWEN3_8B = LlamaConfig(arch="qwen3", name="Qwen3-8B", n_layers=36, hidden=4096, ffn=12288, n_heads=32,
+                       n_kv_heads=8, vocab=151936, ctx_train=40960, rope_base=1000000.0, rms_eps=1e-6, qk_norm=True)
 
 
 def tiny_config(**kw) -> LlamaConfig:

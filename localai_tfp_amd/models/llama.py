@@ -29,6 +29,7 @@ from ..formats.gguf import QType
 from ..ops import core as K
 from ..ops.linear import (ACT_DTYPE, EPI_ADD_F32, EPI_BF16, EPI_F32, EPI_SWIGLU, QWeight, concat_rows, interleave_gate_up,
                           qmatmul)
+from ..ops.moe import MoEWeights, moe_ffn
 from .config import LlamaConfig
 
 GEMV_MAX_M = 4
@@ -44,7 +45,10 @@ class LlamaLayer:
     wgu: QWeight | None  # interleaved gate|up
     wg: QWeight | None
     wu: QWeight | None
-    wd: QWeight
+    wd: QWeight | None
+    moe: "MoEWeights | None" = None
+    q_norm: torch.Tensor | None = None  # [head_dim] fp32 (Qwen3 per-head q/k RMSNorm)
+    k_norm: torch.Tensor | None = None
 
 
 @dataclass
@@ -149,12 +153,33 @@ class LlamaModel:
                 raw, N_, K_ = TP.shard_raw(raw, qt, N_, K_, split, tp_rank, tp_size, cfg)
             return QWeight.from_ggml(raw, qt, N_, K_, dev, name)
 
+        def qw_rows(name, row_counts, splits):
+            """Split a fused [sum(rows), K] ggml tensor into per-part QWeights (phi3 attn_qkv / ffn_up)."""
+            t = get_tensor(name)
+            raw, qt, shape = t
+            K_ = int(shape[0])
+            raw = np.asarray(raw).view(np.uint8).reshape(int(np.prod(shape[1:])), -1)
+            out, r0 = [], 0
+            for n_, sp in zip(row_counts, splits):
+                part = raw[r0:r0 + n_]
+                r0 += n_
+                N_ = n_
+                if tp_size > 1:
+                    part, N_, K2 = TP.shard_raw(part, qt, N_, K_, sp, tp_rank, tp_size, cfg)
+                out.append(QWeight.from_ggml(np.ascontiguousarray(part), qt, N_, K_, dev, name))
+            return out
+
         hd = cfg.head_dim
         for i in range(cfg.n_layers):
             p = f"blk.{i}."
-            wq = qw(p + "attn_q.weight", ("col_heads", cfg.n_heads, hd))
-            wk = qw(p + "attn_k.weight", ("col_heads", cfg.n_kv_heads, hd))
-            wv = qw(p + "attn_v.weight", ("col_heads", cfg.n_kv_heads, hd))
+            if get_tensor(p + "attn_qkv.weight") is not None:  # phi3: fused Q|K|V rows
+                wq, wk, wv = qw_rows(p + "attn_qkv.weight", [cfg.q_dim, cfg.kv_dim, cfg.kv_dim],
+                                     [("col_heads", cfg.n_heads, hd), ("col_heads", cfg.n_kv_heads, hd),
+                                      ("col_heads", cfg.n_kv_heads, hd)])
+            else:
+                wq = qw(p + "attn_q.weight", ("col_heads", cfg.n_heads, hd))
+                wk = qw(p + "attn_k.weight", ("col_heads", cfg.n_kv_heads, hd))
+                wv = qw(p + "attn_v.weight", ("col_heads", cfg.n_kv_heads, hd))
             bias = None
             if cfg.qkv_bias:
                 bq, bk, bv = f32(p + "attn_q.bias"), f32(p + "attn_k.bias"), f32(p + "attn_v.bias")
@@ -170,16 +195,31 @@ class LlamaModel:
                 else:
                     parts.append([w])
             qkv_parts = [g[0] if len(g) == 1 else concat_rows(g, p + "attn_qkv") for g in parts]
-            wg = qw(p + "ffn_gate.weight", ("col", cfg.ffn))
-            wu = qw(p + "ffn_up.weight", ("col", cfg.ffn))
-            wgu = interleave_gate_up(wg, wu, p + "ffn_gate_up") if fuse else None
+            moe = None
+            wg = wu = wgu = wd = None
+            if cfg.n_expert:
+                if tp_size > 1:
+                    raise NotImplementedError("tensor-parallel MoE layers (expert parallelism) are not supported yet")
+                moe = load_moe(m, get_tensor, p, f32, qw, fuse)
+            else:
+                if get_tensor(p + "ffn_gate.weight") is None and get_tensor(p + "ffn_up.weight") is not None:
+                    wg, wu = qw_rows(p + "ffn_up.weight", [cfg.ffn, cfg.ffn], [("col", cfg.ffn), ("col", cfg.ffn)])
+                else:
+                    wg = qw(p + "ffn_gate.weight", ("col", cfg.ffn))
+                    wu = qw(p + "ffn_up.weight", ("col", cfg.ffn))
+                wgu = interleave_gate_up(wg, wu, p + "ffn_gate_up") if fuse else None
+                wd = qw(p + "ffn_down.weight", ("row", cfg.ffn))
+            qn = f32(p + "attn_q_norm.weight") if cfg.qk_norm else None
+            kn = f32(p + "attn_k_norm.weight") if cfg.qk_norm else None
             layer = LlamaLayer(
                 attn_norm=f32(p + "attn_norm.weight").float(),
                 ffn_norm=f32(p + "ffn_norm.weight").float(),
                 qkv_parts=qkv_parts, bqkv=bias,
                 wo=qw(p + "attn_output.weight", ("row", cfg.q_dim)),
                 wgu=wgu, wg=None if wgu is not None else wg, wu=None if wgu is not None else wu,
-                wd=qw(p + "ffn_down.weight", ("row", cfg.ffn)),
+                wd=wd, moe=moe,
+                q_norm=qn.float().contiguous() if qn is not None else None,
+                k_norm=kn.float().contiguous() if kn is not None else None,
             )
             m.layers.append(layer)
             if progress:
@@ -203,6 +243,8 @@ class LlamaModel:
             for w in (*L.qkv_parts, L.wo, L.wgu, L.wg, L.wu, L.wd):
                 if w is not None:
                     n += w.nbytes()
+            if L.moe is not None:
+                n += L.moe.nbytes()
         n += self.lm_head.nbytes()
         if self.tok_embd is not self.lm_head:
             n += self.tok_embd.nbytes()
@@ -214,6 +256,8 @@ class LlamaModel:
             for w in (*L.qkv_parts, L.wo, L.wgu, L.wg, L.wu, L.wd):
                 if w is not None:
                     w.build_bf16_cache()
+            if L.moe is not None:
+                L.moe.build_bf16_cache()
         if isinstance(self.lm_head, QWeight) and self.lm_head.is_quant:
             self.lm_head.build_bf16_cache()
 
@@ -245,7 +289,7 @@ class LlamaModel:
         D = cfg.head_dim
         Hq, Hkv = self.n_heads, self.n_kv
         qd, kvd = Hq * D, Hkv * D
-        F = self.layers[0].wd.K if self.layers else 0
+        F = self.layers[0].wd.K if self.layers and self.layers[0].wd is not None else 0
         eps = cfg.rms_eps
         gemv = T <= GEMV_MAX_M and self.device.type == "cuda"
         nd = fb.n_decode
@@ -274,7 +318,8 @@ class LlamaModel:
                 off += w.N
             q = ws.q[:T]
             K.rope_kv(qkv, L.bqkv, fb.positions, fb.slots, self.inv_freq, self.attn_factor, Hq, Hkv, D,
-                      cfg.rope_dim, cfg.neox, q.view(T, Hq, D), kc, vc, kv.block_size)
+                      cfg.rope_dim, cfg.neox, q.view(T, Hq, D), kc, vc, kv.block_size,
+                      qk_norm=(L.q_norm, L.k_norm, eps) if L.q_norm is not None else None)
             attn = ws.attn[:T]
             if nd:
                 K.attn_decode(q[:nd].view(nd, Hq, D), kc, vc, fb.dec_block_tables, fb.dec_seq_lens, self.scale,
@@ -293,6 +338,11 @@ class LlamaModel:
                 qmatmul(L.wo, attn, EPI_ADD_F32, h)
             self._allreduce(h)
             # ---- FFN block ----
+            if L.moe is not None:
+                K.rmsnorm(h, L.ffn_norm, eps, out_bf16=xb)
+                moe_ffn(L.moe, xb, h)
+                self._allreduce(h)
+                continue
             if gemv:
                 xq, xds = ws.q8(T, H)
                 K.rmsnorm(h, L.ffn_norm, eps, out_q8=(xq, xds))
@@ -339,3 +389,28 @@ class LlamaModel:
             K.rmsnorm(hs, self.out_norm, eps, out_bf16=xbs)
             qmatmul(self.lm_head, xbs, EPI_F32, logits)
         return logits
+
+
+def load_moe(m: LlamaModel, get_tensor, p: str, f32, qw, fuse: bool) -> MoEWeights:
+    """Stacked expert tensors (ggml [K, N, E]) -> MoEWeights; gate|up interleaved per expert on GPU."""
+    cfg = m.cfg
+    E, Fe, H = cfg.n_expert, cfg.expert_ffn, cfg.hidden
+    router = f32(p + "ffn_gate_inp.weight").float().view(E, H).contiguous()
+    wg = qw(p + "ffn_gate_exps.weight")
+    wu = qw(p + "ffn_up_exps.weight")
+    wd = qw(p + "ffn_down_exps.weight")
+    on_gpu = m.device.type == "cuda"
+    gu = interleave_gate_up(wg, wu, p + "ffn_gate_up_exps") if (fuse or on_gpu) else None
+    if on_gpu and (gu is None or not gu.is_quant or not wd.is_quant):
+        raise NotImplementedError(f"{p}: MoE experts need Q4_K/Q6_K/Q8_0 weights with F % 16 == 0 on the GPU")
+    moe = MoEWeights(router=router, gate=None if on_gpu else wg, up=None if on_gpu else wu, gate_up=gu, down=wd,
+                     n_expert=E, n_used=cfg.n_expert_used, ffn=Fe, renorm=cfg.moe_renorm)
+    if cfg.expert_shared_ffn:
+        sg, su = qw(p + "ffn_gate_shexp.weight"), qw(p + "ffn_up_shexp.weight")
+        moe.sh_down = qw(p + "ffn_down_shexp.weight")
+        moe.sh_gate_up = interleave_gate_up(sg, su, p + "ffn_gate_up_shexp") if on_gpu else None
+        if moe.sh_gate_up is None:
+            moe.sh_gate, moe.sh_up = sg, su
+        si = f32(p + "ffn_gate_inp_shexp.weight")
+        moe.sh_inp = si.float().contiguous() if si is not None else None
+    return moe

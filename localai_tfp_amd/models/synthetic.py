@@ -38,10 +38,29 @@ def llama_tensor_plan(cfg: LlamaConfig, ftype: str = "Q4_K_M"):
             (p + "attn_v.weight", (H, kvd), hi if mb else base),
             (p + "attn_output.weight", (qd, H), base),
             (p + "ffn_norm.weight", (H,), QType.F32),
-            (p + "ffn_gate.weight", (H, F), base),
-            (p + "ffn_up.weight", (H, F), base),
-            (p + "ffn_down.weight", (F, H), hi if mb else base),
         ]
+        if cfg.n_expert:
+            E, Fe = cfg.n_expert, cfg.expert_ffn
+            out += [
+                (p + "ffn_gate_inp.weight", (H, E), QType.F32),
+                (p + "ffn_gate_exps.weight", (H, Fe, E), base),
+                (p + "ffn_up_exps.weight", (H, Fe, E), base),
+                (p + "ffn_down_exps.weight", (Fe, H, E), hi if mb else base),
+            ]
+            if cfg.expert_shared_ffn:
+                Fs = cfg.expert_shared_ffn
+                out += [(p + "ffn_gate_inp_shexp.weight", (H,), QType.F32),
+                        (p + "ffn_gate_shexp.weight", (H, Fs), base), (p + "ffn_up_shexp.weight", (H, Fs), base),
+                        (p + "ffn_down_shexp.weight", (Fs, H), hi if mb else base)]
+        else:
+            out += [
+                (p + "ffn_gate.weight", (H, F), base),
+                (p + "ffn_up.weight", (H, F), base),
+                (p + "ffn_down.weight", (F, H), hi if mb else base),
+            ]
+        if cfg.qk_norm:
+            out += [(p + "attn_q_norm.weight", (cfg.head_dim,), QType.F32),
+                    (p + "attn_k_norm.weight", (cfg.head_dim,), QType.F32)]
         if cfg.qkv_bias:
             out += [(p + "attn_q.bias", (qd,), QType.F32), (p + "attn_k.bias", (kvd,), QType.F32),
                     (p + "attn_v.bias", (kvd,), QType.F32)]
@@ -54,13 +73,19 @@ def llama_tensor_plan(cfg: LlamaConfig, ftype: str = "Q4_K_M"):
 def _gen(rng, name, shape, qt, cfg):
     n = int(np.prod(shape))
     if qt == QType.F32:
-        if name.endswith("norm.weight"):
-            return (1.0 + 0.05 * rng.standard_normal(n, dtype=np.float32)).astype(np.float32).view(np.uint8)
-        return (0.02 * rng.standard_normal(n, dtype=np.float32)).view(np.uint8)
+        return _gen_f32(rng, name, n).view(np.uint8)
     std = 0.02
     if name.startswith("token_embd"):
         std = 1.0 / np.sqrt(cfg.hidden) * 4
     return random_quantized(rng, qt, n // shape[0], shape[0], std=std)
+
+
+def _gen_f32(rng, name, n):
+    if name.endswith("norm.weight"):
+        return (1.0 + 0.05 * rng.standard_normal(n, dtype=np.float32)).astype(np.float32)
+    if "gate_inp" in name:  # router: logits with a spread large enough to make top-k choices distinct
+        return (0.5 * rng.standard_normal(n, dtype=np.float32)).astype(np.float32)
+    return (0.02 * rng.standard_normal(n, dtype=np.float32)).astype(np.float32)
 
 
 def synthetic_source(cfg: LlamaConfig, ftype: str = "Q4_K_M", seed: int = 0):
@@ -95,6 +120,12 @@ def gguf_metadata(cfg: LlamaConfig, ftype: str = "Q4_K_M") -> dict:
         f"{a}.rope.dimension_count": cfg.rope_dim,
         f"{a}.vocab_size": cfg.vocab,
     }
+    if cfg.n_expert:
+        md[f"{a}.expert_count"] = cfg.n_expert
+        md[f"{a}.expert_used_count"] = cfg.n_expert_used
+        md[f"{a}.expert_feed_forward_length"] = cfg.expert_ffn
+        if cfg.expert_shared_ffn:
+            md[f"{a}.expert_shared_feed_forward_length"] = cfg.expert_shared_ffn
     if cfg.head_dim * cfg.n_heads != cfg.hidden:
         md[f"{a}.attention.key_length"] = cfg.head_dim
         md[f"{a}.attention.value_length"] = cfg.head_dim

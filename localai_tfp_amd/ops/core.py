@@ -219,7 +219,8 @@ def rope_inv_freq(rot_dim: int, base: float = 10000.0, scale: float = 1.0, scali
 
 def rope_kv(qkv: torch.Tensor, bias: torch.Tensor | None, positions: torch.Tensor, slots: torch.Tensor,
             inv_freq: torch.Tensor, attn_factor: float, Hq: int, Hkv: int, D: int, rot_dim: int, neox: bool,
-            q_out: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, block_size: int):
+            q_out: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, block_size: int,
+            qk_norm: tuple | None = None):
     """qkv fp32 [T, (Hq+2Hkv)*D] -> q_out bf16 [T, Hq, D]; K/V scattered into the paged cache
     [num_blocks, Hkv, block_size, D] at `slots` (flat block*bs+offset; -1 skips)."""
     T = qkv.shape[0]
@@ -232,6 +233,10 @@ def rope_kv(qkv: torch.Tensor, bias: torch.Tensor | None, positions: torch.Tenso
         q = x[:, : Hq * D].reshape(T, Hq, D)
         k = x[:, Hq * D:(Hq + Hkv) * D].reshape(T, Hkv, D)
         v = x[:, (Hq + Hkv) * D:].reshape(T, Hkv, D)
+        if qk_norm is not None:
+            qn, kn, eps = qk_norm
+            q = q * torch.rsqrt(q.pow(2).mean(-1, keepdim=True) + eps) * qn
+            k = k * torch.rsqrt(k.pow(2).mean(-1, keepdim=True) + eps) * kn
         ang = positions.double()[:, None] * inv_freq.double()[None, :]
         cos = (torch.cos(ang) * attn_factor).float()
         sin = (torch.sin(ang) * attn_factor).float()
@@ -264,7 +269,8 @@ def rope_kv(qkv: torch.Tensor, bias: torch.Tensor | None, positions: torch.Tenso
         return
     N.kcall("mxk_rope_kv", qkv.data_ptr(), N.ptr(bias), positions.data_ptr(), slots.data_ptr(), inv_freq.data_ptr(),
             float(attn_factor), T, Hq, Hkv, D, rot_dim, int(neox), q_out.data_ptr(), k_cache.data_ptr(),
-            v_cache.data_ptr(), block_size, N.stream_ptr())
+            v_cache.data_ptr(), block_size, N.ptr(qk_norm[0]) if qk_norm else None,
+            N.ptr(qk_norm[1]) if qk_norm else None, float(qk_norm[2]) if qk_norm else 0.0, N.stream_ptr())
 
 
 # ------------------------------------------------------------------------------------------------

@@ -1,0 +1,154 @@
+"""Mixture-of-experts FFN (Mixtral, Qwen2-MoE, Qwen3-MoE GGUF layouts).
+
+Parity target: llama.cpp's build_moe_ffn as the reference's llama-cpp backend runs it (router
+softmax, top-k, optional weight renormalisation, ggml_mul_mat_id over the stacked
+`ffn_{gate,up,down}_exps` tensors, optional shared expert with a sigmoid gate for Qwen2-MoE).
+
+GPU path (all device-side, hipGraph-capturable — csrc/kernels/moe.hip + qgemm16.hip grouped mode):
+    logits = x W_router^T (fp32)  ->  moe_route (softmax + top-k per wave)  ->  moe_sort (counting
+    sort of token-expert pairs, per-expert tile prefix)  ->  grouped SwiGLU GEMM over the stacked,
+    16-row-interleaved gate|up experts (A rows gathered by index)  ->  grouped down GEMM into a
+    [P, H] fp32 buffer  ->  moe_combine (h += sum_j w_j * y_j, fixed order).
+CPU path: the same math with dequantised fp32 expert weights (numerics oracle).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+
+from .. import _native as N
+from .linear import ACT_DTYPE, EPI_F32, EPI_SWIGLU, QWeight, qmatmul
+
+E16_F32, E16_SWIGLU = 0, 3
+
+
+@dataclass
+class MoEWeights:
+    router: torch.Tensor  # fp32 [E, H]
+    gate: QWeight | None  # [E*F, H] stacked (CPU / non-interleavable)
+    up: QWeight | None
+    gate_up: QWeight | None  # [E*2F, H], gate|up interleaved in 16-row groups per expert (GPU)
+    down: QWeight  # [E*H, F] stacked
+    n_expert: int
+    n_used: int
+    ffn: int  # per-expert F
+    renorm: bool
+    sh_gate_up: QWeight | None = None  # shared expert (Qwen2-MoE)
+    sh_gate: QWeight | None = None
+    sh_up: QWeight | None = None
+    sh_down: QWeight | None = None
+    sh_inp: torch.Tensor | None = None  # fp32 [H] sigmoid gate of the shared expert
+
+    def nbytes(self) -> int:
+        n = self.router.numel() * 4
+        for w in (self.gate, self.up, self.gate_up, self.down, self.sh_gate_up, self.sh_gate, self.sh_up,
+                  self.sh_down):
+            if w is not None:
+                n += w.nbytes()
+        return n
+
+    def build_bf16_cache(self):
+        for w in (self.sh_gate_up, self.sh_down):
+            if w is not None:
+                w.build_bf16_cache()
+
+
+def route_ref(logits: torch.Tensor, k: int, renorm: bool):
+    p = torch.softmax(logits.float(), -1)
+    w, ids = torch.topk(p, k, -1)  # ties -> lower index (torch.topk is stable on CPU for equal values)
+    if renorm:
+        w = w / w.sum(-1, keepdim=True)
+    return ids.int(), w
+
+
+def _grouped_wm(P: int, E: int) -> int:
+    avg = P / max(1, min(E, P))
+    return 1 if avg <= 16 else 2 if avg <= 40 else 4
+
+
+def moe_ffn(W: MoEWeights, x: torch.Tensor, h: torch.Tensor) -> torch.Tensor:
+    """h [T, H] fp32 += MoE(x); x is the normed hidden state in 16-bit (GPU) or fp32 (CPU)."""
+    T = x.shape[0]
+    if T == 0:
+        return h
+    E, k, F = W.n_expert, W.n_used, W.ffn
+    H = h.shape[1]
+    if not x.is_cuda:
+        return _moe_ref(W, x.float(), h)
+    logits = x.float() @ W.router.t()
+    ids = torch.empty(T, k, dtype=torch.int32, device=x.device)
+    wts = torch.empty(T, k, dtype=torch.float32, device=x.device)
+    st = N.stream_ptr()
+    N.kcall("mxk_moe_route", logits.data_ptr(), logits.stride(0), T, E, k, int(W.renorm), ids.data_ptr(),
+            wts.data_ptr(), st)
+    P = T * k
+    wm = _grouped_wm(P, E)
+    off = torch.empty(E + 1, dtype=torch.int32, device=x.device)
+    tiles = torch.empty(E + 1, dtype=torch.int32, device=x.device)
+    stok = torch.empty(P, dtype=torch.int32, device=x.device)
+    inv = torch.empty(P, dtype=torch.int32, device=x.device)
+    N.kcall("mxk_moe_sort", ids.data_ptr(), P, k, E, 16 * wm, off.data_ptr(), tiles.data_ptr(), stok.data_ptr(),
+            inv.data_ptr(), st)
+    act = torch.empty(P, F, dtype=x.dtype, device=x.device)
+    N.ensure_act(x.dtype)
+    gu = W.gate_up
+    N.kcall("mxk_moe_qgemm16", int(gu.qtype), E16_SWIGLU, wm, x.data_ptr(), x.stride(0), stok.data_ptr(),
+            gu.data.data_ptr(), N.ptr(gu.dplane), off.data_ptr(), tiles.data_ptr(), E, P, 2 * F, gu.K,
+            act.data_ptr(), act.stride(0), st)
+    y = torch.empty(P, H, dtype=torch.float32, device=x.device)
+    d = W.down
+    N.kcall("mxk_moe_qgemm16", int(d.qtype), E16_F32, wm, act.data_ptr(), act.stride(0), None, d.data.data_ptr(),
+            N.ptr(d.dplane), off.data_ptr(), tiles.data_ptr(), E, P, H, d.K, y.data_ptr(), y.stride(0), st)
+    N.kcall("mxk_moe_combine", y.data_ptr(), y.stride(0), inv.data_ptr(), wts.data_ptr(), T, k, H, h.data_ptr(),
+            h.stride(0), 1, st)
+    if W.sh_down is not None:
+        _shared(W, x, h)
+    return h
+
+
+def _shared(W: MoEWeights, x: torch.Tensor, h: torch.Tensor):
+    T = x.shape[0]
+    Fs = W.sh_down.K
+    act = torch.empty(T, Fs, dtype=x.dtype, device=x.device)
+    if W.sh_gate_up is not None:
+        qmatmul(W.sh_gate_up, x, EPI_SWIGLU, act)
+    else:
+        g = torch.empty(T, Fs, dtype=x.dtype, device=x.device)
+        u = torch.empty(T, Fs, dtype=x.dtype, device=x.device)
+        qmatmul(W.sh_gate, x, 1, g)
+        qmatmul(W.sh_up, x, 1, u)
+        act.copy_(torch.nn.functional.silu(g.float()) * u.float())
+    ys = torch.zeros(T, h.shape[1], dtype=torch.float32, device=x.device)
+    qmatmul(W.sh_down, act, EPI_F32, ys, out_zeroed=True)
+    if W.sh_inp is not None:
+        ys.mul_(torch.sigmoid(x.float() @ W.sh_inp)[:, None])
+    h.add_(ys)
+
+
+def _moe_ref(W: MoEWeights, x: torch.Tensor, h: torch.Tensor) -> torch.Tensor:
+    E, k, F = W.n_expert, W.n_used, W.ffn
+    H = h.shape[1]
+    ids, wts = route_ref(x @ W.router.t(), k, W.renorm)
+    g = W.gate.dense_f32().view(E, F, -1)
+    u = W.up.dense_f32().view(E, F, -1)
+    d = W.down.dense_f32().view(E, H, F)
+    out = torch.zeros_like(h)
+    for e in range(E):
+        tok, slot = (ids == e).nonzero(as_tuple=True)
+        if tok.numel() == 0:
+            continue
+        xe = x[tok]
+        a = torch.nn.functional.silu(xe @ g[e].t()) * (xe @ u[e].t())
+        out.index_add_(0, tok, (a @ d[e].t()) * wts[tok, slot][:, None])
+    h.add_(out)
+    if W.sh_down is not None:
+        gs, us = W.sh_gate.dense_f32(), W.sh_up.dense_f32()
+        ys = (torch.nn.functional.silu(x @ gs.t()) * (x @ us.t())) @ W.sh_down.dense_f32().t()
+        if W.sh_inp is not None:
+            ys = ys * torch.sigmoid(x @ W.sh_inp)[:, None]
+        h.add_(ys)
+    return h
+
+
+__all__ = ["MoEWeights", "moe_ffn", "route_ref", "ACT_DTYPE"]
