@@ -78,6 +78,7 @@ def add_run_args(ap: argparse.ArgumentParser):
     ap.add_argument("--enable-watchdog-busy", action="store_true", default=None)
     ap.add_argument("--watchdog-busy-timeout")
     ap.add_argument("--federated", action="store_true", default=None)
+    ap.add_argument("--p2p-peers", help="comma-separated federator / peer URLs to announce this node to")
     ap.add_argument("--disable-gallery-endpoint", action="store_true", default=None)
     ap.add_argument("--machine-tag")
     ap.add_argument("--load-to-memory", nargs="*")
@@ -135,6 +136,8 @@ def app_config_from_args(a):
     c.models = models
     if a.gpus:
         os.environ["LOCALAI_GPUS"] = a.gpus
+    if a.p2p_peers:
+        c.p2p_peers = [x for x in a.p2p_peers.split(",") if x]
     return c
 
 
@@ -269,6 +272,31 @@ def cmd_util(a):
     return 0
 
 
+def cmd_federated(a):
+    """`local-ai federated` (core/cli/federated.go): the load-balancing proxy over announced nodes."""
+    from . import p2p as P
+    token = a.p2ptoken or os.environ.get("LOCALAI_P2P_TOKEN") or os.environ.get("TOKEN") or ""
+    reg = P.Registry(token, a.network_id or os.environ.get("LOCALAI_P2P_NETWORK_ID", ""))
+    for n in (a.nodes or "").split(","):
+        if n:  # static nodes (id=host:port or host:port), kept online by re-adding
+            nid, _, addr = n.rpartition("=")
+            reg.add(P.NodeData(id=nid or addr, address=addr, service=P.FEDERATED_ID))
+    fs = P.FederatedServer(a.address, reg, P.FEDERATED_ID, load_balanced=a.load_balanced,
+                           worker_target=a.target_worker or "")
+    if a.nodes:
+        import threading
+        import time
+
+        def keep():
+            while True:
+                for nd in reg.nodes(P.FEDERATED_ID):
+                    reg.add(nd)
+                time.sleep(10)
+        threading.Thread(target=keep, daemon=True).start()
+    fs.serve_forever()
+    return 0
+
+
 def cmd_worker(a):
     from . import workers as W
     import importlib
@@ -319,6 +347,15 @@ def main(argv=None):
     uh = usub.add_parser("usecase-heuristic")
     uh.add_argument("names", nargs="*")
     uh.add_argument("--models-path")
+    fd = sub.add_parser("federated", help="run the federated load-balancing proxy")
+    fd.add_argument("--address", default=os.environ.get("LOCALAI_ADDRESS", "0.0.0.0:8080"))
+    fd.add_argument("--p2ptoken")
+    fd.add_argument("--network-id")
+    fd.add_argument("--load-balanced", action="store_true",
+                    default=_bool_env(["LOCALAI_LOAD_BALANCED", "LOAD_BALANCED"]))
+    fd.add_argument("--target-worker", default=os.environ.get("LOCALAI_TARGET_WORKER", ""))
+    fd.add_argument("--nodes", default=os.environ.get("LOCALAI_FEDERATED_NODES", ""),
+                    help="static nodes: id=host:port,...")
     w = sub.add_parser("worker", help="run a single backend worker process")
     w.add_argument("kind", help="backend name, e.g. llama-cpp, whisper, bert-embeddings")
     w.add_argument("--addr", default="127.0.0.1:50051")
@@ -326,7 +363,8 @@ def main(argv=None):
     logging.basicConfig(level=getattr(logging, str(getattr(a, "log_level", "info") or "info").upper(), logging.INFO),
                         format="%(asctime)s %(levelname)s %(name)s: %(message)s")
     fn = {"run": cmd_run, "models": cmd_models, "tts": cmd_tts, "transcript": cmd_transcript,
-          "sound-generation": cmd_sound, "util": cmd_util, "worker": cmd_worker}.get(a.cmd)
+          "sound-generation": cmd_sound, "util": cmd_util, "worker": cmd_worker,
+          "federated": cmd_federated}.get(a.cmd)
     if fn is None:
         ap.print_help()
         return 1

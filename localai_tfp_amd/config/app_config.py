@@ -64,6 +64,8 @@ class ApplicationConfig:
     p2p: bool = field(default_factory=lambda: _env(["LOCALAI_P2P", "P2P"], False, bool))
     p2p_token: str = field(default_factory=lambda: _env(["LOCALAI_P2P_TOKEN", "P2P_TOKEN", "TOKEN"], ""))
     p2p_network_id: str = field(default_factory=lambda: _env(["LOCALAI_P2P_NETWORK_ID", "P2P_NETWORK_ID"], ""))
+    # federator / peer URLs this instance announces itself to (libp2p discovery replacement)
+    p2p_peers: list = field(default_factory=lambda: _env(["LOCALAI_P2P_PEERS", "P2P_PEERS"], [], list))
     federated: bool = field(default_factory=lambda: _env(["LOCALAI_FEDERATED", "FEDERATED"], False, bool))
     # MI355X specifics
     gpus: str = field(default_factory=lambda: _env(["LOCALAI_GPUS", "HIP_VISIBLE_DEVICES"], ""))

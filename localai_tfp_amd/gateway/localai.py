@@ -9,7 +9,7 @@ from __future__ import annotations
 import os
 
 from fastapi import APIRouter, Request
-from fastapi.responses import Response
+from fastapi.responses import JSONResponse, Response
 
 from ..config.model_config import FLAG_TOKENIZE, FLAG_VAD, ModelConfig
 from ..grpc import pb
@@ -274,6 +274,21 @@ async def p2p_nodes(request: Request):
     if p is None:
         return {"nodes": [], "federated_nodes": []}
     return {"nodes": p.nodes("worker"), "federated_nodes": p.nodes("federated")}
+
+
+@router.post("/api/p2p/register")
+async def p2p_register(request: Request):
+    """Node announcement (replaces the libp2p ledger write of p2p.go nodeAnnounce)."""
+    from .. import p2p as P
+    a = app_of(request)
+    if a.p2p is None:
+        return JSONResponse({"error": "p2p is not enabled"}, status_code=404)
+    if not a.p2p.registry.authorised(request.headers.get("authorization")):
+        return JSONResponse({"error": "invalid token"}, status_code=401)
+    d = await request.json()
+    a.p2p.registry.add(P.NodeData(id=str(d["id"]), name=d.get("name", ""), address=d.get("address", ""),
+                                  service=d.get("service", P.WORKER_ID)))
+    return {"ok": True}
 
 
 @router.get("/api/p2p/token")

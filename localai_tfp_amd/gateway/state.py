@@ -65,6 +65,13 @@ class Application:
         self.started = time.time()
         self._watch_stop = threading.Event()
         self.p2p = None
+        if c.p2p:
+            from .. import p2p as P
+            if not c.p2p_token:
+                c.p2p_token = P.generate_token()
+                log.info("p2p enabled without a token; generated network token: %s", c.p2p_token)
+            me = P.self_node(c.address, P.FEDERATED_ID if c.federated else P.WORKER_ID)
+            self.p2p = P.P2PNode(c.p2p_token, c.p2p_network_id, list(c.p2p_peers), me)
 
     # ------------------------------------------------------------------ startup
     def startup(self):
@@ -125,6 +132,8 @@ class Application:
 
     def shutdown(self):
         self._watch_stop.set()
+        if self.p2p is not None:
+            self.p2p.stop()
         self.gallery.close()
         self.loader.stop_all()
 

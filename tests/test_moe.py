@@ -181,7 +181,12 @@ def test_moe_model_gpu_matches_cpu_and_engine():
     for x, y in zip(a, b):
         assert float((x - y).norm() / x.norm()) < 6e-2
     tok = ByteTokenizer(cfg.vocab)
-    eng = LLMEngine(mg, tok, EngineConfig(num_blocks=256, max_num_seqs=8, max_batched_tokens=256, max_model_len=512))
-    outs = [eng.generate(tok.encode(f"moe prompt {i}"), SamplingParams(temperature=0.0), max_tokens=12)
-            for i in range(2)]
-    assert all(len(o.token_ids) == 12 for o in outs)
+    streams = []
+    for graphs in (False, True):  # the MoE layer (route/sort/grouped GEMMs) inside a captured hipGraph
+        eng = LLMEngine(mg, tok, EngineConfig(num_blocks=256, max_num_seqs=8, max_batched_tokens=256,
+                                              max_model_len=512, use_graphs=graphs))
+        outs = [eng.generate(tok.encode(f"moe prompt {i}"), SamplingParams(temperature=0.0, ignore_eos=True),
+                             max_tokens=12) for i in range(2)]
+        assert all(len(o.token_ids) == 12 for o in outs)
+        streams.append([o.token_ids for o in outs])
+    assert streams[0] == streams[1]

@@ -1,0 +1,104 @@
+"""Federation (reference: core/p2p/federated.go selection + request table, federated_server.go
+503 when no node, node.go 40 s liveness; the reference has no test for p2p — its transport is
+libp2p — so these pin the selection/proxy semantics with loopback instances)."""
+import asyncio
+import json
+import threading
+import time
+import urllib.request
+
+import pytest
+
+from localai_tfp_amd import p2p as P
+
+
+def test_registry_liveness_and_token():
+    r = P.Registry("tok", "net")
+    r.add(P.NodeData(id="a", address="127.0.0.1:1"))
+    r.add(P.NodeData(id="b", address="127.0.0.1:2"))
+    r._nodes["net_federated"]["b"].last_seen = time.time() - 41
+    assert [n.id for n in r.nodes("federated") if n.is_online()] == ["a"]
+    assert r.authorised("Bearer tok") and not r.authorised("Bearer nope") and not r.authorised(None)
+    assert P.network_id("", "worker") == "worker" and P.network_id("n", "worker") == "n_worker"
+
+
+def test_least_used_and_target_selection():
+    r = P.Registry()
+    for i in "abc":
+        r.add(P.NodeData(id=i, address="127.0.0.1:1"))
+    fs = P.FederatedServer("127.0.0.1:0", r, load_balanced=True)
+    seen = []
+    for _ in range(6):
+        n = fs.pick()
+        fs.record_request(n)
+        seen.append(n)
+    assert sorted(seen) == ["a", "a", "b", "b", "c", "c"]
+    r._nodes["federated"]["a"].last_seen = 0  # offline nodes leave the table
+    assert fs.pick() in ("b", "c") and "a" not in fs.request_table
+    assert P.FederatedServer("x:1", r, worker_target="zz").pick() == "zz"
+    assert P.FederatedServer("x:1", P.Registry()).pick() == ""
+
+
+def _serve_http(body: bytes):
+    import http.server
+
+    class H(http.server.BaseHTTPRequestHandler):
+        def do_GET(self):
+            self.send_response(200)
+            self.send_header("Content-Length", str(len(body)))
+            self.end_headers()
+            self.wfile.write(body)
+
+        def log_message(self, *a):
+            pass
+    srv = http.server.ThreadingHTTPServer(("127.0.0.1", 0), H)
+    threading.Thread(target=srv.serve_forever, daemon=True).start()
+    return srv
+
+
+def test_proxy_register_forward_and_503():
+    backends = [_serve_http(b"node-%d" % i) for i in range(2)]
+    reg = P.Registry("secret")
+    fs = P.FederatedServer("127.0.0.1:0", reg, load_balanced=True)
+    loop = asyncio.new_event_loop()
+    srv = loop.run_until_complete(fs.start())
+    port = srv.sockets[0].getsockname()[1]
+    threading.Thread(target=loop.run_forever, daemon=True).start()
+    base = f"http://127.0.0.1:{port}"
+    try:
+        with pytest.raises(urllib.error.HTTPError) as e:
+            urllib.request.urlopen(base + "/v1/models", timeout=5)
+        assert e.value.code == 503
+        bad = P.Announcer(P.NodeData(id="x", address="127.0.0.1:1"), [base], "wrong")
+        assert bad.announce_once() == 0
+        for i, b in enumerate(backends):
+            a = P.Announcer(P.NodeData(id=f"n{i}", address=f"127.0.0.1:{b.server_address[1]}"), [base], "secret")
+            assert a.announce_once() == 1
+        listing = json.loads(urllib.request.urlopen(base + "/api/p2p", timeout=5).read())
+        assert sorted(n["id"] for n in listing["federated_nodes"]) == ["n0", "n1"]
+        got = {urllib.request.urlopen(base + "/v1/models", timeout=5).read() for _ in range(4)}
+        assert got == {b"node-0", b"node-1"}  # least-used alternates between the two nodes
+    finally:
+        loop.call_soon_threadsafe(srv.close)
+        for b in backends:
+            b.shutdown()
+
+
+def test_gateway_register_route(tmp_path):
+    from fastapi.testclient import TestClient
+
+    from localai_tfp_amd.config.app_config import ApplicationConfig
+    from localai_tfp_amd.gateway.app import create_app
+    cfg = ApplicationConfig(models_path=str(tmp_path), generated_content_dir=str(tmp_path / "g"),
+                            upload_dir=str(tmp_path / "u"), config_dir=str(tmp_path / "c"), api_keys=[],
+                            p2p=True, p2p_token="t0k")
+    app = create_app(cfg, inproc=True)
+    with TestClient(app) as c:
+        assert c.post("/api/p2p/register", json={"id": "w1", "address": "127.0.0.1:9"},
+                      headers={"Authorization": "Bearer bad"}).status_code == 401
+        assert c.post("/api/p2p/register", json={"id": "w1", "address": "127.0.0.1:9"},
+                      headers={"Authorization": "Bearer t0k"}).status_code == 200
+        j = c.get("/api/p2p").json()
+        assert [n["id"] for n in j["nodes"]] == ["w1"] and j["nodes"][0]["online"]
+        assert c.get("/api/p2p/token").text == "t0k"
+    app.state.localai.shutdown()
