@@ -368,6 +368,16 @@ class LLMEngine:
             off += it.n
         plan = {"nd": nd, "tokens": tokens, "positions": positions, "slots": slots,
                 "lidx": np.asarray(lidx, np.int32), "keep_hidden": False}
+        mm = []
+        row = nd
+        for it in pf:  # multimodal spans intersecting this chunk -> (row in T, embedding rows)
+            for p0, emb in it.seq.req.mm_embeds:
+                lo, hi = max(p0, it.start), min(p0 + emb.shape[0], it.start + it.n)
+                if lo < hi:
+                    mm.append((row + lo - it.start, emb[lo - p0:hi - p0]))
+            row += it.n
+        if mm:
+            plan["mm"] = mm
         if nd:
             maxb = max(len(it.seq.blocks) for it in dec)
             bt = np.zeros((nd, maxb), np.int32)
@@ -445,6 +455,7 @@ class LLMEngine:
             fb.pf_q_lens_host = [int(cu[k + 1] - cu[k]) for k in range(len(cu) - 1)]
             fb.pf_ctx_lens_host = [int(x) for x in plan["pf_ctx"]]
         fb.keep_hidden = bool(plan.get("keep_hidden"))
+        fb.embed_rows = plan.get("mm")
         return fb
 
     # ------------------------------------------------------------------ tensor-parallel follower

@@ -167,6 +167,8 @@ class Scheduler:
         for item in sched.decode + sched.prefill:
             s = item.seq
             s.num_computed = item.start + item.n
+            if not s.req.cache_prompt:  # e.g. image placeholders: token ids do not identify the KV
+                continue
             ids = None
             nfull = s.num_computed // self.bs
             while len(s.block_hashes) < nfull:

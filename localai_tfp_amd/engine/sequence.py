@@ -31,6 +31,9 @@ class Request:
     rid: int = field(default_factory=lambda: next(_ids))
     arrival: float = field(default_factory=time.perf_counter)
     cache_prompt: bool = True
+    # multimodal: (prompt position, fp32 [n, hidden] device tensor) spans whose input embeddings
+    # replace the placeholder tokens there (llava image embeddings, grpc-server.cpp:1455-1520)
+    mm_embeds: list = field(default_factory=list)
 
 
 @dataclass

@@ -69,6 +69,7 @@ class ForwardBatch:
     pf_ctx_lens_host: list = field(default_factory=list)
     want_hidden: bool = False  # embeddings: return normalised hidden rows instead of logits
     keep_hidden: bool = False  # also stash the final-normed hidden rows in model.last_hidden
+    embed_rows: list | None = None  # [(row, fp32 [n, hidden])] input embeddings replacing token rows
 
     @property
     def T(self) -> int:
@@ -295,6 +296,9 @@ class LlamaModel:
         nd = fb.n_decode
         h = ws.h[:T]
         self.embed(fb.tokens, h)
+        if fb.embed_rows:
+            for r0, e in fb.embed_rows:
+                h[r0:r0 + e.shape[0]].copy_(e)
         xb = ws.xb[:T, :H]
         for li, L in enumerate(self.layers):
             kc, vc = kv.layer(li)

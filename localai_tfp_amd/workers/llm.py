@@ -137,6 +137,7 @@ class LLMServicer(BackendServicer):
         self._channels: dict = {}
         self.mxstream = None  # serving.mxstream.StreamServer once a model is loaded
         self.embeddings_enabled = False
+        self.vision = None  # models.vision.ClipVision when ModelOptions.MMProj is set
         self.state = pb.STATE_UNINITIALIZED
 
     # ---------------------------------------------------------------- load
@@ -209,6 +210,16 @@ class LLMServicer(BackendServicer):
                 model, tok, mcfg, _ = load_llm(path, self.device, self.tp.rank, self.tp.world, None, ov)
             else:
                 model, tok, mcfg, _ = load_llm(path, self.device, overrides=ov)
+            self.vision = None
+            if request.MMProj:
+                from ..models.vision import load_mmproj
+                mp = request.MMProj
+                if not mp.startswith("synthetic:") and not os.path.isabs(mp) and request.ModelPath:
+                    mp = os.path.join(request.ModelPath, mp)
+                self.vision = load_mmproj(mp, self.device)
+                if self.vision.cfg.proj_hidden != mcfg.hidden:
+                    raise ValueError(f"mmproj projects to {self.vision.cfg.proj_hidden} but the LLM hidden size is "
+                                     f"{mcfg.hidden}; make sure that you use the correct mmproj file")
             self.engine = LLMEngine(model, tok, ec, tp=self.tp)
             if not opts.get("lazy_graphs"):
                 self.engine.precapture_graphs()
@@ -234,15 +245,46 @@ class LLMServicer(BackendServicer):
         if self.engine is None:
             context.abort(grpc.StatusCode.FAILED_PRECONDITION, "model not loaded")
 
-    def _prompt_ids(self, r) -> list[int]:
+    def _prompt_text(self, r) -> tuple[str, bool]:
+        """-> (prompt text, whether BOS/special tokens still need adding)."""
         if r.UseTokenizerTemplate and len(r.Messages) and getattr(self.tok, "chat_template", None):
             from ..templates.chat import render_chat
             msgs = [{"role": m.role, "content": m.content} for m in r.Messages]
-            text = render_chat(msgs, self.tok, add_generation_prompt=True)
-            return self.tok.encode(text, add_special=False)
-        if len(r.EmbeddingTokens) and not r.Prompt:
+            return render_chat(msgs, self.tok, add_generation_prompt=True), False
+        return r.Prompt, True
+
+    def _prompt_ids(self, r) -> list[int]:
+        if len(r.EmbeddingTokens) and not r.Prompt and not (r.UseTokenizerTemplate and len(r.Messages)):
             return list(r.EmbeddingTokens)
-        return self.tok.encode(r.Prompt, add_special=True)
+        text, special = self._prompt_text(r)
+        return self.tok.encode(text, add_special=special)
+
+    def _mm_prompt(self, r) -> tuple[list[int], list]:
+        """Images: encode with the CLIP tower + projector and splice the embeddings where the prompt
+        has `[img-N]` (grpc-server.cpp:900-944; without markers the images precede the prompt, as
+        the reference's input_suffix handling does). Placeholder rows use token id 0."""
+        from ..models.vision import split_prompt
+        text, special = self._prompt_text(r)
+        imgs = list(r.Images)
+        parts = split_prompt(text, len(imgs))
+        if len(parts) == 1 and imgs:  # no markers: images first, then the prompt
+            parts = [""]
+            for i in range(len(imgs)):
+                parts += [i, ""]
+            parts[-1] = text
+        embs = self.vision.embed_images(imgs)
+        ids: list[int] = []
+        mm = []
+        first = True
+        for part in parts:
+            if isinstance(part, int):
+                e = embs[part]
+                mm.append((len(ids), e))
+                ids.extend([0] * e.shape[0])
+            else:
+                ids.extend(self.tok.encode(part, add_special=special and first) if (part or first) else [])
+            first = False
+        return ids, mm
 
     def _grammar(self, gbnf: str):
         from ..runtime_native import GrammarMatcher, NativeGrammar, NativeVocab
@@ -266,17 +308,24 @@ class LLMServicer(BackendServicer):
         return make
 
     def _request(self, r) -> Request:
-        ids = self._prompt_ids(r)
+        mm = []
+        if len(r.Images) and self.vision is not None:
+            if self.tp is not None:
+                raise ValueError("images with a tensor-parallel LLM worker are not supported")
+            ids, mm = self._mm_prompt(r)
+        else:
+            ids = self._prompt_ids(r)
         mt = int(r.Tokens)
         max_tokens = mt if mt > 0 else self.engine.cfg.max_model_len
         req = Request(ids, sampling_from_predict(r), max_tokens, [s for s in r.StopPrompts if s])
-        req.cache_prompt = True
+        req.cache_prompt = not mm  # image placeholders must not enter the prefix cache (reference: same)
+        req.mm_embeds = mm
         req.n_keep = int(r.NKeep) if r.NKeep > 0 else 0
         if r.Grammar:
             req.grammar = self._grammar(r.Grammar)
-        if len(r.Images) or len(r.Videos) or len(r.Audios):
-            log.warning("multimodal inputs are not supported by the LLM worker; ignoring %d images",
-                        len(r.Images))
+        if (len(r.Images) and self.vision is None) or len(r.Videos) or len(r.Audios):
+            log.warning("ignoring %d images / %d videos / %d audios: this model has no multimodal projector",
+                        len(r.Images), len(r.Videos), len(r.Audios))
         return req
 
     @staticmethod
