@@ -297,6 +297,22 @@ def cmd_federated(a):
     return 0
 
 
+def cmd_explorer(a):
+    """`local-ai explorer` (core/cli/explorer.go): network directory + discovery loop."""
+    import uvicorn
+    from .p2p.explorer import Database, DiscoveryServer, create_explorer_app
+    db = Database(a.pool_database)
+    ds = DiscoveryServer(db, a.connection_timeout, a.connection_error_threshold)
+    if a.only_sync:
+        ds.run_once()
+        return 0
+    if a.with_sync:
+        ds.start()
+    host, _, port = a.address.rpartition(":")
+    uvicorn.run(create_explorer_app(db), host=host or "0.0.0.0", port=int(port))
+    return 0
+
+
 def cmd_worker(a):
     from . import workers as W
     import importlib
@@ -356,6 +372,13 @@ def main(argv=None):
     fd.add_argument("--target-worker", default=os.environ.get("LOCALAI_TARGET_WORKER", ""))
     fd.add_argument("--nodes", default=os.environ.get("LOCALAI_FEDERATED_NODES", ""),
                     help="static nodes: id=host:port,...")
+    ex = sub.add_parser("explorer", help="run the p2p network explorer")
+    ex.add_argument("--address", default=os.environ.get("LOCALAI_ADDRESS", "0.0.0.0:8080"))
+    ex.add_argument("--pool-database", default=os.environ.get("LOCALAI_POOL_DATABASE", "explorer.json"))
+    ex.add_argument("--connection-timeout", type=float, default=50.0)
+    ex.add_argument("--connection-error-threshold", type=int, default=3)
+    ex.add_argument("--with-sync", action="store_true")
+    ex.add_argument("--only-sync", action="store_true")
     w = sub.add_parser("worker", help="run a single backend worker process")
     w.add_argument("kind", help="backend name, e.g. llama-cpp, whisper, bert-embeddings")
     w.add_argument("--addr", default="127.0.0.1:50051")
@@ -364,7 +387,7 @@ def main(argv=None):
                         format="%(asctime)s %(levelname)s %(name)s: %(message)s")
     fn = {"run": cmd_run, "models": cmd_models, "tts": cmd_tts, "transcript": cmd_transcript,
           "sound-generation": cmd_sound, "util": cmd_util, "worker": cmd_worker,
-          "federated": cmd_federated}.get(a.cmd)
+          "federated": cmd_federated, "explorer": cmd_explorer}.get(a.cmd)
     if fn is None:
         ap.print_help()
         return 1

@@ -102,3 +102,39 @@ def test_gateway_register_route(tmp_path):
         assert [n["id"] for n in j["nodes"]] == ["w1"] and j["nodes"][0]["online"]
         assert c.get("/api/p2p/token").text == "t0k"
     app.state.localai.shutdown()
+
+
+def test_explorer_db_discovery_and_routes(tmp_path):
+    from fastapi.testclient import TestClient
+
+    from localai_tfp_amd.p2p import explorer as X
+    backend = _serve_http(b"x")
+    reg = P.Registry("k3y")
+    fs = P.FederatedServer("127.0.0.1:0", reg)
+    loop = asyncio.new_event_loop()
+    srv = loop.run_until_complete(fs.start())
+    threading.Thread(target=loop.run_forever, daemon=True).start()
+    fed = f"http://127.0.0.1:{srv.sockets[0].getsockname()[1]}"
+    try:
+        db = X.Database(str(tmp_path / "pool.json"))
+        c = TestClient(X.create_explorer_app(db))
+        good = X.make_network_token(fed, "k3y")
+        dead = X.make_network_token("http://127.0.0.1:9", "k")
+        assert c.post("/network/add", json={"token": good, "name": "n"}).status_code == 400  # description missing
+        assert c.post("/network/add", json={"token": "***", "name": "n", "description": "d"}).json()["error"] == "Invalid token"
+        for t in (good, dead):
+            assert c.post("/network/add", json={"token": t, "name": "n", "description": "d"}).status_code == 200
+        assert c.post("/network/add", json={"token": good, "name": "n", "description": "d"}).status_code == 400
+        assert c.get("/networks").json() == []  # no workers seen yet
+        P.Announcer(P.NodeData(id="w0", address=f"127.0.0.1:{backend.server_address[1]}", service="worker"),
+                    [fed], "k3y").announce_once()
+        ds = X.DiscoveryServer(db, 5, 1)
+        ds.run_once()
+        nets = c.get("/networks").json()
+        assert len(nets) == 1 and nets[0]["token"] == good and nets[0]["Clusters"][0]["Workers"] == ["w0"]
+        ds.run_once()  # the dead network exceeds the failure threshold and is removed
+        assert db.token_list() == [good]
+        assert c.get("/", headers={"content-type": "application/json"}).json()["Version"]
+    finally:
+        loop.call_soon_threadsafe(srv.close)
+        backend.shutdown()
