@@ -62,63 +62,75 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restri
 #pragma unroll
         for (int j = 0; j < 8; ++j) o[h][j] = 0.f;
     }
+    // The partition's block ids are staged in LDS once (no dependent global load in front of every
+    // K/V fetch), and K/V are double-buffered in registers: the loads of step i+1 are in flight
+    // while step i is scored, so each lane keeps 2*U 16-byte loads outstanding (memory-level
+    // parallelism is what bounds this kernel, not VALU).
+    constexpr int MAXB = 256;  // part_size / bs + 1 <= MAXB (host checks)
+    __shared__ int sbt[MAXB];
     const int* bt = block_tables + (size_t)b * bt_stride;
-    // U positions per lane group per iteration: all 2U 16-byte K/V loads are issued before any of
-    // them is consumed (memory-level parallelism), then one online-softmax update covers U keys.
-    constexpr int U = 4;
-    for (int base = p0; base < p1; base += PPB * U) {
-        uint4 kr[U], vr[U];
-        bool valid[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int p = base + u * PPB + wave * PPW + pg;
-            valid[u] = p < p1;
-            if (valid[u]) {
-                const int blk = bt[p / bs], off = p % bs;
-                const size_t eo = (((size_t)blk * Hkv + kvh) * bs + off) * D + dl * 8;
-                kr[u] = *(const uint4*)(kc + eo);
-                vr[u] = *(const uint4*)(vc + eo);
-            } else {
-                kr[u] = vr[u] = make_uint4(0, 0, 0, 0);
-            }
-        }
-#pragma unroll
-        for (int h = 0; h < G; ++h) {
-            float s[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const uint32_t kw[4] = {kr[u].x, kr[u].y, kr[u].z, kr[u].w};
-                float acc = 0.f;
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    acc = fmaf(qf[h][2 * j], __uint_as_float(kw[j] << 16), acc);
-                    acc = fmaf(qf[h][2 * j + 1], __uint_as_float(kw[j] & 0xFFFF0000u), acc);
-                }
-                s[u] = group_sum<LPP>(acc);
-                if (!valid[u]) s[u] = -INFINITY;
-            }
-            float mx = m[h];
-#pragma unroll
-            for (int u = 0; u < U; ++u) mx = fmaxf(mx, s[u]);
-            if (mx == -INFINITY) continue;  // nothing valid for this lane group yet
-            const float a = exp2f(m[h] - mx);
-            l[h] *= a;
-#pragma unroll
-            for (int j = 0; j < 8; ++j) o[h][j] *= a;
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const float pr = exp2f(s[u] - mx);  // invalid -> exp2(-inf) = 0
-                l[h] += pr;
-                const uint32_t vw[4] = {vr[u].x, vr[u].y, vr[u].z, vr[u].w};
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    o[h][2 * j] = fmaf(pr, __uint_as_float(vw[j] << 16), o[h][2 * j]);
-                    o[h][2 * j + 1] = fmaf(pr, __uint_as_float(vw[j] & 0xFFFF0000u), o[h][2 * j + 1]);
-                }
-            }
-            m[h] = mx;
-        }
+    const int blk0 = p0 / bs;
+    const int nblk = p1 > p0 ? (p1 - 1) / bs - blk0 + 1 : 0;
+    for (int i = threadIdx.x; i < nblk; i += 256) sbt[i] = bt[blk0 + i];
+    __syncthreads();
+    constexpr int U = 2;
+    constexpr int STEP = PPB * U;
+    // two register buffers with compile-time names (a runtime buffer index, or arrays passed by
+    // reference to helpers, would put them in scratch): the step is a macro over (K, V)
+    u32x4 ka[U], va[U], kb[U], vb[U];
+#define DEC_LOAD(K, V, BASE)                                                                  \
+    _Pragma("unroll") for (int u = 0; u < U; ++u) {                                           \
+        const int p = (BASE) + u * PPB + wave * PPW + pg;                                     \
+        if (p < p1) {                                                                         \
+            const int blk = sbt[p / bs - blk0], off = p % bs;                                 \
+            const size_t eo = (((size_t)blk * Hkv + kvh) * bs + off) * D + dl * 8;            \
+            K[u] = __builtin_nontemporal_load((const u32x4*)(kc + eo));                       \
+            V[u] = __builtin_nontemporal_load((const u32x4*)(vc + eo));                       \
+        } else {                                                                              \
+            K[u] = V[u] = (u32x4){0u, 0u, 0u, 0u};                                            \
+        }                                                                                     \
     }
+#define DEC_CONSUME(K, V, BASE)                                                               \
+    _Pragma("unroll") for (int h = 0; h < G; ++h) {                                           \
+        float s[U];                                                                           \
+        _Pragma("unroll") for (int u = 0; u < U; ++u) {                                       \
+            float acc = 0.f;                                                                  \
+            _Pragma("unroll") for (int j = 0; j < 4; ++j) {                                   \
+                const uint32_t kw = K[u][j];                                                  \
+                acc = fmaf(qf[h][2 * j], __uint_as_float(kw << 16), acc);                     \
+                acc = fmaf(qf[h][2 * j + 1], __uint_as_float(kw & 0xFFFF0000u), acc);         \
+            }                                                                                 \
+            s[u] = group_sum<LPP>(acc);                                                       \
+            if ((BASE) + u * PPB + wave * PPW + pg >= p1) s[u] = -INFINITY;                   \
+        }                                                                                     \
+        float mx = m[h];                                                                      \
+        _Pragma("unroll") for (int u = 0; u < U; ++u) mx = fmaxf(mx, s[u]);                  \
+        if (mx != -INFINITY) {                                                                \
+            const float a = exp2f(m[h] - mx);                                                 \
+            l[h] *= a;                                                                        \
+            _Pragma("unroll") for (int j = 0; j < 8; ++j) o[h][j] *= a;                       \
+            _Pragma("unroll") for (int u = 0; u < U; ++u) {                                   \
+                const float pr = exp2f(s[u] - mx);                                            \
+                l[h] += pr;                                                                   \
+                _Pragma("unroll") for (int j = 0; j < 4; ++j) {                               \
+                    const uint32_t vw = V[u][j];                                              \
+                    o[h][2 * j] = fmaf(pr, __uint_as_float(vw << 16), o[h][2 * j]);           \
+                    o[h][2 * j + 1] = fmaf(pr, __uint_as_float(vw & 0xFFFF0000u), o[h][2 * j + 1]); \
+                }                                                                             \
+            }                                                                                 \
+            m[h] = mx;                                                                        \
+        }                                                                                     \
+    }
+    if (p0 < p1) { DEC_LOAD(ka, va, p0) }
+    for (int base = p0; base < p1; base += 2 * STEP) {
+        if (base + STEP < p1) { DEC_LOAD(kb, vb, base + STEP) }
+        DEC_CONSUME(ka, va, base)
+        if (base + STEP >= p1) break;
+        if (base + 2 * STEP < p1) { DEC_LOAD(ka, va, base + 2 * STEP) }
+        DEC_CONSUME(kb, vb, base + STEP)
+    }
+#undef DEC_LOAD
+#undef DEC_CONSUME
     // merge the PPW position groups of the wave (xor over lane offsets LPP, 2LPP, ...)
 #pragma unroll
     for (int off = LPP; off < 64; off <<= 1) {
@@ -217,6 +229,7 @@ extern "C" int mxk_attn_decode(const bf16_t* q, int q_stride, const bf16_t* kc, 
     if (Hq % Hkv) return (int)hipErrorInvalidValue;
     const int G = Hq / Hkv;
     if (n_parts > 1 && (!part_ml || !part_o)) return (int)hipErrorInvalidValue;
+    if (bs <= 0 || part_size / bs + 1 > 256) return (int)hipErrorInvalidValue;  // LDS block-id stage
 #define DEC(D_, G_) \
     if (D == D_ && G == G_) return launch_decode<D_, G_>(q, q_stride, kc, vc, bt, bt_stride, seq_lens, B, Hkv, bs, scale, part_size, n_parts, out, out_stride, part_ml, part_o, st);
     DEC(128, 1) DEC(128, 2) DEC(128, 3) DEC(128, 4) DEC(128, 5) DEC(128, 6) DEC(128, 7) DEC(128, 8)

@@ -1,0 +1,185 @@
+"""Text-to-image / image-to-image for UNet (epsilon-prediction) models: SD 1.x / 2.x (one CLIP
+text encoder) and SDXL (CLIP-L + CLIP-G, pooled text embedding + size/crop time ids). Reference:
+the diffusers backend's StableDiffusionPipeline / StableDiffusionXLPipeline
+(backend/python/diffusers/backend.py:169-191) and sd.cpp's txt2img (gosd.cpp:164-226: cfg scale,
+steps, seed, sampler / schedule, CLIP skip).
+
+Sampling uses the shared k-diffusion samplers over the discrete DDPM schedule (samplers.EpsSchedule):
+x_in = x / sqrt(sigma^2 + 1), t = t(sigma), x0 = x - sigma * eps; classifier-free guidance runs the
+positive and negative branches as one batch of 2 through the UNet, and the text context's
+cross-attention K/V are computed once per generation (unet.py).
+"""
+from __future__ import annotations
+
+import json
+import math
+import os
+from dataclasses import dataclass
+
+import torch
+import torch.nn.functional as F
+
+from ...tokenizer.clip import CLIPTokenizer
+from . import samplers as S
+from .nn import cast_module, init_synthetic
+from .pipeline import GenParams
+from .text_encoders import CLIP_G, CLIP_L, CLIPTextConfig, CLIPTextEncoder
+from .unet import SD15_UNET, SDXL_UNET, UNET_TEST, UNET_XL_TEST, UNet2DConditionModel, UNetConfig, config_from_diffusers
+from .vae import VAE_SD15, AutoencoderKL, VAEConfig
+
+
+@dataclass
+class UNetPreset:
+    unet: UNetConfig
+    clip_l: CLIPTextConfig
+    clip_g: CLIPTextConfig | None  # SDXL second encoder
+    vae: VAEConfig
+    default_size: int = 512
+
+
+_T_L = CLIPTextConfig(vocab=600, hidden=32, layers=2, heads=2, ffn=64, proj=32)
+_T_G = CLIPTextConfig(vocab=600, hidden=16, layers=2, heads=2, ffn=32, act="gelu", proj=32)
+_VAE4_TEST = VAEConfig(latent=4, channels=(32, 32, 64, 64), layers=1, groups=8, scaling=0.18215, shift=0.0,
+                       quant_conv=True)
+PRESETS = {
+    "sd15": UNetPreset(SD15_UNET, CLIP_L, None, VAE_SD15, 512),
+    "sdxl": UNetPreset(SDXL_UNET, CLIP_L, CLIP_G, VAEConfig(latent=4, scaling=0.13025, shift=0.0, quant_conv=True),
+                       1024),
+    "sd15-test": UNetPreset(UNET_TEST, _T_L, None, _VAE4_TEST, 64),
+    "sdxl-test": UNetPreset(UNET_XL_TEST, _T_L, _T_G, _VAE4_TEST, 64),
+}
+
+
+class UNetPipeline:
+    def __init__(self, preset: UNetPreset, unet: UNet2DConditionModel, te1: CLIPTextEncoder,
+                 te2: CLIPTextEncoder | None, vae: AutoencoderKL, tok1: CLIPTokenizer, tok2: CLIPTokenizer | None,
+                 device):
+        self.p = preset
+        self.unet, self.te1, self.te2, self.vae = unet, te1, te2, vae
+        self.tok1, self.tok2 = tok1, tok2
+        self.device = torch.device(device)
+        self.sched = S.EpsSchedule()
+
+    @property
+    def xl(self) -> bool:
+        return self.te2 is not None
+
+    # ------------------------------------------------------------------ construction
+    @classmethod
+    def synthetic(cls, name: str, device, dtype=None, seed: int = 0) -> "UNetPipeline":
+        pr = PRESETS[name]
+        dev = torch.device(device)
+        dtype = dtype or (torch.float16 if dev.type == "cuda" else torch.float32)
+
+        def build(mod, s):
+            with torch.device(dev):
+                m = mod()
+            init_synthetic(m, seed + s)
+            return cast_module(m, dev, dtype).eval()
+        un = build(lambda: UNet2DConditionModel(pr.unet), 1)
+        t1 = build(lambda: CLIPTextEncoder(pr.clip_l, with_projection=False), 2)
+        t2 = build(lambda: CLIPTextEncoder(pr.clip_g), 3) if pr.clip_g is not None else None
+        vae = build(lambda: AutoencoderKL(pr.vae), 4)
+        tk1 = CLIPTokenizer.synthetic(pr.clip_l.vocab)
+        tk2 = CLIPTokenizer.synthetic(pr.clip_g.vocab, pad_token="!") if pr.clip_g is not None else None
+        return cls(pr, un, t1, t2, vae, tk1, tk2, dev)
+
+    @classmethod
+    def from_diffusers(cls, d: str, device, dtype=None) -> "UNetPipeline":
+        """diffusers-layout SD1.x / SD2.x / SDXL directory (unet/, vae/, text_encoder[_2]/, tokenizer[_2]/)."""
+        from safetensors.torch import load_file
+        dev = torch.device(device)
+        dtype = dtype or (torch.float16 if dev.type == "cuda" else torch.float32)
+
+        def cfg_of(sub):
+            with open(os.path.join(d, sub, "config.json")) as f:
+                return json.load(f)
+
+        def load(m, sub):
+            sd = {}
+            for fn in sorted(os.listdir(os.path.join(d, sub))):
+                if fn.endswith(".safetensors"):
+                    sd.update(load_file(os.path.join(d, sub, fn)))
+            missing, unexpected = m.load_state_dict(sd, strict=False)
+            missing = [k for k in missing if "position_ids" not in k]
+            if missing:
+                raise ValueError(f"{sub}: missing weights {missing[:5]}")
+            return cast_module(m, dev, dtype).eval()
+        uc = config_from_diffusers(cfg_of("unet"))
+        un = load(UNet2DConditionModel(uc), "unet")
+
+        def clip(sub, proj):
+            c = cfg_of(sub)
+            cc = CLIPTextConfig(vocab=c["vocab_size"], hidden=c["hidden_size"], layers=c["num_hidden_layers"],
+                                heads=c["num_attention_heads"], ffn=c["intermediate_size"],
+                                max_pos=c["max_position_embeddings"], act=c.get("hidden_act", "quick_gelu"),
+                                proj=c.get("projection_dim", c["hidden_size"]), eps=c.get("layer_norm_eps", 1e-5))
+            return load(CLIPTextEncoder(cc, with_projection=proj), sub)
+        xl = os.path.isdir(os.path.join(d, "text_encoder_2"))
+        t1 = clip("text_encoder", False)
+        t2 = clip("text_encoder_2", True) if xl else None
+        vc = cfg_of("vae")
+        vae = load(AutoencoderKL(VAEConfig(latent=vc["latent_channels"], channels=tuple(vc["block_out_channels"]),
+                                           layers=vc["layers_per_block"], groups=vc.get("norm_num_groups", 32),
+                                           scaling=vc.get("scaling_factor", 0.18215), shift=vc.get("shift_factor") or 0.0,
+                                           quant_conv=vc.get("use_quant_conv", True))), "vae")
+        tk1 = CLIPTokenizer.from_dir(os.path.join(d, "tokenizer"))
+        tk2 = CLIPTokenizer.from_dir(os.path.join(d, "tokenizer_2"), pad_token="!") if xl else None
+        pr = UNetPreset(uc, t1.cfg, t2.cfg if t2 is not None else None, vae.cfg, uc.sample_size * 8)
+        return cls(pr, un, t1, t2, vae, tk1, tk2, dev)
+
+    # ------------------------------------------------------------------ conditioning
+    @torch.no_grad()
+    def encode_prompts(self, prompts: list[str], clip_skip: int = 0):
+        dev = self.device
+        i1 = torch.tensor([self.tok1(p) for p in prompts], device=dev)
+        if not self.xl:
+            # SD1.x/2.x: last hidden state through the final LayerNorm (clip_skip N: layer -(N+1), normed)
+            h, _ = self.te1(i1, self.tok1.eos, max(0, clip_skip - 1) if clip_skip > 1 else 0)
+            if clip_skip > 1:
+                tm = self.te1.text_model
+                h = F.layer_norm(h, (h.shape[-1],), tm.final_layer_norm.weight.float(),
+                                 tm.final_layer_norm.bias.float(), self.te1.cfg.eps)
+            return h, None
+        # SDXL: penultimate hidden states of both encoders (no final LN), pooled from CLIP-G
+        skip = 1 + max(0, clip_skip - 1)
+        h1, _ = self.te1(i1, self.tok1.eos, skip)
+        i2 = torch.tensor([self.tok2(p) for p in prompts], device=dev)
+        h2, pooled = self.te2(i2, self.tok2.eos, skip)
+        return torch.cat([h1, h2], -1), pooled
+
+    # ------------------------------------------------------------------ generation
+    @torch.no_grad()
+    def generate(self, prompt: str, gp: GenParams, init_image: torch.Tensor | None = None) -> torch.Tensor:
+        """-> image [3, H, W] in [0, 1] (fp32, CPU)."""
+        dev = self.device
+        W, H = (gp.width // 8) * 8, (gp.height // 8) * 8
+        ctx, pooled = self.encode_prompts([prompt, gp.negative], gp.extra.get("clip_skip", 0))
+        gen = torch.Generator(device=dev).manual_seed(int(gp.seed) & 0x7FFFFFFFFFFFFFFF)
+        shape = (1, self.p.unet.in_channels, H // 8, W // 8)
+        sig = S.get_sigmas(self.sched, gp.steps, gp.schedule)
+        noise = torch.randn(shape, generator=gen, device=dev, dtype=torch.float32)
+        if init_image is not None:
+            x0 = self.vae.encode(init_image.to(dev)[None] * 2 - 1)
+            x0 = F.interpolate(x0, size=shape[2:], mode="bilinear") if x0.shape[2:] != shape[2:] else x0
+            k = min(len(sig) - 2, int(round((1 - gp.strength) * (len(sig) - 1))))
+            sig = sig[k:]
+            x = x0 + noise * sig[0]
+        else:
+            x = noise * sig[0]
+        cfg = float(gp.cfg_scale)
+        added = None
+        if self.xl:
+            tid = torch.tensor([[H, W, 0, 0, H, W]], dtype=torch.float32, device=dev)
+            added = {"text_embeds": pooled, "time_ids": tid.expand(2, 6)}
+        ctx_key = ctx
+
+        def denoise(xt: torch.Tensor, sigma: float) -> torch.Tensor:
+            xin = torch.cat([xt, xt]) / math.sqrt(sigma * sigma + 1.0)
+            t = torch.full((2,), self.sched.t_of(sigma), device=dev)
+            eps = self.unet(xin, t, ctx, added, ctx_key)
+            e = eps[1:] + cfg * (eps[:1] - eps[1:])
+            return xt - sigma * e
+        x = S.sample(denoise, x, sig, gp.sampler, flow=False, generator=gen)
+        img = self.vae.decode(x)[0]
+        return ((img + 1) / 2).clamp(0, 1).cpu()

@@ -253,10 +253,15 @@ def dense_min_m(dtype, epi: int = EPI_ADD_F32, can_split: bool = True) -> int:
     if dtype != torch.float16:
         return 128
     if epi == EPI_SWIGLU:
-        return 96
+        return DENSE_MIN_M_SWIGLU
     if not can_split:
-        return 48
-    return 320
+        return DENSE_MIN_M_NOSPLIT
+    return DENSE_MIN_M_SPLIT
+
+
+DENSE_MIN_M_SWIGLU = int(os.environ.get("MX_DENSE_MIN_M_SWIGLU", "96"))
+DENSE_MIN_M_NOSPLIT = int(os.environ.get("MX_DENSE_MIN_M_NOSPLIT", "48"))
+DENSE_MIN_M_SPLIT = int(os.environ.get("MX_DENSE_MIN_M_SPLIT", "320"))
 
 
 Q32_MIN_M = int(os.environ.get("MX_Q32_MIN_M", "48"))

@@ -1,8 +1,9 @@
 """Image generation worker: the reference's `stablediffusion-ggml` (sd.cpp, gosd.cpp/gosd.go) and
 `diffusers` backends behind one GenerateImage RPC.
 
-LoadModel: a diffusers-layout SD3 directory, or `synthetic:sd3-medium | sd3-medium-no-t5 | sd3-test`
-(random-init weights). ModelOptions.Options ("key:value", as gosd.cpp:56-162 parses them):
+LoadModel: a diffusers-layout SD3 directory (MMDiT) or SD1.x / SD2.x / SDXL directory (UNet), or
+`synthetic:sd3-medium | sd3-medium-no-t5 | sd3-test | sd15 | sdxl | sd15-test | sdxl-test` (random-init
+weights). ModelOptions.Options ("key:value", as gosd.cpp:56-162 parses them):
   sampler:<euler|euler_a|heun|dpm2|dpm++2s_a|dpm++2m|dpm++2mv2|ipndm|ipndm_v|lcm|ddim_trailing|tcd>
   scheduler:<default|discrete|karras|exponential|ays|gits>
   cfg_scale:<float>   (ModelOptions.CFGScale also honoured)
@@ -43,18 +44,25 @@ class DiffusionServicer(BackendServicer):
                 k, _, v = kv.partition(":")
                 opts[k.strip()] = v.strip()
             use_t5 = opts.get("t5", "true").lower() not in ("0", "false", "no")
+            from ..models.diffusion import sd_pipeline as U
             path = request.ModelFile or request.Model
             if path.startswith("synthetic:"):
                 name = path.split(":", 1)[1]
                 if not use_t5 and name == "sd3-medium":
                     name = "sd3-medium-no-t5"
-                self.pipe = SD3Pipeline.synthetic(name, self.device)
+                if name in U.PRESETS:  # SD1.x / SDXL UNet models
+                    self.pipe = U.UNetPipeline.synthetic(name, self.device)
+                else:
+                    self.pipe = SD3Pipeline.synthetic(name, self.device)
             else:
                 if not os.path.isabs(path) and request.ModelPath:
                     path = os.path.join(request.ModelPath, path)
                 if not os.path.isdir(path):
                     raise ValueError(f"{path}: expected a diffusers-layout model directory")
-                self.pipe = SD3Pipeline.from_diffusers(path, self.device, use_t5=use_t5)
+                if os.path.isdir(os.path.join(path, "unet")):
+                    self.pipe = U.UNetPipeline.from_diffusers(path, self.device)
+                else:
+                    self.pipe = SD3Pipeline.from_diffusers(path, self.device, use_t5=use_t5)
             self.defaults = dict(sampler=opts.get("sampler", "euler"), schedule=opts.get("scheduler", "default"),
                                  cfg_scale=float(opts.get("cfg_scale", request.CFGScale or 7.0)),
                                  strength=float(opts.get("strength", 0.75)))
