@@ -13,8 +13,12 @@
 // so the normalisation costs one extra read of the row instead of a separate kernel.
 #include "mx_common.h"
 
-template <bool NEOX, bool HAS_BIAS, bool QKN>
-__global__ __launch_bounds__(256) void rope_kv_kernel(const float* __restrict__ qkv, const float* __restrict__ bias,
+// Grid (T, NG): workgroup (t, g) handles heads [g*HPG, (g+1)*HPG) of the Hq+Hkv rotated heads and
+// its share of the Hkv V heads, so short decode batches still spread over the CUs. ZERO: after
+// reading its rows the kernel writes them back as zeros — the fp32 QKV buffer is the target of the
+// next layer's split-K GEMM (atomic accumulate), which then needs no separate zero-fill launch.
+template <bool NEOX, bool HAS_BIAS, bool QKN, bool ZERO>
+__global__ __launch_bounds__(256) void rope_kv_kernel(float* __restrict__ qkv, const float* __restrict__ bias,
                                                       const int* __restrict__ pos, const int* __restrict__ slots,
                                                       const float* __restrict__ inv_freq, float attn_factor,
                                                       int Hq, int Hkv, int D, int rot_dim, bf16_t* __restrict__ qo,
@@ -23,6 +27,10 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(const float* __restrict__ 
                                                       const float* __restrict__ kn, float eps) {
     __shared__ float cs[256], sn[256], rsh[QKN ? 256 : 1];
     const int t = blockIdx.x;
+    const int nh = Hq + Hkv;
+    const int hpg = (nh + gridDim.y - 1) / gridDim.y, vpg = (Hkv + gridDim.y - 1) / gridDim.y;
+    const int h_lo = blockIdx.y * hpg, h_hi = min(nh, h_lo + hpg);
+    const int v_lo = blockIdx.y * vpg, v_hi = min(Hkv, v_lo + vpg);
     const int p = pos[t];
     const int half = rot_dim / 2;
     for (int i = threadIdx.x; i < half; i += 256) {
@@ -32,10 +40,10 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(const float* __restrict__ 
         sn[i] = s * attn_factor;
     }
     const int W = (Hq + 2 * Hkv) * D;
-    const float* row = qkv + (size_t)t * W;
+    float* row = qkv + (size_t)t * W;
     if constexpr (QKN) {
         const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-        for (int h = wave; h < Hq + Hkv; h += 4) {
+        for (int h = h_lo + wave; h < h_hi; h += 4) {
             float ss = 0.f;
             for (int d = lane; d < D; d += 64) {
                 float x = row[h * D + d];
@@ -50,10 +58,9 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(const float* __restrict__ 
     const int slot = slots[t];
     const int blk = slot >= 0 ? slot / block_size : 0, off = slot >= 0 ? slot % block_size : 0;
     // rotate q and k heads: one thread per output element; dims >= rot_dim pass through.
-    const int nh = Hq + Hkv;
-    const int total = nh * D;
+    const int total = (h_hi - h_lo) * D;
     for (int idx = threadIdx.x; idx < total; idx += 256) {
-        const int h = idx / D, d = idx % D;
+        const int h = h_lo + idx / D, d = idx % D;
         float x = row[h * D + d];
         if (HAS_BIAS) x += bias[h * D + d];
         float nscale = 1.f;
@@ -82,31 +89,43 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(const float* __restrict__ 
             kc[(((size_t)blk * Hkv + kh) * block_size + off) * D + d] = f32_to_bf16(y);
         }
     }
+    float* vr = row + (Hq + Hkv) * D;
     if (slot >= 0) {
-        const float* vr = row + (Hq + Hkv) * D;
-        for (int idx = threadIdx.x; idx < Hkv * D; idx += 256) {
+        for (int idx = v_lo * D + threadIdx.x; idx < v_hi * D; idx += 256) {
             const int kh = idx / D, d = idx % D;
             float v = vr[idx];
             if (HAS_BIAS) v += bias[(Hq + Hkv) * D + idx];
             vc[(((size_t)blk * Hkv + kh) * block_size + off) * D + d] = f32_to_bf16(v);
         }
     }
+    if constexpr (ZERO) {
+        __syncthreads();  // every read of this group's q/k elements (incl. rotation partners) is done
+        for (int idx = h_lo * D + threadIdx.x; idx < h_hi * D; idx += 256) row[idx] = 0.f;
+        for (int idx = v_lo * D + threadIdx.x; idx < v_hi * D; idx += 256) vr[idx] = 0.f;
+    }
 }
 
-extern "C" int mxk_rope_kv(const float* qkv, const float* bias, const int* pos, const int* slots,
+extern "C" int mxk_rope_kv(float* qkv, const float* bias, const int* pos, const int* slots,
                            const float* inv_freq, float attn_factor, int T, int Hq, int Hkv, int D, int rot_dim,
                            int neox, bf16_t* qo, bf16_t* kc, bf16_t* vc, int block_size, const float* qn,
-                           const float* kn, float eps, hipStream_t st) {
+                           const float* kn, float eps, int zero_after, hipStream_t st) {
     if (T <= 0) return 0;
     if (rot_dim > 512 || (rot_dim & 1) || D & 1) return (int)hipErrorInvalidValue;
     const bool qkn = qn != nullptr && kn != nullptr;
     if (qkn && Hq + Hkv > 256) return (int)hipErrorInvalidValue;
-#define RK(N_, B_, Q_) rope_kv_kernel<N_, B_, Q_><<<T, 256, 0, st>>>(qkv, bias, pos, slots, inv_freq, attn_factor, Hq, Hkv, D, rot_dim, qo, kc, vc, block_size, qn, kn, eps)
-#define RKQ(N_, B_) { if (qkn) RK(N_, B_, true); else RK(N_, B_, false); }
+    // enough workgroups for the 256 CUs even at small decode batches, >= 1 head per group
+    int ng = (512 + T - 1) / T;
+    ng = max(1, min(ng, min(8, Hkv)));
+    const dim3 grid(T, ng);
+#define RKZ(N_, B_, Q_) { if (zero_after) rope_kv_kernel<N_, B_, Q_, true><<<grid, 256, 0, st>>>(qkv, bias, pos, slots, inv_freq, attn_factor, Hq, Hkv, D, rot_dim, qo, kc, vc, block_size, qn, kn, eps); \
+    else rope_kv_kernel<N_, B_, Q_, false><<<grid, 256, 0, st>>>(qkv, bias, pos, slots, inv_freq, attn_factor, Hq, Hkv, D, rot_dim, qo, kc, vc, block_size, qn, kn, eps); }
+#define RK(N_, B_, Q_) RKZ(N_, B_, Q_)
+#define RKQ(N_, B_) { if (qkn) RK(N_, B_, true) else RK(N_, B_, false) }
     if (neox) { if (bias) RKQ(true, true) else RKQ(true, false) }
     else { if (bias) RKQ(false, true) else RKQ(false, false) }
 #undef RKQ
 #undef RK
+#undef RKZ
     MXK_CHECK_LAUNCH();
 }
 

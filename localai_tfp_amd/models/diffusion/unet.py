@@ -139,7 +139,7 @@ class BasicTransformerBlock(nn.Module):
         D = C // H
         dt = ctx.dtype
         a1 = self.attn1
-        if a1._qkv is None:
+        if a1._qkv is None or a1._qkv.device != a1.to_q.weight.device or a1._qkv.dtype != a1.to_q.weight.dtype:
             a1._qkv = torch.cat([a1.to_q.weight, a1.to_k.weight, a1.to_v.weight])
         h = layernorm16(x, self.norm1.weight, self.norm1.bias, 1e-5, dt)
         qkv = F.linear(h, a1._qkv)
@@ -147,7 +147,8 @@ class BasicTransformerBlock(nn.Module):
         linear_acc(o, a1.to_out[0], x)
         a2 = self.attn2
         Sc = ctx.shape[0] // B
-        if a2._kv is None or a2._kv[0] is not ctx_key:  # text K|V: once per generation, reused every step
+        if a2._kv is None or a2._kv[0] is not ctx_key or a2._kv[1].device != ctx.device:
+            # text K|V: once per generation, reused every sampler step
             wkv = torch.cat([a2.to_k.weight, a2.to_v.weight])
             a2._kv = (ctx_key, F.linear(ctx, wkv))
         kv = a2._kv[1]
@@ -270,7 +271,8 @@ class UNet2DConditionModel(nn.Module):
 
     def _time_proj(self):
         """All ResNet time_emb_proj weights stacked: one GEMM per step for the whole net."""
-        if self._tproj is None:
+        if self._tproj is None or self._tproj[0].device != self.conv_in.weight.device \
+                or self._tproj[0].dtype != self.conv_in.weight.dtype:  # (re)built after .to() / cast
             rs = self._resnets()
             w = torch.cat([r.time_emb_proj.weight for r in rs])
             b = torch.cat([r.time_emb_proj.bias for r in rs])

@@ -93,7 +93,9 @@ class Workspace:
         kmax = max(H, F, qd)
         self.xq = torch.empty((T * kmax,), dtype=torch.int8, device=dev)
         self.xds = torch.empty((T * kmax // 32 * 2,), dtype=torch.float32, device=dev)
-        self.qkv = torch.empty((T, qd + 2 * kvd), dtype=torch.float32, device=dev)
+        # zero-initialised and kept zero between uses: rope_kv re-zeroes the rows it consumes, so the
+        # split-K QKV GEMM (atomic accumulate) never needs a separate fill launch
+        self.qkv = torch.zeros((T, qd + 2 * kvd), dtype=torch.float32, device=dev)
         self.q = torch.empty((T, qd), dtype=torch.bfloat16, device=dev)
         self.attn = torch.empty((T, qd), dtype=act, device=dev)
         self.act = torch.empty((T, F), dtype=act, device=dev)
@@ -310,7 +312,7 @@ class LlamaModel:
                 K.rmsnorm(h, L.attn_norm, eps, out_bf16=xb)
                 xq = xds = None
             qkv = ws.qkv[:T]
-            if not gemv:
+            if not gemv and not qkv.is_cuda:
                 qkv.zero_()
             off = 0
             for w in L.qkv_parts:
@@ -323,7 +325,7 @@ class LlamaModel:
             q = ws.q[:T]
             K.rope_kv(qkv, L.bqkv, fb.positions, fb.slots, self.inv_freq, self.attn_factor, Hq, Hkv, D,
                       cfg.rope_dim, cfg.neox, q.view(T, Hq, D), kc, vc, kv.block_size,
-                      qk_norm=(L.q_norm, L.k_norm, eps) if L.q_norm is not None else None)
+                      qk_norm=(L.q_norm, L.k_norm, eps) if L.q_norm is not None else None, zero_after=True)
             attn = ws.attn[:T]
             if nd:
                 K.attn_decode(q[:nd].view(nd, Hq, D), kc, vc, fb.dec_block_tables, fb.dec_seq_lens, self.scale,

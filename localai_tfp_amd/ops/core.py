@@ -220,9 +220,10 @@ def rope_inv_freq(rot_dim: int, base: float = 10000.0, scale: float = 1.0, scali
 def rope_kv(qkv: torch.Tensor, bias: torch.Tensor | None, positions: torch.Tensor, slots: torch.Tensor,
             inv_freq: torch.Tensor, attn_factor: float, Hq: int, Hkv: int, D: int, rot_dim: int, neox: bool,
             q_out: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, block_size: int,
-            qk_norm: tuple | None = None):
+            qk_norm: tuple | None = None, zero_after: bool = False):
     """qkv fp32 [T, (Hq+2Hkv)*D] -> q_out bf16 [T, Hq, D]; K/V scattered into the paged cache
-    [num_blocks, Hkv, block_size, D] at `slots` (flat block*bs+offset; -1 skips)."""
+    [num_blocks, Hkv, block_size, D] at `slots` (flat block*bs+offset; -1 skips). zero_after (GPU):
+    the consumed qkv rows are left zeroed, ready for the next split-K accumulation into them."""
     T = qkv.shape[0]
     if T == 0:
         return
@@ -270,7 +271,8 @@ def rope_kv(qkv: torch.Tensor, bias: torch.Tensor | None, positions: torch.Tenso
     N.kcall("mxk_rope_kv", qkv.data_ptr(), N.ptr(bias), positions.data_ptr(), slots.data_ptr(), inv_freq.data_ptr(),
             float(attn_factor), T, Hq, Hkv, D, rot_dim, int(neox), q_out.data_ptr(), k_cache.data_ptr(),
             v_cache.data_ptr(), block_size, N.ptr(qk_norm[0]) if qk_norm else None,
-            N.ptr(qk_norm[1]) if qk_norm else None, float(qk_norm[2]) if qk_norm else 0.0, N.stream_ptr())
+            N.ptr(qk_norm[1]) if qk_norm else None, float(qk_norm[2]) if qk_norm else 0.0, int(zero_after),
+            N.stream_ptr())
 
 
 # ------------------------------------------------------------------------------------------------
