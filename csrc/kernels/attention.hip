@@ -23,9 +23,11 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restri
                                                           const bf16_t* __restrict__ vc,
                                                           const int* __restrict__ block_tables, int bt_stride,
                                                           const int* __restrict__ seq_lens, int Hkv, int bs,
-                                                          float scale, int part_size, int n_parts,
-                                                          bf16_t* __restrict__ out, int out_stride,
+                                                          float scale, int window, float softcap, int part_size,
+                                                          int n_parts, bf16_t* __restrict__ out, int out_stride,
                                                           float2* __restrict__ part_ml, float* __restrict__ part_o) {
+    // window > 0: sliding-window attention, keys p >= L - window only (Gemma 2/3 local layers);
+    // softcap > 0: scores s -> softcap * tanh(s / softcap) before the softmax (Gemma 2).
     constexpr int LPP = D / 8;        // lanes per position
     constexpr int PPW = 64 / LPP;     // positions per wave step
     constexpr int PPB = 4 * PPW;      // positions per workgroup step
@@ -44,6 +46,8 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restri
 
     float qf[G][8];
     const float qs = scale * LOG2E;
+    const float sc_l2 = softcap * LOG2E, sc_inv = softcap > 0.f ? 1.f / (softcap * LOG2E) : 0.f;
+    const int p_start = window > 0 ? max(p0, L - window) : p0;
 #pragma unroll
     for (int h = 0; h < G; ++h) {
         const uint4 raw = *(const uint4*)(q + (size_t)b * q_stride + (size_t)(kvh * G + h) * D + dl * 8);
@@ -101,6 +105,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restri
                 acc = fmaf(qf[h][2 * j + 1], __uint_as_float(kw & 0xFFFF0000u), acc);         \
             }                                                                                 \
             s[u] = group_sum<LPP>(acc);                                                       \
+            if (softcap > 0.f) s[u] = sc_l2 * tanhf(s[u] * sc_inv);                           \
             if ((BASE) + u * PPB + wave * PPW + pg >= p1) s[u] = -INFINITY;                   \
         }                                                                                     \
         float mx = m[h];                                                                      \
@@ -121,8 +126,8 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restri
             m[h] = mx;                                                                        \
         }                                                                                     \
     }
-    if (p0 < p1) { DEC_LOAD(ka, va, p0) }
-    for (int base = p0; base < p1; base += 2 * STEP) {
+    if (p_start < p1) { DEC_LOAD(ka, va, p_start) }
+    for (int base = p_start; base < p1; base += 2 * STEP) {
         if (base + STEP < p1) { DEC_LOAD(kb, vb, base + STEP) }
         DEC_CONSUME(ka, va, base)
         if (base + STEP >= p1) break;
@@ -207,13 +212,14 @@ __global__ __launch_bounds__(128) void attn_decode_reduce_kernel(const float2* _
 
 template <int D, int G>
 static int launch_decode(const bf16_t* q, int q_stride, const bf16_t* kc, const bf16_t* vc, const int* bt,
-                         int bt_stride, const int* seq_lens, int B, int Hkv, int bs, float scale, int part_size,
-                         int n_parts, bf16_t* out, int out_stride, float2* part_ml, float* part_o,
-                         hipStream_t st) {
+                         int bt_stride, const int* seq_lens, int B, int Hkv, int bs, float scale, int window,
+                         float softcap, int part_size, int n_parts, bf16_t* out, int out_stride, float2* part_ml,
+                         float* part_o, hipStream_t st) {
     dim3 grid(Hkv, B, n_parts);
     MX_ACT_DISPATCH({
         attn_decode_kernel<D, G, F16><<<grid, 256, 0, st>>>(q, q_stride, kc, vc, bt, bt_stride, seq_lens, Hkv, bs,
-                                                            scale, part_size, n_parts, out, out_stride, part_ml, part_o);
+                                                            scale, window, softcap, part_size, n_parts, out,
+                                                            out_stride, part_ml, part_o);
         if (n_parts > 1)
             attn_decode_reduce_kernel<F16><<<B * Hkv * G, 128, 0, st>>>(part_ml, part_o, n_parts, Hkv * G, D, seq_lens,
                                                                         part_size, out, out_stride);
@@ -223,15 +229,15 @@ static int launch_decode(const bf16_t* q, int q_stride, const bf16_t* kc, const 
 
 extern "C" int mxk_attn_decode(const bf16_t* q, int q_stride, const bf16_t* kc, const bf16_t* vc, const int* bt,
                                int bt_stride, const int* seq_lens, int B, int Hq, int Hkv, int D, int bs,
-                               float scale, int part_size, int n_parts, bf16_t* out, int out_stride,
-                               float2* part_ml, float* part_o, hipStream_t st) {
+                               float scale, int window, float softcap, int part_size, int n_parts, bf16_t* out,
+                               int out_stride, float2* part_ml, float* part_o, hipStream_t st) {
     if (B <= 0) return 0;
     if (Hq % Hkv) return (int)hipErrorInvalidValue;
     const int G = Hq / Hkv;
     if (n_parts > 1 && (!part_ml || !part_o)) return (int)hipErrorInvalidValue;
     if (bs <= 0 || part_size / bs + 1 > 256) return (int)hipErrorInvalidValue;  // LDS block-id stage
 #define DEC(D_, G_) \
-    if (D == D_ && G == G_) return launch_decode<D_, G_>(q, q_stride, kc, vc, bt, bt_stride, seq_lens, B, Hkv, bs, scale, part_size, n_parts, out, out_stride, part_ml, part_o, st);
+    if (D == D_ && G == G_) return launch_decode<D_, G_>(q, q_stride, kc, vc, bt, bt_stride, seq_lens, B, Hkv, bs, scale, window, softcap, part_size, n_parts, out, out_stride, part_ml, part_o, st);
     DEC(128, 1) DEC(128, 2) DEC(128, 3) DEC(128, 4) DEC(128, 5) DEC(128, 6) DEC(128, 7) DEC(128, 8)
     DEC(64, 1) DEC(64, 2) DEC(64, 4) DEC(64, 8) DEC(256, 1) DEC(256, 2) DEC(256, 4) DEC(256, 8)
 #undef DEC
@@ -267,7 +273,8 @@ __global__ __launch_bounds__(512) void attn_prefill_kernel(const bf16_t* __restr
                                                            const int* __restrict__ tile_q0,
                                                            const int* __restrict__ cu_q,
                                                            const int* __restrict__ ctx_lens, int Hq, int Hkv,
-                                                           int G, int bs, float scale, bf16_t* __restrict__ out) {
+                                                           int G, int bs, float scale, int window, float softcap,
+                                                           bf16_t* __restrict__ out) {
     constexpr int NW = GW >= 3 ? GW : 4;      // waves per workgroup
     constexpr int RT = NW / GW;               // 16-row query tiles per workgroup
     constexpr int KT = 64;                    // keys per tile
@@ -295,6 +302,9 @@ __global__ __launch_bounds__(512) void attn_prefill_kernel(const bf16_t* __restr
     const int wg_rows = RT * 16;
     const int kv_end = min(ctx, pos_off + min(qlen, q0 + wg_rows));
     const float qs = scale * LOG2E;
+    const float sc_l2 = softcap * LOG2E, sc_inv = softcap > 0.f ? 1.f / (softcap * LOG2E) : 0.f;
+    // sliding window: key tiles entirely before the earliest query's window are skipped
+    const int kt_begin = window > 0 ? (max(0, pos_off + q0 - window + 1) / 64) * 64 : 0;
 
     // Q fragments: lane row = col, dims 32ks + 8g
     bf16x8 qf[D / 32];
@@ -314,7 +324,7 @@ __global__ __launch_bounds__(512) void attn_prefill_kernel(const bf16_t* __restr
     for (int i = 0; i < 4; ++i) { mrow[i] = -INFINITY; lrow[i] = 0.f; }
     char* pw = p_lds + wave * 16 * PSTRIDE;
 
-    for (int kt0 = 0; kt0 < kv_end; kt0 += KT) {
+    for (int kt0 = kt_begin; kt0 < kv_end; kt0 += KT) {
         // ---- stage K and V tiles (64 keys x D) ----
         constexpr int CH = KT * D / 8;  // 16-byte chunks per tile
         for (int id = threadIdx.x; id < CH; id += NT) {
@@ -360,7 +370,8 @@ __global__ __launch_bounds__(512) void attn_prefill_kernel(const bf16_t* __restr
             for (int t = 0; t < 4; ++t) {
                 const int kp = kt0 + 16 * t + col;
                 float v = sacc[t][i] * qs;
-                if (kp > qpos || kp >= ctx || qi >= qlen) v = -INFINITY;
+                if (softcap > 0.f) v = sc_l2 * tanhf(v * sc_inv);
+                if (kp > qpos || kp >= ctx || qi >= qlen || (window > 0 && kp <= qpos - window)) v = -INFINITY;
                 sacc[t][i] = v;
                 mx = fmaxf(mx, v);
             }
@@ -436,19 +447,37 @@ __global__ __launch_bounds__(512) void attn_prefill_kernel(const bf16_t* __restr
 template <int D, int GW>
 static int launch_prefill(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, const int* bt, int bt_stride,
                           const int* tile_seq, const int* tile_q0, int n_tiles, const int* cu_q,
-                          const int* ctx_lens, int Hq, int Hkv, int bs, float scale, bf16_t* out, int vmode,
-                          hipStream_t st) {
+                          const int* ctx_lens, int Hq, int Hkv, int bs, float scale, int window, float softcap,
+                          bf16_t* out, int vmode, hipStream_t st) {
     constexpr int NW = GW >= 3 ? GW : 4;
     dim3 grid(n_tiles, Hq / GW);
     MX_ACT_DISPATCH({
         if (vmode == 0) {
             const size_t lds = 2 * 64 * D * 2 + NW * 16 * (64 + 8) * 2;
+            if (lds > 65536) {  // D=256 tiles (73-82 KB): opt in to the large LDS allocation once
+                static bool opted = false;
+                if (!opted) {
+                    hipFuncSetAttribute((const void*)attn_prefill_kernel<D, GW, 0, F16>,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+                    opted = true;
+                }
+            }
             attn_prefill_kernel<D, GW, 0, F16><<<grid, NW * 64, lds, st>>>(
-                q, kc, vc, bt, bt_stride, tile_seq, tile_q0, cu_q, ctx_lens, Hq, Hkv, Hq / Hkv, bs, scale, out);
+                q, kc, vc, bt, bt_stride, tile_seq, tile_q0, cu_q, ctx_lens, Hq, Hkv, Hq / Hkv, bs, scale, window,
+                softcap, out);
         } else {
             const size_t lds = 64 * D * 2 + D * (64 + 8) * 2 + NW * 16 * (64 + 8) * 2;
+            if (lds > 65536) {
+                static bool opted = false;
+                if (!opted) {
+                    hipFuncSetAttribute((const void*)attn_prefill_kernel<D, GW, 1, F16>,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+                    opted = true;
+                }
+            }
             attn_prefill_kernel<D, GW, 1, F16><<<grid, NW * 64, lds, st>>>(
-                q, kc, vc, bt, bt_stride, tile_seq, tile_q0, cu_q, ctx_lens, Hq, Hkv, Hq / Hkv, bs, scale, out);
+                q, kc, vc, bt, bt_stride, tile_seq, tile_q0, cu_q, ctx_lens, Hq, Hkv, Hq / Hkv, bs, scale, window,
+                softcap, out);
         }
     });
     MXK_CHECK_LAUNCH();
@@ -464,17 +493,18 @@ extern "C" int mxk_attn_prefill_rows(int Hq, int Hkv) {
 
 extern "C" int mxk_attn_prefill(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, const int* bt, int bt_stride,
                                 const int* tile_seq, const int* tile_q0, int n_tiles, const int* cu_q,
-                                const int* ctx_lens, int Hq, int Hkv, int D, int bs, float scale, bf16_t* out,
-                                int vmode, hipStream_t st) {
+                                const int* ctx_lens, int Hq, int Hkv, int D, int bs, float scale, int window,
+                                float softcap, bf16_t* out, int vmode, hipStream_t st) {
     if (n_tiles <= 0) return 0;
     if (Hq % Hkv) return (int)hipErrorInvalidValue;
     const int G = Hq / Hkv;
     const int GW = G <= 8 ? G : 8;
     if (G > 8 && G % 8) return (int)hipErrorInvalidValue;
 #define PF(D_, GW_) \
-    if (D == D_ && GW == GW_) return launch_prefill<D_, GW_>(q, kc, vc, bt, bt_stride, tile_seq, tile_q0, n_tiles, cu_q, ctx_lens, Hq, Hkv, bs, scale, out, vmode, st);
+    if (D == D_ && GW == GW_) return launch_prefill<D_, GW_>(q, kc, vc, bt, bt_stride, tile_seq, tile_q0, n_tiles, cu_q, ctx_lens, Hq, Hkv, bs, scale, window, softcap, out, vmode, st);
     PF(128, 1) PF(128, 2) PF(128, 3) PF(128, 4) PF(128, 5) PF(128, 6) PF(128, 7) PF(128, 8)
     PF(64, 1) PF(64, 2) PF(64, 4) PF(64, 8)
+    PF(256, 1) PF(256, 2) PF(256, 4)
 #undef PF
     return (int)hipErrorInvalidValue;
 }

@@ -52,7 +52,7 @@ extern "C" int mxk_glu(int act, const bf16_t* g, const bf16_t* u, int ld_in, bf1
 
 // SwiGLU over a gate|up product whose columns are interleaved in 16-column groups (the layout of
 // the fused gate_up weight): y[m, 32*(f/16) + f%16] = gate, y[m, 32*(f/16) + 16 + f%16] = up.
-template <bool F16>
+template <bool F16, int EPI>
 __global__ __launch_bounds__(256) void swiglu_il16_kernel(const bf16_t* __restrict__ y, int ldy,
                                                           bf16_t* __restrict__ out, int ldo, int F) {
     const int m = blockIdx.y;
@@ -69,16 +69,19 @@ __global__ __launch_bounds__(256) void swiglu_il16_kernel(const bf16_t* __restri
         float g0, g1, u0, u1;
         unpack_act2<F16>(gw[j], g0, g1);
         unpack_act2<F16>(uw[j], u0, u1);
-        o[j] = pack_act2<F16>(silu_f(g0) * u0, silu_f(g1) * u1);
+        o[j] = pack_act2<F16>(glu_gate_f<EPI>(g0) * u0, glu_gate_f<EPI>(g1) * u1);
     }
     *(uint4*)(out + (size_t)m * ldo + f) = make_uint4(o[0], o[1], o[2], o[3]);
 }
 
-extern "C" int mxk_swiglu_il16(const bf16_t* y, int ldy, bf16_t* out, int ldo, int M, int F, hipStream_t st) {
+// gelu: 0 SwiGLU, 1 GeGLU (gelu tanh)
+extern "C" int mxk_swiglu_il16(const bf16_t* y, int ldy, bf16_t* out, int ldo, int M, int F, int gelu,
+                               hipStream_t st) {
     if (M <= 0) return 0;
     if (F % 16) return (int)hipErrorInvalidValue;
     dim3 grid((F / 8 + 255) / 256, M);
-    MX_ACT_DISPATCH(swiglu_il16_kernel<F16><<<grid, 256, 0, st>>>(y, ldy, out, ldo, F));
+    if (gelu) MX_ACT_DISPATCH((swiglu_il16_kernel<F16, 4><<<grid, 256, 0, st>>>(y, ldy, out, ldo, F)));
+    else MX_ACT_DISPATCH((swiglu_il16_kernel<F16, 3><<<grid, 256, 0, st>>>(y, ldy, out, ldo, F)));
     MXK_CHECK_LAUNCH();
 }
 

@@ -151,6 +151,12 @@ MX_DEV float gelu_tanh_f(float x) {
     return 0.5f * x * (1.f + tanhf(k0 * (x + k1 * x * x * x)));
 }
 MX_DEV float gelu_erf_f(float x) { return 0.5f * x * (1.f + erff(x * 0.7071067811865476f)); }
+// gate activation of the fused gated-FFN epilogues: EPI 3 = SwiGLU (silu), EPI 4 = GeGLU (gelu tanh)
+template <int EPI>
+MX_DEV float glu_gate_f(float g) {
+    if constexpr (EPI == 4) return gelu_tanh_f(g);
+    else return silu_f(g);
+}
 
 #define MXK_CHECK_LAUNCH() return (int)hipGetLastError()
 

@@ -135,6 +135,42 @@ extern "C" int mxk_rmsnorm(const float* x, int ldx, const bf16_t* res, int ldr, 
 }
 
 // ---------------------------------------------------------------------------------------------
+// h += y / rms(y) * w — Gemma 2/3 post-attention / post-FFN norm fused into the residual add.
+// One 256-thread workgroup per row, float4 over H (H % 4 == 0); y is re-read from L2 for the add.
+__global__ __launch_bounds__(256) void rmsnorm_add_kernel(const float* __restrict__ y, int ldy,
+                                                          const float* __restrict__ w, float* __restrict__ h,
+                                                          int ldh, int H, float eps) {
+    __shared__ float red[4];
+    const float* yr = y + (size_t)blockIdx.x * ldy;
+    float* hr = h + (size_t)blockIdx.x * ldh;
+    float ss = 0.f;
+    for (int c = threadIdx.x * 4; c < H; c += 1024) {
+        const float4 v = *(const float4*)(yr + c);
+        ss += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+    }
+    ss = block_sum<256>(ss, red);
+    const float rs = rsqrtf(ss / (float)H + eps);
+    for (int c = threadIdx.x * 4; c < H; c += 1024) {
+        const float4 v = *(const float4*)(yr + c);
+        const float4 g = *(const float4*)(w + c);
+        float4 o = *(const float4*)(hr + c);
+        o.x += v.x * rs * g.x;
+        o.y += v.y * rs * g.y;
+        o.z += v.z * rs * g.z;
+        o.w += v.w * rs * g.w;
+        *(float4*)(hr + c) = o;
+    }
+}
+
+extern "C" int mxk_rmsnorm_add(const float* y, int ldy, const float* w, float* h, int ldh, int rows, int H, float eps,
+                               hipStream_t st) {
+    if (rows <= 0) return 0;
+    if ((H & 3) || (ldy & 3) || (ldh & 3)) return (int)hipErrorInvalidValue;
+    rmsnorm_add_kernel<<<rows, 256, 0, st>>>(y, ldy, w, h, ldh, H, eps);
+    MXK_CHECK_LAUNCH();
+}
+
+// ---------------------------------------------------------------------------------------------
 // quantise bf16 rows to q8 blocks (for the GEMV path after attention / SwiGLU). One wave per
 // 64 x 32-element block group: lane l handles 8 elements; 4 lanes per block.
 template <bool F16>

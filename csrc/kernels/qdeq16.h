@@ -3,7 +3,7 @@
 #pragma once
 #include "mx_common.h"
 
-enum { E16_F32 = 0, E16_ACT = 1, E16_ADD_F32 = 2, E16_SWIGLU = 3 };
+enum { E16_F32 = 0, E16_ACT = 1, E16_ADD_F32 = 2, E16_SWIGLU = 3, E16_GEGLU = 4 };
 
 static constexpr uint32_t MAGIC = 0x64646464u;
 static constexpr uint32_t SEL_LO = 0x04010400u;  // bytes (t0, 0x64, t1, 0x64)

@@ -18,7 +18,7 @@
 // (gate/up rows interleaved in 16-row groups at load time -> silu(g)*u written as bf16).
 #include "mx_common.h"
 
-enum { EPI_F32 = 0, EPI_BF16 = 1, EPI_ADD_F32 = 2, EPI_SWIGLU = 3 };
+enum { EPI_F32 = 0, EPI_BF16 = 1, EPI_ADD_F32 = 2, EPI_SWIGLU = 3, EPI_GEGLU = 4 };
 
 // ---------------------------------------------------------------------------------------------
 // Per-lane weight fragment: the 64 elements [64g, 64g+64) of super-block `kb` of row `n`.
@@ -265,7 +265,7 @@ __global__ __launch_bounds__(256) void qgemm_mfma_kernel(const bf16_t* __restric
     for (int i = 0; i < WM; ++i) {
 #pragma unroll
         for (int t = 0; t < WN; ++t) {
-            if constexpr (EPI == EPI_SWIGLU) {
+            if constexpr (EPI == EPI_SWIGLU || EPI == EPI_GEGLU) {
                 if (t & 1) continue;
                 const int feat = (n_base >> 1) + (t >> 1) * 16 + col;
                 if (n_base + t * 16 + col >= N) continue;
@@ -274,7 +274,7 @@ __global__ __launch_bounds__(256) void qgemm_mfma_kernel(const bf16_t* __restric
                     const int m = m_base + i * 16 + 4 * g + e;
                     if (m < M) {
                         const float gv = acc[i][t][e], uv = acc[i][t + 1][e];
-                        ((bf16_t*)Cv)[(size_t)m * ldc + feat] = f32_to_bf16(silu_f(gv) * uv);
+                        ((bf16_t*)Cv)[(size_t)m * ldc + feat] = f32_to_bf16(glu_gate_f<EPI>(gv) * uv);
                     }
                 }
             } else {
@@ -376,7 +376,7 @@ __global__ __launch_bounds__(256) void qgemv_dot4_kernel(const int8_t* __restric
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int slot = blockIdx.x * 4 + wave;  // each slot produces 2 rows (or 1 SwiGLU feature)
     int r0, r1;
-    if constexpr (EPI == EPI_SWIGLU) {
+    if constexpr (EPI == EPI_SWIGLU || EPI == EPI_GEGLU) {
         r0 = 32 * (slot >> 4) + (slot & 15);
         r1 = r0 + 16;
     } else {
@@ -411,8 +411,8 @@ __global__ __launch_bounds__(256) void qgemv_dot4_kernel(const int8_t* __restric
         const float a0 = wave_sum(acc0[m]);
         const float a1 = wave_sum(acc1[m]);
         if (lane == 0) {
-            if constexpr (EPI == EPI_SWIGLU) {
-                ((bf16_t*)Cv)[(size_t)m * ldc + slot] = f32_to_act<F16>(silu_f(a0) * a1);
+            if constexpr (EPI == EPI_SWIGLU || EPI == EPI_GEGLU) {
+                ((bf16_t*)Cv)[(size_t)m * ldc + slot] = f32_to_act<F16>(glu_gate_f<EPI>(a0) * a1);
             } else if constexpr (EPI == EPI_F32) {
                 ((float*)Cv)[(size_t)m * ldc + r0] = a0;
                 if (v1) ((float*)Cv)[(size_t)m * ldc + r1] = a1;
@@ -500,8 +500,8 @@ extern "C" int mxk_qgemm_mfma(int qtype, int epi, int wm, int wn, const bf16_t* 
                               hipStream_t st) {
     if (M <= 0) return 0;
     if (K % 256) return (int)hipErrorInvalidValue;
-    if ((epi == EPI_SWIGLU || epi == EPI_BF16 || epi == EPI_F32) && splits != 1) return (int)hipErrorInvalidValue;
-    if (epi == EPI_SWIGLU && (wn & 1)) return (int)hipErrorInvalidValue;
+    if ((epi == EPI_SWIGLU || epi == EPI_GEGLU || epi == EPI_BF16 || epi == EPI_F32) && splits != 1) return (int)hipErrorInvalidValue;
+    if ((epi == EPI_SWIGLU || epi == EPI_GEGLU) && (wn & 1)) return (int)hipErrorInvalidValue;
 #define QG_EPI(QT_)                                                                                     \
     switch (epi) {                                                                                      \
         case EPI_F32: return dispatch_mfma<QT_, EPI_F32>(wm, wn, A, lda, W, WD, M, N, K, splits, C, ldc, st);   \
@@ -510,6 +510,8 @@ extern "C" int mxk_qgemm_mfma(int qtype, int epi, int wm, int wn, const bf16_t* 
             return dispatch_mfma<QT_, EPI_ADD_F32>(wm, wn, A, lda, W, WD, M, N, K, splits, C, ldc, st);        \
         case EPI_SWIGLU:                                                                                \
             return dispatch_mfma<QT_, EPI_SWIGLU>(wm, wn, A, lda, W, WD, M, N, K, splits, C, ldc, st);         \
+        case EPI_GEGLU:                                                                                 \
+            return dispatch_mfma<QT_, EPI_GEGLU>(wm, wn, A, lda, W, WD, M, N, K, splits, C, ldc, st);          \
     }
     switch (qtype) {
         case MXQ_Q4_K: QG_EPI(MXQ_Q4_K) break;
@@ -523,7 +525,7 @@ extern "C" int mxk_qgemm_mfma(int qtype, int epi, int wm, int wn, const bf16_t* 
 template <int QT, int MM, int EPI>
 static int launch_gemv(const int8_t* xq, const float2* xds, const uint8_t* W, const uint16_t* WD, int M, int N,
                        int K, void* C, int ldc, hipStream_t st) {
-    const int slots = EPI == EPI_SWIGLU ? N / 2 : (N + 1) / 2;
+    const int slots = (EPI == EPI_SWIGLU || EPI == EPI_GEGLU) ? N / 2 : (N + 1) / 2;
     dim3 grid((slots + 3) / 4);
     MX_ACT_DISPATCH(qgemv_dot4_kernel<QT, MM, EPI, F16><<<grid, 256, 0, st>>>(xq, xds, W, WD, M, N, K, C, ldc));
     MXK_CHECK_LAUNCH();
@@ -533,7 +535,7 @@ extern "C" int mxk_qgemv(int qtype, int epi, const int8_t* xq, const float2* xds
                          const uint16_t* WD, int M, int N, int K, void* C, int ldc, hipStream_t st) {
     if (M <= 0) return 0;
     if (M > 4 || K % 256) return (int)hipErrorInvalidValue;
-    if (epi == EPI_SWIGLU && (N % 32)) return (int)hipErrorInvalidValue;
+    if ((epi == EPI_SWIGLU || epi == EPI_GEGLU) && (N % 32)) return (int)hipErrorInvalidValue;
 #define GV_M(QT_, EPI_)                                                                 \
     if (M == 1) return launch_gemv<QT_, 1, EPI_>(xq, xds, W, WD, M, N, K, C, ldc, st);  \
     if (M == 2) return launch_gemv<QT_, 2, EPI_>(xq, xds, W, WD, M, N, K, C, ldc, st);  \
@@ -544,6 +546,7 @@ extern "C" int mxk_qgemv(int qtype, int epi, const int8_t* xq, const float2* xds
         case EPI_BF16: { GV_M(QT_, EPI_BF16) }        \
         case EPI_ADD_F32: { GV_M(QT_, EPI_ADD_F32) }  \
         case EPI_SWIGLU: { GV_M(QT_, EPI_SWIGLU) }    \
+        case EPI_GEGLU: { GV_M(QT_, EPI_GEGLU) }      \
     }
     switch (qtype) {
         case MXQ_Q4_K: GV_EPI(MXQ_Q4_K) break;

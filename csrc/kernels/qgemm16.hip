@@ -148,7 +148,7 @@ __global__ __launch_bounds__(256, (WM >= 8 ? 1 : 2)) void qgemm16_kernel(const u
     for (int i = 0; i < WM; ++i) {
 #pragma unroll
         for (int t = 0; t < WN; ++t) {
-            if constexpr (EPI == E16_SWIGLU) {
+            if constexpr (EPI == E16_SWIGLU || EPI == E16_GEGLU) {
                 if (t & 1) continue;
                 const int feat = (n_base >> 1) + (t >> 1) * 16 + col;
                 if (n_base + t * 16 + col >= N) continue;
@@ -157,7 +157,7 @@ __global__ __launch_bounds__(256, (WM >= 8 ? 1 : 2)) void qgemm16_kernel(const u
                     const int m = m_base + i * 16 + 4 * g + e;
                     if (m < m_end) {
                         const float gv = acc[i][t][e], uv = acc[i][t + 1][e];
-                        ((uint16_t*)Cv)[(size_t)m * ldc + feat] = f32_to_act<true>(silu_f(gv) * uv);
+                        ((uint16_t*)Cv)[(size_t)m * ldc + feat] = f32_to_act<true>(glu_gate_f<EPI>(gv) * uv);
                     }
                 }
             } else {
@@ -207,14 +207,15 @@ extern "C" int mxk_qgemm16(int qtype, int epi, int wm, int wn, const uint16_t* A
                            const uint16_t* WD, int M, int N, int K, int splits, void* C, int ldc, hipStream_t st) {
     if (M <= 0) return 0;
     if (K % 256) return (int)hipErrorInvalidValue;
-    if ((epi == E16_SWIGLU || epi == E16_ACT || epi == E16_F32) && splits != 1) return (int)hipErrorInvalidValue;
-    if (epi == E16_SWIGLU && (wn & 1)) return (int)hipErrorInvalidValue;
+    if ((epi == E16_SWIGLU || epi == E16_GEGLU || epi == E16_ACT || epi == E16_F32) && splits != 1) return (int)hipErrorInvalidValue;
+    if ((epi == E16_SWIGLU || epi == E16_GEGLU) && (wn & 1)) return (int)hipErrorInvalidValue;
 #define Q16_EPI(QT_)                                                                                          \
     switch (epi) {                                                                                            \
         case E16_F32: return dispatch16<QT_, E16_F32>(wm, wn, A, lda, W, WD, M, N, K, splits, C, ldc, st);         \
         case E16_ACT: return dispatch16<QT_, E16_ACT>(wm, wn, A, lda, W, WD, M, N, K, splits, C, ldc, st);         \
         case E16_ADD_F32: return dispatch16<QT_, E16_ADD_F32>(wm, wn, A, lda, W, WD, M, N, K, splits, C, ldc, st); \
         case E16_SWIGLU: return dispatch16<QT_, E16_SWIGLU>(wm, wn, A, lda, W, WD, M, N, K, splits, C, ldc, st);   \
+        case E16_GEGLU: return dispatch16<QT_, E16_GEGLU>(wm, wn, A, lda, W, WD, M, N, K, splits, C, ldc, st);     \
     }
     switch (qtype) {
         case MXQ_Q4_K: Q16_EPI(MXQ_Q4_K) break;
@@ -258,6 +259,8 @@ extern "C" int mxk_moe_qgemm16(int qtype, int epi, int wm, const uint16_t* A, in
         case E16_ACT: return launch16g<QT_, E16_ACT>(wm, A, lda, a_rows, W, WD, off, tile_start, E, P, N, K, C, ldc, st); \
         case E16_SWIGLU:                                                                                            \
             return launch16g<QT_, E16_SWIGLU>(wm, A, lda, a_rows, W, WD, off, tile_start, E, P, N, K, C, ldc, st);  \
+        case E16_GEGLU:                                                                                             \
+            return launch16g<QT_, E16_GEGLU>(wm, A, lda, a_rows, W, WD, off, tile_start, E, P, N, K, C, ldc, st);   \
     }
     switch (qtype) {
         case MXQ_Q4_K: Q16G_EPI(MXQ_Q4_K) break;

@@ -150,7 +150,7 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
     for (int t = 0; t < WN; ++t) {
         const int nt = n_base + 32 * t;
         const int n = nt + col;
-        if constexpr (EPI == E16_SWIGLU) {
+        if constexpr (EPI == E16_SWIGLU || EPI == E16_GEGLU) {
             // W rows interleaved in 16-row groups: tile columns 0..15 gate, 16..31 up of the same features
 #pragma unroll
             for (int i = 0; i < WM; ++i)
@@ -160,7 +160,7 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
                     const float up = __shfl_xor(v, 16);
                     const int m = m_base + i * 32 + 8 * (r >> 2) + 4 * h + (r & 3);
                     if (col < 16 && n < N && m < M)
-                        ((uint16_t*)Cv)[(size_t)m * ldc + (nt >> 1) + col] = f32_to_act<true>(silu_f(v) * up);
+                        ((uint16_t*)Cv)[(size_t)m * ldc + (nt >> 1) + col] = f32_to_act<true>(glu_gate_f<EPI>(v) * up);
                 }
             continue;
         }
@@ -209,13 +209,14 @@ extern "C" int mxk_qgemm32(int qtype, int epi, int wm, int wn, const uint16_t* A
     if (M <= 0) return 0;
     if (K % 256 || (lda & 7)) return (int)hipErrorInvalidValue;
     if (epi != E16_ADD_F32 && splits != 1) return (int)hipErrorInvalidValue;
-    if (epi == E16_SWIGLU && (N & 31)) return (int)hipErrorInvalidValue;
+    if ((epi == E16_SWIGLU || epi == E16_GEGLU) && (N & 31)) return (int)hipErrorInvalidValue;
 #define Q32_EPI(QT_)                                                                                       \
     switch (epi) {                                                                                         \
         case E16_F32: return dispatch32<QT_, E16_F32>(wm, wn, A, lda, W, WD, M, N, K, splits, C, ldc, st);         \
         case E16_ACT: return dispatch32<QT_, E16_ACT>(wm, wn, A, lda, W, WD, M, N, K, splits, C, ldc, st);         \
         case E16_ADD_F32: return dispatch32<QT_, E16_ADD_F32>(wm, wn, A, lda, W, WD, M, N, K, splits, C, ldc, st); \
         case E16_SWIGLU: return dispatch32<QT_, E16_SWIGLU>(wm, wn, A, lda, W, WD, M, N, K, splits, C, ldc, st);   \
+        case E16_GEGLU: return dispatch32<QT_, E16_GEGLU>(wm, wn, A, lda, W, WD, M, N, K, splits, C, ldc, st);     \
     }
     switch (qtype) {
         case MXQ_Q4_K: Q32_EPI(MXQ_Q4_K) break;

@@ -42,15 +42,16 @@ KERNEL_SIGS = {
     "mxk_dequant_rows": [I, P, P, P, I, I, P, P, I, P],
     "mxk_rope_kv": [P, P, P, P, P, F, I, I, I, I, I, I, P, P, P, I, P, P, F, I, P],
     "mxk_copy_blocks": [P, P, P, I, I, P],
-    "mxk_attn_decode": [P, I, P, P, P, I, P, I, I, I, I, I, F, I, I, P, I, P, P, P],
-    "mxk_attn_prefill": [P, P, P, P, I, P, P, I, P, P, I, I, I, I, F, P, I, P],
+    "mxk_attn_decode": [P, I, P, P, P, I, P, I, I, I, I, I, F, I, F, I, I, P, I, P, P, P],
+    "mxk_attn_prefill": [P, P, P, P, I, P, P, I, P, P, I, I, I, I, F, I, F, P, I, P],
     "mxk_probe_tr16": [P, P],
     "mxk_attn_prefill_rows": [I, I],
     "mxk_sample": [P, I, I, I, P, P, P, P, P, I, P, P, P],
     "mxk_sample_params_size": [],
     "mxk_argmax": [P, I, I, I, P, P],
     "mxk_glu": [I, P, P, I, P, I, I, I, P],
-    "mxk_swiglu_il16": [P, I, P, I, I, I, P],
+    "mxk_rmsnorm_add": [P, I, P, P, I, I, I, F, P],
+    "mxk_swiglu_il16": [P, I, P, I, I, I, I, P],
     "mxk_act_f32": [P, SZ, I, P],
     "mxk_cast_f32_bf16": [P, I, P, I, I, I, P],
     "mxk_gather_rows": [P, I, P, I, I, F, P, P],

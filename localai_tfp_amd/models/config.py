@@ -36,7 +36,16 @@ class LlamaConfig:
     expert_ffn: int = 0
     expert_shared_ffn: int = 0
     moe_renorm: bool = True  # renormalise the top-k router weights (Mixtral, Qwen3-MoE; not Qwen2-MoE)
-    qk_norm: bool = False  # per-head RMSNorm of q and k before RoPE (Qwen3)
+    qk_norm: bool = False  # per-head RMSNorm of q and k before RoPE (Qwen3, Gemma 3)
+    # Gemma family (llama.cpp src/llama-model.cpp build_gemma*/ LLM_ARCH_GEMMA2/3 hparams)
+    ffn_act: str = "silu"  # gate activation: silu (SwiGLU) | gelu (GeGLU, tanh approximation)
+    post_norms: bool = False  # RMSNorm of the attention / FFN output before the residual add (Gemma 2/3)
+    attn_softcap: float = 0.0  # scores -> c * tanh(scores / c) (Gemma 2)
+    final_softcap: float = 0.0  # logits -> c * tanh(logits / c) (Gemma 2)
+    sliding_window: int = 0  # local-attention window of the windowed layers (0 = none)
+    swa_pattern: int = 0  # layer i is global iff (i + 1) % swa_pattern == 0 (Gemma 2: 2, Gemma 3: 6); 0/1 = all windowed
+    rope_base_local: float = 0.0  # RoPE base of the windowed layers (Gemma 3: 10000; 0 = rope_base)
+    attn_scale: float = 0.0  # softmax scale (0 = 1/sqrt(head_dim))
     name: str = "llama"
     extra: dict = field(default_factory=dict)
 
@@ -51,6 +60,14 @@ class LlamaConfig:
     @property
     def kv_dim(self) -> int:
         return self.n_kv_heads * self.head_dim
+
+    def layer_window(self, i: int) -> int:
+        """Sliding-window size of layer i (0 = full causal attention)."""
+        if self.sliding_window <= 0:
+            return 0
+        if self.swa_pattern > 1 and (i + 1) % self.swa_pattern == 0:
+            return 0
+        return self.sliding_window
 
     def n_params(self) -> int:
         h, f, L = self.hidden, self.ffn, self.n_layers
@@ -104,7 +121,26 @@ class LlamaConfig:
             name=str(md.get("general.name", arch)),
         )
         if arch in ("gemma", "gemma2", "gemma3"):
+            # llama.cpp build_gemma*: embeddings * sqrt(n_embd), GeGLU FFN, norms stored as (1 + w)
             cfg.embed_scale = hidden ** 0.5
+            cfg.ffn_act = "gelu"
+            cfg.tie_embeddings = True
+        if arch == "gemma2":
+            cfg.post_norms = True
+            cfg.attn_softcap = float(g("attn_logit_softcapping", 50.0) or 0.0)
+            cfg.final_softcap = float(g("final_logit_softcapping", 30.0) or 0.0)
+            cfg.sliding_window = int(g("attention.sliding_window", 4096) or 0)
+            cfg.swa_pattern = 2
+            if cfg.n_layers == 46:  # Gemma-2-27B: query_pre_attn_scalar = n_embd / n_head
+                cfg.attn_scale = (hidden / n_heads) ** -0.5
+        if arch == "gemma3":
+            cfg.post_norms = True
+            cfg.sliding_window = int(g("attention.sliding_window", 1024) or 0)
+            cfg.swa_pattern = int(g("attention.sliding_window_pattern", 6) or 6)
+            cfg.rope_base_local = 10000.0
+            cfg.final_softcap = float(g("final_logit_softcapping", 0.0) or 0.0)
+            if cfg.n_layers == 62:  # Gemma-3-27B: query_pre_attn_scalar = n_embd / n_head
+                cfg.attn_scale = (hidden / n_heads) ** -0.5
         ne = int(g("expert_count", 0) or 0)
         if ne:
             cfg.n_expert = ne
@@ -112,7 +148,7 @@ class LlamaConfig:
             cfg.expert_ffn = int(g("expert_feed_forward_length", 0) or 0) or cfg.ffn
             cfg.expert_shared_ffn = int(g("expert_shared_feed_forward_length", 0) or 0)
             cfg.moe_renorm = bool(g("expert_weights_norm", arch != "qwen2moe"))
-        cfg.qk_norm = arch in ("qwen3", "qwen3moe")
+        cfg.qk_norm = arch in ("qwen3", "qwen3moe", "gemma3")
         return cfg
 
 
@@ -132,6 +168,15 @@ MIXTRAL_8X7B = LlamaConfig(name="Mixtral-8x7B-Instruct", n_layers=32, hidden=409
                            n_expert_used=2, expert_ffn=14336)
 QWEN3_8B = LlamaConfig(arch="qwen3", name="Qwen3-8B", n_layers=36, hidden=4096, ffn=12288, n_heads=32,
                        n_kv_heads=8, vocab=151936, ctx_train=40960, rope_base=1000000.0, rms_eps=1e-6, qk_norm=True)
+GEMMA2_9B = LlamaConfig(arch="gemma2", name="gemma-2-9b-it", n_layers=42, hidden=3584, ffn=14336, n_heads=16,
+                        n_kv_heads=8, head_dim=256, rope_dim=256, vocab=256000, ctx_train=8192, rope_base=10000.0,
+                        rms_eps=1e-6, tie_embeddings=True, embed_scale=3584 ** 0.5, ffn_act="gelu", post_norms=True,
+                        attn_softcap=50.0, final_softcap=30.0, sliding_window=4096, swa_pattern=2)
+GEMMA3_12B = LlamaConfig(arch="gemma3", name="gemma-3-12b-it", n_layers=48, hidden=3840, ffn=15360, n_heads=16,
+                         n_kv_heads=8, head_dim=256, rope_dim=256, vocab=262208, ctx_train=131072,
+                         rope_base=1000000.0, rope_scaling="linear", rope_scale=0.125, rms_eps=1e-6,
+                         tie_embeddings=True, embed_scale=3840 ** 0.5, ffn_act="gelu", post_norms=True, qk_norm=True,
+                         sliding_window=1024, swa_pattern=6, rope_base_local=10000.0)
 
 
 def tiny_config(**kw) -> LlamaConfig:

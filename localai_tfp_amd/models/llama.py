@@ -13,6 +13,11 @@ This is the compute graph llama.cpp builds inside `llama_decode` for the referen
     h += act W_d^T
     logits = rmsnorm(h[last]) W_out^T     (only rows that need sampling)
 
+Gemma 2/3 (llama.cpp build_gemma2 / build_gemma3) reuse the same graph with: GeGLU (EPI_GEGLU),
+post-attention / post-FFN RMSNorm fused into the residual add (norm.hip mxk_rmsnorm_add),
+per-layer sliding-window attention (the kernels skip keys outside the window), attention and
+final-logit soft-capping, Gemma 3's per-head QK-norm and local RoPE base on the windowed layers.
+
 Decode batches of <= 4 tokens take the int8-dot GEMV path (norm kernels emit q8 directly);
 larger batches the dequant-MFMA path. Tensor parallelism (parallel/tp.py) shards heads / FFN
 columns and all-reduces the residual after the row-parallel projections.
@@ -27,8 +32,8 @@ import torch
 
 from ..formats.gguf import QType
 from ..ops import core as K
-from ..ops.linear import (ACT_DTYPE, EPI_ADD_F32, EPI_BF16, EPI_F32, EPI_SWIGLU, QWeight, concat_rows, interleave_gate_up,
-                          qmatmul)
+from ..ops.linear import (ACT_DTYPE, EPI_ADD_F32, EPI_BF16, EPI_F32, EPI_GEGLU, EPI_SWIGLU, QWeight, concat_rows,
+                          interleave_gate_up, qmatmul)
 from ..ops.moe import MoEWeights, moe_ffn
 from .config import LlamaConfig
 
@@ -49,6 +54,10 @@ class LlamaLayer:
     moe: "MoEWeights | None" = None
     q_norm: torch.Tensor | None = None  # [head_dim] fp32 (Qwen3 per-head q/k RMSNorm)
     k_norm: torch.Tensor | None = None
+    post_attn_norm: torch.Tensor | None = None  # [hidden] fp32 (Gemma 2/3)
+    post_ffn_norm: torch.Tensor | None = None
+    window: int = 0  # sliding-window attention (0 = full)
+    rope: tuple | None = None  # (inv_freq, attn_factor) of windowed layers with their own RoPE base
 
 
 @dataclass
@@ -101,6 +110,8 @@ class Workspace:
         self.act = torch.empty((T, F), dtype=act, device=dev)
         self.act2 = torch.empty((T, F), dtype=act, device=dev) if dev.type == "cpu" else None
         self.hs = torch.empty((max_seqs, H), dtype=torch.float32, device=dev)
+        # projection output before the post-norm (Gemma 2/3)
+        self.y = torch.empty((T, H), dtype=torch.float32, device=dev) if cfg.post_norms else None
         self.logits = torch.empty((max_seqs, cfg.vocab), dtype=torch.float32, device=dev)
         nh = cfg.n_heads // tp_size
         self.part_ml = torch.empty((max_seqs * nh * max_parts, 2), dtype=torch.float32, device=dev)
@@ -124,7 +135,12 @@ class LlamaModel:
                                   llama3=cfg.rope_llama3, freq_factors=cfg.extra.get("rope_freqs"))
         self.inv_freq = inv.to(self.device)
         self.attn_factor = af
-        self.scale = 1.0 / math.sqrt(cfg.head_dim)
+        self.scale = cfg.attn_scale or 1.0 / math.sqrt(cfg.head_dim)
+        self.local_rope = None
+        if cfg.rope_base_local and cfg.sliding_window:
+            li, la = K.rope_inv_freq(rot, cfg.rope_base_local)
+            self.local_rope = (li.to(self.device), la)
+        self.glu_epi = EPI_GEGLU if cfg.ffn_act == "gelu" else EPI_SWIGLU
         self.n_heads = cfg.n_heads // tp_size
         self.n_kv = max(1, cfg.n_kv_heads // tp_size)
 
@@ -214,6 +230,9 @@ class LlamaModel:
                 wd = qw(p + "ffn_down.weight", ("row", cfg.ffn))
             qn = f32(p + "attn_q_norm.weight") if cfg.qk_norm else None
             kn = f32(p + "attn_k_norm.weight") if cfg.qk_norm else None
+            pan = f32(p + "post_attention_norm.weight") if cfg.post_norms else None
+            pfn = f32(p + "post_ffw_norm.weight") if cfg.post_norms else None
+            win = cfg.layer_window(i)
             layer = LlamaLayer(
                 attn_norm=f32(p + "attn_norm.weight").float(),
                 ffn_norm=f32(p + "ffn_norm.weight").float(),
@@ -223,6 +242,9 @@ class LlamaModel:
                 wd=wd, moe=moe,
                 q_norm=qn.float().contiguous() if qn is not None else None,
                 k_norm=kn.float().contiguous() if kn is not None else None,
+                post_attn_norm=pan.float().contiguous() if pan is not None else None,
+                post_ffn_norm=pfn.float().contiguous() if pfn is not None else None,
+                window=win, rope=m.local_rope if win else None,
             )
             m.layers.append(layer)
             if progress:
@@ -323,26 +345,25 @@ class LlamaModel:
                     qmatmul(w, xb, EPI_F32, sl, out_zeroed=True)
                 off += w.N
             q = ws.q[:T]
-            K.rope_kv(qkv, L.bqkv, fb.positions, fb.slots, self.inv_freq, self.attn_factor, Hq, Hkv, D,
+            inv_freq, attn_factor = L.rope or (self.inv_freq, self.attn_factor)
+            K.rope_kv(qkv, L.bqkv, fb.positions, fb.slots, inv_freq, attn_factor, Hq, Hkv, D,
                       cfg.rope_dim, cfg.neox, q.view(T, Hq, D), kc, vc, kv.block_size,
                       qk_norm=(L.q_norm, L.k_norm, eps) if L.q_norm is not None else None, zero_after=True)
             attn = ws.attn[:T]
             if nd:
                 K.attn_decode(q[:nd].view(nd, Hq, D), kc, vc, fb.dec_block_tables, fb.dec_seq_lens, self.scale,
                               attn[:nd].view(nd, Hq, D), max_seq_len=fb.dec_max_len or None,
-                              workspace=(ws.part_ml, ws.part_o))
+                              workspace=(ws.part_ml, ws.part_o), window=L.window, softcap=cfg.attn_softcap)
             if T > nd:
                 K.attn_prefill(q[nd:].view(T - nd, Hq, D), kc, vc, fb.pf_block_tables, fb.pf_cu_q, fb.pf_ctx_lens,
-                               self.scale, attn[nd:].view(T - nd, Hq, D), fb.pf_q_lens_host, fb.pf_ctx_lens_host)
-            if self.tp_size > 1 and self.tp_rank != 0:
-                h.zero_()
+                               self.scale, attn[nd:].view(T - nd, Hq, D), fb.pf_q_lens_host, fb.pf_ctx_lens_host,
+                               window=L.window, softcap=cfg.attn_softcap)
             if gemv:
                 aq, ads = ws.q8(T, qd)
                 K.quant_q8(attn, aq, ads)
-                qmatmul(L.wo, None, EPI_ADD_F32, h, xq=aq, xds=ads)
             else:
-                qmatmul(L.wo, attn, EPI_ADD_F32, h)
-            self._allreduce(h)
+                aq = ads = None
+            self._residual_proj(L.wo, attn, aq, ads, h, L.post_attn_norm, ws, T, eps)
             # ---- FFN block ----
             if L.moe is not None:
                 K.rmsnorm(h, L.ffn_norm, eps, out_bf16=xb)
@@ -357,25 +378,22 @@ class LlamaModel:
             act = ws.act[:T]
             if L.wgu is not None:
                 if gemv:
-                    qmatmul(L.wgu, None, EPI_SWIGLU, act, xq=xq, xds=xds)
+                    qmatmul(L.wgu, None, self.glu_epi, act, xq=xq, xds=xds)
                 else:
-                    qmatmul(L.wgu, xb, EPI_SWIGLU, act)
+                    qmatmul(L.wgu, xb, self.glu_epi, act)
             else:
                 g_out = torch.empty((T, F), dtype=ACT_DTYPE, device=h.device)
                 u_out = torch.empty((T, F), dtype=ACT_DTYPE, device=h.device)
                 xin = xb if not gemv else None
                 qmatmul(L.wg, xin, EPI_BF16, g_out, xq=xq, xds=xds)
                 qmatmul(L.wu, xin, EPI_BF16, u_out, xq=xq, xds=xds)
-                K.glu(g_out, u_out, act, "silu")
-            if self.tp_size > 1 and self.tp_rank != 0:
-                h.zero_()
+                K.glu(g_out, u_out, act, cfg.ffn_act)
             if gemv:
                 aq, ads = ws.q8(T, F)
                 K.quant_q8(act, aq, ads)
-                qmatmul(L.wd, None, EPI_ADD_F32, h, xq=aq, xds=ads)
             else:
-                qmatmul(L.wd, act, EPI_ADD_F32, h)
-            self._allreduce(h)
+                aq = ads = None
+            self._residual_proj(L.wd, act, aq, ads, h, L.post_ffn_norm, ws, T, eps)
         # ---- head ----
         S = fb.logits_idx.numel()
         hs = ws.hs[:S]
@@ -394,7 +412,31 @@ class LlamaModel:
             xbs = ws.xb[:S, :H]
             K.rmsnorm(hs, self.out_norm, eps, out_bf16=xbs)
             qmatmul(self.lm_head, xbs, EPI_F32, logits)
+        if cfg.final_softcap:
+            c = cfg.final_softcap
+            torch.tanh(logits.div_(c), out=logits).mul_(c)
         return logits
+
+    def _residual_proj(self, W: QWeight, x, xq, xds, h: torch.Tensor, post_norm, ws: Workspace, T: int, eps: float):
+        """h += x W^T — or, with a Gemma post-norm, h += rmsnorm(x W^T) * post_norm. Under tensor
+        parallelism the partial projections are all-reduced before the (replicated) norm."""
+        gemv = xq is not None
+        if post_norm is None:
+            if self.tp_size > 1 and self.tp_rank != 0:
+                h.zero_()
+            if gemv:
+                qmatmul(W, None, EPI_ADD_F32, h, xq=xq, xds=xds)
+            else:
+                qmatmul(W, x, EPI_ADD_F32, h)
+            self._allreduce(h)
+            return
+        y = ws.y[:T]
+        if gemv:
+            qmatmul(W, None, EPI_F32, y, xq=xq, xds=xds)
+        else:
+            qmatmul(W, x, EPI_F32, y)
+        self._allreduce(y)
+        K.rmsnorm_add(y, post_norm, eps, h)
 
 
 def load_moe(m: LlamaModel, get_tensor, p: str, f32, qw, fuse: bool) -> MoEWeights:

@@ -58,6 +58,9 @@ def llama_tensor_plan(cfg: LlamaConfig, ftype: str = "Q4_K_M"):
                 (p + "ffn_up.weight", (H, F), base),
                 (p + "ffn_down.weight", (F, H), hi if mb else base),
             ]
+        if cfg.post_norms:
+            out += [(p + "post_attention_norm.weight", (H,), QType.F32),
+                    (p + "post_ffw_norm.weight", (H,), QType.F32)]
         if cfg.qk_norm:
             out += [(p + "attn_q_norm.weight", (cfg.head_dim,), QType.F32),
                     (p + "attn_k_norm.weight", (cfg.head_dim,), QType.F32)]
@@ -126,6 +129,16 @@ def gguf_metadata(cfg: LlamaConfig, ftype: str = "Q4_K_M") -> dict:
         md[f"{a}.expert_feed_forward_length"] = cfg.expert_ffn
         if cfg.expert_shared_ffn:
             md[f"{a}.expert_shared_feed_forward_length"] = cfg.expert_shared_ffn
+    if cfg.arch == "gemma2":
+        md[f"{a}.attn_logit_softcapping"] = float(cfg.attn_softcap)
+        md[f"{a}.final_logit_softcapping"] = float(cfg.final_softcap)
+        md[f"{a}.attention.sliding_window"] = cfg.sliding_window
+    if cfg.arch == "gemma3":
+        md[f"{a}.attention.sliding_window"] = cfg.sliding_window
+        md[f"{a}.attention.sliding_window_pattern"] = cfg.swa_pattern
+        if cfg.rope_scale != 1.0:
+            md[f"{a}.rope.scaling.type"] = cfg.rope_scaling
+            md[f"{a}.rope.scaling.factor"] = float(1.0 / cfg.rope_scale)
     if cfg.head_dim * cfg.n_heads != cfg.hidden:
         md[f"{a}.attention.key_length"] = cfg.head_dim
         md[f"{a}.attention.value_length"] = cfg.head_dim

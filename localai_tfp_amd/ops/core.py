@@ -42,6 +42,19 @@ def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, *, out_bf16: torch.Ten
             N.stream_ptr())
 
 
+def rmsnorm_add(y: torch.Tensor, w: torch.Tensor, eps: float, h: torch.Tensor):
+    """h += y / rms(y) * w (fp32 rows [M, H]; Gemma's post-attention / post-FFN norm)."""
+    M, H = y.shape
+    if M == 0:
+        return h
+    if not y.is_cuda:
+        h.add_(y * torch.rsqrt(y.pow(2).mean(-1, keepdim=True) + eps) * w)
+        return h
+    N.kcall("mxk_rmsnorm_add", y.data_ptr(), y.stride(0), w.data_ptr(), h.data_ptr(), h.stride(0), M, H,
+            float(eps), N.stream_ptr())
+    return h
+
+
 def _quant_q8_ref(y: torch.Tensor, xq: torch.Tensor, xds: torch.Tensor):
     M, K = y.shape
     b = y.float().reshape(M, K // 32, 32)
@@ -279,8 +292,10 @@ def rope_kv(qkv: torch.Tensor, bias: torch.Tensor | None, positions: torch.Tenso
 # attention
 
 
-def _attn_ref_one(q, k_cache, v_cache, table, ctx: int, qpos0: int, scale: float, block_size: int):
-    """q [t, Hq, D] for query positions qpos0..qpos0+t-1 of one sequence; causal over ctx keys."""
+def _attn_ref_one(q, k_cache, v_cache, table, ctx: int, qpos0: int, scale: float, block_size: int,
+                  window: int = 0, softcap: float = 0.0):
+    """q [t, Hq, D] for query positions qpos0..qpos0+t-1 of one sequence; causal over ctx keys
+    (sliding `window` > 0: keys with qpos - kpos < window; `softcap` > 0: tanh score capping)."""
     t, Hq, D = q.shape
     Hkv = k_cache.shape[1]
     nb = (ctx + block_size - 1) // block_size
@@ -291,16 +306,22 @@ def _attn_ref_one(q, k_cache, v_cache, table, ctx: int, qpos0: int, scale: float
     k = k.repeat_interleave(G, 0)
     v = v.repeat_interleave(G, 0)
     s = torch.einsum("thd,hkd->htk", q.float(), k) * scale
+    if softcap > 0:
+        s = softcap * torch.tanh(s / softcap)
     qp = torch.arange(qpos0, qpos0 + t)[:, None]
     kp = torch.arange(ctx)[None, :]
-    s = s.masked_fill((kp > qp)[None], float("-inf"))
+    bad = kp > qp
+    if window > 0:
+        bad = bad | (kp <= qp - window)
+    s = s.masked_fill(bad[None], float("-inf"))
     p = torch.softmax(s, -1)
     return torch.einsum("htk,hkd->thd", p, v)
 
 
 def attn_decode(q: torch.Tensor, k_cache, v_cache, block_tables: torch.Tensor, seq_lens: torch.Tensor,
                 scale: float, out: torch.Tensor, part_size: int = 256, n_parts: int | None = None,
-                workspace: tuple | None = None, max_seq_len: int | None = None):
+                workspace: tuple | None = None, max_seq_len: int | None = None, window: int = 0,
+                softcap: float = 0.0):
     """q bf16 [B, Hq, D] (one query token per sequence, at position seq_len-1)."""
     B, Hq, D = q.shape
     if B == 0:
@@ -309,7 +330,8 @@ def attn_decode(q: torch.Tensor, k_cache, v_cache, block_tables: torch.Tensor, s
     if not q.is_cuda:
         for b in range(B):
             L = int(seq_lens[b])
-            out[b] = _attn_ref_one(q[b:b + 1], k_cache, v_cache, block_tables[b], L, L - 1, scale, bs)[0].to(out.dtype)
+            out[b] = _attn_ref_one(q[b:b + 1], k_cache, v_cache, block_tables[b], L, L - 1, scale, bs, window,
+                                   softcap)[0].to(out.dtype)
         return out
     if n_parts is None:
         ml = max_seq_len if max_seq_len is not None else int(seq_lens.max())
@@ -325,7 +347,8 @@ def attn_decode(q: torch.Tensor, k_cache, v_cache, block_tables: torch.Tensor, s
     N.ensure_act(out.dtype)
     N.kcall("mxk_attn_decode", q.data_ptr(), q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
             block_tables.data_ptr(), block_tables.stride(0), seq_lens.data_ptr(), B, Hq, Hkv, D, bs, float(scale),
-            part_size, n_parts, out.data_ptr(), out.stride(0), N.ptr(ml_t), N.ptr(po), N.stream_ptr())
+            int(window), float(softcap), part_size, n_parts, out.data_ptr(), out.stride(0), N.ptr(ml_t), N.ptr(po),
+            N.stream_ptr())
     return out
 
 
@@ -343,7 +366,7 @@ ATTN_VMODE = int(__import__("os").environ.get("MX_ATTN_VMODE", "0"))
 
 def attn_prefill(q: torch.Tensor, k_cache, v_cache, block_tables: torch.Tensor, cu_q: torch.Tensor,
                  ctx_lens: torch.Tensor, scale: float, out: torch.Tensor, q_lens_host=None, ctx_lens_host=None,
-                 vmode: int | None = None):
+                 vmode: int | None = None, window: int = 0, softcap: float = 0.0):
     """q bf16 [T, Hq, D] for S sequences (cu_q [S+1]); keys 0..ctx_len-1 from the paged cache."""
     T, Hq, D = q.shape
     if T == 0:
@@ -359,7 +382,7 @@ def attn_prefill(q: torch.Tensor, k_cache, v_cache, block_tables: torch.Tensor, 
         for s, ql in enumerate(q_lens_host):
             ctx = int(ctx_lens_host[s])
             out[off:off + ql] = _attn_ref_one(q[off:off + ql], k_cache, v_cache, block_tables[s], ctx, ctx - ql,
-                                              scale, bs).to(out.dtype)
+                                              scale, bs, window, softcap).to(out.dtype)
             off += ql
         return out
     rows = N.kernels().mxk_attn_prefill_rows(Hq, Hkv)
@@ -368,7 +391,7 @@ def attn_prefill(q: torch.Tensor, k_cache, v_cache, block_tables: torch.Tensor, 
     N.ensure_act(out.dtype)
     N.kcall("mxk_attn_prefill", q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), block_tables.data_ptr(),
             block_tables.stride(0), tiles[0].data_ptr(), tiles[1].data_ptr(), len(seqs), cu_q.data_ptr(),
-            ctx_lens.data_ptr(), Hq, Hkv, D, bs, float(scale), out.data_ptr(),
+            ctx_lens.data_ptr(), Hq, Hkv, D, bs, float(scale), int(window), float(softcap), out.data_ptr(),
             ATTN_VMODE if vmode is None else int(vmode), N.stream_ptr())
     return out
 

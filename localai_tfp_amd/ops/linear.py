@@ -23,7 +23,8 @@ from .. import _native as N
 from ..formats.gguf import QType
 from . import quant as Q
 
-EPI_F32, EPI_BF16, EPI_ADD_F32, EPI_SWIGLU = 0, 1, 2, 3
+EPI_F32, EPI_BF16, EPI_ADD_F32, EPI_SWIGLU, EPI_GEGLU = 0, 1, 2, 3, 4
+GLU_EPIS = (EPI_SWIGLU, EPI_GEGLU)  # gated-FFN epilogues over 16-row interleaved gate|up weights
 EPI_ACT = EPI_BF16  # "16-bit activation out" (bf16 or f16 by the output tensor's dtype)
 CU_COUNT = 256
 _os = __import__("os")
@@ -182,7 +183,8 @@ def qmatmul(W: QWeight, x: torch.Tensor | None, epi: int, out: torch.Tensor, *, 
     """out (+)= x @ W^T with the given epilogue.
 
     x:   bf16 [M, K] (MFMA / dense path) — may be None when (xq, xds) given and M <= 4
-    epi: EPI_F32 (store fp32) | EPI_BF16 | EPI_ADD_F32 (out += ; fp32) | EPI_SWIGLU (bf16 [M, N/2])
+    epi: EPI_F32 (store fp32) | EPI_BF16 | EPI_ADD_F32 (out += ; fp32) | EPI_SWIGLU / EPI_GEGLU
+         (silu- / gelu-gated, 16-bit [M, N/2])
     out_zeroed: for EPI_F32, caller guarantees `out` is zero so split-K may accumulate atomically.
     """
     M = (x if x is not None else xq).shape[0]
@@ -195,7 +197,7 @@ def qmatmul(W: QWeight, x: torch.Tensor | None, epi: int, out: torch.Tensor, *, 
         y = torch.matmul(x, W.data.t()) if x.dtype == W.data.dtype else torch.matmul(x.to(W.data.dtype), W.data.t())
         return _apply_epi_dense(y, epi, out)
     if M <= 4 and xq is not None:
-        if epi in (EPI_BF16, EPI_SWIGLU):
+        if epi in (EPI_BF16, *GLU_EPIS):
             N.ensure_act(out.dtype)
         N.kcall("mxk_qgemv", int(W.qtype), epi, xq.data_ptr(), xds.data_ptr(), W.data.data_ptr(), N.ptr(W.dplane),
                 M, W.N, W.K, out.data_ptr(), out.stride(0), N.stream_ptr())
@@ -213,10 +215,10 @@ def qmatmul(W: QWeight, x: torch.Tensor | None, epi: int, out: torch.Tensor, *, 
                 torch.mm(x, wt, out_dtype=torch.float32, out=out)
             return out
         y = torch.matmul(x, wt)
-        if epi == EPI_SWIGLU:
+        if epi in GLU_EPIS:
             N.ensure_act(out.dtype)
             N.kcall("mxk_swiglu_il16", y.data_ptr(), y.stride(0), out.data_ptr(), out.stride(0), M, W.N // 2,
-                    N.stream_ptr())
+                    int(epi == EPI_GEGLU), N.stream_ptr())
             return out
         return _apply_epi_dense(y, epi, out)
     nblk = W.K // 256
@@ -224,9 +226,9 @@ def qmatmul(W: QWeight, x: torch.Tensor | None, epi: int, out: torch.Tensor, *, 
     if f16 and M >= Q32_MIN_M:
         wm, wn, splits = _mfma32_shape(M, W.N, nblk, can_split)
         e = EPI_ADD_F32 if (epi == EPI_F32 and splits > 1) else epi
-        if e in (EPI_BF16, EPI_SWIGLU) and out.dtype != x.dtype:
+        if e in (EPI_BF16, *GLU_EPIS) and out.dtype != x.dtype:
             raise ValueError(f"qmatmul: {out.dtype} output with {x.dtype} activations")
-        if e in (EPI_BF16, EPI_SWIGLU):
+        if e in (EPI_BF16, *GLU_EPIS):
             N.ensure_act(out.dtype)
         N.kcall("mxk_qgemm32", int(W.qtype), e, wm, wn, x.data_ptr(), x.stride(0), W.data.data_ptr(), N.ptr(W.dplane),
                 M, W.N, W.K, splits, out.data_ptr(), out.stride(0), N.stream_ptr())
@@ -235,7 +237,7 @@ def qmatmul(W: QWeight, x: torch.Tensor | None, epi: int, out: torch.Tensor, *, 
     e = epi
     if epi == EPI_F32 and splits > 1:
         e = EPI_ADD_F32
-    if e in (EPI_BF16, EPI_SWIGLU) and out.dtype != x.dtype:
+    if e in (EPI_BF16, *GLU_EPIS) and out.dtype != x.dtype:
         raise ValueError(f"qmatmul: {out.dtype} output with {x.dtype} activations")
     N.kcall("mxk_qgemm16" if f16 else "mxk_qgemm_mfma", int(W.qtype), e, wm, wn, x.data_ptr(), x.stride(0),
             W.data.data_ptr(), N.ptr(W.dplane), M, W.N, W.K, splits, out.data_ptr(), out.stride(0), N.stream_ptr())
@@ -252,7 +254,7 @@ def dense_min_m(dtype, epi: int = EPI_ADD_F32, can_split: bool = True) -> int:
         return BF16_CACHE_MIN_M
     if dtype != torch.float16:
         return 128
-    if epi == EPI_SWIGLU:
+    if epi in GLU_EPIS:
         return DENSE_MIN_M_SWIGLU
     if not can_split:
         return DENSE_MIN_M_NOSPLIT
@@ -336,7 +338,9 @@ def _apply_epi_dense(y: torch.Tensor, epi: int, out: torch.Tensor):
         g = Nn // 32
         v = yf.reshape(-1, g, 2, 16)
         gate, up = v[:, :, 0, :].reshape(-1, Nn // 2), v[:, :, 1, :].reshape(-1, Nn // 2)
-        out.copy_(torch.nn.functional.silu(gate) * up)
+        act = torch.nn.functional.silu(gate) if epi == EPI_SWIGLU else \
+            torch.nn.functional.gelu(gate, approximate="tanh")
+        out.copy_(act * up)
     return out
 
 
