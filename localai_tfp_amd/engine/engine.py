@@ -44,6 +44,8 @@ class EngineConfig:
     graph_buckets: tuple = (1, 2, 4, 8, 16, 32, 48, 64, 96, 128, 160, 192, 224, 256)
     attn_part_size: int = 256  # must match ops.core.attn_decode's default
     prefill_bf16_cache: bool = True  # dense bf16 copy of the linear weights for M>=128 prefill (GPU)
+    n_draft: int = 0  # speculative decoding: draft tokens per step (needs a draft model; 0 = off)
+    spec_max_batch: int = 32  # speculate only on decode batches up to this size (latency-bound regime)
 
 
 class RequestHandle:
@@ -140,7 +142,8 @@ class DecodeGraph:
 
 
 class LLMEngine:
-    def __init__(self, model: LlamaModel, tokenizer, cfg: EngineConfig | None = None, tp=None):
+    def __init__(self, model: LlamaModel, tokenizer, cfg: EngineConfig | None = None, tp=None,
+                 draft: LlamaModel | None = None):
         self.tp = tp  # parallel.tp_engine.TPLink (leader or follower side) when tensor parallel
         self.model = model
         self.tok = tokenizer
@@ -150,8 +153,14 @@ class LLMEngine:
         c = self.cfg
         c.max_model_len = min(c.max_model_len, max(mc.ctx_train, 256)) if c.max_model_len else mc.ctx_train
         self.max_blocks_per_seq = (c.max_model_len + c.block_size - 1) // c.block_size
+        use_spec = draft is not None and c.n_draft > 0 and tp is None
+        frac = c.kv_mem_fraction
+        if use_spec:  # the draft's cache shares the block ids: split the pool bytes between the two
+            per_t = KVCache.bytes_per_block(mc.n_layers, model.n_kv, c.block_size, mc.head_dim)
+            per_d = KVCache.bytes_per_block(draft.cfg.n_layers, draft.n_kv, c.block_size, draft.cfg.head_dim)
+            frac *= per_t / (per_t + per_d)
         nb = c.num_blocks or KVCache.auto_num_blocks(mc.n_layers, model.n_kv, c.block_size, mc.head_dim, self.device,
-                                                     c.kv_mem_fraction)
+                                                     frac)
         if self.tp is not None:  # every rank must hold the same block ids
             nb = self.tp.allreduce_min(nb)
         self.kv = KVCache(mc.n_layers, nb, model.n_kv, c.block_size, mc.head_dim, self.device)
@@ -178,6 +187,10 @@ class LLMEngine:
         self.batch_sink: BatchedSink | None = None
         if c.prefill_bf16_cache and self.device.type == "cuda":
             model.enable_prefill_bf16_cache()
+        self.spec = None
+        if use_spec:
+            from .speculative import SpeculativeDecoder
+            self.spec = SpeculativeDecoder(self, draft, c.n_draft, c.spec_max_batch)
 
     # ------------------------------------------------------------------ request API
     def submit(self, req: Request, sink=None, batch_key=None) -> RequestHandle:
@@ -297,6 +310,15 @@ class LLMEngine:
                 self.stats["preemptions"] += 1
         if so.empty:
             return
+        if self.spec is not None:
+            for s in so.preempted:
+                self.spec.forget(s.rid)
+            if self.spec.eligible(so) and self.spec.step(so):
+                st = self.stats
+                st["steps"] += 1
+                st["decode_tokens"] += len(so.decode)
+                st["busy_s"] += time.perf_counter() - t0
+                return
         t1 = time.perf_counter()
         toks, lps = self._forward_and_sample(so)
         t2 = time.perf_counter()
@@ -521,16 +543,23 @@ class LLMEngine:
                     else:
                         h.put(o)
                 continue
-            t = int(toks[k])
-            lp = lps[k] if lps is not None else None
+            self._accept_tokens(s, [int(toks[k])], [lps[k]] if lps is not None else None)
+
+    def _accept_tokens(self, s: Sequence, toks: list, lps: list | None):
+        """Append sampled tokens to a sequence (one per plain step, several per speculative step),
+        stopping at the first stop condition; flush text and emit. Returns (tokens appended, reason)."""
+        reason = None
+        n = 0
+        for j, t in enumerate(toks):
+            lp = lps[j] if lps is not None else None
             if s.grammar is not None:
                 s.grammar.accept(t)
             if s.params.mirostat == 2 and lp is not None:
                 # mu <- mu - eta * (surprise - tau)  (surprise in bits)
                 s.mirostat_mu -= s.params.mirostat_eta * (-lp / 0.6931471805599453 - s.params.mirostat_tau)
             s.append_token(t, lp)
+            n += 1
             self.stats["out_tokens"] += 1
-            reason = None
             if (t in self.eos_ids or t in s.req.stop_token_ids) and not s.params.ignore_eos:
                 reason = "stop"
                 s.output_ids.pop()  # EOS is not part of the visible output
@@ -541,12 +570,15 @@ class LLMEngine:
                 reason = "length"
             elif s.grammar is not None and s.grammar.is_done():
                 reason = "stop"
-            text, hit = s.flush_text(final=reason is not None)
-            if hit:
-                reason = "stop"
             if reason:
-                self.sched.finish(s, reason)
-            self._emit(s, text, reason)
+                break
+        text, hit = s.flush_text(final=reason is not None)
+        if hit:
+            reason = "stop"
+        if reason:
+            self.sched.finish(s, reason)
+        self._emit(s, text, reason)
+        return n, reason
 
     def _emit(self, s: Sequence, text: str, reason: str | None):
         h = self.handles.get(s.rid)
@@ -554,6 +586,8 @@ class LLMEngine:
         o = StepOutput(s.rid, text, ids, lp, reason is not None, reason)
         if reason is not None:
             self._fill_usage(s, o)
+            if self.spec is not None:
+                self.spec.forget(s.rid)
             self.handles.pop(s.rid, None)
             self.seqs.pop(s.rid, None)
             st = self.stats

@@ -34,6 +34,7 @@ class Request:
     # multimodal: (prompt position, fp32 [n, hidden] device tensor) spans whose input embeddings
     # replace the placeholder tokens there (llava image embeddings, grpc-server.cpp:1455-1520)
     mm_embeds: list = field(default_factory=list)
+    n_draft: int = 0  # speculative decoding: max draft tokens per step for this request (0 = engine's)
 
 
 @dataclass

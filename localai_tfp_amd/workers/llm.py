@@ -220,7 +220,19 @@ class LLMServicer(BackendServicer):
                 if self.vision.cfg.proj_hidden != mcfg.hidden:
                     raise ValueError(f"mmproj projects to {self.vision.cfg.proj_hidden} but the LLM hidden size is "
                                      f"{mcfg.hidden}; make sure that you use the correct mmproj file")
-            self.engine = LLMEngine(model, tok, ec, tp=self.tp)
+            draft = None
+            if request.DraftModel and self.tp is None:
+                # speculative decoding (llama.cpp `-md` / reference `draft_model`): same tokenizer,
+                # same GPU; k draft tokens per step from the `n_draft` option (default 4)
+                dp = request.DraftModel
+                if not dp.startswith("synthetic:") and not os.path.isabs(dp) and request.ModelPath:
+                    dp = os.path.join(request.ModelPath, dp)
+                draft, _dtok, dcfg, _ = load_llm(dp, self.device)
+                if dcfg.vocab > mcfg.vocab:
+                    raise ValueError(f"draft model vocab ({dcfg.vocab}) does not match the model's ({mcfg.vocab})")
+                ec.n_draft = int(opts.get("n_draft", 4) or 4)
+                ec.spec_max_batch = int(opts.get("spec_max_batch", ec.spec_max_batch))
+            self.engine = LLMEngine(model, tok, ec, tp=self.tp, draft=draft)
             if not opts.get("lazy_graphs"):
                 self.engine.precapture_graphs()
             self.engine.start()
@@ -319,6 +331,7 @@ class LLMServicer(BackendServicer):
         max_tokens = mt if mt > 0 else self.engine.cfg.max_model_len
         req = Request(ids, sampling_from_predict(r), max_tokens, [s for s in r.StopPrompts if s])
         req.cache_prompt = not mm  # image placeholders must not enter the prefix cache (reference: same)
+        req.n_draft = int(r.NDraft or 0)  # per-request cap on speculative draft length (0 = engine default)
         req.mm_embeds = mm
         req.n_keep = int(r.NKeep) if r.NKeep > 0 else 0
         if r.Grammar:
