@@ -1,6 +1,7 @@
 // attention.hip — paged GQA attention for the LLM worker (K4/K5 of SURVEY §2.6).
 //
-// KV cache layout (written by rope_kv.hip): [num_blocks][Hkv][block_size][D] bf16.
+// KV cache layout (written by rope_kv.hip): [num_blocks][Hkv][block_size][D] bf16, or fp8 e4m3
+// (KV8: half the bytes per position; widened to fp32 in registers / to bf16 while staging to LDS).
 //
 // decode  (one query token per sequence): memory-bound split-K over context partitions. A 256-thread
 //   workgroup owns (sequence, kv-head, partition); D/8 lanes cover one cached position with 16-byte
@@ -17,10 +18,10 @@
 #define LOG2E 1.4426950408889634f
 
 // ------------------------------------------------------------------------------------------------
-template <int D, int G, bool F16>
+template <int D, int G, bool F16, bool KV8>
 __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restrict__ q, int q_stride,
-                                                          const bf16_t* __restrict__ kc,
-                                                          const bf16_t* __restrict__ vc,
+                                                          const void* __restrict__ kcv,
+                                                          const void* __restrict__ vcv,
                                                           const int* __restrict__ block_tables, int bt_stride,
                                                           const int* __restrict__ seq_lens, int Hkv, int bs,
                                                           float scale, int window, float softcap, int part_size,
@@ -73,6 +74,10 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restri
     constexpr int MAXB = 256;  // part_size / bs + 1 <= MAXB (host checks)
     __shared__ int sbt[MAXB];
     const int* bt = block_tables + (size_t)b * bt_stride;
+    using kvec = typename KVVec<KV8>::T;
+    constexpr int ES = KV8 ? 1 : 2;  // bytes per cached element
+    const char* kc = (const char*)kcv;
+    const char* vc = (const char*)vcv;
     const int blk0 = p0 / bs;
     const int nblk = p1 > p0 ? (p1 - 1) / bs - blk0 + 1 : 0;
     for (int i = threadIdx.x; i < nblk; i += 256) sbt[i] = bt[blk0 + i];
@@ -81,29 +86,26 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restri
     constexpr int STEP = PPB * U;
     // two register buffers with compile-time names (a runtime buffer index, or arrays passed by
     // reference to helpers, would put them in scratch): the step is a macro over (K, V)
-    u32x4 ka[U], va[U], kb[U], vb[U];
+    kvec ka[U], va[U], kb[U], vb[U];
 #define DEC_LOAD(K, V, BASE)                                                                  \
     _Pragma("unroll") for (int u = 0; u < U; ++u) {                                           \
         const int p = (BASE) + u * PPB + wave * PPW + pg;                                     \
         if (p < p1) {                                                                         \
             const int blk = sbt[p / bs - blk0], off = p % bs;                                 \
             const size_t eo = (((size_t)blk * Hkv + kvh) * bs + off) * D + dl * 8;            \
-            K[u] = __builtin_nontemporal_load((const u32x4*)(kc + eo));                       \
-            V[u] = __builtin_nontemporal_load((const u32x4*)(vc + eo));                       \
+            K[u] = __builtin_nontemporal_load((const kvec*)(kc + eo * ES));                   \
+            V[u] = __builtin_nontemporal_load((const kvec*)(vc + eo * ES));                   \
         } else {                                                                              \
-            K[u] = V[u] = (u32x4){0u, 0u, 0u, 0u};                                            \
+            K[u] = V[u] = kvec{};                                                             \
         }                                                                                     \
     }
 #define DEC_CONSUME(K, V, BASE)                                                               \
     _Pragma("unroll") for (int h = 0; h < G; ++h) {                                           \
         float s[U];                                                                           \
         _Pragma("unroll") for (int u = 0; u < U; ++u) {                                       \
-            float acc = 0.f;                                                                  \
-            _Pragma("unroll") for (int j = 0; j < 4; ++j) {                                   \
-                const uint32_t kw = K[u][j];                                                  \
-                acc = fmaf(qf[h][2 * j], __uint_as_float(kw << 16), acc);                     \
-                acc = fmaf(qf[h][2 * j + 1], __uint_as_float(kw & 0xFFFF0000u), acc);         \
-            }                                                                                 \
+            float acc = 0.f, kf[8];                                                           \
+            kv_unpack8<KV8>(K[u], kf);                                                        \
+            _Pragma("unroll") for (int j = 0; j < 8; ++j) acc = fmaf(qf[h][j], kf[j], acc);   \
             s[u] = group_sum<LPP>(acc);                                                       \
             if (softcap > 0.f) s[u] = sc_l2 * tanhf(s[u] * sc_inv);                           \
             if ((BASE) + u * PPB + wave * PPW + pg >= p1) s[u] = -INFINITY;                   \
@@ -117,11 +119,9 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restri
             _Pragma("unroll") for (int u = 0; u < U; ++u) {                                   \
                 const float pr = exp2f(s[u] - mx);                                            \
                 l[h] += pr;                                                                   \
-                _Pragma("unroll") for (int j = 0; j < 4; ++j) {                               \
-                    const uint32_t vw = V[u][j];                                              \
-                    o[h][2 * j] = fmaf(pr, __uint_as_float(vw << 16), o[h][2 * j]);           \
-                    o[h][2 * j + 1] = fmaf(pr, __uint_as_float(vw & 0xFFFF0000u), o[h][2 * j + 1]); \
-                }                                                                             \
+                float vf[8];                                                                  \
+                kv_unpack8<KV8>(V[u], vf);                                                    \
+                _Pragma("unroll") for (int j = 0; j < 8; ++j) o[h][j] = fmaf(pr, vf[j], o[h][j]); \
             }                                                                                 \
             m[h] = mx;                                                                        \
         }                                                                                     \
@@ -211,15 +211,20 @@ __global__ __launch_bounds__(128) void attn_decode_reduce_kernel(const float2* _
 }
 
 template <int D, int G>
-static int launch_decode(const bf16_t* q, int q_stride, const bf16_t* kc, const bf16_t* vc, const int* bt,
+static int launch_decode(const bf16_t* q, int q_stride, const void* kc, const void* vc, const int* bt,
                          int bt_stride, const int* seq_lens, int B, int Hkv, int bs, float scale, int window,
                          float softcap, int part_size, int n_parts, bf16_t* out, int out_stride, float2* part_ml,
-                         float* part_o, hipStream_t st) {
+                         float* part_o, int kv8, hipStream_t st) {
     dim3 grid(Hkv, B, n_parts);
     MX_ACT_DISPATCH({
-        attn_decode_kernel<D, G, F16><<<grid, 256, 0, st>>>(q, q_stride, kc, vc, bt, bt_stride, seq_lens, Hkv, bs,
-                                                            scale, window, softcap, part_size, n_parts, out,
-                                                            out_stride, part_ml, part_o);
+        if (kv8)
+            attn_decode_kernel<D, G, F16, true><<<grid, 256, 0, st>>>(q, q_stride, kc, vc, bt, bt_stride, seq_lens,
+                                                                      Hkv, bs, scale, window, softcap, part_size,
+                                                                      n_parts, out, out_stride, part_ml, part_o);
+        else
+            attn_decode_kernel<D, G, F16, false><<<grid, 256, 0, st>>>(q, q_stride, kc, vc, bt, bt_stride, seq_lens,
+                                                                       Hkv, bs, scale, window, softcap, part_size,
+                                                                       n_parts, out, out_stride, part_ml, part_o);
         if (n_parts > 1)
             attn_decode_reduce_kernel<F16><<<B * Hkv * G, 128, 0, st>>>(part_ml, part_o, n_parts, Hkv * G, D, seq_lens,
                                                                         part_size, out, out_stride);
@@ -227,17 +232,17 @@ static int launch_decode(const bf16_t* q, int q_stride, const bf16_t* kc, const 
     MXK_CHECK_LAUNCH();
 }
 
-extern "C" int mxk_attn_decode(const bf16_t* q, int q_stride, const bf16_t* kc, const bf16_t* vc, const int* bt,
+extern "C" int mxk_attn_decode(const bf16_t* q, int q_stride, const void* kc, const void* vc, const int* bt,
                                int bt_stride, const int* seq_lens, int B, int Hq, int Hkv, int D, int bs,
                                float scale, int window, float softcap, int part_size, int n_parts, bf16_t* out,
-                               int out_stride, float2* part_ml, float* part_o, hipStream_t st) {
+                               int out_stride, float2* part_ml, float* part_o, int kv8, hipStream_t st) {
     if (B <= 0) return 0;
     if (Hq % Hkv) return (int)hipErrorInvalidValue;
     const int G = Hq / Hkv;
     if (n_parts > 1 && (!part_ml || !part_o)) return (int)hipErrorInvalidValue;
     if (bs <= 0 || part_size / bs + 1 > 256) return (int)hipErrorInvalidValue;  // LDS block-id stage
 #define DEC(D_, G_) \
-    if (D == D_ && G == G_) return launch_decode<D_, G_>(q, q_stride, kc, vc, bt, bt_stride, seq_lens, B, Hkv, bs, scale, window, softcap, part_size, n_parts, out, out_stride, part_ml, part_o, st);
+    if (D == D_ && G == G_) return launch_decode<D_, G_>(q, q_stride, kc, vc, bt, bt_stride, seq_lens, B, Hkv, bs, scale, window, softcap, part_size, n_parts, out, out_stride, part_ml, part_o, kv8, st);
     DEC(128, 1) DEC(128, 2) DEC(128, 3) DEC(128, 4) DEC(128, 5) DEC(128, 6) DEC(128, 7) DEC(128, 8)
     DEC(64, 1) DEC(64, 2) DEC(64, 4) DEC(64, 8) DEC(256, 1) DEC(256, 2) DEC(256, 4) DEC(256, 8)
 #undef DEC
@@ -264,10 +269,10 @@ MX_DEV int v_lds_off(int p, int nt) {
     return p * (D * 2) + ((nt ^ sv) << 5);
 }
 
-template <int D, int GW, int VT, bool F16>
+template <int D, int GW, int VT, bool F16, bool KV8>
 __global__ __launch_bounds__(512) void attn_prefill_kernel(const bf16_t* __restrict__ q,
-                                                           const bf16_t* __restrict__ kc,
-                                                           const bf16_t* __restrict__ vc,
+                                                           const void* __restrict__ kc,
+                                                           const void* __restrict__ vc,
                                                            const int* __restrict__ block_tables, int bt_stride,
                                                            const int* __restrict__ tile_seq,
                                                            const int* __restrict__ tile_q0,
@@ -334,8 +339,13 @@ __global__ __launch_bounds__(512) void attn_prefill_kernel(const bf16_t* __restr
             if (pos < kv_end) {
                 const int blk = bt[pos / bs], off = pos % bs;
                 const size_t eo = (((size_t)blk * Hkv + kvh) * bs + off) * D + c * 8;
-                kv = *(const uint4*)(kc + eo);
-                vv = *(const uint4*)(vc + eo);
+                if constexpr (KV8) {
+                    kv = fp8x8_to_bf16x8(*(const uint2*)((const uint8_t*)kc + eo));
+                    vv = fp8x8_to_bf16x8(*(const uint2*)((const uint8_t*)vc + eo));
+                } else {
+                    kv = *(const uint4*)((const bf16_t*)kc + eo);
+                    vv = *(const uint4*)((const bf16_t*)vc + eo);
+                }
             }
             *(uint4*)(k_lds + k_lds_off<D>(p, c)) = kv;
             if constexpr (VT == 0) {
@@ -444,42 +454,41 @@ __global__ __launch_bounds__(512) void attn_prefill_kernel(const bf16_t* __restr
     }
 }
 
+template <int D, int GW, int VT, bool KV8>
+static void launch_prefill_t(dim3 grid, int threads, size_t lds, const bf16_t* q, const void* kc, const void* vc,
+                             const int* bt, int bt_stride, const int* tile_seq, const int* tile_q0, const int* cu_q,
+                             const int* ctx_lens, int Hq, int Hkv, int bs, float scale, int window, float softcap,
+                             bf16_t* out, hipStream_t st) {
+    MX_ACT_DISPATCH({
+        if (lds > 65536) {  // D=256 tiles (73-82 KB): opt in to the large LDS allocation once
+            static bool opted = false;
+            if (!opted) {
+                (void)hipFuncSetAttribute((const void*)attn_prefill_kernel<D, GW, VT, F16, KV8>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+                opted = true;
+            }
+        }
+        attn_prefill_kernel<D, GW, VT, F16, KV8><<<grid, threads, lds, st>>>(
+            q, kc, vc, bt, bt_stride, tile_seq, tile_q0, cu_q, ctx_lens, Hq, Hkv, Hq / Hkv, bs, scale, window,
+            softcap, out);
+    });
+}
+
 template <int D, int GW>
-static int launch_prefill(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, const int* bt, int bt_stride,
+static int launch_prefill(const bf16_t* q, const void* kc, const void* vc, const int* bt, int bt_stride,
                           const int* tile_seq, const int* tile_q0, int n_tiles, const int* cu_q,
                           const int* ctx_lens, int Hq, int Hkv, int bs, float scale, int window, float softcap,
-                          bf16_t* out, int vmode, hipStream_t st) {
+                          bf16_t* out, int vmode, int kv8, hipStream_t st) {
     constexpr int NW = GW >= 3 ? GW : 4;
     dim3 grid(n_tiles, Hq / GW);
-    MX_ACT_DISPATCH({
-        if (vmode == 0) {
-            const size_t lds = 2 * 64 * D * 2 + NW * 16 * (64 + 8) * 2;
-            if (lds > 65536) {  // D=256 tiles (73-82 KB): opt in to the large LDS allocation once
-                static bool opted = false;
-                if (!opted) {
-                    hipFuncSetAttribute((const void*)attn_prefill_kernel<D, GW, 0, F16>,
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-                    opted = true;
-                }
-            }
-            attn_prefill_kernel<D, GW, 0, F16><<<grid, NW * 64, lds, st>>>(
-                q, kc, vc, bt, bt_stride, tile_seq, tile_q0, cu_q, ctx_lens, Hq, Hkv, Hq / Hkv, bs, scale, window,
-                softcap, out);
-        } else {
-            const size_t lds = 64 * D * 2 + D * (64 + 8) * 2 + NW * 16 * (64 + 8) * 2;
-            if (lds > 65536) {
-                static bool opted = false;
-                if (!opted) {
-                    hipFuncSetAttribute((const void*)attn_prefill_kernel<D, GW, 1, F16>,
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-                    opted = true;
-                }
-            }
-            attn_prefill_kernel<D, GW, 1, F16><<<grid, NW * 64, lds, st>>>(
-                q, kc, vc, bt, bt_stride, tile_seq, tile_q0, cu_q, ctx_lens, Hq, Hkv, Hq / Hkv, bs, scale, window,
-                softcap, out);
-        }
-    });
+    const size_t lds0 = 2 * 64 * D * 2 + NW * 16 * (64 + 8) * 2;
+    const size_t lds1 = 64 * D * 2 + D * (64 + 8) * 2 + NW * 16 * (64 + 8) * 2;
+#define PFL(VT_, K8_)                                                                                          \
+    launch_prefill_t<D, GW, VT_, K8_>(grid, NW * 64, VT_ ? lds1 : lds0, q, kc, vc, bt, bt_stride, tile_seq,    \
+                                      tile_q0, cu_q, ctx_lens, Hq, Hkv, bs, scale, window, softcap, out, st)
+    if (vmode == 0) { if (kv8) PFL(0, true); else PFL(0, false); }
+    else { if (kv8) PFL(1, true); else PFL(1, false); }
+#undef PFL
     MXK_CHECK_LAUNCH();
 }
 
@@ -491,17 +500,17 @@ extern "C" int mxk_attn_prefill_rows(int Hq, int Hkv) {
     return 16 * (NW / GW);
 }
 
-extern "C" int mxk_attn_prefill(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, const int* bt, int bt_stride,
+extern "C" int mxk_attn_prefill(const bf16_t* q, const void* kc, const void* vc, const int* bt, int bt_stride,
                                 const int* tile_seq, const int* tile_q0, int n_tiles, const int* cu_q,
                                 const int* ctx_lens, int Hq, int Hkv, int D, int bs, float scale, int window,
-                                float softcap, bf16_t* out, int vmode, hipStream_t st) {
+                                float softcap, bf16_t* out, int vmode, int kv8, hipStream_t st) {
     if (n_tiles <= 0) return 0;
     if (Hq % Hkv) return (int)hipErrorInvalidValue;
     const int G = Hq / Hkv;
     const int GW = G <= 8 ? G : 8;
     if (G > 8 && G % 8) return (int)hipErrorInvalidValue;
 #define PF(D_, GW_) \
-    if (D == D_ && GW == GW_) return launch_prefill<D_, GW_>(q, kc, vc, bt, bt_stride, tile_seq, tile_q0, n_tiles, cu_q, ctx_lens, Hq, Hkv, bs, scale, window, softcap, out, vmode, st);
+    if (D == D_ && GW == GW_) return launch_prefill<D_, GW_>(q, kc, vc, bt, bt_stride, tile_seq, tile_q0, n_tiles, cu_q, ctx_lens, Hq, Hkv, bs, scale, window, softcap, out, vmode, kv8, st);
     PF(128, 1) PF(128, 2) PF(128, 3) PF(128, 4) PF(128, 5) PF(128, 6) PF(128, 7) PF(128, 8)
     PF(64, 1) PF(64, 2) PF(64, 4) PF(64, 8)
     PF(256, 1) PF(256, 2) PF(256, 4)

@@ -19,6 +19,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 #define MX_DEV __device__ __forceinline__
 #define MX_LDS __attribute__((address_space(3)))
@@ -151,6 +152,38 @@ MX_DEV float gelu_tanh_f(float x) {
     return 0.5f * x * (1.f + tanhf(k0 * (x + k1 * x * x * x)));
 }
 MX_DEV float gelu_erf_f(float x) { return 0.5f * x * (1.f + erff(x * 0.7071067811865476f)); }
+// ---- fp8 (OCP e4m3, gfx950 hardware conversions) paged-KV helpers: K/V are stored unscaled and
+// saturated to +-448 (the e4m3 max finite); loads widen 8 fp8 -> 8 fp32 with two cvt_pk per word.
+MX_DEV uint8_t f32_to_fp8(float x) {
+    x = fminf(fmaxf(x, -448.f), 448.f);
+    return (uint8_t)(__builtin_amdgcn_cvt_pk_fp8_f32(x, 0.f, 0, false) & 0xFF);
+}
+template <bool KV8> struct KVVec { using T = u32x4; };  // 8 elements per lane-load: 16 B bf16
+template <> struct KVVec<true> { using T = u32x2; };    //                           8 B fp8
+template <bool KV8, typename V>
+MX_DEV void kv_unpack8(const V& w, float (&f)[8]) {
+    if constexpr (KV8) {
+        const f32x2 a = __builtin_amdgcn_cvt_pk_f32_fp8((int)w[0], false), b = __builtin_amdgcn_cvt_pk_f32_fp8((int)w[0], true);
+        const f32x2 c = __builtin_amdgcn_cvt_pk_f32_fp8((int)w[1], false), d = __builtin_amdgcn_cvt_pk_f32_fp8((int)w[1], true);
+        f[0] = a.x; f[1] = a.y; f[2] = b.x; f[3] = b.y; f[4] = c.x; f[5] = c.y; f[6] = d.x; f[7] = d.y;
+    } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            f[2 * j] = __uint_as_float(w[j] << 16);
+            f[2 * j + 1] = __uint_as_float(w[j] & 0xFFFF0000u);
+        }
+    }
+}
+// 8 fp8 -> 8 bf16 (exact: e4m3 values are representable in bf16)
+MX_DEV uint4 fp8x8_to_bf16x8(uint2 w) {
+    float f[8];
+    kv_unpack8<true>(u32x2{w.x, w.y}, f);
+    uint32_t o[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = (__float_as_uint(f[2 * j]) >> 16) | (__float_as_uint(f[2 * j + 1]) & 0xFFFF0000u);
+    return make_uint4(o[0], o[1], o[2], o[3]);
+}
+
 // gate activation of the fused gated-FFN epilogues: EPI 3 = SwiGLU (silu), EPI 4 = GeGLU (gelu tanh)
 template <int EPI>
 MX_DEV float glu_gate_f(float g) {

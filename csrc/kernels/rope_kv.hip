@@ -17,12 +17,12 @@
 // its share of the Hkv V heads, so short decode batches still spread over the CUs. ZERO: after
 // reading its rows the kernel writes them back as zeros — the fp32 QKV buffer is the target of the
 // next layer's split-K GEMM (atomic accumulate), which then needs no separate zero-fill launch.
-template <bool NEOX, bool HAS_BIAS, bool QKN, bool ZERO>
+template <bool NEOX, bool HAS_BIAS, bool QKN, bool ZERO, bool KV8>
 __global__ __launch_bounds__(256) void rope_kv_kernel(float* __restrict__ qkv, const float* __restrict__ bias,
                                                       const int* __restrict__ pos, const int* __restrict__ slots,
                                                       const float* __restrict__ inv_freq, float attn_factor,
                                                       int Hq, int Hkv, int D, int rot_dim, bf16_t* __restrict__ qo,
-                                                      bf16_t* __restrict__ kc, bf16_t* __restrict__ vc,
+                                                      void* __restrict__ kc, void* __restrict__ vc,
                                                       int block_size, const float* __restrict__ qn,
                                                       const float* __restrict__ kn, float eps) {
     __shared__ float cs[256], sn[256], rsh[QKN ? 256 : 1];
@@ -86,7 +86,9 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(float* __restrict__ qkv, c
             qo[((size_t)t * Hq + h) * D + d] = f32_to_bf16(y);
         } else if (slot >= 0) {
             const int kh = h - Hq;
-            kc[(((size_t)blk * Hkv + kh) * block_size + off) * D + d] = f32_to_bf16(y);
+            const size_t e = (((size_t)blk * Hkv + kh) * block_size + off) * D + d;
+            if constexpr (KV8) ((uint8_t*)kc)[e] = f32_to_fp8(y);
+            else ((bf16_t*)kc)[e] = f32_to_bf16(y);
         }
     }
     float* vr = row + (Hq + Hkv) * D;
@@ -95,7 +97,9 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(float* __restrict__ qkv, c
             const int kh = idx / D, d = idx % D;
             float v = vr[idx];
             if (HAS_BIAS) v += bias[(Hq + Hkv) * D + idx];
-            vc[(((size_t)blk * Hkv + kh) * block_size + off) * D + d] = f32_to_bf16(v);
+            const size_t e = (((size_t)blk * Hkv + kh) * block_size + off) * D + d;
+            if constexpr (KV8) ((uint8_t*)vc)[e] = f32_to_fp8(v);
+            else ((bf16_t*)vc)[e] = f32_to_bf16(v);
         }
     }
     if constexpr (ZERO) {
@@ -107,8 +111,8 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(float* __restrict__ qkv, c
 
 extern "C" int mxk_rope_kv(float* qkv, const float* bias, const int* pos, const int* slots,
                            const float* inv_freq, float attn_factor, int T, int Hq, int Hkv, int D, int rot_dim,
-                           int neox, bf16_t* qo, bf16_t* kc, bf16_t* vc, int block_size, const float* qn,
-                           const float* kn, float eps, int zero_after, hipStream_t st) {
+                           int neox, bf16_t* qo, void* kc, void* vc, int block_size, const float* qn,
+                           const float* kn, float eps, int zero_after, int kv_fp8, hipStream_t st) {
     if (T <= 0) return 0;
     if (rot_dim > 512 || (rot_dim & 1) || D & 1) return (int)hipErrorInvalidValue;
     const bool qkn = qn != nullptr && kn != nullptr;
@@ -117,9 +121,9 @@ extern "C" int mxk_rope_kv(float* qkv, const float* bias, const int* pos, const 
     int ng = (512 + T - 1) / T;
     ng = max(1, min(ng, min(8, Hkv)));
     const dim3 grid(T, ng);
-#define RKZ(N_, B_, Q_) { if (zero_after) rope_kv_kernel<N_, B_, Q_, true><<<grid, 256, 0, st>>>(qkv, bias, pos, slots, inv_freq, attn_factor, Hq, Hkv, D, rot_dim, qo, kc, vc, block_size, qn, kn, eps); \
-    else rope_kv_kernel<N_, B_, Q_, false><<<grid, 256, 0, st>>>(qkv, bias, pos, slots, inv_freq, attn_factor, Hq, Hkv, D, rot_dim, qo, kc, vc, block_size, qn, kn, eps); }
-#define RK(N_, B_, Q_) RKZ(N_, B_, Q_)
+#define RKZ(N_, B_, Q_, K8_) { if (zero_after) rope_kv_kernel<N_, B_, Q_, true, K8_><<<grid, 256, 0, st>>>(qkv, bias, pos, slots, inv_freq, attn_factor, Hq, Hkv, D, rot_dim, qo, kc, vc, block_size, qn, kn, eps); \
+    else rope_kv_kernel<N_, B_, Q_, false, K8_><<<grid, 256, 0, st>>>(qkv, bias, pos, slots, inv_freq, attn_factor, Hq, Hkv, D, rot_dim, qo, kc, vc, block_size, qn, kn, eps); }
+#define RK(N_, B_, Q_) { if (kv_fp8) RKZ(N_, B_, Q_, true) else RKZ(N_, B_, Q_, false) }
 #define RKQ(N_, B_) { if (qkn) RK(N_, B_, true) else RK(N_, B_, false) }
     if (neox) { if (bias) RKQ(true, true) else RKQ(true, false) }
     else { if (bias) RKQ(false, true) else RKQ(false, false) }

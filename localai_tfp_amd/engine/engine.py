@@ -44,8 +44,21 @@ class EngineConfig:
     graph_buckets: tuple = (1, 2, 4, 8, 16, 32, 48, 64, 96, 128, 160, 192, 224, 256)
     attn_part_size: int = 256  # must match ops.core.attn_decode's default
     prefill_bf16_cache: bool = True  # dense bf16 copy of the linear weights for M>=128 prefill (GPU)
+    kv_dtype: str = "bf16"  # paged KV cache element type: bf16 | fp8 (OCP e4m3, half the bytes per token)
     n_draft: int = 0  # speculative decoding: draft tokens per step (needs a draft model; 0 = off)
     spec_max_batch: int = 32  # speculate only on decode batches up to this size (latency-bound regime)
+
+
+def kv_torch_dtype(name: str) -> torch.dtype:
+    """KV cache type names (engine `kv_dtype`, reference `cache_type_k` / `cache_type_v`:
+    f16 / q8_0 / ...) -> storage dtype. 8-bit llama.cpp types map to fp8 e4m3 (the gfx950-native
+    8-bit float), 16-bit types to bf16."""
+    n = (name or "bf16").lower()
+    if n in ("fp8", "f8", "e4m3", "fp8_e4m3", "q8_0", "q8", "q4_0", "q4_1", "q5_0", "q5_1", "iq4_nl"):
+        return torch.float8_e4m3fn
+    if n in ("bf16", "f16", "fp16", "f32", "auto", ""):
+        return torch.bfloat16
+    raise ValueError(f"unknown KV cache type {name!r}")
 
 
 class RequestHandle:
@@ -155,15 +168,17 @@ class LLMEngine:
         self.max_blocks_per_seq = (c.max_model_len + c.block_size - 1) // c.block_size
         use_spec = draft is not None and c.n_draft > 0 and tp is None
         frac = c.kv_mem_fraction
+        self.kv_dtype = kv_torch_dtype(c.kv_dtype)
+        eb = self.kv_dtype.itemsize
         if use_spec:  # the draft's cache shares the block ids: split the pool bytes between the two
-            per_t = KVCache.bytes_per_block(mc.n_layers, model.n_kv, c.block_size, mc.head_dim)
-            per_d = KVCache.bytes_per_block(draft.cfg.n_layers, draft.n_kv, c.block_size, draft.cfg.head_dim)
+            per_t = KVCache.bytes_per_block(mc.n_layers, model.n_kv, c.block_size, mc.head_dim, eb)
+            per_d = KVCache.bytes_per_block(draft.cfg.n_layers, draft.n_kv, c.block_size, draft.cfg.head_dim, eb)
             frac *= per_t / (per_t + per_d)
         nb = c.num_blocks or KVCache.auto_num_blocks(mc.n_layers, model.n_kv, c.block_size, mc.head_dim, self.device,
-                                                     frac)
+                                                     frac, dtype_bytes=eb)
         if self.tp is not None:  # every rank must hold the same block ids
             nb = self.tp.allreduce_min(nb)
-        self.kv = KVCache(mc.n_layers, nb, model.n_kv, c.block_size, mc.head_dim, self.device)
+        self.kv = KVCache(mc.n_layers, nb, model.n_kv, c.block_size, mc.head_dim, self.device, self.kv_dtype)
         self.bm = make_block_manager(nb, c.block_size, c.enable_prefix_cache)
         self.sched = Scheduler(self.bm, c.block_size, c.max_num_seqs, c.max_batched_tokens, c.max_model_len)
         max_parts = max(1, -(-c.max_model_len // c.attn_part_size))

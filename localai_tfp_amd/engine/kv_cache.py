@@ -41,9 +41,9 @@ class KVCache:
 
     @classmethod
     def auto_num_blocks(cls, n_layers, n_kv, block_size, head_dim, device, fraction: float = 0.85,
-                        reserve_bytes: int = 4 << 30, cap: int | None = None):
+                        reserve_bytes: int = 4 << 30, cap: int | None = None, dtype_bytes: int = 2):
         dev = torch.device(device)
-        per = cls.bytes_per_block(n_layers, n_kv, block_size, head_dim)
+        per = cls.bytes_per_block(n_layers, n_kv, block_size, head_dim, dtype_bytes)
         if dev.type != "cuda":
             n = 4096
         else:

@@ -278,14 +278,29 @@ def rope_kv(qkv: torch.Tensor, bias: torch.Tensor | None, positions: torch.Tenso
             if s < 0:
                 continue
             blk, off = divmod(s, block_size)
-            k_cache[blk, :, off, :] = kr[t].to(k_cache.dtype)
-            v_cache[blk, :, off, :] = v[t].to(v_cache.dtype)
+            k_cache[blk, :, off, :] = _to_cache(kr[t], k_cache.dtype)
+            v_cache[blk, :, off, :] = _to_cache(v[t], v_cache.dtype)
         return
     N.kcall("mxk_rope_kv", qkv.data_ptr(), N.ptr(bias), positions.data_ptr(), slots.data_ptr(), inv_freq.data_ptr(),
             float(attn_factor), T, Hq, Hkv, D, rot_dim, int(neox), q_out.data_ptr(), k_cache.data_ptr(),
             v_cache.data_ptr(), block_size, N.ptr(qk_norm[0]) if qk_norm else None,
             N.ptr(qk_norm[1]) if qk_norm else None, float(qk_norm[2]) if qk_norm else 0.0, int(zero_after),
-            N.stream_ptr())
+            int(is_fp8(k_cache)), N.stream_ptr())
+
+
+FP8_KV = torch.float8_e4m3fn  # OCP e4m3: the gfx950 hardware conversion format
+FP8_MAX = 448.0
+
+
+def is_fp8(t: torch.Tensor) -> bool:
+    return t.dtype == FP8_KV
+
+
+def _to_cache(x: torch.Tensor, dtype) -> torch.Tensor:
+    """Cast for a KV-cache store; fp8 saturates to +-448 like the kernel (torch's cast gives NaN)."""
+    if dtype == FP8_KV:
+        x = x.clamp(-FP8_MAX, FP8_MAX)
+    return x.to(dtype)
 
 
 # ------------------------------------------------------------------------------------------------
@@ -348,7 +363,7 @@ def attn_decode(q: torch.Tensor, k_cache, v_cache, block_tables: torch.Tensor, s
     N.kcall("mxk_attn_decode", q.data_ptr(), q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
             block_tables.data_ptr(), block_tables.stride(0), seq_lens.data_ptr(), B, Hq, Hkv, D, bs, float(scale),
             int(window), float(softcap), part_size, n_parts, out.data_ptr(), out.stride(0), N.ptr(ml_t), N.ptr(po),
-            N.stream_ptr())
+            int(is_fp8(k_cache)), N.stream_ptr())
     return out
 
 
@@ -392,7 +407,7 @@ def attn_prefill(q: torch.Tensor, k_cache, v_cache, block_tables: torch.Tensor, 
     N.kcall("mxk_attn_prefill", q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), block_tables.data_ptr(),
             block_tables.stride(0), tiles[0].data_ptr(), tiles[1].data_ptr(), len(seqs), cu_q.data_ptr(),
             ctx_lens.data_ptr(), Hq, Hkv, D, bs, float(scale), int(window), float(softcap), out.data_ptr(),
-            ATTN_VMODE if vmode is None else int(vmode), N.stream_ptr())
+            ATTN_VMODE if vmode is None else int(vmode), int(is_fp8(k_cache)), N.stream_ptr())
     return out
 
 

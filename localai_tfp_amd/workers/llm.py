@@ -199,6 +199,9 @@ class LLMServicer(BackendServicer):
                 ec.enable_prefix_cache = False
             if request.EnforceEager or opts.get("enforce_eager"):
                 ec.use_graphs = False
+            ct = request.CacheTypeKey or request.CacheTypeValue or opts.get("kv_cache_dtype", "")
+            if ct:  # one storage type for K and V (fp8 e4m3 for the 8-bit llama.cpp cache types)
+                ec.kv_dtype = str(ct)
             if self.device == "cpu":
                 ec.num_blocks = ec.num_blocks or 512
             if self.engine is not None:  # reload: stop the old engine (and the followers' replay)
