@@ -53,6 +53,8 @@ def parse():
     ap.add_argument("--gen-len", type=int, default=256)
     ap.add_argument("--max-batched-tokens", type=int, default=2048)
     ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--kv-dtype", default="bf16", choices=["bf16", "f16", "fp8"],
+                    help="paged KV cache element type (llama.cpp cache_type_k/v); fp8 = e4m3")
     ap.add_argument("--profile-steps", type=int, default=0)
     ap.add_argument("--timeout", type=float, default=900.0, help="abort if the window is not reached")
     return ap.parse_args()
@@ -110,7 +112,8 @@ def main():
     t_load = time.time() - t0
     tok = ByteTokenizer(cfg.vocab)
     ecfg = EngineConfig(max_num_seqs=args.concurrency, max_batched_tokens=args.max_batched_tokens,
-                        max_model_len=max(4096, args.prompt_len + args.gen_len + 64), use_graphs=not args.no_graphs)
+                        max_model_len=max(4096, args.prompt_len + args.gen_len + 64), use_graphs=not args.no_graphs,
+                        kv_dtype=args.kv_dtype)
     if dev.type == "cpu":
         ecfg.num_blocks = 2048
     eng = LLMEngine(model, tok, ecfg)
@@ -166,7 +169,8 @@ def main():
                 "graph_steps": st["graph_steps"], "total_steps": st["steps"],
                 "host_ms_per_step": {k[:-2]: round(st[k] / max(1, st["steps"]) * 1e3, 3)
                                      for k in ("sched_s", "plan_s", "fwd_s", "wait_s", "process_s")},
-                "weights_gb": round(model.weight_bytes() / 1e9, 2), "kv_blocks": eng.kv.num_blocks, **extra,
+                "weights_gb": round(model.weight_bytes() / 1e9, 2), "kv_blocks": eng.kv.num_blocks,
+                "kv_dtype": args.kv_dtype, **extra,
             },
         }
         print(json.dumps(out), flush=True)

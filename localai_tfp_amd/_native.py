@@ -59,6 +59,11 @@ KERNEL_SIGS = {
     "mxk_select_rows_f32": [P, I, P, I, I, P, I, P],
     "mxk_lstm_scan": [P, P, P, P, P, F, P, I, I, I, P],
     "mxk_wavenet_gate": [P, P, I, I, I, P],
+    # xz, ldxz, w, bias, state, kc, slots, positions, slot_div, n_dec, pf_cu, n_pf, xc, xc16, ldo16, Di, stream
+    "mxk_ssm_conv": [P, I, P, P, P, I, P, P, I, I, P, I, P, P, I, I, P],
+    # xc, dbc, lddbc, wdt, dt_bias, A, D, xz, ldxz, state, slots, positions, slot_div, n_dec, pf_cu, n_pf,
+    # y16, ldy, Di, R, d_state, stream
+    "mxk_ssm_scan": [P, P, I, P, P, P, P, P, I, P, P, P, I, I, P, I, P, I, I, I, I, P],
     "mxk_moe_route": [P, I, I, I, I, I, P, P, P],
     "mxk_moe_sort": [P, I, I, I, I, P, P, P, P, P],
     "mxk_moe_combine": [P, I, P, P, I, I, I, P, I, I, P],

@@ -165,6 +165,15 @@ class LLMEngine:
         mc = model.cfg
         c = self.cfg
         c.max_model_len = min(c.max_model_len, max(mc.ctx_train, 256)) if c.max_model_len else mc.ctx_train
+        self.recurrent = bool(getattr(model, "recurrent", False))
+        if self.recurrent:
+            # state-space models (models/mamba.py): one cache "block" per sequence holding its
+            # recurrent state, so the block id is the state slot; no prefix sharing, no drafts, no TP
+            if tp is not None:
+                raise ValueError("tensor parallelism is not supported for recurrent models")
+            c.block_size = c.max_model_len
+            c.enable_prefix_cache = False
+            draft = None
         self.max_blocks_per_seq = (c.max_model_len + c.block_size - 1) // c.block_size
         use_spec = draft is not None and c.n_draft > 0 and tp is None
         frac = c.kv_mem_fraction
@@ -174,16 +183,23 @@ class LLMEngine:
             per_t = KVCache.bytes_per_block(mc.n_layers, model.n_kv, c.block_size, mc.head_dim, eb)
             per_d = KVCache.bytes_per_block(draft.cfg.n_layers, draft.n_kv, c.block_size, draft.cfg.head_dim, eb)
             frac *= per_t / (per_t + per_d)
-        nb = c.num_blocks or KVCache.auto_num_blocks(mc.n_layers, model.n_kv, c.block_size, mc.head_dim, self.device,
-                                                     frac, dtype_bytes=eb)
-        if self.tp is not None:  # every rank must hold the same block ids
-            nb = self.tp.allreduce_min(nb)
-        self.kv = KVCache(mc.n_layers, nb, model.n_kv, c.block_size, mc.head_dim, self.device, self.kv_dtype)
+        if self.recurrent:
+            nb = c.max_num_seqs + 1
+            self.kv = model.make_state_cache(nb, c.block_size)
+        else:
+            nb = c.num_blocks or KVCache.auto_num_blocks(mc.n_layers, model.n_kv, c.block_size, mc.head_dim,
+                                                         self.device, frac, dtype_bytes=eb)
+            if self.tp is not None:  # every rank must hold the same block ids
+                nb = self.tp.allreduce_min(nb)
+            self.kv = KVCache(mc.n_layers, nb, model.n_kv, c.block_size, mc.head_dim, self.device, self.kv_dtype)
         self.bm = make_block_manager(nb, c.block_size, c.enable_prefix_cache)
         self.sched = Scheduler(self.bm, c.block_size, c.max_num_seqs, c.max_batched_tokens, c.max_model_len)
         max_parts = max(1, -(-c.max_model_len // c.attn_part_size))
-        self.ws = Workspace(mc, max(c.max_batched_tokens, c.max_num_seqs), c.max_num_seqs, self.device,
-                            model.tp_size, max_parts)
+        if self.recurrent:
+            self.ws = model.make_workspace(max(c.max_batched_tokens, c.max_num_seqs), c.max_num_seqs)
+        else:
+            self.ws = Workspace(mc, max(c.max_batched_tokens, c.max_num_seqs), c.max_num_seqs, self.device,
+                                model.tp_size, max_parts)
         self.sampler = SamplerBatch(self.device)
         self.handles: dict[int, RequestHandle] = {}
         self.seqs: dict[int, Sequence] = {}
@@ -200,7 +216,7 @@ class LLMEngine:
         self.last_metrics = {}
         self.on_step = None  # optional hook called with the step index before each loop step (bench)
         self.batch_sink: BatchedSink | None = None
-        if c.prefill_bf16_cache and self.device.type == "cuda":
+        if c.prefill_bf16_cache and self.device.type == "cuda" and hasattr(model, "enable_prefill_bf16_cache"):
             model.enable_prefill_bf16_cache()
         self.spec = None
         if use_spec:

@@ -37,6 +37,9 @@ def load_llm(model: str, device="cpu", tp_rank: int = 0, tp_size: int = 1, tp_gr
     """-> (LlamaModel, tokenizer, LlamaConfig, metadata dict)"""
     from ..tokenizer import ByteTokenizer, from_gguf
     ov = overrides or {}
+    rec = _load_recurrent(model, device, tp_size)
+    if rec is not None:
+        return rec
     if model.startswith("synthetic:"):
         from .synthetic import synthetic_source
         key = model.split(":", 1)[1]
@@ -81,3 +84,54 @@ def _apply_overrides(cfg: LlamaConfig, ov: dict):
         cfg.rms_eps = float(ov["rms_norm_eps"])
     if ov.get("context_size"):
         cfg.ctx_train = max(cfg.ctx_train, int(ov["context_size"])) if ov.get("extend_context") else cfg.ctx_train
+
+
+RECURRENT_ARCHS = {"mamba"}
+
+
+def _load_recurrent(model: str, device, tp_size: int):
+    """Mamba checkpoints (models/mamba.py): `synthetic:mamba-*`, an HF MambaForCausalLM directory, or
+    a GGUF with general.architecture = mamba. None for everything else."""
+    from . import mamba as M
+    from ..tokenizer import ByteTokenizer, from_gguf
+    if model.startswith("synthetic:mamba"):
+        key = model.split(":", 1)[1]
+        cfg = {"mamba-130m": M.MAMBA_130M, "mamba-1.4b": M.MAMBA_1_4B, "mamba-2.8b": M.MAMBA_2_8B,
+               "mamba-tiny": M.tiny_mamba_config()}[key]
+        import copy
+        cfg = copy.deepcopy(cfg)
+        return M.MambaModel.load(cfg, M.synthetic_mamba_source(cfg, seed=1), device), ByteTokenizer(cfg.vocab), cfg, {}
+    if os.path.isdir(model) and os.path.isfile(os.path.join(model, "config.json")):
+        import json
+        with open(os.path.join(model, "config.json")) as f:
+            if json.load(f).get("model_type") != "mamba":
+                return None
+        if tp_size > 1:
+            raise ValueError("tensor parallelism is not supported for Mamba models")
+        cfg, get = M.hf_mamba_source(model)
+        tok = ByteTokenizer(cfg.vocab)
+        try:
+            from ..tokenizer import from_hf_dir
+            tok = from_hf_dir(model)
+        except Exception as ex:  # tokenizer.json is optional for synthetic / test checkpoints
+            log.warning("no usable tokenizer in %s (%s); byte-level fallback", model, ex)
+        return M.MambaModel.load(cfg, get, device), tok, cfg, {}
+    if os.path.isfile(model):
+        try:
+            r = GGUFReader(model)
+        except Exception:
+            return None
+        md = dict(r.metadata)
+        if str(md.get("general.architecture")) not in RECURRENT_ARCHS:
+            return None
+        if tp_size > 1:
+            raise ValueError("tensor parallelism is not supported for Mamba models")
+        cfg = M.MambaConfig.from_gguf_metadata(md)
+        m = M.MambaModel.load(cfg, gguf_source(r), device)
+        try:
+            tok = from_gguf(md)
+        except Exception as ex:
+            log.warning("no usable tokenizer in %s (%s); byte-level fallback", model, ex)
+            tok = ByteTokenizer(cfg.vocab)
+        return m, tok, cfg, md
+    return None
