@@ -63,6 +63,10 @@ KERNEL_SIGS = {
     "mxk_ssm_conv": [P, I, P, P, P, I, P, P, I, I, P, I, P, P, I, I, P],
     # xc, dbc, lddbc, wdt, dt_bias, A, D, xz, ldxz, state, slots, positions, slot_div, n_dec, pf_cu, n_pf,
     # y16, ldy, Di, R, d_state, stream
+    # x, ldx, shift_state, sx_in, sx_out, maa, dm, out, n_mix, slots, positions, slot_div, n_dec, pf_cu, n_pf, T, C, st
+    "mxk_rwkv_shift_mix": [P, I, P, P, P, P, P, P, I, P, P, I, I, P, I, I, I, P],
+    # r, k, v, w, g, ld, u, state, lnw, lnb, eps, out, ldo, slots, positions, slot_div, n_dec, pf_cu, n_pf, H, hs, st
+    "mxk_rwkv_wkv6": [P, P, P, P, P, I, P, P, P, P, F, P, I, P, P, I, I, P, I, I, I, P],
     "mxk_ssm_scan": [P, P, I, P, P, P, P, P, I, P, P, P, I, I, P, I, P, I, I, I, I, P],
     "mxk_moe_route": [P, I, I, I, I, I, P, P, P],
     "mxk_moe_sort": [P, I, I, I, I, P, P, P, P, P],

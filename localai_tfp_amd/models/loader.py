@@ -86,14 +86,23 @@ def _apply_overrides(cfg: LlamaConfig, ov: dict):
         cfg.ctx_train = max(cfg.ctx_train, int(ov["context_size"])) if ov.get("extend_context") else cfg.ctx_train
 
 
-RECURRENT_ARCHS = {"mamba"}
+RECURRENT_ARCHS = {"mamba", "rwkv6"}
 
 
 def _load_recurrent(model: str, device, tp_size: int):
-    """Mamba checkpoints (models/mamba.py): `synthetic:mamba-*`, an HF MambaForCausalLM directory, or
-    a GGUF with general.architecture = mamba. None for everything else."""
+    """Recurrent checkpoints: Mamba (models/mamba.py: `synthetic:mamba-*`, an HF MambaForCausalLM
+    directory, GGUF arch `mamba`) and RWKV-6 (models/rwkv.py: `synthetic:rwkv6-*`, GGUF arch
+    `rwkv6`). None for everything else."""
     from . import mamba as M
     from ..tokenizer import ByteTokenizer, from_gguf
+    if model.startswith("synthetic:rwkv"):
+        from . import rwkv as RW
+        key = model.split(":", 1)[1]
+        cfg = {"rwkv6-7b": RW.RWKV6_WORLD_7B, "rwkv6-1b6": RW.RWKV6_WORLD_1B6, "rwkv6-tiny": RW.tiny_rwkv_config()}[key]
+        import copy
+        cfg = copy.deepcopy(cfg)
+        m = RW.RwkvModel.load(cfg, RW.synthetic_rwkv_source(cfg, seed=1), device)
+        return m, ByteTokenizer(cfg.vocab), cfg, {}
     if model.startswith("synthetic:mamba"):
         key = model.split(":", 1)[1]
         cfg = {"mamba-130m": M.MAMBA_130M, "mamba-1.4b": M.MAMBA_1_4B, "mamba-2.8b": M.MAMBA_2_8B,
@@ -126,8 +135,13 @@ def _load_recurrent(model: str, device, tp_size: int):
             return None
         if tp_size > 1:
             raise ValueError("tensor parallelism is not supported for Mamba models")
-        cfg = M.MambaConfig.from_gguf_metadata(md)
-        m = M.MambaModel.load(cfg, gguf_source(r), device)
+        if str(md.get("general.architecture")) == "rwkv6":
+            from . import rwkv as RW
+            cfg = RW.RwkvConfig.from_gguf_metadata(md)
+            m = RW.RwkvModel.load(cfg, gguf_source(r), device)
+        else:
+            cfg = M.MambaConfig.from_gguf_metadata(md)
+            m = M.MambaModel.load(cfg, gguf_source(r), device)
         try:
             tok = from_gguf(md)
         except Exception as ex:
