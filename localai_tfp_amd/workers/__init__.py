@@ -24,6 +24,8 @@ WORKERS = {
     "kokoro": "localai_tfp_amd.workers.tts",
     "transformers-musicgen": "localai_tfp_amd.workers.tts",
     "transformers-tts": "localai_tfp_amd.workers.tts",
+    "huggingface": "localai_tfp_amd.workers.huggingface",
+    "langchain-huggingface": "localai_tfp_amd.workers.huggingface",
 }
 
 ALIASES = {
