@@ -316,6 +316,12 @@ def cmd_explorer(a):
 def cmd_worker(a):
     from . import workers as W
     import importlib
+    if a.kind in ("llama-cpp-rpc", "rpc"):
+        # layer-split stage (reference `local-ai worker llama-cpp-rpc`, worker_llamacpp.go:19-44)
+        from .parallel import pp_rpc
+        host, port = a.addr.rsplit(":", 1)
+        pp_rpc.main(["--host", host, "--port", port])
+        return 0
     mod = importlib.import_module(W.WORKERS[W.resolve(a.kind)])
     mod.main(["--addr", a.addr])
     return 0
@@ -380,7 +386,7 @@ def main(argv=None):
     ex.add_argument("--with-sync", action="store_true")
     ex.add_argument("--only-sync", action="store_true")
     w = sub.add_parser("worker", help="run a single backend worker process")
-    w.add_argument("kind", help="backend name, e.g. llama-cpp, whisper, bert-embeddings")
+    w.add_argument("kind", help="backend name, e.g. llama-cpp, whisper, bert-embeddings; llama-cpp-rpc = layer-split stage")
     w.add_argument("--addr", default="127.0.0.1:50051")
     a = ap.parse_args(argv)
     logging.basicConfig(level=getattr(logging, str(getattr(a, "log_level", "info") or "info").upper(), logging.INFO),

@@ -187,11 +187,16 @@ class LLMEngine:
             nb = c.max_num_seqs + 1
             self.kv = model.make_state_cache(nb, c.block_size)
         else:
-            nb = c.num_blocks or KVCache.auto_num_blocks(mc.n_layers, model.n_kv, c.block_size, mc.head_dim,
+            nl = getattr(model, "kv_layers", mc.n_layers)
+            nb = c.num_blocks or KVCache.auto_num_blocks(max(1, nl), model.n_kv, c.block_size, mc.head_dim,
                                                          self.device, frac, dtype_bytes=eb)
             if self.tp is not None:  # every rank must hold the same block ids
                 nb = self.tp.allreduce_min(nb)
-            self.kv = KVCache(mc.n_layers, nb, model.n_kv, c.block_size, mc.head_dim, self.device, self.kv_dtype)
+            if getattr(model, "remote", None) is not None:  # remote layer ranges: same block ids everywhere
+                nb = model.remote.setup_kv(nb, c.block_size, c.kv_dtype, max(c.max_batched_tokens, c.max_num_seqs),
+                                           c.max_num_seqs, max(1, -(-c.max_model_len // c.attn_part_size)))
+                self.cfg.use_graphs = False  # a network hop cannot live inside a hipGraph
+            self.kv = KVCache(nl, nb, model.n_kv, c.block_size, mc.head_dim, self.device, self.kv_dtype)
         self.bm = make_block_manager(nb, c.block_size, c.enable_prefix_cache)
         self.sched = Scheduler(self.bm, c.block_size, c.max_num_seqs, c.max_batched_tokens, c.max_model_len)
         max_parts = max(1, -(-c.max_model_len // c.attn_part_size))
@@ -508,6 +513,7 @@ class LLMEngine:
             fb.pf_q_lens_host = [int(cu[k + 1] - cu[k]) for k in range(len(cu) - 1)]
             fb.pf_ctx_lens_host = [int(x) for x in plan["pf_ctx"]]
         fb.keep_hidden = bool(plan.get("keep_hidden"))
+        fb.plan = plan  # host copy (remote pipeline stages replay it)
         fb.embed_rows = plan.get("mm")
         return fb
 

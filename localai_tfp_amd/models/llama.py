@@ -143,12 +143,23 @@ class LlamaModel:
         self.glu_epi = EPI_GEGLU if cfg.ffn_act == "gelu" else EPI_SWIGLU
         self.n_heads = cfg.n_heads // tp_size
         self.n_kv = max(1, cfg.n_kv_heads // tp_size)
+        self.stage = False  # middle pipeline stage (hidden in, hidden out)
+        self.remote = None  # parallel.pp_rpc.RemoteStages running the layers after ours
+
+    @property
+    def kv_layers(self) -> int:
+        """Blocks whose KV cache lives in this process (all of them unless the model is split)."""
+        return len(self.layers)
 
     # ------------------------------------------------------------------ loading
     @classmethod
     def load(cls, cfg: LlamaConfig, get_tensor, device="cpu", tp_rank=0, tp_size=1, tp_group=None,
-             fuse: bool = True, progress=None) -> "LlamaModel":
-        """get_tensor(name) -> (raw ndarray, qtype, ggml_shape) or None."""
+             fuse: bool = True, progress=None, layer_range: tuple | None = None,
+             stage: bool = False) -> "LlamaModel":
+        """get_tensor(name) -> (raw ndarray, qtype, ggml_shape) or None.
+
+        layer_range=(l0, l1): load only those blocks (pipeline split, parallel/pp_rpc.py); stage=True:
+        a middle pipeline stage — no embedding / head, forward() maps hidden rows to hidden rows."""
         from ..parallel import tp as TP
         m = cls(cfg, device, tp_rank, tp_size, tp_group)
         dev = m.device
@@ -189,7 +200,9 @@ class LlamaModel:
             return out
 
         hd = cfg.head_dim
-        for i in range(cfg.n_layers):
+        l0, l1 = layer_range or (0, cfg.n_layers)
+        m.stage = stage
+        for i in range(l0, l1):
             p = f"blk.{i}."
             if get_tensor(p + "attn_qkv.weight") is not None:  # phi3: fused Q|K|V rows
                 wq, wk, wv = qw_rows(p + "attn_qkv.weight", [cfg.q_dim, cfg.kv_dim, cfg.kv_dim],
@@ -249,6 +262,8 @@ class LlamaModel:
             m.layers.append(layer)
             if progress:
                 progress(i + 1, cfg.n_layers)
+        if stage:
+            return m
         emb = get_tensor("token_embd.weight")
         raw, qt, shape = emb
         m.tok_embd = QWeight.from_ggml(np.asarray(raw).view(np.uint8).reshape(int(shape[1]), -1), qt,
@@ -319,10 +334,11 @@ class LlamaModel:
         gemv = T <= GEMV_MAX_M and self.device.type == "cuda"
         nd = fb.n_decode
         h = ws.h[:T]
-        self.embed(fb.tokens, h)
-        if fb.embed_rows:
-            for r0, e in fb.embed_rows:
-                h[r0:r0 + e.shape[0]].copy_(e)
+        if not self.stage:  # a pipeline stage finds its input hidden rows in ws.h
+            self.embed(fb.tokens, h)
+            if fb.embed_rows:
+                for r0, e in fb.embed_rows:
+                    h[r0:r0 + e.shape[0]].copy_(e)
         xb = ws.xb[:T, :H]
         for li, L in enumerate(self.layers):
             kc, vc = kv.layer(li)
@@ -394,6 +410,10 @@ class LlamaModel:
             else:
                 aq = ads = None
             self._residual_proj(L.wd, act, aq, ads, h, L.post_ffn_norm, ws, T, eps)
+        if self.stage:
+            return h
+        if self.remote is not None:  # remote layer ranges (parallel/pp_rpc.py), in place on h
+            self.remote.run(fb, h)
         # ---- head ----
         S = fb.logits_idx.numel()
         hs = ws.hs[:S]

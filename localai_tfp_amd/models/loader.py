@@ -18,7 +18,8 @@ log = logging.getLogger("localai_tfp_amd.models")
 SYNTHETIC = {"llama3-8b": C.LLAMA3_8B, "llama3-70b": C.LLAMA3_70B, "llama32-1b": C.LLAMA32_1B,
              "qwen3-8b": C.QWEN3_8B, "qwen3-30b-a3b": C.QWEN3_30B_A3B, "mixtral-8x7b": C.MIXTRAL_8X7B,
              "tiny": C.tiny_config(),
-             "tiny-draft": C.tiny_config(n_layers=1, name="tiny-draft"),  # speculative-decoding draft for "tiny"
+             "tiny-draft": C.tiny_config(n_layers=1, name="tiny-draft"),
+             "tiny-4l": C.tiny_config(n_layers=4, name="tiny-4l"),  # layer-split tests  # speculative-decoding draft for "tiny"
              "tiny-moe": C.tiny_config(arch="qwen3moe", n_expert=8, n_expert_used=2, expert_ffn=256, qk_norm=True)}
 SUPPORTED_ARCHS = {"llama", "mistral", "qwen2", "qwen3", "qwen2moe", "qwen3moe", "phi3", "gemma", "gemma2", "gemma3", "granite", "internlm2", "deci", "exaone", "olmo", "minicpm",
                    "smollm", "codellama"}

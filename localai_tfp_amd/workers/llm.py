@@ -207,10 +207,21 @@ class LLMServicer(BackendServicer):
             if self.engine is not None:  # reload: stop the old engine (and the followers' replay)
                 self.engine.shutdown()
                 self.engine = None
+            rpc = os.environ.get("LLAMACPP_GRPC_SERVERS", "") or str(opts.get("rpc_servers", ""))
+            rpc_servers = [x.strip() for x in rpc.split(",") if x.strip()]
             if self.tp is not None:
                 import dataclasses
                 self.tp.send_control("load", (path, ov, dataclasses.asdict(ec)))
                 model, tok, mcfg, _ = load_llm(path, self.device, self.tp.rank, self.tp.world, None, ov)
+            elif rpc_servers:
+                # remote layer split (reference LLAMACPP_GRPC_SERVERS, grpc-server.cpp:139-161):
+                # contiguous layer ranges on `local-ai worker llama-cpp-rpc` stages, tensor_split weights
+                import re
+                from ..parallel.pp_rpc import load_split
+                ts = [float(x) for x in re.split(r"[,/]", request.TensorSplit) if x.strip()] or None
+                if ts is not None and len(ts) != len(rpc_servers) + 1:
+                    ts = None
+                model, tok, mcfg, _ = load_split(path, rpc_servers, self.device, ts, ov)
             else:
                 model, tok, mcfg, _ = load_llm(path, self.device, overrides=ov)
             self.vision = None
