@@ -67,6 +67,8 @@ KERNEL_SIGS = {
     "mxk_rwkv_shift_mix": [P, I, P, P, P, P, P, P, I, P, P, I, I, P, I, I, I, P],
     # r, k, v, w, g, ld, u, state, lnw, lnb, eps, out, ldo, slots, positions, slot_div, n_dec, pf_cu, n_pf, H, hs, st
     "mxk_rwkv_wkv6": [P, P, P, P, P, I, P, P, P, P, F, P, I, P, P, I, I, P, I, I, I, P],
+    # qkv, ld, rows, D, H, head_dim, wq, wk, cs, L, eps, stream
+    "mxk_qk_norm_rope": [P, I, I, I, I, I, P, P, P, I, F, P],
     "mxk_ssm_scan": [P, P, I, P, P, P, P, P, I, P, P, P, I, I, P, I, P, I, I, I, I, P],
     "mxk_moe_route": [P, I, I, I, I, I, P, P, P],
     "mxk_moe_sort": [P, I, I, I, I, P, P, P, P, P],

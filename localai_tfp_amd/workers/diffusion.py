@@ -1,9 +1,10 @@
 """Image generation worker: the reference's `stablediffusion-ggml` (sd.cpp, gosd.cpp/gosd.go) and
 `diffusers` backends behind one GenerateImage RPC.
 
-LoadModel: a diffusers-layout SD3 directory (MMDiT) or SD1.x / SD2.x / SDXL directory (UNet), or
-`synthetic:sd3-medium | sd3-medium-no-t5 | sd3-test | sd15 | sdxl | sd15-test | sdxl-test` (random-init
-weights). ModelOptions.Options ("key:value", as gosd.cpp:56-162 parses them):
+LoadModel: a diffusers-layout SD3 directory (MMDiT), Flux.1 directory (FluxTransformer2DModel) or
+SD1.x / SD2.x / SDXL directory (UNet), or `synthetic:sd3-medium | sd3-medium-no-t5 | sd3-test | sd15 |
+sdxl | sd15-test | sdxl-test | flux-dev | flux-schnell | flux-test` (random-init weights). For Flux,
+cfg_scale is the distilled guidance (default 3.5). ModelOptions.Options ("key:value", as gosd.cpp:56-162 parses them):
   sampler:<euler|euler_a|heun|dpm2|dpm++2s_a|dpm++2m|dpm++2mv2|ipndm|ipndm_v|lcm|ddim_trailing|tcd>
   scheduler:<default|discrete|karras|exponential|ays|gits>
   cfg_scale:<float>   (ModelOptions.CFGScale also honoured)
@@ -44,6 +45,7 @@ class DiffusionServicer(BackendServicer):
                 k, _, v = kv.partition(":")
                 opts[k.strip()] = v.strip()
             use_t5 = opts.get("t5", "true").lower() not in ("0", "false", "no")
+            from ..models.diffusion import flux as FX
             from ..models.diffusion import sd_pipeline as U
             path = request.ModelFile or request.Model
             if path.startswith("synthetic:"):
@@ -52,6 +54,8 @@ class DiffusionServicer(BackendServicer):
                     name = "sd3-medium-no-t5"
                 if name in U.PRESETS:  # SD1.x / SDXL UNet models
                     self.pipe = U.UNetPipeline.synthetic(name, self.device)
+                elif name.startswith("flux"):
+                    self.pipe = FX.FluxPipeline.synthetic(name, self.device)
                 else:
                     self.pipe = SD3Pipeline.synthetic(name, self.device)
             else:
@@ -61,10 +65,13 @@ class DiffusionServicer(BackendServicer):
                     raise ValueError(f"{path}: expected a diffusers-layout model directory")
                 if os.path.isdir(os.path.join(path, "unet")):
                     self.pipe = U.UNetPipeline.from_diffusers(path, self.device)
+                elif _is_flux(path):
+                    self.pipe = FX.FluxPipeline.from_diffusers(path, self.device)
                 else:
                     self.pipe = SD3Pipeline.from_diffusers(path, self.device, use_t5=use_t5)
             self.defaults = dict(sampler=opts.get("sampler", "euler"), schedule=opts.get("scheduler", "default"),
-                                 cfg_scale=float(opts.get("cfg_scale", request.CFGScale or 7.0)),
+                                 cfg_scale=float(opts.get("cfg_scale", request.CFGScale or
+                                                          (3.5 if isinstance(self.pipe, FX.FluxPipeline) else 7.0))),
                                  strength=float(opts.get("strength", 0.75)))
             return pb.Result(message="loaded", success=True)
         except Exception as ex:
@@ -88,6 +95,15 @@ class DiffusionServicer(BackendServicer):
         except Exception as ex:
             log.exception("GenerateImage failed")
             return pb.Result(message=f"generation failed: {ex}", success=False)
+
+
+def _is_flux(path: str) -> bool:
+    import json
+    try:
+        with open(os.path.join(path, "transformer", "config.json")) as f:
+            return "num_single_layers" in json.load(f)
+    except OSError:
+        return False
 
 
 def main(argv=None):
