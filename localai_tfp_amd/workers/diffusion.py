@@ -10,6 +10,8 @@ cfg_scale is the distilled guidance (default 3.5). ModelOptions.Options ("key:va
   cfg_scale:<float>   (ModelOptions.CFGScale also honoured)
   t5:<true|false>     (drop the T5-XXL encoder; SD3 runs with zero T5 features)
   strength:<float>    (img2img denoise strength)
+LoRA: LoraAdapter (+LoraScale) and LoraAdapters (+LoraScales) — kohya or diffusers/PEFT safetensors —
+are merged into the weights at load (models/diffusion/lora.py).
 GenerateImage: positive / negative prompt, width, height, step, seed, dst (PNG), src (img2img).
 One image per call; data parallelism = one worker replica per GPU (model config `data_parallel`),
 with the gateway spreading concurrent requests across replicas.
@@ -69,6 +71,10 @@ class DiffusionServicer(BackendServicer):
                     self.pipe = FX.FluxPipeline.from_diffusers(path, self.device)
                 else:
                     self.pipe = SD3Pipeline.from_diffusers(path, self.device, use_t5=use_t5)
+            adapters = _lora_list(request)
+            if adapters:
+                from ..models.diffusion.lora import apply_adapters
+                apply_adapters(self.pipe, adapters)
             self.defaults = dict(sampler=opts.get("sampler", "euler"), schedule=opts.get("scheduler", "default"),
                                  cfg_scale=float(opts.get("cfg_scale", request.CFGScale or
                                                           (3.5 if isinstance(self.pipe, FX.FluxPipeline) else 7.0))),
@@ -95,6 +101,19 @@ class DiffusionServicer(BackendServicer):
         except Exception as ex:
             log.exception("GenerateImage failed")
             return pb.Result(message=f"generation failed: {ex}", success=False)
+
+
+def _lora_list(request) -> list[tuple[str, float]]:
+    """LoraAdapter (+LoraScale, default 1) and LoraAdapters (+LoraScales), relative to ModelPath."""
+    def full(p):
+        return p if os.path.isabs(p) or not request.ModelPath else os.path.join(request.ModelPath, p)
+    out = []
+    if request.LoraAdapter:
+        out.append((full(request.LoraAdapter), request.LoraScale or 1.0))
+    scales = list(request.LoraScales)
+    for i, p in enumerate(request.LoraAdapters):
+        out.append((full(p), scales[i] if i < len(scales) else 1.0))
+    return out
 
 
 def _is_flux(path: str) -> bool:
