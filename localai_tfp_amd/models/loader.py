@@ -48,7 +48,8 @@ def load_llm(model: str, device="cpu", tp_rank: int = 0, tp_size: int = 1, tp_gr
         import copy
         cfg = copy.deepcopy(cfg)
         _apply_overrides(cfg, ov)
-        m = LlamaModel.load(cfg, synthetic_source(cfg, "Q4_K_M", seed=1), device, tp_rank, tp_size, tp_group)
+        src = _lora_source(synthetic_source(cfg, "Q4_K_M", seed=1), ov, cfg)
+        m = LlamaModel.load(cfg, src, device, tp_rank, tp_size, tp_group)
         return m, ByteTokenizer(cfg.vocab), cfg, {}
     if not os.path.isfile(model):
         raise FileNotFoundError(model)
@@ -63,13 +64,24 @@ def load_llm(model: str, device="cpu", tp_rank: int = 0, tp_size: int = 1, tp_gr
         ti = r.tensors["rope_freqs.weight"]
         cfg.extra["rope_freqs"] = dequantize(r.tensor_bytes("rope_freqs.weight"), ti.qtype, ti.shape).tolist()
     _apply_overrides(cfg, ov)
-    m = LlamaModel.load(cfg, gguf_source(r), device, tp_rank, tp_size, tp_group)
+    m = LlamaModel.load(cfg, _lora_source(gguf_source(r), ov, cfg), device, tp_rank, tp_size, tp_group)
     try:
         tok = from_gguf(md)
     except Exception as ex:
         log.warning("no usable tokenizer in %s (%s); byte-level fallback", model, ex)
         tok = ByteTokenizer(cfg.vocab)
     return m, tok, cfg, md
+
+
+def _lora_source(get_tensor, ov: dict, cfg: LlamaConfig):
+    """overrides["lora"] = [(adapter path, scale), ...] -> a source yielding LoRA-merged weights."""
+    if not ov.get("lora"):
+        return get_tensor
+    from .lora import load_adapter, with_adapters
+    ads = [load_adapter(p, s, cfg) for p, s in ov["lora"]]
+    src = with_adapters(get_tensor, ads, ov.get("lora_requant") or "q8_0")
+    log.info("LoRA: %d adapter(s), %d weight tensors merged", len(ads), src.lora_targets)
+    return src
 
 
 def _apply_overrides(cfg: LlamaConfig, ov: dict):

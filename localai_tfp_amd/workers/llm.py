@@ -181,10 +181,9 @@ class LLMServicer(BackendServicer):
                     self.device = f"cuda:{int(mg)}" if mg.isdigit() else "cuda:0"
                 else:
                     self.device = "cpu"
-            if request.LoraAdapter or len(request.LoraAdapters):
-                log.warning("LoRA adapters are not supported by this worker yet; ignoring")
             ov = {"rope_freq_base": request.RopeFreqBase, "rope_freq_scale": request.RopeFreqScale,
-                  "rope_scaling": request.RopeScaling, "rms_norm_eps": request.RMSNormEps}
+                  "rope_scaling": request.RopeScaling, "rms_norm_eps": request.RMSNormEps,
+                  "lora": _lora_list(request, path), "lora_requant": opts.get("lora_requant", "q8_0")}
             ec = EngineConfig()
             if request.ContextSize > 0:
                 ec.max_model_len = int(request.ContextSize)
@@ -473,6 +472,23 @@ class LLMServicer(BackendServicer):
         for k in ("prompt_tokens_total", "gen_tokens_total", "cached_tokens_total", "preemptions"):
             st.memory.breakdown[k] = int(e.stats.get(k, 0))
         return st
+
+
+def _lora_list(request, model_path: str) -> list:
+    """LoraAdapter (+LoraScale, default 1.0; relative to the model file's directory, as
+    grpc-server.cpp:2402-2410) and LoraAdapters (+LoraScales) -> [(path, scale)]."""
+    base = os.path.dirname(model_path) if model_path and not model_path.startswith("synthetic:") \
+        else (request.ModelPath or "")
+
+    def full(p):
+        return p if os.path.isabs(p) or not base else os.path.join(base, p)
+    out = []
+    if request.LoraAdapter:
+        out.append((full(request.LoraAdapter), request.LoraScale or 1.0))
+    sc = list(request.LoraScales)
+    for i, p in enumerate(request.LoraAdapters):
+        out.append((full(p), sc[i] if i < len(sc) else 1.0))
+    return out
 
 
 def main(argv=None):
