@@ -128,6 +128,19 @@ class UNetPipeline:
         pr = UNetPreset(uc, t1.cfg, t2.cfg if t2 is not None else None, vae.cfg, uc.sample_size * 8)
         return cls(pr, un, t1, t2, vae, tk1, tk2, dev)
 
+    def set_controlnet(self, path: str, seed: int = 0):
+        """diffusers ControlNetModel directory, or `synthetic` (random init with this UNet's config)."""
+        from .controlnet import ControlNetModel, controlnet_from_diffusers
+        dtype = self.unet.conv_in.weight.dtype
+        if path.startswith("synthetic"):
+            with torch.device(self.device):
+                m = ControlNetModel(self.p.unet)
+            init_synthetic(m, seed + 7)
+            self.controlnet = cast_module(m, self.device, dtype).eval()
+        else:
+            self.controlnet = controlnet_from_diffusers(path, self.device, dtype)
+        return self
+
     # ------------------------------------------------------------------ conditioning
     @torch.no_grad()
     def encode_prompts(self, prompts: list[str], clip_skip: int = 0):
@@ -173,11 +186,19 @@ class UNetPipeline:
             tid = torch.tensor([[H, W, 0, 0, H, W]], dtype=torch.float32, device=dev)
             added = {"text_embeds": pooled, "time_ids": tid.expand(2, 6)}
         ctx_key = ctx
+        cn = getattr(self, "controlnet", None)
+        cimg = gp.extra.get("control_image")
+        if cn is not None and cimg is not None:
+            cimg = F.interpolate(cimg[None].float(), size=(H, W), mode="bilinear") if cimg.shape[1:] != (H, W) \
+                else cimg[None].float()
+            cimg = cimg.to(dev).expand(2, -1, -1, -1)
+        cscale = float(gp.extra.get("control_scale", 1.0))
 
         def denoise(xt: torch.Tensor, sigma: float) -> torch.Tensor:
             xin = torch.cat([xt, xt]) / math.sqrt(sigma * sigma + 1.0)
             t = torch.full((2,), self.sched.t_of(sigma), device=dev)
-            eps = self.unet(xin, t, ctx, added, ctx_key)
+            ctl = cn(xin, t, ctx, cimg, cscale, added, ctx_key) if cn is not None and cimg is not None else None
+            eps = self.unet(xin, t, ctx, added, ctx_key, control=ctl)
             e = eps[1:] + cfg * (eps[:1] - eps[1:])
             return xt - sigma * e
         x = S.sample(denoise, x, sig, gp.sampler, flow=False, generator=gen)

@@ -280,10 +280,8 @@ class UNet2DConditionModel(nn.Module):
             self._tproj = (w, b, sizes)
         return self._tproj
 
-    @torch.no_grad()
-    def forward(self, x: torch.Tensor, t: torch.Tensor, ctx: torch.Tensor, added: dict | None = None,
-                ctx_key=None) -> torch.Tensor:
-        """x [B, Cin, h, w] fp32 (scaled input), t [B] timesteps, ctx [B, S, cross_dim] -> eps fp32."""
+    def _prologue(self, x, t, ctx, added, ctx_key):
+        """Time (+SDXL text_time) embedding -> per-ResNet projections (one GEMM), fp16 context, input."""
         c = self.cfg
         dt = self.conv_in.weight.dtype
         B = x.shape[0]
@@ -299,7 +297,10 @@ class UNet2DConditionModel(nn.Module):
         key = ctx_key if ctx_key is not None else ctx
         h = x.to(dt)
         h = h.contiguous(memory_format=torch.channels_last) if h.is_cuda else h
-        h = conv(h, self.conv_in)
+        return ti, ctx16, key, h
+
+    def _encode(self, h, ti, ctx16, key):
+        """conv_in output -> (skip activations, mid-block output): the part ControlNet shares."""
         skips = [h]
         for blk in self.down_blocks:
             for i, r in enumerate(blk.resnets):
@@ -314,6 +315,18 @@ class UNet2DConditionModel(nn.Module):
         h = m.resnets[0].run(h, next(ti))
         h = m.attentions[0].run(h, ctx16, key)
         h = m.resnets[1].run(h, next(ti))
+        return skips, h
+
+    @torch.no_grad()
+    def forward(self, x: torch.Tensor, t: torch.Tensor, ctx: torch.Tensor, added: dict | None = None,
+                ctx_key=None, control: tuple | None = None) -> torch.Tensor:
+        """x [B, Cin, h, w] fp32 (scaled input), t [B] timesteps, ctx [B, S, cross_dim] -> eps fp32.
+        control = (down residuals, mid residual) from ControlNetModel, added to the skips / mid output."""
+        ti, ctx16, key, h = self._prologue(x, t, ctx, added, ctx_key)
+        skips, h = self._encode(conv(h, self.conv_in), ti, ctx16, key)
+        if control is not None:
+            skips = [s + r for s, r in zip(skips, control[0])]
+            h = h + control[1]
         for blk in self.up_blocks:
             for i, r in enumerate(blk.resnets):
                 s = skips.pop()
@@ -341,7 +354,9 @@ def config_from_diffusers(d: dict) -> UNetConfig:
     tl = d.get("transformer_layers_per_block", 1)
     tl = tuple(tl) if isinstance(tl, (list, tuple)) else (tl,) * len(ch)
     return UNetConfig(in_channels=d.get("in_channels", 4), out_channels=d.get("out_channels", 4), channels=ch,
-                      down_types=tuple(d["down_block_types"]), up_types=tuple(d["up_block_types"]),
+                      down_types=tuple(d["down_block_types"]),
+                      up_types=tuple(d.get("up_block_types") or  # ControlNet configs have no decoder
+                                     [t.replace("Down", "Up") for t in reversed(d["down_block_types"])]),
                       layers=d.get("layers_per_block", 2), heads=heads, transformer_layers=tl,
                       cross_dim=d.get("cross_attention_dim", 768), linear_proj=d.get("use_linear_projection", False),
                       groups=d.get("norm_num_groups", 32), addition_embed=d.get("addition_embed_type") or "",

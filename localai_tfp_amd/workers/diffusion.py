@@ -11,7 +11,8 @@ cfg_scale is the distilled guidance (default 3.5). ModelOptions.Options ("key:va
   t5:<true|false>     (drop the T5-XXL encoder; SD3 runs with zero T5 features)
   strength:<float>    (img2img denoise strength)
 LoRA: LoraAdapter (+LoraScale) and LoraAdapters (+LoraScales) — kohya or diffusers/PEFT safetensors —
-are merged into the weights at load (models/diffusion/lora.py).
+are merged into the weights at load (models/diffusion/lora.py). ControlNet (UNet pipelines): a diffusers
+ControlNetModel directory or `synthetic`; with it set, `src` is the control image (option control_scale).
 GenerateImage: positive / negative prompt, width, height, step, seed, dst (PNG), src (img2img).
 One image per call; data parallelism = one worker replica per GPU (model config `data_parallel`),
 with the gateway spreading concurrent requests across replicas.
@@ -71,6 +72,13 @@ class DiffusionServicer(BackendServicer):
                     self.pipe = FX.FluxPipeline.from_diffusers(path, self.device)
                 else:
                     self.pipe = SD3Pipeline.from_diffusers(path, self.device, use_t5=use_t5)
+            if request.ControlNet:
+                if not isinstance(self.pipe, U.UNetPipeline):
+                    raise ValueError("ControlNet is supported with SD1.x / SD2.x / SDXL UNet pipelines")
+                cpath = request.ControlNet
+                if not cpath.startswith("synthetic") and not os.path.isabs(cpath) and request.ModelPath:
+                    cpath = os.path.join(request.ModelPath, cpath)
+                self.pipe.set_controlnet(cpath)
             adapters = _lora_list(request)
             if adapters:
                 from ..models.diffusion.lora import apply_adapters
@@ -78,7 +86,8 @@ class DiffusionServicer(BackendServicer):
             self.defaults = dict(sampler=opts.get("sampler", "euler"), schedule=opts.get("scheduler", "default"),
                                  cfg_scale=float(opts.get("cfg_scale", request.CFGScale or
                                                           (3.5 if isinstance(self.pipe, FX.FluxPipeline) else 7.0))),
-                                 strength=float(opts.get("strength", 0.75)))
+                                 strength=float(opts.get("strength", 0.75)),
+                                 control_scale=float(opts.get("control_scale", 1.0)))
             return pb.Result(message="loaded", success=True)
         except Exception as ex:
             log.exception("LoadModel failed")
@@ -92,9 +101,13 @@ class DiffusionServicer(BackendServicer):
             w = request.width or 512
             h = request.height or 512
             gp = GenParams(width=w, height=h, steps=request.step or 20, seed=request.seed,
-                           negative=request.negative_prompt, **self.defaults)
+                           negative=request.negative_prompt,
+                           **{k: v for k, v in self.defaults.items() if k != "control_scale"})
             gp.extra["clip_skip"] = request.CLIPSkip
             init = load_image(request.src, w, h) if request.src else None
+            if init is not None and getattr(self.pipe, "controlnet", None) is not None:
+                gp.extra["control_image"], init = init, None  # src is the control image (backend.py:309-312)
+                gp.extra["control_scale"] = self.defaults.get("control_scale", 1.0)
             img = self.pipe.generate(request.positive_prompt, gp, init)
             save_png(img, request.dst)
             return pb.Result(message="ok", success=True)
