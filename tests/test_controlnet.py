@@ -61,7 +61,14 @@ import pytest  # noqa: E402
 
 @pytest.mark.gpu
 def test_controlnet_gpu_matches_cpu():
-    pc, pg = _pipe("cpu"), _pipe("cuda:0")
+    import copy
+
+    from localai_tfp_amd.models.diffusion.nn import cast_module
+    pc = _pipe("cpu")  # same weights on both sides: cast the CPU modules to the GPU (fp16)
+    dev = torch.device("cuda:0")
+    pg = type("P", (), {})()
+    pg.controlnet = cast_module(copy.deepcopy(pc.controlnet), dev, torch.float16)
+    pg.unet = cast_module(copy.deepcopy(pc.unet), dev, torch.float16)
     x = torch.randn(2, 4, 8, 8)
     t = torch.tensor([300.0, 300.0])
     ctx = torch.randn(2, 77, pc.unet.cfg.cross_dim)
