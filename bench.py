@@ -56,6 +56,8 @@ def parse():
     ap.add_argument("--kv-dtype", default="bf16", choices=["bf16", "f16", "fp8"],
                     help="paged KV cache element type (llama.cpp cache_type_k/v); fp8 = e4m3")
     ap.add_argument("--profile-steps", type=int, default=0)
+    ap.add_argument("--steady-finished", type=int, default=-1,
+                    help="completed requests before the warmup count starts (-1: concurrency/2)")
     ap.add_argument("--timeout", type=float, default=900.0, help="abort if the window is not reached")
     return ap.parse_args()
 
@@ -179,10 +181,20 @@ def main():
 
 
 class Window:
-    """Engine-thread hook: sync + barrier at step W and W+K; exactly K steps timed."""
+    """Engine-thread hook that times exactly K engine steps of the STEADY serving state.
 
-    def __init__(self, eng, warmup, steps, dev, dist):
+    Steady state: at least `steady_finished` requests have completed since the load started (with
+    the load generator's staggered first lengths, completions and re-arrivals are then spread
+    evenly, so every step holds the stationary mix of decode rows plus arriving prefill chunks).
+    From the first steady step, W more steps run untimed (the driver's warmup), then sync +
+    barrier, t0, K steps, sync + barrier, t1. Under DP every rank gates on its own engine and
+    the barrier aligns the windows.
+    """
+
+    def __init__(self, eng, warmup, steps, dev, dist, steady_finished: int):
         self.eng, self.W, self.K, self.dev, self.dist = eng, warmup, steps, dev, dist
+        self.steady_finished = steady_finished
+        self.steady_step = None
         self.t0 = self.t1 = None
         self.tok0 = self.tok1 = 0
         self.done = threading.Event()
@@ -194,15 +206,26 @@ class Window:
             self.dist.barrier()
 
     def __call__(self, i):
-        if i == self.W and self.t0 is None:
+        if self.steady_step is None:
+            if self.eng.stats["finished"] < self.steady_finished:
+                return
+            self.steady_step = i
+        j = i - self.steady_step
+        if j == self.W and self.t0 is None:
             self._sync()
             self.t0 = time.monotonic()
             self.tok0 = self.eng.stats["out_tokens"]
-        elif i == self.W + self.K and self.t1 is None:
+            self.step0 = i
+        elif j == self.W + self.K and self.t1 is None:
             self._sync()
             self.t1 = time.monotonic()
             self.tok1 = self.eng.stats["out_tokens"]
             self.done.set()
+
+
+def steady_gate(args) -> int:
+    """Completed requests after which the serving mix is stationary (see Window)."""
+    return args.steady_finished if args.steady_finished >= 0 else max(1, args.concurrency // 2)
 
 
 def run_http(args, eng, tok, cfg, dev, dist):
@@ -213,7 +236,7 @@ def run_http(args, eng, tok, cfg, dev, dist):
     sys.setswitchinterval(0.0005)  # same as workers/llm.py main(): engine thread + gRPC loop share the GIL
     svc = LLMServicer(device=str(dev))
     svc.attach(eng, tok)
-    win = Window(eng, args.warmup, args.steps, dev, dist)
+    win = Window(eng, args.warmup, args.steps, dev, dist, steady_gate(args))
     eng.on_step = win
     eng.start()
     server = AioServer(svc, "127.0.0.1:0", max_workers=16)
@@ -247,6 +270,7 @@ def run_http(args, eng, tok, cfg, dev, dist):
                                "--concurrency", str(args.concurrency),
                                "--prompt-chars", str(max(1, args.prompt_len - TEMPLATE_OVERHEAD)),
                                "--gen-len", str(args.gen_len), "--seed", str(int(os.environ.get("RANK", "0"))),
+                               "--stagger",
                                "--out", rec_path], env=env, cwd=ROOT, start_new_session=True)
         t_start = time.time()
         last = -1
@@ -285,8 +309,16 @@ def run_http(args, eng, tok, cfg, dev, dist):
     done = [r for r in recs if r.get("ok") and t0 <= r["t_end"] <= t1]
     client_tps = sum(r["tokens"] for r in done) / (t1 - t0) if done else 0.0
     errors = sum(1 for r in recs if r.get("error") not in (None, "CancelledError"))
+    # inter-token latency: gaps between consecutive content chunks of one stream, both inside the window
+    itl = [(b - a) * 1e3 for r in recs for a, b in zip(r.get("t_chunks", []), r.get("t_chunks", [])[1:])
+           if t0 <= a and b <= t1]
+    chunks_in = sum(1 for r in recs for t in r.get("t_chunks", []) if t0 <= t <= t1)
     extra = {"client_completed_requests": len(done), "client_tokens_per_s_completed": round(client_tps, 1),
-             "http_errors": errors, "ttft_samples": len(ttfts)}
+             "client_chunks_per_s": round(chunks_in / (t1 - t0), 1),
+             "http_errors": errors, "ttft_samples": len(ttfts),
+             "p50_itl_ms": round(float(np.percentile(itl, 50)), 2) if itl else None,
+             "p99_itl_ms": round(float(np.percentile(itl, 99)), 2) if itl else None,
+             "steady_at_step": win.steady_step, "window_first_step": getattr(win, "step0", None)}
     return t1 - t0, win.tok1 - win.tok0, ttfts, extra
 
 
@@ -306,12 +338,13 @@ def run_engine(args, eng, tok, dev, dist):
     ttfts = []
     timed = {"on": False}
 
-    def submit():
-        req = Request(make_prompt(), sp, max_tokens=args.gen_len)
+    def submit(gen=None):
+        req = Request(make_prompt(), sp, max_tokens=gen or args.gen_len)
         handles[req.rid] = (eng.submit(req), time.monotonic())
 
-    for _ in range(args.concurrency):
-        submit()
+    C = args.concurrency
+    for i in range(C):  # staggered first lengths (see tools/loadgen.py --stagger)
+        submit(-(-args.gen_len * (i + 1) // C))
 
     def drain():
         done = []
@@ -333,6 +366,11 @@ def run_engine(args, eng, tok, dev, dist):
         eng.step()
         drain()
 
+    gate = steady_gate(args)
+    n_pre = 0
+    while eng.stats["finished"] < gate and n_pre < 100000:
+        step()
+        n_pre += 1
     for _ in range(args.warmup):
         step()
     if dev.type == "cuda":
@@ -349,7 +387,7 @@ def run_engine(args, eng, tok, dev, dist):
     if dist:
         dist.barrier()
     t_el = time.monotonic() - t_start
-    return t_el, eng.stats["out_tokens"] - tok0, ttfts, {}
+    return t_el, eng.stats["out_tokens"] - tok0, ttfts, {"steady_at_step": n_pre}
 
 
 if __name__ == "__main__":

@@ -217,7 +217,7 @@ class LLMEngine:
         self.eos_ids = set(getattr(tokenizer, "eos_token_ids", []) or [])
         self.stats = dict(steps=0, decode_tokens=0, prefill_tokens=0, graph_steps=0, preemptions=0,
                           busy_s=0.0, prompt_tokens_total=0, gen_tokens_total=0, cached_tokens_total=0,
-                          out_tokens=0, sched_s=0.0, plan_s=0.0, fwd_s=0.0, wait_s=0.0, process_s=0.0)
+                          out_tokens=0, finished=0, sched_s=0.0, plan_s=0.0, fwd_s=0.0, wait_s=0.0, process_s=0.0)
         self.last_metrics = {}
         self.on_step = None  # optional hook called with the step index before each loop step (bench)
         self.batch_sink: BatchedSink | None = None
@@ -628,6 +628,7 @@ class LLMEngine:
             self.handles.pop(s.rid, None)
             self.seqs.pop(s.rid, None)
             st = self.stats
+            st["finished"] += 1
             st["prompt_tokens_total"] += len(s.prompt_ids)
             st["gen_tokens_total"] += len(s.output_ids)
             st["cached_tokens_total"] += s.num_cached

@@ -20,7 +20,7 @@ WORDS = ["the", "model", "serves", "tokens", "fast", "on", "MI355X", "with", "pa
 
 async def one(session, url, body, rec, stop):
     t0 = time.monotonic()
-    r = {"t_send": t0, "t_first": None, "t_end": None, "tokens": 0, "chunks": 0, "ok": False}
+    r = {"t_send": t0, "t_first": None, "t_end": None, "tokens": 0, "chunks": 0, "ok": False, "t_chunks": []}
     try:
         async with session.post(url, json=body) as resp:
             buf = b""
@@ -38,9 +38,11 @@ async def one(session, url, body, rec, stop):
                     ch = (j.get("choices") or [{}])
                     d = ch[0].get("delta") or {} if ch else {}
                     if d.get("content"):
+                        now = time.monotonic()
                         r["chunks"] += 1
+                        r["t_chunks"].append(now)
                         if r["t_first"] is None:
-                            r["t_first"] = time.monotonic()
+                            r["t_first"] = now
                     u = j.get("usage")
                     if u:
                         r["tokens"] = u.get("completion_tokens", r["tokens"])
@@ -50,9 +52,14 @@ async def one(session, url, body, rec, stop):
     rec.append(r)
 
 
-async def user(session, url, mk_body, rec, stop: asyncio.Event):
+async def user(session, url, mk_body, rec, stop: asyncio.Event, first_len: int | None = None):
+    n = 0
     while not stop.is_set():
-        await one(session, url, mk_body(), rec, stop)
+        body = mk_body()
+        if n == 0 and first_len:
+            body["max_tokens"] = first_len
+        n += 1
+        await one(session, url, body, rec, stop)
 
 
 async def run(a):
@@ -73,7 +80,13 @@ async def run(a):
     conn = aiohttp.TCPConnector(limit=0, force_close=False)
     timeout = aiohttp.ClientTimeout(total=None, sock_read=600)
     async with aiohttp.ClientSession(connector=conn, timeout=timeout) as session:
-        tasks = [asyncio.ensure_future(user(session, url, mk_body, rec, stop)) for _ in range(a.concurrency)]
+        # --stagger: user i's first request asks for ceil(gen_len * (i + 1) / concurrency) tokens, so
+        # completions (and re-arrivals) are spread evenly from the start: the server reaches the
+        # stationary continuous-batching mix (decode rows + arriving prefill chunks) after about
+        # one generation length instead of oscillating in lock-step waves.
+        C = a.concurrency
+        firsts = [(-(-a.gen_len * (i + 1) // C) if a.stagger else None) for i in range(C)]
+        tasks = [asyncio.ensure_future(user(session, url, mk_body, rec, stop, firsts[i])) for i in range(C)]
         if a.duration:
             try:
                 await asyncio.wait_for(stop.wait(), a.duration)
@@ -98,6 +111,7 @@ def main(argv=None):
     ap.add_argument("--temperature", type=float, default=0.0)
     ap.add_argument("--duration", type=float, default=0.0)
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--stagger", action="store_true", help="spread the first requests' lengths evenly")
     ap.add_argument("--out", required=True)
     a = ap.parse_args(argv)
     asyncio.run(run(a))
