@@ -41,37 +41,50 @@ async def index(request: Request):
                              f"{rows}</table><h3>Model files without config</h3><ul>{loose}</ul>")
 
 
+# All page scripts build DOM nodes with createElement/textContent: model output, user input and gallery
+# metadata (remote, untrusted) are never parsed as HTML (the reference renders through Go's
+# auto-escaping html/template).
+_JS_UTIL = """
+function el(tag,text,cls){const e=document.createElement(tag);if(text!==undefined)e.textContent=text;if(cls)e.className=cls;return e;}
+function msgDiv(who,text){const d=el('div',undefined,'msg');const b=el('b',who+': ');const s=el('span',text);d.appendChild(b);d.appendChild(s);return [d,s];}
+async function streamChat(model,msgs,onText){const r=await fetch('/v1/chat/completions',{method:'POST',
+headers:{'Content-Type':'application/json'},body:JSON.stringify({model:model,messages:msgs,stream:true})});
+const rd=r.body.getReader();const dec=new TextDecoder();let acc='',buf='';
+for(;;){const {done,value}=await rd.read();if(done)break;buf+=dec.decode(value,{stream:true});let i;
+while((i=buf.indexOf('\\n\\n'))>=0){const line=buf.slice(0,i);buf=buf.slice(i+2);if(!line.startsWith('data: '))continue;
+const p=line.slice(6);if(p==='[DONE]')continue;const j=JSON.parse(p);
+const c=j.choices&&j.choices[0]&&j.choices[0].delta&&j.choices[0].delta.content;if(c){acc+=c;onText(acc);}}}return acc;}
+"""
+
+
 @router.get("/chat")
 @router.get("/chat/{model}")
 async def chat_page(request: Request, model: str = ""):
     a = app_of(request)
-    js = """
+    js = _JS_UTIL + """
 const log=document.getElementById('log');let msgs=[];
 async function send(){const t=document.getElementById('in');const m=document.getElementById('model').value;
-msgs.push({role:'user',content:t.value});log.innerHTML+='<div class=msg><b>you:</b> '+t.value+'</div>';t.value='';
-const d=document.createElement('div');d.className='msg';d.innerHTML='<b>ai:</b> ';log.appendChild(d);
-const r=await fetch('/v1/chat/completions',{method:'POST',headers:{'Content-Type':'application/json'},
-body:JSON.stringify({model:m,messages:msgs,stream:true})});const rd=r.body.getReader();const dec=new TextDecoder();
-let acc='',buf='';for(;;){const {done,value}=await rd.read();if(done)break;buf+=dec.decode(value,{stream:true});
-let i;while((i=buf.indexOf('\\n\\n'))>=0){const line=buf.slice(0,i);buf=buf.slice(i+2);
-if(!line.startsWith('data: '))continue;const p=line.slice(6);if(p==='[DONE]')continue;
-const j=JSON.parse(p);const c=j.choices&&j.choices[0]&&j.choices[0].delta&&j.choices[0].delta.content;
-if(c){acc+=c;d.innerText='ai: '+acc;}}}msgs.push({role:'assistant',content:acc});}
+msgs.push({role:'user',content:t.value});log.appendChild(msgDiv('you',t.value)[0]);t.value='';
+const [d,span]=msgDiv('ai','');log.appendChild(d);
+const acc=await streamChat(m,msgs,x=>{span.textContent=x;});msgs.push({role:'assistant',content:acc});}
+document.getElementById('send').addEventListener('click',send);
 """
     return _page("Chat", f"<h2>Chat</h2>{_model_select(a, model)}<div id=log></div>"
-                         f"<textarea id=in rows=3></textarea><button onclick='send()'>Send</button><script>{js}</script>")
+                         f"<textarea id=in rows=3></textarea><button id=send>Send</button><script>{js}</script>")
 
 
 @router.get("/text2image")
 @router.get("/text2image/{model}")
 async def t2i_page(request: Request, model: str = ""):
     a = app_of(request)
-    js = """async function gen(){const r=await fetch('/v1/images/generations',{method:'POST',
+    js = _JS_UTIL + """async function gen(){const r=await fetch('/v1/images/generations',{method:'POST',
 headers:{'Content-Type':'application/json'},body:JSON.stringify({model:document.getElementById('model').value,
 prompt:document.getElementById('p').value,size:'512x512'})});const j=await r.json();
-document.getElementById('out').innerHTML=(j.data||[]).map(d=>'<img width=512 src="'+d.url+'">').join('');}"""
+const out=document.getElementById('out');out.replaceChildren();
+for(const d of (j.data||[])){const im=el('img');im.width=512;im.src=d.url||('data:image/png;base64,'+d.b64_json);out.appendChild(im);}}
+document.getElementById('go').addEventListener('click',gen);"""
     return _page("Images", f"<h2>Text to image</h2>{_model_select(a, model)}<input id=p placeholder=prompt>"
-                           f"<button onclick='gen()'>Generate</button><div id=out></div><script>{js}</script>")
+                           f"<button id=go>Generate</button><div id=out></div><script>{js}</script>")
 
 
 @router.get("/tts")
@@ -80,24 +93,58 @@ async def tts_page(request: Request, model: str = ""):
     a = app_of(request)
     js = """async function say(){const r=await fetch('/tts',{method:'POST',headers:{'Content-Type':'application/json'},
 body:JSON.stringify({model:document.getElementById('model').value,input:document.getElementById('t').value})});
-const b=await r.blob();const au=document.getElementById('au');au.src=URL.createObjectURL(b);au.play();}"""
+const b=await r.blob();const au=document.getElementById('au');au.src=URL.createObjectURL(b);au.play();}
+document.getElementById('go').addEventListener('click',say);"""
     return _page("TTS", f"<h2>Text to speech</h2>{_model_select(a, model)}<input id=t>"
-                        f"<button onclick='say()'>Speak</button><audio id=au controls></audio><script>{js}</script>")
+                        f"<button id=go>Speak</button><audio id=au controls></audio><script>{js}</script>")
 
 
 @router.get("/talk")
 async def talk_page(request: Request):
-    return _page("Talk", "<h2>Talk</h2><p>Record audio, transcribe with a whisper model, answer with an LLM "
-                         "and speak the answer: uses /v1/audio/transcriptions, /v1/chat/completions and /tts.</p>")
+    """Record -> /v1/audio/transcriptions -> /v1/chat/completions -> /tts (core/http/views/talk.html)."""
+    a = app_of(request)
+    names = a.list_models()
+
+    def sel(i):
+        return f'<select id="{i}">' + "".join(f"<option>{html.escape(n)}</option>" for n in names) + "</select>"
+    js = _JS_UTIL + """
+let rec=null,chunks=[];const log=document.getElementById('log');const msgs=[];
+async function start(){const st=await navigator.mediaDevices.getUserMedia({audio:true});rec=new MediaRecorder(st);
+chunks=[];rec.ondataavailable=e=>chunks.push(e.data);rec.onstop=turn;rec.start();}
+function stop(){if(rec)rec.stop();}
+async function turn(){const fd=new FormData();fd.append('file',new Blob(chunks),'talk.webm');
+fd.append('model',document.getElementById('stt').value);
+const tr=await (await fetch('/v1/audio/transcriptions',{method:'POST',body:fd})).json();const text=tr.text||'';
+log.appendChild(msgDiv('you',text)[0]);msgs.push({role:'user',content:text});
+const [d,span]=msgDiv('ai','');log.appendChild(d);
+const ans=await streamChat(document.getElementById('llm').value,msgs,x=>{span.textContent=x;});
+msgs.push({role:'assistant',content:ans});
+const r=await fetch('/tts',{method:'POST',headers:{'Content-Type':'application/json'},
+body:JSON.stringify({model:document.getElementById('voice').value,input:ans})});
+const au=document.getElementById('au');au.src=URL.createObjectURL(await r.blob());au.play();}
+document.getElementById('rec').addEventListener('click',start);document.getElementById('stop').addEventListener('click',stop);
+"""
+    return _page("Talk", f"<h2>Talk</h2><p>Transcription {sel('stt')} LLM {sel('llm')} Voice {sel('voice')}</p>"
+                         f"<button id=rec>Record</button><button id=stop>Stop &amp; send</button>"
+                         f"<div id=log></div><audio id=au controls></audio><script>{js}</script>")
 
 
 @router.get("/browse")
 async def browse_page(request: Request):
-    js = """async function load(){const r=await fetch('/models/available');const ms=await r.json();
-document.getElementById('g').innerHTML=ms.map(m=>'<tr><td>'+m.name+'</td><td>'+(m.description||'')+
-'</td><td><button onclick="inst(\\''+m.gallery.name+'@'+m.name+'\\')">install</button></td></tr>').join('');}
-async function inst(id){const r=await fetch('/models/apply',{method:'POST',headers:{'Content-Type':'application/json'},
-body:JSON.stringify({id:id})});const j=await r.json();alert('job '+j.uuid);}load();"""
+    """Gallery browser with install progress (core/http/routes/ui.go /browse + elements/gallery.go):
+    install posts /models/apply and polls /models/jobs/<uuid> until processed."""
+    js = _JS_UTIL + """
+async function load(){const r=await fetch('/models/available');const ms=await r.json();const tb=document.getElementById('g');
+tb.replaceChildren();for(const m of ms){const tr=el('tr');tr.appendChild(el('td',m.name));
+tr.appendChild(el('td',m.description||''));const td=el('td');const b=el('button','install');
+b.dataset.id=(m.gallery&&m.gallery.name?m.gallery.name+'@':'')+m.name;const st=el('span','');
+b.addEventListener('click',()=>inst(b.dataset.id,st,b));td.appendChild(b);td.appendChild(st);tr.appendChild(td);tb.appendChild(tr);}}
+async function inst(id,st,b){b.disabled=true;const r=await fetch('/models/apply',{method:'POST',
+headers:{'Content-Type':'application/json'},body:JSON.stringify({id:id})});const j=await r.json();
+for(;;){await new Promise(res=>setTimeout(res,1000));const s=await (await fetch('/models/jobs/'+encodeURIComponent(j.uuid))).json();
+const pct=s.progress!==undefined?Math.round(s.progress)+'%':'';st.textContent=' '+(s.message||'')+' '+pct;
+if(s.processed||s.error){st.textContent=s.error?' error: '+s.error:' installed';b.disabled=false;break;}}}
+load();"""
     return _page("Models", f"<h2>Model gallery</h2><table id=g></table><script>{js}</script>")
 
 

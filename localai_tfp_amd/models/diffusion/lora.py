@@ -12,9 +12,18 @@ merged weights. Key layouts understood:
 
 * kohya / sd-scripts:  `lora_unet_<path_with_underscores>.lora_down.weight|lora_up.weight|alpha`,
   `lora_te_` / `lora_te1_` / `lora_te2_` (text encoders), `lora_transformer_` (MMDiT / Flux);
+* kohya over the original (SGM / LDM) UNet names, as SDXL LoRAs trained with sd-scripts ship:
+  `lora_unet_input_blocks_4_1_transformer_blocks_0_attn1_to_q`, `..._middle_block_1_...`,
+  `..._output_blocks_2_1_conv` — renamed onto the diffusers module tree (sgm_names.py);
+* kohya over Black Forest Labs' Flux names: `lora_unet_double_blocks_<i>_img_attn_qkv` (split into
+  to_q/to_k/to_v), `..._txt_attn_proj`, `..._img_mlp_0`, `lora_unet_single_blocks_<i>_linear1` (split
+  into to_q/to_k/to_v/proj_mlp), `..._linear2`, `..._modulation_lin`;
 * diffusers / PEFT:    `<root>.<dotted.path>.lora_A.weight|lora_B.weight` (optional `.alpha`),
   and the older `<root>.<dotted.path>.lora.down.weight|lora.up.weight`; `<root>` is `unet`,
   `transformer`, `text_encoder`, `text_encoder_2`, `text_encoder_3`, or absent (= the denoiser).
+
+A denoiser (UNet / transformer) group that matches no layer fails the load: silently dropping the
+denoiser half of an adapter would serve the base model under the adapter's name.
 """
 from __future__ import annotations
 
@@ -23,6 +32,8 @@ import os
 
 import torch
 import torch.nn as nn
+
+from .sgm_names import bfl_flux_targets, sgm_unet_path
 
 log = logging.getLogger("localai_tfp_amd.diffusion.lora")
 
@@ -97,11 +108,24 @@ def _module_index(root: nn.Module) -> tuple[dict[str, nn.Module], dict[str, nn.M
     return dotted, under
 
 
+def _targets(root: str, path: str, kohya: bool, mod_root: nn.Module):
+    """-> [(module path, under?, up-row slice or None)] for one adapter group."""
+    if kohya and root in ("unet", "transformer"):
+        bfl = bfl_flux_targets(path, getattr(getattr(mod_root, "cfg", None), "dim", 0))
+        if bfl is not None:
+            return [(p, False, sl) for p, sl in bfl]
+        sgm = sgm_unet_path(path, mod_root, underscore=True)
+        if sgm is not None:
+            return [(sgm, False, None)]
+    return [(path, kohya, None)]
+
+
 @torch.no_grad()
 def merge_lora(roots: dict[str, nn.Module], sd: dict[str, torch.Tensor], scale: float = 1.0) -> int:
     """Merge one adapter into the modules under `roots`; returns the number of layers patched."""
     idx = {}
     n = 0
+    missing = []
     for (root, path, kohya), t in _group(sd).items():
         if "down" not in t or "up" not in t:
             continue
@@ -112,20 +136,30 @@ def merge_lora(roots: dict[str, nn.Module], sd: dict[str, torch.Tensor], scale: 
         if id(mod_root) not in idx:
             idx[id(mod_root)] = _module_index(mod_root)
         dotted, under = idx[id(mod_root)]
-        mod = (under if kohya else dotted).get(path)
-        if mod is None:
-            log.warning("LoRA: no layer %s.%s", root, path)
-            continue
         down = t["down"].float()
-        up = t["up"].float()
+        up_all = t["up"].float()
         r = down.shape[0]
         alpha = float(t["alpha"]) if "alpha" in t else float(r)
-        w = mod.weight
-        delta = up.reshape(up.shape[0], r) @ down.reshape(r, -1)
-        if delta.numel() != w.numel():
-            raise ValueError(f"LoRA {root}.{path}: delta {tuple(delta.shape)} vs weight {tuple(w.shape)}")
-        w.add_((delta * (scale * alpha / r)).reshape(w.shape).to(device=w.device, dtype=w.dtype))
-        n += 1
+        for tpath, tunder, rows in _targets(root, path, kohya, mod_root):
+            mod = (under if tunder else dotted).get(tpath)
+            if mod is None:
+                if root in ("unet", "transformer"):
+                    missing.append(f"{root}.{path}")
+                else:
+                    log.warning("LoRA: no layer %s.%s", root, path)
+                break
+            up = up_all.reshape(up_all.shape[0], -1)
+            if rows is not None:
+                up = up[rows[0]:rows[1]]
+            w = mod.weight
+            delta = up.reshape(up.shape[0], r) @ down.reshape(r, -1)
+            if delta.numel() != w.numel():
+                raise ValueError(f"LoRA {root}.{path}: delta {tuple(delta.shape)} vs weight {tuple(w.shape)}")
+            w.add_((delta * (scale * alpha / r)).reshape(w.shape).to(device=w.device, dtype=w.dtype))
+            n += 1
+    if missing:
+        raise ValueError(f"LoRA: {len(missing)} denoiser layer group(s) match no module of this model, e.g. "
+                         + ", ".join(missing[:4]))
     for m in roots.values():  # fused caches rebuild from the merged weights on next use
         for sub in m.modules():
             if getattr(sub, "_prep", None) is not None:

@@ -40,6 +40,8 @@ def load_llm(model: str, device="cpu", tp_rank: int = 0, tp_size: int = 1, tp_gr
     ov = overrides or {}
     rec = _load_recurrent(model, device, tp_size)
     if rec is not None:
+        if ov.get("lora"):
+            raise NotImplementedError("LoRA adapters are not supported for recurrent (Mamba / RWKV) models")
         return rec
     if model.startswith("synthetic:"):
         from .synthetic import synthetic_source

@@ -116,7 +116,10 @@ def merged_tensor(raw, qtype: int, shape, deltas: list[np.ndarray], requant: str
     for d in deltas:
         w += d
     qt = QType(qtype)
-    if requant != "same" and qt in _REQUANT:
+    # requant "q8_0" (default): every block-quantised base (Q4_K, Q5_K, Q4_0, IQ*, ...) comes back as
+    # Q8_0 when K allows it, never as 4-byte F32; "same": keep the base type where it can be re-encoded
+    dense = qt in (QType.F32, QType.F16, QType.BF16)
+    if requant != "same" and not dense and K_ % 32 == 0:
         qt = QType.Q8_0
     if qt in _REQUANT and K_ % (32 if qt == QType.Q8_0 else 256) == 0:
         return _REQUANT[qt](w).reshape(N_, -1), int(qt), shape
@@ -132,13 +135,17 @@ def with_adapters(get_tensor, adapters: list[Adapter], requant: str = "q8_0"):
     missing = [n for n in targets if get_tensor(n) is None]
     if missing:
         raise ValueError(f"LoRA targets not in the base model: {missing[:4]}")
-    cache = {}
+    # only the most recent merges are kept: the model loader asks for a tensor at most twice in a row
+    # (an existence check, then the load), so holding every merged tensor would multiply peak host RAM
+    cache: dict = {}
 
     def get(name):
         t = get_tensor(name)
         if t is None or name not in targets:
             return t
         if name not in cache:
+            while len(cache) >= 2:
+                cache.pop(next(iter(cache)))
             raw, qt, shape = t
             K_, N_ = int(shape[0]), int(np.prod(shape[1:]))
             deltas = []

@@ -78,7 +78,7 @@ class _Stage:
     def __init__(self, req: dict, device):
         from ..engine.kv_cache import KVCache
         from ..models.llama import Workspace
-        from ..models.loader import _apply_overrides, gguf_source, SYNTHETIC
+        from ..models.loader import _apply_overrides, _lora_source, gguf_source, SYNTHETIC
         from ..models.llama import LlamaModel
         from ..engine.engine import kv_torch_dtype
         model = req["model"]
@@ -96,6 +96,8 @@ class _Stage:
             cfg = LlamaConfig.from_gguf_metadata(dict(r.metadata))
             _apply_overrides(cfg, req.get("overrides") or {})
             src = gguf_source(r)
+        # LoRA adapters merge on every stage (adapter paths must resolve on the stage's host)
+        src = _lora_source(src, req.get("overrides") or {}, cfg)
         self.model = LlamaModel.load(cfg, src, device, layer_range=(l0, l1), stage=True)
         self.cfg = cfg
         self.device = torch.device(device)
@@ -266,7 +268,7 @@ def split_layers(n_layers: int, n_parts: int, weights: list[float] | None = None
 def load_split(model_ref: str, servers: list[str], device, tensor_split: list[float] | None = None, overrides=None):
     """-> (leader LlamaModel holding the first range + embedding/head, tokenizer, cfg, metadata).
     `servers`: "host:port" stages, in pipeline order (LLAMACPP_GRPC_SERVERS)."""
-    from ..models.loader import _apply_overrides, gguf_source, SYNTHETIC
+    from ..models.loader import _apply_overrides, _lora_source, gguf_source, SYNTHETIC
     from ..models.llama import LlamaModel
     from ..tokenizer import ByteTokenizer, from_gguf
     md = {}
@@ -290,7 +292,7 @@ def load_split(model_ref: str, servers: list[str], device, tensor_split: list[fl
         except Exception:
             tok = ByteTokenizer(cfg.vocab)
     ranges = split_layers(cfg.n_layers, 1 + len(servers), tensor_split)
-    m = LlamaModel.load(cfg, src, device, layer_range=ranges[0])
+    m = LlamaModel.load(cfg, _lora_source(src, overrides or {}, cfg), device, layer_range=ranges[0])
     m.remote = RemoteStages(model_ref, servers, ranges[1:], overrides)
     log.info("layer split: local %s, remote %s", ranges[0], list(zip(servers, ranges[1:])))
     return m, tok, cfg, md

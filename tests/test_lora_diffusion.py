@@ -108,7 +108,7 @@ def test_worker_lora_options(tmp_path):
               str(tmp_path / "bad.safetensors"))
     r = bad.LoadModel(pb.ModelOptions(Model="synthetic:sd15-test", ModelPath=str(tmp_path),
                                       LoraAdapter="bad.safetensors"), None)
-    assert not r.success and "matched no layer" in r.message
+    assert not r.success and ("matched no layer" in r.message or "match no module" in r.message)
 
 
 @pytest.mark.gpu
@@ -128,3 +128,67 @@ def test_lora_merge_on_gpu(tmp_path):
     torch.testing.assert_close(mod.weight.double().cpu(), want, rtol=1e-2, atol=2e-3)
     img = p.generate("x", gp)
     assert torch.isfinite(img).all()
+
+
+def test_sgm_unet_names_map_onto_diffusers_tree():
+    """SDXL kohya LoRAs use the original SGM UNet numbering (they used to match nothing)."""
+    from localai_tfp_amd.models.diffusion.sgm_names import sgm_unet_path
+    from localai_tfp_amd.models.diffusion.unet import UNET_XL_TEST, UNet2DConditionModel
+    unet = UNet2DConditionModel(UNET_XL_TEST)  # layers=1; level 0 plain, level 1 cross-attention
+    mods = dict(unet.named_modules())
+    cases = {
+        "input_blocks_1_0_in_layers_2": "down_blocks.0.resnets.0.conv1",
+        "input_blocks_2_0_op": "down_blocks.0.downsamplers.0.conv",
+        "input_blocks_3_1_transformer_blocks_0_attn1_to_q": "down_blocks.1.attentions.0.transformer_blocks.0.attn1.to_q",
+        "input_blocks_3_1_proj_in": "down_blocks.1.attentions.0.proj_in",
+        "middle_block_0_emb_layers_1": "mid_block.resnets.0.time_emb_proj",
+        "middle_block_1_transformer_blocks_1_ff_net_0_proj": "mid_block.attentions.0.transformer_blocks.1.ff.net.0.proj",
+        "middle_block_2_out_layers_3": "mid_block.resnets.1.conv2",
+        "output_blocks_0_1_transformer_blocks_0_attn2_to_out_0": "up_blocks.0.attentions.0.transformer_blocks.0.attn2.to_out.0",
+        "output_blocks_1_0_skip_connection": "up_blocks.0.resnets.1.conv_shortcut",
+        "output_blocks_1_2_conv": "up_blocks.0.upsamplers.0.conv",
+        "output_blocks_3_0_in_layers_2": "up_blocks.1.resnets.1.conv1",
+        "time_embed_0": "time_embedding.linear_1",
+        "label_emb_0_2": "add_embedding.linear_2",
+    }
+    for k, want in cases.items():
+        got = sgm_unet_path(k, unet, underscore=True)
+        assert got == want, (k, got)
+        assert want in mods
+    assert sgm_unet_path("input_blocks.3.1.transformer_blocks.0.attn1.to_q", unet) == \
+        "down_blocks.1.attentions.0.transformer_blocks.0.attn1.to_q"
+    # merge through the kohya path
+    g = torch.Generator().manual_seed(1)
+    w = mods["down_blocks.1.attentions.0.transformer_blocks.0.attn1.to_q"].weight
+    w0 = w.detach().clone()
+    up, down = _ud(w.shape[0], w.shape[1], 2, g)
+    sd = {"lora_unet_input_blocks_3_1_transformer_blocks_0_attn1_to_q.lora_up.weight": up,
+          "lora_unet_input_blocks_3_1_transformer_blocks_0_attn1_to_q.lora_down.weight": down}
+    assert L.merge_lora({"unet": unet}, sd, 1.0) == 1
+    torch.testing.assert_close(w.double(), w0.double() + _delta(up, down, 2, 2, 1.0, w0.shape), rtol=1e-6, atol=1e-6)
+
+
+def test_bfl_flux_lora_splits_fused_qkv():
+    from localai_tfp_amd.models.diffusion import flux as FX
+    tr = FX.FluxTransformer(FX.FLUX_TEST)
+    d = FX.FLUX_TEST.dim
+    mods = dict(tr.named_modules())
+    g = torch.Generator().manual_seed(2)
+    r = 4
+    down = torch.randn(r, d, generator=g) * 0.05
+    up_qkv = torch.randn(3 * d, r, generator=g) * 0.05
+    up_l1 = torch.randn(7 * d, r, generator=g) * 0.05
+    before = {k: mods[k].weight.detach().clone() for k in (
+        "transformer_blocks.0.attn.to_q", "transformer_blocks.0.attn.to_v",
+        "single_transformer_blocks.1.attn.to_k", "single_transformer_blocks.1.proj_mlp")}
+    sd = {"lora_unet_double_blocks_0_img_attn_qkv.lora_up.weight": up_qkv,
+          "lora_unet_double_blocks_0_img_attn_qkv.lora_down.weight": down,
+          "lora_unet_single_blocks_1_linear1.lora_up.weight": up_l1,
+          "lora_unet_single_blocks_1_linear1.lora_down.weight": down}
+    assert L.merge_lora({"transformer": tr}, sd, 1.0) == 3 + 4
+    chk = {"transformer_blocks.0.attn.to_q": up_qkv[:d], "transformer_blocks.0.attn.to_v": up_qkv[2 * d:],
+           "single_transformer_blocks.1.attn.to_k": up_l1[d:2 * d], "single_transformer_blocks.1.proj_mlp": up_l1[3 * d:]}
+    for k, u in chk.items():
+        w0 = before[k]
+        torch.testing.assert_close(mods[k].weight.double(), w0.double() + _delta(u, down, r, r, 1.0, w0.shape),
+                                   rtol=1e-6, atol=1e-6)

@@ -86,3 +86,26 @@ def test_layer_split_gpu_matches_unsplit():
         split.remote.close()
     finally:
         s.shutdown()
+
+
+def test_layer_split_applies_lora_on_every_stage(stages, tmp_path):
+    """the split path used to serve the base model silently when LoraAdapter was set."""
+    from localai_tfp_amd.formats.gguf import GGUFWriter
+    full0, tok, cfg, _ = load_llm("synthetic:tiny-4l", "cpu")
+    rng = np.random.default_rng(5)
+    wr = GGUFWriter(str(tmp_path / "ad.gguf"))
+    wr.add("general.type", "adapter")
+    wr.add("adapter.type", "lora")
+    wr.add("adapter.lora.alpha", 4.0)
+    for i in range(cfg.n_layers):  # every layer, so remote stages must merge too
+        wr.add_tensor(f"blk.{i}.ffn_down.weight.lora_a", rng.standard_normal((4, cfg.ffn)).astype(np.float32))
+        wr.add_tensor(f"blk.{i}.ffn_down.weight.lora_b", rng.standard_normal((cfg.hidden, 4)).astype(np.float32))
+    wr.write()
+    ov = {"lora": [(str(tmp_path / "ad.gguf"), 1.0)]}
+    full, _, _, _ = load_llm("synthetic:tiny-4l", "cpu", overrides=ov)
+    split, tok2, _, _ = pp_rpc.load_split("synthetic:tiny-4l", stages, "cpu", overrides=ov)
+    prompts = [rng.integers(0, cfg.vocab, n).tolist() for n in (30, 7)]
+    want = _run(full, tok, prompts)
+    assert want != _run(full0, tok, prompts)
+    assert _run(split, tok2, prompts) == want
+    split.remote.close()

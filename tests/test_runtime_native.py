@@ -55,6 +55,20 @@ def test_grammar_parse_errors():
         rn.NativeGrammar("root ::= undefined-rule")
 
 
+@pytest.mark.timeout(30)
+def test_grammar_left_recursion_rejected():
+    # direct, indirect and behind a nullable prefix: rejected at parse time (llama.cpp semantics),
+    # instead of an exponential expansion when the matcher is created
+    for src in ('root ::= root "a" | root "b" | "c"',
+                'root ::= x "z"\nx ::= root "y" | "w"',
+                'root ::= opt root "a" | "b"\nopt ::= "q"?'):
+        with pytest.raises(rn.GrammarError, match="left recursion"):
+            rn.NativeGrammar(src)
+    # right recursion stays legal
+    g = rn.NativeGrammar('root ::= "a" root | "c"')
+    assert g is not None
+
+
 def _allowed(m, V):
     mk = m.allowed_mask(V)
     return {i for i in range(V) if (int(mk[i // 32]) >> (i % 32)) & 1}
