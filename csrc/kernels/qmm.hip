@@ -1,0 +1,485 @@
+// qmm.hip — quantised-weight GEMM for the M >= 64 regime (mixed continuous-batching steps, prefill):
+//
+//   C[M, N] (+)= A[M, K] · W[N, K]^T,   A f16 (act16 mode f16), W in Q4_K / Q6_K(repacked) / Q8_0(repacked)
+//
+// Replaces the dense-f16-weight-copy + hipBLASLt path for large M: the weights stay in their GGUF
+// block format in HBM (3.5x fewer bytes than f16) and are dequantised on the fly into MFMA operands.
+//
+// Structure (one 256-thread workgroup = 4 waves; BM = 32*WM rows x BN = 128*WN columns):
+//   * every operand reaches the CU through `global_load_lds` (LDS-DMA, no VGPR staging) into an
+//     NSTAGE-deep ring of KT = 64-wide k-tiles, so NSTAGE-1 tiles of weights are in flight per
+//     workgroup (the memory-level parallelism a weight-streaming GEMM needs at 1 workgroup per CU);
+//   * the ring is advanced with a COUNTED `s_waitcnt vmcnt(N)` + raw `s_barrier` (never vmcnt(0) in
+//     the loop: every load in this kernel is an LDS-DMA, so the count is exact);
+//   * the A tile (BM x 64 f16) is shared by the 4 waves (XOR-swizzled 128-B rows, conflict-free
+//     ds_read_b128 fragment reads); the 4 waves split N, so each weight is dequantised exactly once
+//     per workgroup, by the wave that owns its column, straight from the raw block bytes in LDS into
+//     a 32x32x16 f16 MFMA B fragment (packed-f16 magic-number dequantisation, qdeq16.h);
+//   * k order inside a tile is the natural one for all three block formats: MFMA k-step s, lane half h,
+//     element j <-> k = 16 s + 8 h + j, which for Q4_K/Q6_K is low nibbles (s < 2) / high nibbles
+//     (s >= 2) of the same 32 bytes, so one 8-byte LDS read feeds two k-steps;
+//   * the block index -> (column tile, split, row tile) map is XCD-aware (bijective remap; the row
+//     tiles that share a column panel of W run on one XCD and re-read it from that XCD's L2).
+// Split-K over K (fp32 atomics) only for accumulating outputs; otherwise a plain store / RMW add.
+#include "qdeq16.h"
+
+namespace {
+
+constexpr int QMM_KT = 64;
+constexpr int QMM_LDS_BUDGET = 160 * 1024;
+constexpr int QMM_MAX_STAGES = 8;
+
+// ---- "t32" tiled weight layout (ops/quant.py: tile32) -------------------------------------------
+// Columns are grouped 32 at a time; per (group g, super-block kb) the bytes of the 32 columns are
+// stored together, split so that every LDS-DMA wave-instruction of a k-tile reads CONTIGUOUS memory
+// (the ggml row-major layout puts each of a wave's 32-64 columns in a different cache line, which
+// made the load path, not HBM or the MFMAs, the bottleneck):
+//   Q4_K (4608 B / group / kb): [hdr: 32 x 16 B {d, dmin, scales}] [quarter jq: 2 x (32 x 16 B qs)]
+//   Q6_K (6784 B / group / kb): [sc: 32 x 16 B] [d: 32 x 4 B] [quarter jq: ql0, ql1, qh (32 x 16 B each)]
+//   Q8_0 (2176 B / group / k-tile): [d: 32 x {f16 d0, f16 d1}] [4 x (32 x 16 B qs)]
+template <int QT>
+struct QmmFmt;
+template <>
+struct QmmFmt<MXQ_Q4_K> {
+    static constexpr int UNIT = 4608, PER_UNIT = 4;       // bytes per group per kb; k-tiles per unit
+    static constexpr int QOFF = 512, QSTRIDE = 1024, QB = 1024;
+    static constexpr int MOFF = 0, MB = 512;               // header chunks
+    static constexpr int DOFF = 0, DSTRIDE = 0, HAS_D = 0;
+};
+template <>
+struct QmmFmt<MXQ_Q6_K> {
+    static constexpr int UNIT = 6784, PER_UNIT = 4;
+    static constexpr int QOFF = 640, QSTRIDE = 1536, QB = 1536;
+    static constexpr int MOFF = 0, MB = 512;               // int8 scales
+    static constexpr int DOFF = 512, DSTRIDE = 0, HAS_D = 1;
+};
+template <>
+struct QmmFmt<MXQ_Q8_0> {
+    static constexpr int UNIT = 2176, PER_UNIT = 1;
+    static constexpr int QOFF = 128, QSTRIDE = 0, QB = 2048;
+    static constexpr int MOFF = 0, MB = 0;
+    static constexpr int DOFF = 0, DSTRIDE = 0, HAS_D = 1;
+};
+
+template <int QT, int WN>
+struct QmmGeom {
+    using F = QmmFmt<QT>;
+    static constexpr int COLS = 32 * WN;                   // columns per wave (WN groups)
+    static constexpr int QCH = F::QB / 16;                 // 16-B chunks per group per k-tile
+    static constexpr int QI = (WN * QCH + 63) / 64;        // quant-data wave-instructions
+    static constexpr int MI = (WN * F::MB / 16 + 63) / 64; // meta (header / scales) wave-instructions
+    static constexpr int DI = F::HAS_D;                    // d-word wave-instructions (WN <= 2)
+    static constexpr int NI = QI + MI + DI;
+    static constexpr int Q_OFF = 0, M_OFF = QI * 1024, D_OFF = M_OFF + MI * 1024;
+    static constexpr int WBYTES = D_OFF + DI * 256;        // per wave per stage
+};
+
+// ring depth: as many k-tiles in flight as the LDS holds (memory-level parallelism), capped
+template <int QT, int WM, int WN, int NW>
+struct QmmRing {
+    static constexpr int STAGE = 32 * WM * 128 + NW * QmmGeom<QT, WN>::WBYTES;
+    static constexpr int S0 = QMM_LDS_BUDGET / STAGE;
+    static constexpr int STAGES = S0 > QMM_MAX_STAGES ? QMM_MAX_STAGES : S0;
+};
+
+MX_DEV int qmm_a_off(int r, int c) { return r * 128 + ((c ^ ((r >> 1) & 7)) << 4); }
+
+template <int N_>
+MX_DEV void qmm_wait_barrier() {
+    asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(N_) : "memory");
+}
+// wait until at most `ahead` stages (NI LDS-DMA instructions each) are still in flight, then barrier
+template <int NI, int A_>
+MX_DEV void qmm_wait_ahead(int ahead) {
+    if constexpr (A_ <= 0) {
+        qmm_wait_barrier<0>();
+    } else {
+        if (ahead >= A_) qmm_wait_barrier<A_ * NI>();
+        else qmm_wait_ahead<NI, A_ - 1>(ahead);
+    }
+}
+
+// ---- per-format B fragment builders (raw bytes in LDS -> f16x8 for k-step s) ----
+// q: this group's quant chunks for the k-tile (32 x 16 B per chunk row), m: its 32 meta chunks,
+// d: its 32 d-words; r = column in the group, h = lane half, jq = k-tile within the super-block
+template <int QT>
+struct QmmB;
+
+template <>
+struct QmmB<MXQ_Q4_K> {
+    u32x2 v0, v1;
+    f16x2 s2[2], m2[2];
+    MX_DEV void load(const char* q, const char* m, const char*, int r, int h, int jq) {
+        const u32x4 hd = *(const u32x4*)(m + r * 16);
+        v0 = *(const u32x2*)(q + r * 16 + 8 * h);
+        v1 = *(const u32x2*)(q + (32 + r) * 16 + 8 * h);
+        const float d = half_to_f32(hd[0] & 0xFFFF), dm = half_to_f32(hd[0] >> 16);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            int sc, mn;
+            q4k_scale_min_w(hd[1], hd[2], hd[3], 2 * jq + i, sc, mn);
+            const _Float16 s = (_Float16)(d * (float)sc), mm = (_Float16)(-dm * (float)mn);
+            s2[i] = (f16x2){s, s};
+            m2[i] = (f16x2){mm, mm};
+        }
+    }
+    template <int S>
+    MX_DEV f16x8 frag() const {
+        const u32x2 src = (S & 1) ? v1 : v0;
+        constexpr int sh = 4 * (S >> 1);
+        const uint32_t t0 = (src[0] >> sh) & 0x0F0F0F0Fu, t1 = (src[1] >> sh) & 0x0F0F0F0Fu;
+        const f16x2 k = {(_Float16)1024.f, (_Float16)1024.f};
+        f16x2 p[4];
+        magic4(t0, p[0], p[1]);
+        magic4(t1, p[2], p[3]);
+        f16x8 r;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const f16x2 v = (p[i] - k) * s2[S >> 1] + m2[S >> 1];
+            r[2 * i] = v[0];
+            r[2 * i + 1] = v[1];
+        }
+        return r;
+    }
+};
+
+template <>
+struct QmmB<MXQ_Q6_K> {
+    u32x2 v0, v1, vh;
+    f16x2 s2[4];
+    MX_DEV void load(const char* q, const char* m, const char* d, int r, int h, int jq) {
+        v0 = *(const u32x2*)(q + r * 16 + 8 * h);
+        v1 = *(const u32x2*)(q + (32 + r) * 16 + 8 * h);
+        vh = *(const u32x2*)(q + (64 + r) * 16 + 8 * h);
+        const uint32_t sc = *(const uint32_t*)(m + r * 16 + 4 * jq);
+        const float df = half_to_f32(*(const uint32_t*)(d + r * 4) & 0xFFFF);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const _Float16 s = (_Float16)(df * (float)(int8_t)((sc >> (8 * i)) & 0xFF));
+            s2[i] = (f16x2){s, s};
+        }
+    }
+    template <int S>
+    MX_DEV f16x8 frag() const {
+        const u32x2 src = (S & 1) ? v1 : v0;
+        constexpr int sh = 4 * (S >> 1), qsh = 2 * S;
+        const uint32_t t0 = ((src[0] >> sh) & 0x0F0F0F0Fu) | (((vh[0] >> qsh) & 0x03030303u) << 4);
+        const uint32_t t1 = ((src[1] >> sh) & 0x0F0F0F0Fu) | (((vh[1] >> qsh) & 0x03030303u) << 4);
+        const f16x2 k = {(_Float16)1056.f, (_Float16)1056.f};  // 1024 magic + 32 code offset
+        f16x2 p[4];
+        magic4(t0, p[0], p[1]);
+        magic4(t1, p[2], p[3]);
+        f16x8 r;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const f16x2 v = (p[i] - k) * s2[S];
+            r[2 * i] = v[0];
+            r[2 * i + 1] = v[1];
+        }
+        return r;
+    }
+};
+
+template <>
+struct QmmB<MXQ_Q8_0> {
+    u32x2 qv[4];
+    f16x2 s2[2];
+    MX_DEV void load(const char* q, const char*, const char* d, int r, int h, int) {
+#pragma unroll
+        for (int s = 0; s < 4; ++s) qv[s] = *(const u32x2*)(q + (s * 32 + r) * 16 + 8 * h);
+        const f16x2 dd = __builtin_bit_cast(f16x2, *(const uint32_t*)(d + 4 * r));
+        s2[0] = (f16x2){dd[0], dd[0]};
+        s2[1] = (f16x2){dd[1], dd[1]};
+    }
+    template <int S>
+    MX_DEV f16x8 frag() const {
+        const uint32_t t0 = qv[S][0] ^ 0x80808080u, t1 = qv[S][1] ^ 0x80808080u;  // int8 -> u8 + 128
+        const f16x2 k = {(_Float16)1152.f, (_Float16)1152.f};
+        f16x2 p[4];
+        magic4(t0, p[0], p[1]);
+        magic4(t1, p[2], p[3]);
+        f16x8 r;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const f16x2 v = (p[i] - k) * s2[S >> 1];
+            r[2 * i] = v[0];
+            r[2 * i + 1] = v[1];
+        }
+        return r;
+    }
+};
+
+}  // namespace
+
+template <int QT, int WM, int WN, int NW, int EPI>
+__global__ __launch_bounds__(64 * NW) void qmm_kernel(const uint16_t* __restrict__ A, int lda, const uint8_t* __restrict__ W,
+                                                  const uint16_t* __restrict__ WD, int M, int N, int K, int n_ct,
+                                                  int n_mt, int splits, int kt_per_split, void* __restrict__ Cv,
+                                                  int ldc) {
+    using G = QmmGeom<QT, WN>;
+    using F = QmmFmt<QT>;
+    constexpr int BM = 32 * WM, COLS = G::COLS;
+    constexpr int A_BYTES = BM * 128;
+    constexpr int STAGE = A_BYTES + NW * G::WBYTES;
+    constexpr int NS = QmmRing<QT, WM, WN, NW>::STAGES;
+    static_assert(STAGE == QmmRing<QT, WM, WN, NW>::STAGE && NS >= 3, "ring");
+    constexpr int WA = BM / 8 / NW;  // A-tile LDS-DMA instructions per wave (8 rows x 128 B each)
+    static_assert(WA >= 1 && WA * 8 * NW == BM, "A tile split");
+    constexpr int NI = WA + G::NI;  // LDS-DMA wave-instructions per stage per wave
+    static_assert((NS - 2) * NI <= 63, "vmcnt range");
+    static_assert(WN <= 2, "one d / meta instruction covers at most 2 groups");
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int h = lane >> 5, col = lane & 31;
+
+    // XCD-aware bijective remap of the 1-D grid: consecutive logical ids share an XCD
+    const int nwg = gridDim.x, bid = blockIdx.x;
+    const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+    const int lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+    const int mt = lid % n_mt;
+    const int rest = lid / n_mt;
+    const int split = rest % splits;
+    const int ct = rest / splits;
+    (void)n_ct;
+
+    const int m_base = mt * BM;
+    const int n_wave = ct * NW * COLS + wave * COLS;
+    const int nkt = K / QMM_KT;
+    const int kt0 = split * kt_per_split;
+    const int kt1 = min(kt0 + kt_per_split, nkt);
+    if (kt0 >= kt1) return;
+    const int ngrp = N >> 5;
+    const size_t gstride = (size_t)(nkt / F::PER_UNIT) * F::UNIT;  // bytes per 32-column group
+
+    // ---- per-lane LDS-DMA source offsets (k-tile independent parts) ----
+    uint32_t aoff[WA];
+#pragma unroll
+    for (int i = 0; i < WA; ++i) {
+        const int r = (wave * WA + i) * 8 + (lane >> 3);
+        const int c = (lane & 7) ^ ((r >> 1) & 7);
+        aoff[i] = (uint32_t)(min(m_base + r, M - 1) * lda + c * 8);
+    }
+    // quant chunk slot q = ci*64 + lane -> group t = q / QCH, chunk j = q % QCH (contiguous per group)
+    const uint8_t* qsrc[G::QI];
+    bool qact[G::QI];
+#pragma unroll
+    for (int ci = 0; ci < G::QI; ++ci) {
+        const int q = ci * 64 + lane;
+        const int t = q / G::QCH, j = q % G::QCH;
+        qact[ci] = q < WN * G::QCH;
+        const int g = min((n_wave >> 5) + (qact[ci] ? t : 0), ngrp - 1);  // groups past N: re-read the last
+        qsrc[ci] = W + (size_t)g * gstride + F::QOFF + j * 16;
+    }
+    // meta / d slots: lane -> group t = lane / 32, column r = lane % 32
+    const int mg = min((n_wave >> 5) + (lane >> 5), ngrp - 1);
+    const uint8_t* msrc = W + (size_t)mg * gstride + F::MOFF + (lane & 31) * 16;
+    const uint8_t* dsrc = W + (size_t)mg * gstride + F::DOFF + (lane & 31) * 4;
+    const bool mact = lane < 32 * WN;
+
+    auto issue = [&](int kt, int slot) {
+        char* sb = smem + slot * STAGE;
+        const uint16_t* ak = A + (size_t)kt * QMM_KT;
+#pragma unroll
+        for (int i = 0; i < WA; ++i)
+            __builtin_amdgcn_global_load_lds((const void*)(ak + aoff[i]),
+                                             (MX_LDS void*)(sb + (wave * WA + i) * 1024), 16, 0, 0);
+        char* wb = sb + A_BYTES + wave * G::WBYTES;
+        const size_t unit = (size_t)(kt / F::PER_UNIT) * F::UNIT;
+        const int jq = kt % F::PER_UNIT;
+#pragma unroll
+        for (int ci = 0; ci < G::QI; ++ci)
+            if (qact[ci])
+                __builtin_amdgcn_global_load_lds((const void*)(qsrc[ci] + unit + jq * F::QSTRIDE),
+                                                 (MX_LDS void*)(wb + G::Q_OFF + ci * 1024), 16, 0, 0);
+        if constexpr (G::MI > 0) {
+            if (mact)
+                __builtin_amdgcn_global_load_lds((const void*)(msrc + unit), (MX_LDS void*)(wb + G::M_OFF), 16, 0, 0);
+        }
+        if constexpr (G::DI > 0) {
+            if (mact)
+                __builtin_amdgcn_global_load_lds((const void*)(dsrc + unit), (MX_LDS void*)(wb + G::D_OFF), 4, 0, 0);
+        }
+    };
+
+    f32x16 acc[WM][WN];
+#pragma unroll
+    for (int i = 0; i < WM; ++i)
+#pragma unroll
+        for (int t = 0; t < WN; ++t)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][t][r] = 0.f;
+
+    // prologue: NSTAGE-1 tiles in flight
+#pragma unroll
+    for (int s = 0; s < NS - 1; ++s)
+        if (kt0 + s < kt1) issue(kt0 + s, s);
+
+    int slot = 0;
+    for (int kt = kt0; kt < kt1; ++kt) {
+        // stages issued after kt so far: min(kt1 - 1, kt + NSTAGE - 2) - kt
+        const int ahead = min(kt1 - 1, kt + NS - 2) - kt;
+        qmm_wait_ahead<NI, NS - 2>(ahead);
+        if (kt + NS - 1 < kt1) {
+            int ns = slot + NS - 1;
+            if (ns >= NS) ns -= NS;
+            issue(kt + NS - 1, ns);
+        }
+        const char* sb = smem + slot * STAGE;
+        const char* wl = sb + A_BYTES + wave * G::WBYTES;
+        const int jq = kt & 3;
+        QmmB<QT> bw[WN];
+#pragma unroll
+        for (int t = 0; t < WN; ++t)
+            bw[t].load(wl + G::Q_OFF + t * F::QB, wl + G::M_OFF + t * 512, wl + G::D_OFF + t * 128, col, h, jq);
+#define QMM_KSTEP(S)                                                                                       \
+    {                                                                                                      \
+        f16x8 a[WM], b[WN];                                                                                \
+        _Pragma("unroll") for (int i = 0; i < WM; ++i) a[i] = *(const f16x8*)(sb + qmm_a_off(i * 32 + col, 2 * (S) + h)); \
+        _Pragma("unroll") for (int t = 0; t < WN; ++t) b[t] = bw[t].template frag<S>();                    \
+        _Pragma("unroll") for (int i = 0; i < WM; ++i)                                                     \
+            _Pragma("unroll") for (int t = 0; t < WN; ++t) acc[i][t] =                                     \
+                __builtin_amdgcn_mfma_f32_32x32x16_f16(a[i], b[t], acc[i][t], 0, 0, 0);                    \
+    }
+        QMM_KSTEP(0) QMM_KSTEP(1) QMM_KSTEP(2) QMM_KSTEP(3)
+#undef QMM_KSTEP
+        if (++slot == NS) slot = 0;
+    }
+
+    // ---- epilogue: 32x32 C/D layout: col = lane & 31, row = 8*(r>>2) + 4*(lane>>5) + (r&3) ----
+#pragma unroll
+    for (int t = 0; t < WN; ++t) {
+        const int nt = n_wave + 32 * t;
+        const int n = nt + col;
+        if constexpr (EPI == E16_SWIGLU || EPI == E16_GEGLU) {
+            // W rows interleaved in 16-row groups: tile columns 0..15 gate, 16..31 up of the same features
+#pragma unroll
+            for (int i = 0; i < WM; ++i)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const float v = acc[i][t][r];
+                    const float up = __shfl_xor(v, 16);
+                    const int m = m_base + i * 32 + 8 * (r >> 2) + 4 * h + (r & 3);
+                    if (col < 16 && n < N && m < M)
+                        ((uint16_t*)Cv)[(size_t)m * ldc + (nt >> 1) + col] = f32_to_act<true>(glu_gate_f<EPI>(v) * up);
+                }
+            continue;
+        }
+        if (n >= N) continue;
+#pragma unroll
+        for (int i = 0; i < WM; ++i) {
+            const int m0 = m_base + i * 32 + 4 * h;
+            float* cf = ((float*)Cv) + (size_t)m0 * ldc + n;
+            uint16_t* ch = ((uint16_t*)Cv) + (size_t)m0 * ldc + n;
+            auto roff = [&](int r) { return (size_t)(8 * (r >> 2) + (r & 3)) * ldc; };
+            if (m_base + i * 32 + 32 <= M) {
+                // full tile: branch-free, so the RMW loads issue back to back and wait once
+                if constexpr (EPI == E16_ADD_F32) {
+                    if (splits == 1) {
+                        float old[16];
+#pragma unroll
+                        for (int r = 0; r < 16; ++r) old[r] = cf[roff(r)];
+#pragma unroll
+                        for (int r = 0; r < 16; ++r) cf[roff(r)] = old[r] + acc[i][t][r];
+                    } else {
+#pragma unroll
+                        for (int r = 0; r < 16; ++r) atomicAdd(cf + roff(r), acc[i][t][r]);
+                    }
+                } else {
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        if constexpr (EPI == E16_F32) cf[roff(r)] = acc[i][t][r];
+                        else ch[roff(r)] = f32_to_act<true>(acc[i][t][r]);
+                    }
+                }
+                continue;
+            }
+            // partial tile (rows past M): clamp the RMW loads so they still issue together
+            float old[16];
+            if constexpr (EPI == E16_ADD_F32) {
+                if (splits == 1) {
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const int rr = min(m0 + 8 * (r >> 2) + (r & 3), M - 1) - m0;
+                        old[r] = cf[(size_t)rr * ldc];
+                    }
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                if (m0 + 8 * (r >> 2) + (r & 3) >= M) continue;
+                const float v = acc[i][t][r];
+                if constexpr (EPI == E16_F32) cf[roff(r)] = v;
+                else if constexpr (EPI == E16_ACT) ch[roff(r)] = f32_to_act<true>(v);
+                else if (splits == 1) cf[roff(r)] = old[r] + v;  // sole owner of the tile: plain RMW
+                else atomicAdd(cf + roff(r), v);
+            }
+        }
+    }
+}
+
+template <int QT, int WM, int WN, int NW, int EPI>
+static int launch_qmm(const uint16_t* A, int lda, const uint8_t* W, const uint16_t* WD, int M, int N, int K,
+                      int splits, void* C, int ldc, hipStream_t st) {
+    using G = QmmGeom<QT, WN>;
+    constexpr int BM = 32 * WM, BN = NW * G::COLS;
+    constexpr int STAGE = BM * 128 + NW * G::WBYTES;
+    constexpr size_t lds = (size_t)QmmRing<QT, WM, WN, NW>::STAGES * STAGE;
+    static_assert(lds <= 160 * 1024, "LDS");
+    const int nkt = K / QMM_KT;
+    splits = max(1, min(splits, nkt));
+    const int ktps = (nkt + splits - 1) / splits;
+    splits = (nkt + ktps - 1) / ktps;  // no empty splits
+    const int n_ct = (N + BN - 1) / BN, n_mt = (M + BM - 1) / BM;
+    const long nwg = (long)n_ct * splits * n_mt;
+    if (nwg <= 0 || nwg > 0x7fffffff) return (int)hipErrorInvalidValue;
+    static bool attr_set = false;
+    if (!attr_set) {
+        (void)hipFuncSetAttribute((const void*)qmm_kernel<QT, WM, WN, NW, EPI>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)lds);
+        attr_set = true;
+    }
+    qmm_kernel<QT, WM, WN, NW, EPI><<<dim3((unsigned)nwg), 64 * NW, lds, st>>>(A, lda, W, WD, M, N, K, n_ct, n_mt, splits,
+                                                                          ktps, C, ldc);
+    MXK_CHECK_LAUNCH();
+}
+
+template <int QT, int EPI>
+static int dispatch_qmm(int wm, int wn, int nw, const uint16_t* A, int lda, const uint8_t* W, const uint16_t* WD, int M,
+                        int N, int K, int splits, void* C, int ldc, hipStream_t st) {
+#define QMM_CASE(WM_, WN_, NW_) \
+    if (wm == WM_ && wn == WN_ && nw == NW_) return launch_qmm<QT, WM_, WN_, NW_, EPI>(A, lda, W, WD, M, N, K, splits, C, ldc, st);
+    QMM_CASE(1, 1, 4) QMM_CASE(2, 1, 4) QMM_CASE(4, 1, 4) QMM_CASE(1, 2, 4) QMM_CASE(2, 2, 4) QMM_CASE(4, 2, 4)
+    QMM_CASE(2, 1, 8) QMM_CASE(4, 1, 8) QMM_CASE(2, 2, 8) QMM_CASE(4, 2, 8)
+#undef QMM_CASE
+    return (int)hipErrorInvalidValue;
+}
+
+// A must be f16 (act16 mode f16), 16-B aligned rows (lda % 8 == 0); K % 256 == 0; W in the t32 tiled
+// layout (N % 32 == 0; WD unused). epi: 0 fp32 store, 1 act16 store, 2 fp32 accumulate (split-K via
+// atomics when splits > 1), 3/4 SwiGLU/GeGLU over 16-row interleaved gate/up -> act16 [M, N/2].
+// (wm, wn, nw): 32*wm-row x 32*wn*nw-column tiles, nw waves (4 or 8: 8 = 2 waves per SIMD, whose
+// dequant / LDS phases overlap each other's MFMAs).
+extern "C" int mxk_qmm(int qtype, int epi, int wm, int wn, int nw, const uint16_t* A, int lda, const uint8_t* W,
+                       const uint16_t* WD, int M, int N, int K, int splits, void* C, int ldc, hipStream_t st) {
+    if (M <= 0) return 0;
+    if (K % 256 || (lda & 7) || ((uintptr_t)A & 15) || ((uintptr_t)W & 15)) return (int)hipErrorInvalidValue;
+    if (epi != E16_ADD_F32 && splits != 1) return (int)hipErrorInvalidValue;
+    if ((epi == E16_SWIGLU || epi == E16_GEGLU) && (N & 31)) return (int)hipErrorInvalidValue;
+    if (N & 31) return (int)hipErrorInvalidValue;
+#define QMM_EPI(QT_)                                                                                           \
+    switch (epi) {                                                                                             \
+        case E16_F32: return dispatch_qmm<QT_, E16_F32>(wm, wn, nw, A, lda, W, WD, M, N, K, splits, C, ldc, st);         \
+        case E16_ACT: return dispatch_qmm<QT_, E16_ACT>(wm, wn, nw, A, lda, W, WD, M, N, K, splits, C, ldc, st);         \
+        case E16_ADD_F32: return dispatch_qmm<QT_, E16_ADD_F32>(wm, wn, nw, A, lda, W, WD, M, N, K, splits, C, ldc, st); \
+        case E16_SWIGLU: return dispatch_qmm<QT_, E16_SWIGLU>(wm, wn, nw, A, lda, W, WD, M, N, K, splits, C, ldc, st);   \
+        case E16_GEGLU: return dispatch_qmm<QT_, E16_GEGLU>(wm, wn, nw, A, lda, W, WD, M, N, K, splits, C, ldc, st);     \
+    }
+    switch (qtype) {
+        case MXQ_Q4_K: QMM_EPI(MXQ_Q4_K) break;
+        case MXQ_Q6_K: QMM_EPI(MXQ_Q6_K) break;
+        case MXQ_Q8_0: QMM_EPI(MXQ_Q8_0) break;
+    }
+#undef QMM_EPI
+    return (int)hipErrorInvalidValue;
+}

@@ -1,0 +1,290 @@
+// qmv.hip — decode GEMV (M <= 4 rows) and row dequantisation for weights in the "t32" tiled layout
+// (see qmm.hip / ops/quant.py tile32):
+//
+//   C[M, N] (+)= X[M, K] · W[N, K]^T   with X as q8 activations (int8 [M][K] + float2 {d, d*sum} per 32)
+//
+// One workgroup (8 waves) owns one 32-column group and splits its K range over the waves; lane
+// (r = lane & 31, h = lane >> 5) owns column r and half h of every 64-element quarter, so each wave's
+// weight loads are 1 KB contiguous wave-instructions (the tiled layout's point), all issued before
+// the int8 dot products (sdot4) consume them. Partial sums meet in LDS; the epilogue (fp32 store /
+// act16 store / fp32 accumulate / SwiGLU|GeGLU over the 16+16 interleaved gate|up rows) is fused.
+#include "qdeq16.h"
+
+namespace {
+constexpr int QMV_WAVES = 8;
+
+// per-lane weight state for one unit (Q4_K/Q6_K: one 256-element super-block; Q8_0: one 64-k tile)
+template <int QT>
+struct TUnit;
+
+template <>
+struct TUnit<MXQ_Q4_K> {
+    static constexpr int BYTES = 4608, ELEMS = 256;
+    u32x4 hd, q[4];
+    MX_DEV void load(const uint8_t* u, int r, int h) {
+        hd = *(const u32x4*)(u + r * 16);
+#pragma unroll
+        for (int jq = 0; jq < 4; ++jq) q[jq] = __builtin_nontemporal_load((const u32x4*)(u + 512 + jq * 1024 + h * 512 + r * 16));
+    }
+    // this lane's contribution against activation row x (k offset of the unit already applied)
+    MX_DEV float dot(const int8_t* x, const float2* ds, int h) const {
+        const float d = half_to_f32(hd[0] & 0xFFFF), dm = half_to_f32(hd[0] >> 16);
+        float acc = 0.f, mins = 0.f;
+#pragma unroll
+        for (int jq = 0; jq < 4; ++jq) {
+            const u32x4 xl = *(const u32x4*)(x + 64 * jq + 16 * h);
+            const u32x4 xh = *(const u32x4*)(x + 64 * jq + 32 + 16 * h);
+            int il = 0, ih = 0;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                il = __builtin_amdgcn_sdot4((int)(q[jq][i] & 0x0F0F0F0Fu), (int)xl[i], il, false);
+                ih = __builtin_amdgcn_sdot4((int)((q[jq][i] >> 4) & 0x0F0F0F0Fu), (int)xh[i], ih, false);
+            }
+            int sc0, m0, sc1, m1;
+            q4k_scale_min_w(hd[1], hd[2], hd[3], 2 * jq, sc0, m0);
+            q4k_scale_min_w(hd[1], hd[2], hd[3], 2 * jq + 1, sc1, m1);
+            const float2 dl = ds[2 * jq], dh = ds[2 * jq + 1];
+            acc += (float)sc0 * dl.x * (float)il + (float)sc1 * dh.x * (float)ih;
+            mins += (float)m0 * dl.y + (float)m1 * dh.y;  // {d, d*sum} covers the whole 32-block
+        }
+        return d * acc - (h == 0 ? dm * mins : 0.f);
+    }
+};
+
+template <>
+struct TUnit<MXQ_Q6_K> {
+    static constexpr int BYTES = 6784, ELEMS = 256;
+    u32x4 sc, ql[4], qh[4];
+    uint32_t dw;
+    MX_DEV void load(const uint8_t* u, int r, int h) {
+        sc = *(const u32x4*)(u + r * 16);
+        dw = *(const uint32_t*)(u + 512 + r * 4);
+#pragma unroll
+        for (int jq = 0; jq < 4; ++jq) {
+            const uint8_t* p = u + 640 + jq * 1536;
+            ql[jq] = __builtin_nontemporal_load((const u32x4*)(p + h * 512 + r * 16));
+            qh[jq] = __builtin_nontemporal_load((const u32x4*)(p + 1024 + r * 16));
+        }
+    }
+    MX_DEV float dot(const int8_t* x, const float2* ds, int h) const {
+        const float d = half_to_f32(dw & 0xFFFF);
+        float acc = 0.f;
+#pragma unroll
+        for (int jq = 0; jq < 4; ++jq) {
+            const u32x4 xl = *(const u32x4*)(x + 64 * jq + 16 * h);
+            const u32x4 xh = *(const u32x4*)(x + 64 * jq + 32 + 16 * h);
+            int il = 0, ih = 0;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const uint32_t lo = (ql[jq][i] & 0x0F0F0F0Fu) | (((qh[jq][i] >> (2 * h)) & 0x03030303u) << 4);
+                const uint32_t hi = ((ql[jq][i] >> 4) & 0x0F0F0F0Fu) | (((qh[jq][i] >> (2 * (2 + h))) & 0x03030303u) << 4);
+                il = __builtin_amdgcn_sdot4((int)q6_bias_bytes(lo), (int)xl[i], il, false);
+                ih = __builtin_amdgcn_sdot4((int)q6_bias_bytes(hi), (int)xh[i], ih, false);
+            }
+            const int s_lo = (int8_t)((sc[jq] >> (8 * h)) & 0xFF), s_hi = (int8_t)((sc[jq] >> (8 * (2 + h))) & 0xFF);
+            acc += (float)s_lo * ds[2 * jq].x * (float)il + (float)s_hi * ds[2 * jq + 1].x * (float)ih;
+        }
+        return d * acc;
+    }
+};
+
+template <>
+struct TUnit<MXQ_Q8_0> {
+    static constexpr int BYTES = 2176, ELEMS = 64;
+    uint32_t dw;
+    u32x4 q0, q1;
+    MX_DEV void load(const uint8_t* u, int r, int h) {
+        dw = *(const uint32_t*)(u + r * 4);
+        q0 = __builtin_nontemporal_load((const u32x4*)(u + 128 + (2 * h) * 512 + r * 16));
+        q1 = __builtin_nontemporal_load((const u32x4*)(u + 128 + (2 * h + 1) * 512 + r * 16));
+    }
+    MX_DEV float dot(const int8_t* x, const float2* ds, int h) const {
+        const u32x4 x0 = *(const u32x4*)(x + 32 * h), x1 = *(const u32x4*)(x + 32 * h + 16);
+        int s = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            s = __builtin_amdgcn_sdot4((int)q0[i], (int)x0[i], s, false);
+            s = __builtin_amdgcn_sdot4((int)q1[i], (int)x1[i], s, false);
+        }
+        const float d = half_to_f32(h ? (dw >> 16) : (dw & 0xFFFF));
+        return d * ds[h].x * (float)s;
+    }
+};
+
+}  // namespace
+
+template <int QT, int MM, int EPI, bool F16>
+__global__ __launch_bounds__(64 * QMV_WAVES) void qmv_kernel(const int8_t* __restrict__ xq,
+                                                             const float2* __restrict__ xds,
+                                                             const uint8_t* __restrict__ W, int M, int N, int K,
+                                                             void* __restrict__ Cv, int ldc) {
+    using U = TUnit<QT>;
+    __shared__ float red[QMV_WAVES][MM][32];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int r = lane & 31, h = lane >> 5;
+    const int g = blockIdx.x;
+    const int nunit = K / U::ELEMS;
+    const uint8_t* wg = W + (size_t)g * nunit * U::BYTES;
+    float acc[MM];
+#pragma unroll
+    for (int m = 0; m < MM; ++m) acc[m] = 0.f;
+    // two units in flight per wave: both loads issue before either dot product
+    int u = wave;
+    for (; u + QMV_WAVES < nunit; u += 2 * QMV_WAVES) {
+        U a, b;
+        a.load(wg + (size_t)u * U::BYTES, r, h);
+        b.load(wg + (size_t)(u + QMV_WAVES) * U::BYTES, r, h);
+#pragma unroll
+        for (int m = 0; m < MM; ++m) {
+            if (m < M) {
+                const int8_t* x = xq + (size_t)m * K;
+                const float2* ds = xds + (size_t)m * (K / 32);
+                acc[m] += a.dot(x + (size_t)u * U::ELEMS, ds + u * (U::ELEMS / 32), h);
+                acc[m] += b.dot(x + (size_t)(u + QMV_WAVES) * U::ELEMS, ds + (u + QMV_WAVES) * (U::ELEMS / 32), h);
+            }
+        }
+    }
+    if (u < nunit) {
+        U a;
+        a.load(wg + (size_t)u * U::BYTES, r, h);
+#pragma unroll
+        for (int m = 0; m < MM; ++m)
+            if (m < M)
+                acc[m] += a.dot(xq + (size_t)m * K + (size_t)u * U::ELEMS, xds + (size_t)m * (K / 32) + u * (U::ELEMS / 32), h);
+    }
+#pragma unroll
+    for (int m = 0; m < MM; ++m) {
+        const float v = acc[m] + __shfl_xor(acc[m], 32);
+        if (h == 0) red[wave][m][r] = v;
+    }
+    __syncthreads();
+    if (wave != 0) return;
+#pragma unroll
+    for (int m = 0; m < MM; ++m) {
+        if (m >= M) break;
+        float v = 0.f;
+        if (h == 0) {
+#pragma unroll
+            for (int w = 0; w < QMV_WAVES; ++w) v += red[w][m][r];
+        }
+        const int n = g * 32 + r;
+        if constexpr (EPI == E16_SWIGLU || EPI == E16_GEGLU) {
+            const float up = __shfl_down(v, 16);
+            if (h == 0 && r < 16) ((uint16_t*)Cv)[(size_t)m * ldc + g * 16 + r] = f32_to_act<F16>(glu_gate_f<EPI>(v) * up);
+        } else if (h == 0) {
+            if constexpr (EPI == E16_F32) ((float*)Cv)[(size_t)m * ldc + n] = v;
+            else if constexpr (EPI == E16_ACT) ((uint16_t*)Cv)[(size_t)m * ldc + n] = f32_to_act<F16>(v);
+            else ((float*)Cv)[(size_t)m * ldc + n] += v;
+        }
+    }
+}
+
+// ---- dequantise whole rows (output features) of a t32 weight: embedding gather / debugging ----
+template <int QT, bool F16>
+__global__ __launch_bounds__(256) void dequant_t32_kernel(const uint8_t* __restrict__ W, const int* __restrict__ rows,
+                                                          int K, uint16_t* __restrict__ ob, float* __restrict__ of,
+                                                          int ldo) {
+    const int orow = blockIdx.y;
+    const int n = rows ? rows[orow] : orow;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int chunk = blockIdx.x * 4 + wave;  // 256 elements per wave
+    if (chunk * 256 >= K) return;
+    const int g = n >> 5, r = n & 31;
+    const int e = 4 * lane;  // this lane's 4 consecutive elements of the chunk
+    float v[4];
+    if constexpr (QT == MXQ_Q8_0) {
+        const int kt = chunk * 4 + (e >> 6), u = e & 63;
+        const uint8_t* base = W + ((size_t)g * (K / 64) + kt) * 2176;
+        const uint32_t dw = *(const uint32_t*)(base + r * 4);
+        const float d = half_to_f32(u < 32 ? (dw & 0xFFFF) : (dw >> 16));
+        const uint32_t qq = *(const uint32_t*)(base + 128 + (u >> 4) * 512 + r * 16 + (u & 15));
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = d * (float)(int8_t)((qq >> (8 * i)) & 0xFF);
+    } else if constexpr (QT == MXQ_Q4_K) {
+        const uint8_t* base = W + ((size_t)g * (K / 256) + chunk) * 4608;
+        const u32x4 hd = *(const u32x4*)(base + r * 16);
+        const int jq = e >> 6, u = e & 63, b = u & 31;
+        const uint32_t qq = *(const uint32_t*)(base + 512 + jq * 1024 + (b >> 4) * 512 + r * 16 + (b & 15));
+        int sc, mn;
+        q4k_scale_min_w(hd[1], hd[2], hd[3], 2 * jq + (u >> 5), sc, mn);
+        const float d = half_to_f32(hd[0] & 0xFFFF) * (float)sc, m = half_to_f32(hd[0] >> 16) * (float)mn;
+        const int sh = (u >> 5) * 4;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = d * (float)((qq >> (8 * i + sh)) & 0xF) - m;
+    } else {
+        const uint8_t* base = W + ((size_t)g * (K / 256) + chunk) * 6784;
+        const int jq = e >> 6, u = e & 63, b = u & 31, s16 = u >> 4;
+        const uint8_t* p = base + 640 + jq * 1536;
+        const uint32_t ql = *(const uint32_t*)(p + (b >> 4) * 512 + r * 16 + (b & 15));
+        const uint32_t qh = *(const uint32_t*)(p + 1024 + r * 16 + (u & 15));
+        const float d = half_to_f32(*(const uint32_t*)(base + 512 + r * 4) & 0xFFFF) *
+                        (float)(int8_t)base[r * 16 + 4 * jq + s16];
+        const int sh = (u >> 5) * 4;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int q = (int)((ql >> (8 * i + sh)) & 0xF) | (int)(((qh >> (8 * i + 2 * s16)) & 0x3) << 4);
+            v[i] = d * (float)(q - 32);
+        }
+    }
+    const int k0 = chunk * 256 + e;
+    if (ob) {
+        uint2 p;
+        p.x = pack_act2<F16>(v[0], v[1]);
+        p.y = pack_act2<F16>(v[2], v[3]);
+        *(uint2*)(ob + (size_t)orow * ldo + k0) = p;
+    }
+    if (of) *(float4*)(of + (size_t)orow * ldo + k0) = make_float4(v[0], v[1], v[2], v[3]);
+}
+
+template <int QT, int MM, int EPI>
+static int launch_qmv(const int8_t* xq, const float2* xds, const uint8_t* W, int M, int N, int K, void* C, int ldc,
+                      hipStream_t st) {
+    MX_ACT_DISPATCH(qmv_kernel<QT, MM, EPI, F16><<<N / 32, 64 * QMV_WAVES, 0, st>>>(xq, xds, W, M, N, K, C, ldc));
+    MXK_CHECK_LAUNCH();
+}
+
+// X as q8 (int8 [M][K] + float2 [M][K/32]); W t32-tiled; M <= 4; N % 32 == 0; K % 256 == 0.
+// epi: 0 fp32 store, 1 act16 store, 2 fp32 accumulate, 3/4 SwiGLU/GeGLU (act16 [M, N/2]).
+extern "C" int mxk_qmv(int qtype, int epi, const int8_t* xq, const float2* xds, const uint8_t* W, int M, int N,
+                       int K, void* C, int ldc, hipStream_t st) {
+    if (M <= 0) return 0;
+    if (M > 4 || K % 256 || N % 32) return (int)hipErrorInvalidValue;
+#define QMV_M(QT_, EPI_)                                                            \
+    if (M == 1) return launch_qmv<QT_, 1, EPI_>(xq, xds, W, M, N, K, C, ldc, st);   \
+    if (M == 2) return launch_qmv<QT_, 2, EPI_>(xq, xds, W, M, N, K, C, ldc, st);   \
+    return launch_qmv<QT_, 4, EPI_>(xq, xds, W, M, N, K, C, ldc, st);
+#define QMV_EPI(QT_)                                    \
+    switch (epi) {                                      \
+        case E16_F32: { QMV_M(QT_, E16_F32) }           \
+        case E16_ACT: { QMV_M(QT_, E16_ACT) }           \
+        case E16_ADD_F32: { QMV_M(QT_, E16_ADD_F32) }   \
+        case E16_SWIGLU: { QMV_M(QT_, E16_SWIGLU) }     \
+        case E16_GEGLU: { QMV_M(QT_, E16_GEGLU) }       \
+    }
+    switch (qtype) {
+        case MXQ_Q4_K: QMV_EPI(MXQ_Q4_K) break;
+        case MXQ_Q6_K: QMV_EPI(MXQ_Q6_K) break;
+        case MXQ_Q8_0: QMV_EPI(MXQ_Q8_0) break;
+    }
+#undef QMV_EPI
+#undef QMV_M
+    return (int)hipErrorInvalidValue;
+}
+
+extern "C" int mxk_dequant_t32(int qtype, const uint8_t* W, const int* rows, int nrows, int K, uint16_t* ob,
+                               float* of, int ldo, hipStream_t st) {
+    if (nrows <= 0) return 0;
+    if (K % 256) return (int)hipErrorInvalidValue;
+    dim3 grid((K / 256 + 3) / 4, nrows);
+    int rc = 0;
+    MX_ACT_DISPATCH({
+        switch (qtype) {
+            case MXQ_Q4_K: dequant_t32_kernel<MXQ_Q4_K, F16><<<grid, 256, 0, st>>>(W, rows, K, ob, of, ldo); break;
+            case MXQ_Q6_K: dequant_t32_kernel<MXQ_Q6_K, F16><<<grid, 256, 0, st>>>(W, rows, K, ob, of, ldo); break;
+            case MXQ_Q8_0: dequant_t32_kernel<MXQ_Q8_0, F16><<<grid, 256, 0, st>>>(W, rows, K, ob, of, ldo); break;
+            default: rc = (int)hipErrorInvalidValue;
+        }
+    });
+    if (rc) return rc;
+    MXK_CHECK_LAUNCH();
+}

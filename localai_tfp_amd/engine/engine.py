@@ -43,7 +43,9 @@ class EngineConfig:
     use_graphs: bool = True
     graph_buckets: tuple = (1, 2, 4, 8, 16, 32, 48, 64, 96, 128, 160, 192, 224, 256)
     attn_part_size: int = 256  # must match ops.core.attn_decode's default
-    prefill_bf16_cache: bool = True  # dense bf16 copy of the linear weights for M>=128 prefill (GPU)
+    # dense 16-bit copy of the layer projections for hipBLASLt at the M where it still beats the qmm
+    # kernels on t32-tiled weights (ops/linear.py DENSE_MIN_M_*; never for the LM head)
+    prefill_bf16_cache: bool = True
     kv_dtype: str = "bf16"  # paged KV cache element type: bf16 | fp8 (OCP e4m3, half the bytes per token)
     n_draft: int = 0  # speculative decoding: draft tokens per step (needs a draft model; 0 = off)
     spec_max_batch: int = 32  # speculate only on decode batches up to this size (latency-bound regime)

@@ -263,6 +263,7 @@ class LlamaModel:
             if progress:
                 progress(i + 1, cfg.n_layers)
         if stage:
+            m.finalize_layout()
             return m
         emb = get_tensor("token_embd.weight")
         raw, qt, shape = emb
@@ -275,7 +276,21 @@ class LlamaModel:
             cfg.tie_embeddings = True
         else:
             m.lm_head = qw("output.weight")
+        m.finalize_layout()
         return m
+
+    def finalize_layout(self):
+        """Re-lay the dense-layer projections (and the LM head) out in the t32 tiled layout the qmm /
+        qmv kernels stream (ops/quant.py tile32). After gate|up interleaving and Q|K|V fusion, which
+        work on the row layout; MoE expert stacks keep theirs (moe.py kernels). No-op on CPU / bf16 mode."""
+        if self.device.type != "cuda":
+            return
+        for L in self.layers:
+            for w in (*L.qkv_parts, L.wo, L.wgu, L.wg, L.wu, L.wd):
+                if isinstance(w, QWeight):
+                    w.to_t32()
+        if isinstance(self.lm_head, QWeight):
+            self.lm_head.to_t32()  # tied embeddings follow (embed() reads either layout)
 
     def weight_bytes(self) -> int:
         n = 0
@@ -298,8 +313,8 @@ class LlamaModel:
                     w.build_bf16_cache()
             if L.moe is not None:
                 L.moe.build_bf16_cache()
-        if isinstance(self.lm_head, QWeight) and self.lm_head.is_quant:
-            self.lm_head.build_bf16_cache()
+        if isinstance(self.lm_head, QWeight) and self.lm_head.is_quant and self.lm_head.layout != "t32":
+            self.lm_head.build_bf16_cache()  # t32 LM heads run qmm at every M (measured faster)
 
     # ------------------------------------------------------------------ forward
     def embed(self, tokens: torch.Tensor, out: torch.Tensor):
@@ -311,8 +326,12 @@ class LlamaModel:
                 K.gather_rows(E.data, tokens, out, self.cfg.embed_scale)
             return out
         from .. import _native as N
-        N.kcall("mxk_dequant_rows", int(E.qtype), E.data.data_ptr(), N.ptr(E.dplane), tokens.data_ptr(),
-                tokens.numel(), E.K, None, out.data_ptr(), out.stride(0), N.stream_ptr())
+        if E.layout == "t32":
+            N.kcall("mxk_dequant_t32", int(E.qtype), E.data.data_ptr(), tokens.data_ptr(), tokens.numel(), E.K,
+                    None, out.data_ptr(), out.stride(0), N.stream_ptr())
+        else:
+            N.kcall("mxk_dequant_rows", int(E.qtype), E.data.data_ptr(), N.ptr(E.dplane), tokens.data_ptr(),
+                    tokens.numel(), E.K, None, out.data_ptr(), out.stride(0), N.stream_ptr())
         if self.cfg.embed_scale != 1.0:
             out.mul_(self.cfg.embed_scale)
         return out

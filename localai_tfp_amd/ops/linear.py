@@ -50,6 +50,7 @@ class QWeight:
         self._raw_qtype = raw_qtype
         self._dense_f32: torch.Tensor | None = None
         self.bf16_cache: torch.Tensor | None = None
+        self.layout = "ggml"  # "ggml" (GPU-native block rows) | "t32" (tiled, ops/quant.py tile32)
 
     # ---------------------------------------------------------------- construction
     @classmethod
@@ -111,9 +112,24 @@ class QWeight:
         of = out if dtype == torch.float32 else None
         if ob is not None:
             N.ensure_act(dtype)
+        if self.layout == "t32":
+            N.kcall("mxk_dequant_t32", int(self.qtype), self.data.data_ptr(), N.ptr(rows), n, self.K, N.ptr(ob),
+                    N.ptr(of), self.K, N.stream_ptr())
+            return out
         N.kcall("mxk_dequant_rows", int(self.qtype), self.data.data_ptr(), N.ptr(self.dplane),
                 N.ptr(rows), n, self.K, N.ptr(ob), N.ptr(of), self.K, N.stream_ptr())
         return out
+
+    def to_t32(self) -> bool:
+        """Re-lay the GPU copy out in the t32 tiled layout (qmm / qmv kernels). In place; returns False
+        (layout unchanged) when the weight does not qualify (CPU, dense, N % 32, K % 256, bf16 mode)."""
+        if (self.layout == "t32" or not self.is_quant or not self.data.is_cuda or self.N % 32 or self.K % 256
+                or ACT_DTYPE != torch.float16 or int(self.qtype) not in (int(q) for q in Q.T32_UNIT)):
+            return self.layout == "t32"
+        self.data = Q.tile32(self.data, self.dplane, int(self.qtype), self.N, self.K)
+        self.dplane = None
+        self.layout = "t32"
+        return True
 
     def build_bf16_cache(self, dtype=None):
         """Optional dense 16-bit (ACT_DTYPE) copy for large-M prefill through hipBLASLt (288 GB HBM
@@ -125,7 +141,7 @@ class QWeight:
 
 def concat_rows(ws: list[QWeight], name: str = "") -> QWeight | None:
     """Fuse projections sharing K and qtype along N (e.g. Q|K|V). None if not fusable."""
-    if not ws or any(w.qtype != ws[0].qtype or w.K != ws[0].K for w in ws):
+    if not ws or any(w.qtype != ws[0].qtype or w.K != ws[0].K or w.layout != "ggml" for w in ws):
         return None
     if ws[0].device.type == "cpu":
         if any(w._raw is None for w in ws):
@@ -140,7 +156,7 @@ def concat_rows(ws: list[QWeight], name: str = "") -> QWeight | None:
 
 def interleave_gate_up(gate: QWeight, up: QWeight, name: str = "") -> QWeight | None:
     """Gate/up rows interleaved in 16-row groups for the fused SwiGLU epilogue."""
-    if gate.qtype != up.qtype or gate.K != up.K or gate.N != up.N or gate.N % 16:
+    if gate.qtype != up.qtype or gate.K != up.K or gate.N != up.N or gate.N % 16 or gate.layout != "ggml":
         return None
     if gate.device.type == "cpu":
         if gate._raw is None:
@@ -196,6 +212,8 @@ def qmatmul(W: QWeight, x: torch.Tensor | None, epi: int, out: torch.Tensor, *, 
     if not W.is_quant:
         y = torch.matmul(x, W.data.t()) if x.dtype == W.data.dtype else torch.matmul(x.to(W.data.dtype), W.data.t())
         return _apply_epi_dense(y, epi, out)
+    if W.layout == "t32":
+        return _qmatmul_t32(W, x, epi, out, xq, xds, M, out_zeroed)
     if M <= 4 and xq is not None:
         if epi in (EPI_BF16, *GLU_EPIS):
             N.ensure_act(out.dtype)
@@ -206,21 +224,7 @@ def qmatmul(W: QWeight, x: torch.Tensor | None, epi: int, out: torch.Tensor, *, 
         raise ValueError("qmatmul: MFMA path needs 16-bit activations")
     can_split = epi == EPI_ADD_F32 or (epi == EPI_F32 and out_zeroed)
     if W.bf16_cache is not None and M >= dense_min_m(x.dtype, epi, can_split) and W.bf16_cache.dtype == x.dtype:
-        wt = W.bf16_cache.t()
-        if epi in (EPI_ADD_F32, EPI_F32) and out.is_contiguous() and _fp32_out_ok(x.dtype):
-            # hipBLASLt bf16 x bf16 -> fp32 with the residual add fused as beta = 1
-            if epi == EPI_ADD_F32:
-                torch.addmm(out, x, wt, out_dtype=torch.float32, out=out)
-            else:
-                torch.mm(x, wt, out_dtype=torch.float32, out=out)
-            return out
-        y = torch.matmul(x, wt)
-        if epi in GLU_EPIS:
-            N.ensure_act(out.dtype)
-            N.kcall("mxk_swiglu_il16", y.data_ptr(), y.stride(0), out.data_ptr(), out.stride(0), M, W.N // 2,
-                    int(epi == EPI_GEGLU), N.stream_ptr())
-            return out
-        return _apply_epi_dense(y, epi, out)
+        return _dense_cached(W, x, epi, out, M)
     nblk = W.K // 256
     f16 = x.dtype == torch.float16
     if f16 and M >= Q32_MIN_M:
@@ -244,6 +248,49 @@ def qmatmul(W: QWeight, x: torch.Tensor | None, epi: int, out: torch.Tensor, *, 
     return out
 
 
+def _dense_cached(W: QWeight, x, epi: int, out, M: int):
+    """hipBLASLt on the dense 16-bit weight copy (only where it measured faster than qmm)."""
+    wt = W.bf16_cache.t()
+    if epi in (EPI_ADD_F32, EPI_F32) and out.is_contiguous() and _fp32_out_ok(x.dtype):
+        # hipBLASLt 16-bit x 16-bit -> fp32 with the residual add fused as beta = 1
+        if epi == EPI_ADD_F32:
+            torch.addmm(out, x, wt, out_dtype=torch.float32, out=out)
+        else:
+            torch.mm(x, wt, out_dtype=torch.float32, out=out)
+        return out
+    y = torch.matmul(x, wt)
+    if epi in GLU_EPIS:
+        N.ensure_act(out.dtype)
+        N.kcall("mxk_swiglu_il16", y.data_ptr(), y.stride(0), out.data_ptr(), out.stride(0), M, W.N // 2,
+                int(epi == EPI_GEGLU), N.stream_ptr())
+        return out
+    return _apply_epi_dense(y, epi, out)
+
+
+def _qmatmul_t32(W: QWeight, x, epi: int, out, xq, xds, M: int, out_zeroed: bool):
+    """t32 tiled weights: qmv (q8 activations, M <= 4) or qmm (f16 activations, any M)."""
+    if M <= 4 and xq is not None:
+        if epi in (EPI_BF16, *GLU_EPIS):
+            N.ensure_act(out.dtype)
+        N.kcall("mxk_qmv", int(W.qtype), epi, xq.data_ptr(), xds.data_ptr(), W.data.data_ptr(), M, W.N, W.K,
+                out.data_ptr(), out.stride(0), N.stream_ptr())
+        return out
+    if x is None or x.dtype != torch.float16:
+        raise ValueError("qmatmul: t32 weights need f16 activations (or q8 activations with M <= 4)")
+    can_split = epi == EPI_ADD_F32 or (epi == EPI_F32 and out_zeroed)
+    if W.bf16_cache is not None and M >= dense_min_m(x.dtype, epi, can_split) and W.bf16_cache.dtype == x.dtype:
+        return _dense_cached(W, x, epi, out, M)
+    wm, wn, nw, splits = _qmm_shape(M, W.N, W.K, can_split)
+    e = EPI_ADD_F32 if (epi == EPI_F32 and splits > 1) else epi
+    if e in (EPI_BF16, *GLU_EPIS):
+        if out.dtype != x.dtype:
+            raise ValueError(f"qmatmul: {out.dtype} output with {x.dtype} activations")
+        N.ensure_act(out.dtype)
+    N.kcall("mxk_qmm", int(W.qtype), e, wm, wn, nw, x.data_ptr(), x.stride(0), W.data.data_ptr(), None,
+            M, W.N, W.K, splits, out.data_ptr(), out.stride(0), N.stream_ptr())
+    return out
+
+
 def dense_min_m(dtype, epi: int = EPI_ADD_F32, can_split: bool = True) -> int:
     """Smallest M routed to the dense weight cache (hipBLASLt). From tools/bench_qgemm.py +
     tools/tune_qgemm16.py on MI355X (Llama-3-8B shapes): the bf16 dequant-MFMA kernel loses to the
@@ -261,13 +308,38 @@ def dense_min_m(dtype, epi: int = EPI_ADD_F32, can_split: bool = True) -> int:
     return DENSE_MIN_M_SPLIT
 
 
+# From tools/tune_qmm.py on MI355X (profiles/r2_qmm_tune.jsonl): qmm on t32 weights beats the dense copy
+# below these M; above, hipBLASLt on 2 B/weight still wins for the layer projections (not the LM head,
+# which never gets a dense copy).
 DENSE_MIN_M_SWIGLU = int(os.environ.get("MX_DENSE_MIN_M_SWIGLU", "96"))
-DENSE_MIN_M_NOSPLIT = int(os.environ.get("MX_DENSE_MIN_M_NOSPLIT", "48"))
-DENSE_MIN_M_SPLIT = int(os.environ.get("MX_DENSE_MIN_M_SPLIT", "320"))
+DENSE_MIN_M_NOSPLIT = int(os.environ.get("MX_DENSE_MIN_M_NOSPLIT", "96"))
+DENSE_MIN_M_SPLIT = int(os.environ.get("MX_DENSE_MIN_M_SPLIT", "192"))
 
 
 Q32_MIN_M = int(os.environ.get("MX_Q32_MIN_M", "48"))
 Q32_FORCE: tuple | None = None  # (wm, wn, splits) override for tuning (tools/tune_qgemm32.py)
+# qmm.hip (LDS-DMA ring, counted vmcnt) runs every f16 GEMM on t32-tiled weights
+QMM_FORCE: tuple | None = None  # (wm, wn, nw, splits) override for tuning (tools/tune_qmm.py)
+
+
+def _qmm_shape(M: int, N_: int, K: int, can_split: bool):
+    """qmm tile choice -> (wm, wn, nw, splits): 32*wm-row x 32*wn*nw-column workgroup tiles with nw
+    waves (8 = two per SIMD, which overlap each other's dequant / LDS phases with MFMAs), K splits
+    (fp32 atomics, split-able outputs only) until the grid holds >= 2 workgroups per CU, keeping >= 8
+    k-tiles (512 k) per split. Fitted to the tools/tune_qmm.py sweep (Llama-3-8B shapes, M 64..2048)."""
+    if QMM_FORCE is not None:
+        wm, wn, nw, splits = QMM_FORCE
+        return wm, wn, nw, (splits if can_split else 1)
+    wm = 1 if M <= 32 else 2 if (M <= 64 or (can_split and M <= 256)) else 4
+    mt = -(-M // (32 * wm))
+    nw = 8 if wm >= 2 and (-(-N_ // 256) * mt >= 200 or (can_split and N_ >= 6144)) else 4
+    wn = 2 if -(-N_ // (64 * nw)) * mt >= 200 else 1
+    cols = -(-N_ // (32 * wn * nw))
+    splits = 1
+    if can_split:
+        while cols * mt * splits < 2 * CU_COUNT and (K // 64) // (splits * 2) >= 8:
+            splits *= 2
+    return wm, wn, nw, splits
 
 
 def _mfma32_shape(M: int, N_: int, nblk: int, can_split: bool):

@@ -398,6 +398,49 @@ def repack_for_gpu(raw: np.ndarray, qtype: int, n_rows: int, row_len: int):
     raise NotImplementedError(f"{q.name} has no native GPU layout")
 
 
+T32_UNIT = {QType.Q4_K: (4608, 256), QType.Q6_K: (6784, 256), QType.Q8_0: (2176, 64)}
+
+
+def tile32(data, dplane, qtype: int, n_rows: int, row_len: int):
+    """GPU-native layout (see csrc/kernels/qmm.hip) -> "t32" tiled layout: columns (output rows)
+    grouped 32 at a time, per (group, unit) the 32 columns' bytes stored together so every LDS-DMA /
+    load wave-instruction of the qmm / qmv kernels reads contiguous memory. Works on torch tensors
+    (the GPU copy, via reshapes/permutes) or numpy arrays. Returns uint8 [n_rows / 32, n_units * UNIT]."""
+    import torch
+    q = QType(qtype)
+    if n_rows % 32 or row_len % 256 or q not in T32_UNIT:
+        raise ValueError(f"t32 layout needs N % 32 == 0, K % 256 == 0 and Q4_K/Q6_K/Q8_0 (got {q.name} {n_rows}x{row_len})")
+    t = data if isinstance(data, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(data))
+    if t.dtype != torch.uint8:
+        t = t.contiguous().view(torch.uint8)
+    t = t.reshape(n_rows, -1)
+    G = n_rows // 32
+    if q == QType.Q4_K:
+        nb = row_len // 256
+        b = t.reshape(G, 32, nb, 144)
+        hdr = b[..., :16].permute(0, 2, 1, 3).reshape(G, nb, 512)
+        qs = b[..., 16:].reshape(G, 32, nb, 4, 2, 16).permute(0, 2, 3, 4, 1, 5).reshape(G, nb, 4096)
+        out = torch.cat([hdr, qs], 2)
+    elif q == QType.Q6_K:
+        nb = row_len // 256
+        b = t.reshape(G, 32, nb, 208)
+        ql = b[..., :128].reshape(G, 32, nb, 4, 2, 16)
+        qh = b[..., 128:192].reshape(G, 32, nb, 4, 1, 16)
+        quarters = torch.cat([ql, qh], 4).permute(0, 2, 3, 4, 1, 5).reshape(G, nb, 6144)
+        sc = b[..., 192:208].permute(0, 2, 1, 3).reshape(G, nb, 512)
+        d = dplane if isinstance(dplane, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(dplane))
+        d = d.reshape(n_rows, nb).contiguous().view(torch.uint8).reshape(G, 32, nb, 2)
+        d4 = torch.cat([d, torch.zeros_like(d)], 3).permute(0, 2, 1, 3).reshape(G, nb, 128)
+        out = torch.cat([sc, d4, quarters], 2)
+    else:
+        nt = row_len // 64
+        qs = t.reshape(G, 32, nt, 4, 16).permute(0, 2, 3, 1, 4).reshape(G, nt, 2048)
+        d = dplane if isinstance(dplane, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(dplane))
+        d = d.reshape(n_rows, nt * 2).contiguous().view(torch.uint8).reshape(G, 32, nt, 4).permute(0, 2, 1, 3)
+        out = torch.cat([d.reshape(G, nt, 128), qs], 2)
+    return out.reshape(G, -1).contiguous()
+
+
 def interleave_rows16(a: np.ndarray, b: np.ndarray) -> np.ndarray:
     """Interleave two [N, X] row matrices in 16-row groups: [a0..a15, b0..b15, a16..a31, ...].
     This is the gate/up layout the fused SwiGLU epilogue expects (N multiple of 16)."""

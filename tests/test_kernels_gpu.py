@@ -81,7 +81,7 @@ def test_qgemv(qt, M):
     n, k = 512, 4096
     raw, dense = make_w(qt, n, k, seed=M)
     W = QWeight.from_ggml(raw, qt, n, k, DEV)
-    x = torch.randn(M, k, device=DEV)
+    x = torch.randn(M, k, device=DEV).half()
     xq = torch.empty(M, k, dtype=torch.int8, device=DEV)
     xds = torch.empty(M, k // 32, 2, device=DEV)
     K.quant_q8(x.bfloat16(), xq, xds)
@@ -350,6 +350,108 @@ def test_qgemm32(qt, M, wm, wn, splits, monkeypatch):
     g = ref.reshape(M, n // 32, 2, 16)
     ref_sw = torch.nn.functional.silu(g[:, :, 0].reshape(M, -1)) * g[:, :, 1].reshape(M, -1)
     assert rel(sw, ref_sw) < 1e-2
+
+
+@pytest.mark.parametrize("qt", [QType.Q4_K, QType.Q6_K, QType.Q8_0])
+@pytest.mark.parametrize("M,wm,wn,nw,splits", [(64, 2, 1, 4, 1), (77, 4, 2, 4, 2), (128, 4, 1, 4, 1), (128, 2, 2, 4, 4),
+                                                (200, 4, 2, 4, 3), (300, 4, 1, 4, 2), (7, 1, 1, 4, 2), (33, 1, 2, 4, 1),
+                                                (100, 2, 1, 8, 2), (300, 4, 2, 8, 1), (129, 4, 1, 8, 3), (64, 2, 2, 8, 1)])
+def test_qmm(qt, M, wm, wn, nw, splits, monkeypatch):
+    """qmm.hip (LDS-DMA ring GEMM) for every epilogue and tile / split-K choice, incl. ragged M / N
+    tails and split counts that do not divide the k-tiles."""
+    from localai_tfp_amd.ops import linear as L
+    monkeypatch.setattr(L, "QMM_FORCE", (wm, wn, nw, splits))
+    n, k = 416, 2304  # 416 = 3.25 x 128 columns: partial column tiles (multiple of 32 for the GLU)
+    raw, dense = make_w(qt, n, k, seed=M + 7 * wm)
+    W = QWeight.from_ggml(raw, qt, n, k, DEV)
+    assert W.to_t32() and W.layout == "t32"
+    x = torch.randn(M, k, device=DEV).half()
+    ref = x.float().cpu() @ dense.t()
+    out = torch.empty(M, n, device=DEV)
+    qmatmul(W, x, EPI_F32, out)
+    assert rel(out, ref) < 5e-3
+    z = torch.zeros(M, n, device=DEV)
+    qmatmul(W, x, EPI_F32, z, out_zeroed=True)
+    assert rel(z, ref) < 5e-3
+    acc = torch.randn(M, n, device=DEV)
+    acc0 = acc.clone()
+    qmatmul(W, x, EPI_ADD_F32, acc)
+    assert rel(acc - acc0, ref) < 5e-3
+    ob = torch.empty(M, n, dtype=torch.float16, device=DEV)
+    qmatmul(W, x, EPI_BF16, ob)
+    assert rel(ob, ref) < 5e-3
+    sw = torch.empty(M, n // 2, dtype=torch.float16, device=DEV)
+    qmatmul(W, x, EPI_SWIGLU, sw)
+    g = ref.reshape(M, n // 32, 2, 16)
+    ref_sw = torch.nn.functional.silu(g[:, :, 0].reshape(M, -1)) * g[:, :, 1].reshape(M, -1)
+    assert rel(sw, ref_sw) < 1e-2
+
+
+@pytest.mark.parametrize("name,qt,n,k,epi", [
+    ("qkv", QType.Q4_K, 6144, 4096, EPI_F32), ("o_proj", QType.Q4_K, 4096, 4096, EPI_ADD_F32),
+    ("gate_up", QType.Q4_K, 28672, 4096, EPI_SWIGLU), ("down", QType.Q4_K, 4096, 14336, EPI_ADD_F32),
+    ("down_q6", QType.Q6_K, 4096, 14336, EPI_ADD_F32), ("v_q6", QType.Q6_K, 1024, 4096, EPI_F32)])
+@pytest.mark.parametrize("M", [7, 128, 320])
+def test_qmatmul_llama3_8b_shapes(name, qt, n, k, epi, M):
+    """Production Llama-3-8B projection shapes through the DEFAULT dispatch (qmm tiles and split-K as
+    chosen for these M) against an fp32 reference of the dequantised weight."""
+    raw, dense = make_w(qt, n, k, seed=n + k + M)
+    W = QWeight.from_ggml(raw, qt, n, k, DEV)
+    assert W.to_t32()
+    torch.manual_seed(M)
+    x = torch.randn(M, k, device=DEV).half()
+    ref = x.float().cpu() @ dense.t()
+    if epi == EPI_SWIGLU:
+        out = torch.empty(M, n // 2, dtype=torch.float16, device=DEV)
+        qmatmul(W, x, epi, out)
+        g = ref.reshape(M, n // 32, 2, 16)
+        ref = torch.nn.functional.silu(g[:, :, 0].reshape(M, -1)) * g[:, :, 1].reshape(M, -1)
+        assert rel(out, ref) < 1e-2
+        return
+    if epi == EPI_ADD_F32:
+        out = torch.randn(M, n, device=DEV)
+        base = out.clone()
+        qmatmul(W, x, epi, out)
+        assert rel(out - base, ref) < 5e-3
+        return
+    out = torch.zeros(M, n, device=DEV)
+    qmatmul(W, x, epi, out, out_zeroed=True)
+    assert rel(out, ref) < 5e-3
+
+
+@pytest.mark.parametrize("qt", [QType.Q4_K, QType.Q6_K, QType.Q8_0])
+@pytest.mark.parametrize("M", [1, 2, 3, 4])
+def test_qmv_t32(qt, M):
+    """qmv.hip decode GEMV on t32 weights (q8 activations) for every epilogue, and the t32 row
+    dequantisation (embedding gather), against fp32 references."""
+    n, k = 384, 2816
+    raw, dense = make_w(qt, n, k, seed=11 * M)
+    W = QWeight.from_ggml(raw, qt, n, k, DEV)
+    assert W.to_t32()
+    x = torch.randn(M, k, device=DEV).half()
+    xq = torch.empty(M, k, dtype=torch.int8, device=DEV)
+    xds = torch.empty(M, k // 32, 2, dtype=torch.float32, device=DEV)
+    K.quant_q8(x, xq, xds)
+    xr = (xq.float().reshape(M, k // 32, 32) * xds[:, :, :1]).reshape(M, k).cpu()  # the operand qmv sees
+    ref = xr @ dense.t()
+    out = torch.empty(M, n, device=DEV)
+    qmatmul(W, None, EPI_F32, out, xq=xq, xds=xds)
+    assert rel(out, ref) < 2e-3
+    acc = torch.randn(M, n, device=DEV)
+    acc0 = acc.clone()
+    qmatmul(W, None, EPI_ADD_F32, acc, xq=xq, xds=xds)
+    assert rel(acc - acc0, ref) < 2e-3
+    ob = torch.empty(M, n, dtype=torch.float16, device=DEV)
+    qmatmul(W, None, EPI_BF16, ob, xq=xq, xds=xds)
+    assert rel(ob, ref) < 3e-3
+    sw = torch.empty(M, n // 2, dtype=torch.float16, device=DEV)
+    qmatmul(W, None, EPI_SWIGLU, sw, xq=xq, xds=xds)
+    g = ref.reshape(M, n // 32, 2, 16)
+    ref_sw = torch.nn.functional.silu(g[:, :, 0].reshape(M, -1)) * g[:, :, 1].reshape(M, -1)
+    assert rel(sw, ref_sw) < 1e-2
+    rows = torch.tensor([0, 5, n - 1, 37], dtype=torch.int32, device=DEV)
+    deq = W.dequant_gpu(torch.float32, rows)
+    assert rel(deq, dense[rows.long().cpu()]) < 1e-5
 
 
 def test_f16_producers():

@@ -1,0 +1,49 @@
+#!/usr/bin/env python3
+"""Run one qmm configuration in a loop (for rocprofv3 --pmc passes / kernel traces).
+
+    python tools/prof_qmm.py --shape gate_up --M 2048 --cfg 4,2,8,1 --iters 20
+"""
+import argparse
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+SHAPES = {"qkv": (6144, 4096, 12, 0), "wo": (4096, 4096, 12, 2), "gate_up": (28672, 4096, 12, 3),
+          "down": (4096, 14336, 12, 2), "down_q6": (4096, 14336, 14, 2), "lm_head": (128256, 4096, 14, 0)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--shape", default="gate_up")
+    ap.add_argument("--M", type=int, default=2048)
+    ap.add_argument("--cfg", default="")
+    ap.add_argument("--iters", type=int, default=20)
+    a = ap.parse_args()
+    from localai_tfp_amd.ops import linear as L
+    from localai_tfp_amd.ops.quant import random_quantized
+    N, K, qt, epi = SHAPES[a.shape]
+    W = L.QWeight.from_ggml(random_quantized(np.random.default_rng(1), qt, N, K), qt, N, K, "cuda")
+    assert W.to_t32()
+    if a.cfg:
+        L.QMM_FORCE = tuple(int(v) for v in a.cfg.split(","))
+    x = (torch.randn(a.M, K, device="cuda") * 0.5).half()
+    out = (torch.empty(a.M, N // 2, device="cuda", dtype=torch.float16) if epi == 3
+           else torch.zeros(a.M, N, device="cuda"))
+    for _ in range(a.iters):
+        L.qmatmul(W, x, epi, out, out_zeroed=True)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(a.iters):
+        L.qmatmul(W, x, epi, out, out_zeroed=True)
+    e1.record()
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) / a.iters * 1e3
+    print(f"{a.shape} M={a.M} cfg={L._qmm_shape(a.M, N, K, epi in (0, 2))} {us:.1f} us {2*a.M*N*K/us/1e6:.0f} TF")
+
+
+if __name__ == "__main__":
+    main()
