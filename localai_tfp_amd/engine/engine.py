@@ -47,6 +47,9 @@ class EngineConfig:
     # kernels on t32-tiled weights (ops/linear.py DENSE_MIN_M_*; never for the LM head)
     prefill_bf16_cache: bool = True
     kv_dtype: str = "bf16"  # paged KV cache element type: bf16 | fp8 (OCP e4m3, half the bytes per token)
+    # overlap the host with the GPU: launch step N, then read step N-1's sampled tokens (async
+    # device->host copy) and schedule N+1 while N runs; decode inputs come from the device
+    overlap: bool = True
     n_draft: int = 0  # speculative decoding: draft tokens per step (needs a draft model; 0 = off)
     spec_max_batch: int = 32  # speculate only on decode batches up to this size (latency-bound regime)
 
@@ -142,8 +145,11 @@ class DecodeGraph:
                     self.argmax.data_ptr(), N.stream_ptr())
         self.graph = g
 
-    def run(self, tokens, positions, slots, bt, lens, n: int):
+    def run(self, tokens, positions, slots, bt, lens, n: int, fix=None):
         self.tokens[:n].copy_(tokens, non_blocking=True)
+        if fix is not None:  # decode inputs sampled by the previous (unread) step, gathered on device
+            dst, src, prev = fix
+            self.tokens.index_copy_(0, dst, prev.index_select(0, src))
         self.positions[:n].copy_(positions, non_blocking=True)
         self.slots[:n].copy_(slots, non_blocking=True)
         self.bt[:n, : bt.shape[1]].copy_(bt, non_blocking=True)
@@ -225,6 +231,19 @@ class LLMEngine:
         self.batch_sink: BatchedSink | None = None
         if c.prefill_bf16_cache and self.device.type == "cuda" and hasattr(model, "enable_prefill_bf16_cache"):
             model.enable_prefill_bf16_cache()
+        # overlap mode state: the launched-but-unread step, the device tokens it samples, and pinned
+        # host staging (ring of 3: a buffer is rewritten only after the step that used it was read)
+        self.overlap = bool(c.overlap and tp is None and not use_spec and not self.recurrent
+                            and getattr(model, "remote", None) is None)
+        self._inflight = None
+        self._prev_dev = None  # (device int32 tokens of the last launched step, {rid: row})
+        self._pin_tok = self._pin_lp = self._pin_in = None
+        self._pin_i = 0
+        if self.overlap:
+            n = max(c.max_num_seqs, 1)
+            pin = self.device.type == "cuda"
+            self._pin_tok = [torch.empty(n, dtype=torch.int32, pin_memory=pin) for _ in range(3)]
+            self._pin_lp = [torch.empty(n, dtype=torch.float32, pin_memory=pin) for _ in range(3)]
         self.spec = None
         if use_spec:
             from .speculative import SpeculativeDecoder
@@ -313,6 +332,10 @@ class LLMEngine:
             self._drain_inbox()
             self.flush_outputs()
             if not self.sched.has_work():
+                if self._inflight is not None:
+                    self._drain_inflight()
+                    self.flush_outputs()
+                    continue
                 with self._cv:
                     self._cv.wait(timeout=0.05)
                 continue
@@ -322,7 +345,9 @@ class LLMEngine:
                 self.step()
             except Exception as ex:  # fail every in-flight request loudly, keep the worker alive
                 log.exception("engine step failed")
+                self._inflight, self._prev_dev = None, None
                 for s in list(self.sched.running) + list(self.sched.waiting):
+                    s.n_pending = 0
                     self.sched.abort(s.rid)
                     self._finish(s, f"error:{type(ex).__name__}: {ex}")
             self.flush_outputs()
@@ -331,8 +356,11 @@ class LLMEngine:
         """Synchronous driver (tests / bench): step until every submitted request finished."""
         self._drain_inbox()
         n = 0
-        while self.sched.has_work() and n < max_steps:
-            self.step()
+        while (self.sched.has_work() or self._inflight is not None) and n < max_steps:
+            if self.sched.has_work():
+                self.step()
+            else:
+                self._drain_inflight()
             self._drain_inbox()
             n += 1
         return n
@@ -347,7 +375,20 @@ class LLMEngine:
             else:
                 self.stats["preemptions"] += 1
         if so.empty:
+            if self._inflight is not None:
+                self._drain_inflight()
             return
+        if self.overlap and self._overlap_ok(so):
+            return self._step_overlap(so, t0)
+        if self._inflight is not None:  # this step needs host-known tokens: read the in-flight one first
+            self._drain_inflight()
+            if any(it.seq.status == Status.FINISHED for it in so.decode + so.prefill):
+                # a sequence of this plan finished on the drained step: re-plan without it
+                self.sched.running = [x for x in self.sched.running if x.status != Status.FINISHED]
+                so = SchedulerOutput([it for it in so.decode if it.seq.status != Status.FINISHED],
+                                     [it for it in so.prefill if it.seq.status != Status.FINISHED])
+                if so.empty:
+                    return
         if self.spec is not None:
             for s in so.preempted:
                 self.spec.forget(s.rid)
@@ -372,6 +413,99 @@ class LLMEngine:
         st["decode_tokens"] += len(so.decode)
         st["prefill_tokens"] += sum(p.n for p in so.prefill)
         st["busy_s"] += dt
+
+    # ------------------------------------------------------------------ overlap mode
+    @staticmethod
+    def _simple_params(p) -> bool:
+        """Sampling that needs no host-side token history or per-token host state."""
+        return (p.mirostat != 2 and p.repeat_penalty == 1.0 and not p.presence_penalty and not p.frequency_penalty)
+
+    def _overlap_ok(self, so: SchedulerOutput) -> bool:
+        for it in so.decode:
+            if it.seq.grammar is not None or it.seq.req.embedding or not self._simple_params(it.seq.params):
+                return False
+        for it in so.prefill:
+            if it.sample and (it.seq.grammar is not None or it.seq.req.embedding or not self._simple_params(it.seq.params)):
+                return False
+        return True
+
+    def _step_overlap(self, so: SchedulerOutput, t0: float):
+        """Launch this step without waiting for it; then read the previous step's tokens (its async
+        copy has landed or lands while this step runs) and post-process them."""
+        t1 = time.perf_counter()
+        plan = self._plan(so)
+        self.stats["plan_s"] += time.perf_counter() - t1
+        items = list(so.decode) + [it for it in so.prefill if it.sample]
+        logits, am = self._execute(plan)
+        tok_dev, lp_dev = None, None
+        if items:
+            if am is not None and all(it.seq.params.greedy and not it.seq.params.logit_bias for it in items):
+                tok_dev = am
+            elif not logits.is_cuda:  # CPU reference sampler (host lists)
+                t, l = self.sampler.sample(logits, [it.seq.params for it in items], [[] for _ in items],
+                                           [it.seq.n_generated for it in items], None, None)
+                tok_dev = torch.as_tensor(t, dtype=torch.int32)
+                lp_dev = torch.as_tensor(l, dtype=torch.float32) if l is not None else None
+            else:
+                tok_dev, lp_dev = self.sampler.sample(logits, [it.seq.params for it in items], [[] for _ in items],
+                                                      [it.seq.n_generated for it in items], None, None)
+            k = self._pin_i
+            self._pin_i = (k + 1) % 3
+            S = len(items)
+            self._pin_tok[k][:S].copy_(tok_dev[:S], non_blocking=True)
+            if lp_dev is not None:
+                self._pin_lp[k][:S].copy_(lp_dev[:S], non_blocking=True)
+            ev = None
+            if self.device.type == "cuda":
+                ev = torch.cuda.Event()
+                ev.record()
+            new = (ev, k, items, lp_dev is not None)
+        else:
+            new = None
+        t2 = time.perf_counter()
+        self.sched.commit(so)
+        for it in items:
+            it.seq.n_pending += 1
+        prev, self._inflight = self._inflight, new
+        self._prev_dev = (tok_dev, {it.seq.rid: r for r, it in enumerate(items)}) if items else None
+        if prev is not None:
+            self._process_inflight(prev)
+        t3 = time.perf_counter()
+        st = self.stats
+        st["sched_s"] += t1 - t0
+        st["fwd_s"] += t2 - t1
+        st["process_s"] += t3 - t2
+        st["steps"] += 1
+        st["decode_tokens"] += len(so.decode)
+        st["prefill_tokens"] += sum(p.n for p in so.prefill)
+        st["busy_s"] += t3 - t0
+
+    def _process_inflight(self, inf):
+        ev, k, items, has_lp = inf
+        t0 = time.perf_counter()
+        if ev is not None:
+            ev.synchronize()
+        self.stats["wait_s"] += time.perf_counter() - t0
+        S = len(items)
+        toks = self._pin_tok[k][:S].tolist()
+        lps = self._pin_lp[k][:S].tolist() if has_lp else None
+        now = time.perf_counter()
+        for j, it in enumerate(items):
+            s = it.seq
+            s.n_pending -= 1
+            if s.status == Status.FINISHED:
+                continue  # finished on an earlier token (or aborted): this sample is discarded
+            if s.t_first_token is None:
+                s.t_first_token = now
+            self._accept_tokens(s, [int(toks[j])], [lps[j]] if lps is not None else None)
+        if self.sched.deferred:
+            self.sched.release_deferred()
+
+    def _drain_inflight(self):
+        inf, self._inflight = self._inflight, None
+        self._prev_dev = None
+        if inf is not None:
+            self._process_inflight(inf)
 
     def _graph_for(self, n: int) -> DecodeGraph | None:
         if not self.use_graphs:
@@ -403,10 +537,17 @@ class LLMEngine:
         positions = np.empty(T, np.int32)
         slots = np.empty(T, np.int32)
         i = 0
+        fix_dst, fix_src = [], []
+        prev_rows = self._prev_dev[1] if self._prev_dev is not None else {}
         for it in dec:
             s = it.seq
             p = s.num_computed
-            tokens[i] = s.output_ids[-1] if s.output_ids else s.prompt_ids[-1]
+            if s.n_pending:  # input token sampled by the previous, still unread step: take it on device
+                tokens[i] = 0
+                fix_dst.append(i)
+                fix_src.append(prev_rows[s.rid])
+            else:
+                tokens[i] = s.output_ids[-1] if s.output_ids else s.prompt_ids[-1]
             positions[i] = p
             slots[i] = s.blocks[p // bs] * bs + p % bs
             i += 1
@@ -428,6 +569,8 @@ class LLMEngine:
             off += it.n
         plan = {"nd": nd, "tokens": tokens, "positions": positions, "slots": slots,
                 "lidx": np.asarray(lidx, np.int32), "keep_hidden": False}
+        if fix_dst:
+            plan["fix"] = (np.asarray(fix_dst, np.int64), np.asarray(fix_src, np.int64))
         mm = []
         row = nd
         for it in pf:  # multimodal spans intersecting this chunk -> (row in T, embedding rows)
@@ -468,17 +611,43 @@ class LLMEngine:
             g = self._graph_for(nd)
             bt = plan["dec_bt"]
             maxb = bt.shape[1]
-            h = torch.from_numpy(np.concatenate([plan["tokens"], plan["positions"], plan["slots"], plan["dec_lens"],
-                                                 bt.reshape(-1)])).pin_memory()
-            d = h.to(dev, non_blocking=True)
+            flat = np.concatenate([plan["tokens"], plan["positions"], plan["slots"], plan["dec_lens"], bt.reshape(-1)])
+            d = self._stage_h2d(flat)
             logits, am = g.run(d[:nd], d[nd:2 * nd], d[2 * nd:3 * nd], d[4 * nd:].view(nd, maxb),
-                               d[3 * nd:4 * nd], nd)
+                               d[3 * nd:4 * nd], nd, fix=self._fix_tensors(plan))
             self.stats["graph_steps"] += 1
             return logits, am
         fb = self._build_fb(plan)
+        fix = self._fix_tensors(plan)
+        if fix is not None:
+            dst, src, prev = fix
+            fb.tokens.index_copy_(0, dst, prev.index_select(0, src))
         logits = self.model.forward(fb, self.kv, self.ws)
         self._hidden = self.model.last_hidden if fb.keep_hidden else None
         return logits, None
+
+    def _stage_h2d(self, flat: np.ndarray) -> torch.Tensor:
+        """int32 host array -> device, through a ring of 3 persistent pinned buffers (a buffer is
+        reused only after the step that last used it has been read back, so the async copy that
+        sourced it has completed); a fresh pinned allocation per step costs ~ms on the host."""
+        n = flat.size
+        if self._pin_in is None or self._pin_in[0].numel() < n:
+            cap = max(n, self.cfg.max_num_seqs * (4 + self.max_blocks_per_seq))
+            self._pin_in = [torch.empty(cap, dtype=torch.int32).pin_memory() for _ in range(3)]
+            self._pin_in_i = 0
+        k = self._pin_in_i
+        self._pin_in_i = (k + 1) % 3
+        hb = self._pin_in[k][:n]
+        hb.numpy()[:] = flat
+        return hb.to(self.device, non_blocking=True)
+
+    def _fix_tensors(self, plan):
+        if "fix" not in plan:
+            return None
+        dst, src = plan["fix"]
+        dev = self.device
+        return (torch.from_numpy(dst).to(dev, non_blocking=True), torch.from_numpy(src).to(dev, non_blocking=True),
+                self._prev_dev[0])
 
     def _forward_and_sample(self, so: SchedulerOutput):
         t0 = time.perf_counter()
@@ -605,7 +774,7 @@ class LLMEngine:
                 s._pending_ids.pop() if s._pending_ids else None
             elif len(s.output_ids) >= s.req.max_tokens:
                 reason = "length"
-            elif s.total_len >= self.cfg.max_model_len:
+            elif s.known_len >= self.cfg.max_model_len:
                 reason = "length"
             elif s.grammar is not None and s.grammar.is_done():
                 reason = "stop"

@@ -52,6 +52,9 @@ class Scheduler:
         self.prefill_chunk = prefill_chunk or max_batched_tokens
         self.waiting: collections.deque[Sequence] = collections.deque()
         self.running: list[Sequence] = []
+        # finished sequences whose blocks a launched-but-unread step still writes (overlap mode):
+        # released by release_deferred() once that step's results were processed
+        self.deferred: list[Sequence] = []
 
     # ---------------------------------------------------------------- queue management
     def add(self, seq: Sequence):
@@ -65,7 +68,10 @@ class Scheduler:
             for s in list(q):
                 if s.rid == rid:
                     q.remove(s)
-                    self.free(s)
+                    if s.n_pending:
+                        self.deferred.append(s)  # blocks still written by a launched step
+                    else:
+                        self.free(s)
                     return s
         return None
 
@@ -86,7 +92,16 @@ class Scheduler:
         seq.blocks.extend(self.bm.allocate(need))
         return True
 
+    def _held(self, s: Sequence) -> bool:
+        """A sequence whose in-flight samples already reach its length limits: its last step is on
+        the GPU, nothing more to schedule (overlap mode; never true when n_pending == 0)."""
+        return s.n_pending > 0 and (s.n_generated >= s.req.max_tokens or s.total_len >= self.max_model_len)
+
     def _preempt(self, seq: Sequence, out: SchedulerOutput):
+        if seq.n_pending:
+            # its in-flight token is not known yet: re-prefill would need it. Overlap mode keeps
+            # such sequences (victim selection skips them; see schedule())
+            raise RuntimeError("preempting a sequence with in-flight tokens")
         self.running.remove(seq)
         self.free(seq)
         seq.num_computed = 0
@@ -100,12 +115,12 @@ class Scheduler:
         out = SchedulerOutput()
         budget = self.max_batched_tokens
         # 1. decode phase sequences
-        decoding = [s for s in self.running if s.in_decode]
+        decoding = [s for s in self.running if s.in_decode and not self._held(s)]
         for s in list(decoding):
             if s not in self.running:
                 continue
             while not self._grow(s, s.total_len):
-                victim = next((v for v in reversed(self.running) if v is not s), None)
+                victim = next((v for v in reversed(self.running) if v is not s and not v.n_pending), None)
                 if victim is None:
                     break
                 self._preempt(victim, out)
@@ -114,8 +129,10 @@ class Scheduler:
             if s not in self.running:
                 continue
             if self._blocks_for(s.total_len) > len(s.blocks):
-                # could not grow even after preemption: preempt itself
-                self._preempt(s, out)
+                # could not grow even after preemption: preempt itself (or, with a token in flight,
+                # sit this step out)
+                if not s.n_pending:
+                    self._preempt(s, out)
                 decoding.remove(s)
                 continue
         for s in decoding:
@@ -129,7 +146,7 @@ class Scheduler:
             if n <= 0 or not self._grow(s, s.num_computed + n):
                 continue
             done = s.num_computed + n >= s.prefill_target
-            out.prefill.append(ScheduledSeq(s, s.num_computed, n, done and not s.output_ids))
+            out.prefill.append(ScheduledSeq(s, s.num_computed, n, done and not s.output_ids and not s.n_pending))
             budget -= n
         # 3. admit new sequences
         while self.waiting and budget > 0 and len(self.running) < self.max_num_seqs:
@@ -170,7 +187,8 @@ class Scheduler:
             if not s.req.cache_prompt:  # e.g. image placeholders: token ids do not identify the KV
                 continue
             ids = None
-            nfull = s.num_computed // self.bs
+            # only blocks whose token ids are all known on the host can be hashed
+            nfull = min(s.num_computed, s.known_len) // self.bs
             while len(s.block_hashes) < nfull:
                 i = len(s.block_hashes)
                 if ids is None:
@@ -185,4 +203,17 @@ class Scheduler:
         seq.t_finish = time.perf_counter()
         if seq in self.running:
             self.running.remove(seq)
-        self.free(seq)
+        if seq.n_pending:
+            self.deferred.append(seq)  # a launched step still writes its KV blocks
+        else:
+            self.free(seq)
+
+    def release_deferred(self):
+        """Free the blocks of finished sequences whose in-flight steps have all been read."""
+        keep = []
+        for s in self.deferred:
+            if s.n_pending:
+                keep.append(s)
+            else:
+                self.free(s)
+        self.deferred = keep

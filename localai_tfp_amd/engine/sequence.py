@@ -61,6 +61,10 @@ class Sequence:
         self.params = req.params
         self.prompt_ids = list(req.prompt_ids)
         self.output_ids: list[int] = []
+        # tokens sampled on the GPU by launched steps whose results the host has not read yet
+        # (engine overlap mode): they count towards the sequence length / KV position but their ids
+        # are only known after the step's async device->host copy lands (engine._process_inflight)
+        self.n_pending = 0
         self.logprobs: list[float] = []
         self.status = Status.WAITING
         self.blocks: list[int] = []
@@ -90,17 +94,26 @@ class Sequence:
 
     @property
     def total_len(self) -> int:
+        return len(self.prompt_ids) + len(self.output_ids) + self.n_pending
+
+    @property
+    def known_len(self) -> int:
+        """Tokens whose ids are on the host (excludes in-flight samples)."""
         return len(self.prompt_ids) + len(self.output_ids)
 
     @property
     def prefill_target(self) -> int:
         """KV length to reach before decoding: the whole prompt (its last row yields the first
         token's logits), or all but the newest token when resuming after a preemption."""
-        return self.total_len - 1 if self.output_ids else self.total_len
+        return self.total_len - 1 if (self.output_ids or self.n_pending) else self.total_len
 
     @property
     def in_decode(self) -> bool:
-        return bool(self.output_ids) and self.num_computed == self.total_len - 1
+        return bool(self.output_ids or self.n_pending) and self.num_computed == self.total_len - 1
+
+    @property
+    def n_generated(self) -> int:
+        return len(self.output_ids) + self.n_pending
 
     def remaining_prefill(self) -> int:
         return self.prefill_target - self.num_computed

@@ -129,3 +129,74 @@ def test_block_manager_prefix_and_eviction():
     assert len(set(got)) == 8 and 0 not in got
     with pytest.raises(MemoryError):
         bm.allocate(1)
+
+
+def _run_all(e, reqs):
+    hs = [e.submit(r) for r in reqs]
+    e.run_until_done()
+    out = []
+    for h in hs:
+        ids, text, last = [], "", None
+        while not h.q.empty():
+            o = h.q.get_nowait()
+            ids += o.token_ids
+            text += o.text
+            last = o
+        out.append((ids, text, last.finish_reason if last else None, last.completion_tokens if last else None))
+    return out
+
+
+def _mixed_requests(seed=0):
+    rng = np.random.default_rng(seed)
+    reqs = []
+    for i in range(10):
+        p = [int(x) for x in rng.integers(1, 250, size=int(rng.integers(5, 90)))]
+        kw = {}
+        if i % 3 == 1:
+            sp = SamplingParams(temperature=0.8, top_k=40, top_p=0.9, seed=100 + i)
+        elif i % 3 == 2:
+            sp = SamplingParams(temperature=0.0, logit_bias={7: 3.0})
+        else:
+            sp = SamplingParams(temperature=0.0)
+        if i == 4:
+            kw["stop"] = ["a"]
+        if i == 5:
+            kw["stop_token_ids"] = [p[-1]]
+        reqs.append(Request(p, sp, max_tokens=int(rng.integers(1, 24)), **kw))
+    return reqs
+
+
+@pytest.mark.parametrize("max_tokens_budget", [64, 16])
+def test_overlap_mode_matches_sync(model, max_tokens_budget):
+    """Overlap mode (step N launched before step N-1's tokens are read; decode inputs gathered on the
+    device) must produce exactly the synchronous engine's outputs, incl. length / stop-string /
+    stop-token finishes, seeded sampling, logit bias, chunked prefill and preemption (small cache)."""
+    for kw in ({}, dict(num_blocks=24)):
+        e_sync, _ = mk(model, overlap=False, max_batched_tokens=max_tokens_budget, **kw)
+        e_ovl, _ = mk(model, overlap=True, max_batched_tokens=max_tokens_budget, **kw)
+        assert e_ovl.overlap and not e_sync.overlap
+        a = _run_all(e_sync, _mixed_requests())
+        b = _run_all(e_ovl, _mixed_requests())
+        assert a == b
+        # every block returned once everything finished
+        assert e_ovl.bm.num_free == e_sync.bm.num_free
+        assert not e_ovl.sched.deferred and e_ovl._inflight is None
+
+
+def test_overlap_abort_mid_flight(model):
+    e, tok = mk(model, overlap=True)
+    free0 = e.bm.num_free
+    r1 = Request(list(range(20, 60)), SamplingParams(temperature=0.0), max_tokens=40)
+    r2 = Request(list(range(70, 90)), SamplingParams(temperature=0.0), max_tokens=8)
+    h1, h2 = e.submit(r1), e.submit(r2)
+    e._drain_inbox()
+    for _ in range(6):
+        e.step()
+    e.abort(r1.rid)
+    e.run_until_done()
+    outs1 = []
+    while not h1.q.empty():
+        outs1.append(h1.q.get_nowait())
+    assert outs1[-1].finished and outs1[-1].finish_reason == "abort"
+    assert e.bm.num_free == free0 or e.cfg.enable_prefix_cache  # cached blocks may stay resident
+    assert not e.sched.deferred and e._inflight is None
