@@ -124,13 +124,16 @@ __global__ __launch_bounds__(64 * QMV_WAVES) void qmv_kernel(const int8_t* __res
     const int r = lane & 31, h = lane >> 5;
     const int g = blockIdx.x;
     const int nunit = K / U::ELEMS;
+    // K split over gridDim.y workgroups (fp32 atomic accumulate epilogue)
+    const int per = (nunit + gridDim.y - 1) / gridDim.y;
+    const int u0 = blockIdx.y * per, u1 = min(nunit, u0 + per);
     const uint8_t* wg = W + (size_t)g * nunit * U::BYTES;
     float acc[MM];
 #pragma unroll
     for (int m = 0; m < MM; ++m) acc[m] = 0.f;
     // two units in flight per wave: both loads issue before either dot product
-    int u = wave;
-    for (; u + QMV_WAVES < nunit; u += 2 * QMV_WAVES) {
+    int u = u0 + wave;
+    for (; u + QMV_WAVES < u1; u += 2 * QMV_WAVES) {
         U a, b;
         a.load(wg + (size_t)u * U::BYTES, r, h);
         b.load(wg + (size_t)(u + QMV_WAVES) * U::BYTES, r, h);
@@ -144,7 +147,7 @@ __global__ __launch_bounds__(64 * QMV_WAVES) void qmv_kernel(const int8_t* __res
             }
         }
     }
-    if (u < nunit) {
+    if (u < u1) {
         U a;
         a.load(wg + (size_t)u * U::BYTES, r, h);
 #pragma unroll
@@ -174,6 +177,7 @@ __global__ __launch_bounds__(64 * QMV_WAVES) void qmv_kernel(const int8_t* __res
         } else if (h == 0) {
             if constexpr (EPI == E16_F32) ((float*)Cv)[(size_t)m * ldc + n] = v;
             else if constexpr (EPI == E16_ACT) ((uint16_t*)Cv)[(size_t)m * ldc + n] = f32_to_act<F16>(v);
+            else if (gridDim.y > 1) atomicAdd(((float*)Cv) + (size_t)m * ldc + n, v);
             else ((float*)Cv)[(size_t)m * ldc + n] += v;
         }
     }
@@ -237,22 +241,23 @@ __global__ __launch_bounds__(256) void dequant_t32_kernel(const uint8_t* __restr
 }
 
 template <int QT, int MM, int EPI>
-static int launch_qmv(const int8_t* xq, const float2* xds, const uint8_t* W, int M, int N, int K, void* C, int ldc,
-                      hipStream_t st) {
-    MX_ACT_DISPATCH(qmv_kernel<QT, MM, EPI, F16><<<N / 32, 64 * QMV_WAVES, 0, st>>>(xq, xds, W, M, N, K, C, ldc));
+static int launch_qmv(const int8_t* xq, const float2* xds, const uint8_t* W, int M, int N, int K, int ks, void* C,
+                      int ldc, hipStream_t st) {
+    MX_ACT_DISPATCH(qmv_kernel<QT, MM, EPI, F16><<<dim3(N / 32, ks), 64 * QMV_WAVES, 0, st>>>(xq, xds, W, M, N, K, C, ldc));
     MXK_CHECK_LAUNCH();
 }
 
 // X as q8 (int8 [M][K] + float2 [M][K/32]); W t32-tiled; M <= 4; N % 32 == 0; K % 256 == 0.
 // epi: 0 fp32 store, 1 act16 store, 2 fp32 accumulate, 3/4 SwiGLU/GeGLU (act16 [M, N/2]).
+// ks > 1 splits K over workgroups and needs epi 2 (fp32 atomics).
 extern "C" int mxk_qmv(int qtype, int epi, const int8_t* xq, const float2* xds, const uint8_t* W, int M, int N,
-                       int K, void* C, int ldc, hipStream_t st) {
+                       int K, int ks, void* C, int ldc, hipStream_t st) {
     if (M <= 0) return 0;
-    if (M > 4 || K % 256 || N % 32) return (int)hipErrorInvalidValue;
-#define QMV_M(QT_, EPI_)                                                            \
-    if (M == 1) return launch_qmv<QT_, 1, EPI_>(xq, xds, W, M, N, K, C, ldc, st);   \
-    if (M == 2) return launch_qmv<QT_, 2, EPI_>(xq, xds, W, M, N, K, C, ldc, st);   \
-    return launch_qmv<QT_, 4, EPI_>(xq, xds, W, M, N, K, C, ldc, st);
+    if (M > 4 || K % 256 || N % 32 || ks < 1 || (ks > 1 && epi != E16_ADD_F32)) return (int)hipErrorInvalidValue;
+#define QMV_M(QT_, EPI_)                                                                \
+    if (M == 1) return launch_qmv<QT_, 1, EPI_>(xq, xds, W, M, N, K, ks, C, ldc, st);   \
+    if (M == 2) return launch_qmv<QT_, 2, EPI_>(xq, xds, W, M, N, K, ks, C, ldc, st);   \
+    return launch_qmv<QT_, 4, EPI_>(xq, xds, W, M, N, K, ks, C, ldc, st);
 #define QMV_EPI(QT_)                                    \
     switch (epi) {                                      \
         case E16_F32: { QMV_M(QT_, E16_F32) }           \

@@ -117,6 +117,16 @@ class Workspace:
         self.part_ml = torch.empty((max_seqs * nh * max_parts, 2), dtype=torch.float32, device=dev)
         self.part_o = torch.empty((max_seqs * nh * max_parts, cfg.head_dim), dtype=torch.float32, device=dev)
 
+    def decode_part_size(self, B: int, Hq: int, max_len: int) -> int:
+        """Split-K partition length of the paged decode attention: small batches split the context
+        finer so the grid still covers the CUs (B x Hkv x parts workgroups), within the partial-
+        result workspace (rows = B * Hq * parts)."""
+        cap = self.part_ml.shape[0]
+        for part in ((64, 128, 256) if B < 8 else (128, 256) if B < 32 else (256,)):
+            if B * Hq * max(1, -(-max_len // part)) <= cap:
+                return part
+        return 256
+
     def q8(self, M: int, K_: int):
         return self.xq[: M * K_].view(M, K_), self.xds[: M * K_ // 16].view(M, K_ // 32, 2)
 
@@ -375,7 +385,7 @@ class LlamaModel:
             for w in L.qkv_parts:
                 sl = qkv[:, off:off + w.N] if len(L.qkv_parts) > 1 else qkv
                 if gemv:
-                    qmatmul(w, None, EPI_F32, sl, xq=xq, xds=xds)
+                    qmatmul(w, None, EPI_F32, sl, xq=xq, xds=xds, out_zeroed=qkv.is_cuda)
                 else:
                     qmatmul(w, xb, EPI_F32, sl, out_zeroed=True)
                 off += w.N
@@ -388,7 +398,8 @@ class LlamaModel:
             if nd:
                 K.attn_decode(q[:nd].view(nd, Hq, D), kc, vc, fb.dec_block_tables, fb.dec_seq_lens, self.scale,
                               attn[:nd].view(nd, Hq, D), max_seq_len=fb.dec_max_len or None,
-                              workspace=(ws.part_ml, ws.part_o), window=L.window, softcap=cfg.attn_softcap)
+                              workspace=(ws.part_ml, ws.part_o), window=L.window, softcap=cfg.attn_softcap,
+                              part_size=ws.decode_part_size(nd, Hq, fb.dec_max_len or cfg.ctx_train))
             if T > nd:
                 K.attn_prefill(q[nd:].view(T - nd, Hq, D), kc, vc, fb.pf_block_tables, fb.pf_cu_q, fb.pf_ctx_lens,
                                self.scale, attn[nd:].view(T - nd, Hq, D), fb.pf_q_lens_host, fb.pf_ctx_lens_host,

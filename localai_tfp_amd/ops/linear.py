@@ -272,8 +272,14 @@ def _qmatmul_t32(W: QWeight, x, epi: int, out, xq, xds, M: int, out_zeroed: bool
     if M <= 4 and xq is not None:
         if epi in (EPI_BF16, *GLU_EPIS):
             N.ensure_act(out.dtype)
-        N.kcall("mxk_qmv", int(W.qtype), epi, xq.data_ptr(), xds.data_ptr(), W.data.data_ptr(), M, W.N, W.K,
-                out.data_ptr(), out.stride(0), N.stream_ptr())
+        ks = 1
+        if epi == EPI_ADD_F32 or (epi == EPI_F32 and out_zeroed):
+            # narrow outputs (o_proj / down / qkv: N/32 groups < CUs): split K over workgroups, fp32 atomics
+            units = W.K // (64 if int(W.qtype) == int(QType.Q8_0) else 256)
+            while (W.N // 32) * ks < 2 * CU_COUNT and units // (ks * 2) >= 2:
+                ks *= 2
+        N.kcall("mxk_qmv", int(W.qtype), EPI_ADD_F32 if ks > 1 else epi, xq.data_ptr(), xds.data_ptr(),
+                W.data.data_ptr(), M, W.N, W.K, ks, out.data_ptr(), out.stride(0), N.stream_ptr())
         return out
     if x is None or x.dtype != torch.float16:
         raise ValueError("qmatmul: t32 weights need f16 activations (or q8 activations with M <= 4)")

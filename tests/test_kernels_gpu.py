@@ -92,8 +92,11 @@ def test_qgemv(qt, M):
     assert rel(out, ref) < 2e-3
     acc = torch.randn(M, n, device=DEV)
     acc0 = acc.clone()
-    qmatmul(W, None, EPI_ADD_F32, acc, xq=xq, xds=xds)
+    qmatmul(W, None, EPI_ADD_F32, acc, xq=xq, xds=xds)  # split-K over workgroups (atomics)
     assert rel(acc - acc0, ref) < 2e-3
+    z = torch.zeros(M, n, device=DEV)
+    qmatmul(W, None, EPI_F32, z, xq=xq, xds=xds, out_zeroed=True)
+    assert rel(z, ref) < 2e-3
     sw = torch.empty(M, n // 2, dtype=torch.bfloat16, device=DEV)
     qmatmul(W, None, EPI_SWIGLU, sw, xq=xq, xds=xds)
     g = ref.reshape(M, n // 32, 2, 16)
@@ -192,7 +195,7 @@ def test_attn_decode(Hq, Hkv, D, lens):
     scale = 1 / math.sqrt(D)
     ref = torch.empty(B, Hq, D)
     K.attn_decode(q, kc, vc, bt, seq, scale, ref)
-    for part in (512, 128):
+    for part in (512, 128, 64):
         out = torch.empty(B, Hq, D, dtype=torch.bfloat16, device=DEV)
         K.attn_decode(q.to(DEV), kc.to(DEV), vc.to(DEV), bt.to(DEV), seq.to(DEV), scale, out, part_size=part)
         assert rel(out, ref) < 1e-2, part
@@ -439,8 +442,11 @@ def test_qmv_t32(qt, M):
     assert rel(out, ref) < 2e-3
     acc = torch.randn(M, n, device=DEV)
     acc0 = acc.clone()
-    qmatmul(W, None, EPI_ADD_F32, acc, xq=xq, xds=xds)
+    qmatmul(W, None, EPI_ADD_F32, acc, xq=xq, xds=xds)  # split-K over workgroups (atomics)
     assert rel(acc - acc0, ref) < 2e-3
+    z = torch.zeros(M, n, device=DEV)
+    qmatmul(W, None, EPI_F32, z, xq=xq, xds=xds, out_zeroed=True)
+    assert rel(z, ref) < 2e-3
     ob = torch.empty(M, n, dtype=torch.float16, device=DEV)
     qmatmul(W, None, EPI_BF16, ob, xq=xq, xds=xds)
     assert rel(ob, ref) < 3e-3
