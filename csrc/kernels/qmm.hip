@@ -86,7 +86,9 @@ MX_DEV int qmm_a_off(int r, int c) { return r * 128 + ((c ^ ((r >> 1) & 7)) << 4
 
 template <int N_>
 MX_DEV void qmm_wait_barrier() {
-    asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(N_) : "memory");
+    // LDS reads are NOT drained here: every read of the slot about to be refilled has been consumed by
+    // its wave before that wave reaches the barrier, and the compiler counts the in-flight ones itself
+    asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N_) : "memory");
 }
 // wait until at most `ahead` stages (NI LDS-DMA instructions each) are still in flight, then barrier
 template <int NI, int A_>
@@ -108,11 +110,14 @@ struct QmmB;
 template <>
 struct QmmB<MXQ_Q4_K> {
     u32x2 v0, v1;
+    u32x4 hd;
     f16x2 s2[2], m2[2];
-    MX_DEV void load(const char* q, const char* m, const char*, int r, int h, int jq) {
-        const u32x4 hd = *(const u32x4*)(m + r * 16);
+    MX_DEV void load(const char* q, const char* m, const char*, int r, int h, int) {
+        hd = *(const u32x4*)(m + r * 16);
         v0 = *(const u32x2*)(q + r * 16 + 8 * h);
         v1 = *(const u32x2*)(q + (32 + r) * 16 + 8 * h);
+    }
+    MX_DEV void prep(int jq) {
         const float d = half_to_f32(hd[0] & 0xFFFF), dm = half_to_f32(hd[0] >> 16);
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
@@ -146,13 +151,17 @@ struct QmmB<MXQ_Q4_K> {
 template <>
 struct QmmB<MXQ_Q6_K> {
     u32x2 v0, v1, vh;
+    uint32_t sc, dw;
     f16x2 s2[4];
     MX_DEV void load(const char* q, const char* m, const char* d, int r, int h, int jq) {
         v0 = *(const u32x2*)(q + r * 16 + 8 * h);
         v1 = *(const u32x2*)(q + (32 + r) * 16 + 8 * h);
         vh = *(const u32x2*)(q + (64 + r) * 16 + 8 * h);
-        const uint32_t sc = *(const uint32_t*)(m + r * 16 + 4 * jq);
-        const float df = half_to_f32(*(const uint32_t*)(d + r * 4) & 0xFFFF);
+        sc = *(const uint32_t*)(m + r * 16 + 4 * jq);
+        dw = *(const uint32_t*)(d + r * 4);
+    }
+    MX_DEV void prep(int) {
+        const float df = half_to_f32(dw & 0xFFFF);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const _Float16 s = (_Float16)(df * (float)(int8_t)((sc >> (8 * i)) & 0xFF));
@@ -183,11 +192,15 @@ struct QmmB<MXQ_Q6_K> {
 template <>
 struct QmmB<MXQ_Q8_0> {
     u32x2 qv[4];
+    uint32_t dw;
     f16x2 s2[2];
     MX_DEV void load(const char* q, const char*, const char* d, int r, int h, int) {
 #pragma unroll
         for (int s = 0; s < 4; ++s) qv[s] = *(const u32x2*)(q + (s * 32 + r) * 16 + 8 * h);
-        const f16x2 dd = __builtin_bit_cast(f16x2, *(const uint32_t*)(d + 4 * r));
+        dw = *(const uint32_t*)(d + 4 * r);
+    }
+    MX_DEV void prep(int) {
+        const f16x2 dd = __builtin_bit_cast(f16x2, dw);
         s2[0] = (f16x2){dd[0], dd[0]};
         s2[1] = (f16x2){dd[1], dd[1]};
     }
@@ -211,11 +224,17 @@ struct QmmB<MXQ_Q8_0> {
 
 }  // namespace
 
-template <int QT, int WM, int WN, int NW, int EPI>
-__global__ __launch_bounds__(64 * NW) void qmm_kernel(const uint16_t* __restrict__ A, int lda, const uint8_t* __restrict__ W,
-                                                  const uint16_t* __restrict__ WD, int M, int N, int K, int n_ct,
-                                                  int n_mt, int splits, int kt_per_split, void* __restrict__ Cv,
-                                                  int ldc) {
+// KS waves share each of the NW column groups and split every k-tile's four k-steps between them
+// (wave kh runs k-steps kh, kh+KS, ...; fp32 partials summed through LDS before the epilogue): at small M
+// a workgroup of 4 waves leaves one wave per SIMD, whose dequant VALU, LDS-read latency and MFMAs then
+// serialise (measured: loads alone took half the kernel time); KS = 2 puts two waves on every SIMD
+// without dequantising any weight twice.
+template <int QT, int WM, int WN, int NW, int KS, int EPI>
+// The ring takes the whole LDS, so a CU holds one workgroup: tell the scheduler that NW*KS/4 waves per SIMD
+// is the occupancy (it otherwise sinks the LDS reads next to their MFMAs to save registers nobody can use).
+__global__ __launch_bounds__(64 * NW * KS) __attribute__((amdgpu_waves_per_eu(NW * KS / 4, NW * KS / 4))) void
+qmm_kernel(const uint16_t* __restrict__ A, int lda, const uint8_t* __restrict__ W, const uint16_t* __restrict__ WD,
+           int M, int N, int K, int n_ct, int n_mt, int splits, int kt_per_split, void* __restrict__ Cv, int ldc) {
     using G = QmmGeom<QT, WN>;
     using F = QmmFmt<QT>;
     constexpr int BM = 32 * WM, COLS = G::COLS;
@@ -223,15 +242,17 @@ __global__ __launch_bounds__(64 * NW) void qmm_kernel(const uint16_t* __restrict
     constexpr int STAGE = A_BYTES + NW * G::WBYTES;
     constexpr int NS = QmmRing<QT, WM, WN, NW>::STAGES;
     static_assert(STAGE == QmmRing<QT, WM, WN, NW>::STAGE && NS >= 3, "ring");
-    constexpr int WA = BM / 8 / NW;  // A-tile LDS-DMA instructions per wave (8 rows x 128 B each)
-    static_assert(WA >= 1 && WA * 8 * NW == BM, "A tile split");
-    constexpr int NI = WA + G::NI;  // LDS-DMA wave-instructions per stage per wave
-    static_assert((NS - 2) * NI <= 63, "vmcnt range");
+    constexpr int NT = NW * KS;       // waves
+    constexpr int WA = BM / 8 / NT;   // A-tile LDS-DMA instructions per wave (8 rows x 128 B each)
+    static_assert(WA >= 1 && WA * 8 * NT == BM, "A tile split");
+    static_assert(KS == 1 || KS == 2, "k-step split");
+    static_assert((NS - 2) * (WA + G::NI) <= 63, "vmcnt range");
     static_assert(WN <= 2, "one d / meta instruction covers at most 2 groups");
     extern __shared__ __attribute__((aligned(16))) char smem[];
 
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int h = lane >> 5, col = lane & 31;
+    const int cg = wave % NW, kh = wave / NW;  // column group, k-step phase
 
     // XCD-aware bijective remap of the 1-D grid: consecutive logical ids share an XCD
     const int nwg = gridDim.x, bid = blockIdx.x;
@@ -244,7 +265,7 @@ __global__ __launch_bounds__(64 * NW) void qmm_kernel(const uint16_t* __restrict
     (void)n_ct;
 
     const int m_base = mt * BM;
-    const int n_wave = ct * NW * COLS + wave * COLS;
+    const int n_wave = ct * NW * COLS + cg * COLS;
     const int nkt = K / QMM_KT;
     const int kt0 = split * kt_per_split;
     const int kt1 = min(kt0 + kt_per_split, nkt);
@@ -277,28 +298,31 @@ __global__ __launch_bounds__(64 * NW) void qmm_kernel(const uint16_t* __restrict
     const uint8_t* dsrc = W + (size_t)mg * gstride + F::DOFF + (lane & 31) * 4;
     const bool mact = lane < 32 * WN;
 
-    auto issue = [&](int kt, int slot) {
+    // every wave streams its share of the A rows; the kh == 0 wave of a column group its weight bytes
+    auto issue = [&](int kt, int slot, auto wl_c) {
         char* sb = smem + slot * STAGE;
         const uint16_t* ak = A + (size_t)kt * QMM_KT;
 #pragma unroll
         for (int i = 0; i < WA; ++i)
             __builtin_amdgcn_global_load_lds((const void*)(ak + aoff[i]),
                                              (MX_LDS void*)(sb + (wave * WA + i) * 1024), 16, 0, 0);
-        char* wb = sb + A_BYTES + wave * G::WBYTES;
-        const size_t unit = (size_t)(kt / F::PER_UNIT) * F::UNIT;
-        const int jq = kt % F::PER_UNIT;
+        if constexpr (decltype(wl_c)::value) {
+            char* wb = sb + A_BYTES + cg * G::WBYTES;
+            const size_t unit = (size_t)(kt / F::PER_UNIT) * F::UNIT;
+            const int jq = kt % F::PER_UNIT;
 #pragma unroll
-        for (int ci = 0; ci < G::QI; ++ci)
-            if (qact[ci])
-                __builtin_amdgcn_global_load_lds((const void*)(qsrc[ci] + unit + jq * F::QSTRIDE),
-                                                 (MX_LDS void*)(wb + G::Q_OFF + ci * 1024), 16, 0, 0);
-        if constexpr (G::MI > 0) {
-            if (mact)
-                __builtin_amdgcn_global_load_lds((const void*)(msrc + unit), (MX_LDS void*)(wb + G::M_OFF), 16, 0, 0);
-        }
-        if constexpr (G::DI > 0) {
-            if (mact)
-                __builtin_amdgcn_global_load_lds((const void*)(dsrc + unit), (MX_LDS void*)(wb + G::D_OFF), 4, 0, 0);
+            for (int ci = 0; ci < G::QI; ++ci)
+                if (qact[ci])
+                    __builtin_amdgcn_global_load_lds((const void*)(qsrc[ci] + unit + jq * F::QSTRIDE),
+                                                     (MX_LDS void*)(wb + G::Q_OFF + ci * 1024), 16, 0, 0);
+            if constexpr (G::MI > 0) {
+                if (mact)
+                    __builtin_amdgcn_global_load_lds((const void*)(msrc + unit), (MX_LDS void*)(wb + G::M_OFF), 16, 0, 0);
+            }
+            if constexpr (G::DI > 0) {
+                if (mact)
+                    __builtin_amdgcn_global_load_lds((const void*)(dsrc + unit), (MX_LDS void*)(wb + G::D_OFF), 4, 0, 0);
+            }
         }
     };
 
@@ -310,40 +334,104 @@ __global__ __launch_bounds__(64 * NW) void qmm_kernel(const uint16_t* __restrict
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][t][r] = 0.f;
 
-    // prologue: NSTAGE-1 tiles in flight
+    // Register-level software pipeline, one k-step deep: the A fragments of the wave's next k-step
+    // (across the tile boundary too: tile kt+1 is waited for at the top of tile kt) are read while the
+    // MFMAs of the current one run, and the raw weight bytes of tile kt+1 while tile kt computes. The
+    // scale prep (VALU) of a tile runs at the start of its compute, when its raw bytes have landed.
+    f16x8 ar[2][WM];
+    QmmB<QT> bw[WN], bn[WN];
+    auto load_a = [&](const char* sb, int s, f16x8 (&dst)[WM]) {
 #pragma unroll
-    for (int s = 0; s < NS - 1; ++s)
-        if (kt0 + s < kt1) issue(kt0 + s, s);
-
-    int slot = 0;
-    for (int kt = kt0; kt < kt1; ++kt) {
-        // stages issued after kt so far: min(kt1 - 1, kt + NSTAGE - 2) - kt
-        const int ahead = min(kt1 - 1, kt + NS - 2) - kt;
-        qmm_wait_ahead<NI, NS - 2>(ahead);
-        if (kt + NS - 1 < kt1) {
-            int ns = slot + NS - 1;
-            if (ns >= NS) ns -= NS;
-            issue(kt + NS - 1, ns);
-        }
-        const char* sb = smem + slot * STAGE;
-        const char* wl = sb + A_BYTES + wave * G::WBYTES;
-        const int jq = kt & 3;
-        QmmB<QT> bw[WN];
+        for (int i = 0; i < WM; ++i) dst[i] = *(const f16x8*)(sb + qmm_a_off(i * 32 + col, 2 * s + h));
+    };
+    auto load_b = [&](const char* sb, QmmB<QT> (&dst)[WN], int jq) {
+        const char* wl = sb + A_BYTES + cg * G::WBYTES;
 #pragma unroll
         for (int t = 0; t < WN; ++t)
-            bw[t].load(wl + G::Q_OFF + t * F::QB, wl + G::M_OFF + t * 512, wl + G::D_OFF + t * 128, col, h, jq);
-#define QMM_KSTEP(S)                                                                                       \
+            dst[t].load(wl + G::Q_OFF + t * F::QB, wl + G::M_OFF + t * 512, wl + G::D_OFF + t * 128, col, h, jq);
+    };
+
+    auto mainloop = [&](auto kh_c) {
+        constexpr int KH = decltype(kh_c)::value;
+        constexpr bool WLOAD = KH == 0;
+        constexpr int NI = WA + (WLOAD ? G::NI : 0);  // LDS-DMA wave-instructions per stage of this wave
+        using WLc = std::integral_constant<bool, WLOAD>;
+        // prologue: NSTAGE-1 tiles in flight; wait for the first
+#pragma unroll
+        for (int s = 0; s < NS - 1; ++s)
+            if (kt0 + s < kt1) issue(kt0 + s, s, WLc{});
+        qmm_wait_ahead<NI, NS - 2>(min(kt1 - 1, kt0 + NS - 2) - kt0);
+        load_b(smem, bw, kt0 & 3);
+        load_a(smem, KH, ar[0]);
+
+        int slot = 0;
+        for (int kt = kt0; kt < kt1; ++kt) {
+            int nslot = slot + 1;
+            if (nslot == NS) nslot = 0;
+            const char* sb = smem + slot * STAGE;
+            const char* nb = smem + nslot * STAGE;
+            if (kt + 1 < kt1) {
+                // tile kt+1 landed (at most min(kt1-1, kt+NS-2) - (kt+1) tiles still in flight behind it);
+                // every wave is past tile kt-1 (all its reads consumed), so that slot takes tile kt+NS-1
+                qmm_wait_ahead<NI, NS - 3>(min(kt1 - 1, kt + NS - 2) - (kt + 1));
+                if (kt + NS - 1 < kt1) {
+                    int ns = slot + NS - 1;
+                    if (ns >= NS) ns -= NS;
+                    issue(kt + NS - 1, ns, WLc{});
+                }
+            }
+            // next-tile reads are unconditional (on the last tile they read a stale slot and are
+            // discarded): one straight-line body keeps the compiler's LDS counter exact across the edge
+            load_b(nb, bn, (kt + 1) & 3);
+#pragma unroll
+            for (int t = 0; t < WN; ++t) bw[t].prep(kt & 3);
+            // each k-step first issues the next k-step's A reads, then (sched_barrier: not sunk)
+            // dequantises its B fragment and runs its MFMAs
+#define QMM_KSTEP(J)                                                                                       \
     {                                                                                                      \
-        f16x8 a[WM], b[WN];                                                                                \
-        _Pragma("unroll") for (int i = 0; i < WM; ++i) a[i] = *(const f16x8*)(sb + qmm_a_off(i * 32 + col, 2 * (S) + h)); \
+        constexpr int S = KH + KS * (J), CUR = (J) & 1;                                                    \
+        constexpr bool LAST = S + KS >= 4;                                                                 \
+        load_a(LAST ? nb : sb, LAST ? KH : S + KS, ar[CUR ^ 1]);                                           \
+        __builtin_amdgcn_sched_barrier(0);                                                                 \
+        f16x8 b[WN];                                                                                       \
         _Pragma("unroll") for (int t = 0; t < WN; ++t) b[t] = bw[t].template frag<S>();                    \
         _Pragma("unroll") for (int i = 0; i < WM; ++i)                                                     \
             _Pragma("unroll") for (int t = 0; t < WN; ++t) acc[i][t] =                                     \
-                __builtin_amdgcn_mfma_f32_32x32x16_f16(a[i], b[t], acc[i][t], 0, 0, 0);                    \
+                __builtin_amdgcn_mfma_f32_32x32x16_f16(ar[CUR][i], b[t], acc[i][t], 0, 0, 0);              \
     }
-        QMM_KSTEP(0) QMM_KSTEP(1) QMM_KSTEP(2) QMM_KSTEP(3)
+            QMM_KSTEP(0) QMM_KSTEP(1)
+            if constexpr (KS == 1) { QMM_KSTEP(2) QMM_KSTEP(3) }
 #undef QMM_KSTEP
-        if (++slot == NS) slot = 0;
+            // an even number of k-steps per tile: the next tile's first A fragments are in ar[0]
+#pragma unroll
+            for (int t = 0; t < WN; ++t) bw[t] = bn[t];
+            slot = nslot;
+        }
+    };
+    if constexpr (KS == 1) {
+        mainloop(std::integral_constant<int, 0>{});
+    } else {
+        if (kh == 0) mainloop(std::integral_constant<int, 0>{});
+        else mainloop(std::integral_constant<int, 1>{});
+        // sum the two k-step phases: kh = 1 waves park their partials in the (drained) ring
+        __syncthreads();
+        float* red = (float*)smem + (size_t)cg * (WM * WN * 16 * 64) + lane;
+        if (kh == 1) {
+#pragma unroll
+            for (int i = 0; i < WM; ++i)
+#pragma unroll
+                for (int t = 0; t < WN; ++t)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) red[((i * WN + t) * 16 + r) * 64] = acc[i][t][r];
+        }
+        __syncthreads();
+        if (kh == 1) return;
+#pragma unroll
+        for (int i = 0; i < WM; ++i)
+#pragma unroll
+            for (int t = 0; t < WN; ++t)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[i][t][r] += red[((i * WN + t) * 16 + r) * 64];
     }
 
     // ---- epilogue: 32x32 C/D layout: col = lane & 31, row = 8*(r>>2) + 4*(lane>>5) + (r&3) ----
@@ -418,7 +506,7 @@ __global__ __launch_bounds__(64 * NW) void qmm_kernel(const uint16_t* __restrict
     }
 }
 
-template <int QT, int WM, int WN, int NW, int EPI>
+template <int QT, int WM, int WN, int NW, int KS, int EPI>
 static int launch_qmm(const uint16_t* A, int lda, const uint8_t* W, const uint16_t* WD, int M, int N, int K,
                       int splits, void* C, int ldc, hipStream_t st) {
     using G = QmmGeom<QT, WN>;
@@ -435,22 +523,24 @@ static int launch_qmm(const uint16_t* A, int lda, const uint8_t* W, const uint16
     if (nwg <= 0 || nwg > 0x7fffffff) return (int)hipErrorInvalidValue;
     static bool attr_set = false;
     if (!attr_set) {
-        (void)hipFuncSetAttribute((const void*)qmm_kernel<QT, WM, WN, NW, EPI>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)lds);
+        (void)hipFuncSetAttribute((const void*)qmm_kernel<QT, WM, WN, NW, KS, EPI>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         attr_set = true;
     }
-    qmm_kernel<QT, WM, WN, NW, EPI><<<dim3((unsigned)nwg), 64 * NW, lds, st>>>(A, lda, W, WD, M, N, K, n_ct, n_mt, splits,
-                                                                          ktps, C, ldc);
+    qmm_kernel<QT, WM, WN, NW, KS, EPI><<<dim3((unsigned)nwg), 64 * NW * KS, lds, st>>>(A, lda, W, WD, M, N, K, n_ct,
+                                                                                     n_mt, splits, ktps, C, ldc);
     MXK_CHECK_LAUNCH();
 }
 
 template <int QT, int EPI>
-static int dispatch_qmm(int wm, int wn, int nw, const uint16_t* A, int lda, const uint8_t* W, const uint16_t* WD, int M,
-                        int N, int K, int splits, void* C, int ldc, hipStream_t st) {
-#define QMM_CASE(WM_, WN_, NW_) \
-    if (wm == WM_ && wn == WN_ && nw == NW_) return launch_qmm<QT, WM_, WN_, NW_, EPI>(A, lda, W, WD, M, N, K, splits, C, ldc, st);
-    QMM_CASE(1, 1, 4) QMM_CASE(2, 1, 4) QMM_CASE(4, 1, 4) QMM_CASE(1, 2, 4) QMM_CASE(2, 2, 4) QMM_CASE(4, 2, 4)
-    QMM_CASE(2, 1, 8) QMM_CASE(4, 1, 8) QMM_CASE(2, 2, 8) QMM_CASE(4, 2, 8)
+static int dispatch_qmm(int wm, int wn, int nw, int ks, const uint16_t* A, int lda, const uint8_t* W, const uint16_t* WD,
+                        int M, int N, int K, int splits, void* C, int ldc, hipStream_t st) {
+#define QMM_CASE(WM_, WN_, NW_, KS_)                                                                          \
+    if (wm == WM_ && wn == WN_ && nw == NW_ && ks == KS_)                                                     \
+        return launch_qmm<QT, WM_, WN_, NW_, KS_, EPI>(A, lda, W, WD, M, N, K, splits, C, ldc, st);
+    QMM_CASE(1, 1, 4, 1) QMM_CASE(2, 1, 4, 1) QMM_CASE(4, 1, 4, 1) QMM_CASE(1, 2, 4, 1) QMM_CASE(2, 2, 4, 1)
+    QMM_CASE(4, 2, 4, 1) QMM_CASE(2, 1, 8, 1) QMM_CASE(4, 1, 8, 1) QMM_CASE(2, 2, 8, 1) QMM_CASE(4, 2, 8, 1)
+    QMM_CASE(2, 1, 4, 2) QMM_CASE(4, 1, 4, 2) QMM_CASE(2, 2, 4, 2)
 #undef QMM_CASE
     return (int)hipErrorInvalidValue;
 }
@@ -458,22 +548,21 @@ static int dispatch_qmm(int wm, int wn, int nw, const uint16_t* A, int lda, cons
 // A must be f16 (act16 mode f16), 16-B aligned rows (lda % 8 == 0); K % 256 == 0; W in the t32 tiled
 // layout (N % 32 == 0; WD unused). epi: 0 fp32 store, 1 act16 store, 2 fp32 accumulate (split-K via
 // atomics when splits > 1), 3/4 SwiGLU/GeGLU over 16-row interleaved gate/up -> act16 [M, N/2].
-// (wm, wn, nw): 32*wm-row x 32*wn*nw-column tiles, nw waves (4 or 8: 8 = 2 waves per SIMD, whose
-// dequant / LDS phases overlap each other's MFMAs).
-extern "C" int mxk_qmm(int qtype, int epi, int wm, int wn, int nw, const uint16_t* A, int lda, const uint8_t* W,
+// (wm, wn, nw, ks): 32*wm-row x 32*wn*nw-column tiles, nw*ks waves (ks waves per column group split the
+// k-steps; nw*ks = 8 -> 2 waves per SIMD, whose dequant / LDS phases overlap each other's MFMAs).
+extern "C" int mxk_qmm(int qtype, int epi, int wm, int wn, int nw, int ks, const uint16_t* A, int lda, const uint8_t* W,
                        const uint16_t* WD, int M, int N, int K, int splits, void* C, int ldc, hipStream_t st) {
     if (M <= 0) return 0;
     if (K % 256 || (lda & 7) || ((uintptr_t)A & 15) || ((uintptr_t)W & 15)) return (int)hipErrorInvalidValue;
     if (epi != E16_ADD_F32 && splits != 1) return (int)hipErrorInvalidValue;
-    if ((epi == E16_SWIGLU || epi == E16_GEGLU) && (N & 31)) return (int)hipErrorInvalidValue;
     if (N & 31) return (int)hipErrorInvalidValue;
-#define QMM_EPI(QT_)                                                                                           \
-    switch (epi) {                                                                                             \
-        case E16_F32: return dispatch_qmm<QT_, E16_F32>(wm, wn, nw, A, lda, W, WD, M, N, K, splits, C, ldc, st);         \
-        case E16_ACT: return dispatch_qmm<QT_, E16_ACT>(wm, wn, nw, A, lda, W, WD, M, N, K, splits, C, ldc, st);         \
-        case E16_ADD_F32: return dispatch_qmm<QT_, E16_ADD_F32>(wm, wn, nw, A, lda, W, WD, M, N, K, splits, C, ldc, st); \
-        case E16_SWIGLU: return dispatch_qmm<QT_, E16_SWIGLU>(wm, wn, nw, A, lda, W, WD, M, N, K, splits, C, ldc, st);   \
-        case E16_GEGLU: return dispatch_qmm<QT_, E16_GEGLU>(wm, wn, nw, A, lda, W, WD, M, N, K, splits, C, ldc, st);     \
+#define QMM_EPI(QT_)                                                                                                \
+    switch (epi) {                                                                                                  \
+        case E16_F32: return dispatch_qmm<QT_, E16_F32>(wm, wn, nw, ks, A, lda, W, WD, M, N, K, splits, C, ldc, st);         \
+        case E16_ACT: return dispatch_qmm<QT_, E16_ACT>(wm, wn, nw, ks, A, lda, W, WD, M, N, K, splits, C, ldc, st);         \
+        case E16_ADD_F32: return dispatch_qmm<QT_, E16_ADD_F32>(wm, wn, nw, ks, A, lda, W, WD, M, N, K, splits, C, ldc, st); \
+        case E16_SWIGLU: return dispatch_qmm<QT_, E16_SWIGLU>(wm, wn, nw, ks, A, lda, W, WD, M, N, K, splits, C, ldc, st);   \
+        case E16_GEGLU: return dispatch_qmm<QT_, E16_GEGLU>(wm, wn, nw, ks, A, lda, W, WD, M, N, K, splits, C, ldc, st);     \
     }
     switch (qtype) {
         case MXQ_Q4_K: QMM_EPI(MXQ_Q4_K) break;

@@ -286,13 +286,13 @@ def _qmatmul_t32(W: QWeight, x, epi: int, out, xq, xds, M: int, out_zeroed: bool
     can_split = epi == EPI_ADD_F32 or (epi == EPI_F32 and out_zeroed)
     if W.bf16_cache is not None and M >= dense_min_m(x.dtype, epi, can_split) and W.bf16_cache.dtype == x.dtype:
         return _dense_cached(W, x, epi, out, M)
-    wm, wn, nw, splits = _qmm_shape(M, W.N, W.K, can_split)
+    wm, wn, nw, ks, splits = _qmm_shape(M, W.N, W.K, can_split)
     e = EPI_ADD_F32 if (epi == EPI_F32 and splits > 1) else epi
     if e in (EPI_BF16, *GLU_EPIS):
         if out.dtype != x.dtype:
             raise ValueError(f"qmatmul: {out.dtype} output with {x.dtype} activations")
         N.ensure_act(out.dtype)
-    N.kcall("mxk_qmm", int(W.qtype), e, wm, wn, nw, x.data_ptr(), x.stride(0), W.data.data_ptr(), None,
+    N.kcall("mxk_qmm", int(W.qtype), e, wm, wn, nw, ks, x.data_ptr(), x.stride(0), W.data.data_ptr(), None,
             M, W.N, W.K, splits, out.data_ptr(), out.stride(0), N.stream_ptr())
     return out
 
@@ -325,27 +325,36 @@ DENSE_MIN_M_SPLIT = int(os.environ.get("MX_DENSE_MIN_M_SPLIT", "192"))
 Q32_MIN_M = int(os.environ.get("MX_Q32_MIN_M", "48"))
 Q32_FORCE: tuple | None = None  # (wm, wn, splits) override for tuning (tools/tune_qgemm32.py)
 # qmm.hip (LDS-DMA ring, counted vmcnt) runs every f16 GEMM on t32-tiled weights
-QMM_FORCE: tuple | None = None  # (wm, wn, nw, splits) override for tuning (tools/tune_qmm.py)
+QMM_FORCE: tuple | None = None  # (wm, wn, nw, ks, splits) override for tuning (tools/tune_qmm.py)
+# tile configurations compiled into qmm.hip (wm, wn, nw, ks)
+QMM_CONFIGS = ((1, 1, 4, 1), (2, 1, 4, 1), (4, 1, 4, 1), (1, 2, 4, 1), (2, 2, 4, 1), (4, 2, 4, 1), (2, 1, 8, 1),
+               (4, 1, 8, 1), (2, 2, 8, 1), (4, 2, 8, 1), (2, 1, 4, 2), (4, 1, 4, 2), (2, 2, 4, 2))
 
 
 def _qmm_shape(M: int, N_: int, K: int, can_split: bool):
-    """qmm tile choice -> (wm, wn, nw, splits): 32*wm-row x 32*wn*nw-column workgroup tiles with nw
-    waves (8 = two per SIMD, which overlap each other's dequant / LDS phases with MFMAs), K splits
-    (fp32 atomics, split-able outputs only) until the grid holds >= 2 workgroups per CU, keeping >= 8
-    k-tiles (512 k) per split. Fitted to the tools/tune_qmm.py sweep (Llama-3-8B shapes, M 64..2048)."""
+    """qmm tile choice -> (wm, wn, nw, ks, splits): 32*wm-row x 32*wn*nw-column workgroup tiles with
+    nw*ks waves (ks waves per column group split each k-tile's k-steps; 8 waves = two per SIMD, which
+    overlap each other's dequant / LDS phases with MFMAs), K splits (fp32 atomics, split-able outputs
+    only) until the grid holds >= 2 workgroups per CU, keeping >= 8 k-tiles (512 k) per split. Fitted
+    to the tools/tune_qmm.py sweep (Llama-3-8B shapes, M 64..2048)."""
     if QMM_FORCE is not None:
-        wm, wn, nw, splits = QMM_FORCE
-        return wm, wn, nw, (splits if can_split else 1)
-    wm = 1 if M <= 32 else 2 if (M <= 64 or (can_split and M <= 256)) else 4
+        wm, wn, nw, ks, splits = QMM_FORCE
+        return wm, wn, nw, ks, (splits if can_split else 1)
+    # profiles/r2_qmm_tune_ks.jsonl (MI355X, Llama-3-8B projections): up to M = 512 the 4-column-group
+    # tiles with the k-steps split over two waves per group win; beyond, 8 column groups (BN 256/512)
+    # amortise the A-tile reads better. Split-K until ~3/4 of the CUs hold a workgroup.
+    if M <= 512 and (can_split or M <= 128):
+        wm = 2 if M <= 64 or (can_split and N_ <= 4096 and K <= 4096 and M <= 256) else 4
+        wn, nw, ks = 1, 4, 2
+    else:
+        wm, wn, nw, ks = 4, (2 if (M > 256 and N_ >= 6144) else 1), 8, 1
     mt = -(-M // (32 * wm))
-    nw = 8 if wm >= 2 and (-(-N_ // 256) * mt >= 200 or (can_split and N_ >= 6144)) else 4
-    wn = 2 if -(-N_ // (64 * nw)) * mt >= 200 else 1
     cols = -(-N_ // (32 * wn * nw))
     splits = 1
     if can_split:
-        while cols * mt * splits < 2 * CU_COUNT and (K // 64) // (splits * 2) >= 8:
+        while cols * mt * splits < (3 * CU_COUNT) // 4 and (K // 64) // (splits * 2) >= 8:
             splits *= 2
-    return wm, wn, nw, splits
+    return wm, wn, nw, ks, splits
 
 
 def _mfma32_shape(M: int, N_: int, nblk: int, can_split: bool):

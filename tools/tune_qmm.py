@@ -68,8 +68,7 @@ def main():
             res["qmm_auto_cfg"] = list(L._qmm_shape(M, N, K, can_split))
             best = None
             errs = []
-            cfgs = [(wm, wn, nw, sp) for wm in (1, 2, 4) for wn in (1, 2) for nw in (4, 8) if not (nw == 8 and wm == 1)
-                    for sp in ((1, 2, 4, 8) if can_split else (1,))] if full else []
+            cfgs = [(*c, sp) for c in L.QMM_CONFIGS for sp in ((1, 2, 4, 8) if can_split else (1,))] if full else []
             for cfg in cfgs:
                 L.QMM_FORCE = cfg
                 if epi != L.EPI_SWIGLU:
