@@ -53,6 +53,22 @@ def load_llm(model: str, device="cpu", tp_rank: int = 0, tp_size: int = 1, tp_gr
         src = _lora_source(synthetic_source(cfg, "Q4_K_M", seed=1), ov, cfg)
         m = LlamaModel.load(cfg, src, device, tp_rank, tp_size, tp_group)
         return m, ByteTokenizer(cfg.vocab), cfg, {}
+    from .hf import QUANTS, hf_source, is_hf_dir
+    if is_hf_dir(model):  # vllm / transformers backends: HF safetensors directory (models/hf.py)
+        q = str(ov.get("hf_quant") or "q8_0").lower()
+        if q not in QUANTS:
+            log.warning("quantization %r is not a load-time format here; using q8_0", q)
+            q = "q8_0"
+        cfg, get = hf_source(model, q)
+        _apply_overrides(cfg, ov)
+        m = LlamaModel.load(cfg, _lora_source(get, ov, cfg), device, tp_rank, tp_size, tp_group)
+        try:
+            from ..tokenizer import from_hf_dir
+            tok = from_hf_dir(model)
+        except Exception as ex:  # tokenizer.json is optional for synthetic / test checkpoints
+            log.warning("no usable tokenizer in %s (%s); byte-level fallback", model, ex)
+            tok = ByteTokenizer(cfg.vocab)
+        return m, tok, cfg, {"tokenizer.chat_template": getattr(tok, "chat_template", None)}
     if not os.path.isfile(model):
         raise FileNotFoundError(model)
     r = GGUFReader(model)

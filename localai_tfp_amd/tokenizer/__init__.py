@@ -11,3 +11,4 @@ from __future__ import annotations
 
 from .byte import ByteTokenizer  # noqa: F401
 from .gguf import from_gguf  # noqa: F401
+from .hf import from_hf_dir  # noqa: F401
