@@ -59,7 +59,48 @@ def parse():
     ap.add_argument("--steady-finished", type=int, default=-1,
                     help="completed requests before the warmup count starts (-1: concurrency/2)")
     ap.add_argument("--timeout", type=float, default=900.0, help="abort if the window is not reached")
+    ap.add_argument("--tp", type=int, default=1,
+                    help="tensor-parallel ranks per serving replica (BASELINE config #3: --model llama3-70b "
+                         "--gpus 8 --tp 8); world = dp x tp, rank 0 of every group leads")
+    ap.add_argument("--no-tp-check", action="store_true", help="skip the TP-vs-unsharded logits self-check")
     return ap.parse_args()
+
+
+class _GroupSync:
+    """dist-like facade whose barrier / all_reduce run on one process group (the replica leaders)."""
+
+    def __init__(self, dist, group):
+        self.dist, self.group = dist, group
+        self.ReduceOp = dist.ReduceOp
+
+    def barrier(self):
+        self.dist.barrier(group=self.group)
+
+    def all_reduce(self, t, op=None):
+        self.dist.all_reduce(t, op=op if op is not None else self.dist.ReduceOp.SUM, group=self.group)
+
+
+def setup_tp(args, world, rank, dev):
+    """world = dp x tp: RCCL group per replica (model all-reduces), two gloo groups per replica (plan
+    channel + collectives, parallel/tp_engine.py), and a leaders group for the bench's barriers."""
+    import torch.distributed as dist
+    from localai_tfp_amd.parallel.tp_engine import TPLink, tp_timeout
+    tp = args.tp
+    if world % tp:
+        raise SystemExit(f"--tp {tp} does not divide world size {world}")
+    dp = world // tp
+    mine = None
+    for g in range(dp):
+        ranks = list(range(g * tp, (g + 1) * tp))
+        gpu = dist.new_group(ranks)
+        cpu = dist.new_group(ranks, backend="gloo", timeout=tp_timeout())
+        sync = dist.new_group(ranks, backend="gloo", timeout=tp_timeout())
+        if rank in ranks:
+            mine = (g, gpu, cpu, sync, ranks[0])
+    leaders = dist.new_group([g * tp for g in range(dp)])
+    g, gpu, cpu, sync, src = mine
+    link = TPLink(rank % tp, tp, cpu, gpu, src=src, sync_group=sync)
+    return link, gpu, (_GroupSync(dist, leaders) if dp > 1 else None), dp
 
 
 def free_port() -> int:
@@ -92,8 +133,11 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if torch.cuda.is_available():
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:  # CPU rehearsal of the multi-rank paths (gloo)
+            dist.init_process_group("gloo")
     dev = torch.device("cuda", local) if torch.cuda.is_available() else torch.device("cpu")
     if dev.type == "cuda":
         torch.cuda.set_device(dev)
@@ -107,10 +151,27 @@ def main():
     from localai_tfp_amd.tokenizer import ByteTokenizer
 
     cfg = {"llama3-8b": C.LLAMA3_8B, "llama3-70b": C.LLAMA3_70B, "llama32-1b": C.LLAMA32_1B}[args.model]
-    if dev.type == "cpu":  # plumbing only
-        cfg = C.tiny_config()
+    if dev.type == "cpu":  # plumbing only (row-parallel shards need whole 256-wide super-blocks: tp <= 2)
+        cfg = C.tiny_config(hidden=512, ffn=1024, n_heads=8, n_kv_heads=2)
+    tp, link, tp_group, dp = args.tp, None, None, world
+    tp_rel = None
+    if tp > 1:
+        link, tp_group, dist_leaders, dp = setup_tp(args, world, rank, dev)
+        if not args.no_tp_check:
+            # the measured sharded graph against the unsharded one: 2 layers of the same architecture,
+            # identical weights, one prefill step (parallel/tp_engine.tp_selfcheck)
+            import copy
+            from localai_tfp_amd.parallel.tp_engine import tp_selfcheck
+            small = copy.deepcopy(cfg)
+            small.n_layers = 2
+            tp_rel = tp_selfcheck(small, synthetic_source(small, "Q4_K_M", seed=3), dev, link.rank, tp, tp_group)
+            if tp_rel is not None:
+                print(f"[bench rank {rank}] tp self-check: max|dlogit|/max|logit| = {tp_rel:.2e}", file=sys.stderr,
+                      flush=True)
+        dist = dist_leaders  # bench barriers / reductions run among the replica leaders only
     t0 = time.time()
-    model = LlamaModel.load(cfg, synthetic_source(cfg, "Q4_K_M", seed=1), dev)
+    src = synthetic_source(cfg, "Q4_K_M", seed=1, shard_gen=tp > 1)
+    model = LlamaModel.load(cfg, src, dev, rank % tp, tp, tp_group)
     t_load = time.time() - t0
     tok = ByteTokenizer(cfg.vocab)
     ecfg = EngineConfig(max_num_seqs=args.concurrency, max_batched_tokens=args.max_batched_tokens,
@@ -118,7 +179,13 @@ def main():
                         kv_dtype=args.kv_dtype)
     if dev.type == "cpu":
         ecfg.num_blocks = 2048
-    eng = LLMEngine(model, tok, ecfg)
+    eng = LLMEngine(model, tok, ecfg, tp=link)
+    if link is not None and not link.is_leader:
+        eng.follow()  # replay the leader's plans until it stops the engine
+        link.close()
+        import torch.distributed as tdist
+        tdist.destroy_process_group()
+        return
     t0 = time.time()
     n_graphs = eng.precapture_graphs()
     t_capture = time.time() - t0
@@ -127,6 +194,7 @@ def main():
         res = run_http(args, eng, tok, cfg, dev, dist)
     else:
         res = run_engine(args, eng, tok, dev, dist)
+        eng.shutdown()  # tensor parallel: releases the followers from engine.follow()
     t_el, tokens, ttfts, extra = res
 
     p50 = float(np.percentile(ttfts, 50)) if len(ttfts) else float("nan")
@@ -139,7 +207,7 @@ def main():
         sm = tt.clone()
         dist.all_reduce(sm, op=dist.ReduceOp.SUM)
         t_max, tok_sum = float(mx[0]), float(sm[1])
-        p50_all, p99_all = float(sm[2] / world), float(mx[3])
+        p50_all, p99_all = float(sm[2] / dp), float(mx[3])
     value = tok_sum / t_max
     from localai_tfp_amd.ops.linear import ACT_DTYPE
     # 16-bit MFMA operands (Q4_K_M weights dequantised in-register), fp32 accumulation everywhere
@@ -158,13 +226,15 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": act_name,
-            "data": "synthetic (random-init Llama-3-8B weights in real Q4_K_M block formats; synthetic chat prompts)",
+            "data": f"synthetic (random-init {cfg.name} weights in real Q4_K_M block formats; synthetic chat prompts)",
             "p50_ttft_ms": round(p50_all, 2),
             "p99_ttft_ms": round(p99_all, 2),
             "config": {
-                "model": cfg.name + " Q4_K_M", "global_batch": args.concurrency * world,
+                "model": cfg.name + " Q4_K_M", "global_batch": args.concurrency * dp,
                 "seq_len": args.prompt_len + args.gen_len, "prompt_len": args.prompt_len, "gen_len": args.gen_len,
-                "concurrency_per_gpu": args.concurrency, "parallelism": f"dp{world}",
+                "concurrency_per_replica": args.concurrency,
+                "parallelism": f"dp{dp}" if tp == 1 else (f"tp{tp}" if dp == 1 else f"dp{dp}xtp{tp}"),
+                **({"tp_selfcheck_rel_err": tp_rel} if tp_rel is not None else {}),
                 "path": ("HTTP /v1/chat/completions (SSE) -> FastAPI gateway -> mxstream (batched gRPC-side channel) -> LLM worker engine" if args.path == "http"
                          else "engine in-process (gateway/gRPC excluded)"),
                 "load_s": round(t_load, 1), "graph_capture_s": round(t_capture, 1), "graphs": n_graphs,
@@ -176,8 +246,11 @@ def main():
             },
         }
         print(json.dumps(out), flush=True)
-    if dist:
-        dist.destroy_process_group()
+    if link is not None:
+        link.close()
+    if world > 1:
+        import torch.distributed as tdist
+        tdist.destroy_process_group()
 
 
 class Window:

@@ -20,7 +20,8 @@ final-logit soft-capping, Gemma 3's per-head QK-norm and local RoPE base on the 
 
 Decode batches of <= 4 tokens take the int8-dot GEMV path (norm kernels emit q8 directly);
 larger batches the dequant-MFMA path. Tensor parallelism (parallel/tp.py) shards heads / FFN
-columns and all-reduces the residual after the row-parallel projections.
+columns, all-reduces the row-parallel projections' 16-bit partial sums into the replicated residual,
+runs MoE layers expert-parallel and the LM head vocab-parallel.
 """
 from __future__ import annotations
 
@@ -38,6 +39,11 @@ from ..ops.moe import MoEWeights, moe_ffn
 from .config import LlamaConfig
 
 GEMV_MAX_M = 4
+
+
+def vocab_shard(V: int, tp: int) -> int:
+    """Rows of the vocab-parallel LM head per rank (whole 32-row t32 groups; the tail is zero-padded)."""
+    return -(-V // (tp * 32)) * 32
 
 
 @dataclass
@@ -113,6 +119,14 @@ class Workspace:
         # projection output before the post-norm (Gemma 2/3)
         self.y = torch.empty((T, H), dtype=torch.float32, device=dev) if cfg.post_norms else None
         self.logits = torch.empty((max_seqs, cfg.vocab), dtype=torch.float32, device=dev)
+        if tp_size > 1:
+            # row-parallel partial projections, all-reduced in 16 bits (fp32 on the CPU oracle path)
+            self.y16 = torch.empty((T, H), dtype=act if dev.type == "cuda" else torch.float32, device=dev)
+            # vocab-parallel LM head: this rank's logits, then the all-gathered [tp, S, V/tp] block
+            vl = vocab_shard(cfg.vocab, tp_size)
+            self.logits_local = torch.empty((max_seqs, vl), dtype=torch.float32, device=dev)
+            self.logits_gather = torch.empty((tp_size, max_seqs, vl), dtype=torch.float32, device=dev)
+            self.moe_y = torch.empty((T, H), dtype=torch.float32, device=dev) if cfg.n_expert else None
         nh = cfg.n_heads // tp_size
         self.part_ml = torch.empty((max_seqs * nh * max_parts, 2), dtype=torch.float32, device=dev)
         self.part_o = torch.empty((max_seqs * nh * max_parts, cfg.head_dim), dtype=torch.float32, device=dev)
@@ -173,6 +187,10 @@ class LlamaModel:
         from ..parallel import tp as TP
         m = cls(cfg, device, tp_rank, tp_size, tp_group)
         dev = m.device
+        plan = getattr(get_tensor, "plan", None)
+
+        def has(name):  # existence without materialising the tensor (synthetic sources carry a plan)
+            return (name in plan) if plan is not None else get_tensor(name) is not None
 
         def f32(name):
             t = get_tensor(name)
@@ -183,6 +201,11 @@ class LlamaModel:
             return torch.from_numpy(np.ascontiguousarray(dequantize(raw, qt, shape)).reshape(-1).copy()).to(dev)
 
         def qw(name, split=None):
+            shard = getattr(get_tensor, "shard", None)
+            if tp_size > 1 and split is not None and shard is not None and has(name):
+                # source that generates only this rank's slice (synthetic multi-GPU benches)
+                raw, qt, N_, K_ = shard(name, split, tp_rank, tp_size)
+                return QWeight.from_ggml(raw, qt, N_, K_, dev, name)
             t = get_tensor(name)
             if t is None:
                 return None
@@ -214,7 +237,7 @@ class LlamaModel:
         m.stage = stage
         for i in range(l0, l1):
             p = f"blk.{i}."
-            if get_tensor(p + "attn_qkv.weight") is not None:  # phi3: fused Q|K|V rows
+            if has(p + "attn_qkv.weight"):  # phi3: fused Q|K|V rows
                 wq, wk, wv = qw_rows(p + "attn_qkv.weight", [cfg.q_dim, cfg.kv_dim, cfg.kv_dim],
                                      [("col_heads", cfg.n_heads, hd), ("col_heads", cfg.n_kv_heads, hd),
                                       ("col_heads", cfg.n_kv_heads, hd)])
@@ -240,11 +263,9 @@ class LlamaModel:
             moe = None
             wg = wu = wgu = wd = None
             if cfg.n_expert:
-                if tp_size > 1:
-                    raise NotImplementedError("tensor-parallel MoE layers (expert parallelism) are not supported yet")
-                moe = load_moe(m, get_tensor, p, f32, qw, fuse)
+                moe = load_moe(m, get_tensor, p, f32, qw, fuse)  # expert-parallel under TP
             else:
-                if get_tensor(p + "ffn_gate.weight") is None and get_tensor(p + "ffn_up.weight") is not None:
+                if not has(p + "ffn_gate.weight") and has(p + "ffn_up.weight"):
                     wg, wu = qw_rows(p + "ffn_up.weight", [cfg.ffn, cfg.ffn], [("col", cfg.ffn), ("col", cfg.ffn)])
                 else:
                     wg = qw(p + "ffn_gate.weight", ("col", cfg.ffn))
@@ -280,8 +301,21 @@ class LlamaModel:
         m.tok_embd = QWeight.from_ggml(np.asarray(raw).view(np.uint8).reshape(int(shape[1]), -1), qt,
                                        int(shape[1]), int(shape[0]), dev, "token_embd")
         m.out_norm = f32("output_norm.weight").float()
-        head = get_tensor("output.weight")
-        if head is None:
+        if tp_size > 1:
+            # vocab-parallel LM head: rank r holds vocab rows [r*V/tp, (r+1)*V/tp) (tied embeddings: a
+            # slice of token_embd; the lookup keeps the full table)
+            hname = "output.weight" if has("output.weight") else "token_embd.weight"
+            if not has("output.weight"):
+                cfg.tie_embeddings = True
+            raw, qt, shape = get_tensor(hname)
+            V, K_ = int(shape[1]), int(shape[0])
+            rows = np.asarray(raw).view(np.uint8).reshape(V, -1)
+            vl = vocab_shard(V, tp_size)
+            lo, hi = min(V, tp_rank * vl), min(V, (tp_rank + 1) * vl)
+            part = np.zeros((vl, rows.shape[1]), np.uint8)
+            part[:hi - lo] = rows[lo:hi]  # zero rows past V: logits 0, trimmed after the gather
+            m.lm_head = QWeight.from_ggml(part, qt, vl, K_, dev, "output.shard")
+        elif not has("output.weight"):
             m.lm_head = m.tok_embd
             cfg.tie_embeddings = True
         else:
@@ -413,8 +447,14 @@ class LlamaModel:
             # ---- FFN block ----
             if L.moe is not None:
                 K.rmsnorm(h, L.ffn_norm, eps, out_bf16=xb)
-                moe_ffn(L.moe, xb, h)
-                self._allreduce(h)
+                if self.tp_size > 1:  # expert parallel: this rank's experts' share, summed over ranks
+                    y = ws.moe_y[:T]
+                    y.zero_()
+                    moe_ffn(L.moe, xb, y)
+                    self._allreduce(y)
+                    h.add_(y)
+                else:
+                    moe_ffn(L.moe, xb, h)
                 continue
             if gemv:
                 xq, xds = ws.q8(T, H)
@@ -453,7 +493,7 @@ class LlamaModel:
             if fb.want_hidden:
                 return hn
             self.last_hidden = hn
-        logits = ws.logits[:S]
+        logits = ws.logits[:S] if self.tp_size == 1 else ws.logits_local[:S]
         if S <= GEMV_MAX_M and self.device.type == "cuda" and self.lm_head.is_quant:
             xq, xds = ws.q8(S, H)
             K.rmsnorm(hs, self.out_norm, eps, out_q8=(xq, xds))
@@ -462,18 +502,51 @@ class LlamaModel:
             xbs = ws.xb[:S, :H]
             K.rmsnorm(hs, self.out_norm, eps, out_bf16=xbs)
             qmatmul(self.lm_head, xbs, EPI_F32, logits)
+        if self.tp_size > 1:
+            logits = self._gather_vocab(logits, ws, S)
         if cfg.final_softcap:
             c = cfg.final_softcap
             torch.tanh(logits.div_(c), out=logits).mul_(c)
         return logits
 
+    def _gather_vocab(self, logits_local: torch.Tensor, ws: Workspace, S: int) -> torch.Tensor:
+        """Vocab-parallel head: all-gather the [S, V/tp] slices into the full [S, V] logits."""
+        import torch.distributed as dist
+        vl, tp = logits_local.shape[1], self.tp_size
+        g = ws.logits_gather.view(-1)[: tp * S * vl].view(tp * S, vl)  # rank r's rows at [r*S, (r+1)*S)
+        if dist.is_initialized():
+            dist.all_gather_into_tensor(g, logits_local.contiguous(), group=self.tp_group)
+        else:
+            g.copy_(logits_local.repeat(tp, 1))
+        out = ws.logits[:S]
+        V = out.shape[1]
+        for r in range(tp):
+            lo = r * vl
+            if lo >= V:
+                break
+            out[:, lo:min(V, lo + vl)] = g[r * S:(r + 1) * S, :min(V, lo + vl) - lo]
+        return out
+
     def _residual_proj(self, W: QWeight, x, xq, xds, h: torch.Tensor, post_norm, ws: Workspace, T: int, eps: float):
         """h += x W^T — or, with a Gemma post-norm, h += rmsnorm(x W^T) * post_norm. Under tensor
-        parallelism the partial projections are all-reduced before the (replicated) norm."""
+        parallelism each rank's partial projection is all-reduced in 16 bits (half the fp32 residual's
+        bytes; one message per row-parallel projection) and added to the replicated residual."""
         gemv = xq is not None
+        if self.tp_size > 1:
+            y16 = ws.y16[:T]
+            if gemv:
+                qmatmul(W, None, EPI_BF16, y16, xq=xq, xds=xds)
+            else:
+                qmatmul(W, x, EPI_BF16, y16)
+            self._allreduce(y16)
+            if post_norm is None:
+                h.add_(y16)
+            else:
+                y = ws.y[:T]
+                y.copy_(y16)
+                K.rmsnorm_add(y, post_norm, eps, h)
+            return
         if post_norm is None:
-            if self.tp_size > 1 and self.tp_rank != 0:
-                h.zero_()
             if gemv:
                 qmatmul(W, None, EPI_ADD_F32, h, xq=xq, xds=xds)
             else:
@@ -490,20 +563,37 @@ class LlamaModel:
 
 
 def load_moe(m: LlamaModel, get_tensor, p: str, f32, qw, fuse: bool) -> MoEWeights:
-    """Stacked expert tensors (ggml [K, N, E]) -> MoEWeights; gate|up interleaved per expert on GPU."""
+    """Stacked expert tensors (ggml [K, N, E]) -> MoEWeights; gate|up interleaved per expert on GPU.
+    Under tensor parallelism the experts are distributed (expert parallelism): rank r keeps experts
+    [r*E/tp, (r+1)*E/tp) whole — no block-size constraint on the expert FFN width — and the shared
+    expert lives on rank 0; the per-rank partial outputs are all-reduced by the caller."""
     cfg = m.cfg
     E, Fe, H = cfg.n_expert, cfg.expert_ffn, cfg.hidden
+    tp, r = m.tp_size, m.tp_rank
+    if E % tp:
+        raise ValueError(f"{E} experts do not divide over tensor-parallel size {tp}")
+    El = E // tp
+    e0 = r * El
     router = f32(p + "ffn_gate_inp.weight").float().view(E, H).contiguous()
-    wg = qw(p + "ffn_gate_exps.weight")
-    wu = qw(p + "ffn_up_exps.weight")
-    wd = qw(p + "ffn_down_exps.weight")
+
+    def experts(name, rows_per):
+        if tp == 1:
+            return qw(name)
+        raw, qt, shape = get_tensor(name)
+        K_ = int(shape[0])
+        rows = np.asarray(raw).view(np.uint8).reshape(E * rows_per, -1)[e0 * rows_per:(e0 + El) * rows_per]
+        return QWeight.from_ggml(np.ascontiguousarray(rows), qt, El * rows_per, K_, m.device, name)
+
+    wg = experts(p + "ffn_gate_exps.weight", Fe)
+    wu = experts(p + "ffn_up_exps.weight", Fe)
+    wd = experts(p + "ffn_down_exps.weight", H)
     on_gpu = m.device.type == "cuda"
     gu = interleave_gate_up(wg, wu, p + "ffn_gate_up_exps") if (fuse or on_gpu) else None
     if on_gpu and (gu is None or not gu.is_quant or not wd.is_quant):
         raise NotImplementedError(f"{p}: MoE experts need Q4_K/Q6_K/Q8_0 weights with F % 16 == 0 on the GPU")
     moe = MoEWeights(router=router, gate=None if on_gpu else wg, up=None if on_gpu else wu, gate_up=gu, down=wd,
-                     n_expert=E, n_used=cfg.n_expert_used, ffn=Fe, renorm=cfg.moe_renorm)
-    if cfg.expert_shared_ffn:
+                     n_expert=E, n_used=cfg.n_expert_used, ffn=Fe, renorm=cfg.moe_renorm, e0=e0, n_local=El)
+    if cfg.expert_shared_ffn and r == 0:
         sg, su = qw(p + "ffn_gate_shexp.weight"), qw(p + "ffn_up_shexp.weight")
         moe.sh_down = qw(p + "ffn_down_shexp.weight")
         moe.sh_gate_up = interleave_gate_up(sg, su, p + "ffn_gate_up_shexp") if on_gpu else None

@@ -91,7 +91,12 @@ def _gen_f32(rng, name, n):
     return (0.02 * rng.standard_normal(n, dtype=np.float32)).astype(np.float32)
 
 
-def synthetic_source(cfg: LlamaConfig, ftype: str = "Q4_K_M", seed: int = 0):
+def synthetic_source(cfg: LlamaConfig, ftype: str = "Q4_K_M", seed: int = 0, shard_gen: bool = False):
+    """get_tensor(name) -> (raw, qtype, ggml_shape). shard_gen=True also exposes
+    get_tensor.shard(name, split, rank, size) -> (raw, qtype, N, K), which generates ONLY that rank's
+    tensor-parallel slice (same shapes and block formats, independent random values): a 70B model on 8
+    ranks then costs each rank 1/8 of the generation time and host memory. Slices are not slices of
+    get_tensor(name) — TP-vs-TP=1 parity checks use the plain source."""
     plan = {n: (s, q) for n, s, q in llama_tensor_plan(cfg, ftype)}
     order = {n: i for i, n in enumerate(plan)}
 
@@ -102,7 +107,24 @@ def synthetic_source(cfg: LlamaConfig, ftype: str = "Q4_K_M", seed: int = 0):
         rng = np.random.default_rng(seed * 100003 + order[name])
         return _gen(rng, name, shape, qt, cfg), int(qt), shape
 
+    def shard(name, split, rank, size):
+        shape, qt = plan[name]
+        K, N = int(shape[0]), int(np.prod(shape[1:]))
+        kind = split[0]
+        if kind == "col_heads":
+            n_heads, hd = split[1], split[2]
+            N = (n_heads // size if n_heads >= size else 1) * hd
+        elif kind == "col":
+            N //= size
+        elif kind == "row":
+            K //= size
+        rng = np.random.default_rng((seed * 100003 + order[name]) * 64 + rank + 1)
+        raw = _gen(rng, name, [K, N], qt, cfg)
+        return np.asarray(raw).view(np.uint8).reshape(N, -1), int(qt), N, K
+
     get_tensor.plan = plan
+    if shard_gen:
+        get_tensor.shard = shard
     return get_tensor
 
 

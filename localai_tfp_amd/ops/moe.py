@@ -39,6 +39,8 @@ class MoEWeights:
     sh_up: QWeight | None = None
     sh_down: QWeight | None = None
     sh_inp: torch.Tensor | None = None  # fp32 [H] sigmoid gate of the shared expert
+    e0: int = 0  # expert parallelism: this rank holds experts [e0, e0 + n_local) of the n_expert
+    n_local: int = 0  # 0 = all
 
     def nbytes(self) -> int:
         n = self.router.numel() * 4
@@ -82,21 +84,33 @@ def moe_ffn(W: MoEWeights, x: torch.Tensor, h: torch.Tensor) -> torch.Tensor:
     st = N.stream_ptr()
     N.kcall("mxk_moe_route", logits.data_ptr(), logits.stride(0), T, E, k, int(W.renorm), ids.data_ptr(),
             wts.data_ptr(), st)
+    El = W.n_local or E
+    y_zero = False
+    if El != E:
+        # expert parallelism: pairs routed to other ranks' experts go to a null bucket El (sorted last,
+        # never computed) with weight 0; the grouped GEMMs run over the El local experts only
+        loc = ids - W.e0
+        off_rank = (loc < 0) | (loc >= El)
+        ids = torch.where(off_rank, torch.full_like(loc, El), loc)
+        wts = wts.masked_fill(off_rank, 0.0)
+        y_zero = True
     P = T * k
     wm = _grouped_wm(P, E)
-    off = torch.empty(E + 1, dtype=torch.int32, device=x.device)
-    tiles = torch.empty(E + 1, dtype=torch.int32, device=x.device)
+    Eb = El + (1 if El != E else 0)  # sort buckets (+ the null bucket)
+    off = torch.empty(Eb + 1, dtype=torch.int32, device=x.device)
+    tiles = torch.empty(Eb + 1, dtype=torch.int32, device=x.device)
     stok = torch.empty(P, dtype=torch.int32, device=x.device)
     inv = torch.empty(P, dtype=torch.int32, device=x.device)
-    N.kcall("mxk_moe_sort", ids.data_ptr(), P, k, E, 16 * wm, off.data_ptr(), tiles.data_ptr(), stok.data_ptr(),
+    N.kcall("mxk_moe_sort", ids.data_ptr(), P, k, Eb, 16 * wm, off.data_ptr(), tiles.data_ptr(), stok.data_ptr(),
             inv.data_ptr(), st)
+    E = El
     act = torch.empty(P, F, dtype=x.dtype, device=x.device)
     N.ensure_act(x.dtype)
     gu = W.gate_up
     N.kcall("mxk_moe_qgemm16", int(gu.qtype), E16_SWIGLU, wm, x.data_ptr(), x.stride(0), stok.data_ptr(),
             gu.data.data_ptr(), N.ptr(gu.dplane), off.data_ptr(), tiles.data_ptr(), E, P, 2 * F, gu.K,
             act.data_ptr(), act.stride(0), st)
-    y = torch.empty(P, H, dtype=torch.float32, device=x.device)
+    y = (torch.zeros if y_zero else torch.empty)(P, H, dtype=torch.float32, device=x.device)
     d = W.down
     N.kcall("mxk_moe_qgemm16", int(d.qtype), E16_F32, wm, act.data_ptr(), act.stride(0), None, d.data.data_ptr(),
             N.ptr(d.dplane), off.data_ptr(), tiles.data_ptr(), E, P, H, d.K, y.data_ptr(), y.stride(0), st)
@@ -130,12 +144,13 @@ def _moe_ref(W: MoEWeights, x: torch.Tensor, h: torch.Tensor) -> torch.Tensor:
     E, k, F = W.n_expert, W.n_used, W.ffn
     H = h.shape[1]
     ids, wts = route_ref(x @ W.router.t(), k, W.renorm)
-    g = W.gate.dense_f32().view(E, F, -1)
-    u = W.up.dense_f32().view(E, F, -1)
-    d = W.down.dense_f32().view(E, H, F)
+    El = W.n_local or E
+    g = W.gate.dense_f32().view(El, F, -1)
+    u = W.up.dense_f32().view(El, F, -1)
+    d = W.down.dense_f32().view(El, H, F)
     out = torch.zeros_like(h)
-    for e in range(E):
-        tok, slot = (ids == e).nonzero(as_tuple=True)
+    for e in range(El):
+        tok, slot = (ids == W.e0 + e).nonzero(as_tuple=True)
         if tok.numel() == 0:
             continue
         xe = x[tok]

@@ -6,9 +6,11 @@ backend/python/vllm/backend.py:106-107 `tensor_parallel_size`):
   * column-parallel: Q/K/V by heads (KV heads replicated when Hkv < world), gate/up by FFN columns;
   * row-parallel: o_proj and down_proj by input columns, in whole 256-element super-blocks so the
     quantised bytes split without re-quantisation;
-  * the residual stream is replicated; after each row-parallel projection rank 0 keeps the
-    residual and the others contribute only their partial sums, so ONE all-reduce of h per
-    projection (2 per layer; message = tokens x hidden x 4 B) restores it.
+  * the residual stream is replicated; each row-parallel projection writes this rank's partial sum
+    in 16 bits (the GEMM epilogue's activation format) and ONE all-reduce of it per projection (2 per
+    layer; message = tokens x hidden x 2 B, half of an fp32 residual all-reduce) is added to h;
+  * MoE layers are expert-parallel (whole experts per rank, models/llama.py load_moe) and the LM head
+    vocab-parallel (rows of the vocabulary per rank, logits all-gathered): no rank holds the full head.
 """
 from __future__ import annotations
 

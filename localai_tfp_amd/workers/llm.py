@@ -213,7 +213,8 @@ class LLMServicer(BackendServicer):
             if self.tp is not None:
                 import dataclasses
                 self.tp.send_control("load", (path, ov, dataclasses.asdict(ec)))
-                model, tok, mcfg, _ = load_llm(path, self.device, self.tp.rank, self.tp.world, None, ov)
+                with self.tp.quiet():  # followers load too: no heartbeats until they listen again
+                    model, tok, mcfg, _ = load_llm(path, self.device, self.tp.rank, self.tp.world, None, ov)
             elif rpc_servers:
                 # remote layer split (reference LLAMACPP_GRPC_SERVERS, grpc-server.cpp:139-161):
                 # contiguous layer ranges on `local-ai worker llama-cpp-rpc` stages, tensor_split weights

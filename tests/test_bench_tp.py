@@ -1,0 +1,31 @@
+"""bench.py tensor-parallel mode (BASELINE config #3 shape: --tp N; world = dp x tp) rehearsed on the
+CPU with gloo: the TP-vs-unsharded self-check runs, followers replay the leader's plans, the leaders'
+JSON line carries the parallelism layout. The 8-GPU RCCL run itself is the driver's."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_bench_dp2_tp2_cpu(tmp_path):
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="2")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "4", "--master-addr",
+           "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "bench.py"), "--gpus", "4", "--tp", "2",
+           "--path", "engine", "--steps", "3", "--warmup", "1", "--concurrency", "4", "--prompt-len", "32",
+           "--gen-len", "6"]
+    p = subprocess.run(cmd, env=env, cwd=str(tmp_path), capture_output=True, text=True, timeout=600)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    out = json.loads(lines[0])
+    assert out["config"]["parallelism"] == "dp2xtp2" and out["n_gpus"] == 4 and out["value"] > 0
+    assert out["config"]["tp_selfcheck_rel_err"] < 1e-3

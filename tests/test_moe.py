@@ -190,3 +190,36 @@ def test_moe_model_gpu_matches_cpu_and_engine():
         assert all(len(o.token_ids) == 12 for o in outs)
         streams.append([o.token_ids for o in outs])
     assert streams[0] == streams[1]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tp", [2, 4])
+def test_moe_expert_parallel_gpu(tp):
+    """Expert parallelism (tensor-parallel MoE layers): every rank's share computed by the GPU kernels
+    with the off-rank pairs in the null bucket; the shares sum to the unsharded MoE output."""
+    from localai_tfp_amd.ops.linear import ACT_DTYPE, interleave_gate_up
+    E, k, H, F, qt = 8, 2, 256, 256, QType.Q4_K
+    rng = np.random.default_rng(11)
+    raws = {n: random_quantized(rng, qt, r, c, std=0.05).reshape(r, -1)
+            for n, r, c in (("g", E * F, H), ("u", E * F, H), ("d", E * H, F))}
+    router = torch.randn(E, H) * 0.5
+
+    def build(e0, el):
+        g = QWeight.from_ggml(np.ascontiguousarray(raws["g"][e0 * F:(e0 + el) * F]), int(qt), el * F, H, "cuda")
+        u = QWeight.from_ggml(np.ascontiguousarray(raws["u"][e0 * F:(e0 + el) * F]), int(qt), el * F, H, "cuda")
+        d = QWeight.from_ggml(np.ascontiguousarray(raws["d"][e0 * H:(e0 + el) * H]), int(qt), el * H, F, "cuda")
+        return MO.MoEWeights(router=router.cuda(), gate=None, up=None, gate_up=interleave_gate_up(g, u), down=d,
+                             n_expert=E, n_used=k, ffn=F, renorm=True, e0=e0, n_local=0 if el == E else el)
+    full = build(0, E)
+    shards = [build(r * E // tp, E // tp) for r in range(tp)]
+    for T in (1, 5, 64):
+        x = torch.randn(T, H).to(ACT_DTYPE).cuda()
+        ref = MO.moe_ffn(full, x, torch.zeros(T, H, device="cuda"))
+        acc = torch.zeros(T, H, device="cuda")
+        for w in shards:
+            y = torch.zeros(T, H, device="cuda")
+            MO.moe_ffn(w, x, y)
+            acc += y
+        torch.cuda.synchronize()
+        rel = float((acc - ref).norm() / ref.norm())
+        assert rel < 1e-4, (T, rel)

@@ -18,29 +18,42 @@ def _port():
 PROMPTS = [list(b"tensor parallel test prompt one"), list(b"another, somewhat longer prompt for the second seq")]
 
 
-def _build(rank, world, link):
-    from localai_tfp_amd.engine.engine import EngineConfig, LLMEngine
+def _cfg(kind):
     from localai_tfp_amd.models.config import tiny_config
+    # row-parallel shards must be whole 256-element Q4_K/Q6_K super-blocks: hidden 512 / tp 2
+    if kind == "moe":  # expert parallel: 8 experts, 4 per rank, top-2 routing + renorm
+        return tiny_config(arch="qwen3moe", n_layers=2, hidden=512, ffn=1024, n_heads=8, n_kv_heads=2, head_dim=64,
+                           rope_dim=64, n_expert=8, n_expert_used=2, expert_ffn=256, qk_norm=True)
+    return tiny_config(n_layers=2, hidden=512, ffn=1024, n_heads=8, n_kv_heads=2, head_dim=64, rope_dim=64)
+
+
+def _build(rank, world, link, kind="dense"):
+    from localai_tfp_amd.engine.engine import EngineConfig, LLMEngine
     from localai_tfp_amd.models.llama import LlamaModel
     from localai_tfp_amd.models.synthetic import synthetic_source
     from localai_tfp_amd.tokenizer import ByteTokenizer
-    # row-parallel shards must be whole 256-element Q4_K/Q6_K super-blocks: hidden 512 / tp 2
-    cfg = tiny_config(n_layers=2, hidden=512, ffn=1024, n_heads=8, n_kv_heads=2, head_dim=64, rope_dim=64)
+    cfg = _cfg(kind)
     model = LlamaModel.load(cfg, synthetic_source(cfg, "Q4_K_M", seed=7), "cpu", rank, world, None)
     ec = EngineConfig(num_blocks=128, max_num_seqs=4, max_batched_tokens=32, max_model_len=256)
     return LLMEngine(model, ByteTokenizer(cfg.vocab), ec, tp=link)
 
 
-def _worker(rank, world, port, q):
+def _link(rank, world, port, timeout_s=120, heartbeat_s=None):
     import datetime
     import torch.distributed as dist
     from localai_tfp_amd.parallel.tp_engine import TPLink
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    cpu = dist.new_group(backend="gloo", timeout=datetime.timedelta(seconds=120))
-    link = TPLink(rank, world, cpu)
-    eng = _build(rank, world, link)
+    cpu = dist.new_group(backend="gloo", timeout=datetime.timedelta(seconds=timeout_s))
+    sync = dist.new_group(backend="gloo", timeout=datetime.timedelta(seconds=timeout_s))
+    return TPLink(rank, world, cpu, sync_group=sync, heartbeat_s=heartbeat_s)
+
+
+def _worker(rank, world, port, q, kind="dense"):
+    import torch.distributed as dist
+    link = _link(rank, world, port, heartbeat_s=0.5)  # heartbeats interleave with real plans
+    eng = _build(rank, world, link, kind)
     if rank == 0:
         from localai_tfp_amd.engine.sequence import Request
         from localai_tfp_amd.ops.sampling import SamplingParams
@@ -59,8 +72,9 @@ def _worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def test_tp2_matches_single_process():
-    eng = _build(0, 1, None)
+@pytest.mark.parametrize("kind", ["dense", "moe"])
+def test_tp2_matches_single_process(kind):
+    eng = _build(0, 1, None, kind)
     from localai_tfp_amd.engine.sequence import Request
     from localai_tfp_amd.ops.sampling import SamplingParams
     hs = [eng.submit(Request(p, SamplingParams(temperature=0.0), 10)) for p in PROMPTS]
@@ -74,7 +88,7 @@ def test_tp2_matches_single_process():
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    ps = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    ps = [ctx.Process(target=_worker, args=(r, 2, port, q, kind)) for r in range(2)]
     for p in ps:
         p.start()
     import queue as _q
@@ -95,3 +109,61 @@ def test_tp2_matches_single_process():
                 p.kill()
     assert [len(o) for o in outs] == [10, 10]
     assert outs == ref
+
+
+def test_plan_codec_roundtrip():
+    import numpy as np
+    from localai_tfp_amd.parallel.tp_engine import decode_plan, encode_plan
+    rng = np.random.default_rng(0)
+    plan = {"nd": 3, "tokens": rng.integers(0, 999, 9).astype(np.int32), "positions": np.arange(9, dtype=np.int32),
+            "slots": np.arange(9, dtype=np.int32) + 16, "lidx": np.array([0, 1, 2, 8], np.int32),
+            "dec_bt": rng.integers(0, 50, (3, 5)).astype(np.int32), "dec_lens": np.array([4, 5, 6], np.int32),
+            "pf_bt": rng.integers(0, 50, (1, 2)).astype(np.int32), "pf_cu": np.array([0, 6], np.int32),
+            "pf_ctx": np.array([6], np.int32), "keep_hidden": True, "graph": False,
+            "fix": (np.array([0, 2], np.int64), np.array([1, 0], np.int64))}
+    buf = encode_plan(plan)
+    assert buf.dtype == np.int32
+    out = decode_plan(buf)
+    assert out["nd"] == 3 and out["keep_hidden"] and not out["graph"]
+    for k in ("tokens", "positions", "slots", "lidx", "dec_bt", "dec_lens", "pf_bt", "pf_cu", "pf_ctx"):
+        assert np.array_equal(out[k], plan[k]) and out[k].shape == plan[k].shape, k
+    assert all(np.array_equal(a, b) for a, b in zip(out["fix"], plan["fix"]))
+    dec_only = decode_plan(encode_plan({"nd": 1, "tokens": np.array([5], np.int32), "positions": np.array([3], np.int32),
+                                        "slots": np.array([19], np.int32), "lidx": np.array([0], np.int32),
+                                        "graph": True}))
+    assert dec_only["graph"] and "pf_cu" not in dec_only and "fix" not in dec_only
+
+
+def _die_worker(rank, world, port, who):
+    link = _link(rank, world, port, timeout_s=6, heartbeat_s=0.5)
+    import time
+    if rank == who:
+        time.sleep(1.0)
+        os._exit(0)  # crash without tearing down the group
+    if rank == 0:  # leader: keep sending until the dead follower is noticed
+        for _ in range(200):
+            link.send_control("noop")
+            time.sleep(0.1)
+    else:
+        while True:
+            link.recv_control()
+
+
+@pytest.mark.parametrize("who", [0, 1])
+def test_dead_rank_exits_nonzero(who):
+    """A crashed leader (follower side) or follower (leader side) ends the survivor with
+    EXIT_TP_FAILURE within the group timeout instead of hanging it."""
+    from localai_tfp_amd.parallel.tp_engine import EXIT_TP_FAILURE
+    ctx = mp.get_context("spawn")
+    port = _port()
+    ps = [ctx.Process(target=_die_worker, args=(r, 2, port, who)) for r in range(2)]
+    for p in ps:
+        p.start()
+    for p in ps:
+        p.join(timeout=90)
+    alive = [p.is_alive() for p in ps]
+    for p in ps:
+        if p.is_alive():
+            p.kill()
+    assert not any(alive), alive
+    assert ps[1 - who].exitcode == EXIT_TP_FAILURE, [p.exitcode for p in ps]
