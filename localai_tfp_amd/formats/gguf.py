@@ -67,12 +67,23 @@ class QType(IntEnum):
     Q5_K = 13
     Q6_K = 14
     Q8_K = 15
+    IQ2_XXS = 16
+    IQ2_XS = 17
+    IQ3_XXS = 18
+    IQ1_S = 19
+    IQ4_NL = 20
+    IQ3_S = 21
+    IQ2_S = 22
+    IQ4_XS = 23
     I8 = 24
     I16 = 25
     I32 = 26
     I64 = 27
     F64 = 28
+    IQ1_M = 29
     BF16 = 30
+    TQ1_0 = 34
+    TQ2_0 = 35
 
 
 # (elements per block, bytes per block)
@@ -83,6 +94,9 @@ BLOCK = {
     QType.Q8_0: (32, 34), QType.Q8_1: (32, 36),
     QType.Q2_K: (256, 84), QType.Q3_K: (256, 110), QType.Q4_K: (256, 144), QType.Q5_K: (256, 176),
     QType.Q6_K: (256, 210), QType.Q8_K: (256, 292),
+    QType.IQ2_XXS: (256, 66), QType.IQ2_XS: (256, 74), QType.IQ3_XXS: (256, 98), QType.IQ1_S: (256, 50),
+    QType.IQ4_NL: (32, 18), QType.IQ3_S: (256, 110), QType.IQ2_S: (256, 82), QType.IQ4_XS: (256, 136),
+    QType.IQ1_M: (256, 56), QType.TQ1_0: (256, 54), QType.TQ2_0: (256, 66),
 }
 
 # GGUF file-type ids (general.file_type) for naming

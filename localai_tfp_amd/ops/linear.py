@@ -14,6 +14,7 @@ numerics oracle for the HIP kernels.
 """
 from __future__ import annotations
 
+import logging
 import os
 
 import numpy as np
@@ -22,6 +23,8 @@ import torch
 from .. import _native as N
 from ..formats.gguf import QType
 from . import quant as Q
+
+log = logging.getLogger("localai_tfp_amd.ops")
 
 EPI_F32, EPI_BF16, EPI_ADD_F32, EPI_SWIGLU, EPI_GEGLU = 0, 1, 2, 3, 4
 GLU_EPIS = (EPI_SWIGLU, EPI_GEGLU)  # gated-FFN epilogues over 16-row interleaved gate|up weights
@@ -51,22 +54,31 @@ class QWeight:
         self._dense_f32: torch.Tensor | None = None
         self.bf16_cache: torch.Tensor | None = None
         self.layout = "ggml"  # "ggml" (GPU-native block rows) | "t32" (tiled, ops/quant.py tile32)
+        self.src_qtype = raw_qtype  # block format of the checkpoint (Q4_0 etc. run as Q8_0: see Q8_EXACT)
 
     # ---------------------------------------------------------------- construction
     @classmethod
     def from_ggml(cls, raw: np.ndarray, qtype: int, N_: int, K: int, device="cpu", name: str = "",
                   dense_dtype=torch.bfloat16):
-        qt = QType(qtype)
+        qt = raw_qtype_in = QType(qtype)
         dev = torch.device(device)
         if dev.type == "cpu":
             # CPU: keep the ggml bytes, dequantise lazily for the reference path
             return cls(N_, K, int(qt) if qt in Q.GPU_NATIVE else "dense",
                        torch.empty(0), None, np.asarray(raw), int(qt), name)
+        if qt in (*Q.Q8_EXACT, *Q.Q8_REQUANT) and K % 256 == 0:
+            # no dedicated layout for this block format: carried on the Q8_0 kernels, never densified
+            raw, qt = Q.to_q8_0(raw, qt, N_, K), QType.Q8_0
         if qt in Q.GPU_NATIVE and K % 256 == 0:
             data, dpl = Q.repack_for_gpu(raw, qt, N_, K)
             t = torch.from_numpy(np.ascontiguousarray(data)).to(dev)
             d = torch.from_numpy(np.ascontiguousarray(dpl).view(np.int16)).to(dev) if dpl is not None else None
-            return cls(N_, K, int(qt), t, d, None, int(qt), name)
+            w = cls(N_, K, int(qt), t, d, None, int(qt), name)
+            w.src_qtype = int(QType(raw_qtype_in))
+            return w
+        if qt not in (QType.F32, QType.F16, QType.BF16):
+            log.warning("%s: %s weight with K=%d densified to 16 bits (no quantised kernel layout for it)",
+                        name, qt.name, K)
         dense = Q.dequantize(raw, qt, (K, N_))
         t = torch.from_numpy(dense).to(dev, dense_dtype)
         return cls(N_, K, "dense", t, None, None, int(qt), name)

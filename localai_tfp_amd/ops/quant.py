@@ -223,7 +223,40 @@ def dq_q6_k(raw):
     return ((q - 32).astype(np.float32) * s).reshape(-1)
 
 
+# IQ4_NL / IQ4_XS: 4-bit indices into a fixed non-linear int8 codebook (ggml kvalues_iq4nl)
+IQ4_KVALUES = np.array([-127, -104, -83, -65, -49, -35, -22, -10, 1, 13, 25, 38, 53, 69, 89, 113], np.int8)
+
+
+def _iq4_codes(qs):
+    """[nb, 16] packed nibbles -> [nb, 32] codebook values (low nibbles first, as ggml)."""
+    return IQ4_KVALUES[np.concatenate([qs & 0xF, qs >> 4], 1)]
+
+
+def dq_iq4_nl(raw):
+    b = _blocks(raw, QType.IQ4_NL)
+    d = _f16(b[:, 0:2].copy())
+    return (_iq4_codes(b[:, 2:18]).astype(np.float32) * d[:, None]).reshape(-1)
+
+
+def iq4_xs_scales(b):
+    """[nb, 136] IQ4_XS blocks -> per-32 scales d * (ls - 32), float32 [nb, 8]."""
+    d = _f16(b[:, 0:2].copy())
+    sh = b[:, 2:4].copy().view(np.uint16).reshape(-1).astype(np.int32)
+    sl = b[:, 4:8].astype(np.int32)
+    ib = np.arange(8)
+    ls = ((sl[:, ib // 2] >> (4 * (ib % 2))) & 0xF) | (((sh[:, None] >> (2 * ib)) & 3) << 4)
+    return d[:, None] * (ls - 32).astype(np.float32)
+
+
+def dq_iq4_xs(raw):
+    b = _blocks(raw, QType.IQ4_XS)
+    dl = iq4_xs_scales(b)
+    codes = _iq4_codes(b[:, 8:136].reshape(-1, 16)).reshape(-1, 8, 32).astype(np.float32)
+    return (codes * dl[:, :, None]).reshape(-1)
+
+
 _DQ = {
+    QType.IQ4_NL: dq_iq4_nl, QType.IQ4_XS: dq_iq4_xs,
     QType.Q4_0: dq_q4_0, QType.Q4_1: dq_q4_1, QType.Q5_0: dq_q5_0, QType.Q5_1: dq_q5_1,
     QType.Q8_0: dq_q8_0, QType.Q2_K: dq_q2_k, QType.Q3_K: dq_q3_k, QType.Q4_K: dq_q4_k,
     QType.Q5_K: dq_q5_k, QType.Q6_K: dq_q6_k,
@@ -244,7 +277,9 @@ def dequantize(raw: np.ndarray, qtype: int, shape) -> np.ndarray:
         u = raw.reshape(-1).view(np.uint16).astype(np.uint32) << 16
         return u.view(np.float32).reshape(np_shape)
     if q not in _DQ:
-        raise NotImplementedError(f"dequantize {q.name}")
+        raise NotImplementedError(f"dequantize {q.name}" + (": the IQ1/IQ2/IQ3 codebook grids are not built into this "
+                                                           "framework; re-quantise the model to a K-quant or IQ4"
+                                                           if q.name.startswith(("IQ", "TQ")) else ""))
     return _DQ[q](raw.reshape(-1).view(np.uint8)).reshape(np_shape)
 
 
@@ -384,6 +419,40 @@ def repack_q8_0(raw: np.ndarray, n_rows: int, row_len: int):
 
 
 GPU_NATIVE = (QType.Q4_K, QType.Q6_K, QType.Q8_0)
+
+# Block formats without a dedicated kernel layout yet, carried on the Q8_0 kernels (qmm / qmv) instead of
+# a dense 16-bit copy: the integer code of every weight is kept EXACTLY where the format is "scale x
+# small int" per <= 32 weights (Q4_0, Q5_0, IQ4_NL; Q3_K's (sc-32)(q-4) fits int8 against the
+# super-block d; IQ4_XS up to the f16 rounding of its per-32 scale); the offset formats (Q4_1, Q5_1,
+# Q2_K, Q5_K) are re-quantised to 8 bits (error ~1/254 of the block max, well under their own).
+Q8_EXACT = (QType.Q4_0, QType.Q5_0, QType.IQ4_NL, QType.IQ4_XS, QType.Q3_K)
+Q8_REQUANT = (QType.Q4_1, QType.Q5_1, QType.Q2_K, QType.Q5_K)
+
+
+def to_q8_0(raw: np.ndarray, qtype: int, n_rows: int, row_len: int) -> np.ndarray:
+    """ggml rows of another block format -> Q8_0 rows [n_rows, row_len/32 * 34] (see Q8_EXACT)."""
+    q = QType(qtype)
+    w = dequantize(raw, q, (row_len, n_rows)).reshape(-1, 32)
+    if q not in Q8_EXACT:
+        return quantize_q8_0(w).reshape(n_rows, -1)
+    b = _blocks(np.asarray(raw).reshape(-1).view(np.uint8), q)
+    if q in (QType.Q4_0, QType.Q5_0, QType.IQ4_NL):
+        dd = _f16(b[:, 0:2].copy())                          # one block = 32 weights
+    elif q == QType.Q3_K:
+        dd = np.repeat(_f16(b[:, 108:110].copy()), 8)        # super-block d for its 8 x 32 weights
+    else:  # IQ4_XS
+        dd = iq4_xs_scales(b).reshape(-1)
+    d16 = dd.astype(np.float16)
+    safe = np.where(d16.astype(np.float32) != 0, d16.astype(np.float32), 1.0)
+    ci = np.rint(w / safe[:, None])
+    codes = np.clip(ci, -127, 127).astype(np.int8)
+    out = np.empty((w.shape[0], 34), np.uint8)
+    out[:, 0:2] = d16.view(np.uint8).reshape(-1, 2)
+    out[:, 2:] = codes.view(np.uint8)
+    over = np.abs(ci).max(1) > 127  # Q3_K's (-32)(-4) = 128 corner: that block re-quantised to 8 bits
+    if over.any():
+        out[over] = quantize_q8_0(w[over]).reshape(-1, 34)
+    return out.reshape(n_rows, -1)
 
 
 def repack_for_gpu(raw: np.ndarray, qtype: int, n_rows: int, row_len: int):
