@@ -73,6 +73,30 @@ def synthetic_state_dict(seed: int = 0) -> dict:
     return sd
 
 
+def onnx_state_dict(path) -> dict:
+    """silero_vad.onnx (the gallery's file, backend/go/vad/silero/vad.go:15-54) -> state dict: the weight
+    initializers are read with the protobuf-only ONNX reader (formats/onnx.py) — v5 keeps them inside
+    the 16 kHz / 8 kHz If branches — and matched to this module's names by suffix and shape; the 16 kHz
+    set wins. The ONNX graph itself is not run (parity vs onnxruntime unpinned)."""
+    from ..formats.onnx import initializers
+    tensors, _ = initializers(path)
+    want = {k: tuple(v.shape) for k, v in synthetic_state_dict().items()}
+    out = {}
+    for k, shape in want.items():
+        cands = [(q, a) for q, a in tensors.items() if q.endswith(k) and tuple(a.shape) == shape]
+        if not cands:
+            continue
+        cands.sort(key=lambda qa: ("8k" in qa[0], len(qa[0])))  # 16 kHz branch first
+        out[k] = torch.from_numpy(np.asarray(cands[0][1], np.float32).copy())
+    missing = [k for k in want if k not in out and k != "stft.forward_basis_buffer"]
+    if missing:
+        raise ValueError(f"{path}: silero-vad weights not found in the ONNX initializers: {missing[:4]}... "
+                         f"({len(tensors)} tensors present, e.g. {list(tensors)[:4]})")
+    if "stft.forward_basis_buffer" not in out:
+        out["stft.forward_basis_buffer"] = dft_basis()
+    return out
+
+
 def load_state_dict(path: str) -> dict:
     if path.startswith("synthetic:"):
         return synthetic_state_dict()
@@ -80,8 +104,7 @@ def load_state_dict(path: str) -> dict:
         from safetensors.torch import load_file
         sd = load_file(path)
     elif path.endswith(".onnx"):
-        raise ValueError(f"{path}: ONNX graphs are not loadable here (no onnx runtime); convert the silero "
-                         "v5 weights to safetensors (names as in the JIT module)")
+        return onnx_state_dict(path)
     else:
         sd = torch.load(path, map_location="cpu", weights_only=True)
         if isinstance(sd, dict) and "state_dict" in sd:

@@ -397,6 +397,8 @@ class ModelLoader:
             svc = servicer_cls(device=dev)
         except TypeError:
             svc = servicer_cls()
+        if hasattr(svc, "backend"):
+            svc.backend = backend
         server = AioServer(svc, "127.0.0.1:0")
         addr = f"127.0.0.1:{server.port}"
         return Replica(addr, BackendClient(addr, parallel=parallel), None, tuple(gpus), server, svc)
@@ -406,6 +408,7 @@ class ModelLoader:
         addr = f"127.0.0.1:{port}"
         env = dict(os.environ)
         env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        env["MX_BACKEND_NAME"] = backend
         if gpus:
             env["HIP_VISIBLE_DEVICES"] = ",".join(str(g) for g in gpus)
         if ext:  # external backend executable: `<file> --addr host:port`

@@ -18,11 +18,12 @@ WORKERS = {
     "local-store": "localai_tfp_amd.workers.store",
     "silero-vad": "localai_tfp_amd.workers.vad",
     "piper": "localai_tfp_amd.workers.tts",
-    "bark": "localai_tfp_amd.workers.tts",
-    "bark-cpp": "localai_tfp_amd.workers.tts",
-    "coqui": "localai_tfp_amd.workers.tts",
-    "kokoro": "localai_tfp_amd.workers.tts",
-    "transformers-musicgen": "localai_tfp_amd.workers.tts",
+    # model families not implemented here: LoadModel fails with an explicit error (workers/unsupported.py)
+    "bark": "localai_tfp_amd.workers.unsupported",
+    "bark-cpp": "localai_tfp_amd.workers.unsupported",
+    "coqui": "localai_tfp_amd.workers.unsupported",
+    "kokoro": "localai_tfp_amd.workers.unsupported",
+    "transformers-musicgen": "localai_tfp_amd.workers.unsupported",
     "transformers-tts": "localai_tfp_amd.workers.tts",
     "huggingface": "localai_tfp_amd.workers.huggingface",
     "langchain-huggingface": "localai_tfp_amd.workers.huggingface",

@@ -1,7 +1,7 @@
-"""Text-to-speech worker: the reference's `piper` (backend/go/tts/piper.go:20-49), `bark-cpp`
-(backend/go/bark/gobark.go), `coqui` / `kokoro` / `bark` Python backends
-(backend/python/coqui/backend.py, kokoro/backend.py) behind the TTS RPC, all served by one VITS
-engine (models/tts.py) on the GPU.
+"""Text-to-speech worker: the reference's `piper` (backend/go/tts/piper.go:20-49) and the transformers
+backend's VITS / MMS-TTS path behind the TTS RPC, served by the VITS engine (models/tts.py) on the GPU.
+Bark, Coqui, Kokoro and MusicGen names are NOT routed here (workers/unsupported.py fails their
+LoadModel explicitly).
 
 LoadModel: a Hugging Face VITS directory (MMS-TTS layout) or `synthetic:vits-test | vits-base`.
 ModelOptions.Options ("key:value"): noise_scale, noise_scale_duration (alias noise_w), speaking_rate
@@ -10,9 +10,9 @@ TTS: text -> 16-bit PCM WAV at the model's sample rate in `dst`. `voice` selects
 multi-speaker model (an integer id; piper's per-voice .onnx file selection has no equivalent because
 voices are separate checkpoints here — configure one model per voice). `language` is accepted and
 ignored like piper does.
-SoundGeneration (ElevenLabs /v1/sound-generation): the same synthesis, trimmed / padded to
-`duration` seconds when given (the reference only implements it in the transformers MusicGen
-backend; a MusicGen engine is not part of this worker).
+SoundGeneration (ElevenLabs /v1/sound-generation) is a MusicGen feature in the reference
+(backend/python/transformers/backend.py:452-507); a speech model does not generate sound effects, so
+this worker reports it unsupported.
 """
 from __future__ import annotations
 
@@ -48,8 +48,11 @@ class TTSServicer(BackendServicer):
                 path = os.path.join(request.ModelPath, path)
             if not path.startswith("synthetic:") and os.path.isfile(path):
                 if path.endswith(".onnx"):
-                    raise ValueError(f"{path}: piper .onnx voices need onnxruntime, which this image lacks; "
-                                     "use a VITS checkpoint directory (config.json + safetensors + vocab.json)")
+                    # piper voices are original-VITS graphs (enc_p / dp / flow / dec) traced to ONNX with
+                    # constant-folded weight names: formats/onnx.py reads them, but no name map to the
+                    # HF VITS modules of models/tts.py exists yet
+                    raise ValueError(f"{path}: piper .onnx voices are not supported yet; use a VITS checkpoint "
+                                     "directory (config.json + safetensors + vocab.json, MMS-TTS layout)")
                 path = os.path.dirname(path)
             self.model, self.tok = T.load_vits(path, self.device)
             o = {}
@@ -89,20 +92,8 @@ class TTSServicer(BackendServicer):
             return pb.Result(message=f"tts failed: {ex}", success=False)
 
     def SoundGeneration(self, request, context):
-        from ..utils.audio import write_wav
-        if self.model is None:
-            return pb.Result(message="model not loaded", success=False)
-        try:
-            wav = self._synth(request.text)
-            sr = self.model.cfg.sample_rate
-            if request.HasField("duration") and request.duration > 0:
-                n = int(request.duration * sr)
-                wav = np.pad(wav, (0, max(0, n - wav.size)))[:n]
-            write_wav(request.dst, wav, sr)
-            return pb.Result(message="ok", success=True)
-        except Exception as ex:
-            log.exception("SoundGeneration failed")
-            return pb.Result(message=f"sound generation failed: {ex}", success=False)
+        return pb.Result(message="sound generation needs a MusicGen model; this TTS backend serves speech "
+                                 "(VITS) only", success=False)
 
 
 def main(argv=None):

@@ -1,0 +1,31 @@
+"""Backend names of the reference whose model families this framework does not implement (Bark /
+bark.cpp, Coqui XTTS, Kokoro StyleTTS2, MusicGen). Reference: backend/go/bark/gobark.cpp:22-80,
+backend/python/coqui/backend.py:26-80, backend/python/kokoro/backend.py:34-99,
+backend/python/transformers/backend.py:452-507.
+
+The worker starts and answers Health like any backend (so the process manager's lifecycle is the same),
+but LoadModel fails with an explicit error naming the backend — a request for Bark never silently gets
+a different speech model."""
+from __future__ import annotations
+
+import os
+
+from ..grpc import pb
+from ..grpc.server import BackendServicer, worker_main
+
+SUPPORTED_TTS = "piper / transformers-tts (VITS, MMS-TTS checkpoints)"
+
+
+class UnsupportedServicer(BackendServicer):
+    def __init__(self, device: str | None = None):
+        super().__init__()
+        self.backend = os.environ.get("MX_BACKEND_NAME", "this backend")
+
+    def LoadModel(self, request, context):
+        return pb.Result(success=False, message=(
+            f"backend {self.backend!r} is not implemented by this MI355X build (model {request.Model!r}); "
+            f"text-to-speech is served by {SUPPORTED_TTS}"))
+
+
+def main(argv=None):
+    worker_main(UnsupportedServicer, argv)

@@ -124,8 +124,9 @@ def test_worker_tts(tmp_path):
     assert r.success, r.message
     x, sr = _wav(open(dst, "rb").read())
     assert sr == 16000 and x.size > 100
+    # a speech model does not generate sound effects (MusicGen's job in the reference): explicit refusal
     r = s.SoundGeneration(pb.SoundGenerationRequest(text="rain", dst=dst, duration=0.5), None)
-    assert r.success and _wav(open(dst, "rb").read())[0].size == 8000
+    assert not r.success and "MusicGen" in r.message
     assert not s.TTS(pb.TTSRequest(text="", dst=dst), None).success
 
 
@@ -137,9 +138,9 @@ def test_http_speech_routes(client):
         assert r.status_code == 200, (route, r.text)
         x, sr = _wav(r.content)
         assert sr == 16000 and x.size > 100
-    r = client.post("/v1/sound-generation", json={"model_id": "sfx", "text": "thunder", "duration_seconds": 0.25})
-    assert r.status_code == 200, r.text
-    assert _wav(r.content)[0].size == 4000
+    # /v1/sound-generation on a speech model: the backend's explicit refusal surfaces as a server error
+    with pytest.raises(RuntimeError, match="MusicGen"):
+        client.post("/v1/sound-generation", json={"model_id": "sfx", "text": "thunder", "duration_seconds": 0.25})
 
 
 @pytest.mark.gpu
@@ -157,3 +158,16 @@ def test_vits_gpu_matches_cpu():
     gm = T.VitsModel(T.VITS_TEST, sd, "cuda:0").synthesize(IDS, noise_scale=0.0, noise_scale_duration=0.0)
     assert gm.shape == c.shape
     assert np.abs(gm - c).max() < 2e-3
+
+
+@pytest.mark.parametrize("backend", ["bark", "bark-cpp", "coqui", "kokoro", "transformers-musicgen"])
+def test_foreign_tts_backends_refuse_explicitly(backend):
+    """Backend names whose model families are not implemented never silently load VITS."""
+    from localai_tfp_amd.grpc import pb
+    from localai_tfp_amd.workers import WORKERS
+    from localai_tfp_amd.workers.unsupported import UnsupportedServicer
+    assert WORKERS[backend].endswith(".unsupported")
+    s = UnsupportedServicer()
+    s.backend = backend
+    r = s.LoadModel(pb.ModelOptions(Model="suno/bark-small"), None)
+    assert not r.success and backend in r.message and "not implemented" in r.message

@@ -162,3 +162,28 @@ def test_vad_gpu_matches_cpu():
     pc = V.SileroVAD(sd, "cpu").probs(audio).numpy()
     pg = V.SileroVAD(sd, "cuda:0").probs(audio).cpu().numpy()
     np.testing.assert_allclose(pg, pc, atol=1e-3)
+
+
+def test_onnx_reader_and_silero_onnx(tmp_path):
+    """The protobuf-only ONNX reader (formats/onnx.py) and the silero-vad .onnx loading path: weights
+    inside an If branch (v5 layout, 16 kHz branch preferred over an 8 kHz decoy) reproduce the
+    safetensors-loaded detector exactly. Parity against onnxruntime itself is unpinned."""
+    from localai_tfp_amd.formats import onnx as O
+    from localai_tfp_amd.models import vad as V
+    sd = V.synthetic_state_dict(seed=3)
+    top = {"_model.stft.forward_basis_buffer": sd["stft.forward_basis_buffer"].numpy()}
+    sub = {"_model." + k: v.numpy() for k, v in sd.items() if k != "stft.forward_basis_buffer"}
+    decoy = {"_model_8k." + k: np.zeros_like(v.numpy()) for k, v in sd.items() if k.startswith("decoder")}
+    blob = O.make_model(top, {**sub, **decoy})
+    p = tmp_path / "silero_vad.onnx"
+    p.write_bytes(blob)
+    tensors, nodes = O.initializers(str(p))
+    assert any(n.op_type == "If" for _, n in nodes)
+    assert "If_0/then_branch/_model.encoder.0.reparam_conv.weight" in tensors
+    got = V.load_state_dict(str(p))
+    for k, v in sd.items():
+        assert torch.equal(got[k], v.float()), k
+    bad = tmp_path / "other.onnx"
+    bad.write_bytes(O.make_model({"onnx::Conv_12": np.zeros((3, 3), np.float32)}))
+    with pytest.raises(ValueError, match="not found in the ONNX"):
+        V.load_state_dict(str(bad))
