@@ -22,6 +22,7 @@ from dataclasses import dataclass
 import numpy as np
 import torch
 
+from ..utils import roctx
 from ..models.llama import ForwardBatch, LlamaModel, Workspace
 from ..ops.sampling import SamplerBatch
 from .kv_cache import KVCache, make_block_manager
@@ -367,6 +368,12 @@ class LLMEngine:
 
     # ------------------------------------------------------------------ one iteration
     def step(self):
+        if roctx.ENABLED:
+            with roctx.range(f"engine.step {self.stats['steps']}"):
+                return self._step()
+        return self._step()
+
+    def _step(self):
         t0 = time.perf_counter()
         so = self.sched.schedule()
         for s in so.preempted:
@@ -399,6 +406,8 @@ class LLMEngine:
                 st["busy_s"] += time.perf_counter() - t0
                 return
         t1 = time.perf_counter()
+        if roctx.ENABLED:
+            roctx.mark(f"decode={len(so.decode)} prefill={sum(p.n for p in so.prefill)}")
         toks, lps = self._forward_and_sample(so)
         t2 = time.perf_counter()
         self.sched.commit(so)

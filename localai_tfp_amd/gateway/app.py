@@ -9,6 +9,7 @@ from __future__ import annotations
 
 import contextlib
 import hmac
+import asyncio
 import logging
 import re
 import time
@@ -22,16 +23,7 @@ from .state import Application
 
 log = logging.getLogger("localai_tfp_amd.gateway")
 
-try:
-    import prometheus_client as prom
-    _REGISTRY = prom.CollectorRegistry()
-    API_LATENCY = prom.Histogram("api_call", "duration of API calls", ["method", "path"], registry=_REGISTRY,
-                                 buckets=(0.005, 0.01, 0.025, 0.05, 0.1, 0.25, 0.5, 1, 2.5, 5, 10, 30, 60, 120))
-except ImportError:  # pragma: no cover
-    prom = None
-    _REGISTRY = None
-    API_LATENCY = None
-
+from .observability import API_LATENCY, REGISTRY as _REGISTRY, prom
 
 def _error(status: int, msg: str, typ: str = "invalid_request_error") -> JSONResponse:
     return JSONResponse({"error": {"code": status, "message": msg, "type": typ}}, status_code=status)
@@ -155,6 +147,9 @@ def create_app(cfg: ApplicationConfig | None = None, inproc: bool | None = None,
     async def metrics():
         if prom is None:
             return PlainTextResponse("", status_code=404)
+        from . import observability as obs
+        await obs.scrape_backends(state)
+        await asyncio.to_thread(obs.export_gpu_metrics)
         return PlainTextResponse(prom.generate_latest(_REGISTRY).decode(), media_type=prom.CONTENT_TYPE_LATEST)
 
     from . import localai as localai_routes

@@ -252,15 +252,10 @@ async def system(request: Request):
     from .. import workers as W
     a = app_of(request)
     loaded = [{"id": n} for n in a.loader.list_loaded()]
-    gpus = []
-    try:
-        import torch
-        for i in range(torch.cuda.device_count()):
-            p = torch.cuda.get_device_properties(i)
-            gpus.append({"index": i, "name": p.name, "total_memory": p.total_memory,
-                         "arch": getattr(p, "gcnArchName", "")})
-    except Exception:
-        pass
+    import asyncio
+    from .observability import gpu_metrics
+    # AMD SMI (driver interface: utilisation, HBM use, power, temperature) — no HIP context in the gateway
+    gpus = await asyncio.to_thread(gpu_metrics)
     return {"backends": sorted(W.WORKERS), "loaded_models": loaded, "gpus": gpus}
 
 

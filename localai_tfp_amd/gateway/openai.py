@@ -19,6 +19,7 @@ from fastapi.responses import JSONResponse, Response
 from .. import functions as F
 from ..config.model_config import FLAG_CHAT, FLAG_COMPLETION, FLAG_EDIT, FLAG_EMBEDDINGS
 from ..templates.evaluator import COMPLETION, EDIT
+from .observability import StreamTimer
 from .inference import LLMResponse, TokenUsage, finetune
 from .request import OpenAIRequest, RequestError, merge_request
 
@@ -264,15 +265,23 @@ async def _chat_stream(a, req, cfg, prompt, base, extra_usage, include_usage):
     yield sse({**base, "object": "chat.completion.chunk",
                "choices": [{"index": 0, "finish_reason": None, "delta": {"role": "assistant", "content": ""}}]})
     imgs, vids, auds = _media(req)
+    timer = StreamTimer(getattr(cfg, "name", "") or req.model)
+    ok = True
     try:
         for _ in range(req.n or 1):
+            seen = 0
             async for text, u in a.inference.predict_stream(cfg, prompt, req.messages, imgs, vids, auds,
                                                             req.correlation_id):
                 usage = u
+                timer.chunk(max(1, u.completion - seen) if u.completion else 1)
+                seen = u.completion or seen
                 yield fmt.content(text, u)
     except Exception as ex:  # surface as an error event, then terminate the stream cleanly
+        ok = False
         log.error("chat stream failed: %s", ex)
         yield sse({"error": {"message": str(ex), "type": "server_error"}})
+    finally:
+        timer.close(ok)
     yield sse({**base, "object": "chat.completion.chunk",
                "choices": [{"index": 0, "finish_reason": "stop", "delta": {"content": ""}}],
                "usage": usage.openai(extra_usage)})
@@ -377,13 +386,21 @@ async def _completion_stream(a, req, cfg, prompt, base, extra_usage):
     pre = ("data: " + head + ',"choices":[{"index":0,"finish_reason":null,"text":').encode()
     fmt = _ChunkFmt(base, "text_completion", extra_usage)
     usage = TokenUsage()
+    timer = StreamTimer(getattr(cfg, "name", "") or req.model)
+    ok = True
     try:
+        seen = 0
         async for text, u in a.inference.predict_stream(cfg, prompt, req.messages, (), (), (), req.correlation_id):
             usage = u
+            timer.chunk(max(1, u.completion - seen) if u.completion else 1)
+            seen = u.completion or seen
             yield pre + _dumps(text).encode() + b'}],"usage":' + fmt.usage(u) + b"}\n\n"
     except Exception as ex:
+        ok = False
         log.error("completion stream failed: %s", ex)
         yield sse({"error": {"message": str(ex), "type": "server_error"}})
+    finally:
+        timer.close(ok)
     yield sse({**base, "object": "text_completion", "choices": [{"index": 0, "finish_reason": "stop"}],
                "usage": usage.openai(extra_usage)})
     yield SSE_DONE

@@ -472,8 +472,19 @@ class LLMServicer(BackendServicer):
                 st.memory.breakdown["weights"] = int(e.model.weight_bytes())
         except Exception:
             pass
-        for k in ("prompt_tokens_total", "gen_tokens_total", "cached_tokens_total", "preemptions"):
+        for k in ("prompt_tokens_total", "gen_tokens_total", "cached_tokens_total", "preemptions", "steps",
+                  "graph_steps", "finished"):
             st.memory.breakdown[k] = int(e.stats.get(k, 0))
+        # engine state for the gateway's /metrics gauges (gateway/observability.py scrape_backends)
+        st.memory.breakdown["busy_ms"] = int(e.stats.get("busy_s", 0.0) * 1e3)
+        st.memory.breakdown["running_seqs"] = len(e.sched.running)
+        st.memory.breakdown["waiting_seqs"] = len(e.sched.waiting)
+        try:
+            nb = int(e.kv.num_blocks)
+            st.memory.breakdown["kv_blocks_total"] = nb
+            st.memory.breakdown["kv_blocks_used"] = nb - int(e.sched.bm.num_free)
+        except Exception:
+            pass
         return st
 
 

@@ -186,7 +186,18 @@ def test_monitor_metrics_shutdown(env):
     c.post("/v1/completions", json={"model": "tiny", "prompt": "x"})
     r = c.get("/backend/monitor", params={"model": "tiny"})
     assert r.status_code == 200 and "memory" in r.json()
-    assert "api_call" in c.get("/metrics").text
+    body = {"model": "tiny", "stream": True, "messages": [{"role": "user", "content": "metrics"}], "max_tokens": 6}
+    with c.stream("POST", "/v1/chat/completions", json=body) as r:
+        assert r.status_code == 200
+        for _ in r.iter_lines():
+            pass
+    m = c.get("/metrics").text
+    assert "api_call" in m
+    # serving metrics: client-observed TTFT / TPOT histograms, engine state scraped from the backend
+    assert 'localai_time_to_first_token_seconds_count{model="tiny"}' in m
+    assert 'localai_time_per_output_token_seconds_count{model="tiny"}' in m
+    assert 'localai_backend_state{key="kv_blocks_total",model="tiny"}' in m
+    assert 'localai_backend_state{key="steps",model="tiny"}' in m
     assert c.get("/v1/tokenMetrics", params={"model": "tiny"}).json()["tokens_generated"] > 0
     assert c.post("/backend/shutdown", json={"model": "tiny"}).status_code == 200
     assert a.loader.get("tiny") is None
