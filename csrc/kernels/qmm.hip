@@ -363,6 +363,12 @@ qmm_kernel(const uint16_t* __restrict__ A, int lda, const uint8_t* __restrict__ 
         qmm_wait_ahead<NI, NS - 2>(min(kt1 - 1, kt0 + NS - 2) - kt0);
         load_b(smem, bw, kt0 & 3);
         load_a(smem, KH, ar[0]);
+        f16x8 bcur[WN];
+#pragma unroll
+        for (int t = 0; t < WN; ++t) {
+            bw[t].prep(kt0 & 3);
+            bcur[t] = bw[t].template frag<KH>();
+        }
 
         int slot = 0;
         for (int kt = kt0; kt < kt1; ++kt) {
@@ -383,26 +389,41 @@ qmm_kernel(const uint16_t* __restrict__ A, int lda, const uint8_t* __restrict__ 
             // next-tile reads are unconditional (on the last tile they read a stale slot and are
             // discarded): one straight-line body keeps the compiler's LDS counter exact across the edge
             load_b(nb, bn, (kt + 1) & 3);
-#pragma unroll
-            for (int t = 0; t < WN; ++t) bw[t].prep(kt & 3);
-            // each k-step first issues the next k-step's A reads, then (sched_barrier: not sunk)
-            // dequantises its B fragment and runs its MFMAs
+            // Each k-step region: issue the A reads of the wave's next k-step, then run this k-step's
+            // MFMAs with the B fragment dequantised in the PREVIOUS region, interleaved (sched_group_barrier:
+            // one MFMA, then a slice of VALU) with the dequant of the next k-step's fragment — on the last
+            // k-step the next tile's scale prep + first fragment — so the VALU issue hides under the
+            // matrix pipe instead of serialising in front of it.
 #define QMM_KSTEP(J)                                                                                       \
     {                                                                                                      \
         constexpr int S = KH + KS * (J), CUR = (J) & 1;                                                    \
         constexpr bool LAST = S + KS >= 4;                                                                 \
         load_a(LAST ? nb : sb, LAST ? KH : S + KS, ar[CUR ^ 1]);                                           \
         __builtin_amdgcn_sched_barrier(0);                                                                 \
-        f16x8 b[WN];                                                                                       \
-        _Pragma("unroll") for (int t = 0; t < WN; ++t) b[t] = bw[t].template frag<S>();                    \
+        f16x8 bnx[WN];                                                                                     \
+        if constexpr (LAST) {                                                                              \
+            _Pragma("unroll") for (int t = 0; t < WN; ++t) {                                               \
+                bn[t].prep((kt + 1) & 3);                                                                  \
+                bnx[t] = bn[t].template frag<KH>();                                                        \
+            }                                                                                              \
+        } else {                                                                                           \
+            _Pragma("unroll") for (int t = 0; t < WN; ++t) bnx[t] = bw[t].template frag<(LAST ? KH : S + KS)>(); \
+        }                                                                                                  \
         _Pragma("unroll") for (int i = 0; i < WM; ++i)                                                     \
             _Pragma("unroll") for (int t = 0; t < WN; ++t) acc[i][t] =                                     \
-                __builtin_amdgcn_mfma_f32_32x32x16_f16(ar[CUR][i], b[t], acc[i][t], 0, 0, 0);              \
+                __builtin_amdgcn_mfma_f32_32x32x16_f16(ar[CUR][i], bcur[t], acc[i][t], 0, 0, 0);           \
+        _Pragma("unroll") for (int i = 0; i < WM * WN; ++i) {                                              \
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                                             \
+            __builtin_amdgcn_sched_group_barrier(0x002, (LAST ? 40 : 16) * WN / (WM * WN) + 1, 0);         \
+        }                                                                                                  \
+        __builtin_amdgcn_sched_barrier(0);                                                                 \
+        _Pragma("unroll") for (int t = 0; t < WN; ++t) bcur[t] = bnx[t];                                   \
     }
             QMM_KSTEP(0) QMM_KSTEP(1)
             if constexpr (KS == 1) { QMM_KSTEP(2) QMM_KSTEP(3) }
 #undef QMM_KSTEP
-            // an even number of k-steps per tile: the next tile's first A fragments are in ar[0]
+            // an even number of k-steps per tile: the next tile's first A fragments are in ar[0] and its
+            // first B fragment in bcur
 #pragma unroll
             for (int t = 0; t < WN; ++t) bw[t] = bn[t];
             slot = nslot;
