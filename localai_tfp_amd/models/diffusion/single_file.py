@@ -1,0 +1,407 @@
+"""stable-diffusion.cpp-style checkpoints: ONE file holding a model in its original training-code
+names — .safetensors, .ckpt or a GGUF with quantised tensors — plus optional separate component files
+given by the model options `clip_l_path`, `clip_g_path`, `t5xxl_path`, `vae_path`. Reference:
+backend/go/image/stablediffusion-ggml/gosd.cpp:56-162 (new_sd_ctx with those paths); the gallery's
+sd-ggml / flux-ggml configs (SD1.5 Q4_0 GGUF, Flux.1-dev Q2_K GGUF + ae / clip_l / t5xxl files).
+
+Families are recognised by their tensor names and mapped onto this framework's (diffusers-layout)
+modules:
+* Flux.1 (Black Forest Labs names: img_in, double_blocks.*, single_blocks.*, final_layer): fused
+  img/txt qkv and the single-block linear1 are split into q / k / v (/ mlp), the final adaLN's
+  (shift, scale) halves swapped to diffusers' (scale, shift);
+* SD1.x / SD2.x / SDXL (CompVis LDM / SGM UNet names under model.diffusion_model., via sgm_names);
+  CLIP-L from cond_stage_model.transformer. / conditioner.embedders.0.transformer., OpenCLIP-G
+  (conditioner.embedders.1.model.: fused in_proj split, c_fc / c_proj, transposed text_projection);
+* LDM VAE (first_stage_model. or a bare ae.safetensors): down/up/mid blocks renamed, up blocks
+  reversed, 1x1-conv attention weights flattened to linears.
+GGUF tensors are dequantised on load to the pipeline's 16-bit dtype (the diffusion GEMMs run on
+dense operands; the quantised-LLM kernels' t32 layouts are not used for these models yet).
+Tokenizer files (CLIP vocab.json + merges.txt, T5 spiece.model) are searched next to the model and
+component files; without them a byte-level stand-in is used and a warning logged.
+"""
+from __future__ import annotations
+
+import logging
+import os
+import re
+
+import numpy as np
+import torch
+
+log = logging.getLogger("localai_tfp_amd.diffusion")
+
+
+# ---------------------------------------------------------------- reading
+def read_tensors(path: str) -> dict[str, torch.Tensor]:
+    """All tensors of a .safetensors / .gguf / .ckpt|.pt file (fp32 for GGUF block formats)."""
+    if path.endswith(".safetensors"):
+        from safetensors import safe_open
+        out = {}
+        with safe_open(path, framework="pt") as f:
+            for k in f.keys():
+                out[k] = f.get_tensor(k)
+        return out
+    if path.endswith(".gguf"):
+        from ...formats.gguf import GGUFReader
+        from ...ops.quant import dequantize
+        r = GGUFReader(path)
+        out = {}
+        for name, ti in r.tensors.items():
+            a = dequantize(r.tensor_bytes(name), ti.qtype, ti.shape)
+            out[name] = torch.from_numpy(np.ascontiguousarray(a).reshape(tuple(reversed(ti.shape))).copy())
+        return out
+    sd = torch.load(path, map_location="cpu", weights_only=True)
+    if isinstance(sd, dict) and "state_dict" in sd:
+        sd = sd["state_dict"]
+    return dict(sd)
+
+
+def strip(sd: dict, prefix: str) -> dict:
+    return {k[len(prefix):]: v for k, v in sd.items() if k.startswith(prefix)}
+
+
+def detect(sd: dict) -> str:
+    keys = sd.keys()
+    if any(k.startswith(("double_blocks.", "model.diffusion_model.double_blocks.")) for k in keys):
+        return "flux"
+    if any(".joint_blocks." in k or k.startswith("joint_blocks.") for k in keys):
+        return "sd3"
+    if any(k.startswith("model.diffusion_model.label_emb.") for k in keys):
+        return "sdxl"
+    if any(k.startswith("model.diffusion_model.input_blocks.") for k in keys):
+        return "sd1"
+    raise ValueError("unrecognised single-file diffusion checkpoint (no Flux / SD3 / SD UNet tensor names)")
+
+
+# ---------------------------------------------------------------- LDM VAE
+def ldm_vae_to_diffusers(sd: dict) -> dict:
+    """first_stage_model.* (prefix already stripped) / ae.safetensors names -> AutoencoderKL names."""
+    n_up = 1 + max((int(m.group(1)) for k in sd for m in [re.match(r"decoder\.up\.(\d+)\.", k)] if m), default=-1)
+    out = {}
+    res = {"nin_shortcut": "conv_shortcut"}
+    attn = {"norm": "group_norm", "q": "to_q", "k": "to_k", "v": "to_v", "proj_out": "to_out.0"}
+    for k, v in sd.items():
+        nk = None
+        m = re.match(r"(encoder|decoder)\.(.*)$", k)
+        if m:
+            side, rest = m.groups()
+            mm = re.match(r"down\.(\d+)\.block\.(\d+)\.(\w+)\.(weight|bias)$", rest)
+            mu = re.match(r"up\.(\d+)\.block\.(\d+)\.(\w+)\.(weight|bias)$", rest)
+            if mm:
+                nk = f"{side}.down_blocks.{mm[1]}.resnets.{mm[2]}.{res.get(mm[3], mm[3])}.{mm[4]}"
+            elif mu:
+                nk = f"{side}.up_blocks.{n_up - 1 - int(mu[1])}.resnets.{mu[2]}.{res.get(mu[3], mu[3])}.{mu[4]}"
+            elif re.match(r"down\.(\d+)\.downsample\.conv\.", rest):
+                i = rest.split(".")[1]
+                nk = f"{side}.down_blocks.{i}.downsamplers.0.conv.{rest.split('.')[-1]}"
+            elif re.match(r"up\.(\d+)\.upsample\.conv\.", rest):
+                i = int(rest.split(".")[1])
+                nk = f"{side}.up_blocks.{n_up - 1 - i}.upsamplers.0.conv.{rest.split('.')[-1]}"
+            elif (mb := re.match(r"mid\.block_(\d)\.(\w+)\.(weight|bias)$", rest)):
+                nk = f"{side}.mid_block.resnets.{int(mb[1]) - 1}.{res.get(mb[2], mb[2])}.{mb[3]}"
+            elif (ma := re.match(r"mid\.attn_1\.(\w+)\.(weight|bias)$", rest)):
+                nk = f"{side}.mid_block.attentions.0.{attn[ma[1]]}.{ma[2]}"
+                if ma[1] != "norm" and v.dim() == 4:
+                    v = v[:, :, 0, 0]
+            elif rest.startswith("norm_out."):
+                nk = f"{side}.conv_norm_out.{rest.split('.')[-1]}"
+            elif rest.startswith(("conv_in.", "conv_out.")):
+                nk = f"{side}.{rest}"
+        elif k.startswith(("quant_conv.", "post_quant_conv.")):
+            nk = k
+        if nk is not None:
+            out[nk] = v
+    return out
+
+
+def vae_config_from(sd: dict, scaling: float, shift: float):
+    from .vae import VAEConfig
+    lat = int(sd["decoder.conv_in.weight"].shape[1])
+    levels = sorted({int(m.group(1)) for k in sd for m in [re.match(r"encoder\.down_blocks\.(\d+)\.resnets", k)] if m})
+    ch = tuple(int(sd[f"encoder.down_blocks.{i}.resnets.0.conv1.weight"].shape[0]) for i in levels)
+    layers = 1 + max(int(m.group(1)) for k in sd for m in [re.match(r"encoder\.down_blocks\.0\.resnets\.(\d+)\.", k)] if m)
+    return VAEConfig(latent=lat, channels=ch, layers=layers, groups=32, scaling=scaling, shift=shift,
+                     quant_conv="quant_conv.weight" in sd)
+
+
+# ---------------------------------------------------------------- Flux (BFL names)
+def bfl_flux_to_diffusers(sd: dict) -> dict:
+    sd = strip(sd, "model.diffusion_model.") or sd
+    d = int(sd["img_in.weight"].shape[0])
+    top = {"img_in": "x_embedder", "txt_in": "context_embedder",
+           "time_in.in_layer": "time_text_embed.timestep_embedder.linear_1",
+           "time_in.out_layer": "time_text_embed.timestep_embedder.linear_2",
+           "vector_in.in_layer": "time_text_embed.text_embedder.linear_1",
+           "vector_in.out_layer": "time_text_embed.text_embedder.linear_2",
+           "guidance_in.in_layer": "time_text_embed.guidance_embedder.linear_1",
+           "guidance_in.out_layer": "time_text_embed.guidance_embedder.linear_2",
+           "final_layer.linear": "proj_out"}
+    dbl = {"img_mod.lin": "norm1.linear", "txt_mod.lin": "norm1_context.linear", "img_attn.proj": "attn.to_out.0",
+           "txt_attn.proj": "attn.to_add_out", "img_mlp.0": "ff.net.0.proj", "img_mlp.2": "ff.net.2",
+           "txt_mlp.0": "ff_context.net.0.proj", "txt_mlp.2": "ff_context.net.2",
+           "img_attn.norm.query_norm.scale": "attn.norm_q.weight", "img_attn.norm.key_norm.scale": "attn.norm_k.weight",
+           "txt_attn.norm.query_norm.scale": "attn.norm_added_q.weight",
+           "txt_attn.norm.key_norm.scale": "attn.norm_added_k.weight"}
+    sgl = {"linear2": "proj_out", "modulation.lin": "norm.linear", "norm.query_norm.scale": "attn.norm_q.weight",
+           "norm.key_norm.scale": "attn.norm_k.weight"}
+    out = {}
+    for k, v in sd.items():
+        stem, _, leaf = k.rpartition(".")
+        if stem in top:
+            out[f"{top[stem]}.{leaf}"] = v
+        elif stem == "final_layer.adaLN_modulation.1":  # BFL (shift, scale) -> diffusers (scale, shift)
+            out[f"norm_out.linear.{leaf}"] = torch.cat([v[d:], v[:d]], 0)
+        elif (m := re.match(r"double_blocks\.(\d+)\.(.+)$", k)):
+            i, rest = m.groups()
+            b = f"transformer_blocks.{i}."
+            if rest in dbl:
+                out[b + dbl[rest]] = v
+            elif rest.rpartition(".")[0] in dbl:
+                s, _, lf = rest.rpartition(".")
+                out[b + dbl[s] + "." + lf] = v
+            elif rest.startswith(("img_attn.qkv.", "txt_attn.qkv.")):
+                lf = rest.rpartition(".")[2]
+                names = ("to_q", "to_k", "to_v") if rest.startswith("img") else ("add_q_proj", "add_k_proj", "add_v_proj")
+                for j, nm in enumerate(names):
+                    out[f"{b}attn.{nm}.{lf}"] = v[j * d:(j + 1) * d]
+        elif (m := re.match(r"single_blocks\.(\d+)\.(.+)$", k)):
+            i, rest = m.groups()
+            b = f"single_transformer_blocks.{i}."
+            if rest in sgl:
+                out[b + sgl[rest]] = v
+            elif rest.rpartition(".")[0] in sgl:
+                s, _, lf = rest.rpartition(".")
+                out[b + sgl[s] + "." + lf] = v
+            elif rest.startswith("linear1."):
+                lf = rest.rpartition(".")[2]
+                for j, nm in enumerate(("attn.to_q", "attn.to_k", "attn.to_v")):
+                    out[f"{b}{nm}.{lf}"] = v[j * d:(j + 1) * d]
+                out[f"{b}proj_mlp.{lf}"] = v[3 * d:]
+    return out
+
+
+def flux_config_from(sd: dict):
+    """Diffusers-named Flux state dict -> FluxConfig (block counts and widths from the shapes)."""
+    from .flux import FluxConfig
+    d = int(sd["x_embedder.weight"].shape[0])
+    nd = 1 + max(int(m.group(1)) for k in sd for m in [re.match(r"transformer_blocks\.(\d+)\.", k)] if m)
+    ns = 1 + max(int(m.group(1)) for k in sd for m in [re.match(r"single_transformer_blocks\.(\d+)\.", k)] if m)
+    hd = int(sd["transformer_blocks.0.attn.norm_q.weight"].shape[0])
+    return FluxConfig(in_channels=int(sd["x_embedder.weight"].shape[1]), layers=nd, single_layers=ns, head_dim=hd,
+                      heads=d // hd, joint_dim=int(sd["context_embedder.weight"].shape[1]),
+                      pooled_dim=int(sd["time_text_embed.text_embedder.linear_1.weight"].shape[1]),
+                      guidance="time_text_embed.guidance_embedder.linear_1.weight" in sd)
+
+
+# ---------------------------------------------------------------- text encoders
+def openclip_to_hf(sd: dict) -> dict:
+    """OpenCLIP text tower (SDXL conditioner.embedders.1.model.*) -> HF CLIPTextModelWithProjection names."""
+    out = {}
+    for k, v in sd.items():
+        if k == "token_embedding.weight":
+            out["text_model.embeddings.token_embedding.weight"] = v
+        elif k == "positional_embedding":
+            out["text_model.embeddings.position_embedding.weight"] = v
+        elif k.startswith("ln_final."):
+            out["text_model.final_layer_norm." + k.split(".")[-1]] = v
+        elif k == "text_projection":
+            out["text_projection.weight"] = v.t().contiguous()
+        elif (m := re.match(r"transformer\.resblocks\.(\d+)\.(.+)$", k)):
+            i, rest = m.groups()
+            p = f"text_model.encoder.layers.{i}."
+            if rest in ("attn.in_proj_weight", "attn.in_proj_bias"):
+                lf = "weight" if rest.endswith("weight") else "bias"
+                h = v.shape[0] // 3
+                for j, nm in enumerate(("q_proj", "k_proj", "v_proj")):
+                    out[f"{p}self_attn.{nm}.{lf}"] = v[j * h:(j + 1) * h]
+            else:
+                ren = {"attn.out_proj": "self_attn.out_proj", "ln_1": "layer_norm1", "ln_2": "layer_norm2",
+                       "mlp.c_fc": "mlp.fc1", "mlp.c_proj": "mlp.fc2"}
+                s, _, lf = rest.rpartition(".")
+                if s in ren:
+                    out[f"{p}{ren[s]}.{lf}"] = v
+    return out
+
+
+def clip_config_from(sd: dict):
+    from .text_encoders import CLIPTextConfig
+    te = sd["text_model.embeddings.token_embedding.weight"]
+    hidden = int(te.shape[1])
+    layers = 1 + max(int(m.group(1)) for k in sd for m in [re.match(r"text_model\.encoder\.layers\.(\d+)\.", k)] if m)
+    proj = int(sd["text_projection.weight"].shape[0]) if "text_projection.weight" in sd else hidden
+    # head width 64 in every released CLIP text tower (L: 12 x 64, H: 16 x 64, bigG: 20 x 64); the weights
+    # do not carry it. Test-size towers (< 512 wide) use 16-wide heads.
+    heads = hidden // 64 if hidden >= 512 else max(1, hidden // 16)
+    return CLIPTextConfig(vocab=int(te.shape[0]), hidden=hidden, layers=layers, heads=heads,
+                          ffn=int(sd["text_model.encoder.layers.0.mlp.fc1.weight"].shape[0]),
+                          max_pos=int(sd["text_model.embeddings.position_embedding.weight"].shape[0]),
+                          act="gelu" if hidden >= 1024 else "quick_gelu", proj=proj)
+
+
+def t5_config_from(sd: dict):
+    from .text_encoders import T5Config
+    sd_ = sd
+    emb = sd_.get("shared.weight", sd_.get("encoder.embed_tokens.weight"))
+    layers = 1 + max(int(m.group(1)) for k in sd_ for m in [re.match(r"encoder\.block\.(\d+)\.", k)] if m)
+    rab = sd_["encoder.block.0.layer.0.SelfAttention.relative_attention_bias.weight"]
+    heads = int(rab.shape[1])
+    q = sd_["encoder.block.0.layer.0.SelfAttention.q.weight"]
+    return T5Config(vocab=int(emb.shape[0]), d_model=int(emb.shape[1]), heads=heads, d_kv=int(q.shape[0]) // heads,
+                    d_ff=int(sd_["encoder.block.0.layer.1.DenseReluDense.wi_0.weight"].shape[0]), layers=layers,
+                    buckets=int(rab.shape[0]))
+
+
+# ---------------------------------------------------------------- tokenizers
+def _clip_tokenizer(search: list[str], vocab: int, pad_token=None):
+    from ...tokenizer.clip import CLIPTokenizer
+    for d in search:
+        for sub in ("", "tokenizer", "tokenizer_2" if pad_token else "tokenizer"):
+            p = os.path.join(d, sub)
+            if os.path.isfile(os.path.join(p, "vocab.json")) and os.path.isfile(os.path.join(p, "merges.txt")):
+                return CLIPTokenizer.from_dir(p, pad_token=pad_token)
+    log.warning("no CLIP vocab.json / merges.txt next to %s: byte-level prompt tokens (images will not follow "
+                "the prompt)", search[:1])
+    return CLIPTokenizer.synthetic(vocab, pad_token=pad_token)
+
+
+def _t5_tokenizer(search: list[str], vocab: int, max_len: int):
+    from ...tokenizer.clip import T5Tokenizer
+    for d in search:
+        for p in (os.path.join(d, "spiece.model"), os.path.join(d, "tokenizer_2", "spiece.model")):
+            if os.path.isfile(p):
+                return T5Tokenizer.from_file(p, max_len)
+    log.warning("no T5 spiece.model next to %s: byte-level prompt tokens", search[:1])
+    return T5Tokenizer(None, vocab, max_len)
+
+
+def _dirs(*paths) -> list[str]:
+    return [os.path.dirname(os.path.abspath(p)) for p in paths if p]
+
+
+def _load(make, sd: dict, what: str, device, dtype, allow_missing=("position_ids",)):
+    """Build the module directly on the target device (a 12B Flux transformer is not staged in host
+    RAM twice), load the converted weights, cast to the pipeline dtype."""
+    from .nn import cast_module
+    with torch.device(device):
+        module = make()
+    missing, _ = module.load_state_dict(sd, strict=False)
+    missing = [k for k in missing if not any(a in k for a in allow_missing)]
+    if missing:
+        raise ValueError(f"{what}: missing weights {missing[:5]} ({len(missing)} in all)")
+    return cast_module(module, device, dtype).eval()
+
+
+# ---------------------------------------------------------------- pipelines
+def flux_from_single_file(model: str, device, clip_l_path: str = "", t5xxl_path: str = "", vae_path: str = "",
+                          dtype=None):
+    """Flux.1 transformer file (BFL names; safetensors or GGUF) + ae / clip_l / t5xxl component files."""
+    from .flux import FluxPipeline, FluxTransformer
+    from .text_encoders import CLIPTextEncoder, T5Encoder
+    from .vae import AutoencoderKL
+    dev = torch.device(device)
+    dtype = dtype or (torch.bfloat16 if dev.type == "cuda" else torch.float32)
+    raw = read_tensors(model)
+    if not vae_path and any(k.startswith("vae.") for k in raw):
+        vae_sd = ldm_vae_to_diffusers(strip(raw, "vae."))
+    else:
+        if not vae_path:
+            raise ValueError("Flux needs the autoencoder: set the option vae_path:<ae.safetensors>")
+        vae_sd = ldm_vae_to_diffusers(read_tensors(vae_path))
+    tsd = bfl_flux_to_diffusers(raw)
+    del raw
+    fc = flux_config_from(tsd)
+    tr = _load(lambda: FluxTransformer(fc), tsd, "flux transformer", dev, dtype)
+    del tsd
+    if not clip_l_path or not t5xxl_path:
+        raise ValueError("Flux needs clip_l_path:<clip_l.safetensors> and t5xxl_path:<t5xxl.safetensors|gguf>")
+    csd = read_tensors(clip_l_path)
+    csd = strip(csd, "text_encoders.clip_l.transformer.") or csd
+    cl = _load(lambda: CLIPTextEncoder(clip_config_from(csd)), csd, "clip_l", dev, dtype)
+    t5sd = read_tensors(t5xxl_path)
+    t5c = t5_config_from(t5sd)
+    t5 = _load(lambda: T5Encoder(t5c), t5sd, "t5xxl", dev, dtype)
+    vae = _load(lambda: AutoencoderKL(vae_config_from(vae_sd, 0.3611, 0.1159)), vae_sd, "vae", dev, dtype)
+    nt = 512 if fc.guidance else 256
+    search = _dirs(model, clip_l_path, t5xxl_path)
+    return FluxPipeline(fc, tr, cl, t5, vae, _clip_tokenizer(search, cl.cfg.vocab), _t5_tokenizer(search, t5c.vocab, nt),
+                        dev, t5_tokens=nt, dynamic_shift=fc.guidance)
+
+
+def unet_from_single_file(model: str, device, kind: str, vae_path: str = "", clip_l_path: str = "",
+                          clip_g_path: str = "", dtype=None):
+    """SD1.x / SD2.x / SDXL single file (LDM/SGM names) -> UNetPipeline; component files override."""
+    from .sd_pipeline import UNetPipeline, UNetPreset
+    from .sgm_names import sgm_unet_path
+    from .text_encoders import CLIPTextEncoder
+    from .unet import SD15_UNET, SDXL_UNET, UNet2DConditionModel
+    from .vae import AutoencoderKL
+    import dataclasses
+    dev = torch.device(device)
+    dtype = dtype or (torch.float16 if dev.type == "cuda" else torch.float32)
+    raw = read_tensors(model)
+    usd_ldm = strip(raw, "model.diffusion_model.")
+    xl = kind == "sdxl"
+    if xl:
+        uc = SDXL_UNET
+    else:
+        ctx = next(int(v.shape[1]) for k, v in usd_ldm.items() if k.endswith("attn2.to_k.weight"))
+        lin = next(v for k, v in usd_ldm.items() if k.endswith("proj_in.weight")).dim() == 2
+        # SD2.x: 1024-wide OpenCLIP-H context, linear projections, 64-channel heads
+        uc = SD15_UNET if ctx == 768 else dataclasses.replace(SD15_UNET, cross_dim=ctx, linear_proj=lin,
+                                                              heads=(5, 10, 20, 20), sample_size=96)
+    with torch.device("meta"):  # the block numbering only (sgm_unet_path)
+        shape_ref = UNet2DConditionModel(uc)
+    usd = {}
+    for k, v in usd_ldm.items():
+        stem, _, leaf = k.rpartition(".")
+        p = sgm_unet_path(stem, shape_ref)
+        if p is not None:
+            usd[f"{p}.{leaf}"] = v
+    un = _load(lambda: UNet2DConditionModel(uc), usd, "unet", dev, dtype)
+    del usd, usd_ldm
+    vae_sd = ldm_vae_to_diffusers(read_tensors(vae_path) if vae_path else strip(raw, "first_stage_model."))
+    scaling = 0.13025 if xl else 0.18215
+    vae = _load(lambda: AutoencoderKL(vae_config_from(vae_sd, scaling, 0.0)), vae_sd, "vae", dev, dtype)
+    if clip_l_path:
+        lsd = read_tensors(clip_l_path)
+    else:
+        lsd = strip(raw, "conditioner.embedders.0.transformer.") if xl else strip(raw, "cond_stage_model.transformer.")
+    if not lsd and not xl and any(k.startswith("cond_stage_model.model.") for k in raw):  # SD2.x OpenCLIP-H
+        lsd = openclip_to_hf(strip(raw, "cond_stage_model.model."))
+    t1 = _load(lambda: CLIPTextEncoder(clip_config_from(lsd), with_projection=False), lsd, "clip_l", dev, dtype,
+               allow_missing=("position_ids", "text_projection"))
+    t2 = None
+    if xl:
+        gsd = read_tensors(clip_g_path) if clip_g_path else openclip_to_hf(strip(raw, "conditioner.embedders.1.model."))
+        t2 = _load(lambda: CLIPTextEncoder(clip_config_from(gsd), with_projection=True), gsd, "clip_g", dev, dtype)
+    del raw
+    search = _dirs(model, clip_l_path, clip_g_path)
+    tk1 = _clip_tokenizer(search, t1.cfg.vocab)
+    tk2 = _clip_tokenizer(search, t2.cfg.vocab, pad_token="!") if xl else None
+    pr = UNetPreset(uc, t1.cfg, t2.cfg if t2 is not None else None, vae.cfg, uc.sample_size * 8)
+    return UNetPipeline(pr, un, t1, t2, vae, tk1, tk2, dev)
+
+
+def from_single_file(model: str, device, opts: dict):
+    """Entry point of the diffusion worker for a model FILE (gosd.cpp load_model)."""
+    head = read_tensor_names(model)
+    kind = detect(dict.fromkeys(head))
+    if kind == "flux":
+        return flux_from_single_file(model, device, opts.get("clip_l_path", ""), opts.get("t5xxl_path", ""),
+                                     opts.get("vae_path", ""))
+    if kind in ("sd1", "sdxl"):
+        return unet_from_single_file(model, device, kind, opts.get("vae_path", ""), opts.get("clip_l_path", ""),
+                                     opts.get("clip_g_path", ""))
+    raise ValueError("SD3 / SD3.5 single-file checkpoints (MMDiT SAI names) are not mapped yet; use the "
+                     "diffusers layout of the model")
+
+
+def read_tensor_names(path: str) -> list[str]:
+    if path.endswith(".safetensors"):
+        from safetensors import safe_open
+        with safe_open(path, framework="pt") as f:
+            return list(f.keys())
+    if path.endswith(".gguf"):
+        from ...formats.gguf import GGUFReader
+        return list(GGUFReader(path).tensors)
+    return list(read_tensors(path))

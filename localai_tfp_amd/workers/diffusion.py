@@ -2,7 +2,9 @@
 `diffusers` backends behind one GenerateImage RPC.
 
 LoadModel: a diffusers-layout SD3 directory (MMDiT), Flux.1 directory (FluxTransformer2DModel) or
-SD1.x / SD2.x / SDXL directory (UNet), or `synthetic:sd3-medium | sd3-medium-no-t5 | sd3-test | sd15 |
+SD1.x / SD2.x / SDXL directory (UNet); a stable-diffusion.cpp-style single file (.safetensors / .ckpt /
+GGUF: Flux.1 in BFL names, SD1.x / SD2.x / SDXL in LDM/SGM names) with the component options
+clip_l_path / clip_g_path / t5xxl_path / vae_path (models/diffusion/single_file.py); or `synthetic:sd3-medium | sd3-medium-no-t5 | sd3-test | sd15 |
 sdxl | sd15-test | sdxl-test | flux-dev | flux-schnell | flux-test` (random-init weights). For Flux,
 cfg_scale is the distilled guidance (default 3.5). ModelOptions.Options ("key:value", as gosd.cpp:56-162 parses them):
   sampler:<euler|euler_a|heun|dpm2|dpm++2s_a|dpm++2m|dpm++2mv2|ipndm|ipndm_v|lcm|ddim_trailing|tcd>
@@ -64,9 +66,18 @@ class DiffusionServicer(BackendServicer):
             else:
                 if not os.path.isabs(path) and request.ModelPath:
                     path = os.path.join(request.ModelPath, path)
-                if not os.path.isdir(path):
-                    raise ValueError(f"{path}: expected a diffusers-layout model directory")
-                if os.path.isdir(os.path.join(path, "unet")):
+                if os.path.isfile(path):
+                    # stable-diffusion.cpp-style single file / GGUF + component files (gosd.cpp:56-162)
+                    from ..models.diffusion.single_file import from_single_file
+
+                    def comp(k):
+                        v = opts.get(k, "")
+                        return os.path.join(request.ModelPath, v) if v and not os.path.isabs(v) and request.ModelPath else v
+                    self.pipe = from_single_file(path, self.device, {k: comp(k) for k in (
+                        "clip_l_path", "clip_g_path", "t5xxl_path", "vae_path")})
+                elif not os.path.isdir(path):
+                    raise ValueError(f"{path}: expected a model file or a diffusers-layout model directory")
+                elif os.path.isdir(os.path.join(path, "unet")):
                     self.pipe = U.UNetPipeline.from_diffusers(path, self.device)
                 elif _is_flux(path):
                     self.pipe = FX.FluxPipeline.from_diffusers(path, self.device)
