@@ -12,6 +12,8 @@ modules:
 * SD1.x / SD2.x / SDXL (CompVis LDM / SGM UNet names under model.diffusion_model., via sgm_names);
   CLIP-L from cond_stage_model.transformer. / conditioner.embedders.0.transformer., OpenCLIP-G
   (conditioner.embedders.1.model.: fused in_proj split, c_fc / c_proj, transposed text_projection);
+* SD3 / SD3.5-large (Stability MMDiT names: joint_blocks.i.{x,context}_block, fused qkv, pre-only
+  last context block, ln_q / ln_k QK-norm) with text_encoders.{clip_l,clip_g,t5xxl}.transformer.*;
 * LDM VAE (first_stage_model. or a bare ae.safetensors): down/up/mid blocks renamed, up blocks
   reversed, 1x1-conv attention weights flattened to linears.
 GGUF tensors are dequantised on load to the pipeline's 16-bit dtype (the diffusion GEMMs run on
@@ -191,6 +193,65 @@ def flux_config_from(sd: dict):
                       heads=d // hd, joint_dim=int(sd["context_embedder.weight"].shape[1]),
                       pooled_dim=int(sd["time_text_embed.text_embedder.linear_1.weight"].shape[1]),
                       guidance="time_text_embed.guidance_embedder.linear_1.weight" in sd)
+
+
+# ---------------------------------------------------------------- SD3 / SD3.5 (Stability MMDiT names)
+def sai_mmdit_to_diffusers(sd: dict) -> dict:
+    """model.diffusion_model.* MMDiT (joint_blocks.i.{x,context}_block) -> SD3Transformer2DModel names.
+    The last block's context stream is pre-only (adaLN with 2 vectors, no attention output / MLP)."""
+    sd = strip(sd, "model.diffusion_model.") or sd
+    d = int(sd["x_embedder.proj.weight"].shape[0])
+    top = {"x_embedder.proj": "pos_embed.proj", "t_embedder.mlp.0": "time_text_embed.timestep_embedder.linear_1",
+           "t_embedder.mlp.2": "time_text_embed.timestep_embedder.linear_2",
+           "y_embedder.mlp.0": "time_text_embed.text_embedder.linear_1",
+           "y_embedder.mlp.2": "time_text_embed.text_embedder.linear_2", "context_embedder": "context_embedder",
+           "final_layer.linear": "proj_out"}
+    blk = {"x_block.adaLN_modulation.1": "norm1.linear", "x_block.attn.proj": "attn.to_out.0",
+           "x_block.mlp.fc1": "ff.net.0.proj", "x_block.mlp.fc2": "ff.net.2",
+           "context_block.attn.proj": "attn.to_add_out", "context_block.mlp.fc1": "ff_context.net.0.proj",
+           "context_block.mlp.fc2": "ff_context.net.2", "x_block.attn.ln_q": "attn.norm_q",
+           "x_block.attn.ln_k": "attn.norm_k", "context_block.attn.ln_q": "attn.norm_added_q",
+           "context_block.attn.ln_k": "attn.norm_added_k"}
+    n = 1 + max(int(m.group(1)) for k in sd for m in [re.match(r"joint_blocks\.(\d+)\.", k)] if m)
+    out = {}
+    for k, v in sd.items():
+        stem, _, leaf = k.rpartition(".")
+        if k == "pos_embed":
+            out["pos_embed.pos_embed"] = v
+        elif stem in top:
+            out[f"{top[stem]}.{leaf}"] = v
+        elif stem == "final_layer.adaLN_modulation.1":  # (shift, scale) -> diffusers (scale, shift)
+            out[f"norm_out.linear.{leaf}"] = torch.cat([v[d:], v[:d]], 0)
+        elif (m := re.match(r"joint_blocks\.(\d+)\.(.+)$", stem)):
+            i, rest = int(m.group(1)), m.group(2)
+            b = f"transformer_blocks.{i}."
+            if rest in blk:
+                out[f"{b}{blk[rest]}.{leaf}"] = v
+            elif rest == "context_block.adaLN_modulation.1":
+                # last block: AdaLayerNormContinuous (2 vectors, swapped like norm_out)
+                out[f"{b}norm1_context.linear.{leaf}"] = (torch.cat([v[d:], v[:d]], 0) if i == n - 1 and
+                                                          v.shape[0] == 2 * d else v)
+            elif rest in ("x_block.attn.qkv", "context_block.attn.qkv"):
+                names = ("to_q", "to_k", "to_v") if rest.startswith("x_") else ("add_q_proj", "add_k_proj", "add_v_proj")
+                for j, nm in enumerate(names):
+                    out[f"{b}attn.{nm}.{leaf}"] = v[j * d:(j + 1) * d]
+            elif rest.startswith("x_block.attn2."):
+                raise ValueError("SD3.5-medium MMDiT-X dual-attention blocks (attn2) are not supported")
+    return out
+
+
+def mmdit_config_from(sd: dict):
+    from .mmdit import MMDiTConfig
+    w = sd["pos_embed.proj.weight"]
+    d = int(w.shape[0])
+    layers = 1 + max(int(m.group(1)) for k in sd for m in [re.match(r"transformer_blocks\.(\d+)\.", k)] if m)
+    pos = sd.get("pos_embed.pos_embed")
+    pos_max = int(round(float(pos.shape[1]) ** 0.5)) if pos is not None else 192
+    return MMDiTConfig(patch=int(w.shape[2]), in_channels=int(w.shape[1]),
+                       out_channels=int(sd["proj_out.weight"].shape[0]) // int(w.shape[2]) ** 2, layers=layers,
+                       head_dim=64, heads=d // 64, joint_dim=int(sd["context_embedder.weight"].shape[1]),
+                       caption_dim=d, pooled_dim=int(sd["time_text_embed.text_embedder.linear_1.weight"].shape[1]),
+                       pos_max=pos_max, sample_size=128, qk_norm="transformer_blocks.0.attn.norm_q.weight" in sd)
 
 
 # ---------------------------------------------------------------- text encoders
@@ -382,6 +443,54 @@ def unet_from_single_file(model: str, device, kind: str, vae_path: str = "", cli
     return UNetPipeline(pr, un, t1, t2, vae, tk1, tk2, dev)
 
 
+def _component(raw: dict, path: str, prefixes: tuple) -> dict:
+    """A text encoder from its own file (any of the known prefixes stripped) or from the model file."""
+    src = read_tensors(path) if path else raw
+    for p in prefixes:
+        got = strip(src, p)
+        if got:
+            return got
+    return src if path else {}
+
+
+def sd3_from_single_file(model: str, device, clip_l_path: str = "", clip_g_path: str = "", t5xxl_path: str = "",
+                         vae_path: str = "", dtype=None):
+    """SD3 / SD3.5 (large) single file in Stability's names (+ optional component files)."""
+    from .mmdit import MMDiT
+    from .pipeline import SD3Pipeline, SD3Preset
+    from .text_encoders import CLIPTextEncoder, T5Encoder
+    from .vae import AutoencoderKL
+    dev = torch.device(device)
+    dtype = dtype or (torch.bfloat16 if dev.type == "cuda" else torch.float32)
+    raw = read_tensors(model)
+    msd = sai_mmdit_to_diffusers(raw)
+    mc = mmdit_config_from(msd)
+    mm = _load(lambda: MMDiT(mc), msd, "mmdit", dev, dtype, allow_missing=("pos_embed.pos_embed",))
+    del msd
+    vae_sd = ldm_vae_to_diffusers(read_tensors(vae_path) if vae_path else strip(raw, "first_stage_model."))
+    if not vae_sd:
+        raise ValueError("SD3 needs its VAE: bundled first_stage_model.* tensors or the option vae_path")
+    vae = _load(lambda: AutoencoderKL(vae_config_from(vae_sd, 1.5305, 0.0609)), vae_sd, "vae", dev, dtype)
+    lsd = _component(raw, clip_l_path, ("text_encoders.clip_l.transformer.", "cond_stage_model.transformer."))
+    gsd = _component(raw, clip_g_path, ("text_encoders.clip_g.transformer.",))
+    tsd = _component(raw, t5xxl_path, ("text_encoders.t5xxl.transformer.",))
+    if not lsd or not gsd:
+        raise ValueError("SD3 needs CLIP-L and CLIP-G: bundled text_encoders.* tensors or clip_l_path / clip_g_path")
+    cl = _load(lambda: CLIPTextEncoder(clip_config_from(lsd)), lsd, "clip_l", dev, dtype,
+               allow_missing=("position_ids", "text_projection"))
+    cg = _load(lambda: CLIPTextEncoder(clip_config_from(gsd)), gsd, "clip_g", dev, dtype)
+    t5 = None
+    if tsd:
+        t5c = t5_config_from(tsd)
+        t5 = _load(lambda: T5Encoder(t5c), tsd, "t5xxl", dev, dtype)
+    del raw
+    search = _dirs(model, clip_l_path, clip_g_path, t5xxl_path)
+    pr = SD3Preset(mc, cl.cfg, cg.cfg, t5.cfg if t5 is not None else None, vae.cfg)
+    return SD3Pipeline(pr, mm, cl, cg, t5, vae, _clip_tokenizer(search, cl.cfg.vocab),
+                       _clip_tokenizer(search, cg.cfg.vocab, pad_token="!"),
+                       _t5_tokenizer(search, t5.cfg.vocab, 256) if t5 is not None else None, dev)
+
+
 def from_single_file(model: str, device, opts: dict):
     """Entry point of the diffusion worker for a model FILE (gosd.cpp load_model)."""
     head = read_tensor_names(model)
@@ -392,8 +501,8 @@ def from_single_file(model: str, device, opts: dict):
     if kind in ("sd1", "sdxl"):
         return unet_from_single_file(model, device, kind, opts.get("vae_path", ""), opts.get("clip_l_path", ""),
                                      opts.get("clip_g_path", ""))
-    raise ValueError("SD3 / SD3.5 single-file checkpoints (MMDiT SAI names) are not mapped yet; use the "
-                     "diffusers layout of the model")
+    return sd3_from_single_file(model, device, opts.get("clip_l_path", ""), opts.get("clip_g_path", ""),
+                                opts.get("t5xxl_path", ""), opts.get("vae_path", ""))
 
 
 def read_tensor_names(path: str) -> list[str]:

@@ -260,3 +260,62 @@ def test_worker_loads_flux_ggml_gallery_layout(tmp_path):
     assert r.success, r.message
     with open(dst, "rb") as f:
         assert f.read(8) == b"\x89PNG\r\n\x1a\n"
+
+
+def _mmdit_to_sai(sd, d, n):
+    """diffusers SD3Transformer2DModel names -> Stability MMDiT names (inverse of the loader's map)."""
+    out = {"pos_embed": sd["pos_embed.pos_embed"]}
+    top = {"pos_embed.proj": "x_embedder.proj", "time_text_embed.timestep_embedder.linear_1": "t_embedder.mlp.0",
+           "time_text_embed.timestep_embedder.linear_2": "t_embedder.mlp.2",
+           "time_text_embed.text_embedder.linear_1": "y_embedder.mlp.0",
+           "time_text_embed.text_embedder.linear_2": "y_embedder.mlp.2", "context_embedder": "context_embedder",
+           "proj_out": "final_layer.linear"}
+    blk = {"norm1.linear": "x_block.adaLN_modulation.1", "attn.to_out.0": "x_block.attn.proj",
+           "ff.net.0.proj": "x_block.mlp.fc1", "ff.net.2": "x_block.mlp.fc2", "attn.to_add_out": "context_block.attn.proj",
+           "ff_context.net.0.proj": "context_block.mlp.fc1", "ff_context.net.2": "context_block.mlp.fc2",
+           "attn.norm_q": "x_block.attn.ln_q", "attn.norm_k": "x_block.attn.ln_k",
+           "attn.norm_added_q": "context_block.attn.ln_q", "attn.norm_added_k": "context_block.attn.ln_k"}
+    for k, v in sd.items():
+        stem, _, leaf = k.rpartition(".")
+        if stem in top:
+            out[f"{top[stem]}.{leaf}"] = v
+        elif stem == "norm_out.linear":
+            out[f"final_layer.adaLN_modulation.1.{leaf}"] = torch.cat([v[d:], v[:d]], 0)
+        elif (m := re.match(r"transformer_blocks\.(\d+)\.(.+)$", stem)):
+            i, rest = int(m[1]), m[2]
+            b = f"joint_blocks.{i}."
+            if rest in blk:
+                out[f"{b}{blk[rest]}.{leaf}"] = v
+            elif rest == "norm1_context.linear":
+                out[f"{b}context_block.adaLN_modulation.1.{leaf}"] = (
+                    torch.cat([v[d:], v[:d]], 0) if i == n - 1 and v.shape[0] == 2 * d else v)
+    for i in range(n):
+        for lf in ("weight", "bias"):
+            p = f"transformer_blocks.{i}.attn."
+            out[f"joint_blocks.{i}.x_block.attn.qkv.{lf}"] = torch.cat([sd[f"{p}to_{x}.{lf}"] for x in "qkv"])
+            out[f"joint_blocks.{i}.context_block.attn.qkv.{lf}"] = torch.cat([sd[f"{p}add_{x}_proj.{lf}"] for x in "qkv"])
+    return out
+
+
+def test_sd3_single_file_bundled(tmp_path):
+    """SD3 single file with everything bundled (Stability layout): model.diffusion_model.*,
+    first_stage_model.*, text_encoders.{clip_l,clip_g,t5xxl}.transformer.*"""
+    from localai_tfp_amd.models.diffusion.pipeline import GenParams, SD3Pipeline
+    ref = SD3Pipeline.synthetic("sd3-test", "cpu")
+    msd = {k: v.contiguous() for k, v in ref.mmdit.state_dict().items()}
+    n = ref.p.mmdit.layers
+    f = {"model.diffusion_model." + k: v for k, v in _mmdit_to_sai(msd, ref.p.mmdit.dim, n).items()}
+    f.update({"first_stage_model." + k: v for k, v in _vae_to_ldm(
+        {k: v.contiguous() for k, v in ref.vae.state_dict().items()}).items()})
+    for name, m in (("clip_l", ref.clip_l), ("clip_g", ref.clip_g), ("t5xxl", ref.t5)):
+        f.update({f"text_encoders.{name}.transformer.{k}": v.contiguous() for k, v in m.state_dict().items()})
+    mp = str(tmp_path / "sd3_test.safetensors")
+    save_file(f, mp)
+    pipe = SF.from_single_file(mp, "cpu", {})
+    import dataclasses  # the default sample size is not stored in the weights (SD3: 128 latents)
+    assert dataclasses.replace(pipe.p.mmdit, sample_size=ref.p.mmdit.sample_size) == ref.p.mmdit
+    for a, b in ((pipe.mmdit, ref.mmdit), (pipe.clip_l, ref.clip_l), (pipe.clip_g, ref.clip_g), (pipe.t5, ref.t5),
+                 (pipe.vae, ref.vae)):
+        sa, sb = a.state_dict(), b.state_dict()
+        bad = [k for k in sb if k not in sa or not torch.equal(sa[k], sb[k])]
+        assert not bad, bad[:4]
