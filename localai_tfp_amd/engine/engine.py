@@ -614,20 +614,20 @@ class LLMEngine:
 
     def _execute(self, plan: dict):
         """Run the step's forward on this rank. Returns (logits, argmax-or-None)."""
-        dev = self.device
         nd = plan["nd"]
         if plan["graph"]:
             g = self._graph_for(nd)
             bt = plan["dec_bt"]
             maxb = bt.shape[1]
-            flat = np.concatenate([plan["tokens"], plan["positions"], plan["slots"], plan["dec_lens"], bt.reshape(-1)])
-            d = self._stage_h2d(flat)
-            logits, am = g.run(d[:nd], d[nd:2 * nd], d[2 * nd:3 * nd], d[4 * nd:].view(nd, maxb),
-                               d[3 * nd:4 * nd], nd, fix=self._fix_tensors(plan))
+            t = self._stage_plan(plan, ("tokens", "positions", "slots", "dec_lens", "dec_bt"))
+            logits, am = g.run(t["tokens"], t["positions"], t["slots"], t["dec_bt"].view(nd, maxb), t["dec_lens"], nd,
+                               fix=self._fix_tensors(t))
             self.stats["graph_steps"] += 1
             return logits, am
-        fb = self._build_fb(plan)
-        fix = self._fix_tensors(plan)
+        t = self._stage_plan(plan, ("tokens", "positions", "slots", "lidx", "dec_bt", "dec_lens", "pf_bt", "pf_cu",
+                                    "pf_ctx"))
+        fb = self._build_fb(plan, t)
+        fix = self._fix_tensors(t)
         if fix is not None:
             dst, src, prev = fix
             fb.tokens.index_copy_(0, dst, prev.index_select(0, src))
@@ -635,13 +635,34 @@ class LLMEngine:
         self._hidden = self.model.last_hidden if fb.keep_hidden else None
         return logits, None
 
+    def _stage_plan(self, plan: dict, keys) -> dict:
+        """Every int32 array of the step (and the overlap-mode fix-up indices) in ONE pinned H2D copy.
+        Never torch.from_numpy(...).to(dev): a copy from pageable memory makes the host wait for the
+        stream to drain, i.e. the GPU idles while the rest of the step is launched."""
+        arrays = [(k, plan[k]) for k in keys if k in plan]
+        if "fix" in plan:
+            arrays += [("fix_dst", plan["fix"][0]), ("fix_src", plan["fix"][1])]
+        parts, spec, off = [], [], 0
+        for k, a in arrays:
+            a = np.asarray(a)
+            parts.append(a.reshape(-1).astype(np.int32, copy=False))
+            spec.append((k, off, a.shape))
+            off += a.size
+        d = self._stage_h2d(np.concatenate(parts) if parts else np.zeros(1, np.int32))
+        return {k: d[o:o + int(np.prod(sh))].view(sh) for k, o, sh in spec}
+
     def _stage_h2d(self, flat: np.ndarray) -> torch.Tensor:
         """int32 host array -> device, through a ring of 3 persistent pinned buffers (a buffer is
         reused only after the step that last used it has been read back, so the async copy that
         sourced it has completed); a fresh pinned allocation per step costs ~ms on the host."""
         n = flat.size
+        if self.device.type != "cuda":
+            return torch.from_numpy(np.array(flat, dtype=np.int32))
         if self._pin_in is None or self._pin_in[0].numel() < n:
-            cap = max(n, self.cfg.max_num_seqs * (4 + self.max_blocks_per_seq))
+            c = self.cfg
+            cap = max(n, 4 * c.max_batched_tokens + c.max_num_seqs * (6 + 2 * self.max_blocks_per_seq) + 1024)
+            if self._pin_in is not None and self.device.type == "cuda":
+                torch.cuda.synchronize(self.device)  # the old ring may still source in-flight copies
             self._pin_in = [torch.empty(cap, dtype=torch.int32).pin_memory() for _ in range(3)]
             self._pin_in_i = 0
         k = self._pin_in_i
@@ -650,13 +671,10 @@ class LLMEngine:
         hb.numpy()[:] = flat
         return hb.to(self.device, non_blocking=True)
 
-    def _fix_tensors(self, plan):
-        if "fix" not in plan:
+    def _fix_tensors(self, t: dict):
+        if "fix_dst" not in t:
             return None
-        dst, src = plan["fix"]
-        dev = self.device
-        return (torch.from_numpy(dst).to(dev, non_blocking=True), torch.from_numpy(src).to(dev, non_blocking=True),
-                self._prev_dev[0])
+        return t["fix_dst"].long(), t["fix_src"].long(), self._prev_dev[0]
 
     def _forward_and_sample(self, so: SchedulerOutput):
         t0 = time.perf_counter()
@@ -678,11 +696,11 @@ class LLMEngine:
             return out, None
         return self._sample(logits, sample_items)
 
-    def _build_fb(self, plan: dict) -> ForwardBatch:
-        dev = self.device
+    def _build_fb(self, plan: dict, t: dict | None = None) -> ForwardBatch:
         nd = plan["nd"]
-        keys = ["tokens", "positions", "slots", "lidx", "dec_bt", "dec_lens", "pf_bt", "pf_cu", "pf_ctx"]
-        t = {k: torch.from_numpy(np.ascontiguousarray(plan[k])).to(dev, non_blocking=True) for k in keys if k in plan}
+        if t is None:
+            t = self._stage_plan(plan, ("tokens", "positions", "slots", "lidx", "dec_bt", "dec_lens", "pf_bt",
+                                        "pf_cu", "pf_ctx"))
         fb = ForwardBatch(t["tokens"], t["positions"], t["slots"], t["lidx"], n_decode=nd)
         if nd:
             fb.dec_block_tables, fb.dec_seq_lens = t["dec_bt"], t["dec_lens"]

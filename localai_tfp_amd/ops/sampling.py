@@ -92,6 +92,28 @@ class SamplerBatch:
                 bias.append(b)
         return arr, np.asarray(toks or [0], np.int32), np.asarray(cnts or [0], np.int32), np.asarray(bias or [0.0], np.float32)
 
+    def _stage(self, dev, parts: list[np.ndarray]) -> list[torch.Tensor]:
+        """Byte arrays -> device views (16-B aligned) through ONE copy from a ring of 3 pinned buffers:
+        a pageable H2D copy would make the host wait for the stream, stalling the next step's launch."""
+        offs, n = [], 0
+        for a in parts:
+            offs.append(n)
+            n += -(-a.size // 16) * 16
+        ring = getattr(self, "_pin", None)
+        if ring is None or ring[0].numel() < n:
+            if ring is not None:
+                torch.cuda.synchronize(dev)  # the old buffers may still source in-flight copies
+            self._pin = [torch.empty(max(n, 1 << 20), dtype=torch.uint8).pin_memory() for _ in range(3)]
+            self._pin_k = 0
+        k = self._pin_k
+        self._pin_k = (k + 1) % 3
+        hb = self._pin[k][:n]
+        hv = hb.numpy()
+        for o, a in zip(offs, parts):
+            hv[o:o + a.size] = a
+        d = hb.to(dev, non_blocking=True)
+        return [d[o:o + a.size] for o, a in zip(offs, parts)]
+
     def sample(self, logits: torch.Tensor, params: list[SamplingParams], histories: list[list[int]],
                steps: list[int], allow_mask: torch.Tensor | None = None, mirostat_mu=None):
         """logits fp32 [B, V] (modified in place) -> (tokens int32 [B], logprobs fp32 [B]) on device."""
@@ -108,10 +130,8 @@ class SamplerBatch:
             return tok, None
         arr, toks, cnts, bias = self.pack(params, histories, steps, mirostat_mu)
         dev = logits.device
-        pbuf = torch.from_numpy(arr.view(np.uint8)).to(dev, non_blocking=True)
-        t_t = torch.from_numpy(toks).to(dev, non_blocking=True)
-        c_t = torch.from_numpy(cnts).to(dev, non_blocking=True)
-        b_t = torch.from_numpy(bias).to(dev, non_blocking=True)
+        pbuf, t_t, c_t, b_t = self._stage(dev, [arr.view(np.uint8), toks.view(np.uint8), cnts.view(np.uint8),
+                                                bias.view(np.uint8)])
         tok = torch.empty(B, dtype=torch.int32, device=dev)
         lp = torch.empty(B, dtype=torch.float32, device=dev)
         N.kcall("mxk_sample", logits.data_ptr(), logits.stride(0), B, V, pbuf.data_ptr(), t_t.data_ptr(),
