@@ -241,6 +241,7 @@ def main():
                 "graph_steps": st["graph_steps"], "total_steps": st["steps"],
                 "host_ms_per_step": {k[:-2]: round(st[k] / max(1, st["steps"]) * 1e3, 3)
                                      for k in ("sched_s", "plan_s", "fwd_s", "wait_s", "process_s")},
+                "graph_replay_host_ms": round(sum(g.replay_s for g in eng.graphs.values()) / max(1, st["graph_steps"]) * 1e3, 3),
                 "weights_gb": round(model.weight_bytes() / 1e9, 2), "kv_blocks": eng.kv.num_blocks,
                 "kv_dtype": args.kv_dtype, **extra,
             },
@@ -452,6 +453,7 @@ def run_engine(args, eng, tok, dev, dist):
         dist.barrier()
     timed["on"] = True
     tok0 = eng.stats["out_tokens"]
+    s0 = _host_snapshot(eng)
     t_start = time.monotonic()
     for _ in range(args.steps):
         step()
@@ -460,7 +462,28 @@ def run_engine(args, eng, tok, dev, dist):
     if dist:
         dist.barrier()
     t_el = time.monotonic() - t_start
-    return t_el, eng.stats["out_tokens"] - tok0, ttfts, {"steady_at_step": n_pre}
+    return t_el, eng.stats["out_tokens"] - tok0, ttfts, {"steady_at_step": n_pre,
+                                                         "window_host": _host_delta(s0, _host_snapshot(eng))}
+
+
+def _host_snapshot(eng):
+    st = dict(eng.stats)
+    st["replay_s"] = sum(g.replay_s for g in eng.graphs.values())
+    return st
+
+
+def _host_delta(a, b):
+    """Host-side engine time per step inside the timed window (ms): scheduler, plan, launch (fwd),
+    wait for the in-flight step, post-processing; plus how many window steps replayed a hipGraph."""
+    n = max(1, b["steps"] - a["steps"])
+    out = {k[:-2] + "_ms": round((b[k] - a[k]) / n * 1e3, 3)
+           for k in ("sched_s", "plan_s", "fwd_s", "wait_s", "process_s", "replay_s")}
+    out["steps"] = b["steps"] - a["steps"]
+    out["graph_steps"] = g = b["graph_steps"] - a["graph_steps"]
+    out["fwd_graph_step_ms"] = round((b["fwd_graph_s"] - a["fwd_graph_s"]) / max(1, g) * 1e3, 3)
+    out["fwd_eager_step_ms"] = round((b["fwd_s"] - a["fwd_s"] - b["fwd_graph_s"] + a["fwd_graph_s"]) / max(1, n - g) * 1e3, 3)
+    out["prefill_tokens_per_step"] = round((b["prefill_tokens"] - a["prefill_tokens"]) / n, 1)
+    return out
 
 
 if __name__ == "__main__":

@@ -296,6 +296,7 @@ __global__ __launch_bounds__(512) void attn_prefill_kernel(const bf16_t* __restr
     const int g = lane >> 4, col = lane & 15;
     const int tile = blockIdx.x;
     const int s = tile_seq[tile], q0 = tile_q0[tile];
+    if (s < 0) return;  // padding tile of a graph-captured step (uniform across the workgroup)
     const int hq = blockIdx.y * GW + (wave % GW);
     const int kvh = (blockIdx.y * GW) / G;
     const int rt = wave / GW;

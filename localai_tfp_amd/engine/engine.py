@@ -43,6 +43,11 @@ class EngineConfig:
     enable_prefix_cache: bool = True
     use_graphs: bool = True
     graph_buckets: tuple = (1, 2, 4, 8, 16, 32, 48, 64, 96, 128, 160, 192, 224, 256)
+    # mixed steps (decode rows + prompt chunks) replay graphs too: prefill-token buckets, max prompt
+    # sequences per graphed step, and a cap on captured graphs (captured lazily, first use of a shape)
+    mixed_graph_tokens: tuple = (64, 128, 256, 384, 512, 768, 1024)
+    mixed_graph_seqs: int = 4
+    max_graphs: int = 64
     attn_part_size: int = 256  # must match ops.core.attn_decode's default
     # dense 16-bit copy of the layer projections for hipBLASLt at the M where it still beats the qmm
     # kernels on t32-tiled weights (ops/linear.py DENSE_MIN_M_*; never for the LM head)
@@ -109,58 +114,153 @@ class BatchedSink:
             ch.deliver(its)
 
 
-class DecodeGraph:
-    """Static-input hipGraph of one decode step (forward + greedy argmax) for a batch bucket."""
+class StepGraph:
+    """hipGraph of one engine step for a shape bucket (forward + greedy argmax).
 
-    def __init__(self, engine: "LLMEngine", B: int):
+    Bucket (B, P, PS): B decode rows (padded: slot -1, length 1) followed by room for P prefill
+    tokens in up to PS prefill sequences (padded sequences have q_len 0; padded attention tiles carry
+    sequence -1 and exit). P = 0 is the decode-only graph. Mixed continuous-batching steps (decode rows
+    plus an arriving prompt chunk) replay a graph too, so no step pays the ~7 ms of per-kernel Python
+    launches of the eager forward.
+
+    Every input lives in ONE static int32 device buffer (views below); the host writes the padded
+    image into a pinned ring buffer and refreshes all inputs with ONE async H2D copy per step.
+    """
+
+    def __init__(self, engine: "LLMEngine", B: int, P: int = 0, PS: int = 0):
         e = engine
         dev = e.device
-        self.B = B
-        self.maxb = e.max_blocks_per_seq
-        self.tokens = torch.zeros(B, dtype=torch.int32, device=dev)
-        self.positions = torch.zeros(B, dtype=torch.int32, device=dev)
-        self.slots = torch.full((B,), -1, dtype=torch.int32, device=dev)
-        self.bt = torch.zeros((B, self.maxb), dtype=torch.int32, device=dev)
-        self.lens = torch.ones(B, dtype=torch.int32, device=dev)
-        self.lidx = torch.arange(B, dtype=torch.int32, device=dev)
-        self.argmax = torch.zeros(B, dtype=torch.int32, device=dev)
-        self.fb = ForwardBatch(self.tokens, self.positions, self.slots, self.lidx, n_decode=B,
-                               dec_block_tables=self.bt, dec_seq_lens=self.lens, dec_max_len=e.cfg.max_model_len)
+        self.B, self.P, self.PS = B, P, PS
+        self.maxb = mb = e.max_blocks_per_seq
+        self.rows = e.model.prefill_rows() if P else 1
+        self.NT = (P // self.rows + PS) if P else 0  # prefill attention tile capacity
+        T = B + P
+        self.S = min(B + PS, e.ws.max_seqs)  # logits rows
+        Bp = max(B, 1)
+        # tokens has one dummy row past T: the in-graph fix-up of decode inputs sampled by the previous
+        # (still unread) step scatters into it for the rows that need no fix
+        lay = [("tokens", (T + 1,)), ("positions", (T,)), ("slots", (T,)), ("lidx", (self.S,)),
+               ("dec_bt", (Bp, mb)), ("dec_lens", (Bp,)), ("fix_dst", (Bp,)), ("fix_src", (Bp,))]
+        if P:
+            lay += [("pf_bt", (PS, mb)), ("pf_cu", (PS + 1,)), ("pf_ctx", (PS,)), ("pf_tseq", (self.NT,)),
+                    ("pf_tq0", (self.NT,))]
+        self.off, o = {}, 0
+        for k, sh in lay:
+            self.off[k] = (o, sh)
+            o += int(np.prod(sh))
+        self.n = o
+        img = np.zeros(o, np.int32)
+        self._default = img
+        for k, v in (("slots", -1), ("dec_lens", 1), ("pf_tseq", -1), ("fix_dst", T)):
+            if k in self.off:
+                self.view(img, k)[...] = v
+        self.buf = torch.from_numpy(img.copy()).to(dev)
+        self._pin = [torch.empty(o, dtype=torch.int32).pin_memory() for _ in range(3)] if dev.type == "cuda" else None
+        self._pin_i = 0
+        v = {k: self.view(self.buf, k) for k in self.off}
+        self.v = v
+        self.prev = torch.zeros(e.ws.max_seqs, dtype=torch.int32, device=dev)  # previous step's samples
+        self.argmax = torch.zeros(self.S, dtype=torch.int32, device=dev)
+        self.fb = ForwardBatch(v["tokens"][:T], v["positions"], v["slots"], v["lidx"], n_decode=B,
+                               dec_block_tables=v["dec_bt"][:B], dec_seq_lens=v["dec_lens"][:B],
+                               dec_max_len=e.cfg.max_model_len)
+        if P:
+            self.fb.pf_block_tables, self.fb.pf_cu_q, self.fb.pf_ctx_lens = v["pf_bt"], v["pf_cu"], v["pf_ctx"]
+            self.fb.pf_tiles = (v["pf_tseq"], v["pf_tq0"])
         self.graph = None
         self.logits = None
+        self.replay_s = 0.0  # host time inside hipGraphLaunch (profiling)
 
-    def capture(self, engine: "LLMEngine"):
+    def view(self, flat, k):
+        o, sh = self.off[k]
+        return flat[o:o + int(np.prod(sh))].reshape(sh)
+
+    def fits(self, plan: dict) -> bool:
+        nd = plan["nd"]
+        if nd > self.B:
+            return False
+        if "pf_cu" not in plan:
+            return True
+        cu = plan["pf_cu"]
+        return (self.P and len(cu) - 1 <= self.PS and int(cu[-1]) <= self.P
+                and len(plan["pf_tseq"]) <= self.NT and len(plan["lidx"]) <= self.S)
+
+    def capture(self, engine: "LLMEngine", pool=None):
         from .. import _native as N
         s = torch.cuda.Stream(device=engine.device)
         s.wait_stream(torch.cuda.current_stream(engine.device))
         with torch.cuda.stream(s):
             for _ in range(2):  # warm-up (allocations, lazy init) outside capture
+                self._fix()
                 lg = engine.model.forward(self.fb, engine.kv, engine.ws)
-                N.kcall("mxk_argmax", lg.data_ptr(), lg.stride(0), self.B, lg.shape[1], self.argmax.data_ptr(),
+                N.kcall("mxk_argmax", lg.data_ptr(), lg.stride(0), self.S, lg.shape[1], self.argmax.data_ptr(),
                         N.stream_ptr())
         torch.cuda.current_stream(engine.device).wait_stream(s)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, stream=s):
+        with torch.cuda.graph(g, pool=pool, stream=s):
+            self._fix()
             self.logits = engine.model.forward(self.fb, engine.kv, engine.ws)
-            N.kcall("mxk_argmax", self.logits.data_ptr(), self.logits.stride(0), self.B, self.logits.shape[1],
+            N.kcall("mxk_argmax", self.logits.data_ptr(), self.logits.stride(0), self.S, self.logits.shape[1],
                     self.argmax.data_ptr(), N.stream_ptr())
         self.graph = g
 
-    def run(self, tokens, positions, slots, bt, lens, n: int, fix=None):
-        self.tokens[:n].copy_(tokens, non_blocking=True)
-        if fix is not None:  # decode inputs sampled by the previous (unread) step, gathered on device
-            dst, src, prev = fix
-            self.tokens.index_copy_(0, dst, prev.index_select(0, src))
-        self.positions[:n].copy_(positions, non_blocking=True)
-        self.slots[:n].copy_(slots, non_blocking=True)
-        self.bt[:n, : bt.shape[1]].copy_(bt, non_blocking=True)
-        self.lens[:n].copy_(lens, non_blocking=True)
-        if n < self.B:
-            self.slots[n:].fill_(-1)
-            self.lens[n:].fill_(1)
-            self.bt[n:].zero_()
+    def _fix(self):
+        v = self.v
+        v["tokens"].index_copy_(0, v["fix_dst"].long(), self.prev.index_select(0, v["fix_src"].long()))
+
+    def image(self, plan: dict) -> np.ndarray:
+        """Padded host image of the step's inputs in this bucket's layout."""
+        img = self._default.copy()
+        nd, B = plan["nd"], self.B
+        tok, pos, sl = plan["tokens"], plan["positions"], plan["slots"]
+        npf = len(tok) - nd
+        for k, a in (("tokens", tok), ("positions", pos), ("slots", sl)):
+            d = self.view(img, k)
+            d[:nd] = a[:nd]
+            d[B:B + npf] = a[nd:]
+        lidx = plan["lidx"]
+        d = self.view(img, "lidx")
+        d[:len(lidx)] = lidx
+        d[nd:len(lidx)] += B - nd  # prefill rows sit after the padded decode block
+        if nd:
+            bt = plan["dec_bt"]
+            self.view(img, "dec_bt")[:nd, :bt.shape[1]] = bt
+            self.view(img, "dec_lens")[:nd] = plan["dec_lens"]
+        if "pf_cu" in plan:
+            bt, cu = plan["pf_bt"], plan["pf_cu"]
+            ns = len(cu) - 1
+            self.view(img, "pf_bt")[:ns, :bt.shape[1]] = bt
+            c = self.view(img, "pf_cu")
+            c[:ns + 1] = cu
+            c[ns + 1:] = cu[-1]  # padded sequences: q_len 0
+            self.view(img, "pf_ctx")[:ns] = plan["pf_ctx"]
+            ts = plan["pf_tseq"]
+            self.view(img, "pf_tseq")[:len(ts)] = ts
+            self.view(img, "pf_tq0")[:len(ts)] = plan["pf_tq0"]
+        if "fix" in plan:
+            dst, src = plan["fix"]
+            self.view(img, "fix_dst")[:len(dst)] = dst
+            self.view(img, "fix_src")[:len(src)] = src
+        return img
+
+    def run(self, plan: dict, prev=None):
+        """prev: device int32 tokens of the previous (unread) step when the plan has a "fix" entry."""
+        if "fix" in plan:
+            self.prev[:prev.numel()].copy_(prev, non_blocking=True)
+        img = self.image(plan)
+        if self._pin is not None:
+            k = self._pin_i
+            self._pin_i = (k + 1) % 3
+            hb = self._pin[k]
+            hb.numpy()[:] = img
+            self.buf.copy_(hb, non_blocking=True)
+        else:
+            self.buf.copy_(torch.from_numpy(img))
+        t0 = time.perf_counter()
         self.graph.replay()
-        return self.logits[:n], self.argmax[:n]
+        self.replay_s += time.perf_counter() - t0
+        S = len(plan["lidx"])
+        return self.logits[:S], self.argmax[:S]
 
 
 class LLMEngine:
@@ -221,12 +321,14 @@ class LLMEngine:
         self._cv = threading.Condition()
         self._thread: threading.Thread | None = None
         self._stop = False
-        self.graphs: dict[int, DecodeGraph] = {}
+        self.graphs: dict[tuple, StepGraph] = {}
+        self._graph_pool = None
         self.use_graphs = c.use_graphs and self.device.type == "cuda"
         self.eos_ids = set(getattr(tokenizer, "eos_token_ids", []) or [])
         self.stats = dict(steps=0, decode_tokens=0, prefill_tokens=0, graph_steps=0, preemptions=0,
                           busy_s=0.0, prompt_tokens_total=0, gen_tokens_total=0, cached_tokens_total=0,
-                          out_tokens=0, finished=0, sched_s=0.0, plan_s=0.0, fwd_s=0.0, wait_s=0.0, process_s=0.0)
+                          out_tokens=0, finished=0, sched_s=0.0, plan_s=0.0, fwd_s=0.0, fwd_graph_s=0.0, wait_s=0.0,
+                          process_s=0.0)
         self.last_metrics = {}
         self.on_step = None  # optional hook called with the step index before each loop step (bench)
         self.batch_sink: BatchedSink | None = None
@@ -302,7 +404,7 @@ class LLMEngine:
             self.tp.send_plan("capture")  # followers capture the same buckets in the same order
         n = 0
         for b in self.cfg.graph_buckets:
-            if b <= self.cfg.max_num_seqs and self._graph_for(b) is not None:
+            if b <= self.cfg.max_num_seqs and self._graph_for(b) is not None:  # decode-only buckets
                 n += 1
         return n
 
@@ -445,6 +547,8 @@ class LLMEngine:
         plan = self._plan(so)
         self.stats["plan_s"] += time.perf_counter() - t1
         items = list(so.decode) + [it for it in so.prefill if it.sample]
+        if roctx.ENABLED:
+            roctx.push("launch graph" if plan["graph"] else "launch eager")
         logits, am = self._execute(plan)
         tok_dev, lp_dev = None, None
         if items:
@@ -471,6 +575,8 @@ class LLMEngine:
             new = (ev, k, items, lp_dev is not None)
         else:
             new = None
+        if roctx.ENABLED:
+            roctx.pop()
         t2 = time.perf_counter()
         self.sched.commit(so)
         for it in items:
@@ -483,6 +589,8 @@ class LLMEngine:
         st = self.stats
         st["sched_s"] += t1 - t0
         st["fwd_s"] += t2 - t1
+        if plan["graph"]:
+            st["fwd_graph_s"] += t2 - t1
         st["process_s"] += t3 - t2
         st["steps"] += 1
         st["decode_tokens"] += len(so.decode)
@@ -493,7 +601,11 @@ class LLMEngine:
         ev, k, items, has_lp = inf
         t0 = time.perf_counter()
         if ev is not None:
-            ev.synchronize()
+            if roctx.ENABLED:
+                with roctx.range("wait"):
+                    ev.synchronize()
+            else:
+                ev.synchronize()
         self.stats["wait_s"] += time.perf_counter() - t0
         S = len(items)
         toks = self._pin_tok[k][:S].tolist()
@@ -516,22 +628,51 @@ class LLMEngine:
         if inf is not None:
             self._process_inflight(inf)
 
-    def _graph_for(self, n: int) -> DecodeGraph | None:
+    def _graph_for(self, n: int) -> StepGraph | None:
+        """Decode-only graph of the bucket holding n rows."""
+        b = self._dec_bucket(n)
+        return self._graph_get((b, 0, 0)) if b else None
+
+    def _dec_bucket(self, n: int) -> int | None:
+        return next((x for x in self.cfg.graph_buckets if x >= n and x <= self.cfg.max_num_seqs), None)
+
+    def _graph_key(self, plan: dict):
+        """Shape bucket (B, P, PS) whose graph can run this plan, or None (eager)."""
+        c = self.cfg
+        if not self.use_graphs or "mm" in plan or plan["keep_hidden"]:
+            return None
+        nd = plan["nd"]
+        B = self._dec_bucket(nd) if nd else 0
+        if B is None:
+            return None
+        if "pf_cu" not in plan:
+            return (B, 0, 0) if nd else None
+        if self.recurrent or not hasattr(self.model, "prefill_rows") or len(plan["pf_cu"]) - 1 > c.mixed_graph_seqs:
+            return None
+        npf = int(plan["pf_cu"][-1])
+        P = next((x for x in c.mixed_graph_tokens if x >= npf), None)
+        if P is None or B + P > self.ws.max_tokens:
+            return None
+        return (B, P, c.mixed_graph_seqs)
+
+    def _graph_get(self, key, create: bool = True) -> StepGraph | None:
         if not self.use_graphs:
             return None
-        b = next((x for x in self.cfg.graph_buckets if x >= n and x <= self.cfg.max_num_seqs), None)
-        if b is None:
-            return None
-        g = self.graphs.get(b)
+        key = tuple(int(x) for x in key)
+        g = self.graphs.get(key)
         if g is None:
-            g = DecodeGraph(self, b)
+            if not create or len(self.graphs) >= self.cfg.max_graphs:
+                return None
+            if self._graph_pool is None:
+                self._graph_pool = torch.cuda.graph_pool_handle()
+            g = StepGraph(self, *key)
             try:
-                g.capture(self)
+                g.capture(self, self._graph_pool)
             except Exception:
-                log.exception("hipGraph capture failed for bucket %d; running eager", b)
+                log.exception("hipGraph capture failed for bucket %s; running eager", key)
                 self.use_graphs = False
                 return None
-            self.graphs[b] = g
+            self.graphs[key] = g
         return g
 
     # ------------------------------------------------------------------ step plan / execution
@@ -609,23 +750,27 @@ class LLMEngine:
                 ctx[k] = it.start + it.n
             plan["pf_bt"], plan["pf_cu"], plan["pf_ctx"] = bt, cu, ctx
             plan["keep_hidden"] = any(it.seq.req.embedding for it in pf if it.sample)
-        plan["graph"] = bool(not pf and nd and self.use_graphs and self._graph_for(nd) is not None)
+        if pf and self.device.type == "cuda" and hasattr(self.model, "prefill_rows"):
+            from ..ops.core import prefill_tiles
+            ts, tq = prefill_tiles([it.n for it in pf], self.model.prefill_rows())
+            plan["pf_tseq"], plan["pf_tq0"] = np.asarray(ts, np.int32), np.asarray(tq, np.int32)
+        key = self._graph_key(plan)
+        # tensor parallel: a capture runs collectives, so only graphs every rank captured up front
+        # (precapture_graphs: decode buckets) are used; single-rank engines capture on first use
+        g = self._graph_get(key, create=self.tp is None) if key is not None else None
+        plan["graph"] = key if g is not None and g.fits(plan) else False
         return plan
 
     def _execute(self, plan: dict):
         """Run the step's forward on this rank. Returns (logits, argmax-or-None)."""
         nd = plan["nd"]
         if plan["graph"]:
-            g = self._graph_for(nd)
-            bt = plan["dec_bt"]
-            maxb = bt.shape[1]
-            t = self._stage_plan(plan, ("tokens", "positions", "slots", "dec_lens", "dec_bt"))
-            logits, am = g.run(t["tokens"], t["positions"], t["slots"], t["dec_bt"].view(nd, maxb), t["dec_lens"], nd,
-                               fix=self._fix_tensors(t))
+            g = self._graph_get(plan["graph"])
+            logits, am = g.run(plan, self._prev_dev[0] if "fix" in plan else None)
             self.stats["graph_steps"] += 1
             return logits, am
         t = self._stage_plan(plan, ("tokens", "positions", "slots", "lidx", "dec_bt", "dec_lens", "pf_bt", "pf_cu",
-                                    "pf_ctx"))
+                                    "pf_ctx", "pf_tseq", "pf_tq0"))
         fb = self._build_fb(plan, t)
         fix = self._fix_tensors(t)
         if fix is not None:
@@ -707,6 +852,8 @@ class LLMEngine:
             fb.dec_max_len = int(plan["dec_lens"].max())
         if "pf_cu" in plan:
             fb.pf_block_tables, fb.pf_cu_q, fb.pf_ctx_lens = t["pf_bt"], t["pf_cu"], t["pf_ctx"]
+            if "pf_tseq" in t:
+                fb.pf_tiles = (t["pf_tseq"], t["pf_tq0"])
             cu = plan["pf_cu"]
             fb.pf_q_lens_host = [int(cu[k + 1] - cu[k]) for k in range(len(cu) - 1)]
             fb.pf_ctx_lens_host = [int(x) for x in plan["pf_ctx"]]

@@ -82,6 +82,7 @@ class ForwardBatch:
     pf_ctx_lens: torch.Tensor | None = None  # [S_p]
     pf_q_lens_host: list = field(default_factory=list)
     pf_ctx_lens_host: list = field(default_factory=list)
+    pf_tiles: tuple | None = None  # (seq int32 [n], q0 int32 [n]) prefill attention tiles (seq -1 = skip)
     want_hidden: bool = False  # embeddings: return normalised hidden rows instead of logits
     keep_hidden: bool = False  # also stash the final-normed hidden rows in model.last_hidden
     embed_rows: list | None = None  # [(row, fp32 [n, hidden])] input embeddings replacing token rows
@@ -385,6 +386,11 @@ class LlamaModel:
             from ..parallel import tp as TP
             TP.all_reduce_(t, self.tp_group)
 
+    def prefill_rows(self) -> int:
+        """Query rows per prefill-attention tile (attention.hip) for this model's head layout."""
+        from .. import _native as N
+        return int(N.kernels().mxk_attn_prefill_rows(self.n_heads, self.n_kv))
+
     def forward(self, fb: ForwardBatch, kv, ws: Workspace) -> torch.Tensor:
         cfg = self.cfg
         T = fb.T
@@ -437,7 +443,7 @@ class LlamaModel:
             if T > nd:
                 K.attn_prefill(q[nd:].view(T - nd, Hq, D), kc, vc, fb.pf_block_tables, fb.pf_cu_q, fb.pf_ctx_lens,
                                self.scale, attn[nd:].view(T - nd, Hq, D), fb.pf_q_lens_host, fb.pf_ctx_lens_host,
-                               window=L.window, softcap=cfg.attn_softcap)
+                               window=L.window, softcap=cfg.attn_softcap, tiles=fb.pf_tiles)
             if gemv:
                 aq, ads = ws.q8(T, qd)
                 K.quant_q8(attn, aq, ads)

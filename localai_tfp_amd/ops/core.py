@@ -381,10 +381,20 @@ ATTN_VMODE = int(__import__("os").environ.get("MX_ATTN_VMODE", "0"))
 
 def attn_prefill(q: torch.Tensor, k_cache, v_cache, block_tables: torch.Tensor, cu_q: torch.Tensor,
                  ctx_lens: torch.Tensor, scale: float, out: torch.Tensor, q_lens_host=None, ctx_lens_host=None,
-                 vmode: int | None = None, window: int = 0, softcap: float = 0.0):
-    """q bf16 [T, Hq, D] for S sequences (cu_q [S+1]); keys 0..ctx_len-1 from the paged cache."""
+                 vmode: int | None = None, window: int = 0, softcap: float = 0.0, tiles=None):
+    """q bf16 [T, Hq, D] for S sequences (cu_q [S+1]); keys 0..ctx_len-1 from the paged cache.
+    tiles: optional device (seq, q0) int32 tile lists (prefill_tiles(), padded with seq -1) prepared
+    once per step by the engine — no host lists needed, so the launch is hipGraph-capturable."""
     T, Hq, D = q.shape
     if T == 0:
+        return out
+    if tiles is not None and q.is_cuda:
+        Hkv, bs = k_cache.shape[1], k_cache.shape[2]
+        N.ensure_act(out.dtype)
+        N.kcall("mxk_attn_prefill", q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), block_tables.data_ptr(),
+                block_tables.stride(0), tiles[0].data_ptr(), tiles[1].data_ptr(), int(tiles[0].numel()),
+                cu_q.data_ptr(), ctx_lens.data_ptr(), Hq, Hkv, D, bs, float(scale), int(window), float(softcap),
+                out.data_ptr(), ATTN_VMODE if vmode is None else int(vmode), int(is_fp8(k_cache)), N.stream_ptr())
         return out
     Hkv, bs = k_cache.shape[1], k_cache.shape[2]
     cu = cu_q.tolist() if q_lens_host is None else None

@@ -36,7 +36,7 @@ log = logging.getLogger("localai_tfp_amd.tp")
 MAGIC = 0x4D585450  # "MXTP"
 K_PLAN, K_STOP, K_CAPTURE, K_PICKLE, K_HEARTBEAT = 1, 2, 3, 4, 5
 PLAN_ARRAYS = ("tokens", "positions", "slots", "lidx", "dec_bt", "dec_lens", "pf_bt", "pf_cu", "pf_ctx",
-               "fix_dst", "fix_src")
+               "pf_tseq", "pf_tq0", "fix_dst", "fix_src")
 EXIT_TP_FAILURE = 75
 
 STOP = None
@@ -44,9 +44,11 @@ STOP = None
 
 # ------------------------------------------------------------------ plan codec (int32, no pickles)
 def encode_plan(plan: dict) -> np.ndarray:
-    """Flat int32 image of a step plan: [nd, flags, then per PLAN_ARRAYS entry: ndim, *shape, *data]."""
-    flags = int(bool(plan.get("graph"))) | (int(bool(plan.get("keep_hidden"))) << 1)
-    parts = [np.array([plan["nd"], flags], np.int32)]
+    """Flat int32 image of a step plan: [nd, flags, graph bucket (B, P, PS), then per PLAN_ARRAYS
+    entry: ndim, *shape, *data]."""
+    g = plan.get("graph")
+    flags = int(bool(g)) | (int(bool(plan.get("keep_hidden"))) << 1)
+    parts = [np.array([plan["nd"], flags, *(tuple(g) if g else (0, 0, 0))], np.int32)]
     arrays = dict(plan)
     if "fix" in plan:
         arrays["fix_dst"], arrays["fix_src"] = plan["fix"]
@@ -63,8 +65,9 @@ def encode_plan(plan: dict) -> np.ndarray:
 
 def decode_plan(buf: np.ndarray) -> dict:
     nd, flags = int(buf[0]), int(buf[1])
-    plan = {"nd": nd, "graph": bool(flags & 1), "keep_hidden": bool(flags & 2)}
-    i = 2
+    plan = {"nd": nd, "graph": tuple(int(x) for x in buf[2:5]) if flags & 1 else False,
+            "keep_hidden": bool(flags & 2)}
+    i = 5
     for k in PLAN_ARRAYS:
         ndim = int(buf[i])
         i += 1

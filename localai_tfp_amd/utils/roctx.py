@@ -15,7 +15,10 @@ ENABLED = os.environ.get("MX_ROCTX") == "1"
 def _lib():
     global _LIB, ENABLED
     if _LIB is None:
-        for p in ("libroctx64.so", "/opt/rocm/lib/libroctx64.so"):
+        # rocprofv3 intercepts the rocprofiler-sdk roctx library; the roctracer-era libroctx64 is
+        # only seen by the legacy tools
+        for p in ("librocprofiler-sdk-roctx.so", "/opt/rocm/lib/librocprofiler-sdk-roctx.so", "libroctx64.so",
+                  "/opt/rocm/lib/libroctx64.so"):
             try:
                 _LIB = ctypes.CDLL(p)
                 _LIB.roctxRangePushA.argtypes = [ctypes.c_char_p]

@@ -100,3 +100,41 @@ def test_engine_concurrent_batch():
         outs = list(h)
         assert outs[-1].finished and outs[-1].finish_reason == "length"
         assert sum(len(o.token_ids) for o in outs) == 10 + i % 7
+
+
+def test_mixed_step_graph_matches_eager():
+    """A continuous-batching step holding decode rows AND a prompt chunk replays a bucketed hipGraph
+    (padded decode block, padded prefill tokens / sequences / attention tiles); its logits must match
+    the eager forward of the same plan (re-running a step rewrites identical KV entries)."""
+    from localai_tfp_amd.engine.sequence import Request
+    cfg = _cfg()
+    model = LlamaModel.load(cfg, synthetic_source(cfg, "Q4_K_M", seed=8), "cuda")
+    tok = ByteTokenizer(cfg.vocab)
+    e = LLMEngine(model, tok, EngineConfig(num_blocks=512, max_num_seqs=16, max_batched_tokens=512,
+                                           max_model_len=1024, overlap=False))
+    sp = SamplingParams(temperature=0.0, ignore_eos=True)
+    hs = [e.submit(Request(tok.encode(f"decode row {i} " * (2 + i)), sp, max_tokens=12)) for i in range(5)]
+    e._drain_inbox()
+    for _ in range(3):
+        e.step()
+    hs += [e.submit(Request(tok.encode("a longer arriving prompt " * (4 + 3 * i)), sp, max_tokens=6)) for i in range(2)]
+    e._drain_inbox()
+    so = e.sched.schedule()
+    assert so.decode and so.prefill
+    plan = e._plan(so)
+    assert plan["graph"] and plan["graph"][1] > 0, plan["graph"]
+    lg_g, am = e._execute(plan)
+    lg_g = lg_g.float().clone()
+    toks = am.cpu().tolist()
+    lg_e, _ = e._execute(dict(plan, graph=False))
+    lg_e = lg_e.float()
+    assert lg_g.shape == lg_e.shape == (len(plan["lidx"]), cfg.vocab)
+    r = float((lg_g - lg_e).norm() / lg_e.norm())
+    assert r < 2e-2, r
+    ref = lg_e.argmax(-1).int().cpu().tolist()
+    assert sum(a == b for a, b in zip(toks, ref)) >= 0.9 * len(ref), (toks, ref)
+    e.sched.commit(so)
+    e._process(so, toks, None)
+    e.run_until_done()
+    for h in hs:
+        assert list(h)[-1].finished

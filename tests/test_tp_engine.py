@@ -119,19 +119,20 @@ def test_plan_codec_roundtrip():
             "slots": np.arange(9, dtype=np.int32) + 16, "lidx": np.array([0, 1, 2, 8], np.int32),
             "dec_bt": rng.integers(0, 50, (3, 5)).astype(np.int32), "dec_lens": np.array([4, 5, 6], np.int32),
             "pf_bt": rng.integers(0, 50, (1, 2)).astype(np.int32), "pf_cu": np.array([0, 6], np.int32),
-            "pf_ctx": np.array([6], np.int32), "keep_hidden": True, "graph": False,
+            "pf_ctx": np.array([6], np.int32), "pf_tseq": np.array([0], np.int32), "pf_tq0": np.array([0], np.int32),
+            "keep_hidden": True, "graph": False,
             "fix": (np.array([0, 2], np.int64), np.array([1, 0], np.int64))}
     buf = encode_plan(plan)
     assert buf.dtype == np.int32
     out = decode_plan(buf)
     assert out["nd"] == 3 and out["keep_hidden"] and not out["graph"]
-    for k in ("tokens", "positions", "slots", "lidx", "dec_bt", "dec_lens", "pf_bt", "pf_cu", "pf_ctx"):
+    for k in ("tokens", "positions", "slots", "lidx", "dec_bt", "dec_lens", "pf_bt", "pf_cu", "pf_ctx", "pf_tseq", "pf_tq0"):
         assert np.array_equal(out[k], plan[k]) and out[k].shape == plan[k].shape, k
     assert all(np.array_equal(a, b) for a, b in zip(out["fix"], plan["fix"]))
     dec_only = decode_plan(encode_plan({"nd": 1, "tokens": np.array([5], np.int32), "positions": np.array([3], np.int32),
                                         "slots": np.array([19], np.int32), "lidx": np.array([0], np.int32),
-                                        "graph": True}))
-    assert dec_only["graph"] and "pf_cu" not in dec_only and "fix" not in dec_only
+                                        "graph": (8, 0, 0)}))
+    assert dec_only["graph"] == (8, 0, 0) and "pf_cu" not in dec_only and "fix" not in dec_only
 
 
 def _die_worker(rank, world, port, who):
