@@ -269,6 +269,265 @@ MX_DEV int v_lds_off(int p, int nt) {
     return p * (D * 2) + ((nt ^ sv) << 5);
 }
 
+// ------------------------------------------------------------------------------------------------
+// decode on MFMA. The VALU kernel above spends its time on the per-position dot products and the
+// 16-lane shuffle reductions (~30% of HBM bandwidth at B=128); here the G query heads of a kv head are
+// the rows of a 16x16x32 bf16 MFMA tile, so QK^T and PV run on the matrix cores and the softmax
+// reductions happen once per 32-key tile.
+//   workgroup = (kv head, sequence, partition), 4 waves; wave w takes the partition's 32-key tiles
+//   w, w+4, ...: K fragments come straight from the paged cache into MFMA B operands (16-byte loads,
+//   one cached position x 8 dims per lane), V is staged in the wave's LDS slice and read back with
+//   the hardware-transposing ds_read_b64_tr_b16 (same V image as the prefill kernel), P goes
+//   register -> LDS -> A fragment. The 4 waves' (m, l, O) merge through LDS at the end, in the same
+//   partial-result format as attn_decode_kernel (attn_decode_reduce merges partitions).
+// Occupancy, not register double buffering, hides HBM latency: ~9.3 KB of LDS per wave lets 4
+// workgroups (16 waves) share a CU, each with one tile's 16 KB of K/V loads in flight.
+template <int D>
+constexpr int dec_wave_lds() { return 32 * D * 2 + 16 * (32 + 8) * 2; }
+
+template <int D, bool F16, bool KV8>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KV8 ? 2 : 4, KV8 ? 2 : 4))) void attn_decode_mfma_kernel(
+    const bf16_t* __restrict__ q, int q_stride, const void* __restrict__ kcv, const void* __restrict__ vcv,
+    const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ seq_lens, int Hkv, int G, int bs,
+    float scale, int window, float softcap, int part_size, int n_parts, bf16_t* __restrict__ out, int out_stride,
+    float2* __restrict__ part_ml, float* __restrict__ part_o) {
+    constexpr int KT = 32;                      // keys per wave tile
+    constexpr int VBYTES = KT * D * 2;
+    constexpr int PSTRIDE = (KT + 8) * 2;       // bytes per P row (padded)
+    constexpr int WB = dec_wave_lds<D>();
+    constexpr int NVC = KT * D / 8 / 64;        // 16-byte V chunks per lane per tile
+    constexpr int ES = KV8 ? 1 : 2;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    constexpr int MAXB = 256;
+    __shared__ int sbt[MAXB];
+    const int kvh = blockIdx.x, b = blockIdx.y, part = blockIdx.z;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int g = lane >> 4, col = lane & 15;
+    const int L = seq_lens[b];
+    const int p0 = part * part_size;
+    const int p1 = min(L, p0 + part_size);
+    if (p0 >= L && part > 0) return;  // uniform: graphs launch n_parts for max_model_len
+    const int Hq = Hkv * G;
+    const int p_start = window > 0 ? max(p0, L - window) : p0;
+    const float qs = scale * LOG2E;
+    const float sc_l2 = softcap * LOG2E, sc_inv = softcap > 0.f ? 1.f / (softcap * LOG2E) : 0.f;
+    const int* bt = block_tables + (size_t)b * bt_stride;
+    const int blk0 = p0 / bs;
+    const int nblk = p1 > p0 ? (p1 - 1) / bs - blk0 + 1 : 0;
+    for (int i = threadIdx.x; i < nblk; i += 256) sbt[i] = bt[blk0 + i];
+    __syncthreads();
+
+    // Q as the A operand: row = head (lane col), k = dims 32 ks + 8 g
+    bf16x8 qf[D / 32];
+#pragma unroll
+    for (int ks = 0; ks < D / 32; ++ks) {
+        if (col < G) qf[ks] = *(const bf16x8*)(q + (size_t)b * q_stride + (size_t)(kvh * G + col) * D + 32 * ks + 8 * g);
+        else qf[ks] = (bf16x8){};
+    }
+    f32x4 oacc[D / 16];
+#pragma unroll
+    for (int i = 0; i < D / 16; ++i) oacc[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    float mrow[4], lrow[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { mrow[i] = -INFINITY; lrow[i] = 0.f; }
+    char* v_lds = smem + wave * WB;
+    char* pw = v_lds + VBYTES;
+    const char* kc = (const char*)kcv;
+    const char* vc = (const char*)vcv;
+
+    for (int kt0 = p_start + wave * KT; kt0 < p1; kt0 += 4 * KT) {
+        // ---- issue the tile's K fragment loads and V chunk loads ----
+        bf16x8 kf[2][D / 32];
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            const int key = kt0 + 16 * t + col;
+            const bool ok = key < p1;
+            const size_t eo = ok ? (((size_t)sbt[key / bs - blk0] * Hkv + kvh) * bs + key % bs) * D : 0;
+#pragma unroll
+            for (int ks = 0; ks < D / 32; ++ks) {
+                if constexpr (KV8) {
+                    const uint2 w = ok ? *(const uint2*)(kc + (eo + 32 * ks + 8 * g)) : make_uint2(0, 0);
+                    kf[t][ks] = __builtin_bit_cast(bf16x8, fp8x8_to_bf16x8(w));
+                } else {
+                    kf[t][ks] = ok ? *(const bf16x8*)(kc + (eo + 32 * ks + 8 * g) * ES) : (bf16x8){};
+                }
+            }
+        }
+        // V: bf16 caches go HBM -> LDS by DMA (global_load_lds, no VGPR staging): instruction j fills
+        // bytes [1024 j, 1024 j + 1024) of the slice linearly by lane, so each lane fetches the chunk
+        // that the swizzled V image (v_lds_off) places at its slot; fp8 caches widen in registers.
+        [[maybe_unused]] uint4 vv[KV8 ? NVC : 1];
+#pragma unroll
+        for (int j = 0; j < NVC; ++j) {
+            int p, c;
+            if constexpr (KV8) {
+                const int id = lane + 64 * j;
+                p = id / (D / 8);
+                c = id % (D / 8);
+            } else {
+                const int X = 1024 * j + 16 * lane;  // slot in the V image
+                p = X / (D * 2);
+                const int o = X % (D * 2);
+                int sv;
+                if constexpr (D == 128) sv = (p & 3) | (((p >> 3) & 1) << 2);
+                else sv = ((p >> 1) & 1) | (((p >> 3) & 1) << 1);
+                c = 2 * ((o >> 5) ^ sv) + ((o >> 4) & 1);
+            }
+            const int key = kt0 + p < p1 ? kt0 + p : kt0;  // past the end: a valid row (P = 0 there)
+            const size_t eo = (((size_t)sbt[key / bs - blk0] * Hkv + kvh) * bs + key % bs) * D + c * 8;
+            if constexpr (KV8) {
+                vv[j] = kt0 + p < p1 ? fp8x8_to_bf16x8(*(const uint2*)(vc + eo)) : make_uint4(0, 0, 0, 0);
+            } else {
+                __builtin_amdgcn_global_load_lds((const void*)(vc + eo * ES), (MX_LDS void*)(v_lds + 1024 * j), 16, 0, 0);
+            }
+        }
+        // ---- S = Q K^T : 16 head rows x 32 keys ----
+        f32x4 sacc[2];
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            sacc[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int ks = 0; ks < D / 32; ++ks)
+                sacc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qf[ks], kf[t][ks], sacc[t], 0, 0, 0);
+        }
+        if constexpr (KV8) {  // V -> this wave's LDS slice (the previous tile's reads have returned)
+#pragma unroll
+            for (int j = 0; j < NVC; ++j) {
+                const int id = lane + 64 * j, p = id / (D / 8), c = id % (D / 8);
+                *(uint4*)(v_lds + v_lds_off<D>(p, c >> 1) + 16 * (c & 1)) = vv[j];
+            }
+        }
+        // ---- online softmax over the tile (rows 4g+i, keys 16t+col) ----
+        float alpha[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            float mx = -INFINITY;
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                float v = sacc[t][i] * qs;
+                if (softcap > 0.f) v = sc_l2 * tanhf(v * sc_inv);
+                if (kt0 + 16 * t + col >= p1) v = -INFINITY;
+                sacc[t][i] = v;
+                mx = fmaxf(mx, v);
+            }
+            mx = group_max<16>(mx);
+            const float mn = fmaxf(mrow[i], mx);
+            alpha[i] = mn == -INFINITY ? 1.f : exp2f(mrow[i] - mn);
+            float rs = 0.f;
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                const float pv = mn == -INFINITY ? 0.f : exp2f(sacc[t][i] - mn);
+                sacc[t][i] = pv;
+                rs += pv;
+            }
+            lrow[i] = lrow[i] * alpha[i] + group_sum<16>(rs);
+            mrow[i] = mn;
+        }
+#pragma unroll
+        for (int nt = 0; nt < D / 16; ++nt)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) oacc[nt][i] *= alpha[i];
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                *(bf16_t*)(pw + (4 * g + i) * PSTRIDE + (16 * t + col) * 2) = f32_to_bf16(sacc[t][i]);
+        // vmcnt(0) + lgkmcnt(0): the V DMA has landed and the P (and fp8 V) writes are visible
+        __builtin_amdgcn_s_waitcnt(0);
+        __builtin_amdgcn_wave_barrier();
+        // ---- O += P V ----
+        const bf16x8 pa = *(const bf16x8*)(pw + col * PSTRIDE + 8 * g * 2);
+        const int r0 = 8 * g, q4 = col >> 2, p4 = col & 3;
+#pragma unroll
+        for (int nt = 0; nt < D / 16; ++nt) {
+            const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                (MX_LDS s16x4*)(v_lds + v_lds_off<D>(r0 + q4, nt) + 8 * p4));
+            const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                (MX_LDS s16x4*)(v_lds + v_lds_off<D>(r0 + 4 + q4, nt) + 8 * p4));
+            const u32x2 l2 = __builtin_bit_cast(u32x2, lo), h2 = __builtin_bit_cast(u32x2, hi);
+            const u32x4 w4 = {l2[0], l2[1], h2[0], h2[1]};
+            oacc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, __builtin_bit_cast(bf16x8, w4), oacc[nt], 0, 0, 0);
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // the transposed reads have returned before V is rewritten
+        __builtin_amdgcn_wave_barrier();
+    }
+    // ---- merge the 4 waves: (m, l) per row and O rows through the (now free) LDS slices ----
+    __syncthreads();
+    float* wo = (float*)(smem + wave * WB);        // [16 rows][D] fp32 (8 KB for D=128 <= WB)
+    float* wml = (float*)(smem + 4 * WB) + wave * 32;  // [16 rows] m, [16 rows] l
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int r = 4 * g + i;
+#pragma unroll
+        for (int nt = 0; nt < D / 16; ++nt) wo[r * D + 16 * nt + col] = oacc[nt][i];
+        if (col == 0) { wml[r] = mrow[i]; wml[16 + r] = lrow[i]; }
+    }
+    __syncthreads();
+    const float* ml = (const float*)(smem + 4 * WB);
+    for (int idx = threadIdx.x; idx < G * D; idx += 256) {
+        const int h = idx / D, d = idx % D;
+        float mx = -INFINITY;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) mx = fmaxf(mx, ml[w * 32 + h]);
+        float ls = 0.f, os = 0.f;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            const float a = mx == -INFINITY ? 0.f : exp2f(ml[w * 32 + h] - mx);
+            ls += ml[w * 32 + 16 + h] * a;
+            os += ((const float*)(smem + w * WB))[h * D + d] * a;
+        }
+        const int hq = kvh * G + h;
+        if (n_parts == 1) {
+            out[(size_t)b * out_stride + (size_t)hq * D + d] = f32_to_act<F16>(ls > 0.f ? os / ls : 0.f);
+        } else {
+            const size_t pi = ((size_t)b * Hq + hq) * n_parts + part;
+            if (d == 0) part_ml[pi] = make_float2(mx, ls);
+            part_o[pi * D + d] = os;
+        }
+    }
+}
+
+template <int D>
+static int launch_decode_mfma(const bf16_t* q, int q_stride, const void* kc, const void* vc, const int* bt,
+                              int bt_stride, const int* seq_lens, int B, int Hkv, int G, int bs, float scale,
+                              int window, float softcap, int part_size, int n_parts, bf16_t* out, int out_stride,
+                              float2* part_ml, float* part_o, int kv8, hipStream_t st) {
+    dim3 grid(Hkv, B, n_parts);
+    static_assert(16 * D * 4 <= dec_wave_lds<D>(), "merge buffer");
+    const size_t lds = 4 * dec_wave_lds<D>() + 4 * 32 * 4;
+    MX_ACT_DISPATCH({
+        if (kv8)
+            attn_decode_mfma_kernel<D, F16, true><<<grid, 256, lds, st>>>(q, q_stride, kc, vc, bt, bt_stride, seq_lens,
+                                                                         Hkv, G, bs, scale, window, softcap, part_size,
+                                                                         n_parts, out, out_stride, part_ml, part_o);
+        else
+            attn_decode_mfma_kernel<D, F16, false><<<grid, 256, lds, st>>>(q, q_stride, kc, vc, bt, bt_stride,
+                                                                          seq_lens, Hkv, G, bs, scale, window, softcap,
+                                                                          part_size, n_parts, out, out_stride, part_ml,
+                                                                          part_o);
+        if (n_parts > 1)
+            attn_decode_reduce_kernel<F16><<<B * Hkv * G, 128, 0, st>>>(part_ml, part_o, n_parts, Hkv * G, D, seq_lens,
+                                                                        part_size, out, out_stride);
+    });
+    MXK_CHECK_LAUNCH();
+}
+
+// MFMA decode for D in {64, 128} and up to 16 query heads per kv head; other shapes return
+// hipErrorInvalidValue (the caller falls back to mxk_attn_decode).
+extern "C" int mxk_attn_decode_mfma(const bf16_t* q, int q_stride, const void* kc, const void* vc, const int* bt,
+                                    int bt_stride, const int* seq_lens, int B, int Hq, int Hkv, int D, int bs,
+                                    float scale, int window, float softcap, int part_size, int n_parts, bf16_t* out,
+                                    int out_stride, float2* part_ml, float* part_o, int kv8, hipStream_t st) {
+    if (B <= 0) return 0;
+    if (Hq % Hkv || Hq / Hkv > 16) return (int)hipErrorInvalidValue;
+    if (n_parts > 1 && (!part_ml || !part_o)) return (int)hipErrorInvalidValue;
+    if (bs <= 0 || part_size / bs + 1 > 256) return (int)hipErrorInvalidValue;
+    const int G = Hq / Hkv;
+    if (D == 128) return launch_decode_mfma<128>(q, q_stride, kc, vc, bt, bt_stride, seq_lens, B, Hkv, G, bs, scale, window, softcap, part_size, n_parts, out, out_stride, part_ml, part_o, kv8, st);
+    if (D == 64) return launch_decode_mfma<64>(q, q_stride, kc, vc, bt, bt_stride, seq_lens, B, Hkv, G, bs, scale, window, softcap, part_size, n_parts, out, out_stride, part_ml, part_o, kv8, st);
+    return (int)hipErrorInvalidValue;
+}
+
 template <int D, int GW, int VT, bool F16, bool KV8>
 __global__ __launch_bounds__(512) void attn_prefill_kernel(const bf16_t* __restrict__ q,
                                                            const void* __restrict__ kc,

@@ -333,11 +333,16 @@ def _attn_ref_one(q, k_cache, v_cache, table, ctx: int, qpos0: int, scale: float
     return torch.einsum("htk,hkd->thd", p, v)
 
 
+ATTN_DECODE_IMPL = __import__("os").environ.get("MX_ATTN_DECODE", "mfma")
+
+
 def attn_decode(q: torch.Tensor, k_cache, v_cache, block_tables: torch.Tensor, seq_lens: torch.Tensor,
                 scale: float, out: torch.Tensor, part_size: int = 256, n_parts: int | None = None,
                 workspace: tuple | None = None, max_seq_len: int | None = None, window: int = 0,
-                softcap: float = 0.0):
-    """q bf16 [B, Hq, D] (one query token per sequence, at position seq_len-1)."""
+                softcap: float = 0.0, impl: str | None = None):
+    """q bf16 [B, Hq, D] (one query token per sequence, at position seq_len-1).
+    impl: "mfma" (QK^T / PV on the matrix cores, head dims 64/128, <= 16 q heads per kv head) or
+    "valu" (any shape); default MX_ATTN_DECODE (mfma)."""
     B, Hq, D = q.shape
     if B == 0:
         return out
@@ -360,7 +365,9 @@ def attn_decode(q: torch.Tensor, k_cache, v_cache, block_tables: torch.Tensor, s
     else:
         ml_t = po = None
     N.ensure_act(out.dtype)
-    N.kcall("mxk_attn_decode", q.data_ptr(), q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
+    fn = "mxk_attn_decode_mfma" if (impl or ATTN_DECODE_IMPL) == "mfma" and D in (64, 128) and Hq // Hkv <= 16 \
+        else "mxk_attn_decode"
+    N.kcall(fn, q.data_ptr(), q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
             block_tables.data_ptr(), block_tables.stride(0), seq_lens.data_ptr(), B, Hq, Hkv, D, bs, float(scale),
             int(window), float(softcap), part_size, n_parts, out.data_ptr(), out.stride(0), N.ptr(ml_t), N.ptr(po),
             int(is_fp8(k_cache)), N.stream_ptr())

@@ -182,10 +182,11 @@ def test_attention_window_softcap_gpu(D, Hq, Hkv, window, softcap):
     ref = torch.empty(B, Hq, D)
     K.attn_decode(q, kc, vc, bt, seq, scale, ref, window=window, softcap=softcap)
     for part in (256, 128):
-        out = torch.empty(B, Hq, D, dtype=torch.bfloat16, device="cuda")
-        K.attn_decode(q.cuda(), kc.cuda(), vc.cuda(), bt.cuda(), seq.cuda(), scale, out, part_size=part,
-                      window=window, softcap=softcap)
-        assert rel(out, ref) < 1.5e-2, ("decode", part)
+        for impl in ("mfma", "valu"):
+            out = torch.empty(B, Hq, D, dtype=torch.bfloat16, device="cuda")
+            K.attn_decode(q.cuda(), kc.cuda(), vc.cuda(), bt.cuda(), seq.cuda(), scale, out, part_size=part,
+                          window=window, softcap=softcap, impl=impl)
+            assert rel(out, ref) < 1.5e-2, ("decode", part, impl)
     # prefill with cached prefixes (query 0 of a chunk sits mid-context)
     q_lens, ctx = [37, 1, 130, 64], [37, 20, 300, 200]
     S = len(q_lens)

@@ -181,7 +181,8 @@ def _paged_kv(nb, Hkv, bs, D, seed):
 
 @pytest.mark.parametrize("Hq,Hkv,D", [(32, 8, 128), (8, 8, 128), (28, 4, 128), (32, 8, 64), (64, 8, 128)])
 @pytest.mark.parametrize("lens", [[1, 17, 300], [1200, 5, 2049]])
-def test_attn_decode(Hq, Hkv, D, lens):
+@pytest.mark.parametrize("impl", ["mfma", "valu"])
+def test_attn_decode(Hq, Hkv, D, lens, impl):
     bs, nb = 16, 512
     kc, vc = _paged_kv(nb, Hkv, bs, D, 1)
     B = len(lens)
@@ -197,8 +198,16 @@ def test_attn_decode(Hq, Hkv, D, lens):
     K.attn_decode(q, kc, vc, bt, seq, scale, ref)
     for part in (512, 128, 64):
         out = torch.empty(B, Hq, D, dtype=torch.bfloat16, device=DEV)
-        K.attn_decode(q.to(DEV), kc.to(DEV), vc.to(DEV), bt.to(DEV), seq.to(DEV), scale, out, part_size=part)
+        K.attn_decode(q.to(DEV), kc.to(DEV), vc.to(DEV), bt.to(DEV), seq.to(DEV), scale, out, part_size=part,
+                      impl=impl)
         assert rel(out, ref) < 1e-2, part
+    # graph-style launch: partition count for a long max_seq_len, most partitions empty
+    out = torch.empty(B, Hq, D, dtype=torch.bfloat16, device=DEV)
+    nparts = -(-4096 // 256)
+    ws = (torch.empty(B * Hq * nparts, 2, device=DEV), torch.empty(B * Hq * nparts, D, device=DEV))
+    K.attn_decode(q.to(DEV), kc.to(DEV), vc.to(DEV), bt.to(DEV), seq.to(DEV), scale, out, part_size=256,
+                  workspace=ws, max_seq_len=4096, impl=impl)
+    assert rel(out, ref) < 1e-2
 
 
 def test_probe_tr16_semantics():

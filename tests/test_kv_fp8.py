@@ -121,9 +121,10 @@ def test_attention_fp8_cache_gpu(D, Hq, Hkv):
     q = torch.randn(B, Hq, D, generator=g).bfloat16()
     ref = torch.empty(B, Hq, D)
     K.attn_decode(q, kc, vc, bt, seq, scale, ref)
-    out = torch.empty(B, Hq, D, dtype=torch.bfloat16, device="cuda")
-    K.attn_decode(q.cuda(), kc.cuda(), vc.cuda(), bt.cuda(), seq.cuda(), scale, out)
-    assert rel(out, ref) < 1.5e-2
+    for impl in ("mfma", "valu"):
+        out = torch.empty(B, Hq, D, dtype=torch.bfloat16, device="cuda")
+        K.attn_decode(q.cuda(), kc.cuda(), vc.cuda(), bt.cuda(), seq.cuda(), scale, out, impl=impl)
+        assert rel(out, ref) < 1.5e-2, impl
     q_lens, ctx = [37, 1, 130, 64], [37, 20, 300, 200]
     S = len(q_lens)
     maxb = max((c + bs - 1) // bs for c in ctx)

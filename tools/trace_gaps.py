@@ -18,7 +18,7 @@ def main(path):
     rows = []
     with open(f[0]) as fh:
         for r in csv.DictReader(fh):
-            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"][:60]))
+            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
     rows.sort()
     # last 40% of the run (steady state of the bench window)
     rows = rows[int(len(rows) * 0.6):]
@@ -43,7 +43,29 @@ def main(path):
         if b in hist:
             print(f"  gaps {b:7s} n={hist[b][0]:6d} total {hist[b][1]/1e6:.2f} ms")
     for g, n in sorted(gaps, reverse=True)[:10]:
-        print(f"  gap {g/1e3:8.1f} us before {n}")
+        print(f"  gap {g/1e3:8.1f} us before {n[:60]}")
+    # steady-tail kernel breakdown per engine step (one argmax launch per step)
+    steps = sum(1 for _, _, n in rows if n.startswith("argmax_kernel")) or 1
+    agg = {}
+    for s, e, n in rows:
+        k = _short(n)
+        a = agg.setdefault(k, [0, 0])
+        a[0] += 1
+        a[1] += e - s
+    tot = sum(v[1] for v in agg.values())
+    print(f"\nsteady tail: {steps} steps, GPU busy {tot / steps / 1e3:.1f} us/step")
+    print("| kernel | calls/step | us/step | % |\n|---|---:|---:|---:|")
+    for k, (c, t) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:25]:
+        print(f"| {k} | {c / steps:.1f} | {t / steps / 1e3:.1f} | {100 * t / tot:.1f} |")
+
+
+def _short(name):
+    import re
+    name = re.sub(r"\(.*$", "", name)
+    if name.startswith("Cijk_"):
+        mt = re.search(r"MT\d+x\d+x\d+", name)
+        return "hipBLASLt " + (mt.group(0) if mt else "")
+    return name.replace("void ", "")[:70]
 
 
 if __name__ == "__main__":
