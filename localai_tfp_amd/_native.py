@@ -78,6 +78,10 @@ KERNEL_SIGS = {
     "mxk_moe_sort": [P, I, I, I, I, P, P, P, P, P],
     "mxk_moe_combine": [P, I, P, P, I, I, I, P, I, I, P],
     "mxk_moe_qgemm16": [I, I, I, P, I, P, P, P, P, P, I, I, I, I, P, I, P],
+    # x, Nb, H, W, Cp, w, Cout, KH, KW, Kp, stride, dil, pad_h, pad_w, up, Ho, Wo, bias, tadd, ldt, res, ldr, y,
+    # ldy, act, zero, cfg, stream
+    "mxk_conv2d": [P, I, I, I, I, P, I, I, I, I, I, I, I, I, I, I, I, P, P, I, P, I, P, I, I, P, I, P],
+    "mxk_conv_tile_auto": [I, I],
 }
 
 HIP_ERRORS = {1: "hipErrorInvalidValue", 2: "hipErrorOutOfMemory", 98: "hipErrorInvalidDeviceFunction",

@@ -38,9 +38,9 @@ class ControlNetConditioningEmbedding(nn.Module):
         self.conv_out = nn.Conv2d(channels[-1], out_ch, 3, 1, 1)
 
     def run(self, x):
-        x = F.silu(conv(x, self.conv_in))
+        x = conv(x, self.conv_in, act="silu")
         for b in self.blocks:
-            x = F.silu(conv(x, b))
+            x = conv(x, b, act="silu")
         return conv(x, self.conv_out)
 
 
@@ -71,7 +71,7 @@ class ControlNetModel(UNet2DConditionModel):
         ti, ctx16, key, h = self._prologue(x, t, ctx, added, ctx_key)
         cd = cond.to(h.dtype)
         cd = cd.contiguous(memory_format=torch.channels_last) if cd.is_cuda else cd
-        h = conv(h, self.conv_in) + self.controlnet_cond_embedding.run(cd)
+        h = conv(h, self.conv_in, residual=self.controlnet_cond_embedding.run(cd))
         skips, h = self._encode(h, ti, ctx16, key)
         down = [conv(s, zc) * scale for s, zc in zip(skips, self.controlnet_down_blocks)]
         return down, conv(h, self.controlnet_mid_block) * scale

@@ -5,7 +5,8 @@ Parameters live in `torch.nn.Module`s named like the public Hugging Face / diffu
 hipBLASLt GEMMs (F.linear / addmm with fp32 accumulate into residual streams), attention on the
 MFMA flash kernel (attention_dense.hip, head dim <= 128; larger heads — only the VAE mid-block's
 single 512-wide head — use PyTorch SDPA), adaLN / gated residual / GroupNorm kernels
-(diffusion.hip), and MIOpen convolutions in channels_last (NHWC) layout.
+(diffusion.hip), and convolutions on the implicit-GEMM MFMA kernel (conv.hip, ops/conv.py) over
+channels_last (NHWC) activations, with bias / time-embedding / residual / SiLU / 2x upsampling fused.
 """
 from __future__ import annotations
 
@@ -15,6 +16,7 @@ import torch
 import torch.nn.functional as F
 from torch import nn
 
+from ...ops import conv as CV
 from ...ops import core as K
 from ...ops.linear import _fp32_out_ok
 
@@ -84,8 +86,13 @@ class GroupNorm(nn.GroupNorm):
         return K.groupnorm16(x, self.weight, self.bias, self.num_groups, self.eps, silu)
 
 
-def conv(x: torch.Tensor, m: nn.Conv2d) -> torch.Tensor:
-    return F.conv2d(x, m.weight, m.bias, m.stride, m.padding)
+def conv(x: torch.Tensor, m: nn.Conv2d, **fused) -> torch.Tensor:
+    """m(x) with optional fused epilogue / prologue (ops/conv.py: tadd, residual, act, upsample, pad)."""
+    if x.is_cuda and x.dtype in (torch.float16, torch.bfloat16):
+        return CV.conv2d(x, m, **fused)
+    if not fused:
+        return F.conv2d(x, m.weight, m.bias, m.stride, m.padding)
+    return CV.conv2d(x, m, **fused)
 
 
 def cast_module(m: nn.Module, device, dtype) -> nn.Module:

@@ -147,6 +147,17 @@ class T5Config:
     buckets: int = 32
     max_distance: int = 128
     eps: float = 1e-6
+    ff: str = "gated-gelu"  # T5 v1.1 / Flan (SD3, Flux); "relu" = original T5 (MusicGen's t5-base)
+
+    @classmethod
+    def from_hf(cls, d: dict) -> "T5Config":
+        ff = d.get("feed_forward_proj", "relu")
+        if ff not in ("relu", "gated-gelu"):
+            raise NotImplementedError(f"T5 feed_forward_proj {ff!r}")
+        return cls(vocab=d.get("vocab_size", 32128), d_model=d["d_model"], heads=d["num_heads"], d_kv=d["d_kv"],
+                   d_ff=d["d_ff"], layers=d["num_layers"], buckets=d.get("relative_attention_num_buckets", 32),
+                   max_distance=d.get("relative_attention_max_distance", 128),
+                   eps=d.get("layer_norm_epsilon", 1e-6), ff=ff)
 
 
 T5_XXL = T5Config()
@@ -180,8 +191,11 @@ class _T5SA(nn.Module):
 class _T5DRD(nn.Module):
     def __init__(self, c):
         super().__init__()
-        self.wi_0 = nn.Linear(c.d_model, c.d_ff, bias=False)
-        self.wi_1 = nn.Linear(c.d_model, c.d_ff, bias=False)
+        if c.ff == "relu":
+            self.wi = nn.Linear(c.d_model, c.d_ff, bias=False)
+        else:
+            self.wi_0 = nn.Linear(c.d_model, c.d_ff, bias=False)
+            self.wi_1 = nn.Linear(c.d_model, c.d_ff, bias=False)
         self.wo = nn.Linear(c.d_ff, c.d_model, bias=False)
 
 
@@ -232,8 +246,8 @@ class T5Encoder(nn.Module):
         return out
 
     @torch.no_grad()
-    def forward(self, ids: torch.Tensor) -> torch.Tensor:
-        """ids [B, S] -> last hidden state [B, S, d_model] fp32."""
+    def forward(self, ids: torch.Tensor, mask: torch.Tensor | None = None) -> torch.Tensor:
+        """ids [B, S] (mask [B, S]: 1 = token, 0 = padding) -> last hidden state [B, S, d_model] fp32."""
         c = self.cfg
         B, S = ids.shape
         dt = self.shared.weight.dtype
@@ -242,21 +256,27 @@ class T5Encoder(nn.Module):
         bucket = t5_buckets(pos[None, :] - pos[:, None], c.buckets, c.max_distance)
         rel = self.encoder.block[0].layer[0].SelfAttention.relative_attention_bias
         bias = rel.weight[bucket].permute(2, 0, 1)[None].to(dt)  # [1, H, S, S]
+        if mask is not None:
+            neg = torch.finfo(dt).min
+            bias = bias + torch.where(mask.to(ids.device)[:, None, None, :].bool(), 0.0, neg).to(dt)
         inner = c.heads * c.d_kv
         for blk in self.encoder.block:
             sa, ff = blk.layer[0], blk.layer[1]
             a = sa.SelfAttention
             h = self._rms(x, sa.layer_norm.weight, dt)
             q, k, v = (F.linear(h, w.weight).view(B, S, c.heads, c.d_kv).transpose(1, 2) for w in (a.q, a.k, a.v))
-            o = F.scaled_dot_product_attention(q, k, v, attn_mask=bias.expand(B, -1, -1, -1), scale=1.0)
+            o = F.scaled_dot_product_attention(q, k, v, attn_mask=bias.expand(B, -1, -1, -1).to(q.dtype), scale=1.0)
             o = o.transpose(1, 2).reshape(B * S, inner)
             linear_acc(o, a.o, x)
             h = self._rms(x, ff.layer_norm.weight, dt)
             d = ff.DenseReluDense
-            g = F.linear(h, d.wi_0.weight)
-            u = F.linear(h, d.wi_1.weight)
-            act = torch.empty_like(g)
-            K.glu(g, u, act, act="gelu_tanh")
+            if c.ff == "relu":
+                act = F.relu(F.linear(h, d.wi.weight))
+            else:
+                g = F.linear(h, d.wi_0.weight)
+                u = F.linear(h, d.wi_1.weight)
+                act = torch.empty_like(g)
+                K.glu(g, u, act, act="gelu_tanh")
             linear_acc(act, d.wo, x)
         out = self._rms(x, self.encoder.final_layer_norm.weight, torch.float32)
         return out.view(B, S, c.d_model)

@@ -90,11 +90,9 @@ class ResnetBlock2D(nn.Module):
 
     def run(self, x, t):
         """t: this block's projected time embedding [B, cout] (batched with all other blocks)."""
-        h = conv(self.norm1.run(x, silu=True), self.conv1)
-        h = h + t.to(h.dtype)[:, :, None, None]
-        h = conv(self.norm2.run(h, silu=True), self.conv2)
+        h = conv(self.norm1.run(x, silu=True), self.conv1, tadd=t)
         sc = conv(x, self.conv_shortcut) if self.conv_shortcut is not None else x
-        return sc + h
+        return conv(self.norm2.run(h, silu=True), self.conv2, residual=sc)
 
 
 class Attention(nn.Module):
@@ -337,10 +335,7 @@ class UNet2DConditionModel(nn.Module):
                 if blk.attentions is not None:
                     h = blk.attentions[i].run(h, ctx16, key)
             if blk.upsamplers is not None:
-                h = F.interpolate(h, scale_factor=2.0, mode="nearest")
-                if h.is_cuda:
-                    h = h.contiguous(memory_format=torch.channels_last)
-                h = conv(h, blk.upsamplers[0].conv)
+                h = conv(h, blk.upsamplers[0].conv, upsample=True)  # nearest 2x fused into the conv
         h = conv(self.conv_norm_out.run(h, silu=True), self.conv_out)
         return h.float()
 

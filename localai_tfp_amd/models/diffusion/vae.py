@@ -40,9 +40,8 @@ class Resnet(nn.Module):
 
     def run(self, x):
         h = conv(self.norm1.run(x, silu=True), self.conv1)
-        h = conv(self.norm2.run(h, silu=True), self.conv2)
         sc = conv(x, self.conv_shortcut) if self.conv_shortcut is not None else x
-        return sc + h
+        return conv(self.norm2.run(h, silu=True), self.conv2, residual=sc)
 
 
 class _AttnProc(nn.Module):
@@ -91,8 +90,7 @@ class _UpBlock(nn.Module):
         for r in self.resnets:
             x = r.run(x)
         if self.upsamplers is not None:
-            x = F.interpolate(x, scale_factor=2.0, mode="nearest").contiguous(memory_format=torch.channels_last)
-            x = conv(x, self.upsamplers[0].conv)
+            x = conv(x, self.upsamplers[0].conv, upsample=True)  # nearest 2x fused into the conv
         return x
 
 
@@ -106,7 +104,7 @@ class _DownBlock(nn.Module):
         for r in self.resnets:
             x = r.run(x)
         if self.downsamplers is not None:
-            x = conv(F.pad(x, (0, 1, 0, 1)), self.downsamplers[0].conv)
+            x = conv(x, self.downsamplers[0].conv, pad=(0, 0, 1, 1))  # (top, left, bottom, right)
         return x
 
 

@@ -5,7 +5,7 @@ faster-whisper backend (backend/python/faster-whisper/backend.py:26-62).
 MI355X design:
 * log-mel front end as two fp32 GEMMs on the matrix cores: framed audio x (Hann-windowed DFT basis)
   -> power spectrum -> x mel filterbank; no FFT library, one pass over the padded signal.
-* conv1d stem as implicit im2col GEMMs (three shifted views concatenated, one GEMM per conv, GELU).
+* conv1d stem as H = 1 convolutions on the implicit-GEMM MFMA kernel (ops/conv.py, bias + GELU fused).
 * transformer blocks: hipBLASLt GEMMs with the residual add fused as beta = 1 into an fp32
   residual stream; LayerNorm from norm.hip; attention on the fused MFMA flash kernel
   (attention_dense.hip) — bidirectional in the encoder, cross-attention to the audio states and
@@ -30,6 +30,7 @@ import torch
 import torch.nn.functional as F
 
 from ..ops import core as K
+from ..ops import conv as CV
 from ..ops.dense import Dense, model_dtype, to_dev
 
 SAMPLE_RATE = 16000
@@ -232,10 +233,13 @@ class WhisperModel:
         self.dtype = dt = model_dtype(device)
         dev = self.device
         self.mel = LogMel(mel_filters if mel_filters is not None else mel_filterbank(n_mels=cfg.n_mels), dev)
-        c1, c2 = get("encoder.conv1.weight"), get("encoder.conv2.weight")
-        # conv weight [out, in, 3] -> [out, 3*in] in (tap, channel) order for the im2col GEMM
-        self.conv1 = Dense(np.transpose(c1, (0, 2, 1)).reshape(c1.shape[0], -1), get("encoder.conv1.bias"), dev, dt)
-        self.conv2 = Dense(np.transpose(c2, (0, 2, 1)).reshape(c2.shape[0], -1), get("encoder.conv2.bias"), dev, dt)
+        # conv1d stem as H = 1 2-D convs on the implicit-GEMM MFMA kernel (ops/conv.py, GELU fused):
+        # weights [out, in, 3] -> [out, in, 1, 3], packed once
+        self.stem = []
+        for n in ("conv1", "conv2"):
+            w = to_dev(get(f"encoder.{n}.weight"), dev, torch.float32)[:, :, None, :]
+            b = to_dev(get(f"encoder.{n}.bias"), dev, torch.float32)
+            self.stem.append((w.to(dt), b, CV.pack_weight(w, dt) if dev.type == "cuda" else None))
         pe = get("encoder.positional_embedding")
         self.enc_pos = to_dev(pe if pe is not None else sinusoids(cfg.n_audio_ctx, cfg.n_audio_state), dev,
                               torch.float32)
@@ -268,13 +272,13 @@ class WhisperModel:
         cfg = self.cfg
         B, C, T = mel.shape
         d = cfg.n_audio_state
-        x = F.pad(mel.transpose(1, 2).to(self.dtype), (0, 0, 1, 1))  # [B, T+2, C]
-        cols = torch.cat([x[:, 0:T], x[:, 1:T + 1], x[:, 2:T + 2]], -1).reshape(B * T, 3 * C)
-        y = self.conv1(cols, act="gelu").view(B, T, d)
-        y = F.pad(y, (0, 0, 1, 1))
-        T2 = T // 2
-        cols = torch.cat([y[:, 0:2 * T2:2], y[:, 1:2 * T2 + 1:2], y[:, 2:2 * T2 + 2:2]], -1).reshape(B * T2, 3 * d)
-        h = self.conv2(cols, act="gelu").float().view(B, T2, d)
+        # [B, T, C] rows viewed as NCHW-shaped channels_last [B, C, 1, T]
+        x = mel.transpose(1, 2).to(self.dtype).contiguous()[:, None].permute(0, 3, 1, 2)
+        (w1, b1, p1), (w2, b2, p2) = self.stem
+        y = CV.conv2d(x, weight=w1, bias=b1, stride=1, pad=(0, 1, 0, 1), act="gelu", packed=p1)
+        y = CV.conv2d(y, weight=w2, bias=b2, stride=2, pad=(0, 1, 0, 1), act="gelu", packed=p2)
+        T2 = y.shape[-1]
+        h = y.permute(0, 2, 3, 1).reshape(B, T2, d).float()
         h = (h + self.enc_pos[:T2]).reshape(B * T2, d).contiguous()
         H = cfg.n_audio_head
         hd = d // H

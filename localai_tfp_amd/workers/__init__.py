@@ -23,7 +23,7 @@ WORKERS = {
     "bark-cpp": "localai_tfp_amd.workers.unsupported",
     "coqui": "localai_tfp_amd.workers.unsupported",
     "kokoro": "localai_tfp_amd.workers.unsupported",
-    "transformers-musicgen": "localai_tfp_amd.workers.unsupported",
+    "transformers-musicgen": "localai_tfp_amd.workers.musicgen",  # models/musicgen.py
     "transformers-tts": "localai_tfp_amd.workers.tts",
     "huggingface": "localai_tfp_amd.workers.huggingface",
     "langchain-huggingface": "localai_tfp_amd.workers.huggingface",
