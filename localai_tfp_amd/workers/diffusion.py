@@ -94,7 +94,10 @@ class DiffusionServicer(BackendServicer):
             if adapters:
                 from ..models.diffusion.lora import apply_adapters
                 apply_adapters(self.pipe, adapters)
-            self.defaults = dict(sampler=opts.get("sampler", "euler"), schedule=opts.get("scheduler", "default"),
+            sampler, schedule = opts.get("sampler", "euler"), opts.get("scheduler", "default")
+            if request.SchedulerType:
+                sampler, schedule = diffusers_scheduler(request.SchedulerType)
+            self.defaults = dict(sampler=sampler, schedule=schedule,
                                  cfg_scale=float(opts.get("cfg_scale", request.CFGScale or
                                                           (3.5 if isinstance(self.pipe, FX.FluxPipeline) else 7.0))),
                                  strength=float(opts.get("strength", 0.75)),
@@ -155,3 +158,24 @@ def main(argv=None):
 
 if __name__ == "__main__":
     main()
+
+
+# diffusers SchedulerType names of the reference (backend/python/diffusers/backend.py:81-133) -> this
+# framework's k-diffusion-style samplers (models/diffusion/samplers.py); a "k_" prefix selects Karras sigmas
+# like use_karras_sigmas. Exact for euler / euler_a / heun / dpm_2 / dpmpp_2m; the rest map to the
+# same-order sampler of the family (parity with diffusers' implementations unpinned: not importable here).
+DIFFUSERS_SCHEDULERS = {
+    "euler": "euler", "euler_a": "euler_a", "heun": "heun", "dpm_2": "dpm2", "dpmpp_2m": "dpm++2m",
+    "ddim": "ddim_trailing", "pndm": "ipndm", "lms": "ipndm", "unipc": "dpm++2m", "dpm_2_a": "dpm++2s_a",
+    "dpmpp_sde": "dpm++2s_a", "dpmpp_2m_sde": "dpm++2m",
+}
+
+
+def diffusers_scheduler(name: str) -> tuple[str, str]:
+    n = (name or "").strip().lower()
+    karras = n.startswith("k_")
+    if karras:
+        n = n[2:]
+    if n not in DIFFUSERS_SCHEDULERS:
+        raise ValueError(f"Invalid scheduler {name!r} (have {sorted(DIFFUSERS_SCHEDULERS)} and k_ variants)")
+    return DIFFUSERS_SCHEDULERS[n], ("karras" if karras else "default")

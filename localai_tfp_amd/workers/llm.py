@@ -121,6 +121,24 @@ class _QKey:
         self.channel, self.q = channel, q
 
 
+def _is_musicgen(request) -> bool:
+    if "musicgen" in (request.Type or "").lower():
+        return True
+    path = request.ModelFile or request.Model or ""
+    if path.startswith("synthetic:musicgen"):
+        return True
+    if path and not os.path.isabs(path) and request.ModelPath:
+        path = os.path.join(request.ModelPath, path)
+    cfg = os.path.join(path, "config.json")
+    if os.path.isfile(cfg):
+        try:
+            with open(cfg) as f:
+                return json.load(f).get("model_type") == "musicgen"
+        except (OSError, ValueError):
+            return False
+    return False
+
+
 class LLMServicer(BackendServicer):
     def __init__(self, device: str | None = None, tp=None):
         super().__init__()
@@ -166,6 +184,12 @@ class LLMServicer(BackendServicer):
     def LoadModel(self, request, context):
         import torch
         from ..models.loader import load_llm
+        if _is_musicgen(request):
+            # the reference's transformers backend serves `type: MusicgenForConditionalGeneration` models
+            # through SoundGeneration / TTS (backend/python/transformers/backend.py:452-507)
+            from .musicgen import MusicgenServicer
+            self._audio = MusicgenServicer(self.device)
+            return self._audio.LoadModel(request, context)
         if getattr(self, "preloaded", False):
             mx = self._start_mxstream()
             return pb.Result(message="preloaded" + (f"; mxstream={mx}" if mx else ""), success=True)
@@ -426,6 +450,19 @@ class LLMServicer(BackendServicer):
         finally:
             if not h.done:  # client went away: free the sequence's KV blocks now
                 self.engine.abort(req.rid)
+
+    def SoundGeneration(self, request, context):
+        a = getattr(self, "_audio", None)
+        if a is None:
+            return pb.Result(message="SoundGeneration needs a MusicGen model (type: MusicgenForConditionalGeneration)",
+                             success=False)
+        return a.SoundGeneration(request, context)
+
+    def TTS(self, request, context):
+        a = getattr(self, "_audio", None)
+        if a is None:
+            return pb.Result(message="TTS needs a MusicGen model on the transformers backend", success=False)
+        return a.TTS(request, context)
 
     def Embedding(self, request, context):
         self._need_engine(context)

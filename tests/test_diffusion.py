@@ -220,3 +220,15 @@ def test_pipeline_gpu_generates():
     a, b = vae_c.decode(z), vae_g.decode(z.cuda()).cpu()
     assert (a - b).abs().max() < 0.1
     assert math.isfinite(float(b.mean()))
+
+
+def test_diffusers_scheduler_type_names():
+    from localai_tfp_amd.models.diffusion.samplers import SAMPLERS
+    from localai_tfp_amd.workers.diffusion import DIFFUSERS_SCHEDULERS, diffusers_scheduler
+    assert diffusers_scheduler("k_dpmpp_2m") == ("dpm++2m", "karras")
+    assert diffusers_scheduler("euler_a") == ("euler_a", "default")
+    for n in DIFFUSERS_SCHEDULERS:
+        assert diffusers_scheduler(n)[0] in SAMPLERS
+    import pytest
+    with pytest.raises(ValueError):
+        diffusers_scheduler("nope")

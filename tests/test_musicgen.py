@@ -125,3 +125,14 @@ def test_musicgen_small_synthetic_gpu_runs():
     wav = m.decode_audio(codes)
     assert codes.shape == (1, 4, 13) and torch.isfinite(wav).all()
     assert wav.shape[-1] == 13 * 640
+
+
+def test_transformers_backend_serves_musicgen_type(tmp_path):
+    from localai_tfp_amd.grpc import pb
+    from localai_tfp_amd.workers.llm import LLMServicer
+    s = LLMServicer("cpu")
+    r = s.LoadModel(pb.ModelOptions(Model="synthetic:musicgen-test", Type="MusicgenForConditionalGeneration"), None)
+    assert r.success, r.message
+    dst = str(tmp_path / "a.wav")
+    r = s.SoundGeneration(pb.SoundGenerationRequest(text="drums", dst=dst, duration=0.4, sample=True), None)
+    assert r.success, r.message
