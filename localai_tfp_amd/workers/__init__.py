@@ -19,8 +19,8 @@ WORKERS = {
     "silero-vad": "localai_tfp_amd.workers.vad",
     "piper": "localai_tfp_amd.workers.tts",
     # model families not implemented here: LoadModel fails with an explicit error (workers/unsupported.py)
-    "bark": "localai_tfp_amd.workers.unsupported",
-    "bark-cpp": "localai_tfp_amd.workers.unsupported",
+    "bark": "localai_tfp_amd.workers.bark",  # models/bark.py
+    "bark-cpp": "localai_tfp_amd.workers.bark",
     "coqui": "localai_tfp_amd.workers.unsupported",
     "kokoro": "localai_tfp_amd.workers.unsupported",
     "transformers-musicgen": "localai_tfp_amd.workers.musicgen",  # models/musicgen.py

@@ -1,7 +1,6 @@
-"""Backend names of the reference whose model families this framework does not implement (Bark /
-bark.cpp, Coqui XTTS, Kokoro StyleTTS2; MusicGen is served by workers/musicgen.py). Reference:
-backend/go/bark/gobark.cpp:22-80, backend/python/coqui/backend.py:26-80,
-backend/python/kokoro/backend.py:34-99.
+"""Backend names of the reference whose model families this framework does not implement (Coqui XTTS,
+Kokoro StyleTTS2; Bark is served by workers/bark.py, MusicGen by workers/musicgen.py). Reference:
+backend/python/coqui/backend.py:26-80, backend/python/kokoro/backend.py:34-99.
 
 The worker starts and answers Health like any backend (so the process manager's lifecycle is the same),
 but LoadModel fails with an explicit error naming the backend — a request for Bark never silently gets

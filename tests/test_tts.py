@@ -160,7 +160,7 @@ def test_vits_gpu_matches_cpu():
     assert np.abs(gm - c).max() < 2e-3
 
 
-@pytest.mark.parametrize("backend", ["bark", "bark-cpp", "coqui", "kokoro"])
+@pytest.mark.parametrize("backend", ["coqui", "kokoro"])
 def test_foreign_tts_backends_refuse_explicitly(backend):
     """Backend names whose model families are not implemented never silently load VITS."""
     from localai_tfp_amd.grpc import pb
