@@ -1,0 +1,107 @@
+// allreduce.hip — one-shot all-reduce for small tensor-parallel messages (<= ~1 MB: the two row-parallel
+// partial sums per decode layer) over hipIpc-mapped peer buffers on xGMI, instead of an RCCL ring whose
+// per-hop latency dominates at these sizes (SURVEY §5 "distributed communication backend").
+//
+// Protocol ("data is the flag", 8-byte granules): every rank PUSHES each pair of its 16-bit partials to
+// every rank (itself included) as one 8-byte system-scope atomic store {tag = epoch, 2 x 16-bit payload}
+// into slot [parity][src rank] of the destination's receive buffer (uncached device memory, so a remote
+// xGMI write is seen by the owner's polling loads without any fence); then each rank polls its OWN
+// receive slots until every granule carries this call's tag and sums them in fp32. No separate flag, no
+// barrier: a granule is complete when its tag matches.
+//  * epoch lives in device memory (read at kernel start, bumped by a one-thread kernel after it), so a
+//    captured hipGraph replays correctly; epoch >= 1, the buffers are zeroed at allocation;
+//  * two parity halves: a rank can only start call e+2 (writing parity e%2 again) after it received
+//    every peer's call-e+1 data, which each peer pushes only after finishing its call-e reads;
+//  * spins are bounded: a peer that never arrives sets *err and the kernel exits (the host raises).
+// Grid: <= 128 workgroups (all resident, so no cross-rank scheduling dependency), grid-stride granules.
+#include "mx_common.h"
+
+#define MX_AR_MAX_WORLD 8
+
+struct MxArPeers {
+    unsigned long long* recv[MX_AR_MAX_WORLD];  // peer receive buffers (IPC-mapped; [rank] = local)
+};
+
+template <bool F16>
+__global__ __launch_bounds__(256) void allreduce_1shot_kernel(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
+                                                              int ng, int rank, int world, MxArPeers peers,
+                                                              long slot_granules, const uint32_t* epoch_ctr,
+                                                              int* err) {
+    const uint32_t epoch = *epoch_ctr + 1u;
+    const long par = epoch & 1u;
+    const int stride = gridDim.x * blockDim.x;
+    // phase 1: push this rank's granules to every rank's slot [par][rank]
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < ng; i += stride) {
+        const unsigned long long g = ((unsigned long long)epoch << 32) | in[i];
+        for (int p = 0; p < world; ++p) {
+            unsigned long long* dst = peers.recv[p] + (par * world + rank) * slot_granules + i;
+            __hip_atomic_store(dst, g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+    // phase 2: gather every rank's granule i from the local receive buffer, sum in fp32
+    unsigned long long* local = peers.recv[rank];
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < ng; i += stride) {
+        float a = 0.f, b = 0.f;
+        for (int p = 0; p < world; ++p) {
+            unsigned long long* src = local + (par * world + p) * slot_granules + i;
+            unsigned long long g = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            unsigned spins = 0;
+            while ((uint32_t)(g >> 32) != epoch) {
+                if (++spins > (1u << 22)) {  // ~seconds: a dead peer, not a slow one
+                    __hip_atomic_fetch_max(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    return;
+                }
+                __builtin_amdgcn_s_sleep(1);
+                g = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+            float lo, hi;
+            unpack_act2<F16>((uint32_t)g, lo, hi);
+            a += lo;
+            b += hi;
+        }
+        out[i] = pack_act2<F16>(a, b);
+    }
+}
+
+__global__ void allreduce_epoch_bump_kernel(uint32_t* epoch_ctr) {
+    if (threadIdx.x == 0) epoch_ctr[0] += 1u;
+}
+
+// ---- host side ----------------------------------------------------------------------------------
+// Receive buffer: 2 parities x world slots x slot_granules 8-byte granules, uncached device memory.
+extern "C" int mxk_ar_alloc(size_t bytes, void** ptr) {
+    hipError_t e = hipExtMallocWithFlags(ptr, bytes, hipDeviceMallocUncached);
+    if (e != hipSuccess) return (int)e;
+    return (int)hipMemset(*ptr, 0, bytes);
+}
+extern "C" int mxk_ar_free(void* ptr) { return (int)hipFree(ptr); }
+extern "C" int mxk_ar_ipc_handle(void* ptr, void* out /* 64 B */) {
+    return (int)hipIpcGetMemHandle((hipIpcMemHandle_t*)out, ptr);
+}
+extern "C" int mxk_ar_ipc_open(const void* handle /* 64 B */, void** ptr) {
+    hipIpcMemHandle_t h;
+    __builtin_memcpy(&h, handle, sizeof(h));
+    return (int)hipIpcOpenMemHandle(ptr, h, hipIpcMemLazyEnablePeerAccess);
+}
+extern "C" int mxk_ar_ipc_close(void* ptr) { return (int)hipIpcCloseMemHandle(ptr); }
+extern "C" int mxk_ar_handle_size() { return (int)sizeof(hipIpcMemHandle_t); }
+
+// in/out: n 16-bit elements (n even, 4-B aligned; out may alias in); peers: world receive-buffer pointers
+// (host array; [rank] = this rank's own buffer); slot_granules >= n / 2; epoch_ctr / err: device words.
+extern "C" int mxk_allreduce_1shot(const uint16_t* in, uint16_t* out, int n, int rank, int world,
+                                   unsigned long long* const* peers, long slot_granules, uint32_t* epoch_ctr,
+                                   int* err, hipStream_t st) {
+    if (n <= 0) return 0;
+    if ((n & 1) || world < 1 || world > MX_AR_MAX_WORLD || rank < 0 || rank >= world || (long)(n / 2) > slot_granules ||
+        ((uintptr_t)in & 3) || ((uintptr_t)out & 3))
+        return (int)hipErrorInvalidValue;
+    MxArPeers pp{};
+    for (int p = 0; p < world; ++p) pp.recv[p] = peers[p];
+    const int ng = n / 2;
+    int blocks = (ng + 255) / 256;
+    if (blocks > 128) blocks = 128;
+    MX_ACT_DISPATCH((allreduce_1shot_kernel<F16><<<blocks, 256, 0, st>>>((const uint32_t*)in, (uint32_t*)out, ng, rank,
+                                                                          world, pp, slot_granules, epoch_ctr, err)));
+    allreduce_epoch_bump_kernel<<<1, 64, 0, st>>>(epoch_ctr);
+    MXK_CHECK_LAUNCH();
+}

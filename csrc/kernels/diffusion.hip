@@ -118,15 +118,16 @@ __global__ __launch_bounds__(256) void gn_stats_kernel(const uint16_t* __restric
     __shared__ float gs[GN_MAXG], gss[GN_MAXG];
     const int n = blockIdx.y;
     const int cpr = C / 8;                 // 8-channel chunks per pixel row
-    const int rpi = 256 / cpr;             // pixel rows per iteration (cpr <= 256)
+    const int tpr = cpr < 256 ? cpr : 256; // threads per pixel row (wider rows: each thread loops chunks)
+    const int rpi = 256 / tpr;             // pixel rows per iteration
     const int t = threadIdx.x;
     if (t < GN_MAXG) { gs[t] = 0.f; gss[t] = 0.f; }
     __syncthreads();
     const int p0 = blockIdx.x * rows_per_block;
     const int p1 = min(HW, p0 + rows_per_block);
-    float s[8] = {0, 0, 0, 0, 0, 0, 0, 0}, ss[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    const int cc = t % cpr, pr = t / cpr;
-    if (pr < rpi) {
+    const int pr = t / tpr;
+    for (int cc = t % tpr; pr < rpi && cc < cpr; cc += tpr) {
+        float s[8] = {0, 0, 0, 0, 0, 0, 0, 0}, ss[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         const uint16_t* xb = x + (size_t)n * HW * C + cc * 8;
         for (int p = p0 + pr; p < p1; p += rpi) {
             const uint4 v = *(const uint4*)(xb + (size_t)p * C);
@@ -202,9 +203,9 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const uint16_t* __restric
 extern "C" int mxk_groupnorm16(const uint16_t* x, uint16_t* y, const float* gamma, const float* beta, int N, int HW,
                                int C, int G, float eps, int silu, double* ws, hipStream_t st) {
     if (N <= 0 || HW <= 0) return 0;
-    if (C % 8 || C % G || G > GN_MAXG || C / 8 > 256) return (int)hipErrorInvalidValue;
+    if (C % 8 || C % G || G > GN_MAXG) return (int)hipErrorInvalidValue;
     hipMemsetAsync(ws, 0, sizeof(double) * N * G * 2, st);
-    const int rpi = 256 / (C / 8);
+    const int rpi = 256 / (C / 8 < 256 ? C / 8 : 256);
     int rows_per_block = max(rpi * 8, (HW + 255) / 256);          // >= 8 iterations, <= 256 blocks per sample
     rows_per_block = (rows_per_block + rpi - 1) / rpi * rpi;
     dim3 g1((HW + rows_per_block - 1) / rows_per_block, N);

@@ -11,6 +11,7 @@ channels_last (NHWC) activations, with bias / time-embedding / residual / SiLU /
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 import torch.nn.functional as F
@@ -86,13 +87,37 @@ class GroupNorm(nn.GroupNorm):
         return K.groupnorm16(x, self.weight, self.bias, self.num_groups, self.eps, silu)
 
 
+_VENDOR_CONV = os.environ.get("MX_CONV", "").lower() == "miopen"  # A/B switch for benchmarks only
+
+
 def conv(x: torch.Tensor, m: nn.Conv2d, **fused) -> torch.Tensor:
     """m(x) with optional fused epilogue / prologue (ops/conv.py: tadd, residual, act, upsample, pad)."""
+    if _VENDOR_CONV and x.is_cuda:
+        return _vendor_conv(x, m, **fused)
     if x.is_cuda and x.dtype in (torch.float16, torch.bfloat16):
         return CV.conv2d(x, m, **fused)
     if not fused:
         return F.conv2d(x, m.weight, m.bias, m.stride, m.padding)
     return CV.conv2d(x, m, **fused)
+
+
+def _vendor_conv(x, m, upsample=False, pad=None, tadd=None, residual=None, act=None):
+    """The same fused op as unfused PyTorch/MIOpen calls (MX_CONV=miopen; benchmark baseline)."""
+    if upsample:
+        x = F.interpolate(x, scale_factor=2.0, mode="nearest").contiguous(memory_format=torch.channels_last)
+    if pad is not None:
+        t, l, b, r = pad
+        x = F.pad(x, (l, r, t, b))
+        y = F.conv2d(x, m.weight, m.bias, m.stride, 0)
+    else:
+        y = F.conv2d(x, m.weight, m.bias, m.stride, m.padding)
+    if tadd is not None:
+        y = y + tadd.to(y.dtype)[:, :, None, None]
+    if residual is not None:
+        y = y + residual
+    if act == "silu":
+        y = F.silu(y)
+    return y
 
 
 def cast_module(m: nn.Module, device, dtype) -> nn.Module:

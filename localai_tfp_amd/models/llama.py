@@ -322,6 +322,8 @@ class LlamaModel:
         else:
             m.lm_head = qw("output.weight")
         m.finalize_layout()
+        if tp_size > 1 and m.device.type == "cuda":
+            m.enable_custom_allreduce()  # collective: every TP rank loads the model at the same point
         return m
 
     def finalize_layout(self):
@@ -383,8 +385,22 @@ class LlamaModel:
 
     def _allreduce(self, t: torch.Tensor):
         if self.tp_size > 1:
+            ar = getattr(self, "custom_ar", None)
+            if ar is not None:
+                ar(t)  # one-shot IPC kernel for small messages, RCCL above its max_bytes
+                return
             from ..parallel import tp as TP
             TP.all_reduce_(t, self.tp_group)
+
+    def enable_custom_allreduce(self, max_bytes: int = 1 << 20):
+        """Collective over the TP group (call on every rank, outside graph capture): small row-parallel
+        all-reduces go through the one-shot hipIpc kernel (parallel/custom_ar.py). MX_CUSTOM_AR=0 disables."""
+        import os
+        if self.tp_size <= 1 or self.device.type != "cuda" or os.environ.get("MX_CUSTOM_AR", "1") == "0":
+            return None
+        from ..parallel.custom_ar import OneShotAllReduce
+        self.custom_ar = OneShotAllReduce(self.tp_group, self.device, max_bytes)
+        return self.custom_ar
 
     def prefill_rows(self) -> int:
         """Query rows per prefill-attention tile (attention.hip) for this model's head layout."""

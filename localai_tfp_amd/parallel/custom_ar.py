@@ -1,0 +1,123 @@
+"""One-shot all-reduce over hipIpc-mapped peer buffers (csrc/kernels/allreduce.hip) for the small
+tensor-parallel messages of decode steps; RCCL (torch.distributed "nccl") above ``max_bytes``.
+
+Set-up is collective over the TP group: every rank allocates an uncached receive buffer
+(2 parities x world slots x max_bytes/4 granules of 8 bytes), exports its hipIpc handle as 64 raw bytes,
+all-gathers the handles as a uint8 tensor (no pickles) and opens its peers' buffers. Works for ranks on
+different GPUs of one node (xGMI) and for several processes sharing one GPU (the CPU-launched test).
+
+    ar = OneShotAllReduce(group, device, max_bytes=1 << 20)
+    ar(t)          # in place, t: 16-bit CUDA tensor; falls back to dist.all_reduce when too large
+    ar.check()     # raises if a peer never arrived (bounded spin in the kernel)
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import torch
+
+from .. import _native as N
+
+_SIGS = {
+    "mxk_ar_alloc": [C.c_size_t, C.POINTER(C.c_void_p)],
+    "mxk_ar_free": [C.c_void_p],
+    "mxk_ar_ipc_handle": [C.c_void_p, C.c_void_p],
+    "mxk_ar_ipc_open": [C.c_void_p, C.POINTER(C.c_void_p)],
+    "mxk_ar_ipc_close": [C.c_void_p],
+    "mxk_ar_handle_size": [],
+    "mxk_allreduce_1shot": [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_void_p), C.c_long,
+                            C.c_void_p, C.c_void_p, C.c_void_p],
+}
+
+
+def _lib():
+    lib = N.kernels()
+    for n, a in _SIGS.items():
+        f = getattr(lib, n)
+        f.argtypes = a
+        f.restype = C.c_int
+    return lib
+
+
+def _ok(rc, what):
+    if rc != 0:
+        raise N.NativeError(f"{what} failed: {N.HIP_ERRORS.get(rc, rc)} ({rc})")
+
+
+class OneShotAllReduce:
+    MAX_WORLD = 8
+
+    def __init__(self, group, device, max_bytes: int = 1 << 20, rank: int | None = None, world: int | None = None):
+        import torch.distributed as dist
+        self.group = group
+        self.rank = dist.get_rank(group) if rank is None else rank
+        self.world = dist.get_world_size(group) if world is None else world
+        if self.world > self.MAX_WORLD:
+            raise ValueError(f"one-shot all-reduce supports up to {self.MAX_WORLD} ranks")
+        self.device = torch.device(device)
+        self.max_bytes = int(max_bytes)
+        self.slot = self.max_bytes // 4  # granules (2 x 16-bit elements each) per source slot
+        lib = _lib()
+        self.lib = lib
+        with torch.cuda.device(self.device):
+            self.buf = C.c_void_p()
+            _ok(lib.mxk_ar_alloc(2 * self.world * self.slot * 8, C.byref(self.buf)), "mxk_ar_alloc")
+            hs = lib.mxk_ar_handle_size()
+            h = (C.c_ubyte * hs)()
+            _ok(lib.mxk_ar_ipc_handle(self.buf, h), "hipIpcGetMemHandle")
+            mine = torch.tensor(bytearray(h), dtype=torch.uint8)
+            # the handle exchange runs on the group's backend: CPU tensors for gloo, device tensors for RCCL
+            on_dev = dist.get_backend(group) == "nccl"
+            src = mine.to(self.device) if on_dev else mine
+            allh = [torch.empty_like(src) for _ in range(self.world)]
+            dist.all_gather(allh, src, group=group)
+            self.ptrs = (C.c_void_p * self.world)()
+            self._opened = []
+            for p in range(self.world):
+                if p == self.rank:
+                    self.ptrs[p] = self.buf
+                    continue
+                hb = bytes(allh[p].cpu().numpy().tobytes())
+                ptr = C.c_void_p()
+                _ok(lib.mxk_ar_ipc_open(hb, C.byref(ptr)), "hipIpcOpenMemHandle")
+                self.ptrs[p] = ptr
+                self._opened.append(ptr)
+            self.epoch = torch.zeros(1, dtype=torch.int32, device=self.device)
+            self.err = torch.zeros(1, dtype=torch.int32, device=self.device)
+        dist.barrier(group=group)
+
+    def __call__(self, t: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+        out = t if out is None else out
+        n = t.numel()
+        if (t.dtype not in (torch.float16, torch.bfloat16) or n * 2 > self.max_bytes or n % 2
+                or not t.is_contiguous() or not out.is_contiguous()):
+            import torch.distributed as dist
+            if out is not t:
+                out.copy_(t)
+            dist.all_reduce(out, group=self.group)
+            return out
+        N.ensure_act(t.dtype)
+        _ok(self.lib.mxk_allreduce_1shot(t.data_ptr(), out.data_ptr(), n, self.rank, self.world, self.ptrs,
+                                         self.slot, self.epoch.data_ptr(), self.err.data_ptr(),
+                                         N.stream_ptr(self.device)), "mxk_allreduce_1shot")
+        return out
+
+    def check(self):
+        if int(self.err.item()):
+            raise RuntimeError("one-shot all-reduce: a peer never delivered its data (rank dead or desynchronised)")
+
+    def close(self):
+        for p in self._opened:
+            self.lib.mxk_ar_ipc_close(p)
+        self._opened = []
+        if self.buf:
+            self.lib.mxk_ar_free(self.buf)
+            self.buf = C.c_void_p()
+
+    def __del__(self):
+        try:
+            if os.environ.get("MX_AR_NO_FREE") is None:
+                self.close()
+        except Exception:
+            pass

@@ -1,0 +1,61 @@
+"""Helper process for test_custom_ar.py: one rank of a one-shot all-reduce group (gloo for the handle
+exchange and the reference; all ranks may share one GPU)."""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+
+def main():
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    ndev = torch.cuda.device_count()
+    dev = torch.device("cuda", rank % ndev)
+    torch.cuda.set_device(dev)
+    from localai_tfp_amd.parallel.custom_ar import OneShotAllReduce
+    ar = OneShotAllReduce(dist.group.WORLD, dev, max_bytes=1 << 20)
+    ok = True
+    for it, (n, dt) in enumerate([(2, torch.float16), (4096, torch.bfloat16), (8192 * 4, torch.float16),
+                                  (131072, torch.bfloat16), (524288, torch.float16), (4096, torch.float16)]):
+        g = torch.Generator().manual_seed(1000 * it + rank)
+        x = torch.randn(n, generator=g)
+        parts = [torch.randn(n, generator=torch.Generator().manual_seed(1000 * it + r)) for r in range(world)]
+        ref = sum(p.to(dt).float() for p in parts)
+        t = x.to(dev, dt)
+        ar(t)
+        torch.cuda.synchronize()
+        ar.check()
+        err = (t.float().cpu() - ref).abs().max().item()
+        tol = 1e-2 if dt == torch.float16 else 6e-2
+        ok &= err < tol * max(1.0, ref.abs().max().item())
+        print(f"rank {rank} n={n} {dt} err={err:.3g}", flush=True)
+    # hipGraph capture + replays (epoch counter lives on the device)
+    t = torch.zeros(8192, device=dev, dtype=torch.float16)
+    s = torch.cuda.Stream(dev)
+    s.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(s):
+        t.fill_(rank + 1)
+        ar(t)
+    torch.cuda.current_stream(dev).wait_stream(s)
+    torch.cuda.synchronize()
+    dist.barrier()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        t.fill_(rank + 1)
+        ar(t)
+    for _ in range(5):
+        graph.replay()
+        torch.cuda.synchronize()
+        ar.check()
+        ok &= bool((t.float() == world * (world + 1) / 2).all())
+    print(f"rank {rank} graph ok={ok}", flush=True)
+    dist.barrier()
+    ar.close()
+    dist.destroy_process_group()
+    sys.exit(0 if ok else 3)
+
+
+if __name__ == "__main__":
+    main()

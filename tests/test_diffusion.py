@@ -180,7 +180,8 @@ def test_diffusion_kernels_gpu(dt):
     K.gate_add(xg, y.cuda(), md[:, 2 * H:3 * H], Sq)
     assert (xg.cpu() - xr).abs().max() < 1e-4 * xr.abs().max()
     # groupnorm (+silu) NHWC for VAE / UNet channel counts
-    for C, G, HW in ((128, 32, (64, 48)), (512, 32, (17, 9)), (320, 32, (8, 8))):
+    # 2560 / 2880: SDXL up-block concatenations (more than 256 8-channel chunks per pixel)
+    for C, G, HW in ((128, 32, (64, 48)), (512, 32, (17, 9)), (320, 32, (8, 8)), (2560, 32, (16, 16)), (2880, 32, (5, 7))):
         t = (torch.randn(2, C, *HW, generator=g) * 2 + 0.5).to(dt)
         w = torch.rand(C, generator=g) + 0.5
         b = torch.randn(C, generator=g)
