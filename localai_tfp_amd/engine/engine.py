@@ -31,6 +31,36 @@ from .sequence import Request, Sequence, Status, StepOutput
 
 log = logging.getLogger("localai_tfp_amd.engine")
 
+# ---- serving-loop GC policy ----------------------------------------------------------------------
+# A full (generation-2) collection walks every live Python object — the model's parameter wrappers,
+# tokenizer tables, request state — and stalls the engine thread for milliseconds while the GPU idles
+# (profiles: 5-7 ms host bubbles). After load / graph capture everything alive is frozen into the
+# permanent generation (never rescanned) and young collections are made rarer; pauses are counted.
+GC_STATS = {"gc_s": 0.0, "gc_n": 0, "gc_max_ms": 0.0}
+_gc_t0 = [0.0]
+
+
+def _gc_cb(phase, info):
+    if phase == "start":
+        _gc_t0[0] = time.perf_counter()
+    else:
+        dt = time.perf_counter() - _gc_t0[0]
+        GC_STATS["gc_s"] += dt
+        GC_STATS["gc_n"] += 1
+        GC_STATS["gc_max_ms"] = max(GC_STATS["gc_max_ms"], dt * 1e3)
+
+
+def gc_tune():
+    import gc
+    import os
+    if _gc_cb not in gc.callbacks:
+        gc.callbacks.append(_gc_cb)
+    if os.environ.get("MX_GC_TUNE", "1") == "0":
+        return
+    gc.collect()
+    gc.freeze()
+    gc.set_threshold(50_000, 50, 1000)
+
 
 @dataclass
 class EngineConfig:
@@ -406,6 +436,7 @@ class LLMEngine:
         for b in self.cfg.graph_buckets:
             if b <= self.cfg.max_num_seqs and self._graph_for(b) is not None:  # decode-only buckets
                 n += 1
+        gc_tune()
         return n
 
     def start(self):
@@ -431,6 +462,7 @@ class LLMEngine:
     def _loop(self):
         if self.device.type == "cuda":
             torch.cuda.set_device(self.device)
+        gc_tune()
         while not self._stop:
             self._drain_inbox()
             self.flush_outputs()
@@ -477,7 +509,11 @@ class LLMEngine:
 
     def _step(self):
         t0 = time.perf_counter()
-        so = self.sched.schedule()
+        if roctx.ENABLED:
+            with roctx.range("schedule"):
+                so = self.sched.schedule()
+        else:
+            so = self.sched.schedule()
         for s in so.preempted:
             if s.status == Status.FINISHED:
                 self._finish(s, s.finish_reason or "error")
@@ -544,7 +580,11 @@ class LLMEngine:
         """Launch this step without waiting for it; then read the previous step's tokens (its async
         copy has landed or lands while this step runs) and post-process them."""
         t1 = time.perf_counter()
+        if roctx.ENABLED:
+            roctx.push("plan")
         plan = self._plan(so)
+        if roctx.ENABLED:
+            roctx.pop()
         self.stats["plan_s"] += time.perf_counter() - t1
         items = list(so.decode) + [it for it in so.prefill if it.sample]
         if roctx.ENABLED:
@@ -584,7 +624,11 @@ class LLMEngine:
         prev, self._inflight = self._inflight, new
         self._prev_dev = (tok_dev, {it.seq.rid: r for r, it in enumerate(items)}) if items else None
         if prev is not None:
-            self._process_inflight(prev)
+            if roctx.ENABLED:
+                with roctx.range("process_prev"):
+                    self._process_inflight(prev)
+            else:
+                self._process_inflight(prev)
         t3 = time.perf_counter()
         st = self.stats
         st["sched_s"] += t1 - t0
