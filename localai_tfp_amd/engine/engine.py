@@ -13,6 +13,7 @@ receives `StepOutput`s (the reference's task/result queues, utils.hpp:192-409).
 """
 from __future__ import annotations
 
+import collections
 import logging
 import queue
 import threading
@@ -86,6 +87,9 @@ class EngineConfig:
     # overlap the host with the GPU: launch step N, then read step N-1's sampled tokens (async
     # device->host copy) and schedule N+1 while N runs; decode inputs come from the device
     overlap: bool = True
+    # launched-but-unread steps kept in flight (2: the host post-processes step N-2 while N-1 runs and N
+    # is queued, so a slow host step — request arrivals, finishes — no longer idles the GPU)
+    overlap_depth: int = int(__import__("os").environ.get("MX_OVERLAP_DEPTH", "2"))
     n_draft: int = 0  # speculative decoding: draft tokens per step (needs a draft model; 0 = off)
     spec_max_batch: int = 32  # speculate only on decode batches up to this size (latency-bound regime)
 
@@ -185,7 +189,9 @@ class StepGraph:
             if k in self.off:
                 self.view(img, k)[...] = v
         self.buf = torch.from_numpy(img.copy()).to(dev)
-        self._pin = [torch.empty(o, dtype=torch.int32).pin_memory() for _ in range(3)] if dev.type == "cuda" else None
+        # pinned staging ring: a buffer is rewritten only after the step that used it was read back
+        self._pin = [torch.empty(o, dtype=torch.int32).pin_memory() for _ in range(e.pin_ring)] \
+            if dev.type == "cuda" else None
         self._pin_i = 0
         v = {k: self.view(self.buf, k) for k in self.off}
         self.v = v
@@ -280,7 +286,7 @@ class StepGraph:
         img = self.image(plan)
         if self._pin is not None:
             k = self._pin_i
-            self._pin_i = (k + 1) % 3
+            self._pin_i = (k + 1) % len(self._pin)
             hb = self._pin[k]
             hb.numpy()[:] = img
             self.buf.copy_(hb, non_blocking=True)
@@ -368,15 +374,17 @@ class LLMEngine:
         # host staging (ring of 3: a buffer is rewritten only after the step that used it was read)
         self.overlap = bool(c.overlap and tp is None and not use_spec and not self.recurrent
                             and getattr(model, "remote", None) is None)
-        self._inflight = None
+        self._inflight = collections.deque()  # launched-but-unread steps, oldest first
         self._prev_dev = None  # (device int32 tokens of the last launched step, {rid: row})
         self._pin_tok = self._pin_lp = self._pin_in = None
         self._pin_i = 0
+        # pinned rings: one buffer per step that can be launched-but-unread (+1 being written)
+        self.pin_ring = max(3, c.overlap_depth + 1)
         if self.overlap:
             n = max(c.max_num_seqs, 1)
             pin = self.device.type == "cuda"
-            self._pin_tok = [torch.empty(n, dtype=torch.int32, pin_memory=pin) for _ in range(3)]
-            self._pin_lp = [torch.empty(n, dtype=torch.float32, pin_memory=pin) for _ in range(3)]
+            self._pin_tok = [torch.empty(n, dtype=torch.int32, pin_memory=pin) for _ in range(self.pin_ring)]
+            self._pin_lp = [torch.empty(n, dtype=torch.float32, pin_memory=pin) for _ in range(self.pin_ring)]
         self.spec = None
         if use_spec:
             from .speculative import SpeculativeDecoder
@@ -467,7 +475,7 @@ class LLMEngine:
             self._drain_inbox()
             self.flush_outputs()
             if not self.sched.has_work():
-                if self._inflight is not None:
+                if self._inflight:
                     self._drain_inflight()
                     self.flush_outputs()
                     continue
@@ -480,7 +488,7 @@ class LLMEngine:
                 self.step()
             except Exception as ex:  # fail every in-flight request loudly, keep the worker alive
                 log.exception("engine step failed")
-                self._inflight, self._prev_dev = None, None
+                self._inflight, self._prev_dev = collections.deque(), None
                 for s in list(self.sched.running) + list(self.sched.waiting):
                     s.n_pending = 0
                     self.sched.abort(s.rid)
@@ -491,7 +499,7 @@ class LLMEngine:
         """Synchronous driver (tests / bench): step until every submitted request finished."""
         self._drain_inbox()
         n = 0
-        while (self.sched.has_work() or self._inflight is not None) and n < max_steps:
+        while (self.sched.has_work() or self._inflight) and n < max_steps:
             if self.sched.has_work():
                 self.step()
             else:
@@ -520,20 +528,19 @@ class LLMEngine:
             else:
                 self.stats["preemptions"] += 1
         if so.empty:
-            if self._inflight is not None:
+            if self._inflight:
                 self._drain_inflight()
             return
         if self.overlap and self._overlap_ok(so):
-            return self._step_overlap(so, t0)
-        if self._inflight is not None:  # this step needs host-known tokens: read the in-flight one first
-            self._drain_inflight()
-            if any(it.seq.status == Status.FINISHED for it in so.decode + so.prefill):
-                # a sequence of this plan finished on the drained step: re-plan without it
-                self.sched.running = [x for x in self.sched.running if x.status != Status.FINISHED]
-                so = SchedulerOutput([it for it in so.decode if it.seq.status != Status.FINISHED],
-                                     [it for it in so.prefill if it.seq.status != Status.FINISHED])
-                if so.empty:
+            if self._inflight and not self._pending_on_device(so):
+                so = self._drain_and_filter(so)  # a pending token lives in an older step's buffer
+                if so is None:
                     return
+            return self._step_overlap(so, t0)
+        if self._inflight:  # this step needs host-known tokens: read the in-flight ones first
+            so = self._drain_and_filter(so)
+            if so is None:
+                return
         if self.spec is not None:
             for s in so.preempted:
                 self.spec.forget(s.rid)
@@ -603,7 +610,7 @@ class LLMEngine:
                 tok_dev, lp_dev = self.sampler.sample(logits, [it.seq.params for it in items], [[] for _ in items],
                                                       [it.seq.n_generated for it in items], None, None)
             k = self._pin_i
-            self._pin_i = (k + 1) % 3
+            self._pin_i = (k + 1) % self.pin_ring
             S = len(items)
             self._pin_tok[k][:S].copy_(tok_dev[:S], non_blocking=True)
             if lp_dev is not None:
@@ -621,9 +628,14 @@ class LLMEngine:
         self.sched.commit(so)
         for it in items:
             it.seq.n_pending += 1
-        prev, self._inflight = self._inflight, new
+        if new is not None:
+            self._inflight.append(new)
         self._prev_dev = (tok_dev, {it.seq.rid: r for r, it in enumerate(items)}) if items else None
-        if prev is not None:
+        # read back the oldest launched steps, keeping `overlap_depth - 1` of them (plus this one) in
+        # flight; a step without samples is a sync point (the next plan cannot gather from it)
+        keep = max(0, self.cfg.overlap_depth - 1) if items else 0
+        while len(self._inflight) > keep + (1 if new is not None else 0):
+            prev = self._inflight.popleft()
             if roctx.ENABLED:
                 with roctx.range("process_prev"):
                     self._process_inflight(prev)
@@ -666,11 +678,25 @@ class LLMEngine:
         if self.sched.deferred:
             self.sched.release_deferred()
 
+    def _pending_on_device(self, so: SchedulerOutput) -> bool:
+        """Every decode row whose input token is still in flight can gather it from the latest step."""
+        rows = self._prev_dev[1] if self._prev_dev is not None else {}
+        return all(it.seq.rid in rows for it in so.decode if it.seq.n_pending)
+
+    def _drain_and_filter(self, so: SchedulerOutput) -> SchedulerOutput | None:
+        """Read every in-flight step; drop sequences that finished on those tokens from the plan."""
+        self._drain_inflight()
+        if any(it.seq.status == Status.FINISHED for it in so.decode + so.prefill):
+            self.sched.running = [x for x in self.sched.running if x.status != Status.FINISHED]
+            so = SchedulerOutput([it for it in so.decode if it.seq.status != Status.FINISHED],
+                                 [it for it in so.prefill if it.seq.status != Status.FINISHED])
+        return None if so.empty else so
+
     def _drain_inflight(self):
-        inf, self._inflight = self._inflight, None
+        q, self._inflight = self._inflight, collections.deque()
         self._prev_dev = None
-        if inf is not None:
-            self._process_inflight(inf)
+        while q:
+            self._process_inflight(q.popleft())
 
     def _graph_for(self, n: int) -> StepGraph | None:
         """Decode-only graph of the bucket holding n rows."""
@@ -852,10 +878,10 @@ class LLMEngine:
             cap = max(n, 4 * c.max_batched_tokens + c.max_num_seqs * (6 + 2 * self.max_blocks_per_seq) + 1024)
             if self._pin_in is not None and self.device.type == "cuda":
                 torch.cuda.synchronize(self.device)  # the old ring may still source in-flight copies
-            self._pin_in = [torch.empty(cap, dtype=torch.int32).pin_memory() for _ in range(3)]
+            self._pin_in = [torch.empty(cap, dtype=torch.int32).pin_memory() for _ in range(self.pin_ring)]
             self._pin_in_i = 0
         k = self._pin_in_i
-        self._pin_in_i = (k + 1) % 3
+        self._pin_in_i = (k + 1) % len(self._pin_in)
         hb = self._pin_in[k][:n]
         hb.numpy()[:] = flat
         return hb.to(self.device, non_blocking=True)

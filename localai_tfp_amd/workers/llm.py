@@ -454,15 +454,20 @@ class LLMServicer(BackendServicer):
     def SoundGeneration(self, request, context):
         a = getattr(self, "_audio", None)
         if a is None:
-            return pb.Result(message="SoundGeneration needs a MusicGen model (type: MusicgenForConditionalGeneration)",
-                             success=False)
+            return self._no_audio(context, "SoundGeneration needs a MusicGen model (type: MusicgenForConditionalGeneration)")
         return a.SoundGeneration(request, context)
 
     def TTS(self, request, context):
         a = getattr(self, "_audio", None)
         if a is None:
-            return pb.Result(message="TTS needs a MusicGen model on the transformers backend", success=False)
+            return self._no_audio(context, "TTS is not implemented by the LLM backend (MusicGen models only)")
         return a.TTS(request, context)
+
+    @staticmethod
+    def _no_audio(context, msg):
+        if context is not None:
+            context.abort(grpc.StatusCode.UNIMPLEMENTED, msg)
+        return pb.Result(message=msg, success=False)
 
     def Embedding(self, request, context):
         self._need_engine(context)

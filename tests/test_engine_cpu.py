@@ -180,7 +180,16 @@ def test_overlap_mode_matches_sync(model, max_tokens_budget):
         assert a == b
         # every block returned once everything finished
         assert e_ovl.bm.num_free == e_sync.bm.num_free
-        assert not e_ovl.sched.deferred and e_ovl._inflight is None
+        assert not e_ovl.sched.deferred and not e_ovl._inflight
+
+
+@pytest.mark.parametrize("depth", [1, 3])
+def test_overlap_depth_matches_sync(model, depth):
+    """Deeper overlap pipelines (several launched-but-unread steps) give the synchronous outputs too."""
+    e_sync, _ = mk(model, overlap=False, max_batched_tokens=64)
+    e_ovl, _ = mk(model, overlap=True, max_batched_tokens=64, overlap_depth=depth)
+    assert _run_all(e_sync, _mixed_requests()) == _run_all(e_ovl, _mixed_requests())
+    assert e_ovl.bm.num_free == e_sync.bm.num_free and not e_ovl._inflight
 
 
 def test_overlap_abort_mid_flight(model):
@@ -199,4 +208,4 @@ def test_overlap_abort_mid_flight(model):
         outs1.append(h1.q.get_nowait())
     assert outs1[-1].finished and outs1[-1].finish_reason == "abort"
     assert e.bm.num_free == free0 or e.cfg.enable_prefix_cache  # cached blocks may stay resident
-    assert not e.sched.deferred and e._inflight is None
+    assert not e.sched.deferred and not e._inflight

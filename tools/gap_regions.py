@@ -15,7 +15,17 @@ def main(path, min_us=300.0):
     db = sqlite3.connect(glob.glob(os.path.join(path, "**", "*.db"), recursive=True)[0])
     ks = list(db.execute("select start,end from kernels order by start"))
     ks = ks[int(len(ks) * 0.5):]
-    regs = list(db.execute("select start,end,name from regions where category like '%MARKER%' order by start"))
+    cols = [r[1] for r in db.execute("pragma table_info(regions)")]
+    # the roctx message (range label) is in the region's args / extdata JSON, the name is the API call
+    lab = next((c for c in ("extdata", "args", "message") if c in cols), "name")
+    sample = list(db.execute(f"select name, {lab} from regions where category like '%MARKER%' limit 3"))
+    print("regions columns:", cols, "label column:", lab, "sample:", sample)
+    raw = list(db.execute(f"select start,end,{lab} from regions where category like '%MARKER%' order by start"))
+    import re
+    regs = []
+    for s, e, t in raw:
+        m = re.search(r'(engine\.step|schedule|plan|launch graph|launch eager|process_prev|wait|decode=)', str(t))
+        regs.append((s, e, m.group(1) if m else str(t)[:30]))
     gaps, end = [], ks[0][0]
     for s, e in ks:
         if s - end > min_us * 1e3:
