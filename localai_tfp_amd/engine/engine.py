@@ -88,8 +88,10 @@ class EngineConfig:
     # device->host copy) and schedule N+1 while N runs; decode inputs come from the device
     overlap: bool = True
     # launched-but-unread steps kept in flight (2: the host post-processes step N-2 while N-1 runs and N
-    # is queued, so a slow host step — request arrivals, finishes — no longer idles the GPU)
-    overlap_depth: int = int(__import__("os").environ.get("MX_OVERLAP_DEPTH", "2"))
+    # is queued, so a slow host step no longer idles the GPU). Default 1: at c128 the step is GPU-bound
+    # and depth 2 measured the same throughput with a worse TTFT (profiles/r2_verify_depth_{1,2}.json:
+    # 13618 vs 13590 tok/s, p50 TTFT 18.8 vs 30.2 ms)
+    overlap_depth: int = int(__import__("os").environ.get("MX_OVERLAP_DEPTH", "1"))
     n_draft: int = 0  # speculative decoding: draft tokens per step (needs a draft model; 0 = off)
     spec_max_batch: int = 32  # speculate only on decode batches up to this size (latency-bound regime)
 
