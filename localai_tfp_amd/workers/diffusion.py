@@ -16,6 +16,11 @@ LoRA: LoraAdapter (+LoraScale) and LoraAdapters (+LoraScales) — kohya or diffu
 are merged into the weights at load (models/diffusion/lora.py). ControlNet (UNet pipelines): a diffusers
 ControlNetModel directory or `synthetic`; with it set, `src` is the control image (option control_scale).
 GenerateImage: positive / negative prompt, width, height, step, seed, dst (PNG), src (img2img).
+Video (models/diffusion/svd.py): PipelineType StableVideoDiffusionPipeline (or `synthetic:svd | svd-xt |
+svd-test`, or a directory whose model_index.json names that pipeline) loads Stable Video Diffusion;
+GenerateImage with src = start image, or GenerateVideo (start_image, width, height, num_frames, fps, seed,
+cfg_scale = max guidance), writes the clip to dst (MP4 Motion-JPEG, or .gif / .webp). Options: steps, fps,
+motion_bucket_id, noise_aug_strength, min_guidance_scale, max_guidance_scale, decode_chunk_size.
 One image per call; data parallelism = one worker replica per GPU (model config `data_parallel`),
 with the gateway spreading concurrent requests across replicas.
 """
@@ -53,6 +58,21 @@ class DiffusionServicer(BackendServicer):
             from ..models.diffusion import flux as FX
             from ..models.diffusion import sd_pipeline as U
             path = request.ModelFile or request.Model
+            from ..models.diffusion import svd as SV
+            if _is_svd(request, path):
+                if path.startswith("synthetic:"):
+                    self.pipe = SV.SVDPipeline.synthetic(path.split(":", 1)[1] or "svd-xt", self.device)
+                else:
+                    if not os.path.isabs(path) and request.ModelPath:
+                        path = os.path.join(request.ModelPath, path)
+                    self.pipe = SV.SVDPipeline.from_diffusers(path, self.device)
+                self.defaults = dict(steps=int(opts.get("steps", 25)), fps=int(opts.get("fps", 7)),
+                                     motion_bucket_id=int(opts.get("motion_bucket_id", 127)),
+                                     noise_aug_strength=float(opts.get("noise_aug_strength", 0.02)),
+                                     min_guidance=float(opts.get("min_guidance_scale", 1.0)),
+                                     max_guidance=float(opts.get("max_guidance_scale", request.CFGScale or 3.0)),
+                                     decode_chunk=int(opts.get("decode_chunk_size", 8)))
+                return pb.Result(message="loaded", success=True)
             if path.startswith("synthetic:"):
                 name = path.split(":", 1)[1]
                 if not use_t5 and name == "sd3-medium":
@@ -107,10 +127,49 @@ class DiffusionServicer(BackendServicer):
             log.exception("LoadModel failed")
             return pb.Result(message=f"failed to load model: {ex}", success=False)
 
+    def _video(self, src: str, dst: str, width: int, height: int, frames: int, fps: int, seed: int,
+               cfg_scale: float):
+        from PIL import Image
+
+        from ..models.diffusion.svd import VideoParams
+        from ..utils.video import write_video
+        if not src:
+            raise ValueError("image-to-video needs a start image (src / start_image)")
+        d = self.defaults
+        vp = VideoParams(width=width or 1024, height=height or 576, num_frames=frames, steps=d["steps"],
+                         fps=fps or d["fps"], motion_bucket_id=d["motion_bucket_id"],
+                         noise_aug_strength=d["noise_aug_strength"], min_guidance=d["min_guidance"],
+                         max_guidance=cfg_scale or d["max_guidance"], seed=seed, decode_chunk=d["decode_chunk"])
+        with Image.open(src) as im:
+            out = self.pipe.generate(im.convert("RGB"), vp)
+        write_video(out, dst, fps=vp.fps)
+
+    def GenerateVideo(self, request, context):
+        """backend.proto GenerateVideoRequest (core/backend/video.go:22): start_image -> video at dst."""
+        from ..models.diffusion.svd import SVDPipeline
+        if not isinstance(self.pipe, SVDPipeline):
+            return pb.Result(message="this model does not generate video (load a StableVideoDiffusionPipeline)",
+                             success=False)
+        try:
+            self._video(request.start_image, request.dst, request.width, request.height, request.num_frames,
+                        request.fps, request.seed, request.cfg_scale)
+            return pb.Result(message="Media generated successfully", success=True)
+        except Exception as ex:
+            log.exception("GenerateVideo failed")
+            return pb.Result(message=f"generation failed: {ex}", success=False)
+
     def GenerateImage(self, request, context):
         from ..models.diffusion.pipeline import GenParams, load_image, save_png
+        from ..models.diffusion.svd import SVDPipeline
         if self.pipe is None:
             return pb.Result(message="model not loaded", success=False)
+        if isinstance(self.pipe, SVDPipeline):  # img2vid through GenerateImage (backend.py:338-341)
+            try:
+                self._video(request.src, request.dst, request.width, request.height, 0, 0, request.seed, 0.0)
+                return pb.Result(message="Media generated successfully", success=True)
+            except Exception as ex:
+                log.exception("img2vid failed")
+                return pb.Result(message=f"generation failed: {ex}", success=False)
         try:
             w = request.width or 512
             h = request.height or 512
@@ -141,6 +200,21 @@ def _lora_list(request) -> list[tuple[str, float]]:
     for i, p in enumerate(request.LoraAdapters):
         out.append((full(p), scales[i] if i < len(scales) else 1.0))
     return out
+
+
+def _is_svd(request, path: str) -> bool:
+    """StableVideoDiffusionPipeline by pipeline type, synthetic preset name or model_index.json."""
+    import json
+    if request.PipelineType == "StableVideoDiffusionPipeline":
+        return True
+    if path.startswith("synthetic:"):
+        return path.split(":", 1)[1].startswith("svd")
+    try:
+        with open(os.path.join(path if os.path.isabs(path) else os.path.join(request.ModelPath or "", path),
+                               "model_index.json")) as f:
+            return json.load(f).get("_class_name") == "StableVideoDiffusionPipeline"
+    except (OSError, ValueError):
+        return False
 
 
 def _is_flux(path: str) -> bool:
