@@ -74,11 +74,12 @@ struct QmmGeom {
     static constexpr int WBYTES = D_OFF + DI * 256;        // per wave per stage
 };
 
-// ring depth: as many k-tiles in flight as the LDS holds (memory-level parallelism), capped
-template <int QT, int WM, int WN, int NW>
+// ring depth: as many k-tiles in flight as the LDS holds (memory-level parallelism), capped. OCC = 2 halves
+// the budget so two workgroups share a CU (twice the waves to hide dequant / LDS latency, at a shallower ring)
+template <int QT, int WM, int WN, int NW, int OCC = 1>
 struct QmmRing {
     static constexpr int STAGE = 32 * WM * 128 + NW * QmmGeom<QT, WN>::WBYTES;
-    static constexpr int S0 = QMM_LDS_BUDGET / STAGE;
+    static constexpr int S0 = QMM_LDS_BUDGET / OCC / STAGE;
     static constexpr int STAGES = S0 > QMM_MAX_STAGES ? QMM_MAX_STAGES : S0;
 };
 
@@ -229,10 +230,11 @@ struct QmmB<MXQ_Q8_0> {
 // a workgroup of 4 waves leaves one wave per SIMD, whose dequant VALU, LDS-read latency and MFMAs then
 // serialise (measured: loads alone took half the kernel time); KS = 2 puts two waves on every SIMD
 // without dequantising any weight twice.
-template <int QT, int WM, int WN, int NW, int KS, int EPI>
-// The ring takes the whole LDS, so a CU holds one workgroup: tell the scheduler that NW*KS/4 waves per SIMD
-// is the occupancy (it otherwise sinks the LDS reads next to their MFMAs to save registers nobody can use).
-__global__ __launch_bounds__(64 * NW * KS) __attribute__((amdgpu_waves_per_eu(NW * KS / 4, NW * KS / 4))) void
+template <int QT, int WM, int WN, int NW, int KS, int OCC, int EPI>
+// The ring takes the whole LDS (1/OCC of it), so a CU holds OCC workgroups: tell the scheduler that
+// OCC*NW*KS/4 waves per SIMD is the occupancy (it otherwise sinks the LDS reads next to their MFMAs to save
+// registers nobody can use).
+__global__ __launch_bounds__(64 * NW * KS) __attribute__((amdgpu_waves_per_eu(OCC * NW * KS / 4, OCC * NW * KS / 4))) void
 qmm_kernel(const uint16_t* __restrict__ A, int lda, const uint8_t* __restrict__ W, const uint16_t* __restrict__ WD,
            int M, int N, int K, int n_ct, int n_mt, int splits, int kt_per_split, void* __restrict__ Cv, int ldc) {
     using G = QmmGeom<QT, WN>;
@@ -240,8 +242,9 @@ qmm_kernel(const uint16_t* __restrict__ A, int lda, const uint8_t* __restrict__ 
     constexpr int BM = 32 * WM, COLS = G::COLS;
     constexpr int A_BYTES = BM * 128;
     constexpr int STAGE = A_BYTES + NW * G::WBYTES;
-    constexpr int NS = QmmRing<QT, WM, WN, NW>::STAGES;
-    static_assert(STAGE == QmmRing<QT, WM, WN, NW>::STAGE && NS >= 3, "ring");
+    constexpr int NS = QmmRing<QT, WM, WN, NW, OCC>::STAGES;
+    static_assert(STAGE == QmmRing<QT, WM, WN, NW, OCC>::STAGE && NS >= 3, "ring");
+    static_assert(KS == 1 || NW * WM * WN * 16 * 64 * 4 <= NS * STAGE, "k-split partials fit in the ring");
     constexpr int NT = NW * KS;       // waves
     constexpr int WA = BM / 8 / NT;   // A-tile LDS-DMA instructions per wave (8 rows x 128 B each)
     static_assert(WA >= 1 && WA * 8 * NT == BM, "A tile split");
@@ -527,14 +530,18 @@ qmm_kernel(const uint16_t* __restrict__ A, int lda, const uint8_t* __restrict__ 
     }
 }
 
-template <int QT, int WM, int WN, int NW, int KS, int EPI>
+template <int QT, int WM, int WN, int NW, int KS, int OCC, int EPI>
 static int launch_qmm(const uint16_t* A, int lda, const uint8_t* W, const uint16_t* WD, int M, int N, int K,
                       int splits, void* C, int ldc, hipStream_t st) {
     using G = QmmGeom<QT, WN>;
     constexpr int BM = 32 * WM, BN = NW * G::COLS;
     constexpr int STAGE = BM * 128 + NW * G::WBYTES;
-    constexpr size_t lds = (size_t)QmmRing<QT, WM, WN, NW>::STAGES * STAGE;
-    static_assert(lds <= 160 * 1024, "LDS");
+    constexpr int NS = QmmRing<QT, WM, WN, NW, OCC>::STAGES;
+    if constexpr (NS < 3 || (KS > 1 && NW * WM * WN * 16 * 64 * 4 > NS * STAGE)) {
+        return (int)hipErrorInvalidValue;  // this format's stage does not fit OCC rings of >= 3 k-tiles
+    } else {
+    constexpr size_t lds = (size_t)NS * STAGE;
+    static_assert(lds * OCC <= 160 * 1024, "LDS");
     const int nkt = K / QMM_KT;
     splits = max(1, min(splits, nkt));
     const int ktps = (nkt + splits - 1) / splits;
@@ -544,24 +551,30 @@ static int launch_qmm(const uint16_t* A, int lda, const uint8_t* W, const uint16
     if (nwg <= 0 || nwg > 0x7fffffff) return (int)hipErrorInvalidValue;
     static bool attr_set = false;
     if (!attr_set) {
-        (void)hipFuncSetAttribute((const void*)qmm_kernel<QT, WM, WN, NW, KS, EPI>,
+        (void)hipFuncSetAttribute((const void*)qmm_kernel<QT, WM, WN, NW, KS, OCC, EPI>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         attr_set = true;
     }
-    qmm_kernel<QT, WM, WN, NW, KS, EPI><<<dim3((unsigned)nwg), 64 * NW * KS, lds, st>>>(A, lda, W, WD, M, N, K, n_ct,
+    qmm_kernel<QT, WM, WN, NW, KS, OCC, EPI><<<dim3((unsigned)nwg), 64 * NW * KS, lds, st>>>(A, lda, W, WD, M, N, K, n_ct,
                                                                                      n_mt, splits, ktps, C, ldc);
     MXK_CHECK_LAUNCH();
+    }
 }
 
 template <int QT, int EPI>
 static int dispatch_qmm(int wm, int wn, int nw, int ks, const uint16_t* A, int lda, const uint8_t* W, const uint16_t* WD,
                         int M, int N, int K, int splits, void* C, int ldc, hipStream_t st) {
-#define QMM_CASE(WM_, WN_, NW_, KS_)                                                                          \
-    if (wm == WM_ && wn == WN_ && nw == NW_ && ks == KS_)                                                     \
-        return launch_qmm<QT, WM_, WN_, NW_, KS_, EPI>(A, lda, W, WD, M, N, K, splits, C, ldc, st);
-    QMM_CASE(1, 1, 4, 1) QMM_CASE(2, 1, 4, 1) QMM_CASE(4, 1, 4, 1) QMM_CASE(1, 2, 4, 1) QMM_CASE(2, 2, 4, 1)
-    QMM_CASE(4, 2, 4, 1) QMM_CASE(2, 1, 8, 1) QMM_CASE(4, 1, 8, 1) QMM_CASE(2, 2, 8, 1) QMM_CASE(4, 2, 8, 1)
-    QMM_CASE(2, 1, 4, 2) QMM_CASE(4, 1, 4, 2) QMM_CASE(2, 2, 4, 2)
+    const int occ = 1 + (ks >> 4);
+    ks &= 15;
+#define QMM_CASE(WM_, WN_, NW_, KS_, OCC_)                                                                    \
+    if (wm == WM_ && wn == WN_ && nw == NW_ && ks == KS_ && occ == OCC_)                                      \
+        return launch_qmm<QT, WM_, WN_, NW_, KS_, OCC_, EPI>(A, lda, W, WD, M, N, K, splits, C, ldc, st);
+    QMM_CASE(1, 1, 4, 1, 1) QMM_CASE(2, 1, 4, 1, 1) QMM_CASE(4, 1, 4, 1, 1) QMM_CASE(1, 2, 4, 1, 1)
+    QMM_CASE(2, 2, 4, 1, 1) QMM_CASE(4, 2, 4, 1, 1) QMM_CASE(2, 1, 8, 1, 1) QMM_CASE(4, 1, 8, 1, 1)
+    QMM_CASE(2, 2, 8, 1, 1) QMM_CASE(4, 2, 8, 1, 1) QMM_CASE(2, 1, 4, 2, 1) QMM_CASE(4, 1, 4, 2, 1)
+    QMM_CASE(2, 2, 4, 2, 1)
+    // two workgroups per CU (half-LDS ring)
+    QMM_CASE(2, 1, 4, 1, 2) QMM_CASE(4, 1, 4, 1, 2) QMM_CASE(2, 2, 4, 1, 2) QMM_CASE(2, 1, 4, 2, 2)
 #undef QMM_CASE
     return (int)hipErrorInvalidValue;
 }
@@ -571,6 +584,7 @@ static int dispatch_qmm(int wm, int wn, int nw, int ks, const uint16_t* A, int l
 // atomics when splits > 1), 3/4 SwiGLU/GeGLU over 16-row interleaved gate/up -> act16 [M, N/2].
 // (wm, wn, nw, ks): 32*wm-row x 32*wn*nw-column tiles, nw*ks waves (ks waves per column group split the
 // k-steps; nw*ks = 8 -> 2 waves per SIMD, whose dequant / LDS phases overlap each other's MFMAs).
+// ks | 16: the half-LDS ring variant, two workgroups resident per CU.
 extern "C" int mxk_qmm(int qtype, int epi, int wm, int wn, int nw, int ks, const uint16_t* A, int lda, const uint8_t* W,
                        const uint16_t* WD, int M, int N, int K, int splits, void* C, int ldc, hipStream_t st) {
     if (M <= 0) return 0;

@@ -340,7 +340,9 @@ Q32_FORCE: tuple | None = None  # (wm, wn, splits) override for tuning (tools/tu
 QMM_FORCE: tuple | None = None  # (wm, wn, nw, ks, splits) override for tuning (tools/tune_qmm.py)
 # tile configurations compiled into qmm.hip (wm, wn, nw, ks)
 QMM_CONFIGS = ((1, 1, 4, 1), (2, 1, 4, 1), (4, 1, 4, 1), (1, 2, 4, 1), (2, 2, 4, 1), (4, 2, 4, 1), (2, 1, 8, 1),
-               (4, 1, 8, 1), (2, 2, 8, 1), (4, 2, 8, 1), (2, 1, 4, 2), (4, 1, 4, 2), (2, 2, 4, 2))
+               (4, 1, 8, 1), (2, 2, 8, 1), (4, 2, 8, 1), (2, 1, 4, 2), (4, 1, 4, 2), (2, 2, 4, 2),
+               # ks | 16: half-LDS ring, two workgroups per CU
+               (2, 1, 4, 17), (4, 1, 4, 17), (2, 2, 4, 17), (2, 1, 4, 18))
 
 
 def _qmm_shape(M: int, N_: int, K: int, can_split: bool):

@@ -369,11 +369,16 @@ def test_qgemm32(qt, M, wm, wn, splits, monkeypatch):
     (64, 2, 1, 4, 1, 1), (77, 4, 2, 4, 1, 2), (128, 4, 1, 4, 1, 1), (128, 2, 2, 4, 1, 4), (200, 4, 2, 4, 1, 3),
     (300, 4, 1, 4, 1, 2), (7, 1, 1, 4, 1, 2), (33, 1, 2, 4, 1, 1), (100, 2, 1, 8, 1, 2), (300, 4, 2, 8, 1, 1),
     (129, 4, 1, 8, 1, 3), (64, 2, 2, 8, 1, 1), (128, 4, 1, 4, 2, 1), (77, 2, 1, 4, 2, 2), (200, 2, 2, 4, 2, 3),
-    (5, 4, 1, 4, 2, 1)])
+    (5, 4, 1, 4, 2, 1),
+    # ks | 16: half-LDS ring, two workgroups per CU
+    (128, 2, 1, 4, 17, 1), (77, 4, 1, 4, 17, 2), (200, 2, 2, 4, 17, 3), (130, 2, 1, 4, 18, 2), (64, 4, 1, 4, 17, 1)])
 def test_qmm(qt, M, wm, wn, nw, ks, splits, monkeypatch):
     """qmm.hip (LDS-DMA ring GEMM) for every epilogue and tile / split-K choice, incl. ragged M / N
-    tails, split counts that do not divide the k-tiles and the in-workgroup k-step split (ks = 2)."""
+    tails, split counts that do not divide the k-tiles, the in-workgroup k-step split (ks = 2) and the
+    two-workgroups-per-CU ring (ks | 16)."""
     from localai_tfp_amd.ops import linear as L
+    if ks >= 16 and wm == 4 and qt == QType.Q6_K:
+        pytest.skip("a Q6_K 128-row stage does not fit a half-LDS ring of 3 k-tiles")
     monkeypatch.setattr(L, "QMM_FORCE", (wm, wn, nw, ks, splits))
     n, k = 416, 2304  # 416 = 3.25 x 128 columns: partial column tiles (multiple of 32 for the GLU)
     raw, dense = make_w(qt, n, k, seed=M + 7 * wm)
