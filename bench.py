@@ -242,7 +242,8 @@ def main():
                 "host_ms_per_step": {k[:-2]: round(st[k] / max(1, st["steps"]) * 1e3, 3)
                                      for k in ("sched_s", "plan_s", "fwd_s", "wait_s", "process_s")},
                 "graph_replay_host_ms": round(sum(g.replay_s for g in eng.graphs.values()) / max(1, st["graph_steps"]) * 1e3, 3),
-                "weights_gb": round(model.weight_bytes() / 1e9, 2), "kv_blocks": eng.kv.num_blocks,
+                "weights_gb": round(model.weight_bytes() / 1e9, 2),
+                "dense_weight_copy_gb": round(model.dense_cache_bytes() / 1e9, 2) if hasattr(model, "dense_cache_bytes") else 0.0, "kv_blocks": eng.kv.num_blocks,
                 "kv_dtype": args.kv_dtype,
                 "host_gc": {k: round(v, 4) for k, v in __import__("localai_tfp_amd.engine.engine",
                                                                   fromlist=["GC_STATS"]).GC_STATS.items()},

@@ -363,6 +363,16 @@ class LlamaModel:
         if isinstance(self.lm_head, QWeight) and self.lm_head.is_quant and self.lm_head.layout != "t32":
             self.lm_head.build_bf16_cache()  # t32 LM heads run qmm at every M (measured faster)
 
+    def dense_cache_bytes(self) -> int:
+        """Bytes held by the dense 16-bit weight copies (0 unless enable_prefill_bf16_cache ran)."""
+        ws = [self.lm_head] if isinstance(self.lm_head, QWeight) else []
+        for L in self.layers:
+            ws += [w for w in (*L.qkv_parts, L.wo, L.wgu, L.wg, L.wu, L.wd) if w is not None]
+            if L.moe is not None:
+                ws += [w for w in (L.moe.sh_gate_up, L.moe.sh_down) if w is not None]
+        return sum(w.bf16_cache.numel() * w.bf16_cache.element_size() for w in ws
+                   if getattr(w, "bf16_cache", None) is not None)
+
     # ------------------------------------------------------------------ forward
     def embed(self, tokens: torch.Tensor, out: torch.Tensor):
         E = self.tok_embd

@@ -345,6 +345,9 @@ QMM_CONFIGS = ((1, 1, 4, 1), (2, 1, 4, 1), (4, 1, 4, 1), (1, 2, 4, 1), (2, 2, 4,
                (2, 1, 4, 17), (4, 1, 4, 17), (2, 2, 4, 17), (2, 1, 4, 18))
 
 
+QMM_OCC = os.environ.get("MX_QMM_OCC", "1") != "0"  # A/B switch for the two-workgroups-per-CU tiles
+
+
 def _qmm_shape(M: int, N_: int, K: int, can_split: bool):
     """qmm tile choice -> (wm, wn, nw, ks, splits): 32*wm-row x 32*wn*nw-column workgroup tiles with
     nw*ks waves (ks waves per column group split each k-tile's k-steps; 8 waves = two per SIMD, which
@@ -357,8 +360,15 @@ def _qmm_shape(M: int, N_: int, K: int, can_split: bool):
     # profiles/r2_qmm_tune_ks.jsonl (MI355X, Llama-3-8B projections): up to M = 512 the 4-column-group
     # tiles with the k-steps split over two waves per group win; beyond, 8 column groups (BN 256/512)
     # amortise the A-tile reads better. Split-K until ~3/4 of the CUs hold a workgroup.
-    if M <= 512 and (can_split or M <= 128):
-        wm = 2 if M <= 64 or (can_split and N_ <= 4096 and K <= 4096 and M <= 256) else 4
+    if M <= 64 and QMM_OCC:
+        # two workgroups per CU (half-LDS ring, ks | 16): profiles/r2_qmm_tune_occ.jsonl M=64 — gate_up 37.6 vs
+        # 44.2 us, qkv 16.0 vs 16.8, wo 13.5 vs 14.2, down 24.6 vs 25.7
+        wm, wn, nw, ks = 2, 1, 4, 18
+    elif M <= 128 and QMM_OCC and can_split and N_ <= 6144 and K <= 4096:
+        # qkv 22.6 vs 23.8 us, o_proj 17.9 vs 18.3 at M=128 (same sweep)
+        wm, wn, nw, ks = 2, 1, 4, 18
+    elif M <= 512 and (can_split or M <= 128):
+        wm = 2 if (can_split and N_ <= 4096 and K <= 4096 and M <= 256) else 4
         wn, nw, ks = 1, 4, 2
     else:
         wm, wn, nw, ks = 4, (2 if (M > 256 and N_ >= 6144) else 1), 8, 1
