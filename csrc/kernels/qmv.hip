@@ -113,11 +113,21 @@ struct TUnit<MXQ_Q8_0> {
 
 }  // namespace
 
-template <int QT, int MM, int EPI, bool F16>
+// Activation source of the GEMV: SRC_Q8 = q8 rows prepared by a separate kernel (quant_q8 / rmsnorm);
+// SRC_ACT = 16-bit rows quantised in the prologue; SRC_NORM = fp32 residual rows RMS-normalised (weight nw)
+// and quantised in the prologue. The fused sources remove the rmsnorm / quant_q8 launch in front of every
+// decode GEMV (at batch 1 those tiny kernels cost as much as the weight streaming): each workgroup
+// quantises only its own K slice into LDS (the norm's sum of squares still spans the whole row, read
+// from L2 — every workgroup of the launch reads the same row).
+enum { SRC_Q8 = 0, SRC_ACT = 1, SRC_NORM = 2 };
+
+template <int QT, int MM, int EPI, bool F16, int SRC>
 __global__ __launch_bounds__(64 * QMV_WAVES) void qmv_kernel(const int8_t* __restrict__ xq,
                                                              const float2* __restrict__ xds,
                                                              const uint8_t* __restrict__ W, int M, int N, int K,
-                                                             void* __restrict__ Cv, int ldc) {
+                                                             void* __restrict__ Cv, int ldc,
+                                                             const void* __restrict__ xsrc, int ldx,
+                                                             const float* __restrict__ nw, float eps) {
     using U = TUnit<QT>;
     __shared__ float red[QMV_WAVES][MM][32];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -128,6 +138,64 @@ __global__ __launch_bounds__(64 * QMV_WAVES) void qmv_kernel(const int8_t* __res
     const int per = (nunit + gridDim.y - 1) / gridDim.y;
     const int u0 = blockIdx.y * per, u1 = min(nunit, u0 + per);
     const uint8_t* wg = W + (size_t)g * nunit * U::BYTES;
+    int ldq = K, ubase = 0;
+    if constexpr (SRC != SRC_Q8) {
+        extern __shared__ __attribute__((aligned(16))) char qmv_smem[];
+        const int SL = per * U::ELEMS;  // slice capacity per row (dynamic LDS: MM x (SL + SL/32 x 8) bytes)
+        int8_t* sq = (int8_t*)qmv_smem;
+        float2* sd = (float2*)(qmv_smem + MM * SL);
+        const int k0 = u0 * U::ELEMS, klen = max(0, u1 - u0) * U::ELEMS;
+        __shared__ float nred[QMV_WAVES];
+        for (int m = 0; m < M; ++m) {
+            float rs = 1.f;
+            if constexpr (SRC == SRC_NORM) {
+                const float* xr = (const float*)xsrc + (size_t)m * ldx;
+                float ss = 0.f;
+                for (int c = threadIdx.x * 4; c < K; c += 64 * QMV_WAVES * 4) {
+                    const float4 v = *(const float4*)(xr + c);
+                    ss += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+                }
+                rs = rsqrtf(block_sum<64 * QMV_WAVES>(ss, nred) / (float)K + eps);
+            }
+            // 8 consecutive elements per lane, 4 lanes per 32-element q8 block (klen % 256 == 0, so the
+            // 4-lane groups enter and leave the loop together)
+            for (int e = threadIdx.x * 8; e < klen; e += 64 * QMV_WAVES * 8) {
+                float a[8];
+                if constexpr (SRC == SRC_NORM) {
+                    const float* xr = (const float*)xsrc + (size_t)m * ldx + k0 + e;
+                    const float4 v0 = *(const float4*)xr, v1 = *(const float4*)(xr + 4);
+                    const float4 w0 = *(const float4*)(nw + k0 + e), w1 = *(const float4*)(nw + k0 + e + 4);
+                    a[0] = v0.x * rs * w0.x; a[1] = v0.y * rs * w0.y; a[2] = v0.z * rs * w0.z; a[3] = v0.w * rs * w0.w;
+                    a[4] = v1.x * rs * w1.x; a[5] = v1.y * rs * w1.y; a[6] = v1.z * rs * w1.z; a[7] = v1.w * rs * w1.w;
+                } else {
+                    const uint4 raw = *(const uint4*)((const bf16_t*)xsrc + (size_t)m * ldx + k0 + e);
+                    unpack_act2<F16>(raw.x, a[0], a[1]);
+                    unpack_act2<F16>(raw.y, a[2], a[3]);
+                    unpack_act2<F16>(raw.z, a[4], a[5]);
+                    unpack_act2<F16>(raw.w, a[6], a[7]);
+                }
+                float am = 0.f;
+#pragma unroll
+                for (int i = 0; i < 8; ++i) am = fmaxf(am, fabsf(a[i]));
+                am = group_max<4>(am);
+                const float d = am / 127.f, id = d > 0.f ? 1.f / d : 0.f;
+                int q[8], sum = 0;
+#pragma unroll
+                for (int i = 0; i < 8; ++i) { q[i] = __float2int_rn(a[i] * id); sum += q[i]; }
+                const float sf = group_sum<4>((float)sum);
+                uint2 pk;
+                pk.x = (q[0] & 0xFF) | ((q[1] & 0xFF) << 8) | ((q[2] & 0xFF) << 16) | ((uint32_t)(q[3] & 0xFF) << 24);
+                pk.y = (q[4] & 0xFF) | ((q[5] & 0xFF) << 8) | ((q[6] & 0xFF) << 16) | ((uint32_t)(q[7] & 0xFF) << 24);
+                *(uint2*)(sq + m * SL + e) = pk;
+                if ((threadIdx.x & 3) == 0) sd[m * (SL / 32) + e / 32] = make_float2(d, d * sf);
+            }
+        }
+        __syncthreads();
+        xq = sq;
+        xds = sd;
+        ldq = SL;
+        ubase = u0;
+    }
     float acc[MM];
 #pragma unroll
     for (int m = 0; m < MM; ++m) acc[m] = 0.f;
@@ -137,23 +205,25 @@ __global__ __launch_bounds__(64 * QMV_WAVES) void qmv_kernel(const int8_t* __res
         U a, b;
         a.load(wg + (size_t)u * U::BYTES, r, h);
         b.load(wg + (size_t)(u + QMV_WAVES) * U::BYTES, r, h);
+        const int ul = u - ubase;
 #pragma unroll
         for (int m = 0; m < MM; ++m) {
             if (m < M) {
-                const int8_t* x = xq + (size_t)m * K;
-                const float2* ds = xds + (size_t)m * (K / 32);
-                acc[m] += a.dot(x + (size_t)u * U::ELEMS, ds + u * (U::ELEMS / 32), h);
-                acc[m] += b.dot(x + (size_t)(u + QMV_WAVES) * U::ELEMS, ds + (u + QMV_WAVES) * (U::ELEMS / 32), h);
+                const int8_t* x = xq + (size_t)m * ldq;
+                const float2* ds = xds + (size_t)m * (ldq / 32);
+                acc[m] += a.dot(x + (size_t)ul * U::ELEMS, ds + ul * (U::ELEMS / 32), h);
+                acc[m] += b.dot(x + (size_t)(ul + QMV_WAVES) * U::ELEMS, ds + (ul + QMV_WAVES) * (U::ELEMS / 32), h);
             }
         }
     }
     if (u < u1) {
         U a;
         a.load(wg + (size_t)u * U::BYTES, r, h);
+        const int ul = u - ubase;
 #pragma unroll
         for (int m = 0; m < MM; ++m)
             if (m < M)
-                acc[m] += a.dot(xq + (size_t)m * K + (size_t)u * U::ELEMS, xds + (size_t)m * (K / 32) + u * (U::ELEMS / 32), h);
+                acc[m] += a.dot(xq + (size_t)m * ldq + (size_t)ul * U::ELEMS, xds + (size_t)m * (ldq / 32) + ul * (U::ELEMS / 32), h);
     }
 #pragma unroll
     for (int m = 0; m < MM; ++m) {
@@ -242,8 +312,24 @@ __global__ __launch_bounds__(256) void dequant_t32_kernel(const uint8_t* __restr
 
 template <int QT, int MM, int EPI>
 static int launch_qmv(const int8_t* xq, const float2* xds, const uint8_t* W, int M, int N, int K, int ks, void* C,
-                      int ldc, hipStream_t st) {
-    MX_ACT_DISPATCH(qmv_kernel<QT, MM, EPI, F16><<<dim3(N / 32, ks), 64 * QMV_WAVES, 0, st>>>(xq, xds, W, M, N, K, C, ldc));
+                      int ldc, hipStream_t st, int src = SRC_Q8, const void* xsrc = nullptr, int ldx = 0,
+                      const float* nw = nullptr, float eps = 0.f) {
+    if (src == SRC_Q8) {
+        MX_ACT_DISPATCH(qmv_kernel<QT, MM, EPI, F16, SRC_Q8><<<dim3(N / 32, ks), 64 * QMV_WAVES, 0, st>>>(
+            xq, xds, W, M, N, K, C, ldc, nullptr, 0, nullptr, 0.f));
+    } else {
+        const int per = (K / TUnit<QT>::ELEMS + ks - 1) / ks;
+        const size_t sl = (size_t)per * TUnit<QT>::ELEMS;
+        const size_t lds = MM * (sl + sl / 32 * sizeof(float2));
+        if (lds > 64 * 1024) return (int)hipErrorInvalidValue;
+        if (src == SRC_ACT) {
+            MX_ACT_DISPATCH(qmv_kernel<QT, MM, EPI, F16, SRC_ACT><<<dim3(N / 32, ks), 64 * QMV_WAVES, lds, st>>>(
+                nullptr, nullptr, W, M, N, K, C, ldc, xsrc, ldx, nullptr, 0.f));
+        } else {
+            MX_ACT_DISPATCH(qmv_kernel<QT, MM, EPI, F16, SRC_NORM><<<dim3(N / 32, ks), 64 * QMV_WAVES, lds, st>>>(
+                nullptr, nullptr, W, M, N, K, C, ldc, xsrc, ldx, nw, eps));
+        }
+    }
     MXK_CHECK_LAUNCH();
 }
 
@@ -273,6 +359,36 @@ extern "C" int mxk_qmv(int qtype, int epi, const int8_t* xq, const float2* xds, 
     }
 #undef QMV_EPI
 #undef QMV_M
+    return (int)hipErrorInvalidValue;
+}
+
+// The same GEMV with the activation quantisation (and optionally the RMSNorm in front of it) fused into
+// the prologue: src 1 = x 16-bit [M, K] (row stride ldx); src 2 = x fp32 residual [M, K], y = x / rms(x) * nw.
+extern "C" int mxk_qmv_x(int qtype, int epi, int src, const void* x, int ldx, const float* nw, float eps,
+                         const uint8_t* W, int M, int N, int K, int ks, void* C, int ldc, hipStream_t st) {
+    if (M <= 0) return 0;
+    if (M > 4 || K % 256 || N % 32 || ks < 1 || (ks > 1 && epi != E16_ADD_F32) || (src != SRC_ACT && src != SRC_NORM) ||
+        (src == SRC_NORM && !nw) || ((uintptr_t)x & 15) || (ldx % 8))
+        return (int)hipErrorInvalidValue;
+#define QMVX_M(QT_, EPI_)                                                                                   \
+    if (M == 1) return launch_qmv<QT_, 1, EPI_>(nullptr, nullptr, W, M, N, K, ks, C, ldc, st, src, x, ldx, nw, eps); \
+    if (M == 2) return launch_qmv<QT_, 2, EPI_>(nullptr, nullptr, W, M, N, K, ks, C, ldc, st, src, x, ldx, nw, eps); \
+    return launch_qmv<QT_, 4, EPI_>(nullptr, nullptr, W, M, N, K, ks, C, ldc, st, src, x, ldx, nw, eps);
+#define QMVX_EPI(QT_)                                   \
+    switch (epi) {                                      \
+        case E16_F32: { QMVX_M(QT_, E16_F32) }          \
+        case E16_ACT: { QMVX_M(QT_, E16_ACT) }          \
+        case E16_ADD_F32: { QMVX_M(QT_, E16_ADD_F32) }  \
+        case E16_SWIGLU: { QMVX_M(QT_, E16_SWIGLU) }    \
+        case E16_GEGLU: { QMVX_M(QT_, E16_GEGLU) }      \
+    }
+    switch (qtype) {
+        case MXQ_Q4_K: QMVX_EPI(MXQ_Q4_K) break;
+        case MXQ_Q6_K: QMVX_EPI(MXQ_Q6_K) break;
+        case MXQ_Q8_0: QMVX_EPI(MXQ_Q8_0) break;
+    }
+#undef QMVX_EPI
+#undef QMVX_M
     return (int)hipErrorInvalidValue;
 }
 

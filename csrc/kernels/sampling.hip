@@ -232,10 +232,27 @@ __global__ __launch_bounds__(1024) void argmax_kernel(const float* __restrict__ 
     const float* r = x + (size_t)blockIdx.x * ld;
     float best = -INFINITY;
     int bi = 0x7fffffff;
-    for (int i = threadIdx.x; i < V; i += 1024) {
-        const float v = r[i];
-        if (v > best) { best = v; bi = i; }
+    auto take = [&](float v, int i) {
+        if (v > best) { best = v; bi = i; }  // ascending i per lane: the first maximum wins ties
+    };
+    int tail = 0;
+    if ((((uintptr_t)r) & 15) == 0) {
+        // 16-B loads, two in flight per lane (one block streams the row: at batch 1 a scalar loop was
+        // load-latency bound, ~39 us for a 128k vocabulary)
+        const int V4 = V & ~3;
+        int i = threadIdx.x * 4;
+        for (; i + 4096 < V4; i += 8192) {
+            const float4 a = *(const float4*)(r + i), c = *(const float4*)(r + i + 4096);
+            take(a.x, i); take(a.y, i + 1); take(a.z, i + 2); take(a.w, i + 3);
+            take(c.x, i + 4096); take(c.y, i + 4097); take(c.z, i + 4098); take(c.w, i + 4099);
+        }
+        if (i < V4) {
+            const float4 a = *(const float4*)(r + i);
+            take(a.x, i); take(a.y, i + 1); take(a.z, i + 2); take(a.w, i + 3);
+        }
+        tail = V4;
     }
+    for (int i = tail + threadIdx.x; i < V; i += 1024) take(r[i], i);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
         const float ob = __shfl_xor(best, o, 64);

@@ -37,6 +37,7 @@ KERNEL_SIGS = {
     "mxk_qgemm32": [I, I, I, I, P, I, P, P, I, I, I, I, P, I, P],
     "mxk_qmm": [I, I, I, I, I, I, P, I, P, P, I, I, I, I, P, I, P],
     "mxk_qmv": [I, I, P, P, P, I, I, I, I, P, I, P],
+    "mxk_qmv_x": [I, I, I, P, I, P, F, P, I, I, I, I, P, I, P],
     "mxk_dequant_t32": [I, P, P, I, I, P, P, I, P],
     "mxk_set_act_f16": [I],
     "mxk_attn_dense": [P, I, P, I, P, I, P, I, I, I, I, I, I, I, P, P, I, F, I, P],

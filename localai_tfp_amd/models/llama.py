@@ -34,11 +34,15 @@ import torch
 from ..formats.gguf import QType
 from ..ops import core as K
 from ..ops.linear import (ACT_DTYPE, EPI_ADD_F32, EPI_BF16, EPI_F32, EPI_GEGLU, EPI_SWIGLU, QWeight, concat_rows,
-                          interleave_gate_up, qmatmul)
+                          interleave_gate_up, qmatmul, qmv_fusable, qmv_fused)
 from ..ops.moe import MoEWeights, moe_ffn
 from .config import LlamaConfig
 
 GEMV_MAX_M = 4
+# decode batches up to this size run the RMSNorm / q8 quantisation inside the GEMV prologue (qmv.hip
+# SRC_NORM / SRC_ACT). Every workgroup of the GEMV redoes the row statistics, so the fusion pays only at
+# batch 1 (profiles/r2_qmv_fuse_fuse{0,1}_c{1,4}.json: c1 387 -> 442 tok/s, c4 961 -> 861)
+QMV_FUSE_MAX_M = int(__import__("os").environ.get("MX_QMV_FUSE_MAX_M", "1"))
 
 
 def vocab_shard(V: int, tp: int) -> int:
@@ -438,19 +442,26 @@ class LlamaModel:
         for li, L in enumerate(self.layers):
             kc, vc = kv.layer(li)
             # ---- attention block ----
-            if gemv:
+            qkv = ws.qkv[:T]
+            # batch <= 4: RMSNorm + q8 quantisation fused into each projection's GEMV prologue
+            fuse_in = gemv and T <= QMV_FUSE_MAX_M
+            fuse_qkv = fuse_in and all(qmv_fusable(w, T, EPI_F32, True) for w in L.qkv_parts)
+            if fuse_qkv:
+                xq = xds = None
+            elif gemv:
                 xq, xds = ws.q8(T, H)
                 K.rmsnorm(h, L.attn_norm, eps, out_q8=(xq, xds))
             else:
                 K.rmsnorm(h, L.attn_norm, eps, out_bf16=xb)
                 xq = xds = None
-            qkv = ws.qkv[:T]
             if not gemv and not qkv.is_cuda:
                 qkv.zero_()
             off = 0
             for w in L.qkv_parts:
                 sl = qkv[:, off:off + w.N] if len(L.qkv_parts) > 1 else qkv
-                if gemv:
+                if fuse_qkv:
+                    qmv_fused(w, h, EPI_F32, sl, norm=L.attn_norm, eps=eps, out_zeroed=True)
+                elif gemv:
                     qmatmul(w, None, EPI_F32, sl, xq=xq, xds=xds, out_zeroed=qkv.is_cuda)
                 else:
                     qmatmul(w, xb, EPI_F32, sl, out_zeroed=True)
@@ -470,12 +481,15 @@ class LlamaModel:
                 K.attn_prefill(q[nd:].view(T - nd, Hq, D), kc, vc, fb.pf_block_tables, fb.pf_cu_q, fb.pf_ctx_lens,
                                self.scale, attn[nd:].view(T - nd, Hq, D), fb.pf_q_lens_host, fb.pf_ctx_lens_host,
                                window=L.window, softcap=cfg.attn_softcap, tiles=fb.pf_tiles)
-            if gemv:
-                aq, ads = ws.q8(T, qd)
-                K.quant_q8(attn, aq, ads)
+            if fuse_in and L.post_attn_norm is None and self.tp_size == 1 and qmv_fusable(L.wo, T, EPI_ADD_F32):
+                qmv_fused(L.wo, attn, EPI_ADD_F32, h)  # h += attn W_o^T, q8 quantisation in the prologue
             else:
-                aq = ads = None
-            self._residual_proj(L.wo, attn, aq, ads, h, L.post_attn_norm, ws, T, eps)
+                if gemv:
+                    aq, ads = ws.q8(T, qd)
+                    K.quant_q8(attn, aq, ads)
+                else:
+                    aq = ads = None
+                self._residual_proj(L.wo, attn, aq, ads, h, L.post_attn_norm, ws, T, eps)
             # ---- FFN block ----
             if L.moe is not None:
                 K.rmsnorm(h, L.ffn_norm, eps, out_bf16=xb)
@@ -488,14 +502,19 @@ class LlamaModel:
                 else:
                     moe_ffn(L.moe, xb, h)
                 continue
-            if gemv:
+            act = ws.act[:T]
+            fuse_gu = fuse_in and L.wgu is not None and qmv_fusable(L.wgu, T, self.glu_epi)
+            if fuse_gu:
+                pass
+            elif gemv:
                 xq, xds = ws.q8(T, H)
                 K.rmsnorm(h, L.ffn_norm, eps, out_q8=(xq, xds))
             else:
                 K.rmsnorm(h, L.ffn_norm, eps, out_bf16=xb)
-            act = ws.act[:T]
             if L.wgu is not None:
-                if gemv:
+                if fuse_gu:
+                    qmv_fused(L.wgu, h, self.glu_epi, act, norm=L.ffn_norm, eps=eps)
+                elif gemv:
                     qmatmul(L.wgu, None, self.glu_epi, act, xq=xq, xds=xds)
                 else:
                     qmatmul(L.wgu, xb, self.glu_epi, act)
@@ -506,6 +525,9 @@ class LlamaModel:
                 qmatmul(L.wg, xin, EPI_BF16, g_out, xq=xq, xds=xds)
                 qmatmul(L.wu, xin, EPI_BF16, u_out, xq=xq, xds=xds)
                 K.glu(g_out, u_out, act, cfg.ffn_act)
+            if fuse_in and L.post_ffn_norm is None and self.tp_size == 1 and qmv_fusable(L.wd, T, EPI_ADD_F32):
+                qmv_fused(L.wd, act, EPI_ADD_F32, h)
+                continue
             if gemv:
                 aq, ads = ws.q8(T, F)
                 K.quant_q8(act, aq, ads)

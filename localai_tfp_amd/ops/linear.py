@@ -309,6 +309,49 @@ def _qmatmul_t32(W: QWeight, x, epi: int, out, xq, xds, M: int, out_zeroed: bool
     return out
 
 
+QMV_FUSE = os.environ.get("MX_QMV_FUSE", "1") != "0"
+
+
+def qmv_fusable(W, M: int, epi: int, out_zeroed: bool = False) -> int:
+    """K-split count of the fused-input decode GEMV for this weight / batch, or 0 if it does not apply
+    (not t32, M > 4, or the per-workgroup LDS slice of the q8 activations would exceed 64 KB)."""
+    if not QMV_FUSE or not isinstance(W, QWeight) or W.layout != "t32" or not 0 < M <= 4 or W.data.device.type != "cuda":
+        return 0
+    ks = 1
+    elem = 64 if int(W.qtype) == int(QType.Q8_0) else 256
+    if epi == EPI_ADD_F32 or (epi == EPI_F32 and out_zeroed):
+        units = W.K // elem
+        while (W.N // 32) * ks < 2 * CU_COUNT and units // (ks * 2) >= 2:
+            ks *= 2
+    mm = 1 if M == 1 else 2 if M == 2 else 4
+    sl = -(-(W.K // elem) // ks) * elem
+    return 0 if mm * (sl + sl // 4) > 64 * 1024 else ks
+
+
+def qmv_fused(W: QWeight, x: torch.Tensor, epi: int, out: torch.Tensor, *, norm: torch.Tensor | None = None,
+              eps: float = 0.0, out_zeroed: bool = False) -> bool:
+    """Decode GEMV (M <= 4, t32 weights) with the q8 quantisation of `x` — and with `norm`, the RMSNorm
+    x / rms(x) * norm of the fp32 residual rows `x` — fused into the GEMV prologue (qmv.hip mxk_qmv_x).
+    Returns False (nothing launched) where the fused kernel does not apply; the caller then runs
+    rmsnorm / quant_q8 + qmatmul."""
+    M = x.shape[0]
+    ks = qmv_fusable(W, M, epi, out_zeroed)
+    if (not ks or not x.is_cuda or x.stride(-1) != 1
+            or (norm is None and x.dtype not in (torch.float16, torch.bfloat16))
+            or (norm is not None and x.dtype != torch.float32)):
+        return False
+    if epi in (EPI_BF16, *GLU_EPIS):
+        if norm is None and out.dtype != x.dtype:
+            return False
+        N.ensure_act(out.dtype)
+    elif norm is None:
+        N.ensure_act(x.dtype)
+    N.kcall("mxk_qmv_x", int(W.qtype), EPI_ADD_F32 if ks > 1 else epi, 2 if norm is not None else 1, x.data_ptr(),
+            x.stride(0), N.ptr(norm), float(eps), W.data.data_ptr(), M, W.N, W.K, ks, out.data_ptr(), out.stride(0),
+            N.stream_ptr())
+    return True
+
+
 def dense_min_m(dtype, epi: int = EPI_ADD_F32, can_split: bool = True) -> int:
     """Smallest M routed to the dense weight cache (hipBLASLt). From tools/bench_qgemm.py +
     tools/tune_qgemm16.py on MI355X (Llama-3-8B shapes): the bf16 dequant-MFMA kernel loses to the

@@ -572,3 +572,66 @@ def test_attn_dense_kv_capacity(causal):
     kw = dict(klen=None if causal else klen.to(DEV), kv_rows=cap)
     K.attn_dense(q.to(DEV), k.to(DEV), v.to(DEV), out, B, Sq, Sk, H, H, D, 0.125, causal, **kw)
     assert rel(out, ref) < 1.5e-2
+
+
+@pytest.mark.parametrize("qt", [QType.Q4_K, QType.Q6_K, QType.Q8_0])
+@pytest.mark.parametrize("M", [1, 2, 3, 4])
+def test_qmv_fused_input(qt, M):
+    """qmv with the q8 quantisation (src 16-bit) or RMSNorm + quantisation (src fp32 residual) fused into
+    the prologue == rmsnorm / quant_q8 kernels followed by the plain qmv, for every epilogue incl. the
+    K-split accumulate (ks > 1) and the interleaved SwiGLU; and both against the fp32 reference."""
+    from localai_tfp_amd.ops.linear import qmv_fusable, qmv_fused
+    n, k = 512, 2048
+    raw, dense = make_w(qt, n, k, seed=3 * M + int(qt))
+    W = QWeight.from_ggml(raw, qt, n, k, DEV)
+    assert W.to_t32()
+    g = torch.Generator().manual_seed(M)
+    h = torch.randn(M, k, generator=g).to(DEV) * 3
+    nw = (torch.rand(k, generator=g) + 0.5).to(DEV)
+    eps = 1e-5
+    x16 = (torch.randn(M, k, generator=g) * 2).half().to(DEV)
+    N.ensure_act(torch.float16)
+    xq = torch.empty(M, k, dtype=torch.int8, device=DEV)
+    xds = torch.empty(M, k // 32, 2, device=DEV)
+    y_ref_norm = (h / torch.sqrt(h.pow(2).mean(-1, keepdim=True) + eps) * nw).cpu() @ dense.t()
+    y_ref_act = x16.float().cpu() @ dense.t()
+    for src in ("norm", "act"):
+        if src == "norm":
+            K.rmsnorm(h, nw, eps, out_q8=(xq, xds))
+        else:
+            K.quant_q8(x16, xq, xds)
+        xin, kw = (h, dict(norm=nw, eps=eps)) if src == "norm" else (x16, {})
+        ref = y_ref_norm if src == "norm" else y_ref_act
+        # fp32 store (zeroed -> split-K over workgroups)
+        assert qmv_fusable(W, M, EPI_F32, True)
+        a = torch.zeros(M, n, device=DEV)
+        b = torch.zeros(M, n, device=DEV)
+        qmatmul(W, None, EPI_F32, a, xq=xq, xds=xds, out_zeroed=True)
+        assert qmv_fused(W, xin, EPI_F32, b, out_zeroed=True, **kw)
+        assert rel(b, a) < 1e-5 and rel(b, ref) < 2e-2, (src, rel(b, a), rel(b, ref))
+        # accumulate
+        acc0 = torch.randn(M, n, device=DEV)
+        a, b = acc0.clone(), acc0.clone()
+        qmatmul(W, None, EPI_ADD_F32, a, xq=xq, xds=xds)
+        assert qmv_fused(W, xin, EPI_ADD_F32, b, **kw)
+        assert rel(b - acc0, a - acc0) < 1e-5
+        # SwiGLU over interleaved gate|up rows
+        sa = torch.empty(M, n // 2, dtype=torch.float16, device=DEV)
+        sb = torch.empty_like(sa)
+        qmatmul(W, None, EPI_SWIGLU, sa, xq=xq, xds=xds)
+        assert qmv_fused(W, xin, EPI_SWIGLU, sb, **kw)
+        assert rel(sb, sa) < 2e-3
+
+
+@pytest.mark.parametrize("V", [1001, 4096, 128256, 128259])
+def test_argmax_rows(V):
+    """argmax_kernel: 16-B loads on aligned rows, scalar tail / unaligned rows, first index on ties."""
+    g = torch.Generator().manual_seed(V)
+    x = torch.randn(5, V, generator=g)
+    x[1] = 0.5  # all ties -> index 0
+    x[2, V - 1] = 100.0  # maximum in the tail
+    x[3, 7] = x[3, V // 2] = 50.0  # tie -> the lower index
+    xd = x.to(DEV)
+    out = torch.empty(5, dtype=torch.int32, device=DEV)
+    N.kcall("mxk_argmax", xd.data_ptr(), xd.stride(0), 5, V, out.data_ptr(), N.stream_ptr())
+    assert out.cpu().tolist() == [int(x[0].argmax()), 0, V - 1, 7, int(x[4].argmax())]
