@@ -34,7 +34,7 @@ import torch
 from ..formats.gguf import QType
 from ..ops import core as K
 from ..ops.linear import (ACT_DTYPE, EPI_ADD_F32, EPI_BF16, EPI_F32, EPI_GEGLU, EPI_SWIGLU, QWeight, concat_rows,
-                          interleave_gate_up, qmatmul, qmv_fusable, qmv_fused)
+                          _fp32_out_ok, dense_min_m, interleave_gate_up, qmatmul, qmv_fusable, qmv_fused)
 from ..ops.moe import MoEWeights, moe_ffn
 from .config import LlamaConfig
 
@@ -68,6 +68,7 @@ class LlamaLayer:
     post_ffn_norm: torch.Tensor | None = None
     window: int = 0  # sliding-window attention (0 = full)
     rope: tuple | None = None  # (inv_freq, attn_factor) of windowed layers with their own RoPE base
+    qkv_dense: torch.Tensor | None = None  # dense 16-bit Q|K|V (large-M path) when the parts' quant types differ
 
 
 @dataclass
@@ -359,7 +360,13 @@ class LlamaModel:
     def enable_prefill_bf16_cache(self):
         """Dense 16-bit copies of the projections (+ LM head) for the hipBLASLt large-M path."""
         for L in self.layers:
-            for w in (*L.qkv_parts, L.wo, L.wgu, L.wg, L.wu, L.wd):
+            parts = L.qkv_parts
+            if len(parts) > 1 and all(w.is_quant for w in parts) and parts[0].data.is_cuda:
+                # one dense Q|K|V matrix: a single GEMM straight into the contiguous fp32 qkv rows instead
+                # of one GEMM per quant-type group plus a widening copy into the strided slices
+                L.qkv_dense = torch.cat([w.dequant_gpu(ACT_DTYPE) for w in parts])
+                parts = ()
+            for w in (*parts, L.wo, L.wgu, L.wg, L.wu, L.wd):
                 if w is not None:
                     w.build_bf16_cache()
             if L.moe is not None:
@@ -374,8 +381,9 @@ class LlamaModel:
             ws += [w for w in (*L.qkv_parts, L.wo, L.wgu, L.wg, L.wu, L.wd) if w is not None]
             if L.moe is not None:
                 ws += [w for w in (L.moe.sh_gate_up, L.moe.sh_down) if w is not None]
-        return sum(w.bf16_cache.numel() * w.bf16_cache.element_size() for w in ws
-                   if getattr(w, "bf16_cache", None) is not None)
+        n = sum(L.qkv_dense.numel() * L.qkv_dense.element_size() for L in self.layers if L.qkv_dense is not None)
+        return n + sum(w.bf16_cache.numel() * w.bf16_cache.element_size() for w in ws
+                       if getattr(w, "bf16_cache", None) is not None)
 
     # ------------------------------------------------------------------ forward
     def embed(self, tokens: torch.Tensor, out: torch.Tensor):
@@ -457,7 +465,11 @@ class LlamaModel:
             if not gemv and not qkv.is_cuda:
                 qkv.zero_()
             off = 0
-            for w in L.qkv_parts:
+            if (not gemv and L.qkv_dense is not None and qkv.is_cuda and xb.dtype == L.qkv_dense.dtype
+                    and T >= dense_min_m(xb.dtype, EPI_F32, True) and _fp32_out_ok(xb.dtype)):
+                torch.mm(xb, L.qkv_dense.t(), out_dtype=torch.float32, out=qkv)
+                off = qkv.shape[1]
+            for w in (L.qkv_parts if off == 0 else ()):
                 sl = qkv[:, off:off + w.N] if len(L.qkv_parts) > 1 else qkv
                 if fuse_qkv:
                     qmv_fused(w, h, EPI_F32, sl, norm=L.attn_norm, eps=eps, out_zeroed=True)
