@@ -39,6 +39,11 @@ from ..ops.moe import MoEWeights, moe_ffn
 from .config import LlamaConfig
 
 GEMV_MAX_M = 4
+# decode-attention partition length at >= 64 sequences (B x Hkv workgroups already fill the chip; longer
+# partitions mean fewer split-K partials to merge; c128 14278 vs 14151 tok/s at 256, within run-to-run noise:
+# profiles/r2_decode_part_c128_p{256,512}.json)
+DECODE_PART_LARGE_B = int(__import__("os").environ.get("MX_DECODE_PART_LARGE_B", "512"))
+DECODE_PART_SMALL_B = int(__import__("os").environ.get("MX_DECODE_PART_SMALL_B", "64"))  # < 8 sequences
 # decode batches up to this size run the RMSNorm / q8 quantisation inside the GEMV prologue (qmv.hip
 # SRC_NORM / SRC_ACT). Every workgroup of the GEMV redoes the row statistics, so the fusion pays only at
 # batch 1 (profiles/r2_qmv_fuse_fuse{0,1}_c{1,4}.json: c1 387 -> 442 tok/s, c4 961 -> 861)
@@ -142,7 +147,9 @@ class Workspace:
         finer so the grid still covers the CUs (B x Hkv x parts workgroups), within the partial-
         result workspace (rows = B * Hq * parts)."""
         cap = self.part_ml.shape[0]
-        for part in ((64, 128, 256) if B < 8 else (128, 256) if B < 32 else (256,)):
+        big = (DECODE_PART_LARGE_B, 256) if B >= 64 else (256,)
+        small = (DECODE_PART_SMALL_B, 128, 256) if DECODE_PART_SMALL_B != 64 else (64, 128, 256)
+        for part in (small if B < 8 else (128, 256) if B < 32 else big):
             if B * Hq * max(1, -(-max_len // part)) <= cap:
                 return part
         return 256
