@@ -44,6 +44,7 @@ GEMV_MAX_M = 4
 # profiles/r2_decode_part_c128_p{256,512}.json)
 DECODE_PART_LARGE_B = int(__import__("os").environ.get("MX_DECODE_PART_LARGE_B", "512"))
 DECODE_PART_SMALL_B = int(__import__("os").environ.get("MX_DECODE_PART_SMALL_B", "64"))  # < 8 sequences
+# (batch 1: 64 -> 450, 256 -> 448, 512 -> 431 tok/s, profiles/r2_decode_part_c1_p*.json)
 # decode batches up to this size run the RMSNorm / q8 quantisation inside the GEMV prologue (qmv.hip
 # SRC_NORM / SRC_ACT). Every workgroup of the GEMV redoes the row statistics, so the fusion pays only at
 # batch 1 (profiles/r2_qmv_fuse_fuse{0,1}_c{1,4}.json: c1 387 -> 442 tok/s, c4 961 -> 861)
