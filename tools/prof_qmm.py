@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--M", type=int, default=2048)
     ap.add_argument("--cfg", default="")
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--gemv", action="store_true", help="M <= 4 decode GEMV with the fused RMSNorm / q8 prologue")
     a = ap.parse_args()
     from localai_tfp_amd.ops import linear as L
     from localai_tfp_amd.ops.quant import random_quantized
@@ -32,17 +33,27 @@ def main():
     x = (torch.randn(a.M, K, device="cuda") * 0.5).half()
     out = (torch.empty(a.M, N // 2, device="cuda", dtype=torch.float16) if epi == 3
            else torch.zeros(a.M, N, device="cuda"))
+    if a.gemv:  # h fp32 residual rows -> rmsnorm -> q8 -> qmv, one launch
+        h = torch.randn(a.M, K, device="cuda")
+        nw = torch.ones(K, device="cuda")
+        call = (lambda: L.qmv_fused(W, h, epi, out, norm=nw, eps=1e-5, out_zeroed=True)) if K == 4096 else \
+            (lambda: L.qmv_fused(W, x, epi, out, out_zeroed=True))
+        assert call()
+    else:
+        def call():
+            L.qmatmul(W, x, epi, out, out_zeroed=True)
     for _ in range(a.iters):
-        L.qmatmul(W, x, epi, out, out_zeroed=True)
+        call()
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(a.iters):
-        L.qmatmul(W, x, epi, out, out_zeroed=True)
+        call()
     e1.record()
     torch.cuda.synchronize()
     us = e0.elapsed_time(e1) / a.iters * 1e3
-    print(f"{a.shape} M={a.M} cfg={L._qmm_shape(a.M, N, K, epi in (0, 2))} {us:.1f} us {2*a.M*N*K/us/1e6:.0f} TF")
+    cfg = "qmv_fused" if a.gemv else L._qmm_shape(a.M, N, K, epi in (0, 2))
+    print(f"{a.shape} M={a.M} cfg={cfg} {us:.1f} us {2*a.M*N*K/us/1e6:.0f} TF {W.data.numel() / us / 1e6:.2f} TB/s weights")
 
 
 if __name__ == "__main__":
