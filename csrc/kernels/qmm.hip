@@ -76,9 +76,9 @@ struct QmmGeom {
 
 // ring depth: as many k-tiles in flight as the LDS holds (memory-level parallelism), capped. OCC = 2 halves
 // the budget so two workgroups share a CU (twice the waves to hide dequant / LDS latency, at a shallower ring)
-template <int QT, int WM, int WN, int NW, int OCC = 1>
+template <int QT, int WM, int WN, int NW, int OCC = 1, int WMW = 1>
 struct QmmRing {
-    static constexpr int STAGE = 32 * WM * 128 + NW * QmmGeom<QT, WN>::WBYTES;
+    static constexpr int STAGE = 32 * WM * WMW * 128 + NW * QmmGeom<QT, WN>::WBYTES;
     static constexpr int S0 = QMM_LDS_BUDGET / OCC / STAGE;
     static constexpr int STAGES = S0 > QMM_MAX_STAGES ? QMM_MAX_STAGES : S0;
 };
@@ -230,22 +230,26 @@ struct QmmB<MXQ_Q8_0> {
 // a workgroup of 4 waves leaves one wave per SIMD, whose dequant VALU, LDS-read latency and MFMAs then
 // serialise (measured: loads alone took half the kernel time); KS = 2 puts two waves on every SIMD
 // without dequantising any weight twice.
-template <int QT, int WM, int WN, int NW, int KS, int OCC, int EPI>
+// WMW waves split the BM rows of each column group (wave tile 32*WM x 32*WN): with WMW = 1 every wave
+// re-reads the whole A tile from LDS for its 32*WN columns, and at WN = 1 those A-fragment reads alone
+// saturate the CU's LDS port (64 KB of reads per 64-k tile against 512 MFMA cycles); squarer wave tiles
+// (64x64, 128x64) halve that traffic at the price of dequantising each weight fragment WMW times.
+template <int QT, int WM, int WN, int NW, int KS, int OCC, int EPI, int WMW>
 // The ring takes the whole LDS (1/OCC of it), so a CU holds OCC workgroups: tell the scheduler that
 // OCC*NW*KS/4 waves per SIMD is the occupancy (it otherwise sinks the LDS reads next to their MFMAs to save
 // registers nobody can use).
-__global__ __launch_bounds__(64 * NW * KS) __attribute__((amdgpu_waves_per_eu(OCC * NW * KS / 4, OCC * NW * KS / 4))) void
+__global__ __launch_bounds__(64 * NW * KS * WMW) __attribute__((amdgpu_waves_per_eu(OCC * NW * KS * WMW / 4, OCC * NW * KS * WMW / 4))) void
 qmm_kernel(const uint16_t* __restrict__ A, int lda, const uint8_t* __restrict__ W, const uint16_t* __restrict__ WD,
            int M, int N, int K, int n_ct, int n_mt, int splits, int kt_per_split, void* __restrict__ Cv, int ldc) {
     using G = QmmGeom<QT, WN>;
     using F = QmmFmt<QT>;
-    constexpr int BM = 32 * WM, COLS = G::COLS;
+    constexpr int BM = 32 * WM * WMW, COLS = G::COLS;
     constexpr int A_BYTES = BM * 128;
     constexpr int STAGE = A_BYTES + NW * G::WBYTES;
-    constexpr int NS = QmmRing<QT, WM, WN, NW, OCC>::STAGES;
-    static_assert(STAGE == QmmRing<QT, WM, WN, NW, OCC>::STAGE && NS >= 3, "ring");
-    static_assert(KS == 1 || NW * WM * WN * 16 * 64 * 4 <= NS * STAGE, "k-split partials fit in the ring");
-    constexpr int NT = NW * KS;       // waves
+    constexpr int NS = QmmRing<QT, WM, WN, NW, OCC, WMW>::STAGES;
+    static_assert(STAGE == QmmRing<QT, WM, WN, NW, OCC, WMW>::STAGE && NS >= 3, "ring");
+    static_assert(KS == 1 || NW * WMW * WM * WN * 16 * 64 * 4 <= NS * STAGE, "k-split partials fit in the ring");
+    constexpr int NT = NW * KS * WMW;  // waves
     constexpr int WA = BM / 8 / NT;   // A-tile LDS-DMA instructions per wave (8 rows x 128 B each)
     static_assert(WA >= 1 && WA * 8 * NT == BM, "A tile split");
     static_assert(KS == 1 || KS == 2, "k-step split");
@@ -255,7 +259,7 @@ qmm_kernel(const uint16_t* __restrict__ A, int lda, const uint8_t* __restrict__ 
 
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int h = lane >> 5, col = lane & 31;
-    const int cg = wave % NW, kh = wave / NW;  // column group, k-step phase
+    const int cg = wave % NW, mw = (wave / NW) % WMW, kh = wave / (NW * WMW);  // column group, row slice, k-step phase
 
     // XCD-aware bijective remap of the 1-D grid: consecutive logical ids share an XCD
     const int nwg = gridDim.x, bid = blockIdx.x;
@@ -301,7 +305,7 @@ qmm_kernel(const uint16_t* __restrict__ A, int lda, const uint8_t* __restrict__ 
     const uint8_t* dsrc = W + (size_t)mg * gstride + F::DOFF + (lane & 31) * 4;
     const bool mact = lane < 32 * WN;
 
-    // every wave streams its share of the A rows; the kh == 0 wave of a column group its weight bytes
+    // every wave streams its share of the A rows; the (kh, mw) == 0 wave of a column group its weight bytes
     auto issue = [&](int kt, int slot, auto wl_c) {
         char* sb = smem + slot * STAGE;
         const uint16_t* ak = A + (size_t)kt * QMM_KT;
@@ -345,7 +349,7 @@ qmm_kernel(const uint16_t* __restrict__ A, int lda, const uint8_t* __restrict__ 
     QmmB<QT> bw[WN], bn[WN];
     auto load_a = [&](const char* sb, int s, f16x8 (&dst)[WM]) {
 #pragma unroll
-        for (int i = 0; i < WM; ++i) dst[i] = *(const f16x8*)(sb + qmm_a_off(i * 32 + col, 2 * s + h));
+        for (int i = 0; i < WM; ++i) dst[i] = *(const f16x8*)(sb + qmm_a_off((mw * WM + i) * 32 + col, 2 * s + h));
     };
     auto load_b = [&](const char* sb, QmmB<QT> (&dst)[WN], int jq) {
         const char* wl = sb + A_BYTES + cg * G::WBYTES;
@@ -354,9 +358,9 @@ qmm_kernel(const uint16_t* __restrict__ A, int lda, const uint8_t* __restrict__ 
             dst[t].load(wl + G::Q_OFF + t * F::QB, wl + G::M_OFF + t * 512, wl + G::D_OFF + t * 128, col, h, jq);
     };
 
-    auto mainloop = [&](auto kh_c) {
+    auto mainloop = [&](auto kh_c, auto wl_c) {
         constexpr int KH = decltype(kh_c)::value;
-        constexpr bool WLOAD = KH == 0;
+        constexpr bool WLOAD = decltype(wl_c)::value;
         constexpr int NI = WA + (WLOAD ? G::NI : 0);  // LDS-DMA wave-instructions per stage of this wave
         using WLc = std::integral_constant<bool, WLOAD>;
         // prologue: NSTAGE-1 tiles in flight; wait for the first
@@ -432,14 +436,21 @@ qmm_kernel(const uint16_t* __restrict__ A, int lda, const uint8_t* __restrict__ 
             slot = nslot;
         }
     };
+    using T_ = std::integral_constant<bool, true>;
+    using F_ = std::integral_constant<bool, false>;
     if constexpr (KS == 1) {
-        mainloop(std::integral_constant<int, 0>{});
+        if (WMW == 1 || mw == 0) mainloop(std::integral_constant<int, 0>{}, T_{});
+        else mainloop(std::integral_constant<int, 0>{}, F_{});
     } else {
-        if (kh == 0) mainloop(std::integral_constant<int, 0>{});
-        else mainloop(std::integral_constant<int, 1>{});
+        if (kh == 0) {
+            if (WMW == 1 || mw == 0) mainloop(std::integral_constant<int, 0>{}, T_{});
+            else mainloop(std::integral_constant<int, 0>{}, F_{});
+        } else {
+            mainloop(std::integral_constant<int, 1>{}, F_{});
+        }
         // sum the two k-step phases: kh = 1 waves park their partials in the (drained) ring
         __syncthreads();
-        float* red = (float*)smem + (size_t)cg * (WM * WN * 16 * 64) + lane;
+        float* red = (float*)smem + (size_t)(cg * WMW + mw) * (WM * WN * 16 * 64) + lane;
         if (kh == 1) {
 #pragma unroll
             for (int i = 0; i < WM; ++i)
@@ -459,6 +470,7 @@ qmm_kernel(const uint16_t* __restrict__ A, int lda, const uint8_t* __restrict__ 
     }
 
     // ---- epilogue: 32x32 C/D layout: col = lane & 31, row = 8*(r>>2) + 4*(lane>>5) + (r&3) ----
+    const int m_wave = m_base + mw * WM * 32;
 #pragma unroll
     for (int t = 0; t < WN; ++t) {
         const int nt = n_wave + 32 * t;
@@ -471,7 +483,7 @@ qmm_kernel(const uint16_t* __restrict__ A, int lda, const uint8_t* __restrict__ 
                 for (int r = 0; r < 16; ++r) {
                     const float v = acc[i][t][r];
                     const float up = __shfl_xor(v, 16);
-                    const int m = m_base + i * 32 + 8 * (r >> 2) + 4 * h + (r & 3);
+                    const int m = m_wave + i * 32 + 8 * (r >> 2) + 4 * h + (r & 3);
                     if (col < 16 && n < N && m < M)
                         ((uint16_t*)Cv)[(size_t)m * ldc + (nt >> 1) + col] = f32_to_act<true>(glu_gate_f<EPI>(v) * up);
                 }
@@ -480,11 +492,11 @@ qmm_kernel(const uint16_t* __restrict__ A, int lda, const uint8_t* __restrict__ 
         if (n >= N) continue;
 #pragma unroll
         for (int i = 0; i < WM; ++i) {
-            const int m0 = m_base + i * 32 + 4 * h;
+            const int m0 = m_wave + i * 32 + 4 * h;
             float* cf = ((float*)Cv) + (size_t)m0 * ldc + n;
             uint16_t* ch = ((uint16_t*)Cv) + (size_t)m0 * ldc + n;
             auto roff = [&](int r) { return (size_t)(8 * (r >> 2) + (r & 3)) * ldc; };
-            if (m_base + i * 32 + 32 <= M) {
+            if (m_wave + i * 32 + 32 <= M) {
                 // full tile: branch-free, so the RMW loads issue back to back and wait once
                 if constexpr (EPI == E16_ADD_F32) {
                     if (splits == 1) {
@@ -530,14 +542,14 @@ qmm_kernel(const uint16_t* __restrict__ A, int lda, const uint8_t* __restrict__ 
     }
 }
 
-template <int QT, int WM, int WN, int NW, int KS, int OCC, int EPI>
+template <int QT, int WM, int WN, int NW, int KS, int OCC, int EPI, int WMW>
 static int launch_qmm(const uint16_t* A, int lda, const uint8_t* W, const uint16_t* WD, int M, int N, int K,
                       int splits, void* C, int ldc, hipStream_t st) {
     using G = QmmGeom<QT, WN>;
-    constexpr int BM = 32 * WM, BN = NW * G::COLS;
+    constexpr int BM = 32 * WM * WMW, BN = NW * G::COLS;
     constexpr int STAGE = BM * 128 + NW * G::WBYTES;
-    constexpr int NS = QmmRing<QT, WM, WN, NW, OCC>::STAGES;
-    if constexpr (NS < 3 || (KS > 1 && NW * WM * WN * 16 * 64 * 4 > NS * STAGE)) {
+    constexpr int NS = QmmRing<QT, WM, WN, NW, OCC, WMW>::STAGES;
+    if constexpr (NS < 3 || (KS > 1 && NW * WMW * WM * WN * 16 * 64 * 4 > NS * STAGE)) {
         return (int)hipErrorInvalidValue;  // this format's stage does not fit OCC rings of >= 3 k-tiles
     } else {
     constexpr size_t lds = (size_t)NS * STAGE;
@@ -551,12 +563,12 @@ static int launch_qmm(const uint16_t* A, int lda, const uint8_t* W, const uint16
     if (nwg <= 0 || nwg > 0x7fffffff) return (int)hipErrorInvalidValue;
     static bool attr_set = false;
     if (!attr_set) {
-        (void)hipFuncSetAttribute((const void*)qmm_kernel<QT, WM, WN, NW, KS, OCC, EPI>,
+        (void)hipFuncSetAttribute((const void*)qmm_kernel<QT, WM, WN, NW, KS, OCC, EPI, WMW>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         attr_set = true;
     }
-    qmm_kernel<QT, WM, WN, NW, KS, OCC, EPI><<<dim3((unsigned)nwg), 64 * NW * KS, lds, st>>>(A, lda, W, WD, M, N, K, n_ct,
-                                                                                     n_mt, splits, ktps, C, ldc);
+    qmm_kernel<QT, WM, WN, NW, KS, OCC, EPI, WMW><<<dim3((unsigned)nwg), 64 * NW * KS * WMW, lds, st>>>(
+        A, lda, W, WD, M, N, K, n_ct, n_mt, splits, ktps, C, ldc);
     MXK_CHECK_LAUNCH();
     }
 }
@@ -564,17 +576,22 @@ static int launch_qmm(const uint16_t* A, int lda, const uint8_t* W, const uint16
 template <int QT, int EPI>
 static int dispatch_qmm(int wm, int wn, int nw, int ks, const uint16_t* A, int lda, const uint8_t* W, const uint16_t* WD,
                         int M, int N, int K, int splits, void* C, int ldc, hipStream_t st) {
-    const int occ = 1 + (ks >> 4);
+    const int occ = 1 + ((ks >> 4) & 1);
+    const int wmw = 1 + ((ks >> 5) & 3);
     ks &= 15;
-#define QMM_CASE(WM_, WN_, NW_, KS_, OCC_)                                                                    \
-    if (wm == WM_ && wn == WN_ && nw == NW_ && ks == KS_ && occ == OCC_)                                      \
-        return launch_qmm<QT, WM_, WN_, NW_, KS_, OCC_, EPI>(A, lda, W, WD, M, N, K, splits, C, ldc, st);
-    QMM_CASE(1, 1, 4, 1, 1) QMM_CASE(2, 1, 4, 1, 1) QMM_CASE(4, 1, 4, 1, 1) QMM_CASE(1, 2, 4, 1, 1)
-    QMM_CASE(2, 2, 4, 1, 1) QMM_CASE(4, 2, 4, 1, 1) QMM_CASE(2, 1, 8, 1, 1) QMM_CASE(4, 1, 8, 1, 1)
-    QMM_CASE(2, 2, 8, 1, 1) QMM_CASE(4, 2, 8, 1, 1) QMM_CASE(2, 1, 4, 2, 1) QMM_CASE(4, 1, 4, 2, 1)
-    QMM_CASE(2, 2, 4, 2, 1)
+#define QMM_CASE(WM_, WN_, NW_, KS_, OCC_, WMW_)                                                              \
+    if (wm == WM_ && wn == WN_ && nw == NW_ && ks == KS_ && occ == OCC_ && wmw == WMW_)                       \
+        return launch_qmm<QT, WM_, WN_, NW_, KS_, OCC_, EPI, WMW_>(A, lda, W, WD, M, N, K, splits, C, ldc, st);
+    QMM_CASE(1, 1, 4, 1, 1, 1) QMM_CASE(2, 1, 4, 1, 1, 1) QMM_CASE(4, 1, 4, 1, 1, 1) QMM_CASE(1, 2, 4, 1, 1, 1)
+    QMM_CASE(2, 2, 4, 1, 1, 1) QMM_CASE(4, 2, 4, 1, 1, 1) QMM_CASE(2, 1, 8, 1, 1, 1) QMM_CASE(4, 1, 8, 1, 1, 1)
+    QMM_CASE(2, 2, 8, 1, 1, 1) QMM_CASE(4, 2, 8, 1, 1, 1) QMM_CASE(2, 1, 4, 2, 1, 1) QMM_CASE(4, 1, 4, 2, 1, 1)
+    QMM_CASE(2, 2, 4, 2, 1, 1)
     // two workgroups per CU (half-LDS ring)
-    QMM_CASE(2, 1, 4, 1, 2) QMM_CASE(4, 1, 4, 1, 2) QMM_CASE(2, 2, 4, 1, 2) QMM_CASE(2, 1, 4, 2, 2)
+    QMM_CASE(2, 1, 4, 1, 2, 1) QMM_CASE(4, 1, 4, 1, 2, 1) QMM_CASE(2, 2, 4, 1, 2, 1) QMM_CASE(2, 1, 4, 2, 2, 1)
+    // row-split wave grids (WMW waves along M): 64x64 / 128x64 / 64x32 / 128x32 wave tiles
+    QMM_CASE(2, 2, 2, 1, 1, 2) QMM_CASE(4, 2, 2, 1, 1, 2) QMM_CASE(2, 2, 2, 2, 1, 2) QMM_CASE(2, 1, 4, 1, 1, 2)
+    QMM_CASE(4, 1, 4, 1, 1, 2) QMM_CASE(2, 2, 4, 1, 1, 2) QMM_CASE(4, 2, 4, 1, 1, 2) QMM_CASE(1, 2, 4, 1, 1, 2)
+    QMM_CASE(2, 2, 2, 1, 2, 2) QMM_CASE(1, 2, 2, 1, 1, 4) QMM_CASE(2, 2, 2, 1, 1, 4)
 #undef QMM_CASE
     return (int)hipErrorInvalidValue;
 }

@@ -24,6 +24,7 @@ import numpy as np
 import torch
 
 from ..utils import roctx
+from ..utils.pinned import PinnedRing
 from ..models.llama import ForwardBatch, LlamaModel, Workspace
 from ..ops.sampling import SamplerBatch
 from .kv_cache import KVCache, make_block_manager
@@ -191,10 +192,8 @@ class StepGraph:
             if k in self.off:
                 self.view(img, k)[...] = v
         self.buf = torch.from_numpy(img.copy()).to(dev)
-        # pinned staging ring: a buffer is rewritten only after the step that used it was read back
-        self._pin = [torch.empty(o, dtype=torch.int32).pin_memory() for _ in range(e.pin_ring)] \
-            if dev.type == "cuda" else None
-        self._pin_i = 0
+        # pinned staging ring: a slot is rewritten only after the H2D copy that read it has run
+        self._pin = PinnedRing(e.pin_ring, 4 * o, dev) if dev.type == "cuda" else None
         v = {k: self.view(self.buf, k) for k in self.off}
         self.v = v
         self.prev = torch.zeros(e.ws.max_seqs, dtype=torch.int32, device=dev)  # previous step's samples
@@ -287,11 +286,7 @@ class StepGraph:
             self.prev[:prev.numel()].copy_(prev, non_blocking=True)
         img = self.image(plan)
         if self._pin is not None:
-            k = self._pin_i
-            self._pin_i = (k + 1) % len(self._pin)
-            hb = self._pin[k]
-            hb.numpy()[:] = img
-            self.buf.copy_(hb, non_blocking=True)
+            self._pin.stage(img, self.buf)
         else:
             self.buf.copy_(torch.from_numpy(img))
         t0 = time.perf_counter()
@@ -869,24 +864,15 @@ class LLMEngine:
         return {k: d[o:o + int(np.prod(sh))].view(sh) for k, o, sh in spec}
 
     def _stage_h2d(self, flat: np.ndarray) -> torch.Tensor:
-        """int32 host array -> device, through a ring of 3 persistent pinned buffers (a buffer is
-        reused only after the step that last used it has been read back, so the async copy that
-        sourced it has completed); a fresh pinned allocation per step costs ~ms on the host."""
-        n = flat.size
+        """int32 host array -> device through the pinned ring (utils/pinned.py: a slot is reused only
+        after the async copy that sourced it has run); a fresh pinned allocation per step costs ~ms."""
         if self.device.type != "cuda":
             return torch.from_numpy(np.array(flat, dtype=np.int32))
-        if self._pin_in is None or self._pin_in[0].numel() < n:
+        if self._pin_in is None:
             c = self.cfg
-            cap = max(n, 4 * c.max_batched_tokens + c.max_num_seqs * (6 + 2 * self.max_blocks_per_seq) + 1024)
-            if self._pin_in is not None and self.device.type == "cuda":
-                torch.cuda.synchronize(self.device)  # the old ring may still source in-flight copies
-            self._pin_in = [torch.empty(cap, dtype=torch.int32).pin_memory() for _ in range(self.pin_ring)]
-            self._pin_in_i = 0
-        k = self._pin_in_i
-        self._pin_in_i = (k + 1) % len(self._pin_in)
-        hb = self._pin_in[k][:n]
-        hb.numpy()[:] = flat
-        return hb.to(self.device, non_blocking=True)
+            cap = 4 * (4 * c.max_batched_tokens + c.max_num_seqs * (6 + 2 * self.max_blocks_per_seq) + 1024)
+            self._pin_in = PinnedRing(self.pin_ring, cap, self.device)
+        return self._pin_in.stage(np.ascontiguousarray(flat, dtype=np.int32))
 
     def _fix_tensors(self, t: dict):
         if "fix_dst" not in t:
@@ -910,8 +896,28 @@ class LLMEngine:
             t0 = time.perf_counter()
             out = am.cpu().tolist()
             self.stats["wait_s"] += time.perf_counter() - t0
+            self._check_collectives()
             return out, None
-        return self._sample(logits, sample_items)
+        out = self._sample(logits, sample_items)
+        self._check_collectives()
+        return out
+
+    def _check_collectives(self, every: int = 1):
+        """Tensor parallel: the one-shot all-reduce kernel flags a peer that never delivered (bounded
+        spin) instead of hanging; read that flag at a point where the stream is already synchronised
+        and fail the rank loudly (exit non-zero through TPLink) rather than serve wrong logits."""
+        if self.tp is None:
+            return
+        ar = getattr(self.model, "custom_ar", None)
+        if ar is None:
+            return
+        self._ar_checks = getattr(self, "_ar_checks", 0) + 1
+        if self._ar_checks % every:
+            return
+        try:
+            ar.check()
+        except RuntimeError as ex:
+            self.tp._fail("one-shot all-reduce", ex)
 
     def _build_fb(self, plan: dict, t: dict | None = None) -> ForwardBatch:
         nd = plan["nd"]
@@ -948,6 +954,7 @@ class LLMEngine:
                 self.precapture_graphs()
                 continue
             self._execute(msg)
+            self._check_collectives(every=64)
 
     def _sample(self, logits, items):
         params = [it.seq.params for it in items]

@@ -382,10 +382,25 @@ Q32_FORCE: tuple | None = None  # (wm, wn, splits) override for tuning (tools/tu
 # qmm.hip (LDS-DMA ring, counted vmcnt) runs every f16 GEMM on t32-tiled weights
 QMM_FORCE: tuple | None = None  # (wm, wn, nw, ks, splits) override for tuning (tools/tune_qmm.py)
 # tile configurations compiled into qmm.hip (wm, wn, nw, ks)
+# ks field: bits 0-3 k-step split KS, bit 4 half-LDS ring (two workgroups per CU), bits 5-6 WMW - 1 (waves
+# splitting the rows of a column group: wave tile 32*wm x 32*wn, workgroup tile 32*wm*WMW x 32*wn*nw)
+def qmm_ks(ks: int = 1, occ2: bool = False, wmw: int = 1) -> int:
+    return ks | (16 if occ2 else 0) | ((wmw - 1) << 5)
+
+
 QMM_CONFIGS = ((1, 1, 4, 1), (2, 1, 4, 1), (4, 1, 4, 1), (1, 2, 4, 1), (2, 2, 4, 1), (4, 2, 4, 1), (2, 1, 8, 1),
                (4, 1, 8, 1), (2, 2, 8, 1), (4, 2, 8, 1), (2, 1, 4, 2), (4, 1, 4, 2), (2, 2, 4, 2),
                # ks | 16: half-LDS ring, two workgroups per CU
-               (2, 1, 4, 17), (4, 1, 4, 17), (2, 2, 4, 17), (2, 1, 4, 18))
+               (2, 1, 4, 17), (4, 1, 4, 17), (2, 2, 4, 17), (2, 1, 4, 18),
+               # row-split wave grids
+               (2, 2, 2, 33), (4, 2, 2, 33), (2, 2, 2, 34), (2, 1, 4, 33), (4, 1, 4, 33), (2, 2, 4, 33),
+               (4, 2, 4, 33), (1, 2, 4, 33), (2, 2, 2, 49), (1, 2, 2, 97), (2, 2, 2, 97))
+
+
+def qmm_geom(wm: int, wn: int, nw: int, ks: int):
+    """-> (BM, BN, waves) of a qmm configuration."""
+    wmw = 1 + ((ks >> 5) & 3)
+    return 32 * wm * wmw, 32 * wn * nw, nw * (ks & 15) * wmw
 
 
 QMM_OCC = os.environ.get("MX_QMM_OCC", "1") != "0"  # A/B switch for the two-workgroups-per-CU tiles
@@ -415,8 +430,9 @@ def _qmm_shape(M: int, N_: int, K: int, can_split: bool):
         wn, nw, ks = 1, 4, 2
     else:
         wm, wn, nw, ks = 4, (2 if (M > 256 and N_ >= 6144) else 1), 8, 1
-    mt = -(-M // (32 * wm))
-    cols = -(-N_ // (32 * wn * nw))
+    bm, bn, _ = qmm_geom(wm, wn, nw, ks)
+    mt = -(-M // bm)
+    cols = -(-N_ // bn)
     splits = 1
     if can_split:
         while cols * mt * splits < (3 * CU_COUNT) // 4 and (K // 64) // (splits * 2) >= 8:

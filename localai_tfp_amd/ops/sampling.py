@@ -93,25 +93,21 @@ class SamplerBatch:
         return arr, np.asarray(toks or [0], np.int32), np.asarray(cnts or [0], np.int32), np.asarray(bias or [0.0], np.float32)
 
     def _stage(self, dev, parts: list[np.ndarray]) -> list[torch.Tensor]:
-        """Byte arrays -> device views (16-B aligned) through ONE copy from a ring of 3 pinned buffers:
-        a pageable H2D copy would make the host wait for the stream, stalling the next step's launch."""
+        """Byte arrays -> device views (16-B aligned) through ONE copy from a pinned ring whose slots
+        are reused only after the copy that read them ran (utils/pinned.py): a pageable H2D copy
+        would make the host wait for the stream, stalling the next step's launch."""
+        from ..utils.pinned import PinnedRing
         offs, n = [], 0
         for a in parts:
             offs.append(n)
             n += -(-a.size // 16) * 16
         ring = getattr(self, "_pin", None)
-        if ring is None or ring[0].numel() < n:
-            if ring is not None:
-                torch.cuda.synchronize(dev)  # the old buffers may still source in-flight copies
-            self._pin = [torch.empty(max(n, 1 << 20), dtype=torch.uint8).pin_memory() for _ in range(3)]
-            self._pin_k = 0
-        k = self._pin_k
-        self._pin_k = (k + 1) % 3
-        hb = self._pin[k][:n]
-        hv = hb.numpy()
+        if ring is None:
+            ring = self._pin = PinnedRing(4, max(n, 1 << 20), dev)
+        img = np.zeros(n, np.uint8)
         for o, a in zip(offs, parts):
-            hv[o:o + a.size] = a
-        d = hb.to(dev, non_blocking=True)
+            img[o:o + a.size] = a
+        d = ring.stage(img)
         return [d[o:o + a.size] for o, a in zip(offs, parts)]
 
     def sample(self, logits: torch.Tensor, params: list[SamplingParams], histories: list[list[int]],
