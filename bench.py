@@ -63,7 +63,41 @@ def parse():
                     help="tensor-parallel ranks per serving replica (BASELINE config #3: --model llama3-70b "
                          "--gpus 8 --tp 8); world = dp x tp, rank 0 of every group leads")
     ap.add_argument("--no-tp-check", action="store_true", help="skip the TP-vs-unsharded logits self-check")
+    ap.add_argument("--tokenizer", default="bpe", choices=["bpe", "byte"],
+                    help="bpe: a synthetic Llama-3-sized byte-level BPE vocabulary (128,256 ids, tokenizer/synth_bpe.py) "
+                         "served through the GGUF BPE tokenizer; byte: one token per byte (no detokenisation work)")
+    ap.add_argument("--phases", default="reference,greedy",
+                    help="comma list of sampling phases measured back to back on the same server: reference = "
+                         "the reference's defaults (temperature 0.9, top_k 40, top_p 0.95; backend_config.go "
+                         "SetDefaults) on the GPU sampler; greedy = argmax. The first phase is the headline")
     return ap.parse_args()
+
+
+SAMPLING = {"reference": {"temperature": 0.9, "top_k": 40, "top_p": 0.95},
+            "greedy": {"temperature": 0.0}}
+
+
+def make_tokenizer(kind: str, vocab: int):
+    from localai_tfp_amd.tokenizer import ByteTokenizer
+    if kind == "byte":
+        return ByteTokenizer(vocab)
+    from localai_tfp_amd.tokenizer.synth_bpe import llama3_like_tokenizer
+    tok = llama3_like_tokenizer()
+    if tok.vocab_size != vocab:
+        raise SystemExit(f"synthetic BPE vocabulary has {tok.vocab_size} ids, the model {vocab}")
+    return tok
+
+
+def prompt_sizing(tok, prompt_len: int):
+    """(template tokens, words of the load generator's vocabulary per prompt) so that a chat request's
+    prompt is ~prompt_len tokens after the chat template."""
+    from localai_tfp_amd.templates.chat import render_chat
+    from localai_tfp_amd.tools.loadgen import WORDS
+    overhead = len(tok.encode(render_chat([{"role": "user", "content": ""}], tok)))
+    rng = np.random.default_rng(0)
+    sample = " ".join(rng.choice(WORDS, size=2000))
+    per_word = len(tok.encode(sample, add_special=False)) / 2000.0
+    return overhead, max(1, int(round((prompt_len - overhead) / per_word)))
 
 
 class _GroupSync:
@@ -173,7 +207,9 @@ def main():
     src = synthetic_source(cfg, "Q4_K_M", seed=1, shard_gen=tp > 1)
     model = LlamaModel.load(cfg, src, dev, rank % tp, tp, tp_group)
     t_load = time.time() - t0
-    tok = ByteTokenizer(cfg.vocab)
+    if args.tokenizer == "bpe" and cfg.vocab != 128256:  # CPU plumbing model / other vocabularies
+        args.tokenizer = "byte"
+    tok = make_tokenizer(args.tokenizer, cfg.vocab)
     ecfg = EngineConfig(max_num_seqs=args.concurrency, max_batched_tokens=args.max_batched_tokens,
                         max_model_len=max(4096, args.prompt_len + args.gen_len + 64), use_graphs=not args.no_graphs,
                         kv_dtype=args.kv_dtype)
@@ -195,7 +231,14 @@ def main():
     else:
         res = run_engine(args, eng, tok, dev, dist)
         eng.shutdown()  # tensor parallel: releases the followers from engine.follow()
-    t_el, tokens, ttfts, extra = res
+    t_el, tokens, ttfts, extra = res[0]
+    phase_extra = {}
+    for ph, (t2, tok2, tt2, ex2) in zip(args.phases.split(",")[1:], res[1:]):
+        phase_extra[ph] = {"value": round(tok2 / t2, 2) if t2 else None,
+                           "p50_ttft_ms": round(float(np.percentile(tt2, 50)), 2) if len(tt2) else None,
+                           "p99_ttft_ms": round(float(np.percentile(tt2, 99)), 2) if len(tt2) else None,
+                           "ms_per_step": round(t2 / args.steps * 1e3, 3), **{k: ex2[k] for k in (
+                               "client_completed_requests", "ttft_samples", "p50_itl_ms") if k in ex2}}
 
     p50 = float(np.percentile(ttfts, 50)) if len(ttfts) else float("nan")
     p99 = float(np.percentile(ttfts, 99)) if len(ttfts) else float("nan")
@@ -245,6 +288,10 @@ def main():
                 "weights_gb": round(model.weight_bytes() / 1e9, 2),
                 "dense_weight_copy_gb": round(model.dense_cache_bytes() / 1e9, 2) if hasattr(model, "dense_cache_bytes") else 0.0, "kv_blocks": eng.kv.num_blocks,
                 "kv_dtype": args.kv_dtype,
+                "tokenizer": ("synthetic Llama-3-sized byte-level BPE (128,256 ids) through the GGUF BPE tokenizer"
+                              if args.tokenizer == "bpe" else "byte"),
+                "sampling": {"phase": args.phases.split(",")[0], **SAMPLING[args.phases.split(",")[0]]},
+                **({"other_phases": phase_extra} if phase_extra else {}),
                 "host_gc": {k: round(v, 4) for k, v in __import__("localai_tfp_amd.engine.engine",
                                                                   fromlist=["GC_STATS"]).GC_STATS.items()},
                 **extra,
@@ -269,9 +316,9 @@ class Window:
     the barrier aligns the windows.
     """
 
-    def __init__(self, eng, warmup, steps, dev, dist, steady_finished: int):
+    def __init__(self, eng, warmup, steps, dev, dist, steady_finished: int, base_finished: int = 0):
         self.eng, self.W, self.K, self.dev, self.dist = eng, warmup, steps, dev, dist
-        self.steady_finished = steady_finished
+        self.steady_finished = steady_finished + base_finished
         self.steady_step = None
         self.t0 = self.t1 = None
         self.tok0 = self.tok1 = 0
@@ -307,6 +354,8 @@ def steady_gate(args) -> int:
 
 
 def run_http(args, eng, tok, cfg, dev, dist):
+    """One gateway + worker; one closed-loop load generator per sampling phase, each with its own
+    steady-state window. Returns [(window_s, tokens, ttfts, extra)] per phase."""
     import yaml
     from localai_tfp_amd.grpc.server import AioServer
     from localai_tfp_amd.workers.llm import LLMServicer
@@ -314,8 +363,6 @@ def run_http(args, eng, tok, cfg, dev, dist):
     sys.setswitchinterval(0.0005)  # same as workers/llm.py main(): engine thread + gRPC loop share the GIL
     svc = LLMServicer(device=str(dev))
     svc.attach(eng, tok)
-    win = Window(eng, args.warmup, args.steps, dev, dist, steady_gate(args))
-    eng.on_step = win
     eng.start()
     server = AioServer(svc, "127.0.0.1:0", max_workers=16)
     work = tempfile.mkdtemp(prefix="mxbench")
@@ -324,7 +371,7 @@ def run_http(args, eng, tok, cfg, dev, dist):
     with open(os.path.join(models, "llama-3-8b-instruct.yaml"), "w") as f:
         yaml.safe_dump({"name": "llama-3-8b-instruct", "backend": "llama-cpp",
                         "context_size": eng.cfg.max_model_len,
-                        "parameters": {"model": f"synthetic:{args.model}", "temperature": 0.0},
+                        "parameters": {"model": f"synthetic:{args.model}"},
                         "template": {"use_tokenizer_template": True},
                         "known_usecases": ["chat"]}, f)
     port = free_port()
@@ -339,35 +386,54 @@ def run_http(args, eng, tok, cfg, dev, dist):
                            "--upload-path", os.path.join(work, "up"),
                            "--external-grpc-backends", f"llama-cpp:127.0.0.1:{server.port}"],
                           env=env, cwd=ROOT, stdout=gw_log, stderr=subprocess.STDOUT, start_new_session=True)
-    lg = None
+    if args.tokenizer == "byte":
+        size_args = ["--prompt-chars", str(max(1, args.prompt_len - TEMPLATE_OVERHEAD))]
+    else:
+        _, n_words = prompt_sizing(tok, args.prompt_len)
+        size_args = ["--prompt-words", str(n_words)]
+    out = []
     try:
         wait_http(f"http://127.0.0.1:{port}/readyz", 120, gw)
-        rec_path = os.path.join(work, "loadgen.json")
-        lg = subprocess.Popen([sys.executable, "-m", "localai_tfp_amd.tools.loadgen",
-                               "--url", f"http://127.0.0.1:{port}", "--model", "llama-3-8b-instruct",
-                               "--concurrency", str(args.concurrency),
-                               "--prompt-chars", str(max(1, args.prompt_len - TEMPLATE_OVERHEAD)),
-                               "--gen-len", str(args.gen_len), "--seed", str(int(os.environ.get("RANK", "0"))),
-                               "--stagger",
-                               "--out", rec_path], env=env, cwd=ROOT, start_new_session=True)
-        t_start = time.time()
-        last = -1
-        while not win.done.wait(30):
-            n = eng.stats["steps"]
-            print(f"[bench rank {os.environ.get('RANK', '0')}] steps={n} out_tokens={eng.stats['out_tokens']}",
-                  file=sys.stderr, flush=True)
-            if lg.poll() is not None or gw.poll() is not None:
-                raise RuntimeError("load generator or gateway exited early; see " + work)
-            if time.time() - t_start > args.timeout or (n == last and n > 0):
-                raise TimeoutError(f"window not reached (steps={n}); see {work}")
-            last = n
-    finally:
-        if lg is not None and lg.poll() is None:
-            lg.send_signal(signal.SIGTERM)
+        for pi, phase in enumerate(args.phases.split(",")):
+            sp = SAMPLING[phase]
+            samp_args = ["--temperature", str(sp["temperature"])]
+            if "top_k" in sp:
+                samp_args += ["--top-k", str(sp["top_k"]), "--top-p", str(sp["top_p"])]
+            win = Window(eng, args.warmup, args.steps, dev, dist, steady_gate(args),
+                         base_finished=eng.stats["finished"])
+            eng.on_step = win
+            rec_path = os.path.join(work, f"loadgen_{pi}.json")
+            lg = subprocess.Popen([sys.executable, "-m", "localai_tfp_amd.tools.loadgen",
+                                   "--url", f"http://127.0.0.1:{port}", "--model", "llama-3-8b-instruct",
+                                   "--concurrency", str(args.concurrency), *size_args, *samp_args,
+                                   "--gen-len", str(args.gen_len), "--seed", str(int(os.environ.get("RANK", "0")) + 97 * pi),
+                                   "--stagger", "--out", rec_path], env=env, cwd=ROOT, start_new_session=True)
             try:
-                lg.wait(timeout=60)
-            except subprocess.TimeoutExpired:
-                lg.kill()
+                t_start = time.time()
+                last = -1
+                while not win.done.wait(30):
+                    n = eng.stats["steps"]
+                    print(f"[bench rank {os.environ.get('RANK', '0')}] phase={phase} steps={n} "
+                          f"out_tokens={eng.stats['out_tokens']}", file=sys.stderr, flush=True)
+                    if lg.poll() is not None or gw.poll() is not None:
+                        raise RuntimeError("load generator or gateway exited early; see " + work)
+                    if time.time() - t_start > args.timeout or (n == last and n > 0):
+                        raise TimeoutError(f"window not reached (steps={n}); see {work}")
+                    last = n
+            finally:
+                eng.on_step = None
+                if lg.poll() is None:
+                    lg.send_signal(signal.SIGTERM)
+                    try:
+                        lg.wait(timeout=60)
+                    except subprocess.TimeoutExpired:
+                        lg.kill()
+            out.append(_http_phase_result(win, rec_path))
+            # the cancelled streams of this phase must leave the engine before the next phase's gate counts
+            t_d = time.time()
+            while (eng.sched.running or eng.sched.waiting) and time.time() - t_d < 120:
+                time.sleep(0.1)
+    finally:
         eng.on_step = None
         eng.shutdown()
         gw.terminate()
@@ -376,6 +442,10 @@ def run_http(args, eng, tok, cfg, dev, dist):
         except subprocess.TimeoutExpired:
             gw.kill()
         server.stop()
+    return out
+
+
+def _http_phase_result(win, rec_path):
     recs = []
     try:
         with open(rec_path) as f:
@@ -405,13 +475,23 @@ def run_engine(args, eng, tok, dev, dist):
     from localai_tfp_amd.ops.sampling import SamplingParams
     from localai_tfp_amd.templates.chat import render_chat
     rng = np.random.default_rng(1234 + int(os.environ.get("RANK", "0")))
-    words = ["the", "model", "serves", "tokens", "fast", "on", "MI355X", "with", "paged", "attention"]
+    from localai_tfp_amd.tools.loadgen import WORDS as words
+
+    if args.tokenizer == "byte":
+        n_words = None
+    else:
+        _, n_words = prompt_sizing(tok, args.prompt_len)
 
     def make_prompt():
-        body = " ".join(rng.choice(words, size=args.prompt_len))[: max(1, args.prompt_len - TEMPLATE_OVERHEAD)]
+        if n_words is None:
+            body = " ".join(rng.choice(words, size=args.prompt_len))[: max(1, args.prompt_len - TEMPLATE_OVERHEAD)]
+        else:
+            body = " ".join(rng.choice(words, size=n_words))
         return tok.encode(render_chat([{"role": "user", "content": body}], tok))
 
-    sp = SamplingParams(temperature=0.0, top_k=1, ignore_eos=True)
+    phase = args.phases.split(",")[0]
+    sp = SamplingParams(**SAMPLING[phase], ignore_eos=True) if phase != "greedy" else \
+        SamplingParams(temperature=0.0, top_k=1, ignore_eos=True)
     handles = {}
     ttfts = []
     timed = {"on": False}
@@ -466,8 +546,8 @@ def run_engine(args, eng, tok, dev, dist):
     if dist:
         dist.barrier()
     t_el = time.monotonic() - t_start
-    return t_el, eng.stats["out_tokens"] - tok0, ttfts, {"steady_at_step": n_pre,
-                                                         "window_host": _host_delta(s0, _host_snapshot(eng))}
+    return [(t_el, eng.stats["out_tokens"] - tok0, ttfts, {"steady_at_step": n_pre,
+                                                          "window_host": _host_delta(s0, _host_snapshot(eng))})]
 
 
 def _host_snapshot(eng):

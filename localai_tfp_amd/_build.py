@@ -59,12 +59,18 @@ def _jobs():
     return max(1, min(n, 16))
 
 
+# per-source extra flags. qmm8.hip: MFMA results in VGPRs (gfx950's unified register file) — the integer
+# sub-block scales are applied by VALU right after every MFMA, and AGPR results would cost one
+# v_accvgpr_read per element.
+FILE_FLAGS = {"qmm8.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]}
+
+
 def _build_lib(name: str, srcs, headers, compiler, cflags, ldflags, verbose=False) -> Path:
     LIB.mkdir(parents=True, exist_ok=True)
     BUILD.mkdir(parents=True, exist_ok=True)
     out = LIB / name
     stamp = BUILD / (name + ".stamp")
-    key = _hash(list(srcs) + list(headers)) + "|" + " ".join(cflags) + "|" + ARCH
+    key = _hash(list(srcs) + list(headers)) + "|" + " ".join(cflags) + "|" + ARCH + "|" + repr(sorted(FILE_FLAGS.items()))
     if out.exists() and stamp.exists() and stamp.read_text() == key:
         return out
     objs = []
@@ -72,10 +78,11 @@ def _build_lib(name: str, srcs, headers, compiler, cflags, ldflags, verbose=Fals
     def compile_one(src: Path):
         obj = BUILD / (name + "." + src.stem + ".o")
         okey = BUILD / (name + "." + src.stem + ".key")
-        k = _hash([src] + list(headers)) + "|" + " ".join(cflags)
+        flags = list(cflags) + FILE_FLAGS.get(src.name, [])
+        k = _hash([src] + list(headers)) + "|" + " ".join(flags)
         if obj.exists() and okey.exists() and okey.read_text() == k:
             return obj
-        cmd = [compiler, *cflags, "-c", str(src), "-o", str(obj)]
+        cmd = [compiler, *flags, "-c", str(src), "-o", str(obj)]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         _run(cmd)

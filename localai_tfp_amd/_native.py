@@ -27,6 +27,9 @@ U64 = C.c_uint64
 KERNEL_SIGS = {
     "mxk_rmsnorm": [P, I, P, I, P, P, P, I, P, P, I, I, F, P],
     "mxk_quant_q8": [P, I, P, P, I, I, P],
+    "mxk_quant_q8k": [P, I, I, P, P, P, I, I, P],
+    "mxk_rmsnorm_q8k": [P, I, P, P, I, P, P, P, I, I, F, P],
+    "mxk_qmm8": [I, I, I, I, I, I, I, P, I, P, P, P, I, I, I, I, P, I, P],
     "mxk_layernorm": [P, I, P, I, P, P, P, P, P, I, I, I, F, P],
     "mxk_groupnorm_nhwc": [P, P, P, P, I, I, I, I, F, I, P],
     "mxk_layernorm_mod": [P, I, P, P, I, I, P, I, I, I, F, P],

@@ -81,9 +81,10 @@ class EngineConfig:
     mixed_graph_seqs: int = 4
     max_graphs: int = 64
     attn_part_size: int = 256  # must match ops.core.attn_decode's default
-    # dense 16-bit copy of the layer projections for hipBLASLt at the M where it still beats the qmm
-    # kernels on t32-tiled weights (ops/linear.py DENSE_MIN_M_*; never for the LM head)
-    prefill_bf16_cache: bool = True
+    # dense 16-bit copy of the layer projections for hipBLASLt (ops/linear.py DENSE_MIN_M_*). Off: the
+    # int8-MFMA kernels on Q8_K activations (qmm8.hip) run every M > 4 GEMM on the quantised weights;
+    # MX_DENSE_CACHE=1 restores the copy (A/B only; it costs 2 B/param of HBM)
+    prefill_bf16_cache: bool = __import__("os").environ.get("MX_DENSE_CACHE", "0") == "1"
     kv_dtype: str = "bf16"  # paged KV cache element type: bf16 | fp8 (OCP e4m3, half the bytes per token)
     # overlap the host with the GPU: launch step N, then read step N-1's sampled tokens (async
     # device->host copy) and schedule N+1 while N runs; decode inputs come from the device

@@ -309,6 +309,59 @@ def _qmatmul_t32(W: QWeight, x, epi: int, out, xq, xds, M: int, out_zeroed: bool
     return out
 
 
+# ------------------------------------------------------------------------------------------------
+# int8-MFMA GEMM on Q8_K activations (csrc/kernels/qmm8.hip): llama.cpp's K-quant dot-product numerics.
+QMM8 = os.environ.get("MX_QMM8", "1") != "0"
+QMM8_FORCE: tuple | None = None  # (wm, wn, nw, wmw, occ, splits) override for tuning (tools/tune_qmm8.py)
+QMM8_CONFIGS = ((2, 1, 4, 1, 1), (2, 1, 4, 2, 1), (2, 1, 4, 1, 2), (1, 2, 4, 2, 1), (2, 1, 8, 1, 1),
+                (1, 2, 2, 2, 1), (1, 2, 4, 1, 2))
+
+
+def qmm8_ok(W) -> bool:
+    """Weight eligible for the int8-MFMA path (t32 Q4_K / Q6_K on the GPU)."""
+    return (QMM8 and isinstance(W, QWeight) and W.layout == "t32" and W.data.is_cuda
+            and int(W.qtype) in (int(QType.Q4_K), int(QType.Q6_K)))
+
+
+def _qmm8_shape(M: int, N_: int, K: int, can_split: bool):
+    if QMM8_FORCE is not None:
+        wm, wn, nw, wmw, occ, splits = QMM8_FORCE
+        return wm, wn, nw, wmw, occ, (splits if can_split else 1)
+    if M <= 64:
+        wm, wn, nw, wmw, occ = 2, 1, 4, 1, 2
+    else:
+        wm, wn, nw, wmw, occ = 2, 1, 4, 2, 1
+    bm, bn = 32 * wm * wmw, 32 * wn * nw
+    tiles = -(-M // bm) * -(-N_ // bn)
+    splits = 1
+    if can_split:
+        while tiles * splits < (3 * CU_COUNT) // 4 and (K // 256) // (splits * 2) >= 2:
+            splits *= 2
+    return wm, wn, nw, wmw, occ, splits
+
+
+def qmatmul8(W: QWeight, a, epi: int, out: torch.Tensor, *, out_zeroed: bool = False):
+    """out (+)= A @ W^T for Q8_K activations `a` (ops.core.Q8KAct) and a t32 Q4_K / Q6_K weight
+    (qmm8_ok). CPU: fp32 reference on the dequantised operands."""
+    M = a.q.shape[0]
+    if M == 0:
+        return out
+    if not a.q.is_cuda:
+        return _qmatmul_ref(W, a.dequant(), epi, out)
+    can_split = epi == EPI_ADD_F32 or (epi == EPI_F32 and out_zeroed)
+    wm, wn, nw, wmw, occ, splits = _qmm8_shape(M, W.N, W.K, can_split)
+    e = EPI_ADD_F32 if (epi == EPI_F32 and splits > 1) else epi
+    if e in (EPI_BF16, *GLU_EPIS):
+        if out.dtype != torch.float16:
+            raise ValueError("qmatmul8: 16-bit outputs are f16")
+        N.ensure_act(out.dtype)
+    if a.q.stride(0) % 16 or not a.d.is_contiguous() or not a.bs.is_contiguous():
+        raise ValueError("qmatmul8: Q8_K operand needs 16-B aligned code rows and contiguous d / bsums")
+    N.kcall("mxk_qmm8", int(W.qtype), e, wm, wn, nw, wmw, occ, a.q.data_ptr(), a.q.stride(0), a.d.data_ptr(),
+            a.bs.data_ptr(), W.data.data_ptr(), M, W.N, W.K, splits, out.data_ptr(), out.stride(0), N.stream_ptr())
+    return out
+
+
 QMV_FUSE = os.environ.get("MX_QMV_FUSE", "1") != "0"
 
 

@@ -68,10 +68,18 @@ async def run(a):
     url = a.url.rstrip("/") + "/v1/chat/completions"
 
     def mk_body():
-        n_words = max(1, a.prompt_chars // 6)
-        content = " ".join(rng.choice(WORDS) for _ in range(n_words))[: a.prompt_chars]
-        return {"model": a.model, "stream": True, "max_tokens": a.gen_len, "temperature": a.temperature,
+        if a.prompt_words:  # subword tokenizer: the caller sized the word count to the token budget
+            content = " ".join(rng.choice(WORDS) for _ in range(a.prompt_words))
+        else:  # byte tokenizer: one token per character
+            n_words = max(1, a.prompt_chars // 6)
+            content = " ".join(rng.choice(WORDS) for _ in range(n_words))[: a.prompt_chars]
+        body = {"model": a.model, "stream": True, "max_tokens": a.gen_len, "temperature": a.temperature,
                 "ignore_eos": True, "messages": [{"role": "user", "content": content}]}
+        if a.top_k is not None:
+            body["top_k"] = a.top_k
+        if a.top_p is not None:
+            body["top_p"] = a.top_p
+        return body
     rec: list = []
     stop = asyncio.Event()
     loop = asyncio.get_running_loop()
@@ -108,7 +116,10 @@ def main(argv=None):
     ap.add_argument("--concurrency", type=int, default=64)
     ap.add_argument("--prompt-chars", type=int, default=220)
     ap.add_argument("--gen-len", type=int, default=256)
+    ap.add_argument("--prompt-words", type=int, default=0, help="prompt of N words (overrides --prompt-chars)")
     ap.add_argument("--temperature", type=float, default=0.0)
+    ap.add_argument("--top-k", type=int, default=None)
+    ap.add_argument("--top-p", type=float, default=None)
     ap.add_argument("--duration", type=float, default=0.0)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--stagger", action="store_true", help="spread the first requests' lengths evenly")
