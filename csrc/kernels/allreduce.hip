@@ -22,11 +22,13 @@ struct MxArPeers {
     unsigned long long* recv[MX_AR_MAX_WORLD];  // peer receive buffers (IPC-mapped; [rank] = local)
 };
 
-template <bool F16>
+// RES: instead of writing the 16-bit sum, add it into an fp32 residual stream (res[2i], res[2i+1]) — the
+// row-parallel projection's all-reduce and the residual add in one pass.
+template <bool F16, bool RES>
 __global__ __launch_bounds__(256) void allreduce_1shot_kernel(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
                                                               int ng, int rank, int world, MxArPeers peers,
                                                               long slot_granules, const uint32_t* epoch_ctr,
-                                                              int* err) {
+                                                              int* err, float2* __restrict__ res) {
     const uint32_t epoch = *epoch_ctr + 1u;
     const long par = epoch & 1u;
     const int stride = gridDim.x * blockDim.x;
@@ -59,7 +61,14 @@ __global__ __launch_bounds__(256) void allreduce_1shot_kernel(const uint32_t* __
             a += lo;
             b += hi;
         }
-        out[i] = pack_act2<F16>(a, b);
+        if constexpr (RES) {
+            float2 r = res[i];
+            r.x += a;
+            r.y += b;
+            res[i] = r;
+        } else {
+            out[i] = pack_act2<F16>(a, b);
+        }
     }
 }
 
@@ -100,8 +109,27 @@ extern "C" int mxk_allreduce_1shot(const uint16_t* in, uint16_t* out, int n, int
     const int ng = n / 2;
     int blocks = (ng + 255) / 256;
     if (blocks > 128) blocks = 128;
-    MX_ACT_DISPATCH((allreduce_1shot_kernel<F16><<<blocks, 256, 0, st>>>((const uint32_t*)in, (uint32_t*)out, ng, rank,
-                                                                          world, pp, slot_granules, epoch_ctr, err)));
+    MX_ACT_DISPATCH((allreduce_1shot_kernel<F16, false><<<blocks, 256, 0, st>>>(
+        (const uint32_t*)in, (uint32_t*)out, ng, rank, world, pp, slot_granules, epoch_ctr, err, nullptr)));
+    allreduce_epoch_bump_kernel<<<1, 64, 0, st>>>(epoch_ctr);
+    MXK_CHECK_LAUNCH();
+}
+
+// same, but res (fp32, n elements, 8-B aligned) += the sum; `in` is not overwritten.
+extern "C" int mxk_allreduce_1shot_add(const uint16_t* in, float* res, int n, int rank, int world,
+                                       unsigned long long* const* peers, long slot_granules, uint32_t* epoch_ctr,
+                                       int* err, hipStream_t st) {
+    if (n <= 0) return 0;
+    if ((n & 1) || world < 1 || world > MX_AR_MAX_WORLD || rank < 0 || rank >= world || (long)(n / 2) > slot_granules ||
+        ((uintptr_t)in & 3) || ((uintptr_t)res & 7))
+        return (int)hipErrorInvalidValue;
+    MxArPeers pp{};
+    for (int p = 0; p < world; ++p) pp.recv[p] = peers[p];
+    const int ng = n / 2;
+    int blocks = (ng + 255) / 256;
+    if (blocks > 128) blocks = 128;
+    MX_ACT_DISPATCH((allreduce_1shot_kernel<F16, true><<<blocks, 256, 0, st>>>(
+        (const uint32_t*)in, nullptr, ng, rank, world, pp, slot_granules, epoch_ctr, err, (float2*)res)));
     allreduce_epoch_bump_kernel<<<1, 64, 0, st>>>(epoch_ctr);
     MXK_CHECK_LAUNCH();
 }

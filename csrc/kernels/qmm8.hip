@@ -54,7 +54,8 @@ struct Q8Geom {
     static constexpr int BM = 32 * WM * WMW, NG = NW * WN;
     static constexpr int A_B = BM * 64;                    // codes
     static constexpr int BS_OFF = A_B, DA_OFF = A_B + BM * 32;
-    static constexpr int W_OFF = A_B + BM * 36;            // NG x codes, NG x 512 B headers, NG x 128 B d words
+    static constexpr int DA_B = (BM < 64 ? 64 : BM) * 4;   // one 4-B LDS-DMA instruction covers 64 rows
+    static constexpr int W_OFF = A_B + BM * 32 + DA_B;     // NG x codes, NG x 512 B headers, NG x 128 B d words
     static constexpr int WH_OFF = W_OFF + NG * F::QB;
     static constexpr int WD_OFF = WH_OFF + NG * 512;
     static constexpr int STAGE = (WD_OFF + (F::HB > 512 ? NG * 128 : 0) + 15) & ~15;
@@ -224,7 +225,7 @@ qmm8_kernel(const int8_t* __restrict__ A, int lda, const float* __restrict__ AD,
                 __builtin_amdgcn_global_load_lds((const void*)(AS + (size_t)r * nk16 + sbk * 16 + (lane & 1) * 8),
                                                  (MX_LDS void*)(sb + G::BS_OFF + j * 1024), 16, 0, 0);
             }
-            for (int j = wave; j < BM / 64; j += NT) {
+            for (int j = wave; j < (BM + 63) / 64; j += NT) {
                 const int r = min(m_base + j * 64 + lane, M - 1);
                 __builtin_amdgcn_global_load_lds((const void*)(AD + (size_t)r * nsb + sbk),
                                                  (MX_LDS void*)(sb + G::DA_OFF + j * 256), 4, 0, 0);

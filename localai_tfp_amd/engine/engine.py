@@ -14,6 +14,7 @@ receives `StepOutput`s (the reference's task/result queues, utils.hpp:192-409).
 from __future__ import annotations
 
 import collections
+import os
 import logging
 import queue
 import threading
@@ -370,8 +371,12 @@ class LLMEngine:
             model.enable_prefill_bf16_cache()
         # overlap mode state: the launched-but-unread step, the device tokens it samples, and pinned
         # host staging (ring of 3: a buffer is rewritten only after the step that used it was read)
-        self.overlap = bool(c.overlap and tp is None and not use_spec and not self.recurrent
-                            and getattr(model, "remote", None) is None)
+        # tensor parallel: the leader ships each plan before launching it and broadcasts the sampled
+        # tokens on the device (RCCL), so followers gather decode inputs exactly like the leader
+        self.overlap = bool(c.overlap and not use_spec and not self.recurrent
+                            and getattr(model, "remote", None) is None
+                            and os.environ.get("MX_TP_OVERLAP", "1") != "0" if tp is not None else
+                            c.overlap and not use_spec and not self.recurrent and getattr(model, "remote", None) is None)
         self._inflight = collections.deque()  # launched-but-unread steps, oldest first
         self._prev_dev = None  # (device int32 tokens of the last launched step, {rid: row})
         self._pin_tok = self._pin_lp = self._pin_in = None
@@ -592,6 +597,9 @@ class LLMEngine:
             roctx.pop()
         self.stats["plan_s"] += time.perf_counter() - t1
         items = list(so.decode) + [it for it in so.prefill if it.sample]
+        if self.tp is not None:
+            plan["ns"] = len(items)
+            self.tp.send_plan(plan)
         if roctx.ENABLED:
             roctx.push("launch graph" if plan["graph"] else "launch eager")
         logits, am = self._execute(plan)
@@ -607,6 +615,8 @@ class LLMEngine:
             else:
                 tok_dev, lp_dev = self.sampler.sample(logits, [it.seq.params for it in items], [[] for _ in items],
                                                       [it.seq.n_generated for it in items], None, None)
+            if self.tp is not None:
+                tok_dev = self._tp_bcast_tokens(tok_dev, len(items))
             k = self._pin_i
             self._pin_i = (k + 1) % self.pin_ring
             S = len(items)
@@ -661,6 +671,7 @@ class LLMEngine:
             else:
                 ev.synchronize()
         self.stats["wait_s"] += time.perf_counter() - t0
+        self._check_collectives()
         S = len(items)
         toks = self._pin_tok[k][:S].tolist()
         lps = self._pin_lp[k][:S].tolist() if has_lp else None
@@ -955,7 +966,24 @@ class LLMEngine:
                 self.precapture_graphs()
                 continue
             self._execute(msg)
+            ns = int(msg.get("ns", 0))
+            if ns:  # overlap mode: the leader's sampled tokens, for the next plan's device-side fix-up
+                self._prev_dev = (self._tp_bcast_tokens(None, ns), None)
             self._check_collectives(every=64)
+
+    def _tp_bcast_tokens(self, tok_dev, n: int):
+        """Leader: broadcast its n sampled token ids (device int32) to the TP group on the compute stream;
+        follower: receive them into a persistent device buffer (stream order makes one buffer enough: the
+        next plan's fix-up reads it before the next broadcast rewrites it)."""
+        import torch.distributed as dist
+        buf = getattr(self, "_tp_tok", None)
+        if buf is None or buf.numel() < n:
+            buf = self._tp_tok = torch.zeros(max(n, self.cfg.max_num_seqs), dtype=torch.int32, device=self.device)
+        v = buf[:n]
+        if tok_dev is not None:
+            v.copy_(tok_dev[:n].to(torch.int32))
+        dist.broadcast(v, src=self.tp.src, group=self.tp.gpu_group)
+        return v
 
     def _sample(self, logits, items):
         params = [it.seq.params for it in items]

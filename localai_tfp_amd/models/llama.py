@@ -662,6 +662,10 @@ class LlamaModel:
                 mm(W, None, EPI_BF16, y16, xq=xq, xds=xds)
             else:
                 mm(W, x, EPI_BF16, y16)
+            ar = getattr(self, "custom_ar", None)
+            if post_norm is None and ar is not None and h.is_contiguous():
+                ar.add_into(y16, h)  # all-reduce + residual add in one kernel
+                return
             self._allreduce(y16)
             if post_norm is None:
                 h.add_(y16)

@@ -28,6 +28,8 @@ _SIGS = {
     "mxk_ar_handle_size": [],
     "mxk_allreduce_1shot": [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_void_p), C.c_long,
                             C.c_void_p, C.c_void_p, C.c_void_p],
+    "mxk_allreduce_1shot_add": [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_void_p), C.c_long,
+                                C.c_void_p, C.c_void_p, C.c_void_p],
 }
 
 
@@ -102,6 +104,23 @@ class OneShotAllReduce:
                                          self.slot, self.epoch.data_ptr(), self.err.data_ptr(),
                                          N.stream_ptr(self.device)), "mxk_allreduce_1shot")
         return out
+
+    def fits(self, t: torch.Tensor) -> bool:
+        return (t.dtype in (torch.float16, torch.bfloat16) and t.numel() * 2 <= self.max_bytes and t.numel() % 2 == 0
+                and t.is_contiguous())
+
+    def add_into(self, t: torch.Tensor, res: torch.Tensor):
+        """res (fp32, same shape) += all-reduce(t) in one kernel (the row-parallel projection's all-reduce
+        fused with the residual add); falls back to RCCL + add for large or unsupported tensors."""
+        if not self.fits(t) or res.dtype != torch.float32 or not res.is_contiguous() or res.numel() != t.numel():
+            self(t)
+            res.add_(t)
+            return res
+        N.ensure_act(t.dtype)
+        _ok(self.lib.mxk_allreduce_1shot_add(t.data_ptr(), res.data_ptr(), t.numel(), self.rank, self.world, self.ptrs,
+                                             self.slot, self.epoch.data_ptr(), self.err.data_ptr(),
+                                             N.stream_ptr(self.device)), "mxk_allreduce_1shot_add")
+        return res
 
     def check(self):
         if int(self.err.item()):

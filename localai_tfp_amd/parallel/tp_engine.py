@@ -44,11 +44,11 @@ STOP = None
 
 # ------------------------------------------------------------------ plan codec (int32, no pickles)
 def encode_plan(plan: dict) -> np.ndarray:
-    """Flat int32 image of a step plan: [nd, flags, graph bucket (B, P, PS), then per PLAN_ARRAYS
-    entry: ndim, *shape, *data]."""
+    """Flat int32 image of a step plan: [nd, flags, graph bucket (B, P, PS), ns (rows the leader samples and
+    broadcasts on the device: overlap mode), then per PLAN_ARRAYS entry: ndim, *shape, *data]."""
     g = plan.get("graph")
     flags = int(bool(g)) | (int(bool(plan.get("keep_hidden"))) << 1)
-    parts = [np.array([plan["nd"], flags, *(tuple(g) if g else (0, 0, 0))], np.int32)]
+    parts = [np.array([plan["nd"], flags, *(tuple(g) if g else (0, 0, 0)), int(plan.get("ns", 0))], np.int32)]
     arrays = dict(plan)
     if "fix" in plan:
         arrays["fix_dst"], arrays["fix_src"] = plan["fix"]
@@ -66,8 +66,8 @@ def encode_plan(plan: dict) -> np.ndarray:
 def decode_plan(buf: np.ndarray) -> dict:
     nd, flags = int(buf[0]), int(buf[1])
     plan = {"nd": nd, "graph": tuple(int(x) for x in buf[2:5]) if flags & 1 else False,
-            "keep_hidden": bool(flags & 2)}
-    i = 5
+            "keep_hidden": bool(flags & 2), "ns": int(buf[5])}
+    i = 6
     for k in PLAN_ARRAYS:
         ndim = int(buf[i])
         i += 1
@@ -91,7 +91,7 @@ class TPLink:
     matched against a follower's all-reduce."""
 
     def __init__(self, rank: int, world: int, cpu_group, gpu_group=None, src: int = 0, heartbeat_s: float | None = None,
-                 sync_group=None):
+                 sync_group=None, shm: bool | None = None):
         self.rank, self.world = rank, world
         self.cpu_group, self.gpu_group = cpu_group, gpu_group
         self.sync_group = sync_group if sync_group is not None else cpu_group
@@ -104,10 +104,32 @@ class TPLink:
         self._last_send = time.monotonic()
         self._hb = None
         hb = float(os.environ.get("MX_TP_HEARTBEAT_S", "5")) if heartbeat_s is None else heartbeat_s
-        if self.is_leader and world > 1 and hb > 0:
+        self.shm = None
+        if shm is None:
+            shm = os.environ.get("MX_TP_SHM", "1") != "0"
+        if shm and world > 1:
+            self.shm = self._open_shm(max(hb, 0.5))
+        if self.is_leader and world > 1 and hb > 0 and self.shm is None:
             self._hb_stop = threading.Event()
             self._hb = threading.Thread(target=self._heartbeat, args=(hb,), daemon=True, name="tp-heartbeat")
             self._hb.start()
+
+    def _open_shm(self, heartbeat: float):
+        """Plans over a /dev/shm ring (parallel/shm_channel.py): all ranks of a group are on one node. The
+        leader draws a random name and broadcasts it (16 raw bytes over the gloo group, no pickles)."""
+        import torch.distributed as dist
+        from .shm_channel import ChannelDead, ShmChannel, channel_name
+        tok = torch.from_numpy(np.frombuffer(os.urandom(16), np.uint8).copy()) if self.is_leader else \
+            torch.empty(16, dtype=torch.uint8)
+        dist.broadcast(tok, src=self.src, group=self.cpu_group)
+        name = channel_name(bytes(tok.numpy()).hex()[:20])
+        to = tp_timeout().total_seconds()
+        try:
+            ch = ShmChannel(name, self.rank, self.world, create=self.is_leader, timeout=to, heartbeat=heartbeat)
+        except (ChannelDead, OSError) as ex:
+            self._fail("shared-memory channel setup", ex)
+        dist.barrier(group=self.cpu_group)  # every follower attached before the leader may publish
+        return ch
 
     # -------------------------------------------------------------- failure handling
     def _fail(self, what: str, ex: BaseException):
@@ -140,10 +162,28 @@ class TPLink:
     def close(self):
         if self._hb is not None:
             self._hb_stop.set()
+        if self.shm is not None:
+            self.shm.close()
 
     # -------------------------------------------------------------- raw channel
     def _send(self, kind: int, body: np.ndarray | None = None, obj=None):
         import torch.distributed as dist
+        if self.shm is not None:
+            from .shm_channel import ChannelDead
+            with self._lock:
+                try:
+                    b = None if body is None else np.ascontiguousarray(body, np.int32)
+                    if b is not None and b.nbytes > self.shm.max_body():
+                        self.shm.send(K_PICKLE)  # oversized plan: object over gloo
+                        dist.broadcast_object_list([decode_plan(b)], src=self.src, group=self.cpu_group)
+                    else:
+                        self.shm.send(kind, b)
+                        if kind == K_PICKLE:
+                            dist.broadcast_object_list([obj], src=self.src, group=self.cpu_group)
+                    self._last_send = time.monotonic()
+                except (ChannelDead, RuntimeError) as ex:
+                    self._fail("send", ex)
+            return
         with self._lock:
             try:
                 self._seq += 1
@@ -161,6 +201,24 @@ class TPLink:
 
     def _recv(self):
         import torch.distributed as dist
+        if self.shm is not None:
+            from .shm_channel import ChannelDead
+            try:
+                kind, raw = self.shm.recv()
+                body = np.frombuffer(raw, np.int32).copy() if raw else None
+                obj = None
+                if kind == K_PICKLE:
+                    buf = [None]
+                    dist.broadcast_object_list(buf, src=self.src, group=self.cpu_group)
+                    obj = buf[0]
+                    if isinstance(obj, dict):
+                        kind = K_PLAN
+                        body = encode_plan(obj) if "mm" not in obj else None
+                        if body is None:
+                            kind = K_PICKLE
+                return kind, body, obj
+            except (ChannelDead, RuntimeError) as ex:
+                self._fail("receive", ex)
         while True:
             try:
                 hdr = torch.empty(4, dtype=torch.int32)

@@ -31,6 +31,17 @@ def main():
         tol = 1e-2 if dt == torch.float16 else 6e-2
         ok &= err < tol * max(1.0, ref.abs().max().item())
         print(f"rank {rank} n={n} {dt} err={err:.3g}", flush=True)
+    # fused all-reduce + fp32 residual add (row-parallel projection epilogue)
+    for n in (4096, 8192 * 4):
+        parts = [torch.randn(n, generator=torch.Generator().manual_seed(77 + r)) for r in range(world)]
+        ref = sum(p.half().float() for p in parts) + 1.5
+        res = torch.full((n,), 1.5, device=dev)
+        ar.add_into(parts[rank].to(dev, torch.float16), res)
+        torch.cuda.synchronize()
+        ar.check()
+        err = (res.cpu() - ref).abs().max().item()
+        ok &= err < 1e-2 * max(1.0, ref.abs().max().item())
+        print(f"rank {rank} add_into n={n} err={err:.3g}", flush=True)
     # hipGraph capture + replays (epoch counter lives on the device)
     t = torch.zeros(8192, device=dev, dtype=torch.float16)
     s = torch.cuda.Stream(dev)

@@ -20,6 +20,9 @@ PROMPTS = [list(b"tensor parallel test prompt one"), list(b"another, somewhat lo
 
 def _cfg(kind):
     from localai_tfp_amd.models.config import tiny_config
+    if kind == "wide":  # TP 4 / 8 with whole 256-wide super-blocks per shard: hidden 2048, ffn 2048, 8 kv heads
+        return tiny_config(n_layers=2, hidden=2048, ffn=2048, n_heads=16, n_kv_heads=8, head_dim=128, rope_dim=128,
+                           vocab=1024)
     # row-parallel shards must be whole 256-element Q4_K/Q6_K super-blocks: hidden 512 / tp 2
     if kind == "moe":  # expert parallel: 8 experts, 4 per rank, top-2 routing + renorm
         return tiny_config(arch="qwen3moe", n_layers=2, hidden=512, ffn=1024, n_heads=8, n_kv_heads=2, head_dim=64,
@@ -72,8 +75,10 @@ def _worker(rank, world, port, q, kind="dense"):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("kind", ["dense", "moe"])
-def test_tp2_matches_single_process(kind):
+@pytest.mark.parametrize("kind,world", [("dense", 2), ("moe", 2), ("wide", 4), ("wide", 8)])
+def test_tp_matches_single_process(kind, world):
+    """Greedy output of a TP group (leader + followers replaying plans over the /dev/shm ring, sampled
+    tokens broadcast each overlap-mode step) equals the single-process engine."""
     eng = _build(0, 1, None, kind)
     from localai_tfp_amd.engine.sequence import Request
     from localai_tfp_amd.ops.sampling import SamplingParams
@@ -88,7 +93,7 @@ def test_tp2_matches_single_process(kind):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    ps = [ctx.Process(target=_worker, args=(r, 2, port, q, kind)) for r in range(2)]
+    ps = [ctx.Process(target=_worker, args=(r, world, port, q, kind)) for r in range(world)]
     for p in ps:
         p.start()
     import queue as _q
