@@ -43,6 +43,10 @@ struct Q8W<MXQ_Q4_K> {
     static constexpr int UNIT = 4608, HB = 512, QOFF = 512, QB = 1024;  // hdr: 32 x {f16 d, f16 dmin, 12 B scales}
 };
 template <>
+struct Q8W<MXQ_Q5_K> {  // Q4_K + qh (2 chunks x 32 cols x 16 B after the codes: bit 2jq+s of byte b = 5th bit)
+    static constexpr int UNIT = 5632, HB = 512, QOFF = 512, QB = 1024;
+};
+template <>
 struct Q8W<MXQ_Q6_K> {
     static constexpr int UNIT = 6784, HB = 640, QOFF = 640, QB = 1536;  // hdr: 32 x 16 int8 scales, 32 x 4 B f16 d
 };
@@ -58,7 +62,8 @@ struct Q8Geom {
     static constexpr int W_OFF = A_B + BM * 32 + DA_B;     // NG x codes, NG x 512 B headers, NG x 128 B d words
     static constexpr int WH_OFF = W_OFF + NG * F::QB;
     static constexpr int WD_OFF = WH_OFF + NG * 512;
-    static constexpr int STAGE = (WD_OFF + (F::HB > 512 ? NG * 128 : 0) + 15) & ~15;
+    static constexpr int QH_OFF = WD_OFF + (F::HB > 512 ? NG * 128 : 0);  // Q5_K high bits: NG x 1 KB
+    static constexpr int STAGE = (QH_OFF + (QT == MXQ_Q5_K ? NG * 1024 : 0) + 15) & ~15;
     static constexpr int AI = BM / 16;                      // A-code wave-instructions per stage
     static constexpr int WA = (AI + NT - 1) / NT;           // per wave (the last ones may issue one less)
     static constexpr int WA0 = AI / NT;
@@ -107,6 +112,10 @@ struct Q8Hdr<MXQ_Q4_K> {
     MX_DEV int sc(int sb) const {  // sub-block scale (0..7)
         return (int)(((sb < 4 ? sc0 : sc1) >> (8 * (sb & 3))) & 0xFF);
     }
+};
+template <>
+struct Q8Hdr<MXQ_Q5_K> : Q8Hdr<MXQ_Q4_K> {
+    u32x4 qh;  // this lane's 16 high-bit bytes (chunk h of its column)
 };
 template <>
 struct Q8Hdr<MXQ_Q6_K> {
@@ -217,6 +226,16 @@ qmm8_kernel(const int8_t* __restrict__ A, int lda, const float* __restrict__ AD,
                     __builtin_amdgcn_global_load_lds((const void*)(dsrc + unit),
                                                      (MX_LDS void*)(sb + G::WD_OFF + cg * WN * 128), 4, 0, 0);
             }
+            if constexpr (QT == MXQ_Q5_K) {
+                if (jq == 0) {
+#pragma unroll
+                    for (int t = 0; t < WN; ++t) {
+                        const int g = min(g_wave + t, ngrp - 1);
+                        __builtin_amdgcn_global_load_lds((const void*)(W + (size_t)g * gstride + unit + 4608 + lane * 16),
+                                                         (MX_LDS void*)(sb + G::QH_OFF + (cg * WN + t) * 1024), 16, 0, 0);
+                    }
+                }
+            }
         }
         if constexpr (jq == 3) {
             const int sbk = kt >> 2;
@@ -254,18 +273,25 @@ qmm8_kernel(const int8_t* __restrict__ A, int lda, const float* __restrict__ AD,
         const char* wq = sb + G::W_OFF + cg * WN * F::QB;
         if constexpr (JQ == 0) {
 #pragma unroll
-            for (int t = 0; t < WN; ++t)
+            for (int t = 0; t < WN; ++t) {
                 hd[t].load(sb + G::WH_OFF + (cg * WN + t) * 512, sb + G::WD_OFF + (cg * WN + t) * 128, col, h);
+                if constexpr (QT == MXQ_Q5_K) hd[t].qh = *(const u32x4*)(sb + G::QH_OFF + (cg * WN + t) * 1024 + (h * 32 + col) * 16);
+            }
         }
-        if constexpr (QT == MXQ_Q4_K) {
+        if constexpr (QT == MXQ_Q4_K || QT == MXQ_Q5_K) {
             i32x4 bf[WN][2];
 #pragma unroll
             for (int t = 0; t < WN; ++t) {
                 const u32x4 raw = *(const u32x4*)(wq + t * F::QB + (h * 32 + col) * 16);
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
-                    bf[t][0][e] = (int32_t)(raw[e] & 0x0F0F0F0Fu);
-                    bf[t][1][e] = (int32_t)((raw[e] >> 4) & 0x0F0F0F0Fu);
+                    uint32_t lo = raw[e] & 0x0F0F0F0Fu, hi = (raw[e] >> 4) & 0x0F0F0F0Fu;
+                    if constexpr (QT == MXQ_Q5_K) {
+                        lo |= ((hd[t].qh[e] >> (2 * JQ)) & 0x01010101u) << 4;
+                        hi |= ((hd[t].qh[e] >> (2 * JQ + 1)) & 0x01010101u) << 4;
+                    }
+                    bf[t][0][e] = (int32_t)lo;
+                    bf[t][1][e] = (int32_t)hi;
                 }
             }
             i32x4 af[2][WM];
@@ -365,7 +391,7 @@ qmm8_kernel(const int8_t* __restrict__ A, int lda, const float* __restrict__ AD,
 #pragma unroll
                     for (int r = 0; r < 16; ++r) {
                         const float da = dav[r >> 2][r & 3];
-                        if constexpr (QT == MXQ_Q4_K) {
+                        if constexpr (QT == MXQ_Q4_K || QT == MXQ_Q5_K) {
                             const float v = fmaf((float)J[i][t][r], hd[t].d, -hd[t].dmin * Mi[r]);
                             acc[i][t][r] = fmaf(v, da, acc[i][t][r]);
                         } else {
@@ -521,6 +547,7 @@ extern "C" int mxk_qmm8(int qtype, int epi, int wm, int wn, int nw, int wmw, int
     }
     switch (qtype) {
         case MXQ_Q4_K: Q8_EPI(MXQ_Q4_K) break;
+        case MXQ_Q5_K: Q8_EPI(MXQ_Q5_K) break;
         case MXQ_Q6_K: Q8_EPI(MXQ_Q6_K) break;
     }
 #undef Q8_EPI

@@ -51,6 +51,44 @@ struct TUnit<MXQ_Q4_K> {
     }
 };
 
+// Q5_K: the Q4_K unit plus one high bit per code: qh (32 B per column, bit 2jq / 2jq+1 of byte b = code b of
+// quarter jq's low / high half), stored after the codes as 2 chunks x 32 columns x 16 B.
+template <>
+struct TUnit<MXQ_Q5_K> {
+    static constexpr int BYTES = 5632, ELEMS = 256;
+    u32x4 hd, q[4], qh;
+    MX_DEV void load(const uint8_t* u, int r, int h) {
+        hd = *(const u32x4*)(u + r * 16);
+#pragma unroll
+        for (int jq = 0; jq < 4; ++jq) q[jq] = __builtin_nontemporal_load((const u32x4*)(u + 512 + jq * 1024 + h * 512 + r * 16));
+        qh = __builtin_nontemporal_load((const u32x4*)(u + 4608 + h * 512 + r * 16));
+    }
+    MX_DEV float dot(const int8_t* x, const float2* ds, int h) const {
+        const float d = half_to_f32(hd[0] & 0xFFFF), dm = half_to_f32(hd[0] >> 16);
+        float acc = 0.f, mins = 0.f;
+#pragma unroll
+        for (int jq = 0; jq < 4; ++jq) {
+            const u32x4 xl = *(const u32x4*)(x + 64 * jq + 16 * h);
+            const u32x4 xh = *(const u32x4*)(x + 64 * jq + 32 + 16 * h);
+            int il = 0, ih = 0;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const uint32_t lo = (q[jq][i] & 0x0F0F0F0Fu) | (((qh[i] >> (2 * jq)) & 0x01010101u) << 4);
+                const uint32_t hi = ((q[jq][i] >> 4) & 0x0F0F0F0Fu) | (((qh[i] >> (2 * jq + 1)) & 0x01010101u) << 4);
+                il = __builtin_amdgcn_sdot4((int)lo, (int)xl[i], il, false);
+                ih = __builtin_amdgcn_sdot4((int)hi, (int)xh[i], ih, false);
+            }
+            int sc0, m0, sc1, m1;
+            q4k_scale_min_w(hd[1], hd[2], hd[3], 2 * jq, sc0, m0);
+            q4k_scale_min_w(hd[1], hd[2], hd[3], 2 * jq + 1, sc1, m1);
+            const float2 dl = ds[2 * jq], dh = ds[2 * jq + 1];
+            acc += (float)sc0 * dl.x * (float)il + (float)sc1 * dh.x * (float)ih;
+            mins += (float)m0 * dl.y + (float)m1 * dh.y;
+        }
+        return d * acc - (h == 0 ? dm * mins : 0.f);
+    }
+};
+
 template <>
 struct TUnit<MXQ_Q6_K> {
     static constexpr int BYTES = 6784, ELEMS = 256;
@@ -274,8 +312,9 @@ __global__ __launch_bounds__(256) void dequant_t32_kernel(const uint8_t* __restr
         const uint32_t qq = *(const uint32_t*)(base + 128 + (u >> 4) * 512 + r * 16 + (u & 15));
 #pragma unroll
         for (int i = 0; i < 4; ++i) v[i] = d * (float)(int8_t)((qq >> (8 * i)) & 0xFF);
-    } else if constexpr (QT == MXQ_Q4_K) {
-        const uint8_t* base = W + ((size_t)g * (K / 256) + chunk) * 4608;
+    } else if constexpr (QT == MXQ_Q4_K || QT == MXQ_Q5_K) {
+        constexpr int UB = QT == MXQ_Q4_K ? 4608 : 5632;
+        const uint8_t* base = W + ((size_t)g * (K / 256) + chunk) * UB;
         const u32x4 hd = *(const u32x4*)(base + r * 16);
         const int jq = e >> 6, u = e & 63, b = u & 31;
         const uint32_t qq = *(const uint32_t*)(base + 512 + jq * 1024 + (b >> 4) * 512 + r * 16 + (b & 15));
@@ -283,8 +322,14 @@ __global__ __launch_bounds__(256) void dequant_t32_kernel(const uint8_t* __restr
         q4k_scale_min_w(hd[1], hd[2], hd[3], 2 * jq + (u >> 5), sc, mn);
         const float d = half_to_f32(hd[0] & 0xFFFF) * (float)sc, m = half_to_f32(hd[0] >> 16) * (float)mn;
         const int sh = (u >> 5) * 4;
+        uint32_t hb = 0;
+        if constexpr (QT == MXQ_Q5_K) hb = *(const uint32_t*)(base + 4608 + (b >> 4) * 512 + r * 16 + (b & 15));
 #pragma unroll
-        for (int i = 0; i < 4; ++i) v[i] = d * (float)((qq >> (8 * i + sh)) & 0xF) - m;
+        for (int i = 0; i < 4; ++i) {
+            int qv = (int)((qq >> (8 * i + sh)) & 0xF);
+            if constexpr (QT == MXQ_Q5_K) qv |= (int)(((hb >> (8 * i + 2 * jq + (u >> 5))) & 1) << 4);
+            v[i] = d * (float)qv - m;
+        }
     } else {
         const uint8_t* base = W + ((size_t)g * (K / 256) + chunk) * 6784;
         const int jq = e >> 6, u = e & 63, b = u & 31, s16 = u >> 4;
@@ -354,6 +399,7 @@ extern "C" int mxk_qmv(int qtype, int epi, const int8_t* xq, const float2* xds, 
     }
     switch (qtype) {
         case MXQ_Q4_K: QMV_EPI(MXQ_Q4_K) break;
+        case MXQ_Q5_K: QMV_EPI(MXQ_Q5_K) break;
         case MXQ_Q6_K: QMV_EPI(MXQ_Q6_K) break;
         case MXQ_Q8_0: QMV_EPI(MXQ_Q8_0) break;
     }
@@ -384,6 +430,7 @@ extern "C" int mxk_qmv_x(int qtype, int epi, int src, const void* x, int ldx, co
     }
     switch (qtype) {
         case MXQ_Q4_K: QMVX_EPI(MXQ_Q4_K) break;
+        case MXQ_Q5_K: QMVX_EPI(MXQ_Q5_K) break;
         case MXQ_Q6_K: QMVX_EPI(MXQ_Q6_K) break;
         case MXQ_Q8_0: QMVX_EPI(MXQ_Q8_0) break;
     }
@@ -401,6 +448,7 @@ extern "C" int mxk_dequant_t32(int qtype, const uint8_t* W, const int* rows, int
     MX_ACT_DISPATCH({
         switch (qtype) {
             case MXQ_Q4_K: dequant_t32_kernel<MXQ_Q4_K, F16><<<grid, 256, 0, st>>>(W, rows, K, ob, of, ldo); break;
+            case MXQ_Q5_K: dequant_t32_kernel<MXQ_Q5_K, F16><<<grid, 256, 0, st>>>(W, rows, K, ob, of, ldo); break;
             case MXQ_Q6_K: dequant_t32_kernel<MXQ_Q6_K, F16><<<grid, 256, 0, st>>>(W, rows, K, ob, of, ldo); break;
             case MXQ_Q8_0: dequant_t32_kernel<MXQ_Q8_0, F16><<<grid, 256, 0, st>>>(W, rows, K, ob, of, ldo); break;
             default: rc = (int)hipErrorInvalidValue;

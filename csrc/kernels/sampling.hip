@@ -61,20 +61,9 @@ MX_DEV float bmax(float v, float* red) {
     return t;
 }
 
-__global__ __launch_bounds__(SNT) void sample_kernel(float* __restrict__ logits, int ld, int V,
-                                                     const SampleParams* __restrict__ params,
-                                                     const int* __restrict__ pen_tok,
-                                                     const int* __restrict__ pen_cnt,
-                                                     const float* __restrict__ pen_bias,
-                                                     const uint32_t* __restrict__ allow_mask, int mask_ld,
-                                                     int* __restrict__ out_tok, float* __restrict__ out_logp) {
-    __shared__ float red[SNT / 64];
-    __shared__ float rv[SNT / 64];
-    __shared__ int ri[SNT / 64];
-    const int row = blockIdx.x;
-    const SampleParams P = params[row];
-    float* x = logits + (size_t)row * ld;
-    // 1. sparse penalties + logit bias (unique tokens per row -> no write conflicts)
+// sparse penalties + logit bias, in place (unique tokens per row -> no write conflicts)
+MX_DEV void apply_penalties(float* x, int V, const SampleParams& P, const int* pen_tok, const int* pen_cnt,
+                            const float* pen_bias) {
     for (int i = threadIdx.x; i < P.pen_count; i += SNT) {
         const int t = pen_tok[P.pen_offset + i];
         if (t < 0 || t >= V) continue;
@@ -88,9 +77,15 @@ __global__ __launch_bounds__(SNT) void sample_kernel(float* __restrict__ logits,
         x[t] = v;
     }
     __syncthreads();
+}
+
+// General chain by bisection on the value axis (every pass streams the whole row): typical-p, mirostat,
+// and the rare rows whose truncation keeps more candidates than the fast path's LDS holds.
+MX_DEV void sample_row_bisect(float* __restrict__ x, int V, const SampleParams& P, const uint32_t* am,
+                              int row, int* __restrict__ out_tok, float* __restrict__ out_logp, float* red, float* rv,
+                              int* ri) {
     const bool greedy = P.temperature <= 0.f;
     const float itemp = greedy ? 1.f : 1.f / P.temperature;
-    const uint32_t* am = allow_mask ? allow_mask + (size_t)row * mask_ld : nullptr;
     auto val = [&](int i) -> float {
         float v = x[i];
         if (am && !((am[i >> 5] >> (i & 31)) & 1u)) return -INFINITY;
@@ -210,6 +205,191 @@ __global__ __launch_bounds__(SNT) void sample_kernel(float* __restrict__ logits,
         }
         Z = bsum(Z, red);
         if (threadIdx.x == 0) out_logp[row] = val(id) - mx - __logf(fmaxf(Z, 1e-30f));
+    }
+}
+
+// ---- fast path: histogram -> candidate set in LDS -> exact truncation on the candidates ----------------
+// Streams the row three times (max, histogram of the distance to the max with per-bin exp mass, candidate
+// gather) instead of the ~60 passes of the bisection chain: at 128 rows x 128k vocabulary that is ~40 us
+// instead of ~2.5 ms per step. The histogram picks the lowest bin that must be kept (top-k by count,
+// top-p by mass, min-p by value); every token at or above it is gathered (value, id) into LDS, sorted
+// (bitonic, descending), truncated exactly, and drawn by the same Gumbel-max as the bisection path, so
+// both paths pick the same token for the same kept set.
+constexpr int SHB = 2048;           // histogram bins over d = max - v in [0, SHR)
+constexpr float SHR = 48.f;         // exp(-48) ~ 1e-21: mass beyond is negligible
+constexpr int SCAP = 4096;          // candidate capacity (power of two for the bitonic sort)
+
+__global__ __launch_bounds__(SNT) void sample_kernel(float* __restrict__ logits, int ld, int V,
+                                                     const SampleParams* __restrict__ params,
+                                                     const int* __restrict__ pen_tok,
+                                                     const int* __restrict__ pen_cnt,
+                                                     const float* __restrict__ pen_bias,
+                                                     const uint32_t* __restrict__ allow_mask, int mask_ld,
+                                                     int* __restrict__ out_tok, float* __restrict__ out_logp) {
+    __shared__ float red[SNT / 64];
+    __shared__ float rv[SNT / 64];
+    __shared__ int ri[SNT / 64];
+    __shared__ unsigned hcnt[SHB];
+    __shared__ float hmass[SHB];
+    __shared__ float cv[SCAP];
+    __shared__ int ci[SCAP];
+    __shared__ int s_n, s_bin;
+    const int row = blockIdx.x;
+    const SampleParams P = params[row];
+    float* x = logits + (size_t)row * ld;
+    const uint32_t* am = allow_mask ? allow_mask + (size_t)row * mask_ld : nullptr;
+    apply_penalties(x, V, P, pen_tok, pen_cnt, pen_bias);
+    const bool greedy = P.temperature <= 0.f;
+    const bool fast_ok = !greedy && !(P.typical_p < 1.f && P.typical_p > 0.f) && !(P.mirostat_tau > 0.f) &&
+                         ((P.top_k > 0 && P.top_k <= SCAP) || (P.top_p < 1.f && P.top_p > 0.f) || P.min_p > 0.f);
+    if (!fast_ok) {
+        sample_row_bisect(x, V, P, am, row, out_tok, out_logp, red, rv, ri);
+        return;
+    }
+    const float itemp = 1.f / P.temperature;
+    auto val = [&](int i, float v) -> float {
+        if (am && !((am[i >> 5] >> (i & 31)) & 1u)) return -INFINITY;
+        return v * itemp;
+    };
+    const bool vec = ((((uintptr_t)x) & 15) == 0);
+    const int V4 = vec ? (V & ~3) : 0;
+    // pass 1: max
+    float mx = -INFINITY;
+    for (int i = threadIdx.x * 4; i < V4; i += SNT * 4) {
+        const float4 a = *(const float4*)(x + i);
+        mx = fmaxf(fmaxf(fmaxf(mx, val(i, a.x)), val(i + 1, a.y)), fmaxf(val(i + 2, a.z), val(i + 3, a.w)));
+    }
+    for (int i = V4 + threadIdx.x; i < V; i += SNT) mx = fmaxf(mx, val(i, x[i]));
+    mx = bmax(mx, red);
+    for (int b = threadIdx.x; b < SHB; b += SNT) { hcnt[b] = 0u; hmass[b] = 0.f; }
+    __syncthreads();
+    // pass 2: histogram of d = mx - v (count and exp mass per bin); Z over the whole row
+    constexpr float BW = SHR / (float)SHB, IBW = (float)SHB / SHR;
+    float Zt = 0.f;
+    auto hist = [&](float v) {
+        if (v == -INFINITY) return;
+        const float e = __expf(v - mx);
+        Zt += e;
+        const int b = min(SHB - 1, (int)((mx - v) * IBW));
+        atomicAdd(&hcnt[b], 1u);
+        atomicAdd(&hmass[b], e);
+    };
+    for (int i = threadIdx.x * 4; i < V4; i += SNT * 4) {
+        const float4 a = *(const float4*)(x + i);
+        hist(val(i, a.x)); hist(val(i + 1, a.y)); hist(val(i + 2, a.z)); hist(val(i + 3, a.w));
+    }
+    for (int i = V4 + threadIdx.x; i < V; i += SNT) hist(val(i, x[i]));
+    const float Z = bsum(Zt, red);
+    // lowest bin that must be kept: the first (from the top) where top-k's count or top-p's mass is reached;
+    // min-p caps it from above
+    if (threadIdx.x == 0) {
+        int lim = SHB - 1;
+        if (P.min_p > 0.f && P.min_p <= 1.f) lim = min(lim, (int)(-__logf(P.min_p) * IBW));
+        unsigned c = 0;
+        float m = 0.f;
+        int b = 0;
+        for (; b < lim; ++b) {
+            c += hcnt[b];
+            m += hmass[b];
+            if (P.top_k > 0 && c >= (unsigned)P.top_k) break;
+            if (P.top_p < 1.f && P.top_p > 0.f && m >= P.top_p * Z) break;
+        }
+        s_bin = b;
+        s_n = 0;
+    }
+    __syncthreads();
+    const float cut = mx - ((float)s_bin + 1.01f) * BW;  // gather every v > cut (a superset of the kept set)
+    // pass 3: gather candidates
+    auto gather = [&](int i, float v) {
+        if (v == -INFINITY || !(v > cut || v == mx)) return;
+        const int k = atomicAdd(&s_n, 1);
+        if (k < SCAP) { cv[k] = v; ci[k] = i; }
+    };
+    for (int i = threadIdx.x * 4; i < V4; i += SNT * 4) {
+        const float4 a = *(const float4*)(x + i);
+        gather(i, val(i, a.x)); gather(i + 1, val(i + 1, a.y)); gather(i + 2, val(i + 2, a.z)); gather(i + 3, val(i + 3, a.w));
+    }
+    for (int i = V4 + threadIdx.x; i < V; i += SNT) gather(i, val(i, x[i]));
+    __syncthreads();
+    const int n = s_n;
+    if (n > SCAP) {  // a flat distribution: more candidates than LDS holds
+        sample_row_bisect(x, V, P, am, row, out_tok, out_logp, red, rv, ri);
+        return;
+    }
+    // bitonic sort of the candidates, descending by value (ties: ascending id), padded to a power of two
+    int np = 1;
+    while (np < n) np <<= 1;
+    for (int k = n + threadIdx.x; k < np; k += SNT) { cv[k] = -INFINITY; ci[k] = 0x7fffffff; }
+    __syncthreads();
+    for (int size = 2; size <= np; size <<= 1) {
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            for (int t = threadIdx.x; t < np / 2; t += SNT) {
+                const int lo = 2 * t - (t & (stride - 1)), hi = lo + stride;
+                const bool desc = (lo & size) == 0;
+                const float a = cv[lo], bb = cv[hi];
+                const int ia = ci[lo], ib = ci[hi];
+                const bool a_first = a > bb || (a == bb && ia < ib);
+                if (a_first != desc) { cv[lo] = bb; cv[hi] = a; ci[lo] = ib; ci[hi] = ia; }
+            }
+            __syncthreads();
+        }
+    }
+    // exact truncation on the sorted candidates (thread 0: at most SCAP steps), then Gumbel-max draw
+    if (threadIdx.x == 0) {
+        // same semantics as the bisection chain: top-k (ties at the k-th value kept), then top-p's target
+        // mass is top_p x the top-k set's mass, measured over the set that also passes min-p
+        int keep = n;
+        if (P.top_k > 0 && P.top_k < keep) {
+            const float kv = cv[P.top_k - 1];
+            keep = P.top_k;
+            while (keep < n && cv[keep] == kv) ++keep;
+        }
+        float zk = 0.f;
+        if (P.top_p < 1.f && P.top_p > 0.f)
+            for (int k = 0; k < keep; ++k) zk += __expf(cv[k] - mx);
+        if (P.min_p > 0.f && P.min_p <= 1.f) {
+            const float mv = mx + __logf(P.min_p);
+            while (keep > 1 && cv[keep - 1] < mv) --keep;
+        }
+        if (P.top_p < 1.f && P.top_p > 0.f) {
+            float cum = 0.f;
+            int k = 0;
+            while (k < keep) {
+                cum += __expf(cv[k] - mx);
+                ++k;
+                if (cum >= P.top_p * zk) break;
+            }
+            while (k < keep && cv[k] == cv[k - 1]) ++k;  // equal values stay together
+            keep = max(1, k);
+        }
+        s_n = keep;
+    }
+    __syncthreads();
+    const int keep = s_n;
+    float best = -INFINITY, zk = 0.f;
+    int bi = 0x7fffffff;
+    for (int k = threadIdx.x; k < keep; k += SNT) {
+        const float sc = cv[k] + gumbel(P.seed, (uint32_t)ci[k]);
+        zk += __expf(cv[k] - mx);
+        if (sc > best || (sc == best && ci[k] < bi)) { best = sc; bi = ci[k]; }
+    }
+    zk = bsum(zk, red);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const float ob = __shfl_xor(best, o, 64);
+        const int oi = __shfl_xor(bi, o, 64);
+        if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+    }
+    if ((threadIdx.x & 63) == 0) { rv[threadIdx.x >> 6] = best; ri[threadIdx.x >> 6] = bi; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float b = rv[0];
+        int id = ri[0];
+        for (int w = 1; w < SNT / 64; ++w)
+            if (rv[w] > b || (rv[w] == b && ri[w] < id)) { b = rv[w]; id = ri[w]; }
+        if (id == 0x7fffffff) id = 0;
+        out_tok[row] = id;
+        if (out_logp) out_logp[row] = val(id, x[id]) - mx - __logf(fmaxf(zk, 1e-30f));
     }
 }
 

@@ -361,6 +361,18 @@ class LlamaModel:
                     w.to_t32()
         if isinstance(self.lm_head, QWeight):
             self.lm_head.to_t32()  # tied embeddings follow (embed() reads either layout)
+        if isinstance(self.tok_embd, QWeight) and self.tok_embd is not self.lm_head and \
+                int(self.tok_embd.qtype if self.tok_embd.is_quant else -1) == int(QType.Q5_K):
+            self.tok_embd.to_t32()  # Q5_K rows are gathered by the t32 dequant kernel
+        # anything a t32-only format left in the row layout (expert stacks, odd shapes) -> Q8_0 kernels
+        ws = [self.tok_embd, self.lm_head]
+        for L in self.layers:
+            ws += [*L.qkv_parts, L.wo, L.wgu, L.wg, L.wu, L.wd]
+            if L.moe is not None:
+                ws += [getattr(L.moe, a, None) for a in ("gate_up", "down", "sh_gate_up", "sh_down", "sh_gate", "sh_up")]
+        for w in ws:
+            if isinstance(w, QWeight):
+                w.ensure_kernel_layout()
 
     def weight_bytes(self) -> int:
         n = 0

@@ -66,6 +66,9 @@ class QWeight:
             # CPU: keep the ggml bytes, dequantise lazily for the reference path
             return cls(N_, K, int(qt) if qt in Q.GPU_NATIVE else "dense",
                        torch.empty(0), None, np.asarray(raw), int(qt), name)
+        t32_only_ok = N_ % 32 == 0 and ACT_DTYPE == torch.float16
+        if qt in Q.T32_ONLY and not t32_only_ok and K % 256 == 0:
+            raw, qt = Q.to_q8_0(raw, qt, N_, K), QType.Q8_0  # no t32 tiling possible: Q8_0 kernels
         if qt in (*Q.Q8_EXACT, *Q.Q8_REQUANT) and K % 256 == 0:
             # no dedicated layout for this block format: carried on the Q8_0 kernels, never densified
             raw, qt = Q.to_q8_0(raw, qt, N_, K), QType.Q8_0
@@ -141,6 +144,22 @@ class QWeight:
         self.data = Q.tile32(self.data, self.dplane, int(self.qtype), self.N, self.K)
         self.dplane = None
         self.layout = "t32"
+        return True
+
+    def ensure_kernel_layout(self) -> bool:
+        """A block format that only has t32 kernels (Q5_K) but stayed in the row layout (an expert stack, a
+        weight that never went through to_t32) is re-laid onto the Q8_0 kernels. Returns True if changed."""
+        if not self.is_quant or not self.data.is_cuda or self.layout != "ggml" or \
+                int(self.qtype) not in (int(q) for q in Q.T32_ONLY):
+            return False
+        raw = self.data.cpu().numpy()
+        q8 = Q.to_q8_0(raw, int(self.qtype), self.N, self.K)
+        data, dpl = Q.repack_for_gpu(q8, QType.Q8_0, self.N, self.K)
+        dev = self.data.device
+        self.data = torch.from_numpy(np.ascontiguousarray(data)).to(dev)
+        self.dplane = torch.from_numpy(np.ascontiguousarray(dpl).view(np.int16)).to(dev)
+        self.qtype = int(QType.Q8_0)
+        log.info("%s: Q5_K weight outside the t32 layout carried on the Q8_0 kernels", self.name)
         return True
 
     def build_bf16_cache(self, dtype=None):
@@ -295,6 +314,11 @@ def _qmatmul_t32(W: QWeight, x, epi: int, out, xq, xds, M: int, out_zeroed: bool
         return out
     if x is None or x.dtype != torch.float16:
         raise ValueError("qmatmul: t32 weights need f16 activations (or q8 activations with M <= 4)")
+    if int(W.qtype) in (int(q) for q in Q.T32_ONLY):
+        # formats with int8-MFMA kernels only: quantise the rows to Q8_K on the fly
+        from .core import Q8KAct, quant_q8k
+        a = quant_q8k(x, Q8KAct.empty(M, W.K, x.device))
+        return qmatmul8(W, a, epi, out, out_zeroed=out_zeroed)
     can_split = epi == EPI_ADD_F32 or (epi == EPI_F32 and out_zeroed)
     if W.bf16_cache is not None and M >= dense_min_m(x.dtype, epi, can_split) and W.bf16_cache.dtype == x.dtype:
         return _dense_cached(W, x, epi, out, M)
@@ -311,7 +335,7 @@ def _qmatmul_t32(W: QWeight, x, epi: int, out, xq, xds, M: int, out_zeroed: bool
 
 # ------------------------------------------------------------------------------------------------
 # int8-MFMA GEMM on Q8_K activations (csrc/kernels/qmm8.hip): llama.cpp's K-quant dot-product numerics.
-QMM8 = os.environ.get("MX_QMM8", "1") != "0"
+QMM8 = os.environ.get("MX_QMM8", "0") == "1"  # off by default: slower than qmm.hip at every tuned shape (profiles/r3_tune_qmm8.jsonl)
 QMM8_FORCE: tuple | None = None  # (wm, wn, nw, wmw, occ, splits) override for tuning (tools/tune_qmm8.py)
 QMM8_CONFIGS = ((2, 1, 4, 1, 1), (2, 1, 4, 2, 1), (2, 1, 4, 1, 2), (1, 2, 4, 2, 1), (2, 1, 8, 1, 1),
                 (1, 2, 2, 2, 1), (1, 2, 4, 1, 2))
@@ -320,7 +344,7 @@ QMM8_CONFIGS = ((2, 1, 4, 1, 1), (2, 1, 4, 2, 1), (2, 1, 4, 1, 2), (1, 2, 4, 2, 
 def qmm8_ok(W) -> bool:
     """Weight eligible for the int8-MFMA path (t32 Q4_K / Q6_K on the GPU)."""
     return (QMM8 and isinstance(W, QWeight) and W.layout == "t32" and W.data.is_cuda
-            and int(W.qtype) in (int(QType.Q4_K), int(QType.Q6_K)))
+            and int(W.qtype) in (int(QType.Q4_K), int(QType.Q6_K), int(QType.Q5_K)))
 
 
 def _qmm8_shape(M: int, N_: int, K: int, can_split: bool):

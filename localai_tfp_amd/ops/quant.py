@@ -369,6 +369,15 @@ def random_quantized(rng: np.random.Generator, qtype: int, n_rows: int, row_len:
         out[:, 2:4] = (d * 7.5).astype(np.float16).view(np.uint8).reshape(-1, 2)
         out[:, 4:16] = _pack_q4k_scales(sc, mn)
         return out.reshape(-1)
+    if q == QType.Q5_K:
+        out = rng.integers(0, 256, size=(nb, 176), dtype=np.uint8)
+        sc = rng.integers(40, 64, size=(nb, 8))
+        mn = sc.copy()
+        d = np.full(nb, std / (52 * 9.23), np.float32)  # q uniform 0..31: std 9.23, centre dmin = 15.5 d
+        out[:, 0:2] = d.astype(np.float16).view(np.uint8).reshape(-1, 2)
+        out[:, 2:4] = (d * 15.5).astype(np.float16).view(np.uint8).reshape(-1, 2)
+        out[:, 4:16] = _pack_q4k_scales(sc, mn)
+        return out.reshape(-1)
     if q == QType.Q6_K:
         out = rng.integers(0, 256, size=(nb, 210), dtype=np.uint8)
         sc = rng.integers(40, 80, size=(nb, 16)).astype(np.int8)
@@ -418,7 +427,10 @@ def repack_q8_0(raw: np.ndarray, n_rows: int, row_len: int):
     return np.ascontiguousarray(qs), np.ascontiguousarray(d)
 
 
-GPU_NATIVE = (QType.Q4_K, QType.Q6_K, QType.Q8_0)
+GPU_NATIVE = (QType.Q4_K, QType.Q6_K, QType.Q8_0, QType.Q5_K)
+# native only in the t32 tiled layout (qmv / qmm8 / dequant_t32 kernels); a Q5_K weight that cannot be tiled
+# (N % 32, expert stacks) is carried on the Q8_0 kernels instead (QWeight.ensure_kernel_layout)
+T32_ONLY = (QType.Q5_K,)
 
 # Block formats without a dedicated kernel layout yet, carried on the Q8_0 kernels (qmm / qmv) instead of
 # a dense 16-bit copy: the integer code of every weight is kept EXACTLY where the format is "scale x
@@ -426,7 +438,7 @@ GPU_NATIVE = (QType.Q4_K, QType.Q6_K, QType.Q8_0)
 # super-block d; IQ4_XS up to the f16 rounding of its per-32 scale); the offset formats (Q4_1, Q5_1,
 # Q2_K, Q5_K) are re-quantised to 8 bits (error ~1/254 of the block max, well under their own).
 Q8_EXACT = (QType.Q4_0, QType.Q5_0, QType.IQ4_NL, QType.IQ4_XS, QType.Q3_K)
-Q8_REQUANT = (QType.Q4_1, QType.Q5_1, QType.Q2_K, QType.Q5_K)
+Q8_REQUANT = (QType.Q4_1, QType.Q5_1, QType.Q2_K)
 
 
 def to_q8_0(raw: np.ndarray, qtype: int, n_rows: int, row_len: int) -> np.ndarray:
@@ -458,7 +470,7 @@ def to_q8_0(raw: np.ndarray, qtype: int, n_rows: int, row_len: int) -> np.ndarra
 def repack_for_gpu(raw: np.ndarray, qtype: int, n_rows: int, row_len: int):
     """-> (data uint8 [n_rows, bytes_per_row], dplane uint16 [n_rows, x] or None)."""
     q = QType(qtype)
-    if q == QType.Q4_K:
+    if q in (QType.Q4_K, QType.Q5_K):
         return np.ascontiguousarray(np.asarray(raw).reshape(n_rows, -1)), None
     if q == QType.Q6_K:
         return repack_q6_k(raw, n_rows, row_len)
@@ -467,7 +479,7 @@ def repack_for_gpu(raw: np.ndarray, qtype: int, n_rows: int, row_len: int):
     raise NotImplementedError(f"{q.name} has no native GPU layout")
 
 
-T32_UNIT = {QType.Q4_K: (4608, 256), QType.Q6_K: (6784, 256), QType.Q8_0: (2176, 64)}
+T32_UNIT = {QType.Q4_K: (4608, 256), QType.Q6_K: (6784, 256), QType.Q8_0: (2176, 64), QType.Q5_K: (5632, 256)}
 
 
 def tile32(data, dplane, qtype: int, n_rows: int, row_len: int):
@@ -490,6 +502,14 @@ def tile32(data, dplane, qtype: int, n_rows: int, row_len: int):
         hdr = b[..., :16].permute(0, 2, 1, 3).reshape(G, nb, 512)
         qs = b[..., 16:].reshape(G, 32, nb, 4, 2, 16).permute(0, 2, 3, 4, 1, 5).reshape(G, nb, 4096)
         out = torch.cat([hdr, qs], 2)
+    elif q == QType.Q5_K:
+        # ggml block {d, dmin, scales[12], qh[32], qs[128]} -> [hdr 32 x 16 B][qs as Q4_K][qh: 2 chunks x 32 x 16 B]
+        nb = row_len // 256
+        b = t.reshape(G, 32, nb, 176)
+        hdr = b[..., :16].permute(0, 2, 1, 3).reshape(G, nb, 512)
+        qh = b[..., 16:48].reshape(G, 32, nb, 2, 16).permute(0, 2, 3, 1, 4).reshape(G, nb, 1024)
+        qs = b[..., 48:].reshape(G, 32, nb, 4, 2, 16).permute(0, 2, 3, 4, 1, 5).reshape(G, nb, 4096)
+        out = torch.cat([hdr, qs, qh], 2)
     elif q == QType.Q6_K:
         nb = row_len // 256
         b = t.reshape(G, 32, nb, 208)

@@ -438,7 +438,7 @@ def test_qmatmul_llama3_8b_shapes(name, qt, n, k, epi, M):
     assert rel(out, ref) < 5e-3
 
 
-@pytest.mark.parametrize("qt", [QType.Q4_K, QType.Q6_K, QType.Q8_0])
+@pytest.mark.parametrize("qt", [QType.Q4_K, QType.Q6_K, QType.Q8_0, QType.Q5_K])
 @pytest.mark.parametrize("M", [1, 2, 3, 4])
 def test_qmv_t32(qt, M):
     """qmv.hip decode GEMV on t32 weights (q8 activations) for every epilogue, and the t32 row
@@ -635,3 +635,73 @@ def test_argmax_rows(V):
     out = torch.empty(5, dtype=torch.int32, device=DEV)
     N.kcall("mxk_argmax", xd.data_ptr(), xd.stride(0), 5, V, out.data_ptr(), N.stream_ptr())
     assert out.cpu().tolist() == [int(x[0].argmax()), 0, V - 1, 7, int(x[4].argmax())]
+
+
+def _kept_set_ref(row: torch.Tensor, temp: float, top_k: int, top_p: float, min_p: float):
+    """Kept token set + normaliser of the sampler chain (temperature, top-k with ties, top-p over the top-k
+    mass measured within the min-p set, min-p), on the CPU."""
+    v = row.double() / temp
+    mx = float(v.max())
+    order = torch.argsort(v, descending=True, stable=True)
+    sv = v[order]
+    keep = len(sv)
+    if 0 < top_k < keep:
+        kv = sv[top_k - 1]
+        keep = top_k
+        while keep < len(sv) and sv[keep] == kv:
+            keep += 1
+    zk = float(torch.exp(sv[:keep] - mx).sum())
+    if min_p > 0:
+        mv = mx + np.log(min_p)
+        while keep > 1 and sv[keep - 1] < mv:
+            keep -= 1
+    if 0 < top_p < 1:
+        cum, k = 0.0, 0
+        while k < keep:
+            cum += float(torch.exp(sv[k] - mx))
+            k += 1
+            if cum >= top_p * zk:
+                break
+        while k < keep and sv[k] == sv[k - 1]:
+            k += 1
+        keep = max(1, k)
+    kept = order[:keep]
+    return set(kept.tolist()), float(torch.exp(sv[:keep] - mx).sum()), mx
+
+
+@pytest.mark.parametrize("top_k,top_p,min_p", [(40, 0.95, 0.05), (40, 1.0, 0.0), (0, 0.9, 0.0), (0, 1.0, 0.1),
+                                                (1000, 0.95, 0.05)])
+def test_sampling_fast_path_kept_set(top_k, top_p, min_p):
+    """The histogram / candidate-set sampler (llama.cpp defaults top_k 40, top_p 0.95, min_p 0.05 at 128k
+    vocabulary) draws inside the exact kept set and reports the log-probability under it."""
+    from localai_tfp_amd.ops.sampling import SamplerBatch, SamplingParams
+    torch.manual_seed(3)
+    V, B = 128256, 8
+    logits = torch.randn(B, V, device=DEV) * 2.5
+    logits[0, :50] += 6.0  # a peaked row
+    sb = SamplerBatch(DEV)
+    ps = [SamplingParams(temperature=0.9, top_k=top_k, top_p=top_p, min_p=min_p, seed=r) for r in range(B)]
+    refs = [_kept_set_ref(logits[r].cpu(), 0.9, top_k, top_p, min_p) for r in range(B)]
+    for step in range(3):
+        tok, lp = sb.sample(logits.clone(), ps, [[]] * B, [step] * B)
+        tok, lp = tok.cpu().tolist(), lp.cpu().tolist()
+        for r in range(B):
+            kept, z, mx = refs[r]
+            assert tok[r] in kept, (r, tok[r], len(kept))
+            want = float(logits[r, tok[r]].double().cpu() / 0.9 - mx - np.log(z))
+            assert abs(lp[r] - want) < 1e-3, (lp[r], want)
+
+
+def test_sampling_fast_path_distribution():
+    from localai_tfp_amd.ops.sampling import SamplerBatch, SamplingParams
+    V = 1000
+    logits = torch.full((1, V), -30.0, device=DEV)
+    logits[0, :4] = torch.log(torch.tensor([0.1, 0.2, 0.3, 0.4], device=DEV))
+    sb = SamplerBatch(DEV)
+    cnt = np.zeros(4)
+    for s in range(2000):
+        tok, _ = sb.sample(logits.clone(), [SamplingParams(temperature=1.0, top_k=3, top_p=1.0, min_p=0.0, seed=s)],
+                           [[]], [0])
+        cnt[int(tok[0])] += 1
+    freq = cnt / cnt.sum()
+    assert np.allclose(freq, [0.0, 0.2 / 0.9, 0.3 / 0.9, 0.4 / 0.9], atol=0.04), freq

@@ -68,7 +68,7 @@ def test_rmsnorm_q8k():
 CFGS = [c for c in L.QMM8_CONFIGS]
 
 
-@pytest.mark.parametrize("qt", [QType.Q4_K, QType.Q6_K])
+@pytest.mark.parametrize("qt", [QType.Q4_K, QType.Q6_K, QType.Q5_K])
 @pytest.mark.parametrize("cfg", CFGS, ids=lambda c: "x".join(map(str, c)))
 def test_qmm8_configs(qt, cfg, monkeypatch):
     """Every compiled tile configuration, every epilogue, ragged M / N tails and split-K, against the
@@ -76,6 +76,7 @@ def test_qmm8_configs(qt, cfg, monkeypatch):
     n, k = 416, 2304  # partial column tiles; 9 super-blocks (odd split counts)
     raw, dense = make_w(qt, n, k, seed=sum(cfg) + 3)
     W = QWeight.from_ggml(raw, qt, n, k, DEV)
+    monkeypatch.setattr(L, "QMM8", True)
     assert W.to_t32() and L.qmm8_ok(W)
     for M, splits in ((77, 1), (130, 3)):
         torch.manual_seed(M)
@@ -137,3 +138,30 @@ def test_qmm8_llama3_8b_shapes(name, qt, n, k, epi, M):
     out = torch.zeros(M, n, device=DEV)
     L.qmatmul8(W, a, epi, out, out_zeroed=True)
     assert rel(out, ref) < 2e-5
+
+
+def test_q5k_native_paths():
+    """Q5_K stays Q5_K on the GPU (t32 layout, no re-quantisation): the decode GEMV (q8 activations and the
+    fused RMSNorm prologue), the int8-MFMA GEMM, the f16-activation entry (quantised to Q8_K on the fly) and
+    the row dequantisation all match the fp32 dequantised reference."""
+    n, k = 384, 1024
+    raw, dense = make_w(QType.Q5_K, n, k, seed=5)
+    W = QWeight.from_ggml(raw, QType.Q5_K, n, k, DEV)
+    assert int(W.qtype) == int(QType.Q5_K) and W.to_t32()
+    rows = torch.tensor([0, 5, 383, 77], dtype=torch.int32, device=DEV)
+    got = W.dequant_gpu(torch.float32, rows)
+    assert rel(got, dense[rows.long().cpu()]) < 1e-6
+    torch.manual_seed(0)
+    for M in (1, 3, 40):
+        x = torch.randn(M, k, device=DEV)
+        ref = x.cpu() @ dense.t()
+        out = torch.zeros(M, n, device=DEV)
+        L.qmatmul(W, x.half(), EPI_F32, out, out_zeroed=True)
+        assert rel(out, ref) < 2e-2, M
+        if M <= 4:
+            xq = torch.empty(M, k, dtype=torch.int8, device=DEV)
+            xds = torch.empty(M, k // 32, 2, device=DEV)
+            K.quant_q8(x.half(), xq, xds)
+            o2 = torch.zeros(M, n, device=DEV)
+            L.qmatmul(W, None, EPI_F32, o2, xq=xq, xds=xds)
+            assert rel(o2, ref) < 2e-2, M
