@@ -348,7 +348,36 @@ def quantize_q6_k(x: np.ndarray) -> np.ndarray:
     return out.reshape(-1)
 
 
-QUANTIZERS = {QType.Q4_K: quantize_q4_k, QType.Q6_K: quantize_q6_k, QType.Q8_0: quantize_q8_0}
+def quantize_q5_k(x: np.ndarray) -> np.ndarray:
+    """Q5_K: the Q4_K scheme with 5-bit codes (0..31) whose high bits go to qh (ggml block layout)."""
+    x = np.asarray(x, np.float32).reshape(-1, 8, 32)
+    lo = np.minimum(x.min(2), 0.0)
+    hi = x.max(2)
+    scale = (hi - lo) / 31.0
+    mins = -lo
+    d16 = (scale.max(1) / 63.0).astype(np.float16).astype(np.float32)
+    dm16 = (mins.max(1) / 63.0).astype(np.float16).astype(np.float32)
+    sc = np.clip(np.rint(np.where(d16[:, None] > 0, scale / np.maximum(d16[:, None], 1e-30), 0)), 0, 63)
+    mn = np.clip(np.rint(np.where(dm16[:, None] > 0, mins / np.maximum(dm16[:, None], 1e-30), 0)), 0, 63)
+    eff_s = d16[:, None] * sc
+    eff_m = dm16[:, None] * mn
+    q = np.where(eff_s[:, :, None] > 0, np.rint((x + eff_m[:, :, None]) / np.maximum(eff_s[:, :, None], 1e-30)), 0)
+    q = np.clip(q, 0, 31).astype(np.uint8).reshape(-1, 256)
+    nb = q.shape[0]
+    out = np.zeros((nb, 176), np.uint8)
+    out[:, 0:2] = d16.astype(np.float16).view(np.uint8).reshape(-1, 2)
+    out[:, 2:4] = dm16.astype(np.float16).view(np.uint8).reshape(-1, 2)
+    out[:, 4:16] = _pack_q4k_scales(sc.astype(np.int32), mn.astype(np.int32))
+    qh = np.zeros((nb, 32), np.uint8)
+    for c in range(4):
+        a, b_ = q[:, 64 * c:64 * c + 32], q[:, 64 * c + 32:64 * c + 64]
+        out[:, 48 + 32 * c:48 + 32 * c + 32] = (a & 0xF) | ((b_ & 0xF) << 4)
+        qh |= ((a >> 4) << (2 * c)).astype(np.uint8) | ((b_ >> 4) << (2 * c + 1)).astype(np.uint8)
+    out[:, 16:48] = qh
+    return out.reshape(-1)
+
+
+QUANTIZERS = {QType.Q4_K: quantize_q4_k, QType.Q6_K: quantize_q6_k, QType.Q8_0: quantize_q8_0, QType.Q5_K: quantize_q5_k}
 
 
 def random_quantized(rng: np.random.Generator, qtype: int, n_rows: int, row_len: int, std: float = 0.02) -> np.ndarray:
