@@ -48,8 +48,14 @@ class MMDiTConfig:
 
 SD3_MEDIUM = MMDiTConfig()
 SD35_LARGE = MMDiTConfig(layers=38, heads=38, caption_dim=2432, qk_norm=True)
+# SD3.5-medium = MMDiT-X: blocks 0..12 add a second, image-only self-attention (attn2) with its own
+# three modulation vectors (adaLN 9*D instead of 6*D); position table 384 x 384.
+SD35_MEDIUM = MMDiTConfig(layers=24, heads=24, caption_dim=1536, qk_norm=True, pos_max=384,
+                          dual_attention_layers=tuple(range(13)))
 MMDIT_TEST = MMDiTConfig(layers=2, heads=2, joint_dim=64, caption_dim=128, pooled_dim=64, pos_max=32,
                          sample_size=16)
+MMDITX_TEST = MMDiTConfig(layers=3, heads=2, joint_dim=64, caption_dim=128, pooled_dim=64, pos_max=32,
+                          sample_size=16, qk_norm=True, dual_attention_layers=(0, 1))
 
 
 def sincos_2d(dim: int, grid: int, base_size: int, interp: float = 1.0) -> np.ndarray:
@@ -108,6 +114,21 @@ class _Attn(nn.Module):
                 setattr(self, n, m)
 
 
+class _SelfAttn(nn.Module):
+    """MMDiT-X attn2: image-stream-only self-attention (diffusers `Attention` without added projections)."""
+
+    def __init__(self, c: MMDiTConfig):
+        super().__init__()
+        d = c.dim
+        self.to_q, self.to_k, self.to_v = nn.Linear(d, d), nn.Linear(d, d), nn.Linear(d, d)
+        self.to_out = nn.ModuleList([nn.Linear(d, d)])
+        if c.qk_norm:
+            for n in ("norm_q", "norm_k"):
+                m = nn.Module()
+                m.weight = nn.Parameter(torch.ones(c.head_dim))
+                setattr(self, n, m)
+
+
 class _FF(nn.Module):
     def __init__(self, d):
         super().__init__()
@@ -117,11 +138,13 @@ class _FF(nn.Module):
 
 
 class _Block(nn.Module):
-    def __init__(self, c: MMDiTConfig, pre_only: bool):
+    def __init__(self, c: MMDiTConfig, pre_only: bool, dual: bool = False):
         super().__init__()
         d = c.dim
-        self.pre_only = pre_only
-        self.norm1 = _Lin(d, 6 * d)
+        self.pre_only, self.dual = pre_only, dual
+        self.norm1 = _Lin(d, (9 if dual else 6) * d)
+        if dual:
+            self.attn2 = _SelfAttn(c)
         self.norm1_context = _Lin(d, (2 if pre_only else 6) * d)
         self.attn = _Attn(c, pre_only)
         self.ff = _FF(d)
@@ -136,7 +159,8 @@ class MMDiT(nn.Module):
         self.pos_embed = _PatchEmbed(c)
         self.time_text_embed = _TimeText(c)
         self.context_embedder = nn.Linear(c.joint_dim, c.caption_dim if c.caption_dim else c.dim)
-        self.transformer_blocks = nn.ModuleList(_Block(c, i == c.layers - 1) for i in range(c.layers))
+        self.transformer_blocks = nn.ModuleList(_Block(c, i == c.layers - 1, i in c.dual_attention_layers)
+                                                for i in range(c.layers))
         self.norm_out = _Lin(c.dim, 2 * c.dim)
         self.proj_out = nn.Linear(c.dim, c.patch * c.patch * c.out_channels)
         self._prep = None
@@ -163,9 +187,12 @@ class MMDiT(nn.Module):
                           torch.cat([a.to_q.bias, a.to_k.bias, a.to_v.bias]),
                           torch.cat([a.add_q_proj.weight, a.add_k_proj.weight, a.add_v_proj.weight]),
                           torch.cat([a.add_q_proj.bias, a.add_k_proj.bias, a.add_v_proj.bias])))
+        qkv2 = [(torch.cat([b.attn2.to_q.weight, b.attn2.to_k.weight, b.attn2.to_v.weight]),
+                 torch.cat([b.attn2.to_q.bias, b.attn2.to_k.bias, b.attn2.to_v.bias])) if b.dual else None
+                for b in self.transformer_blocks]
         c = self.cfg
         pw = self.pos_embed.proj.weight.reshape(c.dim, -1).contiguous()  # [D, C*p*p] (c, ph, pw) order
-        self._prep = dict(wm=wm, bm=bm, offs=offs, qkv=fused, pw=pw)
+        self._prep = dict(wm=wm, bm=bm, offs=offs, qkv=fused, qkv2=qkv2, pw=pw)
         return self
 
     def _pos(self, h: int, w: int) -> torch.Tensor:
@@ -213,9 +240,12 @@ class MMDiT(nn.Module):
         cn = torch.empty(B * T, D, dtype=dt, device=x.device)
         for i, blk in enumerate(self.transformer_blocks):
             o1, o2 = P["offs"][2 * i], P["offs"][2 * i + 1]
-            m = mod[:, o1:o1 + 6 * D]
+            m = mod[:, o1:o1 + (9 if blk.dual else 6) * D]
             sh, sc, g, sh2, sc2, g2 = (m[:, k * D:(k + 1) * D] for k in range(6))
             mc = mod[:, o2:o2 + (2 if blk.pre_only else 6) * D]
+            if blk.dual:  # attn2's input is modulated from the block INPUT (same LayerNorm, own shift/scale)
+                xn2 = torch.empty_like(xn)
+                K.layernorm_mod(x, m[:, 7 * D:8 * D], m[:, 6 * D:7 * D], S, xn2)
             K.layernorm_mod(x, sc, sh, S, xn)
             if blk.pre_only:  # AdaLayerNormContinuous: (scale, shift)
                 K.layernorm_mod(cx, mc[:, :D], mc[:, D:2 * D], T, cn)
@@ -235,6 +265,15 @@ class MMDiT(nn.Module):
             o = attention(qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], B, S + T, S + T, H, hd).view(B, S + T, D)
             y = torch.matmul(o[:, :S], a.to_out[0].weight.t()) + a.to_out[0].bias
             K.gate_add(x, y.view(B * S, D), g, S)
+            if blk.dual:
+                w2, b2 = P["qkv2"][i]
+                q2 = F.linear(xn2, w2, b2)
+                if c.qk_norm:
+                    q2[:, :D] = self._qk_norm(q2[:, :D], blk.attn2.norm_q.weight, H)
+                    q2[:, D:2 * D] = self._qk_norm(q2[:, D:2 * D], blk.attn2.norm_k.weight, H)
+                o2_ = attention(q2[:, :D], q2[:, D:2 * D], q2[:, 2 * D:], B, S, S, H, hd)
+                K.gate_add(x, F.linear(o2_.reshape(B * S, D), blk.attn2.to_out[0].weight, blk.attn2.to_out[0].bias),
+                           m[:, 8 * D:9 * D], S)
             K.layernorm_mod(x, sc2, sh2, S, xn)
             u = F.gelu(F.linear(xn, blk.ff.net[0].proj.weight, blk.ff.net[0].proj.bias), approximate="tanh")
             K.gate_add(x, F.linear(u, blk.ff.net[2].weight, blk.ff.net[2].bias), g2, S)

@@ -19,7 +19,7 @@ import torch.nn.functional as F
 
 from ...tokenizer.clip import CLIPTokenizer, T5Tokenizer
 from . import samplers as S
-from .mmdit import MMDIT_TEST, SD3_MEDIUM, MMDiT, MMDiTConfig
+from .mmdit import MMDIT_TEST, MMDITX_TEST, SD3_MEDIUM, SD35_LARGE, SD35_MEDIUM, MMDiT, MMDiTConfig
 from .nn import cast_module, init_synthetic
 from .text_encoders import CLIP_G, CLIP_L, T5_XXL, CLIPTextConfig, CLIPTextEncoder, T5Config, T5Encoder
 from .vae import VAE_SD3, VAE_TEST, AutoencoderKL, VAEConfig
@@ -41,7 +41,10 @@ _T5_T = T5Config(vocab=300, d_model=64, heads=2, d_kv=32, d_ff=128, layers=2)
 PRESETS = {
     "sd3-medium": SD3Preset(SD3_MEDIUM, CLIP_L, CLIP_G, T5_XXL, VAE_SD3),
     "sd3-medium-no-t5": SD3Preset(SD3_MEDIUM, CLIP_L, CLIP_G, None, VAE_SD3),
+    "sd3.5-medium": SD3Preset(SD35_MEDIUM, CLIP_L, CLIP_G, T5_XXL, VAE_SD3),
+    "sd3.5-large": SD3Preset(SD35_LARGE, CLIP_L, CLIP_G, T5_XXL, VAE_SD3),
     "sd3-test": SD3Preset(MMDIT_TEST, _CLIP_T1, _CLIP_T2, _T5_T, VAE_TEST, t5_tokens=16),
+    "sd3.5m-test": SD3Preset(MMDITX_TEST, _CLIP_T1, _CLIP_T2, _T5_T, VAE_TEST, t5_tokens=16),
 }
 
 

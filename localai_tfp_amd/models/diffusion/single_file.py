@@ -235,8 +235,12 @@ def sai_mmdit_to_diffusers(sd: dict) -> dict:
                 names = ("to_q", "to_k", "to_v") if rest.startswith("x_") else ("add_q_proj", "add_k_proj", "add_v_proj")
                 for j, nm in enumerate(names):
                     out[f"{b}attn.{nm}.{leaf}"] = v[j * d:(j + 1) * d]
-            elif rest.startswith("x_block.attn2."):
-                raise ValueError("SD3.5-medium MMDiT-X dual-attention blocks (attn2) are not supported")
+            elif rest == "x_block.attn2.qkv":  # MMDiT-X (SD3.5-medium) image-only second attention
+                for j, nm in enumerate(("to_q", "to_k", "to_v")):
+                    out[f"{b}attn2.{nm}.{leaf}"] = v[j * d:(j + 1) * d]
+            elif rest in ("x_block.attn2.proj", "x_block.attn2.ln_q", "x_block.attn2.ln_k"):
+                nm = {"proj": "to_out.0", "ln_q": "norm_q", "ln_k": "norm_k"}[rest.rsplit(".", 1)[1]]
+                out[f"{b}attn2.{nm}.{leaf}"] = v
     return out
 
 
@@ -251,7 +255,9 @@ def mmdit_config_from(sd: dict):
                        out_channels=int(sd["proj_out.weight"].shape[0]) // int(w.shape[2]) ** 2, layers=layers,
                        head_dim=64, heads=d // 64, joint_dim=int(sd["context_embedder.weight"].shape[1]),
                        caption_dim=d, pooled_dim=int(sd["time_text_embed.text_embedder.linear_1.weight"].shape[1]),
-                       pos_max=pos_max, sample_size=128, qk_norm="transformer_blocks.0.attn.norm_q.weight" in sd)
+                       pos_max=pos_max, sample_size=128, qk_norm="transformer_blocks.0.attn.norm_q.weight" in sd,
+                       dual_attention_layers=tuple(i for i in range(layers)
+                                                   if f"transformer_blocks.{i}.attn2.to_q.weight" in sd))
 
 
 # ---------------------------------------------------------------- text encoders

@@ -11,7 +11,7 @@ import torch.nn.functional as F
 import yaml
 
 from localai_tfp_amd.models.diffusion import samplers as S
-from localai_tfp_amd.models.diffusion.mmdit import MMDIT_TEST, MMDiT
+from localai_tfp_amd.models.diffusion.mmdit import MMDIT_TEST, MMDITX_TEST, MMDiT
 from localai_tfp_amd.models.diffusion.nn import cast_module, init_synthetic, timestep_embedding
 from localai_tfp_amd.models.diffusion.pipeline import GenParams, SD3Pipeline
 from localai_tfp_amd.models.diffusion.vae import VAE_TEST, AutoencoderKL
@@ -35,11 +35,19 @@ def ref_mmdit(m: MMDiT, latent, t, ctx, pooled):
     def attn(q, k, v):
         q, k, v = (z.view(B, -1, H, D // H).transpose(1, 2) for z in (q, k, v))
         return F.scaled_dot_product_attention(q, k, v).transpose(1, 2).reshape(B, -1, D)
+
+    def rms(z, mod, name):  # per-head RMS QK-norm (diffusers qk_norm="rms_norm", eps 1e-6)
+        if not c.qk_norm:
+            return z
+        zh = z.view(*z.shape[:-1], H, D // H)
+        return (zh * torch.rsqrt(zh.pow(2).mean(-1, keepdim=True) + 1e-6) * getattr(mod, name).weight).flatten(-2)
     S_ = x.shape[1]
     for blk in m.transformer_blocks:
         e = blk.norm1.linear(F.silu(temb))
-        sh, sc, g, sh2, sc2, g2 = e.chunk(6, 1)
+        sh, sc, g, sh2, sc2, g2, *dual = e.chunk(9 if blk.dual else 6, 1)
         xn = ln(x) * (1 + sc[:, None]) + sh[:, None]
+        if blk.dual:  # SD35AdaLayerNormZeroX: second modulation of the same normalised input
+            xn2 = ln(x) * (1 + dual[1][:, None]) + dual[0][:, None]
         ec = blk.norm1_context.linear(F.silu(temb))
         if blk.pre_only:
             csc, csh = ec.chunk(2, 1)
@@ -47,11 +55,15 @@ def ref_mmdit(m: MMDiT, latent, t, ctx, pooled):
             csh, csc, cg, csh2, csc2, cg2 = ec.chunk(6, 1)
         cn = ln(cx) * (1 + csc[:, None]) + csh[:, None]
         a = blk.attn
-        q = torch.cat([a.to_q(xn), a.add_q_proj(cn)], 1)
-        k = torch.cat([a.to_k(xn), a.add_k_proj(cn)], 1)
+        q = torch.cat([rms(a.to_q(xn), a, "norm_q"), rms(a.add_q_proj(cn), a, "norm_added_q")], 1)
+        k = torch.cat([rms(a.to_k(xn), a, "norm_k"), rms(a.add_k_proj(cn), a, "norm_added_k")], 1)
         v = torch.cat([a.to_v(xn), a.add_v_proj(cn)], 1)
         o = attn(q, k, v)
         x = x + g[:, None] * a.to_out[0](o[:, :S_])
+        if blk.dual:
+            a2 = blk.attn2
+            o2 = attn(rms(a2.to_q(xn2), a2, "norm_q"), rms(a2.to_k(xn2), a2, "norm_k"), a2.to_v(xn2))
+            x = x + dual[2][:, None] * a2.to_out[0](o2)
         xn = ln(x) * (1 + sc2[:, None]) + sh2[:, None]
         x = x + g2[:, None] * blk.ff.net[2](F.gelu(blk.ff.net[0].proj(xn), approximate="tanh"))
         if not blk.pre_only:
@@ -78,6 +90,21 @@ def test_mmdit_matches_reference():
     t = torch.tensor([500.0, 20.0])
     ctx = torch.randn(2, 9, MMDIT_TEST.joint_dim, generator=g)
     pooled = torch.randn(2, MMDIT_TEST.pooled_dim, generator=g)
+    with torch.no_grad():
+        ref = ref_mmdit(m, lat, t, ctx, pooled)
+        got = m(lat, t, ctx, pooled)
+    assert (got - ref).abs().max() < 1e-3 * max(1.0, ref.abs().max().item())
+
+
+def test_mmditx_dual_attention_matches_reference():
+    """SD3.5-medium MMDiT-X blocks (attn2 + 9-vector adaLN) and RMS QK-norm against the fp32 reference."""
+    m = init_synthetic(MMDiT(MMDITX_TEST), 4)
+    assert m.transformer_blocks[0].dual and not m.transformer_blocks[2].dual
+    g = torch.Generator().manual_seed(1)
+    lat = torch.randn(2, 16, 16, 16, generator=g)
+    t = torch.tensor([700.0, 3.0])
+    ctx = torch.randn(2, 7, MMDITX_TEST.joint_dim, generator=g)
+    pooled = torch.randn(2, MMDITX_TEST.pooled_dim, generator=g)
     with torch.no_grad():
         ref = ref_mmdit(m, lat, t, ctx, pooled)
         got = m(lat, t, ctx, pooled)
@@ -191,9 +218,10 @@ def test_diffusion_kernels_gpu(dt):
 
 
 @pytest.mark.gpu
-def test_mmdit_gpu_matches_fp32():
-    m = _mmdit()
-    gm = cast_module(MMDiT(MMDIT_TEST), "cuda", torch.bfloat16)
+@pytest.mark.parametrize("cfg", [MMDIT_TEST, MMDITX_TEST], ids=["mmdit", "mmditx"])
+def test_mmdit_gpu_matches_fp32(cfg):
+    m = init_synthetic(MMDiT(cfg), 3)
+    gm = cast_module(MMDiT(cfg), "cuda", torch.bfloat16)
     gm.load_state_dict({k: v.to(torch.bfloat16) if v.dim() > 1 else v for k, v in m.state_dict().items()})
     cast_module(gm, "cuda", torch.bfloat16)
     # reference sees the same bf16-rounded weights
@@ -201,8 +229,8 @@ def test_mmdit_gpu_matches_fp32():
     g = torch.Generator().manual_seed(0)
     lat = torch.randn(2, 16, 32, 32, generator=g)
     t = torch.tensor([500.0, 20.0])
-    ctx = torch.randn(2, 77, MMDIT_TEST.joint_dim, generator=g)
-    pooled = torch.randn(2, MMDIT_TEST.pooled_dim, generator=g)
+    ctx = torch.randn(2, 77, cfg.joint_dim, generator=g)
+    pooled = torch.randn(2, cfg.pooled_dim, generator=g)
     with torch.no_grad():
         ref = ref_mmdit(m, lat, t, ctx, pooled)
         got = gm(lat.cuda(), t.cuda(), ctx.cuda(), pooled.cuda()).cpu()

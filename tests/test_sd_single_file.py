@@ -274,7 +274,9 @@ def _mmdit_to_sai(sd, d, n):
            "ff.net.0.proj": "x_block.mlp.fc1", "ff.net.2": "x_block.mlp.fc2", "attn.to_add_out": "context_block.attn.proj",
            "ff_context.net.0.proj": "context_block.mlp.fc1", "ff_context.net.2": "context_block.mlp.fc2",
            "attn.norm_q": "x_block.attn.ln_q", "attn.norm_k": "x_block.attn.ln_k",
-           "attn.norm_added_q": "context_block.attn.ln_q", "attn.norm_added_k": "context_block.attn.ln_k"}
+           "attn.norm_added_q": "context_block.attn.ln_q", "attn.norm_added_k": "context_block.attn.ln_k",
+           "attn2.to_out.0": "x_block.attn2.proj", "attn2.norm_q": "x_block.attn2.ln_q",
+           "attn2.norm_k": "x_block.attn2.ln_k"}
     for k, v in sd.items():
         stem, _, leaf = k.rpartition(".")
         if stem in top:
@@ -294,7 +296,30 @@ def _mmdit_to_sai(sd, d, n):
             p = f"transformer_blocks.{i}.attn."
             out[f"joint_blocks.{i}.x_block.attn.qkv.{lf}"] = torch.cat([sd[f"{p}to_{x}.{lf}"] for x in "qkv"])
             out[f"joint_blocks.{i}.context_block.attn.qkv.{lf}"] = torch.cat([sd[f"{p}add_{x}_proj.{lf}"] for x in "qkv"])
+            p2 = f"transformer_blocks.{i}.attn2."
+            if f"{p2}to_q.{lf}" in sd:
+                out[f"joint_blocks.{i}.x_block.attn2.qkv.{lf}"] = torch.cat([sd[f"{p2}to_{x}.{lf}"] for x in "qkv"])
     return out
+
+
+def test_sd35_medium_mmditx_single_file(tmp_path):
+    """SD3.5-medium (MMDiT-X) Stability layout: x_block.attn2.{qkv,proj,ln_q,ln_k} and 9-vector adaLN map to
+    diffusers attn2 names; the config recovers dual_attention_layers from the tensor names."""
+    from localai_tfp_amd.models.diffusion.mmdit import MMDITX_TEST, MMDiT
+    from localai_tfp_amd.models.diffusion.nn import init_synthetic
+    m = init_synthetic(MMDiT(MMDITX_TEST), 5)
+    msd = {k: v.contiguous() for k, v in m.state_dict().items()}
+    f = {"model.diffusion_model." + k: v for k, v in _mmdit_to_sai(msd, MMDITX_TEST.dim, MMDITX_TEST.layers).items()}
+    assert "model.diffusion_model.joint_blocks.1.x_block.attn2.qkv.weight" in f
+    sd = SF.sai_mmdit_to_diffusers(f)
+    cfg = SF.mmdit_config_from(sd)
+    assert cfg.dual_attention_layers == (0, 1) and cfg.qk_norm
+    import dataclasses
+    assert dataclasses.replace(cfg, sample_size=MMDITX_TEST.sample_size) == MMDITX_TEST
+    m2 = MMDiT(cfg)
+    miss, unexp = m2.load_state_dict(sd, strict=False)
+    assert not unexp and not miss
+    assert all(torch.equal(m2.state_dict()[k], v) for k, v in msd.items())
 
 
 def test_sd3_single_file_bundled(tmp_path):
