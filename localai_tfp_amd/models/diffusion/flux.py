@@ -30,7 +30,7 @@ from torch import nn
 
 from ... import _native as N
 from ...ops import core as K
-from .nn import attention, cast_module, init_synthetic, linear_f32, timestep_embedding
+from .nn import attention, cast_module, cat_w, init_synthetic, lin, linear_f32, timestep_embedding
 
 
 @dataclass
@@ -69,7 +69,7 @@ class _TE(nn.Module):
         self.linear_2 = nn.Linear(o, o)
 
     def run(self, x):
-        return F.linear(F.silu(F.linear(x, self.linear_1.weight, self.linear_1.bias)), self.linear_2.weight,
+        return lin(F.silu(lin(x, self.linear_1.weight, self.linear_1.bias)), self.linear_2.weight,
                         self.linear_2.bias)
 
 
@@ -186,19 +186,19 @@ class FluxTransformer(nn.Module):
             o += b.norm.linear.out_features
         mods.append(self.norm_out.linear)
         offs.append(o)
-        wm = torch.cat([m.weight for m in mods])
+        wm = cat_w([m.weight for m in mods])
         bm = torch.cat([m.bias for m in mods]).float()
         dbl = []
         for b in self.transformer_blocks:
             a = b.attn
-            dbl.append((torch.cat([a.to_q.weight, a.to_k.weight, a.to_v.weight]),
+            dbl.append((cat_w([a.to_q.weight, a.to_k.weight, a.to_v.weight]),
                         torch.cat([a.to_q.bias, a.to_k.bias, a.to_v.bias]),
-                        torch.cat([a.add_q_proj.weight, a.add_k_proj.weight, a.add_v_proj.weight]),
+                        cat_w([a.add_q_proj.weight, a.add_k_proj.weight, a.add_v_proj.weight]),
                         torch.cat([a.add_q_proj.bias, a.add_k_proj.bias, a.add_v_proj.bias])))
         sgl = []
         for b in self.single_transformer_blocks:
             a = b.attn
-            sgl.append((torch.cat([a.to_q.weight, a.to_k.weight, a.to_v.weight, b.proj_mlp.weight]),
+            sgl.append((cat_w([a.to_q.weight, a.to_k.weight, a.to_v.weight, b.proj_mlp.weight]),
                         torch.cat([a.to_q.bias, a.to_k.bias, a.to_v.bias, b.proj_mlp.bias])))
         f32 = lambda n: n.weight.float().contiguous()  # noqa: E731
         norms = [(f32(b.attn.norm_q), f32(b.attn.norm_k), f32(b.attn.norm_added_q), f32(b.attn.norm_added_k))
@@ -225,7 +225,7 @@ class FluxTransformer(nn.Module):
             g = guidance if guidance is not None else torch.full((B,), 3.5, device=x.device)
             temb = temb + te.guidance_embedder.run(timestep_embedding(g * 1000.0, 256, shift=0.0).to(dt))
         temb = temb.float() + te.text_embedder.run(pooled.to(dt)).float()
-        mod = F.linear(F.silu(temb).to(dt), P["wm"]).float() + P["bm"]
+        mod = lin(F.silu(temb).to(dt), P["wm"]).float() + P["bm"]
         ids = torch.cat([torch.zeros(T, 3, device=img_ids.device, dtype=img_ids.dtype), img_ids], 0)
         cs = rope_table(ids.cpu(), c.axes, c.theta).to(x.device)
         cs_t, cs_i = cs[:T].contiguous(), cs[T:].contiguous()
@@ -241,24 +241,24 @@ class FluxTransformer(nn.Module):
             K.layernorm_mod(cx, csc, csh, T, cn)
             wq, bq, wcq, bcq = P["dbl"][i]
             nq, nk, naq, nak = P["norms"][i]
-            qc = F.linear(cn, wcq, bcq)  # [B*T, 3D]; table row = r % T, so batches need no loop
-            qx = F.linear(hn, wq, bq)
+            qc = lin(cn, wcq, bcq)  # [B*T, 3D]; table row = r % T, so batches need no loop
+            qx = lin(hn, wq, bq)
             qk_norm_rope(qc, D, H, naq, nak, cs_t, T)
             qk_norm_rope(qx, D, H, nq, nk, cs_i, S)
             qkv = torch.cat([qc.view(B, T, 3 * D), qx.view(B, S, 3 * D)], 1)
             f = qkv.view(B * L, 3 * D)
             o = attention(f[:, :D], f[:, D:2 * D], f[:, 2 * D:], B, L, L, H, c.head_dim).view(B, L, D)
             a = blk.attn
-            K.gate_add(h, (torch.matmul(o[:, T:], a.to_out[0].weight.t()) + a.to_out[0].bias).reshape(B * S, D), gt, S)
-            K.gate_add(cx, (torch.matmul(o[:, :T], a.to_add_out.weight.t()) + a.to_add_out.bias).reshape(B * T, D),
+            K.gate_add(h, lin(o[:, T:], a.to_out[0].weight, a.to_out[0].bias).reshape(B * S, D), gt, S)
+            K.gate_add(cx, lin(o[:, :T], a.to_add_out.weight, a.to_add_out.bias).reshape(B * T, D),
                        cg, T)
             K.layernorm_mod(h, sc2, sh2, S, hn)
-            u = F.gelu(F.linear(hn, blk.ff.net[0].proj.weight, blk.ff.net[0].proj.bias), approximate="tanh")
-            K.gate_add(h, F.linear(u, blk.ff.net[2].weight, blk.ff.net[2].bias), g2, S)
+            u = F.gelu(lin(hn, blk.ff.net[0].proj.weight, blk.ff.net[0].proj.bias), approximate="tanh")
+            K.gate_add(h, lin(u, blk.ff.net[2].weight, blk.ff.net[2].bias), g2, S)
             K.layernorm_mod(cx, csc2, csh2, T, cn)
-            u = F.gelu(F.linear(cn, blk.ff_context.net[0].proj.weight, blk.ff_context.net[0].proj.bias),
+            u = F.gelu(lin(cn, blk.ff_context.net[0].proj.weight, blk.ff_context.net[0].proj.bias),
                        approximate="tanh")
-            K.gate_add(cx, F.linear(u, blk.ff_context.net[2].weight, blk.ff_context.net[2].bias), cg2, T)
+            K.gate_add(cx, lin(u, blk.ff_context.net[2].weight, blk.ff_context.net[2].bias), cg2, T)
         xs = torch.cat([cx.view(B, T, D), h.view(B, S, D)], 1).reshape(B * L, D).contiguous()
         xn = torch.empty(B * L, D, dtype=dt, device=x.device)
         nb = len(self.transformer_blocks)
@@ -267,7 +267,7 @@ class FluxTransformer(nn.Module):
             sh, sc, gt = (mod[:, o1 + k * D:o1 + (k + 1) * D] for k in range(3))
             K.layernorm_mod(xs, sc, sh, L, xn)
             w, b = P["sgl"][j]
-            y = F.linear(xn, w, b)  # [B*L, 7D] = q | k | v | mlp_in
+            y = lin(xn, w, b)  # [B*L, 7D] = q | k | v | mlp_in
             nq, nk = P["snorms"][j]
             qk_norm_rope(y, D, H, nq, nk, cs, L)
             o = attention(y[:, :D], y[:, D:2 * D], y[:, 2 * D:3 * D], B, L, L, H, c.head_dim)
@@ -275,7 +275,7 @@ class FluxTransformer(nn.Module):
             cat = y[:, 2 * D:]  # [B*L, 5D] view: v | mlp_in  -> overwritten with attn | gelu(mlp)
             cat[:, D:] = F.gelu(cat[:, D:], approximate="tanh")
             cat[:, :D] = o
-            K.gate_add(xs, F.linear(cat, blk.proj_out.weight, blk.proj_out.bias), gt, L)
+            K.gate_add(xs, lin(cat, blk.proj_out.weight, blk.proj_out.bias), gt, L)
         on = P["offs"][-1]
         img = xs.view(B, L, D)[:, T:].reshape(B * S, D).contiguous()
         K.layernorm_mod(img, mod[:, on:on + D], mod[:, on + D:on + 2 * D], S, hn)

@@ -22,7 +22,7 @@ import torch.nn.functional as F
 from torch import nn
 
 from ...ops import core as K
-from .nn import attention, timestep_embedding
+from .nn import attention, cat_w, lin, timestep_embedding
 
 
 @dataclass
@@ -178,16 +178,16 @@ class MMDiT(nn.Module):
         mods.append(self.norm_out.linear)
         offs.append(o)
         o += self.norm_out.linear.out_features
-        wm = torch.cat([m.weight for m in mods])
+        wm = cat_w([m.weight for m in mods])
         bm = torch.cat([m.bias for m in mods]).float()
         fused = []
         for b in self.transformer_blocks:
             a = b.attn
-            fused.append((torch.cat([a.to_q.weight, a.to_k.weight, a.to_v.weight]),
+            fused.append((cat_w([a.to_q.weight, a.to_k.weight, a.to_v.weight]),
                           torch.cat([a.to_q.bias, a.to_k.bias, a.to_v.bias]),
-                          torch.cat([a.add_q_proj.weight, a.add_k_proj.weight, a.add_v_proj.weight]),
+                          cat_w([a.add_q_proj.weight, a.add_k_proj.weight, a.add_v_proj.weight]),
                           torch.cat([a.add_q_proj.bias, a.add_k_proj.bias, a.add_v_proj.bias])))
-        qkv2 = [(torch.cat([b.attn2.to_q.weight, b.attn2.to_k.weight, b.attn2.to_v.weight]),
+        qkv2 = [(cat_w([b.attn2.to_q.weight, b.attn2.to_k.weight, b.attn2.to_v.weight]),
                  torch.cat([b.attn2.to_q.bias, b.attn2.to_k.bias, b.attn2.to_v.bias])) if b.dual else None
                 for b in self.transformer_blocks]
         c = self.cfg
@@ -222,19 +222,19 @@ class MMDiT(nn.Module):
         D = c.dim
         # patchify (conv p x p stride p == GEMM over (c, ph, pw) patches)
         patches = latent.to(dt).view(B, C, h, p, w, p).permute(0, 2, 4, 1, 3, 5).reshape(B * S, C * p * p)
-        x = F.linear(patches, P["pw"], self.pos_embed.proj.bias).float()
+        x = lin(patches, P["pw"], self.pos_embed.proj.bias).float()
         x = (x.view(B, S, D) + self._pos(h, w)[None]).reshape(B * S, D).contiguous()
         # conditioning
         te = self.time_text_embed
-        temb = F.linear(timestep_embedding(t, 256).to(dt), te.timestep_embedder.linear_1.weight,
+        temb = lin(timestep_embedding(t, 256).to(dt), te.timestep_embedder.linear_1.weight,
                         te.timestep_embedder.linear_1.bias)
-        temb = F.linear(F.silu(temb), te.timestep_embedder.linear_2.weight, te.timestep_embedder.linear_2.bias)
-        pe = F.linear(pooled.to(dt), te.text_embedder.linear_1.weight, te.text_embedder.linear_1.bias)
-        pe = F.linear(F.silu(pe), te.text_embedder.linear_2.weight, te.text_embedder.linear_2.bias)
+        temb = lin(F.silu(temb), te.timestep_embedder.linear_2.weight, te.timestep_embedder.linear_2.bias)
+        pe = lin(pooled.to(dt), te.text_embedder.linear_1.weight, te.text_embedder.linear_1.bias)
+        pe = lin(F.silu(pe), te.text_embedder.linear_2.weight, te.text_embedder.linear_2.bias)
         cond = F.silu((temb.float() + pe.float()).to(dt))
-        mod = F.linear(cond, P["wm"]).float() + P["bm"]  # [B, sum of all modulation widths]
+        mod = lin(cond, P["wm"]).float() + P["bm"]  # [B, sum of all modulation widths]
         T = ctx.shape[1]
-        cx = F.linear(ctx.reshape(B * T, -1).to(dt), self.context_embedder.weight, self.context_embedder.bias).float()
+        cx = lin(ctx.reshape(B * T, -1).to(dt), self.context_embedder.weight, self.context_embedder.bias).float()
         H, hd = c.heads, c.head_dim
         xn = torch.empty(B * S, D, dtype=dt, device=x.device)
         cn = torch.empty(B * T, D, dtype=dt, device=x.device)
@@ -252,8 +252,8 @@ class MMDiT(nn.Module):
             else:
                 K.layernorm_mod(cx, mc[:, D:2 * D], mc[:, :D], T, cn)
             wq, bq, wcq, bcq = P["qkv"][i]
-            qx = F.linear(xn, wq, bq).view(B, S, 3 * D)
-            qc = F.linear(cn, wcq, bcq).view(B, T, 3 * D)
+            qx = lin(xn, wq, bq).view(B, S, 3 * D)
+            qc = lin(cn, wcq, bcq).view(B, T, 3 * D)
             a = blk.attn
             if c.qk_norm:
                 qx, qc = qx.clone(), qc.clone()
@@ -263,30 +263,30 @@ class MMDiT(nn.Module):
                     f[:, D:2 * D] = self._qk_norm(f[:, D:2 * D], nk.weight, H)
             qkv = torch.cat([qx, qc], 1).view(B * (S + T), 3 * D)
             o = attention(qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], B, S + T, S + T, H, hd).view(B, S + T, D)
-            y = torch.matmul(o[:, :S], a.to_out[0].weight.t()) + a.to_out[0].bias
+            y = lin(o[:, :S], a.to_out[0].weight, a.to_out[0].bias)
             K.gate_add(x, y.view(B * S, D), g, S)
             if blk.dual:
                 w2, b2 = P["qkv2"][i]
-                q2 = F.linear(xn2, w2, b2)
+                q2 = lin(xn2, w2, b2)
                 if c.qk_norm:
                     q2[:, :D] = self._qk_norm(q2[:, :D], blk.attn2.norm_q.weight, H)
                     q2[:, D:2 * D] = self._qk_norm(q2[:, D:2 * D], blk.attn2.norm_k.weight, H)
                 o2_ = attention(q2[:, :D], q2[:, D:2 * D], q2[:, 2 * D:], B, S, S, H, hd)
-                K.gate_add(x, F.linear(o2_.reshape(B * S, D), blk.attn2.to_out[0].weight, blk.attn2.to_out[0].bias),
+                K.gate_add(x, lin(o2_.reshape(B * S, D), blk.attn2.to_out[0].weight, blk.attn2.to_out[0].bias),
                            m[:, 8 * D:9 * D], S)
             K.layernorm_mod(x, sc2, sh2, S, xn)
-            u = F.gelu(F.linear(xn, blk.ff.net[0].proj.weight, blk.ff.net[0].proj.bias), approximate="tanh")
-            K.gate_add(x, F.linear(u, blk.ff.net[2].weight, blk.ff.net[2].bias), g2, S)
+            u = F.gelu(lin(xn, blk.ff.net[0].proj.weight, blk.ff.net[0].proj.bias), approximate="tanh")
+            K.gate_add(x, lin(u, blk.ff.net[2].weight, blk.ff.net[2].bias), g2, S)
             if not blk.pre_only:
                 csh, csc, cg, csh2, csc2, cg2 = (mc[:, k * D:(k + 1) * D] for k in range(6))
-                yc = torch.matmul(o[:, S:], a.to_add_out.weight.t()) + a.to_add_out.bias
+                yc = lin(o[:, S:], a.to_add_out.weight, a.to_add_out.bias)
                 K.gate_add(cx, yc.reshape(B * T, D), cg, T)
                 K.layernorm_mod(cx, csc2, csh2, T, cn)
-                u = F.gelu(F.linear(cn, blk.ff_context.net[0].proj.weight, blk.ff_context.net[0].proj.bias),
+                u = F.gelu(lin(cn, blk.ff_context.net[0].proj.weight, blk.ff_context.net[0].proj.bias),
                            approximate="tanh")
-                K.gate_add(cx, F.linear(u, blk.ff_context.net[2].weight, blk.ff_context.net[2].bias), cg2, T)
+                K.gate_add(cx, lin(u, blk.ff_context.net[2].weight, blk.ff_context.net[2].bias), cg2, T)
         on = P["offs"][-1]
         K.layernorm_mod(x, mod[:, on:on + D], mod[:, on + D:on + 2 * D], S, xn)
-        out = F.linear(xn, self.proj_out.weight, self.proj_out.bias).float()
+        out = lin(xn, self.proj_out.weight, self.proj_out.bias).float()
         out = out.view(B, h, w, p, p, c.out_channels).permute(0, 5, 1, 3, 2, 4).reshape(B, c.out_channels, Hh, Ww)
         return out

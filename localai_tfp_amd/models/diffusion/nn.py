@@ -7,6 +7,11 @@ MFMA flash kernel (attention_dense.hip, head dim <= 128; larger heads — only t
 single 512-wide head — use PyTorch SDPA), adaLN / gated residual / GroupNorm kernels
 (diffusion.hip), and convolutions on the implicit-GEMM MFMA kernel (conv.hip, ops/conv.py) over
 channels_last (NHWC) activations, with bias / time-embedding / residual / SiLU / 2x upsampling fused.
+
+Linear weights may also be `QParam`s — ggml block-quantised matrices from a GGUF checkpoint kept in their
+block format on the GPU (stable-diffusion.cpp's Q4_0 / Q8_0 / K-quant files; reference gosd.cpp:56-162)
+and run through the quantised GEMM (`ops.linear.qmatmul`) instead of being densified at load. Every
+linear of the diffusion models goes through `lin` / `cat_w`, which accept either kind.
 """
 from __future__ import annotations
 
@@ -19,7 +24,80 @@ from torch import nn
 
 from ...ops import conv as CV
 from ...ops import core as K
+from ...ops import linear as L
 from ...ops.linear import _fp32_out_ok
+
+
+class QParam:
+    """A [N, K] linear weight held block-quantised (ops.linear.QWeight, ggml row layout) in place of an
+    nn.Linear's dense parameter. `dtype` is the pipeline's compute dtype (activations in and out)."""
+
+    def __init__(self, qw: "L.QWeight", dtype):
+        self.qw, self.dtype = qw, dtype
+
+    @classmethod
+    def from_ggml(cls, raw, qtype: int, N_: int, K_: int, device, dtype):
+        """QParam, or a dense tensor when the block format / shape has no quantised kernel."""
+        qw = L.QWeight.from_ggml(raw, qtype, N_, K_, device, dense_dtype=dtype)
+        if not qw.is_quant and torch.device(device).type != "cpu":
+            return qw.data.to(dtype)
+        return cls(qw, dtype)  # CPU: the ggml bytes, dequantised by the reference GEMM
+
+    @property
+    def shape(self):
+        return torch.Size((self.qw.N, self.qw.K))
+
+    @property
+    def device(self):
+        return self.qw.device
+
+    def dim(self) -> int:
+        return 2
+
+    def nbytes(self) -> int:
+        return self.qw.nbytes() if self.qw.data.numel() else int(getattr(self.qw._raw, "nbytes", 0))
+
+    def dense(self) -> torch.Tensor:
+        if self.qw.data.is_cuda:
+            return self.qw.dequant_gpu(self.dtype if self.dtype in (torch.bfloat16, torch.float16) else torch.float32)
+        return self.qw.dense_f32().to(self.dtype)
+
+    def linear(self, x: torch.Tensor, b: torch.Tensor | None = None) -> torch.Tensor:
+        lead, K_ = x.shape[:-1], x.shape[-1]
+        x2 = x.reshape(-1, K_)
+        cdt = x2.dtype
+        if x2.is_cuda and cdt not in (torch.bfloat16, torch.float16):
+            x2 = x2.to(self.dtype if self.dtype in (torch.bfloat16, torch.float16) else torch.bfloat16)
+        x2 = x2.contiguous()
+        out = torch.empty(x2.shape[0], self.qw.N, dtype=x2.dtype, device=x2.device)
+        L.qmatmul(self.qw, x2, L.EPI_BF16, out)
+        if b is not None:
+            out += b.to(out.dtype)
+        return out.to(cdt).view(*lead, self.qw.N)
+
+    @staticmethod
+    def concat(ws: list["QParam"]):
+        q = L.concat_rows([w.qw for w in ws])
+        return QParam(q, ws[0].dtype) if q is not None else None
+
+
+def lin(x: torch.Tensor, w, b: torch.Tensor | None = None) -> torch.Tensor:
+    """F.linear over a dense weight or a QParam."""
+    if isinstance(w, QParam):
+        return w.linear(x, b)
+    return F.linear(x, w, b)
+
+
+def cat_w(ws: list) -> "torch.Tensor | QParam":
+    """Row-concatenation of linear weights for a fused GEMM (Q|K|V, all adaLN modulations, ...): quantised
+    weights of one block format stay quantised; a mix is densified."""
+    if not any(isinstance(w, QParam) for w in ws):
+        return torch.cat(ws)
+    if all(isinstance(w, QParam) for w in ws):
+        q = QParam.concat(ws)
+        if q is not None:
+            return q
+    return torch.cat([w.dense() if isinstance(w, QParam) else w for w in ws])
 
 
 def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, B: int, Sq: int, Sk: int, H: int, D: int,
@@ -41,6 +119,9 @@ def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, B: int, Sq: int
 
 def linear_acc(x: torch.Tensor, lin: nn.Linear, acc: torch.Tensor) -> torch.Tensor:
     """acc (fp32) += lin(x): the residual add runs as GEMM beta = 1 where the build supports fp32 out."""
+    if isinstance(lin.weight, QParam):
+        acc.add_(lin.weight.linear(x, lin.bias).float())
+        return acc
     if x.is_cuda and x.dtype != torch.float32 and _fp32_out_ok(x.dtype) and acc.is_contiguous():
         if lin.bias is not None:
             acc.add_(lin.bias)
@@ -51,6 +132,8 @@ def linear_acc(x: torch.Tensor, lin: nn.Linear, acc: torch.Tensor) -> torch.Tens
 
 
 def linear_f32(x: torch.Tensor, lin: nn.Linear) -> torch.Tensor:
+    if isinstance(lin.weight, QParam):
+        return lin.weight.linear(x, lin.bias).float()
     if x.is_cuda and x.dtype != torch.float32 and _fp32_out_ok(x.dtype):
         out = torch.empty(x.shape[0], lin.out_features, dtype=torch.float32, device=x.device)
         if lin.bias is not None:

@@ -38,6 +38,12 @@ class SD3Preset:
 _CLIP_T1 = CLIPTextConfig(vocab=600, hidden=32, layers=2, heads=2, ffn=64, proj=32)
 _CLIP_T2 = CLIPTextConfig(vocab=600, hidden=32, layers=2, heads=2, ffn=64, act="gelu", proj=32)
 _T5_T = T5Config(vocab=300, d_model=64, heads=2, d_kv=32, d_ff=128, layers=2)
+# quantisation tests: every GEMM dimension a multiple of 256 so GGUF block weights stay quantised
+_CLIP_Q1 = CLIPTextConfig(vocab=600, hidden=256, layers=2, heads=4, ffn=512, proj=256)
+_CLIP_Q2 = CLIPTextConfig(vocab=600, hidden=256, layers=2, heads=4, ffn=512, act="gelu", proj=256)
+_T5_Q = T5Config(vocab=300, d_model=512, heads=4, d_kv=64, d_ff=512, layers=2)
+_MMDITX_Q = MMDiTConfig(layers=3, heads=4, joint_dim=512, caption_dim=256, pooled_dim=512, pos_max=32, sample_size=16,
+                        qk_norm=True, dual_attention_layers=(0, 1))
 PRESETS = {
     "sd3-medium": SD3Preset(SD3_MEDIUM, CLIP_L, CLIP_G, T5_XXL, VAE_SD3),
     "sd3-medium-no-t5": SD3Preset(SD3_MEDIUM, CLIP_L, CLIP_G, None, VAE_SD3),
@@ -45,6 +51,7 @@ PRESETS = {
     "sd3.5-large": SD3Preset(SD35_LARGE, CLIP_L, CLIP_G, T5_XXL, VAE_SD3),
     "sd3-test": SD3Preset(MMDIT_TEST, _CLIP_T1, _CLIP_T2, _T5_T, VAE_TEST, t5_tokens=16),
     "sd3.5m-test": SD3Preset(MMDITX_TEST, _CLIP_T1, _CLIP_T2, _T5_T, VAE_TEST, t5_tokens=16),
+    "sd3.5m-qtest": SD3Preset(_MMDITX_Q, _CLIP_Q1, _CLIP_Q2, _T5_Q, VAE_TEST, t5_tokens=16),
 }
 
 

@@ -16,8 +16,10 @@ modules:
   last context block, ln_q / ln_k QK-norm) with text_encoders.{clip_l,clip_g,t5xxl}.transformer.*;
 * LDM VAE (first_stage_model. or a bare ae.safetensors): down/up/mid blocks renamed, up blocks
   reversed, 1x1-conv attention weights flattened to linears.
-GGUF tensors are dequantised on load to the pipeline's 16-bit dtype (the diffusion GEMMs run on
-dense operands; the quantised-LLM kernels' t32 layouts are not used for these models yet).
+GGUF block-quantised matrices (Q4_0 / Q5_0 / Q8_0 / Q4_K / Q6_K / Q2_K ... with K % 256 == 0) stay
+quantised: they travel through the name mapping as `GGMLTensor`s (row slices and row concatenations act
+on the ggml bytes) and every nn.Linear weight among them becomes a `nn.QParam` run by the quantised
+GEMM; only non-linear tensors (embeddings, convolutions, norms) are dequantised at load.
 Tokenizer files (CLIP vocab.json + merges.txt, T5 spiece.model) are searched next to the model and
 component files; without them a byte-level stand-in is used and a warning logged.
 """
@@ -34,8 +36,71 @@ log = logging.getLogger("localai_tfp_amd.diffusion")
 
 
 # ---------------------------------------------------------------- reading
-def read_tensors(path: str) -> dict[str, torch.Tensor]:
-    """All tensors of a .safetensors / .gguf / .ckpt|.pt file (fp32 for GGUF block formats)."""
+class GGMLTensor:
+    """A GGUF block-quantised [N, K] matrix in its ggml row bytes. Supports what the name mappings do to
+    weights — `.shape`, row slices, `torch.cat` along rows — without dequantising; anything else
+    (a reshape, arithmetic) dequantises to fp32 first."""
+
+    def __init__(self, raw: np.ndarray, qtype: int, n: int, k: int):
+        self.raw, self.qtype, self.n, self.k = raw.reshape(n, -1), int(qtype), int(n), int(k)
+
+    @property
+    def shape(self):
+        return torch.Size((self.n, self.k))
+
+    ndim = 2
+
+    def dim(self) -> int:
+        return 2
+
+    def contiguous(self):
+        return self
+
+    def dense(self) -> torch.Tensor:
+        from ...ops.quant import dequantize
+        return torch.from_numpy(np.ascontiguousarray(dequantize(self.raw, self.qtype, (self.k, self.n))).reshape(
+            self.n, self.k).copy())
+
+    def __getitem__(self, idx):
+        if isinstance(idx, slice) and idx.step in (None, 1):
+            r = self.raw[idx]
+            return GGMLTensor(r, self.qtype, r.shape[0], self.k)
+        return self.dense()[idx]
+
+    @classmethod
+    def __torch_function__(cls, func, types, args=(), kwargs=None):
+        kwargs = kwargs or {}
+        if func is torch.cat and kwargs.get("dim", args[1] if len(args) > 1 else 0) == 0:
+            parts = list(args[0])
+            if all(isinstance(p, GGMLTensor) and p.qtype == parts[0].qtype and p.k == parts[0].k for p in parts):
+                raw = np.concatenate([p.raw for p in parts], 0)
+                return GGMLTensor(raw, parts[0].qtype, raw.shape[0], parts[0].k)
+
+        def dq(a):
+            if isinstance(a, GGMLTensor):
+                return a.dense()
+            if isinstance(a, (list, tuple)):
+                return type(a)(dq(x) for x in a)
+            return a
+        return func(*dq(tuple(args)), **{k: dq(v) for k, v in kwargs.items()})
+
+    def __getattr__(self, name):  # any other tensor method: on the dequantised matrix
+        if name.startswith("__"):
+            raise AttributeError(name)
+        return getattr(self.dense(), name)
+
+
+def _keep_quant(ti) -> bool:
+    from ...formats.gguf import QType
+    from ...ops import quant as Q
+    q = QType(ti.qtype)
+    return (len(ti.shape) == 2 and ti.shape[0] % 256 == 0 and
+            q in (*Q.GPU_NATIVE, *Q.Q8_EXACT, *Q.Q8_REQUANT))
+
+
+def read_tensors(path: str, keep_quant: bool = False) -> dict[str, torch.Tensor]:
+    """All tensors of a .safetensors / .gguf / .ckpt|.pt file. GGUF block formats: fp32, or with
+    keep_quant GGMLTensors for the matrices a quantised GEMM can run (see _keep_quant)."""
     if path.endswith(".safetensors"):
         from safetensors import safe_open
         out = {}
@@ -49,6 +114,9 @@ def read_tensors(path: str) -> dict[str, torch.Tensor]:
         r = GGUFReader(path)
         out = {}
         for name, ti in r.tensors.items():
+            if keep_quant and _keep_quant(ti):
+                out[name] = GGMLTensor(np.array(r.tensor_bytes(name)), ti.qtype, ti.shape[1], ti.shape[0])
+                continue
             a = dequantize(r.tensor_bytes(name), ti.qtype, ti.shape)
             out[name] = torch.from_numpy(np.ascontiguousarray(a).reshape(tuple(reversed(ti.shape))).copy())
         return out
@@ -347,15 +415,42 @@ def _dirs(*paths) -> list[str]:
 
 def _load(make, sd: dict, what: str, device, dtype, allow_missing=("position_ids",)):
     """Build the module directly on the target device (a 12B Flux transformer is not staged in host
-    RAM twice), load the converted weights, cast to the pipeline dtype."""
-    from .nn import cast_module
+    RAM twice), load the converted weights, cast to the pipeline dtype. GGMLTensor weights of nn.Linear
+    layers become QParams (kept quantised); other GGMLTensors are dequantised."""
+    from torch import nn as tnn
+    from .nn import QParam, cast_module
     with torch.device(device):
         module = make()
-    missing, _ = module.load_state_dict(sd, strict=False)
-    missing = [k for k in missing if not any(a in k for a in allow_missing)]
+    dense, quant = {}, {}
+    for k, v in sd.items():
+        if isinstance(v, GGMLTensor):
+            mname, _, leaf = k.rpartition(".")
+            try:
+                mod = module.get_submodule(mname)
+            except AttributeError:
+                mod = None
+            if leaf == "weight" and isinstance(mod, tnn.Linear) and tuple(mod.weight.shape) == tuple(v.shape):
+                quant[k] = (mod, v)
+                continue
+            v = v.dense()
+        dense[k] = v
+    missing, _ = module.load_state_dict(dense, strict=False)
+    missing = [k for k in missing if k not in quant and not any(a in k for a in allow_missing)]
     if missing:
         raise ValueError(f"{what}: missing weights {missing[:5]} ({len(missing)} in all)")
-    return cast_module(module, device, dtype).eval()
+    module = cast_module(module, device, dtype).eval()
+    nq = 0
+    for k, (mod, v) in quant.items():
+        qp = QParam.from_ggml(v.raw, v.qtype, v.n, v.k, device, dtype)
+        del mod._parameters["weight"]
+        if isinstance(qp, QParam):
+            mod.weight = qp
+            nq += 1
+        else:
+            mod.weight = tnn.Parameter(qp, requires_grad=False)
+    if quant:
+        log.info("%s: %d of %d linear weights kept block-quantised", what, nq, len(quant))
+    return module
 
 
 # ---------------------------------------------------------------- pipelines
@@ -367,7 +462,7 @@ def flux_from_single_file(model: str, device, clip_l_path: str = "", t5xxl_path:
     from .vae import AutoencoderKL
     dev = torch.device(device)
     dtype = dtype or (torch.bfloat16 if dev.type == "cuda" else torch.float32)
-    raw = read_tensors(model)
+    raw = read_tensors(model, keep_quant=True)
     if not vae_path and any(k.startswith("vae.") for k in raw):
         vae_sd = ldm_vae_to_diffusers(strip(raw, "vae."))
     else:
@@ -381,10 +476,10 @@ def flux_from_single_file(model: str, device, clip_l_path: str = "", t5xxl_path:
     del tsd
     if not clip_l_path or not t5xxl_path:
         raise ValueError("Flux needs clip_l_path:<clip_l.safetensors> and t5xxl_path:<t5xxl.safetensors|gguf>")
-    csd = read_tensors(clip_l_path)
+    csd = read_tensors(clip_l_path, keep_quant=True)
     csd = strip(csd, "text_encoders.clip_l.transformer.") or csd
     cl = _load(lambda: CLIPTextEncoder(clip_config_from(csd)), csd, "clip_l", dev, dtype)
-    t5sd = read_tensors(t5xxl_path)
+    t5sd = read_tensors(t5xxl_path, keep_quant=True)
     t5c = t5_config_from(t5sd)
     t5 = _load(lambda: T5Encoder(t5c), t5sd, "t5xxl", dev, dtype)
     vae = _load(lambda: AutoencoderKL(vae_config_from(vae_sd, 0.3611, 0.1159)), vae_sd, "vae", dev, dtype)
@@ -405,7 +500,7 @@ def unet_from_single_file(model: str, device, kind: str, vae_path: str = "", cli
     import dataclasses
     dev = torch.device(device)
     dtype = dtype or (torch.float16 if dev.type == "cuda" else torch.float32)
-    raw = read_tensors(model)
+    raw = read_tensors(model, keep_quant=True)
     usd_ldm = strip(raw, "model.diffusion_model.")
     xl = kind == "sdxl"
     if xl:
@@ -430,7 +525,7 @@ def unet_from_single_file(model: str, device, kind: str, vae_path: str = "", cli
     scaling = 0.13025 if xl else 0.18215
     vae = _load(lambda: AutoencoderKL(vae_config_from(vae_sd, scaling, 0.0)), vae_sd, "vae", dev, dtype)
     if clip_l_path:
-        lsd = read_tensors(clip_l_path)
+        lsd = read_tensors(clip_l_path, keep_quant=True)
     else:
         lsd = strip(raw, "conditioner.embedders.0.transformer.") if xl else strip(raw, "cond_stage_model.transformer.")
     if not lsd and not xl and any(k.startswith("cond_stage_model.model.") for k in raw):  # SD2.x OpenCLIP-H
@@ -439,7 +534,7 @@ def unet_from_single_file(model: str, device, kind: str, vae_path: str = "", cli
                allow_missing=("position_ids", "text_projection"))
     t2 = None
     if xl:
-        gsd = read_tensors(clip_g_path) if clip_g_path else openclip_to_hf(strip(raw, "conditioner.embedders.1.model."))
+        gsd = read_tensors(clip_g_path, keep_quant=True) if clip_g_path else openclip_to_hf(strip(raw, "conditioner.embedders.1.model."))
         t2 = _load(lambda: CLIPTextEncoder(clip_config_from(gsd), with_projection=True), gsd, "clip_g", dev, dtype)
     del raw
     search = _dirs(model, clip_l_path, clip_g_path)
@@ -451,7 +546,7 @@ def unet_from_single_file(model: str, device, kind: str, vae_path: str = "", cli
 
 def _component(raw: dict, path: str, prefixes: tuple) -> dict:
     """A text encoder from its own file (any of the known prefixes stripped) or from the model file."""
-    src = read_tensors(path) if path else raw
+    src = read_tensors(path, keep_quant=True) if path else raw
     for p in prefixes:
         got = strip(src, p)
         if got:
@@ -468,7 +563,7 @@ def sd3_from_single_file(model: str, device, clip_l_path: str = "", clip_g_path:
     from .vae import AutoencoderKL
     dev = torch.device(device)
     dtype = dtype or (torch.bfloat16 if dev.type == "cuda" else torch.float32)
-    raw = read_tensors(model)
+    raw = read_tensors(model, keep_quant=True)
     msd = sai_mmdit_to_diffusers(raw)
     mc = mmdit_config_from(msd)
     mm = _load(lambda: MMDiT(mc), msd, "mmdit", dev, dtype, allow_missing=("pos_embed.pos_embed",))

@@ -16,7 +16,7 @@ import torch.nn.functional as F
 from torch import nn
 
 from ...ops import core as K
-from .nn import attention, layernorm16, linear_acc
+from .nn import attention, cat_w, layernorm16, lin, linear_acc
 
 
 @dataclass
@@ -92,7 +92,7 @@ class CLIPTextEncoder(nn.Module):
 
     def _fused(self):
         if self._qkv is None:
-            self._qkv = [(torch.cat([l.self_attn.q_proj.weight, l.self_attn.k_proj.weight, l.self_attn.v_proj.weight]),
+            self._qkv = [(cat_w([l.self_attn.q_proj.weight, l.self_attn.k_proj.weight, l.self_attn.v_proj.weight]),
                           torch.cat([l.self_attn.q_proj.bias, l.self_attn.k_proj.bias, l.self_attn.v_proj.bias]))
                          for l in self.text_model.encoder.layers]
         return self._qkv
@@ -114,12 +114,12 @@ class CLIPTextEncoder(nn.Module):
             if i == want:
                 sel = x.clone()
             h = layernorm16(x, l.layer_norm1.weight, l.layer_norm1.bias, c.eps, dt)
-            qkv = F.linear(h, wqkv, bqkv)
+            qkv = lin(h, wqkv, bqkv)
             o = attention(qkv[:, :c.hidden], qkv[:, c.hidden:2 * c.hidden], qkv[:, 2 * c.hidden:], B, S, S, H, D,
                           causal=True)
             linear_acc(o, l.self_attn.out_proj, x)
             h = layernorm16(x, l.layer_norm2.weight, l.layer_norm2.bias, c.eps, dt)
-            u = F.linear(h, l.mlp.fc1.weight, l.mlp.fc1.bias)
+            u = lin(h, l.mlp.fc1.weight, l.mlp.fc1.bias)
             u = u * torch.sigmoid(1.702 * u) if c.act == "quick_gelu" else F.gelu(u)
             linear_acc(u, l.mlp.fc2, x)
         final = F.layer_norm(x, (c.hidden,), tm.final_layer_norm.weight, tm.final_layer_norm.bias, c.eps)
@@ -129,7 +129,7 @@ class CLIPTextEncoder(nn.Module):
         eos_pos = (ids == eos_id).int().argmax(1)
         pooled = final3[torch.arange(B, device=ids.device), eos_pos]
         if self.text_projection is not None:
-            pooled = F.linear(pooled.to(dt), self.text_projection.weight).float()
+            pooled = lin(pooled.to(dt), self.text_projection.weight).float()
         return sel.view(B, S, -1), pooled
 
 
@@ -264,17 +264,17 @@ class T5Encoder(nn.Module):
             sa, ff = blk.layer[0], blk.layer[1]
             a = sa.SelfAttention
             h = self._rms(x, sa.layer_norm.weight, dt)
-            q, k, v = (F.linear(h, w.weight).view(B, S, c.heads, c.d_kv).transpose(1, 2) for w in (a.q, a.k, a.v))
+            q, k, v = (lin(h, w.weight).view(B, S, c.heads, c.d_kv).transpose(1, 2) for w in (a.q, a.k, a.v))
             o = F.scaled_dot_product_attention(q, k, v, attn_mask=bias.expand(B, -1, -1, -1).to(q.dtype), scale=1.0)
             o = o.transpose(1, 2).reshape(B * S, inner)
             linear_acc(o, a.o, x)
             h = self._rms(x, ff.layer_norm.weight, dt)
             d = ff.DenseReluDense
             if c.ff == "relu":
-                act = F.relu(F.linear(h, d.wi.weight))
+                act = F.relu(lin(h, d.wi.weight))
             else:
-                g = F.linear(h, d.wi_0.weight)
-                u = F.linear(h, d.wi_1.weight)
+                g = lin(h, d.wi_0.weight)
+                u = lin(h, d.wi_1.weight)
                 act = torch.empty_like(g)
                 K.glu(g, u, act, act="gelu_tanh")
             linear_acc(act, d.wo, x)

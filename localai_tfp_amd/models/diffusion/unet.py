@@ -24,7 +24,7 @@ import torch
 import torch.nn.functional as F
 from torch import nn
 
-from .nn import GroupNorm, attention, conv, layernorm16, linear_acc, timestep_embedding
+from .nn import GroupNorm, attention, cat_w, conv, layernorm16, lin, linear_acc, timestep_embedding
 
 
 @dataclass
@@ -138,24 +138,24 @@ class BasicTransformerBlock(nn.Module):
         dt = ctx.dtype
         a1 = self.attn1
         if a1._qkv is None or a1._qkv.device != a1.to_q.weight.device or a1._qkv.dtype != a1.to_q.weight.dtype:
-            a1._qkv = torch.cat([a1.to_q.weight, a1.to_k.weight, a1.to_v.weight])
+            a1._qkv = cat_w([a1.to_q.weight, a1.to_k.weight, a1.to_v.weight])
         h = layernorm16(x, self.norm1.weight, self.norm1.bias, 1e-5, dt)
-        qkv = F.linear(h, a1._qkv)
+        qkv = lin(h, a1._qkv)
         o = attention(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], B, S, S, H, D)
         linear_acc(o, a1.to_out[0], x)
         a2 = self.attn2
         Sc = ctx.shape[0] // B
         if a2._kv is None or a2._kv[0] is not ctx_key or a2._kv[1].device != ctx.device:
             # text K|V: once per generation, reused every sampler step
-            wkv = torch.cat([a2.to_k.weight, a2.to_v.weight])
-            a2._kv = (ctx_key, F.linear(ctx, wkv))
+            wkv = cat_w([a2.to_k.weight, a2.to_v.weight])
+            a2._kv = (ctx_key, lin(ctx, wkv))
         kv = a2._kv[1]
         h = layernorm16(x, self.norm2.weight, self.norm2.bias, 1e-5, dt)
-        q = F.linear(h, a2.to_q.weight)
+        q = lin(h, a2.to_q.weight)
         o = attention(q, kv[:, :C], kv[:, C:], B, S, Sc, H, D)
         linear_acc(o, a2.to_out[0], x)
         h = layernorm16(x, self.norm3.weight, self.norm3.bias, 1e-5, dt)
-        g = F.linear(h, self.ff.net[0].proj.weight, self.ff.net[0].proj.bias)
+        g = lin(h, self.ff.net[0].proj.weight, self.ff.net[0].proj.bias)
         inner = g.shape[1] // 2
         u = g[:, :inner] * F.gelu(g[:, inner:])
         linear_acc(u, self.ff.net[2], x)
@@ -173,8 +173,8 @@ class Transformer2DModel(nn.Module):
 
     def _lin(self, t, m):
         if isinstance(m, nn.Linear):
-            return F.linear(t, m.weight, m.bias)
-        return F.linear(t, m.weight.reshape(m.weight.shape[0], -1), m.bias)  # 1x1 conv on NHWC tokens
+            return lin(t, m.weight, m.bias)
+        return lin(t, m.weight.reshape(m.weight.shape[0], -1), m.bias)  # 1x1 conv on NHWC tokens
 
     def run(self, x, ctx, ctx_key):
         B, C, H, W = x.shape
@@ -289,7 +289,7 @@ class UNet2DConditionModel(nn.Module):
             tid = timestep_embedding(added["time_ids"].reshape(-1), c.addition_time_dim, True, 0.0).reshape(B, -1)
             emb = emb + self.add_embedding.run(torch.cat([added["text_embeds"], tid], -1).to(dt))
         w, b, sizes = self._time_proj()
-        tp = F.linear(F.silu(emb), w, b).split(sizes, -1)
+        tp = lin(F.silu(emb), w, b).split(sizes, -1)
         ti = iter(tp)
         ctx16 = ctx.reshape(-1, ctx.shape[-1]).to(dt).contiguous()
         key = ctx_key if ctx_key is not None else ctx

@@ -299,6 +299,20 @@ def quantize_q8_0(x: np.ndarray) -> np.ndarray:
     return out.reshape(-1)
 
 
+def quantize_q4_0(x: np.ndarray) -> np.ndarray:
+    """ggml quantize_row_q4_0: d = (signed max) / -8, codes x/d + 8.5 truncated into [0, 15]."""
+    x = np.asarray(x, np.float32).reshape(-1, 32)
+    idx = np.abs(x).argmax(1)
+    mx = x[np.arange(x.shape[0]), idx]
+    d = mx / -8.0
+    idd = np.where(d != 0, 1.0 / np.where(d != 0, d, 1.0), 0.0).astype(np.float32)
+    q = np.minimum(15, (x * idd[:, None] + 8.5).astype(np.int8)).astype(np.uint8)
+    out = np.empty((x.shape[0], 18), np.uint8)
+    out[:, 0:2] = d.astype(np.float16).view(np.uint8).reshape(-1, 2)
+    out[:, 2:] = q[:, :16] | (q[:, 16:] << 4)
+    return out.reshape(-1)
+
+
 def quantize_q4_k(x: np.ndarray) -> np.ndarray:
     x = np.asarray(x, np.float32).reshape(-1, 8, 32)
     lo = np.minimum(x.min(2), 0.0)
@@ -377,7 +391,7 @@ def quantize_q5_k(x: np.ndarray) -> np.ndarray:
     return out.reshape(-1)
 
 
-QUANTIZERS = {QType.Q4_K: quantize_q4_k, QType.Q6_K: quantize_q6_k, QType.Q8_0: quantize_q8_0, QType.Q5_K: quantize_q5_k}
+QUANTIZERS = {QType.Q4_0: quantize_q4_0, QType.Q4_K: quantize_q4_k, QType.Q6_K: quantize_q6_k, QType.Q8_0: quantize_q8_0, QType.Q5_K: quantize_q5_k}
 
 
 def random_quantized(rng: np.random.Generator, qtype: int, n_rows: int, row_len: int, std: float = 0.02) -> np.ndarray:
