@@ -203,7 +203,14 @@ enum MxQuantType : int {
     MXQ_Q8_0 = 8,
     MXQ_Q5_K = 13,
     MXQ_Q4_0 = 2,
+    // this framework's t32-only layouts of the 32-weight "scale (+ offset)" formats (ops/quant.py to_mxf):
+    // w = s * code + m per 32 weights, s / m f16; 4-bit (Q4_0 / Q4_1) or 5-bit (Q5_0 / Q5_1) codes
+    MXQ_MX4F = 240,
+    MXQ_MX5F = 241,
 };
+
+// 4 bits (n & 15) -> bit 0 of each byte of a word (bit i -> byte i)
+MX_DEV uint32_t mx_spread4(uint32_t n) { return ((n & 15u) * 0x00204081u) & 0x01010101u; }
 
 // Q4_K 6-bit packed (scale, min) for sub-block j (0..7) out of the 12 scale bytes.
 MX_DEV void q4k_scale_min(const uint8_t* q, int j, int& sc, int& m) {

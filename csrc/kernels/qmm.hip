@@ -43,21 +43,37 @@ template <>
 struct QmmFmt<MXQ_Q4_K> {
     static constexpr int UNIT = 4608, PER_UNIT = 4;       // bytes per group per kb; k-tiles per unit
     static constexpr int QOFF = 512, QSTRIDE = 1024, QB = 1024;
-    static constexpr int MOFF = 0, MB = 512;               // header chunks
+    static constexpr int MOFF = 0, MB = 512, MSTEP = 0;    // header chunks (the same for every k-tile)
+    static constexpr int DOFF = 0, DSTRIDE = 0, HAS_D = 0;
+};
+// MX4F / MX5F (5120 / 6144 B): [hdr: 2 halves x 32 x 16 B {f16 s[4], m[4]}: k-tiles 0-1 read half 0, 2-3 half 1]
+// [k-tile jq: 2 x (32 x 16 B) codes (+ MX5F: 32 x 8 B high bits)]
+template <>
+struct QmmFmt<MXQ_MX4F> {
+    static constexpr int UNIT = 5120, PER_UNIT = 4;
+    static constexpr int QOFF = 1024, QSTRIDE = 1024, QB = 1024;
+    static constexpr int MOFF = 0, MB = 512, MSTEP = 512;  // header half (jq >> 1)
+    static constexpr int DOFF = 0, DSTRIDE = 0, HAS_D = 0;
+};
+template <>
+struct QmmFmt<MXQ_MX5F> {
+    static constexpr int UNIT = 6144, PER_UNIT = 4;
+    static constexpr int QOFF = 1024, QSTRIDE = 1280, QB = 1280;
+    static constexpr int MOFF = 0, MB = 512, MSTEP = 512;
     static constexpr int DOFF = 0, DSTRIDE = 0, HAS_D = 0;
 };
 template <>
 struct QmmFmt<MXQ_Q6_K> {
     static constexpr int UNIT = 6784, PER_UNIT = 4;
     static constexpr int QOFF = 640, QSTRIDE = 1536, QB = 1536;
-    static constexpr int MOFF = 0, MB = 512;               // int8 scales
+    static constexpr int MOFF = 0, MB = 512, MSTEP = 0;    // int8 scales
     static constexpr int DOFF = 512, DSTRIDE = 0, HAS_D = 1;
 };
 template <>
 struct QmmFmt<MXQ_Q8_0> {
     static constexpr int UNIT = 2176, PER_UNIT = 1;
     static constexpr int QOFF = 128, QSTRIDE = 0, QB = 2048;
-    static constexpr int MOFF = 0, MB = 0;
+    static constexpr int MOFF = 0, MB = 0, MSTEP = 0;
     static constexpr int DOFF = 0, DSTRIDE = 0, HAS_D = 1;
 };
 
@@ -148,6 +164,61 @@ struct QmmB<MXQ_Q4_K> {
         return r;
     }
 };
+
+// MX4F / MX5F: the Q4_K fragment with the sub-block (scale, offset) read as f16 pairs from the header half; MX5F
+// ORs each code's bit 4 from the k-tile's 64-bit high-bit word (bit u = weight u = 16 S + 8 h + j)
+template <bool FIVE>
+struct QmmBMX {
+    u32x2 v0, v1;
+    uint32_t vh0, vh1;  // high-bit words pre-shifted by 8 h
+    u32x4 hd;
+    f16x2 s2[2], m2[2];
+    MX_DEV void load(const char* q, const char* m, const char*, int r, int h, int) {
+        hd = *(const u32x4*)(m + r * 16);
+        v0 = *(const u32x2*)(q + r * 16 + 8 * h);
+        v1 = *(const u32x2*)(q + (32 + r) * 16 + 8 * h);
+        if constexpr (FIVE) {
+            const u32x2 w = *(const u32x2*)(q + 1024 + r * 8);
+            vh0 = w[0] >> (8 * h);
+            vh1 = w[1] >> (8 * h);
+        }
+    }
+    MX_DEV void prep(int jq) {
+        const int w = jq & 1;  // entries 2w, 2w+1 of the header half
+        const f16x2 s = __builtin_bit_cast(f16x2, hd[w]), mm = __builtin_bit_cast(f16x2, hd[2 + w]);
+        s2[0] = (f16x2){s[0], s[0]};
+        s2[1] = (f16x2){s[1], s[1]};
+        m2[0] = (f16x2){mm[0], mm[0]};
+        m2[1] = (f16x2){mm[1], mm[1]};
+    }
+    template <int S>
+    MX_DEV f16x8 frag() const {
+        const u32x2 src = (S & 1) ? v1 : v0;
+        constexpr int sh = 4 * (S >> 1);
+        uint32_t t0 = (src[0] >> sh) & 0x0F0F0F0Fu, t1 = (src[1] >> sh) & 0x0F0F0F0Fu;
+        if constexpr (FIVE) {
+            const uint32_t hw = ((S >> 1) ? vh1 : vh0) >> (16 * (S & 1));
+            t0 |= mx_spread4(hw) << 4;
+            t1 |= mx_spread4(hw >> 4) << 4;
+        }
+        const f16x2 k = {(_Float16)1024.f, (_Float16)1024.f};
+        f16x2 p[4];
+        magic4(t0, p[0], p[1]);
+        magic4(t1, p[2], p[3]);
+        f16x8 r;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const f16x2 v = (p[i] - k) * s2[S >> 1] + m2[S >> 1];
+            r[2 * i] = v[0];
+            r[2 * i + 1] = v[1];
+        }
+        return r;
+    }
+};
+template <>
+struct QmmB<MXQ_MX4F> : QmmBMX<false> {};
+template <>
+struct QmmB<MXQ_MX5F> : QmmBMX<true> {};
 
 template <>
 struct QmmB<MXQ_Q6_K> {
@@ -324,7 +395,8 @@ qmm_kernel(const uint16_t* __restrict__ A, int lda, const uint8_t* __restrict__ 
                                                      (MX_LDS void*)(wb + G::Q_OFF + ci * 1024), 16, 0, 0);
             if constexpr (G::MI > 0) {
                 if (mact)
-                    __builtin_amdgcn_global_load_lds((const void*)(msrc + unit), (MX_LDS void*)(wb + G::M_OFF), 16, 0, 0);
+                    __builtin_amdgcn_global_load_lds((const void*)(msrc + unit + (jq >> 1) * F::MSTEP),
+                                                     (MX_LDS void*)(wb + G::M_OFF), 16, 0, 0);
             }
             if constexpr (G::DI > 0) {
                 if (mact)
@@ -620,6 +692,8 @@ extern "C" int mxk_qmm(int qtype, int epi, int wm, int wn, int nw, int ks, const
         case MXQ_Q4_K: QMM_EPI(MXQ_Q4_K) break;
         case MXQ_Q6_K: QMM_EPI(MXQ_Q6_K) break;
         case MXQ_Q8_0: QMM_EPI(MXQ_Q8_0) break;
+        case MXQ_MX4F: QMM_EPI(MXQ_MX4F) break;
+        case MXQ_MX5F: QMM_EPI(MXQ_MX5F) break;
     }
 #undef QMM_EPI
     return (int)hipErrorInvalidValue;

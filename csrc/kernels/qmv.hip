@@ -89,6 +89,59 @@ struct TUnit<MXQ_Q5_K> {
     }
 };
 
+// MX4F / MX5F (t32 unit of 256 weights): [hdr: 2 halves x 32 columns x 16 B {f16 s[4], f16 m[4]}]
+// [k-tile jq: 2 x (32 x 16 B) codes in the Q4_K nibble order (+ MX5F: 32 x 8 B high bits)]. The high bits of
+// k-tile jq are one little-endian 64-bit word per column: bit u = bit 4 of weight 64 jq + u.
+template <bool FIVE>
+struct TUnitMX {
+    static constexpr int KTB = FIVE ? 1280 : 1024, BYTES = 1024 + 4 * KTB, ELEMS = 256;
+    u32x4 h0, h1, q[4];
+    u32x2 qh[4];
+    MX_DEV void load(const uint8_t* u, int r, int h) {
+        h0 = *(const u32x4*)(u + r * 16);
+        h1 = *(const u32x4*)(u + 512 + r * 16);
+#pragma unroll
+        for (int jq = 0; jq < 4; ++jq) {
+            q[jq] = __builtin_nontemporal_load((const u32x4*)(u + 1024 + jq * KTB + h * 512 + r * 16));
+            if constexpr (FIVE) qh[jq] = __builtin_nontemporal_load((const u32x2*)(u + 1024 + jq * KTB + 1024 + r * 8));
+        }
+    }
+    MX_DEV static float hf(uint32_t w, int hi) { return half_to_f32(hi ? (w >> 16) : (w & 0xFFFF)); }
+    MX_DEV float dot(const int8_t* x, const float2* ds, int h) const {
+        float acc = 0.f, mins = 0.f;
+#pragma unroll
+        for (int jq = 0; jq < 4; ++jq) {
+            const u32x4 xl = *(const u32x4*)(x + 64 * jq + 16 * h);
+            const u32x4 xh = *(const u32x4*)(x + 64 * jq + 32 + 16 * h);
+            int il = 0, ih = 0;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                uint32_t lo = q[jq][i] & 0x0F0F0F0Fu, hi = (q[jq][i] >> 4) & 0x0F0F0F0Fu;
+                if constexpr (FIVE) {
+                    // weights 16 h + 4 i .. +3 (low nibbles) / 32 + 16 h + 4 i .. +3 (high nibbles) of the k-tile
+                    const uint32_t wl = qh[jq][0], wh = qh[jq][1];
+                    lo |= mx_spread4(wl >> (16 * h + 4 * i)) << 4;
+                    hi |= mx_spread4(wh >> (16 * h + 4 * i)) << 4;
+                }
+                il = __builtin_amdgcn_sdot4((int)lo, (int)xl[i], il, false);
+                ih = __builtin_amdgcn_sdot4((int)hi, (int)xh[i], ih, false);
+            }
+            const u32x4& hd = jq < 2 ? h0 : h1;
+            const int i0 = 2 * (jq & 1);  // sub-blocks 2 jq, 2 jq + 1 = entries i0, i0 + 1 of the half
+            const float s0 = hf(hd[0 + (i0 >> 1)], 0), s1 = hf(hd[0 + (i0 >> 1)], 1);
+            const float m0 = hf(hd[2 + (i0 >> 1)], 0), m1 = hf(hd[2 + (i0 >> 1)], 1);
+            const float2 dl = ds[2 * jq], dh = ds[2 * jq + 1];
+            acc += s0 * dl.x * (float)il + s1 * dh.x * (float)ih;
+            mins += m0 * dl.y + m1 * dh.y;  // {d, d*sum} covers the whole 32-block
+        }
+        return acc + (h == 0 ? mins : 0.f);
+    }
+};
+template <>
+struct TUnit<MXQ_MX4F> : TUnitMX<false> {};
+template <>
+struct TUnit<MXQ_MX5F> : TUnitMX<true> {};
+
 template <>
 struct TUnit<MXQ_Q6_K> {
     static constexpr int BYTES = 6784, ELEMS = 256;
@@ -330,6 +383,25 @@ __global__ __launch_bounds__(256) void dequant_t32_kernel(const uint8_t* __restr
             if constexpr (QT == MXQ_Q5_K) qv |= (int)(((hb >> (8 * i + 2 * jq + (u >> 5))) & 1) << 4);
             v[i] = d * (float)qv - m;
         }
+    } else if constexpr (QT == MXQ_MX4F || QT == MXQ_MX5F) {
+        constexpr int KTB = QT == MXQ_MX5F ? 1280 : 1024;
+        const uint8_t* base = W + ((size_t)g * (K / 256) + chunk) * (1024 + 4 * KTB);
+        const int jq = e >> 6, u = e & 63, b = u & 31, sb = 2 * jq + (u >> 5);
+        const uint8_t* kt = base + 1024 + jq * KTB;
+        const uint32_t qq = *(const uint32_t*)(kt + (b >> 4) * 512 + r * 16 + (b & 15));
+        const uint32_t hw = *(const uint32_t*)(base + (sb >> 2) * 512 + r * 16 + 4 * ((sb & 3) >> 1));
+        const uint32_t mw = *(const uint32_t*)(base + (sb >> 2) * 512 + r * 16 + 8 + 4 * ((sb & 3) >> 1));
+        const float s = half_to_f32((sb & 1) ? (hw >> 16) : (hw & 0xFFFF));
+        const float m = half_to_f32((sb & 1) ? (mw >> 16) : (mw & 0xFFFF));
+        const int sh = (u >> 5) * 4;
+        uint32_t hb = 0;
+        if constexpr (QT == MXQ_MX5F) hb = *(const uint32_t*)(kt + 1024 + r * 8 + (u >> 5) * 4) >> (u & 31);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            int qv = (int)((qq >> (8 * i + sh)) & 0xF);
+            if constexpr (QT == MXQ_MX5F) qv |= (int)((hb >> i) & 1) << 4;
+            v[i] = s * (float)qv + m;
+        }
     } else {
         const uint8_t* base = W + ((size_t)g * (K / 256) + chunk) * 6784;
         const int jq = e >> 6, u = e & 63, b = u & 31, s16 = u >> 4;
@@ -402,6 +474,8 @@ extern "C" int mxk_qmv(int qtype, int epi, const int8_t* xq, const float2* xds, 
         case MXQ_Q5_K: QMV_EPI(MXQ_Q5_K) break;
         case MXQ_Q6_K: QMV_EPI(MXQ_Q6_K) break;
         case MXQ_Q8_0: QMV_EPI(MXQ_Q8_0) break;
+        case MXQ_MX4F: QMV_EPI(MXQ_MX4F) break;
+        case MXQ_MX5F: QMV_EPI(MXQ_MX5F) break;
     }
 #undef QMV_EPI
 #undef QMV_M
@@ -433,6 +507,8 @@ extern "C" int mxk_qmv_x(int qtype, int epi, int src, const void* x, int ldx, co
         case MXQ_Q5_K: QMVX_EPI(MXQ_Q5_K) break;
         case MXQ_Q6_K: QMVX_EPI(MXQ_Q6_K) break;
         case MXQ_Q8_0: QMVX_EPI(MXQ_Q8_0) break;
+        case MXQ_MX4F: QMVX_EPI(MXQ_MX4F) break;
+        case MXQ_MX5F: QMVX_EPI(MXQ_MX5F) break;
     }
 #undef QMVX_EPI
 #undef QMVX_M
@@ -451,6 +527,8 @@ extern "C" int mxk_dequant_t32(int qtype, const uint8_t* W, const int* rows, int
             case MXQ_Q5_K: dequant_t32_kernel<MXQ_Q5_K, F16><<<grid, 256, 0, st>>>(W, rows, K, ob, of, ldo); break;
             case MXQ_Q6_K: dequant_t32_kernel<MXQ_Q6_K, F16><<<grid, 256, 0, st>>>(W, rows, K, ob, of, ldo); break;
             case MXQ_Q8_0: dequant_t32_kernel<MXQ_Q8_0, F16><<<grid, 256, 0, st>>>(W, rows, K, ob, of, ldo); break;
+            case MXQ_MX4F: dequant_t32_kernel<MXQ_MX4F, F16><<<grid, 256, 0, st>>>(W, rows, K, ob, of, ldo); break;
+            case MXQ_MX5F: dequant_t32_kernel<MXQ_MX5F, F16><<<grid, 256, 0, st>>>(W, rows, K, ob, of, ldo); break;
             default: rc = (int)hipErrorInvalidValue;
         }
     });

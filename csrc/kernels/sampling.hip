@@ -280,19 +280,25 @@ __global__ __launch_bounds__(SNT) void sample_kernel(float* __restrict__ logits,
     }
     for (int i = V4 + threadIdx.x; i < V; i += SNT) hist(val(i, x[i]));
     const float Z = bsum(Zt, red);
-    // lowest bin that must be kept: the first (from the top) where top-k's count or top-p's mass is reached;
-    // min-p caps it from above
+    // lowest bin that must be gathered. With top-k on, the candidates must hold the whole top-k set: top-p's
+    // target mass is top_p x the top-k set's mass (the bisection chain's semantics), so its mass is needed even
+    // where min-p later trims the set. With top-k off the target is top_p x Z (Z: the whole row) and the
+    // candidates stop at that mass; min-p caps the search wherever the top-k mass is not needed.
+    const bool tk = P.top_k > 0 && P.top_k < V, tp = P.top_p < 1.f && P.top_p > 0.f;
     if (threadIdx.x == 0) {
         int lim = SHB - 1;
-        if (P.min_p > 0.f && P.min_p <= 1.f) lim = min(lim, (int)(-__logf(P.min_p) * IBW));
+        if (P.min_p > 0.f && P.min_p <= 1.f && !(tk && tp)) lim = min(lim, (int)(-__logf(P.min_p) * IBW));
         unsigned c = 0;
         float m = 0.f;
         int b = 0;
         for (; b < lim; ++b) {
             c += hcnt[b];
             m += hmass[b];
-            if (P.top_k > 0 && c >= (unsigned)P.top_k) break;
-            if (P.top_p < 1.f && P.top_p > 0.f && m >= P.top_p * Z) break;
+            if (tk) {
+                if (c >= (unsigned)P.top_k) break;
+            } else if (tp && m >= P.top_p * Z) {
+                break;
+            }
         }
         s_bin = b;
         s_n = 0;
@@ -344,9 +350,11 @@ __global__ __launch_bounds__(SNT) void sample_kernel(float* __restrict__ logits,
             keep = P.top_k;
             while (keep < n && cv[keep] == kv) ++keep;
         }
-        float zk = 0.f;
-        if (P.top_p < 1.f && P.top_p > 0.f)
+        float zk = Z;  // top-k off: the whole row's mass
+        if (tp && tk) {
+            zk = 0.f;
             for (int k = 0; k < keep; ++k) zk += __expf(cv[k] - mx);
+        }
         if (P.min_p > 0.f && P.min_p <= 1.f) {
             const float mv = mx + __logf(P.min_p);
             while (keep > 1 && cv[keep - 1] < mv) --keep;

@@ -84,6 +84,10 @@ class QType(IntEnum):
     BF16 = 30
     TQ1_0 = 34
     TQ2_0 = 35
+    # this framework's GPU block layouts (never stored in a GGUF file): 4- / 5-bit codes with an f16 scale and
+    # offset per 32 weights, w = s * code + m — Q4_0 / Q4_1 / Q5_0 / Q5_1 rows re-laid out exactly (ops/quant.py)
+    MX4F = 240
+    MX5F = 241
 
 
 # (elements per block, bytes per block)
@@ -97,6 +101,7 @@ BLOCK = {
     QType.IQ2_XXS: (256, 66), QType.IQ2_XS: (256, 74), QType.IQ3_XXS: (256, 98), QType.IQ1_S: (256, 50),
     QType.IQ4_NL: (32, 18), QType.IQ3_S: (256, 110), QType.IQ2_S: (256, 82), QType.IQ4_XS: (256, 136),
     QType.IQ1_M: (256, 56), QType.TQ1_0: (256, 54), QType.TQ2_0: (256, 66),
+    QType.MX4F: (256, 160), QType.MX5F: (256, 192),
 }
 
 # GGUF file-type ids (general.file_type) for naming

@@ -33,6 +33,7 @@ import torch
 
 from ..formats.gguf import QType
 from ..ops import core as K
+from ..ops import quant as Q
 from ..ops.linear import (ACT_DTYPE, EPI_ADD_F32, EPI_BF16, EPI_F32, EPI_GEGLU, EPI_SWIGLU, QWeight, concat_rows,
                           _fp32_out_ok, dense_min_m, interleave_gate_up, qmatmul, qmatmul8, qmm8_ok, qmv_fusable,
                           qmv_fused)
@@ -229,7 +230,7 @@ class LlamaModel:
             if tp_size > 1 and split is not None and shard is not None and has(name):
                 # source that generates only this rank's slice (synthetic multi-GPU benches)
                 raw, qt, N_, K_ = shard(name, split, tp_rank, tp_size)
-                return QWeight.from_ggml(raw, qt, N_, K_, dev, name)
+                return QWeight.from_ggml(raw, qt, N_, K_, dev, name, t32=True)
             t = get_tensor(name)
             if t is None:
                 return None
@@ -238,7 +239,7 @@ class LlamaModel:
             raw = np.asarray(raw).view(np.uint8).reshape(N_, -1)  # ggml bytes, one row per output
             if tp_size > 1 and split is not None:
                 raw, N_, K_ = TP.shard_raw(raw, qt, N_, K_, split, tp_rank, tp_size, cfg)
-            return QWeight.from_ggml(raw, qt, N_, K_, dev, name)
+            return QWeight.from_ggml(raw, qt, N_, K_, dev, name, t32=True)
 
         def qw_rows(name, row_counts, splits):
             """Split a fused [sum(rows), K] ggml tensor into per-part QWeights (phi3 attn_qkv / ffn_up)."""
@@ -253,7 +254,7 @@ class LlamaModel:
                 N_ = n_
                 if tp_size > 1:
                     part, N_, K2 = TP.shard_raw(part, qt, N_, K_, sp, tp_rank, tp_size, cfg)
-                out.append(QWeight.from_ggml(np.ascontiguousarray(part), qt, N_, K_, dev, name))
+                out.append(QWeight.from_ggml(np.ascontiguousarray(part), qt, N_, K_, dev, name, t32=True))
             return out
 
         hd = cfg.head_dim
@@ -323,7 +324,7 @@ class LlamaModel:
         emb = get_tensor("token_embd.weight")
         raw, qt, shape = emb
         m.tok_embd = QWeight.from_ggml(np.asarray(raw).view(np.uint8).reshape(int(shape[1]), -1), qt,
-                                       int(shape[1]), int(shape[0]), dev, "token_embd")
+                                       int(shape[1]), int(shape[0]), dev, "token_embd", t32=True)
         m.out_norm = f32("output_norm.weight").float()
         if tp_size > 1:
             # vocab-parallel LM head: rank r holds vocab rows [r*V/tp, (r+1)*V/tp) (tied embeddings: a
@@ -338,7 +339,7 @@ class LlamaModel:
             lo, hi = min(V, tp_rank * vl), min(V, (tp_rank + 1) * vl)
             part = np.zeros((vl, rows.shape[1]), np.uint8)
             part[:hi - lo] = rows[lo:hi]  # zero rows past V: logits 0, trimmed after the gather
-            m.lm_head = QWeight.from_ggml(part, qt, vl, K_, dev, "output.shard")
+            m.lm_head = QWeight.from_ggml(part, qt, vl, K_, dev, "output.shard", t32=True)
         elif not has("output.weight"):
             m.lm_head = m.tok_embd
             cfg.tie_embeddings = True
@@ -362,8 +363,8 @@ class LlamaModel:
         if isinstance(self.lm_head, QWeight):
             self.lm_head.to_t32()  # tied embeddings follow (embed() reads either layout)
         if isinstance(self.tok_embd, QWeight) and self.tok_embd is not self.lm_head and \
-                int(self.tok_embd.qtype if self.tok_embd.is_quant else -1) == int(QType.Q5_K):
-            self.tok_embd.to_t32()  # Q5_K rows are gathered by the t32 dequant kernel
+                int(self.tok_embd.qtype if self.tok_embd.is_quant else -1) in (int(q) for q in Q.T32_ONLY):
+            self.tok_embd.to_t32()  # Q5_K / MX4F / MX5F rows are gathered by the t32 dequant kernel
         # anything a t32-only format left in the row layout (expert stacks, odd shapes) -> Q8_0 kernels
         ws = [self.tok_embd, self.lm_head]
         for L in self.layers:

@@ -59,14 +59,19 @@ class QWeight:
     # ---------------------------------------------------------------- construction
     @classmethod
     def from_ggml(cls, raw: np.ndarray, qtype: int, N_: int, K: int, device="cpu", name: str = "",
-                  dense_dtype=torch.bfloat16):
+                  dense_dtype=torch.bfloat16, t32: bool = False):
+        """t32: the caller re-lays the weight out with to_t32() (or ensure_kernel_layout()) before use, so
+        formats whose kernels exist only in the t32 layout (Q5_K, and Q4_0/Q4_1/Q5_0/Q5_1 as MX4F/MX5F) stay
+        in their own bit width; otherwise those run on the Q8_0 kernels."""
         qt = raw_qtype_in = QType(qtype)
         dev = torch.device(device)
         if dev.type == "cpu":
             # CPU: keep the ggml bytes, dequantise lazily for the reference path
             return cls(N_, K, int(qt) if qt in Q.GPU_NATIVE else "dense",
                        torch.empty(0), None, np.asarray(raw), int(qt), name)
-        t32_only_ok = N_ % 32 == 0 and ACT_DTYPE == torch.float16
+        t32_only_ok = t32 and N_ % 32 == 0 and ACT_DTYPE == torch.float16
+        if qt in Q.Q32_FAMILY and t32_only_ok and K % 256 == 0:
+            raw, qt = Q.to_mxf(raw, qt, N_, K)  # exact: 4/5-bit codes + f16 scale/offset per 32
         if qt in Q.T32_ONLY and not t32_only_ok and K % 256 == 0:
             raw, qt = Q.to_q8_0(raw, qt, N_, K), QType.Q8_0  # no t32 tiling possible: Q8_0 kernels
         if qt in (*Q.Q8_EXACT, *Q.Q8_REQUANT) and K % 256 == 0:
@@ -306,7 +311,7 @@ def _qmatmul_t32(W: QWeight, x, epi: int, out, xq, xds, M: int, out_zeroed: bool
         ks = 1
         if epi == EPI_ADD_F32 or (epi == EPI_F32 and out_zeroed):
             # narrow outputs (o_proj / down / qkv: N/32 groups < CUs): split K over workgroups, fp32 atomics
-            units = W.K // (64 if int(W.qtype) == int(QType.Q8_0) else 256)
+            units = W.K // Q.T32_UNIT[QType(int(W.qtype))][1]
             while (W.N // 32) * ks < 2 * CU_COUNT and units // (ks * 2) >= 2:
                 ks *= 2
         N.kcall("mxk_qmv", int(W.qtype), EPI_ADD_F32 if ks > 1 else epi, xq.data_ptr(), xds.data_ptr(),
@@ -314,7 +319,7 @@ def _qmatmul_t32(W: QWeight, x, epi: int, out, xq, xds, M: int, out_zeroed: bool
         return out
     if x is None or x.dtype != torch.float16:
         raise ValueError("qmatmul: t32 weights need f16 activations (or q8 activations with M <= 4)")
-    if int(W.qtype) in (int(q) for q in Q.T32_ONLY):
+    if int(W.qtype) in (int(q) for q in Q.QMM8_ONLY):
         # formats with int8-MFMA kernels only: quantise the rows to Q8_K on the fly
         from .core import Q8KAct, quant_q8k
         a = quant_q8k(x, Q8KAct.empty(M, W.K, x.device))

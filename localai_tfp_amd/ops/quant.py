@@ -263,6 +263,79 @@ _DQ = {
 }
 
 
+# ---- MX4F / MX5F: the t32 kernels' layout for the 32-weight "scale (+ offset)" formats ----------------
+# Row format per 256 weights (8 sub-blocks of 32), w = s_i * code + m_i exactly (Q4_0: m = -8 d; Q5_0: m = -16 d):
+#   [0:16)  f16 s0..s3, m0..m3   [16:32) f16 s4..s7, m4..m7          (header halves: k-tiles 0-1 / 2-3)
+#   MX4F: [32:160) codes in Q4_K order (byte 32 jq + b: low nibble = weight 64 jq + b, high = 64 jq + 32 + b)
+#   MX5F: per 64-weight k-tile jq: [32 B low-nibble codes as above | 8 B high bits, bit u of the k-tile's
+#         64-bit little-endian word = bit 4 of weight 64 jq + u]
+Q32_FAMILY = (QType.Q4_0, QType.Q4_1, QType.Q5_0, QType.Q5_1)
+
+
+def q32_parts(raw: np.ndarray, qtype: int):
+    """ggml Q4_0/Q4_1/Q5_0/Q5_1 blocks -> (codes uint8 [nb, 32], s f16 [nb], m f16 [nb]), w = s * code + m."""
+    q = QType(qtype)
+    b = _blocks(raw, q)
+    s = b[:, 0:2].copy().view(np.float16).reshape(-1)
+    if q in (QType.Q4_1, QType.Q5_1):
+        m = b[:, 2:4].copy().view(np.float16).reshape(-1)
+        o = 4
+    else:
+        m = (s.astype(np.float32) * (-8.0 if q == QType.Q4_0 else -16.0)).astype(np.float16)  # exact (x 2^k)
+        o = 2
+    if q in (QType.Q4_0, QType.Q4_1):
+        qs = b[:, o:o + 16]
+        codes = np.concatenate([qs & 0xF, qs >> 4], 1)
+    else:
+        hb = _q5_high(b[:, o:o + 4])
+        qs = b[:, o + 4:o + 20]
+        codes = np.concatenate([(qs & 0xF) | (hb[:, :16] << 4), (qs >> 4) | (hb[:, 16:] << 4)], 1)
+    return codes.astype(np.uint8), s, m
+
+
+def to_mxf(raw: np.ndarray, qtype: int, n_rows: int, row_len: int) -> tuple[np.ndarray, QType]:
+    """Q4_0/Q4_1 -> MX4F rows, Q5_0/Q5_1 -> MX5F rows (uint8 [n_rows, row_len / 256 * 160|192]); exact."""
+    q = QType(qtype)
+    codes, s, m = q32_parts(raw, q)
+    nu = row_len // 256
+    five = q in (QType.Q5_0, QType.Q5_1)
+    c = codes.reshape(n_rows, nu, 8, 32)
+    s8 = s.reshape(n_rows, nu, 2, 4)
+    m8 = m.reshape(n_rows, nu, 2, 4)
+    hdr = np.concatenate([s8, m8], 3).view(np.uint8).reshape(n_rows, nu, 32)
+    lo = (c[:, :, 0::2] & 0xF) | ((c[:, :, 1::2] & 0xF) << 4)  # [n, nu, 4 k-tiles, 32 bytes]
+    if not five:
+        body = lo.reshape(n_rows, nu, 128)
+    else:
+        hb = ((c >> 4) & 1).reshape(n_rows, nu, 4, 64)
+        qh8 = np.packbits(hb, axis=3, bitorder="little")  # [n, nu, 4, 8]
+        body = np.concatenate([lo, qh8], 3).reshape(n_rows, nu, 160)
+    out = np.concatenate([hdr, body], 2).astype(np.uint8)
+    return out.reshape(n_rows, -1), (QType.MX5F if five else QType.MX4F)
+
+
+def _dq_mxf(raw, five: bool):
+    B = 192 if five else 160
+    u = raw.reshape(-1, B)
+    hdr = u[:, :32].copy().view(np.float16).astype(np.float32).reshape(-1, 2, 2, 4)  # [nu, half, s|m, 4]
+    s = hdr[:, :, 0].reshape(-1, 8)
+    m = hdr[:, :, 1].reshape(-1, 8)
+    if five:
+        body = u[:, 32:].reshape(-1, 4, 40)
+        lo, qh8 = body[:, :, :32], body[:, :, 32:]
+        hb = np.unpackbits(qh8, axis=2, bitorder="little").reshape(-1, 4, 2, 32)
+    else:
+        lo = u[:, 32:].reshape(-1, 4, 32)
+        hb = np.zeros((u.shape[0], 4, 2, 32), np.uint8)
+    codes = np.stack([lo & 0xF, lo >> 4], 2) | (hb << 4)  # [nu, 4, 2, 32] = sub-block 2 jq + i
+    w = codes.reshape(-1, 8, 32).astype(np.float32) * s[:, :, None] + m[:, :, None]
+    return w.reshape(-1)
+
+
+_DQ[QType.MX4F] = lambda r: _dq_mxf(r, False)
+_DQ[QType.MX5F] = lambda r: _dq_mxf(r, True)
+
+
 def dequantize(raw: np.ndarray, qtype: int, shape) -> np.ndarray:
     """raw bytes (any shape) of a ggml tensor with ggml `shape` -> float32 numpy array of
     shape reversed(shape)."""
@@ -433,6 +506,15 @@ def random_quantized(rng: np.random.Generator, qtype: int, n_rows: int, row_len:
         d = np.full(nb, std / 73.6, np.float32)
         out[:, 0:2] = d.astype(np.float16).view(np.uint8).reshape(-1, 2)
         return out.reshape(-1)
+    if q in Q32_FAMILY:  # random codes, d per block around std / code-std, offsets centring the codes
+        out = rng.integers(0, 256, size=(nb, bb), dtype=np.uint8)
+        five = q in (QType.Q5_0, QType.Q5_1)
+        cstd, centre = (9.23, 15.5) if five else (4.61, 7.5)
+        d = (std / cstd) * rng.uniform(0.7, 1.3, nb).astype(np.float32)
+        out[:, 0:2] = d.astype(np.float16).view(np.uint8).reshape(-1, 2)
+        if q in (QType.Q4_1, QType.Q5_1):
+            out[:, 2:4] = (-d * centre * rng.uniform(0.9, 1.1, nb)).astype(np.float16).view(np.uint8).reshape(-1, 2)
+        return out.reshape(-1)
     if q == QType.F32:
         return (rng.standard_normal(nel, dtype=np.float32) * std).view(np.uint8)
     if q == QType.F16:
@@ -470,10 +552,11 @@ def repack_q8_0(raw: np.ndarray, n_rows: int, row_len: int):
     return np.ascontiguousarray(qs), np.ascontiguousarray(d)
 
 
-GPU_NATIVE = (QType.Q4_K, QType.Q6_K, QType.Q8_0, QType.Q5_K)
-# native only in the t32 tiled layout (qmv / qmm8 / dequant_t32 kernels); a Q5_K weight that cannot be tiled
-# (N % 32, expert stacks) is carried on the Q8_0 kernels instead (QWeight.ensure_kernel_layout)
-T32_ONLY = (QType.Q5_K,)
+GPU_NATIVE = (QType.Q4_K, QType.Q6_K, QType.Q8_0, QType.Q5_K, QType.MX4F, QType.MX5F)
+# native only in the t32 tiled layout (qmv / qmm / qmm8 / dequant_t32 kernels); a weight of these formats that
+# cannot be tiled (N % 32, expert stacks) is carried on the Q8_0 kernels instead (QWeight.ensure_kernel_layout)
+T32_ONLY = (QType.Q5_K, QType.MX4F, QType.MX5F)
+QMM8_ONLY = (QType.Q5_K,)  # M > 4 through the int8-MFMA GEMM on Q8_K activations (no f16 qmm variant)
 
 # Block formats without a dedicated kernel layout yet, carried on the Q8_0 kernels (qmm / qmv) instead of
 # a dense 16-bit copy: the integer code of every weight is kept EXACTLY where the format is "scale x
@@ -488,6 +571,18 @@ def to_q8_0(raw: np.ndarray, qtype: int, n_rows: int, row_len: int) -> np.ndarra
     """ggml rows of another block format -> Q8_0 rows [n_rows, row_len/32 * 34] (see Q8_EXACT)."""
     q = QType(qtype)
     w = dequantize(raw, q, (row_len, n_rows)).reshape(-1, 32)
+    if q in (QType.MX4F, QType.MX5F):  # exact where the block's offset is a code multiple (Q4_0 / Q5_0 origin)
+        s = np.asarray(raw).reshape(-1, 192 if q == QType.MX5F else 160)[:, :32].copy().view(np.float16)
+        d16 = s.reshape(-1, 2, 2, 4)[:, :, 0].reshape(-1)
+        safe = np.where(d16.astype(np.float32) != 0, d16.astype(np.float32), 1.0)
+        ci = np.rint(w / safe[:, None])
+        out = np.empty((w.shape[0], 34), np.uint8)
+        out[:, 0:2] = d16.view(np.uint8).reshape(-1, 2)
+        out[:, 2:] = np.clip(ci, -127, 127).astype(np.int8).view(np.uint8)
+        bad = (np.abs(ci).max(1) > 127) | (np.abs(ci * d16.astype(np.float32)[:, None] - w).max(1) > 0)
+        if bad.any():
+            out[bad] = quantize_q8_0(w[bad]).reshape(-1, 34)
+        return out.reshape(n_rows, -1)
     if q not in Q8_EXACT:
         return quantize_q8_0(w).reshape(n_rows, -1)
     b = _blocks(np.asarray(raw).reshape(-1).view(np.uint8), q)
@@ -513,7 +608,7 @@ def to_q8_0(raw: np.ndarray, qtype: int, n_rows: int, row_len: int) -> np.ndarra
 def repack_for_gpu(raw: np.ndarray, qtype: int, n_rows: int, row_len: int):
     """-> (data uint8 [n_rows, bytes_per_row], dplane uint16 [n_rows, x] or None)."""
     q = QType(qtype)
-    if q in (QType.Q4_K, QType.Q5_K):
+    if q in (QType.Q4_K, QType.Q5_K, QType.MX4F, QType.MX5F):
         return np.ascontiguousarray(np.asarray(raw).reshape(n_rows, -1)), None
     if q == QType.Q6_K:
         return repack_q6_k(raw, n_rows, row_len)
@@ -522,7 +617,8 @@ def repack_for_gpu(raw: np.ndarray, qtype: int, n_rows: int, row_len: int):
     raise NotImplementedError(f"{q.name} has no native GPU layout")
 
 
-T32_UNIT = {QType.Q4_K: (4608, 256), QType.Q6_K: (6784, 256), QType.Q8_0: (2176, 64), QType.Q5_K: (5632, 256)}
+T32_UNIT = {QType.Q4_K: (4608, 256), QType.Q6_K: (6784, 256), QType.Q8_0: (2176, 64), QType.Q5_K: (5632, 256),
+            QType.MX4F: (5120, 256), QType.MX5F: (6144, 256)}
 
 
 def tile32(data, dplane, qtype: int, n_rows: int, row_len: int):
@@ -553,6 +649,18 @@ def tile32(data, dplane, qtype: int, n_rows: int, row_len: int):
         qh = b[..., 16:48].reshape(G, 32, nb, 2, 16).permute(0, 2, 3, 1, 4).reshape(G, nb, 1024)
         qs = b[..., 48:].reshape(G, 32, nb, 4, 2, 16).permute(0, 2, 3, 4, 1, 5).reshape(G, nb, 4096)
         out = torch.cat([hdr, qs, qh], 2)
+    elif q in (QType.MX4F, QType.MX5F):
+        # rows [hdr 32 | k-tile bodies] -> [hdr: 2 halves x 32 x 16 B][k-tile jq: 2 x (32 x 16 B codes) (+ 32 x 8 B qh8)]
+        nb = row_len // 256
+        kb = 40 if q == QType.MX5F else 32
+        b = t.reshape(G, 32, nb, 32 + 4 * kb)
+        hdr = b[..., :32].reshape(G, 32, nb, 2, 16).permute(0, 2, 3, 1, 4).reshape(G, nb, 1024)
+        body = b[..., 32:].reshape(G, 32, nb, 4, kb)
+        codes = body[..., :32].reshape(G, 32, nb, 4, 2, 16).permute(0, 2, 3, 4, 1, 5).reshape(G, nb, 4, 1024)
+        if q == QType.MX5F:
+            qh8 = body[..., 32:].permute(0, 2, 3, 1, 4).reshape(G, nb, 4, 256)
+            codes = torch.cat([codes, qh8], 3)
+        out = torch.cat([hdr, codes.reshape(G, nb, -1)], 2)
     elif q == QType.Q6_K:
         nb = row_len // 256
         b = t.reshape(G, 32, nb, 208)

@@ -382,7 +382,7 @@ def test_qmm(qt, M, wm, wn, nw, ks, splits, monkeypatch):
     monkeypatch.setattr(L, "QMM_FORCE", (wm, wn, nw, ks, splits))
     n, k = 416, 2304  # 416 = 3.25 x 128 columns: partial column tiles (multiple of 32 for the GLU)
     raw, dense = make_w(qt, n, k, seed=M + 7 * wm)
-    W = QWeight.from_ggml(raw, qt, n, k, DEV)
+    W = QWeight.from_ggml(raw, qt, n, k, DEV, t32=True)
     assert W.to_t32() and W.layout == "t32"
     x = torch.randn(M, k, device=DEV).half()
     ref = x.float().cpu() @ dense.t()
@@ -415,7 +415,7 @@ def test_qmatmul_llama3_8b_shapes(name, qt, n, k, epi, M):
     """Production Llama-3-8B projection shapes through the DEFAULT dispatch (qmm tiles and split-K as
     chosen for these M) against an fp32 reference of the dequantised weight."""
     raw, dense = make_w(qt, n, k, seed=n + k + M)
-    W = QWeight.from_ggml(raw, qt, n, k, DEV)
+    W = QWeight.from_ggml(raw, qt, n, k, DEV, t32=True)
     assert W.to_t32()
     torch.manual_seed(M)
     x = torch.randn(M, k, device=DEV).half()
@@ -445,7 +445,7 @@ def test_qmv_t32(qt, M):
     dequantisation (embedding gather), against fp32 references."""
     n, k = 384, 2816
     raw, dense = make_w(qt, n, k, seed=11 * M)
-    W = QWeight.from_ggml(raw, qt, n, k, DEV)
+    W = QWeight.from_ggml(raw, qt, n, k, DEV, t32=True)
     assert W.to_t32()
     x = torch.randn(M, k, device=DEV).half()
     xq = torch.empty(M, k, dtype=torch.int8, device=DEV)

@@ -75,7 +75,7 @@ def test_qmm8_configs(qt, cfg, monkeypatch):
     dequantised-operand fp32 product (tight) and the unquantised product (loose)."""
     n, k = 416, 2304  # partial column tiles; 9 super-blocks (odd split counts)
     raw, dense = make_w(qt, n, k, seed=sum(cfg) + 3)
-    W = QWeight.from_ggml(raw, qt, n, k, DEV)
+    W = QWeight.from_ggml(raw, qt, n, k, DEV, t32=True)
     monkeypatch.setattr(L, "QMM8", True)
     assert W.to_t32() and L.qmm8_ok(W)
     for M, splits in ((77, 1), (130, 3)):
@@ -115,7 +115,7 @@ def test_qmm8_configs(qt, cfg, monkeypatch):
 def test_qmm8_llama3_8b_shapes(name, qt, n, k, epi, M):
     """Llama-3-8B projection shapes through the default int8 dispatch against fp32 references."""
     raw, dense = make_w(qt, n, k, seed=n + k + M)
-    W = QWeight.from_ggml(raw, qt, n, k, DEV)
+    W = QWeight.from_ggml(raw, qt, n, k, DEV, t32=True)
     assert W.to_t32()
     torch.manual_seed(M)
     x = torch.randn(M, k, device=DEV)
@@ -146,7 +146,7 @@ def test_q5k_native_paths():
     the row dequantisation all match the fp32 dequantised reference."""
     n, k = 384, 1024
     raw, dense = make_w(QType.Q5_K, n, k, seed=5)
-    W = QWeight.from_ggml(raw, QType.Q5_K, n, k, DEV)
+    W = QWeight.from_ggml(raw, QType.Q5_K, n, k, DEV, t32=True)
     assert int(W.qtype) == int(QType.Q5_K) and W.to_t32()
     rows = torch.tensor([0, 5, 383, 77], dtype=torch.int32, device=DEV)
     got = W.dequant_gpu(torch.float32, rows)

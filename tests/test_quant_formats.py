@@ -99,3 +99,92 @@ def test_carried_formats_gpu(qt):
             tol = 1e-2
         rel = float((out.cpu() - ref).norm() / ref.norm())
         assert rel < tol, (qt.name, M, rel)
+
+
+# ---- MX4F / MX5F: Q4_0 / Q4_1 / Q5_0 / Q5_1 at their own bit width in the t32 kernels --------------------
+Q32 = [QType.Q4_0, QType.Q4_1, QType.Q5_0, QType.Q5_1]
+
+
+@pytest.mark.parametrize("qt", Q32)
+def test_to_mxf_exact(qt):
+    """The re-layout is exact (w = s * code + m with the checkpoint's own f16 s / m; Q4_0 / Q5_0 offsets
+    -8 d / -16 d are exact f16 products), 5 / 6 bits per weight instead of Q8_0's 8.5, and the t32 tiling is a
+    byte permutation."""
+    n, k = 64, 768
+    raw = rand_blocks(qt, n, k, seed=3)
+    ref = Q.dequantize(raw, qt, (k, n))
+    mx, mt = Q.to_mxf(raw, qt, n, k)
+    assert mt == (QType.MX5F if qt in (QType.Q5_0, QType.Q5_1) else QType.MX4F)
+    assert mx.shape == (n, k // 256 * BLOCK[mt][1])
+    assert np.array_equal(Q.dequantize(mx, mt, (k, n)), ref)
+    t = Q.tile32(mx, None, mt, n, k)
+    assert t.numel() == mx.size and np.array_equal(np.sort(t.numpy().reshape(-1)), np.sort(mx.reshape(-1)))
+    q8 = Q.to_q8_0(mx, mt, n, k)  # the fallback for weights that cannot be tiled: exact for Q4_0 / Q5_0
+    err = np.abs(Q.dequantize(q8, QType.Q8_0, (k, n)) - ref).max()
+    assert err == 0.0 if qt in (QType.Q4_0, QType.Q5_0) else err < 5e-3 * np.abs(ref).max()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("qt", Q32)
+def test_mxf_kernels_gpu(qt, monkeypatch):
+    """MX4F / MX5F through every t32 kernel: decode GEMV (q8 rows and the fused quantise / RMSNorm prologue,
+    every epilogue, split-K), the LDS-DMA MFMA GEMM (several tile shapes, ragged M / N, split-K, SwiGLU) and the
+    row dequantisation, against the fp32 product with the checkpoint's own dequantisation."""
+    from localai_tfp_amd.ops import core as K
+    from localai_tfp_amd.ops import linear as L
+    from localai_tfp_amd.ops.linear import EPI_ADD_F32, EPI_BF16, EPI_F32, EPI_SWIGLU, QWeight, qmatmul
+    n, k = 416, 2304
+    raw = rand_blocks(qt, n, k, seed=int(qt) + 5)
+    dense = torch.from_numpy(Q.dequantize(raw, qt, (k, n)).copy())
+    W = QWeight.from_ggml(raw, int(qt), n, k, "cuda", t32=True)
+    assert int(W.qtype) in (int(QType.MX4F), int(QType.MX5F)) and W.src_qtype == int(qt)
+    assert W.to_t32() and W.layout == "t32"
+    rows = torch.tensor([0, 7, n - 1, 100], dtype=torch.int32, device="cuda")
+    assert torch.equal(W.dequant_gpu(torch.float32, rows).cpu(), dense[rows.long().cpu()])
+
+    def rel(a, b):
+        return float((a.float().cpu() - b).norm() / b.norm())
+    g = torch.Generator().manual_seed(1)
+    for M in (1, 3, 4):
+        x = torch.randn(M, k, generator=g).half().cuda()
+        xq = torch.empty(M, k, dtype=torch.int8, device="cuda")
+        xds = torch.empty(M, k // 32, 2, device="cuda")
+        K.quant_q8(x, xq, xds)
+        xr = (xq.float().reshape(M, k // 32, 32) * xds[:, :, :1]).reshape(M, k).cpu()
+        ref = xr @ dense.t()
+        out = torch.empty(M, n, device="cuda")
+        qmatmul(W, None, EPI_F32, out, xq=xq, xds=xds)
+        assert rel(out, ref) < 2e-3, M
+        acc = torch.randn(M, n, device="cuda")
+        acc0 = acc.clone()
+        qmatmul(W, None, EPI_ADD_F32, acc, xq=xq, xds=xds)
+        assert rel(acc - acc0, ref) < 2e-3
+        sw = torch.empty(M, n // 2, dtype=torch.float16, device="cuda")
+        qmatmul(W, None, EPI_SWIGLU, sw, xq=xq, xds=xds)
+        gg = ref.reshape(M, n // 32, 2, 16)
+        assert rel(sw, torch.nn.functional.silu(gg[:, :, 0].reshape(M, -1)) * gg[:, :, 1].reshape(M, -1)) < 1e-2
+        # fused prologue: 16-bit rows quantised in the GEMV / fp32 residual rows RMS-normalised first
+        o2 = torch.zeros(M, n, device="cuda")
+        assert L.qmv_fused(W, x, EPI_F32, o2, out_zeroed=True)
+        assert rel(o2, x.float().cpu() @ dense.t()) < 2e-2
+        r32 = torch.randn(M, k, generator=g).cuda()
+        nw = (torch.rand(k, generator=g) + 0.5).cuda()
+        o3 = torch.empty(M, n, device="cuda")
+        assert L.qmv_fused(W, r32, EPI_F32, o3, norm=nw, eps=1e-5)
+        y = (r32 * torch.rsqrt(r32.pow(2).mean(-1, keepdim=True) + 1e-5) * nw).cpu()
+        assert rel(o3, y @ dense.t()) < 2e-2
+    for M, cfg in ((40, None), (200, None), (77, (4, 2, 4, 1, 2)), (130, (2, 1, 4, 17, 2)), (96, (2, 2, 4, 2, 1)),
+                   (256, (2, 2, 2, 33, 1))):
+        monkeypatch.setattr(L, "QMM_FORCE", cfg)
+        x = torch.randn(M, k, generator=g).half()
+        ref = x.float() @ dense.t()
+        out = torch.zeros(M, n, device="cuda")
+        qmatmul(W, x.cuda(), EPI_F32, out, out_zeroed=True)
+        assert rel(out, ref) < 5e-3, (M, cfg)
+        ob = torch.empty(M, n, dtype=torch.float16, device="cuda")
+        qmatmul(W, x.cuda(), EPI_BF16, ob)
+        assert rel(ob, ref) < 5e-3, (M, cfg)
+        sw = torch.empty(M, n // 2, dtype=torch.float16, device="cuda")
+        qmatmul(W, x.cuda(), EPI_SWIGLU, sw)
+        gg = ref.reshape(M, n // 32, 2, 16)
+        assert rel(sw, torch.nn.functional.silu(gg[:, :, 0].reshape(M, -1)) * gg[:, :, 1].reshape(M, -1)) < 1e-2
