@@ -6,7 +6,7 @@ Parity targets: the reference's `piper` backend (backend/go/tts/piper.go:20-49, 
 piper C++ -> onnxruntime VITS) and the Python `coqui` / `transformers` (VitsModel) TTS backends.
 Weights load from a Hugging Face VITS directory (config.json + model.safetensors + vocab.json, e.g.
 the MMS-TTS voices; weight-norm parametrisations are folded at load) or `synthetic:vits-*`
-(random init). Piper's .onnx voices are not loadable here (no onnx runtime in the image).
+(random init). Piper .onnx voices load through models/piper.py (initializer renaming, no onnx runtime).
 
 MI355X path: the encoder, flows and vocoder run as fp32 conv/GEMM ops on the GPU (MIOpen /
 hipBLASLt — plain library convolutions), the WaveNet gate (tanh(a) * sigmoid(b) over the two

@@ -344,6 +344,9 @@ class ModelLoader:
     def _load_with(self, cfg, name: str, backend: str) -> LoadedModel:
         backend = W.resolve(backend)
         opts = model_options(cfg, self.app, self.app.models_path)
+        if backend == "piper":  # pkg/model/initializers.go:451-453: espeak-ng data under the backend assets
+            opts.LibrarySearchPath = os.path.join(getattr(self.app, "backend_assets_path", "") or "",
+                                                  "backend-assets", "espeak-ng-data")
         ext = (getattr(self.app, "external_grpc_backends", None) or {}).get(backend)
         parallel = bool(getattr(self.app, "parallel_backend_requests", True))
         tp = max(1, int(cfg.tensor_parallel_size or 1))

@@ -3,7 +3,9 @@ backend's VITS / MMS-TTS path behind the TTS RPC, served by the VITS engine (mod
 Bark, Coqui, Kokoro and MusicGen names are NOT routed here (workers/unsupported.py fails their
 LoadModel explicitly).
 
-LoadModel: a Hugging Face VITS directory (MMS-TTS layout) or `synthetic:vits-test | vits-base`.
+LoadModel: a piper voice (`<voice>.onnx` + `<voice>.onnx.json`, models/piper.py; espeak-ng data from
+LibrarySearchPath or the `espeak_data` option), a Hugging Face VITS directory (MMS-TTS layout) or
+`synthetic:vits-test | vits-base`.
 ModelOptions.Options ("key:value"): noise_scale, noise_scale_duration (alias noise_w), speaking_rate
 (alias length_scale = 1 / rate), seed.
 TTS: text -> 16-bit PCM WAV at the model's sample rate in `dst`. `voice` selects the speaker of a
@@ -46,20 +48,20 @@ class TTSServicer(BackendServicer):
             path = request.ModelFile or request.Model
             if not path.startswith("synthetic:") and not os.path.isabs(path) and request.ModelPath:
                 path = os.path.join(request.ModelPath, path)
-            if not path.startswith("synthetic:") and os.path.isfile(path):
-                if path.endswith(".onnx"):
-                    # piper voices are original-VITS graphs (enc_p / dp / flow / dec) traced to ONNX with
-                    # constant-folded weight names: formats/onnx.py reads them, but no name map to the
-                    # HF VITS modules of models/tts.py exists yet
-                    raise ValueError(f"{path}: piper .onnx voices are not supported yet; use a VITS checkpoint "
-                                     "directory (config.json + safetensors + vocab.json, MMS-TTS layout)")
-                path = os.path.dirname(path)
-            self.model, self.tok = T.load_vits(path, self.device)
             o = {}
             for kv in request.Options:
                 k, _, v = kv.partition(":")
                 o[k.strip()] = v.strip()
             self.opts = o
+            if not path.startswith("synthetic:") and os.path.isfile(path) and path.endswith(".onnx"):
+                # piper voice: <voice>.onnx + <voice>.onnx.json (models/piper.py)
+                from ..models.piper import load_piper
+                self.model, self.tok = load_piper(path, self.device,
+                                                  o.get("espeak_data", "") or request.LibrarySearchPath)
+                return pb.Result(message=f"loaded piper voice {os.path.basename(path)}", success=True)
+            if not path.startswith("synthetic:") and os.path.isfile(path):
+                path = os.path.dirname(path)
+            self.model, self.tok = T.load_vits(path, self.device)
             return pb.Result(message=f"loaded {self.model.cfg.name}", success=True)
         except Exception as ex:
             log.exception("LoadModel failed")

@@ -2,7 +2,7 @@
 (stochastic and deterministic duration predictors, multi-speaker conditioning), the rational-quadratic
 spline inverse, the tokenizer, HF-directory loading, the worker RPC and the /v1/audio/speech, /tts and
 /v1/sound-generation routes (reference coverage: core/http/app_test.go "tts" label, the AIO e2e TTS
-case; piper .onnx voices cannot be loaded here, so parity with piper output is unpinned)."""
+case; piper .onnx voices: tests/test_piper.py)."""
 import io
 import json
 import os
