@@ -31,6 +31,7 @@ import numpy as np
 import torch
 import torch.nn.functional as F
 
+from ..ops.core import attn_dense
 from .encodec import EncodecConfig, EncodecDecoder
 
 
@@ -97,29 +98,31 @@ class _GPT:
         return F.layer_norm(x, (self.D,), wb[0], wb[1], 1e-5).to(self.dtype)
 
     def new_cache(self, B: int, T: int):
-        hd = self.D // self.H
-        return [[torch.empty(B, self.H, T, hd, device=self.device, dtype=self.dtype),
-                 torch.empty(B, self.H, T, hd, device=self.device, dtype=self.dtype)] for _ in self.layers]
+        """Token-major K / V rows [B, T, D] per layer (the layout attn_dense reads, capacity T)."""
+        return [[torch.empty(B, T, self.D, device=self.device, dtype=self.dtype),
+                 torch.empty(B, T, self.D, device=self.device, dtype=self.dtype)] for _ in self.layers]
 
     def forward(self, x: torch.Tensor, pos0: int = 0, cache=None, head: int = 0) -> torch.Tensor:
-        """x: input embeddings [B, S, D] fp32 (positions pos0..pos0+S) -> logits [B, S, V] fp32."""
+        """x: input embeddings [B, S, D] fp32 (positions pos0..pos0+S) -> logits [B, S, V] fp32.
+        Attention runs on the MFMA flash kernel (ops.core.attn_dense): causal masks are bottom-right aligned,
+        so a cached chunk at pos0 attends keys 0..pos0+S-1 exactly as the reference's chunk mask."""
         B, S, _ = x.shape
-        hd = self.D // self.H
+        D, hd = self.D, self.D // self.H
         x = x + self.pos[pos0:pos0 + S][None]
         for li, L in enumerate(self.layers):
             h = self._ln(x, L["ln1"])
-            qkv = F.linear(h, L["qkv"], L["qkv_b"]).view(B, S, 3, self.H, hd).permute(2, 0, 3, 1, 4)
-            q, k, v = qkv[0], qkv[1], qkv[2]
+            qkv = F.linear(h, L["qkv"], L["qkv_b"]).view(B * S, 3 * D)
+            q, k, v = qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:]
+            Sk, rows = S, 0
             if cache is not None:
                 kc, vc = cache[li]
-                kc[:, :, pos0:pos0 + S] = k
-                vc[:, :, pos0:pos0 + S] = v
-                k, v = kc[:, :, :pos0 + S], vc[:, :, :pos0 + S]
-            a = F.scaled_dot_product_attention(q, k, v, is_causal=self.causal and S > 1 and pos0 == 0) \
-                if not (self.causal and S > 1 and pos0 > 0) else \
-                F.scaled_dot_product_attention(q, k, v, attn_mask=_chunk_mask(S, pos0, x.device))
-            a = a.transpose(1, 2).reshape(B, S, self.D)
-            x = x + F.linear(a, L["o"], L["o_b"]).float()
+                kc[:, pos0:pos0 + S] = k.view(B, S, D)
+                vc[:, pos0:pos0 + S] = v.view(B, S, D)
+                k, v = kc.view(-1, D), vc.view(-1, D)
+                Sk, rows = pos0 + S, kc.shape[1]
+            a = torch.empty(B * S, D, dtype=qkv.dtype, device=qkv.device)
+            attn_dense(q, k, v, a, B, S, Sk, self.H, self.H, hd, hd ** -0.5, causal=self.causal, kv_rows=rows)
+            x = x + F.linear(a.view(B, S, D), L["o"], L["o_b"]).float()
             h = self._ln(x, L["ln2"])
             x = x + F.linear(F.gelu(F.linear(h, L["fc1"], L["fc1_b"])), L["fc2"], L["fc2_b"]).float()
         h = self._ln(x, self.ln_f)
@@ -127,12 +130,6 @@ class _GPT:
 
     def embed(self, ids: torch.Tensor, table: int = 0) -> torch.Tensor:
         return self.emb[table][ids.to(self.device).long()].float()
-
-
-def _chunk_mask(S: int, pos0: int, device):
-    q = torch.arange(S, device=device)[:, None] + pos0
-    k = torch.arange(pos0 + S, device=device)[None, :]
-    return k <= q
 
 
 def _pick(logits: torch.Tensor, temp: float | None, gen) -> torch.Tensor:

@@ -30,6 +30,7 @@ import numpy as np
 import torch
 import torch.nn.functional as F
 
+from ..ops.core import attn_dense
 from .diffusion.text_encoders import T5Config, T5Encoder
 from .encodec import EncodecDecoder, EncodecConfig
 
@@ -115,46 +116,48 @@ class MusicgenDecoder:
         return F.layer_norm(x.float(), (x.shape[-1],), wb[0], wb[1], 1e-5).to(self.dtype)
 
     def cross_kv(self, enc: torch.Tensor):
-        """enc [B, S, D] (decoder width) -> per layer (k, v) [B, H, S, hd]."""
-        c = self.c
-        B, S, _ = enc.shape
-        hd = c.hidden // c.heads
+        """enc [B, S, D] (decoder width) -> per layer (k, v) token-major rows [B*S, D]."""
+        B, S, D = enc.shape
         out = []
         e = enc.to(self.dtype)
         for L in self.layers:
-            kv = F.linear(e, L["xkv"]).view(B, S, 2, c.heads, hd)
-            out.append((kv[:, :, 0].transpose(1, 2).contiguous(), kv[:, :, 1].transpose(1, 2).contiguous()))
+            kv = F.linear(e, L["xkv"]).view(B * S, 2 * D)
+            out.append((kv[:, :D].contiguous(), kv[:, D:].contiguous()))
         return out
 
     def new_cache(self, B: int, T: int):
-        c = self.c
-        hd = c.hidden // c.heads
-        return [(torch.zeros(B, c.heads, T, hd, device=self.device, dtype=self.dtype),
-                 torch.zeros(B, c.heads, T, hd, device=self.device, dtype=self.dtype)) for _ in self.layers]
+        """Token-major self-attention K / V rows [B, T, D] per layer (attn_dense layout, capacity T)."""
+        D = self.c.hidden
+        return [(torch.zeros(B, T, D, device=self.device, dtype=self.dtype),
+                 torch.zeros(B, T, D, device=self.device, dtype=self.dtype)) for _ in self.layers]
 
-    def step(self, ids: torch.Tensor, pos: torch.Tensor, cache, xkv, xmask) -> torch.Tensor:
+    def step(self, ids: torch.Tensor, pos: torch.Tensor, cache, xkv, xlen) -> torch.Tensor:
         """One decode step. ids [B, K] int64, pos [1] int64 (device); cache from new_cache; xkv from
-        cross_kv; xmask [B, 1, 1, S] additive fp mask or None -> logits [B, K, V] fp32."""
+        cross_kv; xlen int32 [B]: valid encoder keys per row (device) -> logits [B, K, V] fp32. Both attentions
+        run on the flash kernel (ops.core.attn_dense) with device-side key lengths, so the step stays
+        shape-static for the HIP graph."""
         c = self.c
         B = ids.shape[0]
-        hd = c.hidden // c.heads
+        D, hd = c.hidden, c.hidden // c.heads
         x = self.pos.index_select(0, pos).expand(B, -1).clone()
         for k in range(c.codebooks):
             x = x + self.emb[k].index_select(0, ids[:, k]).float()
-        T = cache[0][0].shape[2]
-        smask = (torch.arange(T, device=x.device) <= pos).view(1, 1, 1, T)  # keys written so far
+        T = cache[0][0].shape[1]
+        S = xkv[0][0].shape[0] // B
+        klen = (pos.to(torch.int32) + 1).expand(B).contiguous()  # keys written so far
+        a = torch.empty(B, D, dtype=self.dtype, device=x.device)
         for L, (kc, vc), (xk, xv) in zip(self.layers, cache, xkv):
             h = self._ln(x, L["ln1"])
-            qkv = F.linear(h, L["qkv"]).view(B, 3, c.heads, hd)
-            kc.index_copy_(2, pos, qkv[:, 1].unsqueeze(2))
-            vc.index_copy_(2, pos, qkv[:, 2].unsqueeze(2))
-            q = qkv[:, 0].unsqueeze(2)  # [B, H, 1, hd]
-            a = F.scaled_dot_product_attention(q, kc, vc, attn_mask=smask)
-            x = x + F.linear(a.reshape(B, c.hidden), L["o"]).float()
+            qkv = F.linear(h, L["qkv"])  # [B, 3D]
+            kc.index_copy_(1, pos, qkv[:, None, D:2 * D])
+            vc.index_copy_(1, pos, qkv[:, None, 2 * D:])
+            attn_dense(qkv, kc.view(-1, D), vc.view(-1, D), a, B, 1, T, c.heads, c.heads, hd, hd ** -0.5,
+                         klen=klen, kv_rows=T)
+            x = x + F.linear(a, L["o"]).float()
             h = self._ln(x, L["ln2"])
-            q = F.linear(h, L["xq"]).view(B, c.heads, 1, hd)
-            a = F.scaled_dot_product_attention(q, xk, xv, attn_mask=xmask)
-            x = x + F.linear(a.reshape(B, c.hidden), L["xo"]).float()
+            q = F.linear(h, L["xq"])
+            attn_dense(q, xk, xv, a, B, 1, S, c.heads, c.heads, hd, hd ** -0.5, klen=xlen)
+            x = x + F.linear(a, L["xo"]).float()
             h = self._ln(x, L["ln3"])
             x = x + F.linear(_act(F.linear(h, L["fc1"]), c.act), L["fc2"]).float()
         h = self._ln(x, self.ln_f)
@@ -214,9 +217,11 @@ class MusicGen:
             m = torch.cat([m, torch.zeros_like(m)], 0)
         if self.proj is not None:
             h = F.linear(h, self.proj[0], self.proj[1])
-        # fully masked rows (the CFG null row) attend uniformly, as a finite-min additive mask does in HF
-        xmask = torch.where(m[:, None, None, :].bool(), 0.0, torch.finfo(self.dtype).min).to(self.dtype)
-        return h, xmask
+        # valid (right-padded) encoder keys per row; a fully masked row (the CFG null row) attends uniformly to
+        # all of its keys, as HF's finite-min additive mask makes it do
+        n = m.sum(-1).to(torch.int32)
+        xlen = torch.where(n > 0, n, torch.full_like(n, m.shape[-1])).contiguous()
+        return h, xlen
 
     # ------------------------------------------------------------------ generation
     @torch.no_grad()
@@ -230,7 +235,7 @@ class MusicGen:
         K = c.codebooks
         if max_new_tokens < 2 * K:
             raise ValueError(f"max_new_tokens must be >= {2 * K} (delay pattern of {K} codebooks)")
-        enc, xmask = self.encode_text(input_ids, attention_mask, guidance_scale)
+        enc, xlen = self.encode_text(input_ids, attention_mask, guidance_scale)
         BB = enc.shape[0]
         max_len = max_new_tokens + 1
         pat = delay_pattern(c, max_len).to(self.device)
@@ -245,7 +250,7 @@ class MusicGen:
         pos_t = torch.zeros(1, dtype=torch.long, device=self.device)
 
         def run_step():
-            return self.decoder.step(step_in, pos_t, cache, xkv, xmask)
+            return self.decoder.step(step_in, pos_t, cache, xkv, xlen)
 
         graph, g_out = None, None
         for t in range(max_len - 1):
