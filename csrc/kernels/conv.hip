@@ -207,6 +207,12 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(MxConvP p) {
                     } else if (p.act == 3) {
 #pragma unroll
                         for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : expm1f(v[e]);
+                    } else if (p.act == 4) {
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : 0.1f * v[e];
+                    } else if (p.act == 5) {
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) v[e] = tanhf(v[e]);
                     }
                     u32x2 o = {pack_act2<F16>(v[0], v[1]), pack_act2<F16>(v[2], v[3])};
                     *(u32x2*)(p.y + (size_t)pix * p.ldy + co0) = o;
@@ -222,6 +228,8 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(MxConvP p) {
                         if (p.act == 1) t = silu_f(t);
                         else if (p.act == 2) t = gelu_erf_f(t);
                         else if (p.act == 3) t = t > 0.f ? t : expm1f(t);
+                        else if (p.act == 4) t = t > 0.f ? t : 0.1f * t;
+                        else if (p.act == 5) t = tanhf(t);
                         p.y[(size_t)pix * p.ldy + co] = f32_to_act<F16>(t);
                     }
                 }
@@ -269,7 +277,7 @@ extern "C" int mxk_conv_tile_auto(int P, int Cout) {
 // x: [Nb, H, W, Cp] act16 NHWC (Cp % 8 == 0, 16-B aligned); w: [Cout, Kp] act16, k = (kh*KW + kw)*Cp + ci,
 // zero for k >= KH*KW*Cp, Kp % 64 == 0; y: [Nb*Ho*Wo, ldy]; res: [Nb*Ho*Wo, ldr] or null; tadd fp32 [Nb, ldt]
 // or null; bias fp32 [Cout] or null; up: fused nearest 2x upsample of x; act: 0 none, 1 SiLU, 2 GELU (erf),
-// 3 ELU; dil: filter dilation (both axes).
+// 3 ELU, 4 leaky ReLU (slope 0.1, HiFi-GAN), 5 tanh; dil: filter dilation (both axes).
 // zero: >= 16 zero bytes of device memory. cfg: tm*16 + tn, or < 0 for mxk_conv_tile_auto.
 extern "C" int mxk_conv2d(const uint16_t* x, int Nb, int H, int W, int Cp, const uint16_t* w, int Cout, int KH, int KW,
                           int Kp, int stride, int dil, int pad_h, int pad_w, int up, int Ho, int Wo, const float* bias,

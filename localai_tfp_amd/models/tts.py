@@ -24,6 +24,8 @@ import numpy as np
 import torch
 import torch.nn.functional as F
 
+from ..ops import conv as CV
+
 
 @dataclass
 class VitsConfig:
@@ -413,7 +415,79 @@ class VitsModel:
             z = torch.cat([a, b - m], 1)
         return z
 
+    def _vocoder_plan(self):
+        """HiFi-GAN convolutions as conv.hip convs over [B, T, C] 16-bit rows (built once): transposed convs
+        (k = 2r, padding r/2) as one k = 2 conv producing the r output phases per frame (models/encodec.py)."""
+        from types import SimpleNamespace
+        from .encodec import _ConvT
+        c = self.cfg
+        dt = torch.float16
+        cf = SimpleNamespace(use_causal_conv=False, pad_mode="constant", trim_right_ratio=1.0)
+
+        def c1(name):
+            w = self.w[name + ".weight"]
+            b = self.w.get(name + ".bias")
+            w4 = w[:, :, None, :].to(dt).contiguous()
+            return (w4, b.float() if b is not None else None, CV.pack_weight(w4, dt), int(w.shape[2]))
+        if c.slope != 0.1:
+            return None  # the fused epilogue's leaky slope is 0.1
+        ups = []
+        for i, (r, k) in enumerate(zip(c.upsample_rates, c.upsample_kernels)):
+            if k != 2 * r or r % 2:
+                return None  # not the k = 2r, padding r/2 HiFi-GAN geometry: library path
+            ups.append(_ConvT(self.w[f"decoder.upsampler.{i}.weight"], self.w.get(f"decoder.upsampler.{i}.bias"), r, cf,
+                              self.device, dt))
+        nk = len(c.resblock_kernels)
+        res = {}
+        for i in range(len(ups)):
+            for j, dils in enumerate(c.resblock_dilations):
+                pre = f"decoder.resblocks.{i * nk + j}."
+                res[i * nk + j] = [(c1(f"{pre}convs1.{n}"), c1(f"{pre}convs2.{n}")) for n in range(len(dils))]
+        return dict(pre=c1("decoder.conv_pre"), post=c1("decoder.conv_post"), ups=ups, res=res,
+                    cond=c1("decoder.cond") if "decoder.cond.weight" in self.w else None)
+
+    @staticmethod
+    def _c1(x, cw, dil=1, act=None, residual=None, tadd=None):
+        """One stride-1 'same' Conv1d on conv.hip: x [B, T, C] 16-bit rows -> [B, T, Cout] rows."""
+        w4, b, packed, k = cw
+        p = dil * (k - 1) // 2
+        xin = x[:, None].permute(0, 3, 1, 2)
+        res = residual[:, None].permute(0, 3, 1, 2) if residual is not None else None
+        y = CV.conv2d(xin, weight=w4, bias=b, stride=1, pad=(0, p, 0, dil * (k - 1) - p), dilation=dil, act=act,
+                      residual=res, tadd=tadd, packed=packed)
+        return y.permute(0, 2, 3, 1)[:, 0]
+
     def vocoder(self, z, g=None):
+        c = self.cfg
+        if self.device.type == "cuda":
+            if not hasattr(self, "_vplan"):
+                self._vplan = self._vocoder_plan()
+            if self._vplan is not None:
+                return self._vocoder_gpu(z, g)
+        return self._vocoder_ref(z, g)
+
+    def _vocoder_gpu(self, z, g=None):
+        c, P = self.cfg, self._vplan
+        nk = len(c.resblock_kernels)
+        tadd = None
+        if g is not None and P["cond"] is not None:
+            w4, b, _, _ = P["cond"]
+            tadd = F.conv1d(g, w4[:, :, 0].float(), b)[:, :, 0]  # [B, C] per-utterance channel offset
+        x = self._c1(z.transpose(1, 2).to(torch.float16).contiguous(), P["pre"], tadd=tadd)
+        for i in range(len(P["ups"])):
+            x = P["ups"][i](F.leaky_relu(x, c.slope).contiguous())
+            acc = None
+            for j, dils in enumerate(c.resblock_dilations):
+                h = x
+                for (cw1, cw2), d in zip(P["res"][i * nk + j], dils):
+                    t = self._c1(F.leaky_relu(h, c.slope).contiguous(), cw1, dil=d, act="leaky")
+                    h = self._c1(t, cw2, residual=h)
+                acc = h.float() if acc is None else acc + h.float()
+            x = (acc / nk).to(torch.float16)
+        y = self._c1(F.leaky_relu(x, 0.01).contiguous(), P["post"], act="tanh")
+        return y.float().transpose(1, 2)
+
+    def _vocoder_ref(self, z, g=None):
         c = self.cfg
         x = self.conv(z, "decoder.conv_pre", padding=3)
         if g is not None:

@@ -8,7 +8,7 @@ fuses what the UNet / VAE / ControlNet blocks do around a convolution into the k
 * ``pad=(t, l, b, r)`` asymmetric zero padding (the VAE encoder's ``F.pad(x, (0, 1, 0, 1))`` + stride 2);
 * ``tadd``            a per-image channel vector added after the bias (ResNet time embedding);
 * ``residual``        an NHWC tensor of the output's shape added in the epilogue (ResNet skip);
-* ``act="silu"|"gelu"|"elu"`` SiLU / exact (erf) GELU / ELU on the result;
+* ``act="silu"|"gelu"|"elu"|"leaky"|"tanh"`` SiLU / exact (erf) GELU / ELU / leaky ReLU (0.1) / tanh on the result;
 * ``dilation``        filter dilation (EnCodec residual units).
 
 The packed weight ([Cout, KH*KW*Cp] with Cp = Cin rounded up to 8 and k rounded up to 64, zero padded)
@@ -28,7 +28,7 @@ import torch.nn.functional as F
 from .. import _native as N
 
 _ZERO: dict = {}
-_ACT = {None: 0, "silu": 1, "gelu": 2, "elu": 3}
+_ACT = {None: 0, "silu": 1, "gelu": 2, "elu": 3, "leaky": 4, "tanh": 5}
 
 
 def _zero_page(device) -> torch.Tensor:
@@ -98,6 +98,10 @@ def _reference(x, weight, bias, stride, pad, upsample, tadd, residual, act, dila
         y = F.gelu(y)
     elif act == "elu":
         y = F.elu(y)
+    elif act == "leaky":
+        y = F.leaky_relu(y, 0.1)
+    elif act == "tanh":
+        y = torch.tanh(y)
     return y.to(x.dtype)
 
 

@@ -145,7 +145,7 @@ def test_http_speech_routes(client):
 
 @pytest.mark.gpu
 def test_vits_gpu_matches_cpu():
-    """GPU path (MIOpen convs, audio.hip wavenet_gate) vs the fp32 CPU model."""
+    """GPU path (HiFi-GAN on conv.hip, audio.hip wavenet_gate) vs the fp32 CPU model."""
     from localai_tfp_amd.ops import core as K
     x = torch.randn(2, 64, 37)
     g = K.wavenet_gate(x.cuda(), 32).cpu()
@@ -155,9 +155,11 @@ def test_vits_gpu_matches_cpu():
     assert torch.allclose(g, torch.tanh(x[:, :64]) * torch.sigmoid(x[:, 64:]), atol=1e-5)
     _, sd = hf_pair(T.VITS_TEST)
     c = T.VitsModel(T.VITS_TEST, sd, "cpu").synthesize(IDS, noise_scale=0.0, noise_scale_duration=0.0)
-    gm = T.VitsModel(T.VITS_TEST, sd, "cuda:0").synthesize(IDS, noise_scale=0.0, noise_scale_duration=0.0)
+    m = T.VitsModel(T.VITS_TEST, sd, "cuda:0")
+    gm = m.synthesize(IDS, noise_scale=0.0, noise_scale_duration=0.0)
+    assert m._vplan is not None  # the HiFi-GAN ran on conv.hip (f16 rows, fused leaky / residual / tanh)
     assert gm.shape == c.shape
-    assert np.abs(gm - c).max() < 2e-3
+    assert np.linalg.norm(gm - c) / np.linalg.norm(c) < 2e-2 and np.abs(gm - c).max() < 3e-2
 
 
 @pytest.mark.parametrize("backend", ["coqui", "kokoro"])
