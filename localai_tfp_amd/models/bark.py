@@ -128,6 +128,28 @@ class _GPT:
         h = self._ln(x, self.ln_f)
         return F.linear(h, self.heads[head]).float()
 
+    def decode_step(self, tok: torch.Tensor, pos: torch.Tensor, cache, head: int = 0) -> torch.Tensor:
+        """One token (int64 [1], device) at device position pos (int64 [1]) against the cache -> logits [1, V]
+        fp32. Shape-static (no host values), so the decode loop replays it as one HIP graph."""
+        D, hd = self.D, self.D // self.H
+        T = cache[0][0].shape[1]
+        x = (self.emb[0].index_select(0, tok).float() + self.pos.index_select(0, pos))[None]  # [1, 1, D]
+        klen = pos.to(torch.int32) + 1
+        a = torch.empty(1, D, dtype=self.dtype, device=self.device)
+        for li, L in enumerate(self.layers):
+            h = self._ln(x, L["ln1"])
+            qkv = F.linear(h, L["qkv"], L["qkv_b"]).view(1, 3 * D)
+            kc, vc = cache[li]
+            kc.index_copy_(1, pos, qkv[:, None, D:2 * D])
+            vc.index_copy_(1, pos, qkv[:, None, 2 * D:])
+            attn_dense(qkv, kc.view(-1, D), vc.view(-1, D), a, 1, 1, T, self.H, self.H, hd, hd ** -0.5, klen=klen,
+                       kv_rows=T)
+            x = x + F.linear(a.view(1, 1, D), L["o"], L["o_b"]).float()
+            h = self._ln(x, L["ln2"])
+            x = x + F.linear(F.gelu(F.linear(h, L["fc1"], L["fc1_b"])), L["fc2"], L["fc2_b"]).float()
+        h = self._ln(x, self.ln_f)
+        return F.linear(h, self.heads[head]).float()[:, -1]
+
     def embed(self, ids: torch.Tensor, table: int = 0) -> torch.Tensor:
         return self.emb[table][ids.to(self.device).long()].float()
 
@@ -159,6 +181,8 @@ class Bark:
         S = prefix_emb.shape[1]
         cache = gpt.new_cache(1, S + max_new)
         logits = gpt.forward(prefix_emb, 0, cache)[:, -1]
+        if gpt.device.type == "cuda" and max_new > 1:
+            return self._ar_graph(gpt, cache, logits, S, max_new, process, temp, gen, stop)
         out = []
         for i in range(max_new):
             nxt = int(_pick(process(logits, len(out)), temp, gen))
@@ -169,6 +193,40 @@ class Bark:
                 break
             logits = gpt.forward(gpt.embed(torch.tensor([[nxt]])), S + i, cache)[:, -1]
         return out
+
+    def _ar_graph(self, gpt: _GPT, cache, logits, S: int, max_new: int, process, temp, gen, stop, check: int = 32):
+        """The decode loop on the GPU without a host round trip per token: each step's transformer is one HIP
+        graph replay (decode_step captured once per loop), sampling stays on the device and feeds the next
+        step's input buffer; the stop token is looked for every `check` tokens (steps run past it are
+        discarded — the same tokens as the eager loop, which stops at the first stop token)."""
+        dev = gpt.device
+        tok = torch.zeros(1, dtype=torch.long, device=dev)
+        pos = torch.full((1,), S, dtype=torch.long, device=dev)
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            gpt.decode_step(tok, pos, cache)  # warm-up outside capture (writes slot S, rewritten by step 0)
+        torch.cuda.current_stream().wait_stream(side)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            g_out = gpt.decode_step(tok, pos, cache)
+        toks = torch.empty(max_new, dtype=torch.long, device=dev)
+        n = max_new
+        for i in range(max_new):
+            nxt = _pick(process(logits, i), temp, gen).view(-1)
+            toks[i:i + 1].copy_(nxt)
+            if stop is not None and (i % check == check - 1 or i + 1 == max_new):
+                hit = (toks[i + 1 - (i % check + 1):i + 1] == stop).nonzero()
+                if hit.numel():
+                    n = i + 1 - (i % check + 1) + int(hit[0, 0]) + 1
+                    break
+            if i + 1 == max_new:
+                break
+            tok.copy_(nxt)
+            pos.fill_(S + i)
+            graph.replay()
+            logits = g_out
+        return toks[:n].tolist()
 
     @torch.no_grad()
     def semantic_tokens(self, text_ids: list[int], history=None, temp=None, gen=None, min_eos_p=None,
@@ -191,12 +249,11 @@ class Bark:
 
         def process(logits, _n):
             lg = logits.masked_fill(supp, float("-inf"))
-            if min_eos_p:
+            if min_eos_p:  # device-side: no host sync per token
                 p = torch.softmax(lg, -1)
-                if float(p[0, g.eos]) > min_eos_p:
-                    only = torch.full_like(lg, float("-inf"))
-                    only[:, g.eos] = lg[:, g.eos]
-                    lg = only
+                only = torch.full_like(lg, float("-inf"))
+                only[:, g.eos] = lg[:, g.eos]
+                lg = torch.where(p[:, g.eos:g.eos + 1] > min_eos_p, only, lg)
             return lg
 
         out = self._ar(gp, x, max_new or g.max_semantic_new, process, temp, gen, stop=g.eos)

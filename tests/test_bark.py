@@ -91,6 +91,8 @@ def test_bark_gpu_matches_cpu_codes():
     s_g = gpu.semantic_tokens(text, None, None, None, None, 16)
     assert np.mean(np.array(s_c) == np.array(s_g[:len(s_c)])) > 0.8
     co = cpu.coarse_tokens(s_c, None, None, None)
+    co_g = gpu.coarse_tokens(s_c, None, None, None)  # HIP-graph decode loop (Bark._ar_graph)
+    assert co_g.shape == co.shape and np.mean(co_g == co) > 0.8
     fi = cpu.fine_tokens(co, None, None, None)
     a_c = cpu.codec.decode(torch.from_numpy(fi)[None])
     a_g = gpu.codec.decode(torch.from_numpy(fi)[None].cuda()).cpu()
