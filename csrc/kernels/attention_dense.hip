@@ -11,7 +11,8 @@
 // Workgroup: 4 waves x 16 query rows of one head; K/V staged 64 keys at a time into the XOR-swizzled
 // LDS images of attention.hip (conflict-free ds_read_b128 for K^T, ds_read_b64_tr_b16 for V).
 // Masks: `causal` (key position > query position + (Sk - Sq) dropped) and per-batch key lengths
-// `klen` (BERT padding); rows past `qlen[b]` are not written.
+// `klen` (BERT padding); rows past `qlen[b]` are not written. Optional additive relative-position bias
+// `rbias[h][j - i + Sq - 1]` (fp32, T5's bucketed bias table expanded per offset; shared by the batch).
 #include "mx_common.h"
 
 #define LOG2E_D 1.4426950408889634f
@@ -49,7 +50,7 @@ __global__ __launch_bounds__(256) void attn_dense_kernel(const uint16_t* __restr
                                                          uint16_t* __restrict__ o, int o_stride, int Sq, int Sk,
                                                          int Hq, int Hkv, const int* __restrict__ qlen_b,
                                                          const int* __restrict__ klen_b, int causal, float scale,
-                                                         int kv_rows) {
+                                                         int kv_rows, const float* __restrict__ rbias, int rb_ld) {
     constexpr int KT = 64;
     constexpr int KBYTES = KT * D * 2;
     constexpr int PSTRIDE = (KT + 8) * 2;
@@ -122,6 +123,7 @@ __global__ __launch_bounds__(256) void attn_dense_kernel(const uint16_t* __restr
                 const int kp = kt0 + 16 * t + col;
                 float s = sacc[t][i] * qs;
                 if (kp >= kv_end || qi >= qlen || (causal && kp > qi + shift)) s = -INFINITY;
+                else if (rbias) s += rbias[(size_t)h * rb_ld + (kp - qi + Sq - 1)] * LOG2E_D;
                 sacc[t][i] = s;
                 mx = fmaxf(mx, s);
             }
@@ -190,7 +192,7 @@ __global__ __launch_bounds__(256) void attn_dense_kernel(const uint16_t* __restr
 extern "C" int mxk_attn_dense(const uint16_t* q, int q_stride, const uint16_t* k, int k_stride, const uint16_t* v,
                               int v_stride, uint16_t* o, int o_stride, int B, int Sq, int Sk, int Hq, int Hkv, int D,
                               const int* qlen, const int* klen, int causal, float scale, int kv_rows,
-                              hipStream_t st) {
+                              const float* rbias, int rb_ld, hipStream_t st) {
     if (B <= 0 || Sq <= 0) return 0;
     if (kv_rows <= 0) kv_rows = Sk;
     if (Hq % Hkv || (D != 64 && D != 128)) return (int)hipErrorInvalidValue;
@@ -199,10 +201,10 @@ extern "C" int mxk_attn_dense(const uint16_t* q, int q_stride, const uint16_t* k
     MX_ACT_DISPATCH({
         if (D == 128)
             attn_dense_kernel<128, F16><<<grid, 256, 0, st>>>(q, q_stride, k, k_stride, v, v_stride, o, o_stride, Sq, Sk,
-                                                             Hq, Hkv, qlen, klen, causal, scale, kv_rows);
+                                                             Hq, Hkv, qlen, klen, causal, scale, kv_rows, rbias, rb_ld);
         else
             attn_dense_kernel<64, F16><<<grid, 256, 0, st>>>(q, q_stride, k, k_stride, v, v_stride, o, o_stride, Sq, Sk,
-                                                            Hq, Hkv, qlen, klen, causal, scale, kv_rows);
+                                                            Hq, Hkv, qlen, klen, causal, scale, kv_rows, rbias, rb_ld);
     });
     MXK_CHECK_LAUNCH();
 }

@@ -43,7 +43,7 @@ KERNEL_SIGS = {
     "mxk_qmv_x": [I, I, I, P, I, P, F, P, I, I, I, I, P, I, P],
     "mxk_dequant_t32": [I, P, P, I, I, P, P, I, P],
     "mxk_set_act_f16": [I],
-    "mxk_attn_dense": [P, I, P, I, P, I, P, I, I, I, I, I, I, I, P, P, I, F, I, P],
+    "mxk_attn_dense": [P, I, P, I, P, I, P, I, I, I, I, I, I, I, P, P, I, F, I, P, I, P],
     "mxk_get_act_f16": [],
     "mxk_qgemv": [I, I, P, P, P, P, I, I, I, P, I, P],
     "mxk_dequant_rows": [I, P, P, P, I, I, P, P, I, P],

@@ -252,21 +252,38 @@ class T5Encoder(nn.Module):
         B, S = ids.shape
         dt = self.shared.weight.dtype
         x = self.shared.weight[ids].float().reshape(B * S, c.d_model).contiguous()
-        pos = torch.arange(S, device=ids.device)
-        bucket = t5_buckets(pos[None, :] - pos[:, None], c.buckets, c.max_distance)
         rel = self.encoder.block[0].layer[0].SelfAttention.relative_attention_bias
-        bias = rel.weight[bucket].permute(2, 0, 1)[None].to(dt)  # [1, H, S, S]
-        if mask is not None:
-            neg = torch.finfo(dt).min
-            bias = bias + torch.where(mask.to(ids.device)[:, None, None, :].bool(), 0.0, neg).to(dt)
         inner = c.heads * c.d_kv
+        flash = ids.is_cuda and dt != torch.float32 and c.d_kv <= 128
+        if flash:
+            # the flash kernel adds T5's bias by key-minus-query offset: one [H, 2S-1] table per forward;
+            # padding (right-padded prompts) as per-row key lengths
+            offs = torch.arange(-(S - 1), S, device=ids.device)
+            rb = rel.weight[t5_buckets(offs, c.buckets, c.max_distance)].t().float().contiguous()  # [H, 2S-1]
+            klen = None
+            if mask is not None:
+                n = mask.to(ids.device).sum(-1).to(torch.int32)
+                klen = torch.where(n > 0, n, torch.full_like(n, S)).contiguous()
+        else:
+            pos = torch.arange(S, device=ids.device)
+            bucket = t5_buckets(pos[None, :] - pos[:, None], c.buckets, c.max_distance)
+            bias = rel.weight[bucket].permute(2, 0, 1)[None].to(dt)  # [1, H, S, S]
+            if mask is not None:
+                neg = torch.finfo(dt).min
+                bias = bias + torch.where(mask.to(ids.device)[:, None, None, :].bool(), 0.0, neg).to(dt)
         for blk in self.encoder.block:
             sa, ff = blk.layer[0], blk.layer[1]
             a = sa.SelfAttention
             h = self._rms(x, sa.layer_norm.weight, dt)
-            q, k, v = (lin(h, w.weight).view(B, S, c.heads, c.d_kv).transpose(1, 2) for w in (a.q, a.k, a.v))
-            o = F.scaled_dot_product_attention(q, k, v, attn_mask=bias.expand(B, -1, -1, -1).to(q.dtype), scale=1.0)
-            o = o.transpose(1, 2).reshape(B * S, inner)
+            if flash:
+                q, k, v = (lin(h, w.weight) for w in (a.q, a.k, a.v))
+                o = torch.empty(B * S, inner, dtype=q.dtype, device=q.device)
+                K.attn_dense(q, k, v, o, B, S, S, c.heads, c.heads, c.d_kv, 1.0, klen=klen, rbias=rb)
+            else:
+                q, k, v = (lin(h, w.weight).view(B, S, c.heads, c.d_kv).transpose(1, 2) for w in (a.q, a.k, a.v))
+                o = F.scaled_dot_product_attention(q, k, v, attn_mask=bias.expand(B, -1, -1, -1).to(q.dtype),
+                                                   scale=1.0)
+                o = o.transpose(1, 2).reshape(B * S, inner)
             linear_acc(o, a.o, x)
             h = self._rms(x, ff.layer_norm.weight, dt)
             d = ff.DenseReluDense

@@ -516,14 +516,16 @@ def attn_prefill(q: torch.Tensor, k_cache, v_cache, block_tables: torch.Tensor, 
 
 def attn_dense(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, out: torch.Tensor, B: int, Sq: int, Sk: int,
                Hq: int, Hkv: int, D: int, scale: float, causal: bool = False,
-               qlen: torch.Tensor | None = None, klen: torch.Tensor | None = None, kv_rows: int = 0):
+               qlen: torch.Tensor | None = None, klen: torch.Tensor | None = None, kv_rows: int = 0,
+               rbias: torch.Tensor | None = None):
     """Flash attention over dense token-major 16-bit tensors (attention_dense.hip).
 
     q/out: [B*Sq, >= Hq*D] (row stride = .stride(0)); k/v: [B*kv_rows, >= Hkv*D] of which the first
     Sk rows per batch are read (kv_rows = 0 -> Sk; a fixed-capacity KV cache passes its capacity).
     Head dims other than 64/128 are zero-padded to the next supported size (exact: padded dims add
     0 to q.k and produce 0 output columns that are dropped). klen/qlen: optional int32 [B] valid
-    lengths (padding)."""
+    lengths (padding). rbias: optional fp32 [Hq, Sq + Sk - 1] additive bias by key-minus-query offset
+    (index j - i + Sq - 1; T5's relative position bias), added to the scaled logits."""
     if B == 0 or Sq == 0:
         return out
     R = kv_rows or Sk
@@ -536,6 +538,9 @@ def attn_dense(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, out: torch.Ten
             vf = vf.repeat_interleave(Hq // Hkv, 1)
         s = torch.einsum("bhqd,bhkd->bhqk", qf, kf) * scale
         kp = torch.arange(Sk)
+        if rbias is not None:
+            off = kp[None, :] - torch.arange(Sq)[:, None] + Sq - 1
+            s = s + rbias.float().cpu()[:, off][None]
         mask = torch.zeros(B, 1, Sq, Sk, dtype=torch.bool)
         if causal:
             mask |= (kp[None, :] > (torch.arange(Sq)[:, None] + (Sk - Sq)))[None, None]
@@ -556,15 +561,18 @@ def attn_dense(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, out: torch.Ten
             return torch.nn.functional.pad(x, (0, Dp - D)).reshape(t.shape[0], H * Dp)
         qp, kp_, vp = pad(q, Hq), pad(k[:B * R], Hkv), pad(v[:B * R], Hkv)
         op = torch.empty((out.shape[0], Hq * Dp), dtype=out.dtype, device=out.device)
-        attn_dense(qp, kp_, vp, op, B, Sq, Sk, Hq, Hkv, Dp, scale, causal, qlen, klen, R)
+        attn_dense(qp, kp_, vp, op, B, Sq, Sk, Hq, Hkv, Dp, scale, causal, qlen, klen, R, rbias)
         out[:, :Hq * D].copy_(op.view(-1, Hq, Dp)[..., :D].reshape(-1, Hq * D))
         return out
     if not (q.dtype == k.dtype == v.dtype == out.dtype):
         raise ValueError("attn_dense: q/k/v/out must share one 16-bit dtype")
+    if rbias is not None and (rbias.dtype != torch.float32 or not rbias.is_contiguous() or
+                              tuple(rbias.shape) != (Hq, Sq + Sk - 1)):
+        raise ValueError(f"attn_dense: rbias must be contiguous fp32 [{Hq}, {Sq + Sk - 1}]")
     N.ensure_act(out.dtype)
     N.kcall("mxk_attn_dense", q.data_ptr(), q.stride(0), k.data_ptr(), k.stride(0), v.data_ptr(), v.stride(0),
             out.data_ptr(), out.stride(0), B, Sq, Sk, Hq, Hkv, D, N.ptr(qlen), N.ptr(klen), int(causal),
-            float(scale), int(R), N.stream_ptr())
+            float(scale), int(R), N.ptr(rbias), Sq + Sk - 1, N.stream_ptr())
     return out
 
 

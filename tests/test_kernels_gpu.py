@@ -550,6 +550,32 @@ def test_attn_dense(dt, D, Hq, Hkv, causal):
     assert rel(out, ref) < 1.5e-2
 
 
+@pytest.mark.parametrize("D", [64, 32])
+def test_attn_dense_relative_bias(D):
+    """T5's relative-position bias as an additive [H, Sq + Sk - 1] table by key-minus-query offset, with key
+    padding, against an explicit [B, H, Sq, Sk] bias + mask in fp32."""
+    from localai_tfp_amd.models.diffusion.text_encoders import t5_buckets
+    B, S, H = 2, 77, 8
+    g = torch.Generator().manual_seed(5)
+    q, k, v = (torch.randn(B * S, H * D, generator=g).half() for _ in range(3))
+    table = torch.randn(32, H, generator=g) * 2
+    offs = torch.arange(-(S - 1), S)
+    rb = table[t5_buckets(offs, 32, 128)].t().contiguous()
+    klen = torch.tensor([S, 50], dtype=torch.int32)
+    pos = torch.arange(S)
+    bias = table[t5_buckets(pos[None, :] - pos[:, None], 32, 128)].permute(2, 0, 1)  # [H, S, S]
+    qf, kf, vf = (t.float().view(B, S, H, D).transpose(1, 2) for t in (q, k, v))
+    sc = qf @ kf.transpose(-1, -2) + bias[None]
+    sc = sc.masked_fill(pos[None, None, None, :] >= klen.view(B, 1, 1, 1), float("-inf"))
+    ref = (sc.softmax(-1) @ vf).transpose(1, 2).reshape(B * S, H * D)
+    cpu = torch.empty(B * S, H * D)
+    K.attn_dense(q, k, v, cpu, B, S, S, H, H, D, 1.0, klen=klen, rbias=rb)
+    assert rel(cpu, ref) < 1e-2
+    out = torch.empty(B * S, H * D, dtype=torch.float16, device=DEV)
+    K.attn_dense(q.to(DEV), k.to(DEV), v.to(DEV), out, B, S, S, H, H, D, 1.0, klen=klen.to(DEV), rbias=rb.to(DEV))
+    assert rel(out, ref) < 1.5e-2
+
+
 @pytest.mark.parametrize("causal", [False, True])
 def test_attn_dense_kv_capacity(causal):
     """Fixed-capacity KV cache read in place (kv_rows): Whisper decoder self-attention layout."""
