@@ -58,23 +58,38 @@ class SamplerBatch:
         self.device = torch.device(device)
         self._checked = False
 
+    @staticmethod
+    def _record(p: SamplingParams):
+        """The request-constant part of a row (cached on the params object: a request's sampling settings do
+        not change while it runs) and its base seed."""
+        c = p.__dict__.get("_mx_rec")
+        if c is None:
+            r = np.zeros(1, SAMPLE_DTYPE)
+            r["temperature"] = 0.0 if p.greedy else p.temperature
+            r["top_k"], r["top_p"], r["min_p"], r["typical_p"] = p.top_k, p.top_p, p.min_p, p.typical_p
+            r["repeat_penalty"] = p.repeat_penalty
+            r["presence_penalty"], r["frequency_penalty"] = p.presence_penalty, p.frequency_penalty
+            seed = p.seed if p.seed is not None and p.seed >= 0 else 0x5DEECE66D
+            simple = not (p.mirostat == 2 or p.repeat_penalty != 1.0 or p.presence_penalty or p.frequency_penalty
+                          or p.logit_bias)
+            c = p.__dict__["_mx_rec"] = (r, int(seed) & 0xFFFFFFFFFFFFFFFF, simple)
+        return c
+
     def pack(self, params: list[SamplingParams], histories: list[list[int]], steps: list[int],
              mirostat_mu: list[float] | None = None):
+        """Vectorised over rows: cached per-request records, seeds advanced per step in numpy; only rows with
+        penalties / logit bias / mirostat are visited in Python."""
         B = len(params)
-        arr = np.zeros(B, SAMPLE_DTYPE)
+        recs = [self._record(p) for p in params]
+        arr = np.concatenate([r[0] for r in recs]) if B else np.zeros(0, SAMPLE_DTYPE)
+        base = np.fromiter((r[1] for r in recs), np.uint64, B)
+        st = np.asarray(steps, np.uint64)
+        with np.errstate(over="ignore"):
+            arr["seed"] = base * np.uint64(1000003) + st
         toks, cnts, bias = [], [], []
-        for i, p in enumerate(params):
-            arr[i]["temperature"] = 0.0 if p.greedy else p.temperature
-            arr[i]["top_k"] = p.top_k
-            arr[i]["top_p"] = p.top_p
-            arr[i]["min_p"] = p.min_p
-            arr[i]["typical_p"] = p.typical_p
+        for i in (i for i, r in enumerate(recs) if not r[2]):
+            p = params[i]
             arr[i]["mirostat_tau"] = (mirostat_mu[i] if mirostat_mu else 2 * p.mirostat_tau) if p.mirostat == 2 else 0.0
-            arr[i]["repeat_penalty"] = p.repeat_penalty
-            arr[i]["presence_penalty"] = p.presence_penalty
-            arr[i]["frequency_penalty"] = p.frequency_penalty
-            seed = p.seed if p.seed is not None and p.seed >= 0 else 0x5DEECE66D
-            arr[i]["seed"] = (int(seed) * 1000003 + int(steps[i])) & 0xFFFFFFFFFFFFFFFF
             d: dict[int, list] = {}
             if p.repeat_penalty != 1.0 or p.presence_penalty or p.frequency_penalty:
                 hist = histories[i][-p.repeat_last_n:] if p.repeat_last_n > 0 else histories[i]
