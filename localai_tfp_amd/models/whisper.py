@@ -683,8 +683,8 @@ def _logsumexp(x: np.ndarray) -> float:
 # loading
 
 def load_whisper(path: str, device="cpu"):
-    """-> (WhisperModel, WhisperTokenizer). `path`: ggml .bin, HF directory / .safetensors, or
-    `synthetic:<preset>`."""
+    """-> (WhisperModel, WhisperTokenizer). `path`: ggml .bin, HF directory / .safetensors, a CTranslate2
+    (faster-whisper) directory with model.bin, or `synthetic:<preset>`."""
     import os
     from ..tokenizer.whisper import WhisperTokenizer
     if path.startswith("synthetic:"):
@@ -694,6 +694,26 @@ def load_whisper(path: str, device="cpu"):
             raise ValueError(f"unknown synthetic whisper preset {name!r}")
         w = synthetic_whisper(cfg, 0)
         return WhisperModel(cfg, w.get, device), WhisperTokenizer.synthetic(cfg.n_vocab)
+    ct2 = os.path.join(path, "model.bin") if os.path.isdir(path) else path if path.endswith("model.bin") else ""
+    if ct2 and os.path.isfile(ct2):
+        # CTranslate2 (faster-whisper) directory: model.bin + config.json + tokenizer / vocabulary files
+        from ..formats.ctranslate2 import read_model_bin, whisper_to_openai
+        d = os.path.dirname(ct2)
+        v, meta = read_model_bin(ct2)
+        if not meta["spec"].startswith("Whisper"):
+            raise ValueError(f"{ct2}: CTranslate2 spec {meta['spec']!r} is not a Whisper model")
+        w, heads = whisper_to_openai(v)
+
+        def nl(side):
+            return 1 + max(int(k.split(".")[2]) for k in w if k.startswith(f"{side}.blocks."))
+        cfg = WhisperConfig(n_vocab=w["decoder.token_embedding.weight"].shape[0],
+                            n_audio_ctx=w["encoder.positional_embedding"].shape[0],
+                            n_audio_state=w["encoder.conv1.weight"].shape[0], n_audio_head=heads["enc_heads"],
+                            n_audio_layer=nl("encoder"), n_text_ctx=w["decoder.positional_embedding"].shape[0],
+                            n_text_state=w["decoder.token_embedding.weight"].shape[1], n_text_head=heads["dec_heads"],
+                            n_text_layer=nl("decoder"), n_mels=w["encoder.conv1.weight"].shape[1],
+                            name=os.path.basename(os.path.abspath(d)))
+        return WhisperModel(cfg, w.get, device), WhisperTokenizer.from_hf_dir(d, cfg.n_vocab)
     if os.path.isdir(path) or path.endswith(".safetensors"):
         import json
         from safetensors.numpy import load_file

@@ -62,8 +62,23 @@ class WhisperTokenizer:
 
     @classmethod
     def from_hf_dir(cls, d: str, n_vocab: int) -> "WhisperTokenizer":
-        with open(os.path.join(d, "vocab.json"), encoding="utf-8") as f:
-            vocab = json.load(f)
+        """vocab.json (HF), else tokenizer.json's BPE vocab, else a CTranslate2 vocabulary.json / .txt
+        (faster-whisper model directories): byte-level unicode token strings -> ids."""
+        if os.path.isfile(os.path.join(d, "vocab.json")):
+            with open(os.path.join(d, "vocab.json"), encoding="utf-8") as f:
+                vocab = json.load(f)
+        elif os.path.isfile(os.path.join(d, "tokenizer.json")):
+            with open(os.path.join(d, "tokenizer.json"), encoding="utf-8") as f:
+                tj = json.load(f)
+            vocab = dict(tj["model"]["vocab"])
+            for t in tj.get("added_tokens", []):
+                vocab[t["content"]] = t["id"]
+        elif os.path.isfile(os.path.join(d, "vocabulary.json")):
+            with open(os.path.join(d, "vocabulary.json"), encoding="utf-8") as f:
+                vocab = {t: i for i, t in enumerate(json.load(f))}
+        else:
+            with open(os.path.join(d, "vocabulary.txt"), encoding="utf-8") as f:
+                vocab = {t.rstrip("\n"): i for i, t in enumerate(f)}
         dec = {c: b for b, c in _bytes_to_unicode().items()}
         pieces: list[bytes] = [b""] * (max(vocab.values()) + 1)
         for s, i in vocab.items():

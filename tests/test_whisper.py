@@ -242,3 +242,79 @@ def test_whisper_gpu_matches_cpu(weights):
         b = g.decode_step(sg, torch.tensor([t], device="cuda:0"))
         assert (b.cpu() - a).abs().max() < 5e-2
     assert sg.graph is not None
+
+
+def _openai_to_ct2(w: dict, cfg, int8: bool) -> dict:
+    """OpenAI names -> CTranslate2 WhisperSpec variables (written independently of the loader's map)."""
+    v = {"encoder/num_heads": np.int16(cfg.n_audio_head), "decoder/num_heads": np.int16(cfg.n_text_head)}
+
+    def q8(name, a):  # CTranslate2 int8: per-row scale 127 / amax, q = round(w * scale)
+        if not int8 or a.ndim != 2 or "embedding" in name or "position" in name:
+            v[name] = a.astype(np.float16) if int8 and a.ndim >= 2 else a
+            return
+        sc = 127.0 / np.maximum(np.abs(a).max(1), 1e-8)
+        v[name] = np.clip(np.rint(a * sc[:, None]), -127, 127).astype(np.int8)
+        v[name + "_scale"] = sc.astype(np.float32)
+    for n in ("conv1", "conv2"):
+        q8(f"encoder/{n}/weight", w[f"encoder.{n}.weight"])
+        v[f"encoder/{n}/bias"] = w[f"encoder.{n}.bias"]
+    v["encoder/position_encodings/encodings"] = w["encoder.positional_embedding"]
+    v["decoder/position_encodings/encodings"] = w["decoder.positional_embedding"]
+    v["decoder/embeddings/weight"] = w["decoder.token_embedding.weight"]
+    for side, ln_ in (("encoder", "ln_post"), ("decoder", "ln")):
+        v[f"{side}/layer_norm/gamma"], v[f"{side}/layer_norm/beta"] = w[f"{side}.{ln_}.weight"], w[f"{side}.{ln_}.bias"]
+    for side, n in (("encoder", cfg.n_audio_layer), ("decoder", cfg.n_text_layer)):
+        for i in range(n):
+            p, o = f"{side}/layer_{i}", f"{side}.blocks.{i}."
+            d = w[o + "attn.query.weight"].shape[0]
+            v[f"{p}/self_attention/layer_norm/gamma"] = w[o + "attn_ln.weight"]
+            v[f"{p}/self_attention/layer_norm/beta"] = w[o + "attn_ln.bias"]
+            q8(f"{p}/self_attention/linear_0/weight", np.concatenate([w[o + f"attn.{x}.weight"] for x in ("query", "key", "value")]))
+            v[f"{p}/self_attention/linear_0/bias"] = np.concatenate([w[o + "attn.query.bias"], np.zeros(d, np.float32), w[o + "attn.value.bias"]])
+            q8(f"{p}/self_attention/linear_1/weight", w[o + "attn.out.weight"])
+            v[f"{p}/self_attention/linear_1/bias"] = w[o + "attn.out.bias"]
+            if side == "decoder":
+                v[f"{p}/attention/layer_norm/gamma"] = w[o + "cross_attn_ln.weight"]
+                v[f"{p}/attention/layer_norm/beta"] = w[o + "cross_attn_ln.bias"]
+                q8(f"{p}/attention/linear_0/weight", w[o + "cross_attn.query.weight"])
+                v[f"{p}/attention/linear_0/bias"] = w[o + "cross_attn.query.bias"]
+                q8(f"{p}/attention/linear_1/weight", np.concatenate([w[o + "cross_attn.key.weight"], w[o + "cross_attn.value.weight"]]))
+                v[f"{p}/attention/linear_1/bias"] = np.concatenate([np.zeros(d, np.float32), w[o + "cross_attn.value.bias"]])
+                q8(f"{p}/attention/linear_2/weight", w[o + "cross_attn.out.weight"])
+                v[f"{p}/attention/linear_2/bias"] = w[o + "cross_attn.out.bias"]
+            v[f"{p}/ffn/layer_norm/gamma"], v[f"{p}/ffn/layer_norm/beta"] = w[o + "mlp_ln.weight"], w[o + "mlp_ln.bias"]
+            q8(f"{p}/ffn/linear_0/weight", w[o + "mlp.0.weight"])
+            v[f"{p}/ffn/linear_0/bias"] = w[o + "mlp.0.bias"]
+            q8(f"{p}/ffn/linear_1/weight", w[o + "mlp.2.weight"])
+            v[f"{p}/ffn/linear_1/bias"] = w[o + "mlp.2.bias"]
+    return v
+
+
+@pytest.mark.parametrize("int8", [False, True])
+def test_ctranslate2_faster_whisper_dir(tmp_path, weights, int8):
+    """faster-whisper (backend/python/faster-whisper/backend.py:26-62) model directories: CTranslate2 model.bin
+    (float32 or int8 + per-row scales, fused QKV / KV linears, projection aliased to the embeddings) +
+    config.json + tokenizer.json load into the same model as the OpenAI-named weights; parity with
+    ctranslate2 itself is unpinned (no ctranslate2 here, synthetic file)."""
+    import json as _json
+    from localai_tfp_amd.formats.ctranslate2 import read_model_bin, write_model_bin
+    d = tmp_path / "faster-whisper-test"
+    d.mkdir()
+    v = _openai_to_ct2(weights, CFG, int8)
+    write_model_bin(str(d / "model.bin"), v, "WhisperSpec", revision=3,
+                    aliases={"decoder/projection/weight": "decoder/embeddings/weight"})
+    back, meta = read_model_bin(str(d / "model.bin"))
+    assert meta["spec"] == "WhisperSpec" and back["decoder/projection/weight"].shape == v["decoder/embeddings/weight"].shape
+    (d / "config.json").write_text(_json.dumps({"suppress_ids": [], "suppress_ids_begin": [220, 50257]}))
+    tok = WhisperTokenizer.synthetic()
+    from localai_tfp_amd.tokenizer.whisper import _bytes_to_unicode
+    b2u = _bytes_to_unicode()
+    vocab = {"".join(b2u[b] for b in p): i for i, p in enumerate(tok.pieces)}
+    (d / "tokenizer.json").write_text(_json.dumps({"model": {"type": "BPE", "vocab": vocab}}), encoding="utf-8")
+    m, t2 = W.load_whisper(str(d), "cpu")
+    assert (m.cfg.n_audio_head, m.cfg.n_text_layer, m.cfg.n_vocab) == (CFG.n_audio_head, CFG.n_text_layer, CFG.n_vocab)
+    a = W.WhisperModel(CFG, weights.get, "cpu")
+    mel = torch.from_numpy(np.random.default_rng(2).standard_normal((1, CFG.n_mels, W.N_FRAMES)).astype(np.float32) * 0.5)
+    xa, xb = m.encode(mel), a.encode(mel)
+    assert (xa - xb).abs().max() < (5e-2 if int8 else 1e-4)
+    assert t2.decode(t2.encode("hello world")) == "hello world"
