@@ -184,8 +184,10 @@ struct QmmBMX {
         }
     }
     MX_DEV void prep(int jq) {
-        const int w = jq & 1;  // entries 2w, 2w+1 of the header half
-        const f16x2 s = __builtin_bit_cast(f16x2, hd[w]), mm = __builtin_bit_cast(f16x2, hd[2 + w]);
+        // entries 2w, 2w+1 of the header half (w = jq & 1). The words go through scalars first: a
+        // __builtin_bit_cast of a runtime-indexed ext_vector element reads element 0 (clang, ROCm 7.2)
+        const uint32_t sw = (jq & 1) ? hd[1] : hd[0], mw = (jq & 1) ? hd[3] : hd[2];
+        const f16x2 s = __builtin_bit_cast(f16x2, sw), mm = __builtin_bit_cast(f16x2, mw);
         s2[0] = (f16x2){s[0], s[0]};
         s2[1] = (f16x2){s[1], s[1]};
         m2[0] = (f16x2){mm[0], mm[0]};
