@@ -109,6 +109,112 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(float* __restrict__ qkv, c
     }
 }
 
+// Vectorised variant for the common case (rot_dim == D in {64, 128}, no per-head QK norm): each thread owns
+// whole rotation pairs — 4 consecutive dims (NORM: two adjacent pairs) or 4 dims + their partners D/2 away
+// (NEOX) — so every element is loaded once as a float4, written as 8-byte bf16 / 4-byte fp8 runs, and the
+// head / dim split is shifts instead of divisions.
+template <int D, bool NEOX, bool HAS_BIAS, bool ZERO, bool KV8>
+__global__ __launch_bounds__(256) void rope_kv4_kernel(float* __restrict__ qkv, const float* __restrict__ bias,
+                                                       const int* __restrict__ pos, const int* __restrict__ slots,
+                                                       const float* __restrict__ inv_freq, float attn_factor, int Hq,
+                                                       int Hkv, bf16_t* __restrict__ qo, void* __restrict__ kc,
+                                                       void* __restrict__ vc, int block_size) {
+    constexpr int HALF = D / 2;
+    constexpr int UPH = NEOX ? D / 8 : D / 4;  // work units per head
+    constexpr int USH = UPH == 8 ? 3 : UPH == 16 ? 4 : 5;
+    static_assert((1 << USH) == UPH, "units per head");
+    __shared__ float cs[HALF], sn[HALF];
+    const int t = blockIdx.x;
+    const int nh = Hq + Hkv;
+    const int hpg = (nh + gridDim.y - 1) / gridDim.y, vpg = (Hkv + gridDim.y - 1) / gridDim.y;
+    const int h_lo = blockIdx.y * hpg, h_hi = min(nh, h_lo + hpg);
+    const int v_lo = blockIdx.y * vpg, v_hi = min(Hkv, v_lo + vpg);
+    const int p = pos[t];
+    for (int i = threadIdx.x; i < HALF; i += 256) {
+        float sv, cv;
+        sincosf((float)p * inv_freq[i], &sv, &cv);
+        cs[i] = cv * attn_factor;
+        sn[i] = sv * attn_factor;
+    }
+    __syncthreads();
+    const int W = (Hq + 2 * Hkv) * D;
+    float* row = qkv + (size_t)t * W;
+    const int slot = slots[t];
+    const int blk = slot >= 0 ? slot / block_size : 0, off = slot >= 0 ? slot % block_size : 0;
+    auto ld4 = [&](int e) {
+        float4 x = *(const float4*)(row + e);
+        if (HAS_BIAS) {
+            const float4 b = *(const float4*)(bias + e);
+            x.x += b.x; x.y += b.y; x.z += b.z; x.w += b.w;
+        }
+        return x;
+    };
+    auto st4 = [&](int h, int d, float4 y) {
+        if (h < Hq) {
+            uint2 o = {pack_bf16x2(y.x, y.y), pack_bf16x2(y.z, y.w)};
+            *(uint2*)(qo + ((size_t)t * Hq + h) * D + d) = o;
+        } else if (slot >= 0) {
+            const size_t e = (((size_t)blk * Hkv + (h - Hq)) * block_size + off) * D + d;
+            if constexpr (KV8) {
+                ((uint8_t*)kc)[e] = f32_to_fp8(y.x); ((uint8_t*)kc)[e + 1] = f32_to_fp8(y.y);
+                ((uint8_t*)kc)[e + 2] = f32_to_fp8(y.z); ((uint8_t*)kc)[e + 3] = f32_to_fp8(y.w);
+            } else {
+                uint2 o = {pack_bf16x2(y.x, y.y), pack_bf16x2(y.z, y.w)};
+                *(uint2*)((bf16_t*)kc + e) = o;
+            }
+        }
+    };
+    const int total = (h_hi - h_lo) << USH;
+    for (int idx = threadIdx.x; idx < total; idx += 256) {
+        const int h = h_lo + (idx >> USH), u = idx & (UPH - 1);
+        if constexpr (NEOX) {
+            const int d = 4 * u;  // dims d..d+3 and their partners d+HALF..
+            const float4 a = ld4(h * D + d), b = ld4(h * D + d + HALF);
+            float4 ya, yb;
+            ya.x = a.x * cs[d] - b.x * sn[d];         yb.x = b.x * cs[d] + a.x * sn[d];
+            ya.y = a.y * cs[d + 1] - b.y * sn[d + 1]; yb.y = b.y * cs[d + 1] + a.y * sn[d + 1];
+            ya.z = a.z * cs[d + 2] - b.z * sn[d + 2]; yb.z = b.z * cs[d + 2] + a.z * sn[d + 2];
+            ya.w = a.w * cs[d + 3] - b.w * sn[d + 3]; yb.w = b.w * cs[d + 3] + a.w * sn[d + 3];
+            st4(h, d, ya);
+            st4(h, d + HALF, yb);
+        } else {
+            const int d = 4 * u, f = 2 * u;  // pairs (d, d+1) and (d+2, d+3): frequencies f, f+1
+            const float4 x = ld4(h * D + d);
+            float4 y;
+            y.x = x.x * cs[f] - x.y * sn[f];
+            y.y = x.y * cs[f] + x.x * sn[f];
+            y.z = x.z * cs[f + 1] - x.w * sn[f + 1];
+            y.w = x.w * cs[f + 1] + x.z * sn[f + 1];
+            st4(h, d, y);
+        }
+    }
+    float* vr = row + (Hq + Hkv) * D;
+    if (slot >= 0) {
+        for (int idx = v_lo * (D / 4) + threadIdx.x; idx < v_hi * (D / 4); idx += 256) {
+            const int kh = idx / (D / 4), d = (idx % (D / 4)) * 4;
+            float4 v = *(const float4*)(vr + kh * D + d);
+            if (HAS_BIAS) {
+                const float4 b = *(const float4*)(bias + (Hq + Hkv) * D + kh * D + d);
+                v.x += b.x; v.y += b.y; v.z += b.z; v.w += b.w;
+            }
+            const size_t e = (((size_t)blk * Hkv + kh) * block_size + off) * D + d;
+            if constexpr (KV8) {
+                ((uint8_t*)vc)[e] = f32_to_fp8(v.x); ((uint8_t*)vc)[e + 1] = f32_to_fp8(v.y);
+                ((uint8_t*)vc)[e + 2] = f32_to_fp8(v.z); ((uint8_t*)vc)[e + 3] = f32_to_fp8(v.w);
+            } else {
+                uint2 o = {pack_bf16x2(v.x, v.y), pack_bf16x2(v.z, v.w)};
+                *(uint2*)((bf16_t*)vc + e) = o;
+            }
+        }
+    }
+    if constexpr (ZERO) {
+        __syncthreads();
+        const float4 z = {0.f, 0.f, 0.f, 0.f};
+        for (int idx = h_lo * (D / 4) + threadIdx.x; idx < h_hi * (D / 4); idx += 256) *(float4*)(row + 4 * idx) = z;
+        for (int idx = v_lo * (D / 4) + threadIdx.x; idx < v_hi * (D / 4); idx += 256) *(float4*)(vr + 4 * idx) = z;
+    }
+}
+
 extern "C" int mxk_rope_kv(float* qkv, const float* bias, const int* pos, const int* slots,
                            const float* inv_freq, float attn_factor, int T, int Hq, int Hkv, int D, int rot_dim,
                            int neox, bf16_t* qo, void* kc, void* vc, int block_size, const float* qn,
@@ -121,6 +227,18 @@ extern "C" int mxk_rope_kv(float* qkv, const float* bias, const int* pos, const 
     int ng = (512 + T - 1) / T;
     ng = max(1, min(ng, min(8, Hkv)));
     const dim3 grid(T, ng);
+    if (!qkn && rot_dim == D && (D == 64 || D == 128) && !(((uintptr_t)qkv) & 15) && !(((uintptr_t)bias) & 15)) {
+#define RK4(D_, N_, B_, Z_, K8_) rope_kv4_kernel<D_, N_, B_, Z_, K8_><<<grid, 256, 0, st>>>(qkv, bias, pos, slots, inv_freq, attn_factor, Hq, Hkv, qo, kc, vc, block_size)
+#define RK4Z(D_, N_, B_) { if (zero_after) { if (kv_fp8) RK4(D_, N_, B_, true, true); else RK4(D_, N_, B_, true, false); } \
+                           else { if (kv_fp8) RK4(D_, N_, B_, false, true); else RK4(D_, N_, B_, false, false); } }
+#define RK4B(D_, N_) { if (bias) RK4Z(D_, N_, true) else RK4Z(D_, N_, false) }
+        if (D == 128) { if (neox) RK4B(128, true) else RK4B(128, false) }
+        else { if (neox) RK4B(64, true) else RK4B(64, false) }
+#undef RK4B
+#undef RK4Z
+#undef RK4
+        MXK_CHECK_LAUNCH();
+    }
 #define RKZ(N_, B_, Q_, K8_) { if (zero_after) rope_kv_kernel<N_, B_, Q_, true, K8_><<<grid, 256, 0, st>>>(qkv, bias, pos, slots, inv_freq, attn_factor, Hq, Hkv, D, rot_dim, qo, kc, vc, block_size, qn, kn, eps); \
     else rope_kv_kernel<N_, B_, Q_, false, K8_><<<grid, 256, 0, st>>>(qkv, bias, pos, slots, inv_freq, attn_factor, Hq, Hkv, D, rot_dim, qo, kc, vc, block_size, qn, kn, eps); }
 #define RK(N_, B_, Q_) { if (kv_fp8) RKZ(N_, B_, Q_, true) else RKZ(N_, B_, Q_, false) }

@@ -170,6 +170,16 @@ def test_rope_kv(neox, D, rot):
         outs.append((q.cpu(), kc.cpu(), vc.cpu()))
     for a, b in zip(*outs):
         assert rel(b, a) < 1e-2
+    # zero_after: the fp32 QKV rows are handed back zeroed (the next split-K GEMM accumulates into them)
+    qd = qkv.to(DEV)
+    q = torch.empty(T, Hq, D, dtype=torch.bfloat16, device=DEV)
+    kc = torch.zeros(nb, Hkv, bs, D, dtype=torch.bfloat16, device=DEV)
+    vc = torch.zeros_like(kc)
+    K.rope_kv(qd, bias.to(DEV), pos.to(DEV), slots.to(DEV), inv.to(DEV), af, Hq, Hkv, D, rot, neox, q, kc, vc, bs,
+              zero_after=True)
+    assert int((qd != 0).sum()) == 0
+    for a, b in zip(outs[0], (q.cpu(), kc.cpu(), vc.cpu())):
+        assert rel(b, a) < 1e-2
 
 
 def _paged_kv(nb, Hkv, bs, D, seed):
