@@ -144,8 +144,22 @@ class UNetPipeline:
     # ------------------------------------------------------------------ conditioning
     @torch.no_grad()
     def encode_prompts(self, prompts: list[str], clip_skip: int = 0):
+        """-> (context [B, 77, D], pooled or None). With prompt weighting on (env COMPEL=1, as the reference's
+        diffusers backend, or the pipeline's `compel` attribute) and weighted prompts, per-token weights scale
+        each position's offset from the empty-prompt embedding (models/diffusion/prompt_weights.py)."""
+        from . import prompt_weights as PW
+        if (os.environ.get("COMPEL", "0") == "1" or getattr(self, "compel", False)) and \
+                any(PW.has_syntax(p) for p in prompts):
+            parts = [PW.weighted_ids(self.tok1, p) for p in prompts]
+            h, pooled = self._encode_ids([x[0] for x in parts], [PW.parse(p) for p in prompts], clip_skip)
+            he, _ = self._encode_ids([self.tok1("")] * len(prompts), None, clip_skip)
+            h = torch.stack([PW.apply(h[b], he[b], parts[b][1]) for b in range(len(prompts))])
+            return h, pooled
+        return self._encode_ids([self.tok1(p) for p in prompts], None, clip_skip, prompts)
+
+    def _encode_ids(self, ids1: list, chunks, clip_skip: int, prompts: list[str] | None = None):
         dev = self.device
-        i1 = torch.tensor([self.tok1(p) for p in prompts], device=dev)
+        i1 = torch.tensor(ids1, device=dev)
         if not self.xl:
             # SD1.x/2.x: last hidden state through the final LayerNorm (clip_skip N: layer -(N+1), normed)
             h, _ = self.te1(i1, self.tok1.eos, max(0, clip_skip - 1) if clip_skip > 1 else 0)
@@ -157,7 +171,13 @@ class UNetPipeline:
         # SDXL: penultimate hidden states of both encoders (no final LN), pooled from CLIP-G
         skip = 1 + max(0, clip_skip - 1)
         h1, _ = self.te1(i1, self.tok1.eos, skip)
-        i2 = torch.tensor([self.tok2(p) for p in prompts], device=dev)
+        if chunks is not None:  # weighted prompts: CLIP-G sees the same syntax-free text
+            from . import prompt_weights as PW
+            i2 = torch.tensor([PW.weighted_ids(self.tok2, "".join(t for t, _ in c))[0] for c in chunks], device=dev)
+        elif prompts is not None:
+            i2 = torch.tensor([self.tok2(p) for p in prompts], device=dev)
+        else:
+            i2 = torch.tensor([self.tok2("")] * len(ids1), device=dev)
         h2, pooled = self.te2(i2, self.tok2.eos, skip)
         return torch.cat([h1, h2], -1), pooled
 

@@ -4,7 +4,7 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out; export TMPDIR=/tmp PYTHONPATH=$PWD
 timeout -k 10 300 python -u -m pytest tests/test_diffusion.py tests/test_sd_gguf_quant.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/j6_diff.log 2>&1 || { tail -30 gpurun_out/j6_diff.log; exit 1; }
 tail -1 gpurun_out/j6_diff.log
-timeout -k 10 300 python -u -m pytest tests/test_quant_formats.py tests/test_kernels_gpu.py -m gpu -k "mxf or carried or qmm or qmv_t32 or qmatmul or relative_bias" -x -q --timeout 120 --timeout-method thread > gpurun_out/j6_mxf.log 2>&1 || { tail -30 gpurun_out/j6_mxf.log; exit 1; }
+timeout -k 10 300 python -u -m pytest tests/test_quant_formats.py tests/test_kernels_gpu.py -m gpu -k "mxf or carried or qmm or qmv_t32 or qmatmul or relative_bias or rope" -x -q --timeout 120 --timeout-method thread > gpurun_out/j6_mxf.log 2>&1 || { tail -30 gpurun_out/j6_mxf.log; exit 1; }
 tail -1 gpurun_out/j6_mxf.log
 timeout -k 10 300 python -u -m pytest tests/test_tts.py tests/test_bark.py tests/test_musicgen.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/j6_audio.log 2>&1 || { tail -30 gpurun_out/j6_audio.log; exit 1; }
 tail -1 gpurun_out/j6_audio.log
