@@ -10,9 +10,10 @@ model directory (``config.json`` + ``*.safetensors`` [+ ``model.safetensors.inde
 * HF tensor names -> the GGUF names the model loader consumes, with the conversions llama.cpp's
   convert_hf_to_gguf applies: Q/K rows permuted to adjacent-pair rotary order for NORM-rope
   architectures, Gemma RMSNorm weights stored as (1 + w), per-expert tensors stacked;
-* weights are quantised at load into a GPU-native block format (``quant``: q8_0 default — 8.5 bits,
-  within the dequant error of the bf16 checkpoint — or q4_k / q6_k), so the qmm / qmv kernels stream
-  them like any GGUF model; ``f16`` / ``bf16`` / ``f32`` keep a dense copy (hipBLASLt path).
+* weights stay bf16 by default (the precision the reference's vLLM / transformers backends serve;
+  hipBLASLt GEMMs), or are quantised at load into a GPU-native block format with the ``quant`` option
+  (q8_0 — 8.5 bits, within the dequant error of the bf16 checkpoint — q4_k / q6_k), so the qmm / qmv
+  kernels stream them like any GGUF model; ``f16`` / ``f32`` keep other dense copies.
 """
 from __future__ import annotations
 

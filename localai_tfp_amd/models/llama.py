@@ -354,6 +354,10 @@ class LlamaModel:
         """Re-lay the dense-layer projections (and the LM head) out in the t32 tiled layout the qmm /
         qmv kernels stream (ops/quant.py tile32). After gate|up interleaving and Q|K|V fusion, which
         work on the row layout; MoE expert stacks keep theirs (moe.py kernels). No-op on CPU / bf16 mode."""
+        # the q8-activation decode GEMVs need block-quantised weights: a dense (F16 / BF16) checkpoint runs
+        # its small batches through the 16-bit GEMM path instead
+        self._gemv_ok = all(not isinstance(w, QWeight) or w.is_quant for L in self.layers
+                            for w in (*L.qkv_parts, L.wo, L.wgu, L.wg, L.wu, L.wd))
         if self.device.type != "cuda":
             return
         for L in self.layers:
@@ -469,7 +473,7 @@ class LlamaModel:
         qd, kvd = Hq * D, Hkv * D
         F = self.layers[0].wd.K if self.layers and self.layers[0].wd is not None else 0
         eps = cfg.rms_eps
-        gemv = T <= GEMV_MAX_M and self.device.type == "cuda"
+        gemv = T <= GEMV_MAX_M and self.device.type == "cuda" and getattr(self, "_gemv_ok", True)
         nd = fb.n_decode
         h = ws.h[:T]
         if not self.stage:  # a pipeline stage finds its input hidden rows in ws.h

@@ -55,10 +55,12 @@ def load_llm(model: str, device="cpu", tp_rank: int = 0, tp_size: int = 1, tp_gr
         return m, ByteTokenizer(cfg.vocab), cfg, {}
     from .hf import QUANTS, hf_source, is_hf_dir
     if is_hf_dir(model):  # vllm / transformers backends: HF safetensors directory (models/hf.py)
-        q = str(ov.get("hf_quant") or "q8_0").lower()
+        # bf16 by default, as the reference's vLLM / transformers backends serve HF checkpoints; `quant:
+        # q8_0 | q4_k | q6_k` opts into the quantised kernels
+        q = str(ov.get("hf_quant") or "bf16").lower()
         if q not in QUANTS:
-            log.warning("quantization %r is not a load-time format here; using q8_0", q)
-            q = "q8_0"
+            log.warning("quantization %r is not a load-time format here; using bf16", q)
+            q = "bf16"
         cfg, get = hf_source(model, q)
         _apply_overrides(cfg, ov)
         m = LlamaModel.load(cfg, _lora_source(get, ov, cfg), device, tp_rank, tp_size, tp_group)

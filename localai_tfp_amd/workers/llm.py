@@ -209,7 +209,7 @@ class LLMServicer(BackendServicer):
                   "rope_scaling": request.RopeScaling, "rms_norm_eps": request.RMSNormEps,
                   "lora": _lora_list(request, path), "lora_requant": opts.get("lora_requant", "q8_0"),
                   # HF safetensors checkpoints (vllm / transformers backends): load-time block format
-                  "hf_quant": opts.get("quant") or request.Quantization or "q8_0"}
+                  "hf_quant": opts.get("quant") or request.Quantization or "bf16"}
             ec = EngineConfig()
             if request.ContextSize > 0:
                 ec.max_model_len = int(request.ContextSize)

@@ -81,8 +81,12 @@ def test_hf_dir_matches_transformers(arch, tmp_path):
     got = _ours(model, prompt)
     rel = float((got - ref).norm() / ref.norm())
     assert rel < 5e-3, (arch, rel)
-    # default load-time format: Q8_0 blocks (the GPU-native qmm / qmv layout)
-    model8, *_ = load_llm(d, "cpu")
+    # default: bf16 (the reference's vLLM / transformers precision); `quant: q8_0` -> Q8_0 blocks (qmm / qmv layout)
+    modelb, *_ = load_llm(d, "cpu")
+    assert modelb.layers[0].wo.qtype == "dense"
+    relb = float((_ours(modelb, prompt) - ref).norm() / ref.norm())
+    assert relb < 2e-2, (arch, relb)
+    model8, *_ = load_llm(d, "cpu", overrides={"hf_quant": "q8_0"})
     assert model8.layers[0].wo.qtype == 8
     got8 = _ours(model8, prompt)
     rel8 = float((got8 - ref).norm() / ref.norm())
@@ -140,10 +144,16 @@ def test_hf_dir_gpu_q8_0(tmp_path):
     prompt = [int(x) for x in np.random.default_rng(5).integers(3, 512, 23)]
     with torch.no_grad():
         ref = hm(torch.tensor([prompt])).logits[0, -1].float()
-    model, *_ = load_llm(str(tmp_path), "cuda:0")
+    model, *_ = load_llm(str(tmp_path), "cuda:0", overrides={"hf_quant": "q8_0"})
     w = model.layers[0].wo
     assert w.is_quant and w.layout == "t32" and w.bf16_cache is None
     from test_model_gpu import _run
     got = _run(model, "cuda", prompt, [])[0][0].float().cpu()
     rel = float((got - ref).norm() / ref.norm())
     assert rel < 5e-2, rel
+    # default: bf16 weights (the reference's vLLM / transformers precision), small batches on the 16-bit path
+    model, *_ = load_llm(str(tmp_path), "cuda:0")
+    assert not model.layers[0].wo.is_quant and not model._gemv_ok
+    got = _run(model, "cuda", prompt, [])[0][0].float().cpu()
+    rel = float((got - ref).norm() / ref.norm())
+    assert rel < 3e-2, rel
