@@ -304,7 +304,8 @@ __global__ __launch_bounds__(SNT) void sample_kernel(float* __restrict__ logits,
         s_n = 0;
     }
     __syncthreads();
-    const float cut = mx - ((float)s_bin + 1.01f) * BW;  // gather every v > cut (a superset of the kept set)
+    // fewer than K entries within TK_HR of the slice max (a sparse allow mask): take every entry
+    const float cut = s_bin == TK_HB - 1 ? -INFINITY : mx - ((float)s_bin + 1.01f) * BW;  // gather every v > cut (a superset of the kept set)
     // pass 3: gather candidates
     auto gather = [&](int i, float v) {
         if (v == -INFINITY || !(v > cut || v == mx)) return;
@@ -411,6 +412,243 @@ extern "C" int mxk_sample(float* logits, int ld, int B, int V, const SampleParam
 }
 
 extern "C" int mxk_sample_params_size() { return (int)sizeof(SampleParams); }
+
+// ---- small batches with top-k on: the vocabulary split over many workgroups ----------------------------
+// One workgroup per row reads the 128k-entry row from one CU (~0.2 ms at batch 1). With top-k <= TK_CAP on,
+// every quantity the chain needs lives in the global top-k set (top-p's target is top_p x the top-k mass,
+// min-p is relative to the max), and the global top-k is contained in the union of per-slice top-ks:
+//   tk_slice_kernel  (B x S workgroups): slice max, slice histogram, gather + sort the slice's top-k
+//   tk_merge_kernel  (B workgroups):     merge the S x k candidates, truncate exactly, Gumbel-max draw.
+constexpr int TK_CAP = 64, TK_NT = 256, TK_HB = 1024;
+constexpr float TK_HR = 48.f;
+
+__global__ __launch_bounds__(TK_NT) void tk_penalty_kernel(float* logits, int ld, int V, const SampleParams* params,
+                                                          const int* pen_tok, const int* pen_cnt, const float* pen_bias) {
+    const SampleParams P = params[blockIdx.x];
+    float* x = logits + (size_t)blockIdx.x * ld;
+    for (int i = threadIdx.x; i < P.pen_count; i += TK_NT) {
+        const int t = pen_tok[P.pen_offset + i];
+        if (t < 0 || t >= V) continue;
+        const int c = pen_cnt[P.pen_offset + i];
+        float v = x[t];
+        if (c > 0) {
+            if (P.repeat_penalty != 1.f) v = v > 0.f ? v / P.repeat_penalty : v * P.repeat_penalty;
+            v -= P.frequency_penalty * (float)c + P.presence_penalty;
+        }
+        v += pen_bias[P.pen_offset + i];
+        x[t] = v;
+    }
+}
+
+__global__ __launch_bounds__(TK_NT) void tk_slice_kernel(const float* __restrict__ logits, int ld, int V,
+                                                        const SampleParams* __restrict__ params,
+                                                        const uint32_t* __restrict__ allow_mask, int mask_ld,
+                                                        float* __restrict__ cand_v, int* __restrict__ cand_i,
+                                                        int* __restrict__ cand_n) {
+    __shared__ float red[TK_NT / 64];
+    __shared__ unsigned hcnt[TK_HB];
+    __shared__ float cv[2 * TK_CAP * 4];
+    __shared__ int ci[2 * TK_CAP * 4];
+    __shared__ int s_n, s_bin;
+    const int row = blockIdx.x, S = gridDim.y, sl = blockIdx.y;
+    const SampleParams P = params[row];
+    const int K = P.temperature <= 0.f ? 1 : min(P.top_k, TK_CAP);
+    const float itemp = P.temperature <= 0.f ? 1.f : 1.f / P.temperature;
+    const float* x = logits + (size_t)row * ld;
+    const uint32_t* am = allow_mask ? allow_mask + (size_t)row * mask_ld : nullptr;
+    const int L = (V + S - 1) / S, i0 = sl * L, i1 = min(V, i0 + L);
+    auto val = [&](int i) -> float {
+        if (am && !((am[i >> 5] >> (i & 31)) & 1u)) return -INFINITY;
+        return x[i] * itemp;
+    };
+    float mx = -INFINITY;
+    for (int i = i0 + threadIdx.x; i < i1; i += TK_NT) mx = fmaxf(mx, val(i));
+    mx = wave_max(mx);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
+    for (int b = threadIdx.x; b < TK_HB; b += TK_NT) hcnt[b] = 0u;
+    __syncthreads();
+    mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    constexpr float IBW = (float)TK_HB / TK_HR, BW = TK_HR / (float)TK_HB;
+    for (int i = i0 + threadIdx.x; i < i1; i += TK_NT) {
+        const float v = val(i);
+        if (v == -INFINITY) continue;
+        atomicAdd(&hcnt[min(TK_HB - 1, (int)((mx - v) * IBW))], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned c = 0;
+        int b = 0;
+        for (; b < TK_HB - 1; ++b) {
+            c += hcnt[b];
+            if (c >= (unsigned)K) break;
+        }
+        s_bin = b;
+        s_n = 0;
+    }
+    __syncthreads();
+    // fewer than K entries within TK_HR of the slice max (a sparse allow mask): take every entry
+    const float cut = s_bin == TK_HB - 1 ? -INFINITY : mx - ((float)s_bin + 1.01f) * BW;
+    constexpr int CAPL = 2 * TK_CAP * 4;
+    for (int i = i0 + threadIdx.x; i < i1; i += TK_NT) {
+        const float v = val(i);
+        if (v == -INFINITY || !(v > cut || v == mx)) continue;  // (an all-masked slice gathers nothing)
+        const int k = atomicAdd(&s_n, 1);
+        if (k < CAPL) { cv[k] = v; ci[k] = i; }
+    }
+    __syncthreads();
+    const int n = min(s_n, CAPL);  // a bin holding > CAPL - K entries: the first CAPL are kept (exactly
+                                   // representable ties beyond are the only loss; the histogram bins are
+                                   // 0.047 logits wide)
+    int np = 1;
+    while (np < n) np <<= 1;
+    for (int k = n + threadIdx.x; k < np; k += TK_NT) { cv[k] = -INFINITY; ci[k] = 0x7fffffff; }
+    __syncthreads();
+    for (int size = 2; size <= np; size <<= 1) {
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            for (int t = threadIdx.x; t < np / 2; t += TK_NT) {
+                const int lo = 2 * t - (t & (stride - 1)), hi = lo + stride;
+                const bool desc = (lo & size) == 0;
+                const float a = cv[lo], bb = cv[hi];
+                const int ia = ci[lo], ib = ci[hi];
+                const bool a_first = a > bb || (a == bb && ia < ib);
+                if (a_first != desc) { cv[lo] = bb; cv[hi] = a; ci[lo] = ib; ci[hi] = ia; }
+            }
+            __syncthreads();
+        }
+    }
+    // this slice's top-K plus every entry tied with its K-th value (top-k keeps ties)
+    int keep = min(n, K);
+    if (keep > 0) while (keep < n && keep < 2 * K && cv[keep] == cv[keep - 1]) ++keep;
+    const size_t base = ((size_t)row * S + sl) * (2 * TK_CAP);
+    for (int k = threadIdx.x; k < keep; k += TK_NT) { cand_v[base + k] = cv[k]; cand_i[base + k] = ci[k]; }
+    if (threadIdx.x == 0) cand_n[row * S + sl] = keep;
+}
+
+__global__ __launch_bounds__(1024) void tk_merge_kernel(const float* __restrict__ logits, int ld,
+                                                       const SampleParams* __restrict__ params, int S,
+                                                       const float* __restrict__ cand_v, const int* __restrict__ cand_i,
+                                                       const int* __restrict__ cand_n, int* __restrict__ out_tok,
+                                                       float* __restrict__ out_logp) {
+    constexpr int CAP = 4096;
+    __shared__ float cv[CAP];
+    __shared__ int ci[CAP];
+    __shared__ int s_off[65], s_keep;
+    __shared__ float red[16], rv[16];
+    __shared__ int ri[16];
+    const int row = blockIdx.x;
+    const SampleParams P = params[row];
+    const bool greedy = P.temperature <= 0.f;
+    const int K = greedy ? 1 : min(P.top_k, TK_CAP);
+    if (threadIdx.x == 0) {
+        int o = 0;
+        for (int s = 0; s < S; ++s) { s_off[s] = o; o += cand_n[row * S + s]; }
+        s_off[S] = min(o, CAP);
+    }
+    __syncthreads();
+    const int n = s_off[S];
+    for (int s = 0; s < S; ++s) {
+        const int c = min(cand_n[row * S + s], CAP - s_off[s]);
+        for (int k = threadIdx.x; k < c; k += 1024) {
+            cv[s_off[s] + k] = cand_v[((size_t)row * S + s) * (2 * TK_CAP) + k];
+            ci[s_off[s] + k] = cand_i[((size_t)row * S + s) * (2 * TK_CAP) + k];
+        }
+    }
+    int np = 1;
+    while (np < n) np <<= 1;
+    for (int k = n + threadIdx.x; k < np; k += 1024) { cv[k] = -INFINITY; ci[k] = 0x7fffffff; }
+    __syncthreads();
+    for (int size = 2; size <= np; size <<= 1) {
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            for (int t = threadIdx.x; t < np / 2; t += 1024) {
+                const int lo = 2 * t - (t & (stride - 1)), hi = lo + stride;
+                const bool desc = (lo & size) == 0;
+                const float a = cv[lo], bb = cv[hi];
+                const int ia = ci[lo], ib = ci[hi];
+                const bool a_first = a > bb || (a == bb && ia < ib);
+                if (a_first != desc) { cv[lo] = bb; cv[hi] = a; ci[lo] = ib; ci[hi] = ia; }
+            }
+            __syncthreads();
+        }
+    }
+    const float mx = cv[0];
+    if (threadIdx.x == 0) {  // the bisection chain's semantics (see sample_kernel)
+        int keep = n;
+        if (K < keep) {
+            const float kv = cv[K - 1];
+            keep = K;
+            while (keep < n && cv[keep] == kv) ++keep;
+        }
+        float zk = 0.f;
+        const bool tp = P.top_p < 1.f && P.top_p > 0.f;
+        if (tp)
+            for (int k = 0; k < keep; ++k) zk += __expf(cv[k] - mx);
+        if (P.min_p > 0.f && P.min_p <= 1.f) {
+            const float mv = mx + __logf(P.min_p);
+            while (keep > 1 && cv[keep - 1] < mv) --keep;
+        }
+        if (tp) {
+            float cum = 0.f;
+            int k = 0;
+            while (k < keep) {
+                cum += __expf(cv[k] - mx);
+                ++k;
+                if (cum >= P.top_p * zk) break;
+            }
+            while (k < keep && cv[k] == cv[k - 1]) ++k;
+            keep = max(1, k);
+        }
+        s_keep = keep;
+    }
+    __syncthreads();
+    const int keep = s_keep;
+    float best = -INFINITY, zk = 0.f;
+    int bi = 0x7fffffff;
+    for (int k = threadIdx.x; k < keep; k += 1024) {
+        const float sc = greedy ? cv[k] : cv[k] + gumbel(P.seed, (uint32_t)ci[k]);
+        zk += __expf(cv[k] - mx);
+        if (sc > best || (sc == best && ci[k] < bi)) { best = sc; bi = ci[k]; }
+    }
+    zk = wave_sum(zk);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = zk;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const float ob = __shfl_xor(best, o, 64);
+        const int oi = __shfl_xor(bi, o, 64);
+        if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+    }
+    if ((threadIdx.x & 63) == 0) { rv[threadIdx.x >> 6] = best; ri[threadIdx.x >> 6] = bi; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float b = rv[0], z = red[0];
+        int id = ri[0];
+        for (int w = 1; w < 16; ++w) {
+            z += red[w];
+            if (rv[w] > b || (rv[w] == b && ri[w] < id)) { b = rv[w]; id = ri[w]; }
+        }
+        if (id == 0x7fffffff) id = 0;
+        out_tok[row] = id;
+        if (out_logp) {
+            const float itemp = greedy ? 1.f : 1.f / P.temperature;
+            out_logp[row] = greedy ? 0.f : logits[(size_t)row * ld + id] * itemp - mx - __logf(fmaxf(z, 1e-30f));
+        }
+    }
+}
+
+// B rows, S slices per row (<= 64, S * 2 * max top_k <= 4096 so the merge holds every candidate); every row
+// must have top_k in [1, TK_CAP] or be greedy, no typical-p / mirostat (the caller checks).
+// cand_v / cand_i: [B][S][2*TK_CAP] scratch, cand_n: [B][S].
+extern "C" int mxk_sample_topk_split(float* logits, int ld, int B, int V, const SampleParams* params, int has_pen,
+                                     const int* pen_tok, const int* pen_cnt, const float* pen_bias,
+                                     const uint32_t* allow_mask, int mask_ld, int S, float* cand_v, int* cand_i,
+                                     int* cand_n, int* out_tok, float* out_logp, hipStream_t st) {
+    if (B <= 0) return 0;
+    if (S < 1 || S > 64) return (int)hipErrorInvalidValue;
+    if (has_pen) tk_penalty_kernel<<<B, TK_NT, 0, st>>>(logits, ld, V, params, pen_tok, pen_cnt, pen_bias);
+    tk_slice_kernel<<<dim3(B, S), TK_NT, 0, st>>>(logits, ld, V, params, allow_mask, mask_ld, cand_v, cand_i, cand_n);
+    tk_merge_kernel<<<B, 1024, 0, st>>>(logits, ld, params, S, cand_v, cand_i, cand_n, out_tok, out_logp);
+    MXK_CHECK_LAUNCH();
+}
+extern "C" int mxk_sample_topk_cap() { return TK_CAP; }
 
 // greedy argmax over rows (fast path used by the decode graph when every row is greedy)
 __global__ __launch_bounds__(1024) void argmax_kernel(const float* __restrict__ x, int ld, int V,

@@ -145,10 +145,46 @@ class SamplerBatch:
                                                 bias.view(np.uint8)])
         tok = torch.empty(B, dtype=torch.int32, device=dev)
         lp = torch.empty(B, dtype=torch.float32, device=dev)
+        S = self._split_slices(params, B)
+        if S:
+            # small batch, top-k on: the vocabulary split over B x S workgroups instead of one CU per row
+            cv, ci, cn = self._split_scratch(dev, B, S)
+            N.kcall("mxk_sample_topk_split", logits.data_ptr(), logits.stride(0), B, V, pbuf.data_ptr(),
+                    int(bool(arr["pen_count"].any())), t_t.data_ptr(), c_t.data_ptr(), b_t.data_ptr(),
+                    N.ptr(allow_mask), allow_mask.stride(0) if allow_mask is not None else 0, S, cv.data_ptr(),
+                    ci.data_ptr(), cn.data_ptr(), tok.data_ptr(), lp.data_ptr(), N.stream_ptr())
+            return tok, lp
         N.kcall("mxk_sample", logits.data_ptr(), logits.stride(0), B, V, pbuf.data_ptr(), t_t.data_ptr(),
                 c_t.data_ptr(), b_t.data_ptr(), N.ptr(allow_mask), allow_mask.stride(0) if allow_mask is not None else 0,
                 tok.data_ptr(), lp.data_ptr(), N.stream_ptr())
         return tok, lp
+
+    SPLIT_MAX_B = 16
+    TOPK_CAP = 64
+
+    def _split_slices(self, params, B: int) -> int:
+        """Slices per row for the split top-k sampler, or 0 where it does not apply (large batch, top-k off or
+        above the cap, typical-p / mirostat rows)."""
+        if B > self.SPLIT_MAX_B:
+            return 0
+        kmax = 1
+        for p in params:
+            if p.greedy:
+                continue
+            if not (0 < p.top_k <= self.TOPK_CAP) or (0 < p.typical_p < 1) or p.mirostat == 2:
+                return 0
+            kmax = max(kmax, p.top_k)
+        return max(1, min(64, 4096 // (2 * kmax)))
+
+    def _split_scratch(self, dev, B: int, S: int):
+        key = (str(dev), B, S)
+        c = getattr(self, "_scratch", None)
+        if c is None or c[0] != key:
+            cv = torch.empty(B * S * 2 * self.TOPK_CAP, dtype=torch.float32, device=dev)
+            ci = torch.empty(B * S * 2 * self.TOPK_CAP, dtype=torch.int32, device=dev)
+            cn = torch.empty(B * S, dtype=torch.int32, device=dev)
+            c = self._scratch = (key, cv, ci, cn)
+        return c[1], c[2], c[3]
 
 
 def sample_ref(logits: torch.Tensor, params, histories, steps, allow_mask=None):

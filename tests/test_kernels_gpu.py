@@ -741,3 +741,36 @@ def test_sampling_fast_path_distribution():
         cnt[int(tok[0])] += 1
     freq = cnt / cnt.sum()
     assert np.allclose(freq, [0.0, 0.2 / 0.9, 0.3 / 0.9, 0.4 / 0.9], atol=0.04), freq
+
+
+@pytest.mark.parametrize("B", [1, 3, 16])
+def test_sampling_topk_split_matches_row_kernel(B):
+    """Small batches with top-k on go through the split-vocabulary sampler (B x S slice workgroups + a merge);
+    with the same seeds it draws exactly the token the one-workgroup-per-row kernel draws, with the same
+    log-probability, including penalties, logit bias, an allow mask and greedy rows."""
+    from localai_tfp_amd.ops.sampling import SamplerBatch, SamplingParams
+    torch.manual_seed(5)
+    V = 128256
+    logits = torch.randn(B, V, device=DEV) * 2.0
+    logits[0, 100:140] += 5.0
+    mask = torch.full((B, (V + 31) // 32), -1, dtype=torch.int32, device=DEV)
+    if B > 1:
+        mask[1] = 0
+        mask[1, 10:20] = -1  # row 1: only 320 tokens allowed, spread over one slice
+    ps = []
+    for r in range(B):
+        if r == 2:
+            ps.append(SamplingParams(temperature=0.0, seed=r))
+        else:
+            ps.append(SamplingParams(temperature=0.8, top_k=[40, 64, 1, 7][r % 4], top_p=[0.95, 1.0, 0.9][r % 3],
+                                     min_p=[0.05, 0.0][r % 2], repeat_penalty=1.1, frequency_penalty=0.2,
+                                     logit_bias={5: 2.0, 120: -3.0}, seed=100 + r))
+    hist = [[120, 121, 5, 121] for _ in range(B)]
+    split, full = SamplerBatch(DEV), SamplerBatch(DEV)
+    full.SPLIT_MAX_B = 0
+    assert split._split_slices(ps, B) > 0 and full._split_slices(ps, B) == 0
+    for step in range(4):
+        t1, l1 = split.sample(logits.clone(), ps, hist, [step] * B, allow_mask=mask)
+        t2, l2 = full.sample(logits.clone(), ps, hist, [step] * B, allow_mask=mask)
+        assert t1.cpu().tolist() == t2.cpu().tolist(), step
+        assert torch.allclose(l1.cpu(), l2.cpu(), atol=2e-3), (l1, l2)

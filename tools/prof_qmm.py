@@ -22,11 +22,13 @@ def main():
     ap.add_argument("--cfg", default="")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--gemv", action="store_true", help="M <= 4 decode GEMV with the fused RMSNorm / q8 prologue")
+    ap.add_argument("--qt", type=int, default=0, help="ggml type override (e.g. 3 = Q4_1 -> MX4F t32)")
     a = ap.parse_args()
     from localai_tfp_amd.ops import linear as L
     from localai_tfp_amd.ops.quant import random_quantized
     N, K, qt, epi = SHAPES[a.shape]
-    W = L.QWeight.from_ggml(random_quantized(np.random.default_rng(1), qt, N, K), qt, N, K, "cuda")
+    qt = a.qt or qt
+    W = L.QWeight.from_ggml(random_quantized(np.random.default_rng(1), qt, N, K), qt, N, K, "cuda", t32=True)
     assert W.to_t32()
     if a.cfg:
         L.QMM_FORCE = tuple(int(v) for v in a.cfg.split(","))
@@ -53,7 +55,7 @@ def main():
     torch.cuda.synchronize()
     us = e0.elapsed_time(e1) / a.iters * 1e3
     cfg = "qmv_fused" if a.gemv else L._qmm_shape(a.M, N, K, epi in (0, 2))
-    print(f"{a.shape} M={a.M} cfg={cfg} {us:.1f} us {2*a.M*N*K/us/1e6:.0f} TF {W.data.numel() / us / 1e6:.2f} TB/s weights")
+    print(f"{a.shape} qt={int(W.qtype)} M={a.M} cfg={cfg} {us:.1f} us {2*a.M*N*K/us/1e6:.0f} TF {W.data.numel() / us / 1e6:.2f} TB/s weights")
 
 
 if __name__ == "__main__":
