@@ -290,7 +290,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KV8 ? 2 : 4
     const bf16_t* __restrict__ q, int q_stride, const void* __restrict__ kcv, const void* __restrict__ vcv,
     const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ seq_lens, int Hkv, int G, int bs,
     float scale, int window, float softcap, int part_size, int n_parts, bf16_t* __restrict__ out, int out_stride,
-    float2* __restrict__ part_ml, float* __restrict__ part_o) {
+    float2* __restrict__ part_ml, float* __restrict__ part_o, int* __restrict__ part_cnt) {
     constexpr int KT = 32;                      // keys per wave tile
     constexpr int VBYTES = KT * D * 2;
     constexpr int PSTRIDE = (KT + 8) * 2;       // bytes per P row (padded)
@@ -485,13 +485,43 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KV8 ? 2 : 4
             part_o[pi * D + d] = os;
         }
     }
+    if (n_parts == 1 || !part_cnt) return;
+    // fused split-K merge: the last of the (b, kvh) partition workgroups to finish merges all of them,
+    // instead of a separate reduce launch (at batch 1 that launch costs as much as the attention itself).
+    // The counter is left at zero for the next launch / graph replay.
+    __shared__ int s_last;
+    const int np = min(n_parts, (L + part_size - 1) / part_size);  // partitions that did not return early
+    __threadfence();  // release: this workgroup's partials reach device scope (every XCD's L2)
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const int old = atomicAdd(&part_cnt[b * Hkv + kvh], 1);
+        s_last = old == np - 1;
+        if (old == np - 1) atomicExch(&part_cnt[b * Hkv + kvh], 0);
+    }
+    __syncthreads();
+    if (!s_last) return;
+    __threadfence();  // acquire: the other workgroups' partials
+    for (int idx = threadIdx.x; idx < G * D; idx += 256) {
+        const int h = idx / D, d = idx % D, hq = kvh * G + h;
+        const size_t pb = ((size_t)b * Hq + hq) * n_parts;
+        float mx = -INFINITY;
+        for (int p = 0; p < np; ++p) mx = fmaxf(mx, part_ml[pb + p].x);
+        float ls = 0.f, os = 0.f;
+        for (int p = 0; p < np; ++p) {
+            const float2 pm = part_ml[pb + p];
+            const float a = mx == -INFINITY ? 0.f : exp2f(pm.x - mx);
+            ls += pm.y * a;
+            os += part_o[(pb + p) * D + d] * a;
+        }
+        out[(size_t)b * out_stride + (size_t)hq * D + d] = f32_to_act<F16>(ls > 0.f ? os / ls : 0.f);
+    }
 }
 
 template <int D>
 static int launch_decode_mfma(const bf16_t* q, int q_stride, const void* kc, const void* vc, const int* bt,
                               int bt_stride, const int* seq_lens, int B, int Hkv, int G, int bs, float scale,
                               int window, float softcap, int part_size, int n_parts, bf16_t* out, int out_stride,
-                              float2* part_ml, float* part_o, int kv8, hipStream_t st) {
+                              float2* part_ml, float* part_o, int* part_cnt, int kv8, hipStream_t st) {
     dim3 grid(Hkv, B, n_parts);
     static_assert(16 * D * 4 <= dec_wave_lds<D>(), "merge buffer");
     const size_t lds = 4 * dec_wave_lds<D>() + 4 * 32 * 4;
@@ -499,13 +529,14 @@ static int launch_decode_mfma(const bf16_t* q, int q_stride, const void* kc, con
         if (kv8)
             attn_decode_mfma_kernel<D, F16, true><<<grid, 256, lds, st>>>(q, q_stride, kc, vc, bt, bt_stride, seq_lens,
                                                                          Hkv, G, bs, scale, window, softcap, part_size,
-                                                                         n_parts, out, out_stride, part_ml, part_o);
+                                                                         n_parts, out, out_stride, part_ml, part_o,
+                                                                         part_cnt);
         else
             attn_decode_mfma_kernel<D, F16, false><<<grid, 256, lds, st>>>(q, q_stride, kc, vc, bt, bt_stride,
                                                                           seq_lens, Hkv, G, bs, scale, window, softcap,
                                                                           part_size, n_parts, out, out_stride, part_ml,
-                                                                          part_o);
-        if (n_parts > 1)
+                                                                          part_o, part_cnt);
+        if (n_parts > 1 && !part_cnt)
             attn_decode_reduce_kernel<F16><<<B * Hkv * G, 128, 0, st>>>(part_ml, part_o, n_parts, Hkv * G, D, seq_lens,
                                                                         part_size, out, out_stride);
     });
@@ -513,18 +544,20 @@ static int launch_decode_mfma(const bf16_t* q, int q_stride, const void* kc, con
 }
 
 // MFMA decode for D in {64, 128} and up to 16 query heads per kv head; other shapes return
-// hipErrorInvalidValue (the caller falls back to mxk_attn_decode).
+// hipErrorInvalidValue (the caller falls back to mxk_attn_decode). part_cnt: B x Hkv zero-initialised
+// counters for the in-kernel partition merge (nullptr: a separate reduce launch).
 extern "C" int mxk_attn_decode_mfma(const bf16_t* q, int q_stride, const void* kc, const void* vc, const int* bt,
                                     int bt_stride, const int* seq_lens, int B, int Hq, int Hkv, int D, int bs,
                                     float scale, int window, float softcap, int part_size, int n_parts, bf16_t* out,
-                                    int out_stride, float2* part_ml, float* part_o, int kv8, hipStream_t st) {
+                                    int out_stride, float2* part_ml, float* part_o, int kv8, int* part_cnt,
+                                    hipStream_t st) {
     if (B <= 0) return 0;
     if (Hq % Hkv || Hq / Hkv > 16) return (int)hipErrorInvalidValue;
     if (n_parts > 1 && (!part_ml || !part_o)) return (int)hipErrorInvalidValue;
     if (bs <= 0 || part_size / bs + 1 > 256) return (int)hipErrorInvalidValue;
     const int G = Hq / Hkv;
-    if (D == 128) return launch_decode_mfma<128>(q, q_stride, kc, vc, bt, bt_stride, seq_lens, B, Hkv, G, bs, scale, window, softcap, part_size, n_parts, out, out_stride, part_ml, part_o, kv8, st);
-    if (D == 64) return launch_decode_mfma<64>(q, q_stride, kc, vc, bt, bt_stride, seq_lens, B, Hkv, G, bs, scale, window, softcap, part_size, n_parts, out, out_stride, part_ml, part_o, kv8, st);
+    if (D == 128) return launch_decode_mfma<128>(q, q_stride, kc, vc, bt, bt_stride, seq_lens, B, Hkv, G, bs, scale, window, softcap, part_size, n_parts, out, out_stride, part_ml, part_o, part_cnt, kv8, st);
+    if (D == 64) return launch_decode_mfma<64>(q, q_stride, kc, vc, bt, bt_stride, seq_lens, B, Hkv, G, bs, scale, window, softcap, part_size, n_parts, out, out_stride, part_ml, part_o, part_cnt, kv8, st);
     return (int)hipErrorInvalidValue;
 }
 

@@ -304,8 +304,7 @@ __global__ __launch_bounds__(SNT) void sample_kernel(float* __restrict__ logits,
         s_n = 0;
     }
     __syncthreads();
-    // fewer than K entries within TK_HR of the slice max (a sparse allow mask): take every entry
-    const float cut = s_bin == TK_HB - 1 ? -INFINITY : mx - ((float)s_bin + 1.01f) * BW;  // gather every v > cut (a superset of the kept set)
+    const float cut = mx - ((float)s_bin + 1.01f) * BW;  // gather every v > cut (a superset of the kept set)
     // pass 3: gather candidates
     auto gather = [&](int i, float v) {
         if (v == -INFINITY || !(v > cut || v == mx)) return;

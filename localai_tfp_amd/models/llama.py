@@ -148,6 +148,8 @@ class Workspace:
         nh = cfg.n_heads // tp_size
         self.part_ml = torch.empty((max_seqs * nh * max_parts, 2), dtype=torch.float32, device=dev)
         self.part_o = torch.empty((max_seqs * nh * max_parts, cfg.head_dim), dtype=torch.float32, device=dev)
+        # per-(sequence, kv head) arrival counters of the decode kernel's fused partition merge (self-resetting)
+        self.part_cnt = torch.zeros(max_seqs * max(1, cfg.n_kv_heads // tp_size), dtype=torch.int32, device=dev)
 
     def decode_part_size(self, B: int, Hq: int, max_len: int) -> int:
         """Split-K partition length of the paged decode attention: small batches split the context
@@ -533,7 +535,7 @@ class LlamaModel:
             if nd:
                 K.attn_decode(q[:nd].view(nd, Hq, D), kc, vc, fb.dec_block_tables, fb.dec_seq_lens, self.scale,
                               attn[:nd].view(nd, Hq, D), max_seq_len=fb.dec_max_len or None,
-                              workspace=(ws.part_ml, ws.part_o), window=L.window, softcap=cfg.attn_softcap,
+                              workspace=(ws.part_ml, ws.part_o, ws.part_cnt), window=L.window, softcap=cfg.attn_softcap,
                               part_size=ws.decode_part_size(nd, Hq, fb.dec_max_len or cfg.ctx_train))
             if T > nd:
                 K.attn_prefill(q[nd:].view(T - nd, Hq, D), kc, vc, fb.pf_block_tables, fb.pf_cu_q, fb.pf_ctx_lens,

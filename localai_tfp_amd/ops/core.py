@@ -420,6 +420,7 @@ def _attn_ref_one(q, k_cache, v_cache, table, ctx: int, qpos0: int, scale: float
 
 
 ATTN_DECODE_IMPL = __import__("os").environ.get("MX_ATTN_DECODE", "mfma")
+FUSED_DECODE_MERGE = __import__("os").environ.get("MX_ATTN_FUSED_MERGE", "1") != "0"
 
 
 def attn_decode(q: torch.Tensor, k_cache, v_cache, block_tables: torch.Tensor, seq_lens: torch.Tensor,
@@ -442,21 +443,29 @@ def attn_decode(q: torch.Tensor, k_cache, v_cache, block_tables: torch.Tensor, s
     if n_parts is None:
         ml = max_seq_len if max_seq_len is not None else int(seq_lens.max())
         n_parts = max(1, -(-ml // part_size))
+    cnt = None
     if n_parts > 1:
         if workspace is None:
             ml_t = torch.empty((B * Hq * n_parts, 2), dtype=torch.float32, device=q.device)
             po = torch.empty((B * Hq * n_parts, D), dtype=torch.float32, device=q.device)
+            cnt = torch.zeros(B * Hkv, dtype=torch.int32, device=q.device)
         else:
-            ml_t, po = workspace
+            ml_t, po = workspace[:2]
+            cnt = workspace[2] if len(workspace) > 2 else None
     else:
         ml_t = po = None
     N.ensure_act(out.dtype)
-    fn = "mxk_attn_decode_mfma" if (impl or ATTN_DECODE_IMPL) == "mfma" and D in (64, 128) and Hq // Hkv <= 16 \
-        else "mxk_attn_decode"
-    N.kcall(fn, q.data_ptr(), q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
-            block_tables.data_ptr(), block_tables.stride(0), seq_lens.data_ptr(), B, Hq, Hkv, D, bs, float(scale),
-            int(window), float(softcap), part_size, n_parts, out.data_ptr(), out.stride(0), N.ptr(ml_t), N.ptr(po),
-            int(is_fp8(k_cache)), N.stream_ptr())
+    mfma = (impl or ATTN_DECODE_IMPL) == "mfma" and D in (64, 128) and Hq // Hkv <= 16
+    args = [q.data_ptr(), q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(), block_tables.data_ptr(),
+            block_tables.stride(0), seq_lens.data_ptr(), B, Hq, Hkv, D, bs, float(scale), int(window), float(softcap),
+            part_size, n_parts, out.data_ptr(), out.stride(0), N.ptr(ml_t), N.ptr(po), int(is_fp8(k_cache))]
+    if mfma:
+        # partition merge inside the attention kernel (zeroed per-(seq, kv head) counters), else a reduce launch
+        if cnt is not None and (cnt.numel() < B * Hkv or not FUSED_DECODE_MERGE):
+            cnt = None
+        N.kcall("mxk_attn_decode_mfma", *args, N.ptr(cnt), N.stream_ptr())
+    else:
+        N.kcall("mxk_attn_decode", *args, N.stream_ptr())
     return out
 
 

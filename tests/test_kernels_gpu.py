@@ -218,6 +218,14 @@ def test_attn_decode(Hq, Hkv, D, lens, impl):
     K.attn_decode(q.to(DEV), kc.to(DEV), vc.to(DEV), bt.to(DEV), seq.to(DEV), scale, out, part_size=256,
                   workspace=ws, max_seq_len=4096, impl=impl)
     assert rel(out, ref) < 1e-2
+    # the in-kernel partition merge (MFMA path): arrival counters reset themselves across launches
+    cnt = torch.zeros(B * Hkv, dtype=torch.int32, device=DEV)
+    for part in (64, 256, 64):
+        out = torch.empty(B, Hq, D, dtype=torch.bfloat16, device=DEV)
+        K.attn_decode(q.to(DEV), kc.to(DEV), vc.to(DEV), bt.to(DEV), seq.to(DEV), scale, out, part_size=part,
+                      workspace=ws + (cnt,), max_seq_len=4096, impl=impl)
+        assert rel(out, ref) < 1e-2, part
+        assert int(cnt.abs().sum()) == 0
 
 
 def test_probe_tr16_semantics():
