@@ -230,49 +230,61 @@ __global__ __launch_bounds__(64 * QMV_WAVES) void qmv_kernel(const int8_t* __res
     const int u0 = blockIdx.y * per, u1 = min(nunit, u0 + per);
     const uint8_t* wg = W + (size_t)g * nunit * U::BYTES;
     int ldq = K, ubase = 0;
+    // the wave's first two units are in flight before the activation prologue runs (HBM latency overlaps
+    // the norm / quantisation; at batch 1 the whole weight stream is usually these two loads per wave)
+    U a, b;
+    int u = u0 + wave;
+    if (u < u1) a.load(wg + (size_t)u * U::BYTES, r, h);
+    if (u + QMV_WAVES < u1) b.load(wg + (size_t)(u + QMV_WAVES) * U::BYTES, r, h);
+    float rsv[MM];
+#pragma unroll
+    for (int m = 0; m < MM; ++m) rsv[m] = 1.f;
     if constexpr (SRC != SRC_Q8) {
         extern __shared__ __attribute__((aligned(16))) char qmv_smem[];
         const int SL = per * U::ELEMS;  // slice capacity per row (dynamic LDS: MM x (SL + SL/32 x 8) bytes)
         int8_t* sq = (int8_t*)qmv_smem;
         float2* sd = (float2*)(qmv_smem + MM * SL);
         const int k0 = u0 * U::ELEMS, klen = max(0, u1 - u0) * U::ELEMS;
-        __shared__ float nred[QMV_WAVES];
+        __shared__ float nred[MM][QMV_WAVES];
         for (int m = 0; m < M; ++m) {
-            float rs = 1.f;
             if constexpr (SRC == SRC_NORM) {
+                // sum of squares over the whole row (every workgroup reads the same row from L2); the slice
+                // below is quantised without 1/rms — q8 codes are scale invariant, the GEMV result is
+                // multiplied by 1/rms at the end — so the two passes do not wait on each other
                 const float* xr = (const float*)xsrc + (size_t)m * ldx;
                 float ss = 0.f;
                 for (int c = threadIdx.x * 4; c < K; c += 64 * QMV_WAVES * 4) {
                     const float4 v = *(const float4*)(xr + c);
                     ss += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
                 }
-                rs = rsqrtf(block_sum<64 * QMV_WAVES>(ss, nred) / (float)K + eps);
+                ss = wave_sum(ss);
+                if (lane == 0) nred[m][wave] = ss;
             }
             // 8 consecutive elements per lane, 4 lanes per 32-element q8 block (klen % 256 == 0, so the
             // 4-lane groups enter and leave the loop together)
             for (int e = threadIdx.x * 8; e < klen; e += 64 * QMV_WAVES * 8) {
-                float a[8];
+                float a8[8];
                 if constexpr (SRC == SRC_NORM) {
                     const float* xr = (const float*)xsrc + (size_t)m * ldx + k0 + e;
                     const float4 v0 = *(const float4*)xr, v1 = *(const float4*)(xr + 4);
                     const float4 w0 = *(const float4*)(nw + k0 + e), w1 = *(const float4*)(nw + k0 + e + 4);
-                    a[0] = v0.x * rs * w0.x; a[1] = v0.y * rs * w0.y; a[2] = v0.z * rs * w0.z; a[3] = v0.w * rs * w0.w;
-                    a[4] = v1.x * rs * w1.x; a[5] = v1.y * rs * w1.y; a[6] = v1.z * rs * w1.z; a[7] = v1.w * rs * w1.w;
+                    a8[0] = v0.x * w0.x; a8[1] = v0.y * w0.y; a8[2] = v0.z * w0.z; a8[3] = v0.w * w0.w;
+                    a8[4] = v1.x * w1.x; a8[5] = v1.y * w1.y; a8[6] = v1.z * w1.z; a8[7] = v1.w * w1.w;
                 } else {
                     const uint4 raw = *(const uint4*)((const bf16_t*)xsrc + (size_t)m * ldx + k0 + e);
-                    unpack_act2<F16>(raw.x, a[0], a[1]);
-                    unpack_act2<F16>(raw.y, a[2], a[3]);
-                    unpack_act2<F16>(raw.z, a[4], a[5]);
-                    unpack_act2<F16>(raw.w, a[6], a[7]);
+                    unpack_act2<F16>(raw.x, a8[0], a8[1]);
+                    unpack_act2<F16>(raw.y, a8[2], a8[3]);
+                    unpack_act2<F16>(raw.z, a8[4], a8[5]);
+                    unpack_act2<F16>(raw.w, a8[6], a8[7]);
                 }
                 float am = 0.f;
 #pragma unroll
-                for (int i = 0; i < 8; ++i) am = fmaxf(am, fabsf(a[i]));
+                for (int i = 0; i < 8; ++i) am = fmaxf(am, fabsf(a8[i]));
                 am = group_max<4>(am);
                 const float d = am / 127.f, id = d > 0.f ? 1.f / d : 0.f;
                 int q[8], sum = 0;
 #pragma unroll
-                for (int i = 0; i < 8; ++i) { q[i] = __float2int_rn(a[i] * id); sum += q[i]; }
+                for (int i = 0; i < 8; ++i) { q[i] = __float2int_rn(a8[i] * id); sum += q[i]; }
                 const float sf = group_sum<4>((float)sum);
                 uint2 pk;
                 pk.x = (q[0] & 0xFF) | ((q[1] & 0xFF) << 8) | ((q[2] & 0xFF) << 16) | ((uint32_t)(q[3] & 0xFF) << 24);
@@ -282,6 +294,17 @@ __global__ __launch_bounds__(64 * QMV_WAVES) void qmv_kernel(const int8_t* __res
             }
         }
         __syncthreads();
+        if constexpr (SRC == SRC_NORM) {
+#pragma unroll
+            for (int m = 0; m < MM; ++m) {
+                if (m < M) {
+                    float t = 0.f;
+#pragma unroll
+                    for (int w = 0; w < QMV_WAVES; ++w) t += nred[m][w];
+                    rsv[m] = rsqrtf(t / (float)K + eps);
+                }
+            }
+        }
         xq = sq;
         xds = sd;
         ldq = SL;
@@ -291,31 +314,24 @@ __global__ __launch_bounds__(64 * QMV_WAVES) void qmv_kernel(const int8_t* __res
 #pragma unroll
     for (int m = 0; m < MM; ++m) acc[m] = 0.f;
     // two units in flight per wave: both loads issue before either dot product
-    int u = u0 + wave;
-    for (; u + QMV_WAVES < u1; u += 2 * QMV_WAVES) {
-        U a, b;
-        a.load(wg + (size_t)u * U::BYTES, r, h);
-        b.load(wg + (size_t)(u + QMV_WAVES) * U::BYTES, r, h);
+    while (u < u1) {
         const int ul = u - ubase;
+        const bool hb = u + QMV_WAVES < u1;
 #pragma unroll
         for (int m = 0; m < MM; ++m) {
             if (m < M) {
                 const int8_t* x = xq + (size_t)m * ldq;
                 const float2* ds = xds + (size_t)m * (ldq / 32);
                 acc[m] += a.dot(x + (size_t)ul * U::ELEMS, ds + ul * (U::ELEMS / 32), h);
-                acc[m] += b.dot(x + (size_t)(ul + QMV_WAVES) * U::ELEMS, ds + (ul + QMV_WAVES) * (U::ELEMS / 32), h);
+                if (hb) acc[m] += b.dot(x + (size_t)(ul + QMV_WAVES) * U::ELEMS, ds + (ul + QMV_WAVES) * (U::ELEMS / 32), h);
             }
         }
+        u += 2 * QMV_WAVES;
+        if (u < u1) a.load(wg + (size_t)u * U::BYTES, r, h);
+        if (u + QMV_WAVES < u1) b.load(wg + (size_t)(u + QMV_WAVES) * U::BYTES, r, h);
     }
-    if (u < u1) {
-        U a;
-        a.load(wg + (size_t)u * U::BYTES, r, h);
-        const int ul = u - ubase;
 #pragma unroll
-        for (int m = 0; m < MM; ++m)
-            if (m < M)
-                acc[m] += a.dot(xq + (size_t)m * ldq + (size_t)ul * U::ELEMS, xds + (size_t)m * (ldq / 32) + ul * (U::ELEMS / 32), h);
-    }
+    for (int m = 0; m < MM; ++m) acc[m] *= rsv[m];
 #pragma unroll
     for (int m = 0; m < MM; ++m) {
         const float v = acc[m] + __shfl_xor(acc[m], 32);

@@ -651,7 +651,8 @@ extern "C" int mxk_sample_topk_cap() { return TK_CAP; }
 
 // greedy argmax over rows (fast path used by the decode graph when every row is greedy)
 __global__ __launch_bounds__(1024) void argmax_kernel(const float* __restrict__ x, int ld, int V,
-                                                      int* __restrict__ out) {
+                                                      int* __restrict__ out, unsigned long long* __restrict__ keys,
+                                                      int off) {
     __shared__ float rv[16];
     __shared__ int ri[16];
     const float* r = x + (size_t)blockIdx.x * ld;
@@ -691,12 +692,46 @@ __global__ __launch_bounds__(1024) void argmax_kernel(const float* __restrict__ 
         int id = ri[0];
         for (int w = 1; w < 16; ++w)
             if (rv[w] > b || (rv[w] == b && ri[w] < id)) { b = rv[w]; id = ri[w]; }
-        out[blockIdx.x] = id == 0x7fffffff ? 0 : id;
+        if (keys) {
+            // vocabulary shard: (value, global index) as one orderable 64-bit key, larger = better
+            // (higher value, then lower index)
+            const uint32_t u = __float_as_uint(b);
+            const uint32_t hi = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+            const uint32_t gi = id == 0x7fffffff ? 0xFFFFFFFFu : (uint32_t)(id + off);
+            keys[blockIdx.x] = ((unsigned long long)(id == 0x7fffffff ? 0u : hi) << 32) | (0xFFFFFFFFu - gi);
+        } else {
+            out[blockIdx.x] = id == 0x7fffffff ? 0 : id;
+        }
     }
 }
 
 extern "C" int mxk_argmax(const float* x, int ld, int B, int V, int* out, hipStream_t st) {
     if (B <= 0) return 0;
-    argmax_kernel<<<B, 1024, 0, st>>>(x, ld, V, out);
+    argmax_kernel<<<B, 1024, 0, st>>>(x, ld, V, out, nullptr, 0);
+    MXK_CHECK_LAUNCH();
+}
+
+// tensor-parallel greedy head: each rank reduces its [B, V_shard] logits to one key per row
+// (mxk_argmax_keys), the keys are all-gathered ([tp, B] x 8 bytes instead of the B x V fp32 logits),
+// and mxk_argmax_merge picks the winner per row: the same token as an argmax over the gathered logits.
+extern "C" int mxk_argmax_keys(const float* x, int ld, int B, int V, int off, unsigned long long* keys,
+                               hipStream_t st) {
+    if (B <= 0) return 0;
+    argmax_kernel<<<B, 1024, 0, st>>>(x, ld, V, nullptr, keys, off);
+    MXK_CHECK_LAUNCH();
+}
+
+__global__ void argmax_merge_kernel(const unsigned long long* __restrict__ keys, int tp, int B, int* __restrict__ out) {
+    const int row = blockIdx.x * blockDim.x + threadIdx.x;
+    if (row >= B) return;
+    unsigned long long k = 0;
+    for (int r = 0; r < tp; ++r) k = max(k, keys[(size_t)r * B + row]);
+    const uint32_t gi = 0xFFFFFFFFu - (uint32_t)(k & 0xFFFFFFFFull);
+    out[row] = gi == 0xFFFFFFFFu ? 0 : (int)gi;
+}
+
+extern "C" int mxk_argmax_merge(const unsigned long long* keys, int tp, int B, int* out, hipStream_t st) {
+    if (B <= 0) return 0;
+    argmax_merge_kernel<<<(B + 255) / 256, 256, 0, st>>>(keys, tp, B, out);
     MXK_CHECK_LAUNCH();
 }

@@ -34,6 +34,9 @@ from .sequence import Request, Sequence, Status, StepOutput
 
 log = logging.getLogger("localai_tfp_amd.engine")
 
+# tensor-parallel decode graphs end in a vocab-parallel argmax (no per-step logits all-gather)
+VOCAB_PARALLEL_ARGMAX = os.environ.get("MX_TP_VOCAB_ARGMAX", "1") != "0"
+
 # ---- serving-loop GC policy ----------------------------------------------------------------------
 # A full (generation-2) collection walks every live Python object — the model's parameter wrappers,
 # tokenizer tables, request state — and stalls the engine thread for milliseconds while the GPU idles
@@ -228,19 +231,28 @@ class StepGraph:
         from .. import _native as N
         s = torch.cuda.Stream(device=engine.device)
         s.wait_stream(torch.cuda.current_stream(engine.device))
+        # tensor parallel: the graph ends at the vocabulary shards + a vocab-parallel argmax; sampled steps
+        # gather the full logits after the replay (plan["gather"], every rank)
+        self.vp = engine.model.tp_size > 1 and VOCAB_PARALLEL_ARGMAX
+        self.fb.tp_local_logits = self.vp
+
+        def head(lg):
+            if self.vp:
+                engine.model.vocab_argmax(lg, engine.ws, self.argmax)
+            else:
+                N.kcall("mxk_argmax", lg.data_ptr(), lg.stride(0), self.S, lg.shape[1], self.argmax.data_ptr(),
+                        N.stream_ptr())
+
         with torch.cuda.stream(s):
             for _ in range(2):  # warm-up (allocations, lazy init) outside capture
                 self._fix()
-                lg = engine.model.forward(self.fb, engine.kv, engine.ws)
-                N.kcall("mxk_argmax", lg.data_ptr(), lg.stride(0), self.S, lg.shape[1], self.argmax.data_ptr(),
-                        N.stream_ptr())
+                head(engine.model.forward(self.fb, engine.kv, engine.ws))
         torch.cuda.current_stream(engine.device).wait_stream(s)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, pool=pool, stream=s):
             self._fix()
             self.logits = engine.model.forward(self.fb, engine.kv, engine.ws)
-            N.kcall("mxk_argmax", self.logits.data_ptr(), self.logits.stride(0), self.S, self.logits.shape[1],
-                    self.argmax.data_ptr(), N.stream_ptr())
+            head(self.logits)
         self.graph = g
 
     def _fix(self):
@@ -599,6 +611,8 @@ class LLMEngine:
         items = list(so.decode) + [it for it in so.prefill if it.sample]
         if self.tp is not None:
             plan["ns"] = len(items)
+            plan["gather"] = bool(items) and not all(it.seq.params.greedy and not it.seq.params.logit_bias
+                                                     for it in items)
             self.tp.send_plan(plan)
         if roctx.ENABLED:
             roctx.push("launch graph" if plan["graph"] else "launch eager")
@@ -847,6 +861,8 @@ class LLMEngine:
             g = self._graph_get(plan["graph"])
             logits, am = g.run(plan, self._prev_dev[0] if "fix" in plan else None)
             self.stats["graph_steps"] += 1
+            if getattr(g, "vp", False) and plan.get("gather"):
+                logits = self.model.finish_logits(logits, self.ws)
             return logits, am
         t = self._stage_plan(plan, ("tokens", "positions", "slots", "lidx", "dec_bt", "dec_lens", "pf_bt", "pf_cu",
                                     "pf_ctx", "pf_tseq", "pf_tq0"))
@@ -895,15 +911,16 @@ class LLMEngine:
         t0 = time.perf_counter()
         plan = self._plan(so)
         self.stats["plan_s"] += time.perf_counter() - t0
-        if self.tp is not None:
-            self.tp.send_plan(plan)
-        logits, am = self._execute(plan)
         sample_items = [it for it in so.decode] + [it for it in so.prefill if it.sample]
-        if not sample_items:
-            return [], None
         params = [it.seq.params for it in sample_items]
         greedy_only = all(p.greedy and not p.logit_bias and p.repeat_penalty == 1.0 and not p.presence_penalty
                           and not p.frequency_penalty for p in params) and not any(it.seq.grammar for it in sample_items)
+        if self.tp is not None:
+            plan["gather"] = bool(sample_items) and not greedy_only
+            self.tp.send_plan(plan)
+        logits, am = self._execute(plan)
+        if not sample_items:
+            return [], None
         if am is not None and greedy_only:
             t0 = time.perf_counter()
             out = am.cpu().tolist()

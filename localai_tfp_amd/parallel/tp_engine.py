@@ -47,7 +47,7 @@ def encode_plan(plan: dict) -> np.ndarray:
     """Flat int32 image of a step plan: [nd, flags, graph bucket (B, P, PS), ns (rows the leader samples and
     broadcasts on the device: overlap mode), then per PLAN_ARRAYS entry: ndim, *shape, *data]."""
     g = plan.get("graph")
-    flags = int(bool(g)) | (int(bool(plan.get("keep_hidden"))) << 1)
+    flags = int(bool(g)) | (int(bool(plan.get("keep_hidden"))) << 1) | (int(bool(plan.get("gather"))) << 2)
     parts = [np.array([plan["nd"], flags, *(tuple(g) if g else (0, 0, 0)), int(plan.get("ns", 0))], np.int32)]
     arrays = dict(plan)
     if "fix" in plan:
@@ -66,7 +66,7 @@ def encode_plan(plan: dict) -> np.ndarray:
 def decode_plan(buf: np.ndarray) -> dict:
     nd, flags = int(buf[0]), int(buf[1])
     plan = {"nd": nd, "graph": tuple(int(x) for x in buf[2:5]) if flags & 1 else False,
-            "keep_hidden": bool(flags & 2), "ns": int(buf[5])}
+            "keep_hidden": bool(flags & 2), "gather": bool(flags & 4), "ns": int(buf[5])}
     i = 6
     for k in PLAN_ARRAYS:
         ndim = int(buf[i])

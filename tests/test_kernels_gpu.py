@@ -782,3 +782,29 @@ def test_sampling_topk_split_matches_row_kernel(B):
         t2, l2 = full.sample(logits.clone(), ps, hist, [step] * B, allow_mask=mask)
         assert t1.cpu().tolist() == t2.cpu().tolist(), step
         assert torch.allclose(l1.cpu(), l2.cpu(), atol=2e-3), (l1, l2)
+
+
+@pytest.mark.parametrize("tp", [2, 8])
+def test_argmax_keys_merge(tp):
+    """Vocab-parallel greedy head: per-shard 64-bit (value, global index) keys, merged across shards, pick the
+    argmax of the whole row (lowest index on ties, padding columns of the last shard excluded)."""
+    V, S = 128256, 7
+    g = torch.Generator().manual_seed(tp)
+    full = torch.randn(S, V, generator=g)
+    full[1, 5] = full[1, V - 3] = 40.0  # tie across shards
+    full[2] = -2.0  # all equal
+    full[3] = -torch.inf
+    full[3, 77777] = -1e30
+    vl = -(-V // tp)
+    keys = torch.empty(tp * S, dtype=torch.int64, device=DEV)
+    for r in range(tp):
+        lo, hi = r * vl, min(V, (r + 1) * vl)
+        loc = torch.full((S, vl), 1e9)
+        loc[:, :hi - lo] = full[:, lo:hi]
+        loc = loc.to(DEV)
+        N.kcall("mxk_argmax_keys", loc.data_ptr(), loc.stride(0), S, hi - lo, lo, keys[r * S:].data_ptr(),
+                N.stream_ptr())
+    out = torch.empty(S, dtype=torch.int32, device=DEV)
+    N.kcall("mxk_argmax_merge", keys.data_ptr(), tp, S, out.data_ptr(), N.stream_ptr())
+    want = full.argmax(1).tolist()
+    assert out.cpu().tolist() == want and want[1] == 5 and want[2] == 0 and want[3] == 77777

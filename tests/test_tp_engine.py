@@ -125,12 +125,12 @@ def test_plan_codec_roundtrip():
             "dec_bt": rng.integers(0, 50, (3, 5)).astype(np.int32), "dec_lens": np.array([4, 5, 6], np.int32),
             "pf_bt": rng.integers(0, 50, (1, 2)).astype(np.int32), "pf_cu": np.array([0, 6], np.int32),
             "pf_ctx": np.array([6], np.int32), "pf_tseq": np.array([0], np.int32), "pf_tq0": np.array([0], np.int32),
-            "keep_hidden": True, "graph": False,
+            "keep_hidden": True, "graph": False, "gather": True,
             "fix": (np.array([0, 2], np.int64), np.array([1, 0], np.int64))}
     buf = encode_plan(plan)
     assert buf.dtype == np.int32
     out = decode_plan(buf)
-    assert out["nd"] == 3 and out["keep_hidden"] and not out["graph"]
+    assert out["nd"] == 3 and out["keep_hidden"] and not out["graph"] and out["gather"]
     for k in ("tokens", "positions", "slots", "lidx", "dec_bt", "dec_lens", "pf_bt", "pf_cu", "pf_ctx", "pf_tseq", "pf_tq0"):
         assert np.array_equal(out[k], plan[k]) and out[k].shape == plan[k].shape, k
     assert all(np.array_equal(a, b) for a, b in zip(out["fix"], plan["fix"]))
@@ -173,3 +173,44 @@ def test_dead_rank_exits_nonzero(who):
             p.kill()
     assert not any(alive), alive
     assert ps[1 - who].exitcode == EXIT_TP_FAILURE, [p.exitcode for p in ps]
+
+
+def _vocab_argmax_worker(rank, world, port, q):
+    import torch.distributed as dist
+    from localai_tfp_amd.models.llama import LlamaModel
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from localai_tfp_amd.models.config import tiny_config
+    V = 1000  # not a multiple of world: the last shard carries padding columns
+    cfg = tiny_config(vocab=V)
+    m = LlamaModel.__new__(LlamaModel)
+    m.cfg, m.tp_rank, m.tp_size, m.tp_group = cfg, rank, world, None
+    g = torch.Generator().manual_seed(11)
+    full = torch.randn(5, V, generator=g)
+    full[1, 7] = full[1, 900] = 50.0  # tie across shards -> the lower index
+    full[2] = -1.0  # all equal -> index 0
+    vl = -(-V // world)
+    loc = torch.full((5, vl), 1e9)  # padding columns must never win
+    lo, hi = rank * vl, min(V, (rank + 1) * vl)
+    loc[:, :hi - lo] = full[:, lo:hi]
+    out = torch.zeros(5, dtype=torch.int32)
+    m.vocab_argmax(loc, None, out)
+    if rank == 0:
+        q.put((out.tolist(), full.argmax(1).tolist()))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_vocab_parallel_argmax(world):
+    """TP greedy head: per-shard (max, index) merged across ranks == argmax over the gathered logits."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_vocab_argmax_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    got, want = q.get(timeout=120)
+    for p in ps:
+        p.join(timeout=60)
+    assert got == want and got[1] == 7 and got[2] == 0
