@@ -270,7 +270,7 @@ __global__ __launch_bounds__(SNT) void sample_kernel(float* __restrict__ logits,
         if (v == -INFINITY) return;
         const float e = __expf(v - mx);
         Zt += e;
-        const int b = min(SHB - 1, (int)((mx - v) * IBW));
+        const int b = (int)fminf((float)(SHB - 1), (mx - v) * IBW);  // float clamp: no int overflow
         atomicAdd(&hcnt[b], 1u);
         atomicAdd(&hmass[b], e);
     };
@@ -470,8 +470,8 @@ __global__ __launch_bounds__(TK_NT) void tk_slice_kernel(const float* __restrict
     constexpr float IBW = (float)TK_HB / TK_HR, BW = TK_HR / (float)TK_HB;
     for (int i = i0 + threadIdx.x; i < i1; i += TK_NT) {
         const float v = val(i);
-        if (v == -INFINITY) continue;
-        atomicAdd(&hcnt[min(TK_HB - 1, (int)((mx - v) * IBW))], 1u);
+        if (!(v > -INFINITY)) continue;  // masked (and NaN)
+        atomicAdd(&hcnt[(int)fminf((float)(TK_HB - 1), (mx - v) * IBW)], 1u);
     }
     __syncthreads();
     if (threadIdx.x == 0) {

@@ -452,6 +452,9 @@ def attn_decode(q: torch.Tensor, k_cache, v_cache, block_tables: torch.Tensor, s
         else:
             ml_t, po = workspace[:2]
             cnt = workspace[2] if len(workspace) > 2 else None
+            if ml_t.numel() < B * Hq * n_parts * 2 or po.numel() < B * Hq * n_parts * D:
+                raise ValueError(f"attn_decode: workspace holds {ml_t.numel() // 2} partial rows, "
+                                 f"needs {B * Hq * n_parts} (B {B} x Hq {Hq} x {n_parts} partitions)")
     else:
         ml_t = po = None
     N.ensure_act(out.dtype)

@@ -220,6 +220,8 @@ def test_attn_decode(Hq, Hkv, D, lens, impl):
     assert rel(out, ref) < 1e-2
     # the in-kernel partition merge (MFMA path): arrival counters reset themselves across launches
     cnt = torch.zeros(B * Hkv, dtype=torch.int32, device=DEV)
+    nparts = -(-4096 // 64)
+    ws = (torch.empty(B * Hq * nparts, 2, device=DEV), torch.empty(B * Hq * nparts, D, device=DEV))
     for part in (64, 256, 64):
         out = torch.empty(B, Hq, D, dtype=torch.bfloat16, device=DEV)
         K.attn_decode(q.to(DEV), kc.to(DEV), vc.to(DEV), bt.to(DEV), seq.to(DEV), scale, out, part_size=part,
