@@ -80,6 +80,7 @@ KERNEL_SIGS = {
     "mxk_rwkv_wkv6": [P, P, P, P, P, I, P, P, P, P, F, P, I, P, P, I, I, P, I, I, I, P],
     # qkv, ld, rows, D, H, head_dim, wq, wk, cs, L, eps, stream
     "mxk_qk_norm_rope": [P, I, I, I, I, I, P, P, P, I, F, P],
+    "mxk_qk_norm_rope_gqa": [P, I, I, I, I, I, I, P, P, P, I, F, P],
     "mxk_ssm_scan": [P, P, I, P, P, P, P, P, I, P, P, P, I, I, P, I, P, I, I, I, I, P],
     "mxk_moe_route": [P, I, I, I, I, I, P, P, P],
     "mxk_moe_sort": [P, I, I, I, I, P, P, P, P, P],

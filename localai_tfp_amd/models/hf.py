@@ -158,6 +158,8 @@ def hf_source(model_dir: str, quant: str = "q8_0"):
     if qt is None:
         raise ValueError(f"unknown quantization {quant!r} (choose from {sorted(QUANTS)})")
     pre = "model.language_model." if any(k.startswith("model.language_model.") for k in st.where) else "model."
+    if "embed_tokens.weight" in st:  # a bare base model (e.g. a diffusers text_encoder/ Gemma2Model)
+        pre = ""
     gemma = cfg.arch.startswith("gemma")
     permute = cfg.arch not in NEOX_ARCHS
 

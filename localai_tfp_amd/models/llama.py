@@ -100,6 +100,7 @@ class ForwardBatch:
     want_hidden: bool = False  # embeddings: return normalised hidden rows instead of logits
     keep_hidden: bool = False  # also stash the final-normed hidden rows in model.last_hidden
     tp_local_logits: bool = False  # tensor parallel: return this rank's vocabulary shard (no all-gather)
+    stop_layer: int | None = None  # return the fp32 residual rows after this many layers (HF hidden_states[k])
     embed_rows: list | None = None  # [(row, fp32 [n, hidden])] input embeddings replacing token rows
 
     @property
@@ -490,6 +491,8 @@ class LlamaModel:
                     h[r0:r0 + e.shape[0]].copy_(e)
         xb = ws.xb[:T, :H]
         for li, L in enumerate(self.layers):
+            if fb.stop_layer is not None and li >= fb.stop_layer:
+                break
             kc, vc = kv.layer(li)
             # int8-MFMA GEMMs on Q8_K activations for every projection of this layer (qmm8.hip)
             use8 = not gemv and self._layer_i8(L)
@@ -611,7 +614,7 @@ class LlamaModel:
             else:
                 aq = ads = None
             self._residual_proj(L.wd, act, aq, ads, h, L.post_ffn_norm, ws, T, eps)
-        if self.stage:
+        if self.stage or fb.stop_layer is not None:
             return h
         if self.remote is not None:  # remote layer ranges (parallel/pp_rpc.py), in place on h
             self.remote.run(fb, h)
@@ -645,6 +648,29 @@ class LlamaModel:
             c = cfg.final_softcap
             torch.tanh(logits.div_(c), out=logits).mul_(c)
         return logits
+
+    @torch.no_grad()
+    def prompt_hidden(self, ids: list[int], stop_layer: int | None = None) -> torch.Tensor:
+        """Hidden states of one prompt, prefilled on a private paged KV cache: the residual stream after
+        `stop_layer` layers (transformers' hidden_states[stop_layer]; text encoders of diffusion pipelines
+        take hidden_states[-2] = stop_layer n_layers - 1), or the final-normed rows when None.
+        -> fp32 [len(ids), hidden]."""
+        from ..engine.kv_cache import KVCache
+        dev, cfg, P, bs = self.device, self.cfg, len(ids), 16
+        blocks = list(range(1, 2 + P // bs))
+        kv = KVCache(cfg.n_layers, len(blocks) + 1, self.n_kv, bs, cfg.head_dim, dev)
+        ws = Workspace(cfg, max(P, 16), 1, dev)
+        i32 = dict(dtype=torch.int32, device=dev)
+        fb = ForwardBatch(torch.tensor(ids, **i32), torch.arange(P, **i32),
+                          torch.tensor([blocks[p // bs] * bs + p % bs for p in range(P)], **i32),
+                          torch.arange(P, **i32), n_decode=0, pf_block_tables=torch.tensor([blocks], **i32),
+                          pf_cu_q=torch.tensor([0, P], **i32), pf_ctx_lens=torch.tensor([P], **i32),
+                          pf_q_lens_host=[P], pf_ctx_lens_host=[P])
+        fb.stop_layer = cfg.n_layers if stop_layer is None else int(stop_layer)
+        h = self.forward(fb, kv, ws)[:P].float().clone()
+        if stop_layer is None:  # the final norm, as the embeddings path applies it
+            h = h * torch.rsqrt(h.pow(2).mean(-1, keepdim=True) + cfg.rms_eps) * self.out_norm.float()
+        return h
 
     def finish_logits(self, logits_local: torch.Tensor, ws: Workspace) -> torch.Tensor:
         """Full logits from a tp_local_logits forward's shard (a collective: every rank calls it)."""

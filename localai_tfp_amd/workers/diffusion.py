@@ -73,11 +73,15 @@ class DiffusionServicer(BackendServicer):
                                      max_guidance=float(opts.get("max_guidance_scale", request.CFGScale or 3.0)),
                                      decode_chunk=int(opts.get("decode_chunk_size", 8)))
                 return pb.Result(message="loaded", success=True)
+            from ..models.diffusion import lumina2 as LU
+            pcls = _pipeline_class(request, path)
             if path.startswith("synthetic:"):
                 name = path.split(":", 1)[1]
                 if not use_t5 and name == "sd3-medium":
                     name = "sd3-medium-no-t5"
-                if name in U.PRESETS:  # SD1.x / SDXL UNet models
+                if name.startswith("lumina2"):
+                    self.pipe = LU.Lumina2Pipeline.synthetic(name, self.device)
+                elif name in U.PRESETS:  # SD1.x / SDXL UNet models
                     self.pipe = U.UNetPipeline.synthetic(name, self.device)
                 elif name.startswith("flux"):
                     self.pipe = FX.FluxPipeline.synthetic(name, self.device)
@@ -97,6 +101,8 @@ class DiffusionServicer(BackendServicer):
                         "clip_l_path", "clip_g_path", "t5xxl_path", "vae_path")})
                 elif not os.path.isdir(path):
                     raise ValueError(f"{path}: expected a model file or a diffusers-layout model directory")
+                elif pcls.startswith("Lumina2"):  # Lumina2Text2ImgPipeline / Lumina2Pipeline (backend.py:213-216)
+                    self.pipe = LU.Lumina2Pipeline.from_diffusers(path, self.device)
                 elif os.path.isdir(os.path.join(path, "unet")):
                     self.pipe = U.UNetPipeline.from_diffusers(path, self.device)
                 elif _is_flux(path):
@@ -119,7 +125,8 @@ class DiffusionServicer(BackendServicer):
                 sampler, schedule = diffusers_scheduler(request.SchedulerType)
             self.defaults = dict(sampler=sampler, schedule=schedule,
                                  cfg_scale=float(opts.get("cfg_scale", request.CFGScale or
-                                                          (3.5 if isinstance(self.pipe, FX.FluxPipeline) else 7.0))),
+                                                          (3.5 if isinstance(self.pipe, FX.FluxPipeline) else
+                                                           4.0 if isinstance(self.pipe, LU.Lumina2Pipeline) else 7.0))),
                                  strength=float(opts.get("strength", 0.75)),
                                  control_scale=float(opts.get("control_scale", 1.0)))
             return pb.Result(message="loaded", success=True)
@@ -215,6 +222,21 @@ def _is_svd(request, path: str) -> bool:
             return json.load(f).get("_class_name") == "StableVideoDiffusionPipeline"
     except (OSError, ValueError):
         return False
+
+
+def _pipeline_class(request, path: str) -> str:
+    """The request's PipelineType, else model_index.json's _class_name of a diffusers directory ("" if none)."""
+    import json
+    if request.PipelineType:
+        return request.PipelineType
+    if path.startswith("synthetic:"):
+        return ""
+    try:
+        with open(os.path.join(path if os.path.isabs(path) else os.path.join(request.ModelPath or "", path),
+                               "model_index.json")) as f:
+            return str(json.load(f).get("_class_name") or "")
+    except (OSError, ValueError):
+        return ""
 
 
 def _is_flux(path: str) -> bool:
