@@ -218,3 +218,58 @@ extern "C" int mxk_groupnorm16(const uint16_t* x, uint16_t* y, const float* gamm
     });
     MXK_CHECK_LAUNCH();
 }
+
+// ---- Mix-FFN (Sana GLUMBConv) middle: depthwise 3x3 over 2*Ch channels + GLU -----------------------------
+// x 16-bit NHWC [B, H, W, 2*Ch] (optionally SiLU applied on load: the 1x1 expansion's activation), w fp32
+// [2*Ch][9], b fp32 [2*Ch]; out 16-bit [B, H, W, Ch] = dw(x)[c] * silu(dw(x)[Ch + c]). Two channels per
+// thread (4-byte loads), zero padding at the borders. Memory bound: each input element is read by its 9
+// neighbours through L1/L2, the expanded activation never round-trips through HBM twice.
+template <bool F16>
+__global__ __launch_bounds__(256) void dwconv3_glu_kernel(const uint16_t* __restrict__ x, const float* __restrict__ w,
+                                                          const float* __restrict__ b, uint16_t* __restrict__ out,
+                                                          int B, int H, int W, int Ch, int silu_in) {
+    const int pairs = Ch >> 1;
+    const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+    const long long total = (long long)B * H * W * pairs;
+    if (i >= total) return;
+    const int cp = (int)(i % pairs);
+    const long long pix = i / pairs;
+    const int px = (int)(pix % W), py = (int)((pix / W) % H), bb = (int)(pix / ((long long)W * H));
+    const int c = 2 * cp, C2 = 2 * Ch;
+    float v0 = b[c], v1 = b[c + 1], g0 = b[Ch + c], g1 = b[Ch + c + 1];
+#pragma unroll
+    for (int dy = -1; dy <= 1; ++dy) {
+        const int yy = py + dy;
+        if (yy < 0 || yy >= H) continue;
+#pragma unroll
+        for (int dx = -1; dx <= 1; ++dx) {
+            const int xx = px + dx;
+            if (xx < 0 || xx >= W) continue;
+            const int t = (dy + 1) * 3 + (dx + 1);
+            const uint16_t* p = x + (((size_t)bb * H + yy) * W + xx) * C2;
+            float a0, a1, h0, h1;
+            unpack_act2<F16>(*(const uint32_t*)(p + c), a0, a1);
+            unpack_act2<F16>(*(const uint32_t*)(p + Ch + c), h0, h1);
+            if (silu_in) {
+                a0 = a0 / (1.f + __expf(-a0)); a1 = a1 / (1.f + __expf(-a1));
+                h0 = h0 / (1.f + __expf(-h0)); h1 = h1 / (1.f + __expf(-h1));
+            }
+            v0 += a0 * w[c * 9 + t];
+            v1 += a1 * w[(c + 1) * 9 + t];
+            g0 += h0 * w[(Ch + c) * 9 + t];
+            g1 += h1 * w[(Ch + c + 1) * 9 + t];
+        }
+    }
+    const float o0 = v0 * (g0 / (1.f + __expf(-g0))), o1 = v1 * (g1 / (1.f + __expf(-g1)));
+    *(uint32_t*)(out + (size_t)pix * Ch + c) = pack_act2<F16>(o0, o1);
+}
+
+extern "C" int mxk_dwconv3_glu(const uint16_t* x, const float* w, const float* b, uint16_t* out, int B, int H, int W,
+                               int Ch, int silu_in, hipStream_t st) {
+    if ((long long)B * H * W == 0) return 0;
+    if (Ch & 1) return (int)hipErrorInvalidValue;
+    const long long total = (long long)B * H * W * (Ch / 2);
+    const int grid = (int)((total + 255) / 256);
+    MX_ACT_DISPATCH((dwconv3_glu_kernel<F16><<<grid, 256, 0, st>>>(x, w, b, out, B, H, W, Ch, silu_in)));
+    return (int)hipGetLastError();
+}

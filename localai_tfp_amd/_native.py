@@ -34,6 +34,7 @@ KERNEL_SIGS = {
     "mxk_groupnorm_nhwc": [P, P, P, P, I, I, I, I, F, I, P],
     "mxk_layernorm_mod": [P, I, P, P, I, I, P, I, I, I, F, P],
     "mxk_gate_add": [P, I, P, I, P, I, I, I, I, P],
+    "mxk_dwconv3_glu": [P, P, P, P, I, I, I, I, I, P],
     "mxk_groupnorm16": [P, P, P, P, I, I, I, I, F, I, P, P],
     "mxk_qgemm_mfma": [I, I, I, I, P, I, P, P, I, I, I, I, P, I, P],
     "mxk_qgemm16": [I, I, I, I, P, I, P, P, I, I, I, I, P, I, P],

@@ -81,6 +81,9 @@ class DiffusionServicer(BackendServicer):
                     name = "sd3-medium-no-t5"
                 if name.startswith("lumina2"):
                     self.pipe = LU.Lumina2Pipeline.synthetic(name, self.device)
+                elif name.startswith("sana"):
+                    from ..models.diffusion.sana import SanaPipeline
+                    self.pipe = SanaPipeline.synthetic(name, self.device)
                 elif name in U.PRESETS:  # SD1.x / SDXL UNet models
                     self.pipe = U.UNetPipeline.synthetic(name, self.device)
                 elif name.startswith("flux"):
@@ -103,6 +106,9 @@ class DiffusionServicer(BackendServicer):
                     raise ValueError(f"{path}: expected a model file or a diffusers-layout model directory")
                 elif pcls.startswith("Lumina2"):  # Lumina2Text2ImgPipeline / Lumina2Pipeline (backend.py:213-216)
                     self.pipe = LU.Lumina2Pipeline.from_diffusers(path, self.device)
+                elif pcls.startswith("Sana"):  # SanaPipeline (backend.py:218-221)
+                    from ..models.diffusion.sana import SanaPipeline
+                    self.pipe = SanaPipeline.from_diffusers(path, self.device)
                 elif os.path.isdir(os.path.join(path, "unet")):
                     self.pipe = U.UNetPipeline.from_diffusers(path, self.device)
                 elif _is_flux(path):
@@ -126,7 +132,8 @@ class DiffusionServicer(BackendServicer):
             self.defaults = dict(sampler=sampler, schedule=schedule,
                                  cfg_scale=float(opts.get("cfg_scale", request.CFGScale or
                                                           (3.5 if isinstance(self.pipe, FX.FluxPipeline) else
-                                                           4.0 if isinstance(self.pipe, LU.Lumina2Pipeline) else 7.0))),
+                                                           4.0 if isinstance(self.pipe, LU.Lumina2Pipeline) else
+                                                           4.5 if type(self.pipe).__name__ == "SanaPipeline" else 7.0))),
                                  strength=float(opts.get("strength", 0.75)),
                                  control_scale=float(opts.get("control_scale", 1.0)))
             return pb.Result(message="loaded", success=True)
