@@ -443,8 +443,8 @@ __global__ __launch_bounds__(TK_NT) void tk_slice_kernel(const float* __restrict
                                                         const SampleParams* __restrict__ params,
                                                         const uint32_t* __restrict__ allow_mask, int mask_ld,
                                                         float* __restrict__ cand_v, int* __restrict__ cand_i,
-                                                        int* __restrict__ cand_n) {
-    __shared__ float red[TK_NT / 64];
+                                                        int* __restrict__ cand_n, float2* __restrict__ slice_z) {
+    __shared__ float red[TK_NT / 64], zred[TK_NT / 64];
     __shared__ unsigned hcnt[TK_HB];
     __shared__ float cv[2 * TK_CAP * 4];
     __shared__ int ci[2 * TK_CAP * 4];
@@ -468,12 +468,17 @@ __global__ __launch_bounds__(TK_NT) void tk_slice_kernel(const float* __restrict
     __syncthreads();
     mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
     constexpr float IBW = (float)TK_HB / TK_HR, BW = TK_HR / (float)TK_HB;
+    float zs = 0.f;  // the slice's share of the row's partition function (greedy rows report log-softmax)
     for (int i = i0 + threadIdx.x; i < i1; i += TK_NT) {
         const float v = val(i);
         if (!(v > -INFINITY)) continue;  // masked (and NaN)
+        zs += __expf(v - mx);
         atomicAdd(&hcnt[(int)fminf((float)(TK_HB - 1), (mx - v) * IBW)], 1u);
     }
+    zs = wave_sum(zs);
+    if ((threadIdx.x & 63) == 0) zred[threadIdx.x >> 6] = zs;
     __syncthreads();
+    if (threadIdx.x == 0) slice_z[row * S + sl] = make_float2(mx, zred[0] + zred[1] + zred[2] + zred[3]);
     if (threadIdx.x == 0) {
         unsigned c = 0;
         int b = 0;
@@ -526,8 +531,8 @@ __global__ __launch_bounds__(TK_NT) void tk_slice_kernel(const float* __restrict
 __global__ __launch_bounds__(1024) void tk_merge_kernel(const float* __restrict__ logits, int ld,
                                                        const SampleParams* __restrict__ params, int S,
                                                        const float* __restrict__ cand_v, const int* __restrict__ cand_i,
-                                                       const int* __restrict__ cand_n, int* __restrict__ out_tok,
-                                                       float* __restrict__ out_logp) {
+                                                       const int* __restrict__ cand_n, const float2* __restrict__ slice_z,
+                                                       int* __restrict__ out_tok, float* __restrict__ out_logp) {
     constexpr int CAP = 4096;
     __shared__ float cv[CAP];
     __shared__ int ci[CAP];
@@ -627,24 +632,34 @@ __global__ __launch_bounds__(1024) void tk_merge_kernel(const float* __restrict_
         if (id == 0x7fffffff) id = 0;
         out_tok[row] = id;
         if (out_logp) {
-            const float itemp = greedy ? 1.f : 1.f / P.temperature;
-            out_logp[row] = greedy ? 0.f : logits[(size_t)row * ld + id] * itemp - mx - __logf(fmaxf(z, 1e-30f));
+            if (greedy) {  // log-softmax over the whole (allowed) row, from the slices' (max, sum exp)
+                float M = -INFINITY, Z = 0.f;
+                for (int s2 = 0; s2 < S; ++s2) M = fmaxf(M, slice_z[row * S + s2].x);
+                for (int s2 = 0; s2 < S; ++s2) {
+                    const float2 m = slice_z[row * S + s2];
+                    if (m.x > -INFINITY) Z += m.y * __expf(m.x - M);
+                }
+                out_logp[row] = logits[(size_t)row * ld + id] - M - __logf(fmaxf(Z, 1e-30f));
+            } else {
+                out_logp[row] = logits[(size_t)row * ld + id] / P.temperature - mx - __logf(fmaxf(z, 1e-30f));
+            }
         }
     }
 }
 
 // B rows, S slices per row (<= 64, S * 2 * max top_k <= 4096 so the merge holds every candidate); every row
 // must have top_k in [1, TK_CAP] or be greedy, no typical-p / mirostat (the caller checks).
-// cand_v / cand_i: [B][S][2*TK_CAP] scratch, cand_n: [B][S].
+// cand_v / cand_i: [B][S][2*TK_CAP] scratch, cand_n / slice_z: [B][S].
 extern "C" int mxk_sample_topk_split(float* logits, int ld, int B, int V, const SampleParams* params, int has_pen,
                                      const int* pen_tok, const int* pen_cnt, const float* pen_bias,
                                      const uint32_t* allow_mask, int mask_ld, int S, float* cand_v, int* cand_i,
-                                     int* cand_n, int* out_tok, float* out_logp, hipStream_t st) {
+                                     int* cand_n, float2* slice_z, int* out_tok, float* out_logp, hipStream_t st) {
     if (B <= 0) return 0;
     if (S < 1 || S > 64) return (int)hipErrorInvalidValue;
     if (has_pen) tk_penalty_kernel<<<B, TK_NT, 0, st>>>(logits, ld, V, params, pen_tok, pen_cnt, pen_bias);
-    tk_slice_kernel<<<dim3(B, S), TK_NT, 0, st>>>(logits, ld, V, params, allow_mask, mask_ld, cand_v, cand_i, cand_n);
-    tk_merge_kernel<<<B, 1024, 0, st>>>(logits, ld, params, S, cand_v, cand_i, cand_n, out_tok, out_logp);
+    tk_slice_kernel<<<dim3(B, S), TK_NT, 0, st>>>(logits, ld, V, params, allow_mask, mask_ld, cand_v, cand_i, cand_n,
+                                                  slice_z);
+    tk_merge_kernel<<<B, 1024, 0, st>>>(logits, ld, params, S, cand_v, cand_i, cand_n, slice_z, out_tok, out_logp);
     MXK_CHECK_LAUNCH();
 }
 extern "C" int mxk_sample_topk_cap() { return TK_CAP; }

@@ -148,11 +148,11 @@ class SamplerBatch:
         S = self._split_slices(params, B)
         if S:
             # small batch, top-k on: the vocabulary split over B x S workgroups instead of one CU per row
-            cv, ci, cn = self._split_scratch(dev, B, S)
+            cv, ci, cn, sz = self._split_scratch(dev, B, S)
             N.kcall("mxk_sample_topk_split", logits.data_ptr(), logits.stride(0), B, V, pbuf.data_ptr(),
                     int(bool(arr["pen_count"].any())), t_t.data_ptr(), c_t.data_ptr(), b_t.data_ptr(),
                     N.ptr(allow_mask), allow_mask.stride(0) if allow_mask is not None else 0, S, cv.data_ptr(),
-                    ci.data_ptr(), cn.data_ptr(), tok.data_ptr(), lp.data_ptr(), N.stream_ptr())
+                    ci.data_ptr(), cn.data_ptr(), sz.data_ptr(), tok.data_ptr(), lp.data_ptr(), N.stream_ptr())
             return tok, lp
         N.kcall("mxk_sample", logits.data_ptr(), logits.stride(0), B, V, pbuf.data_ptr(), t_t.data_ptr(),
                 c_t.data_ptr(), b_t.data_ptr(), N.ptr(allow_mask), allow_mask.stride(0) if allow_mask is not None else 0,
@@ -183,8 +183,9 @@ class SamplerBatch:
             cv = torch.empty(B * S * 2 * self.TOPK_CAP, dtype=torch.float32, device=dev)
             ci = torch.empty(B * S * 2 * self.TOPK_CAP, dtype=torch.int32, device=dev)
             cn = torch.empty(B * S, dtype=torch.int32, device=dev)
-            c = self._scratch = (key, cv, ci, cn)
-        return c[1], c[2], c[3]
+            sz = torch.empty(B * S * 2, dtype=torch.float32, device=dev)  # per-slice (max, sum exp)
+            c = self._scratch = (key, cv, ci, cn, sz)
+        return c[1], c[2], c[3], c[4]
 
 
 def sample_ref(logits: torch.Tensor, params, histories, steps, allow_mask=None):

@@ -2,7 +2,7 @@
 # then qmm on Q4_K vs MX4F (pre-decoded scales) at the serving shapes.
 set -o pipefail
 cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out; export TMPDIR=/tmp PYTHONPATH=$PWD
-timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py tests/test_lumina2.py -m gpu -k "sampling or attn_decode or argmax or qmv or lumina2 or gqa" -x -q --timeout 120 --timeout-method thread > gpurun_out/j8_k.log 2>&1 || { tail -30 gpurun_out/j8_k.log; exit 1; }
+timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py tests/test_lumina2.py tests/test_sana.py -m gpu -k "sampling or attn_decode or argmax or qmv or lumina2 or gqa or sana or dwconv" -x -q --timeout 120 --timeout-method thread > gpurun_out/j8_k.log 2>&1 || { tail -30 gpurun_out/j8_k.log; exit 1; }
 tail -1 gpurun_out/j8_k.log
 timeout -k 10 300 python -u -m pytest tests/test_model_gpu.py tests/test_kv_fp8.py tests/test_gemma.py tests/test_speculative.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/j8_e.log 2>&1 || { tail -30 gpurun_out/j8_e.log; exit 1; }
 tail -1 gpurun_out/j8_e.log
