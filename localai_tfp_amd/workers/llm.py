@@ -184,6 +184,11 @@ class LLMServicer(BackendServicer):
     def LoadModel(self, request, context):
         import torch
         from ..models.loader import load_llm
+        if (request.Type or "").lower() == "outetts":
+            # the transformers backend's OuteTTS type (backend/python/transformers/backend.py:205-243)
+            from .outetts import OuteTTSServicer
+            self._audio = OuteTTSServicer(self.device)
+            return self._audio.LoadModel(request, context)
         if _is_musicgen(request):
             # the reference's transformers backend serves `type: MusicgenForConditionalGeneration` models
             # through SoundGeneration / TTS (backend/python/transformers/backend.py:452-507)
@@ -460,7 +465,7 @@ class LLMServicer(BackendServicer):
     def TTS(self, request, context):
         a = getattr(self, "_audio", None)
         if a is None:
-            return self._no_audio(context, "TTS is not implemented by the LLM backend (MusicGen models only)")
+            return self._no_audio(context, "TTS is not implemented by the LLM backend (MusicGen / OuteTTS models only)")
         return a.TTS(request, context)
 
     @staticmethod
