@@ -246,8 +246,10 @@ def test_lumina2_synthetic_pipeline_type():
 @pytest.mark.gpu
 def test_lumina2_transformer_gpu():
     """bf16 on the repo kernels (GQA q/k norm + RoPE at head dim 96, grouped-query flash attention) vs fp32 CPU."""
-    tr = _synthetic_tr()
-    trg = _synthetic_tr("cuda", torch.bfloat16)
+    import copy
+    from localai_tfp_amd.models.diffusion.nn import cast_module
+    tr = _synthetic_tr()  # weights drawn on the CPU (a CUDA generator would draw different ones)
+    trg = cast_module(copy.deepcopy(tr), "cuda", torch.bfloat16)
     g = torch.Generator().manual_seed(0)
     x = torch.randn(16, 24, 32, generator=g)
     cap = torch.randn(19, LU.LUMINA2_TEST.cap_dim, generator=g)

@@ -249,7 +249,10 @@ def test_sana_prompt_selection():
 
 @pytest.mark.gpu
 def test_sana_transformer_gpu():
-    tr, trg = _tr(), _tr("cuda", torch.bfloat16)
+    import copy
+    from localai_tfp_amd.models.diffusion.nn import cast_module
+    tr = _tr()  # weights drawn on the CPU (a CUDA generator would draw different ones)
+    trg = cast_module(copy.deepcopy(tr), "cuda", torch.bfloat16)
     x, t, ctx, kl = _inputs()
     ref = tr(x, t, ctx, kl)
     got = trg(x.cuda(), t.cuda(), ctx.cuda(), kl.cuda()).cpu()
