@@ -22,7 +22,7 @@ WORKERS = {
     "bark": "localai_tfp_amd.workers.bark",  # models/bark.py
     "bark-cpp": "localai_tfp_amd.workers.bark",
     "coqui": "localai_tfp_amd.workers.unsupported",
-    "kokoro": "localai_tfp_amd.workers.unsupported",
+    "kokoro": "localai_tfp_amd.workers.kokoro",
     "transformers-musicgen": "localai_tfp_amd.workers.musicgen",  # models/musicgen.py
     "transformers-tts": "localai_tfp_amd.workers.tts",
     "huggingface": "localai_tfp_amd.workers.huggingface",

@@ -162,7 +162,7 @@ def test_vits_gpu_matches_cpu():
     assert np.linalg.norm(gm - c) / np.linalg.norm(c) < 2e-2 and np.abs(gm - c).max() < 3e-2
 
 
-@pytest.mark.parametrize("backend", ["coqui", "kokoro"])
+@pytest.mark.parametrize("backend", ["coqui"])
 def test_foreign_tts_backends_refuse_explicitly(backend):
     """Backend names whose model families are not implemented never silently load VITS."""
     from localai_tfp_amd.grpc import pb
