@@ -420,7 +420,10 @@ def _attn_ref_one(q, k_cache, v_cache, table, ctx: int, qpos0: int, scale: float
 
 
 ATTN_DECODE_IMPL = __import__("os").environ.get("MX_ATTN_DECODE", "mfma")
-FUSED_DECODE_MERGE = __import__("os").environ.get("MX_ATTN_FUSED_MERGE", "1") != "0"
+# in-kernel split-K merge (last-arriving workgroup): measured slower on MI355X at batch 1 and 2.3x slower at
+# 128 sequences (profiles/r2_attn_decode_fused_merge_negative.md: the device-scope fences serialise the
+# workgroups); kept as an opt-in for experiments, the separate reduce launch is the default
+FUSED_DECODE_MERGE = __import__("os").environ.get("MX_ATTN_FUSED_MERGE", "0") == "1"
 
 
 def attn_decode(q: torch.Tensor, k_cache, v_cache, block_tables: torch.Tensor, seq_lens: torch.Tensor,
