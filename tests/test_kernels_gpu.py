@@ -218,7 +218,8 @@ def test_attn_decode(Hq, Hkv, D, lens, impl):
     K.attn_decode(q.to(DEV), kc.to(DEV), vc.to(DEV), bt.to(DEV), seq.to(DEV), scale, out, part_size=256,
                   workspace=ws, max_seq_len=4096, impl=impl)
     assert rel(out, ref) < 1e-2
-    # the in-kernel partition merge (MFMA path): arrival counters reset themselves across launches
+    # the opt-in in-kernel partition merge (MFMA path): arrival counters reset themselves across launches
+    K.FUSED_DECODE_MERGE, saved = True, K.FUSED_DECODE_MERGE
     cnt = torch.zeros(B * Hkv, dtype=torch.int32, device=DEV)
     nparts = -(-4096 // 64)
     ws = (torch.empty(B * Hq * nparts, 2, device=DEV), torch.empty(B * Hq * nparts, D, device=DEV))
@@ -228,6 +229,7 @@ def test_attn_decode(Hq, Hkv, D, lens, impl):
                       workspace=ws + (cnt,), max_seq_len=4096, impl=impl)
         assert rel(out, ref) < 1e-2, part
         assert int(cnt.abs().sum()) == 0
+    K.FUSED_DECODE_MERGE = saved
 
 
 def test_probe_tr16_semantics():
