@@ -327,6 +327,17 @@ def _qmatmul_t32(W: QWeight, x, epi: int, out, xq, xds, M: int, out_zeroed: bool
     can_split = epi == EPI_ADD_F32 or (epi == EPI_F32 and out_zeroed)
     if W.bf16_cache is not None and M >= dense_min_m(x.dtype, epi, can_split) and W.bf16_cache.dtype == x.dtype:
         return _dense_cached(W, x, epi, out, M)
+    ws = _qmm_ws_shape(M, W.N, W.K, can_split, int(W.qtype))
+    if ws is not None:
+        cfg, splits = ws
+        e = EPI_ADD_F32 if (epi == EPI_F32 and splits > 1) else epi
+        if e in (EPI_BF16, *GLU_EPIS):
+            if out.dtype != x.dtype:
+                raise ValueError(f"qmatmul: {out.dtype} output with {x.dtype} activations")
+            N.ensure_act(out.dtype)
+        N.kcall("mxk_qmm_ws", int(W.qtype), e, cfg, x.data_ptr(), x.stride(0), W.data.data_ptr(), M, W.N, W.K, splits,
+                out.data_ptr(), out.stride(0), N.stream_ptr())
+        return out
     wm, wn, nw, ks, splits = _qmm_shape(M, W.N, W.K, can_split)
     e = EPI_ADD_F32 if (epi == EPI_F32 and splits > 1) else epi
     if e in (EPI_BF16, *GLU_EPIS):
@@ -520,6 +531,37 @@ def _qmm_shape(M: int, N_: int, K: int, can_split: bool):
         while cols * mt * splits < (3 * CU_COUNT) // 4 and (K // 64) // (splits * 2) >= 8:
             splits *= 2
     return wm, wn, nw, ks, splits
+
+
+# qmm_ws.hip: warp-specialised variant (4 producer waves: LDS-DMA + dequant into an f16 B tile; 4 MFMA-only
+# consumer waves). cfg = CM*10000 + WM*1000 + WN*100 + GP*10 + LEAD: consumer grid CM x (4/CM), wave tile
+# 32WM x 32WN, GP weight groups (32 columns) per producer wave (BN = 128 GP), producers LEAD k-tiles ahead.
+QMM_WS = os.environ.get("MX_QMM_WS", "0") == "1"
+QMM_WS_FORCE: tuple | None = None  # (cfg, splits) override for tuning (tools/tune_qmm_ws.py)
+QMM_WS_CONFIGS = (22211, 22212, 24211, 22421, 12111, 12112, 12221, 41411, 41412)
+
+
+def qmm_ws_geom(cfg: int):
+    """-> (BM, BN) of a qmm_ws configuration."""
+    cm, wm, wn = cfg // 10000, (cfg // 1000) % 10, (cfg // 100) % 10
+    return 32 * wm * cm, 32 * wn * (4 // cm)
+
+
+def _qmm_ws_shape(M: int, N_: int, K: int, can_split: bool, qtype: int):
+    """(cfg, splits) for the warp-specialised qmm, or None for the monolithic kernel."""
+    if QMM_WS_FORCE is not None:
+        cfg, splits = QMM_WS_FORCE
+        return cfg, (splits if can_split else 1)
+    if not QMM_WS or M < 64:
+        return None
+    cfg = 22212 if M <= 128 else 24211
+    bm, bn = qmm_ws_geom(cfg)
+    tiles = -(-M // bm) * -(-N_ // bn)
+    splits = 1
+    if can_split:
+        while tiles * splits < (3 * CU_COUNT) // 4 and (K // 64) // (splits * 2) >= 8:
+            splits *= 2
+    return cfg, splits
 
 
 def _mfma32_shape(M: int, N_: int, nblk: int, can_split: bool):
