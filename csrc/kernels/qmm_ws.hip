@@ -50,7 +50,7 @@ MX_DEV void qws_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" :::
 template <int QT, int CM, int WM, int WN, int GP, int LEAD, int EPI>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void
 qmm_ws_kernel(const uint16_t* __restrict__ A, int lda, const uint8_t* __restrict__ W, int M, int N, int K, int n_mt,
-              int splits, int kt_per_split, void* __restrict__ Cv, int ldc) {
+              int splits, int kt_per_split, void* __restrict__ Cv, int ldc, int dbg) {
     using C = QwsCfg<QT, CM, WM, WN, GP, LEAD>;
     using G = typename C::G;
     using F = QmmFmt<QT>;
@@ -107,10 +107,12 @@ qmm_ws_kernel(const uint16_t* __restrict__ A, int lda, const uint8_t* __restrict
         auto issue = [&](int kt) {
             char* sb = smem + ((kt - kt0) % NS) * C::STAGE;
             const uint16_t* ak = A + (size_t)kt * QMM_KT;
+            if (!(dbg & 4))
 #pragma unroll
             for (int i = 0; i < WA; ++i)
                 __builtin_amdgcn_global_load_lds((const void*)(ak + aoff[i]), (MX_LDS void*)(sb + (p * WA + i) * 1024), 16,
                                                  0, 0);
+            if (dbg & 8) return;
             char* wb = sb + C::A_BYTES + p * G::WBYTES;
             const size_t unit = (size_t)(kt / F::PER_UNIT) * F::UNIT;
             const int jq = kt % F::PER_UNIT;
@@ -131,6 +133,7 @@ qmm_ws_kernel(const uint16_t* __restrict__ A, int lda, const uint8_t* __restrict
         };
         // raw bytes of k-tile kt (landed) -> f16 B tile buffer (kt - kt0) % NB, rows n = p*GP*32 + g*32 + col
         auto dequant = [&](int kt) {
+            if (dbg & 2) return;
             const char* wl = smem + ((kt - kt0) % NS) * C::STAGE + C::A_BYTES + p * G::WBYTES;
             char* dst = b16 + ((kt - kt0) % NB) * C::B16;
             const int jq = kt % F::PER_UNIT;
@@ -198,6 +201,7 @@ qmm_ws_kernel(const uint16_t* __restrict__ A, int lda, const uint8_t* __restrict
             const int cur = s & 1;
             if (s < 3) rd(t, s + 1, ar[cur ^ 1], br[cur ^ 1]);
             else if constexpr (LEAD >= 2) rd(t + 1, 0, ar[0], br[0]);  // published at barrier #t (a stale slot past kt1: unused)
+            if (!(dbg & 1))
 #pragma unroll
             for (int i = 0; i < WM; ++i)
 #pragma unroll
@@ -267,6 +271,12 @@ qmm_ws_kernel(const uint16_t* __restrict__ A, int lda, const uint8_t* __restrict
     }
 }
 
+static int g_qws_dbg = 0;  // isolation experiments (tools/tune_qmm_ws.py --dbg): 1 no MFMA, 2 no dequant, 4 no A loads, 8 no W loads
+extern "C" int mxk_qmm_ws_dbg(int v) {
+    g_qws_dbg = v;
+    return 0;
+}
+
 template <int QT, int CM, int WM, int WN, int GP, int LEAD, int EPI>
 static int launch_qmm_ws(const uint16_t* A, int lda, const uint8_t* W, int M, int N, int K, int splits, void* C, int ldc,
                          hipStream_t st) {
@@ -290,7 +300,7 @@ static int launch_qmm_ws(const uint16_t* A, int lda, const uint8_t* W, int M, in
             attr_set = true;
         }
         qmm_ws_kernel<QT, CM, WM, WN, GP, LEAD, EPI><<<dim3((unsigned)nwg), 512, lds, st>>>(A, lda, W, M, N, K, n_mt, splits,
-                                                                                          ktps, C, ldc);
+                                                                                          ktps, C, ldc, g_qws_dbg);
         MXK_CHECK_LAUNCH();
     }
 }

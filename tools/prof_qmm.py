@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--cfg", default="")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--gemv", action="store_true", help="M <= 4 decode GEMV with the fused RMSNorm / q8 prologue")
+    ap.add_argument("--ws", default="", help="qmm_ws cfg,splits (warp-specialised kernel)")
     ap.add_argument("--qt", type=int, default=0, help="ggml type override (e.g. 3 = Q4_1 -> MX4F t32)")
     a = ap.parse_args()
     from localai_tfp_amd.ops import linear as L
@@ -30,6 +31,8 @@ def main():
     qt = a.qt or qt
     W = L.QWeight.from_ggml(random_quantized(np.random.default_rng(1), qt, N, K), qt, N, K, "cuda", t32=True)
     assert W.to_t32()
+    if a.ws:
+        L.QMM_WS_FORCE = tuple(int(v) for v in a.ws.split(","))
     if a.cfg:
         L.QMM_FORCE = tuple(int(v) for v in a.cfg.split(","))
     x = (torch.randn(a.M, K, device="cuda") * 0.5).half()

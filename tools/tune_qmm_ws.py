@@ -38,6 +38,7 @@ def main():
     ap.add_argument("--M", default="128,256,384")
     ap.add_argument("--cfgs", default="")
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--dbg", default="", help="isolation flag sets, e.g. 1,2,3,4,8 (1 no MFMA, 2 no dequant, 4 no A loads, 8 no W loads)")
     a = ap.parse_args()
     from localai_tfp_amd.ops import linear as L
     from localai_tfp_amd.ops.quant import random_quantized
@@ -78,6 +79,12 @@ def main():
                     us = timeit(lambda: L.qmatmul(W, x, epi, o2, out_zeroed=True), a.iters)
                     rec["ws"].append({"cfg": cfg, "splits": splits, "us": round(us, 2), "rel_err": float(f"{err:.2e}"),
                                       "tflops": round(2 * M * N * K / us / 1e6, 1)})
+                    if a.dbg and splits == 1:
+                        from localai_tfp_amd import _native as NN
+                        for fl in (int(f) for f in a.dbg.split(",")):
+                            NN.kcall("mxk_qmm_ws_dbg", fl)
+                            rec["ws"][-1][f"dbg{fl}_us"] = round(timeit(lambda: L.qmatmul(W, x, epi, o2, out_zeroed=True), a.iters), 2)
+                        NN.kcall("mxk_qmm_ws_dbg", 0)
             L.QMM_WS_FORCE = None
             ok = [w for w in rec["ws"] if "us" in w]
             if ok:
