@@ -21,7 +21,7 @@ WORKERS = {
     # model families not implemented here: LoadModel fails with an explicit error (workers/unsupported.py)
     "bark": "localai_tfp_amd.workers.bark",  # models/bark.py
     "bark-cpp": "localai_tfp_amd.workers.bark",
-    "coqui": "localai_tfp_amd.workers.unsupported",
+    "coqui": "localai_tfp_amd.workers.tts",
     "kokoro": "localai_tfp_amd.workers.kokoro",
     "transformers-musicgen": "localai_tfp_amd.workers.musicgen",  # models/musicgen.py
     "transformers-tts": "localai_tfp_amd.workers.tts",

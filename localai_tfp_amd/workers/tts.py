@@ -1,15 +1,17 @@
 """Text-to-speech worker: the reference's `piper` (backend/go/tts/piper.go:20-49) and the transformers
 backend's VITS / MMS-TTS path behind the TTS RPC, served by the VITS engine (models/tts.py) on the GPU.
-Bark, Coqui, Kokoro and MusicGen names are NOT routed here (workers/unsupported.py fails their
-LoadModel explicitly).
+The reference's `coqui` backend (backend/python/coqui/backend.py:26-80) is routed here too: Coqui VITS
+model directories (config.json + model_file.pth, models/coqui.py), found by path or by Coqui model name
+("tts_models/en/vctk/vits") in the models directory or Coqui's local cache; XTTS refuses explicitly.
+Bark, Kokoro and MusicGen have workers of their own.
 
 LoadModel: a piper voice (`<voice>.onnx` + `<voice>.onnx.json`, models/piper.py; espeak-ng data from
-LibrarySearchPath or the `espeak_data` option), a Hugging Face VITS directory (MMS-TTS layout) or
-`synthetic:vits-test | vits-base`.
+LibrarySearchPath or the `espeak_data` option), a Coqui VITS directory, a Hugging Face VITS directory
+(MMS-TTS layout) or `synthetic:vits-test | vits-base`.
 ModelOptions.Options ("key:value"): noise_scale, noise_scale_duration (alias noise_w), speaking_rate
 (alias length_scale = 1 / rate), seed.
 TTS: text -> 16-bit PCM WAV at the model's sample rate in `dst`. `voice` selects the speaker of a
-multi-speaker model (an integer id; piper's per-voice .onnx file selection has no equivalent because
+multi-speaker model (an integer id, or a Coqui speaker name such as "p225"; piper's per-voice .onnx file selection has no equivalent because
 voices are separate checkpoints here — configure one model per voice). `language` is accepted and
 ignored like piper does.
 SoundGeneration (ElevenLabs /v1/sound-generation) is a MusicGen feature in the reference
@@ -38,6 +40,7 @@ class TTSServicer(BackendServicer):
         self.model = None
         self.tok = None
         self.opts: dict = {}
+        self.speakers: dict = {}
 
     def LoadModel(self, request, context):
         import torch
@@ -59,6 +62,19 @@ class TTSServicer(BackendServicer):
                 self.model, self.tok = load_piper(path, self.device,
                                                   o.get("espeak_data", "") or request.LibrarySearchPath)
                 return pb.Result(message=f"loaded piper voice {os.path.basename(path)}", success=True)
+            from ..models import coqui as CQ
+            cdir = None if path.startswith("synthetic:") else CQ.resolve_model_dir(request.Model or path, request.ModelPath)
+            if cdir is None and not path.startswith("synthetic:") and CQ.is_coqui_dir(
+                    path if os.path.isdir(path) else os.path.dirname(path)):
+                cdir = path if os.path.isdir(path) else os.path.dirname(path)
+            if cdir is not None and CQ.is_coqui_dir(cdir):
+                self.model, self.tok, self.speakers = CQ.load_coqui(
+                    cdir, self.device, o.get("espeak_data", "") or request.LibrarySearchPath)
+                return pb.Result(message=f"loaded Coqui VITS {os.path.basename(os.path.normpath(cdir))}", success=True)
+            if os.environ.get("MX_BACKEND_NAME") == "coqui" and not path.startswith("synthetic:") and not os.path.exists(path):
+                return pb.Result(success=False, message=(
+                    f"Coqui model {request.Model!r} not found locally (looked in the models directory and the Coqui "
+                    "cache $TTS_HOME/tts, ~/.local/share/tts); this build does not download models"))
             if not path.startswith("synthetic:") and os.path.isfile(path):
                 path = os.path.dirname(path)
             self.model, self.tok = T.load_vits(path, self.device)
@@ -73,6 +89,10 @@ class TTSServicer(BackendServicer):
             1.0 / float(o["length_scale"]) if "length_scale" in o else None)
         nsd = o.get("noise_scale_duration", o.get("noise_w"))
         spk = int(voice) if voice and voice.strip().lstrip("-").isdigit() else None
+        if spk is None and voice and self.speakers:
+            if voice not in self.speakers:
+                raise ValueError(f"unknown speaker {voice!r} (known: {', '.join(sorted(self.speakers)[:8])} ...)")
+            spk = self.speakers[voice]
         ids = self.tok.encode(text)
         if len(ids) <= 1:
             raise ValueError("no speakable characters in the input text")

@@ -1,6 +1,6 @@
-"""Backend names of the reference whose model families this framework does not implement (Coqui XTTS;
-Bark is served by workers/bark.py, MusicGen by workers/musicgen.py, Kokoro by workers/kokoro.py).
-Reference: backend/python/coqui/backend.py:26-80.
+"""Backend names of the reference whose model families this framework does not implement (Bark is served
+by workers/bark.py, MusicGen by workers/musicgen.py, Kokoro by workers/kokoro.py, Coqui VITS by
+workers/tts.py — Coqui XTTS checkpoints are refused by models/coqui.py).
 
 The worker starts and answers Health like any backend (so the process manager's lifecycle is the same),
 but LoadModel fails with an explicit error naming the backend — a request for Bark never silently gets
@@ -12,7 +12,7 @@ import os
 from ..grpc import pb
 from ..grpc.server import BackendServicer, worker_main
 
-SUPPORTED_TTS = "piper / transformers-tts (VITS, MMS-TTS checkpoints, OuteTTS) / kokoro / bark"
+SUPPORTED_TTS = "piper / coqui (VITS) / transformers-tts (VITS, MMS-TTS checkpoints, OuteTTS) / kokoro / bark"
 
 
 class UnsupportedServicer(BackendServicer):

@@ -162,14 +162,8 @@ def test_vits_gpu_matches_cpu():
     assert np.linalg.norm(gm - c) / np.linalg.norm(c) < 2e-2 and np.abs(gm - c).max() < 3e-2
 
 
-@pytest.mark.parametrize("backend", ["coqui"])
-def test_foreign_tts_backends_refuse_explicitly(backend):
-    """Backend names whose model families are not implemented never silently load VITS."""
-    from localai_tfp_amd.grpc import pb
+def test_coqui_backend_routes_to_the_vits_worker():
+    """The reference's `coqui` backend name is served by the VITS worker (Coqui VITS checkpoints,
+    tests/test_coqui.py); XTTS is refused there, never silently replaced by another speech model."""
     from localai_tfp_amd.workers import WORKERS
-    from localai_tfp_amd.workers.unsupported import UnsupportedServicer
-    assert WORKERS[backend].endswith(".unsupported")
-    s = UnsupportedServicer()
-    s.backend = backend
-    r = s.LoadModel(pb.ModelOptions(Model="suno/bark-small"), None)
-    assert not r.success and backend in r.message and "not implemented" in r.message
+    assert WORKERS["coqui"].endswith(".tts")
