@@ -18,20 +18,25 @@
 // with LEAD = 2 the consumers also prefetch the next tile's first fragments before the barrier, so the
 // matrix pipe sees no per-tile bubble.
 // =====================================================================================================
-template <int QT, int CM, int WM, int WN, int GP, int LEAD>
+// AD > 0: the consumer waves read their A fragments straight from global memory (L2-resident rows) into an
+// AD-deep register ring instead of an LDS tile: the LDS then holds only the raw weight ring + the B16 tiles,
+// so far more bytes are in flight per CU, and the A operand never crosses the LDS port.
+template <int QT, int CM, int WM, int WN, int GP, int LEAD, int AD = 0>
 struct QwsCfg {
     static constexpr int CN = 4 / CM;
     static constexpr int BM = 32 * WM * CM, BN = 32 * WN * CN;
     using G = QmmGeom<QT, GP>;
-    static constexpr int A_BYTES = BM * 128;
+    static constexpr int A_BYTES = AD ? 0 : BM * 128;
     static constexpr int STAGE = A_BYTES + 4 * G::WBYTES;
     static constexpr int NB = LEAD + 1;
     static constexpr int B16 = BN * 128;
     static constexpr int S0 = (QMM_LDS_BUDGET - NB * B16) / STAGE;
-    static constexpr int NS = S0 > 6 ? 6 : S0;
-    static constexpr int WA = BM / 32;  // A-tile LDS-DMA instructions per producer wave (8 rows x 128 B each)
+    static constexpr int SCAP = AD ? 10 : 6;
+    static constexpr int NS = S0 > SCAP ? SCAP : S0;
+    static constexpr int WA = AD ? 0 : BM / 32;  // A-tile LDS-DMA instructions per producer wave (8 rows x 128 B each)
     static constexpr int NI = WA + G::NI;
-    static constexpr bool OK = BN == 128 * GP && CM * CN == 4 && NS >= 2 + LEAD && (NS - 2) * NI <= 63 && WA >= 1;
+    static constexpr bool OK =
+        BN == 128 * GP && CM * CN == 4 && NS >= 2 + LEAD && (NS - 2) * NI <= 63 && (AD ? AD * 4 * WM <= 48 : WA >= 1);
 };
 
 // wait (no barrier) until at most `ahead` k-tiles (NI LDS-DMA instructions each) of this wave are in flight
@@ -46,12 +51,16 @@ MX_DEV void qws_wait(int ahead) {
 }
 
 MX_DEV void qws_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+MX_DEV void qws_barrier(int dbg) {
+    if (dbg & 32) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // timing experiment only: no barrier
+    else qws_barrier();
+}
 
-template <int QT, int CM, int WM, int WN, int GP, int LEAD, int EPI>
+template <int QT, int CM, int WM, int WN, int GP, int LEAD, int AD, int EPI>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void
 qmm_ws_kernel(const uint16_t* __restrict__ A, int lda, const uint8_t* __restrict__ W, int M, int N, int K, int n_mt,
               int splits, int kt_per_split, void* __restrict__ Cv, int ldc, int dbg) {
-    using C = QwsCfg<QT, CM, WM, WN, GP, LEAD>;
+    using C = QwsCfg<QT, CM, WM, WN, GP, LEAD, AD>;
     using G = typename C::G;
     using F = QmmFmt<QT>;
     constexpr int NS = C::NS, NB = C::NB, WA = C::WA, NI = C::NI;
@@ -82,7 +91,7 @@ qmm_ws_kernel(const uint16_t* __restrict__ A, int lda, const uint8_t* __restrict
         const int n_p = n_base + p * GP * 32;
         const int ngrp = N >> 5;
         const size_t gstride = (size_t)(nkt / F::PER_UNIT) * F::UNIT;
-        uint32_t aoff[WA];
+        uint32_t aoff[WA > 0 ? WA : 1];
 #pragma unroll
         for (int i = 0; i < WA; ++i) {
             const int r = (p * WA + i) * 8 + (lane >> 3);
@@ -159,7 +168,8 @@ qmm_ws_kernel(const uint16_t* __restrict__ A, int lda, const uint8_t* __restrict
                 dequant(kt0 + j);
             }
         qws_barrier();
-        for (int t = kt0; t < kt1; ++t) {
+        const int pend = AD > 0 ? kt0 + (kt1 - kt0 + AD - 1) / AD * AD : kt1;
+        for (int t = kt0; t < pend; ++t) {
             const int tt = t + LEAD;
             if (tt < kt1) {
                 // issued so far: tiles up to min(kt1 - 1, t + NS - 2)
@@ -168,7 +178,7 @@ qmm_ws_kernel(const uint16_t* __restrict__ A, int lda, const uint8_t* __restrict
             }
             // the slot of tile t - 1 is free: every consumer finished it before barrier #t
             if (t + NS - 1 < kt1) issue(t + NS - 1);
-            qws_barrier();
+            qws_barrier(dbg);
         }
         return;
     }
@@ -183,6 +193,58 @@ qmm_ws_kernel(const uint16_t* __restrict__ A, int lda, const uint8_t* __restrict
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
+    if constexpr (AD > 0) {
+        // A fragments from global memory: lane (col, h) of row block i, k-step s reads the 16 B at
+        // row m_base + (cm WM + i) 32 + col, k = 64 kt + 16 s + 8 h (the 32x32x16 A-operand layout)
+        const uint16_t* arow[WM];
+#pragma unroll
+        for (int i = 0; i < WM; ++i)
+            arow[i] = A + (size_t)min(m_base + (cm * WM + i) * 32 + col, M - 1) * lda + 8 * h;
+        f16x8 abuf[AD][4][WM];
+        auto aload = [&](int kt, f16x8 (&dst)[4][WM]) {
+#pragma unroll
+            for (int s = 0; s < 4; ++s)
+#pragma unroll
+                for (int i = 0; i < WM; ++i) dst[s][i] = *(const f16x8*)(arow[i] + (size_t)kt * QMM_KT + 16 * s);
+        };
+        f16x8 bb[2][WN];
+        auto rdb = [&](int kt, int s, f16x8 (&b)[WN]) {
+            const char* sb = b16 + ((kt - kt0) % NB) * C::B16;
+            if (dbg & 16) return;
+#pragma unroll
+            for (int j = 0; j < WN; ++j) b[j] = *(const f16x8*)(sb + qmm_a_off((cn * WN + j) * 32 + col, 2 * s + h));
+        };
+        // prefetches past kt1 re-read the last tile (unconditional loads keep the compiler's vmcnt counting exact);
+        // the loop runs a multiple of AD tiles, MFMAs only on live ones, one barrier per tile as the producers do
+#pragma unroll
+        for (int d = 0; d < AD; ++d) aload(min(kt0 + d, kt1 - 1), abuf[d]);
+        qws_barrier();
+        if constexpr (LEAD >= 2) rdb(kt0, 0, bb[0]);
+        const int kend = kt0 + (kt1 - kt0 + AD - 1) / AD * AD;
+        for (int tb = kt0; tb < kend; tb += AD) {
+#pragma unroll
+            for (int d = 0; d < AD; ++d) {
+                const int t = tb + d;
+                const bool live = t < kt1;
+                if constexpr (LEAD < 2) rdb(t, 0, bb[0]);
+#pragma unroll
+                for (int s = 0; s < 4; ++s) {
+                    const int cur = s & 1;
+                    if (s < 3) rdb(t, s + 1, bb[cur ^ 1]);
+                    else if constexpr (LEAD >= 2) rdb(t + 1, 0, bb[0]);
+                    if (live && !(dbg & 1))
+#pragma unroll
+                        for (int i = 0; i < WM; ++i)
+#pragma unroll
+                            for (int j = 0; j < WN; ++j)
+                                acc[i][j] =
+                                    __builtin_amdgcn_mfma_f32_32x32x16_f16(abuf[d][s][i], bb[cur][j], acc[i][j], 0, 0, 0);
+                }
+                aload(min(t + AD, kt1 - 1), abuf[d]);
+                qws_barrier(dbg);
+            }
+        }
+    } else {
     f16x8 ar[2][WM], br[2][WN];
     auto rd = [&](int kt, int s, f16x8 (&a)[WM], f16x8 (&b)[WN]) {
         const char* sa = smem + ((kt - kt0) % NS) * C::STAGE;
@@ -209,6 +271,7 @@ qmm_ws_kernel(const uint16_t* __restrict__ A, int lda, const uint8_t* __restrict
                     acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ar[cur][i], br[cur][j], acc[i][j], 0, 0, 0);
         }
         qws_barrier();
+    }
     }
 
     // ---- epilogue (32x32 C/D layout: col = lane & 31, row = 8*(r>>2) + 4*(lane>>5) + (r&3)) ----
@@ -271,16 +334,17 @@ qmm_ws_kernel(const uint16_t* __restrict__ A, int lda, const uint8_t* __restrict
     }
 }
 
-static int g_qws_dbg = 0;  // isolation experiments (tools/tune_qmm_ws.py --dbg): 1 no MFMA, 2 no dequant, 4 no A loads, 8 no W loads
+static int g_qws_dbg = 0;  // isolation experiments (tools/tune_qmm_ws.py --dbg): 1 no MFMA, 2 no dequant, 4 no A loads,
+                           // 8 no W loads, 16 no B16 reads (register-A consumers), 32 no per-tile barrier
 extern "C" int mxk_qmm_ws_dbg(int v) {
     g_qws_dbg = v;
     return 0;
 }
 
-template <int QT, int CM, int WM, int WN, int GP, int LEAD, int EPI>
+template <int QT, int CM, int WM, int WN, int GP, int LEAD, int AD, int EPI>
 static int launch_qmm_ws(const uint16_t* A, int lda, const uint8_t* W, int M, int N, int K, int splits, void* C, int ldc,
                          hipStream_t st) {
-    using Cf = QwsCfg<QT, CM, WM, WN, GP, LEAD>;
+    using Cf = QwsCfg<QT, CM, WM, WN, GP, LEAD, AD>;
     if constexpr (!Cf::OK) {
         return (int)hipErrorInvalidValue;  // this format's stage does not fit the ring at this tile
     } else {
@@ -295,28 +359,33 @@ static int launch_qmm_ws(const uint16_t* A, int lda, const uint8_t* W, int M, in
         if (nwg <= 0 || nwg > 0x7fffffff) return (int)hipErrorInvalidValue;
         static bool attr_set = false;
         if (!attr_set) {
-            (void)hipFuncSetAttribute((const void*)qmm_ws_kernel<QT, CM, WM, WN, GP, LEAD, EPI>,
+            (void)hipFuncSetAttribute((const void*)qmm_ws_kernel<QT, CM, WM, WN, GP, LEAD, AD, EPI>,
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
             attr_set = true;
         }
-        qmm_ws_kernel<QT, CM, WM, WN, GP, LEAD, EPI><<<dim3((unsigned)nwg), 512, lds, st>>>(A, lda, W, M, N, K, n_mt, splits,
+        qmm_ws_kernel<QT, CM, WM, WN, GP, LEAD, AD, EPI><<<dim3((unsigned)nwg), 512, lds, st>>>(A, lda, W, M, N, K, n_mt, splits,
                                                                                           ktps, C, ldc, g_qws_dbg);
         MXK_CHECK_LAUNCH();
     }
 }
 
-// cfg packs (CM, WM, WN, GP, LEAD) as decimal digits CM*10000 + WM*1000 + WN*100 + GP*10 + LEAD
+// cfg packs (AD, CM, WM, WN, GP, LEAD) as decimal digits AD*100000 + CM*10000 + WM*1000 + WN*100 + GP*10 + LEAD
 template <int QT, int EPI>
 static int dispatch_qmm_ws(int cfg, const uint16_t* A, int lda, const uint8_t* W, int M, int N, int K, int splits, void* C,
                            int ldc, hipStream_t st) {
-#define QWS_CASE(CM_, WM_, WN_, GP_, L_)                                                          \
-    if (cfg == CM_ * 10000 + WM_ * 1000 + WN_ * 100 + GP_ * 10 + L_)                              \
-        return launch_qmm_ws<QT, CM_, WM_, WN_, GP_, L_, EPI>(A, lda, W, M, N, K, splits, C, ldc, st);
+#define QWS_CASE(CM_, WM_, WN_, GP_, L_) QWS_CASE_A(0, CM_, WM_, WN_, GP_, L_)
+#define QWS_CASE_A(AD_, CM_, WM_, WN_, GP_, L_)                                                         \
+    if (cfg == AD_ * 100000 + CM_ * 10000 + WM_ * 1000 + WN_ * 100 + GP_ * 10 + L_)                      \
+        return launch_qmm_ws<QT, CM_, WM_, WN_, GP_, L_, AD_, EPI>(A, lda, W, M, N, K, splits, C, ldc, st);
     // BM x BN: 128x128 (2x2 waves of 64x64), 256x128 (2x2 of 128x64), 128x256 (2x2 of 64x128),
     // 64x128 (1x4 of 64x32), 64x256 (1x4 of 64x64), 128x128 (4x1 of 32x128)
     QWS_CASE(2, 2, 2, 1, 1) QWS_CASE(2, 2, 2, 1, 2) QWS_CASE(2, 4, 2, 1, 1) QWS_CASE(2, 2, 4, 2, 1)
     QWS_CASE(1, 2, 1, 1, 1) QWS_CASE(1, 2, 1, 1, 2) QWS_CASE(1, 2, 2, 2, 1) QWS_CASE(4, 1, 4, 1, 1)
     QWS_CASE(4, 1, 4, 1, 2)
+    // A fragments in a register ring (AD tiles deep): 128x128 (4x1 of 32x128), 256x128 (4x1 of 64x128),
+    // 128x256 (4x1 of 32x256), 128x128 (2x2 of 64x64)
+    QWS_CASE_A(4, 4, 1, 4, 1, 2) QWS_CASE_A(2, 4, 2, 4, 1, 2) QWS_CASE_A(2, 4, 1, 8, 2, 1) QWS_CASE_A(4, 2, 2, 2, 1, 2)
+#undef QWS_CASE_A
 #undef QWS_CASE
     return (int)hipErrorInvalidValue;
 }

@@ -535,15 +535,16 @@ def _qmm_shape(M: int, N_: int, K: int, can_split: bool):
 
 # qmm_ws.hip: warp-specialised variant (4 producer waves: LDS-DMA + dequant into an f16 B tile; 4 MFMA-only
 # consumer waves). cfg = CM*10000 + WM*1000 + WN*100 + GP*10 + LEAD: consumer grid CM x (4/CM), wave tile
-# 32WM x 32WN, GP weight groups (32 columns) per producer wave (BN = 128 GP), producers LEAD k-tiles ahead.
+# 32WM x 32WN, GP weight groups (32 columns) per producer wave (BN = 128 GP), producers LEAD k-tiles ahead;
+# + AD*100000: A fragments read by the consumers into an AD-deep register ring instead of an LDS tile.
 QMM_WS = os.environ.get("MX_QMM_WS", "0") == "1"
 QMM_WS_FORCE: tuple | None = None  # (cfg, splits) override for tuning (tools/tune_qmm_ws.py)
-QMM_WS_CONFIGS = (22211, 22212, 24211, 22421, 12111, 12112, 12221, 41411, 41412)
+QMM_WS_CONFIGS = (22211, 22212, 24211, 22421, 12111, 12112, 12221, 41411, 41412, 441412, 242412, 241821, 422212)
 
 
 def qmm_ws_geom(cfg: int):
     """-> (BM, BN) of a qmm_ws configuration."""
-    cm, wm, wn = cfg // 10000, (cfg // 1000) % 10, (cfg // 100) % 10
+    cm, wm, wn = (cfg // 10000) % 10, (cfg // 1000) % 10, (cfg // 100) % 10
     return 32 * wm * cm, 32 * wn * (4 // cm)
 
 
