@@ -248,7 +248,9 @@ class RwkvModel:
         K.layernorm(xn, self.ln0_w, self.ln0_b, eps, h)  # ln0 on the embeddings
         seg = _Segments(fb, T, self.slot_div)
         sx = ws.sx[:T]
-        x16 = ws.x16[:, :T]
+        # the shift-mix kernel writes mix m at m*T*C (a contiguous [n_mix, T, C] block): take a contiguous view of
+        # the workspace, not the strided ws.x16[:, :T] (whose mixes sit max_tokens*C apart)
+        x16 = ws.x16.view(-1)[:5 * T * C].view(5, T, C)
         rkvwg = ws.rkvwg[:, :T]
         for li, L in enumerate(self.layers):
             att_shift, ffn_shift, wkv = state.layer(li)
