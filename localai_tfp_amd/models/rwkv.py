@@ -313,6 +313,9 @@ def shift_mix(x, shift_state, maa, dm, out16, seg: _Segments, sx_in=None, sx_out
     n_mix = maa.shape[0]
     if x.is_cuda:
         from .. import _native as N
+        # the kernel addresses out16 / dm as contiguous [n_mix, T, C] blocks (mix m at m*T*C)
+        if not out16.is_contiguous() or (dm is not None and not dm.is_contiguous()):
+            raise ValueError("shift_mix: out16 / dm must be contiguous [n_mix, T, C]")
         N.ensure_act(out16.dtype)
         N.kcall("mxk_rwkv_shift_mix", x.data_ptr(), x.stride(0), shift_state.data_ptr(), N.ptr(sx_in), N.ptr(sx_out),
                 maa.data_ptr(), N.ptr(dm), out16.data_ptr(), n_mix, seg.slots.data_ptr(), seg.positions.data_ptr(),
