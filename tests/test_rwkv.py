@@ -218,3 +218,24 @@ def test_synthetic_rwkv6_1b6_gpu():
     model, _, cfg, _ = load_llm("synthetic:rwkv6-1b6", "cuda:0")
     out = _engine(model, use_graphs=True).generate(list(range(1, 50)), SamplingParams(temperature=0.0), max_tokens=12)
     assert len(out.token_ids) == 12
+
+
+@pytest.mark.gpu
+def test_rwkv6_engine_workspace_nan_filled_gpu():
+    """Every workspace buffer is written before it is read: NaN-filled workspace + state, eager engine, greedy
+    tokens still match the fp32 reference (caught the strided shift-mix view that read stale rows when
+    T < max_tokens)."""
+    model, src = _model("cuda:0", seed=6)
+    eng = _engine(model, use_graphs=False)
+    for t in list(vars(eng.ws).values()) + list(vars(eng.kv).values()):
+        if isinstance(t, torch.Tensor) and t.is_floating_point():
+            t.fill_(float("nan"))
+    rng = np.random.default_rng(3)
+    prompts = [rng.integers(0, model.cfg.vocab, n).tolist() for n in (9, 26, 4)]
+    from localai_tfp_amd.engine.sequence import Request
+    hs = [eng.submit(Request(p, SamplingParams(temperature=0.0), 4)) for p in prompts]
+    eng.run_until_done()
+    for p, h in zip(prompts, hs):
+        toks = _tokens(h)
+        assert len(toks) == 4
+        _check_greedy(model.cfg, src, p, toks, tol=5e-2)
