@@ -13,7 +13,14 @@ model directory (``config.json`` + ``*.safetensors`` [+ ``model.safetensors.inde
 * weights stay bf16 by default (the precision the reference's vLLM / transformers backends serve;
   hipBLASLt GEMMs), or are quantised at load into a GPU-native block format with the ``quant`` option
   (q8_0 — 8.5 bits, within the dequant error of the bf16 checkpoint — q4_k / q6_k), so the qmm / qmv
-  kernels stream them like any GGUF model; ``f16`` / ``f32`` keep other dense copies.
+  kernels stream them like any GGUF model; ``f16`` / ``f32`` keep other dense copies;
+* GPTQ (AutoGPTQ / optimum ``quant_method: gptq``, 2/4/8-bit, ``g_idx`` act-order, v1 zero-point
+  convention or ``checkpoint_format: gptq_v2``) and AWQ (``quant_method: awq``, GEMM packing, 4-bit)
+  checkpoints — what vLLM's ``quantization: gptq / awq`` and exllama2 load
+  (backend/python/vllm/backend.py:106-107) — are dequantised at load from their packed
+  ``qweight / qzeros / scales [/ g_idx]`` tensors, then served like any other checkpoint (bf16 by default,
+  or re-blocked with ``quant``). Parity with AutoGPTQ / AutoAWQ kernels is unpinned (not installed here);
+  the formulas are pinned by tests/test_hf_gptq.py's independent packer.
 """
 from __future__ import annotations
 
@@ -114,10 +121,62 @@ def config_from_hf(hc: dict) -> LlamaConfig:
     return cfg
 
 
-class _SafetensorsDir:
-    """Lazy tensor access over one or more .safetensors shards (fp32 numpy out)."""
+AWQ_ORDER = (0, 2, 4, 6, 1, 3, 5, 7)  # AWQ GEMM packing: nibble i of an int32 holds column 8c + AWQ_ORDER[i]
 
-    def __init__(self, d: str):
+
+def _unpack_rows(qw: np.ndarray, bits: int) -> np.ndarray:
+    """int32 [R, C] packed along rows (GPTQ qweight: 32/bits values of consecutive k per word, low bits first)
+    -> uint8 [R * 32/bits, C]."""
+    u = np.ascontiguousarray(qw).view(np.uint32)
+    per, mask = 32 // bits, (1 << bits) - 1
+    out = np.empty((u.shape[0] * per, u.shape[1]), np.uint8)
+    for j in range(per):
+        out[j::per] = (u >> (bits * j)) & mask
+    return out
+
+
+def _unpack_cols(qw: np.ndarray, bits: int, order=None) -> np.ndarray:
+    """int32 [R, C] packed along columns (GPTQ qzeros, AWQ qweight / qzeros) -> uint8 [R, C * 32/bits];
+    `order`: the column each bit-field holds within its group of 32/bits (AWQ)."""
+    u = np.ascontiguousarray(qw).view(np.uint32)
+    per, mask = 32 // bits, (1 << bits) - 1
+    out = np.empty((u.shape[0], u.shape[1] * per), np.uint8)
+    for i in range(per):
+        out[:, (order[i] if order else i)::per] = (u >> (bits * i)) & mask
+    return out
+
+
+def dequant_gptq(qweight, qzeros, scales, g_idx=None, bits: int = 4, group_size: int = 128, v2: bool = False):
+    """GPTQ linear -> fp32 weight [N, K] (out, in): W[k, n] = s[g(k), n] * (q[k, n] - (z[g(k), n] + 1)), the +1 being
+    AutoGPTQ's v1 zero-point storage (none for gptq_v2)."""
+    if bits not in (2, 4, 8):
+        raise ValueError(f"GPTQ {bits}-bit weights are not supported (2 / 4 / 8)")
+    N = scales.shape[1]
+    q = _unpack_rows(qweight, bits).astype(np.float32)
+    K = q.shape[0]
+    z = _unpack_cols(qzeros, bits)[:, :N].astype(np.float32) + (0.0 if v2 else 1.0)
+    g = (np.asarray(g_idx, np.int64) if g_idx is not None else np.arange(K) // (group_size if group_size > 0 else K))
+    s = np.asarray(scales, np.float32)
+    return np.ascontiguousarray((s[g] * (q - z[g])).T)
+
+
+def dequant_awq(qweight, qzeros, scales, bits: int = 4, group_size: int = 128):
+    """AWQ (GEMM packing) linear -> fp32 weight [N, K]: W[k, n] = s[k // g, n] * (q[k, n] - z[k // g, n])."""
+    if bits != 4:
+        raise ValueError(f"AWQ {bits}-bit weights are not supported (4-bit GEMM packing)")
+    q = _unpack_cols(qweight, 4, AWQ_ORDER).astype(np.float32)
+    K = q.shape[0]
+    z = _unpack_cols(qzeros, 4, AWQ_ORDER).astype(np.float32)
+    g = np.arange(K) // (group_size if group_size > 0 else K)
+    s = np.asarray(scales, np.float32)
+    return np.ascontiguousarray((s[g] * (q - z[g])).T)
+
+
+class _SafetensorsDir:
+    """Lazy tensor access over one or more .safetensors shards (fp32 numpy out). With a GPTQ / AWQ
+    quantization_config, `<linear>.weight` is served dequantised from `<linear>.qweight / qzeros / scales`."""
+
+    def __init__(self, d: str, qcfg: dict | None = None):
         from safetensors import safe_open
         idx = os.path.join(d, "model.safetensors.index.json")
         if os.path.isfile(idx):
@@ -134,11 +193,31 @@ class _SafetensorsDir:
                 self.where[k] = f
         if wm:
             self.where.update({k: v for k, v in wm.items() if v in self._h})
+        self.qcfg = qcfg or {}
+        self.qmethod = str(self.qcfg.get("quant_method", "") or "").lower()
+        if self.qmethod and self.qmethod not in ("gptq", "awq"):
+            raise ValueError(f"quantization_config.quant_method {self.qmethod!r} is not supported (gptq / awq)")
+
+    def _packed(self, k):
+        return (self.qmethod and k.endswith(".weight") and k not in self.where
+                and k[: -len("weight")] + "qweight" in self.where)
 
     def __contains__(self, k):
-        return k in self.where
+        return k in self.where or bool(self._packed(k))
+
+    def raw(self, k):
+        return self._h[self.where[k]].get_tensor(k).numpy()
 
     def get(self, k) -> np.ndarray:
+        if self._packed(k):
+            b = k[: -len("weight")]
+            c = self.qcfg
+            bits, gs = int(c.get("bits", c.get("w_bit", 4))), int(c.get("group_size", c.get("q_group_size", 128)))
+            if self.qmethod == "gptq":
+                gi = self.raw(b + "g_idx") if b + "g_idx" in self.where else None
+                return dequant_gptq(self.raw(b + "qweight"), self.raw(b + "qzeros"), self.raw(b + "scales"), gi, bits, gs,
+                                    v2=str(c.get("checkpoint_format", "")).lower() == "gptq_v2")
+            return dequant_awq(self.raw(b + "qweight"), self.raw(b + "qzeros"), self.raw(b + "scales"), bits, gs)
         return self._h[self.where[k]].get_tensor(k).float().numpy()
 
 
@@ -153,7 +232,9 @@ def hf_source(model_dir: str, quant: str = "q8_0"):
     with open(os.path.join(model_dir, "config.json")) as f:
         hc = json.load(f)
     cfg = config_from_hf(hc)
-    st = _SafetensorsDir(model_dir)
+    st = _SafetensorsDir(model_dir, hc.get("quantization_config") or (hc.get("text_config") or {}).get("quantization_config"))
+    if str(quant or "").lower() in ("gptq", "awq", "gptq_marlin", "awq_marlin", "marlin", "exl2"):
+        quant = "bf16"  # vLLM's quantization names: the checkpoint's own format is read from config.json
     qt = QUANTS.get(str(quant or "q8_0").lower())
     if qt is None:
         raise ValueError(f"unknown quantization {quant!r} (choose from {sorted(QUANTS)})")
