@@ -159,7 +159,7 @@ class SamplerBatch:
                 tok.data_ptr(), lp.data_ptr(), N.stream_ptr())
         return tok, lp
 
-    SPLIT_MAX_B = 16
+    SPLIT_MAX_B = int(__import__("os").environ.get("MX_SPLIT_SAMPLER_MAX_B", "16"))
     TOPK_CAP = 64
 
     def _split_slices(self, params, B: int) -> int:
