@@ -178,7 +178,7 @@ class CoquiTokenizer:
         self.bos_id = self.ids.get(bos) if bos else None
         self.eos_id = self.ids.get(eos) if eos else None
         self.espeak_data = espeak_data
-        self._espeak = shutil.which("espeak-ng") or shutil.which("espeak") if self.use_phonemes else None
+        self._espeak = (shutil.which("espeak-ng") or shutil.which("espeak")) if self.use_phonemes else None
 
     def clean(self, text: str) -> str:
         t = text
