@@ -66,6 +66,10 @@ class ApplicationConfig:
     p2p_network_id: str = field(default_factory=lambda: _env(["LOCALAI_P2P_NETWORK_ID", "P2P_NETWORK_ID"], ""))
     # federator / peer URLs this instance announces itself to (libp2p discovery replacement)
     p2p_peers: list = field(default_factory=lambda: _env(["LOCALAI_P2P_PEERS", "P2P_PEERS"], [], list))
+    # LAN discovery beacons (the reference's libp2p mDNS, on by default with p2p); unicast targets for
+    # networks without multicast
+    p2p_lan_discovery: bool = field(default_factory=lambda: not _env(["LOCALAI_P2P_DISABLE_LAN_DISCOVERY"], False, bool))
+    p2p_discovery_targets: list = field(default_factory=lambda: _env(["LOCALAI_P2P_DISCOVERY_TARGETS"], [], list))
     federated: bool = field(default_factory=lambda: _env(["LOCALAI_FEDERATED", "FEDERATED"], False, bool))
     # MI355X specifics
     gpus: str = field(default_factory=lambda: _env(["LOCALAI_GPUS", "HIP_VISIBLE_DEVICES"], ""))

@@ -71,7 +71,8 @@ class Application:
                 c.p2p_token = P.generate_token()
                 log.info("p2p enabled without a token; generated network token: %s", c.p2p_token)
             me = P.self_node(c.address, P.FEDERATED_ID if c.federated else P.WORKER_ID)
-            self.p2p = P.P2PNode(c.p2p_token, c.p2p_network_id, list(c.p2p_peers), me)
+            self.p2p = P.P2PNode(c.p2p_token, c.p2p_network_id, list(c.p2p_peers), me,
+                                 lan_discovery=c.p2p_lan_discovery, discovery_targets=list(c.p2p_discovery_targets))
 
     # ------------------------------------------------------------------ startup
     def startup(self):

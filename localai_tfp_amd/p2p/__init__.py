@@ -11,7 +11,9 @@ Reference behaviour (core/p2p/federated.go, federated_server.go, node.go, p2p.go
     (federated_server.go:84-87).
 Transport: the reference rides libp2p/edgevpn tunnels, which this image does not have. Nodes
 announce to the federator over plain HTTP (`POST /api/p2p/register`, bearer token = the network
-token, constant-time compared) and connections are proxied over TCP directly. Selection, the
+token, constant-time compared), find each other on the local link with HMAC-authenticated UDP
+multicast beacons (p2p/discovery.py, the reference's mDNS discovery), and connections are proxied
+over TCP directly. No DHT / NAT traversal. Selection, the
 liveness window, request accounting and the 503 behaviour follow the reference.
 """
 from __future__ import annotations
@@ -130,12 +132,24 @@ class Announcer:
 
 
 class P2PNode:
-    """Per-instance p2p state behind /api/p2p (what `local-ai run --p2p` sets up)."""
+    """Per-instance p2p state behind /api/p2p (what `local-ai run --p2p` sets up): the registry, HTTP
+    announcements to configured peers, and LAN discovery beacons (p2p/discovery.py; the reference's mDNS)
+    unless `lan_discovery` is False."""
 
     def __init__(self, token: str, network: str = "", peers: list[str] | None = None,
-                 self_node: NodeData | None = None):
+                 self_node: NodeData | None = None, lan_discovery: bool = False, discovery_targets=None,
+                 discovery_port: int | None = None):
         self.registry = Registry(token, network)
         self.announcer = Announcer(self_node, peers or [], token).start() if (self_node and peers) else None
+        self.discovery = None
+        if lan_discovery and token:
+            from .discovery import PORT, LanDiscovery
+            try:
+                self.discovery = LanDiscovery(self.registry, self_node, token, network,
+                                              port=discovery_port if discovery_port is not None else PORT,
+                                              targets=list(discovery_targets or [])).start()
+            except OSError as ex:  # port taken / no network: the HTTP announcements still work
+                log.warning("p2p LAN discovery disabled: %s", ex)
 
     def nodes(self, service: str) -> list[dict]:
         return self.registry.json_nodes(service)
@@ -143,6 +157,8 @@ class P2PNode:
     def stop(self):
         if self.announcer:
             self.announcer.stop()
+        if self.discovery:
+            self.discovery.stop()
 
 
 # ------------------------------------------------------------------------------------------------
