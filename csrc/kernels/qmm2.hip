@@ -1,0 +1,467 @@
+// qmm2.hip — quantised-weight GEMM, second generation (M >= 16: mixed continuous-batching steps, prefill).
+//
+//   C[M, N] (+)= A[M, K] · W[N, K]^T,   A f16, W Q4_K / Q6_K in the t32 tiled layout (ops/quant.py tile32)
+//
+// Why a second kernel: qmm.hip's profile at M = 256 (profiles/r3_pmc_qmm_gate_up_m256.md) showed the
+// MFMA pipe busy only ~31 % of the time with 9-15 VALU + 4-7 SALU + 1.2-1.4 LDS instructions per
+// 32-cycle MFMA: the kernel was issue-bound, not memory- or MFMA-bound. Everything here is arranged to
+// cut the instructions per MFMA:
+//   * wave tile = ALL BM rows (WM = 2..8 MFMA row blocks) x one 32-column weight group: every dequantised
+//     B fragment (14 packed-f16 VALU) feeds WM MFMAs, so at BM = 256 the dequant is < 2 VALU per MFMA;
+//   * the k loop is unrolled over one 256-element super-block (4 k-tiles of 64): the Q4_K / Q6_K scale
+//     decode of a k-tile has compile-time sub-block indices (bit-field extracts, exact f16 products), the
+//     super-block header is DMA'd and read once per super-block (not once per k-tile), and with a 4-slot
+//     ring every LDS address is a per-lane base plus an immediate;
+//   * the A tile's LDS image is [8-row block][k-step][row][16-B half], so a k-step's fragment read is the
+//     same base + k-step * 256 B for every lane (ds_read_b128, conflict-free by an XOR of the half index
+//     with the row block's parity), and each A LDS-DMA wave-instruction still reads 8 whole 128-B rows;
+//   * every operand arrives by LDS-DMA (one load kind, so the counted `s_waitcnt vmcnt` is exact) into a
+//     4-deep ring; dummy (clamped) stages past the end keep the count uniform, so the loop has no
+//     data-dependent branches.
+// KS = 2 doubles the waves (two per SIMD): wave pair (kh = 0, 1) shares a column group and splits each
+// k-tile's four k-steps; their fp32 partials are summed through LDS before the epilogue.
+// Reference parity: llama.cpp's MMQ path for these formats (reached via backend/cpp/llama/grpc-server.cpp:2002
+// llama_decode); numerics = f16 dequantised weights x f16 activations, fp32 accumulation.
+#include "qdeq16.h"
+
+namespace {
+
+constexpr int Q2_NS = 4;  // ring slots (k-tiles of 64)
+
+template <int QT>
+struct Q2F;
+// Q4_K t32 unit (per 32-column group, per super-block): [hdr 32 x 16 B][quarter jq: chunk0, chunk1 (32 x 16 B)]
+template <>
+struct Q2F<MXQ_Q4_K> {
+    static constexpr int UNIT = 4608, HB = 512, QOFF = 512, QB = 1024, QI = 1, HI = 1;
+};
+// Q6_K t32 unit: [sc 32 x 16 B][d 32 x 4 B][quarter jq: ql0, ql1, qh (32 x 16 B)]
+template <>
+struct Q2F<MXQ_Q6_K> {
+    static constexpr int UNIT = 6784, HB = 640, QOFF = 640, QB = 1536, QI = 2, HI = 2;
+};
+
+template <int QT>
+struct Q2B;
+
+template <>
+struct Q2B<MXQ_Q4_K> {
+    u32x4 hd;
+    u32x2 v0, v1;
+    f16x2 sm[2];  // per sub-block of the k-tile: (scale, -dmin * min) as exact f16 products
+    MX_DEV void load_hdr(const char* hb, int col) { hd = *(const u32x4*)(hb + col * 16); }
+    MX_DEV void load_q(const char* qb, int col, int h) {
+        v0 = *(const u32x2*)(qb + col * 16 + 8 * h);
+        v1 = *(const u32x2*)(qb + 512 + col * 16 + 8 * h);
+    }
+    template <int JQ>
+    MX_DEV void prep() {
+        const f16x2 dd = __builtin_bit_cast(f16x2, hd[0]);
+        const f16x2 dn = {dd[0], -dd[1]};
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            int sc, mn;
+            q4k_scale_min_w(hd[1], hd[2], hd[3], 2 * JQ + i, sc, mn);
+            // d * sc is exact in f32 (11 x 6 bits), so the f16 product rounds exactly like the f32 path
+            const f16x2 q = {(_Float16)sc, (_Float16)mn};
+            sm[i] = dn * q;
+        }
+    }
+    template <int S>
+    MX_DEV f16x8 frag() const {
+        const u32x2 src = (S & 1) ? v1 : v0;
+        constexpr int sh = 4 * (S >> 1);
+        const uint32_t t0 = (src[0] >> sh) & 0x0F0F0F0Fu, t1 = (src[1] >> sh) & 0x0F0F0F0Fu;
+        const f16x2 k = {(_Float16)1024.f, (_Float16)1024.f};
+        const f16x2 s2 = {sm[S >> 1][0], sm[S >> 1][0]}, m2 = {sm[S >> 1][1], sm[S >> 1][1]};
+        f16x2 p[4];
+        magic4(t0, p[0], p[1]);
+        magic4(t1, p[2], p[3]);
+        f16x8 r;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const f16x2 v = (p[i] - k) * s2 + m2;
+            r[2 * i] = v[0];
+            r[2 * i + 1] = v[1];
+        }
+        return r;
+    }
+};
+
+template <>
+struct Q2B<MXQ_Q6_K> {
+    u32x4 sc;   // 16 int8 sub-block scales (one per 16 k)
+    uint32_t dw;
+    u32x2 v0, v1, vh;
+    f16x2 s2[4];
+    MX_DEV void load_hdr(const char* hb, int col) {
+        sc = *(const u32x4*)(hb + col * 16);
+        dw = *(const uint32_t*)(hb + 512 + col * 4);
+    }
+    MX_DEV void load_q(const char* qb, int col, int h) {
+        v0 = *(const u32x2*)(qb + col * 16 + 8 * h);
+        v1 = *(const u32x2*)(qb + 512 + col * 16 + 8 * h);
+        vh = *(const u32x2*)(qb + 1024 + col * 16 + 8 * h);
+    }
+    template <int JQ>
+    MX_DEV void prep() {
+        const _Float16 d = __builtin_bit_cast(f16x2, dw)[0];
+        const uint32_t w = sc[JQ];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int v = (int)(int8_t)((w >> (8 * i)) & 0xFF);
+            const _Float16 s = d * (_Float16)v;  // 11 x 8 bits: exact product, one f16 rounding
+            s2[i] = (f16x2){s, s};
+        }
+    }
+    template <int S>
+    MX_DEV f16x8 frag() const {
+        const u32x2 src = (S & 1) ? v1 : v0;
+        constexpr int sh = 4 * (S >> 1), qsh = 2 * S;
+        const uint32_t t0 = ((src[0] >> sh) & 0x0F0F0F0Fu) | (((vh[0] >> qsh) & 0x03030303u) << 4);
+        const uint32_t t1 = ((src[1] >> sh) & 0x0F0F0F0Fu) | (((vh[1] >> qsh) & 0x03030303u) << 4);
+        const f16x2 k = {(_Float16)1056.f, (_Float16)1056.f};  // 1024 magic + 32 code offset
+        f16x2 p[4];
+        magic4(t0, p[0], p[1]);
+        magic4(t1, p[2], p[3]);
+        f16x8 r;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const f16x2 v = (p[i] - k) * s2[S];
+            r[2 * i] = v[0];
+            r[2 * i + 1] = v[1];
+        }
+        return r;
+    }
+};
+
+template <int QT, int WM, int KS>
+struct Q2Geom {
+    using F = Q2F<QT>;
+    static constexpr int BM = 32 * WM;
+    static constexpr int NT = 4 * KS;                 // waves
+    static constexpr int A_BYTES = BM * 128;          // one 64-k tile of A
+    static constexpr int STAGE = A_BYTES + 4 * F::QB; // A + the 4 column groups' quant bytes
+    static constexpr int HSZ = 4 * F::HB;             // one super-block header slot (4 groups)
+    static constexpr int LDS = Q2_NS * STAGE + 2 * HSZ;
+    static constexpr int WA = BM / 8 / NT;            // A LDS-DMA instructions per wave per stage
+    // LDS-DMA instructions per stage of a weight-loading wave (kh == 0) / an A-only wave, by the stage's
+    // position in its super-block (JQ == 0 stages also carry the header)
+    template <int JQ, bool WL>
+    static constexpr int cnt() { return WA + (WL ? F::QI + (JQ == 0 ? F::HI : 0) : 0); }
+};
+
+template <int N_>
+MX_DEV void q2_wait_barrier() {
+    asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N_) : "memory");
+}
+
+template <int QT, int WM, int KS, int EPI>
+__global__ __launch_bounds__(256 * KS) void qmm2_kernel(const uint16_t* __restrict__ A, int lda,
+                                                        const uint8_t* __restrict__ W, int M, int N, int K,
+                                                        int n_mt, int splits, int sbps, void* __restrict__ Cv,
+                                                        int ldc) {
+    using G = Q2Geom<QT, WM, KS>;
+    using F = Q2F<QT>;
+    constexpr int BM = G::BM, WA = G::WA, STAGE = G::STAGE, A_BYTES = G::A_BYTES;
+    static_assert(WA >= 1 && WA * 8 * G::NT == BM, "A tile split");
+    static_assert(G::LDS <= 160 * 1024, "LDS");
+    static_assert(G::template cnt<1, true>() + G::template cnt<2, true>() <= 63 &&
+                  G::template cnt<0, true>() + G::template cnt<1, true>() <= 63, "vmcnt range");
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    char* const hdr_lds = smem + Q2_NS * STAGE;
+
+    // wave index as a scalar: every LDS-DMA destination (M0) and weight pointer below is then SGPR math
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int h = lane >> 5, col = lane & 31;
+    const int cg = wave & 3, kh = wave >> 2;
+
+    // XCD-aware bijective remap: consecutive logical ids (the row tiles and splits of one column panel)
+    // run on one XCD and share its L2
+    const int nwg = gridDim.x, bid = blockIdx.x;
+    const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+    const int lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+    const int mt = lid % n_mt;
+    const int rest = lid / n_mt;
+    const int split = rest % splits;
+    const int ct = rest / splits;
+
+    const int nsb = K >> 8;
+    const int sb0 = split * sbps, sb1 = min(sb0 + sbps, nsb);
+    if (sb0 >= sb1) return;
+    const int m_base = mt * BM;
+    const int ngrp = N >> 5;
+    const int g = min(ct * 4 + cg, ngrp - 1);  // groups past N re-read the last (never stored)
+    const uint8_t* wg = W + (size_t)g * ((size_t)nsb * F::UNIT);
+
+    // A LDS-DMA sources: instruction i of this wave fills 8-row block j = wave * WA + i; lane p writes
+    // image slot (k-step p >> 4, row (p >> 1) & 7, half (p & 1) ^ (j & 1)) from 16 B of that row
+    uint32_t aoff[WA];
+#pragma unroll
+    for (int i = 0; i < WA; ++i) {
+        const int j = wave * WA + i;
+        const int s = lane >> 4, r8 = (lane >> 1) & 7, hh = (lane & 1) ^ (j & 1);
+        const int row = min(m_base + 8 * j + r8, M - 1);
+        aoff[i] = (uint32_t)(row * lda + 16 * s + 8 * hh);
+    }
+    // per-lane fragment read bases (byte offsets within a stage)
+    const int rb = col >> 3;
+    const uint32_t a_rd = (uint32_t)(rb * 1024 + (col & 7) * 32 + ((h ^ (rb & 1)) << 4));
+    const uint32_t b_rd = (uint32_t)(A_BYTES + cg * F::QB);
+
+    // stage issue: the A rows of k-tile `kta` and (weight waves) the quant bytes of super-block `sbw`,
+    // quarter JQ, into ring slot JQ; JQ == 0 stages also bring that super-block's header into header slot
+    // `hslot`. Dummy stages past the end pass clamped (valid, never consumed) sources.
+    auto issue = [&](int kta, int sbw, int hslot, auto jq_c, auto wl_c) {
+        constexpr int JQ = decltype(jq_c)::value;
+        char* sb = smem + JQ * STAGE;
+        const uint16_t* ak = A + (size_t)kta * 64;
+#pragma unroll
+        for (int i = 0; i < WA; ++i)
+            __builtin_amdgcn_global_load_lds((const void*)(ak + aoff[i]), (MX_LDS void*)(sb + (wave * WA + i) * 1024),
+                                             16, 0, 0);
+        if constexpr (decltype(wl_c)::value) {
+            const uint8_t* u = wg + (size_t)sbw * F::UNIT;
+            const uint8_t* qs = u + F::QOFF + JQ * F::QB;
+            char* qd = sb + A_BYTES + cg * F::QB;
+            __builtin_amdgcn_global_load_lds((const void*)(qs + lane * 16), (MX_LDS void*)qd, 16, 0, 0);
+            if constexpr (QT == MXQ_Q6_K) {
+                if (lane < 32)
+                    __builtin_amdgcn_global_load_lds((const void*)(qs + 1024 + lane * 16), (MX_LDS void*)(qd + 1024), 16,
+                                                     0, 0);
+            }
+            if constexpr (JQ == 0) {
+                char* hd = hdr_lds + hslot * G::HSZ + cg * F::HB;
+                if (lane < 32) __builtin_amdgcn_global_load_lds((const void*)(u + lane * 16), (MX_LDS void*)hd, 16, 0, 0);
+                if constexpr (QT == MXQ_Q6_K) {
+                    if (lane < 32)
+                        __builtin_amdgcn_global_load_lds((const void*)(u + 512 + lane * 4), (MX_LDS void*)(hd + 512), 4,
+                                                         0, 0);
+                }
+            }
+        }
+    };
+
+    f32x16 acc[WM];
+#pragma unroll
+    for (int i = 0; i < WM; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
+
+    auto mainloop = [&](auto kh_c, auto wl_c) {
+        constexpr int KH = decltype(kh_c)::value;
+        using WLc = decltype(wl_c);
+        constexpr bool WL = WLc::value;
+        using I0 = std::integral_constant<int, 0>;
+        using I1 = std::integral_constant<int, 1>;
+        using I2 = std::integral_constant<int, 2>;
+        using I3 = std::integral_constant<int, 3>;
+        const int kt0 = sb0 * 4, kt1 = sb1 * 4;
+        // prologue: stages kt0 .. kt0+2 (a split holds >= 4 k-tiles, so all real)
+        issue(kt0, sb0, sb0 & 1, I0{}, WLc{});
+        issue(kt0 + 1, sb0, 0, I1{}, WLc{});
+        issue(kt0 + 2, sb0, 0, I2{}, WLc{});
+        q2_wait_barrier<G::template cnt<1, WL>() + G::template cnt<2, WL>()>();
+
+        Q2B<QT> bw;
+        f16x8 af[2][WM];
+        bw.load_hdr(hdr_lds + (sb0 & 1) * G::HSZ + cg * F::HB, col);
+        bw.load_q(smem + b_rd, col, h);
+#pragma unroll
+        for (int i = 0; i < WM; ++i) af[0][i] = *(const f16x8*)(smem + a_rd + i * 4096 + KH * 256);
+
+        // one k-tile (ring slot JQ): the wave's k-steps KH, KH + KS, ...; the A fragments of the next k-step
+        // (on the last one: of the next tile, slot JQ + 1, waited for at the top) are read while this
+        // k-step's MFMAs run; the next tile's quant bytes (and header at a super-block edge) likewise
+        auto tile = [&](int sb, auto jq_c) {
+            constexpr int JQ = decltype(jq_c)::value;
+            constexpr int NJ = (JQ + 1) & 3;
+            const int kt = sb * 4 + JQ;
+            // stage kt+1 landed (only stage kt+2 may still be in flight); every wave is past tile kt-1
+            q2_wait_barrier<G::template cnt<(JQ + 2) & 3, WL>()>();
+            {
+                const int ki = kt + 3;
+                const bool real = ki < kt1;
+                issue(real ? ki : kt1 - 1, real ? (ki >> 2) : sb1 - 1, (ki >> 2) & 1,
+                      std::integral_constant<int, (JQ + 3) & 3>{}, WLc{});
+            }
+            bw.template prep<JQ>();
+            Q2B<QT> bn = bw;
+            constexpr int NSTEP = 4 / KS;
+#pragma unroll
+            for (int t = 0; t < NSTEP; ++t) {
+                const int S = KH + KS * t;  // compile-time after unrolling
+                const int cur = t & 1;
+                if (t + 1 < NSTEP) {
+#pragma unroll
+                    for (int i = 0; i < WM; ++i)
+                        af[cur ^ 1][i] = *(const f16x8*)(smem + JQ * STAGE + a_rd + i * 4096 + (S + KS) * 256);
+                } else {
+#pragma unroll
+                    for (int i = 0; i < WM; ++i)
+                        af[cur ^ 1][i] = *(const f16x8*)(smem + NJ * STAGE + a_rd + i * 4096 + KH * 256);
+                    if constexpr (NJ == 0) bn.load_hdr(hdr_lds + ((sb + 1) & 1) * G::HSZ + cg * F::HB, col);
+                    bn.load_q(smem + NJ * STAGE + b_rd, col, h);
+                }
+                f16x8 bf;
+                switch (S) {
+                    case 0: bf = bw.template frag<0>(); break;
+                    case 1: bf = bw.template frag<1>(); break;
+                    case 2: bf = bw.template frag<2>(); break;
+                    default: bf = bw.template frag<3>(); break;
+                }
+#pragma unroll
+                for (int i = 0; i < WM; ++i) acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[cur][i], bf, acc[i], 0, 0, 0);
+            }
+            // NSTEP is even: the next tile's first fragments are in af[0]
+            bw = bn;
+        };
+        for (int sb = sb0; sb < sb1; ++sb) {
+            tile(sb, I0{});
+            tile(sb, I1{});
+            tile(sb, I2{});
+            tile(sb, I3{});
+        }
+        // drain the dummy stages before the LDS is reused / released
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    };
+    using T_ = std::integral_constant<bool, true>;
+    using F_ = std::integral_constant<bool, false>;
+    if constexpr (KS == 1) {
+        mainloop(std::integral_constant<int, 0>{}, T_{});
+    } else {
+        if (kh == 0) mainloop(std::integral_constant<int, 0>{}, T_{});
+        else mainloop(std::integral_constant<int, 1>{}, F_{});
+        // sum the k-step halves: kh = 1 waves park their partials in the drained ring
+        __syncthreads();
+        float* red = (float*)smem + (size_t)cg * (WM * 16 * 64) + lane;
+        if (kh == 1) {
+#pragma unroll
+            for (int i = 0; i < WM; ++i)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) red[(i * 16 + r) * 64] = acc[i][r];
+        }
+        __syncthreads();
+        if (kh == 1) return;
+#pragma unroll
+        for (int i = 0; i < WM; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][r] += red[(i * 16 + r) * 64];
+    }
+
+    // ---- epilogue: 32x32 C/D layout: col = lane & 31, row = 8*(r>>2) + 4*(lane>>5) + (r&3) ----
+    const int nt = (ct * 4 + cg) * 32;
+    const int n = nt + col;
+    if (nt >= N) return;
+    if constexpr (EPI == E16_SWIGLU || EPI == E16_GEGLU) {
+        // W rows interleaved in 16-row groups: tile columns 0..15 gate, 16..31 up of the same features
+#pragma unroll
+        for (int i = 0; i < WM; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float v = acc[i][r];
+                const float up = __shfl_xor(v, 16);
+                const int m = m_base + i * 32 + 8 * (r >> 2) + 4 * h + (r & 3);
+                if (col < 16 && m < M)
+                    ((uint16_t*)Cv)[(size_t)m * ldc + (nt >> 1) + col] = f32_to_act<true>(glu_gate_f<EPI>(v) * up);
+            }
+        return;
+    }
+#pragma unroll
+    for (int i = 0; i < WM; ++i) {
+        const int m0 = m_base + i * 32 + 4 * h;
+        if (m_base + i * 32 >= M) break;
+        float* cf = ((float*)Cv) + (size_t)m0 * ldc + n;
+        uint16_t* ch = ((uint16_t*)Cv) + (size_t)m0 * ldc + n;
+        auto roff = [&](int r) { return (size_t)(8 * (r >> 2) + (r & 3)) * ldc; };
+        if (m_base + i * 32 + 32 <= M) {
+            if constexpr (EPI == E16_ADD_F32) {
+                if (splits == 1) {
+                    float old[16];
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) old[r] = cf[roff(r)];
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) cf[roff(r)] = old[r] + acc[i][r];
+                } else {
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) atomicAdd(cf + roff(r), acc[i][r]);
+                }
+            } else {
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    if constexpr (EPI == E16_F32) cf[roff(r)] = acc[i][r];
+                    else ch[roff(r)] = f32_to_act<true>(acc[i][r]);
+                }
+            }
+            continue;
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            if (m0 + 8 * (r >> 2) + (r & 3) >= M) continue;
+            const float v = acc[i][r];
+            if constexpr (EPI == E16_F32) cf[roff(r)] = v;
+            else if constexpr (EPI == E16_ACT) ch[roff(r)] = f32_to_act<true>(v);
+            else if (splits == 1) cf[roff(r)] += v;
+            else atomicAdd(cf + roff(r), v);
+        }
+    }
+}
+
+template <int QT, int WM, int KS, int EPI>
+static int launch_qmm2(const uint16_t* A, int lda, const uint8_t* W, int M, int N, int K, int splits, void* C, int ldc,
+                       hipStream_t st) {
+    using G = Q2Geom<QT, WM, KS>;
+    const int nsb = K >> 8;
+    splits = max(1, min(splits, nsb));
+    const int sbps = (nsb + splits - 1) / splits;
+    splits = (nsb + sbps - 1) / sbps;  // no empty splits
+    const int n_ct = (N + 127) / 128, n_mt = (M + G::BM - 1) / G::BM;
+    const long nwg = (long)n_ct * splits * n_mt;
+    if (nwg <= 0 || nwg > 0x7fffffff) return (int)hipErrorInvalidValue;
+    static bool attr_set = false;
+    if (!attr_set) {
+        (void)hipFuncSetAttribute((const void*)qmm2_kernel<QT, WM, KS, EPI>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  G::LDS);
+        attr_set = true;
+    }
+    qmm2_kernel<QT, WM, KS, EPI><<<dim3((unsigned)nwg), 256 * KS, G::LDS, st>>>(A, lda, W, M, N, K, n_mt, splits, sbps,
+                                                                                C, ldc);
+    MXK_CHECK_LAUNCH();
+}
+
+template <int QT, int EPI>
+static int dispatch_qmm2(int wm, int ks, const uint16_t* A, int lda, const uint8_t* W, int M, int N, int K, int splits,
+                         void* C, int ldc, hipStream_t st) {
+#define Q2_CASE(WM_, KS_) \
+    if (wm == WM_ && ks == KS_) return launch_qmm2<QT, WM_, KS_, EPI>(A, lda, W, M, N, K, splits, C, ldc, st);
+    Q2_CASE(2, 1) Q2_CASE(2, 2) Q2_CASE(4, 1) Q2_CASE(4, 2) Q2_CASE(6, 1) Q2_CASE(8, 1) Q2_CASE(8, 2)
+#undef Q2_CASE
+    return (int)hipErrorInvalidValue;
+}
+
+}  // namespace
+
+// A f16 [M, K] (lda % 8 == 0, 16-B aligned), W t32 Q4_K / Q6_K [N, K] (N % 32 == 0, K % 256 == 0).
+// epi: 0 fp32 store, 1 f16 store, 2 fp32 accumulate (split-K via atomics when splits > 1), 3/4 SwiGLU /
+// GeGLU over 16-row interleaved gate|up -> f16 [M, N/2]. wm: 32-row MFMA blocks per wave (BM = 32 wm);
+// ks: 1 (4 waves) or 2 (8 waves, k-steps split per wave pair). splits: K split in whole super-blocks.
+extern "C" int mxk_qmm2(int qtype, int epi, int wm, int ks, const uint16_t* A, int lda, const uint8_t* W, int M, int N,
+                        int K, int splits, void* C, int ldc, hipStream_t st) {
+    if (M <= 0) return 0;
+    if (K % 256 || (lda & 7) || ((uintptr_t)A & 15) || ((uintptr_t)W & 15) || (N & 31)) return (int)hipErrorInvalidValue;
+    if (epi != E16_ADD_F32 && splits != 1) return (int)hipErrorInvalidValue;
+#define Q2_EPI(QT_)                                                                                          \
+    switch (epi) {                                                                                           \
+        case E16_F32: return dispatch_qmm2<QT_, E16_F32>(wm, ks, A, lda, W, M, N, K, splits, C, ldc, st);     \
+        case E16_ACT: return dispatch_qmm2<QT_, E16_ACT>(wm, ks, A, lda, W, M, N, K, splits, C, ldc, st);     \
+        case E16_ADD_F32: return dispatch_qmm2<QT_, E16_ADD_F32>(wm, ks, A, lda, W, M, N, K, splits, C, ldc, st); \
+        case E16_SWIGLU: return dispatch_qmm2<QT_, E16_SWIGLU>(wm, ks, A, lda, W, M, N, K, splits, C, ldc, st); \
+        case E16_GEGLU: return dispatch_qmm2<QT_, E16_GEGLU>(wm, ks, A, lda, W, M, N, K, splits, C, ldc, st);   \
+    }
+    switch (qtype) {
+        case MXQ_Q4_K: Q2_EPI(MXQ_Q4_K) break;
+        case MXQ_Q6_K: Q2_EPI(MXQ_Q6_K) break;
+    }
+#undef Q2_EPI
+    return (int)hipErrorInvalidValue;
+}

@@ -589,6 +589,17 @@ class LLMEngine:
         """Sampling that needs no host-side token history or per-token host state."""
         return (p.mirostat != 2 and p.repeat_penalty == 1.0 and not p.presence_penalty and not p.frequency_penalty)
 
+    @staticmethod
+    def _argmax_only(items) -> bool:
+        """True when every row's token is the plain argmax of its logits (greedy, no logit bias, no
+        penalties, no grammar). The ONE predicate behind both decisions that must agree: whether tensor
+        parallel ranks gather the full logits (plan["gather"] = not this) and whether the step takes the
+        vocab-parallel argmax instead of the sampler (a sampler on an ungathered shard samples this rank's
+        vocabulary slice only)."""
+        return all(it.seq.params.greedy and not it.seq.params.logit_bias and it.seq.params.repeat_penalty == 1.0
+                   and not it.seq.params.presence_penalty and not it.seq.params.frequency_penalty
+                   and it.seq.grammar is None for it in items)
+
     def _overlap_ok(self, so: SchedulerOutput) -> bool:
         for it in so.decode:
             if it.seq.grammar is not None or it.seq.req.embedding or not self._simple_params(it.seq.params):
@@ -611,15 +622,14 @@ class LLMEngine:
         items = list(so.decode) + [it for it in so.prefill if it.sample]
         if self.tp is not None:
             plan["ns"] = len(items)
-            plan["gather"] = bool(items) and not all(it.seq.params.greedy and not it.seq.params.logit_bias
-                                                     for it in items)
+            plan["gather"] = bool(items) and not self._argmax_only(items)
             self.tp.send_plan(plan)
         if roctx.ENABLED:
             roctx.push("launch graph" if plan["graph"] else "launch eager")
         logits, am = self._execute(plan)
         tok_dev, lp_dev = None, None
         if items:
-            if am is not None and all(it.seq.params.greedy and not it.seq.params.logit_bias for it in items):
+            if am is not None and self._argmax_only(items):
                 tok_dev = am
             elif not logits.is_cuda:  # CPU reference sampler (host lists)
                 t, l = self.sampler.sample(logits, [it.seq.params for it in items], [[] for _ in items],
@@ -912,9 +922,7 @@ class LLMEngine:
         plan = self._plan(so)
         self.stats["plan_s"] += time.perf_counter() - t0
         sample_items = [it for it in so.decode] + [it for it in so.prefill if it.sample]
-        params = [it.seq.params for it in sample_items]
-        greedy_only = all(p.greedy and not p.logit_bias and p.repeat_penalty == 1.0 and not p.presence_penalty
-                          and not p.frequency_penalty for p in params) and not any(it.seq.grammar for it in sample_items)
+        greedy_only = self._argmax_only(sample_items)
         if self.tp is not None:
             plan["gather"] = bool(sample_items) and not greedy_only
             self.tp.send_plan(plan)

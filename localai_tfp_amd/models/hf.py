@@ -30,6 +30,7 @@ import os
 from collections import OrderedDict
 
 import numpy as np
+import torch
 
 from ..formats.gguf import QType
 from .config import NEOX_ARCHS, LlamaConfig
@@ -206,7 +207,9 @@ class _SafetensorsDir:
         return k in self.where or bool(self._packed(k))
 
     def raw(self, k):
-        return self._h[self.where[k]].get_tensor(k).numpy()
+        t = self._h[self.where[k]].get_tensor(k)
+        # numpy has no bfloat16: GPTQ / AWQ checkpoints that store scales in bf16 are widened first
+        return (t.float() if t.is_floating_point() and t.dtype != torch.float16 else t).numpy()
 
     def get(self, k) -> np.ndarray:
         if self._packed(k):

@@ -327,6 +327,16 @@ def _qmatmul_t32(W: QWeight, x, epi: int, out, xq, xds, M: int, out_zeroed: bool
     can_split = epi == EPI_ADD_F32 or (epi == EPI_F32 and out_zeroed)
     if W.bf16_cache is not None and M >= dense_min_m(x.dtype, epi, can_split) and W.bf16_cache.dtype == x.dtype:
         return _dense_cached(W, x, epi, out, M)
+    if QMM2 and int(W.qtype) in QMM2_QTYPES and M >= QMM2_MIN_M:
+        wm, ks, splits = _qmm2_shape(M, W.N, W.K, can_split)
+        e = EPI_ADD_F32 if (epi == EPI_F32 and splits > 1) else epi
+        if e in (EPI_BF16, *GLU_EPIS):
+            if out.dtype != x.dtype:
+                raise ValueError(f"qmatmul: {out.dtype} output with {x.dtype} activations")
+            N.ensure_act(out.dtype)
+        N.kcall("mxk_qmm2", int(W.qtype), e, wm, ks, x.data_ptr(), x.stride(0), W.data.data_ptr(), M, W.N, W.K,
+                splits, out.data_ptr(), out.stride(0), N.stream_ptr())
+        return out
     ws = _qmm_ws_shape(M, W.N, W.K, can_split, int(W.qtype))
     if ws is not None:
         cfg, splits = ws
@@ -531,6 +541,39 @@ def _qmm_shape(M: int, N_: int, K: int, can_split: bool):
         while cols * mt * splits < (3 * CU_COUNT) // 4 and (K // 64) // (splits * 2) >= 8:
             splits *= 2
     return wm, wn, nw, ks, splits
+
+
+# qmm2.hip: second-generation quantised GEMM (wave tile = all BM rows x one 32-column group, super-block
+# unrolled k loop, 4-slot LDS-DMA ring) for the Q4_K_M formats. (wm, ks): BM = 32 wm rows, ks = 1 (4 waves)
+# or 2 (8 waves splitting each k-tile's k-steps); 128 columns per workgroup; K split in whole super-blocks.
+QMM2 = os.environ.get("MX_QMM2", "0") != "0"
+QMM2_FORCE: tuple | None = None  # (wm, ks, splits) override for tuning (tools/tune_qmm2.py)
+QMM2_CONFIGS = ((2, 1), (2, 2), (4, 1), (4, 2), (6, 1), (8, 1), (8, 2))
+QMM2_QTYPES = (int(QType.Q4_K), int(QType.Q6_K))
+QMM2_MIN_M = int(os.environ.get("MX_QMM2_MIN_M", "16"))
+
+
+def _qmm2_shape(M: int, N_: int, K: int, can_split: bool):
+    """(wm, ks, splits) for qmm2: the smallest row tile covering M (up to 256 rows per workgroup), then K
+    splits (split-able outputs only) until ~3/4 of the CUs hold a workgroup, >= 2 super-blocks per split."""
+    if QMM2_FORCE is not None:
+        wm, ks, splits = QMM2_FORCE
+        return wm, ks, (splits if can_split else 1)
+    if M <= 64:
+        wm, ks = 2, 2
+    elif M <= 128:
+        wm, ks = 4, 2
+    elif M <= 192:
+        wm, ks = 6, 1
+    else:
+        wm, ks = 8, 1
+    tiles = -(-M // (32 * wm)) * -(-N_ // 128)
+    splits = 1
+    if can_split:
+        nsb = K // 256
+        while tiles * splits < (3 * CU_COUNT) // 4 and nsb // (splits * 2) >= 2:
+            splits *= 2
+    return wm, ks, splits
 
 
 # qmm_ws.hip: warp-specialised variant (4 producer waves: LDS-DMA + dequant into an f16 B tile; 4 MFMA-only

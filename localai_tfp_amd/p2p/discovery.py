@@ -62,6 +62,25 @@ def decode_beacon(data: bytes, token: str, network: str, max_skew: float = 60.0,
         return None
 
 
+_LOCAL_HOSTS = ("", "0.0.0.0", "::", "localhost")
+
+
+def reachable_address(advertised: str, sender_ip: str) -> str:
+    """The address a peer's beacon should be registered under. A node bound to 0.0.0.0 with no
+    LOCALAI_P2P_ADVERTISE advertises a loopback / unspecified host (p2p.self_node); taken literally, every
+    LAN peer would register that worker at ITS OWN loopback and proxy to itself. Such hosts are replaced
+    by the datagram's source IP (the only address known to reach the sender); routable hosts are kept."""
+    host, sep, port = advertised.rpartition(":")
+    if not sep:
+        host, port = advertised, ""
+    h = host.strip("[]")
+    if h in _LOCAL_HOSTS or h.startswith("127.") or h == "::1":
+        if not sender_ip:
+            return advertised
+        return f"{sender_ip}:{port}" if port else sender_ip
+    return advertised
+
+
 class LanDiscovery:
     """Beacon sender + listener for one node (started by p2p.P2PNode when p2p is on)."""
 
@@ -112,12 +131,13 @@ class LanDiscovery:
 
     def poll_once(self) -> NodeData | None:
         try:
-            data, _ = self.rx.recvfrom(4096)
+            data, src = self.rx.recvfrom(4096)
         except (socket.timeout, OSError):
             return None
         node = decode_beacon(data, self.token, self.network)
         if node is None or (self.me is not None and node.id == self.me.id):
             return None
+        node.address = reachable_address(node.address, src[0])
         self.registry.add(node)
         self.received += 1
         return node

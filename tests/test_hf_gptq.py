@@ -73,7 +73,7 @@ def test_gptq_and_awq_dequant_formulas():
     np.testing.assert_array_equal(got, ref.astype(np.float32))
 
 
-@pytest.mark.parametrize("method", ["gptq", "gptq_actorder", "awq"])
+@pytest.mark.parametrize("method", ["gptq", "gptq_actorder", "awq", "gptq_bf16"])
 def test_quantized_hf_dir_matches_transformers(method, tmp_path):
     torch.manual_seed(0)
     T = transformers
@@ -100,7 +100,12 @@ def test_quantized_hf_dir_matches_transformers(method, tmp_path):
         else:
             sd[base + "qweight"] = torch.from_numpy(pack_cols(q, AWQ_ORDER))
             sd[base + "qzeros"] = torch.from_numpy(pack_cols(z, AWQ_ORDER))
-        sd[base + "scales"] = torch.from_numpy(s16)
+        if method == "gptq_bf16":  # scales stored in bf16 (numpy cannot hold them: widened at load)
+            sb = torch.from_numpy(s16).to(torch.bfloat16)
+            sd[base + "scales"] = sb
+            s16 = sb.float().numpy()
+        else:
+            sd[base + "scales"] = torch.from_numpy(s16)
         deq[k] = torch.from_numpy((s16.astype(np.float32)[g_idx] * (q - z[g_idx])).T.astype(np.float32).copy())
     (d / "model.safetensors").unlink()
     save_file(sd, str(d / "model.safetensors"), metadata={"format": "pt"})

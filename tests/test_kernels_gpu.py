@@ -402,7 +402,45 @@ def test_qmm(qt, M, wm, wn, nw, ks, splits, monkeypatch):
     if ks >= 16 and wm == 4 and qt == QType.Q6_K:
         pytest.skip("a Q6_K 128-row stage does not fit a half-LDS ring of 3 k-tiles")
     monkeypatch.setattr(L, "QMM_FORCE", (wm, wn, nw, ks, splits))
+    monkeypatch.setattr(L, "QMM2", False)
     n, k = 416, 2304  # 416 = 3.25 x 128 columns: partial column tiles (multiple of 32 for the GLU)
+    raw, dense = make_w(qt, n, k, seed=M + 7 * wm)
+    W = QWeight.from_ggml(raw, qt, n, k, DEV, t32=True)
+    assert W.to_t32() and W.layout == "t32"
+    x = torch.randn(M, k, device=DEV).half()
+    ref = x.float().cpu() @ dense.t()
+    out = torch.empty(M, n, device=DEV)
+    qmatmul(W, x, EPI_F32, out)
+    assert rel(out, ref) < 5e-3
+    z = torch.zeros(M, n, device=DEV)
+    qmatmul(W, x, EPI_F32, z, out_zeroed=True)
+    assert rel(z, ref) < 5e-3
+    acc = torch.randn(M, n, device=DEV)
+    acc0 = acc.clone()
+    qmatmul(W, x, EPI_ADD_F32, acc)
+    assert rel(acc - acc0, ref) < 5e-3
+    ob = torch.empty(M, n, dtype=torch.float16, device=DEV)
+    qmatmul(W, x, EPI_BF16, ob)
+    assert rel(ob, ref) < 5e-3
+    sw = torch.empty(M, n // 2, dtype=torch.float16, device=DEV)
+    qmatmul(W, x, EPI_SWIGLU, sw)
+    g = ref.reshape(M, n // 32, 2, 16)
+    ref_sw = torch.nn.functional.silu(g[:, :, 0].reshape(M, -1)) * g[:, :, 1].reshape(M, -1)
+    assert rel(sw, ref_sw) < 1e-2
+
+
+@pytest.mark.parametrize("qt", [QType.Q4_K, QType.Q6_K])
+@pytest.mark.parametrize("M,wm,ks,splits", [
+    (64, 2, 1, 1), (64, 2, 2, 3), (17, 2, 2, 1), (128, 4, 2, 1), (77, 4, 2, 2), (128, 4, 1, 4), (200, 6, 1, 1),
+    (256, 8, 1, 1), (300, 8, 1, 3), (256, 8, 2, 2), (511, 8, 1, 1), (100, 2, 1, 5)])
+def test_qmm2(qt, M, wm, ks, splits, monkeypatch):
+    """qmm2.hip for every epilogue and tile / split-K choice, incl. ragged M / N tails (416 columns = 3.25
+    workgroup tiles), split counts that do not divide the super-blocks and the 8-wave k-step split (ks = 2),
+    against the fp32 product of the dequantised weight."""
+    from localai_tfp_amd.ops import linear as L
+    monkeypatch.setattr(L, "QMM2", True)
+    monkeypatch.setattr(L, "QMM2_FORCE", (wm, ks, splits))
+    n, k = 416, 2304
     raw, dense = make_w(qt, n, k, seed=M + 7 * wm)
     W = QWeight.from_ggml(raw, qt, n, k, DEV, t32=True)
     assert W.to_t32() and W.layout == "t32"

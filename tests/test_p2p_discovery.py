@@ -53,3 +53,33 @@ def test_p2p_node_starts_discovery_with_token():
     finally:
         n.stop()
     assert P2PNode("", "", [], None, lan_discovery=True).discovery is None  # no token: no beacons
+
+
+def test_loopback_advertisement_replaced_by_sender_ip():
+    """A node bound to 0.0.0.0 without LOCALAI_P2P_ADVERTISE advertises 127.0.0.1:<port>; the receiver must
+    register it at the datagram's source address, never at its own loopback (which would proxy to itself)."""
+    from localai_tfp_amd.p2p.discovery import reachable_address
+    assert reachable_address("127.0.0.1:8080", "10.1.2.3") == "10.1.2.3:8080"
+    assert reachable_address("0.0.0.0:8080", "10.1.2.3") == "10.1.2.3:8080"
+    assert reachable_address("localhost:9", "10.1.2.3") == "10.1.2.3:9"
+    assert reachable_address("[::1]:9", "10.1.2.3") == "10.1.2.3:9"
+    assert reachable_address("10.0.0.7:8080", "10.1.2.3") == "10.0.0.7:8080"  # routable: kept
+    assert reachable_address("node-b.lan:8080", "10.1.2.3") == "node-b.lan:8080"
+    # over the wire: the advertised host differs from the sender's address
+    ra = Registry("tok")
+    a = LanDiscovery(ra, NodeData(id="A", address="10.9.9.9:1", service=FEDERATED_ID), "tok", port=0,
+                     bind_host="127.0.0.1")
+    b = LanDiscovery(Registry("tok"), NodeData(id="B", address="0.0.0.0:2222", service=FEDERATED_ID), "tok",
+                     port=0, bind_host="127.0.0.1")
+    try:
+        b.targets = [("127.0.0.1", a.port)]
+        assert b.beacon_once() == 1
+        deadline = time.time() + 5
+        node = None
+        while node is None and time.time() < deadline:
+            node = a.poll_once()
+        assert node is not None and node.address == "127.0.0.1:2222"  # the sender's IP, its advertised port
+        assert ra.get(FEDERATED_ID, "B").address == "127.0.0.1:2222"
+    finally:
+        a.stop()
+        b.stop()

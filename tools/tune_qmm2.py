@@ -1,9 +1,10 @@
 #!/usr/bin/env python3
-"""Every compiled qmm.hip configuration x split-K on the Llama-3-8B projections, each checked against an
-fp32 reference of the same quantised weights (SwiGLU epilogue included), against the dense f16 hipBLASLt
-path. One JSON line per (shape, M, config) with "kind": "cfg", and one summary line per (shape, M).
+"""qmm2.hip sweep on the Llama-3-8B projections: every compiled (wm, ks) x split choice against the
+round-3 qmm.hip default and hipBLASLt on a dense f16 copy of the same weights, all in ONE process,
+interleaved, on the same random data. Every qmm2 configuration is checked against the fp32 product of the
+dequantised weights (rel. Frobenius error) so a fast-but-wrong tile cannot win. One JSON line per (shape, M).
 
-    MS=128,256,384,2048 SHAPES=gate_up,down python tools/tune_qmm2.py > gpurun_out/tune_qmm2.jsonl
+    MS=128,256 SHAPES=gate_up,down python tools/tune_qmm2.py > gpurun_out/tune_qmm2.jsonl
 """
 from __future__ import annotations
 
@@ -13,12 +14,13 @@ import sys
 
 import numpy as np
 import torch
-import torch.nn.functional as F
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def main():
+    from localai_tfp_amd import _build
+    _build.build_all()
     from localai_tfp_amd.formats.gguf import QType
     from localai_tfp_amd.ops import linear as L
     from localai_tfp_amd.ops.quant import random_quantized
@@ -29,14 +31,12 @@ def main():
     only = os.environ.get("SHAPES")
     if only:
         shapes = [s for s in shapes if s[0] in only.split(",")]
-    Ms = [int(m) for m in os.environ.get("MS", "128,256,384,2048").split(",")]
-    cfg_filter = os.environ.get("CFGS")  # e.g. "2.2.2.33,4.2.2.33"
-    cfgs_all = list(L.QMM_CONFIGS)
-    if cfg_filter:
-        cfgs_all = [tuple(int(v) for v in c.split(".")) for c in cfg_filter.split(",")]
+    Ms = [int(m) for m in os.environ.get("MS", "64,128,256,512,2048").split(",")]
+    full = os.environ.get("FULL", "1") == "1"
+    rounds = int(os.environ.get("ROUNDS", "3"))
 
     def bench(fn, it=20):
-        for _ in range(3):
+        for _ in range(2):
             fn()
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -50,57 +50,85 @@ def main():
     for name, N, K, qt, epi in shapes:
         raw = random_quantized(np.random.default_rng(1), int(qt), N, K)
         Wt = L.QWeight.from_ggml(raw, int(qt), N, K, dev)
-        wf = Wt.dequant_gpu(torch.float32)  # ggml-layout dequant (the oracle) before tiling
         assert Wt.to_t32()
+        dense = Wt.dequant_gpu(torch.float16)
         can_split = epi in (L.EPI_F32, L.EPI_ADD_F32)
         for M in Ms:
             x = (torch.randn(M, K, device=dev) * 0.5).half()
-            y = x.float() @ wf.t()
             if epi == L.EPI_SWIGLU:
-                v = y.reshape(M, N // 32, 2, 16)
-                ref = (F.silu(v[:, :, 0]) * v[:, :, 1]).reshape(M, N // 2)
                 out = torch.empty(M, N // 2, device=dev, dtype=torch.float16)
             else:
-                ref = y
                 out = torch.zeros(M, N, device=dev, dtype=torch.float32)
-            res = {"kind": "shape", "shape": name, "M": M}
-            res["auto_cfg"] = list(L._qmm_shape(M, N, K, can_split))
-            res["auto_us"] = round(bench(lambda: L.qmatmul(Wt, x, epi, out, out_zeroed=True)), 2)
-            best = None
-            for c in cfgs_all:
-                for sp in ((1, 2, 4) if can_split else (1,)):
-                    L.QMM_FORCE = (*c, sp)
-                    try:
-                        out.zero_()
-                        L.qmatmul(Wt, x, epi, out, out_zeroed=True)
-                        torch.cuda.synchronize()
-                    except Exception as ex:  # configuration not compiled / does not fit this format
-                        L.QMM_FORCE = None
-                        print(json.dumps({"kind": "cfg", "shape": name, "M": M, "cfg": [*c, sp], "error": str(ex)[:80]}))
-                        continue
-                    err = float((out.float() - ref).norm() / ref.norm())
-                    us = bench(lambda: L.qmatmul(Wt, x, epi, out, out_zeroed=True))
-                    L.QMM_FORCE = None
-                    print(json.dumps({"kind": "cfg", "shape": name, "M": M, "cfg": [*c, sp], "us": round(us, 2),
-                                      "tflops": round(2 * M * N * K / us / 1e6, 1), "rel_err": round(err, 5)}), flush=True)
-                    if err < 2e-2 and (best is None or us < best[0]):
-                        best = (us, [*c, sp])
-            if best:
-                res["best_us"], res["best_cfg"] = round(best[0], 2), best[1]
-                res["best_tflops"] = round(2 * M * N * K / best[0] / 1e6, 1)
-            cache = Wt.dequant_gpu(torch.float16) if False else None
-            wd = wf.half()
+            yref = x.float() @ dense.float().t()
             if epi == L.EPI_SWIGLU:
-                fn = lambda: torch.matmul(x, wd.t())
+                v = yref.reshape(M, N // 32, 2, 16)
+                ref = (torch.nn.functional.silu(v[:, :, 0]) * v[:, :, 1]).reshape(M, N // 2)
             else:
-                fn = lambda: torch.addmm(out, x, wd.t(), out_dtype=torch.float32, out=out) if epi == L.EPI_ADD_F32 \
-                    else torch.mm(x, wd.t(), out_dtype=torch.float32, out=out)
-            try:
-                res["dense_us"] = round(bench(fn), 2)
-            except Exception:
-                res["dense_us"] = round(bench(lambda: torch.matmul(x, wd.t())), 2)
-            del wd
+                ref = yref
+
+            def err():
+                if epi == L.EPI_ADD_F32:
+                    out.zero_()
+                elif epi == L.EPI_F32:
+                    out.zero_()
+                L.qmatmul(Wt, x, epi, out, out_zeroed=True)
+                torch.cuda.synchronize()
+                return float((out.float() - ref).norm() / ref.norm())
+
+            cands = {}
+
+            def run_old():
+                L.QMM2 = False
+                L.qmatmul(Wt, x, epi, out, out_zeroed=True)
+                L.QMM2 = True
+
+            cands["qmm_r3"] = run_old
+            if epi == L.EPI_SWIGLU:
+                cands["dense_f16"] = lambda: L._dense_cached(_DW(dense), x, epi, out, M)
+            elif epi == L.EPI_ADD_F32:
+                cands["dense_f16"] = lambda: torch.addmm(out, x, dense.t(), out_dtype=torch.float32, out=out)
+            else:
+                cands["dense_f16"] = lambda: torch.mm(x, dense.t(), out_dtype=torch.float32, out=out)
+            L.QMM2_FORCE = None
+            auto = L._qmm2_shape(M, N, K, can_split)
+            cfgs = [(*c, sp) for c in L.QMM2_CONFIGS for sp in ((1, 2, 4, 8) if can_split else (1,))] if full else []
+            errs = {}
+            for cfg in [auto] + cfgs:
+                L.QMM2_FORCE = cfg
+                e = err()
+                errs[str(list(cfg))] = round(e, 6)
+
+                def mk(c):
+                    def f():
+                        L.QMM2_FORCE = c
+                        L.qmatmul(Wt, x, epi, out, out_zeroed=True)
+                    return f
+                cands["qmm2" + str(list(cfg))] = mk(cfg)
+            L.QMM2_FORCE = None
+            times = {k: [] for k in cands}
+            for _ in range(rounds):
+                for k, f in cands.items():
+                    times[k].append(bench(f))
+            res = {"shape": name, "M": M, "auto": list(auto)}
+            med = {k: float(np.median(v)) for k, v in times.items()}
+            res["qmm_r3_us"] = round(med.pop("qmm_r3"), 2)
+            res["dense_f16_us"] = round(med.pop("dense_f16"), 2)
+            res["qmm2_auto_us"] = round(med["qmm2" + str(list(auto))], 2)
+            best = min(med, key=med.get)
+            res["qmm2_best"] = [best[4:], round(med[best], 2)]
+            flops = 2.0 * M * N * K
+            res["qmm2_auto_tflops"] = round(flops / (res["qmm2_auto_us"] * 1e-6) / 1e12, 1)
+            res["max_rel_err"] = max(errs.values())
+            res["auto_rel_err"] = errs[str(list(auto))]
+            if os.environ.get("VERBOSE"):
+                res["all"] = {k[4:]: round(v, 2) for k, v in med.items()}
             print(json.dumps(res), flush=True)
+
+
+class _DW:
+    def __init__(self, dense):
+        self.bf16_cache = dense
+        self.N = dense.shape[0]
 
 
 if __name__ == "__main__":
