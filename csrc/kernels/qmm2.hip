@@ -156,7 +156,8 @@ MX_DEV void q2_wait_barrier() {
     asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N_) : "memory");
 }
 
-template <int QT, int WM, int KS, int EPI>
+// DBG (isolation builds, tools/prof_qmm.py --q2dbg): 1 no MFMA, 2 no dequant VALU, 4 no A loads, 8 no weight loads
+template <int QT, int WM, int KS, int EPI, int DBG = 0>
 __global__ __launch_bounds__(256 * KS) void qmm2_kernel(const uint16_t* __restrict__ A, int lda,
                                                         const uint8_t* __restrict__ W, int M, int N, int K,
                                                         int n_mt, int splits, int sbps, void* __restrict__ Cv,
@@ -168,6 +169,11 @@ __global__ __launch_bounds__(256 * KS) void qmm2_kernel(const uint16_t* __restri
     static_assert(G::LDS <= 160 * 1024, "LDS");
     static_assert(G::template cnt<1, true>() + G::template cnt<2, true>() <= 63 &&
                   G::template cnt<0, true>() + G::template cnt<1, true>() <= 63, "vmcnt range");
+    // LDS-DMA instructions per stage as issued (the isolation builds drop some)
+    constexpr int WAI = (DBG & 4) ? 0 : WA, QII = (DBG & 8) ? 0 : F::QI, HII = (DBG & 8) ? 0 : F::HI;
+    auto cnt = [](auto jq_c, auto wl_c) constexpr {
+        return WAI + (decltype(wl_c)::value ? QII + (decltype(jq_c)::value == 0 ? HII : 0) : 0);
+    };
     extern __shared__ __attribute__((aligned(16))) char smem[];
     char* const hdr_lds = smem + Q2_NS * STAGE;
 
@@ -217,10 +223,10 @@ __global__ __launch_bounds__(256 * KS) void qmm2_kernel(const uint16_t* __restri
         char* sb = smem + JQ * STAGE;
         const uint16_t* ak = A + (size_t)kta * 64;
 #pragma unroll
-        for (int i = 0; i < WA; ++i)
+        for (int i = 0; i < WAI; ++i)
             __builtin_amdgcn_global_load_lds((const void*)(ak + aoff[i]), (MX_LDS void*)(sb + (wave * WA + i) * 1024),
                                              16, 0, 0);
-        if constexpr (decltype(wl_c)::value) {
+        if constexpr (decltype(wl_c)::value && QII > 0) {
             const uint8_t* u = wg + (size_t)sbw * F::UNIT;
             const uint8_t* qs = u + F::QOFF + JQ * F::QB;
             char* qd = sb + A_BYTES + cg * F::QB;
@@ -261,7 +267,7 @@ __global__ __launch_bounds__(256 * KS) void qmm2_kernel(const uint16_t* __restri
         issue(kt0, sb0, sb0 & 1, I0{}, WLc{});
         issue(kt0 + 1, sb0, 0, I1{}, WLc{});
         issue(kt0 + 2, sb0, 0, I2{}, WLc{});
-        q2_wait_barrier<G::template cnt<1, WL>() + G::template cnt<2, WL>()>();
+        q2_wait_barrier<cnt(I1{}, WLc{}) + cnt(I2{}, WLc{})>();
 
         Q2B<QT> bw;
         f16x8 af[2][WM];
@@ -278,7 +284,7 @@ __global__ __launch_bounds__(256 * KS) void qmm2_kernel(const uint16_t* __restri
             constexpr int NJ = (JQ + 1) & 3;
             const int kt = sb * 4 + JQ;
             // stage kt+1 landed (only stage kt+2 may still be in flight); every wave is past tile kt-1
-            q2_wait_barrier<G::template cnt<(JQ + 2) & 3, WL>()>();
+            q2_wait_barrier<cnt(std::integral_constant<int, (JQ + 2) & 3>{}, WLc{})>();
             {
                 const int ki = kt + 3;
                 const bool real = ki < kt1;
@@ -304,14 +310,22 @@ __global__ __launch_bounds__(256 * KS) void qmm2_kernel(const uint16_t* __restri
                     bn.load_q(smem + NJ * STAGE + b_rd, col, h);
                 }
                 f16x8 bf;
-                switch (S) {
-                    case 0: bf = bw.template frag<0>(); break;
-                    case 1: bf = bw.template frag<1>(); break;
-                    case 2: bf = bw.template frag<2>(); break;
-                    default: bf = bw.template frag<3>(); break;
+                if constexpr (DBG & 2) {
+                    const u32x2 r2 = (S & 1) ? bw.v1 : bw.v0;
+                    bf = __builtin_bit_cast(f16x8, (u32x4){r2[0], r2[1], r2[0] ^ (uint32_t)S, r2[1]});
+                } else {
+                    switch (S) {
+                        case 0: bf = bw.template frag<0>(); break;
+                        case 1: bf = bw.template frag<1>(); break;
+                        case 2: bf = bw.template frag<2>(); break;
+                        default: bf = bw.template frag<3>(); break;
+                    }
                 }
 #pragma unroll
-                for (int i = 0; i < WM; ++i) acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[cur][i], bf, acc[i], 0, 0, 0);
+                for (int i = 0; i < WM; ++i) {
+                    if constexpr (DBG & 1) asm volatile("" ::"v"(af[cur][i]), "v"(bf));
+                    else acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[cur][i], bf, acc[i], 0, 0, 0);
+                }
             }
             // NSTEP is even: the next tile's first fragments are in af[0]
             bw = bn;
@@ -439,7 +453,38 @@ static int dispatch_qmm2(int wm, int ks, const uint16_t* A, int lda, const uint8
     return (int)hipErrorInvalidValue;
 }
 
+template <int DBG>
+static int launch_dbg(int wm, const uint16_t* A, int lda, const uint8_t* W, int M, int N, int K, void* C, int ldc,
+                      hipStream_t st) {
+    constexpr int QT = MXQ_Q4_K, EPI = E16_SWIGLU;
+    auto go = [&](auto kern, int bm, int ks, int lds) {
+        (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+        const int n_ct = (N + 127) / 128, n_mt = (M + bm - 1) / bm;
+        kern<<<dim3(n_ct * n_mt), 256 * ks, lds, st>>>(A, lda, W, M, N, K, n_mt, 1, K >> 8, C, ldc);
+        return (int)hipGetLastError();
+    };
+    if (wm == 8) return go(qmm2_kernel<QT, 8, 1, EPI, DBG>, 256, 1, Q2Geom<QT, 8, 1>::LDS);
+    if (wm == 4) return go(qmm2_kernel<QT, 4, 2, EPI, DBG>, 128, 2, Q2Geom<QT, 4, 2>::LDS);
+    return (int)hipErrorInvalidValue;
+}
+
 }  // namespace
+
+// isolation builds of the Q4_K SwiGLU kernel (wm 8 / ks 1 and wm 4 / ks 2, no split), see DBG above
+extern "C" int mxk_qmm2_dbg(int dbg, int wm, const uint16_t* A, int lda, const uint8_t* W, int M, int N, int K, void* C,
+                            int ldc, hipStream_t st) {
+    switch (dbg) {
+        case 0: return launch_dbg<0>(wm, A, lda, W, M, N, K, C, ldc, st);
+        case 1: return launch_dbg<1>(wm, A, lda, W, M, N, K, C, ldc, st);
+        case 2: return launch_dbg<2>(wm, A, lda, W, M, N, K, C, ldc, st);
+        case 3: return launch_dbg<3>(wm, A, lda, W, M, N, K, C, ldc, st);
+        case 4: return launch_dbg<4>(wm, A, lda, W, M, N, K, C, ldc, st);
+        case 8: return launch_dbg<8>(wm, A, lda, W, M, N, K, C, ldc, st);
+        case 12: return launch_dbg<12>(wm, A, lda, W, M, N, K, C, ldc, st);
+        case 15: return launch_dbg<15>(wm, A, lda, W, M, N, K, C, ldc, st);
+    }
+    return (int)hipErrorInvalidValue;
+}
 
 // A f16 [M, K] (lda % 8 == 0, 16-B aligned), W t32 Q4_K / Q6_K [N, K] (N % 32 == 0, K % 256 == 0).
 // epi: 0 fp32 store, 1 f16 store, 2 fp32 accumulate (split-K via atomics when splits > 1), 3/4 SwiGLU /

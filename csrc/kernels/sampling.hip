@@ -412,14 +412,28 @@ extern "C" int mxk_sample(float* logits, int ld, int B, int V, const SampleParam
 
 extern "C" int mxk_sample_params_size() { return (int)sizeof(SampleParams); }
 
-// ---- small batches with top-k on: the vocabulary split over many workgroups ----------------------------
-// One workgroup per row reads the 128k-entry row from one CU (~0.2 ms at batch 1). With top-k <= TK_CAP on,
-// every quantity the chain needs lives in the global top-k set (top-p's target is top_p x the top-k mass,
-// min-p is relative to the max), and the global top-k is contained in the union of per-slice top-ks:
-//   tk_slice_kernel  (B x S workgroups): slice max, slice histogram, gather + sort the slice's top-k
-//   tk_merge_kernel  (B workgroups):     merge the S x k candidates, truncate exactly, Gumbel-max draw.
-constexpr int TK_CAP = 64, TK_NT = 256, TK_HB = 1024;
-constexpr float TK_HR = 48.f;
+// ---- top-k on (the reference default, top_k 40): the vocabulary split over B x S workgroups -------------
+// One workgroup per row (sample_kernel) reads the 128k-entry row from one CU and builds an LDS histogram
+// whose hot bins serialise on atomics (227 us at 128 rows). With top-k <= TK_CAP on, every quantity the
+// chain needs lives in the global top-k set (top-p's target is top_p x the top-k mass, min-p is relative to
+// the max), and the global top-k set is contained in the union of the per-slice top-k sets:
+//   tk_slice_kernel (B x S workgroups of 256): the slice (NV values per thread) is held in registers as
+//     order-preserving integer keys; the slice's K-th largest key is found by bisection on the key axis
+//     with register counts + one block reduction per step (no atomics, no re-reads), stopping as soon as
+//     the kept set fits; the candidates (>= that key) are written unsorted, with an overflow flag when
+//     exact ties exceed the capacity;
+//   tk_merge_kernel (B workgroups of 1024): the S x <= TK_CAPS candidates in registers, the same exact
+//     bisection for the global K-th value, the kept set sorted in LDS, exact truncation, Gumbel-max draw.
+//     A row whose slices overflowed falls back to the full-row bisection chain (sample_row_bisect).
+constexpr int TK_CAP = 64, TK_NT = 256, TK_NV = 16, TK_CAPS = 2 * TK_CAP, TK_MNT = 1024, TK_MV = 8;
+constexpr int TK_SLICE = TK_NT * TK_NV;  // vocabulary entries per slice
+constexpr float TK_HR = 48.f;            // values more than this below the slice max are never candidates
+
+MX_DEV uint32_t ord_key(float v) {  // order-preserving float -> uint (NaN / -inf / masked -> 0)
+    if (!(v > -INFINITY)) return 0u;
+    const uint32_t b = __float_as_uint(v);
+    return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
 
 __global__ __launch_bounds__(TK_NT) void tk_penalty_kernel(float* logits, int ld, int V, const SampleParams* params,
                                                           const int* pen_tok, const int* pen_cnt, const float* pen_bias) {
@@ -439,131 +453,196 @@ __global__ __launch_bounds__(TK_NT) void tk_penalty_kernel(float* logits, int ld
     }
 }
 
+// block-wide count of keys >= t over NV registers per thread; `red` double-buffered by the caller's parity
+template <int NT, int NV>
+MX_DEV int tk_count(const uint32_t (&u)[NV], uint32_t t, int* red, int par) {
+    int c = 0;
+#pragma unroll
+    for (int j = 0; j < NV; ++j) c += u[j] >= t ? 1 : 0;
+    c = wave_sum_i(c);
+    if ((threadIdx.x & 63) == 0) red[par * (NT / 64) + (threadIdx.x >> 6)] = c;
+    __syncthreads();
+    int s = 0;
+#pragma unroll
+    for (int w = 0; w < NT / 64; ++w) s += red[par * (NT / 64) + w];
+    return s;
+}
+
+// largest key T with count(keys >= T) >= K, searched in [lo, hi) (count(>= lo) known = c_lo >= K,
+// count(>= hi) < K). exact = false: stop as soon as count(>= T) <= cap (a superset of the top-K set that
+// fits); exact = true: stop only at the K-th key itself (or when count(>= T) == K, which is the same set).
+template <int NT, int NV>
+MX_DEV uint32_t tk_bisect(const uint32_t (&u)[NV], int K, uint32_t lo, uint32_t hi, int& c_lo, int cap, bool exact,
+                          int* red, int par) {
+    while (hi - lo > 1u) {
+        if (exact ? c_lo == K : c_lo <= cap) break;
+        const uint32_t mid = lo + ((hi - lo) >> 1);
+        const int c = tk_count<NT, NV>(u, mid, red, par);
+        par ^= 1;
+        if (c >= K) { lo = mid; c_lo = c; }
+        else hi = mid;
+    }
+    return lo;
+}
+
 __global__ __launch_bounds__(TK_NT) void tk_slice_kernel(const float* __restrict__ logits, int ld, int V,
                                                         const SampleParams* __restrict__ params,
                                                         const uint32_t* __restrict__ allow_mask, int mask_ld,
                                                         float* __restrict__ cand_v, int* __restrict__ cand_i,
                                                         int* __restrict__ cand_n, float2* __restrict__ slice_z) {
-    __shared__ float red[TK_NT / 64], zred[TK_NT / 64];
-    __shared__ unsigned hcnt[TK_HB];
-    __shared__ float cv[2 * TK_CAP * 4];
-    __shared__ int ci[2 * TK_CAP * 4];
-    __shared__ int s_n, s_bin;
+    __shared__ float fred[2 * TK_NT / 64];
+    __shared__ int red[2 * TK_NT / 64];
+    __shared__ int s_n;
     const int row = blockIdx.x, S = gridDim.y, sl = blockIdx.y;
     const SampleParams P = params[row];
     const int K = P.temperature <= 0.f ? 1 : min(P.top_k, TK_CAP);
     const float itemp = P.temperature <= 0.f ? 1.f : 1.f / P.temperature;
     const float* x = logits + (size_t)row * ld;
     const uint32_t* am = allow_mask ? allow_mask + (size_t)row * mask_ld : nullptr;
-    const int L = (V + S - 1) / S, i0 = sl * L, i1 = min(V, i0 + L);
-    auto val = [&](int i) -> float {
-        if (am && !((am[i >> 5] >> (i & 31)) & 1u)) return -INFINITY;
-        return x[i] * itemp;
-    };
+    const int i0 = sl * TK_SLICE, i1 = min(V, i0 + TK_SLICE);
+    float v[TK_NV];
+    uint32_t u[TK_NV];
     float mx = -INFINITY;
-    for (int i = i0 + threadIdx.x; i < i1; i += TK_NT) mx = fmaxf(mx, val(i));
+#pragma unroll
+    for (int j = 0; j < TK_NV; ++j) {
+        const int i = i0 + j * TK_NT + threadIdx.x;
+        float t = -INFINITY;
+        if (i < i1) {
+            t = __builtin_nontemporal_load(x + i) * itemp;
+            if (am && !((am[i >> 5] >> (i & 31)) & 1u)) t = -INFINITY;
+        }
+        v[j] = t;
+        mx = fmaxf(mx, t);
+    }
     mx = wave_max(mx);
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
-    for (int b = threadIdx.x; b < TK_HB; b += TK_NT) hcnt[b] = 0u;
+    if ((threadIdx.x & 63) == 0) fred[threadIdx.x >> 6] = mx;
+    if (threadIdx.x == 0) s_n = 0;
     __syncthreads();
-    mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-    constexpr float IBW = (float)TK_HB / TK_HR, BW = TK_HR / (float)TK_HB;
-    float zs = 0.f;  // the slice's share of the row's partition function (greedy rows report log-softmax)
-    for (int i = i0 + threadIdx.x; i < i1; i += TK_NT) {
-        const float v = val(i);
-        if (!(v > -INFINITY)) continue;  // masked (and NaN)
-        zs += __expf(v - mx);
-        atomicAdd(&hcnt[(int)fminf((float)(TK_HB - 1), (mx - v) * IBW)], 1u);
+#pragma unroll
+    for (int w = 0; w < TK_NT / 64; ++w) mx = fmaxf(mx, fred[w]);
+    float zs = 0.f;  // the slice's share of the row's partition function (log-probs of greedy rows)
+#pragma unroll
+    for (int j = 0; j < TK_NV; ++j) {
+        u[j] = ord_key(v[j]);
+        if (v[j] > -INFINITY) zs += __expf(v[j] - mx);
     }
     zs = wave_sum(zs);
-    if ((threadIdx.x & 63) == 0) zred[threadIdx.x >> 6] = zs;
-    __syncthreads();
-    if (threadIdx.x == 0) slice_z[row * S + sl] = make_float2(mx, zred[0] + zred[1] + zred[2] + zred[3]);
+    if ((threadIdx.x & 63) == 0) fred[TK_NT / 64 + (threadIdx.x >> 6)] = zs;
+    // bisection window: [key(mx - TK_HR), key(mx) + 1)
+    uint32_t lo = mx > -INFINITY ? ord_key(mx - TK_HR) : 0u;
+    const uint32_t hi = mx > -INFINITY ? ord_key(mx) + 1u : 1u;
+    int c_lo = tk_count<TK_NT, TK_NV>(u, lo, red, 0);
+    if (c_lo >= K) lo = tk_bisect<TK_NT, TK_NV>(u, K, lo, hi, c_lo, TK_CAPS, false, red, 1);
+    // (fewer than K entries within TK_HR of the slice max: all of them are candidates)
     if (threadIdx.x == 0) {
-        unsigned c = 0;
-        int b = 0;
-        for (; b < TK_HB - 1; ++b) {
-            c += hcnt[b];
-            if (c >= (unsigned)K) break;
-        }
-        s_bin = b;
-        s_n = 0;
+        float z = 0.f;
+#pragma unroll
+        for (int w = 0; w < TK_NT / 64; ++w) z += fred[TK_NT / 64 + w];
+        slice_z[row * S + sl] = make_float2(mx, z);
     }
-    __syncthreads();
-    // fewer than K entries within TK_HR of the slice max (a sparse allow mask): take every entry
-    const float cut = s_bin == TK_HB - 1 ? -INFINITY : mx - ((float)s_bin + 1.01f) * BW;
-    constexpr int CAPL = 2 * TK_CAP * 4;
-    for (int i = i0 + threadIdx.x; i < i1; i += TK_NT) {
-        const float v = val(i);
-        if (v == -INFINITY || !(v > cut || v == mx)) continue;  // (an all-masked slice gathers nothing)
-        const int k = atomicAdd(&s_n, 1);
-        if (k < CAPL) { cv[k] = v; ci[k] = i; }
-    }
-    __syncthreads();
-    const int n = min(s_n, CAPL);  // a bin holding > CAPL - K entries: the first CAPL are kept (exactly
-                                   // representable ties beyond are the only loss; the histogram bins are
-                                   // 0.047 logits wide)
-    int np = 1;
-    while (np < n) np <<= 1;
-    for (int k = n + threadIdx.x; k < np; k += TK_NT) { cv[k] = -INFINITY; ci[k] = 0x7fffffff; }
-    __syncthreads();
-    for (int size = 2; size <= np; size <<= 1) {
-        for (int stride = size >> 1; stride > 0; stride >>= 1) {
-            for (int t = threadIdx.x; t < np / 2; t += TK_NT) {
-                const int lo = 2 * t - (t & (stride - 1)), hi = lo + stride;
-                const bool desc = (lo & size) == 0;
-                const float a = cv[lo], bb = cv[hi];
-                const int ia = ci[lo], ib = ci[hi];
-                const bool a_first = a > bb || (a == bb && ia < ib);
-                if (a_first != desc) { cv[lo] = bb; cv[hi] = a; ci[lo] = ib; ci[hi] = ia; }
+    const size_t base = ((size_t)row * S + sl) * TK_CAPS;
+#pragma unroll
+    for (int j = 0; j < TK_NV; ++j) {
+        if (u[j] >= lo && u[j] != 0u) {
+            const int k = atomicAdd(&s_n, 1);
+            if (k < TK_CAPS) {
+                cand_v[base + k] = v[j];
+                cand_i[base + k] = i0 + j * TK_NT + threadIdx.x;
             }
-            __syncthreads();
         }
     }
-    // this slice's top-K plus every entry tied with its K-th value (top-k keeps ties)
-    int keep = min(n, K);
-    if (keep > 0) while (keep < n && keep < 2 * K && cv[keep] == cv[keep - 1]) ++keep;
-    const size_t base = ((size_t)row * S + sl) * (2 * TK_CAP);
-    for (int k = threadIdx.x; k < keep; k += TK_NT) { cand_v[base + k] = cv[k]; cand_i[base + k] = ci[k]; }
-    if (threadIdx.x == 0) cand_n[row * S + sl] = keep;
+    __syncthreads();
+    if (threadIdx.x == 0) cand_n[row * S + sl] = s_n > TK_CAPS ? (TK_CAPS | (1 << 30)) : s_n;  // bit 30: ties overflowed
 }
 
-__global__ __launch_bounds__(1024) void tk_merge_kernel(const float* __restrict__ logits, int ld,
-                                                       const SampleParams* __restrict__ params, int S,
-                                                       const float* __restrict__ cand_v, const int* __restrict__ cand_i,
-                                                       const int* __restrict__ cand_n, const float2* __restrict__ slice_z,
-                                                       int* __restrict__ out_tok, float* __restrict__ out_logp) {
-    constexpr int CAP = 4096;
-    __shared__ float cv[CAP];
-    __shared__ int ci[CAP];
-    __shared__ int s_off[65], s_keep;
-    __shared__ float red[16], rv[16];
-    __shared__ int ri[16];
+__global__ __launch_bounds__(TK_MNT) void tk_merge_kernel(float* __restrict__ logits, int ld, int V,
+                                                         const SampleParams* __restrict__ params, int S,
+                                                         const uint32_t* __restrict__ allow_mask, int mask_ld,
+                                                         const float* __restrict__ cand_v, const int* __restrict__ cand_i,
+                                                         const int* __restrict__ cand_n, const float2* __restrict__ slice_z,
+                                                         int* __restrict__ out_tok, float* __restrict__ out_logp) {
+    constexpr int KC = 256;  // kept-set capacity (top-k <= 64 plus exact ties)
+    __shared__ float cv[KC];
+    __shared__ int ci[KC];
+    __shared__ int s_off[65], s_keep, s_n, s_ovf;
+    __shared__ float red[2 * TK_MNT / 64], rv[TK_MNT / 64];
+    __shared__ int ired[2 * TK_MNT / 64], ri[TK_MNT / 64];
     const int row = blockIdx.x;
     const SampleParams P = params[row];
     const bool greedy = P.temperature <= 0.f;
     const int K = greedy ? 1 : min(P.top_k, TK_CAP);
     if (threadIdx.x == 0) {
-        int o = 0;
-        for (int s = 0; s < S; ++s) { s_off[s] = o; o += cand_n[row * S + s]; }
-        s_off[S] = min(o, CAP);
+        int o = 0, ovf = 0;
+        for (int s = 0; s < S; ++s) {
+            const int c = cand_n[row * S + s];
+            ovf |= c >> 30;
+            s_off[s] = o;
+            o += c & 0xFFFF;
+        }
+        s_off[S] = o;
+        s_ovf = ovf;
+        s_n = 0;
     }
     __syncthreads();
+    if (s_ovf) {  // exact ties beyond a slice's capacity (flat / degenerate rows): the full-row chain
+        float* x = logits + (size_t)row * ld;
+        const uint32_t* am = allow_mask ? allow_mask + (size_t)row * mask_ld : nullptr;
+        sample_row_bisect(x, V, P, am, row, out_tok, out_logp, red, rv, ri);
+        return;
+    }
     const int n = s_off[S];
-    for (int s = 0; s < S; ++s) {
-        const int c = min(cand_n[row * S + s], CAP - s_off[s]);
-        for (int k = threadIdx.x; k < c; k += 1024) {
-            cv[s_off[s] + k] = cand_v[((size_t)row * S + s) * (2 * TK_CAP) + k];
-            ci[s_off[s] + k] = cand_i[((size_t)row * S + s) * (2 * TK_CAP) + k];
+    // candidate t (concatenated over slices) -> registers
+    float v[TK_MV];
+    int id[TK_MV];
+    uint32_t u[TK_MV];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < TK_MV; ++j) {
+        const int t = j * TK_MNT + threadIdx.x;
+        v[j] = -INFINITY;
+        id[j] = 0x7fffffff;
+        if (t < n) {
+            int s = 0;
+            while (s + 1 < S && s_off[s + 1] <= t) ++s;  // S <= 64
+            const size_t src = ((size_t)row * S + s) * TK_CAPS + (t - s_off[s]);
+            v[j] = cand_v[src];
+            id[j] = cand_i[src];
+        }
+        u[j] = ord_key(v[j]);
+        mx = fmaxf(mx, v[j]);
+    }
+    mx = wave_max(mx);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
+    __syncthreads();
+    mx = -INFINITY;
+#pragma unroll
+    for (int w = 0; w < TK_MNT / 64; ++w) mx = fmaxf(mx, red[w]);
+    // exact global top-K (ties at the K-th value kept)
+    int c_lo = tk_count<TK_MNT, TK_MV>(u, 1u, ired, 0);
+    uint32_t T = 1u;
+    if (c_lo > K) T = tk_bisect<TK_MNT, TK_MV>(u, K, 1u, ord_key(mx) + 1u, c_lo, 0, true, ired, 1);
+#pragma unroll
+    for (int j = 0; j < TK_MV; ++j) {
+        if (u[j] >= T && u[j] != 0u) {
+            const int k = atomicAdd(&s_n, 1);
+            if (k < KC) { cv[k] = v[j]; ci[k] = id[j]; }
         }
     }
+    __syncthreads();
+    if (s_n > KC) {  // more exact ties at the K-th value than the kept-set buffer holds
+        float* x = logits + (size_t)row * ld;
+        const uint32_t* am = allow_mask ? allow_mask + (size_t)row * mask_ld : nullptr;
+        sample_row_bisect(x, V, P, am, row, out_tok, out_logp, red, rv, ri);
+        return;
+    }
+    const int nk = s_n;
     int np = 1;
-    while (np < n) np <<= 1;
-    for (int k = n + threadIdx.x; k < np; k += 1024) { cv[k] = -INFINITY; ci[k] = 0x7fffffff; }
+    while (np < nk) np <<= 1;
+    for (int k = nk + threadIdx.x; k < np; k += TK_MNT) { cv[k] = -INFINITY; ci[k] = 0x7fffffff; }
     __syncthreads();
     for (int size = 2; size <= np; size <<= 1) {
         for (int stride = size >> 1; stride > 0; stride >>= 1) {
-            for (int t = threadIdx.x; t < np / 2; t += 1024) {
+            for (int t = threadIdx.x; t < np / 2; t += TK_MNT) {
                 const int lo = 2 * t - (t & (stride - 1)), hi = lo + stride;
                 const bool desc = (lo & size) == 0;
                 const float a = cv[lo], bb = cv[hi];
@@ -574,14 +653,8 @@ __global__ __launch_bounds__(1024) void tk_merge_kernel(const float* __restrict_
             __syncthreads();
         }
     }
-    const float mx = cv[0];
     if (threadIdx.x == 0) {  // the bisection chain's semantics (see sample_kernel)
-        int keep = n;
-        if (K < keep) {
-            const float kv = cv[K - 1];
-            keep = K;
-            while (keep < n && cv[keep] == kv) ++keep;
-        }
+        int keep = nk;
         float zk = 0.f;
         const bool tp = P.top_p < 1.f && P.top_p > 0.f;
         if (tp)
@@ -607,7 +680,7 @@ __global__ __launch_bounds__(1024) void tk_merge_kernel(const float* __restrict_
     const int keep = s_keep;
     float best = -INFINITY, zk = 0.f;
     int bi = 0x7fffffff;
-    for (int k = threadIdx.x; k < keep; k += 1024) {
+    for (int k = threadIdx.x; k < keep; k += TK_MNT) {
         const float sc = greedy ? cv[k] : cv[k] + gumbel(P.seed, (uint32_t)ci[k]);
         zk += __expf(cv[k] - mx);
         if (sc > best || (sc == best && ci[k] < bi)) { best = sc; bi = ci[k]; }
@@ -624,13 +697,13 @@ __global__ __launch_bounds__(1024) void tk_merge_kernel(const float* __restrict_
     __syncthreads();
     if (threadIdx.x == 0) {
         float b = rv[0], z = red[0];
-        int id = ri[0];
-        for (int w = 1; w < 16; ++w) {
+        int tok = ri[0];
+        for (int w = 1; w < TK_MNT / 64; ++w) {
             z += red[w];
-            if (rv[w] > b || (rv[w] == b && ri[w] < id)) { b = rv[w]; id = ri[w]; }
+            if (rv[w] > b || (rv[w] == b && ri[w] < tok)) { b = rv[w]; tok = ri[w]; }
         }
-        if (id == 0x7fffffff) id = 0;
-        out_tok[row] = id;
+        if (tok == 0x7fffffff) tok = 0;
+        out_tok[row] = tok;
         if (out_logp) {
             if (greedy) {  // log-softmax over the whole (allowed) row, from the slices' (max, sum exp)
                 float M = -INFINITY, Z = 0.f;
@@ -639,29 +712,32 @@ __global__ __launch_bounds__(1024) void tk_merge_kernel(const float* __restrict_
                     const float2 m = slice_z[row * S + s2];
                     if (m.x > -INFINITY) Z += m.y * __expf(m.x - M);
                 }
-                out_logp[row] = logits[(size_t)row * ld + id] - M - __logf(fmaxf(Z, 1e-30f));
+                out_logp[row] = logits[(size_t)row * ld + tok] - M - __logf(fmaxf(Z, 1e-30f));
             } else {
-                out_logp[row] = logits[(size_t)row * ld + id] / P.temperature - mx - __logf(fmaxf(z, 1e-30f));
+                out_logp[row] = logits[(size_t)row * ld + tok] / P.temperature - mx - __logf(fmaxf(z, 1e-30f));
             }
         }
     }
 }
 
-// B rows, S slices per row (<= 64, S * 2 * max top_k <= 4096 so the merge holds every candidate); every row
-// must have top_k in [1, TK_CAP] or be greedy, no typical-p / mirostat (the caller checks).
-// cand_v / cand_i: [B][S][2*TK_CAP] scratch, cand_n / slice_z: [B][S].
+// B rows, S = ceil(V / TK_SLICE) slices per row (<= 64 and S * TK_CAPS <= TK_MNT * TK_MV); every row must have
+// top_k in [1, TK_CAP] or be greedy, no typical-p / mirostat (the caller checks). cand_v / cand_i:
+// [B][S][TK_CAPS] scratch, cand_n / slice_z: [B][S].
 extern "C" int mxk_sample_topk_split(float* logits, int ld, int B, int V, const SampleParams* params, int has_pen,
                                      const int* pen_tok, const int* pen_cnt, const float* pen_bias,
                                      const uint32_t* allow_mask, int mask_ld, int S, float* cand_v, int* cand_i,
                                      int* cand_n, float2* slice_z, int* out_tok, float* out_logp, hipStream_t st) {
     if (B <= 0) return 0;
-    if (S < 1 || S > 64) return (int)hipErrorInvalidValue;
+    if (S != (V + TK_SLICE - 1) / TK_SLICE || S > 64 || S * TK_CAPS > TK_MNT * TK_MV) return (int)hipErrorInvalidValue;
     if (has_pen) tk_penalty_kernel<<<B, TK_NT, 0, st>>>(logits, ld, V, params, pen_tok, pen_cnt, pen_bias);
     tk_slice_kernel<<<dim3(B, S), TK_NT, 0, st>>>(logits, ld, V, params, allow_mask, mask_ld, cand_v, cand_i, cand_n,
                                                   slice_z);
-    tk_merge_kernel<<<B, 1024, 0, st>>>(logits, ld, params, S, cand_v, cand_i, cand_n, slice_z, out_tok, out_logp);
+    tk_merge_kernel<<<B, TK_MNT, 0, st>>>(logits, ld, V, params, S, allow_mask, mask_ld, cand_v, cand_i, cand_n, slice_z,
+                                          out_tok, out_logp);
     MXK_CHECK_LAUNCH();
 }
+extern "C" int mxk_sample_topk_slice() { return TK_SLICE; }
+extern "C" int mxk_sample_topk_caps() { return TK_CAPS; }
 extern "C" int mxk_sample_topk_cap() { return TK_CAP; }
 
 // greedy argmax over rows (fast path used by the decode graph when every row is greedy)

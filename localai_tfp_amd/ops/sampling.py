@@ -145,7 +145,7 @@ class SamplerBatch:
                                                 bias.view(np.uint8)])
         tok = torch.empty(B, dtype=torch.int32, device=dev)
         lp = torch.empty(B, dtype=torch.float32, device=dev)
-        S = self._split_slices(params, B)
+        S = self._split_slices(params, B, V)
         if S:
             # small batch, top-k on: the vocabulary split over B x S workgroups instead of one CU per row
             cv, ci, cn, sz = self._split_scratch(dev, B, S)
@@ -159,29 +159,34 @@ class SamplerBatch:
                 tok.data_ptr(), lp.data_ptr(), N.stream_ptr())
         return tok, lp
 
-    SPLIT_MAX_B = int(__import__("os").environ.get("MX_SPLIT_SAMPLER_MAX_B", "16"))
+    # the split top-k sampler (B x S register-resident slices + a per-row merge) serves every batch size whose
+    # rows all have top-k on (the reference default, top_k 40) or are greedy; MX_SPLIT_SAMPLER_MAX_B caps it
+    SPLIT_MAX_B = int(__import__("os").environ.get("MX_SPLIT_SAMPLER_MAX_B", str(1 << 20)))
     TOPK_CAP = 64
+    SLICE = 4096   # vocabulary entries per slice (sampling.hip TK_SLICE)
+    CAPS = 128     # candidates per slice (TK_CAPS)
 
-    def _split_slices(self, params, B: int) -> int:
-        """Slices per row for the split top-k sampler, or 0 where it does not apply (large batch, top-k off or
-        above the cap, typical-p / mirostat rows)."""
+    def _split_slices(self, params, B: int, V: int = 128256) -> int:
+        """Slices per row for the split top-k sampler, or 0 where it does not apply (top-k off or above the
+        cap, typical-p / mirostat rows, a vocabulary beyond 64 slices)."""
         if B > self.SPLIT_MAX_B:
             return 0
-        kmax = 1
+        S = -(-V // self.SLICE)
+        if S > 64:
+            return 0
         for p in params:
             if p.greedy:
                 continue
             if not (0 < p.top_k <= self.TOPK_CAP) or (0 < p.typical_p < 1) or p.mirostat == 2:
                 return 0
-            kmax = max(kmax, p.top_k)
-        return max(1, min(64, 4096 // (2 * kmax)))
+        return S
 
     def _split_scratch(self, dev, B: int, S: int):
         key = (str(dev), B, S)
         c = getattr(self, "_scratch", None)
         if c is None or c[0] != key:
-            cv = torch.empty(B * S * 2 * self.TOPK_CAP, dtype=torch.float32, device=dev)
-            ci = torch.empty(B * S * 2 * self.TOPK_CAP, dtype=torch.int32, device=dev)
+            cv = torch.empty(B * S * self.CAPS, dtype=torch.float32, device=dev)
+            ci = torch.empty(B * S * self.CAPS, dtype=torch.int32, device=dev)
             cn = torch.empty(B * S, dtype=torch.int32, device=dev)
             sz = torch.empty(B * S * 2, dtype=torch.float32, device=dev)  # per-slice (max, sum exp)
             c = self._scratch = (key, cv, ci, cn, sz)

@@ -793,7 +793,7 @@ def test_sampling_fast_path_distribution():
     assert np.allclose(freq, [0.0, 0.2 / 0.9, 0.3 / 0.9, 0.4 / 0.9], atol=0.04), freq
 
 
-@pytest.mark.parametrize("B", [1, 3, 16])
+@pytest.mark.parametrize("B", [1, 3, 16, 128])
 def test_sampling_topk_split_matches_row_kernel(B):
     """Small batches with top-k on go through the split-vocabulary sampler (B x S slice workgroups + a merge);
     with the same seeds it draws exactly the token the one-workgroup-per-row kernel draws, with the same
@@ -818,12 +818,41 @@ def test_sampling_topk_split_matches_row_kernel(B):
     hist = [[120, 121, 5, 121] for _ in range(B)]
     split, full = SamplerBatch(DEV), SamplerBatch(DEV)
     full.SPLIT_MAX_B = 0
-    assert split._split_slices(ps, B) > 0 and full._split_slices(ps, B) == 0
+    assert split._split_slices(ps, B, V) > 0 and full._split_slices(ps, B, V) == 0
     for step in range(4):
         t1, l1 = split.sample(logits.clone(), ps, hist, [step] * B, allow_mask=mask)
         t2, l2 = full.sample(logits.clone(), ps, hist, [step] * B, allow_mask=mask)
         assert t1.cpu().tolist() == t2.cpu().tolist(), step
         assert torch.allclose(l1.cpu(), l2.cpu(), atol=2e-3), (l1, l2)
+
+
+def test_sampling_topk_split_ties_and_flat_rows():
+    """Rows with massive exact ties (a flat row, a tied top block larger than a slice's candidate capacity)
+    and near-ties (values within 1e-6) through the split sampler: the slices flag the tie overflow and the
+    merge falls back to the full-row chain, so the draw still matches the one-workgroup-per-row kernel."""
+    from localai_tfp_amd.ops.sampling import SamplerBatch, SamplingParams
+    torch.manual_seed(9)
+    B, V = 4, 128256
+    logits = torch.randn(B, V, device=DEV)
+    logits[0] = 1.5                               # flat row: every value tied
+    logits[1, 1000:3000] = 9.0                    # 2000 exact ties above the rest, inside one slice
+    logits[2] = 3.0 + 1e-6 * torch.randn(V, device=DEV)  # near-flat
+    logits[3, 5000:5300] = 7.0 + 1e-5 * torch.arange(300, device=DEV)
+    ps = [SamplingParams(temperature=0.9, top_k=40, top_p=0.95, min_p=0.0, seed=7 + r) for r in range(B)]
+    hist = [[] for _ in range(B)]
+    split, full = SamplerBatch(DEV), SamplerBatch(DEV)
+    full.SPLIT_MAX_B = 0
+    assert split._split_slices(ps, B, V) > 0
+    kth = torch.topk(logits[2], 40).values[-1]
+    for step in range(3):
+        t1, l1 = split.sample(logits.clone(), ps, hist, [step] * B)
+        t2, l2 = full.sample(logits.clone(), ps, hist, [step] * B)
+        t1, t2 = t1.cpu().tolist(), t2.cpu().tolist()
+        # rows 0, 1, 3: identical draws (row 2's row-kernel path is the value-bisection chain, whose
+        # threshold resolution lumps these near-ties differently); row 2: a member of the exact top-40
+        assert [t1[i] for i in (0, 1, 3)] == [t2[i] for i in (0, 1, 3)], step
+        assert float(logits[2, t1[2]]) >= float(kth), step
+        assert 3000 > t1[1] >= 1000 and 5300 > t1[3] >= 5260
 
 
 @pytest.mark.parametrize("tp", [2, 8])
