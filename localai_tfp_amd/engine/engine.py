@@ -647,6 +647,7 @@ class LLMEngine:
             self._pin_tok[k][:S].copy_(tok_dev[:S], non_blocking=True)
             if lp_dev is not None:
                 self._pin_lp[k][:S].copy_(lp_dev[:S], non_blocking=True)
+            self._snapshot_collectives()
             ev = None
             if self.device.type == "cuda":
                 ev = torch.cuda.Event()
@@ -927,6 +928,7 @@ class LLMEngine:
             plan["gather"] = bool(sample_items) and not greedy_only
             self.tp.send_plan(plan)
         logits, am = self._execute(plan)
+        self._snapshot_collectives()
         if not sample_items:
             return [], None
         if am is not None and greedy_only:
@@ -939,10 +941,20 @@ class LLMEngine:
         self._check_collectives()
         return out
 
+    def _snapshot_collectives(self):
+        """After a step's launches: queue the one-shot all-reduce error flag's async read-back (checked later,
+        without blocking, by _check_collectives)."""
+        if self.tp is None:
+            return
+        ar = getattr(self.model, "custom_ar", None)
+        if ar is not None:
+            ar.snapshot()
+
     def _check_collectives(self, every: int = 1):
         """Tensor parallel: the one-shot all-reduce kernel flags a peer that never delivered (bounded
-        spin) instead of hanging; read that flag at a point where the stream is already synchronised
-        and fail the rank loudly (exit non-zero through TPLink) rather than serve wrong logits."""
+        spin) instead of hanging; the flag is read from retired async snapshots (OneShotAllReduce.check never
+        synchronises the stream), and a set flag fails the rank loudly (exit non-zero through TPLink)
+        rather than serving wrong logits."""
         if self.tp is None:
             return
         ar = getattr(self.model, "custom_ar", None)
@@ -994,7 +1006,8 @@ class LLMEngine:
             ns = int(msg.get("ns", 0))
             if ns:  # overlap mode: the leader's sampled tokens, for the next plan's device-side fix-up
                 self._prev_dev = (self._tp_bcast_tokens(None, ns), None)
-            self._check_collectives(every=64)
+            self._snapshot_collectives()
+            self._check_collectives()
 
     def _tp_bcast_tokens(self, tok_dev, n: int):
         """Leader: broadcast its n sampled token ids (device int32) to the TP group on the compute stream;

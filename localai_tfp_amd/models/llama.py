@@ -457,6 +457,58 @@ class LlamaModel:
             from ..parallel import tp as TP
             TP.all_reduce_(t, self.tp_group)
 
+    TP_CHUNK_MIN_ROWS = int(__import__("os").environ.get("MX_TP_CHUNK_MIN_ROWS", "64"))
+    TP_CHUNKS = int(__import__("os").environ.get("MX_TP_CHUNKS", "2"))
+
+    def _tp_chunks(self, T: int, y16: torch.Tensor) -> int:
+        """Row chunks of a row-parallel projection whose all-reduce is overlapped with the next chunk's GEMM:
+        MX_TP_CHUNKS (default 2) from MX_TP_CHUNK_MIN_ROWS rows, more when a chunk would not fit the one-shot
+        all-reduce's buffer (so large decode batches stay off RCCL); 1 = no overlap."""
+        if self.TP_CHUNKS <= 1 or T < self.TP_CHUNK_MIN_ROWS:
+            return 1
+        n = self.TP_CHUNKS
+        ar = getattr(self, "custom_ar", None)
+        if ar is not None:
+            row_bytes = y16.shape[1] * y16.element_size()
+            n = max(n, -(-T * row_bytes // ar.max_bytes))
+        return max(1, min(n, 8, T // max(1, self.TP_CHUNK_MIN_ROWS // 4)))  # chunks of >= MIN_ROWS / 4 rows
+
+    def _chunked_proj_allreduce(self, mm, W: QWeight, x, y16, h, T: int, nch: int):
+        """h += all-reduce(x W^T) in `nch` row chunks: chunk c's GEMM runs on the compute stream while chunk
+        c-1's all-reduce + residual add runs on a second stream (event fork / join, hipGraph-capturable); the
+        compute stream waits for the last all-reduce before the next norm reads h. Without a GPU the chunks
+        run in order (same arithmetic: the all-reduce of a row chunk is that chunk of the all-reduce)."""
+        bounds = [T * c // nch for c in range(nch + 1)]
+        ar = getattr(self, "custom_ar", None)
+        self.tp_chunked_calls = getattr(self, "tp_chunked_calls", 0) + 1
+
+        def reduce_add(r0, r1):
+            if ar is not None and ar.fits(y16[r0:r1]):
+                ar.add_into(y16[r0:r1], h[r0:r1])
+            else:
+                self._allreduce(y16[r0:r1])
+                h[r0:r1].add_(y16[r0:r1])
+
+        if not y16.is_cuda:
+            for r0, r1 in zip(bounds, bounds[1:]):
+                mm(W, x[r0:r1], EPI_BF16, y16[r0:r1])
+                reduce_add(r0, r1)
+            return
+        cur = torch.cuda.current_stream(y16.device)
+        s2 = getattr(self, "_ar_stream", None)
+        if s2 is None:
+            s2 = self._ar_stream = torch.cuda.Stream(y16.device)
+        for r0, r1 in zip(bounds, bounds[1:]):
+            mm(W, x[r0:r1], EPI_BF16, y16[r0:r1])
+            ev = torch.cuda.Event()
+            ev.record(cur)
+            s2.wait_event(ev)
+            with torch.cuda.stream(s2):
+                reduce_add(r0, r1)
+        done = torch.cuda.Event()
+        done.record(s2)
+        cur.wait_event(done)
+
     def enable_custom_allreduce(self, max_bytes: int = 1 << 20):
         """Collective over the TP group (call on every rank, outside graph capture): small row-parallel
         all-reduces go through the one-shot hipIpc kernel (parallel/custom_ar.py). MX_CUSTOM_AR=0 disables."""
@@ -758,6 +810,10 @@ class LlamaModel:
         gemv = xq is not None
         if self.tp_size > 1:
             y16 = ws.y16[:T]
+            nch = self._tp_chunks(T, y16) if (post_norm is None and not gemv and h.is_contiguous()) else 1
+            if nch > 1:
+                self._chunked_proj_allreduce(mm, W, x, y16, h, T, nch)
+                return
             if gemv:
                 mm(W, None, EPI_BF16, y16, xq=xq, xds=xds)
             else:

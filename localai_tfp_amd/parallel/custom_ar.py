@@ -8,12 +8,15 @@ different GPUs of one node (xGMI) and for several processes sharing one GPU (the
 
     ar = OneShotAllReduce(group, device, max_bytes=1 << 20)
     ar(t)          # in place, t: 16-bit CUDA tensor; falls back to dist.all_reduce when too large
-    ar.check()     # raises if a peer never arrived (bounded spin in the kernel)
+    ar.snapshot()  # after a step's launches: async copy of the error flag into a pinned ring + an event
+    ar.check()     # raises if a completed snapshot saw a peer that never arrived (bounded spin in the kernel);
+                   # never blocks on queued work (block=True waits for every snapshot: shutdown / tests)
 """
 from __future__ import annotations
 
 import ctypes as C
 import os
+from collections import deque
 
 import torch
 
@@ -87,6 +90,10 @@ class OneShotAllReduce:
                 self._opened.append(ptr)
             self.epoch = torch.zeros(1, dtype=torch.int32, device=self.device)
             self.err = torch.zeros(1, dtype=torch.int32, device=self.device)
+        # error-flag snapshots: pinned host slots filled by async copies, each with the event that retires it
+        self._err_host = torch.zeros(self.SNAP_RING, dtype=torch.int32, pin_memory=self.device.type == "cuda")
+        self._snaps: deque = deque()
+        self._snap_i = 0
         dist.barrier(group=group)
 
     def __call__(self, t: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
@@ -122,9 +129,44 @@ class OneShotAllReduce:
                                              N.stream_ptr(self.device)), "mxk_allreduce_1shot_add")
         return res
 
-    def check(self):
-        if int(self.err.item()):
+    SNAP_RING = 16
+
+    def snapshot(self):
+        """Queue an async copy of the error flag (behind the work launched so far) into the next pinned slot
+        and record its event. Cheap enough for every step; check() reads only retired snapshots."""
+        if len(self._snaps) >= self.SNAP_RING:  # ring full: retire the oldest (long retired in practice)
+            self._retire(self._snaps.popleft(), block=True)
+        k = self._snap_i
+        self._snap_i = (k + 1) % self.SNAP_RING
+        self._err_host[k:k + 1].copy_(self.err, non_blocking=True)
+        ev = None
+        if self.device.type == "cuda":
+            ev = torch.cuda.Event()
+            ev.record()
+        self._snaps.append((ev, k))
+
+    def _retire(self, snap, block: bool):
+        ev, k = snap
+        if ev is not None:
+            if block:
+                ev.synchronize()
+            elif not ev.query():
+                return False
+        if int(self._err_host[k]):
             raise RuntimeError("one-shot all-reduce: a peer never delivered its data (rank dead or desynchronised)")
+        return True
+
+    def check(self, block: bool = False):
+        """Raise if any retired snapshot saw the error flag. Non-blocking by default: a snapshot whose copy is
+        still queued behind running work is left for a later check (no device->host sync on the stream, so a
+        check between two launched steps never serialises the overlap pipeline). block=True: snapshot now
+        and wait for everything."""
+        if block:
+            self.snapshot()
+        while self._snaps:
+            if not self._retire(self._snaps[0], block):
+                return
+            self._snaps.popleft()
 
     def close(self):
         for p in self._opened:

@@ -26,7 +26,7 @@ def main():
         t = x.to(dev, dt)
         ar(t)
         torch.cuda.synchronize()
-        ar.check()
+        ar.check(block=True)
         err = (t.float().cpu() - ref).abs().max().item()
         tol = 1e-2 if dt == torch.float16 else 6e-2
         ok &= err < tol * max(1.0, ref.abs().max().item())
@@ -38,7 +38,7 @@ def main():
         res = torch.full((n,), 1.5, device=dev)
         ar.add_into(parts[rank].to(dev, torch.float16), res)
         torch.cuda.synchronize()
-        ar.check()
+        ar.check(block=True)
         err = (res.cpu() - ref).abs().max().item()
         ok &= err < 1e-2 * max(1.0, ref.abs().max().item())
         print(f"rank {rank} add_into n={n} err={err:.3g}", flush=True)
@@ -59,9 +59,23 @@ def main():
     for _ in range(5):
         graph.replay()
         torch.cuda.synchronize()
-        ar.check()
+        ar.check(block=True)
         ok &= bool((t.float() == world * (world + 1) / 2).all())
     print(f"rank {rank} graph ok={ok}", flush=True)
+    # check() never blocks on queued work: a long kernel queued after the snapshot leaves it pending,
+    # and the host call returns at once (the overlap pipeline calls it between two launched steps)
+    import time
+    ar(t)
+    ar.snapshot()
+    torch.cuda._sleep(int(1e9))  # ~0.4-0.5 s of device time queued behind the snapshot
+    t0 = time.perf_counter()
+    ar.check()
+    dt = time.perf_counter() - t0
+    busy = not torch.cuda.current_stream(dev).query()
+    torch.cuda.synchronize()
+    ar.check(block=True)
+    ok &= dt < 0.02 and busy
+    print(f"rank {rank} nonblocking check {dt * 1e3:.2f} ms (stream busy={busy}) ok={ok}", flush=True)
     dist.barrier()
     ar.close()
     dist.destroy_process_group()

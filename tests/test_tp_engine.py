@@ -69,16 +69,25 @@ def _worker(rank, world, port, q, kind="dense"):
                 ids += o.token_ids
             outs.append(ids)
         eng.shutdown()
+        import os
+        if int(os.environ.get("MX_TP_CHUNKS", "1")) > 1:
+            assert getattr(eng.model, "tp_chunked_calls", 0) > 0, "chunked row-parallel path never ran"
         q.put(outs)
     else:
         eng.follow()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("kind,world", [("dense", 2), ("moe", 2), ("wide", 4), ("wide", 8)])
-def test_tp_matches_single_process(kind, world):
+@pytest.mark.parametrize("kind,world,chunks", [("dense", 2, 1), ("moe", 2, 1), ("wide", 4, 1), ("wide", 8, 1),
+                                               ("dense", 2, 3), ("wide", 8, 2)])
+def test_tp_matches_single_process(kind, world, chunks, monkeypatch):
     """Greedy output of a TP group (leader + followers replaying plans over the /dev/shm ring, sampled
-    tokens broadcast each overlap-mode step) equals the single-process engine."""
+    tokens broadcast each overlap-mode step) equals the single-process engine. chunks > 1: the row-parallel
+    projections run as row chunks whose all-reduce + residual add is pipelined behind the next chunk's GEMM
+    (models/llama.py _chunked_proj_allreduce; in order on gloo), from 4 rows up so prefill and batched
+    decode steps both take it."""
+    monkeypatch.setenv("MX_TP_CHUNKS", str(chunks))
+    monkeypatch.setenv("MX_TP_CHUNK_MIN_ROWS", "4" if chunks > 1 else "64")
     eng = _build(0, 1, None, kind)
     from localai_tfp_amd.engine.sequence import Request
     from localai_tfp_amd.ops.sampling import SamplingParams
