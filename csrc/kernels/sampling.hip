@@ -23,6 +23,8 @@ struct SampleParams {
     float frequency_penalty;
     int pen_offset;  // into the sparse penalty arrays
     int pen_count;
+    int pend;        // overlap pipeline: index of this row's still-in-flight previous token in pend_tok (-1: none);
+                     // the host's sparse counts lag that token by one, it is counted here
     unsigned long long seed;
 };
 
@@ -61,13 +63,24 @@ MX_DEV float bmax(float v, float* red) {
     return t;
 }
 
-// sparse penalties + logit bias, in place (unique tokens per row -> no write conflicts)
-MX_DEV void apply_penalties(float* x, int V, const SampleParams& P, const int* pen_tok, const int* pen_cnt,
-                            const float* pen_bias) {
-    for (int i = threadIdx.x; i < P.pen_count; i += SNT) {
+// sparse penalties + logit bias, in place (unique tokens per row -> no write conflicts). `pend_tok`: the
+// tokens of the previous, still-in-flight step (overlap pipeline); the row's one pending token counts once
+// more (an entry already in the list, or a penalty-only entry of count 1).
+template <int NT>
+MX_DEV void penalize(float* x, int V, const SampleParams& P, const int* pen_tok, const int* pen_cnt,
+                     const float* pen_bias, const int* pend_tok, int* s_found) {
+    const int tp = (P.pend >= 0 && pend_tok) ? pend_tok[P.pend] : -1;
+    const bool pens = P.repeat_penalty != 1.f || P.presence_penalty != 0.f || P.frequency_penalty != 0.f;
+    if (threadIdx.x == 0) *s_found = 0;
+    __syncthreads();
+    for (int i = threadIdx.x; i < P.pen_count; i += NT) {
         const int t = pen_tok[P.pen_offset + i];
         if (t < 0 || t >= V) continue;
-        const int c = pen_cnt[P.pen_offset + i];
+        int c = pen_cnt[P.pen_offset + i];
+        if (t == tp) {
+            *s_found = 1;
+            if (pens) ++c;
+        }
         float v = x[t];
         if (c > 0) {
             if (P.repeat_penalty != 1.f) v = v > 0.f ? v / P.repeat_penalty : v * P.repeat_penalty;
@@ -77,6 +90,18 @@ MX_DEV void apply_penalties(float* x, int V, const SampleParams& P, const int* p
         x[t] = v;
     }
     __syncthreads();
+    if (threadIdx.x == 0 && pens && tp >= 0 && tp < V && !*s_found) {
+        float v = x[tp];
+        if (P.repeat_penalty != 1.f) v = v > 0.f ? v / P.repeat_penalty : v * P.repeat_penalty;
+        x[tp] = v - P.frequency_penalty - P.presence_penalty;
+    }
+    __syncthreads();
+}
+
+MX_DEV void apply_penalties(float* x, int V, const SampleParams& P, const int* pen_tok, const int* pen_cnt,
+                            const float* pen_bias, const int* pend_tok) {
+    __shared__ int s_found;
+    penalize<SNT>(x, V, P, pen_tok, pen_cnt, pen_bias, pend_tok, &s_found);
 }
 
 // General chain by bisection on the value axis (every pass streams the whole row): typical-p, mirostat,
@@ -225,7 +250,8 @@ __global__ __launch_bounds__(SNT) void sample_kernel(float* __restrict__ logits,
                                                      const int* __restrict__ pen_cnt,
                                                      const float* __restrict__ pen_bias,
                                                      const uint32_t* __restrict__ allow_mask, int mask_ld,
-                                                     int* __restrict__ out_tok, float* __restrict__ out_logp) {
+                                                     int* __restrict__ out_tok, float* __restrict__ out_logp,
+                                                     const int* __restrict__ pend_tok) {
     __shared__ float red[SNT / 64];
     __shared__ float rv[SNT / 64];
     __shared__ int ri[SNT / 64];
@@ -238,7 +264,7 @@ __global__ __launch_bounds__(SNT) void sample_kernel(float* __restrict__ logits,
     const SampleParams P = params[row];
     float* x = logits + (size_t)row * ld;
     const uint32_t* am = allow_mask ? allow_mask + (size_t)row * mask_ld : nullptr;
-    apply_penalties(x, V, P, pen_tok, pen_cnt, pen_bias);
+    apply_penalties(x, V, P, pen_tok, pen_cnt, pen_bias, pend_tok);
     const bool greedy = P.temperature <= 0.f;
     const bool fast_ok = !greedy && !(P.typical_p < 1.f && P.typical_p > 0.f) && !(P.mirostat_tau > 0.f) &&
                          ((P.top_k > 0 && P.top_k <= SCAP) || (P.top_p < 1.f && P.top_p > 0.f) || P.min_p > 0.f);
@@ -403,10 +429,10 @@ __global__ __launch_bounds__(SNT) void sample_kernel(float* __restrict__ logits,
 
 extern "C" int mxk_sample(float* logits, int ld, int B, int V, const SampleParams* params, const int* pen_tok,
                           const int* pen_cnt, const float* pen_bias, const uint32_t* allow_mask, int mask_ld,
-                          int* out_tok, float* out_logp, hipStream_t st) {
+                          int* out_tok, float* out_logp, const int* pend_tok, hipStream_t st) {
     if (B <= 0) return 0;
     sample_kernel<<<B, SNT, 0, st>>>(logits, ld, V, params, pen_tok, pen_cnt, pen_bias, allow_mask, mask_ld, out_tok,
-                                     out_logp);
+                                     out_logp, pend_tok);
     MXK_CHECK_LAUNCH();
 }
 
@@ -436,21 +462,11 @@ MX_DEV uint32_t ord_key(float v) {  // order-preserving float -> uint (NaN / -in
 }
 
 __global__ __launch_bounds__(TK_NT) void tk_penalty_kernel(float* logits, int ld, int V, const SampleParams* params,
-                                                          const int* pen_tok, const int* pen_cnt, const float* pen_bias) {
+                                                          const int* pen_tok, const int* pen_cnt, const float* pen_bias,
+                                                          const int* pend_tok) {
+    __shared__ int s_found;
     const SampleParams P = params[blockIdx.x];
-    float* x = logits + (size_t)blockIdx.x * ld;
-    for (int i = threadIdx.x; i < P.pen_count; i += TK_NT) {
-        const int t = pen_tok[P.pen_offset + i];
-        if (t < 0 || t >= V) continue;
-        const int c = pen_cnt[P.pen_offset + i];
-        float v = x[t];
-        if (c > 0) {
-            if (P.repeat_penalty != 1.f) v = v > 0.f ? v / P.repeat_penalty : v * P.repeat_penalty;
-            v -= P.frequency_penalty * (float)c + P.presence_penalty;
-        }
-        v += pen_bias[P.pen_offset + i];
-        x[t] = v;
-    }
+    penalize<TK_NT>(logits + (size_t)blockIdx.x * ld, V, P, pen_tok, pen_cnt, pen_bias, pend_tok, &s_found);
 }
 
 // block-wide count of keys >= t over NV registers per thread; `red` double-buffered by the caller's parity
@@ -726,10 +742,11 @@ __global__ __launch_bounds__(TK_MNT) void tk_merge_kernel(float* __restrict__ lo
 extern "C" int mxk_sample_topk_split(float* logits, int ld, int B, int V, const SampleParams* params, int has_pen,
                                      const int* pen_tok, const int* pen_cnt, const float* pen_bias,
                                      const uint32_t* allow_mask, int mask_ld, int S, float* cand_v, int* cand_i,
-                                     int* cand_n, float2* slice_z, int* out_tok, float* out_logp, hipStream_t st) {
+                                     int* cand_n, float2* slice_z, int* out_tok, float* out_logp, const int* pend_tok,
+                                     hipStream_t st) {
     if (B <= 0) return 0;
     if (S != (V + TK_SLICE - 1) / TK_SLICE || S > 64 || S * TK_CAPS > TK_MNT * TK_MV) return (int)hipErrorInvalidValue;
-    if (has_pen) tk_penalty_kernel<<<B, TK_NT, 0, st>>>(logits, ld, V, params, pen_tok, pen_cnt, pen_bias);
+    if (has_pen) tk_penalty_kernel<<<B, TK_NT, 0, st>>>(logits, ld, V, params, pen_tok, pen_cnt, pen_bias, pend_tok);
     tk_slice_kernel<<<dim3(B, S), TK_NT, 0, st>>>(logits, ld, V, params, allow_mask, mask_ld, cand_v, cand_i, cand_n,
                                                   slice_z);
     tk_merge_kernel<<<B, TK_MNT, 0, st>>>(logits, ld, V, params, S, allow_mask, mask_ld, cand_v, cand_i, cand_n, slice_z,

@@ -59,8 +59,8 @@ KERNEL_SIGS = {
     "mxk_attn_prefill": [P, P, P, P, I, P, P, I, P, P, I, I, I, I, F, I, F, P, I, I, P],
     "mxk_probe_tr16": [P, P],
     "mxk_attn_prefill_rows": [I, I],
-    "mxk_sample": [P, I, I, I, P, P, P, P, P, I, P, P, P],
-    "mxk_sample_topk_split": [P, I, I, I, P, I, P, P, P, P, I, I, P, P, P, P, P, P, P],
+    "mxk_sample": [P, I, I, I, P, P, P, P, P, I, P, P, P, P],
+    "mxk_sample_topk_split": [P, I, I, I, P, I, P, P, P, P, I, I, P, P, P, P, P, P, P, P],
     "mxk_sample_params_size": [],
     "mxk_argmax": [P, I, I, I, P, P],
     "mxk_argmax_keys": [P, I, I, I, I, P, P],

@@ -551,7 +551,10 @@ class LLMEngine:
                 so = self._drain_and_filter(so)  # a pending token lives in an older step's buffer
                 if so is None:
                     return
+            self.stats["overlap_steps"] = self.stats.get("overlap_steps", 0) + 1
             return self._step_overlap(so, t0)
+        if self.overlap:
+            self.stats["sync_steps"] = self.stats.get("sync_steps", 0) + 1
         if self._inflight:  # this step needs host-known tokens: read the in-flight ones first
             so = self._drain_and_filter(so)
             if so is None:
@@ -600,14 +603,40 @@ class LLMEngine:
                    and not it.seq.params.presence_penalty and not it.seq.params.frequency_penalty
                    and it.seq.grammar is None for it in items)
 
+    def _overlap_params(self, p) -> bool:
+        """Sampling the overlap pipeline can launch before the previous step's tokens reach the host: the
+        simple chain, and repeat / presence / frequency penalties while at most one token per row is in
+        flight (overlap_depth 1: the kernel counts that pending token, ops/sampling.py pack)."""
+        if p.mirostat == 2:
+            return False
+        return self._simple_params(p) or self.cfg.overlap_depth <= 1
+
     def _overlap_ok(self, so: SchedulerOutput) -> bool:
         for it in so.decode:
-            if it.seq.grammar is not None or it.seq.req.embedding or not self._simple_params(it.seq.params):
+            if it.seq.grammar is not None or it.seq.req.embedding or not self._overlap_params(it.seq.params):
                 return False
         for it in so.prefill:
-            if it.sample and (it.seq.grammar is not None or it.seq.req.embedding or not self._simple_params(it.seq.params)):
+            if it.sample and (it.seq.grammar is not None or it.seq.req.embedding or not self._overlap_params(it.seq.params)):
                 return False
         return True
+
+    def _overlap_sample_args(self, items):
+        """(histories, pend_tok, pend) for the overlap sampler: full histories only for penalty rows, and the
+        index of each row's in-flight previous token in the last launched step's token tensor."""
+        params = [it.seq.params for it in items]
+        if all(self._simple_params(p) for p in params) or self._prev_dev is None:
+            return [[] for _ in items], None, None
+        prev_tok, prev_map = self._prev_dev
+        hist, pend = [], []
+        for it, p in zip(items, params):
+            if self._simple_params(p):
+                hist.append([])
+                pend.append(-1)
+                continue
+            hist.append(it.seq.all_ids)
+            r = prev_map.get(it.seq.rid, -1) if (prev_map is not None and it.seq.n_pending > 0) else -1
+            pend.append(r)
+        return hist, prev_tok, pend
 
     def _step_overlap(self, so: SchedulerOutput, t0: float):
         """Launch this step without waiting for it; then read the previous step's tokens (its async
@@ -632,13 +661,15 @@ class LLMEngine:
             if am is not None and self._argmax_only(items):
                 tok_dev = am
             elif not logits.is_cuda:  # CPU reference sampler (host lists)
-                t, l = self.sampler.sample(logits, [it.seq.params for it in items], [[] for _ in items],
-                                           [it.seq.n_generated for it in items], None, None)
+                hist, ptok, pend = self._overlap_sample_args(items)
+                t, l = self.sampler.sample(logits, [it.seq.params for it in items], hist,
+                                           [it.seq.n_generated for it in items], None, None, ptok, pend)
                 tok_dev = torch.as_tensor(t, dtype=torch.int32)
                 lp_dev = torch.as_tensor(l, dtype=torch.float32) if l is not None else None
             else:
-                tok_dev, lp_dev = self.sampler.sample(logits, [it.seq.params for it in items], [[] for _ in items],
-                                                      [it.seq.n_generated for it in items], None, None)
+                hist, ptok, pend = self._overlap_sample_args(items)
+                tok_dev, lp_dev = self.sampler.sample(logits, [it.seq.params for it in items], hist,
+                                                      [it.seq.n_generated for it in items], None, None, ptok, pend)
             if self.tp is not None:
                 tok_dev = self._tp_bcast_tokens(tok_dev, len(items))
             k = self._pin_i

@@ -18,7 +18,7 @@ SAMPLE_DTYPE = np.dtype([
     ("temperature", np.float32), ("top_k", np.int32), ("top_p", np.float32), ("min_p", np.float32),
     ("typical_p", np.float32), ("mirostat_tau", np.float32), ("repeat_penalty", np.float32),
     ("presence_penalty", np.float32), ("frequency_penalty", np.float32), ("pen_offset", np.int32),
-    ("pen_count", np.int32), ("seed", np.uint64)], align=True)
+    ("pen_count", np.int32), ("pend", np.int32), ("seed", np.uint64)], align=True)
 
 
 @dataclass
@@ -65,6 +65,7 @@ class SamplerBatch:
         c = p.__dict__.get("_mx_rec")
         if c is None:
             r = np.zeros(1, SAMPLE_DTYPE)
+            r["pend"] = -1
             r["temperature"] = 0.0 if p.greedy else p.temperature
             r["top_k"], r["top_p"], r["min_p"], r["typical_p"] = p.top_k, p.top_p, p.min_p, p.typical_p
             r["repeat_penalty"] = p.repeat_penalty
@@ -76,9 +77,12 @@ class SamplerBatch:
         return c
 
     def pack(self, params: list[SamplingParams], histories: list[list[int]], steps: list[int],
-             mirostat_mu: list[float] | None = None):
+             mirostat_mu: list[float] | None = None, pend: list[int] | None = None):
         """Vectorised over rows: cached per-request records, seeds advanced per step in numpy; only rows with
-        penalties / logit bias / mirostat are visited in Python."""
+        penalties / logit bias / mirostat are visited in Python. pend[i] >= 0: row i's previous token is still
+        in flight (overlap pipeline) at that index of the device token tensor passed to sample(); its history
+        lacks that token, so the penalty window takes one token fewer here and the kernel counts the
+        pending one."""
         B = len(params)
         recs = [self._record(p) for p in params]
         arr = np.concatenate([r[0] for r in recs]) if B else np.zeros(0, SAMPLE_DTYPE)
@@ -91,8 +95,11 @@ class SamplerBatch:
             p = params[i]
             arr[i]["mirostat_tau"] = (mirostat_mu[i] if mirostat_mu else 2 * p.mirostat_tau) if p.mirostat == 2 else 0.0
             d: dict[int, list] = {}
+            pi = pend[i] if pend is not None else -1
+            arr[i]["pend"] = pi
             if p.repeat_penalty != 1.0 or p.presence_penalty or p.frequency_penalty:
-                hist = histories[i][-p.repeat_last_n:] if p.repeat_last_n > 0 else histories[i]
+                n = p.repeat_last_n - (1 if pi >= 0 else 0)
+                hist = histories[i][-n:] if n > 0 else ([] if p.repeat_last_n > 0 else histories[i])
                 for t in hist:
                     e = d.setdefault(int(t), [0, 0.0])
                     e[0] += 1
@@ -126,10 +133,18 @@ class SamplerBatch:
         return [d[o:o + a.size] for o, a in zip(offs, parts)]
 
     def sample(self, logits: torch.Tensor, params: list[SamplingParams], histories: list[list[int]],
-               steps: list[int], allow_mask: torch.Tensor | None = None, mirostat_mu=None):
-        """logits fp32 [B, V] (modified in place) -> (tokens int32 [B], logprobs fp32 [B]) on device."""
+               steps: list[int], allow_mask: torch.Tensor | None = None, mirostat_mu=None,
+               pend_tok: torch.Tensor | None = None, pend: list[int] | None = None):
+        """logits fp32 [B, V] (modified in place) -> (tokens int32 [B], logprobs fp32 [B]) on device.
+        pend_tok / pend: the previous step's token tensor (still in flight) and, per row, the index of that
+        row's pending token in it or -1 (penalties in the overlap pipeline, see pack)."""
         B, V = logits.shape
+        if pend is not None and (pend_tok is None or all(i < 0 for i in pend)):
+            pend = None
         if not logits.is_cuda:
+            if pend is not None:  # CPU tensors are already computed: append the pending token to the history
+                pt = pend_tok.tolist()
+                histories = [h + [int(pt[i])] if i >= 0 else h for h, i in zip(histories, pend)]
             return sample_ref(logits, params, histories, steps, allow_mask)
         if not self._checked:
             _check_size()
@@ -139,8 +154,12 @@ class SamplerBatch:
             tok = torch.empty(B, dtype=torch.int32, device=logits.device)
             N.kcall("mxk_argmax", logits.data_ptr(), logits.stride(0), B, V, tok.data_ptr(), N.stream_ptr())
             return tok, None
-        arr, toks, cnts, bias = self.pack(params, histories, steps, mirostat_mu)
+        arr, toks, cnts, bias = self.pack(params, histories, steps, mirostat_mu, pend)
         dev = logits.device
+        ptok = None
+        if pend is not None:
+            ptok = pend_tok if (pend_tok.dtype == torch.int32 and pend_tok.is_contiguous()) else \
+                pend_tok.to(torch.int32).contiguous()
         pbuf, t_t, c_t, b_t = self._stage(dev, [arr.view(np.uint8), toks.view(np.uint8), cnts.view(np.uint8),
                                                 bias.view(np.uint8)])
         tok = torch.empty(B, dtype=torch.int32, device=dev)
@@ -149,14 +168,16 @@ class SamplerBatch:
         if S:
             # small batch, top-k on: the vocabulary split over B x S workgroups instead of one CU per row
             cv, ci, cn, sz = self._split_scratch(dev, B, S)
+            has_pen = bool(arr["pen_count"].any()) or bool((arr["pend"] >= 0).any())
             N.kcall("mxk_sample_topk_split", logits.data_ptr(), logits.stride(0), B, V, pbuf.data_ptr(),
-                    int(bool(arr["pen_count"].any())), t_t.data_ptr(), c_t.data_ptr(), b_t.data_ptr(),
+                    int(has_pen), t_t.data_ptr(), c_t.data_ptr(), b_t.data_ptr(),
                     N.ptr(allow_mask), allow_mask.stride(0) if allow_mask is not None else 0, S, cv.data_ptr(),
-                    ci.data_ptr(), cn.data_ptr(), sz.data_ptr(), tok.data_ptr(), lp.data_ptr(), N.stream_ptr())
+                    ci.data_ptr(), cn.data_ptr(), sz.data_ptr(), tok.data_ptr(), lp.data_ptr(), N.ptr(ptok),
+                    N.stream_ptr())
             return tok, lp
         N.kcall("mxk_sample", logits.data_ptr(), logits.stride(0), B, V, pbuf.data_ptr(), t_t.data_ptr(),
                 c_t.data_ptr(), b_t.data_ptr(), N.ptr(allow_mask), allow_mask.stride(0) if allow_mask is not None else 0,
-                tok.data_ptr(), lp.data_ptr(), N.stream_ptr())
+                tok.data_ptr(), lp.data_ptr(), N.ptr(ptok), N.stream_ptr())
         return tok, lp
 
     # the split top-k sampler (B x S register-resident slices + a per-row merge) serves every batch size whose

@@ -183,6 +183,35 @@ def test_overlap_mode_matches_sync(model, max_tokens_budget):
         assert not e_ovl.sched.deferred and not e_ovl._inflight
 
 
+def _penalty_requests(seed=3):
+    rng = np.random.default_rng(seed)
+    reqs = []
+    for i in range(8):
+        p = [int(x) for x in rng.integers(1, 250, size=int(rng.integers(5, 60)))]
+        if i % 4 == 0:
+            sp = SamplingParams(temperature=0.0, frequency_penalty=0.7, presence_penalty=0.3, repeat_last_n=16)
+        elif i % 4 == 1:
+            sp = SamplingParams(temperature=0.8, top_k=40, top_p=0.9, repeat_penalty=1.3, seed=50 + i)
+        elif i % 4 == 2:
+            sp = SamplingParams(temperature=0.0, repeat_penalty=1.5, repeat_last_n=1, logit_bias={9: 1.0})
+        else:
+            sp = SamplingParams(temperature=0.0)
+        reqs.append(Request(p, sp, max_tokens=int(rng.integers(4, 24))))
+    return reqs
+
+
+def test_penalties_stay_on_overlap_pipeline(model):
+    """Repeat / presence / frequency penalties no longer force synchronous steps: the sampler counts each
+    row's still-in-flight previous token on the device (ops/sampling.py pack, `pend`), so the overlap engine
+    gives exactly the synchronous outputs while every step launches overlapped."""
+    e_sync, _ = mk(model, overlap=False, max_batched_tokens=64)
+    e_ovl, _ = mk(model, overlap=True, max_batched_tokens=64)
+    a = _run_all(e_sync, _penalty_requests())
+    b = _run_all(e_ovl, _penalty_requests())
+    assert a == b
+    assert e_ovl.stats.get("overlap_steps", 0) > 0 and e_ovl.stats.get("sync_steps", 0) == 0, e_ovl.stats
+
+
 @pytest.mark.parametrize("depth", [1, 3])
 def test_overlap_depth_matches_sync(model, depth):
     """Deeper overlap pipelines (several launched-but-unread steps) give the synchronous outputs too."""

@@ -826,6 +826,35 @@ def test_sampling_topk_split_matches_row_kernel(B):
         assert torch.allclose(l1.cpu(), l2.cpu(), atol=2e-3), (l1, l2)
 
 
+@pytest.mark.parametrize("split", [True, False])
+def test_sampling_pending_token_penalties(split):
+    """Overlap pipeline: a row's previous token still in flight (device tensor + index `pend`) is counted by
+    the penalty kernels exactly as if it were the newest history entry (window one shorter on the host)."""
+    from localai_tfp_amd.ops.sampling import SamplerBatch, SamplingParams
+    torch.manual_seed(3)
+    B, V = 6, 32000
+    logits = torch.randn(B, V, device=DEV) * 3
+    ps = [SamplingParams(temperature=[0.0, 0.7][r % 2], top_k=40, top_p=0.95, repeat_penalty=1.4,
+                         frequency_penalty=0.5, presence_penalty=0.2, repeat_last_n=[8, 1, 64][r % 3], seed=r)
+          for r in range(B)]
+    hist = [[int(x) for x in torch.randint(0, V, (20,))] for _ in range(B)]
+    prev = torch.randint(0, V, (B + 2,), dtype=torch.int32, device=DEV)
+    prev[3] = hist[1][-1]  # row 1's pending token already in its window: its count goes up
+    pend = [2, 3, -1, 5, 0, 7]
+    for r in range(B):  # make the pending tokens matter: push them to the top of their rows
+        if pend[r] >= 0:
+            logits[r, int(prev[pend[r]])] = 20.0
+    full_hist = [h + [int(prev[i])] if i >= 0 else h for h, i in zip(hist, pend)]
+    a, b = SamplerBatch(DEV), SamplerBatch(DEV)
+    if not split:
+        a.SPLIT_MAX_B = b.SPLIT_MAX_B = 0
+    for step in range(3):
+        t1, l1 = a.sample(logits.clone(), ps, hist, [step] * B, pend_tok=prev, pend=pend)
+        t2, l2 = b.sample(logits.clone(), ps, full_hist, [step] * B)
+        assert t1.cpu().tolist() == t2.cpu().tolist(), step
+        assert torch.allclose(l1.cpu(), l2.cpu(), atol=1e-4)
+
+
 def test_sampling_topk_split_ties_and_flat_rows():
     """Rows with massive exact ties (a flat row, a tied top block larger than a slice's candidate capacity)
     and near-ties (values within 1e-6) through the split sampler: the slices flag the tie overflow and the
