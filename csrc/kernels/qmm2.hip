@@ -27,6 +27,7 @@
 namespace {
 
 constexpr int Q2_NS = 4;  // ring slots (k-tiles of 64)
+int g_qmm2_rot = 0;       // k-order rotation multiplier per column tile (0: natural order), mxk_qmm2_set_rot
 
 template <int QT>
 struct Q2F;
@@ -161,7 +162,7 @@ template <int QT, int WM, int KS, int EPI, int DBG = 0>
 __global__ __launch_bounds__(256 * KS) void qmm2_kernel(const uint16_t* __restrict__ A, int lda,
                                                         const uint8_t* __restrict__ W, int M, int N, int K,
                                                         int n_mt, int splits, int sbps, void* __restrict__ Cv,
-                                                        int ldc) {
+                                                        int ldc, int rot_mul) {
     using G = Q2Geom<QT, WM, KS>;
     using F = Q2F<QT>;
     constexpr int BM = G::BM, WA = G::WA, STAGE = G::STAGE, A_BYTES = G::A_BYTES;
@@ -262,16 +263,26 @@ __global__ __launch_bounds__(256 * KS) void qmm2_kernel(const uint16_t* __restri
         using I1 = std::integral_constant<int, 1>;
         using I2 = std::integral_constant<int, 2>;
         using I3 = std::integral_constant<int, 3>;
-        const int kt0 = sb0 * 4, kt1 = sb1 * 4;
-        // prologue: stages kt0 .. kt0+2 (a split holds >= 4 k-tiles, so all real)
-        issue(kt0, sb0, sb0 & 1, I0{}, WLc{});
-        issue(kt0 + 1, sb0, 0, I1{}, WLc{});
-        issue(kt0 + 2, sb0, 0, I2{}, WLc{});
+        // the split's super-blocks are visited in a rotated order (v -> sb0 + (v + rot) % nv): workgroups that
+        // run side by side on one XCD (consecutive column tiles) then stream different k ranges of the shared
+        // A rows instead of all hitting the same 128-B lines (and L2 channels) at the same time
+        const int nv = sb1 - sb0;
+        const int rot = rot_mul ? (int)(((unsigned)ct * (unsigned)rot_mul) % (unsigned)nv) : 0;
+        auto phys = [&](int v) {
+            int p = v + rot;
+            if (p >= nv) p -= nv;
+            return sb0 + p;
+        };
+        // prologue: stages 0 .. 2 of the (virtual) k-tile sequence (a split holds >= 4 k-tiles, so all real)
+        const int p0 = phys(0);
+        issue(p0 * 4, p0, 0, I0{}, WLc{});
+        issue(p0 * 4 + 1, p0, 0, I1{}, WLc{});
+        issue(p0 * 4 + 2, p0, 0, I2{}, WLc{});
         q2_wait_barrier<cnt(I1{}, WLc{}) + cnt(I2{}, WLc{})>();
 
         Q2B<QT> bw;
         f16x8 af[2][WM];
-        bw.load_hdr(hdr_lds + (sb0 & 1) * G::HSZ + cg * F::HB, col);
+        bw.load_hdr(hdr_lds + cg * F::HB, col);
         bw.load_q(smem + b_rd, col, h);
 #pragma unroll
         for (int i = 0; i < WM; ++i) af[0][i] = *(const f16x8*)(smem + a_rd + i * 4096 + KH * 256);
@@ -279,17 +290,17 @@ __global__ __launch_bounds__(256 * KS) void qmm2_kernel(const uint16_t* __restri
         // one k-tile (ring slot JQ): the wave's k-steps KH, KH + KS, ...; the A fragments of the next k-step
         // (on the last one: of the next tile, slot JQ + 1, waited for at the top) are read while this
         // k-step's MFMAs run; the next tile's quant bytes (and header at a super-block edge) likewise
-        auto tile = [&](int sb, auto jq_c) {
+        auto tile = [&](int sb, auto jq_c) {  // sb: virtual super-block index
             constexpr int JQ = decltype(jq_c)::value;
             constexpr int NJ = (JQ + 1) & 3;
             const int kt = sb * 4 + JQ;
             // stage kt+1 landed (only stage kt+2 may still be in flight); every wave is past tile kt-1
             q2_wait_barrier<cnt(std::integral_constant<int, (JQ + 2) & 3>{}, WLc{})>();
             {
-                const int ki = kt + 3;
-                const bool real = ki < kt1;
-                issue(real ? ki : kt1 - 1, real ? (ki >> 2) : sb1 - 1, (ki >> 2) & 1,
-                      std::integral_constant<int, (JQ + 3) & 3>{}, WLc{});
+                const int ki = kt + 3, vi = ki >> 2;
+                const bool real = vi < nv;
+                const int ps = phys(real ? vi : nv - 1);
+                issue(ps * 4 + (real ? (ki & 3) : 3), ps, vi & 1, std::integral_constant<int, (JQ + 3) & 3>{}, WLc{});
             }
             bw.template prep<JQ>();
             Q2B<QT> bn = bw;
@@ -330,7 +341,7 @@ __global__ __launch_bounds__(256 * KS) void qmm2_kernel(const uint16_t* __restri
             // NSTEP is even: the next tile's first fragments are in af[0]
             bw = bn;
         };
-        for (int sb = sb0; sb < sb1; ++sb) {
+        for (int sb = 0; sb < nv; ++sb) {
             tile(sb, I0{});
             tile(sb, I1{});
             tile(sb, I2{});
@@ -439,7 +450,7 @@ static int launch_qmm2(const uint16_t* A, int lda, const uint8_t* W, int M, int 
         attr_set = true;
     }
     qmm2_kernel<QT, WM, KS, EPI><<<dim3((unsigned)nwg), 256 * KS, G::LDS, st>>>(A, lda, W, M, N, K, n_mt, splits, sbps,
-                                                                                C, ldc);
+                                                                                C, ldc, g_qmm2_rot);
     MXK_CHECK_LAUNCH();
 }
 
@@ -460,7 +471,7 @@ static int launch_dbg(int wm, const uint16_t* A, int lda, const uint8_t* W, int 
     auto go = [&](auto kern, int bm, int ks, int lds) {
         (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
         const int n_ct = (N + 127) / 128, n_mt = (M + bm - 1) / bm;
-        kern<<<dim3(n_ct * n_mt), 256 * ks, lds, st>>>(A, lda, W, M, N, K, n_mt, 1, K >> 8, C, ldc);
+        kern<<<dim3(n_ct * n_mt), 256 * ks, lds, st>>>(A, lda, W, M, N, K, n_mt, 1, K >> 8, C, ldc, g_qmm2_rot);
         return (int)hipGetLastError();
     };
     if (wm == 8) return go(qmm2_kernel<QT, 8, 1, EPI, DBG>, 256, 1, Q2Geom<QT, 8, 1>::LDS);
@@ -469,6 +480,11 @@ static int launch_dbg(int wm, const uint16_t* A, int lda, const uint8_t* W, int 
 }
 
 }  // namespace
+
+extern "C" int mxk_qmm2_set_rot(int r) {
+    g_qmm2_rot = r;
+    return 0;
+}
 
 // isolation builds of the Q4_K SwiGLU kernel (wm 8 / ks 1 and wm 4 / ks 2, no split), see DBG above
 extern "C" int mxk_qmm2_dbg(int dbg, int wm, const uint16_t* A, int lda, const uint8_t* W, int M, int N, int K, void* C,

@@ -104,6 +104,27 @@ def main():
                         L.qmatmul(Wt, x, epi, out, out_zeroed=True)
                     return f
                 cands["qmm2" + str(list(cfg))] = mk(cfg)
+            from localai_tfp_amd import _native as Nn
+            xp = torch.empty(M, K + 64, device=dev, dtype=torch.float16)[:, :K]
+            xp.copy_(x)
+
+            def run_rot():
+                L.QMM2_FORCE = auto
+                Nn.kcall("mxk_qmm2_set_rot", 7)
+                L.qmatmul(Wt, x, epi, out, out_zeroed=True)
+                Nn.kcall("mxk_qmm2_set_rot", 0)
+
+            def run_pad():
+                L.QMM2_FORCE = auto
+                L.qmatmul(Wt, xp, epi, out, out_zeroed=True)
+
+            cands["qmm2_rot"] = run_rot
+            cands["qmm2_pad"] = run_pad
+            # correctness of the rotated order
+            Nn.kcall("mxk_qmm2_set_rot", 7)
+            L.QMM2_FORCE = auto
+            errs["rot"] = round(err(), 6)
+            Nn.kcall("mxk_qmm2_set_rot", 0)
             L.QMM2_FORCE = None
             times = {k: [] for k in cands}
             for _ in range(rounds):
@@ -114,6 +135,8 @@ def main():
             res["qmm_r3_us"] = round(med.pop("qmm_r3"), 2)
             res["dense_f16_us"] = round(med.pop("dense_f16"), 2)
             res["qmm2_auto_us"] = round(med["qmm2" + str(list(auto))], 2)
+            res["qmm2_rot_us"] = round(med.pop("qmm2_rot"), 2)
+            res["qmm2_padlda_us"] = round(med.pop("qmm2_pad"), 2)
             best = min(med, key=med.get)
             res["qmm2_best"] = [best[4:], round(med[best], 2)]
             flops = 2.0 * M * N * K
