@@ -389,6 +389,7 @@ class LLMEngine:
                             and getattr(model, "remote", None) is None
                             and os.environ.get("MX_TP_OVERLAP", "1") != "0" if tp is not None else
                             c.overlap and not use_spec and not self.recurrent and getattr(model, "remote", None) is None)
+        self.sched.hold_host_state = self.overlap and os.environ.get("MX_OVERLAP_HOLD", "1") != "0"
         self._inflight = collections.deque()  # launched-but-unread steps, oldest first
         self._prev_dev = None  # (device int32 tokens of the last launched step, {rid: row})
         self._pin_tok = self._pin_lp = self._pin_in = None
@@ -606,19 +607,23 @@ class LLMEngine:
     def _overlap_params(self, p) -> bool:
         """Sampling the overlap pipeline can launch before the previous step's tokens reach the host: the
         simple chain, and repeat / presence / frequency penalties while at most one token per row is in
-        flight (overlap_depth 1: the kernel counts that pending token, ops/sampling.py pack)."""
+        flight (overlap_depth 1: the kernel counts that pending token, ops/sampling.py pack). Mirostat v2
+        rows are launched only with their previous token processed (scheduler hold_host_state)."""
         if p.mirostat == 2:
-            return False
+            return self.sched.hold_host_state
         return self._simple_params(p) or self.cfg.overlap_depth <= 1
 
+    def _overlap_row_ok(self, it) -> bool:
+        s = it.seq
+        if s.req.embedding or not self._overlap_params(s.params):
+            return False
+        # grammar rows: the scheduler holds them while a token is in flight, so their mask is current here
+        return s.grammar is None or (self.sched.hold_host_state and not s.n_pending)
+
     def _overlap_ok(self, so: SchedulerOutput) -> bool:
-        for it in so.decode:
-            if it.seq.grammar is not None or it.seq.req.embedding or not self._overlap_params(it.seq.params):
-                return False
-        for it in so.prefill:
-            if it.sample and (it.seq.grammar is not None or it.seq.req.embedding or not self._overlap_params(it.seq.params)):
-                return False
-        return True
+        if not all(self._overlap_row_ok(it) for it in so.decode):
+            return False
+        return all(self._overlap_row_ok(it) for it in so.prefill if it.sample)
 
     def _overlap_sample_args(self, items):
         """(histories, pend_tok, pend) for the overlap sampler: full histories only for penalty rows, and the
@@ -662,14 +667,18 @@ class LLMEngine:
                 tok_dev = am
             elif not logits.is_cuda:  # CPU reference sampler (host lists)
                 hist, ptok, pend = self._overlap_sample_args(items)
+                mask = self._grammar_mask(items, logits.shape[1]) if any(it.seq.grammar for it in items) else None
                 t, l = self.sampler.sample(logits, [it.seq.params for it in items], hist,
-                                           [it.seq.n_generated for it in items], None, None, ptok, pend)
+                                           [it.seq.n_generated for it in items], mask, None, ptok, pend)
                 tok_dev = torch.as_tensor(t, dtype=torch.int32)
                 lp_dev = torch.as_tensor(l, dtype=torch.float32) if l is not None else None
             else:
                 hist, ptok, pend = self._overlap_sample_args(items)
+                mask = self._grammar_mask(items, logits.shape[1]) if any(it.seq.grammar for it in items) else None
+                mus = ([it.seq.mirostat_mu for it in items] if any(it.seq.params.mirostat == 2 for it in items)
+                       else None)
                 tok_dev, lp_dev = self.sampler.sample(logits, [it.seq.params for it in items], hist,
-                                                      [it.seq.n_generated for it in items], None, None, ptok, pend)
+                                                      [it.seq.n_generated for it in items], mask, mus, ptok, pend)
             if self.tp is not None:
                 tok_dev = self._tp_bcast_tokens(tok_dev, len(items))
             k = self._pin_i

@@ -41,6 +41,12 @@ class SchedulerOutput:
         return len(self.decode) + sum(p.n for p in self.prefill)
 
 
+def needs_host_state(s: Sequence) -> bool:
+    """The next token's sampler input depends on host state advanced by the previous token: a grammar's
+    allowed-token mask, mirostat v2's running mu."""
+    return s.grammar is not None or s.params.mirostat == 2
+
+
 class Scheduler:
     def __init__(self, block_manager, block_size: int, max_num_seqs: int = 256, max_batched_tokens: int = 2048,
                  max_model_len: int = 8192, prefill_chunk: int | None = None):
@@ -55,6 +61,9 @@ class Scheduler:
         # finished sequences whose blocks a launched-but-unread step still writes (overlap mode):
         # released by release_deferred() once that step's results were processed
         self.deferred: list[Sequence] = []
+        # overlap mode: sequences whose next sample needs host state advanced by their previous token (a
+        # grammar, mirostat-2's mu) sit a step out while that token is in flight (engine sets this)
+        self.hold_host_state = False
 
     # ---------------------------------------------------------------- queue management
     def add(self, seq: Sequence):
@@ -94,8 +103,13 @@ class Scheduler:
 
     def _held(self, s: Sequence) -> bool:
         """A sequence whose in-flight samples already reach its length limits: its last step is on
-        the GPU, nothing more to schedule (overlap mode; never true when n_pending == 0)."""
-        return s.n_pending > 0 and (s.n_generated >= s.req.max_tokens or s.total_len >= self.max_model_len)
+        the GPU, nothing more to schedule; or (hold_host_state) one whose sampler state on the host waits
+        for its in-flight token (overlap mode; never true when n_pending == 0)."""
+        if not s.n_pending:
+            return False
+        if s.n_generated >= s.req.max_tokens or s.total_len >= self.max_model_len:
+            return True
+        return self.hold_host_state and needs_host_state(s)
 
     def _preempt(self, seq: Sequence, out: SchedulerOutput):
         if seq.n_pending:

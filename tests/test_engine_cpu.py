@@ -212,6 +212,39 @@ def test_penalties_stay_on_overlap_pipeline(model):
     assert e_ovl.stats.get("overlap_steps", 0) > 0 and e_ovl.stats.get("sync_steps", 0) == 0, e_ovl.stats
 
 
+def test_grammar_rows_stay_on_overlap_pipeline(model):
+    """Grammar-constrained rows mixed with plain rows: the overlap scheduler holds a grammar row while its
+    token is in flight (its mask needs that token), so its mask is always current when it is sampled and
+    the other rows never fall back to synchronous steps. Outputs equal the synchronous engine's."""
+    from localai_tfp_amd.runtime_native import GrammarMatcher, NativeGrammar, NativeVocab
+    tok = ByteTokenizer(model.cfg.vocab)
+    tb = [bytes([i]) if i < 256 else b"" for i in range(model.cfg.vocab)]
+    vocab = NativeVocab(tb)
+    g = NativeGrammar('root ::= "{" "\\"a\\"" ":" [0-9]{1,3} "}"')
+
+    def reqs():
+        rng = np.random.default_rng(11)
+        out = []
+        for i in range(8):
+            p = [int(x) for x in rng.integers(1, 250, size=int(rng.integers(5, 40)))]
+            if i % 2 == 0:
+                out.append(Request(p, SamplingParams(temperature=0.0), max_tokens=12,
+                                   grammar=lambda: GrammarMatcher(g, vocab, tb, tok.eos_token_id)))
+            else:
+                out.append(Request(p, SamplingParams(temperature=0.7, top_k=20, seed=i), max_tokens=12))
+        return out
+
+    e_sync, _ = mk(model, overlap=False, max_batched_tokens=64)
+    e_ovl, _ = mk(model, overlap=True, max_batched_tokens=64)
+    a = _run_all(e_sync, reqs())
+    b = _run_all(e_ovl, reqs())
+    assert a == b
+    for i in range(0, 8, 2):  # the grammar rows produced valid documents
+        txt = a[i][1]
+        assert txt.startswith('{"a":') and txt.endswith("}"), txt
+    assert e_ovl.stats.get("overlap_steps", 0) > e_ovl.stats.get("sync_steps", 0), e_ovl.stats
+
+
 @pytest.mark.parametrize("depth", [1, 3])
 def test_overlap_depth_matches_sync(model, depth):
     """Deeper overlap pipelines (several launched-but-unread steps) give the synchronous outputs too."""
