@@ -198,6 +198,8 @@ MX_DEV float glu_gate_f(float g) {
 // Q6_K: repacked at load time to a 16B-aligned 208 B block + a separate fp16 d plane (see quant.py)
 // Q8_0: repacked to an int8 plane [N][K] + fp16 d plane [N][K/32]
 enum MxQuantType : int {
+    MXQ_Q2_K = 10,
+    MXQ_Q3_K = 11,
     MXQ_Q4_K = 12,
     MXQ_Q6_K = 14,
     MXQ_Q8_0 = 8,

@@ -32,14 +32,31 @@ int g_qmm2_rot = 0;       // k-order rotation multiplier per column tile (0: nat
 template <int QT>
 struct Q2F;
 // Q4_K t32 unit (per 32-column group, per super-block): [hdr 32 x 16 B][quarter jq: chunk0, chunk1 (32 x 16 B)]
+// QB: quant bytes staged per group per k-tile (source unit offset qoff(JQ)); HB: header bytes per group per
+// super-block (staged with the super-block's first k-tile); QI / HI: LDS-DMA instructions for each.
 template <>
 struct Q2F<MXQ_Q4_K> {
-    static constexpr int UNIT = 4608, HB = 512, QOFF = 512, QB = 1024, QI = 1, HI = 1;
+    static constexpr int UNIT = 4608, HB = 512, QB = 1024, QI = 1, HI = 1;
+    static constexpr int qoff(int jq) { return 512 + jq * 1024; }
 };
 // Q6_K t32 unit: [sc 32 x 16 B][d 32 x 4 B][quarter jq: ql0, ql1, qh (32 x 16 B)]
 template <>
 struct Q2F<MXQ_Q6_K> {
-    static constexpr int UNIT = 6784, HB = 640, QOFF = 640, QB = 1536, QI = 2, HI = 2;
+    static constexpr int UNIT = 6784, HB = 640, QB = 1536, QI = 2, HI = 2;
+    static constexpr int qoff(int jq) { return 640 + jq * 1536; }
+};
+// Q3_K t32 unit: [hdr 32 x 16 B {scales[12], d}][hmask: 2 chunks x 32 x 16 B][qs half n: 2 chunks x 32 x 16 B];
+// k-tiles 2n, 2n+1 use qs half n (the 2-bit fields 0-1 / 2-3) -> header slot = hdr + hmask (1.5 KB)
+template <>
+struct Q2F<MXQ_Q3_K> {
+    static constexpr int UNIT = 3584, HB = 1536, QB = 1024, QI = 1, HI = 2;
+    static constexpr int qoff(int jq) { return 1536 + (jq >> 1) * 1024; }
+};
+// Q2_K t32 unit: [sc 32 x 16 B][dd 32 x 4 B {d, dmin}][qs half n: 2 chunks x 32 x 16 B]
+template <>
+struct Q2F<MXQ_Q2_K> {
+    static constexpr int UNIT = 2688, HB = 640, QB = 1024, QI = 1, HI = 2;
+    static constexpr int qoff(int jq) { return 640 + (jq >> 1) * 1024; }
 };
 
 template <int QT>
@@ -50,7 +67,7 @@ struct Q2B<MXQ_Q4_K> {
     u32x4 hd;
     u32x2 v0, v1;
     f16x2 sm[2];  // per sub-block of the k-tile: (scale, -dmin * min) as exact f16 products
-    MX_DEV void load_hdr(const char* hb, int col) { hd = *(const u32x4*)(hb + col * 16); }
+    MX_DEV void load_hdr(const char* hb, int col, int) { hd = *(const u32x4*)(hb + col * 16); }
     MX_DEV void load_q(const char* qb, int col, int h) {
         v0 = *(const u32x2*)(qb + col * 16 + 8 * h);
         v1 = *(const u32x2*)(qb + 512 + col * 16 + 8 * h);
@@ -68,7 +85,7 @@ struct Q2B<MXQ_Q4_K> {
             sm[i] = dn * q;
         }
     }
-    template <int S>
+    template <int JQ, int S>
     MX_DEV f16x8 frag() const {
         const u32x2 src = (S & 1) ? v1 : v0;
         constexpr int sh = 4 * (S >> 1);
@@ -95,7 +112,7 @@ struct Q2B<MXQ_Q6_K> {
     uint32_t dw;
     u32x2 v0, v1, vh;
     f16x2 s2[4];
-    MX_DEV void load_hdr(const char* hb, int col) {
+    MX_DEV void load_hdr(const char* hb, int col, int) {
         sc = *(const u32x4*)(hb + col * 16);
         dw = *(const uint32_t*)(hb + 512 + col * 4);
     }
@@ -115,7 +132,7 @@ struct Q2B<MXQ_Q6_K> {
             s2[i] = (f16x2){s, s};
         }
     }
-    template <int S>
+    template <int JQ, int S>
     MX_DEV f16x8 frag() const {
         const u32x2 src = (S & 1) ? v1 : v0;
         constexpr int sh = 4 * (S >> 1), qsh = 2 * S;
@@ -129,6 +146,111 @@ struct Q2B<MXQ_Q6_K> {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const f16x2 v = (p[i] - k) * s2[S];
+            r[2 * i] = v[0];
+            r[2 * i + 1] = v[1];
+        }
+        return r;
+    }
+};
+
+// Q3_K: code c = 2-bit field | hmask bit << 2 in [0, 7], weight = d * (sc - 32) * (c - 4). k-tile JQ: qs half
+// n = JQ >> 1, 2-bit fields j = 2 (JQ & 1) + (S >> 1); k-step S uses sub-block scale 4 JQ + S.
+template <>
+struct Q2B<MXQ_Q3_K> {
+    u32x4 hd;           // scales[12] (3 words) + d
+    u32x2 hm0, hm1;     // hmask bytes 8 h .. 8 h + 7 of chunks 0 / 1 (this lane's k)
+    u32x2 v0, v1;
+    f16x2 s2[4];
+    MX_DEV void load_hdr(const char* hb, int col, int h) {
+        hd = *(const u32x4*)(hb + col * 16);
+        hm0 = *(const u32x2*)(hb + 512 + col * 16 + 8 * h);
+        hm1 = *(const u32x2*)(hb + 1024 + col * 16 + 8 * h);
+    }
+    MX_DEV void load_q(const char* qb, int col, int h) {
+        v0 = *(const u32x2*)(qb + col * 16 + 8 * h);
+        v1 = *(const u32x2*)(qb + 512 + col * 16 + 8 * h);
+    }
+    template <int JQ>
+    MX_DEV void prep() {
+        // 16 6-bit scales from 12 bytes (ggml kmask unpack): word JQ of the unpacked array = scales 4 JQ .. 4 JQ + 3
+        constexpr uint32_t km1 = 0x03030303u, km2 = 0x0F0F0F0Fu;
+        uint32_t w;
+        if constexpr (JQ == 0) w = (hd[0] & km2) | ((hd[2] & km1) << 4);
+        else if constexpr (JQ == 1) w = (hd[1] & km2) | (((hd[2] >> 2) & km1) << 4);
+        else if constexpr (JQ == 2) w = ((hd[0] >> 4) & km2) | (((hd[2] >> 4) & km1) << 4);
+        else w = ((hd[1] >> 4) & km2) | (((hd[2] >> 6) & km1) << 4);
+        const _Float16 d = __builtin_bit_cast(f16x2, hd[3])[0];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int v = (int)((w >> (8 * i)) & 0xFF) - 32;
+            const _Float16 sv = d * (_Float16)v;  // 11 x 6 bits: exact product, one f16 rounding
+            s2[i] = (f16x2){sv, sv};
+        }
+    }
+    template <int JQ, int S>
+    MX_DEV f16x8 frag() const {
+        const u32x2 src = (S & 1) ? v1 : v0;
+        const u32x2 hm = (S & 1) ? hm1 : hm0;
+        constexpr int j = 2 * (JQ & 1) + (S >> 1), hb = 4 * (JQ >> 1) + j;
+        const uint32_t t0 = ((src[0] >> (2 * j)) & 0x03030303u) | (((hm[0] >> hb) & 0x01010101u) << 2);
+        const uint32_t t1 = ((src[1] >> (2 * j)) & 0x03030303u) | (((hm[1] >> hb) & 0x01010101u) << 2);
+        const f16x2 k = {(_Float16)1028.f, (_Float16)1028.f};  // 1024 magic + 4 code offset
+        f16x2 p[4];
+        magic4(t0, p[0], p[1]);
+        magic4(t1, p[2], p[3]);
+        f16x8 r;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const f16x2 v = (p[i] - k) * s2[S];
+            r[2 * i] = v[0];
+            r[2 * i + 1] = v[1];
+        }
+        return r;
+    }
+};
+
+// Q2_K: weight = d * (sc & 15) * q - dmin * (sc >> 4), q the 2-bit field j = 2 (JQ & 1) + (S >> 1) of qs half
+// JQ >> 1; k-step S uses sub-block byte 4 JQ + S.
+template <>
+struct Q2B<MXQ_Q2_K> {
+    u32x4 sc;
+    uint32_t dw;
+    u32x2 v0, v1;
+    f16x2 sm[4];
+    MX_DEV void load_hdr(const char* hb, int col, int) {
+        sc = *(const u32x4*)(hb + col * 16);
+        dw = *(const uint32_t*)(hb + 512 + col * 4);
+    }
+    MX_DEV void load_q(const char* qb, int col, int h) {
+        v0 = *(const u32x2*)(qb + col * 16 + 8 * h);
+        v1 = *(const u32x2*)(qb + 512 + col * 16 + 8 * h);
+    }
+    template <int JQ>
+    MX_DEV void prep() {
+        const f16x2 dd = __builtin_bit_cast(f16x2, dw);
+        const f16x2 dn = {dd[0], -dd[1]};
+        const uint32_t w = sc[JQ];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint32_t b = (w >> (8 * i)) & 0xFF;
+            const f16x2 q = {(_Float16)(int)(b & 15), (_Float16)(int)(b >> 4)};
+            sm[i] = dn * q;  // exact f16 products (11 x 4 bits)
+        }
+    }
+    template <int JQ, int S>
+    MX_DEV f16x8 frag() const {
+        const u32x2 src = (S & 1) ? v1 : v0;
+        constexpr int j = 2 * (JQ & 1) + (S >> 1);
+        const uint32_t t0 = (src[0] >> (2 * j)) & 0x03030303u, t1 = (src[1] >> (2 * j)) & 0x03030303u;
+        const f16x2 k = {(_Float16)1024.f, (_Float16)1024.f};
+        const f16x2 s2 = {sm[S][0], sm[S][0]}, m2 = {sm[S][1], sm[S][1]};
+        f16x2 p[4];
+        magic4(t0, p[0], p[1]);
+        magic4(t1, p[2], p[3]);
+        f16x8 r;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const f16x2 v = (p[i] - k) * s2 + m2;
             r[2 * i] = v[0];
             r[2 * i + 1] = v[1];
         }
@@ -229,7 +351,7 @@ __global__ __launch_bounds__(256 * KS) void qmm2_kernel(const uint16_t* __restri
                                              16, 0, 0);
         if constexpr (decltype(wl_c)::value && QII > 0) {
             const uint8_t* u = wg + (size_t)sbw * F::UNIT;
-            const uint8_t* qs = u + F::QOFF + JQ * F::QB;
+            const uint8_t* qs = u + F::qoff(JQ);
             char* qd = sb + A_BYTES + cg * F::QB;
             __builtin_amdgcn_global_load_lds((const void*)(qs + lane * 16), (MX_LDS void*)qd, 16, 0, 0);
             if constexpr (QT == MXQ_Q6_K) {
@@ -239,11 +361,18 @@ __global__ __launch_bounds__(256 * KS) void qmm2_kernel(const uint16_t* __restri
             }
             if constexpr (JQ == 0) {
                 char* hd = hdr_lds + hslot * G::HSZ + cg * F::HB;
-                if (lane < 32) __builtin_amdgcn_global_load_lds((const void*)(u + lane * 16), (MX_LDS void*)hd, 16, 0, 0);
-                if constexpr (QT == MXQ_Q6_K) {
+                if constexpr (QT == MXQ_Q3_K) {  // hdr (512 B) + hmask (1 KB): one full and one half instruction
+                    __builtin_amdgcn_global_load_lds((const void*)(u + lane * 16), (MX_LDS void*)hd, 16, 0, 0);
                     if (lane < 32)
-                        __builtin_amdgcn_global_load_lds((const void*)(u + 512 + lane * 4), (MX_LDS void*)(hd + 512), 4,
-                                                         0, 0);
+                        __builtin_amdgcn_global_load_lds((const void*)(u + 1024 + lane * 16), (MX_LDS void*)(hd + 1024),
+                                                         16, 0, 0);
+                } else {
+                    if (lane < 32) __builtin_amdgcn_global_load_lds((const void*)(u + lane * 16), (MX_LDS void*)hd, 16, 0, 0);
+                    if constexpr (QT == MXQ_Q6_K || QT == MXQ_Q2_K) {  // + the 32 x 4 B d (/ dmin) words
+                        if (lane < 32)
+                            __builtin_amdgcn_global_load_lds((const void*)(u + 512 + lane * 4), (MX_LDS void*)(hd + 512), 4,
+                                                             0, 0);
+                    }
                 }
             }
         }
@@ -282,7 +411,7 @@ __global__ __launch_bounds__(256 * KS) void qmm2_kernel(const uint16_t* __restri
 
         Q2B<QT> bw;
         f16x8 af[2][WM];
-        bw.load_hdr(hdr_lds + cg * F::HB, col);
+        bw.load_hdr(hdr_lds + cg * F::HB, col, h);
         bw.load_q(smem + b_rd, col, h);
 #pragma unroll
         for (int i = 0; i < WM; ++i) af[0][i] = *(const f16x8*)(smem + a_rd + i * 4096 + KH * 256);
@@ -317,7 +446,7 @@ __global__ __launch_bounds__(256 * KS) void qmm2_kernel(const uint16_t* __restri
 #pragma unroll
                     for (int i = 0; i < WM; ++i)
                         af[cur ^ 1][i] = *(const f16x8*)(smem + NJ * STAGE + a_rd + i * 4096 + KH * 256);
-                    if constexpr (NJ == 0) bn.load_hdr(hdr_lds + ((sb + 1) & 1) * G::HSZ + cg * F::HB, col);
+                    if constexpr (NJ == 0) bn.load_hdr(hdr_lds + ((sb + 1) & 1) * G::HSZ + cg * F::HB, col, h);
                     bn.load_q(smem + NJ * STAGE + b_rd, col, h);
                 }
                 f16x8 bf;
@@ -326,10 +455,10 @@ __global__ __launch_bounds__(256 * KS) void qmm2_kernel(const uint16_t* __restri
                     bf = __builtin_bit_cast(f16x8, (u32x4){r2[0], r2[1], r2[0] ^ (uint32_t)S, r2[1]});
                 } else {
                     switch (S) {
-                        case 0: bf = bw.template frag<0>(); break;
-                        case 1: bf = bw.template frag<1>(); break;
-                        case 2: bf = bw.template frag<2>(); break;
-                        default: bf = bw.template frag<3>(); break;
+                        case 0: bf = bw.template frag<JQ, 0>(); break;
+                        case 1: bf = bw.template frag<JQ, 1>(); break;
+                        case 2: bf = bw.template frag<JQ, 2>(); break;
+                        default: bf = bw.template frag<JQ, 3>(); break;
                     }
                 }
 #pragma unroll
@@ -502,7 +631,7 @@ extern "C" int mxk_qmm2_dbg(int dbg, int wm, const uint16_t* A, int lda, const u
     return (int)hipErrorInvalidValue;
 }
 
-// A f16 [M, K] (lda % 8 == 0, 16-B aligned), W t32 Q4_K / Q6_K [N, K] (N % 32 == 0, K % 256 == 0).
+// A f16 [M, K] (lda % 8 == 0, 16-B aligned), W t32 Q4_K / Q6_K / Q3_K / Q2_K [N, K] (N % 32 == 0, K % 256 == 0).
 // epi: 0 fp32 store, 1 f16 store, 2 fp32 accumulate (split-K via atomics when splits > 1), 3/4 SwiGLU /
 // GeGLU over 16-row interleaved gate|up -> f16 [M, N/2]. wm: 32-row MFMA blocks per wave (BM = 32 wm);
 // ks: 1 (4 waves) or 2 (8 waves, k-steps split per wave pair). splits: K split in whole super-blocks.
@@ -522,6 +651,8 @@ extern "C" int mxk_qmm2(int qtype, int epi, int wm, int ks, const uint16_t* A, i
     switch (qtype) {
         case MXQ_Q4_K: Q2_EPI(MXQ_Q4_K) break;
         case MXQ_Q6_K: Q2_EPI(MXQ_Q6_K) break;
+        case MXQ_Q3_K: Q2_EPI(MXQ_Q3_K) break;
+        case MXQ_Q2_K: Q2_EPI(MXQ_Q2_K) break;
     }
 #undef Q2_EPI
     return (int)hipErrorInvalidValue;

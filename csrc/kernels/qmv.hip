@@ -179,6 +179,85 @@ struct TUnit<MXQ_Q6_K> {
     }
 };
 
+// Q3_K t32 unit (3584 B): [hdr 32 x 16 B {scales[12], d}][hmask: 2 chunks x 32 x 16 B][qs half n = 0, 1: 2 chunks x
+// 32 x 16 B]. Lane half h takes bytes 16 h .. 16 h + 15 of every 32-byte run, i.e. elements 128 n + 32 j + 16 h + i:
+// 16 consecutive activations per (n, j), one q8 block half, sub-block scale 8 n + 2 j + h.
+template <>
+struct TUnit<MXQ_Q3_K> {
+    static constexpr int BYTES = 3584, ELEMS = 256;
+    u32x4 hd, hm, q[2];
+    MX_DEV void load(const uint8_t* u, int r, int h) {
+        hd = *(const u32x4*)(u + r * 16);
+        hm = __builtin_nontemporal_load((const u32x4*)(u + 512 + h * 512 + r * 16));
+#pragma unroll
+        for (int n = 0; n < 2; ++n) q[n] = __builtin_nontemporal_load((const u32x4*)(u + 1536 + n * 1024 + h * 512 + r * 16));
+    }
+    MX_DEV float dot(const int8_t* x, const float2* ds, int h) const {
+        constexpr uint32_t km1 = 0x03030303u, km2 = 0x0F0F0F0Fu;
+        const uint32_t sw[4] = {(hd[0] & km2) | ((hd[2] & km1) << 4), (hd[1] & km2) | (((hd[2] >> 2) & km1) << 4),
+                                ((hd[0] >> 4) & km2) | (((hd[2] >> 4) & km1) << 4),
+                                ((hd[1] >> 4) & km2) | (((hd[2] >> 6) & km1) << 4)};
+        const float d = half_to_f32(hd[3] & 0xFFFF);
+        float acc = 0.f;
+#pragma unroll
+        for (int n = 0; n < 2; ++n) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const u32x4 xv = *(const u32x4*)(x + 128 * n + 32 * j + 16 * h);
+                int is = 0;
+#pragma unroll
+                for (int w = 0; w < 4; ++w) {
+                    uint32_t c = ((q[n][w] >> (2 * j)) & 0x03030303u) | (((hm[w] >> (4 * n + j)) & 0x01010101u) << 2);
+                    c ^= 0x04040404u;                  // c - 4 as a 3-bit two's complement field
+                    c |= (c & 0x04040404u) * 62u;      // sign-extend bit 2 to the byte (no carry across bytes)
+                    is = __builtin_amdgcn_sdot4((int)c, (int)xv[w], is, false);
+                }
+                const int isx = 8 * n + 2 * j + h;
+                const int sc = (int)((sw[isx >> 2] >> (8 * (isx & 3))) & 0xFF) - 32;
+                acc += (float)sc * ds[4 * n + j].x * (float)is;
+            }
+        }
+        return d * acc;
+    }
+};
+
+// Q2_K t32 unit (2688 B): [sc 32 x 16 B][dd 32 x 4 B {d, dmin}][qs half n: 2 chunks x 32 x 16 B]; the lane split is
+// Q3_K's. The min term needs the 16-element activation sums: one sdot4 against ones per word.
+template <>
+struct TUnit<MXQ_Q2_K> {
+    static constexpr int BYTES = 2688, ELEMS = 256;
+    u32x4 sc, q[2];
+    uint32_t dw;
+    MX_DEV void load(const uint8_t* u, int r, int h) {
+        sc = *(const u32x4*)(u + r * 16);
+        dw = *(const uint32_t*)(u + 512 + r * 4);
+#pragma unroll
+        for (int n = 0; n < 2; ++n) q[n] = __builtin_nontemporal_load((const u32x4*)(u + 640 + n * 1024 + h * 512 + r * 16));
+    }
+    MX_DEV float dot(const int8_t* x, const float2* ds, int h) const {
+        float acc = 0.f, mins = 0.f;
+#pragma unroll
+        for (int n = 0; n < 2; ++n) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const u32x4 xv = *(const u32x4*)(x + 128 * n + 32 * j + 16 * h);
+                int is = 0, xs = 0;
+#pragma unroll
+                for (int w = 0; w < 4; ++w) {
+                    is = __builtin_amdgcn_sdot4((int)((q[n][w] >> (2 * j)) & 0x03030303u), (int)xv[w], is, false);
+                    xs = __builtin_amdgcn_sdot4(0x01010101, (int)xv[w], xs, false);
+                }
+                const int isx = 8 * n + 2 * j + h;
+                const uint32_t b = (sc[isx >> 2] >> (8 * (isx & 3))) & 0xFF;
+                const float dx = ds[4 * n + j].x;
+                acc += (float)(b & 15) * dx * (float)is;
+                mins += (float)(b >> 4) * dx * (float)xs;
+            }
+        }
+        return half_to_f32(dw & 0xFFFF) * acc - half_to_f32(dw >> 16) * mins;
+    }
+};
+
 template <>
 struct TUnit<MXQ_Q8_0> {
     static constexpr int BYTES = 2176, ELEMS = 64;
@@ -418,6 +497,27 @@ __global__ __launch_bounds__(256) void dequant_t32_kernel(const uint8_t* __restr
             if constexpr (QT == MXQ_MX5F) qv |= (int)((hb >> i) & 1) << 4;
             v[i] = s * (float)qv + m;
         }
+    } else if constexpr (QT == MXQ_Q3_K || QT == MXQ_Q2_K) {
+        // element e = 128 n + 32 j + 16 half + i (4 consecutive i per lane)
+        constexpr int UB = QT == MXQ_Q3_K ? 3584 : 2688, QO = QT == MXQ_Q3_K ? 1536 : 640;
+        const uint8_t* base = W + ((size_t)g * (K / 256) + chunk) * UB;
+        const int n = e >> 7, j = (e >> 5) & 3, half = (e >> 4) & 1, i0 = e & 15;
+        const uint32_t qq = *(const uint32_t*)(base + QO + n * 1024 + half * 512 + r * 16 + i0) >> (2 * j);
+        const int isx = 8 * n + 2 * j + half;
+        if constexpr (QT == MXQ_Q3_K) {
+            const uint32_t hm = *(const uint32_t*)(base + 512 + half * 512 + r * 16 + i0) >> (4 * n + j);
+            const uint8_t* sc = base + r * 16;
+            const int lo = (isx < 8 ? sc[isx] : sc[isx - 8] >> 4) & 15;
+            const int hi = (sc[8 + (isx & 3)] >> (2 * (isx >> 2))) & 3;
+            const float d = half_to_f32(*(const uint16_t*)(base + r * 16 + 12)) * (float)((lo | (hi << 4)) - 32);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) v[i] = d * (float)((int)(((qq >> (8 * i)) & 3) | (((hm >> (8 * i)) & 1) << 2)) - 4);
+        } else {
+            const uint32_t b = base[r * 16 + isx], dw = *(const uint32_t*)(base + 512 + r * 4);
+            const float d = half_to_f32(dw & 0xFFFF) * (float)(b & 15), m = half_to_f32(dw >> 16) * (float)(b >> 4);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) v[i] = d * (float)((qq >> (8 * i)) & 3) - m;
+        }
     } else {
         const uint8_t* base = W + ((size_t)g * (K / 256) + chunk) * 6784;
         const int jq = e >> 6, u = e & 63, b = u & 31, s16 = u >> 4;
@@ -492,6 +592,8 @@ extern "C" int mxk_qmv(int qtype, int epi, const int8_t* xq, const float2* xds, 
         case MXQ_Q8_0: QMV_EPI(MXQ_Q8_0) break;
         case MXQ_MX4F: QMV_EPI(MXQ_MX4F) break;
         case MXQ_MX5F: QMV_EPI(MXQ_MX5F) break;
+        case MXQ_Q3_K: QMV_EPI(MXQ_Q3_K) break;
+        case MXQ_Q2_K: QMV_EPI(MXQ_Q2_K) break;
     }
 #undef QMV_EPI
 #undef QMV_M
@@ -525,6 +627,8 @@ extern "C" int mxk_qmv_x(int qtype, int epi, int src, const void* x, int ldx, co
         case MXQ_Q8_0: QMVX_EPI(MXQ_Q8_0) break;
         case MXQ_MX4F: QMVX_EPI(MXQ_MX4F) break;
         case MXQ_MX5F: QMVX_EPI(MXQ_MX5F) break;
+        case MXQ_Q3_K: QMVX_EPI(MXQ_Q3_K) break;
+        case MXQ_Q2_K: QMVX_EPI(MXQ_Q2_K) break;
     }
 #undef QMVX_EPI
 #undef QMVX_M
@@ -545,6 +649,8 @@ extern "C" int mxk_dequant_t32(int qtype, const uint8_t* W, const int* rows, int
             case MXQ_Q8_0: dequant_t32_kernel<MXQ_Q8_0, F16><<<grid, 256, 0, st>>>(W, rows, K, ob, of, ldo); break;
             case MXQ_MX4F: dequant_t32_kernel<MXQ_MX4F, F16><<<grid, 256, 0, st>>>(W, rows, K, ob, of, ldo); break;
             case MXQ_MX5F: dequant_t32_kernel<MXQ_MX5F, F16><<<grid, 256, 0, st>>>(W, rows, K, ob, of, ldo); break;
+            case MXQ_Q3_K: dequant_t32_kernel<MXQ_Q3_K, F16><<<grid, 256, 0, st>>>(W, rows, K, ob, of, ldo); break;
+            case MXQ_Q2_K: dequant_t32_kernel<MXQ_Q2_K, F16><<<grid, 256, 0, st>>>(W, rows, K, ob, of, ldo); break;
             default: rc = (int)hipErrorInvalidValue;
         }
     });

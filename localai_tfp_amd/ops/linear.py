@@ -74,7 +74,7 @@ class QWeight:
             raw, qt = Q.to_mxf(raw, qt, N_, K)  # exact: 4/5-bit codes + f16 scale/offset per 32
         if qt in Q.T32_ONLY and not t32_only_ok and K % 256 == 0:
             raw, qt = Q.to_q8_0(raw, qt, N_, K), QType.Q8_0  # no t32 tiling possible: Q8_0 kernels
-        if qt in (*Q.Q8_EXACT, *Q.Q8_REQUANT) and K % 256 == 0:
+        if qt in (*Q.Q8_EXACT, *Q.Q8_REQUANT) and qt not in Q.T32_ONLY and K % 256 == 0:
             # no dedicated layout for this block format: carried on the Q8_0 kernels, never densified
             raw, qt = Q.to_q8_0(raw, qt, N_, K), QType.Q8_0
         if qt in Q.GPU_NATIVE and K % 256 == 0:
@@ -327,7 +327,7 @@ def _qmatmul_t32(W: QWeight, x, epi: int, out, xq, xds, M: int, out_zeroed: bool
     can_split = epi == EPI_ADD_F32 or (epi == EPI_F32 and out_zeroed)
     if W.bf16_cache is not None and M >= dense_min_m(x.dtype, epi, can_split) and W.bf16_cache.dtype == x.dtype:
         return _dense_cached(W, x, epi, out, M)
-    if QMM2 and int(W.qtype) in QMM2_QTYPES and M >= QMM2_MIN_M:
+    if (QMM2 and int(W.qtype) in QMM2_QTYPES and M >= QMM2_MIN_M) or int(W.qtype) in QMM2_ONLY:
         wm, ks, splits = _qmm2_shape(M, W.N, W.K, can_split)
         e = EPI_ADD_F32 if (epi == EPI_F32 and splits > 1) else epi
         if e in (EPI_BF16, *GLU_EPIS):
@@ -549,7 +549,8 @@ def _qmm_shape(M: int, N_: int, K: int, can_split: bool):
 QMM2 = os.environ.get("MX_QMM2", "0") != "0"
 QMM2_FORCE: tuple | None = None  # (wm, ks, splits) override for tuning (tools/tune_qmm2.py)
 QMM2_CONFIGS = ((2, 1), (2, 2), (4, 1), (4, 2), (6, 1), (8, 1), (8, 2))
-QMM2_QTYPES = (int(QType.Q4_K), int(QType.Q6_K))
+QMM2_QTYPES = (int(QType.Q4_K), int(QType.Q6_K), int(QType.Q3_K), int(QType.Q2_K))
+QMM2_ONLY = tuple(int(q) for q in Q.QMM2_ONLY)  # no qmm.hip variant: qmm2 for every M > 4
 QMM2_MIN_M = int(os.environ.get("MX_QMM2_MIN_M", "16"))
 
 

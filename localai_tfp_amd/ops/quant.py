@@ -467,6 +467,20 @@ def quantize_q5_k(x: np.ndarray) -> np.ndarray:
 QUANTIZERS = {QType.Q4_0: quantize_q4_0, QType.Q4_K: quantize_q4_k, QType.Q6_K: quantize_q6_k, QType.Q8_0: quantize_q8_0, QType.Q5_K: quantize_q5_k}
 
 
+def _pack_q3k_scales(sc: np.ndarray) -> np.ndarray:
+    """16 6-bit Q3_K scale codes per block -> the 12 packed bytes (inverse of dq_q3_k's kmask unpack)."""
+    sc = sc.astype(np.uint32)
+    lo = sc & 0xF
+    hi = (sc >> 4) & 0x3
+    out = np.zeros((sc.shape[0], 12), np.uint8)
+    # bytes 0..7: low nibbles (scales 0..7 in the low nibble, 8..15 in the high nibble of the same byte)
+    out[:, 0:8] = (lo[:, 0:8] | (lo[:, 8:16] << 4)).astype(np.uint8)
+    # bytes 8..11: 2-bit high parts; byte 8 + i holds scales i, 4 + i, 8 + i, 12 + i at bits 0, 2, 4, 6
+    for i in range(4):
+        out[:, 8 + i] = (hi[:, i] | (hi[:, 4 + i] << 2) | (hi[:, 8 + i] << 4) | (hi[:, 12 + i] << 6)).astype(np.uint8)
+    return out
+
+
 def random_quantized(rng: np.random.Generator, qtype: int, n_rows: int, row_len: int, std: float = 0.02) -> np.ndarray:
     """Random-init blocks directly in the quantised domain (valid scales, uniform codes) with
     element std ~= `std`. Used for multi-GB synthetic checkpoints (quantising 8B fp32 weights
@@ -500,6 +514,21 @@ def random_quantized(rng: np.random.Generator, qtype: int, n_rows: int, row_len:
         d = np.full(nb, std / (60 * 18.5), np.float32)  # q-32 uniform in [-32,31]: std 18.5
         out[:, 192:208] = sc.view(np.uint8)
         out[:, 208:210] = d.astype(np.float16).view(np.uint8).reshape(-1, 2)
+        return out.reshape(-1)
+    if q == QType.Q3_K:  # value = d * (sc - 32) * (q - 4 + 4 h), code uniform in [-4, 3] (std 2.29)
+        out = rng.integers(0, 256, size=(nb, 110), dtype=np.uint8)
+        sc = rng.integers(40, 64, size=(nb, 16)).astype(np.uint32)  # 6-bit codes, (sc - 32) in [8, 31]
+        out[:, 96:108] = _pack_q3k_scales(sc)
+        d = np.full(nb, std / (20 * 2.29), np.float32)
+        out[:, 108:110] = d.astype(np.float16).view(np.uint8).reshape(-1, 2)
+        return out.reshape(-1)
+    if q == QType.Q2_K:  # value = d * (sc & 15) * q - dmin * (sc >> 4), q uniform in 0..3 (std 1.12)
+        out = rng.integers(0, 256, size=(nb, 84), dtype=np.uint8)
+        s4 = rng.integers(8, 16, size=(nb, 16)).astype(np.uint8)
+        out[:, 0:16] = s4 | (s4 << 4)  # min code = scale code: centred around q = 1.5 with dmin = 1.5 d
+        d = np.full(nb, std / (12 * 1.12), np.float32)
+        out[:, 80:82] = d.astype(np.float16).view(np.uint8).reshape(-1, 2)
+        out[:, 82:84] = (d * 1.5).astype(np.float16).view(np.uint8).reshape(-1, 2)
         return out.reshape(-1)
     if q == QType.Q8_0:
         out = rng.integers(0, 256, size=(nb, 34), dtype=np.uint8)
@@ -552,10 +581,13 @@ def repack_q8_0(raw: np.ndarray, n_rows: int, row_len: int):
     return np.ascontiguousarray(qs), np.ascontiguousarray(d)
 
 
-GPU_NATIVE = (QType.Q4_K, QType.Q6_K, QType.Q8_0, QType.Q5_K, QType.MX4F, QType.MX5F)
-# native only in the t32 tiled layout (qmv / qmm / qmm8 / dequant_t32 kernels); a weight of these formats that
-# cannot be tiled (N % 32, expert stacks) is carried on the Q8_0 kernels instead (QWeight.ensure_kernel_layout)
-T32_ONLY = (QType.Q5_K, QType.MX4F, QType.MX5F)
+GPU_NATIVE = (QType.Q4_K, QType.Q6_K, QType.Q8_0, QType.Q5_K, QType.MX4F, QType.MX5F, QType.Q3_K, QType.Q2_K)
+# native only in the t32 tiled layout (qmv / qmm / qmm2 / qmm8 / dequant_t32 kernels); a weight of these formats
+# that cannot be tiled (N % 32, expert stacks) is carried on the Q8_0 kernels instead (QWeight.ensure_kernel_layout;
+# Q3_K exactly, Q2_K re-quantised)
+T32_ONLY = (QType.Q5_K, QType.MX4F, QType.MX5F, QType.Q3_K, QType.Q2_K)
+# formats whose M > 4 GEMM is qmm2.hip only (no qmm.hip variant)
+QMM2_ONLY = (QType.Q3_K, QType.Q2_K)
 QMM8_ONLY = (QType.Q5_K,)  # M > 4 through the int8-MFMA GEMM on Q8_K activations (no f16 qmm variant)
 
 # Block formats without a dedicated kernel layout yet, carried on the Q8_0 kernels (qmm / qmv) instead of
@@ -608,7 +640,7 @@ def to_q8_0(raw: np.ndarray, qtype: int, n_rows: int, row_len: int) -> np.ndarra
 def repack_for_gpu(raw: np.ndarray, qtype: int, n_rows: int, row_len: int):
     """-> (data uint8 [n_rows, bytes_per_row], dplane uint16 [n_rows, x] or None)."""
     q = QType(qtype)
-    if q in (QType.Q4_K, QType.Q5_K, QType.MX4F, QType.MX5F):
+    if q in (QType.Q4_K, QType.Q5_K, QType.MX4F, QType.MX5F, QType.Q3_K, QType.Q2_K):
         return np.ascontiguousarray(np.asarray(raw).reshape(n_rows, -1)), None
     if q == QType.Q6_K:
         return repack_q6_k(raw, n_rows, row_len)
@@ -618,7 +650,7 @@ def repack_for_gpu(raw: np.ndarray, qtype: int, n_rows: int, row_len: int):
 
 
 T32_UNIT = {QType.Q4_K: (4608, 256), QType.Q6_K: (6784, 256), QType.Q8_0: (2176, 64), QType.Q5_K: (5632, 256),
-            QType.MX4F: (5120, 256), QType.MX5F: (6144, 256)}
+            QType.MX4F: (5120, 256), QType.MX5F: (6144, 256), QType.Q3_K: (3584, 256), QType.Q2_K: (2688, 256)}
 
 
 def tile32(data, dplane, qtype: int, n_rows: int, row_len: int):
@@ -661,6 +693,24 @@ def tile32(data, dplane, qtype: int, n_rows: int, row_len: int):
             qh8 = body[..., 32:].permute(0, 2, 3, 1, 4).reshape(G, nb, 4, 256)
             codes = torch.cat([codes, qh8], 3)
         out = torch.cat([hdr, codes.reshape(G, nb, -1)], 2)
+    elif q == QType.Q3_K:
+        # ggml {hmask[32], qs[64], scales[12], d} -> [hdr: 32 x 16 B {scales[12], d, pad}]
+        # [hmask: 2 chunks x 32 x 16 B][qs half n = 0, 1: 2 chunks x 32 x 16 B]
+        nb = row_len // 256
+        b = t.reshape(G, 32, nb, 110)
+        hdr = torch.cat([b[..., 96:110], torch.zeros_like(b[..., 0:2])], 3).permute(0, 2, 1, 3).reshape(G, nb, 512)
+        hm = b[..., 0:32].reshape(G, 32, nb, 2, 16).permute(0, 2, 3, 1, 4).reshape(G, nb, 1024)
+        qs = b[..., 32:96].reshape(G, 32, nb, 2, 2, 16).permute(0, 2, 3, 4, 1, 5).reshape(G, nb, 2048)
+        out = torch.cat([hdr, hm, qs], 2)
+    elif q == QType.Q2_K:
+        # ggml {scales[16], qs[64], d, dmin} -> [sc: 32 x 16 B][dd: 32 x 4 B {d, dmin}]
+        # [qs half n = 0, 1: 2 chunks x 32 x 16 B]
+        nb = row_len // 256
+        b = t.reshape(G, 32, nb, 84)
+        sc = b[..., 0:16].permute(0, 2, 1, 3).reshape(G, nb, 512)
+        dd = b[..., 80:84].permute(0, 2, 1, 3).reshape(G, nb, 128)
+        qs = b[..., 16:80].reshape(G, 32, nb, 2, 2, 16).permute(0, 2, 3, 4, 1, 5).reshape(G, nb, 2048)
+        out = torch.cat([sc, dd, qs], 2)
     elif q == QType.Q6_K:
         nb = row_len // 256
         b = t.reshape(G, 32, nb, 208)

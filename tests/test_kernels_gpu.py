@@ -22,6 +22,10 @@ def rel(a, b):
 
 def make_w(qt, n, k, seed=0):
     rng = np.random.default_rng(seed)
+    if QType(qt) not in Q.QUANTIZERS:  # Q2_K / Q3_K: random blocks in the quantised domain
+        raw = Q.random_quantized(rng, int(qt), n, k, std=0.05)
+        dense = Q.dequantize(raw, qt, (k, n))
+        return raw.reshape(n, -1), torch.from_numpy(dense)
     x = rng.standard_normal((n, k), dtype=np.float32) * 0.05
     raw = Q.QUANTIZERS[QType(qt)](x)
     dense = Q.dequantize(raw, qt, (k, n))
@@ -429,7 +433,7 @@ def test_qmm(qt, M, wm, wn, nw, ks, splits, monkeypatch):
     assert rel(sw, ref_sw) < 1e-2
 
 
-@pytest.mark.parametrize("qt", [QType.Q4_K, QType.Q6_K])
+@pytest.mark.parametrize("qt", [QType.Q4_K, QType.Q6_K, QType.Q3_K, QType.Q2_K])
 @pytest.mark.parametrize("M,wm,ks,splits", [
     (64, 2, 1, 1), (64, 2, 2, 3), (17, 2, 2, 1), (128, 4, 2, 1), (77, 4, 2, 2), (128, 4, 1, 4), (200, 6, 1, 1),
     (256, 8, 1, 1), (300, 8, 1, 3), (256, 8, 2, 2), (511, 8, 1, 1), (100, 2, 1, 5)])
@@ -498,7 +502,7 @@ def test_qmatmul_llama3_8b_shapes(name, qt, n, k, epi, M):
     assert rel(out, ref) < 5e-3
 
 
-@pytest.mark.parametrize("qt", [QType.Q4_K, QType.Q6_K, QType.Q8_0, QType.Q5_K])
+@pytest.mark.parametrize("qt", [QType.Q4_K, QType.Q6_K, QType.Q8_0, QType.Q5_K, QType.Q3_K, QType.Q2_K])
 @pytest.mark.parametrize("M", [1, 2, 3, 4])
 def test_qmv_t32(qt, M):
     """qmv.hip decode GEMV on t32 weights (q8 activations) for every epilogue, and the t32 row
