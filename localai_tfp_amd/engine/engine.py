@@ -57,15 +57,18 @@ def _gc_cb(phase, info):
 
 
 def gc_tune():
+    """Called at engine start-up and after graph capture: collect + freeze what is alive, then count only
+    the collections that happen while serving (the start-up collection itself walks every object created
+    by model loading and is not a serving pause)."""
     import gc
     import os
+    if os.environ.get("MX_GC_TUNE", "1") != "0":
+        gc.collect()
+        gc.freeze()
+        gc.set_threshold(50_000, 50, 1000)
+    GC_STATS.update(gc_s=0.0, gc_n=0, gc_max_ms=0.0)
     if _gc_cb not in gc.callbacks:
         gc.callbacks.append(_gc_cb)
-    if os.environ.get("MX_GC_TUNE", "1") == "0":
-        return
-    gc.collect()
-    gc.freeze()
-    gc.set_threshold(50_000, 50, 1000)
 
 
 @dataclass
