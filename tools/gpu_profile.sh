@@ -1,0 +1,47 @@
+#!/bin/bash
+# The one documented profiling entry point (run on the GPU box through gpurun; writes under gpurun_out/,
+# copy the summaries you want to keep into profiles/):
+#
+#   bash tools/gpu_profile.sh engine [CONC] [STEPS]   rocprofv3 kernel trace of the in-process engine bench at
+#                                                    concurrency CONC (default 128): per-kernel table per step
+#   bash tools/gpu_profile.sh pmc SHAPE M CFG          counter passes (MFMA / VALU / LDS / waits) of one qmm2
+#                                                    configuration "wm,ks,splits" on a Llama-3-8B projection
+#   bash tools/gpu_profile.sh gemm [MS] [SHAPES]       qmm2 vs round-3 qmm vs hipBLASLt-on-dense sweep (JSONL)
+#
+# Every GPU step runs under its own timeout; counter passes stay within the per-block slot limits (8 SQ).
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}/gpurun_out
+mkdir -p "$R"
+export PYTHONUNBUFFERED=1 PYTHONPATH=${GRAFT_REPO_ROOT:-$(pwd)}
+ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
+mode=$1; shift
+case "$mode" in
+  engine)
+    conc=${1:-128}; steps=${2:-40}
+    cd /tmp && export TMPDIR=/tmp
+    timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$R/prof_engine_c$conc" -o run --output-format csv -- \
+      python3 "$ROOT/bench.py" --path engine --concurrency "$conc" --steps "$steps" --warmup 5 > "$R/prof_engine_c$conc.log" 2>&1 || exit 1
+    cd "$ROOT" && python tools/prof_summary.py "$R/prof_engine_c$conc" --top 40 --steps "$steps" > "$R/prof_engine_c$conc.md"
+    tail -45 "$R/prof_engine_c$conc.md"
+    ;;
+  pmc)
+    shape=$1; M=$2; cfg=$3; t=$(echo "$cfg" | tr , _)
+    P1="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU"
+    P2="SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_INSTS_MFMA SQ_INSTS_SALU SQ_WAVES GRBM_GUI_ACTIVE GRBM_COUNT"
+    cd /tmp && export TMPDIR=/tmp
+    for p in 1 2; do
+      eval PP=\$P$p
+      timeout -s KILL 90 rocprofv3 --pmc $PP -d "$R/pmc_${shape}_${M}_${t}_$p" -o run --output-format csv -- \
+        python3 "$ROOT/tools/prof_qmm.py" --shape "$shape" --M "$M" --q2 "$cfg" --iters 5 > "$R/pmc_${shape}_${M}_${t}_$p.log" 2>&1 || exit 1
+    done
+    cd "$ROOT" && python tools/pmc_summary.py "$R"/pmc_${shape}_${M}_${t}_* > "$R/pmc_${shape}_${M}_${t}.md"
+    cat "$R/pmc_${shape}_${M}_${t}.md"
+    ;;
+  gemm)
+    MS=${1:-128,256,512} SHAPES=${2:-gate_up,qkv,wo,down,down_q6} FULL=${FULL:-0} \
+      timeout -k 10 600 python -u tools/tune_qmm2.py > "$R/tune_qmm2.jsonl" || exit 1
+    cat "$R/tune_qmm2.jsonl"
+    ;;
+  *)
+    sed -n 2,12p "$0"; exit 2 ;;
+esac
