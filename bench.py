@@ -63,6 +63,9 @@ def parse():
                     help="tensor-parallel ranks per serving replica (BASELINE config #3: --model llama3-70b "
                          "--gpus 8 --tp 8); world = dp x tp, rank 0 of every group leads")
     ap.add_argument("--no-tp-check", action="store_true", help="skip the TP-vs-unsharded logits self-check")
+    ap.add_argument("--tp-rehearsal", type=int, default=0,
+                    help="one process runs rank 0's shard of a TP=N model with the collectives as no-ops: the "
+                         "per-GPU compute of a TP step on one GPU (config #3 readiness; communication excluded)")
     ap.add_argument("--tokenizer", default="bpe", choices=["bpe", "byte"],
                     help="bpe: a synthetic Llama-3-sized byte-level BPE vocabulary (128,256 ids, tokenizer/synth_bpe.py) "
                          "served through the GGUF BPE tokenizer; byte: one token per byte (no detokenisation work)")
@@ -189,6 +192,9 @@ def main():
         cfg = C.tiny_config(hidden=512, ffn=1024, n_heads=8, n_kv_heads=2)
     tp, link, tp_group, dp = args.tp, None, None, world
     tp_rel = None
+    rehearsal = args.tp_rehearsal
+    if rehearsal and (world > 1 or tp > 1):
+        raise SystemExit("--tp-rehearsal runs one process (no --tp, no torchrun)")
     if tp > 1:
         link, tp_group, dist_leaders, dp = setup_tp(args, world, rank, dev)
         if not args.no_tp_check:
@@ -204,8 +210,11 @@ def main():
                       flush=True)
         dist = dist_leaders  # bench barriers / reductions run among the replica leaders only
     t0 = time.time()
-    src = synthetic_source(cfg, "Q4_K_M", seed=1, shard_gen=tp > 1)
-    model = LlamaModel.load(cfg, src, dev, rank % tp, tp, tp_group)
+    src = synthetic_source(cfg, "Q4_K_M", seed=1, shard_gen=tp > 1 or rehearsal > 1)
+    if rehearsal > 1:
+        model = LlamaModel.load(cfg, src, dev, 0, rehearsal, None)
+    else:
+        model = LlamaModel.load(cfg, src, dev, rank % tp, tp, tp_group)
     t_load = time.time() - t0
     if args.tokenizer == "bpe" and cfg.vocab != 128256:  # CPU plumbing model / other vocabularies
         args.tokenizer = "byte"
@@ -276,7 +285,8 @@ def main():
                 "model": cfg.name + " Q4_K_M", "global_batch": args.concurrency * dp,
                 "seq_len": args.prompt_len + args.gen_len, "prompt_len": args.prompt_len, "gen_len": args.gen_len,
                 "concurrency_per_replica": args.concurrency,
-                "parallelism": f"dp{dp}" if tp == 1 else (f"tp{tp}" if dp == 1 else f"dp{dp}xtp{tp}"),
+                "parallelism": (f"tp{rehearsal}-rehearsal (rank 0 shard on 1 GPU, collectives no-op)" if rehearsal > 1 else
+                                f"dp{dp}" if tp == 1 else (f"tp{tp}" if dp == 1 else f"dp{dp}xtp{tp}")),
                 **({"tp_selfcheck_rel_err": tp_rel} if tp_rel is not None else {}),
                 "path": ("HTTP /v1/chat/completions (SSE) -> FastAPI gateway -> mxstream (batched gRPC-side channel) -> LLM worker engine" if args.path == "http"
                          else "engine in-process (gateway/gRPC excluded)"),

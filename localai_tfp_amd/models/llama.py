@@ -513,7 +513,9 @@ class LlamaModel:
         """Collective over the TP group (call on every rank, outside graph capture): small row-parallel
         all-reduces go through the one-shot hipIpc kernel (parallel/custom_ar.py). MX_CUSTOM_AR=0 disables."""
         import os
-        if self.tp_size <= 1 or self.device.type != "cuda" or os.environ.get("MX_CUSTOM_AR", "1") == "0":
+        import torch.distributed as dist
+        if (self.tp_size <= 1 or self.device.type != "cuda" or os.environ.get("MX_CUSTOM_AR", "1") == "0"
+                or not dist.is_initialized()):  # (single-process shard rehearsal: collectives are no-ops)
             return None
         from ..parallel.custom_ar import OneShotAllReduce
         self.custom_ar = OneShotAllReduce(self.tp_group, self.device, max_bytes)

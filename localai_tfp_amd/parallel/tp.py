@@ -59,6 +59,11 @@ def shard_vec(v: torch.Tensor, n: int, rank: int, size: int) -> torch.Tensor:
 
 
 def all_reduce_(t: torch.Tensor, group=None):
+    """In-place sum over the TP group. Without an initialised process group (a single-process rehearsal of
+    one rank's shard, bench.py --tp-rehearsal) the collective is a no-op: the shard's compute runs at full
+    size, the communication is left out and reported separately."""
     import torch.distributed as dist
+    if not dist.is_initialized():
+        return t
     dist.all_reduce(t, group=group)
     return t
