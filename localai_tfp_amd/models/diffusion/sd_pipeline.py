@@ -4,6 +4,13 @@ the diffusers backend's StableDiffusionPipeline / StableDiffusionXLPipeline
 (backend/python/diffusers/backend.py:169-191) and sd.cpp's txt2img (gosd.cpp:164-226: cfg scale,
 steps, seed, sampler / schedule, CLIP skip).
 
+Depth-to-image (the reference's StableDiffusionDepth2ImgPipeline, backend.py:172-173): a UNet with one
+input channel more than the VAE latent (SD 2 depth: 5) gets, next to the noisy latent, the source image's
+depth map — a DPT depth estimator (transformers DPTForDepthEstimation, the pipeline's depth_estimator/)
+run on the image resized to its feature-extractor size, resampled to the latent grid (bicubic) and
+normalised to [-1, 1] per image; the latent itself starts from the noised source image (strength) as
+in image-to-image.
+
 Sampling uses the shared k-diffusion samplers over the discrete DDPM schedule (samplers.EpsSchedule):
 x_in = x / sqrt(sigma^2 + 1), t = t(sigma), x0 = x - sigma * eps; classifier-free guidance runs the
 positive and negative branches as one batch of 2 through the UNet, and the text context's
@@ -46,6 +53,7 @@ PRESETS = {
     "sdxl": UNetPreset(SDXL_UNET, CLIP_L, CLIP_G, VAEConfig(latent=4, scaling=0.13025, shift=0.0, quant_conv=True),
                        1024),
     "sd15-test": UNetPreset(UNET_TEST, _T_L, None, _VAE4_TEST, 64),
+    "sd2-depth-test": UNetPreset(UNetConfig(**{**UNET_TEST.__dict__, "in_channels": 5}), _T_L, None, _VAE4_TEST, 64),
     "sdxl-test": UNetPreset(UNET_XL_TEST, _T_L, _T_G, _VAE4_TEST, 64),
 }
 
@@ -59,10 +67,35 @@ class UNetPipeline:
         self.tok1, self.tok2 = tok1, tok2
         self.device = torch.device(device)
         self.sched = S.EpsSchedule()
+        self.depth = None  # (DPT depth estimator, input size, mean, std) for depth-conditioned UNets
 
     @property
     def xl(self) -> bool:
         return self.te2 is not None
+
+    @property
+    def depth_cond(self) -> bool:
+        """The UNet takes a depth channel next to the latent (SD 2 depth)."""
+        return self.p.unet.in_channels == self.vae.cfg.latent + 1
+
+    def set_depth_estimator(self, model, size: int = 384, mean=(0.5, 0.5, 0.5), std=(0.5, 0.5, 0.5)):
+        self.depth = (model.to(self.device).float().eval(), int(size), torch.tensor(mean).view(1, 3, 1, 1),
+                      torch.tensor(std).view(1, 3, 1, 1))
+        return self
+
+    @torch.no_grad()
+    def depth_map(self, image: torch.Tensor, h: int, w: int) -> torch.Tensor:
+        """image [3, H, W] in [0, 1] -> depth [1, 1, h, w] in [-1, 1] (diffusers prepare_depth_map)."""
+        if self.depth is None:
+            raise ValueError("this depth-conditioned model has no depth estimator (depth_estimator/)")
+        m, sz, mean, std = self.depth
+        x = F.interpolate(image[None].float(), size=(sz, sz), mode="bicubic", align_corners=False)
+        x = ((x - mean) / std).to(self.device)
+        d = m(pixel_values=x).predicted_depth[:, None].float()
+        d = F.interpolate(d, size=(h, w), mode="bicubic", align_corners=False)
+        lo = d.amin(dim=(1, 2, 3), keepdim=True)
+        hi = d.amax(dim=(1, 2, 3), keepdim=True)
+        return 2.0 * (d - lo) / (hi - lo).clamp_min(1e-6) - 1.0
 
     # ------------------------------------------------------------------ construction
     @classmethod
@@ -82,7 +115,15 @@ class UNetPipeline:
         vae = build(lambda: AutoencoderKL(pr.vae), 4)
         tk1 = CLIPTokenizer.synthetic(pr.clip_l.vocab)
         tk2 = CLIPTokenizer.synthetic(pr.clip_g.vocab, pad_token="!") if pr.clip_g is not None else None
-        return cls(pr, un, t1, t2, vae, tk1, tk2, dev)
+        pipe = cls(pr, un, t1, t2, vae, tk1, tk2, dev)
+        if pipe.depth_cond:  # a tiny random DPT (ViT backbone + reassemble / fusion neck + depth head)
+            from transformers import DPTConfig, DPTForDepthEstimation
+            torch.manual_seed(seed + 5)
+            dc = DPTConfig(hidden_size=32, num_hidden_layers=4, num_attention_heads=2, intermediate_size=64,
+                           image_size=64, patch_size=16, backbone_out_indices=[0, 1, 2, 3],
+                           neck_hidden_sizes=[8, 16, 32, 32], fusion_hidden_size=16, is_hybrid=False)
+            pipe.set_depth_estimator(DPTForDepthEstimation(dc), size=64)
+        return pipe
 
     @classmethod
     def from_diffusers(cls, d: str, device, dtype=None) -> "UNetPipeline":
@@ -126,7 +167,20 @@ class UNetPipeline:
         tk1 = CLIPTokenizer.from_dir(os.path.join(d, "tokenizer"))
         tk2 = CLIPTokenizer.from_dir(os.path.join(d, "tokenizer_2"), pad_token="!") if xl else None
         pr = UNetPreset(uc, t1.cfg, t2.cfg if t2 is not None else None, vae.cfg, uc.sample_size * 8)
-        return cls(pr, un, t1, t2, vae, tk1, tk2, dev)
+        pipe = cls(pr, un, t1, t2, vae, tk1, tk2, dev)
+        de = os.path.join(d, "depth_estimator")
+        if pipe.depth_cond and os.path.isdir(de):
+            from transformers import DPTForDepthEstimation
+            size, mean, std = 384, (0.5, 0.5, 0.5), (0.5, 0.5, 0.5)
+            fe = os.path.join(d, "feature_extractor", "preprocessor_config.json")
+            if os.path.isfile(fe):
+                with open(fe) as f:
+                    pc = json.load(f)
+                sz = pc.get("size", 384)
+                size = sz.get("height", 384) if isinstance(sz, dict) else int(sz)
+                mean, std = pc.get("image_mean", mean), pc.get("image_std", std)
+            pipe.set_depth_estimator(DPTForDepthEstimation.from_pretrained(de, local_files_only=True), size, mean, std)
+        return pipe
 
     def set_controlnet(self, path: str, seed: int = 0):
         """diffusers ControlNetModel directory, or `synthetic` (random init with this UNet's config)."""
@@ -189,7 +243,12 @@ class UNetPipeline:
         W, H = (gp.width // 8) * 8, (gp.height // 8) * 8
         ctx, pooled = self.encode_prompts([prompt, gp.negative], gp.extra.get("clip_skip", 0))
         gen = torch.Generator(device=dev).manual_seed(int(gp.seed) & 0x7FFFFFFFFFFFFFFF)
-        shape = (1, self.p.unet.in_channels, H // 8, W // 8)
+        dmap = None
+        if self.depth_cond:
+            if init_image is None:
+                raise ValueError("depth-to-image needs a source image (src)")
+            dmap = self.depth_map(init_image, H // 8, W // 8).to(dev).expand(2, -1, -1, -1)
+        shape = (1, self.vae.cfg.latent, H // 8, W // 8)
         sig = S.get_sigmas(self.sched, gp.steps, gp.schedule)
         noise = torch.randn(shape, generator=gen, device=dev, dtype=torch.float32)
         if init_image is not None:
@@ -216,6 +275,8 @@ class UNetPipeline:
 
         def denoise(xt: torch.Tensor, sigma: float) -> torch.Tensor:
             xin = torch.cat([xt, xt]) / math.sqrt(sigma * sigma + 1.0)
+            if dmap is not None:  # the depth channel rides unscaled next to the scaled latent
+                xin = torch.cat([xin, dmap.to(xin.dtype)], 1)
             t = torch.full((2,), self.sched.t_of(sigma), device=dev)
             ctl = cn(xin, t, ctx, cimg, cscale, added, ctx_key) if cn is not None and cimg is not None else None
             eps = self.unet(xin, t, ctx, added, ctx_key, control=ctl)

@@ -2,7 +2,8 @@
 `diffusers` backends behind one GenerateImage RPC.
 
 LoadModel: a diffusers-layout SD3 directory (MMDiT), Flux.1 directory (FluxTransformer2DModel) or
-SD1.x / SD2.x / SDXL directory (UNet); a stable-diffusion.cpp-style single file (.safetensors / .ckpt /
+SD1.x / SD2.x / SDXL directory (UNet; a StableDiffusionDepth2ImgPipeline directory — 5-channel UNet plus
+depth_estimator/ — runs depth-to-image with `src` as the source image, synthetic: `sd2-depth-test`); a stable-diffusion.cpp-style single file (.safetensors / .ckpt /
 GGUF: Flux.1 in BFL names, SD1.x / SD2.x / SDXL in LDM/SGM names) with the component options
 clip_l_path / clip_g_path / t5xxl_path / vae_path (models/diffusion/single_file.py); or `synthetic:sd3-medium | sd3-medium-no-t5 | sd3-test | sd15 |
 sdxl | sd15-test | sdxl-test | flux-dev | flux-schnell | flux-test` (random-init weights). For Flux,
