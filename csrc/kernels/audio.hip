@@ -159,3 +159,96 @@ extern "C" int mxk_wavenet_gate(const float* x, float* out, int B, int H, int T,
     wavenet_gate_kernel<<<(unsigned)((work + 255) / 256), 256, 0, st>>>(x, out, H, T, work, vec);
     return (int)hipGetLastError();
 }
+
+// ---------------------------------------------------------------------------------------------
+// lstm_bidir_coop: a bidirectional single-layer LSTM whose hidden size is too large for one workgroup's
+// registers (Kokoro / StyleTTS 2: H = 256 -> W_hh is 1 MB fp32). Each direction is spread over NB = H / 16
+// workgroups; workgroup b owns hidden units [16 b, 16 b + 16), i.e. the 64 gate rows {i, f, g, o} x 16 of
+// W_hh, held in registers (thread = row x quarter of the columns). Per time step every workgroup reads the
+// previous h (H floats, L2) from a double-buffered global vector, computes its 64 gate pre-activations
+// (+ the precomputed input gates gx = W_ih x_t + b_ih + b_hh), updates its 16 cells and publishes its h
+// slice; the direction's workgroups then meet at a grid barrier: agent-scope release + relaxed counter
+// ticket, relaxed polling + agent-scope acquire (placement independent, any XCD). The 2 x NB workgroups are
+// far below one per CU, so all are co-resident; every spin is bounded (err flag, no hang).
+// gx: [2][T][4H] (direction 1 in original time order), whh: [2][4H][H], hbuf: [2][2][H] (parity 0 = h0),
+// out: [T][2H] (forward | backward halves), cnt: [2] zeroed counters; all fp32 except cnt / err.
+template <int H>
+__global__ __launch_bounds__(256) void lstm_bidir_coop_kernel(const float* __restrict__ gx, const float* __restrict__ whh,
+                                                              float* hbuf, float* __restrict__ out, unsigned* cnt,
+                                                              int* err, int T) {
+    constexpr int NB = H / 16, NC = H / 4;  // workgroups per direction, columns per thread
+    const int dir = blockIdx.x / NB, wb = blockIdx.x % NB;
+    const int tid = threadIdx.x, row = tid >> 2, q = tid & 3;
+    const int grow = (row >> 4) * H + wb * 16 + (row & 15);  // gate (row >> 4), unit (row & 15)
+    __shared__ float sg[64];
+    float w[NC];
+    {
+        const float4* wr = reinterpret_cast<const float4*>(whh + ((size_t)dir * 4 * H + grow) * H + q * NC);
+#pragma unroll
+        for (int i = 0; i < NC / 4; ++i) {
+            const float4 v = wr[i];
+            w[4 * i] = v.x;
+            w[4 * i + 1] = v.y;
+            w[4 * i + 2] = v.z;
+            w[4 * i + 3] = v.w;
+        }
+    }
+    float c = 0.f;
+    const float* g_dir = gx + (size_t)dir * T * 4 * H;
+    for (int s = 0; s < T; ++s) {
+        const int t = dir == 0 ? s : T - 1 - s;
+        const float4* hp = reinterpret_cast<const float4*>(hbuf + (size_t)(dir * 2 + (s & 1)) * H + q * NC);
+        float acc = q == 0 ? g_dir[(size_t)t * 4 * H + grow] : 0.f;
+#pragma unroll
+        for (int i = 0; i < NC / 4; ++i) {
+            const float4 h4 = hp[i];
+            acc = fmaf(w[4 * i], h4.x, acc);
+            acc = fmaf(w[4 * i + 1], h4.y, acc);
+            acc = fmaf(w[4 * i + 2], h4.z, acc);
+            acc = fmaf(w[4 * i + 3], h4.w, acc);
+        }
+        acc += __shfl_xor(acc, 1, 64);
+        acc += __shfl_xor(acc, 2, 64);
+        if (q == 0) sg[row] = acc;
+        __syncthreads();
+        if (tid < 16) {  // PyTorch gate order: i, f, g, o
+            const float ig = sigmoid_f(sg[tid]), fg = sigmoid_f(sg[16 + tid]);
+            const float gg = tanh_f(sg[32 + tid]), og = sigmoid_f(sg[48 + tid]);
+            c = fg * c + ig * gg;
+            const float h = og * tanh_f(c);
+            hbuf[(size_t)(dir * 2 + ((s + 1) & 1)) * H + wb * 16 + tid] = h;
+            out[(size_t)t * 2 * H + dir * H + wb * 16 + tid] = h;
+        }
+        if (s + 1 == T) break;
+        // grid barrier of this direction's NB workgroups (release -> ticket; poll -> acquire)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_fetch_add(&cnt[dir], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned target = (unsigned)(s + 1) * NB;
+            int spins = 0;
+            while (__hip_atomic_load(&cnt[dir], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+                __builtin_amdgcn_s_sleep(1);
+                if (++spins > (1 << 22)) {  // a workgroup never arrived: flag it and run on (no hang)
+                    __hip_atomic_fetch_max(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    break;
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __syncthreads();
+    }
+}
+
+// Bidirectional LSTM scan (H in {128, 256}); the caller zeroes cnt / err and fills hbuf parity 0 with h0.
+extern "C" int mxk_lstm_bidir(const float* gx, const float* whh, float* hbuf, float* out, unsigned* cnt, int* err, int T,
+                              int H, hipStream_t st) {
+    if (T <= 0) return 0;
+    if (H == 256) lstm_bidir_coop_kernel<256><<<2 * (256 / 16), 256, 0, st>>>(gx, whh, hbuf, out, cnt, err, T);
+    else if (H == 128) lstm_bidir_coop_kernel<128><<<2 * (128 / 16), 256, 0, st>>>(gx, whh, hbuf, out, cnt, err, T);
+    else return (int)hipErrorInvalidValue;
+    return (int)hipGetLastError();
+}

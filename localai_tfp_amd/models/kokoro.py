@@ -173,7 +173,11 @@ class Kokoro:
         return F.conv1d(x, self.p[name + ".weight"], self.p.get(name + ".bias"), **kw)
 
     def _lstm(self, x, name):
-        """Bidirectional single-layer LSTM over [1, T, C] -> [1, T, 2H] (torch.nn.LSTM, i.e. MIOpen on the GPU)."""
+        """Bidirectional single-layer LSTM over [1, T, C] -> [1, T, 2H]: on the GPU the cooperative scan kernel
+        (ops/rnn.py, audio.hip lstm_bidir_coop), elsewhere torch.nn.LSTM."""
+        if x.is_cuda and self.p[name + ".weight_hh_l0"].shape[1] in (128, 256):
+            from ..ops.rnn import lstm_bidir
+            return lstm_bidir(x[0], self.p, name, self._lstms)[None]
         m = self._lstms.get(name)
         if m is None:
             w = self.p[name + ".weight_ih_l0"]
