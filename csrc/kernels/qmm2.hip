@@ -6,8 +6,12 @@
 // MFMA pipe busy only ~31 % of the time with 9-15 VALU + 4-7 SALU + 1.2-1.4 LDS instructions per
 // 32-cycle MFMA: the kernel was issue-bound, not memory- or MFMA-bound. Everything here is arranged to
 // cut the instructions per MFMA:
-//   * wave tile = ALL BM rows (WM = 2..8 MFMA row blocks) x one 32-column weight group: every dequantised
-//     B fragment (14 packed-f16 VALU) feeds WM MFMAs, so at BM = 256 the dequant is < 2 VALU per MFMA;
+//   * wave tile = WM MFMA row blocks x WN 32-column weight groups (the workgroup's 4 groups take 4 / WN
+//     waves, WN waves split the BM = 32 WM WN rows): every dequantised B fragment (14 packed-f16 VALU) feeds
+//     WM MFMAs and every A fragment read from LDS feeds WN. WN = 1 reads each A fragment from LDS once per
+//     MFMA — 1 KB per 32-cycle MFMA, 128 B/clk per CU, the whole LDS read rate (the round-4 isolation runs:
+//     with MFMA, dequant and global loads all removed the WN = 1, BM = 256 kernel still took 25 of its 95 us
+//     on gate_up M = 256). WN = 2 halves that at twice the dequant VALU per MFMA (still < 4);
 //   * the k loop is unrolled over one 256-element super-block (4 k-tiles of 64): the Q4_K / Q6_K scale
 //     decode of a k-tile has compile-time sub-block indices (bit-field extracts, exact f16 products), the
 //     super-block header is DMA'd and read once per super-block (not once per k-tile), and with a 4-slot
@@ -22,246 +26,17 @@
 // k-tile's four k-steps; their fp32 partials are summed through LDS before the epilogue.
 // Reference parity: llama.cpp's MMQ path for these formats (reached via backend/cpp/llama/grpc-server.cpp:2002
 // llama_decode); numerics = f16 dequantised weights x f16 activations, fp32 accumulation.
-#include "qdeq16.h"
+#include "qmm2_fmt.h"
 
 namespace {
 
 constexpr int Q2_NS = 4;  // ring slots (k-tiles of 64)
 int g_qmm2_rot = 0;       // k-order rotation multiplier per column tile (0: natural order), mxk_qmm2_set_rot
 
-template <int QT>
-struct Q2F;
-// Q4_K t32 unit (per 32-column group, per super-block): [hdr 32 x 16 B][quarter jq: chunk0, chunk1 (32 x 16 B)]
-// QB: quant bytes staged per group per k-tile (source unit offset qoff(JQ)); HB: header bytes per group per
-// super-block (staged with the super-block's first k-tile); QI / HI: LDS-DMA instructions for each.
-template <>
-struct Q2F<MXQ_Q4_K> {
-    static constexpr int UNIT = 4608, HB = 512, QB = 1024, QI = 1, HI = 1;
-    static constexpr int qoff(int jq) { return 512 + jq * 1024; }
-};
-// Q6_K t32 unit: [sc 32 x 16 B][d 32 x 4 B][quarter jq: ql0, ql1, qh (32 x 16 B)]
-template <>
-struct Q2F<MXQ_Q6_K> {
-    static constexpr int UNIT = 6784, HB = 640, QB = 1536, QI = 2, HI = 2;
-    static constexpr int qoff(int jq) { return 640 + jq * 1536; }
-};
-// Q3_K t32 unit: [hdr 32 x 16 B {scales[12], d}][hmask: 2 chunks x 32 x 16 B][qs half n: 2 chunks x 32 x 16 B];
-// k-tiles 2n, 2n+1 use qs half n (the 2-bit fields 0-1 / 2-3) -> header slot = hdr + hmask (1.5 KB)
-template <>
-struct Q2F<MXQ_Q3_K> {
-    static constexpr int UNIT = 3584, HB = 1536, QB = 1024, QI = 1, HI = 2;
-    static constexpr int qoff(int jq) { return 1536 + (jq >> 1) * 1024; }
-};
-// Q2_K t32 unit: [sc 32 x 16 B][dd 32 x 4 B {d, dmin}][qs half n: 2 chunks x 32 x 16 B]
-template <>
-struct Q2F<MXQ_Q2_K> {
-    static constexpr int UNIT = 2688, HB = 640, QB = 1024, QI = 1, HI = 2;
-    static constexpr int qoff(int jq) { return 640 + (jq >> 1) * 1024; }
-};
-
-template <int QT>
-struct Q2B;
-
-template <>
-struct Q2B<MXQ_Q4_K> {
-    u32x4 hd;
-    u32x2 v0, v1;
-    f16x2 sm[2];  // per sub-block of the k-tile: (scale, -dmin * min) as exact f16 products
-    MX_DEV void load_hdr(const char* hb, int col, int) { hd = *(const u32x4*)(hb + col * 16); }
-    MX_DEV void load_q(const char* qb, int col, int h) {
-        v0 = *(const u32x2*)(qb + col * 16 + 8 * h);
-        v1 = *(const u32x2*)(qb + 512 + col * 16 + 8 * h);
-    }
-    template <int JQ>
-    MX_DEV void prep() {
-        const f16x2 dd = __builtin_bit_cast(f16x2, hd[0]);
-        const f16x2 dn = {dd[0], -dd[1]};
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            int sc, mn;
-            q4k_scale_min_w(hd[1], hd[2], hd[3], 2 * JQ + i, sc, mn);
-            // d * sc is exact in f32 (11 x 6 bits), so the f16 product rounds exactly like the f32 path
-            const f16x2 q = {(_Float16)sc, (_Float16)mn};
-            sm[i] = dn * q;
-        }
-    }
-    template <int JQ, int S>
-    MX_DEV f16x8 frag() const {
-        const u32x2 src = (S & 1) ? v1 : v0;
-        constexpr int sh = 4 * (S >> 1);
-        const uint32_t t0 = (src[0] >> sh) & 0x0F0F0F0Fu, t1 = (src[1] >> sh) & 0x0F0F0F0Fu;
-        const f16x2 k = {(_Float16)1024.f, (_Float16)1024.f};
-        const f16x2 s2 = {sm[S >> 1][0], sm[S >> 1][0]}, m2 = {sm[S >> 1][1], sm[S >> 1][1]};
-        f16x2 p[4];
-        magic4(t0, p[0], p[1]);
-        magic4(t1, p[2], p[3]);
-        f16x8 r;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const f16x2 v = (p[i] - k) * s2 + m2;
-            r[2 * i] = v[0];
-            r[2 * i + 1] = v[1];
-        }
-        return r;
-    }
-};
-
-template <>
-struct Q2B<MXQ_Q6_K> {
-    u32x4 sc;   // 16 int8 sub-block scales (one per 16 k)
-    uint32_t dw;
-    u32x2 v0, v1, vh;
-    f16x2 s2[4];
-    MX_DEV void load_hdr(const char* hb, int col, int) {
-        sc = *(const u32x4*)(hb + col * 16);
-        dw = *(const uint32_t*)(hb + 512 + col * 4);
-    }
-    MX_DEV void load_q(const char* qb, int col, int h) {
-        v0 = *(const u32x2*)(qb + col * 16 + 8 * h);
-        v1 = *(const u32x2*)(qb + 512 + col * 16 + 8 * h);
-        vh = *(const u32x2*)(qb + 1024 + col * 16 + 8 * h);
-    }
-    template <int JQ>
-    MX_DEV void prep() {
-        const _Float16 d = __builtin_bit_cast(f16x2, dw)[0];
-        const uint32_t w = sc[JQ];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int v = (int)(int8_t)((w >> (8 * i)) & 0xFF);
-            const _Float16 s = d * (_Float16)v;  // 11 x 8 bits: exact product, one f16 rounding
-            s2[i] = (f16x2){s, s};
-        }
-    }
-    template <int JQ, int S>
-    MX_DEV f16x8 frag() const {
-        const u32x2 src = (S & 1) ? v1 : v0;
-        constexpr int sh = 4 * (S >> 1), qsh = 2 * S;
-        const uint32_t t0 = ((src[0] >> sh) & 0x0F0F0F0Fu) | (((vh[0] >> qsh) & 0x03030303u) << 4);
-        const uint32_t t1 = ((src[1] >> sh) & 0x0F0F0F0Fu) | (((vh[1] >> qsh) & 0x03030303u) << 4);
-        const f16x2 k = {(_Float16)1056.f, (_Float16)1056.f};  // 1024 magic + 32 code offset
-        f16x2 p[4];
-        magic4(t0, p[0], p[1]);
-        magic4(t1, p[2], p[3]);
-        f16x8 r;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const f16x2 v = (p[i] - k) * s2[S];
-            r[2 * i] = v[0];
-            r[2 * i + 1] = v[1];
-        }
-        return r;
-    }
-};
-
-// Q3_K: code c = 2-bit field | hmask bit << 2 in [0, 7], weight = d * (sc - 32) * (c - 4). k-tile JQ: qs half
-// n = JQ >> 1, 2-bit fields j = 2 (JQ & 1) + (S >> 1); k-step S uses sub-block scale 4 JQ + S.
-template <>
-struct Q2B<MXQ_Q3_K> {
-    u32x4 hd;           // scales[12] (3 words) + d
-    u32x2 hm0, hm1;     // hmask bytes 8 h .. 8 h + 7 of chunks 0 / 1 (this lane's k)
-    u32x2 v0, v1;
-    f16x2 s2[4];
-    MX_DEV void load_hdr(const char* hb, int col, int h) {
-        hd = *(const u32x4*)(hb + col * 16);
-        hm0 = *(const u32x2*)(hb + 512 + col * 16 + 8 * h);
-        hm1 = *(const u32x2*)(hb + 1024 + col * 16 + 8 * h);
-    }
-    MX_DEV void load_q(const char* qb, int col, int h) {
-        v0 = *(const u32x2*)(qb + col * 16 + 8 * h);
-        v1 = *(const u32x2*)(qb + 512 + col * 16 + 8 * h);
-    }
-    template <int JQ>
-    MX_DEV void prep() {
-        // 16 6-bit scales from 12 bytes (ggml kmask unpack): word JQ of the unpacked array = scales 4 JQ .. 4 JQ + 3
-        constexpr uint32_t km1 = 0x03030303u, km2 = 0x0F0F0F0Fu;
-        uint32_t w;
-        if constexpr (JQ == 0) w = (hd[0] & km2) | ((hd[2] & km1) << 4);
-        else if constexpr (JQ == 1) w = (hd[1] & km2) | (((hd[2] >> 2) & km1) << 4);
-        else if constexpr (JQ == 2) w = ((hd[0] >> 4) & km2) | (((hd[2] >> 4) & km1) << 4);
-        else w = ((hd[1] >> 4) & km2) | (((hd[2] >> 6) & km1) << 4);
-        const _Float16 d = __builtin_bit_cast(f16x2, hd[3])[0];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int v = (int)((w >> (8 * i)) & 0xFF) - 32;
-            const _Float16 sv = d * (_Float16)v;  // 11 x 6 bits: exact product, one f16 rounding
-            s2[i] = (f16x2){sv, sv};
-        }
-    }
-    template <int JQ, int S>
-    MX_DEV f16x8 frag() const {
-        const u32x2 src = (S & 1) ? v1 : v0;
-        const u32x2 hm = (S & 1) ? hm1 : hm0;
-        constexpr int j = 2 * (JQ & 1) + (S >> 1), hb = 4 * (JQ >> 1) + j;
-        const uint32_t t0 = ((src[0] >> (2 * j)) & 0x03030303u) | (((hm[0] >> hb) & 0x01010101u) << 2);
-        const uint32_t t1 = ((src[1] >> (2 * j)) & 0x03030303u) | (((hm[1] >> hb) & 0x01010101u) << 2);
-        const f16x2 k = {(_Float16)1028.f, (_Float16)1028.f};  // 1024 magic + 4 code offset
-        f16x2 p[4];
-        magic4(t0, p[0], p[1]);
-        magic4(t1, p[2], p[3]);
-        f16x8 r;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const f16x2 v = (p[i] - k) * s2[S];
-            r[2 * i] = v[0];
-            r[2 * i + 1] = v[1];
-        }
-        return r;
-    }
-};
-
-// Q2_K: weight = d * (sc & 15) * q - dmin * (sc >> 4), q the 2-bit field j = 2 (JQ & 1) + (S >> 1) of qs half
-// JQ >> 1; k-step S uses sub-block byte 4 JQ + S.
-template <>
-struct Q2B<MXQ_Q2_K> {
-    u32x4 sc;
-    uint32_t dw;
-    u32x2 v0, v1;
-    f16x2 sm[4];
-    MX_DEV void load_hdr(const char* hb, int col, int) {
-        sc = *(const u32x4*)(hb + col * 16);
-        dw = *(const uint32_t*)(hb + 512 + col * 4);
-    }
-    MX_DEV void load_q(const char* qb, int col, int h) {
-        v0 = *(const u32x2*)(qb + col * 16 + 8 * h);
-        v1 = *(const u32x2*)(qb + 512 + col * 16 + 8 * h);
-    }
-    template <int JQ>
-    MX_DEV void prep() {
-        const f16x2 dd = __builtin_bit_cast(f16x2, dw);
-        const f16x2 dn = {dd[0], -dd[1]};
-        const uint32_t w = sc[JQ];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const uint32_t b = (w >> (8 * i)) & 0xFF;
-            const f16x2 q = {(_Float16)(int)(b & 15), (_Float16)(int)(b >> 4)};
-            sm[i] = dn * q;  // exact f16 products (11 x 4 bits)
-        }
-    }
-    template <int JQ, int S>
-    MX_DEV f16x8 frag() const {
-        const u32x2 src = (S & 1) ? v1 : v0;
-        constexpr int j = 2 * (JQ & 1) + (S >> 1);
-        const uint32_t t0 = (src[0] >> (2 * j)) & 0x03030303u, t1 = (src[1] >> (2 * j)) & 0x03030303u;
-        const f16x2 k = {(_Float16)1024.f, (_Float16)1024.f};
-        const f16x2 s2 = {sm[S][0], sm[S][0]}, m2 = {sm[S][1], sm[S][1]};
-        f16x2 p[4];
-        magic4(t0, p[0], p[1]);
-        magic4(t1, p[2], p[3]);
-        f16x8 r;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const f16x2 v = (p[i] - k) * s2 + m2;
-            r[2 * i] = v[0];
-            r[2 * i + 1] = v[1];
-        }
-        return r;
-    }
-};
-
-template <int QT, int WM, int KS>
+template <int QT, int WM, int KS, int WN>
 struct Q2Geom {
     using F = Q2F<QT>;
-    static constexpr int BM = 32 * WM;
+    static constexpr int BM = 32 * WM * WN;
     static constexpr int NT = 4 * KS;                 // waves
     static constexpr int A_BYTES = BM * 128;          // one 64-k tile of A
     static constexpr int STAGE = A_BYTES + 4 * F::QB; // A + the 4 column groups' quant bytes
@@ -274,20 +49,31 @@ struct Q2Geom {
     static constexpr int cnt() { return WA + (WL ? F::QI + (JQ == 0 ? F::HI : 0) : 0); }
 };
 
-template <int N_>
-MX_DEV void q2_wait_barrier() {
-    asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N_) : "memory");
+
+// per-k-step issue schedule: each MFMA followed by one LDS read (the first NDS) and up to NV VALU, so the next
+// k-step's fragment reads leave early and the dequant VALU fills the MFMA shadows
+constexpr int Q2_VPM = 5;
+template <int I, int NM, int NDS, int NV>
+MX_DEV void q2_interleave() {
+    if constexpr (I < NM) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        if constexpr (I < NDS) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, NV, 0);
+        q2_interleave<I + 1, NM, NDS, NV>();
+    }
 }
 
 // DBG (isolation builds, tools/prof_qmm.py --q2dbg): 1 no MFMA, 2 no dequant VALU, 4 no A loads, 8 no weight loads
-template <int QT, int WM, int KS, int EPI, int DBG = 0>
+template <int QT, int WM, int KS, int WN, int EPI, int DBG = 0>
 __global__ __launch_bounds__(256 * KS) void qmm2_kernel(const uint16_t* __restrict__ A, int lda,
                                                         const uint8_t* __restrict__ W, int M, int N, int K,
                                                         int n_mt, int splits, int sbps, void* __restrict__ Cv,
                                                         int ldc, int rot_mul) {
-    using G = Q2Geom<QT, WM, KS>;
+    using G = Q2Geom<QT, WM, KS, WN>;
     using F = Q2F<QT>;
     constexpr int BM = G::BM, WA = G::WA, STAGE = G::STAGE, A_BYTES = G::A_BYTES;
+    static_assert(WN == 1 || WN == 2, "WN");
+    static_assert(KS == 1 || 4 * WM * WN * 16 * 64 * 4 <= G::LDS, "KS = 2 partials fit in the ring");
     static_assert(WA >= 1 && WA * 8 * G::NT == BM, "A tile split");
     static_assert(G::LDS <= 160 * 1024, "LDS");
     static_assert(G::template cnt<1, true>() + G::template cnt<2, true>() <= 63 &&
@@ -303,7 +89,10 @@ __global__ __launch_bounds__(256 * KS) void qmm2_kernel(const uint16_t* __restri
     // wave index as a scalar: every LDS-DMA destination (M0) and weight pointer below is then SGPR math
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int h = lane >> 5, col = lane & 31;
+    // cg: the column group this wave DMAs; (mw, nw): its compute tile = rows mw * 32 WM .., groups nw * WN + j
     const int cg = wave & 3, kh = wave >> 2;
+    constexpr int NW = 4 / WN;
+    const int nw = cg % NW, mw = cg / NW;
 
     // XCD-aware bijective remap: consecutive logical ids (the row tiles and splits of one column panel)
     // run on one XCD and share its L2
@@ -335,8 +124,9 @@ __global__ __launch_bounds__(256 * KS) void qmm2_kernel(const uint16_t* __restri
     }
     // per-lane fragment read bases (byte offsets within a stage)
     const int rb = col >> 3;
-    const uint32_t a_rd = (uint32_t)(rb * 1024 + (col & 7) * 32 + ((h ^ (rb & 1)) << 4));
-    const uint32_t b_rd = (uint32_t)(A_BYTES + cg * F::QB);
+    const uint32_t a_rd = (uint32_t)(mw * WM * 4096 + rb * 1024 + (col & 7) * 32 + ((h ^ (rb & 1)) << 4));
+    const uint32_t b_rd = (uint32_t)(A_BYTES + nw * WN * F::QB);  // + j * QB for the wave's group j
+    const int hg = nw * WN * F::HB;                                 // header offset of group nw * WN
 
     // stage issue: the A rows of k-tile `kta` and (weight waves) the quant bytes of super-block `sbw`,
     // quarter JQ, into ring slot JQ; JQ == 0 stages also bring that super-block's header into header slot
@@ -378,11 +168,13 @@ __global__ __launch_bounds__(256 * KS) void qmm2_kernel(const uint16_t* __restri
         }
     };
 
-    f32x16 acc[WM];
+    f32x16 acc[WM][WN];
 #pragma unroll
     for (int i = 0; i < WM; ++i)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
+        for (int j = 0; j < WN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
     auto mainloop = [&](auto kh_c, auto wl_c) {
         constexpr int KH = decltype(kh_c)::value;
@@ -409,16 +201,38 @@ __global__ __launch_bounds__(256 * KS) void qmm2_kernel(const uint16_t* __restri
         issue(p0 * 4 + 2, p0, 0, I2{}, WLc{});
         q2_wait_barrier<cnt(I1{}, WLc{}) + cnt(I2{}, WLc{})>();
 
-        Q2B<QT> bw;
-        f16x8 af[2][WM];
-        bw.load_hdr(hdr_lds + cg * F::HB, col, h);
-        bw.load_q(smem + b_rd, col, h);
+        // fragment producers (S is a compile-time constant after unrolling)
+        auto bfrag = [&](const Q2B<QT>& b, auto jq_c, int S) -> f16x8 {
+            constexpr int JQ_ = decltype(jq_c)::value;
+            if constexpr (DBG & 2) {
+                const u32x2 r2 = (S & 1) ? b.v1 : b.v0;
+                return __builtin_bit_cast(f16x8, (u32x4){r2[0], r2[1], r2[0] ^ (uint32_t)S, r2[1]});
+            } else {
+                switch (S) {
+                    case 0: return b.template frag<JQ_, 0>();
+                    case 1: return b.template frag<JQ_, 1>();
+                    case 2: return b.template frag<JQ_, 2>();
+                    default: return b.template frag<JQ_, 3>();
+                }
+            }
+        };
+        Q2B<QT> bw[WN];
+        f16x8 af[2][WM], bfc[WN];
+#pragma unroll
+        for (int j = 0; j < WN; ++j) {
+            bw[j].load_hdr(hdr_lds + hg + j * F::HB, col, h);
+            bw[j].load_q(smem + b_rd + j * F::QB, col, h);
+            bw[j].template prep<0>();
+            bfc[j] = bfrag(bw[j], I0{}, KH);
+        }
 #pragma unroll
         for (int i = 0; i < WM; ++i) af[0][i] = *(const f16x8*)(smem + a_rd + i * 4096 + KH * 256);
 
-        // one k-tile (ring slot JQ): the wave's k-steps KH, KH + KS, ...; the A fragments of the next k-step
-        // (on the last one: of the next tile, slot JQ + 1, waited for at the top) are read while this
-        // k-step's MFMAs run; the next tile's quant bytes (and header at a super-block edge) likewise
+        // one k-tile (ring slot JQ): the wave's k-steps KH, KH + KS, ...; software-pipelined one k-step deep:
+        // k-step S's MFMAs consume A / B fragments read and dequantised during k-step S - KS, while this
+        // k-step reads and dequantises those of the next one (on the last k-step: the next tile's first, from
+        // ring slot JQ + 1, landed at the top). An explicit per-k-step schedule (q2_interleave) keeps the
+        // compiler from sinking the LDS reads next to their MFMAs, which stalled every k-step on lgkmcnt(0).
         auto tile = [&](int sb, auto jq_c) {  // sb: virtual super-block index
             constexpr int JQ = decltype(jq_c)::value;
             constexpr int NJ = (JQ + 1) & 3;
@@ -431,44 +245,51 @@ __global__ __launch_bounds__(256 * KS) void qmm2_kernel(const uint16_t* __restri
                 const int ps = phys(real ? vi : nv - 1);
                 issue(ps * 4 + (real ? (ki & 3) : 3), ps, vi & 1, std::integral_constant<int, (JQ + 3) & 3>{}, WLc{});
             }
-            bw.template prep<JQ>();
-            Q2B<QT> bn = bw;
+            // the next tile's quant bytes (and, at a super-block edge, header): slot NJ landed at the wait above
+            Q2B<QT> bn[WN];
+#pragma unroll
+            for (int j = 0; j < WN; ++j) {
+                bn[j] = bw[j];
+                if constexpr (NJ == 0) bn[j].load_hdr(hdr_lds + ((sb + 1) & 1) * G::HSZ + hg + j * F::HB, col, h);
+                bn[j].load_q(smem + NJ * STAGE + b_rd + j * F::QB, col, h);
+            }
             constexpr int NSTEP = 4 / KS;
 #pragma unroll
             for (int t = 0; t < NSTEP; ++t) {
+                __builtin_amdgcn_sched_barrier(0);
                 const int S = KH + KS * t;  // compile-time after unrolling
                 const int cur = t & 1;
+                f16x8 bfn[WN];
                 if (t + 1 < NSTEP) {
 #pragma unroll
                     for (int i = 0; i < WM; ++i)
                         af[cur ^ 1][i] = *(const f16x8*)(smem + JQ * STAGE + a_rd + i * 4096 + (S + KS) * 256);
+#pragma unroll
+                    for (int j = 0; j < WN; ++j) bfn[j] = bfrag(bw[j], jq_c, S + KS);
                 } else {
 #pragma unroll
                     for (int i = 0; i < WM; ++i)
                         af[cur ^ 1][i] = *(const f16x8*)(smem + NJ * STAGE + a_rd + i * 4096 + KH * 256);
-                    if constexpr (NJ == 0) bn.load_hdr(hdr_lds + ((sb + 1) & 1) * G::HSZ + cg * F::HB, col, h);
-                    bn.load_q(smem + NJ * STAGE + b_rd, col, h);
-                }
-                f16x8 bf;
-                if constexpr (DBG & 2) {
-                    const u32x2 r2 = (S & 1) ? bw.v1 : bw.v0;
-                    bf = __builtin_bit_cast(f16x8, (u32x4){r2[0], r2[1], r2[0] ^ (uint32_t)S, r2[1]});
-                } else {
-                    switch (S) {
-                        case 0: bf = bw.template frag<JQ, 0>(); break;
-                        case 1: bf = bw.template frag<JQ, 1>(); break;
-                        case 2: bf = bw.template frag<JQ, 2>(); break;
-                        default: bf = bw.template frag<JQ, 3>(); break;
+#pragma unroll
+                    for (int j = 0; j < WN; ++j) {
+                        bn[j].template prep<NJ>();
+                        bfn[j] = bfrag(bn[j], std::integral_constant<int, NJ>{}, KH);
                     }
                 }
 #pragma unroll
-                for (int i = 0; i < WM; ++i) {
-                    if constexpr (DBG & 1) asm volatile("" ::"v"(af[cur][i]), "v"(bf));
-                    else acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[cur][i], bf, acc[i], 0, 0, 0);
-                }
+                for (int j = 0; j < WN; ++j)
+#pragma unroll
+                    for (int i = 0; i < WM; ++i) {
+                        if constexpr (DBG & 1) asm volatile("" ::"v"(af[cur][i]), "v"(bfc[j]));
+                        else acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[cur][i], bfc[j], acc[i][j], 0, 0, 0);
+                    }
+                if constexpr (!(DBG & 1)) q2_interleave<0, WM * WN, WM, Q2_VPM>();
+#pragma unroll
+                for (int j = 0; j < WN; ++j) bfc[j] = bfn[j];
             }
             // NSTEP is even: the next tile's first fragments are in af[0]
-            bw = bn;
+#pragma unroll
+            for (int j = 0; j < WN; ++j) bw[j] = bn[j];
         };
         for (int sb = 0; sb < nv; ++sb) {
             tile(sb, I0{});
@@ -488,83 +309,91 @@ __global__ __launch_bounds__(256 * KS) void qmm2_kernel(const uint16_t* __restri
         else mainloop(std::integral_constant<int, 1>{}, F_{});
         // sum the k-step halves: kh = 1 waves park their partials in the drained ring
         __syncthreads();
-        float* red = (float*)smem + (size_t)cg * (WM * 16 * 64) + lane;
+        float* red = (float*)smem + (size_t)cg * (WM * WN * 16 * 64) + lane;
         if (kh == 1) {
 #pragma unroll
             for (int i = 0; i < WM; ++i)
 #pragma unroll
-                for (int r = 0; r < 16; ++r) red[(i * 16 + r) * 64] = acc[i][r];
+                for (int j = 0; j < WN; ++j)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) red[((i * WN + j) * 16 + r) * 64] = acc[i][j][r];
         }
         __syncthreads();
         if (kh == 1) return;
 #pragma unroll
         for (int i = 0; i < WM; ++i)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) acc[i][r] += red[(i * 16 + r) * 64];
+            for (int j = 0; j < WN; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[i][j][r] += red[((i * WN + j) * 16 + r) * 64];
     }
 
     // ---- epilogue: 32x32 C/D layout: col = lane & 31, row = 8*(r>>2) + 4*(lane>>5) + (r&3) ----
-    const int nt = (ct * 4 + cg) * 32;
-    const int n = nt + col;
-    if (nt >= N) return;
-    if constexpr (EPI == E16_SWIGLU || EPI == E16_GEGLU) {
-        // W rows interleaved in 16-row groups: tile columns 0..15 gate, 16..31 up of the same features
+    const int mb = m_base + mw * WM * 32;
 #pragma unroll
-        for (int i = 0; i < WM; ++i)
+    for (int j = 0; j < WN; ++j) {
+        const int nt = (ct * 4 + nw * WN + j) * 32;
+        const int n = nt + col;
+        if (nt >= N) break;
+        if constexpr (EPI == E16_SWIGLU || EPI == E16_GEGLU) {
+            // W rows interleaved in 16-row groups: tile columns 0..15 gate, 16..31 up of the same features
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const float v = acc[i][r];
-                const float up = __shfl_xor(v, 16);
-                const int m = m_base + i * 32 + 8 * (r >> 2) + 4 * h + (r & 3);
-                if (col < 16 && m < M)
-                    ((uint16_t*)Cv)[(size_t)m * ldc + (nt >> 1) + col] = f32_to_act<true>(glu_gate_f<EPI>(v) * up);
-            }
-        return;
-    }
-#pragma unroll
-    for (int i = 0; i < WM; ++i) {
-        const int m0 = m_base + i * 32 + 4 * h;
-        if (m_base + i * 32 >= M) break;
-        float* cf = ((float*)Cv) + (size_t)m0 * ldc + n;
-        uint16_t* ch = ((uint16_t*)Cv) + (size_t)m0 * ldc + n;
-        auto roff = [&](int r) { return (size_t)(8 * (r >> 2) + (r & 3)) * ldc; };
-        if (m_base + i * 32 + 32 <= M) {
-            if constexpr (EPI == E16_ADD_F32) {
-                if (splits == 1) {
-                    float old[16];
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) old[r] = cf[roff(r)];
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) cf[roff(r)] = old[r] + acc[i][r];
-                } else {
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) atomicAdd(cf + roff(r), acc[i][r]);
-                }
-            } else {
+            for (int i = 0; i < WM; ++i)
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
-                    if constexpr (EPI == E16_F32) cf[roff(r)] = acc[i][r];
-                    else ch[roff(r)] = f32_to_act<true>(acc[i][r]);
+                    const float v = acc[i][j][r];
+                    const float up = __shfl_xor(v, 16);
+                    const int m = mb + i * 32 + 8 * (r >> 2) + 4 * h + (r & 3);
+                    if (col < 16 && m < M)
+                        ((uint16_t*)Cv)[(size_t)m * ldc + (nt >> 1) + col] = f32_to_act<true>(glu_gate_f<EPI>(v) * up);
                 }
-            }
             continue;
         }
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            if (m0 + 8 * (r >> 2) + (r & 3) >= M) continue;
-            const float v = acc[i][r];
-            if constexpr (EPI == E16_F32) cf[roff(r)] = v;
-            else if constexpr (EPI == E16_ACT) ch[roff(r)] = f32_to_act<true>(v);
-            else if (splits == 1) cf[roff(r)] += v;
-            else atomicAdd(cf + roff(r), v);
+        for (int i = 0; i < WM; ++i) {
+            const int m0 = mb + i * 32 + 4 * h;
+            if (mb + i * 32 >= M) break;
+            float* cf = ((float*)Cv) + (size_t)m0 * ldc + n;
+            uint16_t* ch = ((uint16_t*)Cv) + (size_t)m0 * ldc + n;
+            auto roff = [&](int r) { return (size_t)(8 * (r >> 2) + (r & 3)) * ldc; };
+            if (mb + i * 32 + 32 <= M) {
+                if constexpr (EPI == E16_ADD_F32) {
+                    if (splits == 1) {
+                        float old[16];
+#pragma unroll
+                        for (int r = 0; r < 16; ++r) old[r] = cf[roff(r)];
+#pragma unroll
+                        for (int r = 0; r < 16; ++r) cf[roff(r)] = old[r] + acc[i][j][r];
+                    } else {
+#pragma unroll
+                        for (int r = 0; r < 16; ++r) atomicAdd(cf + roff(r), acc[i][j][r]);
+                    }
+                } else {
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        if constexpr (EPI == E16_F32) cf[roff(r)] = acc[i][j][r];
+                        else ch[roff(r)] = f32_to_act<true>(acc[i][j][r]);
+                    }
+                }
+                continue;
+            }
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                if (m0 + 8 * (r >> 2) + (r & 3) >= M) continue;
+                const float v = acc[i][j][r];
+                if constexpr (EPI == E16_F32) cf[roff(r)] = v;
+                else if constexpr (EPI == E16_ACT) ch[roff(r)] = f32_to_act<true>(v);
+                else if (splits == 1) cf[roff(r)] += v;
+                else atomicAdd(cf + roff(r), v);
+            }
         }
     }
 }
 
-template <int QT, int WM, int KS, int EPI>
+template <int QT, int WM, int KS, int WN, int EPI>
 static int launch_qmm2(const uint16_t* A, int lda, const uint8_t* W, int M, int N, int K, int splits, void* C, int ldc,
                        hipStream_t st) {
-    using G = Q2Geom<QT, WM, KS>;
+    using G = Q2Geom<QT, WM, KS, WN>;
     const int nsb = K >> 8;
     splits = max(1, min(splits, nsb));
     const int sbps = (nsb + splits - 1) / splits;
@@ -574,27 +403,30 @@ static int launch_qmm2(const uint16_t* A, int lda, const uint8_t* W, int M, int 
     if (nwg <= 0 || nwg > 0x7fffffff) return (int)hipErrorInvalidValue;
     static bool attr_set = false;
     if (!attr_set) {
-        (void)hipFuncSetAttribute((const void*)qmm2_kernel<QT, WM, KS, EPI>, hipFuncAttributeMaxDynamicSharedMemorySize,
+        (void)hipFuncSetAttribute((const void*)qmm2_kernel<QT, WM, KS, WN, EPI>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   G::LDS);
         attr_set = true;
     }
-    qmm2_kernel<QT, WM, KS, EPI><<<dim3((unsigned)nwg), 256 * KS, G::LDS, st>>>(A, lda, W, M, N, K, n_mt, splits, sbps,
-                                                                                C, ldc, g_qmm2_rot);
+    qmm2_kernel<QT, WM, KS, WN, EPI><<<dim3((unsigned)nwg), 256 * KS, G::LDS, st>>>(A, lda, W, M, N, K, n_mt, splits,
+                                                                                    sbps, C, ldc, g_qmm2_rot);
     MXK_CHECK_LAUNCH();
 }
 
 template <int QT, int EPI>
-static int dispatch_qmm2(int wm, int ks, const uint16_t* A, int lda, const uint8_t* W, int M, int N, int K, int splits,
-                         void* C, int ldc, hipStream_t st) {
-#define Q2_CASE(WM_, KS_) \
-    if (wm == WM_ && ks == KS_) return launch_qmm2<QT, WM_, KS_, EPI>(A, lda, W, M, N, K, splits, C, ldc, st);
-    Q2_CASE(2, 1) Q2_CASE(2, 2) Q2_CASE(4, 1) Q2_CASE(4, 2) Q2_CASE(6, 1) Q2_CASE(8, 1) Q2_CASE(8, 2)
+static int dispatch_qmm2(int wm, int ks, int wn, const uint16_t* A, int lda, const uint8_t* W, int M, int N, int K,
+                         int splits, void* C, int ldc, hipStream_t st) {
+#define Q2_CASE(WM_, KS_, WN_)                 \
+    if (wm == WM_ && ks == KS_ && wn == WN_) \
+        return launch_qmm2<QT, WM_, KS_, WN_, EPI>(A, lda, W, M, N, K, splits, C, ldc, st);
+    // (8, 2, 1) / (4, 2, 2) (256-row tiles with 8 waves) exceed the 256 registers a wave has at 2 waves / SIMD
+    Q2_CASE(2, 1, 1) Q2_CASE(2, 2, 1) Q2_CASE(4, 1, 1) Q2_CASE(4, 2, 1) Q2_CASE(8, 1, 1)
+    Q2_CASE(1, 2, 2) Q2_CASE(2, 1, 2) Q2_CASE(2, 2, 2) Q2_CASE(4, 1, 2)
 #undef Q2_CASE
     return (int)hipErrorInvalidValue;
 }
 
 template <int DBG>
-static int launch_dbg(int wm, const uint16_t* A, int lda, const uint8_t* W, int M, int N, int K, void* C, int ldc,
+static int launch_dbg(int wm, int ks, int wn, const uint16_t* A, int lda, const uint8_t* W, int M, int N, int K, void* C, int ldc,
                       hipStream_t st) {
     constexpr int QT = MXQ_Q4_K, EPI = E16_SWIGLU;
     auto go = [&](auto kern, int bm, int ks, int lds) {
@@ -603,8 +435,10 @@ static int launch_dbg(int wm, const uint16_t* A, int lda, const uint8_t* W, int 
         kern<<<dim3(n_ct * n_mt), 256 * ks, lds, st>>>(A, lda, W, M, N, K, n_mt, 1, K >> 8, C, ldc, g_qmm2_rot);
         return (int)hipGetLastError();
     };
-    if (wm == 8) return go(qmm2_kernel<QT, 8, 1, EPI, DBG>, 256, 1, Q2Geom<QT, 8, 1>::LDS);
-    if (wm == 4) return go(qmm2_kernel<QT, 4, 2, EPI, DBG>, 128, 2, Q2Geom<QT, 4, 2>::LDS);
+    if (wm == 8 && ks == 1 && wn == 1) return go(qmm2_kernel<QT, 8, 1, 1, EPI, DBG>, 256, 1, Q2Geom<QT, 8, 1, 1>::LDS);
+    if (wm == 4 && ks == 2 && wn == 1) return go(qmm2_kernel<QT, 4, 2, 1, EPI, DBG>, 128, 2, Q2Geom<QT, 4, 2, 1>::LDS);
+    if (wm == 4 && ks == 1 && wn == 2) return go(qmm2_kernel<QT, 4, 1, 2, EPI, DBG>, 256, 1, Q2Geom<QT, 4, 1, 2>::LDS);
+    if (wm == 2 && ks == 2 && wn == 2) return go(qmm2_kernel<QT, 2, 2, 2, EPI, DBG>, 128, 2, Q2Geom<QT, 2, 2, 2>::LDS);
     return (int)hipErrorInvalidValue;
 }
 
@@ -615,38 +449,40 @@ extern "C" int mxk_qmm2_set_rot(int r) {
     return 0;
 }
 
-// isolation builds of the Q4_K SwiGLU kernel (wm 8 / ks 1 and wm 4 / ks 2, no split), see DBG above
-extern "C" int mxk_qmm2_dbg(int dbg, int wm, const uint16_t* A, int lda, const uint8_t* W, int M, int N, int K, void* C,
-                            int ldc, hipStream_t st) {
+// isolation builds of the Q4_K SwiGLU kernel ((wm, ks, wn) = (8, 1, 1), (4, 2, 1), (4, 1, 2), (2, 2, 2); no split),
+// see DBG above
+extern "C" int mxk_qmm2_dbg(int dbg, int wm, int ks, int wn, const uint16_t* A, int lda, const uint8_t* W, int M, int N,
+                            int K, void* C, int ldc, hipStream_t st) {
     switch (dbg) {
-        case 0: return launch_dbg<0>(wm, A, lda, W, M, N, K, C, ldc, st);
-        case 1: return launch_dbg<1>(wm, A, lda, W, M, N, K, C, ldc, st);
-        case 2: return launch_dbg<2>(wm, A, lda, W, M, N, K, C, ldc, st);
-        case 3: return launch_dbg<3>(wm, A, lda, W, M, N, K, C, ldc, st);
-        case 4: return launch_dbg<4>(wm, A, lda, W, M, N, K, C, ldc, st);
-        case 8: return launch_dbg<8>(wm, A, lda, W, M, N, K, C, ldc, st);
-        case 12: return launch_dbg<12>(wm, A, lda, W, M, N, K, C, ldc, st);
-        case 15: return launch_dbg<15>(wm, A, lda, W, M, N, K, C, ldc, st);
+        case 0: return launch_dbg<0>(wm, ks, wn, A, lda, W, M, N, K, C, ldc, st);
+        case 1: return launch_dbg<1>(wm, ks, wn, A, lda, W, M, N, K, C, ldc, st);
+        case 2: return launch_dbg<2>(wm, ks, wn, A, lda, W, M, N, K, C, ldc, st);
+        case 3: return launch_dbg<3>(wm, ks, wn, A, lda, W, M, N, K, C, ldc, st);
+        case 4: return launch_dbg<4>(wm, ks, wn, A, lda, W, M, N, K, C, ldc, st);
+        case 8: return launch_dbg<8>(wm, ks, wn, A, lda, W, M, N, K, C, ldc, st);
+        case 12: return launch_dbg<12>(wm, ks, wn, A, lda, W, M, N, K, C, ldc, st);
+        case 15: return launch_dbg<15>(wm, ks, wn, A, lda, W, M, N, K, C, ldc, st);
     }
     return (int)hipErrorInvalidValue;
 }
 
 // A f16 [M, K] (lda % 8 == 0, 16-B aligned), W t32 Q4_K / Q6_K / Q3_K / Q2_K [N, K] (N % 32 == 0, K % 256 == 0).
 // epi: 0 fp32 store, 1 f16 store, 2 fp32 accumulate (split-K via atomics when splits > 1), 3/4 SwiGLU /
-// GeGLU over 16-row interleaved gate|up -> f16 [M, N/2]. wm: 32-row MFMA blocks per wave (BM = 32 wm);
-// ks: 1 (4 waves) or 2 (8 waves, k-steps split per wave pair). splits: K split in whole super-blocks.
-extern "C" int mxk_qmm2(int qtype, int epi, int wm, int ks, const uint16_t* A, int lda, const uint8_t* W, int M, int N,
-                        int K, int splits, void* C, int ldc, hipStream_t st) {
+// GeGLU over 16-row interleaved gate|up -> f16 [M, N/2]. wm: 32-row MFMA blocks per wave; wn: 32-column groups
+// per wave (BM = 32 wm wn); ks: 1 (4 waves) or 2 (8 waves, k-steps split per wave pair). splits: K split in
+// whole super-blocks.
+extern "C" int mxk_qmm2(int qtype, int epi, int wm, int ks, int wn, const uint16_t* A, int lda, const uint8_t* W, int M,
+                        int N, int K, int splits, void* C, int ldc, hipStream_t st) {
     if (M <= 0) return 0;
     if (K % 256 || (lda & 7) || ((uintptr_t)A & 15) || ((uintptr_t)W & 15) || (N & 31)) return (int)hipErrorInvalidValue;
     if (epi != E16_ADD_F32 && splits != 1) return (int)hipErrorInvalidValue;
 #define Q2_EPI(QT_)                                                                                          \
     switch (epi) {                                                                                           \
-        case E16_F32: return dispatch_qmm2<QT_, E16_F32>(wm, ks, A, lda, W, M, N, K, splits, C, ldc, st);     \
-        case E16_ACT: return dispatch_qmm2<QT_, E16_ACT>(wm, ks, A, lda, W, M, N, K, splits, C, ldc, st);     \
-        case E16_ADD_F32: return dispatch_qmm2<QT_, E16_ADD_F32>(wm, ks, A, lda, W, M, N, K, splits, C, ldc, st); \
-        case E16_SWIGLU: return dispatch_qmm2<QT_, E16_SWIGLU>(wm, ks, A, lda, W, M, N, K, splits, C, ldc, st); \
-        case E16_GEGLU: return dispatch_qmm2<QT_, E16_GEGLU>(wm, ks, A, lda, W, M, N, K, splits, C, ldc, st);   \
+        case E16_F32: return dispatch_qmm2<QT_, E16_F32>(wm, ks, wn, A, lda, W, M, N, K, splits, C, ldc, st);     \
+        case E16_ACT: return dispatch_qmm2<QT_, E16_ACT>(wm, ks, wn, A, lda, W, M, N, K, splits, C, ldc, st);     \
+        case E16_ADD_F32: return dispatch_qmm2<QT_, E16_ADD_F32>(wm, ks, wn, A, lda, W, M, N, K, splits, C, ldc, st); \
+        case E16_SWIGLU: return dispatch_qmm2<QT_, E16_SWIGLU>(wm, ks, wn, A, lda, W, M, N, K, splits, C, ldc, st); \
+        case E16_GEGLU: return dispatch_qmm2<QT_, E16_GEGLU>(wm, ks, wn, A, lda, W, M, N, K, splits, C, ldc, st);   \
     }
     switch (qtype) {
         case MXQ_Q4_K: Q2_EPI(MXQ_Q4_K) break;

@@ -1,0 +1,246 @@
+// qmm2_fmt.h — the t32 quantised-weight formats as seen by the MFMA GEMMs (qmm2.hip, qmm3.hip): per format the
+// unit / header / quant byte geometry of one 32-column group x 256-k super-block (Q2F) and the per-lane register
+// decoder that turns LDS-staged bytes into 32x32x16 MFMA B fragments (Q2B: load_hdr, load_q, prep<JQ>,
+// frag<JQ, S>). Lane mapping: col = lane & 31, h = lane >> 5 (k 8h .. 8h + 7 of a 16-k step).
+#pragma once
+#include "qdeq16.h"
+
+namespace {
+
+template <int N_>
+MX_DEV void q2_wait_barrier() {
+    asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N_) : "memory");
+}
+
+template <int QT>
+struct Q2F;
+// Q4_K t32 unit (per 32-column group, per super-block): [hdr 32 x 16 B][quarter jq: chunk0, chunk1 (32 x 16 B)]
+// QB: quant bytes staged per group per k-tile (source unit offset qoff(JQ)); HB: header bytes per group per
+// super-block (staged with the super-block's first k-tile); QI / HI: LDS-DMA instructions for each.
+template <>
+struct Q2F<MXQ_Q4_K> {
+    static constexpr int UNIT = 4608, HB = 512, QB = 1024, QI = 1, HI = 1;
+    static constexpr int qoff(int jq) { return 512 + jq * 1024; }
+};
+// Q6_K t32 unit: [sc 32 x 16 B][d 32 x 4 B][quarter jq: ql0, ql1, qh (32 x 16 B)]
+template <>
+struct Q2F<MXQ_Q6_K> {
+    static constexpr int UNIT = 6784, HB = 640, QB = 1536, QI = 2, HI = 2;
+    static constexpr int qoff(int jq) { return 640 + jq * 1536; }
+};
+// Q3_K t32 unit: [hdr 32 x 16 B {scales[12], d}][hmask: 2 chunks x 32 x 16 B][qs half n: 2 chunks x 32 x 16 B];
+// k-tiles 2n, 2n+1 use qs half n (the 2-bit fields 0-1 / 2-3) -> header slot = hdr + hmask (1.5 KB)
+template <>
+struct Q2F<MXQ_Q3_K> {
+    static constexpr int UNIT = 3584, HB = 1536, QB = 1024, QI = 1, HI = 2;
+    static constexpr int qoff(int jq) { return 1536 + (jq >> 1) * 1024; }
+};
+// Q2_K t32 unit: [sc 32 x 16 B][dd 32 x 4 B {d, dmin}][qs half n: 2 chunks x 32 x 16 B]
+template <>
+struct Q2F<MXQ_Q2_K> {
+    static constexpr int UNIT = 2688, HB = 640, QB = 1024, QI = 1, HI = 2;
+    static constexpr int qoff(int jq) { return 640 + (jq >> 1) * 1024; }
+};
+
+template <int QT>
+struct Q2B;
+
+template <>
+struct Q2B<MXQ_Q4_K> {
+    u32x4 hd;
+    u32x2 v0, v1;
+    f16x2 sm[2];  // per sub-block of the k-tile: (scale, -dmin * min) as exact f16 products
+    MX_DEV void load_hdr(const char* hb, int col, int) { hd = *(const u32x4*)(hb + col * 16); }
+    MX_DEV void load_q(const char* qb, int col, int h) {
+        v0 = *(const u32x2*)(qb + col * 16 + 8 * h);
+        v1 = *(const u32x2*)(qb + 512 + col * 16 + 8 * h);
+    }
+    template <int JQ>
+    MX_DEV void prep() {
+        const uint32_t w0 = hd[0];  // scalar first: clang bit-casts the whole vector for bit_cast(T, v[i])
+        const f16x2 dd = __builtin_bit_cast(f16x2, w0);
+        const f16x2 dn = {dd[0], -dd[1]};
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            int sc, mn;
+            q4k_scale_min_w(hd[1], hd[2], hd[3], 2 * JQ + i, sc, mn);
+            // d * sc is exact in f32 (11 x 6 bits), so the f16 product rounds exactly like the f32 path
+            const f16x2 q = {(_Float16)sc, (_Float16)mn};
+            sm[i] = dn * q;
+        }
+    }
+    template <int JQ, int S>
+    MX_DEV f16x8 frag() const {
+        const u32x2 src = (S & 1) ? v1 : v0;
+        constexpr int sh = 4 * (S >> 1);
+        const uint32_t t0 = (src[0] >> sh) & 0x0F0F0F0Fu, t1 = (src[1] >> sh) & 0x0F0F0F0Fu;
+        const f16x2 k = {(_Float16)1024.f, (_Float16)1024.f};
+        const f16x2 s2 = {sm[S >> 1][0], sm[S >> 1][0]}, m2 = {sm[S >> 1][1], sm[S >> 1][1]};
+        f16x2 p[4];
+        magic4(t0, p[0], p[1]);
+        magic4(t1, p[2], p[3]);
+        f16x8 r;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const f16x2 v = (p[i] - k) * s2 + m2;
+            r[2 * i] = v[0];
+            r[2 * i + 1] = v[1];
+        }
+        return r;
+    }
+};
+
+template <>
+struct Q2B<MXQ_Q6_K> {
+    u32x4 sc;   // 16 int8 sub-block scales (one per 16 k)
+    uint32_t dw;
+    u32x2 v0, v1, vh;
+    f16x2 s2[4];
+    MX_DEV void load_hdr(const char* hb, int col, int) {
+        sc = *(const u32x4*)(hb + col * 16);
+        dw = *(const uint32_t*)(hb + 512 + col * 4);
+    }
+    MX_DEV void load_q(const char* qb, int col, int h) {
+        v0 = *(const u32x2*)(qb + col * 16 + 8 * h);
+        v1 = *(const u32x2*)(qb + 512 + col * 16 + 8 * h);
+        vh = *(const u32x2*)(qb + 1024 + col * 16 + 8 * h);
+    }
+    template <int JQ>
+    MX_DEV void prep() {
+        const _Float16 d = __builtin_bit_cast(f16x2, dw)[0];
+        const uint32_t w = sc[JQ];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int v = (int)(int8_t)((w >> (8 * i)) & 0xFF);
+            const _Float16 s = d * (_Float16)v;  // 11 x 8 bits: exact product, one f16 rounding
+            s2[i] = (f16x2){s, s};
+        }
+    }
+    template <int JQ, int S>
+    MX_DEV f16x8 frag() const {
+        const u32x2 src = (S & 1) ? v1 : v0;
+        constexpr int sh = 4 * (S >> 1), qsh = 2 * S;
+        const uint32_t t0 = ((src[0] >> sh) & 0x0F0F0F0Fu) | (((vh[0] >> qsh) & 0x03030303u) << 4);
+        const uint32_t t1 = ((src[1] >> sh) & 0x0F0F0F0Fu) | (((vh[1] >> qsh) & 0x03030303u) << 4);
+        const f16x2 k = {(_Float16)1056.f, (_Float16)1056.f};  // 1024 magic + 32 code offset
+        f16x2 p[4];
+        magic4(t0, p[0], p[1]);
+        magic4(t1, p[2], p[3]);
+        f16x8 r;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const f16x2 v = (p[i] - k) * s2[S];
+            r[2 * i] = v[0];
+            r[2 * i + 1] = v[1];
+        }
+        return r;
+    }
+};
+
+// Q3_K: code c = 2-bit field | hmask bit << 2 in [0, 7], weight = d * (sc - 32) * (c - 4). k-tile JQ: qs half
+// n = JQ >> 1, 2-bit fields j = 2 (JQ & 1) + (S >> 1); k-step S uses sub-block scale 4 JQ + S.
+template <>
+struct Q2B<MXQ_Q3_K> {
+    u32x4 hd;           // scales[12] (3 words) + d
+    u32x2 hm0, hm1;     // hmask bytes 8 h .. 8 h + 7 of chunks 0 / 1 (this lane's k)
+    u32x2 v0, v1;
+    f16x2 s2[4];
+    MX_DEV void load_hdr(const char* hb, int col, int h) {
+        hd = *(const u32x4*)(hb + col * 16);
+        hm0 = *(const u32x2*)(hb + 512 + col * 16 + 8 * h);
+        hm1 = *(const u32x2*)(hb + 1024 + col * 16 + 8 * h);
+    }
+    MX_DEV void load_q(const char* qb, int col, int h) {
+        v0 = *(const u32x2*)(qb + col * 16 + 8 * h);
+        v1 = *(const u32x2*)(qb + 512 + col * 16 + 8 * h);
+    }
+    template <int JQ>
+    MX_DEV void prep() {
+        // 16 6-bit scales from 12 bytes (ggml kmask unpack): word JQ of the unpacked array = scales 4 JQ .. 4 JQ + 3
+        constexpr uint32_t km1 = 0x03030303u, km2 = 0x0F0F0F0Fu;
+        uint32_t w;
+        if constexpr (JQ == 0) w = (hd[0] & km2) | ((hd[2] & km1) << 4);
+        else if constexpr (JQ == 1) w = (hd[1] & km2) | (((hd[2] >> 2) & km1) << 4);
+        else if constexpr (JQ == 2) w = ((hd[0] >> 4) & km2) | (((hd[2] >> 4) & km1) << 4);
+        else w = ((hd[1] >> 4) & km2) | (((hd[2] >> 6) & km1) << 4);
+        const uint32_t w3 = hd[3];  // scalar first (see Q4_K prep)
+        const _Float16 d = __builtin_bit_cast(f16x2, w3)[0];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int v = (int)((w >> (8 * i)) & 0xFF) - 32;
+            const _Float16 sv = d * (_Float16)v;  // 11 x 6 bits: exact product, one f16 rounding
+            s2[i] = (f16x2){sv, sv};
+        }
+    }
+    template <int JQ, int S>
+    MX_DEV f16x8 frag() const {
+        const u32x2 src = (S & 1) ? v1 : v0;
+        const u32x2 hm = (S & 1) ? hm1 : hm0;
+        constexpr int j = 2 * (JQ & 1) + (S >> 1), hb = 4 * (JQ >> 1) + j;
+        const uint32_t t0 = ((src[0] >> (2 * j)) & 0x03030303u) | (((hm[0] >> hb) & 0x01010101u) << 2);
+        const uint32_t t1 = ((src[1] >> (2 * j)) & 0x03030303u) | (((hm[1] >> hb) & 0x01010101u) << 2);
+        const f16x2 k = {(_Float16)1028.f, (_Float16)1028.f};  // 1024 magic + 4 code offset
+        f16x2 p[4];
+        magic4(t0, p[0], p[1]);
+        magic4(t1, p[2], p[3]);
+        f16x8 r;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const f16x2 v = (p[i] - k) * s2[S];
+            r[2 * i] = v[0];
+            r[2 * i + 1] = v[1];
+        }
+        return r;
+    }
+};
+
+// Q2_K: weight = d * (sc & 15) * q - dmin * (sc >> 4), q the 2-bit field j = 2 (JQ & 1) + (S >> 1) of qs half
+// JQ >> 1; k-step S uses sub-block byte 4 JQ + S.
+template <>
+struct Q2B<MXQ_Q2_K> {
+    u32x4 sc;
+    uint32_t dw;
+    u32x2 v0, v1;
+    f16x2 sm[4];
+    MX_DEV void load_hdr(const char* hb, int col, int) {
+        sc = *(const u32x4*)(hb + col * 16);
+        dw = *(const uint32_t*)(hb + 512 + col * 4);
+    }
+    MX_DEV void load_q(const char* qb, int col, int h) {
+        v0 = *(const u32x2*)(qb + col * 16 + 8 * h);
+        v1 = *(const u32x2*)(qb + 512 + col * 16 + 8 * h);
+    }
+    template <int JQ>
+    MX_DEV void prep() {
+        const f16x2 dd = __builtin_bit_cast(f16x2, dw);
+        const f16x2 dn = {dd[0], -dd[1]};
+        const uint32_t w = sc[JQ];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint32_t b = (w >> (8 * i)) & 0xFF;
+            const f16x2 q = {(_Float16)(int)(b & 15), (_Float16)(int)(b >> 4)};
+            sm[i] = dn * q;  // exact f16 products (11 x 4 bits)
+        }
+    }
+    template <int JQ, int S>
+    MX_DEV f16x8 frag() const {
+        const u32x2 src = (S & 1) ? v1 : v0;
+        constexpr int j = 2 * (JQ & 1) + (S >> 1);
+        const uint32_t t0 = (src[0] >> (2 * j)) & 0x03030303u, t1 = (src[1] >> (2 * j)) & 0x03030303u;
+        const f16x2 k = {(_Float16)1024.f, (_Float16)1024.f};
+        const f16x2 s2 = {sm[S][0], sm[S][0]}, m2 = {sm[S][1], sm[S][1]};
+        f16x2 p[4];
+        magic4(t0, p[0], p[1]);
+        magic4(t1, p[2], p[3]);
+        f16x8 r;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const f16x2 v = (p[i] - k) * s2 + m2;
+            r[2 * i] = v[0];
+            r[2 * i + 1] = v[1];
+        }
+        return r;
+    }
+};
+
+}  // namespace

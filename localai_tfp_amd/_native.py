@@ -40,9 +40,11 @@ KERNEL_SIGS = {
     "mxk_qgemm16": [I, I, I, I, P, I, P, P, I, I, I, I, P, I, P],
     "mxk_qgemm32": [I, I, I, I, P, I, P, P, I, I, I, I, P, I, P],
     "mxk_qmm": [I, I, I, I, I, I, P, I, P, P, I, I, I, I, P, I, P],
-    "mxk_qmm2": [I, I, I, I, P, I, P, I, I, I, I, P, I, P],
-    "mxk_qmm2_dbg": [I, I, P, I, P, I, I, I, P, I, P],
+    "mxk_qmm2": [I, I, I, I, I, P, I, P, I, I, I, I, P, I, P],
+    "mxk_qmm2_dbg": [I, I, I, I, P, I, P, I, I, I, P, I, P],
     "mxk_qmm2_set_rot": [I],
+    "mxk_qmm3": [I, I, I, P, I, P, I, I, I, I, P, I, P],
+    "mxk_qmm3_dbg": [I, I, P, I, P, I, I, I, P, I, P],
     "mxk_qmm_ws": [I, I, I, P, I, P, I, I, I, I, P, I, P],
     "mxk_qmm_ws_dbg": [I],
     "mxk_qmv": [I, I, P, P, P, I, I, I, I, P, I, P],

@@ -327,14 +327,25 @@ def _qmatmul_t32(W: QWeight, x, epi: int, out, xq, xds, M: int, out_zeroed: bool
     can_split = epi == EPI_ADD_F32 or (epi == EPI_F32 and out_zeroed)
     if W.bf16_cache is not None and M >= dense_min_m(x.dtype, epi, can_split) and W.bf16_cache.dtype == x.dtype:
         return _dense_cached(W, x, epi, out, M)
-    if (QMM2 and int(W.qtype) in QMM2_QTYPES and M >= QMM2_MIN_M) or int(W.qtype) in QMM2_ONLY:
-        wm, ks, splits = _qmm2_shape(M, W.N, W.K, can_split)
+    pick = _gemm_pick(M, W.N, W.K, int(W.qtype), can_split)
+    if pick is not None and pick[0] == "q3":
+        wm, splits = pick[1:]
         e = EPI_ADD_F32 if (epi == EPI_F32 and splits > 1) else epi
         if e in (EPI_BF16, *GLU_EPIS):
             if out.dtype != x.dtype:
                 raise ValueError(f"qmatmul: {out.dtype} output with {x.dtype} activations")
             N.ensure_act(out.dtype)
-        N.kcall("mxk_qmm2", int(W.qtype), e, wm, ks, x.data_ptr(), x.stride(0), W.data.data_ptr(), M, W.N, W.K,
+        N.kcall("mxk_qmm3", int(W.qtype), e, wm, x.data_ptr(), x.stride(0), W.data.data_ptr(), M, W.N, W.K,
+                splits, out.data_ptr(), out.stride(0), N.stream_ptr())
+        return out
+    if pick is not None:
+        wm, ks, wn, splits = pick[1:]
+        e = EPI_ADD_F32 if (epi == EPI_F32 and splits > 1) else epi
+        if e in (EPI_BF16, *GLU_EPIS):
+            if out.dtype != x.dtype:
+                raise ValueError(f"qmatmul: {out.dtype} output with {x.dtype} activations")
+            N.ensure_act(out.dtype)
+        N.kcall("mxk_qmm2", int(W.qtype), e, wm, ks, wn, x.data_ptr(), x.stride(0), W.data.data_ptr(), M, W.N, W.K,
                 splits, out.data_ptr(), out.stride(0), N.stream_ptr())
         return out
     ws = _qmm_ws_shape(M, W.N, W.K, can_split, int(W.qtype))
@@ -547,34 +558,93 @@ def _qmm_shape(M: int, N_: int, K: int, can_split: bool):
 # unrolled k loop, 4-slot LDS-DMA ring) for the Q4_K_M formats. (wm, ks): BM = 32 wm rows, ks = 1 (4 waves)
 # or 2 (8 waves splitting each k-tile's k-steps); 128 columns per workgroup; K split in whole super-blocks.
 QMM2 = os.environ.get("MX_QMM2", "0") != "0"
-QMM2_FORCE: tuple | None = None  # (wm, ks, splits) override for tuning (tools/tune_qmm2.py)
-QMM2_CONFIGS = ((2, 1), (2, 2), (4, 1), (4, 2), (6, 1), (8, 1), (8, 2))
+QMM2_FORCE: tuple | None = None  # (wm, ks, wn, splits) override for tuning (tools/tune_qmm2.py)
+# compiled (wm, ks, wn): wm 32-row MFMA blocks x wn 32-column groups per wave, ks 1 / 2 waves per SIMD
+QMM2_CONFIGS = ((2, 1, 1), (2, 2, 1), (4, 1, 1), (4, 2, 1), (8, 1, 1), (1, 2, 2), (2, 1, 2), (2, 2, 2), (4, 1, 2))
 QMM2_QTYPES = (int(QType.Q4_K), int(QType.Q6_K), int(QType.Q3_K), int(QType.Q2_K))
 QMM2_ONLY = tuple(int(q) for q in Q.QMM2_ONLY)  # no qmm.hip variant: qmm2 for every M > 4
 QMM2_MIN_M = int(os.environ.get("MX_QMM2_MIN_M", "16"))
 
 
-def _qmm2_shape(M: int, N_: int, K: int, can_split: bool):
-    """(wm, ks, splits) for qmm2: the smallest row tile covering M (up to 256 rows per workgroup), then K
-    splits (split-able outputs only) until ~3/4 of the CUs hold a workgroup, >= 2 super-blocks per split."""
-    if QMM2_FORCE is not None:
-        wm, ks, splits = QMM2_FORCE
-        return wm, ks, (splits if can_split else 1)
-    if M <= 64:
-        wm, ks = 2, 2
-    elif M <= 128:
-        wm, ks = 4, 2
-    elif M <= 192:
-        wm, ks = 6, 1
-    else:
-        wm, ks = 8, 1
-    tiles = -(-M // (32 * wm)) * -(-N_ // 128)
+# K-quant GEMM choice (MX_GEMM_POLICY=auto): per (M bucket, shape class) the kernel / tile that won the round-4
+# sweep on the Llama-3-8B projections (profiles/r4_qmm_tune.md): qmm2 (one role per wave) for M <= 128 except the
+# narrow o_proj, qmm3 (warp-specialised) above; "r3" keeps the round-3 qmm.hip / qmm_ws path.
+GEMM_POLICY = os.environ.get("MX_GEMM_POLICY", "auto")
+
+
+def _split_for(tiles: int, K: int, can_split: bool) -> int:
     splits = 1
     if can_split:
         nsb = K // 256
         while tiles * splits < (3 * CU_COUNT) // 4 and nsb // (splits * 2) >= 2:
             splits *= 2
-    return wm, ks, splits
+    return splits
+
+
+def _gemm_pick(M: int, N_: int, K: int, qtype: int, can_split: bool):
+    """("q3", wm, splits) | ("q2", wm, ks, wn, splits) | None (round-3 kernels) for a t32 K-quant GEMM."""
+    if qtype not in QMM2_QTYPES:
+        return None
+    if QMM3 and M >= QMM3_MIN_M:  # explicit overrides (tests, tuning)
+        return ("q3", *_qmm3_shape(M, N_, K, can_split))
+    if (QMM2 and M >= QMM2_MIN_M) or qtype in QMM2_ONLY:
+        return ("q2", *_qmm2_shape(M, N_, K, can_split))
+    if GEMM_POLICY != "auto" or M < 16 or QMM_FORCE is not None or QMM_WS_FORCE is not None:
+        return None
+    nct = -(-N_ // 128)
+    wide = N_ >= 16384
+    if M <= 64:
+        return ("q2", 2, 2, 1, _split_for(-(-M // 64) * nct, K, can_split))
+    if M <= 128:
+        if not wide and K < 8192 and N_ <= 4096:  # o_proj
+            return ("q3", 1, _split_for(-(-M // 64) * nct, K, can_split))
+        if not wide and K >= 8192:  # down
+            return ("q2", 2, 1, 1, _split_for(-(-M // 64) * nct, K, can_split))
+        return ("q2", 4, 2, 1, _split_for(-(-M // 128) * nct, K, can_split))
+    wm = 4 if wide else (1 if (N_ <= 4096 and K < 8192 and M <= 256) else 2)
+    return ("q3", wm, _split_for(-(-M // (64 * wm)) * nct, K, can_split))
+
+
+# qmm3.hip: warp-specialised (4 DMA / dequant waves + 4 MFMA waves per workgroup), BM = 64 wm rows
+QMM3 = os.environ.get("MX_QMM3", "0") != "0"
+QMM3_FORCE: tuple | None = None  # (wm, splits) override for tuning
+QMM3_MIN_M = int(os.environ.get("MX_QMM3_MIN_M", "64"))
+
+
+def _qmm3_shape(M: int, N_: int, K: int, can_split: bool):
+    """(wm, splits) for qmm3: the smallest row tile (64 / 128 / 256 rows) covering M, then K splits as qmm2."""
+    if QMM3_FORCE is not None:
+        wm, splits = QMM3_FORCE
+        return wm, (splits if can_split else 1)
+    wm = 1 if M <= 64 else 2 if M <= 128 else 4
+    tiles = -(-M // (64 * wm)) * -(-N_ // 128)
+    splits = 1
+    if can_split:
+        nsb = K // 256
+        while tiles * splits < (3 * CU_COUNT) // 4 and nsb // (splits * 2) >= 2:
+            splits *= 2
+    return wm, splits
+
+
+def _qmm2_shape(M: int, N_: int, K: int, can_split: bool):
+    """(wm, ks, wn, splits) for qmm2: the smallest row tile covering M (up to 256 rows per workgroup), then K
+    splits (split-able outputs only) until ~3/4 of the CUs hold a workgroup, >= 2 super-blocks per split."""
+    if QMM2_FORCE is not None:
+        wm, ks, wn, splits = QMM2_FORCE
+        return wm, ks, wn, (splits if can_split else 1)
+    if M <= 64:
+        wm, ks, wn = 1, 2, 2
+    elif M <= 128:
+        wm, ks, wn = 2, 2, 2
+    else:
+        wm, ks, wn = 4, 1, 2
+    tiles = -(-M // (32 * wm * wn)) * -(-N_ // 128)
+    splits = 1
+    if can_split:
+        nsb = K // 256
+        while tiles * splits < (3 * CU_COUNT) // 4 and nsb // (splits * 2) >= 2:
+            splits *= 2
+    return wm, ks, wn, splits
 
 
 # qmm_ws.hip: warp-specialised variant (4 producer waves: LDS-DMA + dequant into an f16 B tile; 4 MFMA-only

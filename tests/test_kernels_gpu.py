@@ -408,6 +408,46 @@ def test_qmm(qt, M, wm, wn, nw, ks, splits, monkeypatch):
     monkeypatch.setattr(L, "QMM_FORCE", (wm, wn, nw, ks, splits))
     monkeypatch.setattr(L, "QMM2", False)
     n, k = 416, 2304  # 416 = 3.25 x 128 columns: partial column tiles (multiple of 32 for the GLU)
+    raw, dense = make_w(qt, n, k, seed=M + 7 * wm + 3 * wn)
+    W = QWeight.from_ggml(raw, qt, n, k, DEV, t32=True)
+    assert W.to_t32() and W.layout == "t32"
+    x = torch.randn(M, k, device=DEV).half()
+    ref = x.float().cpu() @ dense.t()
+    out = torch.empty(M, n, device=DEV)
+    qmatmul(W, x, EPI_F32, out)
+    assert rel(out, ref) < 5e-3
+    z = torch.zeros(M, n, device=DEV)
+    qmatmul(W, x, EPI_F32, z, out_zeroed=True)
+    assert rel(z, ref) < 5e-3
+    acc = torch.randn(M, n, device=DEV)
+    acc0 = acc.clone()
+    qmatmul(W, x, EPI_ADD_F32, acc)
+    assert rel(acc - acc0, ref) < 5e-3
+    ob = torch.empty(M, n, dtype=torch.float16, device=DEV)
+    qmatmul(W, x, EPI_BF16, ob)
+    assert rel(ob, ref) < 5e-3
+    sw = torch.empty(M, n // 2, dtype=torch.float16, device=DEV)
+    qmatmul(W, x, EPI_SWIGLU, sw)
+    g = ref.reshape(M, n // 32, 2, 16)
+    ref_sw = torch.nn.functional.silu(g[:, :, 0].reshape(M, -1)) * g[:, :, 1].reshape(M, -1)
+    assert rel(sw, ref_sw) < 1e-2
+
+
+@pytest.mark.parametrize("qt", [QType.Q4_K, QType.Q6_K, QType.Q3_K, QType.Q2_K])
+@pytest.mark.parametrize("M,wm,ks,wn,splits", [
+    (64, 2, 1, 1, 1), (64, 2, 2, 1, 3), (17, 2, 2, 1, 1), (128, 4, 2, 1, 1), (77, 4, 2, 1, 2), (128, 4, 1, 1, 4),
+    (256, 8, 1, 1, 1), (300, 8, 1, 1, 3), (511, 8, 1, 1, 1), (100, 2, 1, 1, 5),
+    (64, 1, 2, 2, 1), (40, 1, 2, 2, 3), (128, 2, 1, 2, 1), (200, 2, 2, 2, 2), (256, 4, 1, 2, 1), (300, 4, 1, 2, 3),
+    (511, 4, 1, 2, 2)])
+def test_qmm2(qt, M, wm, ks, wn, splits, monkeypatch):
+    """qmm2.hip for every epilogue and tile / split-K choice, incl. ragged M / N tails (416 columns = 3.25
+    workgroup tiles; with wn = 2 a wave's second group may lie past N), split counts that do not divide the
+    super-blocks, the 8-wave k-step split (ks = 2) and the 2-group wave tiles (wn = 2), against the fp32
+    product of the dequantised weight."""
+    from localai_tfp_amd.ops import linear as L
+    monkeypatch.setattr(L, "QMM2", True)
+    monkeypatch.setattr(L, "QMM2_FORCE", (wm, ks, wn, splits))
+    n, k = 416, 2304
     raw, dense = make_w(qt, n, k, seed=M + 7 * wm)
     W = QWeight.from_ggml(raw, qt, n, k, DEV, t32=True)
     assert W.to_t32() and W.layout == "t32"
@@ -434,16 +474,16 @@ def test_qmm(qt, M, wm, wn, nw, ks, splits, monkeypatch):
 
 
 @pytest.mark.parametrize("qt", [QType.Q4_K, QType.Q6_K, QType.Q3_K, QType.Q2_K])
-@pytest.mark.parametrize("M,wm,ks,splits", [
-    (64, 2, 1, 1), (64, 2, 2, 3), (17, 2, 2, 1), (128, 4, 2, 1), (77, 4, 2, 2), (128, 4, 1, 4), (200, 6, 1, 1),
-    (256, 8, 1, 1), (300, 8, 1, 3), (256, 8, 2, 2), (511, 8, 1, 1), (100, 2, 1, 5)])
-def test_qmm2(qt, M, wm, ks, splits, monkeypatch):
-    """qmm2.hip for every epilogue and tile / split-K choice, incl. ragged M / N tails (416 columns = 3.25
-    workgroup tiles), split counts that do not divide the super-blocks and the 8-wave k-step split (ks = 2),
-    against the fp32 product of the dequantised weight."""
+@pytest.mark.parametrize("M,wm,splits", [
+    (64, 1, 1), (40, 1, 3), (128, 2, 1), (77, 2, 2), (200, 2, 5), (256, 4, 1), (300, 4, 3), (511, 4, 2), (17, 1, 1)])
+def test_qmm3(qt, M, wm, splits, monkeypatch):
+    """qmm3.hip (warp-specialised producer / consumer waves) for every epilogue, row tile and split-K choice,
+    incl. ragged M / N tails (416 columns: a consumer's second group past N) and split counts that do not
+    divide the super-blocks, against the fp32 product of the dequantised weight."""
     from localai_tfp_amd.ops import linear as L
-    monkeypatch.setattr(L, "QMM2", True)
-    monkeypatch.setattr(L, "QMM2_FORCE", (wm, ks, splits))
+    monkeypatch.setattr(L, "QMM3", True)
+    monkeypatch.setattr(L, "QMM3_MIN_M", 1)
+    monkeypatch.setattr(L, "QMM3_FORCE", (wm, splits))
     n, k = 416, 2304
     raw, dense = make_w(qt, n, k, seed=M + 7 * wm)
     W = QWeight.from_ggml(raw, qt, n, k, DEV, t32=True)

@@ -5,7 +5,7 @@
 #   bash tools/gpu_profile.sh engine [CONC] [STEPS]   rocprofv3 kernel trace of the in-process engine bench at
 #                                                    concurrency CONC (default 128): per-kernel table per step
 #   bash tools/gpu_profile.sh pmc SHAPE M CFG          counter passes (MFMA / VALU / LDS / waits) of one qmm2
-#                                                    configuration "wm,ks,splits" on a Llama-3-8B projection
+#                                                    configuration "wm,ks,wn,splits" on a Llama-3-8B projection
 #   bash tools/gpu_profile.sh gemm [MS] [SHAPES]       qmm2 vs round-3 qmm vs hipBLASLt-on-dense sweep (JSONL)
 #
 # Every GPU step runs under its own timeout; counter passes stay within the per-block slot limits (8 SQ).

@@ -23,8 +23,9 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--gemv", action="store_true", help="M <= 4 decode GEMV with the fused RMSNorm / q8 prologue")
     ap.add_argument("--ws", default="", help="qmm_ws cfg,splits (warp-specialised kernel)")
-    ap.add_argument("--q2", default="", help="qmm2 wm,ks,splits")
-    ap.add_argument("--q2dbg", default="", help="qmm2 isolation build dbg,wm (Q4_K SwiGLU only)")
+    ap.add_argument("--q2", default="", help="qmm2 wm,ks,wn,splits")
+    ap.add_argument("--q3dbg", default="", help="qmm3 isolation build dbg,wm (Q4_K SwiGLU only)")
+    ap.add_argument("--q2dbg", default="", help="qmm2 isolation build dbg,wm,ks,wn (Q4_K SwiGLU only)")
     ap.add_argument("--qt", type=int, default=0, help="ggml type override (e.g. 3 = Q4_1 -> MX4F t32)")
     a = ap.parse_args()
     from localai_tfp_amd.ops import linear as L
@@ -48,13 +49,21 @@ def main():
         call = (lambda: L.qmv_fused(W, h, epi, out, norm=nw, eps=1e-5, out_zeroed=True)) if K == 4096 else \
             (lambda: L.qmv_fused(W, x, epi, out, out_zeroed=True))
         assert call()
-    elif a.q2dbg:
+    elif a.q3dbg:
         from localai_tfp_amd import _native as Nn
-        dbg, wm = (int(v) for v in a.q2dbg.split(","))
+        dbg, wm = (int(v) for v in a.q3dbg.split(","))
         Nn.ensure_act(torch.float16)
 
         def call():
-            Nn.kcall("mxk_qmm2_dbg", dbg, wm, x.data_ptr(), x.stride(0), W.data.data_ptr(), a.M, N, K, out.data_ptr(),
+            Nn.kcall("mxk_qmm3_dbg", dbg, wm, x.data_ptr(), x.stride(0), W.data.data_ptr(), a.M, N, K, out.data_ptr(),
+                     out.stride(0), Nn.stream_ptr())
+    elif a.q2dbg:
+        from localai_tfp_amd import _native as Nn
+        dbg, wm, ks, wn = (int(v) for v in a.q2dbg.split(","))
+        Nn.ensure_act(torch.float16)
+
+        def call():
+            Nn.kcall("mxk_qmm2_dbg", dbg, wm, ks, wn, x.data_ptr(), x.stride(0), W.data.data_ptr(), a.M, N, K, out.data_ptr(),
                      out.stride(0), Nn.stream_ptr())
     else:
         def call():
@@ -69,7 +78,7 @@ def main():
     e1.record()
     torch.cuda.synchronize()
     us = e0.elapsed_time(e1) / a.iters * 1e3
-    cfg = ("qmv_fused" if a.gemv else f"q2dbg {a.q2dbg}" if a.q2dbg else
+    cfg = ("qmv_fused" if a.gemv else f"q2dbg {a.q2dbg}" if a.q2dbg else f"q3dbg {a.q3dbg}" if a.q3dbg else
            f"qmm2 {L._qmm2_shape(a.M, N, K, epi in (0, 2))}" if a.q2 else L._qmm_shape(a.M, N, K, epi in (0, 2)))
     print(f"{a.shape} qt={int(W.qtype)} M={a.M} cfg={cfg} {us:.1f} us {2*a.M*N*K/us/1e6:.0f} TF {W.data.numel() / us / 1e6:.2f} TB/s weights")
 

@@ -13,6 +13,7 @@ import sqlite3
 
 
 def _short(name: str) -> str:
+    name = name.replace("(anonymous namespace)::", "")
     name = re.sub(r"\(.*\)$", "", name)
     if name.startswith("Cijk_") or name.startswith("Custom_Cijk"):
         mt = re.search(r"MT\d+x\d+x\d+", name)

@@ -78,11 +78,21 @@ def main():
             cands = {}
 
             def run_old():
+                L.QMM2, L.GEMM_POLICY = False, "r3"
+                L.qmatmul(Wt, x, epi, out, out_zeroed=True)
+                L.QMM2, L.GEMM_POLICY = True, "auto"
+
+            def run_policy():
                 L.QMM2 = False
                 L.qmatmul(Wt, x, epi, out, out_zeroed=True)
                 L.QMM2 = True
 
             cands["qmm_r3"] = run_old
+            cands["policy"] = run_policy
+            L.QMM2 = False
+            errs["policy"] = round(err(), 6)
+            pol = L._gemm_pick(M, N, K, int(qt), can_split)
+            L.QMM2 = True
             if epi == L.EPI_SWIGLU:
                 cands["dense_f16"] = lambda: L._dense_cached(_DW(dense), x, epi, out, M)
             elif epi == L.EPI_ADD_F32:
@@ -91,7 +101,10 @@ def main():
                 cands["dense_f16"] = lambda: torch.mm(x, dense.t(), out_dtype=torch.float32, out=out)
             L.QMM2_FORCE = None
             auto = L._qmm2_shape(M, N, K, can_split)
-            cfgs = [(*c, sp) for c in L.QMM2_CONFIGS for sp in ((1, 2, 4, 8) if can_split else (1,))] if full else []
+            if full:
+                cfgs = [(*c, sp) for c in L.QMM2_CONFIGS for sp in ((1, 2, 4, 8) if can_split else (1,))]
+            else:  # every tile shape whose row tile is not more than twice M, at the auto split count
+                cfgs = [(*c, auto[3]) for c in L.QMM2_CONFIGS if 32 * c[0] * c[2] <= 2 * M and (*c, auto[3]) != auto]
             errs = {}
             for cfg in [auto] + cfgs:
                 L.QMM2_FORCE = cfg
@@ -104,6 +117,25 @@ def main():
                         L.qmatmul(Wt, x, epi, out, out_zeroed=True)
                     return f
                 cands["qmm2" + str(list(cfg))] = mk(cfg)
+            # qmm3 (warp-specialised) row tiles, each at the split count qmm3's heuristic gives that tile
+            for wm3 in (1, 2, 4):
+                if wm3 > 1 and 64 * wm3 > 2 * M:
+                    continue
+                tiles3 = -(-M // (64 * wm3)) * -(-N // 128)
+                sp3 = 1
+                while can_split and tiles3 * sp3 < 3 * L.CU_COUNT // 4 and (K // 256) // (sp3 * 2) >= 2:
+                    sp3 *= 2
+                L.QMM3, L.QMM3_FORCE = True, (wm3, sp3)
+                errs[f"q3[{wm3},{sp3}]"] = round(err(), 6)
+                L.QMM3 = False
+
+                def mk3(c):
+                    def f():
+                        L.QMM3, L.QMM3_FORCE = True, c
+                        L.qmatmul(Wt, x, epi, out, out_zeroed=True)
+                        L.QMM3 = False
+                    return f
+                cands[f"qmm3[{wm3}, {sp3}]"] = mk3((wm3, sp3))
             from localai_tfp_amd import _native as Nn
             xp = torch.empty(M, K + 64, device=dev, dtype=torch.float16)[:, :K]
             xp.copy_(x)
@@ -133,10 +165,18 @@ def main():
             res = {"shape": name, "M": M, "auto": list(auto)}
             med = {k: float(np.median(v)) for k, v in times.items()}
             res["qmm_r3_us"] = round(med.pop("qmm_r3"), 2)
+            res["policy"] = [str(pol), round(med.pop("policy"), 2)]
             res["dense_f16_us"] = round(med.pop("dense_f16"), 2)
             res["qmm2_auto_us"] = round(med["qmm2" + str(list(auto))], 2)
             res["qmm2_rot_us"] = round(med.pop("qmm2_rot"), 2)
             res["qmm2_padlda_us"] = round(med.pop("qmm2_pad"), 2)
+            q3 = {k: v for k, v in med.items() if k.startswith("qmm3")}
+            if q3:
+                b3 = min(q3, key=q3.get)
+                res["qmm3_best"] = [b3[4:], round(q3[b3], 2)]
+                for k in q3:
+                    med.pop(k)
+                res["qmm3_all"] = {k[4:]: round(v, 2) for k, v in q3.items()}
             best = min(med, key=med.get)
             res["qmm2_best"] = [best[4:], round(med[best], 2)]
             flops = 2.0 * M * N * K
