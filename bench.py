@@ -48,6 +48,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=200)
     ap.add_argument("--model", default="llama3-8b", choices=["llama3-8b", "llama3-70b", "llama32-1b"])
     ap.add_argument("--path", default="http", choices=["http", "engine"])
+    ap.add_argument("--ftype", default="Q4_K_M", choices=["Q4_K_M", "Q3_K_M"],
+                    help="block-format mix of the synthetic checkpoint (the headline config is Q4_K_M)")
     ap.add_argument("--concurrency", type=int, default=128)
     ap.add_argument("--prompt-len", type=int, default=256)
     ap.add_argument("--gen-len", type=int, default=256)
@@ -77,7 +79,11 @@ def parse():
 
 
 SAMPLING = {"reference": {"temperature": 0.9, "top_k": 40, "top_p": 0.95},
-            "greedy": {"temperature": 0.0}}
+            "greedy": {"temperature": 0.0},
+            # the reference defaults plus a repetition penalty / a JSON-mode grammar (HTTP path only): requests
+            # that need host state per token stay on the overlap pipeline
+            "penalty": {"temperature": 0.9, "top_k": 40, "top_p": 0.95, "frequency_penalty": 0.5},
+            "json": {"temperature": 0.9, "top_k": 40, "top_p": 0.95, "json": True}}
 
 
 def make_tokenizer(kind: str, vocab: int):
@@ -210,7 +216,7 @@ def main():
                       flush=True)
         dist = dist_leaders  # bench barriers / reductions run among the replica leaders only
     t0 = time.time()
-    src = synthetic_source(cfg, "Q4_K_M", seed=1, shard_gen=tp > 1 or rehearsal > 1)
+    src = synthetic_source(cfg, args.ftype, seed=1, shard_gen=tp > 1 or rehearsal > 1)
     if rehearsal > 1:
         model = LlamaModel.load(cfg, src, dev, 0, rehearsal, None)
     else:
@@ -278,11 +284,11 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": act_name,
-            "data": f"synthetic (random-init {cfg.name} weights in real Q4_K_M block formats; synthetic chat prompts)",
+            "data": f"synthetic (random-init {cfg.name} weights in real {args.ftype} block formats; synthetic chat prompts)",
             "p50_ttft_ms": round(p50_all, 2),
             "p99_ttft_ms": round(p99_all, 2),
             "config": {
-                "model": cfg.name + " Q4_K_M", "global_batch": args.concurrency * dp,
+                "model": cfg.name + " " + args.ftype, "global_batch": args.concurrency * dp,
                 "seq_len": args.prompt_len + args.gen_len, "prompt_len": args.prompt_len, "gen_len": args.gen_len,
                 "concurrency_per_replica": args.concurrency,
                 "parallelism": (f"tp{rehearsal}-rehearsal (rank 0 shard on 1 GPU, collectives no-op)" if rehearsal > 1 else
@@ -409,6 +415,10 @@ def run_http(args, eng, tok, cfg, dev, dist):
             samp_args = ["--temperature", str(sp["temperature"])]
             if "top_k" in sp:
                 samp_args += ["--top-k", str(sp["top_k"]), "--top-p", str(sp["top_p"])]
+            if sp.get("frequency_penalty"):
+                samp_args += ["--frequency-penalty", str(sp["frequency_penalty"])]
+            if sp.get("json"):
+                samp_args += ["--json"]
             win = Window(eng, args.warmup, args.steps, dev, dist, steady_gate(args),
                          base_finished=eng.stats["finished"])
             eng.on_step = win
@@ -500,6 +510,8 @@ def run_engine(args, eng, tok, dev, dist):
         return tok.encode(render_chat([{"role": "user", "content": body}], tok))
 
     phase = args.phases.split(",")[0]
+    if SAMPLING[phase].get("json"):
+        raise SystemExit("the json phase needs the HTTP path (response_format is an API-level option)")
     sp = SamplingParams(**SAMPLING[phase], ignore_eos=True) if phase != "greedy" else \
         SamplingParams(temperature=0.0, top_k=1, ignore_eos=True)
     handles = {}

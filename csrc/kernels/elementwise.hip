@@ -162,6 +162,32 @@ extern "C" int mxk_add_bias_f32(float* x, int ld, const float* b, int rows, int 
     MXK_CHECK_LAUNCH();
 }
 
+// h (fp32 residual) += y (16-bit activations), 4 elements per thread: the residual add of a row-parallel
+// projection when no fused all-reduce+add kernel runs (TP rehearsal on one GPU, RCCL fallback) — one pass,
+// instead of PyTorch's mixed-dtype templated add
+template <bool F16>
+__global__ __launch_bounds__(256) void add_act_into_f32_kernel(const uint16_t* __restrict__ y, int ldy,
+                                                               float* __restrict__ h, int ldh, int cols) {
+    const int r = blockIdx.y;
+    for (int c = (blockIdx.x * 256 + threadIdx.x) * 4; c < cols; c += gridDim.x * 256 * 4) {
+        const uint2 raw = *(const uint2*)(y + (size_t)r * ldy + c);
+        float4 o = *(float4*)(h + (size_t)r * ldh + c);
+        float a0, a1, a2, a3;
+        unpack_act2<F16>(raw.x, a0, a1);
+        unpack_act2<F16>(raw.y, a2, a3);
+        o.x += a0; o.y += a1; o.z += a2; o.w += a3;
+        *(float4*)(h + (size_t)r * ldh + c) = o;
+    }
+}
+
+extern "C" int mxk_add_act_into_f32(const uint16_t* y, int ldy, float* h, int ldh, int rows, int cols, hipStream_t st) {
+    if (rows <= 0) return 0;
+    if ((cols & 3) || (ldy & 3) || (ldh & 3) || ((uintptr_t)y & 7) || ((uintptr_t)h & 15)) return (int)hipErrorInvalidValue;
+    dim3 grid(min(16, (cols + 1023) / 1024), rows);
+    MX_ACT_DISPATCH(add_act_into_f32_kernel<F16><<<grid, 256, 0, st>>>(y, ldy, h, ldh, cols));
+    MXK_CHECK_LAUNCH();
+}
+
 // gather selected rows of an fp32 matrix (last-token-of-each-sequence selection before the LM head)
 __global__ __launch_bounds__(256) void select_rows_f32_kernel(const float* __restrict__ x, int ld,
                                                               const int* __restrict__ idx, int cols,

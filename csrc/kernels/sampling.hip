@@ -443,15 +443,14 @@ extern "C" int mxk_sample_params_size() { return (int)sizeof(SampleParams); }
 // whose hot bins serialise on atomics (227 us at 128 rows). With top-k <= TK_CAP on, every quantity the
 // chain needs lives in the global top-k set (top-p's target is top_p x the top-k mass, min-p is relative to
 // the max), and the global top-k set is contained in the union of the per-slice top-k sets:
-//   tk_slice_kernel (B x S workgroups of 256): the slice (NV values per thread) is held in registers as
-//     order-preserving integer keys; the slice's K-th largest key is found by bisection on the key axis
-//     with register counts + one block reduction per step (no atomics, no re-reads), stopping as soon as
-//     the kept set fits; the candidates (>= that key) are written unsorted, with an overflow flag when
-//     exact ties exceed the capacity;
-//   tk_merge_kernel (B workgroups of 1024): the S x <= TK_CAPS candidates in registers, the same exact
-//     bisection for the global K-th value, the kept set sorted in LDS, exact truncation, Gumbel-max draw.
+//   tk_slice_kernel (B x S workgroups of 256): the slice (NV values per thread) held in registers, one LDS
+//     histogram of the distance below the slice max picks the whole bins that hold the slice's top-K
+//     (candidates written unsorted; key bisection only for a bin denser than the capacity);
+//   tk_merge_kernel (B workgroups of 1024): the S x <= TK_CAPS candidates in registers, the same histogram
+//     against the row max for the global top-K's bins, a one-pass rank sort of the <= 256 kept values in
+//     LDS, exact top-K / min-p / top-p truncation, Gumbel-max draw.
 //     A row whose slices overflowed falls back to the full-row bisection chain (sample_row_bisect).
-constexpr int TK_CAP = 64, TK_NT = 256, TK_NV = 16, TK_CAPS = 2 * TK_CAP, TK_MNT = 1024, TK_MV = 8;
+constexpr int TK_CAP = 64, TK_NT = 256, TK_NV = 32, TK_CAPS = 2 * TK_CAP, TK_MNT = 1024, TK_MV = 8;
 constexpr int TK_SLICE = TK_NT * TK_NV;  // vocabulary entries per slice
 constexpr float TK_HR = 48.f;            // values more than this below the slice max are never candidates
 
@@ -469,12 +468,16 @@ __global__ __launch_bounds__(TK_NT) void tk_penalty_kernel(float* logits, int ld
     penalize<TK_NT>(logits + (size_t)blockIdx.x * ld, V, P, pen_tok, pen_cnt, pen_bias, pend_tok, &s_found);
 }
 
-// block-wide count of keys >= t over NV registers per thread; `red` double-buffered by the caller's parity
-template <int NT, int NV>
-MX_DEV int tk_count(const uint32_t (&u)[NV], uint32_t t, int* red, int par) {
+MX_DEV uint32_t tk_key(uint32_t u) { return u; }
+MX_DEV uint32_t tk_key(float v) { return ord_key(v); }
+
+// block-wide count of keys >= t over NV registers per thread (keys, or floats keyed on the fly);
+// `red` double-buffered by the caller's parity
+template <int NT, int NV, typename T>
+MX_DEV int tk_count(const T (&u)[NV], uint32_t t, int* red, int par) {
     int c = 0;
 #pragma unroll
-    for (int j = 0; j < NV; ++j) c += u[j] >= t ? 1 : 0;
+    for (int j = 0; j < NV; ++j) c += tk_key(u[j]) >= t ? 1 : 0;
     c = wave_sum_i(c);
     if ((threadIdx.x & 63) == 0) red[par * (NT / 64) + (threadIdx.x >> 6)] = c;
     __syncthreads();
@@ -487,19 +490,72 @@ MX_DEV int tk_count(const uint32_t (&u)[NV], uint32_t t, int* red, int par) {
 // largest key T with count(keys >= T) >= K, searched in [lo, hi) (count(>= lo) known = c_lo >= K,
 // count(>= hi) < K). exact = false: stop as soon as count(>= T) <= cap (a superset of the top-K set that
 // fits); exact = true: stop only at the K-th key itself (or when count(>= T) == K, which is the same set).
-template <int NT, int NV>
-MX_DEV uint32_t tk_bisect(const uint32_t (&u)[NV], int K, uint32_t lo, uint32_t hi, int& c_lo, int cap, bool exact,
+template <int NT, int NV, typename T>
+MX_DEV uint32_t tk_bisect(const T (&u)[NV], int K, uint32_t lo, uint32_t hi, int& c_lo, int cap, bool exact,
                           int* red, int par) {
     while (hi - lo > 1u) {
         if (exact ? c_lo == K : c_lo <= cap) break;
         const uint32_t mid = lo + ((hi - lo) >> 1);
-        const int c = tk_count<NT, NV>(u, mid, red, par);
+        const int c = tk_count<NT, NV, T>(u, mid, red, par);
         par ^= 1;
         if (c >= K) { lo = mid; c_lo = c; }
         else hi = mid;
     }
     return lo;
 }
+
+// Candidate selection by one LDS histogram of the distance d below the max (TK_NB monotone bins: 1/32 logit
+// unit for d < 4, 1/8 for d < 12, 1/2 for d < 44; beyond that no bin): every value is binned once (an LDS
+// atomic only inside the range), one wave scans the bins from the top for the first cumulative count >= K, and
+// everything in bins <= that one is the candidate set — 4 block barriers instead of a ~20-step bisection
+// (round 3: 45 + 33 us at 128 rows). A bin too dense for the capacity (flat rows, exact ties) or a row with
+// fewer than K values inside the histogram range falls back to the bisection on the key axis.
+constexpr int TK_NB = 256;
+
+MX_DEV int tk_bin(float mx, float v) {  // monotone in v (0 = the top), TK_NB = outside the range / masked
+    const float d = mx - v;
+    if (d < 4.f) return (int)(d * 32.f);                    // bins 0 .. 127
+    if (d < 12.f) return 128 + (int)((d - 4.f) * 8.f);      // 128 .. 191
+    if (d < 44.f) return 192 + (int)((d - 12.f) * 2.f);     // 192 .. 255
+    return TK_NB;                                           // -inf / NaN fail every compare
+}
+
+// first bin b (scanning from the top) whose cumulative count reaches K: {b, cum(b)}; {TK_NB, total} if none.
+// Called by one full wave; hist[TK_NB] in LDS.
+MX_DEV int2 tk_scan_bins(const int* hist, int K) {
+    const int lane = threadIdx.x & 63;
+    int4 h = *(const int4*)(hist + 4 * lane);  // bins 4 lane .. 4 lane + 3
+    const int own = h.x + h.y + h.z + h.w;
+    int inc = own;  // inclusive prefix over lanes
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int t = __shfl_up(inc, o, 64);
+        if (lane >= o) inc += t;
+    }
+    const int exc = inc - own;
+    const unsigned long long hit = __ballot(inc >= K);
+    if (!hit) return make_int2(TK_NB, __shfl(inc, 63, 64));
+    const int L = __builtin_ctzll(hit);
+    int b = 4 * L, c = __shfl(exc, L, 64);
+    const int4 hl = make_int4(__shfl(h.x, L, 64), __shfl(h.y, L, 64), __shfl(h.z, L, 64), __shfl(h.w, L, 64));
+    c += hl.x;
+    if (c < K) { ++b; c += hl.y; }
+    if (c < K) { ++b; c += hl.z; }
+    if (c < K) { ++b; c += hl.w; }
+    return make_int2(b, c);
+}
+
+// block barrier for LDS hand-offs only: __syncthreads() also waits for every outstanding global store of the
+// wave (vmcnt(0) before the barrier), which after the candidate writes cost several microseconds per slice
+MX_DEV void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+__device__ int g_tk_trace;                    // phase timestamps of workgroup (0, 0) (tools/time_sampler.py --trace)
+__device__ unsigned long long g_tk_ts[16];
+#define TK_TS(k)                                                                                         \
+    if (g_tk_trace && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {                          \
+        volatile unsigned long long* ts_ = g_tk_ts;                                                      \
+        ts_[k] = wall_clock64();                                                                         \
+    }
 
 __global__ __launch_bounds__(TK_NT) void tk_slice_kernel(const float* __restrict__ logits, int ld, int V,
                                                         const SampleParams* __restrict__ params,
@@ -508,58 +564,147 @@ __global__ __launch_bounds__(TK_NT) void tk_slice_kernel(const float* __restrict
                                                         int* __restrict__ cand_n, float2* __restrict__ slice_z) {
     __shared__ float fred[2 * TK_NT / 64];
     __shared__ int red[2 * TK_NT / 64];
-    __shared__ int s_n;
+    __shared__ __attribute__((aligned(16))) int hist[TK_NB], hist2[TK_NB];
+    __shared__ int s_n, s_b, s_fb;
     const int row = blockIdx.x, S = gridDim.y, sl = blockIdx.y;
     const SampleParams P = params[row];
     const int K = P.temperature <= 0.f ? 1 : min(P.top_k, TK_CAP);
     const float itemp = P.temperature <= 0.f ? 1.f : 1.f / P.temperature;
     const float* x = logits + (size_t)row * ld;
     const uint32_t* am = allow_mask ? allow_mask + (size_t)row * mask_ld : nullptr;
+    TK_TS(0)
     const int i0 = sl * TK_SLICE, i1 = min(V, i0 + TK_SLICE);
     float v[TK_NV];
-    uint32_t u[TK_NV];
     float mx = -INFINITY;
+    // branch-free loads (clamped index, masked after): a conditional load per value made the compiler wait
+    // for each one before the next (vmcnt(0) per load, ~1 us of HBM latency each)
+#pragma unroll
+    for (int j = 0; j < TK_NV; ++j) v[j] = __builtin_nontemporal_load(x + min(i0 + j * TK_NT + (int)threadIdx.x, i1 - 1));
+    if (am) {
+        uint32_t w[TK_NV];
+#pragma unroll
+        for (int j = 0; j < TK_NV; ++j) w[j] = am[min(i0 + j * TK_NT + (int)threadIdx.x, i1 - 1) >> 5];
+#pragma unroll
+        for (int j = 0; j < TK_NV; ++j)
+            if (!((w[j] >> ((i0 + j * TK_NT + threadIdx.x) & 31)) & 1u)) v[j] = -INFINITY;
+    }
 #pragma unroll
     for (int j = 0; j < TK_NV; ++j) {
-        const int i = i0 + j * TK_NT + threadIdx.x;
-        float t = -INFINITY;
-        if (i < i1) {
-            t = __builtin_nontemporal_load(x + i) * itemp;
-            if (am && !((am[i >> 5] >> (i & 31)) & 1u)) t = -INFINITY;
-        }
-        v[j] = t;
-        mx = fmaxf(mx, t);
+        v[j] = i0 + j * TK_NT + (int)threadIdx.x < i1 ? v[j] * itemp : -INFINITY;
+        mx = fmaxf(mx, v[j]);
     }
+    TK_TS(1)
+    const float tmax = mx;  // this thread's largest value
     mx = wave_max(mx);
     if ((threadIdx.x & 63) == 0) fred[threadIdx.x >> 6] = mx;
+    hist[threadIdx.x] = 0;  // TK_NB == TK_NT
+    hist2[threadIdx.x] = 0;
     if (threadIdx.x == 0) s_n = 0;
     __syncthreads();
 #pragma unroll
     for (int w = 0; w < TK_NT / 64; ++w) mx = fmaxf(mx, fred[w]);
+    // pass 1: the threads' maxima only (one atomic per thread). Its K-th largest is a lower bound of the
+    // slice's K-th largest value (K threads each hold a value >= it), so only values in bins <= that
+    // bin go into pass 2 — a few hundred LDS atomics instead of one per value on flat rows
+    {
+        const int tb = tk_bin(mx, tmax);
+        if (tb < TK_NB) atomicAdd(&hist[tb], 1);
+    }
     float zs = 0.f;  // the slice's share of the row's partition function (log-probs of greedy rows)
 #pragma unroll
-    for (int j = 0; j < TK_NV; ++j) {
-        u[j] = ord_key(v[j]);
+    for (int j = 0; j < TK_NV; ++j)
         if (v[j] > -INFINITY) zs += __expf(v[j] - mx);
-    }
     zs = wave_sum(zs);
     if ((threadIdx.x & 63) == 0) fred[TK_NT / 64 + (threadIdx.x >> 6)] = zs;
-    // bisection window: [key(mx - TK_HR), key(mx) + 1)
-    uint32_t lo = mx > -INFINITY ? ord_key(mx - TK_HR) : 0u;
-    const uint32_t hi = mx > -INFINITY ? ord_key(mx) + 1u : 1u;
-    int c_lo = tk_count<TK_NT, TK_NV>(u, lo, red, 0);
-    if (c_lo >= K) lo = tk_bisect<TK_NT, TK_NV>(u, K, lo, hi, c_lo, TK_CAPS, false, red, 1);
-    // (fewer than K entries within TK_HR of the slice max: all of them are candidates)
+    __syncthreads();
+    if (threadIdx.x < 64) {
+        const int2 bc = tk_scan_bins(hist, K);
+        if (threadIdx.x == 0) s_b = bc.x;  // TK_NB: fewer than K threads hold a value in range
+    }
+    __syncthreads();
+    const int bA = s_b;
+    TK_TS(2)
+    const size_t base = ((size_t)row * S + sl) * TK_CAPS;
+    // direct compaction at the pass-1 bound: every value in bins <= bA (>= K of them). Each lane counts its
+    // own and reserves its range with ONE LDS atomic (a returning atomic per value made every lane wait ~100
+    // cycles per value); the usual case ends here. Too many (clustered maxima) -> pass 2 below.
     if (threadIdx.x == 0) {
         float z = 0.f;
 #pragma unroll
         for (int w = 0; w < TK_NT / 64; ++w) z += fred[TK_NT / 64 + w];
         slice_z[row * S + sl] = make_float2(mx, z);
     }
-    const size_t base = ((size_t)row * S + sl) * TK_CAPS;
+    if (bA < TK_NB) {
+        int myc = 0;
+#pragma unroll
+        for (int j = 0; j < TK_NV; ++j) myc += tk_bin(mx, v[j]) <= bA ? 1 : 0;
+        int off = myc ? atomicAdd(&s_n, myc) : 0;
+        if (myc && off + myc <= TK_CAPS) {
+#pragma unroll
+            for (int j = 0; j < TK_NV; ++j) {
+                if (tk_bin(mx, v[j]) <= bA) {
+                    cand_v[base + off] = v[j];
+                    cand_i[base + off] = i0 + j * TK_NT + threadIdx.x;
+                    ++off;
+                }
+            }
+        }
+        lds_barrier();  // the reservations are done; the candidate stores need no ordering within the block
+        const int tot = s_n;
+        TK_TS(3)
+        if (tot <= TK_CAPS) {
+            if (threadIdx.x == 0) cand_n[row * S + sl] = tot;
+            TK_TS(4)
+            return;
+        }
+        lds_barrier();  // every lane has read s_n
+        if (threadIdx.x == 0) s_n = 0;
+        // pass 2: histogram of the values in bins <= bA, the first bin reaching K
+#pragma unroll
+        for (int j = 0; j < TK_NV; ++j) {  // bins recomputed (not held: 32 more VGPRs would cost occupancy)
+            const int bj = tk_bin(mx, v[j]);
+            if (bj <= bA) atomicAdd(&hist2[bj], 1);
+        }
+        __syncthreads();
+        if (threadIdx.x < 64) {
+            const int2 bc = tk_scan_bins(hist2, K);
+            if (threadIdx.x == 0) {
+                s_b = bc.x;
+                s_fb = bc.x == TK_NB || bc.y > TK_CAPS;
+            }
+        }
+        __syncthreads();
+        if (!s_fb) {
+            const int b = s_b;
+            myc = 0;
+#pragma unroll
+            for (int j = 0; j < TK_NV; ++j) myc += tk_bin(mx, v[j]) <= b ? 1 : 0;
+            off = myc ? atomicAdd(&s_n, myc) : 0;  // <= TK_CAPS in total by the scan
+#pragma unroll
+            for (int j = 0; j < TK_NV; ++j) {
+                if (tk_bin(mx, v[j]) <= b) {
+                    cand_v[base + off] = v[j];
+                    cand_i[base + off] = i0 + j * TK_NT + threadIdx.x;
+                    ++off;
+                }
+            }
+            __syncthreads();
+            if (threadIdx.x == 0) cand_n[row * S + sl] = s_n;
+            return;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) s_n = 0;
+        __syncthreads();
+    }
+    // fallback: bisection on the order-preserving key (computed from the values on the fly)
+    uint32_t lo = mx > -INFINITY ? ord_key(mx - TK_HR) : 0u;
+    const uint32_t hi = mx > -INFINITY ? ord_key(mx) + 1u : 1u;
+    int c_lo = tk_count<TK_NT, TK_NV, float>(v, lo, red, 0);
+    if (c_lo >= K) lo = tk_bisect<TK_NT, TK_NV, float>(v, K, lo, hi, c_lo, TK_CAPS, false, red, 1);
 #pragma unroll
     for (int j = 0; j < TK_NV; ++j) {
-        if (u[j] >= lo && u[j] != 0u) {
+        const uint32_t uj = ord_key(v[j]);
+        if (uj >= lo && uj != 0u) {
             const int k = atomicAdd(&s_n, 1);
             if (k < TK_CAPS) {
                 cand_v[base + k] = v[j];
@@ -577,27 +722,29 @@ __global__ __launch_bounds__(TK_MNT) void tk_merge_kernel(float* __restrict__ lo
                                                          const float* __restrict__ cand_v, const int* __restrict__ cand_i,
                                                          const int* __restrict__ cand_n, const float2* __restrict__ slice_z,
                                                          int* __restrict__ out_tok, float* __restrict__ out_logp) {
-    constexpr int KC = 256;  // kept-set capacity (top-k <= 64 plus exact ties)
-    __shared__ float cv[KC];
-    __shared__ int ci[KC];
-    __shared__ int s_off[65], s_keep, s_n, s_ovf;
+    constexpr int KC = 256;  // kept-set capacity (top-k <= 64 plus the rest of the K-th value's bin)
+    __shared__ __attribute__((aligned(16))) float cv[KC];
+    __shared__ __attribute__((aligned(16))) int ci[KC];
+    __shared__ float sv[KC];
+    __shared__ int si[KC];
+    __shared__ __attribute__((aligned(16))) int hist[TK_NB];
+    __shared__ int s_cnt[64], s_keep, s_n, s_ovf, s_b, s_fb;
+    __shared__ float s_mx, s_Z;
     __shared__ float red[2 * TK_MNT / 64], rv[TK_MNT / 64];
     __shared__ int ired[2 * TK_MNT / 64], ri[TK_MNT / 64];
     const int row = blockIdx.x;
     const SampleParams P = params[row];
     const bool greedy = P.temperature <= 0.f;
     const int K = greedy ? 1 : min(P.top_k, TK_CAP);
-    if (threadIdx.x == 0) {
-        int o = 0, ovf = 0;
-        for (int s = 0; s < S; ++s) {
-            const int c = cand_n[row * S + s];
-            ovf |= c >> 30;
-            s_off[s] = o;
-            o += c & 0xFFFF;
-        }
-        s_off[S] = o;
-        s_ovf = ovf;
-        s_n = 0;
+    if (threadIdx.x < TK_NB) hist[threadIdx.x] = 0;
+    if (threadIdx.x < 64) {  // one wave: per-slice counts, overflow flags and the row max (largest slice max)
+        const int s = threadIdx.x;
+        const int c = s < S ? cand_n[row * S + s] : 0;
+        const float sm = s < S ? slice_z[row * S + s].x : -INFINITY;
+        s_cnt[s] = c & 0xFFFF;
+        const unsigned long long ov = __ballot((c >> 30) != 0);
+        const float m = wave_max(sm);
+        if (s == 0) { s_ovf = ov != 0; s_n = 0; s_mx = m; }
     }
     __syncthreads();
     if (s_ovf) {  // exact ties beyond a slice's capacity (flat / degenerate rows): the full-row chain
@@ -606,88 +753,116 @@ __global__ __launch_bounds__(TK_MNT) void tk_merge_kernel(float* __restrict__ lo
         sample_row_bisect(x, V, P, am, row, out_tok, out_logp, red, rv, ri);
         return;
     }
-    const int n = s_off[S];
-    // candidate t (concatenated over slices) -> registers
+    const float mx = s_mx;
+    // candidate position t = (slice t / TK_CAPS, entry t % TK_CAPS): valid below that slice's count
     float v[TK_MV];
-    int id[TK_MV];
-    uint32_t u[TK_MV];
-    float mx = -INFINITY;
+    int id[TK_MV], bin[TK_MV];
 #pragma unroll
     for (int j = 0; j < TK_MV; ++j) {
-        const int t = j * TK_MNT + threadIdx.x;
-        v[j] = -INFINITY;
-        id[j] = 0x7fffffff;
-        if (t < n) {
-            int s = 0;
-            while (s + 1 < S && s_off[s + 1] <= t) ++s;  // S <= 64
-            const size_t src = ((size_t)row * S + s) * TK_CAPS + (t - s_off[s]);
-            v[j] = cand_v[src];
-            id[j] = cand_i[src];
-        }
-        u[j] = ord_key(v[j]);
-        mx = fmaxf(mx, v[j]);
+        // unconditional (clamped) loads, validity applied after: see tk_slice_kernel
+        const int t = j * TK_MNT + threadIdx.x, s = min(t / TK_CAPS, S - 1), e = t % TK_CAPS;
+        const size_t src = ((size_t)row * S + s) * TK_CAPS + e;
+        v[j] = cand_v[src];
+        id[j] = cand_i[src];
     }
-    mx = wave_max(mx);
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
-    __syncthreads();
-    mx = -INFINITY;
-#pragma unroll
-    for (int w = 0; w < TK_MNT / 64; ++w) mx = fmaxf(mx, red[w]);
-    // exact global top-K (ties at the K-th value kept)
-    int c_lo = tk_count<TK_MNT, TK_MV>(u, 1u, ired, 0);
-    uint32_t T = 1u;
-    if (c_lo > K) T = tk_bisect<TK_MNT, TK_MV>(u, K, 1u, ord_key(mx) + 1u, c_lo, 0, true, ired, 1);
 #pragma unroll
     for (int j = 0; j < TK_MV; ++j) {
-        if (u[j] >= T && u[j] != 0u) {
-            const int k = atomicAdd(&s_n, 1);
-            if (k < KC) { cv[k] = v[j]; ci[k] = id[j]; }
+        const int t = j * TK_MNT + threadIdx.x, s = t / TK_CAPS, e = t % TK_CAPS;
+        if (!(s < S && e < s_cnt[min(s, 63)])) { v[j] = -INFINITY; id[j] = 0x7fffffff; }
+        bin[j] = tk_bin(mx, v[j]);
+        if (bin[j] < TK_NB) atomicAdd(&hist[bin[j]], 1);
+    }
+    __syncthreads();
+    if (threadIdx.x < 64) {
+        const int2 bc = tk_scan_bins(hist, K);
+        if (threadIdx.x == 0) {
+            s_b = bc.x;
+            s_fb = bc.x == TK_NB || bc.y > KC;
         }
     }
     __syncthreads();
-    if (s_n > KC) {  // more exact ties at the K-th value than the kept-set buffer holds
-        float* x = logits + (size_t)row * ld;
-        const uint32_t* am = allow_mask ? allow_mask + (size_t)row * mask_ld : nullptr;
-        sample_row_bisect(x, V, P, am, row, out_tok, out_logp, red, rv, ri);
-        return;
-    }
-    const int nk = s_n;
-    int np = 1;
-    while (np < nk) np <<= 1;
-    for (int k = nk + threadIdx.x; k < np; k += TK_MNT) { cv[k] = -INFINITY; ci[k] = 0x7fffffff; }
-    __syncthreads();
-    for (int size = 2; size <= np; size <<= 1) {
-        for (int stride = size >> 1; stride > 0; stride >>= 1) {
-            for (int t = threadIdx.x; t < np / 2; t += TK_MNT) {
-                const int lo = 2 * t - (t & (stride - 1)), hi = lo + stride;
-                const bool desc = (lo & size) == 0;
-                const float a = cv[lo], bb = cv[hi];
-                const int ia = ci[lo], ib = ci[hi];
-                const bool a_first = a > bb || (a == bb && ia < ib);
-                if (a_first != desc) { cv[lo] = bb; cv[hi] = a; ci[lo] = ib; ci[hi] = ia; }
+    int nk;
+    if (!s_fb) {  // every candidate in bins <= b: a superset of the top-K (whole bins), at most KC
+        const int b = s_b;
+        int myc = 0;
+#pragma unroll
+        for (int j = 0; j < TK_MV; ++j) myc += bin[j] <= b ? 1 : 0;
+        int k = myc ? atomicAdd(&s_n, myc) : 0;  // one returning LDS atomic per lane (see tk_slice_kernel)
+#pragma unroll
+        for (int j = 0; j < TK_MV; ++j) {
+            if (bin[j] <= b) {
+                cv[k] = v[j];
+                ci[k] = id[j];
+                ++k;
             }
-            __syncthreads();
         }
+        __syncthreads();
+        nk = s_n;
+    } else {  // exact global top-K by key bisection (ties at the K-th value kept)
+        uint32_t u[TK_MV];
+#pragma unroll
+        for (int j = 0; j < TK_MV; ++j) u[j] = ord_key(v[j]);
+        int c_lo = tk_count<TK_MNT, TK_MV, uint32_t>(u, 1u, ired, 0);
+        uint32_t T = 1u;
+        if (c_lo > K) T = tk_bisect<TK_MNT, TK_MV, uint32_t>(u, K, 1u, ord_key(mx) + 1u, c_lo, 0, true, ired, 1);
+#pragma unroll
+        for (int j = 0; j < TK_MV; ++j) {
+            if (u[j] >= T && u[j] != 0u) {
+                const int k = atomicAdd(&s_n, 1);
+                if (k < KC) { cv[k] = v[j]; ci[k] = id[j]; }
+            }
+        }
+        __syncthreads();
+        if (s_n > KC) {  // more exact ties at the K-th value than the kept-set buffer holds
+            float* x = logits + (size_t)row * ld;
+            const uint32_t* am = allow_mask ? allow_mask + (size_t)row * mask_ld : nullptr;
+            sample_row_bisect(x, V, P, am, row, out_tok, out_logp, red, rv, ri);
+            return;
+        }
+        nk = s_n;
     }
-    if (threadIdx.x == 0) {  // the bisection chain's semantics (see sample_kernel)
-        int keep = nk;
+    // rank sort of the <= KC kept values (descending value, ascending id): one comparison pass per element
+    if (threadIdx.x < KC) {  // pad to a multiple of 4 for the vector reads (pads rank below every real value)
+        if (threadIdx.x >= nk) { cv[threadIdx.x] = -INFINITY; ci[threadIdx.x] = 0x7fffffff; }
+    }
+    __syncthreads();
+    if (threadIdx.x < nk) {
+        const float a = cv[threadIdx.x];
+        const int ia = ci[threadIdx.x];
+        int r = 0;
+        const int n4 = (nk + 3) & ~3;
+        for (int k = 0; k < n4; k += 4) {  // broadcast LDS reads, 4 candidates per step
+            const float4 bv = *(const float4*)(cv + k);
+            const int4 bi4 = *(const int4*)(ci + k);
+            r += (bv.x > a || (bv.x == a && bi4.x < ia)) ? 1 : 0;
+            r += (bv.y > a || (bv.y == a && bi4.y < ia)) ? 1 : 0;
+            r += (bv.z > a || (bv.z == a && bi4.z < ia)) ? 1 : 0;
+            r += (bv.w > a || (bv.w == a && bi4.w < ia)) ? 1 : 0;
+        }
+        sv[r] = a;
+        si[r] = ia;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {  // top-K (ties at the K-th value kept), then the bisection chain's semantics
+        int keep = min(K, nk);
+        while (keep < nk && sv[keep] == sv[keep - 1]) ++keep;
         float zk = 0.f;
         const bool tp = P.top_p < 1.f && P.top_p > 0.f;
         if (tp)
-            for (int k = 0; k < keep; ++k) zk += __expf(cv[k] - mx);
+            for (int k = 0; k < keep; ++k) zk += __expf(sv[k] - mx);
         if (P.min_p > 0.f && P.min_p <= 1.f) {
             const float mv = mx + __logf(P.min_p);
-            while (keep > 1 && cv[keep - 1] < mv) --keep;
+            while (keep > 1 && sv[keep - 1] < mv) --keep;
         }
         if (tp) {
             float cum = 0.f;
             int k = 0;
             while (k < keep) {
-                cum += __expf(cv[k] - mx);
+                cum += __expf(sv[k] - mx);
                 ++k;
                 if (cum >= P.top_p * zk) break;
             }
-            while (k < keep && cv[k] == cv[k - 1]) ++k;
+            while (k < keep && sv[k] == sv[k - 1]) ++k;
             keep = max(1, k);
         }
         s_keep = keep;
@@ -697,9 +872,9 @@ __global__ __launch_bounds__(TK_MNT) void tk_merge_kernel(float* __restrict__ lo
     float best = -INFINITY, zk = 0.f;
     int bi = 0x7fffffff;
     for (int k = threadIdx.x; k < keep; k += TK_MNT) {
-        const float sc = greedy ? cv[k] : cv[k] + gumbel(P.seed, (uint32_t)ci[k]);
-        zk += __expf(cv[k] - mx);
-        if (sc > best || (sc == best && ci[k] < bi)) { best = sc; bi = ci[k]; }
+        const float sc = greedy ? sv[k] : sv[k] + gumbel(P.seed, (uint32_t)si[k]);
+        zk += __expf(sv[k] - mx);
+        if (sc > best || (sc == best && si[k] < bi)) { best = sc; bi = si[k]; }
     }
     zk = wave_sum(zk);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = zk;
@@ -711,6 +886,12 @@ __global__ __launch_bounds__(TK_MNT) void tk_merge_kernel(float* __restrict__ lo
     }
     if ((threadIdx.x & 63) == 0) { rv[threadIdx.x >> 6] = best; ri[threadIdx.x >> 6] = bi; }
     __syncthreads();
+    if (out_logp && greedy && threadIdx.x < 64) {  // greedy log-softmax over the whole (allowed) row, from the
+        const int s2 = threadIdx.x;                // slices' (max, sum exp); mx is the row max
+        const float2 m = s2 < S ? slice_z[row * S + s2] : make_float2(-INFINITY, 0.f);
+        const float Z = wave_sum(m.x > -INFINITY ? m.y * __expf(m.x - mx) : 0.f);
+        if (s2 == 0) s_Z = Z;  // read below by this same lane
+    }
     if (threadIdx.x == 0) {
         float b = rv[0], z = red[0];
         int tok = ri[0];
@@ -721,17 +902,8 @@ __global__ __launch_bounds__(TK_MNT) void tk_merge_kernel(float* __restrict__ lo
         if (tok == 0x7fffffff) tok = 0;
         out_tok[row] = tok;
         if (out_logp) {
-            if (greedy) {  // log-softmax over the whole (allowed) row, from the slices' (max, sum exp)
-                float M = -INFINITY, Z = 0.f;
-                for (int s2 = 0; s2 < S; ++s2) M = fmaxf(M, slice_z[row * S + s2].x);
-                for (int s2 = 0; s2 < S; ++s2) {
-                    const float2 m = slice_z[row * S + s2];
-                    if (m.x > -INFINITY) Z += m.y * __expf(m.x - M);
-                }
-                out_logp[row] = logits[(size_t)row * ld + tok] - M - __logf(fmaxf(Z, 1e-30f));
-            } else {
-                out_logp[row] = logits[(size_t)row * ld + tok] / P.temperature - mx - __logf(fmaxf(z, 1e-30f));
-            }
+            out_logp[row] = greedy ? logits[(size_t)row * ld + tok] - mx - __logf(fmaxf(s_Z, 1e-30f))
+                                   : logits[(size_t)row * ld + tok] / P.temperature - mx - __logf(fmaxf(z, 1e-30f));
         }
     }
 }
@@ -754,6 +926,11 @@ extern "C" int mxk_sample_topk_split(float* logits, int ld, int B, int V, const 
     MXK_CHECK_LAUNCH();
 }
 extern "C" int mxk_sample_topk_slice() { return TK_SLICE; }
+// debug: enable / read the per-phase wall-clock stamps of tk_slice_kernel's workgroup (0, 0) (100 MHz ticks)
+extern "C" int mxk_sample_trace(int on, unsigned long long* out16) {
+    if (out16) return (int)hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_tk_ts), sizeof(unsigned long long) * 16);
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_tk_trace), &on, sizeof(int));
+}
 extern "C" int mxk_sample_topk_caps() { return TK_CAPS; }
 extern "C" int mxk_sample_topk_cap() { return TK_CAP; }
 

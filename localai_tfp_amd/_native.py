@@ -44,6 +44,7 @@ KERNEL_SIGS = {
     "mxk_qmm2_dbg": [I, I, I, I, P, I, P, I, I, I, P, I, P],
     "mxk_qmm2_set_rot": [I],
     "mxk_qmm3": [I, I, I, P, I, P, I, I, I, I, P, I, P],
+    "mxk_sample_trace": [I, P],
     "mxk_qmm3_dbg": [I, I, P, I, P, I, I, I, P, I, P],
     "mxk_qmm_ws": [I, I, I, P, I, P, I, I, I, I, P, I, P],
     "mxk_qmm_ws_dbg": [I],
@@ -75,6 +76,7 @@ KERNEL_SIGS = {
     "mxk_cast_f32_bf16": [P, I, P, I, I, I, P],
     "mxk_gather_rows": [P, I, P, I, I, F, P, P],
     "mxk_add_bias_f32": [P, I, P, I, I, P],
+    "mxk_add_act_into_f32": [P, I, P, I, I, I, P],
     "mxk_select_rows_f32": [P, I, P, I, I, P, I, P],
     "mxk_lstm_scan": [P, P, P, P, P, F, P, I, I, I, P],
     "mxk_lstm_bidir": [P, P, P, P, P, P, I, I, P],

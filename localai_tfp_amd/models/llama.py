@@ -487,7 +487,12 @@ class LlamaModel:
                 ar.add_into(y16[r0:r1], h[r0:r1])
             else:
                 self._allreduce(y16[r0:r1])
-                h[r0:r1].add_(y16[r0:r1])
+                if h.is_cuda:
+                    N.ensure_act(y16.dtype)
+                    N.kcall("mxk_add_act_into_f32", y16[r0:r1].data_ptr(), y16.stride(0), h[r0:r1].data_ptr(),
+                            h.stride(0), r1 - r0, h.shape[1], N.stream_ptr())
+                else:
+                    h[r0:r1].add_(y16[r0:r1])
 
         if not y16.is_cuda:
             for r0, r1 in zip(bounds, bounds[1:]):
@@ -826,7 +831,12 @@ class LlamaModel:
                 return
             self._allreduce(y16)
             if post_norm is None:
-                h.add_(y16)
+                if h.is_cuda and h.is_contiguous() and y16.is_contiguous():
+                    N.ensure_act(y16.dtype)
+                    N.kcall("mxk_add_act_into_f32", y16.data_ptr(), y16.stride(0), h.data_ptr(), h.stride(0), T,
+                            h.shape[1], N.stream_ptr())
+                else:
+                    h.add_(y16)
             else:
                 y = ws.y[:T]
                 y.copy_(y16)

@@ -24,8 +24,14 @@ def llama_tensor_plan(cfg: LlamaConfig, ftype: str = "Q4_K_M"):
     """[(name, ggml_shape, qtype)] for a Llama-architecture GGUF."""
     H, F, V = cfg.hidden, cfg.ffn, cfg.vocab
     qd, kvd = cfg.q_dim, cfg.kv_dim
-    base = {"Q4_K_M": QType.Q4_K, "Q6_K": QType.Q6_K, "Q8_0": QType.Q8_0, "F16": QType.F16}[ftype]
+    base = {"Q4_K_M": QType.Q4_K, "Q3_K_M": QType.Q3_K, "Q6_K": QType.Q6_K, "Q8_0": QType.Q8_0,
+            "F16": QType.F16}[ftype]
     hi = QType.Q6_K if ftype == "Q4_K_M" else base
+    # Q3_K_M (llama.cpp's mix, approximately): attn_v / ffn_down in Q5_K on the "more bits" layers and Q4_K
+    # elsewhere, attn_output Q4_K, output Q6_K, the rest Q3_K
+    mid = QType.Q4_K if ftype == "Q3_K_M" else None
+    if ftype == "Q3_K_M":
+        hi = QType.Q5_K
     out = [("token_embd.weight", (H, V), base)]
     L = cfg.n_layers
     for i in range(L):
@@ -35,8 +41,8 @@ def llama_tensor_plan(cfg: LlamaConfig, ftype: str = "Q4_K_M"):
             (p + "attn_norm.weight", (H,), QType.F32),
             (p + "attn_q.weight", (H, qd), base),
             (p + "attn_k.weight", (H, kvd), base),
-            (p + "attn_v.weight", (H, kvd), hi if mb else base),
-            (p + "attn_output.weight", (qd, H), base),
+            (p + "attn_v.weight", (H, kvd), hi if mb else (mid or base)),
+            (p + "attn_output.weight", (qd, H), mid or base),
             (p + "ffn_norm.weight", (H,), QType.F32),
         ]
         if cfg.n_expert:
@@ -56,7 +62,7 @@ def llama_tensor_plan(cfg: LlamaConfig, ftype: str = "Q4_K_M"):
             out += [
                 (p + "ffn_gate.weight", (H, F), base),
                 (p + "ffn_up.weight", (H, F), base),
-                (p + "ffn_down.weight", (F, H), hi if mb else base),
+                (p + "ffn_down.weight", (F, H), hi if mb else (mid or base)),
             ]
         if cfg.post_norms:
             out += [(p + "post_attention_norm.weight", (H,), QType.F32),
@@ -69,7 +75,7 @@ def llama_tensor_plan(cfg: LlamaConfig, ftype: str = "Q4_K_M"):
                     (p + "attn_v.bias", (kvd,), QType.F32)]
     out.append(("output_norm.weight", (H,), QType.F32))
     if not cfg.tie_embeddings:
-        out.append(("output.weight", (H, V), QType.Q6_K if ftype == "Q4_K_M" else base))
+        out.append(("output.weight", (H, V), QType.Q6_K if ftype in ("Q4_K_M", "Q3_K_M") else base))
     return out
 
 

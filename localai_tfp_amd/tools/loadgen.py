@@ -75,6 +75,10 @@ async def run(a):
             content = " ".join(rng.choice(WORDS) for _ in range(n_words))[: a.prompt_chars]
         body = {"model": a.model, "stream": True, "max_tokens": a.gen_len, "temperature": a.temperature,
                 "ignore_eos": True, "messages": [{"role": "user", "content": content}]}
+        if a.frequency_penalty:
+            body["frequency_penalty"] = a.frequency_penalty
+        if a.json:
+            body["response_format"] = {"type": "json_object"}
         if a.top_k is not None:
             body["top_k"] = a.top_k
         if a.top_p is not None:
@@ -120,6 +124,8 @@ def main(argv=None):
     ap.add_argument("--temperature", type=float, default=0.0)
     ap.add_argument("--top-k", type=int, default=None)
     ap.add_argument("--top-p", type=float, default=None)
+    ap.add_argument("--frequency-penalty", type=float, default=0.0)
+    ap.add_argument("--json", action="store_true", help="response_format json_object (grammar-constrained)")
     ap.add_argument("--duration", type=float, default=0.0)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--stagger", action="store_true", help="spread the first requests' lengths evenly")

@@ -14,6 +14,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--B", type=int, default=128)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--trace", action="store_true", help="print tk_slice_kernel phase stamps (workgroup 0)")
     a = ap.parse_args()
     from localai_tfp_amd.ops.sampling import SamplerBatch, SamplingParams
     dev = torch.device("cuda")
@@ -40,6 +41,18 @@ def main():
         res[name] = (e0.elapsed_time(e1) / a.iters * 1e3, toks)
     same = all(torch.equal(x, y) for x, y in zip(res["row"][1], res["split"][1]))
     print(f"B={B} row {res['row'][0]:.1f} us/call  split {res['split'][0]:.1f} us/call  same_tokens={same}")
+    if a.trace:
+        import ctypes
+        import numpy as np
+        from localai_tfp_amd import _native as Nn
+        Nn.kcall("mxk_sample_trace", 1, 0)
+        split.sample(logits.clone(), ps, hist, [0] * B)
+        torch.cuda.synchronize()
+        ts = np.zeros(16, np.uint64)
+        Nn.kcall("mxk_sample_trace", 0, ts.ctypes.data)
+        Nn.kcall("mxk_sample_trace", 0, 0)
+        d = np.diff(ts[:5].astype(np.int64)) * 10  # 100 MHz ticks -> ns
+        print("tk_slice phases (ns): load+max", d[0], "pass1+scan", d[1], "pass2+scan", d[2], "compact", d[3])
 
 
 if __name__ == "__main__":
