@@ -187,26 +187,52 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restri
     }
 }
 
+constexpr int DEC_RED_MAXP = 512;  // partitions whose merge weights fit the reduce kernel's LDS table
+
 template <bool F16>
 __global__ __launch_bounds__(128) void attn_decode_reduce_kernel(const float2* __restrict__ part_ml,
                                                                   const float* __restrict__ part_o, int n_parts,
                                                                   int Hq, int D, const int* __restrict__ seq_lens,
                                                                   int part_size, bf16_t* __restrict__ out,
                                                                   int out_stride) {
+    // wave 0 reads the partitions' (m, l) with all its lanes at once and publishes the merge weights through
+    // LDS (a serial loop of dependent loads made this launch as long as the attention itself at batch 1);
+    // every thread then sums its dims over the partitions with independent loads
+    __shared__ float wts[DEC_RED_MAXP];
+    __shared__ float s_mx, s_ls;
     const int bh = blockIdx.x;
     const int b = bh / Hq, h = bh % Hq;
     const int np = min(n_parts, (seq_lens[b] + part_size - 1) / part_size);
-    float mx = -INFINITY;
-    for (int p = 0; p < np; ++p) mx = fmaxf(mx, part_ml[(size_t)bh * n_parts + p].x);
-    for (int d = threadIdx.x; d < D; d += blockDim.x) {
-        float ls = 0.f, os = 0.f;
-        for (int p = 0; p < np; ++p) {
-            const float2 ml = part_ml[(size_t)bh * n_parts + p];
-            const float a = mx == -INFINITY ? 0.f : exp2f(ml.x - mx);
-            ls += ml.y * a;
-            os += part_o[((size_t)bh * n_parts + p) * D + d] * a;
+    const size_t pb = (size_t)bh * n_parts;
+    if (threadIdx.x < 64) {
+        float m = -INFINITY;
+        for (int p = threadIdx.x; p < np; p += 64) m = fmaxf(m, part_ml[pb + p].x);
+        m = wave_max(m);
+        float l = 0.f;
+        for (int p = threadIdx.x; p < np; p += 64) {
+            const float2 ml = part_ml[pb + p];
+            const float a = m == -INFINITY ? 0.f : exp2f(ml.x - m);
+            l += ml.y * a;
+            if (p < DEC_RED_MAXP) wts[p] = a;
         }
-        out[(size_t)b * out_stride + (size_t)h * D + d] = f32_to_act<F16>(ls > 0.f ? os / ls : 0.f);
+        l = wave_sum(l);
+        if (threadIdx.x == 0) { s_mx = m; s_ls = l; }
+    }
+    __syncthreads();
+    const float mx = s_mx, L = s_ls;
+    for (int d = threadIdx.x; d < D; d += blockDim.x) {
+        float os = 0.f;
+        int p = 0;
+        for (; p + 4 <= min(np, DEC_RED_MAXP); p += 4) {
+            const float o0 = part_o[(pb + p) * D + d], o1 = part_o[(pb + p + 1) * D + d];
+            const float o2 = part_o[(pb + p + 2) * D + d], o3 = part_o[(pb + p + 3) * D + d];
+            os += o0 * wts[p] + o1 * wts[p + 1] + o2 * wts[p + 2] + o3 * wts[p + 3];
+        }
+        for (; p < np; ++p) {
+            const float a = p < DEC_RED_MAXP ? wts[p] : (mx == -INFINITY ? 0.f : exp2f(part_ml[pb + p].x - mx));
+            os += part_o[(pb + p) * D + d] * a;
+        }
+        out[(size_t)b * out_stride + (size_t)h * D + d] = f32_to_act<F16>(L > 0.f ? os / L : 0.f);
     }
 }
 
@@ -314,16 +340,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KV8 ? 2 : 4
     const int* bt = block_tables + (size_t)b * bt_stride;
     const int blk0 = p0 / bs;
     const int nblk = p1 > p0 ? (p1 - 1) / bs - blk0 + 1 : 0;
-    for (int i = threadIdx.x; i < nblk; i += 256) sbt[i] = bt[blk0 + i];
-    __syncthreads();
-
-    // Q as the A operand: row = head (lane col), k = dims 32 ks + 8 g
+    // Q as the A operand: row = head (lane col), k = dims 32 ks + 8 g — requested before the block-table
+    // barrier so its latency overlaps the table read
     bf16x8 qf[D / 32];
 #pragma unroll
     for (int ks = 0; ks < D / 32; ++ks) {
         if (col < G) qf[ks] = *(const bf16x8*)(q + (size_t)b * q_stride + (size_t)(kvh * G + col) * D + 32 * ks + 8 * g);
         else qf[ks] = (bf16x8){};
     }
+    for (int i = threadIdx.x; i < nblk; i += 256) sbt[i] = bt[blk0 + i];
+    __syncthreads();
     f32x4 oacc[D / 16];
 #pragma unroll
     for (int i = 0; i < D / 16; ++i) oacc[i] = (f32x4){0.f, 0.f, 0.f, 0.f};

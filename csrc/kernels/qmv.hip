@@ -12,6 +12,7 @@
 
 namespace {
 constexpr int QMV_WAVES = 8;
+int g_qmv1_on = 1;  // mxk_qmv1_enable: the batch-1 fast-prologue kernel (A/B switch)
 
 // per-lane weight state for one unit (Q4_K/Q6_K: one 256-element super-block; Q8_0: one 64-k tile)
 template <int QT>
@@ -439,6 +440,119 @@ __global__ __launch_bounds__(64 * QMV_WAVES) void qmv_kernel(const int8_t* __res
     }
 }
 
+// Batch-1 GEMV with the activation prologue fused (SRC_ACT / SRC_NORM), for K = 4096 and at most two units per
+// wave (every row-parallel split chosen so): straight-line code with no unit loop, and the activation row is
+// read BEFORE the weights are requested — loads complete in issue order for s_waitcnt, so qmv_kernel's
+// prologue (issued after the weights) waited for the wave's whole weight stream before it could start the
+// norm / quantisation. The WHOLE row is read by every workgroup (8 elements per thread): the norm's sum of
+// squares comes from the same registers, and the workgroup quantises the part inside its K slice into LDS.
+template <int QT, int EPI, bool F16, int SRC>
+__global__ __launch_bounds__(64 * QMV_WAVES) void qmv1_kernel(const uint8_t* __restrict__ W, int N, int K,
+                                                              void* __restrict__ Cv, const void* __restrict__ xsrc,
+                                                              const float* __restrict__ nw, float eps) {
+    using U = TUnit<QT>;
+    constexpr int NT = 64 * QMV_WAVES;
+    static_assert(SRC == SRC_ACT || SRC == SRC_NORM, "fused prologue only");
+    __shared__ float red[QMV_WAVES][32];
+    __shared__ float nred[QMV_WAVES];
+    extern __shared__ __attribute__((aligned(16))) char qmv1_smem[];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int r = lane & 31, h = lane >> 5;
+    const int g = blockIdx.x;
+    const int nunit = K / U::ELEMS;  // K == 4096 (checked by the launcher)
+    const int per = (nunit + gridDim.y - 1) / gridDim.y;
+    const int u0 = blockIdx.y * per, u1 = min(nunit, u0 + per);
+    const int k0 = u0 * U::ELEMS, klen = max(0, u1 - u0) * U::ELEMS;
+    const uint8_t* wg = W + (size_t)g * nunit * U::BYTES;
+    // 1. the activation row (8 elements per thread) and, for the norm, its weights
+    const int e = 8 * threadIdx.x;
+    float a8[8], w8[8];
+    if constexpr (SRC == SRC_NORM) {
+        const float* xr = (const float*)xsrc + e;
+        const float4 v0 = *(const float4*)xr, v1 = *(const float4*)(xr + 4);
+        const float4 n0 = *(const float4*)(nw + e), n1 = *(const float4*)(nw + e + 4);
+        a8[0] = v0.x; a8[1] = v0.y; a8[2] = v0.z; a8[3] = v0.w; a8[4] = v1.x; a8[5] = v1.y; a8[6] = v1.z; a8[7] = v1.w;
+        w8[0] = n0.x; w8[1] = n0.y; w8[2] = n0.z; w8[3] = n0.w; w8[4] = n1.x; w8[5] = n1.y; w8[6] = n1.z; w8[7] = n1.w;
+    } else {
+        const uint4 raw = *(const uint4*)((const bf16_t*)xsrc + e);
+        unpack_act2<F16>(raw.x, a8[0], a8[1]);
+        unpack_act2<F16>(raw.y, a8[2], a8[3]);
+        unpack_act2<F16>(raw.z, a8[4], a8[5]);
+        unpack_act2<F16>(raw.w, a8[6], a8[7]);
+    }
+    asm volatile("" ::: "memory");  // the row reads stay ahead of the weight requests
+    // 2. this wave's (at most) two weight units
+    U a, b;
+    const int u = u0 + wave;
+    const bool ha = u < u1, hb = u + QMV_WAVES < u1;
+    if (ha) a.load(wg + (size_t)u * U::BYTES, r, h);
+    if (hb) b.load(wg + (size_t)(u + QMV_WAVES) * U::BYTES, r, h);
+    // 3. norm + quantisation of the slice into LDS while the weights stream
+    int8_t* sq = (int8_t*)qmv1_smem;
+    float2* sd = (float2*)(qmv1_smem + klen);
+    float rs = 1.f;
+    if constexpr (SRC == SRC_NORM) {
+        float ss = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) ss += a8[j] * a8[j];
+        ss = wave_sum(ss);
+        if (lane == 0) nred[wave] = ss;
+    }
+    if (e >= k0 && e < k0 + klen) {  // whole 4-lane groups (k0 % 256 == 0)
+        float v8[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v8[j] = SRC == SRC_NORM ? a8[j] * w8[j] : a8[j];
+        float am = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) am = fmaxf(am, fabsf(v8[j]));
+        am = group_max<4>(am);
+        const float d = am / 127.f, id = d > 0.f ? 1.f / d : 0.f;
+        int q[8], sum = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { q[j] = __float2int_rn(v8[j] * id); sum += q[j]; }
+        const float sf = group_sum<4>((float)sum);
+        uint2 pk;
+        pk.x = (q[0] & 0xFF) | ((q[1] & 0xFF) << 8) | ((q[2] & 0xFF) << 16) | ((uint32_t)(q[3] & 0xFF) << 24);
+        pk.y = (q[4] & 0xFF) | ((q[5] & 0xFF) << 8) | ((q[6] & 0xFF) << 16) | ((uint32_t)(q[7] & 0xFF) << 24);
+        *(uint2*)(sq + (e - k0)) = pk;
+        if ((threadIdx.x & 3) == 0) sd[(e - k0) / 32] = make_float2(d, d * sf);
+    }
+    __syncthreads();
+    if constexpr (SRC == SRC_NORM) {
+        float t = 0.f;
+#pragma unroll
+        for (int w = 0; w < QMV_WAVES; ++w) t += nred[w];
+        rs = rsqrtf(t / (float)K + eps);
+    }
+    // 4. dot products
+    float acc = 0.f;
+    const int ul = u - u0;
+    if (ha) acc += a.dot(sq + (size_t)ul * U::ELEMS, sd + ul * (U::ELEMS / 32), h);
+    if (hb) acc += b.dot(sq + (size_t)(ul + QMV_WAVES) * U::ELEMS, sd + (ul + QMV_WAVES) * (U::ELEMS / 32), h);
+    acc *= rs;
+    {
+        const float v = acc + __shfl_xor(acc, 32);
+        if (h == 0) red[wave][r] = v;
+    }
+    __syncthreads();
+    if (wave != 0) return;
+    float v = 0.f;
+    if (h == 0) {
+#pragma unroll
+        for (int w = 0; w < QMV_WAVES; ++w) v += red[w][r];
+    }
+    const int n = g * 32 + r;
+    if constexpr (EPI == E16_SWIGLU || EPI == E16_GEGLU) {
+        const float up = __shfl_down(v, 16);
+        if (h == 0 && r < 16) ((uint16_t*)Cv)[g * 16 + r] = f32_to_act<F16>(glu_gate_f<EPI>(v) * up);
+    } else if (h == 0) {
+        if constexpr (EPI == E16_F32) ((float*)Cv)[n] = v;
+        else if constexpr (EPI == E16_ACT) ((uint16_t*)Cv)[n] = f32_to_act<F16>(v);
+        else if (gridDim.y > 1) atomicAdd(((float*)Cv) + n, v);
+        else ((float*)Cv)[n] += v;
+    }
+}
+
 // ---- dequantise whole rows (output features) of a t32 weight: embedding gather / debugging ----
 template <int QT, bool F16>
 __global__ __launch_bounds__(256) void dequant_t32_kernel(const uint8_t* __restrict__ W, const int* __restrict__ rows,
@@ -555,6 +669,16 @@ static int launch_qmv(const int8_t* xq, const float2* xds, const uint8_t* W, int
         const size_t sl = (size_t)per * TUnit<QT>::ELEMS;
         const size_t lds = MM * (sl + sl / 32 * sizeof(float2));
         if (lds > 64 * 1024) return (int)hipErrorInvalidValue;
+        if (MM == 1 && M == 1 && K == 4096 && ks == 1 && per <= 2 * QMV_WAVES && g_qmv1_on) {
+            if (src == SRC_ACT) {
+                MX_ACT_DISPATCH(qmv1_kernel<QT, EPI, F16, SRC_ACT><<<dim3(N / 32, ks), 64 * QMV_WAVES, lds, st>>>(
+                    W, N, K, C, xsrc, nullptr, 0.f));
+            } else {
+                MX_ACT_DISPATCH(qmv1_kernel<QT, EPI, F16, SRC_NORM><<<dim3(N / 32, ks), 64 * QMV_WAVES, lds, st>>>(
+                    W, N, K, C, xsrc, nw, eps));
+            }
+            MXK_CHECK_LAUNCH();
+        }
         if (src == SRC_ACT) {
             MX_ACT_DISPATCH(qmv_kernel<QT, MM, EPI, F16, SRC_ACT><<<dim3(N / 32, ks), 64 * QMV_WAVES, lds, st>>>(
                 nullptr, nullptr, W, M, N, K, C, ldc, xsrc, ldx, nullptr, 0.f));
@@ -633,6 +757,11 @@ extern "C" int mxk_qmv_x(int qtype, int epi, int src, const void* x, int ldx, co
 #undef QMVX_EPI
 #undef QMVX_M
     return (int)hipErrorInvalidValue;
+}
+
+extern "C" int mxk_qmv1_enable(int on) {
+    g_qmv1_on = on;
+    return 0;
 }
 
 extern "C" int mxk_dequant_t32(int qtype, const uint8_t* W, const int* rows, int nrows, int K, uint16_t* ob,

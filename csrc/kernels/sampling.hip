@@ -504,21 +504,21 @@ MX_DEV uint32_t tk_bisect(const T (&u)[NV], int K, uint32_t lo, uint32_t hi, int
     return lo;
 }
 
-// Candidate selection by one LDS histogram of the distance d below the max (TK_NB monotone bins: 1/32 logit
-// unit for d < 4, 1/8 for d < 12, 1/2 for d < 44; beyond that no bin): every value is binned once (an LDS
-// atomic only inside the range), one wave scans the bins from the top for the first cumulative count >= K, and
+// Candidate selection by one LDS histogram of the distance below the max (TK_NB bins of 1/TK_BPU logit unit;
+// beyond that no bin): one wave scans the bins from the top for the first cumulative count >= K, and
 // everything in bins <= that one is the candidate set — 4 block barriers instead of a ~20-step bisection
 // (round 3: 45 + 33 us at 128 rows). A bin too dense for the capacity (flat rows, exact ties) or a row with
 // fewer than K values inside the histogram range falls back to the bisection on the key axis.
 constexpr int TK_NB = 256;
 
+constexpr float TK_BPU = 8.f;  // bins per logit unit: 256 bins cover 32 units below the max
+
 MX_DEV int tk_bin(float mx, float v) {  // monotone in v (0 = the top), TK_NB = outside the range / masked
-    const float d = mx - v;
-    if (d < 4.f) return (int)(d * 32.f);                    // bins 0 .. 127
-    if (d < 12.f) return 128 + (int)((d - 4.f) * 8.f);      // 128 .. 191
-    if (d < 44.f) return 192 + (int)((d - 12.f) * 2.f);     // 192 .. 255
-    return TK_NB;                                           // -inf / NaN fail every compare
+    const float d = (mx - v) * TK_BPU;
+    return d < (float)TK_NB ? (int)d : TK_NB;  // -inf / NaN: the compare fails
 }
+// bin(v) <= b  <=>  (mx - v) * TK_BPU < b + 1 (truncation of a non-negative value): one sub, mul and compare
+MX_DEV bool tk_in(float mx, float v, int b) { return (mx - v) * TK_BPU < (float)(b + 1); }
 
 // first bin b (scanning from the top) whose cumulative count reaches K: {b, cum(b)}; {TK_NB, total} if none.
 // Called by one full wave; hist[TK_NB] in LDS.
@@ -610,10 +610,12 @@ __global__ __launch_bounds__(TK_NT) void tk_slice_kernel(const float* __restrict
         const int tb = tk_bin(mx, tmax);
         if (tb < TK_NB) atomicAdd(&hist[tb], 1);
     }
-    float zs = 0.f;  // the slice's share of the row's partition function (log-probs of greedy rows)
+    float zs = 0.f;  // the slice's share of the row's partition function (log-probs of greedy rows only)
+    if (P.temperature <= 0.f) {
 #pragma unroll
-    for (int j = 0; j < TK_NV; ++j)
-        if (v[j] > -INFINITY) zs += __expf(v[j] - mx);
+        for (int j = 0; j < TK_NV; ++j)
+            if (v[j] > -INFINITY) zs += __expf(v[j] - mx);
+    }
     zs = wave_sum(zs);
     if ((threadIdx.x & 63) == 0) fred[TK_NT / 64 + (threadIdx.x >> 6)] = zs;
     __syncthreads();
@@ -637,12 +639,12 @@ __global__ __launch_bounds__(TK_NT) void tk_slice_kernel(const float* __restrict
     if (bA < TK_NB) {
         int myc = 0;
 #pragma unroll
-        for (int j = 0; j < TK_NV; ++j) myc += tk_bin(mx, v[j]) <= bA ? 1 : 0;
+        for (int j = 0; j < TK_NV; ++j) myc += tk_in(mx, v[j], bA) ? 1 : 0;
         int off = myc ? atomicAdd(&s_n, myc) : 0;
         if (myc && off + myc <= TK_CAPS) {
 #pragma unroll
             for (int j = 0; j < TK_NV; ++j) {
-                if (tk_bin(mx, v[j]) <= bA) {
+                if (tk_in(mx, v[j], bA)) {
                     cand_v[base + off] = v[j];
                     cand_i[base + off] = i0 + j * TK_NT + threadIdx.x;
                     ++off;
@@ -678,11 +680,11 @@ __global__ __launch_bounds__(TK_NT) void tk_slice_kernel(const float* __restrict
             const int b = s_b;
             myc = 0;
 #pragma unroll
-            for (int j = 0; j < TK_NV; ++j) myc += tk_bin(mx, v[j]) <= b ? 1 : 0;
+            for (int j = 0; j < TK_NV; ++j) myc += tk_in(mx, v[j], b) ? 1 : 0;
             off = myc ? atomicAdd(&s_n, myc) : 0;  // <= TK_CAPS in total by the scan
 #pragma unroll
             for (int j = 0; j < TK_NV; ++j) {
-                if (tk_bin(mx, v[j]) <= b) {
+                if (tk_in(mx, v[j], b)) {
                     cand_v[base + off] = v[j];
                     cand_i[base + off] = i0 + j * TK_NT + threadIdx.x;
                     ++off;

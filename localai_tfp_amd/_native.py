@@ -45,6 +45,7 @@ KERNEL_SIGS = {
     "mxk_qmm2_set_rot": [I],
     "mxk_qmm3": [I, I, I, P, I, P, I, I, I, I, P, I, P],
     "mxk_sample_trace": [I, P],
+    "mxk_qmv1_enable": [I],
     "mxk_qmm3_dbg": [I, I, P, I, P, I, I, I, P, I, P],
     "mxk_qmm_ws": [I, I, I, P, I, P, I, I, I, I, P, I, P],
     "mxk_qmm_ws_dbg": [I],

@@ -196,6 +196,11 @@ class _SafetensorsDir:
             self.where.update({k: v for k, v in wm.items() if v in self._h})
         self.qcfg = qcfg or {}
         self.qmethod = str(self.qcfg.get("quant_method", "") or "").lower()
+        if self.qmethod == "exl2" or any(k.endswith((".q_invperm", ".q_scale_max", ".q_groups")) for k in self.where):
+            # exllamav2's EXL2 (per-group mixed 2-8-bit codes behind a row permutation): no decoder here —
+            # refused by name instead of failing later on the missing .weight tensors
+            raise ValueError("EXL2 (exllamav2) checkpoints are not supported: convert to GGUF, GPTQ or AWQ "
+                             "(reference backend/python/exllama2/backend.py:45-62)")
         if self.qmethod and self.qmethod not in ("gptq", "awq"):
             raise ValueError(f"quantization_config.quant_method {self.qmethod!r} is not supported (gptq / awq)")
 

@@ -196,6 +196,11 @@ class PiperPhonemes:
         self.espeak_data = espeak_data
         self.lexicon = lexicon or {}
         self._espeak = shutil.which("espeak-ng") if self.kind == "espeak" else None
+        if self.kind == "espeak" and not self._espeak and not self.voice.lower().startswith("en"):
+            # the built-in rules are English only; a non-English voice would be fed English phonemes. No reader
+            # of espeak-ng-data's compiled dictionaries ships here: refuse instead of synthesising garbage
+            raise ValueError(f"piper voice {self.voice!r} needs the espeak-ng program for its phonemes (not found "
+                             "on PATH); only English voices fall back to the built-in letter-to-sound rules")
 
     def phonemize(self, text: str) -> list[str]:
         text = unicodedata.normalize("NFC", text)

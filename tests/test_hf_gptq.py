@@ -125,3 +125,22 @@ def test_quantized_hf_dir_matches_transformers(method, tmp_path):
     got = _run(model, "cpu", prompt, [])[0][0]
     rel = float((got - ref).norm() / ref.norm())
     assert rel < 5e-3, (method, rel)
+
+
+def test_exl2_checkpoint_refused(tmp_path):
+    """exllamav2 EXL2 tensors (q_weight / q_invperm / q_scale_max / q_groups) are refused by name at load."""
+    import json
+    import torch
+    from localai_tfp_amd.models.hf import hf_source
+    d = tmp_path / "exl2"
+    d.mkdir()
+    cfg = {"architectures": ["LlamaForCausalLM"], "model_type": "llama", "hidden_size": 64, "intermediate_size": 128,
+           "num_hidden_layers": 1, "num_attention_heads": 4, "num_key_value_heads": 4, "vocab_size": 32,
+           "rms_norm_eps": 1e-5, "max_position_embeddings": 64}
+    (d / "config.json").write_text(json.dumps(cfg))
+    sd = {"model.layers.0.self_attn.q_proj.q_weight": torch.zeros(8, 64, dtype=torch.int32),
+          "model.layers.0.self_attn.q_proj.q_invperm": torch.zeros(64, dtype=torch.int16),
+          "model.layers.0.self_attn.q_proj.q_scale_max": torch.zeros(4, dtype=torch.float16)}
+    save_file(sd, str(d / "model.safetensors"), metadata={"format": "pt"})
+    with pytest.raises(ValueError, match="EXL2"):
+        hf_source(str(d), "exl2")

@@ -152,3 +152,16 @@ def test_piper_x_low_refused(tmp_path):
     (tmp_path / "x_low.onnx.json").write_text(json.dumps(voice_json()), encoding="utf-8")
     with pytest.raises(ValueError, match="x_low"):
         load_piper(str(p2))
+
+
+def test_piper_non_english_without_espeak_refused(monkeypatch):
+    """No espeak-ng program and no reader of espeak-ng-data's compiled dictionaries: a non-English espeak voice
+    is refused at load instead of being fed the built-in English phonemes (English voices still fall back)."""
+    import localai_tfp_amd.models.piper as P
+    monkeypatch.setattr(P.shutil, "which", lambda name: None)
+    meta = voice_json("espeak")
+    meta["espeak"] = {"voice": "de"}
+    with pytest.raises(ValueError, match="espeak-ng"):
+        PiperPhonemes(meta)
+    meta["espeak"] = {"voice": "en-gb"}
+    assert PiperPhonemes(meta).encode("hi")[:2] == [1, 0]

@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--gemv", action="store_true", help="M <= 4 decode GEMV with the fused RMSNorm / q8 prologue")
     ap.add_argument("--ws", default="", help="qmm_ws cfg,splits (warp-specialised kernel)")
     ap.add_argument("--q2", default="", help="qmm2 wm,ks,wn,splits")
+    ap.add_argument("--qmv1", type=int, default=1, help="0: disable the batch-1 fast-prologue GEMV (qmv1_kernel)")
     ap.add_argument("--q3dbg", default="", help="qmm3 isolation build dbg,wm (Q4_K SwiGLU only)")
     ap.add_argument("--q2dbg", default="", help="qmm2 isolation build dbg,wm,ks,wn (Q4_K SwiGLU only)")
     ap.add_argument("--qt", type=int, default=0, help="ggml type override (e.g. 3 = Q4_1 -> MX4F t32)")
@@ -40,6 +41,8 @@ def main():
         L.QMM_FORCE = tuple(int(v) for v in a.cfg.split(","))
     if a.q2:
         L.QMM2, L.QMM2_FORCE = True, tuple(int(v) for v in a.q2.split(","))
+    from localai_tfp_amd import _native as Nq
+    Nq.kcall("mxk_qmv1_enable", a.qmv1)
     x = (torch.randn(a.M, K, device="cuda") * 0.5).half()
     out = (torch.empty(a.M, N // 2, device="cuda", dtype=torch.float16) if epi == 3
            else torch.zeros(a.M, N, device="cuda"))
