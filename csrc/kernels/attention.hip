@@ -177,7 +177,8 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restri
             os += sm_o[w][h][d] * a;
         }
         const int hq = kvh * G + h;
-        if (n_parts == 1) {
+        // one partition holds the whole sequence: final output here (attn_decode_reduce skips it)
+        if (n_parts == 1 || (part == 0 && L <= part_size)) {
             out[(size_t)b * out_stride + (size_t)hq * D + d] = f32_to_act<F16>(ls > 0.f ? os / ls : 0.f);
         } else {
             const size_t pi = ((size_t)b * Hq + hq) * n_parts + part;
@@ -203,6 +204,7 @@ __global__ __launch_bounds__(128) void attn_decode_reduce_kernel(const float2* _
     const int bh = blockIdx.x;
     const int b = bh / Hq, h = bh % Hq;
     const int np = min(n_parts, (seq_lens[b] + part_size - 1) / part_size);
+    if (np <= 1) return;  // the attention workgroup wrote this sequence's output directly
     const size_t pb = (size_t)bh * n_parts;
     if (threadIdx.x < 64) {
         float m = -INFINITY;
@@ -311,8 +313,10 @@ MX_DEV int v_lds_off(int p, int nt) {
 template <int D>
 constexpr int dec_wave_lds() { return 32 * D * 2 + 16 * (32 + 8) * 2; }
 
-template <int D, bool F16, bool KV8>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KV8 ? 2 : 4, KV8 ? 2 : 4))) void attn_decode_mfma_kernel(
+// NW = 16 (1024 threads, one workgroup per CU): the small-batch form — a 512-key partition per workgroup, so a
+// context of <= 512 keys is ONE partition whose workgroup writes the final output (no reduce work for it).
+template <int D, bool F16, bool KV8, int NW = 4>
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(KV8 ? 2 : 4, KV8 ? 2 : 4))) void attn_decode_mfma_kernel(
     const bf16_t* __restrict__ q, int q_stride, const void* __restrict__ kcv, const void* __restrict__ vcv,
     const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ seq_lens, int Hkv, int G, int bs,
     float scale, int window, float softcap, int part_size, int n_parts, bf16_t* __restrict__ out, int out_stride,
@@ -348,7 +352,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KV8 ? 2 : 4
         if (col < G) qf[ks] = *(const bf16x8*)(q + (size_t)b * q_stride + (size_t)(kvh * G + col) * D + 32 * ks + 8 * g);
         else qf[ks] = (bf16x8){};
     }
-    for (int i = threadIdx.x; i < nblk; i += 256) sbt[i] = bt[blk0 + i];
+    for (int i = threadIdx.x; i < nblk; i += 64 * NW) sbt[i] = bt[blk0 + i];
     __syncthreads();
     f32x4 oacc[D / 16];
 #pragma unroll
@@ -361,7 +365,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KV8 ? 2 : 4
     const char* kc = (const char*)kcv;
     const char* vc = (const char*)vcv;
 
-    for (int kt0 = p_start + wave * KT; kt0 < p1; kt0 += 4 * KT) {
+    for (int kt0 = p_start + wave * KT; kt0 < p1; kt0 += NW * KT) {
         // ---- issue the tile's K fragment loads and V chunk loads ----
         bf16x8 kf[2][D / 32];
 #pragma unroll
@@ -477,10 +481,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KV8 ? 2 : 4
         __builtin_amdgcn_s_waitcnt(0xc07f);  // the transposed reads have returned before V is rewritten
         __builtin_amdgcn_wave_barrier();
     }
-    // ---- merge the 4 waves: (m, l) per row and O rows through the (now free) LDS slices ----
+    // ---- merge the NW waves: (m, l) per row and O rows through the (now free) LDS slices ----
     __syncthreads();
     float* wo = (float*)(smem + wave * WB);        // [16 rows][D] fp32 (8 KB for D=128 <= WB)
-    float* wml = (float*)(smem + 4 * WB) + wave * 32;  // [16 rows] m, [16 rows] l
+    float* wml = (float*)(smem + NW * WB) + wave * 32;  // [16 rows] m, [16 rows] l
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int r = 4 * g + i;
@@ -489,21 +493,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KV8 ? 2 : 4
         if (col == 0) { wml[r] = mrow[i]; wml[16 + r] = lrow[i]; }
     }
     __syncthreads();
-    const float* ml = (const float*)(smem + 4 * WB);
-    for (int idx = threadIdx.x; idx < G * D; idx += 256) {
+    const float* ml = (const float*)(smem + NW * WB);
+    // a sequence that fits this one partition: the final output here, no partials (the reduce skips it)
+    const bool single = n_parts == 1 || (p0 == 0 && L <= part_size);
+    for (int idx = threadIdx.x; idx < G * D; idx += 64 * NW) {
         const int h = idx / D, d = idx % D;
         float mx = -INFINITY;
 #pragma unroll
-        for (int w = 0; w < 4; ++w) mx = fmaxf(mx, ml[w * 32 + h]);
+        for (int w = 0; w < NW; ++w) mx = fmaxf(mx, ml[w * 32 + h]);
         float ls = 0.f, os = 0.f;
 #pragma unroll
-        for (int w = 0; w < 4; ++w) {
+        for (int w = 0; w < NW; ++w) {
             const float a = mx == -INFINITY ? 0.f : exp2f(ml[w * 32 + h] - mx);
             ls += ml[w * 32 + 16 + h] * a;
             os += ((const float*)(smem + w * WB))[h * D + d] * a;
         }
         const int hq = kvh * G + h;
-        if (n_parts == 1) {
+        if (single) {
             out[(size_t)b * out_stride + (size_t)hq * D + d] = f32_to_act<F16>(ls > 0.f ? os / ls : 0.f);
         } else {
             const size_t pi = ((size_t)b * Hq + hq) * n_parts + part;
@@ -511,7 +517,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KV8 ? 2 : 4
             part_o[pi * D + d] = os;
         }
     }
-    if (n_parts == 1 || !part_cnt) return;
+    if (single || !part_cnt) return;
     // fused split-K merge: the last of the (b, kvh) partition workgroups to finish merges all of them,
     // instead of a separate reduce launch (at batch 1 that launch costs as much as the attention itself).
     // The counter is left at zero for the next launch / graph replay.
@@ -550,14 +556,27 @@ static int launch_decode_mfma(const bf16_t* q, int q_stride, const void* kc, con
                               float2* part_ml, float* part_o, int* part_cnt, int kv8, hipStream_t st) {
     dim3 grid(Hkv, B, n_parts);
     static_assert(16 * D * 4 <= dec_wave_lds<D>(), "merge buffer");
-    const size_t lds = 4 * dec_wave_lds<D>() + 4 * 32 * 4;
+    // 512-key partitions run 16 waves per workgroup (one 32-key tile each), smaller ones 4
+    const bool wide = part_size >= 512 && !kv8 && B < 8;  // (large batches keep 4-wave workgroups)
+    const int NWs = wide ? 16 : 4;
+    const size_t lds = NWs * dec_wave_lds<D>() + NWs * 32 * 4;
     MX_ACT_DISPATCH({
         if (kv8)
             attn_decode_mfma_kernel<D, F16, true><<<grid, 256, lds, st>>>(q, q_stride, kc, vc, bt, bt_stride, seq_lens,
                                                                          Hkv, G, bs, scale, window, softcap, part_size,
                                                                          n_parts, out, out_stride, part_ml, part_o,
                                                                          part_cnt);
-        else
+        else if (wide) {
+            static bool attr = false;
+            if (!attr) {
+                (void)hipFuncSetAttribute((const void*)attn_decode_mfma_kernel<D, F16, false, 16>,
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+                attr = true;
+            }
+            attn_decode_mfma_kernel<D, F16, false, 16><<<grid, 1024, lds, st>>>(
+                q, q_stride, kc, vc, bt, bt_stride, seq_lens, Hkv, G, bs, scale, window, softcap, part_size, n_parts,
+                out, out_stride, part_ml, part_o, part_cnt);
+        } else
             attn_decode_mfma_kernel<D, F16, false><<<grid, 256, lds, st>>>(q, q_stride, kc, vc, bt, bt_stride,
                                                                           seq_lens, Hkv, G, bs, scale, window, softcap,
                                                                           part_size, n_parts, out, out_stride, part_ml,

@@ -440,16 +440,32 @@ __global__ __launch_bounds__(64 * QMV_WAVES) void qmv_kernel(const int8_t* __res
     }
 }
 
-// Batch-1 GEMV with the activation prologue fused (SRC_ACT / SRC_NORM), for K = 4096 and at most two units per
-// wave (every row-parallel split chosen so): straight-line code with no unit loop, and the activation row is
-// read BEFORE the weights are requested — loads complete in issue order for s_waitcnt, so qmv_kernel's
-// prologue (issued after the weights) waited for the wave's whole weight stream before it could start the
-// norm / quantisation. The WHOLE row is read by every workgroup (8 elements per thread): the norm's sum of
-// squares comes from the same registers, and the workgroup quantises the part inside its K slice into LDS.
+// Batch-1 GEMV with the activation prologue fused (SRC_ACT / SRC_NORM) for at most two units per wave (K slices
+// of <= 4096): straight-line code with no unit loop, and the workgroup's activation slice is read BEFORE the
+// weights are requested — loads complete in issue order for s_waitcnt, so qmv_kernel's prologue (issued after
+// the weights) waited for the wave's whole weight stream before it could start the norm / quantisation.
+// SRC_NORM runs unsplit (ks = 1, K = 4096): the slice is the whole row and the norm's sum of squares comes
+// from the same registers.
+// EPI_ROPEKV: the qkv projection's epilogue does the RoPE (adjacent-pair rotation over the whole head) and the
+// paged KV append itself — q rows go to `qo` (bf16), k / v rows into the caches at slots[0] — so no separate
+// rope_kv launch runs at batch 1. Column c of this launch is column n_off + c of the fused q|k|v row.
+constexpr int EPI_ROPEKV = 5;
+struct QRope {
+    const int* pos;
+    const int* slots;
+    const float* inv_freq;
+    const float* bias;  // this part's bias (nullptr: none)
+    float attn_factor;
+    int Hq, Hkv, D, n_off, block_size;
+    bf16_t* qo;
+    bf16_t* kc;
+    bf16_t* vc;
+};
+
 template <int QT, int EPI, bool F16, int SRC>
 __global__ __launch_bounds__(64 * QMV_WAVES) void qmv1_kernel(const uint8_t* __restrict__ W, int N, int K,
                                                               void* __restrict__ Cv, const void* __restrict__ xsrc,
-                                                              const float* __restrict__ nw, float eps) {
+                                                              const float* __restrict__ nw, float eps, QRope rp) {
     using U = TUnit<QT>;
     constexpr int NT = 64 * QMV_WAVES;
     static_assert(SRC == SRC_ACT || SRC == SRC_NORM, "fused prologue only");
@@ -464,8 +480,9 @@ __global__ __launch_bounds__(64 * QMV_WAVES) void qmv1_kernel(const uint8_t* __r
     const int u0 = blockIdx.y * per, u1 = min(nunit, u0 + per);
     const int k0 = u0 * U::ELEMS, klen = max(0, u1 - u0) * U::ELEMS;
     const uint8_t* wg = W + (size_t)g * nunit * U::BYTES;
-    // 1. the activation row (8 elements per thread) and, for the norm, its weights
-    const int e = 8 * threadIdx.x;
+    // 1. this workgroup's slice of the activation row (8 elements per thread; SRC_NORM: the whole row, ks = 1)
+    //    and, for the norm, its weights
+    const int er = 8 * threadIdx.x, e = k0 + min(er, max(klen - 8, 0));  // clamped: a valid address
     float a8[8], w8[8];
     if constexpr (SRC == SRC_NORM) {
         const float* xr = (const float*)xsrc + e;
@@ -498,7 +515,7 @@ __global__ __launch_bounds__(64 * QMV_WAVES) void qmv1_kernel(const uint8_t* __r
         ss = wave_sum(ss);
         if (lane == 0) nred[wave] = ss;
     }
-    if (e >= k0 && e < k0 + klen) {  // whole 4-lane groups (k0 % 256 == 0)
+    if (er < klen) {  // whole 4-lane groups (klen % 256 == 0)
         float v8[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) v8[j] = SRC == SRC_NORM ? a8[j] * w8[j] : a8[j];
@@ -514,8 +531,8 @@ __global__ __launch_bounds__(64 * QMV_WAVES) void qmv1_kernel(const uint8_t* __r
         uint2 pk;
         pk.x = (q[0] & 0xFF) | ((q[1] & 0xFF) << 8) | ((q[2] & 0xFF) << 16) | ((uint32_t)(q[3] & 0xFF) << 24);
         pk.y = (q[4] & 0xFF) | ((q[5] & 0xFF) << 8) | ((q[6] & 0xFF) << 16) | ((uint32_t)(q[7] & 0xFF) << 24);
-        *(uint2*)(sq + (e - k0)) = pk;
-        if ((threadIdx.x & 3) == 0) sd[(e - k0) / 32] = make_float2(d, d * sf);
+        *(uint2*)(sq + er) = pk;
+        if ((threadIdx.x & 3) == 0) sd[er / 32] = make_float2(d, d * sf);
     }
     __syncthreads();
     if constexpr (SRC == SRC_NORM) {
@@ -542,7 +559,34 @@ __global__ __launch_bounds__(64 * QMV_WAVES) void qmv1_kernel(const uint8_t* __r
         for (int w = 0; w < QMV_WAVES; ++w) v += red[w][r];
     }
     const int n = g * 32 + r;
-    if constexpr (EPI == E16_SWIGLU || EPI == E16_GEGLU) {
+    if constexpr (EPI == EPI_ROPEKV) {
+        if (rp.bias) v += rp.bias[n];
+        const float partner = __shfl_xor(v, 1);  // the other element of this adjacent rotation pair
+        const int c = rp.n_off + n, hh = c / rp.D, d = c - hh * rp.D;
+        if (h == 0) {
+            float y = v;
+            if (hh < rp.Hq + rp.Hkv) {
+                float sv, cv;
+                sincosf((float)rp.pos[0] * rp.inv_freq[d >> 1], &sv, &cv);
+                cv *= rp.attn_factor;
+                sv *= rp.attn_factor;
+                y = (d & 1) ? partner * sv + v * cv : v * cv - partner * sv;
+            }
+            const uint16_t yb = (uint16_t)(pack_bf16x2(y, 0.f) & 0xFFFF);
+            if (hh < rp.Hq) {
+                rp.qo[(size_t)hh * rp.D + d] = yb;
+            } else {
+                const int slot = rp.slots[0];
+                if (slot >= 0) {
+                    const bool isk = hh < rp.Hq + rp.Hkv;
+                    const int kvh = hh - rp.Hq - (isk ? 0 : rp.Hkv);
+                    const size_t e = (((size_t)(slot / rp.block_size) * rp.Hkv + kvh) * rp.block_size +
+                                      slot % rp.block_size) * rp.D + d;
+                    (isk ? rp.kc : rp.vc)[e] = yb;
+                }
+            }
+        }
+    } else if constexpr (EPI == E16_SWIGLU || EPI == E16_GEGLU) {
         const float up = __shfl_down(v, 16);
         if (h == 0 && r < 16) ((uint16_t*)Cv)[g * 16 + r] = f32_to_act<F16>(glu_gate_f<EPI>(v) * up);
     } else if (h == 0) {
@@ -669,13 +713,15 @@ static int launch_qmv(const int8_t* xq, const float2* xds, const uint8_t* W, int
         const size_t sl = (size_t)per * TUnit<QT>::ELEMS;
         const size_t lds = MM * (sl + sl / 32 * sizeof(float2));
         if (lds > 64 * 1024) return (int)hipErrorInvalidValue;
-        if (MM == 1 && M == 1 && K == 4096 && ks == 1 && per <= 2 * QMV_WAVES && g_qmv1_on) {
+        // qmv1: batch 1, at most two units per wave; the norm needs the whole row in one workgroup (ks = 1)
+        if (MM == 1 && M == 1 && per <= 2 * QMV_WAVES && g_qmv1_on &&
+            (src == SRC_ACT || (K == 4096 && ks == 1))) {
             if (src == SRC_ACT) {
                 MX_ACT_DISPATCH(qmv1_kernel<QT, EPI, F16, SRC_ACT><<<dim3(N / 32, ks), 64 * QMV_WAVES, lds, st>>>(
-                    W, N, K, C, xsrc, nullptr, 0.f));
+                    W, N, K, C, xsrc, nullptr, 0.f, QRope{}));
             } else {
                 MX_ACT_DISPATCH(qmv1_kernel<QT, EPI, F16, SRC_NORM><<<dim3(N / 32, ks), 64 * QMV_WAVES, lds, st>>>(
-                    W, N, K, C, xsrc, nw, eps));
+                    W, N, K, C, xsrc, nw, eps, QRope{}));
             }
             MXK_CHECK_LAUNCH();
         }
@@ -757,6 +803,30 @@ extern "C" int mxk_qmv_x(int qtype, int epi, int src, const void* x, int ldx, co
 #undef QMVX_EPI
 #undef QMVX_M
     return (int)hipErrorInvalidValue;
+}
+
+// Batch-1 qkv GEMV with the input RMSNorm fused in front and RoPE + paged KV append fused behind (EPI_ROPEKV):
+// x fp32 [1, 4096] residual row, W one t32 part (q, k, v or a fused run of them) whose columns start at column
+// n_off of the q|k|v row; rotation over whole heads of D (adjacent pairs, rot_dim == D), bf16 q and caches.
+extern "C" int mxk_qmv1_rope(int qtype, const float* x, const float* nw, float eps, const uint8_t* W, int N, int K,
+                             int n_off, const int* pos, const int* slots, const float* inv_freq, const float* bias,
+                             float attn_factor, int Hq, int Hkv, int D, bf16_t* qo, bf16_t* kc, bf16_t* vc,
+                             int block_size, hipStream_t st) {
+    if (K != 4096 || N % 32 || (D != 64 && D != 128) || n_off % 32 || ((uintptr_t)x & 15)) return (int)hipErrorInvalidValue;
+    const QRope rp{pos, slots, inv_freq, bias, attn_factor, Hq, Hkv, D, n_off, block_size, qo, kc, vc};
+    const size_t lds = (size_t)K + K / 32 * sizeof(float2);
+#define QR1(QT_) \
+    qmv1_kernel<QT_, EPI_ROPEKV, true, SRC_NORM><<<dim3(N / 32, 1), 64 * QMV_WAVES, lds, st>>>(W, N, K, nullptr, x, nw, eps, rp)
+    switch (qtype) {
+        case MXQ_Q4_K: QR1(MXQ_Q4_K); break;
+        case MXQ_Q5_K: QR1(MXQ_Q5_K); break;
+        case MXQ_Q6_K: QR1(MXQ_Q6_K); break;
+        case MXQ_Q3_K: QR1(MXQ_Q3_K); break;
+        case MXQ_Q2_K: QR1(MXQ_Q2_K); break;
+        default: return (int)hipErrorInvalidValue;
+    }
+#undef QR1
+    MXK_CHECK_LAUNCH();
 }
 
 extern "C" int mxk_qmv1_enable(int on) {

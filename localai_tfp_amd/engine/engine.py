@@ -172,10 +172,13 @@ class StepGraph:
     image into a pinned ring buffer and refreshes all inputs with ONE async H2D copy per step.
     """
 
-    def __init__(self, engine: "LLMEngine", B: int, P: int = 0, PS: int = 0):
+    def __init__(self, engine: "LLMEngine", B: int, P: int = 0, PS: int = 0, L: int = 0):
         e = engine
         dev = e.device
         self.B, self.P, self.PS = B, P, PS
+        # L > 0: decode-only graph for contexts of <= L keys (small batches): the decode attention is captured
+        # with ONE partition per sequence — a single pass with no partition-merge launch (models/llama.py)
+        self.L = L
         self.maxb = mb = e.max_blocks_per_seq
         self.rows = e.model.prefill_rows() if P else 1
         self.NT = (P // self.rows + PS) if P else 0  # prefill attention tile capacity
@@ -208,7 +211,7 @@ class StepGraph:
         self.argmax = torch.zeros(self.S, dtype=torch.int32, device=dev)
         self.fb = ForwardBatch(v["tokens"][:T], v["positions"], v["slots"], v["lidx"], n_decode=B,
                                dec_block_tables=v["dec_bt"][:B], dec_seq_lens=v["dec_lens"][:B],
-                               dec_max_len=e.cfg.max_model_len)
+                               dec_max_len=L or e.cfg.max_model_len)
         if P:
             self.fb.pf_block_tables, self.fb.pf_cu_q, self.fb.pf_ctx_lens = v["pf_bt"], v["pf_cu"], v["pf_ctx"]
             self.fb.pf_tiles = (v["pf_tseq"], v["pf_tq0"])
@@ -775,10 +778,14 @@ class LLMEngine:
         while q:
             self._process_inflight(q.popleft())
 
+    # decode-only graphs of fewer than SHORT_CTX_B rows get a second, short-context form (contexts <= SHORT_CTX
+    # keys: one 512-key partition per sequence, no partition-merge launch)
+    SHORT_CTX, SHORT_CTX_B = 512, 8
+
     def _graph_for(self, n: int) -> StepGraph | None:
         """Decode-only graph of the bucket holding n rows."""
         b = self._dec_bucket(n)
-        return self._graph_get((b, 0, 0)) if b else None
+        return self._graph_get((b, 0, 0, 0)) if b else None
 
     def _dec_bucket(self, n: int) -> int | None:
         return next((x for x in self.cfg.graph_buckets if x >= n and x <= self.cfg.max_num_seqs), None)
@@ -793,14 +800,17 @@ class LLMEngine:
         if B is None:
             return None
         if "pf_cu" not in plan:
-            return (B, 0, 0) if nd else None
+            if not nd:
+                return None
+            short = B < self.SHORT_CTX_B and int(plan["dec_lens"].max()) <= self.SHORT_CTX
+            return (B, 0, 0, self.SHORT_CTX if short else 0)
         if self.recurrent or not hasattr(self.model, "prefill_rows") or len(plan["pf_cu"]) - 1 > c.mixed_graph_seqs:
             return None
         npf = int(plan["pf_cu"][-1])
         P = next((x for x in c.mixed_graph_tokens if x >= npf), None)
         if P is None or B + P > self.ws.max_tokens:
             return None
-        return (B, P, c.mixed_graph_seqs)
+        return (B, P, c.mixed_graph_seqs, 0)
 
     def _graph_get(self, key, create: bool = True) -> StepGraph | None:
         if not self.use_graphs:

@@ -37,7 +37,7 @@ from ..ops import core as K
 from ..ops import quant as Q
 from ..ops.linear import (ACT_DTYPE, EPI_ADD_F32, EPI_BF16, EPI_F32, EPI_GEGLU, EPI_SWIGLU, QWeight, concat_rows,
                           _fp32_out_ok, dense_min_m, interleave_gate_up, qmatmul, qmatmul8, qmm8_ok, qmv_fusable,
-                          qmv_fused)
+                          qmv_fused, qmv_rope_fused)
 from ..ops.moe import MoEWeights, moe_ffn
 from .config import LlamaConfig
 
@@ -46,7 +46,7 @@ GEMV_MAX_M = 4
 # partitions mean fewer split-K partials to merge; c128 14278 vs 14151 tok/s at 256, within run-to-run noise:
 # profiles/r2_decode_part_c128_p{256,512}.json)
 DECODE_PART_LARGE_B = int(__import__("os").environ.get("MX_DECODE_PART_LARGE_B", "512"))
-DECODE_PART_SMALL_B = int(__import__("os").environ.get("MX_DECODE_PART_SMALL_B", "64"))  # < 8 sequences
+DECODE_PART_SMALL_B = int(__import__("os").environ.get("MX_DECODE_PART_SMALL_B", "512"))  # < 8 sequences: 16-wave single-pass
 # (batch 1: 64 -> 450, 256 -> 448, 512 -> 431 tok/s, profiles/r2_decode_part_c1_p*.json)
 # decode batches up to this size run the RMSNorm / q8 quantisation inside the GEMV prologue (qmv.hip
 # SRC_NORM / SRC_ACT). Every workgroup of the GEMV redoes the row statistics, so the fusion pays only at
@@ -584,7 +584,23 @@ class LlamaModel:
                     and T >= dense_min_m(xb.dtype, EPI_F32, True) and _fp32_out_ok(xb.dtype)):
                 torch.mm(xb, L.qkv_dense.t(), out_dtype=torch.float32, out=qkv)
                 off = qkv.shape[1]
-            for w in (L.qkv_parts if off == 0 else ()):
+            q = ws.q[:T]
+            inv_freq, attn_factor = L.rope or (self.inv_freq, self.attn_factor)
+            # batch 1: RoPE + KV append in each qkv part's GEMV epilogue (no rope_kv launch); every part or none
+            rope_fused = (fuse_qkv and T == 1 and off == 0 and not cfg.neox and cfg.rope_dim == D
+                          and L.q_norm is None and self.tp_size == 1)
+            if rope_fused:
+                o2 = 0
+                for w in L.qkv_parts:
+                    b = L.bqkv[o2:o2 + w.N] if L.bqkv is not None else None
+                    if not qmv_rope_fused(w, h, L.attn_norm, eps, o2, fb.positions, fb.slots, inv_freq, b, attn_factor,
+                                          Hq, Hkv, D, q.view(T, Hq, D), kc, vc, kv.block_size):
+                        if o2:
+                            raise RuntimeError("qkv RoPE fusion applied to some parts only")
+                        rope_fused = False
+                        break
+                    o2 += w.N
+            for w in (L.qkv_parts if off == 0 and not rope_fused else ()):
                 sl = qkv[:, off:off + w.N] if len(L.qkv_parts) > 1 else qkv
                 if fuse_qkv:
                     qmv_fused(w, h, EPI_F32, sl, norm=L.attn_norm, eps=eps, out_zeroed=True)
@@ -593,11 +609,10 @@ class LlamaModel:
                 else:
                     qmatmul(w, xb, EPI_F32, sl, out_zeroed=True)
                 off += w.N
-            q = ws.q[:T]
-            inv_freq, attn_factor = L.rope or (self.inv_freq, self.attn_factor)
-            K.rope_kv(qkv, L.bqkv, fb.positions, fb.slots, inv_freq, attn_factor, Hq, Hkv, D,
-                      cfg.rope_dim, cfg.neox, q.view(T, Hq, D), kc, vc, kv.block_size,
-                      qk_norm=(L.q_norm, L.k_norm, eps) if L.q_norm is not None else None, zero_after=True)
+            if not rope_fused:
+                K.rope_kv(qkv, L.bqkv, fb.positions, fb.slots, inv_freq, attn_factor, Hq, Hkv, D,
+                          cfg.rope_dim, cfg.neox, q.view(T, Hq, D), kc, vc, kv.block_size,
+                          qk_norm=(L.q_norm, L.k_norm, eps) if L.q_norm is not None else None, zero_after=True)
             attn = ws.attn[:T]
             if nd:
                 K.attn_decode(q[:nd].view(nd, Hq, D), kc, vc, fb.dec_block_tables, fb.dec_seq_lens, self.scale,

@@ -426,13 +426,18 @@ def qmatmul8(W: QWeight, a, epi: int, out: torch.Tensor, *, out_zeroed: bool = F
 QMV_FUSE = os.environ.get("MX_QMV_FUSE", "1") != "0"
 
 
-def qmv_fusable(W, M: int, epi: int, out_zeroed: bool = False) -> int:
+QMV1_NORM_KS1 = os.environ.get("MX_QMV1_NORM_KS1", "1") != "0"
+
+
+def qmv_fusable(W, M: int, epi: int, out_zeroed: bool = False, norm: bool = False) -> int:
     """K-split count of the fused-input decode GEMV for this weight / batch, or 0 if it does not apply
     (not t32, M > 4, or the per-workgroup LDS slice of the q8 activations would exceed 64 KB)."""
     if not QMV_FUSE or not isinstance(W, QWeight) or W.layout != "t32" or not 0 < M <= 4 or W.data.device.type != "cuda":
         return 0
     ks = 1
     elem = 64 if int(W.qtype) == int(QType.Q8_0) else 256
+    if norm and M == 1 and W.K == 4096 and QMV1_NORM_KS1:
+        return 1  # unsplit: the batch-1 qmv1 kernel reads the row once, ahead of the weights (qmv.hip)
     if epi == EPI_ADD_F32 or (epi == EPI_F32 and out_zeroed):
         units = W.K // elem
         while (W.N // 32) * ks < 2 * CU_COUNT and units // (ks * 2) >= 2:
@@ -449,7 +454,7 @@ def qmv_fused(W: QWeight, x: torch.Tensor, epi: int, out: torch.Tensor, *, norm:
     Returns False (nothing launched) where the fused kernel does not apply; the caller then runs
     rmsnorm / quant_q8 + qmatmul."""
     M = x.shape[0]
-    ks = qmv_fusable(W, M, epi, out_zeroed)
+    ks = qmv_fusable(W, M, epi, out_zeroed, norm is not None)
     if (not ks or not x.is_cuda or x.stride(-1) != 1
             or (norm is None and x.dtype not in (torch.float16, torch.bfloat16))
             or (norm is not None and x.dtype != torch.float32)):
@@ -463,6 +468,26 @@ def qmv_fused(W: QWeight, x: torch.Tensor, epi: int, out: torch.Tensor, *, norm:
     N.kcall("mxk_qmv_x", int(W.qtype), EPI_ADD_F32 if ks > 1 else epi, 2 if norm is not None else 1, x.data_ptr(),
             x.stride(0), N.ptr(norm), float(eps), W.data.data_ptr(), M, W.N, W.K, ks, out.data_ptr(), out.stride(0),
             N.stream_ptr())
+    return True
+
+
+QMV_ROPE_QTYPES = (int(QType.Q4_K), int(QType.Q5_K), int(QType.Q6_K), int(QType.Q3_K), int(QType.Q2_K))
+QMV_ROPE_FUSE = os.environ.get("MX_QMV_ROPE", "1") != "0"
+
+
+def qmv_rope_fused(W: QWeight, x: torch.Tensor, norm: torch.Tensor, eps: float, n_off: int, positions, slots,
+                   inv_freq: torch.Tensor, bias, attn_factor: float, Hq: int, Hkv: int, D: int, q_out: torch.Tensor,
+                   k_cache: torch.Tensor, v_cache: torch.Tensor, block_size: int) -> bool:
+    """Batch-1 qkv part: RMSNorm -> q8 -> GEMV -> (+bias) -> RoPE (adjacent pairs, whole head) -> q_out or the
+    paged K/V caches at slots[0], one launch (qmv.hip mxk_qmv1_rope). False: not applicable, nothing launched."""
+    if (not QMV_ROPE_FUSE or not isinstance(W, QWeight) or W.layout != "t32" or int(W.qtype) not in QMV_ROPE_QTYPES
+            or W.K != 4096 or x.shape[0] != 1 or not x.is_cuda or x.dtype != torch.float32 or not x.is_contiguous()
+            or k_cache.dtype != torch.bfloat16 or v_cache.dtype != torch.bfloat16 or q_out.dtype != torch.bfloat16
+            or D not in (64, 128) or n_off % 32):
+        return False
+    N.kcall("mxk_qmv1_rope", int(W.qtype), x.data_ptr(), norm.data_ptr(), float(eps), W.data.data_ptr(), W.N, W.K,
+            n_off, positions.data_ptr(), slots.data_ptr(), inv_freq.data_ptr(), N.ptr(bias), float(attn_factor), Hq,
+            Hkv, D, q_out.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), block_size, N.stream_ptr())
     return True
 
 

@@ -215,19 +215,21 @@ def test_attn_decode(Hq, Hkv, D, lens, impl):
         K.attn_decode(q.to(DEV), kc.to(DEV), vc.to(DEV), bt.to(DEV), seq.to(DEV), scale, out, part_size=part,
                       impl=impl)
         assert rel(out, ref) < 1e-2, part
-    # graph-style launch: partition count for a long max_seq_len, most partitions empty
-    out = torch.empty(B, Hq, D, dtype=torch.bfloat16, device=DEV)
-    nparts = -(-4096 // 256)
-    ws = (torch.empty(B * Hq * nparts, 2, device=DEV), torch.empty(B * Hq * nparts, D, device=DEV))
-    K.attn_decode(q.to(DEV), kc.to(DEV), vc.to(DEV), bt.to(DEV), seq.to(DEV), scale, out, part_size=256,
-                  workspace=ws, max_seq_len=4096, impl=impl)
-    assert rel(out, ref) < 1e-2
+    # graph-style launch: partition count for a long max_seq_len, most partitions empty; 512-key partitions run
+    # the 16-wave single-pass form at B < 8 (sequences of <= 512 keys written directly, the reduce skips them)
+    for part in (256, 512):
+        out = torch.empty(B, Hq, D, dtype=torch.bfloat16, device=DEV)
+        nparts = -(-4096 // part)
+        ws = (torch.empty(B * Hq * nparts, 2, device=DEV), torch.empty(B * Hq * nparts, D, device=DEV))
+        K.attn_decode(q.to(DEV), kc.to(DEV), vc.to(DEV), bt.to(DEV), seq.to(DEV), scale, out, part_size=part,
+                      workspace=ws, max_seq_len=4096, impl=impl)
+        assert rel(out, ref) < 1e-2, part
     # the opt-in in-kernel partition merge (MFMA path): arrival counters reset themselves across launches
     K.FUSED_DECODE_MERGE, saved = True, K.FUSED_DECODE_MERGE
     cnt = torch.zeros(B * Hkv, dtype=torch.int32, device=DEV)
     nparts = -(-4096 // 64)
     ws = (torch.empty(B * Hq * nparts, 2, device=DEV), torch.empty(B * Hq * nparts, D, device=DEV))
-    for part in (64, 256, 64):
+    for part in (64, 256, 512, 64):
         out = torch.empty(B, Hq, D, dtype=torch.bfloat16, device=DEV)
         K.attn_decode(q.to(DEV), kc.to(DEV), vc.to(DEV), bt.to(DEV), seq.to(DEV), scale, out, part_size=part,
                       workspace=ws + (cnt,), max_seq_len=4096, impl=impl)
@@ -952,3 +954,88 @@ def test_argmax_keys_merge(tp):
     N.kcall("mxk_argmax_merge", keys.data_ptr(), tp, S, out.data_ptr(), N.stream_ptr())
     want = full.argmax(1).tolist()
     assert out.cpu().tolist() == want and want[1] == 5 and want[2] == 0 and want[3] == 77777
+
+
+@pytest.mark.parametrize("qt", [QType.Q4_K, QType.Q6_K, QType.Q3_K])
+def test_qmv1_batch1(qt):
+    """The batch-1 qmv1 kernel (activation slice read before the weights, no unit loop): unsplit RMSNorm input at
+    K = 4096 (fp32 store and the interleaved SwiGLU) and split 16-bit input at K = 14336 (accumulate), against
+    the fp32 reference and against the generic kernel (mxk_qmv1_enable(0))."""
+    from localai_tfp_amd.ops.linear import qmv_fused
+    g = torch.Generator().manual_seed(int(qt))
+    eps = 1e-5
+    for k, src in ((4096, "norm"), (14336, "act")):
+        n = 512
+        raw, dense = make_w(qt, n, k, seed=k + int(qt))
+        W = QWeight.from_ggml(raw, qt, n, k, DEV)
+        assert W.to_t32()
+        if src == "norm":
+            h = torch.randn(1, k, generator=g).to(DEV) * 3
+            nw = (torch.rand(k, generator=g) + 0.5).to(DEV)
+            xin, kw = h, dict(norm=nw, eps=eps)
+            ref = (h / torch.sqrt(h.pow(2).mean(-1, keepdim=True) + eps) * nw).cpu() @ dense.t()
+            epis = (EPI_F32, EPI_SWIGLU)
+        else:
+            N.ensure_act(torch.float16)
+            xin, kw = (torch.randn(1, k, generator=g) * 2).half().to(DEV), {}
+            ref = xin.float().cpu() @ dense.t()
+            epis = (EPI_ADD_F32,)
+        for epi in epis:
+            outs = []
+            for on in (1, 0):
+                N.kcall("mxk_qmv1_enable", on)
+                if epi == EPI_SWIGLU:
+                    o = torch.empty(1, n // 2, dtype=torch.float16, device=DEV)
+                else:
+                    o = torch.zeros(1, n, device=DEV)
+                assert qmv_fused(W, xin, epi, o, out_zeroed=True, **kw)
+                outs.append(o.float().cpu())
+            N.kcall("mxk_qmv1_enable", 1)
+            if epi == EPI_SWIGLU:
+                gu = ref.reshape(1, n // 32, 2, 16)
+                r = (torch.nn.functional.silu(gu[:, :, 0]) * gu[:, :, 1]).reshape(1, n // 2)
+            else:
+                r = ref
+            assert rel(outs[0], outs[1]) < 5e-3 and rel(outs[0], r) < 2e-2, (src, epi)
+
+
+@pytest.mark.parametrize("qt", [QType.Q4_K, QType.Q6_K])
+@pytest.mark.parametrize("bias", [False, True])
+def test_qmv_rope_fused(qt, bias):
+    """Batch-1 qkv GEMV with RoPE + paged KV append in the epilogue == the unfused qmv + rope_kv kernels: q rows,
+    the K and V cache rows at the slot, and nothing else in the caches touched."""
+    from localai_tfp_amd.ops.linear import qmv_fused, qmv_rope_fused
+    Hq, Hkv, D, bs, nb = 8, 2, 128, 16, 8
+    n, k = (Hq + 2 * Hkv) * D, 4096
+    raw, _ = make_w(qt, n, k, seed=11)
+    W = QWeight.from_ggml(raw, qt, n, k, DEV)
+    assert W.to_t32()
+    g = torch.Generator().manual_seed(5)
+    h = torch.randn(1, k, generator=g).to(DEV) * 2
+    nw = (torch.rand(k, generator=g) + 0.5).to(DEV)
+    bq = (torch.randn(n, generator=g) * 0.1).to(DEV) if bias else None
+    pos = torch.tensor([37], dtype=torch.int32, device=DEV)
+    slots = torch.tensor([3 * bs + 5], dtype=torch.int32, device=DEV)
+    inv_freq = (1.0 / (500000.0 ** (torch.arange(0, D, 2).float() / D))).to(DEV)
+    # reference: GEMV to fp32 qkv, then rope_kv
+    qkv = torch.zeros(1, n, device=DEV)
+    assert qmv_fused(W, h, EPI_F32, qkv, norm=nw, eps=1e-5, out_zeroed=True)
+    q_ref = torch.zeros(1, Hq, D, dtype=torch.bfloat16, device=DEV)
+    kc_ref = torch.zeros(nb, Hkv, bs, D, dtype=torch.bfloat16, device=DEV)
+    vc_ref = torch.zeros_like(kc_ref)
+    K.rope_kv(qkv, bq, pos, slots, inv_freq, 1.0, Hq, Hkv, D, D, False, q_ref, kc_ref, vc_ref, bs)
+    # fused, as two parts (q|k and v) like a checkpoint whose attn_v has its own block format
+    q = torch.zeros_like(q_ref)
+    kc = torch.zeros_like(kc_ref)
+    vc = torch.zeros_like(vc_ref)
+    split = (Hq + Hkv) * D
+    for off, rows in ((0, slice(0, split)), (split, slice(split, n))):
+        Wp = QWeight.from_ggml(raw.reshape(n, -1)[rows], qt, rows.stop - rows.start, k, DEV)
+        assert Wp.to_t32()
+        b = bq[rows] if bq is not None else None
+        assert qmv_rope_fused(Wp, h, nw, 1e-5, off, pos, slots, inv_freq, b, 1.0, Hq, Hkv, D, q, kc, vc, bs)
+    assert rel(q.float(), q_ref.float()) < 2e-2
+    assert rel(kc.float(), kc_ref.float()) < 2e-2 and rel(vc.float(), vc_ref.float()) < 2e-2
+    touched = torch.zeros(nb, bs, dtype=torch.bool)
+    touched[3, 5] = True
+    assert float(kc.float().abs().sum(dim=(1, 3)).cpu()[~touched].sum()) == 0.0

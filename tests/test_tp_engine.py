@@ -145,8 +145,8 @@ def test_plan_codec_roundtrip():
     assert all(np.array_equal(a, b) for a, b in zip(out["fix"], plan["fix"]))
     dec_only = decode_plan(encode_plan({"nd": 1, "tokens": np.array([5], np.int32), "positions": np.array([3], np.int32),
                                         "slots": np.array([19], np.int32), "lidx": np.array([0], np.int32),
-                                        "graph": (8, 0, 0)}))
-    assert dec_only["graph"] == (8, 0, 0) and "pf_cu" not in dec_only and "fix" not in dec_only
+                                        "graph": (8, 0, 0, 512)}))
+    assert dec_only["graph"] == (8, 0, 0, 512) and "pf_cu" not in dec_only and "fix" not in dec_only
 
 
 def _die_worker(rank, world, port, who):
