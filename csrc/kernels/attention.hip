@@ -333,17 +333,22 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(KV8 ? 2
     const int kvh = blockIdx.x, b = blockIdx.y, part = blockIdx.z;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int g = lane >> 4, col = lane & 15;
-    const int L = seq_lens[b];
     const int p0 = part * part_size;
+    const int* bt = block_tables + (size_t)b * bt_stride;
+    const int blk0 = p0 / bs;
+    // the partition's block-table entries are requested before (not after) the sequence length: the
+    // table read does not wait for seq_lens, entries past the context are loaded but never used
+    {
+        const int nbt = min(part_size / bs + 1, bt_stride - blk0);
+        for (int i = threadIdx.x; i < nbt; i += 64 * NW) sbt[i] = bt[blk0 + i];
+    }
+    const int L = seq_lens[b];
     const int p1 = min(L, p0 + part_size);
     if (p0 >= L && part > 0) return;  // uniform: graphs launch n_parts for max_model_len
     const int Hq = Hkv * G;
     const int p_start = window > 0 ? max(p0, L - window) : p0;
     const float qs = scale * LOG2E;
     const float sc_l2 = softcap * LOG2E, sc_inv = softcap > 0.f ? 1.f / (softcap * LOG2E) : 0.f;
-    const int* bt = block_tables + (size_t)b * bt_stride;
-    const int blk0 = p0 / bs;
-    const int nblk = p1 > p0 ? (p1 - 1) / bs - blk0 + 1 : 0;
     // Q as the A operand: row = head (lane col), k = dims 32 ks + 8 g — requested before the block-table
     // barrier so its latency overlaps the table read
     bf16x8 qf[D / 32];
@@ -352,7 +357,6 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(KV8 ? 2
         if (col < G) qf[ks] = *(const bf16x8*)(q + (size_t)b * q_stride + (size_t)(kvh * G + col) * D + 32 * ks + 8 * g);
         else qf[ks] = (bf16x8){};
     }
-    for (int i = threadIdx.x; i < nblk; i += 64 * NW) sbt[i] = bt[blk0 + i];
     __syncthreads();
     f32x4 oacc[D / 16];
 #pragma unroll
@@ -485,12 +489,17 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(KV8 ? 2
     __syncthreads();
     float* wo = (float*)(smem + wave * WB);        // [16 rows][D] fp32 (8 KB for D=128 <= WB)
     float* wml = (float*)(smem + NW * WB) + wave * 32;  // [16 rows] m, [16 rows] l
+    // waves past the context's last tile hold nothing (m = -inf, l = 0): neither written nor read
+    const int nwa = p1 > p_start ? min(NW, (p1 - p_start + KT - 1) / KT) : 0;
+    if (wave < nwa) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int r = 4 * g + i;
+        for (int i = 0; i < 4; ++i) {
+            const int r = 4 * g + i;
+            if (r >= G) continue;  // only the G real head rows of the 16-row tile
 #pragma unroll
-        for (int nt = 0; nt < D / 16; ++nt) wo[r * D + 16 * nt + col] = oacc[nt][i];
-        if (col == 0) { wml[r] = mrow[i]; wml[16 + r] = lrow[i]; }
+            for (int nt = 0; nt < D / 16; ++nt) wo[r * D + 16 * nt + col] = oacc[nt][i];
+            if (col == 0) { wml[r] = mrow[i]; wml[16 + r] = lrow[i]; }
+        }
     }
     __syncthreads();
     const float* ml = (const float*)(smem + NW * WB);
@@ -499,11 +508,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(KV8 ? 2
     for (int idx = threadIdx.x; idx < G * D; idx += 64 * NW) {
         const int h = idx / D, d = idx % D;
         float mx = -INFINITY;
-#pragma unroll
-        for (int w = 0; w < NW; ++w) mx = fmaxf(mx, ml[w * 32 + h]);
+        for (int w = 0; w < nwa; ++w) mx = fmaxf(mx, ml[w * 32 + h]);
         float ls = 0.f, os = 0.f;
-#pragma unroll
-        for (int w = 0; w < NW; ++w) {
+        for (int w = 0; w < nwa; ++w) {
             const float a = mx == -INFINITY ? 0.f : exp2f(ml[w * 32 + h] - mx);
             ls += ml[w * 32 + 16 + h] * a;
             os += ((const float*)(smem + w * WB))[h * D + d] * a;
@@ -533,7 +540,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(KV8 ? 2
     __syncthreads();
     if (!s_last) return;
     __threadfence();  // acquire: the other workgroups' partials
-    for (int idx = threadIdx.x; idx < G * D; idx += 256) {
+    for (int idx = threadIdx.x; idx < G * D; idx += 64 * NW) {
         const int h = idx / D, d = idx % D, hq = kvh * G + h;
         const size_t pb = ((size_t)b * Hq + hq) * n_parts;
         float mx = -INFINITY;

@@ -54,6 +54,8 @@ def _gc_cb(phase, info):
         GC_STATS["gc_s"] += dt
         GC_STATS["gc_n"] += 1
         GC_STATS["gc_max_ms"] = max(GC_STATS["gc_max_ms"], dt * 1e3)
+        k = f"gen{info.get('generation', 0)}_max_ms"  # which generation the long pauses come from
+        GC_STATS[k] = max(GC_STATS.get(k, 0.0), dt * 1e3)
 
 
 def gc_tune():
@@ -66,6 +68,8 @@ def gc_tune():
         gc.collect()
         gc.freeze()
         gc.set_threshold(50_000, 50, 1000)
+    for k in [k for k in GC_STATS if k.startswith("gen")]:
+        del GC_STATS[k]
     GC_STATS.update(gc_s=0.0, gc_n=0, gc_max_ms=0.0)
     if _gc_cb not in gc.callbacks:
         gc.callbacks.append(_gc_cb)

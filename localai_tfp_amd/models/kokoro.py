@@ -164,13 +164,46 @@ class Kokoro:
         self.device = torch.device(device)
         self.p = {k: v.to(self.device) for k, v in params.items()}
         self._lstms = {}
+        self._cw = {}  # GPU: packed conv.hip weights per conv name
 
     # ---- building blocks
     def _lin(self, x, name, bias=True):
         return F.linear(x, self.p[name + ".weight"], self.p.get(name + ".bias") if bias else None)
 
-    def _conv(self, x, name, **kw):
-        return F.conv1d(x, self.p[name + ".weight"], self.p.get(name + ".bias"), **kw)
+    def _conv(self, x, name, stride=1, padding=0, dilation=1):
+        """Conv1d [B, C, T] -> [B, Cout, T']: on the GPU the implicit-GEMM conv kernel (conv.hip, f16 operands,
+        fp32 accumulation; ops/conv.py conv1d), elsewhere F.conv1d."""
+        if x.is_cuda:
+            from ..ops import conv as CV
+            cw = self._cw.get(name)
+            if cw is None:
+                cw = self._cw[name] = CV.conv1d_weights(self.p[name + ".weight"], self.p.get(name + ".bias"))
+            return CV.conv1d(x, cw, stride=stride, padding=padding, dilation=dilation)
+        return F.conv1d(x, self.p[name + ".weight"], self.p.get(name + ".bias"), stride=stride, padding=padding,
+                        dilation=dilation)
+
+    def _up_transpose(self, x, name, u, k):
+        """The generator's ConvTranspose1d(k, stride u, padding (k - u) / 2): on the GPU, for the HiFi-GAN geometry
+        k = 2u, as the k = 2 conv producing the u output phases per frame (ops/conv.py conv_transpose1d)."""
+        w, b = self.p[name + ".weight"], self.p.get(name + ".bias")
+        if x.is_cuda and k == 2 * u:
+            from ..ops import conv as CV
+            cwt = self._cw.get(name)
+            if cwt is None:
+                cwt = self._cw[name] = CV.conv_transpose1d_weights(w, b, u)
+            return CV.conv_transpose1d(x, cwt, (k - u) // 2)
+        return F.conv_transpose1d(x, w, b, stride=u, padding=(k - u) // 2)
+
+    @staticmethod
+    def _pool_up2(x, w, b):
+        """Depthwise ConvTranspose1d(k 3, stride 2, padding 1, output_padding 1) [B, C, T] -> [B, C, 2T] as two
+        elementwise phases: y[2i] = w1 x[i], y[2i+1] = w2 x[i] + w0 x[i+1] (no library conv)."""
+        w = w[:, 0]  # [C, 3]
+        nxt = F.pad(x[:, :, 1:], (0, 1))
+        ev = w[:, 1, None] * x
+        od = w[:, 2, None] * x + w[:, 0, None] * nxt
+        y = torch.stack([ev, od], -1).reshape(x.shape[0], x.shape[1], 2 * x.shape[2])
+        return y + b[:, None] if b is not None else y
 
     def _lstm(self, x, name):
         """Bidirectional single-layer LSTM over [1, T, C] -> [1, T, 2H]: on the GPU the cooperative scan kernel
@@ -193,7 +226,11 @@ class Kokoro:
         """AdaIN1d: (1 + gamma) * InstanceNorm(x) + beta, (gamma, beta) = fc(s)."""
         h = self._lin(s, name + ".fc")
         g, b = h.chunk(2, dim=-1)
-        xn = F.instance_norm(x, eps=1e-5)
+        if x.is_cuda:  # InstanceNorm1d as reductions (no library norm kernel)
+            var, mean = torch.var_mean(x, dim=-1, keepdim=True, unbiased=False)
+            xn = (x - mean) * torch.rsqrt(var + 1e-5)
+        else:
+            xn = F.instance_norm(x, eps=1e-5)
         return (1 + g[..., None]) * xn + b[..., None]
 
     def _adain_res_blk(self, x, s, name, upsample: bool):
@@ -201,8 +238,11 @@ class Kokoro:
         h = F.leaky_relu(self._adain(x, s, name + ".norm1"), 0.2)
         if upsample:
             w = self.p[name + ".pool.weight"]
-            h = F.conv_transpose1d(h, w, self.p.get(name + ".pool.bias"), stride=2, padding=1, output_padding=1,
-                                   groups=w.shape[0])
+            if h.is_cuda and w.shape[1:] == (1, 3):
+                h = self._pool_up2(h, w, self.p.get(name + ".pool.bias"))
+            else:
+                h = F.conv_transpose1d(h, w, self.p.get(name + ".pool.bias"), stride=2, padding=1, output_padding=1,
+                                       groups=w.shape[0])
         h = self._conv(h, name + ".conv1", padding=1)
         h = F.leaky_relu(self._adain(h, s, name + ".norm2"), 0.2)
         h = self._conv(h, name + ".conv2", padding=1)
@@ -348,8 +388,7 @@ class Kokoro:
                 xs = self._conv(har, f"decoder.generator.noise_convs.{i}")
                 xs = self._snake_res(xs, s, f"decoder.generator.noise_res.{i}", 11, (1, 3, 5))
             u, k = c.upsample_rates[i], c.upsample_kernels[i]
-            x = F.conv_transpose1d(x, self.p[f"decoder.generator.ups.{i}.weight"],
-                                   self.p[f"decoder.generator.ups.{i}.bias"], stride=u, padding=(k - u) // 2)
+            x = self._up_transpose(x, f"decoder.generator.ups.{i}", u, k)
             if i == nu - 1:
                 x = F.pad(x, (1, 0), mode="reflect")
             x = x + xs

@@ -262,6 +262,8 @@ class VitsModel:
         return self.w.get(k)
 
     def conv(self, x, name, **kw):
+        if x.is_cuda:  # fp32 im2col + library GEMM (the text encoder / flows / duration predictor; no MIOpen)
+            return CV.conv1d_gemm(x, self.w[name + ".weight"], self.w.get(name + ".bias"), **kw)
         return F.conv1d(x, self.w[name + ".weight"], self.w.get(name + ".bias"), **kw)
 
     # ---------------------------------------------------------------- text encoder
@@ -326,8 +328,13 @@ class VitsModel:
         ch = x.shape[1]
         for i in range(c.dds_layers):
             dil = c.dp_kernel ** i
-            h = F.conv1d(x, self.p(f"{pre}convs_dilated.{i}.weight"), self.p(f"{pre}convs_dilated.{i}.bias"),
-                         groups=ch, dilation=dil, padding=(c.dp_kernel * dil - dil) // 2)
+            if x.is_cuda:
+                h = CV.depthwise_conv1d(x, self.p(f"{pre}convs_dilated.{i}.weight"),
+                                        self.p(f"{pre}convs_dilated.{i}.bias"), dilation=dil,
+                                        padding=(c.dp_kernel * dil - dil) // 2)
+            else:
+                h = F.conv1d(x, self.p(f"{pre}convs_dilated.{i}.weight"), self.p(f"{pre}convs_dilated.{i}.bias"),
+                             groups=ch, dilation=dil, padding=(c.dp_kernel * dil - dil) // 2)
             h = F.gelu(F.layer_norm(h.transpose(1, 2), (ch,), self.p(f"{pre}norms_1.{i}.weight"),
                                     self.p(f"{pre}norms_1.{i}.bias"), 1e-5).transpose(1, 2))
             h = self.conv(h, f"{pre}convs_pointwise.{i}")
@@ -472,7 +479,7 @@ class VitsModel:
         tadd = None
         if g is not None and P["cond"] is not None:
             w4, b, _, _ = P["cond"]
-            tadd = F.conv1d(g, w4[:, :, 0].float(), b)[:, :, 0]  # [B, C] per-utterance channel offset
+            tadd = CV.conv1d_gemm(g, w4[:, :, 0].float(), b)[:, :, 0]  # [B, C] per-utterance channel offset
         x = self._c1(z.transpose(1, 2).to(torch.float16).contiguous(), P["pre"], tadd=tadd)
         for i in range(len(P["ups"])):
             x = P["ups"][i](F.leaky_relu(x, c.slope).contiguous())

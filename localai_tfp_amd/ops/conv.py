@@ -172,3 +172,87 @@ def conv2d(x: torch.Tensor, m: torch.nn.Conv2d | None = None, *, weight: torch.T
             int(upsample), ho, wo, N.ptr(b32), N.ptr(ta), ldt, N.ptr(res), co, y.data_ptr(), co,
             _ACT[act], _zero_page(x.device).data_ptr(), int(cfg), N.stream_ptr())
     return out
+
+
+# ---- Conv1d / ConvTranspose1d over [B, C, T] tensors (TTS vocoders, Kokoro) on the same kernel ------------------
+# A Conv1d is the H = 1 case of conv2d: the input goes to [B, T, C] 16-bit rows once, the kernel writes
+# [B, T', Cout] rows, and the result comes back as a [B, Cout, T'] view in the caller's dtype. Weights are
+# packed once per (caller cache, name).
+
+def conv1d_weights(w: torch.Tensor, b: torch.Tensor | None, dtype=torch.float16):
+    """[Cout, Cin, K] weight -> (w4 [Cout, Cin, 1, K], fp32 bias, packed) for :func:`conv1d`."""
+    w4 = w[:, :, None, :].to(dtype).contiguous()
+    return w4, (b.float().contiguous() if b is not None else None), pack_weight(w4, dtype)
+
+
+def conv1d(x: torch.Tensor, cw, stride: int = 1, padding: int = 0, dilation: int = 1, act: str | None = None,
+           pad_r: int | None = None) -> torch.Tensor:
+    """y = act(conv1d(x) + bias); x [B, C, T] any float dtype on the GPU, cw from :func:`conv1d_weights`.
+    Zero padding `padding` on the left and `pad_r` (default the same) on the right."""
+    w4, b32, packed = cw
+    dt = w4.dtype
+    B, C, T = x.shape
+    rows = torch.empty((B, T, C), dtype=dt, device=x.device)
+    rows.copy_(x.transpose(1, 2))
+    pr = padding if pad_r is None else pad_r
+    y = conv2d(rows[:, None].permute(0, 3, 1, 2), weight=w4, bias=b32, stride=stride, pad=(0, padding, 0, pr),
+               dilation=dilation, act=act, packed=packed)  # [B, Cout, 1, T'] channels_last
+    return y[:, :, 0, :].to(x.dtype)
+
+
+def conv_transpose1d_weights(w: torch.Tensor, b: torch.Tensor | None, stride: int, dtype=torch.float16):
+    """ConvTranspose1d weight [Cin, Cout, K = 2 stride] -> the k = 2 conv producing the `stride` output phases
+    of each input frame (W'[(phi, co), ci, 0, tap]: tap 0 sees x[m-1] -> w[ci, co, phi + r], tap 1 sees x[m]
+    -> w[ci, co, phi])."""
+    ci, co, k = w.shape
+    r = stride
+    if k != 2 * r:
+        raise ValueError(f"conv_transpose1d: kernel {k} != 2 x stride {r}")
+    wp = torch.stack([w[:, :, r:].permute(2, 1, 0), w[:, :, :r].permute(2, 1, 0)], -1).reshape(r * co, ci, 1, 2)
+    wp = wp.to(dtype).contiguous()
+    bp = b.float().repeat(r).contiguous() if b is not None else None
+    return wp, bp, pack_weight(wp, dtype), r, co
+
+
+def conv_transpose1d(x: torch.Tensor, cwt, padding: int) -> torch.Tensor:
+    """ConvTranspose1d(k = 2r, stride r, padding p) of x [B, Cin, T] -> [B, Cout, (T - 1) r - 2p + 2r]."""
+    wp, bp, packed, r, co = cwt
+    B, C, T = x.shape
+    rows = torch.empty((B, T, C), dtype=wp.dtype, device=x.device)
+    rows.copy_(x.transpose(1, 2))
+    y = conv2d(rows[:, None].permute(0, 3, 1, 2), weight=wp, bias=bp, stride=1, pad=(0, 1, 0, 1),
+               packed=packed)  # [B, r*co, 1, T+1]: frame m, phase phi
+    y = y.permute(0, 2, 3, 1).reshape(B, (T + 1) * r, co)  # the full output: sample m r + phi
+    # the full (unpadded) transposed conv has (T - 1) r + 2r = (T + 1) r samples; padding p trims p per side
+    return y[:, padding:y.shape[1] - padding].transpose(1, 2).to(x.dtype)
+
+
+def conv1d_gemm(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None = None, stride: int = 1, padding: int = 0,
+                dilation: int = 1) -> torch.Tensor:
+    """Conv1d [B, C, T] -> [B, Cout, T'] in the input's precision as an im2col view + one library GEMM (fp32
+    where 16-bit operands would move a rounding decision, e.g. the VITS duration predictor / flows: no MIOpen)."""
+    B, C, T = x.shape
+    co, ci, k = w.shape
+    xp = F.pad(x, (padding, padding)) if padding else x
+    span = dilation * (k - 1) + 1
+    cols = xp.unfold(2, span, stride)  # [B, C, T', span]
+    if dilation > 1:
+        cols = cols[..., ::dilation]
+    To = cols.shape[2]
+    a = cols.permute(0, 2, 1, 3).reshape(B * To, C * k)  # rows = output positions, (c, tap) columns
+    y = a @ w.reshape(co, ci * k).t()
+    if b is not None:
+        y = y + b
+    return y.view(B, To, co).transpose(1, 2)
+
+
+def depthwise_conv1d(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None = None, padding: int = 0,
+                     dilation: int = 1) -> torch.Tensor:
+    """Depthwise (groups = C) stride-1 Conv1d [B, C, T] -> [B, C, T'] as a per-channel tap sum (fp32, no MIOpen)."""
+    k = w.shape[-1]
+    xp = F.pad(x, (padding, padding)) if padding else x
+    cols = xp.unfold(2, dilation * (k - 1) + 1, 1)
+    if dilation > 1:
+        cols = cols[..., ::dilation]
+    y = (cols * w.reshape(1, -1, 1, k)).sum(-1)
+    return y + b[:, None] if b is not None else y

@@ -133,3 +133,12 @@ def test_kokoro_gpu_matches_cpu():
     ref = torch.randn(1, 2 * c.style, generator=torch.Generator().manual_seed(2))
     wav = gpu.synthesize(toks, ref, seed=1)
     assert np.isfinite(wav).all() and len(wav) > 0
+
+
+def test_kokoro_pool_up2_matches_conv_transpose():
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(1, 6, 11, generator=g)
+    w = torch.randn(6, 1, 3, generator=g)
+    b = torch.randn(6, generator=g)
+    want = torch.nn.functional.conv_transpose1d(x, w, b, stride=2, padding=1, output_padding=1, groups=6)
+    assert torch.allclose(KK.Kokoro._pool_up2(x, w, b), want, atol=1e-6)
