@@ -557,6 +557,9 @@ __device__ unsigned long long g_tk_ts[16];
         ts_[k] = wall_clock64();                                                                         \
     }
 
+// VEC = 4: each thread's values come in float4 loads (1 KB per wave instruction instead of 256 B); value
+// j of the thread is vocabulary entry i0 + VEC (floor(j / VEC) TK_NT + thread) + j % VEC
+template <int VEC>
 __global__ __launch_bounds__(TK_NT) void tk_slice_kernel(const float* __restrict__ logits, int ld, int V,
                                                         const SampleParams* __restrict__ params,
                                                         const uint32_t* __restrict__ allow_mask, int mask_ld,
@@ -576,21 +579,34 @@ __global__ __launch_bounds__(TK_NT) void tk_slice_kernel(const float* __restrict
     const int i0 = sl * TK_SLICE, i1 = min(V, i0 + TK_SLICE);
     float v[TK_NV];
     float mx = -INFINITY;
+    auto gidx = [&](int j) { return i0 + VEC * ((j / VEC) * TK_NT + (int)threadIdx.x) + j % VEC; };
     // branch-free loads (clamped index, masked after): a conditional load per value made the compiler wait
     // for each one before the next (vmcnt(0) per load, ~1 us of HBM latency each)
+    if constexpr (VEC == 4) {  // slice lengths are multiples of 4 here (V % 4 == 0)
 #pragma unroll
-    for (int j = 0; j < TK_NV; ++j) v[j] = __builtin_nontemporal_load(x + min(i0 + j * TK_NT + (int)threadIdx.x, i1 - 1));
+        for (int j = 0; j < TK_NV / 4; ++j) {
+            const f32x4 q = __builtin_nontemporal_load(
+                (const f32x4*)(x + min(i0 + 4 * (j * TK_NT + (int)threadIdx.x), i1 - 4)));
+            v[4 * j] = q[0];
+            v[4 * j + 1] = q[1];
+            v[4 * j + 2] = q[2];
+            v[4 * j + 3] = q[3];
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < TK_NV; ++j) v[j] = __builtin_nontemporal_load(x + min(gidx(j), i1 - 1));
+    }
     if (am) {
         uint32_t w[TK_NV];
 #pragma unroll
-        for (int j = 0; j < TK_NV; ++j) w[j] = am[min(i0 + j * TK_NT + (int)threadIdx.x, i1 - 1) >> 5];
+        for (int j = 0; j < TK_NV; ++j) w[j] = am[min(gidx(j), i1 - 1) >> 5];
 #pragma unroll
         for (int j = 0; j < TK_NV; ++j)
-            if (!((w[j] >> ((i0 + j * TK_NT + threadIdx.x) & 31)) & 1u)) v[j] = -INFINITY;
+            if (!((w[j] >> (gidx(j) & 31)) & 1u)) v[j] = -INFINITY;
     }
 #pragma unroll
     for (int j = 0; j < TK_NV; ++j) {
-        v[j] = i0 + j * TK_NT + (int)threadIdx.x < i1 ? v[j] * itemp : -INFINITY;
+        v[j] = gidx(j) < i1 ? v[j] * itemp : -INFINITY;
         mx = fmaxf(mx, v[j]);
     }
     TK_TS(1)
@@ -646,7 +662,7 @@ __global__ __launch_bounds__(TK_NT) void tk_slice_kernel(const float* __restrict
             for (int j = 0; j < TK_NV; ++j) {
                 if (tk_in(mx, v[j], bA)) {
                     cand_v[base + off] = v[j];
-                    cand_i[base + off] = i0 + j * TK_NT + threadIdx.x;
+                    cand_i[base + off] = gidx(j);
                     ++off;
                 }
             }
@@ -686,7 +702,7 @@ __global__ __launch_bounds__(TK_NT) void tk_slice_kernel(const float* __restrict
             for (int j = 0; j < TK_NV; ++j) {
                 if (tk_in(mx, v[j], b)) {
                     cand_v[base + off] = v[j];
-                    cand_i[base + off] = i0 + j * TK_NT + threadIdx.x;
+                    cand_i[base + off] = gidx(j);
                     ++off;
                 }
             }
@@ -710,7 +726,7 @@ __global__ __launch_bounds__(TK_NT) void tk_slice_kernel(const float* __restrict
             const int k = atomicAdd(&s_n, 1);
             if (k < TK_CAPS) {
                 cand_v[base + k] = v[j];
-                cand_i[base + k] = i0 + j * TK_NT + threadIdx.x;
+                cand_i[base + k] = gidx(j);
             }
         }
     }
@@ -732,12 +748,29 @@ __global__ __launch_bounds__(TK_MNT) void tk_merge_kernel(float* __restrict__ lo
     __shared__ __attribute__((aligned(16))) int hist[TK_NB];
     __shared__ int s_cnt[64], s_keep, s_n, s_ovf, s_b, s_fb;
     __shared__ float s_mx, s_Z;
-    __shared__ float red[2 * TK_MNT / 64], rv[TK_MNT / 64];
+    __shared__ float red[2 * TK_MNT / 64], rv[TK_MNT / 64], rbv[TK_MNT / 64];
     __shared__ int ired[2 * TK_MNT / 64], ri[TK_MNT / 64];
     const int row = blockIdx.x;
     const SampleParams P = params[row];
     const bool greedy = P.temperature <= 0.f;
     const int K = greedy ? 1 : min(P.top_k, TK_CAP);
+    // candidate position t = (slice t / TK_CAPS, entry t % TK_CAPS), valid below that slice's count. The loads
+    // are unconditional (clamped; validity applied once the counts are known) and issued before the count /
+    // max prologue, so the two round trips overlap; positions past S x TK_CAPS are skipped (uniform branch)
+    float v[TK_MV];
+    int id[TK_MV], bin[TK_MV];
+#pragma unroll
+    for (int j = 0; j < TK_MV; ++j) {
+        if (j * TK_MNT < S * TK_CAPS) {
+            const int t = j * TK_MNT + threadIdx.x, s = min(t / TK_CAPS, S - 1), e = t % TK_CAPS;
+            const size_t src = ((size_t)row * S + s) * TK_CAPS + e;
+            v[j] = cand_v[src];
+            id[j] = cand_i[src];
+        } else {
+            v[j] = -INFINITY;
+            id[j] = 0x7fffffff;
+        }
+    }
     if (threadIdx.x < TK_NB) hist[threadIdx.x] = 0;
     if (threadIdx.x < 64) {  // one wave: per-slice counts, overflow flags and the row max (largest slice max)
         const int s = threadIdx.x;
@@ -756,17 +789,6 @@ __global__ __launch_bounds__(TK_MNT) void tk_merge_kernel(float* __restrict__ lo
         return;
     }
     const float mx = s_mx;
-    // candidate position t = (slice t / TK_CAPS, entry t % TK_CAPS): valid below that slice's count
-    float v[TK_MV];
-    int id[TK_MV], bin[TK_MV];
-#pragma unroll
-    for (int j = 0; j < TK_MV; ++j) {
-        // unconditional (clamped) loads, validity applied after: see tk_slice_kernel
-        const int t = j * TK_MNT + threadIdx.x, s = min(t / TK_CAPS, S - 1), e = t % TK_CAPS;
-        const size_t src = ((size_t)row * S + s) * TK_CAPS + e;
-        v[j] = cand_v[src];
-        id[j] = cand_i[src];
-    }
 #pragma unroll
     for (int j = 0; j < TK_MV; ++j) {
         const int t = j * TK_MNT + threadIdx.x, s = t / TK_CAPS, e = t % TK_CAPS;
@@ -845,48 +867,84 @@ __global__ __launch_bounds__(TK_MNT) void tk_merge_kernel(float* __restrict__ lo
         si[r] = ia;
     }
     __syncthreads();
-    if (threadIdx.x == 0) {  // top-K (ties at the K-th value kept), then the bisection chain's semantics
-        int keep = min(K, nk);
-        while (keep < nk && sv[keep] == sv[keep - 1]) ++keep;
-        float zk = 0.f;
-        const bool tp = P.top_p < 1.f && P.top_p > 0.f;
-        if (tp)
-            for (int k = 0; k < keep; ++k) zk += __expf(sv[k] - mx);
-        if (P.min_p > 0.f && P.min_p <= 1.f) {
-            const float mv = mx + __logf(P.min_p);
-            while (keep > 1 && sv[keep - 1] < mv) --keep;
-        }
-        if (tp) {
-            float cum = 0.f;
-            int k = 0;
-            while (k < keep) {
-                cum += __expf(sv[k] - mx);
-                ++k;
-                if (cum >= P.top_p * zk) break;
+    if (threadIdx.x < 64) {  // one wave, 4 sorted entries per lane: top-K (ties at the K-th value kept), then
+        const int lane = threadIdx.x;  // the bisection chain's semantics (min-p, then top-p over the top-K mass)
+        float sv4[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) sv4[i] = sv[4 * lane + i];  // entries >= nk are never used below
+        // first index in [k, lim) whose value differs from sv[k - 1] (sorted: the end of its tie run), else lim
+        auto tie_end = [&](int k, int lim) {
+            if (k <= 0 || k >= lim) return k;
+            const float tv = sv[k - 1];
+            int f = 0x7fffffff;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int idx = 4 * lane + i;
+                if (idx >= k && idx < lim && sv4[i] != tv) f = min(f, idx);
             }
-            while (k < keep && sv[k] == sv[k - 1]) ++k;
-            keep = max(1, k);
+            for (int o = 32; o > 0; o >>= 1) f = min(f, __shfl_xor(f, o, 64));
+            return f == 0x7fffffff ? lim : f;
+        };
+        int keep = tie_end(min(K, nk), nk);
+        const bool tp = P.top_p < 1.f && P.top_p > 0.f;
+        float zk = 0.f;
+        if (tp) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) zk += 4 * lane + i < keep ? __expf(sv4[i] - mx) : 0.f;
+            zk = wave_sum(zk);
         }
-        s_keep = keep;
+        if (P.min_p > 0.f && P.min_p <= 1.f) {  // the values below mx + log(min_p) are a suffix of the kept run
+            const float mv = mx + __logf(P.min_p);
+            int c = 0;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) c += (4 * lane + i < keep && sv4[i] >= mv) ? 1 : 0;
+            keep = max(1, wave_sum_i(c));
+        }
+        if (tp) {  // smallest prefix whose mass reaches top_p x zk: inclusive scan over the lanes' 4-entry sums
+            float e[4], own = 0.f;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                e[i] = 4 * lane + i < keep ? __expf(sv4[i] - mx) : 0.f;
+                own += e[i];
+            }
+            float inc = own;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const float t = __shfl_up(inc, o, 64);
+                if (lane >= o) inc += t;
+            }
+            const float target = P.top_p * zk;
+            float cum = inc - own;
+            int f = 0x7fffffff;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                cum += e[i];
+                if (f == 0x7fffffff && 4 * lane + i < keep && cum >= target) f = 4 * lane + i;
+            }
+            for (int o = 32; o > 0; o >>= 1) f = min(f, __shfl_xor(f, o, 64));
+            const int k = f == 0x7fffffff ? keep : f + 1;
+            keep = max(1, tie_end(k, keep));
+        }
+        if (lane == 0) s_keep = keep;
     }
     __syncthreads();
     const int keep = s_keep;
-    float best = -INFINITY, zk = 0.f;
+    float best = -INFINITY, bv = -INFINITY, zk = 0.f;  // bv: the winner's (scaled) logit, for its log-prob
     int bi = 0x7fffffff;
     for (int k = threadIdx.x; k < keep; k += TK_MNT) {
         const float sc = greedy ? sv[k] : sv[k] + gumbel(P.seed, (uint32_t)si[k]);
         zk += __expf(sv[k] - mx);
-        if (sc > best || (sc == best && si[k] < bi)) { best = sc; bi = si[k]; }
+        if (sc > best || (sc == best && si[k] < bi)) { best = sc; bi = si[k]; bv = sv[k]; }
     }
     zk = wave_sum(zk);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = zk;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
-        const float ob = __shfl_xor(best, o, 64);
+        const float ob = __shfl_xor(best, o, 64), obv = __shfl_xor(bv, o, 64);
         const int oi = __shfl_xor(bi, o, 64);
-        if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+        if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; bv = obv; }
     }
-    if ((threadIdx.x & 63) == 0) { rv[threadIdx.x >> 6] = best; ri[threadIdx.x >> 6] = bi; }
+    if ((threadIdx.x & 63) == 0) { rv[threadIdx.x >> 6] = best; ri[threadIdx.x >> 6] = bi; rbv[threadIdx.x >> 6] = bv; }
     __syncthreads();
     if (out_logp && greedy && threadIdx.x < 64) {  // greedy log-softmax over the whole (allowed) row, from the
         const int s2 = threadIdx.x;                // slices' (max, sum exp); mx is the row max
@@ -895,18 +953,19 @@ __global__ __launch_bounds__(TK_MNT) void tk_merge_kernel(float* __restrict__ lo
         if (s2 == 0) s_Z = Z;  // read below by this same lane
     }
     if (threadIdx.x == 0) {
-        float b = rv[0], z = red[0];
+        float b = rv[0], z = red[0], tv = rbv[0];
         int tok = ri[0];
         for (int w = 1; w < TK_MNT / 64; ++w) {
             z += red[w];
-            if (rv[w] > b || (rv[w] == b && ri[w] < tok)) { b = rv[w]; tok = ri[w]; }
+            if (rv[w] > b || (rv[w] == b && ri[w] < tok)) { b = rv[w]; tok = ri[w]; tv = rbv[w]; }
         }
-        if (tok == 0x7fffffff) tok = 0;
+        if (tok == 0x7fffffff) {  // nothing kept (every value masked): token 0, its logit read back
+            tok = 0;
+            tv = logits[(size_t)row * ld] * (greedy ? 1.f : 1.f / P.temperature);
+        }
         out_tok[row] = tok;
-        if (out_logp) {
-            out_logp[row] = greedy ? logits[(size_t)row * ld + tok] - mx - __logf(fmaxf(s_Z, 1e-30f))
-                                   : logits[(size_t)row * ld + tok] / P.temperature - mx - __logf(fmaxf(z, 1e-30f));
-        }
+        // the winner's value is its logit x 1/T as the slices scaled it: no dependent read of the row
+        if (out_logp) out_logp[row] = tv - mx - __logf(fmaxf(greedy ? s_Z : z, 1e-30f));
     }
 }
 
@@ -921,8 +980,12 @@ extern "C" int mxk_sample_topk_split(float* logits, int ld, int B, int V, const 
     if (B <= 0) return 0;
     if (S != (V + TK_SLICE - 1) / TK_SLICE || S > 64 || S * TK_CAPS > TK_MNT * TK_MV) return (int)hipErrorInvalidValue;
     if (has_pen) tk_penalty_kernel<<<B, TK_NT, 0, st>>>(logits, ld, V, params, pen_tok, pen_cnt, pen_bias, pend_tok);
-    tk_slice_kernel<<<dim3(B, S), TK_NT, 0, st>>>(logits, ld, V, params, allow_mask, mask_ld, cand_v, cand_i, cand_n,
-                                                  slice_z);
+    if (V % 4 == 0 && ld % 4 == 0 && ((uintptr_t)logits & 15) == 0)
+        tk_slice_kernel<4><<<dim3(B, S), TK_NT, 0, st>>>(logits, ld, V, params, allow_mask, mask_ld, cand_v, cand_i,
+                                                         cand_n, slice_z);
+    else
+        tk_slice_kernel<1><<<dim3(B, S), TK_NT, 0, st>>>(logits, ld, V, params, allow_mask, mask_ld, cand_v, cand_i,
+                                                         cand_n, slice_z);
     tk_merge_kernel<<<B, TK_MNT, 0, st>>>(logits, ld, V, params, S, allow_mask, mask_ld, cand_v, cand_i, cand_n, slice_z,
                                           out_tok, out_logp);
     MXK_CHECK_LAUNCH();

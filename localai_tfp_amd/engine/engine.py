@@ -67,7 +67,9 @@ def gc_tune():
     if os.environ.get("MX_GC_TUNE", "1") != "0":
         gc.collect()
         gc.freeze()
-        gc.set_threshold(50_000, 50, 1000)
+        # young collections every ~10k net container allocations: each pause scans at most that many objects
+        # (round 3's 50k threshold gave rare but 10+ ms pauses, host_gc.gc_max_ms)
+        gc.set_threshold(10_000, 10, 1000)
     for k in [k for k in GC_STATS if k.startswith("gen")]:
         del GC_STATS[k]
     GC_STATS.update(gc_s=0.0, gc_n=0, gc_max_ms=0.0)
