@@ -315,12 +315,21 @@ constexpr int dec_wave_lds() { return 32 * D * 2 + 16 * (32 + 8) * 2; }
 
 // NW = 16 (1024 threads, one workgroup per CU): the small-batch form — a 512-key partition per workgroup, so a
 // context of <= 512 keys is ONE partition whose workgroup writes the final output (no reduce work for it).
-template <int D, bool F16, bool KV8, int NW = 4>
+// TS: debug instantiation writing wall-clock stamps of workgroup (0, 0, 0) wave 0 to ts[0..7] (tools/prof_attn_decode.py)
+template <int D, bool F16, bool KV8, int NW = 4, bool TS = false>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(KV8 ? 2 : 4, KV8 ? 2 : 4))) void attn_decode_mfma_kernel(
     const bf16_t* __restrict__ q, int q_stride, const void* __restrict__ kcv, const void* __restrict__ vcv,
     const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ seq_lens, int Hkv, int G, int bs,
     float scale, int window, float softcap, int part_size, int n_parts, bf16_t* __restrict__ out, int out_stride,
-    float2* __restrict__ part_ml, float* __restrict__ part_o, int* __restrict__ part_cnt) {
+    float2* __restrict__ part_ml, float* __restrict__ part_o, int* __restrict__ part_cnt,
+    unsigned long long* __restrict__ ts = nullptr) {
+    const bool ts_on = TS && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0 && threadIdx.x == 0;
+#define DEC_TS(k)                                    \
+    if constexpr (TS) {                              \
+        __builtin_amdgcn_s_waitcnt(0);               \
+        if (ts_on) ts[k] = wall_clock64();           \
+    }
+    DEC_TS(0)
     constexpr int KT = 32;                      // keys per wave tile
     constexpr int VBYTES = KT * D * 2;
     constexpr int PSTRIDE = (KT + 8) * 2;       // bytes per P row (padded)
@@ -345,6 +354,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(KV8 ? 2
     const int L = seq_lens[b];
     const int p1 = min(L, p0 + part_size);
     if (p0 >= L && part > 0) return;  // uniform: graphs launch n_parts for max_model_len
+    DEC_TS(1)
     const int Hq = Hkv * G;
     const int p_start = window > 0 ? max(p0, L - window) : p0;
     const float qs = scale * LOG2E;
@@ -358,6 +368,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(KV8 ? 2
         else qf[ks] = (bf16x8){};
     }
     __syncthreads();
+    DEC_TS(2)
     f32x4 oacc[D / 16];
 #pragma unroll
     for (int i = 0; i < D / 16; ++i) oacc[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
@@ -424,6 +435,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(KV8 ? 2
             for (int ks = 0; ks < D / 32; ++ks)
                 sacc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qf[ks], kf[t][ks], sacc[t], 0, 0, 0);
         }
+        if constexpr (TS) {
+            if (kt0 == p_start) DEC_TS(3)  // the K tile has landed (first tile of wave 0)
+        }
         if constexpr (KV8) {  // V -> this wave's LDS slice (the previous tile's reads have returned)
 #pragma unroll
             for (int j = 0; j < NVC; ++j) {
@@ -486,7 +500,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(KV8 ? 2
         __builtin_amdgcn_wave_barrier();
     }
     // ---- merge the NW waves: (m, l) per row and O rows through the (now free) LDS slices ----
+    DEC_TS(4)
     __syncthreads();
+    DEC_TS(5)
     float* wo = (float*)(smem + wave * WB);        // [16 rows][D] fp32 (8 KB for D=128 <= WB)
     float* wml = (float*)(smem + NW * WB) + wave * 32;  // [16 rows] m, [16 rows] l
     // waves past the context's last tile hold nothing (m = -inf, l = 0): neither written nor read
@@ -502,6 +518,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(KV8 ? 2
         }
     }
     __syncthreads();
+    DEC_TS(6)
     const float* ml = (const float*)(smem + NW * WB);
     // a sequence that fits this one partition: the final output here, no partials (the reduce skips it)
     const bool single = n_parts == 1 || (p0 == 0 && L <= part_size);
@@ -524,6 +541,8 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(KV8 ? 2
             part_o[pi * D + d] = os;
         }
     }
+    DEC_TS(7)
+#undef DEC_TS
     if (single || !part_cnt) return;
     // fused split-K merge: the last of the (b, kvh) partition workgroups to finish merges all of them,
     // instead of a separate reduce launch (at batch 1 that launch costs as much as the attention itself).
@@ -592,6 +611,23 @@ static int launch_decode_mfma(const bf16_t* q, int q_stride, const void* kc, con
             attn_decode_reduce_kernel<F16><<<B * Hkv * G, 128, 0, st>>>(part_ml, part_o, n_parts, Hkv * G, D, seq_lens,
                                                                         part_size, out, out_stride);
     });
+    MXK_CHECK_LAUNCH();
+}
+
+// debug: the 16-wave single-pass decode (bf16 activations and cache, D = 128) with phase stamps of workgroup 0's
+// wave 0 in ts[0..7] (s_memrealtime, 100 MHz): entry, past the seq-len check, block table in LDS, first K tile
+// landed, tiles done, merge barrier 1, merge barrier 2, output stored
+extern "C" int mxk_attn_decode_ts(const bf16_t* q, int q_stride, const void* kc, const void* vc, const int* bt,
+                                  int bt_stride, const int* seq_lens, int B, int Hq, int Hkv, int bs, float scale,
+                                  int part_size, bf16_t* out, int out_stride, unsigned long long* ts, hipStream_t st) {
+    if (Hq % Hkv || Hq / Hkv > 16 || part_size < 512 || bs <= 0 || part_size / bs + 1 > 256)
+        return (int)hipErrorInvalidValue;
+    const size_t lds = 16 * dec_wave_lds<128>() + 16 * 32 * 4;
+    (void)hipFuncSetAttribute((const void*)attn_decode_mfma_kernel<128, false, false, 16, true>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attn_decode_mfma_kernel<128, false, false, 16, true><<<dim3(Hkv, B, 1), 1024, lds, st>>>(
+        q, q_stride, kc, vc, bt, bt_stride, seq_lens, Hkv, Hq / Hkv, bs, scale, 0, 0.f, part_size, 1, out, out_stride,
+        nullptr, nullptr, nullptr, ts);
     MXK_CHECK_LAUNCH();
 }
 

@@ -61,6 +61,7 @@ KERNEL_SIGS = {
     "mxk_rope_kv": [P, P, P, P, P, F, I, I, I, I, I, I, P, P, P, I, P, P, F, I, I, P],
     "mxk_copy_blocks": [P, P, P, I, I, P],
     "mxk_attn_decode": [P, I, P, P, P, I, P, I, I, I, I, I, F, I, F, I, I, P, I, P, P, I, P],
+    "mxk_attn_decode_ts": [P, I, P, P, P, I, P, I, I, I, I, F, I, P, I, P, P],
     "mxk_attn_decode_mfma": [P, I, P, P, P, I, P, I, I, I, I, I, F, I, F, I, I, P, I, P, P, I, P, P],
     "mxk_attn_prefill": [P, P, P, P, I, P, P, I, P, P, I, I, I, I, F, I, F, P, I, I, P],
     "mxk_probe_tr16": [P, P],

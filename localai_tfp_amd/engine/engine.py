@@ -29,7 +29,7 @@ from ..utils.pinned import PinnedRing
 from ..models.llama import ForwardBatch, LlamaModel, Workspace
 from ..ops.sampling import SamplerBatch
 from .kv_cache import KVCache, make_block_manager
-from .scheduler import Scheduler, SchedulerOutput
+from .scheduler import Scheduler, SchedulerOutput, needs_host_state
 from .sequence import Request, Sequence, Status, StepOutput
 
 log = logging.getLogger("localai_tfp_amd.engine")
@@ -401,7 +401,11 @@ class LLMEngine:
                             and getattr(model, "remote", None) is None
                             and os.environ.get("MX_TP_OVERLAP", "1") != "0" if tp is not None else
                             c.overlap and not use_spec and not self.recurrent and getattr(model, "remote", None) is None)
-        self.sched.hold_host_state = self.overlap and os.environ.get("MX_OVERLAP_HOLD", "1") != "0"
+        # rows whose next sample needs host state advanced by their in-flight token (a grammar mask, mirostat-2's
+        # mu): by default they stay in every step — the step's forward is launched first and the previous step is
+        # read while it runs, before the sampler (see _step_overlap). MX_OVERLAP_HOLD=1: such a row sits out
+        # every other step instead (round-3 behaviour, kept for A/B)
+        self.sched.hold_host_state = self.overlap and os.environ.get("MX_OVERLAP_HOLD", "0") == "1"
         self._inflight = collections.deque()  # launched-but-unread steps, oldest first
         self._prev_dev = None  # (device int32 tokens of the last launched step, {rid: row})
         self._pin_tok = self._pin_lp = self._pin_in = None
@@ -622,15 +626,16 @@ class LLMEngine:
         flight (overlap_depth 1: the kernel counts that pending token, ops/sampling.py pack). Mirostat v2
         rows are launched only with their previous token processed (scheduler hold_host_state)."""
         if p.mirostat == 2:
-            return self.sched.hold_host_state
+            return True  # held by the scheduler, or its mu advanced by the late read in _step_overlap
         return self._simple_params(p) or self.cfg.overlap_depth <= 1
 
     def _overlap_row_ok(self, it) -> bool:
         s = it.seq
         if s.req.embedding or not self._overlap_params(s.params):
             return False
-        # grammar rows: the scheduler holds them while a token is in flight, so their mask is current here
-        return s.grammar is None or (self.sched.hold_host_state and not s.n_pending)
+        # grammar rows: held by the scheduler while a token is in flight, or masked after the late read of that
+        # token (_step_overlap), so their mask is current when they are sampled
+        return s.grammar is None or not self.sched.hold_host_state or not s.n_pending
 
     def _overlap_ok(self, so: SchedulerOutput) -> bool:
         if not all(self._overlap_row_ok(it) for it in so.decode):
@@ -641,8 +646,10 @@ class LLMEngine:
         """(histories, pend_tok, pend) for the overlap sampler: full histories only for penalty rows, and the
         index of each row's in-flight previous token in the last launched step's token tensor."""
         params = [it.seq.params for it in items]
-        if all(self._simple_params(p) for p in params) or self._prev_dev is None:
+        if all(self._simple_params(p) for p in params):
             return [[] for _ in items], None, None
+        if self._prev_dev is None:  # nothing in flight: the host histories are complete
+            return [[] if self._simple_params(p) else it.seq.all_ids for it, p in zip(items, params)], None, None
         prev_tok, prev_map = self._prev_dev
         hist, pend = [], []
         for it, p in zip(items, params):
@@ -651,7 +658,8 @@ class LLMEngine:
                 pend.append(-1)
                 continue
             hist.append(it.seq.all_ids)
-            r = prev_map.get(it.seq.rid, -1) if (prev_map is not None and it.seq.n_pending > 0) else -1
+            # n_pending counts this step's sample already (_step_overlap): > 1 = the previous token is in flight
+            r = prev_map.get(it.seq.rid, -1) if (prev_map is not None and it.seq.n_pending > 1) else -1
             pend.append(r)
         return hist, prev_tok, pend
 
@@ -674,14 +682,22 @@ class LLMEngine:
             roctx.push("launch graph" if plan["graph"] else "launch eager")
         logits, am = self._execute(plan)
         tok_dev, lp_dev = None, None
+        steps = [it.seq.n_generated for it in items]  # sampler step index (seed advance) of each row's sample
+        for it in items:  # this step's samples are in flight from here on (their KV blocks must stay)
+            it.seq.n_pending += 1
+        if items and not self.sched.hold_host_state and any(
+                needs_host_state(it.seq) and it.seq.n_pending > 1 for it in items):
+            # a grammar mask / mirostat mu needs the previous step's token: read that step now, while this
+            # step's forward (already queued) keeps the GPU busy, then launch the sampler with current state
+            self._drain_inflight()
         if items:
             if am is not None and self._argmax_only(items):
                 tok_dev = am
             elif not logits.is_cuda:  # CPU reference sampler (host lists)
                 hist, ptok, pend = self._overlap_sample_args(items)
                 mask = self._grammar_mask(items, logits.shape[1]) if any(it.seq.grammar for it in items) else None
-                t, l = self.sampler.sample(logits, [it.seq.params for it in items], hist,
-                                           [it.seq.n_generated for it in items], mask, None, ptok, pend)
+                t, l = self.sampler.sample(logits, [it.seq.params for it in items], hist, steps, mask, None, ptok,
+                                           pend)
                 tok_dev = torch.as_tensor(t, dtype=torch.int32)
                 lp_dev = torch.as_tensor(l, dtype=torch.float32) if l is not None else None
             else:
@@ -689,8 +705,8 @@ class LLMEngine:
                 mask = self._grammar_mask(items, logits.shape[1]) if any(it.seq.grammar for it in items) else None
                 mus = ([it.seq.mirostat_mu for it in items] if any(it.seq.params.mirostat == 2 for it in items)
                        else None)
-                tok_dev, lp_dev = self.sampler.sample(logits, [it.seq.params for it in items], hist,
-                                                      [it.seq.n_generated for it in items], mask, mus, ptok, pend)
+                tok_dev, lp_dev = self.sampler.sample(logits, [it.seq.params for it in items], hist, steps, mask,
+                                                      mus, ptok, pend)
             if self.tp is not None:
                 tok_dev = self._tp_bcast_tokens(tok_dev, len(items))
             k = self._pin_i
@@ -711,8 +727,6 @@ class LLMEngine:
             roctx.pop()
         t2 = time.perf_counter()
         self.sched.commit(so)
-        for it in items:
-            it.seq.n_pending += 1
         if new is not None:
             self._inflight.append(new)
         self._prev_dev = (tok_dev, {it.seq.rid: r for r, it in enumerate(items)}) if items else None
@@ -1101,7 +1115,13 @@ class LLMEngine:
             if g is not None:
                 m[k] = g.allowed_mask(V)
         t = torch.from_numpy(m.view(np.int32))
-        return t.to(self.device) if self.device.type == "cuda" else t
+        if self.device.type != "cuda":
+            return t
+        # through a pinned ring (a pageable H2D copy would make the host wait for the queued forward)
+        ring = getattr(self, "_pin_mask", None)
+        if ring is None:
+            ring = self._pin_mask = PinnedRing(self.pin_ring, m.nbytes, self.device)
+        return ring.stage(m.view(np.int32)).view(len(items), words)
 
     # ------------------------------------------------------------------ post-processing
     def _process(self, so: SchedulerOutput, toks, lps):
