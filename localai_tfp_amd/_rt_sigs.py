@@ -19,6 +19,7 @@ RT_SIGS = {
     "mxrt_vocab_free": (None, [P]),
     "mxrt_vocab_num_nodes": (I, [P]),
     "mxrt_matcher_mask": (None, [P, P, P, C.c_int32]),
+    "mxrt_matcher_mask_batch": (None, [P, C.c_int, P, P, C.c_int64, C.c_int32, C.c_int]),
     # block_manager.cpp
     "mxrt_bm_new": (P, [I, I, I]),
     "mxrt_bm_free": (None, [P]),

@@ -1110,10 +1110,20 @@ class LLMEngine:
     def _grammar_mask(self, items, V):
         words = (V + 31) // 32
         m = np.full((len(items), words), 0xFFFFFFFF, np.uint32)
+        from ..runtime_native import GrammarMatcher
+        batch, rows = [], []
         for k, it in enumerate(items):
             g = it.seq.grammar
-            if g is not None:
+            if g is None:
+                continue
+            nm = g if isinstance(g, GrammarMatcher) else getattr(g, "m", None)  # LazyGrammar: after its trigger
+            if isinstance(nm, GrammarMatcher) and (not batch or (nm.v is batch[0].v and nm.eos == batch[0].eos)):
+                batch.append(nm)
+                rows.append(k)
+            else:
                 m[k] = g.allowed_mask(V)
+        # the native rows together, on several threads (a new grammar state walks the whole vocabulary trie)
+        GrammarMatcher.masks_into(batch, m, rows)
         t = torch.from_numpy(m.view(np.int32))
         if self.device.type != "cuda":
             return t

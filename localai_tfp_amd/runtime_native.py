@@ -2,6 +2,7 @@
 from __future__ import annotations
 
 import ctypes as C
+import os
 
 import numpy as np
 
@@ -155,6 +156,21 @@ class GrammarMatcher:
         m = np.zeros(words, np.uint32)
         _rt().mxrt_matcher_mask(self._h, self.v._h, _ptr(m), self.eos)
         return m
+
+    MASK_THREADS = int(os.environ.get("MX_GRAMMAR_THREADS", "8"))
+
+    @staticmethod
+    def masks_into(matchers: list, out: np.ndarray, rows: list[int]):
+        """Masks of several matchers sharing one vocabulary and EOS id into out[rows[i]] ([R, words] uint32),
+        computed on up to MASK_THREADS threads in one native call (libmxrt mxrt_matcher_mask_batch)."""
+        if not matchers:
+            return
+        m0 = matchers[0]
+        hs = (C.c_void_p * len(matchers))(*[m._h for m in matchers])
+        tmp = np.zeros((len(matchers), out.shape[1]), np.uint32)
+        _rt().mxrt_matcher_mask_batch(hs, len(matchers), m0.v._h, _ptr(tmp), out.shape[1], m0.eos,
+                                      GrammarMatcher.MASK_THREADS)
+        out[rows] = tmp
 
 
 class NativeStore:

@@ -139,3 +139,27 @@ def test_vector_store():
     assert s.get(keys[:1]) == ([], [])
     with pytest.raises(ValueError):
         s.set(np.zeros((1, 4), np.float32), [b"x"])
+
+
+def test_grammar_mask_batch_matches_rows():
+    """mxrt_matcher_mask_batch (rows on several threads, memoised stack-set transitions) gives every row the
+    mask the single-row call gives, along random walks through a JSON grammar over a byte + word vocabulary."""
+    from localai_tfp_amd import functions as F
+    from localai_tfp_amd.runtime_native import GrammarMatcher, NativeGrammar, NativeVocab
+    words = [b"{", b"}", b"[", b"]", b'"', b'":', b", ", b"true", b"null", b"12", b"-3.5", b'"a', b'b"', b"\\n",
+             "é".encode(), "日本".encode(), b"e+", b" ", b"\n"]
+    tb = [bytes([i]) for i in range(256)] + words
+    V = len(tb)
+    vocab = NativeVocab(tb)
+    g = NativeGrammar(F.JSON_BNF)
+    rng = np.random.default_rng(5)
+    ms = [GrammarMatcher(g, vocab, tb, -1) for _ in range(12)]
+    W = (V + 31) // 32
+    for _ in range(25):
+        out = np.zeros((len(ms), W), np.uint32)
+        GrammarMatcher.masks_into(ms, out, list(range(len(ms))))
+        for i, m in enumerate(ms):
+            assert (out[i] == m.allowed_mask(V)).all()
+            allowed = np.flatnonzero(np.unpackbits(out[i].view(np.uint8), bitorder="little")[:V])
+            if len(allowed):
+                assert m.accept(int(rng.choice(allowed)))
