@@ -157,7 +157,9 @@ class GrammarMatcher:
         _rt().mxrt_matcher_mask(self._h, self.v._h, _ptr(m), self.eos)
         return m
 
-    MASK_THREADS = int(os.environ.get("MX_GRAMMAR_THREADS", "8"))
+    # rows of a batched mask computed in parallel (a GPU box's CPU share is 16; os.cpu_count() there reports
+    # the whole machine)
+    MASK_THREADS = int(os.environ.get("MX_GRAMMAR_THREADS", str(min(16, max(2, (os.cpu_count() or 4) // 2)))))
 
     @staticmethod
     def masks_into(matchers: list, out: np.ndarray, rows: list[int]):
