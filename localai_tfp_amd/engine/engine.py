@@ -801,6 +801,9 @@ class LLMEngine:
     # decode-only graphs of fewer than SHORT_CTX_B rows get a second, short-context form (contexts <= SHORT_CTX
     # keys: one 512-key partition per sequence, no partition-merge launch)
     SHORT_CTX, SHORT_CTX_B = 512, 8
+    # large decode-only batches with contexts <= 1024 keys: a graph whose attention is one partition per sequence
+    # (models/llama.py SINGLE_PART_*: no partition-merge launch per layer)
+    SINGLE_PART_CTX, SINGLE_PART_B = 1024, int(os.environ.get("MX_SINGLE_PART_MIN_B", "64"))
 
     def _graph_for(self, n: int) -> StepGraph | None:
         """Decode-only graph of the bucket holding n rows."""
@@ -822,8 +825,12 @@ class LLMEngine:
         if "pf_cu" not in plan:
             if not nd:
                 return None
-            short = B < self.SHORT_CTX_B and int(plan["dec_lens"].max()) <= self.SHORT_CTX
-            return (B, 0, 0, self.SHORT_CTX if short else 0)
+            ml = int(plan["dec_lens"].max())
+            if B < self.SHORT_CTX_B and ml <= self.SHORT_CTX:
+                return (B, 0, 0, self.SHORT_CTX)
+            if B >= self.SINGLE_PART_B and ml <= self.SINGLE_PART_CTX:
+                return (B, 0, 0, self.SINGLE_PART_CTX)
+            return (B, 0, 0, 0)
         if self.recurrent or not hasattr(self.model, "prefill_rows") or len(plan["pf_cu"]) - 1 > c.mixed_graph_seqs:
             return None
         npf = int(plan["pf_cu"][-1])
@@ -935,6 +942,11 @@ class LLMEngine:
         # tensor parallel: a capture runs collectives, so only graphs every rank captured up front
         # (precapture_graphs: decode buckets) are used; single-rank engines capture on first use
         g = self._graph_get(key, create=self.tp is None) if key is not None else None
+        if g is None and key is not None and key[3]:
+            # a short-context form that is not captured (tensor parallel replays precaptured buckets only): the
+            # bucket's full-context graph runs the same step
+            key = (key[0], key[1], key[2], 0)
+            g = self._graph_get(key, create=self.tp is None)
         plan["graph"] = key if g is not None and g.fits(plan) else False
         return plan
 

@@ -178,7 +178,18 @@ class Workspace:
                         self.k8bs[: M * K_ // 16].view(M, K_ // 16))
 
 
+# decode batches of at least this many rows whose contexts are all <= SINGLE_PART_MAX keys run the decode
+# attention as ONE partition per sequence (no partition-merge launch; engine short-context graphs capture it)
+SINGLE_PART_MIN_B = int(__import__("os").environ.get("MX_SINGLE_PART_MIN_B", "64"))
+SINGLE_PART_MAX = 1024
+
+
 class LlamaModel:
+    def _decode_part(self, ws, nd: int, Hq: int, max_len: int) -> int:
+        if max_len and nd >= SINGLE_PART_MIN_B and max_len <= SINGLE_PART_MAX:
+            return max(512, -(-max_len // 16) * 16)
+        return ws.decode_part_size(nd, Hq, max_len or self.cfg.ctx_train)
+
     def __init__(self, cfg: LlamaConfig, device="cpu", tp_rank: int = 0, tp_size: int = 1, tp_group=None):
         self.cfg = cfg
         self.device = torch.device(device)
@@ -618,7 +629,7 @@ class LlamaModel:
                 K.attn_decode(q[:nd].view(nd, Hq, D), kc, vc, fb.dec_block_tables, fb.dec_seq_lens, self.scale,
                               attn[:nd].view(nd, Hq, D), max_seq_len=fb.dec_max_len or None,
                               workspace=(ws.part_ml, ws.part_o, ws.part_cnt), window=L.window, softcap=cfg.attn_softcap,
-                              part_size=ws.decode_part_size(nd, Hq, fb.dec_max_len or cfg.ctx_train))
+                              part_size=self._decode_part(ws, nd, Hq, fb.dec_max_len))
             if T > nd:
                 K.attn_prefill(q[nd:].view(T - nd, Hq, D), kc, vc, fb.pf_block_tables, fb.pf_cu_q, fb.pf_ctx_lens,
                                self.scale, attn[nd:].view(T - nd, Hq, D), fb.pf_q_lens_host, fb.pf_ctx_lens_host,
