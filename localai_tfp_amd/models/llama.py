@@ -717,6 +717,9 @@ class LlamaModel:
             a8 = ws.q8k(S, H)
             K.rmsnorm_q8k(hs, self.out_norm, eps, a8)
             qmatmul8(self.lm_head, a8, EPI_F32, logits)
+        elif S <= GEMV_MAX_M and self.device.type == "cuda" and isinstance(self.lm_head, QWeight) and \
+                qmv_fused(self.lm_head, hs, EPI_F32, logits, norm=self.out_norm, eps=eps):
+            pass  # final RMSNorm + q8 quantisation in the LM-head GEMV prologue (one launch)
         elif S <= GEMV_MAX_M and self.device.type == "cuda" and self.lm_head.is_quant:
             xq, xds = ws.q8(S, H)
             K.rmsnorm(hs, self.out_norm, eps, out_q8=(xq, xds))
