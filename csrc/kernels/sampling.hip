@@ -451,7 +451,16 @@ extern "C" int mxk_sample_params_size() { return (int)sizeof(SampleParams); }
 //     LDS, exact top-K / min-p / top-p truncation, Gumbel-max draw.
 //     A row whose slices overflowed falls back to the full-row bisection chain (sample_row_bisect).
 constexpr int TK_CAP = 64, TK_NT = 256, TK_NV = 32, TK_CAPS = 2 * TK_CAP, TK_MNT = 1024, TK_MV = 8;
-constexpr int TK_SLICE = TK_NT * TK_NV;  // vocabulary entries per slice
+constexpr int TK_SLICE = TK_NT * TK_NV;  // vocabulary entries per slice at the default TK_NV (see tk_nv)
+// values per thread of the slice kernel, chosen at run time (MX_TK_NV = 16 | 32): 32 (8192-entry slices) takes 144
+// VGPRs (3 waves per SIMD), 16 (4096-entry slices, twice the workgroups and merge candidates) 80 VGPRs
+static int tk_nv() {
+    static int nv = [] {
+        const char* e = getenv("MX_TK_NV");
+        return e && atoi(e) == 16 ? 16 : 32;
+    }();
+    return nv;
+}
 constexpr float TK_HR = 48.f;            // values more than this below the slice max are never candidates
 
 MX_DEV uint32_t ord_key(float v) {  // order-preserving float -> uint (NaN / -inf / masked -> 0)
@@ -559,7 +568,7 @@ __device__ unsigned long long g_tk_ts[16];
 
 // VEC = 4: each thread's values come in float4 loads (1 KB per wave instruction instead of 256 B); value
 // j of the thread is vocabulary entry i0 + VEC (floor(j / VEC) TK_NT + thread) + j % VEC
-template <int VEC>
+template <int VEC, bool MASK, int NV>
 __global__ __launch_bounds__(TK_NT) void tk_slice_kernel(const float* __restrict__ logits, int ld, int V,
                                                         const SampleParams* __restrict__ params,
                                                         const uint32_t* __restrict__ allow_mask, int mask_ld,
@@ -574,17 +583,17 @@ __global__ __launch_bounds__(TK_NT) void tk_slice_kernel(const float* __restrict
     const int K = P.temperature <= 0.f ? 1 : min(P.top_k, TK_CAP);
     const float itemp = P.temperature <= 0.f ? 1.f : 1.f / P.temperature;
     const float* x = logits + (size_t)row * ld;
-    const uint32_t* am = allow_mask ? allow_mask + (size_t)row * mask_ld : nullptr;
+    const uint32_t* am = MASK ? allow_mask + (size_t)row * mask_ld : nullptr;
     TK_TS(0)
-    const int i0 = sl * TK_SLICE, i1 = min(V, i0 + TK_SLICE);
-    float v[TK_NV];
+    const int i0 = sl * (NV * TK_NT), i1 = min(V, i0 + NV * TK_NT);
+    float v[NV];
     float mx = -INFINITY;
     auto gidx = [&](int j) { return i0 + VEC * ((j / VEC) * TK_NT + (int)threadIdx.x) + j % VEC; };
     // branch-free loads (clamped index, masked after): a conditional load per value made the compiler wait
     // for each one before the next (vmcnt(0) per load, ~1 us of HBM latency each)
     if constexpr (VEC == 4) {  // slice lengths are multiples of 4 here (V % 4 == 0)
 #pragma unroll
-        for (int j = 0; j < TK_NV / 4; ++j) {
+        for (int j = 0; j < NV / 4; ++j) {
             const f32x4 q = __builtin_nontemporal_load(
                 (const f32x4*)(x + min(i0 + 4 * (j * TK_NT + (int)threadIdx.x), i1 - 4)));
             v[4 * j] = q[0];
@@ -594,18 +603,18 @@ __global__ __launch_bounds__(TK_NT) void tk_slice_kernel(const float* __restrict
         }
     } else {
 #pragma unroll
-        for (int j = 0; j < TK_NV; ++j) v[j] = __builtin_nontemporal_load(x + min(gidx(j), i1 - 1));
+        for (int j = 0; j < NV; ++j) v[j] = __builtin_nontemporal_load(x + min(gidx(j), i1 - 1));
     }
-    if (am) {
-        uint32_t w[TK_NV];
+    if constexpr (MASK) {  // grammar rows (a separate instantiation: the mask words cost registers)
+        uint32_t w[NV];
 #pragma unroll
-        for (int j = 0; j < TK_NV; ++j) w[j] = am[min(gidx(j), i1 - 1) >> 5];
+        for (int j = 0; j < NV; ++j) w[j] = am[min(gidx(j), i1 - 1) >> 5];
 #pragma unroll
-        for (int j = 0; j < TK_NV; ++j)
+        for (int j = 0; j < NV; ++j)
             if (!((w[j] >> (gidx(j) & 31)) & 1u)) v[j] = -INFINITY;
     }
 #pragma unroll
-    for (int j = 0; j < TK_NV; ++j) {
+    for (int j = 0; j < NV; ++j) {
         v[j] = gidx(j) < i1 ? v[j] * itemp : -INFINITY;
         mx = fmaxf(mx, v[j]);
     }
@@ -629,7 +638,7 @@ __global__ __launch_bounds__(TK_NT) void tk_slice_kernel(const float* __restrict
     float zs = 0.f;  // the slice's share of the row's partition function (log-probs of greedy rows only)
     if (P.temperature <= 0.f) {
 #pragma unroll
-        for (int j = 0; j < TK_NV; ++j)
+        for (int j = 0; j < NV; ++j)
             if (v[j] > -INFINITY) zs += __expf(v[j] - mx);
     }
     zs = wave_sum(zs);
@@ -655,11 +664,11 @@ __global__ __launch_bounds__(TK_NT) void tk_slice_kernel(const float* __restrict
     if (bA < TK_NB) {
         int myc = 0;
 #pragma unroll
-        for (int j = 0; j < TK_NV; ++j) myc += tk_in(mx, v[j], bA) ? 1 : 0;
+        for (int j = 0; j < NV; ++j) myc += tk_in(mx, v[j], bA) ? 1 : 0;
         int off = myc ? atomicAdd(&s_n, myc) : 0;
         if (myc && off + myc <= TK_CAPS) {
 #pragma unroll
-            for (int j = 0; j < TK_NV; ++j) {
+            for (int j = 0; j < NV; ++j) {
                 if (tk_in(mx, v[j], bA)) {
                     cand_v[base + off] = v[j];
                     cand_i[base + off] = gidx(j);
@@ -679,7 +688,7 @@ __global__ __launch_bounds__(TK_NT) void tk_slice_kernel(const float* __restrict
         if (threadIdx.x == 0) s_n = 0;
         // pass 2: histogram of the values in bins <= bA, the first bin reaching K
 #pragma unroll
-        for (int j = 0; j < TK_NV; ++j) {  // bins recomputed (not held: 32 more VGPRs would cost occupancy)
+        for (int j = 0; j < NV; ++j) {  // bins recomputed (not held: 32 more VGPRs would cost occupancy)
             const int bj = tk_bin(mx, v[j]);
             if (bj <= bA) atomicAdd(&hist2[bj], 1);
         }
@@ -696,10 +705,10 @@ __global__ __launch_bounds__(TK_NT) void tk_slice_kernel(const float* __restrict
             const int b = s_b;
             myc = 0;
 #pragma unroll
-            for (int j = 0; j < TK_NV; ++j) myc += tk_in(mx, v[j], b) ? 1 : 0;
+            for (int j = 0; j < NV; ++j) myc += tk_in(mx, v[j], b) ? 1 : 0;
             off = myc ? atomicAdd(&s_n, myc) : 0;  // <= TK_CAPS in total by the scan
 #pragma unroll
-            for (int j = 0; j < TK_NV; ++j) {
+            for (int j = 0; j < NV; ++j) {
                 if (tk_in(mx, v[j], b)) {
                     cand_v[base + off] = v[j];
                     cand_i[base + off] = gidx(j);
@@ -717,10 +726,10 @@ __global__ __launch_bounds__(TK_NT) void tk_slice_kernel(const float* __restrict
     // fallback: bisection on the order-preserving key (computed from the values on the fly)
     uint32_t lo = mx > -INFINITY ? ord_key(mx - TK_HR) : 0u;
     const uint32_t hi = mx > -INFINITY ? ord_key(mx) + 1u : 1u;
-    int c_lo = tk_count<TK_NT, TK_NV, float>(v, lo, red, 0);
-    if (c_lo >= K) lo = tk_bisect<TK_NT, TK_NV, float>(v, K, lo, hi, c_lo, TK_CAPS, false, red, 1);
+    int c_lo = tk_count<TK_NT, NV, float>(v, lo, red, 0);
+    if (c_lo >= K) lo = tk_bisect<TK_NT, NV, float>(v, K, lo, hi, c_lo, TK_CAPS, false, red, 1);
 #pragma unroll
-    for (int j = 0; j < TK_NV; ++j) {
+    for (int j = 0; j < NV; ++j) {
         const uint32_t uj = ord_key(v[j]);
         if (uj >= lo && uj != 0u) {
             const int k = atomicAdd(&s_n, 1);
@@ -978,19 +987,36 @@ extern "C" int mxk_sample_topk_split(float* logits, int ld, int B, int V, const 
                                      int* cand_n, float2* slice_z, int* out_tok, float* out_logp, const int* pend_tok,
                                      hipStream_t st) {
     if (B <= 0) return 0;
-    if (S != (V + TK_SLICE - 1) / TK_SLICE || S > 64 || S * TK_CAPS > TK_MNT * TK_MV) return (int)hipErrorInvalidValue;
+    const int slice = tk_nv() * TK_NT;
+    if (S != (V + slice - 1) / slice || S > 64 || S * TK_CAPS > TK_MNT * TK_MV) return (int)hipErrorInvalidValue;
     if (has_pen) tk_penalty_kernel<<<B, TK_NT, 0, st>>>(logits, ld, V, params, pen_tok, pen_cnt, pen_bias, pend_tok);
-    if (V % 4 == 0 && ld % 4 == 0 && ((uintptr_t)logits & 15) == 0)
-        tk_slice_kernel<4><<<dim3(B, S), TK_NT, 0, st>>>(logits, ld, V, params, allow_mask, mask_ld, cand_v, cand_i,
-                                                         cand_n, slice_z);
-    else
-        tk_slice_kernel<1><<<dim3(B, S), TK_NT, 0, st>>>(logits, ld, V, params, allow_mask, mask_ld, cand_v, cand_i,
-                                                         cand_n, slice_z);
+    const bool v4 = V % 4 == 0 && ld % 4 == 0 && ((uintptr_t)logits & 15) == 0;
+#define TK_SLICE_LAUNCH(VEC_, MASK_, NV_)                                                                             \
+    tk_slice_kernel<VEC_, MASK_, NV_><<<dim3(B, S), TK_NT, 0, st>>>(logits, ld, V, params, allow_mask, mask_ld,      \
+                                                                    cand_v, cand_i, cand_n, slice_z)
+    if (tk_nv() == 16) {
+        if (allow_mask) {
+            if (v4) TK_SLICE_LAUNCH(4, true, 16);
+            else TK_SLICE_LAUNCH(1, true, 16);
+        } else {
+            if (v4) TK_SLICE_LAUNCH(4, false, 16);
+            else TK_SLICE_LAUNCH(1, false, 16);
+        }
+    } else {
+        if (allow_mask) {
+            if (v4) TK_SLICE_LAUNCH(4, true, 32);
+            else TK_SLICE_LAUNCH(1, true, 32);
+        } else {
+            if (v4) TK_SLICE_LAUNCH(4, false, 32);
+            else TK_SLICE_LAUNCH(1, false, 32);
+        }
+    }
+#undef TK_SLICE_LAUNCH
     tk_merge_kernel<<<B, TK_MNT, 0, st>>>(logits, ld, V, params, S, allow_mask, mask_ld, cand_v, cand_i, cand_n, slice_z,
                                           out_tok, out_logp);
     MXK_CHECK_LAUNCH();
 }
-extern "C" int mxk_sample_topk_slice() { return TK_SLICE; }
+extern "C" int mxk_sample_topk_slice() { return tk_nv() * TK_NT; }
 // debug: enable / read the per-phase wall-clock stamps of tk_slice_kernel's workgroup (0, 0) (100 MHz ticks)
 extern "C" int mxk_sample_trace(int on, unsigned long long* out16) {
     if (out16) return (int)hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_tk_ts), sizeof(unsigned long long) * 16);

@@ -184,7 +184,7 @@ class SamplerBatch:
     # rows all have top-k on (the reference default, top_k 40) or are greedy; MX_SPLIT_SAMPLER_MAX_B caps it
     SPLIT_MAX_B = int(__import__("os").environ.get("MX_SPLIT_SAMPLER_MAX_B", str(1 << 20)))
     TOPK_CAP = 64
-    SLICE = 8192   # vocabulary entries per slice (sampling.hip TK_SLICE, checked against the library on first use)
+    SLICE = 8192   # vocabulary entries per slice (sampling.hip tk_nv() x 256, read from the library on first use)
     CAPS = 128     # candidates per slice (TK_CAPS)
 
     def _split_slices(self, params, B: int, V: int = 128256) -> int:
@@ -193,9 +193,10 @@ class SamplerBatch:
         if B > self.SPLIT_MAX_B:
             return 0
         if not getattr(self, "_slice_checked", False) and N.have_kernels():
-            got = N.kernels().mxk_sample_topk_slice()
-            if got != self.SLICE:
-                raise N.NativeError(f"split sampler slice mismatch: library {got}, Python {self.SLICE}")
+            got = N.kernels().mxk_sample_topk_slice()  # MX_TK_NV selects 4096- or 8192-entry slices
+            if got not in (4096, 8192):
+                raise N.NativeError(f"split sampler: unexpected slice size {got} from the library")
+            self.SLICE = got
             self._slice_checked = True
         S = -(-V // self.SLICE)
         if S > 64:
