@@ -522,16 +522,26 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(KV8 ? 2
     const float* ml = (const float*)(smem + NW * WB);
     // a sequence that fits this one partition: the final output here, no partials (the reduce skips it)
     const bool single = n_parts == 1 || (p0 == 0 && L <= part_size);
+    // per head row: the waves' merge weights exp2(m_w - mx) and the row's (mx, l) — once per row in 16-lane
+    // groups, not once per output element (the output loop below is then one FMA per wave)
+    __shared__ float s_wt[16 * 16];
+    __shared__ float2 s_rml[16];
+    if (threadIdx.x < G * 16) {  // whole 16-lane groups (G * 16 is a multiple of 16)
+        const int h = threadIdx.x >> 4, w = threadIdx.x & 15;
+        const float m = w < nwa ? ml[w * 32 + h] : -INFINITY;
+        const float mx = group_max<16>(m);
+        const float a = (w < nwa && mx != -INFINITY) ? exp2f(m - mx) : 0.f;
+        const float ls = group_sum<16>(w < nwa ? ml[w * 32 + 16 + h] * a : 0.f);
+        s_wt[threadIdx.x] = a;
+        if (w == 0) s_rml[h] = make_float2(mx, ls);
+    }
+    __syncthreads();
     for (int idx = threadIdx.x; idx < G * D; idx += 64 * NW) {
         const int h = idx / D, d = idx % D;
-        float mx = -INFINITY;
-        for (int w = 0; w < nwa; ++w) mx = fmaxf(mx, ml[w * 32 + h]);
-        float ls = 0.f, os = 0.f;
-        for (int w = 0; w < nwa; ++w) {
-            const float a = mx == -INFINITY ? 0.f : exp2f(ml[w * 32 + h] - mx);
-            ls += ml[w * 32 + 16 + h] * a;
-            os += ((const float*)(smem + w * WB))[h * D + d] * a;
-        }
+        const float mx = s_rml[h].x, ls = s_rml[h].y;
+        float os = 0.f;
+#pragma unroll 4
+        for (int w = 0; w < nwa; ++w) os += ((const float*)(smem + w * WB))[h * D + d] * s_wt[h * 16 + w];
         const int hq = kvh * G + h;
         if (single) {
             out[(size_t)b * out_stride + (size_t)hq * D + d] = f32_to_act<F16>(ls > 0.f ? os / ls : 0.f);
