@@ -69,7 +69,7 @@ def gc_tune():
         gc.freeze()
         # young collections every ~10k net container allocations: each pause scans at most that many objects
         # (round 3's 50k threshold gave rare but 10+ ms pauses, host_gc.gc_max_ms)
-        gc.set_threshold(10_000, 10, 1000)
+        gc.set_threshold(10_000, 5, 1000)
     for k in [k for k in GC_STATS if k.startswith("gen")]:
         del GC_STATS[k]
     GC_STATS.update(gc_s=0.0, gc_n=0, gc_max_ms=0.0)
