@@ -129,18 +129,8 @@ __global__ __launch_bounds__(256) void rope_kv4_kernel(float* __restrict__ qkv, 
     const int hpg = (nh + gridDim.y - 1) / gridDim.y, vpg = (Hkv + gridDim.y - 1) / gridDim.y;
     const int h_lo = blockIdx.y * hpg, h_hi = min(nh, h_lo + hpg);
     const int v_lo = blockIdx.y * vpg, v_hi = min(Hkv, v_lo + vpg);
-    const int p = pos[t];
-    for (int i = threadIdx.x; i < HALF; i += 256) {
-        float sv, cv;
-        sincosf((float)p * inv_freq[i], &sv, &cv);
-        cs[i] = cv * attn_factor;
-        sn[i] = sv * attn_factor;
-    }
-    __syncthreads();
     const int W = (Hq + 2 * Hkv) * D;
     float* row = qkv + (size_t)t * W;
-    const int slot = slots[t];
-    const int blk = slot >= 0 ? slot / block_size : 0, off = slot >= 0 ? slot % block_size : 0;
     auto ld4 = [&](int e) {
         float4 x = *(const float4*)(row + e);
         if (HAS_BIAS) {
@@ -149,6 +139,25 @@ __global__ __launch_bounds__(256) void rope_kv4_kernel(float* __restrict__ qkv, 
         }
         return x;
     };
+    const int total = (h_hi - h_lo) << USH;
+    // the first unit's row elements are requested before the rotation table is built: their latency overlaps the
+    // sincosf work and the table barrier
+    float4 a0 = {0.f, 0.f, 0.f, 0.f}, b0 = {0.f, 0.f, 0.f, 0.f};
+    if (threadIdx.x < total) {
+        const int h = h_lo + (threadIdx.x >> USH), u = threadIdx.x & (UPH - 1);
+        a0 = ld4(h * D + 4 * u);
+        if constexpr (NEOX) b0 = ld4(h * D + 4 * u + HALF);
+    }
+    const int p = pos[t];
+    for (int i = threadIdx.x; i < HALF; i += 256) {
+        float sv, cv;
+        sincosf((float)p * inv_freq[i], &sv, &cv);
+        cs[i] = cv * attn_factor;
+        sn[i] = sv * attn_factor;
+    }
+    __syncthreads();
+    const int slot = slots[t];
+    const int blk = slot >= 0 ? slot / block_size : 0, off = slot >= 0 ? slot % block_size : 0;
     auto st4 = [&](int h, int d, float4 y) {
         if (h < Hq) {
             uint2 o = {pack_bf16x2(y.x, y.y), pack_bf16x2(y.z, y.w)};
@@ -164,12 +173,14 @@ __global__ __launch_bounds__(256) void rope_kv4_kernel(float* __restrict__ qkv, 
             }
         }
     };
-    const int total = (h_hi - h_lo) << USH;
+    const float4 z4 = {0.f, 0.f, 0.f, 0.f};
+    // ZERO: every element is read by exactly one thread, which zeroes it after use (the next layer's split GEMM
+    // accumulates into the buffer) — no block barrier, no wait for the other threads' stores
     for (int idx = threadIdx.x; idx < total; idx += 256) {
         const int h = h_lo + (idx >> USH), u = idx & (UPH - 1);
         if constexpr (NEOX) {
             const int d = 4 * u;  // dims d..d+3 and their partners d+HALF..
-            const float4 a = ld4(h * D + d), b = ld4(h * D + d + HALF);
+            const float4 a = idx == threadIdx.x ? a0 : ld4(h * D + d), b = idx == threadIdx.x ? b0 : ld4(h * D + d + HALF);
             float4 ya, yb;
             ya.x = a.x * cs[d] - b.x * sn[d];         yb.x = b.x * cs[d] + a.x * sn[d];
             ya.y = a.y * cs[d + 1] - b.y * sn[d + 1]; yb.y = b.y * cs[d + 1] + a.y * sn[d + 1];
@@ -177,21 +188,26 @@ __global__ __launch_bounds__(256) void rope_kv4_kernel(float* __restrict__ qkv, 
             ya.w = a.w * cs[d + 3] - b.w * sn[d + 3]; yb.w = b.w * cs[d + 3] + a.w * sn[d + 3];
             st4(h, d, ya);
             st4(h, d + HALF, yb);
+            if constexpr (ZERO) {
+                *(float4*)(row + h * D + d) = z4;
+                *(float4*)(row + h * D + d + HALF) = z4;
+            }
         } else {
             const int d = 4 * u, f = 2 * u;  // pairs (d, d+1) and (d+2, d+3): frequencies f, f+1
-            const float4 x = ld4(h * D + d);
+            const float4 x = idx == threadIdx.x ? a0 : ld4(h * D + d);
             float4 y;
             y.x = x.x * cs[f] - x.y * sn[f];
             y.y = x.y * cs[f] + x.x * sn[f];
             y.z = x.z * cs[f + 1] - x.w * sn[f + 1];
             y.w = x.w * cs[f + 1] + x.z * sn[f + 1];
             st4(h, d, y);
+            if constexpr (ZERO) *(float4*)(row + h * D + d) = z4;
         }
     }
     float* vr = row + (Hq + Hkv) * D;
-    if (slot >= 0) {
-        for (int idx = v_lo * (D / 4) + threadIdx.x; idx < v_hi * (D / 4); idx += 256) {
-            const int kh = idx / (D / 4), d = (idx % (D / 4)) * 4;
+    for (int idx = v_lo * (D / 4) + threadIdx.x; idx < v_hi * (D / 4); idx += 256) {
+        const int kh = idx / (D / 4), d = (idx % (D / 4)) * 4;
+        if (slot >= 0) {
             float4 v = *(const float4*)(vr + kh * D + d);
             if (HAS_BIAS) {
                 const float4 b = *(const float4*)(bias + (Hq + Hkv) * D + kh * D + d);
@@ -206,12 +222,7 @@ __global__ __launch_bounds__(256) void rope_kv4_kernel(float* __restrict__ qkv, 
                 *(uint2*)((bf16_t*)vc + e) = o;
             }
         }
-    }
-    if constexpr (ZERO) {
-        __syncthreads();
-        const float4 z = {0.f, 0.f, 0.f, 0.f};
-        for (int idx = h_lo * (D / 4) + threadIdx.x; idx < h_hi * (D / 4); idx += 256) *(float4*)(row + 4 * idx) = z;
-        for (int idx = v_lo * (D / 4) + threadIdx.x; idx < v_hi * (D / 4); idx += 256) *(float4*)(vr + 4 * idx) = z;
+        if constexpr (ZERO) *(float4*)(vr + kh * D + d) = z4;
     }
 }
 
