@@ -165,14 +165,20 @@ struct TUnit<MXQ_Q6_K> {
         for (int jq = 0; jq < 4; ++jq) {
             const u32x4 xl = *(const u32x4*)(x + 64 * jq + 16 * h);
             const u32x4 xh = *(const u32x4*)(x + 64 * jq + 32 + 16 * h);
-            int il = 0, ih = 0;
+            // the 6-bit codes (0..63) are non-negative int8 as they are: sum(q x) by sdot4 directly, and the -32
+            // offset as -32 sum(x) (one more sdot4 against 0x01 per word) instead of re-biasing every code byte
+            int il = 0, ih = 0, sl = 0, sh = 0;
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 const uint32_t lo = (ql[jq][i] & 0x0F0F0F0Fu) | (((qh[jq][i] >> (2 * h)) & 0x03030303u) << 4);
                 const uint32_t hi = ((ql[jq][i] >> 4) & 0x0F0F0F0Fu) | (((qh[jq][i] >> (2 * (2 + h))) & 0x03030303u) << 4);
-                il = __builtin_amdgcn_sdot4((int)q6_bias_bytes(lo), (int)xl[i], il, false);
-                ih = __builtin_amdgcn_sdot4((int)q6_bias_bytes(hi), (int)xh[i], ih, false);
+                il = __builtin_amdgcn_sdot4((int)lo, (int)xl[i], il, false);
+                ih = __builtin_amdgcn_sdot4((int)hi, (int)xh[i], ih, false);
+                sl = __builtin_amdgcn_sdot4(0x01010101, (int)xl[i], sl, false);
+                sh = __builtin_amdgcn_sdot4(0x01010101, (int)xh[i], sh, false);
             }
+            il -= 32 * sl;
+            ih -= 32 * sh;
             const int s_lo = (int8_t)((sc[jq] >> (8 * h)) & 0xFF), s_hi = (int8_t)((sc[jq] >> (8 * (2 + h))) & 0xFF);
             acc += (float)s_lo * ds[2 * jq].x * (float)il + (float)s_hi * ds[2 * jq + 1].x * (float)ih;
         }
