@@ -211,14 +211,16 @@ struct TUnit<MXQ_Q3_K> {
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const u32x4 xv = *(const u32x4*)(x + 128 * n + 32 * j + 16 * h);
-                int is = 0;
+                // 3-bit codes 0..7 straight into sdot4 (non-negative int8); the -4 offset as -4 sum(x) by one more
+                // sdot4 against 0x01 per word instead of sign-extending every code byte
+                int is = 0, sx = 0;
 #pragma unroll
                 for (int w = 0; w < 4; ++w) {
-                    uint32_t c = ((q[n][w] >> (2 * j)) & 0x03030303u) | (((hm[w] >> (4 * n + j)) & 0x01010101u) << 2);
-                    c ^= 0x04040404u;                  // c - 4 as a 3-bit two's complement field
-                    c |= (c & 0x04040404u) * 62u;      // sign-extend bit 2 to the byte (no carry across bytes)
+                    const uint32_t c = ((q[n][w] >> (2 * j)) & 0x03030303u) | (((hm[w] >> (4 * n + j)) & 0x01010101u) << 2);
                     is = __builtin_amdgcn_sdot4((int)c, (int)xv[w], is, false);
+                    sx = __builtin_amdgcn_sdot4(0x01010101, (int)xv[w], sx, false);
                 }
+                is -= 4 * sx;
                 const int isx = 8 * n + 2 * j + h;
                 const int sc = (int)((sw[isx >> 2] >> (8 * (isx & 3))) & 0xFF) - 32;
                 acc += (float)sc * ds[4 * n + j].x * (float)is;
