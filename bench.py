@@ -3,7 +3,10 @@
 Q4_K_M, one serving replica per GPU (BASELINE.json config #2; N GPUs = N data-parallel replicas).
 
 Contract (driver): `python bench.py --gpus N --steps K --warmup W`; for N > 1 it is launched with
-torch.distributed.run, one rank per GPU (RCCL). Each rank:
+torch.distributed.run, one rank per GPU (RCCL) — or, called without a torchrun environment, bench.py starts
+torch.distributed.run itself as a child process with N ranks (spawn_ranks). Every rank checks world == N.
+BASELINE config #3 (Llama-3-70B Q4_K_M, TP=8 over xGMI): `python bench.py --gpus 8 --tp 8 --model llama3-70b`.
+Each rank:
   * builds a random-init Llama-3-8B with the exact Q4_K_M tensor types of a real checkpoint
     (models/synthetic.py; no network for weights) and its LLM engine (paged KV, continuous batching,
     hipGraph decode) inside an LLM gRPC worker (workers/llm.py, grpc.aio server) in this process;
@@ -168,9 +171,28 @@ def wait_http(url: str, timeout: float, proc=None):
     raise TimeoutError(url)
 
 
+def spawn_ranks(args) -> int | None:
+    """`--gpus N` (N > 1) without a torchrun environment: start N ranks as CHILD processes of
+    torch.distributed.run (never exec: this process has not touched the GPU, but the children will), pass the
+    rank-0 JSON line through (inherited stdout) and return their exit code. None: already a rank / one GPU."""
+    if args.gpus <= 1 or "WORLD_SIZE" in os.environ:
+        return None
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(args.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.abspath(__file__), *sys.argv[1:]]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC (RCCL / CUDA-tensor sharing across ranks)
+    p = subprocess.run(cmd, env=env)
+    return p.returncode
+
+
 def main():
     args = parse()
+    rc = spawn_ranks(args)
+    if rc is not None:
+        sys.exit(rc)
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the torchrun world has {world} ranks")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
@@ -296,7 +318,8 @@ def main():
                 **({"tp_selfcheck_rel_err": tp_rel} if tp_rel is not None else {}),
                 "path": ("HTTP /v1/chat/completions (SSE) -> FastAPI gateway -> mxstream (batched gRPC-side channel) -> LLM worker engine" if args.path == "http"
                          else "engine in-process (gateway/gRPC excluded)"),
-                "load_s": round(t_load, 1), "graph_capture_s": round(t_capture, 1), "graphs": n_graphs,
+                "load_s": round(t_load, 1), "gemm_tune_s": round(getattr(eng, "stats_tune_s", 0.0), 1),
+                "graph_capture_s": round(t_capture, 1), "graphs": n_graphs,
                 "graph_steps": st["graph_steps"], "total_steps": st["steps"],
                 "host_ms_per_step": {k[:-2]: round(st[k] / max(1, st["steps"]) * 1e3, 3)
                                      for k in ("sched_s", "plan_s", "fwd_s", "wait_s", "process_s")},

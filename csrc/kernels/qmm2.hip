@@ -163,6 +163,9 @@ __global__ __launch_bounds__(256 * KS) void qmm2_kernel(const uint16_t* __restri
                             __builtin_amdgcn_global_load_lds((const void*)(u + 512 + lane * 4), (MX_LDS void*)(hd + 512), 4,
                                                              0, 0);
                     }
+                    if constexpr (QT == MXQ_Q5_K)  // + the qh chunks (fifth bits of the whole super-block)
+                        __builtin_amdgcn_global_load_lds((const void*)(u + F::QH + lane * 16), (MX_LDS void*)(hd + 512), 16,
+                                                         0, 0);
                 }
             }
         }
@@ -466,7 +469,7 @@ extern "C" int mxk_qmm2_dbg(int dbg, int wm, int ks, int wn, const uint16_t* A, 
     return (int)hipErrorInvalidValue;
 }
 
-// A f16 [M, K] (lda % 8 == 0, 16-B aligned), W t32 Q4_K / Q6_K / Q3_K / Q2_K [N, K] (N % 32 == 0, K % 256 == 0).
+// A f16 [M, K] (lda % 8 == 0, 16-B aligned), W t32 Q4_K / Q5_K / Q6_K / Q3_K / Q2_K [N, K] (N % 32 == 0, K % 256 == 0).
 // epi: 0 fp32 store, 1 f16 store, 2 fp32 accumulate (split-K via atomics when splits > 1), 3/4 SwiGLU /
 // GeGLU over 16-row interleaved gate|up -> f16 [M, N/2]. wm: 32-row MFMA blocks per wave; wn: 32-column groups
 // per wave (BM = 32 wm wn); ks: 1 (4 waves) or 2 (8 waves, k-steps split per wave pair). splits: K split in
@@ -489,6 +492,7 @@ extern "C" int mxk_qmm2(int qtype, int epi, int wm, int ks, int wn, const uint16
         case MXQ_Q6_K: Q2_EPI(MXQ_Q6_K) break;
         case MXQ_Q3_K: Q2_EPI(MXQ_Q3_K) break;
         case MXQ_Q2_K: Q2_EPI(MXQ_Q2_K) break;
+        case MXQ_Q5_K: Q2_EPI(MXQ_Q5_K) break;
     }
 #undef Q2_EPI
     return (int)hipErrorInvalidValue;

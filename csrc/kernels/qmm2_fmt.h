@@ -22,6 +22,14 @@ struct Q2F<MXQ_Q4_K> {
     static constexpr int UNIT = 4608, HB = 512, QB = 1024, QI = 1, HI = 1;
     static constexpr int qoff(int jq) { return 512 + jq * 1024; }
 };
+// Q5_K t32 unit: [hdr 32 x 16 B][qs as Q4_K: quarter jq = chunk0, chunk1][qh: 2 chunks x 32 x 16 B]; the header
+// slot holds hdr + qh (the fifth bit of all four k-tiles, staged once per super-block: qoff(4) = 4608)
+template <>
+struct Q2F<MXQ_Q5_K> {
+    static constexpr int UNIT = 5632, HB = 1536, QB = 1024, QI = 1, HI = 2;
+    static constexpr int qoff(int jq) { return 512 + jq * 1024; }
+    static constexpr int QH = 4608;  // unit offset of the qh chunks
+};
 // Q6_K t32 unit: [sc 32 x 16 B][d 32 x 4 B][quarter jq: ql0, ql1, qh (32 x 16 B)]
 template <>
 struct Q2F<MXQ_Q6_K> {
@@ -74,6 +82,58 @@ struct Q2B<MXQ_Q4_K> {
         const u32x2 src = (S & 1) ? v1 : v0;
         constexpr int sh = 4 * (S >> 1);
         const uint32_t t0 = (src[0] >> sh) & 0x0F0F0F0Fu, t1 = (src[1] >> sh) & 0x0F0F0F0Fu;
+        const f16x2 k = {(_Float16)1024.f, (_Float16)1024.f};
+        const f16x2 s2 = {sm[S >> 1][0], sm[S >> 1][0]}, m2 = {sm[S >> 1][1], sm[S >> 1][1]};
+        f16x2 p[4];
+        magic4(t0, p[0], p[1]);
+        magic4(t1, p[2], p[3]);
+        f16x8 r;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const f16x2 v = (p[i] - k) * s2 + m2;
+            r[2 * i] = v[0];
+            r[2 * i + 1] = v[1];
+        }
+        return r;
+    }
+};
+
+// Q5_K: Q4_K's nibbles plus the fifth bit: qh byte l (l = 16 (S & 1) + 8 h + i, this lane's k) bit 2 JQ + (S >> 1)
+template <>
+struct Q2B<MXQ_Q5_K> {
+    u32x4 hd;
+    u32x2 qh0, qh1;  // qh bytes 8 h .. 8 h + 7 of chunks 0 / 1
+    u32x2 v0, v1;
+    f16x2 sm[2];
+    MX_DEV void load_hdr(const char* hb, int col, int h) {
+        hd = *(const u32x4*)(hb + col * 16);
+        qh0 = *(const u32x2*)(hb + 512 + col * 16 + 8 * h);
+        qh1 = *(const u32x2*)(hb + 1024 + col * 16 + 8 * h);
+    }
+    MX_DEV void load_q(const char* qb, int col, int h) {
+        v0 = *(const u32x2*)(qb + col * 16 + 8 * h);
+        v1 = *(const u32x2*)(qb + 512 + col * 16 + 8 * h);
+    }
+    template <int JQ>
+    MX_DEV void prep() {
+        const uint32_t w0 = hd[0];
+        const f16x2 dd = __builtin_bit_cast(f16x2, w0);
+        const f16x2 dn = {dd[0], -dd[1]};
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            int sc, mn;
+            q4k_scale_min_w(hd[1], hd[2], hd[3], 2 * JQ + i, sc, mn);
+            const f16x2 q = {(_Float16)sc, (_Float16)mn};
+            sm[i] = dn * q;  // exact f16 products (11 x 6 bits)
+        }
+    }
+    template <int JQ, int S>
+    MX_DEV f16x8 frag() const {
+        const u32x2 src = (S & 1) ? v1 : v0;
+        const u32x2 qh = (S & 1) ? qh1 : qh0;
+        constexpr int sh = 4 * (S >> 1), hb = 2 * JQ + (S >> 1);
+        const uint32_t t0 = ((src[0] >> sh) & 0x0F0F0F0Fu) | (((qh[0] >> hb) & 0x01010101u) << 4);
+        const uint32_t t1 = ((src[1] >> sh) & 0x0F0F0F0Fu) | (((qh[1] >> hb) & 0x01010101u) << 4);
         const f16x2 k = {(_Float16)1024.f, (_Float16)1024.f};
         const f16x2 s2 = {sm[S >> 1][0], sm[S >> 1][0]}, m2 = {sm[S >> 1][1], sm[S >> 1][1]};
         f16x2 p[4];

@@ -1,6 +1,6 @@
 // qmm3.hip — warp-specialised quantised-weight GEMM (M >= 64: continuous-batching steps, prefill).
 //
-//   C[M, N] (+)= A[M, K] · W[N, K]^T,   A f16, W Q4_K / Q6_K / Q3_K / Q2_K in the t32 tiled layout
+//   C[M, N] (+)= A[M, K] · W[N, K]^T,   A f16, W Q4_K / Q5_K / Q6_K / Q3_K / Q2_K in the t32 tiled layout
 //
 // Why a third kernel: qmm2.hip's isolation builds (profiles/r4_qmm2_isolation.md) showed its one-wave-per-SIMD
 // instruction stream almost serial: gate_up M = 256 took 88 us, 50 us of it without any MFMA and ~36 us of
@@ -124,6 +124,9 @@ __global__ __launch_bounds__(512) void qmm3_kernel(const uint16_t* __restrict__ 
                             __builtin_amdgcn_global_load_lds((const void*)(u + 512 + lane * 4), (MX_LDS void*)(hd + 512), 4,
                                                              0, 0);
                     }
+                    if constexpr (QT == MXQ_Q5_K)  // + the qh chunks (fifth bits of the whole super-block)
+                        __builtin_amdgcn_global_load_lds((const void*)(u + F::QH + lane * 16), (MX_LDS void*)(hd + 512), 16,
+                                                         0, 0);
                 }
             }
         };
@@ -381,7 +384,7 @@ extern "C" int mxk_qmm3_dbg(int dbg, int wm, const uint16_t* A, int lda, const u
     return (int)hipErrorInvalidValue;
 }
 
-// A f16 [M, K] (lda % 8 == 0, 16-B aligned), W t32 Q4_K / Q6_K / Q3_K / Q2_K [N, K] (N % 32 == 0, K % 256 == 0).
+// A f16 [M, K] (lda % 8 == 0, 16-B aligned), W t32 Q4_K / Q5_K / Q6_K / Q3_K / Q2_K [N, K] (N % 32 == 0, K % 256 == 0).
 // epi as mxk_qmm2 (split-K only with epi 2). wm: 32-row MFMA blocks per consumer wave, BM = 64 wm (1, 2, 4).
 extern "C" int mxk_qmm3(int qtype, int epi, int wm, const uint16_t* A, int lda, const uint8_t* W, int M, int N, int K,
                         int splits, void* C, int ldc, hipStream_t st) {
@@ -401,6 +404,7 @@ extern "C" int mxk_qmm3(int qtype, int epi, int wm, const uint16_t* A, int lda, 
         case MXQ_Q6_K: Q3_EPI(MXQ_Q6_K) break;
         case MXQ_Q3_K: Q3_EPI(MXQ_Q3_K) break;
         case MXQ_Q2_K: Q3_EPI(MXQ_Q2_K) break;
+        case MXQ_Q5_K: Q3_EPI(MXQ_Q5_K) break;
     }
 #undef Q3_EPI
     return (int)hipErrorInvalidValue;

@@ -183,7 +183,8 @@ def cmd_models(a):
     else:
         for name in a.names:
             install_from_gallery(gals, name, c.models_path,
-                                 progress=lambda f, cur, tot, pct: print(f"\r{f} {cur}/{tot} {pct:.1f}%", end=""))
+                                 progress=lambda f, cur, tot, pct: print(f"\r{f} {cur}/{tot} {pct:.1f}%", end=""),
+                                 enforce_scan=not a.disable_predownload_scan)
             print(f"\ninstalled {name}")
     return 0
 
@@ -269,7 +270,35 @@ def cmd_util(a):
             c = cl.load_by_name(name)
             flags = [k for k, v in USECASE_FLAGS.items() if v and c.has_usecases(v)]
             print(f"{name}: {', '.join(flags) or '-'}")
+    elif a.util_cmd == "hf-scan":
+        return _hf_scan(a)
     return 0
+
+
+def _hf_scan(a) -> int:
+    """`local-ai util hf-scan [uri...]` (core/cli/util.go:75-107): best-effort HF safety scan of the given URIs, or
+    of every installed gallery model's files. Exit status 1 when anything is flagged."""
+    from .gallery import Gallery, safety_scan_installed
+    from .gallery import downloader as D
+    print("LocalAI security scanner - BEST EFFORT, limited to models hosted on huggingface.co", file=sys.stderr)
+    bad = []
+    if not a.uris:
+        gal = a.galleries or os.environ.get("LOCALAI_GALLERIES") or os.environ.get("GALLERIES") or "[]"
+        models_path = a.models_path or os.environ.get("LOCALAI_MODELS_PATH") or os.environ.get("MODELS_PATH") or "models"
+        bad = safety_scan_installed([Gallery.parse(g) for g in json.loads(gal)], models_path)
+    for uri in a.uris:
+        try:
+            D.hf_scan(uri)
+        except D.UnsafeFilesFound as ex:
+            bad.append(("", uri, ex.result))
+        except (D.DownloadError, OSError, ValueError) as ex:
+            print(f"{uri}: not scanned ({ex})", file=sys.stderr)
+    for model, uri, res in bad:
+        print(f"! WARNING ! known-unsafe files in {res.get('repositoryId') or uri}{' (model ' + model + ')' if model else ''}: "
+              f"clamAV={res.get('clamAVInfectedFiles') or []} pickles={res.get('dangerousPickles') or []}")
+    if not bad:
+        print("No security warnings were detected. This is a BEST EFFORT tool; not every issue is detected.")
+    return 1 if bad else 0
 
 
 def cmd_federated(a):
@@ -337,6 +366,8 @@ def main(argv=None):
     m.add_argument("names", nargs="*")
     m.add_argument("--models-path")
     m.add_argument("--galleries")
+    m.add_argument("--disable-predownload-scan", action="store_true",
+                   default=_bool_env(["LOCALAI_DISABLE_PREDOWNLOAD_SCAN"]))
     t = sub.add_parser("tts", help="text to speech")
     t.add_argument("text", nargs="+")
     t.add_argument("--model", "-m", required=True)
@@ -369,6 +400,10 @@ def main(argv=None):
     uh = usub.add_parser("usecase-heuristic")
     uh.add_argument("names", nargs="*")
     uh.add_argument("--models-path")
+    hs = usub.add_parser("hf-scan", help="check models for known security issues (best effort, huggingface only)")
+    hs.add_argument("uris", nargs="*")
+    hs.add_argument("--models-path")
+    hs.add_argument("--galleries")
     fd = sub.add_parser("federated", help="run the federated load-balancing proxy")
     fd.add_argument("--address", default=os.environ.get("LOCALAI_ADDRESS", "0.0.0.0:8080"))
     fd.add_argument("--p2ptoken")

@@ -73,7 +73,9 @@ class ApplicationConfig:
     federated: bool = field(default_factory=lambda: _env(["LOCALAI_FEDERATED", "FEDERATED"], False, bool))
     # MI355X specifics
     gpus: str = field(default_factory=lambda: _env(["LOCALAI_GPUS", "HIP_VISIBLE_DEVICES"], ""))
-    enable_hf_scan: bool = False
+    # best-effort HF safety scan before every gallery download (core/cli/run.go:50 DisablePredownloadScan)
+    enforce_predownload_scans: bool = field(
+        default_factory=lambda: not _env(["LOCALAI_DISABLE_PREDOWNLOAD_SCAN"], False, bool))
     version: str = "v0.1.0-mi355x"
 
     @property

@@ -107,6 +107,8 @@ class EngineConfig:
     # and depth 2 measured the same throughput with a worse TTFT (profiles/r2_verify_depth_{1,2}.json:
     # 13618 vs 13590 tok/s, p50 TTFT 18.8 vs 30.2 ms)
     overlap_depth: int = int(__import__("os").environ.get("MX_OVERLAP_DEPTH", "1"))
+    # time every GEMM shape of the model over the compiled tile / split candidates at load (ops/autotune.py)
+    gemm_autotune: bool = __import__("os").environ.get("MX_GEMM_TUNE", "1") != "0"
     n_draft: int = 0  # speculative decoding: draft tokens per step (needs a draft model; 0 = off)
     spec_max_batch: int = 32  # speculate only on decode batches up to this size (latency-bound regime)
 
@@ -393,6 +395,10 @@ class LLMEngine:
         self.batch_sink: BatchedSink | None = None
         if c.prefill_bf16_cache and self.device.type == "cuda" and hasattr(model, "enable_prefill_bf16_cache"):
             model.enable_prefill_bf16_cache()
+        if c.gemm_autotune and self.device.type == "cuda" and hasattr(model, "gemm_specs"):
+            # per-shape GEMM plans timed on this GPU before any graph is captured (ops/autotune.py)
+            from ..ops.autotune import tune_gemms
+            self.stats_tune_s = tune_gemms(model.gemm_specs())
         # overlap mode state: the launched-but-unread step, the device tokens it samples, and pinned
         # host staging (ring of 3: a buffer is rewritten only after the step that used it was read)
         # tensor parallel: the leader ships each plan before launching it and broadcasts the sampled

@@ -13,6 +13,7 @@ from dataclasses import dataclass, field
 
 import yaml
 
+from . import downloader as _dl
 from .downloader import DownloadError, download_file, read_uri, verify_path  # noqa: F401
 
 log = logging.getLogger("localai_tfp_amd.gallery")
@@ -161,10 +162,14 @@ def paginate(models: list, page: int, per_page: int) -> list:
 # install / delete
 
 def install_model(base_path: str, name_override: str, cfg: ModelInstallConfig, overrides: dict | None,
-                  progress=None) -> str:
+                  progress=None, enforce_scan: bool = False) -> str:
+    """Download the files (each behind the HF safety scan when enforce_scan: core/gallery/models.go:121-126),
+    write prompt templates, the merged model YAML and the gallery record."""
     os.makedirs(base_path, exist_ok=True)
     for i, f in enumerate(cfg.files):
         dst = verify_path(f["filename"], base_path)
+        if enforce_scan and f.get("uri"):
+            _dl.enforce_scan(f["uri"], name_override or cfg.name)
         download_file(f.get("uri", ""), dst, f.get("sha256", ""), i, len(cfg.files), progress)
     for t in cfg.prompt_templates:
         dst = verify_path(t["name"] + ".tmpl", base_path)
@@ -190,15 +195,16 @@ def install_model(base_path: str, name_override: str, cfg: ModelInstallConfig, o
 
 
 def install_from_gallery(galleries, name: str, base_path: str, req: GalleryModel | None = None,
-                         progress=None) -> str:
+                         progress=None, enforce_scan: bool = False) -> str:
     models = available_models(galleries, base_path)
     m = find_model(models, name)
     if m is None:
         raise KeyError(f"no model found with name {name!r}")
-    return apply_gallery_model(m, base_path, req, progress)
+    return apply_gallery_model(m, base_path, req, progress, enforce_scan)
 
 
-def apply_gallery_model(m: GalleryModel, base_path: str, req: GalleryModel | None = None, progress=None) -> str:
+def apply_gallery_model(m: GalleryModel, base_path: str, req: GalleryModel | None = None, progress=None,
+                        enforce_scan: bool = False) -> str:
     req = req or GalleryModel()
     if m.url:
         cfg = ModelInstallConfig.from_yaml(read_uri(m.url, base_path))
@@ -212,7 +218,31 @@ def apply_gallery_model(m: GalleryModel, base_path: str, req: GalleryModel | Non
     cfg.icon = m.icon
     cfg.files = list(cfg.files) + list(req.files) + list(m.files)
     ov = deep_merge(copy.deepcopy(m.overrides), req.overrides)
-    return install_model(base_path, req.name or m.name, cfg, ov, progress)
+    return install_model(base_path, req.name or m.name, cfg, ov, progress, enforce_scan)
+
+
+def safety_scan_installed(galleries, base_path: str) -> list[tuple[str, str, dict]]:
+    """`local-ai util hf-scan` without arguments (core/gallery/gallery.go:243-262): every installed gallery
+    model's files through the HF scan. Returns [(model, uri, scan record)] of the flagged ones."""
+    bad = []
+    for m in available_models(galleries, base_path):
+        if not m.installed:
+            continue
+        files = list(m.files)
+        try:
+            files += local_model_config(base_path, m.name).files
+        except (OSError, ValueError):
+            pass
+        for uri in dict.fromkeys(f.get("uri", "") for f in files):
+            if not uri:
+                continue
+            try:
+                _dl.hf_scan(uri)
+            except _dl.UnsafeFilesFound as ex:
+                bad.append((m.name, uri, ex.result))
+            except (_dl.DownloadError, OSError, ValueError):
+                pass
+    return bad
 
 
 def local_model_config(base_path: str, name: str) -> ModelInstallConfig:
@@ -275,8 +305,9 @@ class GalleryOp:
 
 
 class GalleryService:
-    def __init__(self, base_path: str, galleries=None, on_change=None):
+    def __init__(self, base_path: str, galleries=None, on_change=None, enforce_scan: bool = False):
         self.base_path = base_path
+        self.enforce_scan = enforce_scan  # HF safety scan before every download (EnforcePredownloadScans)
         self.galleries = [Gallery.parse(g) for g in (galleries or [])]
         self.status: dict[str, OpStatus] = {}
         self.q: queue.Queue[GalleryOp | None] = queue.Queue()
@@ -327,11 +358,12 @@ class GalleryService:
                     cfg = ModelInstallConfig.from_yaml(read_uri(op.config_url, self.base_path))
                     req = op.req or GalleryModel()
                     cfg.files += req.files
-                    install_model(self.base_path, req.name or cfg.name, cfg, req.overrides, progress)
+                    install_model(self.base_path, req.name or cfg.name, cfg, req.overrides, progress, self.enforce_scan)
                 elif op.req is not None and (op.req.url or op.req.config_file) and not op.gallery_model_name:
-                    apply_gallery_model(op.req, self.base_path, op.req, progress)
+                    apply_gallery_model(op.req, self.base_path, op.req, progress, self.enforce_scan)
                 else:
-                    install_from_gallery(op.galleries, op.gallery_model_name, self.base_path, op.req, progress)
+                    install_from_gallery(op.galleries, op.gallery_model_name, self.base_path, op.req, progress,
+                                         self.enforce_scan)
                 if self.on_change:
                     self.on_change()
                 st.progress, st.processed, st.message = 100.0, True, "completed"

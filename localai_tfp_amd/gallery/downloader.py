@@ -121,6 +121,54 @@ def read_uri(uri: str, base_path: str = "", authorization: str = "") -> bytes:
         return r.read()
 
 
+# ------------------------------------------------------------------------------------------------
+# HuggingFace safety scan (pkg/downloader/huggingface.go:24-47): best effort, HF-hosted files only
+
+class NonHuggingFaceFile(DownloadError):
+    pass
+
+
+class UnsafeFilesFound(DownloadError):
+    def __init__(self, msg: str, result: dict):
+        super().__init__(msg)
+        self.result = result
+
+
+def hf_api_base() -> str:
+    """Scan API root; LOCALAI_HF_API points it at a mirror (or a stand-in server in the tests)."""
+    return os.environ.get("LOCALAI_HF_API", "https://huggingface.co").rstrip("/")
+
+
+def hf_scan(uri: str, timeout: float = 10.0) -> dict:
+    """GET {api}/api/models/<owner>/<repo>/scan for a file hosted on huggingface.co. Returns the scan record
+    (repositoryId, revision, hasUnsafeFile, clamAVInfectedFiles, dangerousPickles, scansDone); raises
+    NonHuggingFaceFile for other hosts and UnsafeFilesFound (carrying the record) when the repo is flagged."""
+    parts = resolve_url(uri).split("/")
+    if len(parts) <= 4 or parts[2] != "huggingface.co":
+        raise NonHuggingFaceFile(f"not a huggingface repo: {uri}")
+    url = f"{hf_api_base()}/api/models/{parts[3]}/{parts[4]}/scan"
+    with _open(url, timeout=timeout) as r:
+        if r.status != 200:
+            raise DownloadError(f"unexpected status code during HuggingFace scan: {r.status}")
+        res = json.loads(r.read() or b"{}")
+    if res.get("hasUnsafeFile"):
+        raise UnsafeFilesFound(f"unsafe files found in {parts[3]}/{parts[4]}", res)
+    return res
+
+
+def enforce_scan(uri: str, model: str = "") -> None:
+    """Pre-download gate: refuse a file of a flagged HF repo. Like the reference, only a positive finding blocks;
+    a non-HF host, an unreachable API or a malformed answer lets the download proceed."""
+    try:
+        hf_scan(uri)
+    except UnsafeFilesFound as ex:
+        log.error("model %s: %s (clamAV: %s, pickles: %s)", model or "?", ex,
+                  ex.result.get("clamAVInfectedFiles") or [], ex.result.get("dangerousPickles") or [])
+        raise
+    except (DownloadError, OSError, ValueError) as ex:
+        log.debug("scan skipped for %s: %s", uri, ex)
+
+
 def _sha256_file(path: str) -> str:
     h = hashlib.sha256()
     with open(path, "rb") as f:

@@ -23,7 +23,7 @@ def install_models(app, refs: list[str]) -> list[str]:
             d = yaml.safe_load(read_uri(ref, base)) or {}
             if "config_file" in d or "files" in d:
                 cfg = ModelInstallConfig.from_yaml(yaml.safe_dump(d))
-                out.append(install_model(base, "", cfg, {}))
+                out.append(install_model(base, "", cfg, {}, enforce_scan=app.cfg.enforce_predownload_scans))
             else:
                 name = d.get("name") or os.path.splitext(filename_from_url(ref))[0]
                 with open(os.path.join(base, name + ".yaml"), "w") as f:
@@ -45,6 +45,7 @@ def install_models(app, refs: list[str]) -> list[str]:
                 yaml.safe_dump(d, f)
             out.append(name)
         else:
-            out.append(install_from_gallery(app.gallery.galleries, ref, base))
+            out.append(install_from_gallery(app.gallery.galleries, ref, base,
+                                            enforce_scan=app.cfg.enforce_predownload_scans))
         app.reload_configs()
     return out

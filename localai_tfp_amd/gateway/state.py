@@ -56,7 +56,8 @@ class Application:
         self.evaluator = Evaluator(c.models_path)
         self.inference = Inference(self)
         from ..gallery import GalleryService
-        self.gallery = GalleryService(c.models_path, c.galleries, on_change=self.reload_configs)
+        self.gallery = GalleryService(c.models_path, c.galleries, on_change=self.reload_configs,
+                                      enforce_scan=c.enforce_predownload_scans)
         self.files = JSONStore(os.path.join(c.upload_dir, "uploadedFiles.json"))
         self.assistants = JSONStore(os.path.join(c.config_dir, "assistants.json"))
         self.assistant_files = JSONStore(os.path.join(c.config_dir, "assistantsFile.json"))

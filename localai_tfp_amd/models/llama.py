@@ -36,7 +36,7 @@ from ..formats.gguf import QType
 from ..ops import core as K
 from ..ops import quant as Q
 from ..ops.linear import (ACT_DTYPE, EPI_ADD_F32, EPI_BF16, EPI_F32, EPI_GEGLU, EPI_SWIGLU, QWeight, concat_rows,
-                          _fp32_out_ok, dense_min_m, interleave_gate_up, qmatmul, qmatmul8, qmm8_ok, qmv_fusable,
+                          _fp32_out_ok, dense_min_m, interleave_gate_up, qmatmul, qmatmul8, qmm8_ok, qmv_fusable, qmv_rope_ok,
                           qmv_fused, qmv_rope_fused)
 from ..ops.moe import MoEWeights, moe_ffn
 from .config import LlamaConfig
@@ -398,6 +398,24 @@ class LlamaModel:
             if isinstance(w, QWeight):
                 w.ensure_kernel_layout()
 
+    def gemm_specs(self):
+        """(QWeight, epilogue, split-able output) of every M > 4 GEMM the forward issues — the shapes the load-time
+        autotuner (ops/autotune.py) times, with the epilogues forward() passes for them."""
+        tp = self.tp_size > 1
+        for L in self.layers:
+            for w in L.qkv_parts:
+                yield w, EPI_F32, True
+            for w in (L.wo, L.wd):
+                if w is not None:
+                    yield (w, EPI_BF16, False) if tp else (w, EPI_ADD_F32, True)
+            if L.wgu is not None:
+                yield L.wgu, self.glu_epi, False
+            for w in (L.wg, L.wu):
+                if w is not None:
+                    yield w, EPI_BF16, False
+        if isinstance(self.lm_head, QWeight):
+            yield self.lm_head, EPI_F32, False
+
     def weight_bytes(self) -> int:
         n = 0
         for L in self.layers:
@@ -601,15 +619,18 @@ class LlamaModel:
             rope_fused = (fuse_qkv and T == 1 and off == 0 and not cfg.neox and cfg.rope_dim == D
                           and L.q_norm is None and self.tp_size == 1)
             if rope_fused:
+                # every part is checked before any launches: parts may mix block formats
+                o2 = 0
+                for w in L.qkv_parts:
+                    rope_fused = rope_fused and qmv_rope_ok(w, h, q, kc, vc, D, o2)
+                    o2 += w.N
+            if rope_fused:
                 o2 = 0
                 for w in L.qkv_parts:
                     b = L.bqkv[o2:o2 + w.N] if L.bqkv is not None else None
                     if not qmv_rope_fused(w, h, L.attn_norm, eps, o2, fb.positions, fb.slots, inv_freq, b, attn_factor,
                                           Hq, Hkv, D, q.view(T, Hq, D), kc, vc, kv.block_size):
-                        if o2:
-                            raise RuntimeError("qkv RoPE fusion applied to some parts only")
-                        rope_fused = False
-                        break
+                        raise RuntimeError("qkv RoPE fusion applied to some parts only")
                     o2 += w.N
             for w in (L.qkv_parts if off == 0 and not rope_fused else ()):
                 sl = qkv[:, off:off + w.N] if len(L.qkv_parts) > 1 else qkv

@@ -22,6 +22,7 @@ import torch
 
 from .. import _native as N
 from ..formats.gguf import QType
+from . import autotune as _AT
 from . import quant as Q
 
 log = logging.getLogger("localai_tfp_amd.ops")
@@ -303,6 +304,46 @@ def _dense_cached(W: QWeight, x, epi: int, out, M: int):
     return _apply_epi_dense(y, epi, out)
 
 
+# Row chunking of wide K-quant GEMMs (M > ROW_CHUNK): every launch holds at most ROW_CHUNK rows. The qmm tiles hold
+# 128 or 256 rows with one workgroup per CU, so M = 384 as one launch runs two row tiles per column panel — 448
+# workgroups, 1.75 waves over 256 CUs, 512 rows of MFMA work (profiles/r4_engine_c128_kernels.md: gate_up 199 us at
+# M = 384 against 74 us at M = 256 and 42 us at M = 128); 256 + 128 as two launches fills the chip twice instead.
+ROW_CHUNK = int(os.environ.get("MX_ROW_CHUNK", "0"))
+
+
+def row_chunks(M: int, chunk: int | None = None) -> list[tuple[int, int]]:
+    """[(r0, r1)] row ranges of at most `chunk` rows (ROW_CHUNK; 0 = one launch)."""
+    c = ROW_CHUNK if chunk is None else chunk
+    if c <= 0 or M <= c:
+        return [(0, M)]
+    return [(r, min(r + c, M)) for r in range(0, M, c)]
+
+
+def run_plan(plan: tuple, W: QWeight, x: torch.Tensor, epi: int, out: torch.Tensor, out_zeroed: bool):
+    """Launch one GEMM plan (ops/autotune.py): ("q3", wm, splits) | ("q2", wm, ks, wn, splits) | ("rows", chunk)."""
+    M = x.shape[0]
+    kind = plan[0]
+    if kind == "rows":
+        for r0, r1 in row_chunks(M, plan[1]):
+            _qmatmul_t32(W, x[r0:r1], epi, out[r0:r1], None, None, r1 - r0, out_zeroed)
+        return out
+    splits = plan[-1]
+    e = EPI_ADD_F32 if (epi == EPI_F32 and splits > 1) else epi
+    if e in (EPI_BF16, *GLU_EPIS):
+        if out.dtype != x.dtype:
+            raise ValueError(f"qmatmul: {out.dtype} output with {x.dtype} activations")
+        N.ensure_act(out.dtype)
+    if kind == "q3":
+        N.kcall("mxk_qmm3", int(W.qtype), e, plan[1], x.data_ptr(), x.stride(0), W.data.data_ptr(), M, W.N, W.K,
+                splits, out.data_ptr(), out.stride(0), N.stream_ptr())
+    elif kind == "q2":
+        N.kcall("mxk_qmm2", int(W.qtype), e, plan[1], plan[2], plan[3], x.data_ptr(), x.stride(0), W.data.data_ptr(),
+                M, W.N, W.K, splits, out.data_ptr(), out.stride(0), N.stream_ptr())
+    else:
+        raise ValueError(f"unknown GEMM plan {plan}")
+    return out
+
+
 def _qmatmul_t32(W: QWeight, x, epi: int, out, xq, xds, M: int, out_zeroed: bool):
     """t32 tiled weights: qmv (q8 activations, M <= 4) or qmm (f16 activations, any M)."""
     if M <= 4 and xq is not None:
@@ -327,38 +368,29 @@ def _qmatmul_t32(W: QWeight, x, epi: int, out, xq, xds, M: int, out_zeroed: bool
     can_split = epi == EPI_ADD_F32 or (epi == EPI_F32 and out_zeroed)
     if W.bf16_cache is not None and M >= dense_min_m(x.dtype, epi, can_split) and W.bf16_cache.dtype == x.dtype:
         return _dense_cached(W, x, epi, out, M)
-    pick = _gemm_pick(M, W.N, W.K, int(W.qtype), can_split)
-    if pick is not None and pick[0] == "q3":
-        wm, splits = pick[1:]
-        e = EPI_ADD_F32 if (epi == EPI_F32 and splits > 1) else epi
-        if e in (EPI_BF16, *GLU_EPIS):
-            if out.dtype != x.dtype:
-                raise ValueError(f"qmatmul: {out.dtype} output with {x.dtype} activations")
-            N.ensure_act(out.dtype)
-        N.kcall("mxk_qmm3", int(W.qtype), e, wm, x.data_ptr(), x.stride(0), W.data.data_ptr(), M, W.N, W.K,
-                splits, out.data_ptr(), out.stride(0), N.stream_ptr())
-        return out
-    if pick is not None:
-        wm, ks, wn, splits = pick[1:]
-        e = EPI_ADD_F32 if (epi == EPI_F32 and splits > 1) else epi
-        if e in (EPI_BF16, *GLU_EPIS):
-            if out.dtype != x.dtype:
-                raise ValueError(f"qmatmul: {out.dtype} output with {x.dtype} activations")
-            N.ensure_act(out.dtype)
-        N.kcall("mxk_qmm2", int(W.qtype), e, wm, ks, wn, x.data_ptr(), x.stride(0), W.data.data_ptr(), M, W.N, W.K,
-                splits, out.data_ptr(), out.stride(0), N.stream_ptr())
-        return out
-    ws = _qmm_ws_shape(M, W.N, W.K, can_split, int(W.qtype))
-    if ws is not None:
-        cfg, splits = ws
-        e = EPI_ADD_F32 if (epi == EPI_F32 and splits > 1) else epi
-        if e in (EPI_BF16, *GLU_EPIS):
-            if out.dtype != x.dtype:
-                raise ValueError(f"qmatmul: {out.dtype} output with {x.dtype} activations")
-            N.ensure_act(out.dtype)
-        N.kcall("mxk_qmm_ws", int(W.qtype), e, cfg, x.data_ptr(), x.stride(0), W.data.data_ptr(), M, W.N, W.K, splits,
-                out.data_ptr(), out.stride(0), N.stream_ptr())
-        return out
+    forced = QMM2 or QMM3 or QMM2_FORCE is not None or QMM3_FORCE is not None or QMM_FORCE is not None
+    plan = _AT.lookup(W.N, W.K, int(W.qtype), epi, can_split, M) if (_AT.TUNED and not forced) else None
+    if plan is None:
+        if len(row_chunks(M)) > 1:
+            plan = ("rows", ROW_CHUNK)
+        else:
+            pick = _gemm_pick(M, W.N, W.K, int(W.qtype), can_split)
+            if pick is None:
+                ws = _qmm_ws_shape(M, W.N, W.K, can_split, int(W.qtype))
+                if ws is not None:
+                    cfg, splits = ws
+                    e = EPI_ADD_F32 if (epi == EPI_F32 and splits > 1) else epi
+                    if e in (EPI_BF16, *GLU_EPIS):
+                        if out.dtype != x.dtype:
+                            raise ValueError(f"qmatmul: {out.dtype} output with {x.dtype} activations")
+                        N.ensure_act(out.dtype)
+                    N.kcall("mxk_qmm_ws", int(W.qtype), e, cfg, x.data_ptr(), x.stride(0), W.data.data_ptr(), M, W.N,
+                            W.K, splits, out.data_ptr(), out.stride(0), N.stream_ptr())
+                    return out
+            else:
+                plan = pick
+    if plan is not None:
+        return run_plan(plan, W, x, epi, out, out_zeroed)
     wm, wn, nw, ks, splits = _qmm_shape(M, W.N, W.K, can_split)
     e = EPI_ADD_F32 if (epi == EPI_F32 and splits > 1) else epi
     if e in (EPI_BF16, *GLU_EPIS):
@@ -475,15 +507,22 @@ QMV_ROPE_QTYPES = (int(QType.Q4_K), int(QType.Q5_K), int(QType.Q6_K), int(QType.
 QMV_ROPE_FUSE = os.environ.get("MX_QMV_ROPE", "1") != "0"
 
 
+def qmv_rope_ok(W, x: torch.Tensor, q_out: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, D: int,
+                n_off: int) -> bool:
+    """Does mxk_qmv1_rope apply to this qkv part? Callers fusing several parts check EVERY part first, so a
+    model whose parts mix block formats (q|k Q4_K, v Q8_0 / MX4F) takes the unfused path for all of them."""
+    return not (not QMV_ROPE_FUSE or not isinstance(W, QWeight) or W.layout != "t32"
+                or int(W.qtype) not in QMV_ROPE_QTYPES or W.K != 4096 or x.shape[0] != 1 or not x.is_cuda
+                or x.dtype != torch.float32 or not x.is_contiguous() or k_cache.dtype != torch.bfloat16
+                or v_cache.dtype != torch.bfloat16 or q_out.dtype != torch.bfloat16 or D not in (64, 128) or n_off % 32)
+
+
 def qmv_rope_fused(W: QWeight, x: torch.Tensor, norm: torch.Tensor, eps: float, n_off: int, positions, slots,
                    inv_freq: torch.Tensor, bias, attn_factor: float, Hq: int, Hkv: int, D: int, q_out: torch.Tensor,
                    k_cache: torch.Tensor, v_cache: torch.Tensor, block_size: int) -> bool:
     """Batch-1 qkv part: RMSNorm -> q8 -> GEMV -> (+bias) -> RoPE (adjacent pairs, whole head) -> q_out or the
     paged K/V caches at slots[0], one launch (qmv.hip mxk_qmv1_rope). False: not applicable, nothing launched."""
-    if (not QMV_ROPE_FUSE or not isinstance(W, QWeight) or W.layout != "t32" or int(W.qtype) not in QMV_ROPE_QTYPES
-            or W.K != 4096 or x.shape[0] != 1 or not x.is_cuda or x.dtype != torch.float32 or not x.is_contiguous()
-            or k_cache.dtype != torch.bfloat16 or v_cache.dtype != torch.bfloat16 or q_out.dtype != torch.bfloat16
-            or D not in (64, 128) or n_off % 32):
+    if not qmv_rope_ok(W, x, q_out, k_cache, v_cache, D, n_off):
         return False
     N.kcall("mxk_qmv1_rope", int(W.qtype), x.data_ptr(), norm.data_ptr(), float(eps), W.data.data_ptr(), W.N, W.K,
             n_off, positions.data_ptr(), slots.data_ptr(), inv_freq.data_ptr(), N.ptr(bias), float(attn_factor), Hq,
@@ -586,7 +625,7 @@ QMM2 = os.environ.get("MX_QMM2", "0") != "0"
 QMM2_FORCE: tuple | None = None  # (wm, ks, wn, splits) override for tuning (tools/tune_qmm2.py)
 # compiled (wm, ks, wn): wm 32-row MFMA blocks x wn 32-column groups per wave, ks 1 / 2 waves per SIMD
 QMM2_CONFIGS = ((2, 1, 1), (2, 2, 1), (4, 1, 1), (4, 2, 1), (8, 1, 1), (1, 2, 2), (2, 1, 2), (2, 2, 2), (4, 1, 2))
-QMM2_QTYPES = (int(QType.Q4_K), int(QType.Q6_K), int(QType.Q3_K), int(QType.Q2_K))
+QMM2_QTYPES = (int(QType.Q4_K), int(QType.Q6_K), int(QType.Q3_K), int(QType.Q2_K), int(QType.Q5_K))
 QMM2_ONLY = tuple(int(q) for q in Q.QMM2_ONLY)  # no qmm.hip variant: qmm2 for every M > 4
 QMM2_MIN_M = int(os.environ.get("MX_QMM2_MIN_M", "16"))
 

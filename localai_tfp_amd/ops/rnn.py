@@ -9,9 +9,13 @@ Reference parity: the StyleTTS 2 / Kokoro text encoder and prosody predictor LST
 """
 from __future__ import annotations
 
+import logging
+
 import torch
 
 from .. import _native as N
+
+log = logging.getLogger("localai_tfp_amd.ops")
 
 
 def _ref(x, p: dict, name: str):
@@ -47,4 +51,9 @@ def lstm_bidir(x: torch.Tensor, p: dict, name: str, cache: dict | None = None) -
     out = torch.empty(T, 2 * H, dtype=torch.float32, device=x.device)
     N.kcall("mxk_lstm_bidir", gx.data_ptr(), whh.data_ptr(), hbuf.data_ptr(), out.data_ptr(), cnt.data_ptr(),
             cnt[2:].data_ptr(), T, H, N.stream_ptr())
+    if int(cnt[2].item()):
+        # a bounded grid-barrier spin timed out (a workgroup never arrived): the states are stale, so the
+        # result is not used — recompute on the reference LSTM and say so
+        log.warning("lstm_bidir %s: cooperative kernel barrier timed out (T=%d, H=%d); reference LSTM used", name, T, H)
+        return _ref(x, p, name)
     return out

@@ -197,6 +197,9 @@ class SamplerBatch:
             if got not in (4096, 8192):
                 raise N.NativeError(f"split sampler: unexpected slice size {got} from the library")
             self.SLICE = got
+            caps = N.kernels().mxk_sample_topk_caps()  # scratch below is sized from it: must match TK_CAPS
+            if caps != self.CAPS:
+                raise N.NativeError(f"split sampler: library TK_CAPS {caps} != host scratch capacity {self.CAPS}")
             self._slice_checked = True
         S = -(-V // self.SLICE)
         if S > 64:

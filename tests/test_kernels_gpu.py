@@ -435,7 +435,7 @@ def test_qmm(qt, M, wm, wn, nw, ks, splits, monkeypatch):
     assert rel(sw, ref_sw) < 1e-2
 
 
-@pytest.mark.parametrize("qt", [QType.Q4_K, QType.Q6_K, QType.Q3_K, QType.Q2_K])
+@pytest.mark.parametrize("qt", [QType.Q4_K, QType.Q6_K, QType.Q3_K, QType.Q2_K, QType.Q5_K])
 @pytest.mark.parametrize("M,wm,ks,wn,splits", [
     (64, 2, 1, 1, 1), (64, 2, 2, 1, 3), (17, 2, 2, 1, 1), (128, 4, 2, 1, 1), (77, 4, 2, 1, 2), (128, 4, 1, 1, 4),
     (256, 8, 1, 1, 1), (300, 8, 1, 1, 3), (511, 8, 1, 1, 1), (100, 2, 1, 1, 5),
@@ -475,7 +475,7 @@ def test_qmm2(qt, M, wm, ks, wn, splits, monkeypatch):
     assert rel(sw, ref_sw) < 1e-2
 
 
-@pytest.mark.parametrize("qt", [QType.Q4_K, QType.Q6_K, QType.Q3_K, QType.Q2_K])
+@pytest.mark.parametrize("qt", [QType.Q4_K, QType.Q6_K, QType.Q3_K, QType.Q2_K, QType.Q5_K])
 @pytest.mark.parametrize("M,wm,splits", [
     (64, 1, 1), (40, 1, 3), (128, 2, 1), (77, 2, 2), (200, 2, 5), (256, 4, 1), (300, 4, 3), (511, 4, 2), (17, 1, 1)])
 def test_qmm3(qt, M, wm, splits, monkeypatch):

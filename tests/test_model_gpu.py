@@ -184,3 +184,32 @@ def test_long_prompt_many_chunks_matches_one_chunk(overlap):
     r = float((caches[0] - caches[1]).norm() / caches[0].norm())
     assert r < 5e-2, r
     assert len(outs[1]) == 3 and outs[0][:2] == outs[1][:2], outs
+
+
+def test_batch1_rope_fusion_with_mixed_qkv_formats():
+    """q|k Q4_K (mxk_qmv1_rope applies) with attn_v Q8_0 (it does not): the batch-1 decode must check every
+    qkv part before fusing any, take the unfused path for all of them, and match the CPU reference
+    (a part-wise decision raised 'RoPE fusion applied to some parts only')."""
+    from localai_tfp_amd.formats.gguf import QType
+    from localai_tfp_amd.ops.quant import random_quantized
+    cfg = tiny_config(hidden=4096, ffn=1024, n_heads=32, n_kv_heads=8, head_dim=128, rope_dim=128, vocab=512,
+                      n_layers=1)
+    base = synthetic_source(cfg, "Q4_K_M", seed=11)
+
+    def src(name):
+        if name.endswith("attn_v.weight"):
+            raw = random_quantized(np.random.default_rng(3), int(QType.Q8_0), cfg.kv_dim, cfg.hidden, std=0.02)
+            return raw, int(QType.Q8_0), (cfg.hidden, cfg.kv_dim)
+        return base(name)
+
+    src.plan = base.plan
+    m_cpu = LlamaModel.load(cfg, src, "cpu")
+    m_gpu = LlamaModel.load(cfg, src, "cuda")
+    assert len({int(w.qtype) for w in m_gpu.layers[0].qkv_parts}) == 2
+    prompt = list(np.random.default_rng(1).integers(0, cfg.vocab, 12))
+    forced = [7, 300, 11]
+    a = _run(m_cpu, "cpu", prompt, forced)
+    b = _run(m_gpu, "cuda", prompt, forced)
+    for x, y in zip(a, b):
+        r = float((x - y).norm() / x.norm())
+        assert r < 6e-2, r
