@@ -337,6 +337,10 @@ def main():
             },
         }
         print(json.dumps(out), flush=True)
+        if os.environ.get("MX_TUNE_REPORT"):
+            from localai_tfp_amd.ops import autotune
+            with open(os.environ["MX_TUNE_REPORT"], "w") as f:
+                json.dump(autotune.report(), f, indent=1)
     if link is not None:
         link.close()
     if world > 1:

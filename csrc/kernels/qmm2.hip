@@ -26,426 +26,8 @@
 // k-tile's four k-steps; their fp32 partials are summed through LDS before the epilogue.
 // Reference parity: llama.cpp's MMQ path for these formats (reached via backend/cpp/llama/grpc-server.cpp:2002
 // llama_decode); numerics = f16 dequantised weights x f16 activations, fp32 accumulation.
-#include "qmm2_fmt.h"
-
-namespace {
-
-constexpr int Q2_NS = 4;  // ring slots (k-tiles of 64)
-int g_qmm2_rot = 0;       // k-order rotation multiplier per column tile (0: natural order), mxk_qmm2_set_rot
-
-template <int QT, int WM, int KS, int WN>
-struct Q2Geom {
-    using F = Q2F<QT>;
-    static constexpr int BM = 32 * WM * WN;
-    static constexpr int NT = 4 * KS;                 // waves
-    static constexpr int A_BYTES = BM * 128;          // one 64-k tile of A
-    static constexpr int STAGE = A_BYTES + 4 * F::QB; // A + the 4 column groups' quant bytes
-    static constexpr int HSZ = 4 * F::HB;             // one super-block header slot (4 groups)
-    static constexpr int LDS = Q2_NS * STAGE + 2 * HSZ;
-    static constexpr int WA = BM / 8 / NT;            // A LDS-DMA instructions per wave per stage
-    // LDS-DMA instructions per stage of a weight-loading wave (kh == 0) / an A-only wave, by the stage's
-    // position in its super-block (JQ == 0 stages also carry the header)
-    template <int JQ, bool WL>
-    static constexpr int cnt() { return WA + (WL ? F::QI + (JQ == 0 ? F::HI : 0) : 0); }
-};
-
-
-// per-k-step issue schedule: each MFMA followed by one LDS read (the first NDS) and up to NV VALU, so the next
-// k-step's fragment reads leave early and the dequant VALU fills the MFMA shadows
-constexpr int Q2_VPM = 5;
-template <int I, int NM, int NDS, int NV>
-MX_DEV void q2_interleave() {
-    if constexpr (I < NM) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        if constexpr (I < NDS) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x002, NV, 0);
-        q2_interleave<I + 1, NM, NDS, NV>();
-    }
-}
-
-// DBG (isolation builds, tools/prof_qmm.py --q2dbg): 1 no MFMA, 2 no dequant VALU, 4 no A loads, 8 no weight loads
-template <int QT, int WM, int KS, int WN, int EPI, int DBG = 0>
-__global__ __launch_bounds__(256 * KS) void qmm2_kernel(const uint16_t* __restrict__ A, int lda,
-                                                        const uint8_t* __restrict__ W, int M, int N, int K,
-                                                        int n_mt, int splits, int sbps, void* __restrict__ Cv,
-                                                        int ldc, int rot_mul) {
-    using G = Q2Geom<QT, WM, KS, WN>;
-    using F = Q2F<QT>;
-    constexpr int BM = G::BM, WA = G::WA, STAGE = G::STAGE, A_BYTES = G::A_BYTES;
-    static_assert(WN == 1 || WN == 2, "WN");
-    static_assert(KS == 1 || 4 * WM * WN * 16 * 64 * 4 <= G::LDS, "KS = 2 partials fit in the ring");
-    static_assert(WA >= 1 && WA * 8 * G::NT == BM, "A tile split");
-    static_assert(G::LDS <= 160 * 1024, "LDS");
-    static_assert(G::template cnt<1, true>() + G::template cnt<2, true>() <= 63 &&
-                  G::template cnt<0, true>() + G::template cnt<1, true>() <= 63, "vmcnt range");
-    // LDS-DMA instructions per stage as issued (the isolation builds drop some)
-    constexpr int WAI = (DBG & 4) ? 0 : WA, QII = (DBG & 8) ? 0 : F::QI, HII = (DBG & 8) ? 0 : F::HI;
-    auto cnt = [](auto jq_c, auto wl_c) constexpr {
-        return WAI + (decltype(wl_c)::value ? QII + (decltype(jq_c)::value == 0 ? HII : 0) : 0);
-    };
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    char* const hdr_lds = smem + Q2_NS * STAGE;
-
-    // wave index as a scalar: every LDS-DMA destination (M0) and weight pointer below is then SGPR math
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    const int h = lane >> 5, col = lane & 31;
-    // cg: the column group this wave DMAs; (mw, nw): its compute tile = rows mw * 32 WM .., groups nw * WN + j
-    const int cg = wave & 3, kh = wave >> 2;
-    constexpr int NW = 4 / WN;
-    const int nw = cg % NW, mw = cg / NW;
-
-    // XCD-aware bijective remap: consecutive logical ids (the row tiles and splits of one column panel)
-    // run on one XCD and share its L2
-    const int nwg = gridDim.x, bid = blockIdx.x;
-    const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
-    const int lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-    const int mt = lid % n_mt;
-    const int rest = lid / n_mt;
-    const int split = rest % splits;
-    const int ct = rest / splits;
-
-    const int nsb = K >> 8;
-    const int sb0 = split * sbps, sb1 = min(sb0 + sbps, nsb);
-    if (sb0 >= sb1) return;
-    const int m_base = mt * BM;
-    const int ngrp = N >> 5;
-    const int g = min(ct * 4 + cg, ngrp - 1);  // groups past N re-read the last (never stored)
-    const uint8_t* wg = W + (size_t)g * ((size_t)nsb * F::UNIT);
-
-    // A LDS-DMA sources: instruction i of this wave fills 8-row block j = wave * WA + i; lane p writes
-    // image slot (k-step p >> 4, row (p >> 1) & 7, half (p & 1) ^ (j & 1)) from 16 B of that row
-    uint32_t aoff[WA];
-#pragma unroll
-    for (int i = 0; i < WA; ++i) {
-        const int j = wave * WA + i;
-        const int s = lane >> 4, r8 = (lane >> 1) & 7, hh = (lane & 1) ^ (j & 1);
-        const int row = min(m_base + 8 * j + r8, M - 1);
-        aoff[i] = (uint32_t)(row * lda + 16 * s + 8 * hh);
-    }
-    // per-lane fragment read bases (byte offsets within a stage)
-    const int rb = col >> 3;
-    const uint32_t a_rd = (uint32_t)(mw * WM * 4096 + rb * 1024 + (col & 7) * 32 + ((h ^ (rb & 1)) << 4));
-    const uint32_t b_rd = (uint32_t)(A_BYTES + nw * WN * F::QB);  // + j * QB for the wave's group j
-    const int hg = nw * WN * F::HB;                                 // header offset of group nw * WN
-
-    // stage issue: the A rows of k-tile `kta` and (weight waves) the quant bytes of super-block `sbw`,
-    // quarter JQ, into ring slot JQ; JQ == 0 stages also bring that super-block's header into header slot
-    // `hslot`. Dummy stages past the end pass clamped (valid, never consumed) sources.
-    auto issue = [&](int kta, int sbw, int hslot, auto jq_c, auto wl_c) {
-        constexpr int JQ = decltype(jq_c)::value;
-        char* sb = smem + JQ * STAGE;
-        const uint16_t* ak = A + (size_t)kta * 64;
-#pragma unroll
-        for (int i = 0; i < WAI; ++i)
-            __builtin_amdgcn_global_load_lds((const void*)(ak + aoff[i]), (MX_LDS void*)(sb + (wave * WA + i) * 1024),
-                                             16, 0, 0);
-        if constexpr (decltype(wl_c)::value && QII > 0) {
-            const uint8_t* u = wg + (size_t)sbw * F::UNIT;
-            const uint8_t* qs = u + F::qoff(JQ);
-            char* qd = sb + A_BYTES + cg * F::QB;
-            __builtin_amdgcn_global_load_lds((const void*)(qs + lane * 16), (MX_LDS void*)qd, 16, 0, 0);
-            if constexpr (QT == MXQ_Q6_K) {
-                if (lane < 32)
-                    __builtin_amdgcn_global_load_lds((const void*)(qs + 1024 + lane * 16), (MX_LDS void*)(qd + 1024), 16,
-                                                     0, 0);
-            }
-            if constexpr (JQ == 0) {
-                char* hd = hdr_lds + hslot * G::HSZ + cg * F::HB;
-                if constexpr (QT == MXQ_Q3_K) {  // hdr (512 B) + hmask (1 KB): one full and one half instruction
-                    __builtin_amdgcn_global_load_lds((const void*)(u + lane * 16), (MX_LDS void*)hd, 16, 0, 0);
-                    if (lane < 32)
-                        __builtin_amdgcn_global_load_lds((const void*)(u + 1024 + lane * 16), (MX_LDS void*)(hd + 1024),
-                                                         16, 0, 0);
-                } else {
-                    if (lane < 32) __builtin_amdgcn_global_load_lds((const void*)(u + lane * 16), (MX_LDS void*)hd, 16, 0, 0);
-                    if constexpr (QT == MXQ_Q6_K || QT == MXQ_Q2_K) {  // + the 32 x 4 B d (/ dmin) words
-                        if (lane < 32)
-                            __builtin_amdgcn_global_load_lds((const void*)(u + 512 + lane * 4), (MX_LDS void*)(hd + 512), 4,
-                                                             0, 0);
-                    }
-                    if constexpr (QT == MXQ_Q5_K)  // + the qh chunks (fifth bits of the whole super-block)
-                        __builtin_amdgcn_global_load_lds((const void*)(u + F::QH + lane * 16), (MX_LDS void*)(hd + 512), 16,
-                                                         0, 0);
-                }
-            }
-        }
-    };
-
-    f32x16 acc[WM][WN];
-#pragma unroll
-    for (int i = 0; i < WM; ++i)
-#pragma unroll
-        for (int j = 0; j < WN; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
-    auto mainloop = [&](auto kh_c, auto wl_c) {
-        constexpr int KH = decltype(kh_c)::value;
-        using WLc = decltype(wl_c);
-        constexpr bool WL = WLc::value;
-        using I0 = std::integral_constant<int, 0>;
-        using I1 = std::integral_constant<int, 1>;
-        using I2 = std::integral_constant<int, 2>;
-        using I3 = std::integral_constant<int, 3>;
-        // the split's super-blocks are visited in a rotated order (v -> sb0 + (v + rot) % nv): workgroups that
-        // run side by side on one XCD (consecutive column tiles) then stream different k ranges of the shared
-        // A rows instead of all hitting the same 128-B lines (and L2 channels) at the same time
-        const int nv = sb1 - sb0;
-        const int rot = rot_mul ? (int)(((unsigned)ct * (unsigned)rot_mul) % (unsigned)nv) : 0;
-        auto phys = [&](int v) {
-            int p = v + rot;
-            if (p >= nv) p -= nv;
-            return sb0 + p;
-        };
-        // prologue: stages 0 .. 2 of the (virtual) k-tile sequence (a split holds >= 4 k-tiles, so all real)
-        const int p0 = phys(0);
-        issue(p0 * 4, p0, 0, I0{}, WLc{});
-        issue(p0 * 4 + 1, p0, 0, I1{}, WLc{});
-        issue(p0 * 4 + 2, p0, 0, I2{}, WLc{});
-        q2_wait_barrier<cnt(I1{}, WLc{}) + cnt(I2{}, WLc{})>();
-
-        // fragment producers (S is a compile-time constant after unrolling)
-        auto bfrag = [&](const Q2B<QT>& b, auto jq_c, int S) -> f16x8 {
-            constexpr int JQ_ = decltype(jq_c)::value;
-            if constexpr (DBG & 2) {
-                const u32x2 r2 = (S & 1) ? b.v1 : b.v0;
-                return __builtin_bit_cast(f16x8, (u32x4){r2[0], r2[1], r2[0] ^ (uint32_t)S, r2[1]});
-            } else {
-                switch (S) {
-                    case 0: return b.template frag<JQ_, 0>();
-                    case 1: return b.template frag<JQ_, 1>();
-                    case 2: return b.template frag<JQ_, 2>();
-                    default: return b.template frag<JQ_, 3>();
-                }
-            }
-        };
-        Q2B<QT> bw[WN];
-        f16x8 af[2][WM], bfc[WN];
-#pragma unroll
-        for (int j = 0; j < WN; ++j) {
-            bw[j].load_hdr(hdr_lds + hg + j * F::HB, col, h);
-            bw[j].load_q(smem + b_rd + j * F::QB, col, h);
-            bw[j].template prep<0>();
-            bfc[j] = bfrag(bw[j], I0{}, KH);
-        }
-#pragma unroll
-        for (int i = 0; i < WM; ++i) af[0][i] = *(const f16x8*)(smem + a_rd + i * 4096 + KH * 256);
-
-        // one k-tile (ring slot JQ): the wave's k-steps KH, KH + KS, ...; software-pipelined one k-step deep:
-        // k-step S's MFMAs consume A / B fragments read and dequantised during k-step S - KS, while this
-        // k-step reads and dequantises those of the next one (on the last k-step: the next tile's first, from
-        // ring slot JQ + 1, landed at the top). An explicit per-k-step schedule (q2_interleave) keeps the
-        // compiler from sinking the LDS reads next to their MFMAs, which stalled every k-step on lgkmcnt(0).
-        auto tile = [&](int sb, auto jq_c) {  // sb: virtual super-block index
-            constexpr int JQ = decltype(jq_c)::value;
-            constexpr int NJ = (JQ + 1) & 3;
-            const int kt = sb * 4 + JQ;
-            // stage kt+1 landed (only stage kt+2 may still be in flight); every wave is past tile kt-1
-            q2_wait_barrier<cnt(std::integral_constant<int, (JQ + 2) & 3>{}, WLc{})>();
-            {
-                const int ki = kt + 3, vi = ki >> 2;
-                const bool real = vi < nv;
-                const int ps = phys(real ? vi : nv - 1);
-                issue(ps * 4 + (real ? (ki & 3) : 3), ps, vi & 1, std::integral_constant<int, (JQ + 3) & 3>{}, WLc{});
-            }
-            // the next tile's quant bytes (and, at a super-block edge, header): slot NJ landed at the wait above
-            Q2B<QT> bn[WN];
-#pragma unroll
-            for (int j = 0; j < WN; ++j) {
-                bn[j] = bw[j];
-                if constexpr (NJ == 0) bn[j].load_hdr(hdr_lds + ((sb + 1) & 1) * G::HSZ + hg + j * F::HB, col, h);
-                bn[j].load_q(smem + NJ * STAGE + b_rd + j * F::QB, col, h);
-            }
-            constexpr int NSTEP = 4 / KS;
-#pragma unroll
-            for (int t = 0; t < NSTEP; ++t) {
-                __builtin_amdgcn_sched_barrier(0);
-                const int S = KH + KS * t;  // compile-time after unrolling
-                const int cur = t & 1;
-                f16x8 bfn[WN];
-                if (t + 1 < NSTEP) {
-#pragma unroll
-                    for (int i = 0; i < WM; ++i)
-                        af[cur ^ 1][i] = *(const f16x8*)(smem + JQ * STAGE + a_rd + i * 4096 + (S + KS) * 256);
-#pragma unroll
-                    for (int j = 0; j < WN; ++j) bfn[j] = bfrag(bw[j], jq_c, S + KS);
-                } else {
-#pragma unroll
-                    for (int i = 0; i < WM; ++i)
-                        af[cur ^ 1][i] = *(const f16x8*)(smem + NJ * STAGE + a_rd + i * 4096 + KH * 256);
-#pragma unroll
-                    for (int j = 0; j < WN; ++j) {
-                        bn[j].template prep<NJ>();
-                        bfn[j] = bfrag(bn[j], std::integral_constant<int, NJ>{}, KH);
-                    }
-                }
-#pragma unroll
-                for (int j = 0; j < WN; ++j)
-#pragma unroll
-                    for (int i = 0; i < WM; ++i) {
-                        if constexpr (DBG & 1) asm volatile("" ::"v"(af[cur][i]), "v"(bfc[j]));
-                        else acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[cur][i], bfc[j], acc[i][j], 0, 0, 0);
-                    }
-                if constexpr (!(DBG & 1)) q2_interleave<0, WM * WN, WM, Q2_VPM>();
-#pragma unroll
-                for (int j = 0; j < WN; ++j) bfc[j] = bfn[j];
-            }
-            // NSTEP is even: the next tile's first fragments are in af[0]
-#pragma unroll
-            for (int j = 0; j < WN; ++j) bw[j] = bn[j];
-        };
-        for (int sb = 0; sb < nv; ++sb) {
-            tile(sb, I0{});
-            tile(sb, I1{});
-            tile(sb, I2{});
-            tile(sb, I3{});
-        }
-        // drain the dummy stages before the LDS is reused / released
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    };
-    using T_ = std::integral_constant<bool, true>;
-    using F_ = std::integral_constant<bool, false>;
-    if constexpr (KS == 1) {
-        mainloop(std::integral_constant<int, 0>{}, T_{});
-    } else {
-        if (kh == 0) mainloop(std::integral_constant<int, 0>{}, T_{});
-        else mainloop(std::integral_constant<int, 1>{}, F_{});
-        // sum the k-step halves: kh = 1 waves park their partials in the drained ring
-        __syncthreads();
-        float* red = (float*)smem + (size_t)cg * (WM * WN * 16 * 64) + lane;
-        if (kh == 1) {
-#pragma unroll
-            for (int i = 0; i < WM; ++i)
-#pragma unroll
-                for (int j = 0; j < WN; ++j)
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) red[((i * WN + j) * 16 + r) * 64] = acc[i][j][r];
-        }
-        __syncthreads();
-        if (kh == 1) return;
-#pragma unroll
-        for (int i = 0; i < WM; ++i)
-#pragma unroll
-            for (int j = 0; j < WN; ++j)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) acc[i][j][r] += red[((i * WN + j) * 16 + r) * 64];
-    }
-
-    // ---- epilogue: 32x32 C/D layout: col = lane & 31, row = 8*(r>>2) + 4*(lane>>5) + (r&3) ----
-    const int mb = m_base + mw * WM * 32;
-#pragma unroll
-    for (int j = 0; j < WN; ++j) {
-        const int nt = (ct * 4 + nw * WN + j) * 32;
-        const int n = nt + col;
-        if (nt >= N) break;
-        if constexpr (EPI == E16_SWIGLU || EPI == E16_GEGLU) {
-            // W rows interleaved in 16-row groups: tile columns 0..15 gate, 16..31 up of the same features
-#pragma unroll
-            for (int i = 0; i < WM; ++i)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const float v = acc[i][j][r];
-                    const float up = __shfl_xor(v, 16);
-                    const int m = mb + i * 32 + 8 * (r >> 2) + 4 * h + (r & 3);
-                    if (col < 16 && m < M)
-                        ((uint16_t*)Cv)[(size_t)m * ldc + (nt >> 1) + col] = f32_to_act<true>(glu_gate_f<EPI>(v) * up);
-                }
-            continue;
-        }
-#pragma unroll
-        for (int i = 0; i < WM; ++i) {
-            const int m0 = mb + i * 32 + 4 * h;
-            if (mb + i * 32 >= M) break;
-            float* cf = ((float*)Cv) + (size_t)m0 * ldc + n;
-            uint16_t* ch = ((uint16_t*)Cv) + (size_t)m0 * ldc + n;
-            auto roff = [&](int r) { return (size_t)(8 * (r >> 2) + (r & 3)) * ldc; };
-            if (mb + i * 32 + 32 <= M) {
-                if constexpr (EPI == E16_ADD_F32) {
-                    if (splits == 1) {
-                        float old[16];
-#pragma unroll
-                        for (int r = 0; r < 16; ++r) old[r] = cf[roff(r)];
-#pragma unroll
-                        for (int r = 0; r < 16; ++r) cf[roff(r)] = old[r] + acc[i][j][r];
-                    } else {
-#pragma unroll
-                        for (int r = 0; r < 16; ++r) atomicAdd(cf + roff(r), acc[i][j][r]);
-                    }
-                } else {
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) {
-                        if constexpr (EPI == E16_F32) cf[roff(r)] = acc[i][j][r];
-                        else ch[roff(r)] = f32_to_act<true>(acc[i][j][r]);
-                    }
-                }
-                continue;
-            }
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                if (m0 + 8 * (r >> 2) + (r & 3) >= M) continue;
-                const float v = acc[i][j][r];
-                if constexpr (EPI == E16_F32) cf[roff(r)] = v;
-                else if constexpr (EPI == E16_ACT) ch[roff(r)] = f32_to_act<true>(v);
-                else if (splits == 1) cf[roff(r)] += v;
-                else atomicAdd(cf + roff(r), v);
-            }
-        }
-    }
-}
-
-template <int QT, int WM, int KS, int WN, int EPI>
-static int launch_qmm2(const uint16_t* A, int lda, const uint8_t* W, int M, int N, int K, int splits, void* C, int ldc,
-                       hipStream_t st) {
-    using G = Q2Geom<QT, WM, KS, WN>;
-    const int nsb = K >> 8;
-    splits = max(1, min(splits, nsb));
-    const int sbps = (nsb + splits - 1) / splits;
-    splits = (nsb + sbps - 1) / sbps;  // no empty splits
-    const int n_ct = (N + 127) / 128, n_mt = (M + G::BM - 1) / G::BM;
-    const long nwg = (long)n_ct * splits * n_mt;
-    if (nwg <= 0 || nwg > 0x7fffffff) return (int)hipErrorInvalidValue;
-    static bool attr_set = false;
-    if (!attr_set) {
-        (void)hipFuncSetAttribute((const void*)qmm2_kernel<QT, WM, KS, WN, EPI>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  G::LDS);
-        attr_set = true;
-    }
-    qmm2_kernel<QT, WM, KS, WN, EPI><<<dim3((unsigned)nwg), 256 * KS, G::LDS, st>>>(A, lda, W, M, N, K, n_mt, splits,
-                                                                                    sbps, C, ldc, g_qmm2_rot);
-    MXK_CHECK_LAUNCH();
-}
-
-template <int QT, int EPI>
-static int dispatch_qmm2(int wm, int ks, int wn, const uint16_t* A, int lda, const uint8_t* W, int M, int N, int K,
-                         int splits, void* C, int ldc, hipStream_t st) {
-#define Q2_CASE(WM_, KS_, WN_)                 \
-    if (wm == WM_ && ks == KS_ && wn == WN_) \
-        return launch_qmm2<QT, WM_, KS_, WN_, EPI>(A, lda, W, M, N, K, splits, C, ldc, st);
-    // (8, 2, 1) / (4, 2, 2) (256-row tiles with 8 waves) exceed the 256 registers a wave has at 2 waves / SIMD
-    Q2_CASE(2, 1, 1) Q2_CASE(2, 2, 1) Q2_CASE(4, 1, 1) Q2_CASE(4, 2, 1) Q2_CASE(8, 1, 1)
-    Q2_CASE(1, 2, 2) Q2_CASE(2, 1, 2) Q2_CASE(2, 2, 2) Q2_CASE(4, 1, 2)
-#undef Q2_CASE
-    return (int)hipErrorInvalidValue;
-}
-
-template <int DBG>
-static int launch_dbg(int wm, int ks, int wn, const uint16_t* A, int lda, const uint8_t* W, int M, int N, int K, void* C, int ldc,
-                      hipStream_t st) {
-    constexpr int QT = MXQ_Q4_K, EPI = E16_SWIGLU;
-    auto go = [&](auto kern, int bm, int ks, int lds) {
-        (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-        const int n_ct = (N + 127) / 128, n_mt = (M + bm - 1) / bm;
-        kern<<<dim3(n_ct * n_mt), 256 * ks, lds, st>>>(A, lda, W, M, N, K, n_mt, 1, K >> 8, C, ldc, g_qmm2_rot);
-        return (int)hipGetLastError();
-    };
-    if (wm == 8 && ks == 1 && wn == 1) return go(qmm2_kernel<QT, 8, 1, 1, EPI, DBG>, 256, 1, Q2Geom<QT, 8, 1, 1>::LDS);
-    if (wm == 4 && ks == 2 && wn == 1) return go(qmm2_kernel<QT, 4, 2, 1, EPI, DBG>, 128, 2, Q2Geom<QT, 4, 2, 1>::LDS);
-    if (wm == 4 && ks == 1 && wn == 2) return go(qmm2_kernel<QT, 4, 1, 2, EPI, DBG>, 256, 1, Q2Geom<QT, 4, 1, 2>::LDS);
-    if (wm == 2 && ks == 2 && wn == 2) return go(qmm2_kernel<QT, 2, 2, 2, EPI, DBG>, 128, 2, Q2Geom<QT, 2, 2, 2>::LDS);
-    return (int)hipErrorInvalidValue;
-}
-
-}  // namespace
+#include "qmm2_impl.h"
+int g_qmm2_rot = 0;
 
 extern "C" int mxk_qmm2_set_rot(int r) {
     g_qmm2_rot = r;
@@ -456,17 +38,7 @@ extern "C" int mxk_qmm2_set_rot(int r) {
 // see DBG above
 extern "C" int mxk_qmm2_dbg(int dbg, int wm, int ks, int wn, const uint16_t* A, int lda, const uint8_t* W, int M, int N,
                             int K, void* C, int ldc, hipStream_t st) {
-    switch (dbg) {
-        case 0: return launch_dbg<0>(wm, ks, wn, A, lda, W, M, N, K, C, ldc, st);
-        case 1: return launch_dbg<1>(wm, ks, wn, A, lda, W, M, N, K, C, ldc, st);
-        case 2: return launch_dbg<2>(wm, ks, wn, A, lda, W, M, N, K, C, ldc, st);
-        case 3: return launch_dbg<3>(wm, ks, wn, A, lda, W, M, N, K, C, ldc, st);
-        case 4: return launch_dbg<4>(wm, ks, wn, A, lda, W, M, N, K, C, ldc, st);
-        case 8: return launch_dbg<8>(wm, ks, wn, A, lda, W, M, N, K, C, ldc, st);
-        case 12: return launch_dbg<12>(wm, ks, wn, A, lda, W, M, N, K, C, ldc, st);
-        case 15: return launch_dbg<15>(wm, ks, wn, A, lda, W, M, N, K, C, ldc, st);
-    }
-    return (int)hipErrorInvalidValue;
+    return qmm2_dbg_q4k(dbg, wm, ks, wn, A, lda, W, M, N, K, C, ldc, st);
 }
 
 // A f16 [M, K] (lda % 8 == 0, 16-B aligned), W t32 Q4_K / Q5_K / Q6_K / Q3_K / Q2_K [N, K] (N % 32 == 0, K % 256 == 0).
@@ -479,21 +51,12 @@ extern "C" int mxk_qmm2(int qtype, int epi, int wm, int ks, int wn, const uint16
     if (M <= 0) return 0;
     if (K % 256 || (lda & 7) || ((uintptr_t)A & 15) || ((uintptr_t)W & 15) || (N & 31)) return (int)hipErrorInvalidValue;
     if (epi != E16_ADD_F32 && splits != 1) return (int)hipErrorInvalidValue;
-#define Q2_EPI(QT_)                                                                                          \
-    switch (epi) {                                                                                           \
-        case E16_F32: return dispatch_qmm2<QT_, E16_F32>(wm, ks, wn, A, lda, W, M, N, K, splits, C, ldc, st);     \
-        case E16_ACT: return dispatch_qmm2<QT_, E16_ACT>(wm, ks, wn, A, lda, W, M, N, K, splits, C, ldc, st);     \
-        case E16_ADD_F32: return dispatch_qmm2<QT_, E16_ADD_F32>(wm, ks, wn, A, lda, W, M, N, K, splits, C, ldc, st); \
-        case E16_SWIGLU: return dispatch_qmm2<QT_, E16_SWIGLU>(wm, ks, wn, A, lda, W, M, N, K, splits, C, ldc, st); \
-        case E16_GEGLU: return dispatch_qmm2<QT_, E16_GEGLU>(wm, ks, wn, A, lda, W, M, N, K, splits, C, ldc, st);   \
-    }
     switch (qtype) {
-        case MXQ_Q4_K: Q2_EPI(MXQ_Q4_K) break;
-        case MXQ_Q6_K: Q2_EPI(MXQ_Q6_K) break;
-        case MXQ_Q3_K: Q2_EPI(MXQ_Q3_K) break;
-        case MXQ_Q2_K: Q2_EPI(MXQ_Q2_K) break;
-        case MXQ_Q5_K: Q2_EPI(MXQ_Q5_K) break;
+        case MXQ_Q4_K: return qmm2_run_q4k(epi, wm, ks, wn, A, lda, W, M, N, K, splits, C, ldc, st);
+        case MXQ_Q5_K: return qmm2_run_q5k(epi, wm, ks, wn, A, lda, W, M, N, K, splits, C, ldc, st);
+        case MXQ_Q6_K: return qmm2_run_q6k(epi, wm, ks, wn, A, lda, W, M, N, K, splits, C, ldc, st);
+        case MXQ_Q3_K: return qmm2_run_q3k(epi, wm, ks, wn, A, lda, W, M, N, K, splits, C, ldc, st);
+        case MXQ_Q2_K: return qmm2_run_q2k(epi, wm, ks, wn, A, lda, W, M, N, K, splits, C, ldc, st);
     }
-#undef Q2_EPI
     return (int)hipErrorInvalidValue;
 }

@@ -65,6 +65,22 @@ def _jobs():
 FILE_FLAGS = {"qmm8.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]}
 
 
+_INC = __import__("re").compile(r'^\s*#\s*include\s*"([^"]+)"', __import__("re").M)
+
+
+def _deps(src: Path, headers) -> list:
+    """The in-tree headers `src` includes, transitively (an object is rebuilt only when one of ITS headers changes)."""
+    by_name = {h.name: h for h in headers}
+    seen, todo = {}, [src]
+    while todo:
+        for inc in _INC.findall(todo.pop().read_text(errors="replace")):
+            h = by_name.get(Path(inc).name)
+            if h is not None and h.name not in seen:
+                seen[h.name] = h
+                todo.append(h)
+    return list(seen.values())
+
+
 def _build_lib(name: str, srcs, headers, compiler, cflags, ldflags, verbose=False) -> Path:
     LIB.mkdir(parents=True, exist_ok=True)
     BUILD.mkdir(parents=True, exist_ok=True)
@@ -79,7 +95,7 @@ def _build_lib(name: str, srcs, headers, compiler, cflags, ldflags, verbose=Fals
         obj = BUILD / (name + "." + src.stem + ".o")
         okey = BUILD / (name + "." + src.stem + ".key")
         flags = list(cflags) + FILE_FLAGS.get(src.name, [])
-        k = _hash([src] + list(headers)) + "|" + " ".join(flags)
+        k = _hash([src] + _deps(src, headers)) + "|" + " ".join(flags)
         if obj.exists() and okey.exists() and okey.read_text() == k:
             return obj
         cmd = [compiler, *flags, "-c", str(src), "-o", str(obj)]

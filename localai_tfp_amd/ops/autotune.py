@@ -29,6 +29,7 @@ BUCKETS = (16, 32, 64, 96, 128, 160, 192, 224, 256, 320, 384, 448, 512)
 SPLITS = (1, 2, 4, 8)
 # (N, K, qtype, epi, can_split) -> [(bucket, plan)] sorted by bucket
 TUNED: dict[tuple, list] = {}
+TIMES: dict[tuple, list] = {}  # key -> [(bucket, plan, us)] of the plans tuned in this process (reports)
 ENABLED = os.environ.get("MX_GEMM_TUNE", "1") != "0"
 
 
@@ -113,8 +114,15 @@ def tune_weight(W, epi: int, can_split: bool, buckets=BUCKETS, iters: int = 8) -
                 best, best_t = plan, t
         if best is not None:
             res.append((b, best))
+            TIMES.setdefault(key, []).append((b, best, round(best_t, 2)))
             log.debug("tune %s M=%d -> %s %.1f us", key, b, best, best_t)
     return res
+
+
+def report() -> list[dict]:
+    """The plans tuned in this process with their times (bench / profiles)."""
+    return [{"N": k[0], "K": k[1], "qtype": k[2], "epi": k[3], "split": k[4],
+             "plans": [[b, list(p), us] for b, p, us in v]} for k, v in TIMES.items()]
 
 
 def _cache_path() -> str:
