@@ -57,6 +57,7 @@ def parse():
     ap.add_argument("--prompt-len", type=int, default=256)
     ap.add_argument("--gen-len", type=int, default=256)
     ap.add_argument("--max-batched-tokens", type=int, default=2048)
+    ap.add_argument("--prefill-chunk", type=int, default=0, help="prompt tokens per sequence per step (0: budget)")
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--kv-dtype", default="bf16", choices=["bf16", "f16", "fp8"],
                     help="paged KV cache element type (llama.cpp cache_type_k/v); fp8 = e4m3")
@@ -248,6 +249,7 @@ def main():
         args.tokenizer = "byte"
     tok = make_tokenizer(args.tokenizer, cfg.vocab)
     ecfg = EngineConfig(max_num_seqs=args.concurrency, max_batched_tokens=args.max_batched_tokens,
+                        prefill_chunk=args.prefill_chunk or None,
                         max_model_len=max(4096, args.prompt_len + args.gen_len + 64), use_graphs=not args.no_graphs,
                         kv_dtype=args.kv_dtype)
     if dev.type == "cpu":
@@ -337,6 +339,9 @@ def main():
             },
         }
         print(json.dumps(out), flush=True)
+        if eng.trace is not None:
+            with open(os.environ["MX_STEP_TRACE"], "w") as f:
+                json.dump(eng.trace, f)
         if os.environ.get("MX_TUNE_REPORT"):
             from localai_tfp_amd.ops import autotune
             with open(os.environ["MX_TUNE_REPORT"], "w") as f:

@@ -9,38 +9,12 @@
 // One 256-thread workgroup per row; float4 loads; the sum of squares never leaves registers/LDS.
 #include "mx_common.h"
 
-// ---- Q8_K activation blocks (ggml quantize_row_q8_K): 256 elements share one fp32 scale ----------
-// The int8-MFMA GEMM (qmm8.hip) consumes activations in llama.cpp's CPU K-quant dot-product format:
-// per 256-element block, max = the element of largest |x| (first one on ties), iscale = -127 / max,
-// q = min(127, round_half_even(iscale * x)), d = 1 / iscale, plus the int sum of every 16 q ("bsums",
-// stored as f16: |sum| <= 2032 is exact). One wave quantises one block, 4 consecutive elements per lane.
-MX_DEV void q8k_block(float a0, float a1, float a2, float a3, int lane, int8_t* __restrict__ oq,
-                      float* __restrict__ od, _Float16* __restrict__ obs) {
-    const float m4 = fmaxf(fmaxf(fabsf(a0), fabsf(a1)), fmaxf(fabsf(a2), fabsf(a3)));
-    const float amax = wave_max(m4);
-    // signed value of the first element (lowest index) whose |x| == amax
-    float first = fabsf(a0) == amax ? a0 : fabsf(a1) == amax ? a1 : fabsf(a2) == amax ? a2 : a3;
-    const unsigned long long hit = __ballot(m4 == amax);
-    const int src = hit ? __builtin_ctzll(hit) : 0;
-    const float mx = __shfl(first, src, 64);
-    const float iscale = amax > 0.f ? -127.f / mx : 0.f;
-    int q0 = min(127, __float2int_rn(iscale * a0)), q1 = min(127, __float2int_rn(iscale * a1));
-    int q2 = min(127, __float2int_rn(iscale * a2)), q3 = min(127, __float2int_rn(iscale * a3));
-    const uint32_t pk = (uint32_t)(q0 & 0xFF) | ((uint32_t)(q1 & 0xFF) << 8) | ((uint32_t)(q2 & 0xFF) << 16) |
-                        ((uint32_t)(q3 & 0xFF) << 24);
-    *(uint32_t*)(oq + 4 * lane) = pk;
-    const float s = group_sum<4>((float)(q0 + q1 + q2 + q3));
-    if ((lane & 3) == 0) obs[lane >> 2] = (_Float16)s;
-    if (lane == 0) *od = amax > 0.f ? 1.f / iscale : 0.f;
-}
-
-template <bool WANT_BF16, bool WANT_Q8, bool HAS_RES, bool F16, bool Q8K = false>
+template <bool WANT_BF16, bool WANT_Q8, bool HAS_RES, bool F16>
 __global__ __launch_bounds__(256) void rmsnorm_kernel(const float* __restrict__ x, int ldx,
                                                       const bf16_t* __restrict__ res, int ldr,
                                                       float* __restrict__ xout, const float* __restrict__ w,
                                                       bf16_t* __restrict__ ob, int ldo, int8_t* __restrict__ oq,
-                                                      float2* __restrict__ ods, int H, float eps,
-                                                      float* __restrict__ kd = nullptr, _Float16* __restrict__ kbs = nullptr) {
+                                                      float2* __restrict__ ods, int H, float eps) {
     __shared__ float red[4];
     const int row = blockIdx.x;
     const float* xr = x + (size_t)row * ldx;
@@ -91,12 +65,6 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(const float* __restrict__ 
                               ((uint32_t)(q3 & 0xFF) << 24);
                 *(uint32_t*)(oq + (size_t)row * H + c) = pk;
                 if ((threadIdx.x & 7) == 0) ods[(size_t)row * (H / 32) + c / 32] = make_float2(d, d * (float)s);
-            }
-            if (Q8K) {
-                // chunk i of the 64 threads of one wave = one 256-element block
-                const int b = c >> 8;
-                q8k_block(a0, a1, a2, a3, threadIdx.x & 63, oq + (size_t)row * H + b * 256,
-                          kd + (size_t)row * (H / 256) + b, kbs + (size_t)row * (H / 16) + b * 16);
             }
         }
     }
@@ -163,52 +131,6 @@ extern "C" int mxk_rmsnorm(const float* x, int ldx, const bf16_t* res, int ldr, 
                 rmsnorm_generic_kernel<false, true, F16><<<rows, 256, 0, st>>>(x, ldx, w, ob, ldo, oq, ods, H, eps);
         });
     }
-    MXK_CHECK_LAUNCH();
-}
-
-// RMSNorm -> Q8_K blocks (int8 [rows][H], fp32 d [rows][H/256], f16 bsums [rows][H/16]) and optionally
-// the 16-bit rows as well; H % 1024 == 0.
-extern "C" int mxk_rmsnorm_q8k(const float* x, int ldx, const float* w, bf16_t* ob, int ldo, int8_t* oq, float* od,
-                               _Float16* obs, int rows, int H, float eps, hipStream_t st) {
-    if (rows <= 0) return 0;
-    if (H % 1024 || H > 8192) return (int)hipErrorInvalidValue;
-    MX_ACT_DISPATCH({
-        if (ob) rmsnorm_kernel<true, false, false, F16, true><<<rows, 256, 0, st>>>(x, ldx, nullptr, 0, nullptr, w, ob, ldo, oq,
-                                                                                      nullptr, H, eps, od, obs);
-        else rmsnorm_kernel<false, false, false, F16, true><<<rows, 256, 0, st>>>(x, ldx, nullptr, 0, nullptr, w, ob, ldo, oq,
-                                                                                    nullptr, H, eps, od, obs);
-    });
-    MXK_CHECK_LAUNCH();
-}
-
-// 16-bit (act16) or fp32 rows -> Q8_K blocks; one wave per 256-element block, 4 blocks per workgroup.
-template <bool F32, bool F16>
-__global__ __launch_bounds__(256) void quant_q8k_kernel(const void* __restrict__ x, int ldx, int8_t* __restrict__ oq,
-                                                        float* __restrict__ od, _Float16* __restrict__ obs, int K) {
-    const int row = blockIdx.y, lane = threadIdx.x & 63;
-    const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (b * 256 >= K) return;
-    const int e0 = b * 256 + 4 * lane;
-    float a[4];
-    if constexpr (F32) {
-        const float4 v = *(const float4*)((const float*)x + (size_t)row * ldx + e0);
-        a[0] = v.x; a[1] = v.y; a[2] = v.z; a[3] = v.w;
-    } else {
-        const uint2 raw = *(const uint2*)((const bf16_t*)x + (size_t)row * ldx + e0);
-        unpack_act2<F16>(raw.x, a[0], a[1]);
-        unpack_act2<F16>(raw.y, a[2], a[3]);
-    }
-    q8k_block(a[0], a[1], a[2], a[3], lane, oq + (size_t)row * K + b * 256, od + (size_t)row * (K / 256) + b,
-              obs + (size_t)row * (K / 16) + b * 16);
-}
-
-extern "C" int mxk_quant_q8k(const void* x, int ldx, int src_f32, int8_t* oq, float* od, _Float16* obs, int rows, int K,
-                             hipStream_t st) {
-    if (rows <= 0) return 0;
-    if (K % 256) return (int)hipErrorInvalidValue;
-    dim3 grid((K / 256 + 3) / 4, rows);
-    if (src_f32) quant_q8k_kernel<true, false><<<grid, 256, 0, st>>>(x, ldx, oq, od, obs, K);
-    else MX_ACT_DISPATCH(quant_q8k_kernel<false, F16><<<grid, 256, 0, st>>>(x, ldx, oq, od, obs, K));
     MXK_CHECK_LAUNCH();
 }
 

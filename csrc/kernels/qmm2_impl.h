@@ -6,10 +6,11 @@ extern int g_qmm2_rot;  // k-order rotation multiplier per column tile (0: natur
 
 namespace {
 
-constexpr int Q2_NS = 4;  // ring slots (k-tiles of 64)
-
-
-template <int QT, int WM, int KS, int WN>
+// NS: ring slots (k-tiles of 64): 4, or 8 for the 64-row tiles ("deep ring", ks | 8 in mxk_qmm2) — a 64-row
+// stage is only 12-14 KB, and with 4 slots a workgroup keeps ~2 stages (24 KB) in flight: at the ~1.1 us
+// issue -> landed latency of LDS-DMA under load that caps the CU at ~30 GB/s, which is what the narrow
+// projections measured (qkv M = 256: 768 KB per workgroup in 25 us). 8 slots keep 6 stages in flight.
+template <int QT, int WM, int KS, int WN, int NS = 4>
 struct Q2Geom {
     using F = Q2F<QT>;
     static constexpr int BM = 32 * WM * WN;
@@ -17,7 +18,8 @@ struct Q2Geom {
     static constexpr int A_BYTES = BM * 128;          // one 64-k tile of A
     static constexpr int STAGE = A_BYTES + 4 * F::QB; // A + the 4 column groups' quant bytes
     static constexpr int HSZ = 4 * F::HB;             // one super-block header slot (4 groups)
-    static constexpr int LDS = Q2_NS * STAGE + 2 * HSZ;
+    static constexpr int NH = NS == 8 ? 3 : 2;         // header slots: super-blocks live at once
+    static constexpr int LDS = NS * STAGE + NH * HSZ;
     static constexpr int WA = BM / 8 / NT;            // A LDS-DMA instructions per wave per stage
     // LDS-DMA instructions per stage of a weight-loading wave (kh == 0) / an A-only wave, by the stage's
     // position in its super-block (JQ == 0 stages also carry the header)
@@ -39,28 +41,39 @@ MX_DEV void q2_interleave() {
     }
 }
 
+// outstanding LDS-DMA instructions of NN consecutive stages from super-block position J0 (a stage: WAI A pieces,
+// plus QII quant pieces and, at position 0, HII header pieces for a weight-loading wave)
+template <int WAI, int QII, int HII, bool WL, int J0, int NN>
+constexpr int q2_cnt_run() {
+    int c = 0;
+    for (int d = 0; d < NN; ++d) c += WAI + (WL ? QII + (((J0 + d) & 3) == 0 ? HII : 0) : 0);
+    return c;
+}
+
 // DBG (isolation builds, tools/prof_qmm.py --q2dbg): 1 no MFMA, 2 no dequant VALU, 4 no A loads, 8 no weight loads
-template <int QT, int WM, int KS, int WN, int EPI, int DBG = 0>
+template <int QT, int WM, int KS, int WN, int EPI, int DBG = 0, int NS = 4>
 __global__ __launch_bounds__(256 * KS) void qmm2_kernel(const uint16_t* __restrict__ A, int lda,
                                                         const uint8_t* __restrict__ W, int M, int N, int K,
                                                         int n_mt, int splits, int sbps, void* __restrict__ Cv,
                                                         int ldc, int rot_mul) {
-    using G = Q2Geom<QT, WM, KS, WN>;
+    using G = Q2Geom<QT, WM, KS, WN, NS>;
     using F = Q2F<QT>;
     constexpr int BM = G::BM, WA = G::WA, STAGE = G::STAGE, A_BYTES = G::A_BYTES;
+    static_assert(NS == 4 || NS == 8, "ring depth");
     static_assert(WN == 1 || WN == 2, "WN");
     static_assert(KS == 1 || 4 * WM * WN * 16 * 64 * 4 <= G::LDS, "KS = 2 partials fit in the ring");
     static_assert(WA >= 1 && WA * 8 * G::NT == BM, "A tile split");
     static_assert(G::LDS <= 160 * 1024, "LDS");
-    static_assert(G::template cnt<1, true>() + G::template cnt<2, true>() <= 63 &&
-                  G::template cnt<0, true>() + G::template cnt<1, true>() <= 63, "vmcnt range");
+    static_assert((NS - 2) * G::template cnt<0, true>() <= 63, "vmcnt range");
     // LDS-DMA instructions per stage as issued (the isolation builds drop some)
     constexpr int WAI = (DBG & 4) ? 0 : WA, QII = (DBG & 8) ? 0 : F::QI, HII = (DBG & 8) ? 0 : F::HI;
     auto cnt = [](auto jq_c, auto wl_c) constexpr {
         return WAI + (decltype(wl_c)::value ? QII + (decltype(jq_c)::value == 0 ? HII : 0) : 0);
     };
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    char* const hdr_lds = smem + Q2_NS * STAGE;
+    char* const hdr_lds = smem + NS * STAGE;
+    // ring slot of k-tile ki = ki % NS; header slot of super-block v = v % NH
+    auto hslot_of = [](int v) { return NS == 8 ? v % 3 : v & 1; };
 
     // wave index as a scalar: every LDS-DMA destination (M0) and weight pointer below is then SGPR math
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -105,11 +118,11 @@ __global__ __launch_bounds__(256 * KS) void qmm2_kernel(const uint16_t* __restri
     const int hg = nw * WN * F::HB;                                 // header offset of group nw * WN
 
     // stage issue: the A rows of k-tile `kta` and (weight waves) the quant bytes of super-block `sbw`,
-    // quarter JQ, into ring slot JQ; JQ == 0 stages also bring that super-block's header into header slot
+    // quarter JQ, into ring slot `slot`; JQ == 0 stages also bring that super-block's header into header slot
     // `hslot`. Dummy stages past the end pass clamped (valid, never consumed) sources.
-    auto issue = [&](int kta, int sbw, int hslot, auto jq_c, auto wl_c) {
+    auto issue = [&](int kta, int sbw, int slot, int hslot, auto jq_c, auto wl_c) {
         constexpr int JQ = decltype(jq_c)::value;
-        char* sb = smem + JQ * STAGE;
+        char* sb = smem + slot * STAGE;
         const uint16_t* ak = A + (size_t)kta * 64;
 #pragma unroll
         for (int i = 0; i < WAI; ++i)
@@ -173,12 +186,25 @@ __global__ __launch_bounds__(256 * KS) void qmm2_kernel(const uint16_t* __restri
             if (p >= nv) p -= nv;
             return sb0 + p;
         };
-        // prologue: stages 0 .. 2 of the (virtual) k-tile sequence (a split holds >= 4 k-tiles, so all real)
-        const int p0 = phys(0);
-        issue(p0 * 4, p0, 0, I0{}, WLc{});
-        issue(p0 * 4 + 1, p0, 0, I1{}, WLc{});
-        issue(p0 * 4 + 2, p0, 0, I2{}, WLc{});
-        q2_wait_barrier<cnt(I1{}, WLc{}) + cnt(I2{}, WLc{})>();
+        // stage ki of the virtual k-tile sequence (ki & 3 == KI & 3, compile-time): past the split's end a dummy
+        // stage re-reads the last real super-block's tile 3 (valid addresses, never consumed)
+        auto issue_stage = [&](int ki, auto jq_c) {
+            const int vi = ki >> 2;
+            const bool real = vi < nv;
+            const int ps = phys(real ? vi : nv - 1);
+            issue(ps * 4 + (real ? (ki & 3) : 3), ps, ki % NS, hslot_of(vi), jq_c, WLc{});
+        };
+        // prologue: stages 0 .. NS - 2, then stage 0 landed
+        issue_stage(0, I0{});
+        issue_stage(1, I1{});
+        issue_stage(2, I2{});
+        if constexpr (NS == 8) {
+            issue_stage(3, I3{});
+            issue_stage(4, I0{});
+            issue_stage(5, I1{});
+            issue_stage(6, I2{});
+        }
+        q2_wait_barrier<q2_cnt_run<WAI, QII, HII, WL, 1, NS - 2>()>();
 
         // fragment producers (S is a compile-time constant after unrolling)
         auto bfrag = [&](const Q2B<QT>& b, auto jq_c, int S) -> f16x8 {
@@ -216,21 +242,17 @@ __global__ __launch_bounds__(256 * KS) void qmm2_kernel(const uint16_t* __restri
             constexpr int JQ = decltype(jq_c)::value;
             constexpr int NJ = (JQ + 1) & 3;
             const int kt = sb * 4 + JQ;
-            // stage kt+1 landed (only stage kt+2 may still be in flight); every wave is past tile kt-1
-            q2_wait_barrier<cnt(std::integral_constant<int, (JQ + 2) & 3>{}, WLc{})>();
-            {
-                const int ki = kt + 3, vi = ki >> 2;
-                const bool real = vi < nv;
-                const int ps = phys(real ? vi : nv - 1);
-                issue(ps * 4 + (real ? (ki & 3) : 3), ps, vi & 1, std::integral_constant<int, (JQ + 3) & 3>{}, WLc{});
-            }
+            const int cs = kt % NS, ns = (kt + 1) % NS;  // ring slots of this tile and the next
+            // stage kt+1 landed (stages kt+2 .. kt+NS-2 may still be in flight); every wave is past tile kt-1
+            q2_wait_barrier<q2_cnt_run<WAI, QII, HII, WL, (JQ + 2) & 3, NS - 3>()>();
+            issue_stage(kt + NS - 1, std::integral_constant<int, (JQ + NS - 1) & 3>{});
             // the next tile's quant bytes (and, at a super-block edge, header): slot NJ landed at the wait above
             Q2B<QT> bn[WN];
 #pragma unroll
             for (int j = 0; j < WN; ++j) {
                 bn[j] = bw[j];
-                if constexpr (NJ == 0) bn[j].load_hdr(hdr_lds + ((sb + 1) & 1) * G::HSZ + hg + j * F::HB, col, h);
-                bn[j].load_q(smem + NJ * STAGE + b_rd + j * F::QB, col, h);
+                if constexpr (NJ == 0) bn[j].load_hdr(hdr_lds + hslot_of(sb + 1) * G::HSZ + hg + j * F::HB, col, h);
+                bn[j].load_q(smem + ns * STAGE + b_rd + j * F::QB, col, h);
             }
             constexpr int NSTEP = 4 / KS;
 #pragma unroll
@@ -242,13 +264,13 @@ __global__ __launch_bounds__(256 * KS) void qmm2_kernel(const uint16_t* __restri
                 if (t + 1 < NSTEP) {
 #pragma unroll
                     for (int i = 0; i < WM; ++i)
-                        af[cur ^ 1][i] = *(const f16x8*)(smem + JQ * STAGE + a_rd + i * 4096 + (S + KS) * 256);
+                        af[cur ^ 1][i] = *(const f16x8*)(smem + cs * STAGE + a_rd + i * 4096 + (S + KS) * 256);
 #pragma unroll
                     for (int j = 0; j < WN; ++j) bfn[j] = bfrag(bw[j], jq_c, S + KS);
                 } else {
 #pragma unroll
                     for (int i = 0; i < WM; ++i)
-                        af[cur ^ 1][i] = *(const f16x8*)(smem + NJ * STAGE + a_rd + i * 4096 + KH * 256);
+                        af[cur ^ 1][i] = *(const f16x8*)(smem + ns * STAGE + a_rd + i * 4096 + KH * 256);
 #pragma unroll
                     for (int j = 0; j < WN; ++j) {
                         bn[j].template prep<NJ>();
@@ -369,10 +391,10 @@ __global__ __launch_bounds__(256 * KS) void qmm2_kernel(const uint16_t* __restri
     }
 }
 
-template <int QT, int WM, int KS, int WN, int EPI>
+template <int QT, int WM, int KS, int WN, int EPI, int NS = 4>
 static int launch_qmm2(const uint16_t* A, int lda, const uint8_t* W, int M, int N, int K, int splits, void* C, int ldc,
                        hipStream_t st) {
-    using G = Q2Geom<QT, WM, KS, WN>;
+    using G = Q2Geom<QT, WM, KS, WN, NS>;
     const int nsb = K >> 8;
     splits = max(1, min(splits, nsb));
     const int sbps = (nsb + splits - 1) / splits;
@@ -382,24 +404,30 @@ static int launch_qmm2(const uint16_t* A, int lda, const uint8_t* W, int M, int 
     if (nwg <= 0 || nwg > 0x7fffffff) return (int)hipErrorInvalidValue;
     static bool attr_set = false;
     if (!attr_set) {
-        (void)hipFuncSetAttribute((const void*)qmm2_kernel<QT, WM, KS, WN, EPI>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  G::LDS);
+        (void)hipFuncSetAttribute((const void*)qmm2_kernel<QT, WM, KS, WN, EPI, 0, NS>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS);
         attr_set = true;
     }
-    qmm2_kernel<QT, WM, KS, WN, EPI><<<dim3((unsigned)nwg), 256 * KS, G::LDS, st>>>(A, lda, W, M, N, K, n_mt, splits,
-                                                                                    sbps, C, ldc, g_qmm2_rot);
+    qmm2_kernel<QT, WM, KS, WN, EPI, 0, NS><<<dim3((unsigned)nwg), 256 * KS, G::LDS, st>>>(A, lda, W, M, N, K, n_mt,
+                                                                                           splits, sbps, C, ldc, g_qmm2_rot);
     MXK_CHECK_LAUNCH();
 }
 
+// ks: 1 / 2 waves per column group; ks | 8 selects the 8-slot ring (64-row tiles only)
 template <int QT, int EPI>
 static int dispatch_qmm2(int wm, int ks, int wn, const uint16_t* A, int lda, const uint8_t* W, int M, int N, int K,
                          int splits, void* C, int ldc, hipStream_t st) {
 #define Q2_CASE(WM_, KS_, WN_)                 \
     if (wm == WM_ && ks == KS_ && wn == WN_) \
         return launch_qmm2<QT, WM_, KS_, WN_, EPI>(A, lda, W, M, N, K, splits, C, ldc, st);
+#define Q2_DEEP(WM_, KS_, WN_)                     \
+    if (wm == WM_ && ks == (KS_ | 8) && wn == WN_) \
+        return launch_qmm2<QT, WM_, KS_, WN_, EPI, 8>(A, lda, W, M, N, K, splits, C, ldc, st);
     // (8, 2, 1) / (4, 2, 2) (256-row tiles with 8 waves) exceed the 256 registers a wave has at 2 waves / SIMD
     Q2_CASE(2, 1, 1) Q2_CASE(2, 2, 1) Q2_CASE(4, 1, 1) Q2_CASE(4, 2, 1) Q2_CASE(8, 1, 1)
     Q2_CASE(1, 2, 2) Q2_CASE(2, 1, 2) Q2_CASE(2, 2, 2) Q2_CASE(4, 1, 2)
+    Q2_DEEP(2, 1, 1) Q2_DEEP(2, 2, 1) Q2_DEEP(1, 2, 2)
+#undef Q2_DEEP
 #undef Q2_CASE
     return (int)hipErrorInvalidValue;
 }

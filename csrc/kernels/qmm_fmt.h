@@ -1,4 +1,4 @@
-// qmm_fmt.h — shared by qmm.hip (monolithic LDS-DMA ring GEMM) and qmm_ws.hip (warp-specialised variant):
+// qmm_fmt.h — the t32 format geometry and B-fragment decoders of qmm.hip (monolithic LDS-DMA ring GEMM):
 // the t32 tiled weight layouts, per-wave LDS geometry, the swizzled 16-bit tile addressing, counted-vmcnt
 // ring waits and the per-format B-fragment builders (raw block bytes in LDS -> f16x8 MFMA operands).
 #pragma once

@@ -59,10 +59,8 @@ def _jobs():
     return max(1, min(n, 16))
 
 
-# per-source extra flags. qmm8.hip: MFMA results in VGPRs (gfx950's unified register file) — the integer
-# sub-block scales are applied by VALU right after every MFMA, and AGPR results would cost one
-# v_accvgpr_read per element.
-FILE_FLAGS = {"qmm8.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]}
+# per-source extra compiler flags (none at present)
+FILE_FLAGS: dict = {}
 
 
 _INC = __import__("re").compile(r'^\s*#\s*include\s*"([^"]+)"', __import__("re").M)

@@ -27,9 +27,6 @@ U64 = C.c_uint64
 KERNEL_SIGS = {
     "mxk_rmsnorm": [P, I, P, I, P, P, P, I, P, P, I, I, F, P],
     "mxk_quant_q8": [P, I, P, P, I, I, P],
-    "mxk_quant_q8k": [P, I, I, P, P, P, I, I, P],
-    "mxk_rmsnorm_q8k": [P, I, P, P, I, P, P, P, I, I, F, P],
-    "mxk_qmm8": [I, I, I, I, I, I, I, P, I, P, P, P, I, I, I, I, P, I, P],
     "mxk_layernorm": [P, I, P, I, P, P, P, P, P, I, I, I, F, P],
     "mxk_groupnorm_nhwc": [P, P, P, P, I, I, I, I, F, I, P],
     "mxk_layernorm_mod": [P, I, P, P, I, I, P, I, I, I, F, P],
@@ -48,7 +45,6 @@ KERNEL_SIGS = {
     "mxk_qmv1_enable": [I],
     "mxk_qmv1_rope": [I, P, P, F, P, I, I, I, P, P, P, P, F, I, I, I, P, P, P, I, P],
     "mxk_qmm3_dbg": [I, I, P, I, P, I, I, I, P, I, P],
-    "mxk_qmm_ws": [I, I, I, P, I, P, I, I, I, I, P, I, P],
     "mxk_qmm_ws_dbg": [I],
     "mxk_qmv": [I, I, P, P, P, I, I, I, I, P, I, P],
     "mxk_qmv_x": [I, I, I, P, I, P, F, P, I, I, I, I, P, I, P],
@@ -121,6 +117,10 @@ def _load(name: str):
             f"{path} is missing: build it with `python -m localai_tfp_amd._build` "
             "(or __graft_entry__.build())")
     return C.CDLL(str(path), mode=C.RTLD_GLOBAL)
+
+
+def kernel_lib_path():
+    return _LIBDIR / "libmxk.so"
 
 
 def kernels():

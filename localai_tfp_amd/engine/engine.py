@@ -81,6 +81,7 @@ def gc_tune():
 class EngineConfig:
     max_num_seqs: int = 256
     max_batched_tokens: int = 2048
+    prefill_chunk: int | None = None  # prompt tokens per sequence per step (None: the whole step budget)
     max_model_len: int = 8192
     block_size: int = 16
     num_blocks: int | None = None  # None -> size from free HBM
@@ -94,9 +95,9 @@ class EngineConfig:
     mixed_graph_seqs: int = 4
     max_graphs: int = 64
     attn_part_size: int = 256  # must match ops.core.attn_decode's default
-    # dense 16-bit copy of the layer projections for hipBLASLt (ops/linear.py DENSE_MIN_M_*). Off: the
-    # int8-MFMA kernels on Q8_K activations (qmm8.hip) run every M > 4 GEMM on the quantised weights;
-    # MX_DENSE_CACHE=1 restores the copy (A/B only; it costs 2 B/param of HBM)
+    # dense 16-bit copy of the layer projections for hipBLASLt (ops/linear.py DENSE_MIN_M_*). Off: the K-quant
+    # MFMA kernels (qmm2 / qmm3) run every M > 4 GEMM on the quantised weights; MX_DENSE_CACHE=1 restores the copy
+    # (A/B only; it costs 2 B/param of HBM)
     prefill_bf16_cache: bool = __import__("os").environ.get("MX_DENSE_CACHE", "0") == "1"
     kv_dtype: str = "bf16"  # paged KV cache element type: bf16 | fp8 (OCP e4m3, half the bytes per token)
     # overlap the host with the GPU: launch step N, then read step N-1's sampled tokens (async
@@ -368,7 +369,8 @@ class LLMEngine:
                 self.cfg.use_graphs = False  # a network hop cannot live inside a hipGraph
             self.kv = KVCache(nl, nb, model.n_kv, c.block_size, mc.head_dim, self.device, self.kv_dtype)
         self.bm = make_block_manager(nb, c.block_size, c.enable_prefix_cache)
-        self.sched = Scheduler(self.bm, c.block_size, c.max_num_seqs, c.max_batched_tokens, c.max_model_len)
+        self.sched = Scheduler(self.bm, c.block_size, c.max_num_seqs, c.max_batched_tokens, c.max_model_len,
+                               prefill_chunk=c.prefill_chunk)
         max_parts = max(1, -(-c.max_model_len // c.attn_part_size))
         if self.recurrent:
             self.ws = model.make_workspace(max(c.max_batched_tokens, c.max_num_seqs), c.max_num_seqs)
@@ -391,6 +393,10 @@ class LLMEngine:
                           out_tokens=0, finished=0, sched_s=0.0, plan_s=0.0, fwd_s=0.0, fwd_graph_s=0.0, wait_s=0.0,
                           process_s=0.0)
         self.last_metrics = {}
+        # per-step host timeline (t0, scheduled, launched, sampler launched, committed, wait s, done, graph, nd,
+        # prefill tokens, sampled rows) when MX_STEP_TRACE is set
+        self.trace = [] if os.environ.get("MX_STEP_TRACE") else None
+        self._trace_wait = 0.0
         self.on_step = None  # optional hook called with the step index before each loop step (bench)
         self.batch_sink: BatchedSink | None = None
         if c.prefill_bf16_cache and self.device.type == "cuda" and hasattr(model, "enable_prefill_bf16_cache"):
@@ -687,6 +693,7 @@ class LLMEngine:
         if roctx.ENABLED:
             roctx.push("launch graph" if plan["graph"] else "launch eager")
         logits, am = self._execute(plan)
+        t_exec = time.perf_counter()
         tok_dev, lp_dev = None, None
         steps = [it.seq.n_generated for it in items]  # sampler step index (seed advance) of each row's sample
         for it in items:  # this step's samples are in flight from here on (their KV blocks must stay)
@@ -731,7 +738,7 @@ class LLMEngine:
             new = None
         if roctx.ENABLED:
             roctx.pop()
-        t2 = time.perf_counter()
+        t_samp = t2 = time.perf_counter()
         self.sched.commit(so)
         if new is not None:
             self._inflight.append(new)
@@ -747,6 +754,10 @@ class LLMEngine:
             else:
                 self._process_inflight(prev)
         t3 = time.perf_counter()
+        if self.trace is not None:  # host timeline of this step (MX_STEP_TRACE; tools: bench.py dumps it)
+            self.trace.append((t0, t1, t_exec, t_samp, t2, self._trace_wait, t3, bool(plan["graph"]), len(so.decode),
+                               sum(p.n for p in so.prefill), len(items)))
+            self._trace_wait = 0.0
         st = self.stats
         st["sched_s"] += t1 - t0
         st["fwd_s"] += t2 - t1
@@ -768,6 +779,8 @@ class LLMEngine:
             else:
                 ev.synchronize()
         self.stats["wait_s"] += time.perf_counter() - t0
+        if self.trace is not None:
+            self._trace_wait += time.perf_counter() - t0
         self._check_collectives()
         S = len(items)
         toks = self._pin_tok[k][:S].tolist()

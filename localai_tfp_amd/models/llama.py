@@ -36,7 +36,7 @@ from ..formats.gguf import QType
 from ..ops import core as K
 from ..ops import quant as Q
 from ..ops.linear import (ACT_DTYPE, EPI_ADD_F32, EPI_BF16, EPI_F32, EPI_GEGLU, EPI_SWIGLU, QWeight, concat_rows,
-                          _fp32_out_ok, dense_min_m, interleave_gate_up, qmatmul, qmatmul8, qmm8_ok, qmv_fusable, qmv_rope_ok,
+                          _fp32_out_ok, dense_min_m, interleave_gate_up, qmatmul, qmv_fusable, qmv_rope_ok,
                           qmv_fused, qmv_rope_fused)
 from ..ops.moe import MoEWeights, moe_ffn
 from .config import LlamaConfig
@@ -147,10 +147,6 @@ class Workspace:
             self.am_keys = torch.empty(max_seqs, dtype=torch.int64, device=dev)
             self.am_keys_all = torch.empty(tp_size * max_seqs, dtype=torch.int64, device=dev)
             self.moe_y = torch.empty((T, H), dtype=torch.float32, device=dev) if cfg.n_expert else None
-        # Q8_K activation blocks for the int8-MFMA GEMMs (ops/linear.qmatmul8): codes, per-256 scales, bsums
-        self.k8q = torch.empty((T * kmax,), dtype=torch.int8, device=dev)
-        self.k8d = torch.empty((T * kmax // 256,), dtype=torch.float32, device=dev)
-        self.k8bs = torch.empty((T * kmax // 16,), dtype=torch.float16, device=dev)
         nh = cfg.n_heads // tp_size
         self.part_ml = torch.empty((max_seqs * nh * max_parts, 2), dtype=torch.float32, device=dev)
         self.part_o = torch.empty((max_seqs * nh * max_parts, cfg.head_dim), dtype=torch.float32, device=dev)
@@ -172,10 +168,6 @@ class Workspace:
     def q8(self, M: int, K_: int):
         return self.xq[: M * K_].view(M, K_), self.xds[: M * K_ // 16].view(M, K_ // 32, 2)
 
-    def q8k(self, M: int, K_: int):
-        """Contiguous Q8_K operand views for M rows of width K_ (K_ % 256 == 0)."""
-        return K.Q8KAct(self.k8q[: M * K_].view(M, K_), self.k8d[: M * K_ // 256].view(M, K_ // 256),
-                        self.k8bs[: M * K_ // 16].view(M, K_ // 16))
 
 
 # decode batches of at least this many rows whose contexts are all <= SINGLE_PART_MAX keys run the decode
@@ -582,23 +574,12 @@ class LlamaModel:
             if fb.stop_layer is not None and li >= fb.stop_layer:
                 break
             kc, vc = kv.layer(li)
-            # int8-MFMA GEMMs on Q8_K activations for every projection of this layer (qmm8.hip)
-            use8 = not gemv and self._layer_i8(L)
             # ---- attention block ----
             qkv = ws.qkv[:T]
-            if use8:
-                a8 = ws.q8k(T, H)
-                K.rmsnorm_q8k(h, L.attn_norm, eps, a8)
-                off = 0
-                for w in L.qkv_parts:
-                    qmatmul8(w, a8, EPI_F32, qkv[:, off:off + w.N] if len(L.qkv_parts) > 1 else qkv, out_zeroed=True)
-                    off += w.N
             # batch <= 4: RMSNorm + q8 quantisation fused into each projection's GEMV prologue
             fuse_in = gemv and T <= QMV_FUSE_MAX_M
             fuse_qkv = fuse_in and all(qmv_fusable(w, T, EPI_F32, True) for w in L.qkv_parts)
-            if use8:
-                pass
-            elif fuse_qkv:
+            if fuse_qkv:
                 xq = xds = None
             elif gemv:
                 xq, xds = ws.q8(T, H)
@@ -608,8 +589,8 @@ class LlamaModel:
                 xq = xds = None
             if not gemv and not qkv.is_cuda:
                 qkv.zero_()
-            off = qkv.shape[1] if use8 else 0
-            if (not use8 and not gemv and L.qkv_dense is not None and qkv.is_cuda and xb.dtype == L.qkv_dense.dtype
+            off = 0
+            if (not gemv and L.qkv_dense is not None and qkv.is_cuda and xb.dtype == L.qkv_dense.dtype
                     and T >= dense_min_m(xb.dtype, EPI_F32, True) and _fp32_out_ok(xb.dtype)):
                 torch.mm(xb, L.qkv_dense.t(), out_dtype=torch.float32, out=qkv)
                 off = qkv.shape[1]
@@ -655,11 +636,7 @@ class LlamaModel:
                 K.attn_prefill(q[nd:].view(T - nd, Hq, D), kc, vc, fb.pf_block_tables, fb.pf_cu_q, fb.pf_ctx_lens,
                                self.scale, attn[nd:].view(T - nd, Hq, D), fb.pf_q_lens_host, fb.pf_ctx_lens_host,
                                window=L.window, softcap=cfg.attn_softcap, tiles=fb.pf_tiles)
-            if use8:
-                a8o = ws.q8k(T, qd)
-                K.quant_q8k(attn, a8o)
-                self._residual_proj(L.wo, None, None, None, h, L.post_attn_norm, ws, T, eps, a8=a8o)
-            elif fuse_in and L.post_attn_norm is None and self.tp_size == 1 and qmv_fusable(L.wo, T, EPI_ADD_F32):
+            if fuse_in and L.post_attn_norm is None and self.tp_size == 1 and qmv_fusable(L.wo, T, EPI_ADD_F32):
                 qmv_fused(L.wo, attn, EPI_ADD_F32, h)  # h += attn W_o^T, q8 quantisation in the prologue
             else:
                 if gemv:
@@ -681,14 +658,6 @@ class LlamaModel:
                     moe_ffn(L.moe, xb, h)
                 continue
             act = ws.act[:T]
-            if use8:
-                a8 = ws.q8k(T, H)
-                K.rmsnorm_q8k(h, L.ffn_norm, eps, a8)
-                qmatmul8(L.wgu, a8, self.glu_epi, act)
-                a8f = ws.q8k(T, F)
-                K.quant_q8k(act, a8f)
-                self._residual_proj(L.wd, None, None, None, h, L.post_ffn_norm, ws, T, eps, a8=a8f)
-                continue
             fuse_gu = fuse_in and L.wgu is not None and qmv_fusable(L.wgu, T, self.glu_epi)
             if fuse_gu:
                 pass
@@ -734,11 +703,7 @@ class LlamaModel:
                 return hn
             self.last_hidden = hn
         logits = ws.logits[:S] if self.tp_size == 1 else ws.logits_local[:S]
-        if S > GEMV_MAX_M and qmm8_ok(self.lm_head):
-            a8 = ws.q8k(S, H)
-            K.rmsnorm_q8k(hs, self.out_norm, eps, a8)
-            qmatmul8(self.lm_head, a8, EPI_F32, logits)
-        elif S <= GEMV_MAX_M and self.device.type == "cuda" and isinstance(self.lm_head, QWeight) and \
+        if S <= GEMV_MAX_M and self.device.type == "cuda" and isinstance(self.lm_head, QWeight) and \
                 qmv_fused(self.lm_head, hs, EPI_F32, logits, norm=self.out_norm, eps=eps):
             pass  # final RMSNorm + q8 quantisation in the LM-head GEMV prologue (one launch)
         elif S <= GEMV_MAX_M and self.device.type == "cuda" and self.lm_head.is_quant:
@@ -847,23 +812,11 @@ class LlamaModel:
             out[:, lo:min(V, lo + vl)] = g[r * S:(r + 1) * S, :min(V, lo + vl) - lo]
         return out
 
-    def _layer_i8(self, L) -> bool:
-        """Every projection of this dense layer runs on the int8-MFMA kernels (cached per layer)."""
-        v = getattr(L, "_i8", None)
-        if v is None:
-            ws_ = [*L.qkv_parts, L.wo, L.wgu, L.wd]
-            v = (L.moe is None and L.wgu is not None and all(w is not None and qmm8_ok(w) for w in ws_)
-                 and all(w.bf16_cache is None for w in ws_) and L.qkv_dense is None)
-            L._i8 = v
-        return v
-
-    def _residual_proj(self, W: QWeight, x, xq, xds, h: torch.Tensor, post_norm, ws: Workspace, T: int, eps: float,
-                       a8=None):
+    def _residual_proj(self, W: QWeight, x, xq, xds, h: torch.Tensor, post_norm, ws: Workspace, T: int, eps: float):
         """h += x W^T — or, with a Gemma post-norm, h += rmsnorm(x W^T) * post_norm. Under tensor
         parallelism each rank's partial projection is all-reduced in 16 bits (half the fp32 residual's
-        bytes; one message per row-parallel projection) and added to the replicated residual. `a8`: Q8_K
-        activations for the int8-MFMA GEMM instead of x / (xq, xds)."""
-        mm = qmatmul if a8 is None else (lambda W_, x_, epi, out, xq=None, xds=None: qmatmul8(W_, a8, epi, out))
+        bytes; one message per row-parallel projection) and added to the replicated residual."""
+        mm = qmatmul
         gemv = xq is not None
         if self.tp_size > 1:
             y16 = ws.y16[:T]

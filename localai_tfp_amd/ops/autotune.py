@@ -130,9 +130,26 @@ def _cache_path() -> str:
                                                            "gemm_tune.json")
 
 
+_LIB_TAG = None
+
+
+def _lib_tag() -> str:
+    """Hash of the kernel library: plans tuned against another build of the kernels are not reused."""
+    global _LIB_TAG
+    if _LIB_TAG is None:
+        import hashlib
+        from .. import _native as N
+        try:
+            with open(N.kernel_lib_path(), "rb") as f:
+                _LIB_TAG = hashlib.sha1(f.read()).hexdigest()[:12]
+        except (OSError, AttributeError):
+            _LIB_TAG = "unknown"
+    return _LIB_TAG
+
+
 def _device_tag() -> str:
     p = torch.cuda.get_device_properties(torch.cuda.current_device())
-    return f"{p.name}|{getattr(p, 'gcnArchName', '')}|{p.multi_processor_count}|v1"
+    return f"{p.name}|{getattr(p, 'gcnArchName', '')}|{p.multi_processor_count}|{_lib_tag()}"
 
 
 def load_cache() -> dict:

@@ -77,92 +77,6 @@ def quant_q8(x: torch.Tensor, xq: torch.Tensor, xds: torch.Tensor):
     N.kcall("mxk_quant_q8", x.data_ptr(), x.stride(0), xq.data_ptr(), xds.data_ptr(), M, K, N.stream_ptr())
 
 
-class Q8KAct:
-    """Activations in llama.cpp's Q8_K block format (the int8-MFMA GEMM operand, ops/linear.qmatmul8):
-    q int8 [M, K], d fp32 [M, K/256] (one scale per 256-element block), bs f16 [M, K/16] (int sums of
-    every 16 codes, exact in f16). Views of preallocated workspace buffers."""
-
-    __slots__ = ("q", "d", "bs")
-
-    def __init__(self, q: torch.Tensor, d: torch.Tensor, bs: torch.Tensor):
-        self.q, self.d, self.bs = q, d, bs
-
-    @classmethod
-    def empty(cls, M: int, K: int, device) -> "Q8KAct":
-        return cls(torch.empty(M, K, dtype=torch.int8, device=device),
-                   torch.empty(M, K // 256, dtype=torch.float32, device=device),
-                   torch.empty(M, K // 16, dtype=torch.float16, device=device))
-
-    def rows(self, M: int, K: int) -> "Q8KAct":
-        return Q8KAct(self.q[:M, :K], self.d[:M, :K // 256], self.bs[:M, :K // 16])
-
-    def dequant(self) -> torch.Tensor:
-        M, K = self.q.shape
-        return (self.q.float().reshape(M, K // 256, 256) * self.d.float()[..., None]).reshape(M, K)
-
-
-def quant_q8k_ref(y: torch.Tensor, out: Q8KAct):
-    """ggml quantize_row_q8_K on fp32 rows: per 256 block, max = the element of largest |x| (first on
-    ties), iscale = -127 / max, q = min(127, round-half-even(iscale * x)), d = 1 / iscale, bsums per 16."""
-    M, K = y.shape
-    b = y.float().reshape(M, K // 256, 256)
-    ax = b.abs()
-    idx = ax.argmax(-1, keepdim=True)  # first maximum
-    mx = torch.gather(b, -1, idx)[..., 0]
-    amax = ax.amax(-1)
-    iscale = torch.where(amax > 0, torch.tensor(-127.0) / torch.where(amax > 0, mx, torch.ones_like(mx)),
-                         torch.zeros_like(mx))
-    q = torch.round(iscale[..., None] * b).clamp(max=127)
-    out.q.copy_(q.reshape(M, K).to(torch.int8))
-    out.d.copy_(torch.where(amax > 0, 1.0 / torch.where(amax > 0, iscale, torch.ones_like(iscale)),
-                            torch.zeros_like(iscale)))
-    out.bs.copy_(q.reshape(M, K // 16, 16).sum(-1).to(torch.float16))
-
-
-def quant_q8k(x: torch.Tensor, out: Q8KAct):
-    """16-bit (act16) or fp32 rows [M, K] -> Q8_K blocks (K % 256 == 0)."""
-    M, K = x.shape
-    if M == 0:
-        return out
-    if not x.is_cuda:
-        quant_q8k_ref(x.float(), out)
-        return out
-    f32 = x.dtype == torch.float32
-    if not f32:
-        N.ensure_act(x.dtype)
-    N.kcall("mxk_quant_q8k", x.data_ptr(), x.stride(0), int(f32), out.q.data_ptr(), out.d.data_ptr(),
-            out.bs.data_ptr(), M, K, N.stream_ptr())
-    return out
-
-
-def rmsnorm_q8k(x: torch.Tensor, w: torch.Tensor, eps: float, out: Q8KAct, out_act: torch.Tensor | None = None):
-    """RMSNorm of fp32 rows straight into Q8_K blocks (and, with out_act, the 16-bit rows too)."""
-    M, H = x.shape
-    if M == 0:
-        return out
-    if not x.is_cuda or H % 1024 or H > 8192:
-        y = x * torch.rsqrt(x.pow(2).mean(-1, keepdim=True) + eps) * w if not x.is_cuda else None
-        if y is None:  # GPU, odd hidden size: two passes
-            tmp = out_act if out_act is not None else torch.empty(M, H, dtype=N_act_dtype(), device=x.device)
-            rmsnorm(x, w, eps, out_bf16=tmp)
-            return quant_q8k(tmp, out)
-        if out_act is not None:
-            out_act.copy_(y)
-        quant_q8k_ref(y, out)
-        return out
-    if out_act is not None:
-        N.ensure_act(out_act.dtype)
-    N.kcall("mxk_rmsnorm_q8k", x.data_ptr(), x.stride(0), w.data_ptr(), N.ptr(out_act),
-            out_act.stride(0) if out_act is not None else 0, out.q.data_ptr(), out.d.data_ptr(), out.bs.data_ptr(),
-            M, H, float(eps), N.stream_ptr())
-    return out
-
-
-def N_act_dtype():
-    from .linear import ACT_DTYPE
-    return ACT_DTYPE
-
-
 def layernorm(x: torch.Tensor, g: torch.Tensor | None, b: torch.Tensor | None, eps: float,
               out: torch.Tensor, residual: torch.Tensor | None = None, xsum: torch.Tensor | None = None):
     """fp32 x [M, H] (+ residual) -> layernorm -> out (bf16 or fp32)."""

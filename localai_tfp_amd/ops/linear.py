@@ -360,11 +360,6 @@ def _qmatmul_t32(W: QWeight, x, epi: int, out, xq, xds, M: int, out_zeroed: bool
         return out
     if x is None or x.dtype != torch.float16:
         raise ValueError("qmatmul: t32 weights need f16 activations (or q8 activations with M <= 4)")
-    if int(W.qtype) in (int(q) for q in Q.QMM8_ONLY):
-        # formats with int8-MFMA kernels only: quantise the rows to Q8_K on the fly
-        from .core import Q8KAct, quant_q8k
-        a = quant_q8k(x, Q8KAct.empty(M, W.K, x.device))
-        return qmatmul8(W, a, epi, out, out_zeroed=out_zeroed)
     can_split = epi == EPI_ADD_F32 or (epi == EPI_F32 and out_zeroed)
     if W.bf16_cache is not None and M >= dense_min_m(x.dtype, epi, can_split) and W.bf16_cache.dtype == x.dtype:
         return _dense_cached(W, x, epi, out, M)
@@ -374,21 +369,7 @@ def _qmatmul_t32(W: QWeight, x, epi: int, out, xq, xds, M: int, out_zeroed: bool
         if len(row_chunks(M)) > 1:
             plan = ("rows", ROW_CHUNK)
         else:
-            pick = _gemm_pick(M, W.N, W.K, int(W.qtype), can_split)
-            if pick is None:
-                ws = _qmm_ws_shape(M, W.N, W.K, can_split, int(W.qtype))
-                if ws is not None:
-                    cfg, splits = ws
-                    e = EPI_ADD_F32 if (epi == EPI_F32 and splits > 1) else epi
-                    if e in (EPI_BF16, *GLU_EPIS):
-                        if out.dtype != x.dtype:
-                            raise ValueError(f"qmatmul: {out.dtype} output with {x.dtype} activations")
-                        N.ensure_act(out.dtype)
-                    N.kcall("mxk_qmm_ws", int(W.qtype), e, cfg, x.data_ptr(), x.stride(0), W.data.data_ptr(), M, W.N,
-                            W.K, splits, out.data_ptr(), out.stride(0), N.stream_ptr())
-                    return out
-            else:
-                plan = pick
+            plan = _gemm_pick(M, W.N, W.K, int(W.qtype), can_split)
     if plan is not None:
         return run_plan(plan, W, x, epi, out, out_zeroed)
     wm, wn, nw, ks, splits = _qmm_shape(M, W.N, W.K, can_split)
@@ -399,59 +380,6 @@ def _qmatmul_t32(W: QWeight, x, epi: int, out, xq, xds, M: int, out_zeroed: bool
         N.ensure_act(out.dtype)
     N.kcall("mxk_qmm", int(W.qtype), e, wm, wn, nw, ks, x.data_ptr(), x.stride(0), W.data.data_ptr(), None,
             M, W.N, W.K, splits, out.data_ptr(), out.stride(0), N.stream_ptr())
-    return out
-
-
-# ------------------------------------------------------------------------------------------------
-# int8-MFMA GEMM on Q8_K activations (csrc/kernels/qmm8.hip): llama.cpp's K-quant dot-product numerics.
-QMM8 = os.environ.get("MX_QMM8", "0") == "1"  # off by default: slower than qmm.hip at every tuned shape (profiles/r3_tune_qmm8.jsonl)
-QMM8_FORCE: tuple | None = None  # (wm, wn, nw, wmw, occ, splits) override for tuning (tools/tune_qmm8.py)
-QMM8_CONFIGS = ((2, 1, 4, 1, 1), (2, 1, 4, 2, 1), (2, 1, 4, 1, 2), (1, 2, 4, 2, 1), (2, 1, 8, 1, 1),
-                (1, 2, 2, 2, 1), (1, 2, 4, 1, 2))
-
-
-def qmm8_ok(W) -> bool:
-    """Weight eligible for the int8-MFMA path (t32 Q4_K / Q6_K on the GPU)."""
-    return (QMM8 and isinstance(W, QWeight) and W.layout == "t32" and W.data.is_cuda
-            and int(W.qtype) in (int(QType.Q4_K), int(QType.Q6_K), int(QType.Q5_K)))
-
-
-def _qmm8_shape(M: int, N_: int, K: int, can_split: bool):
-    if QMM8_FORCE is not None:
-        wm, wn, nw, wmw, occ, splits = QMM8_FORCE
-        return wm, wn, nw, wmw, occ, (splits if can_split else 1)
-    if M <= 64:
-        wm, wn, nw, wmw, occ = 2, 1, 4, 1, 2
-    else:
-        wm, wn, nw, wmw, occ = 2, 1, 4, 2, 1
-    bm, bn = 32 * wm * wmw, 32 * wn * nw
-    tiles = -(-M // bm) * -(-N_ // bn)
-    splits = 1
-    if can_split:
-        while tiles * splits < (3 * CU_COUNT) // 4 and (K // 256) // (splits * 2) >= 2:
-            splits *= 2
-    return wm, wn, nw, wmw, occ, splits
-
-
-def qmatmul8(W: QWeight, a, epi: int, out: torch.Tensor, *, out_zeroed: bool = False):
-    """out (+)= A @ W^T for Q8_K activations `a` (ops.core.Q8KAct) and a t32 Q4_K / Q6_K weight
-    (qmm8_ok). CPU: fp32 reference on the dequantised operands."""
-    M = a.q.shape[0]
-    if M == 0:
-        return out
-    if not a.q.is_cuda:
-        return _qmatmul_ref(W, a.dequant(), epi, out)
-    can_split = epi == EPI_ADD_F32 or (epi == EPI_F32 and out_zeroed)
-    wm, wn, nw, wmw, occ, splits = _qmm8_shape(M, W.N, W.K, can_split)
-    e = EPI_ADD_F32 if (epi == EPI_F32 and splits > 1) else epi
-    if e in (EPI_BF16, *GLU_EPIS):
-        if out.dtype != torch.float16:
-            raise ValueError("qmatmul8: 16-bit outputs are f16")
-        N.ensure_act(out.dtype)
-    if a.q.stride(0) % 16 or not a.d.is_contiguous() or not a.bs.is_contiguous():
-        raise ValueError("qmatmul8: Q8_K operand needs 16-B aligned code rows and contiguous d / bsums")
-    N.kcall("mxk_qmm8", int(W.qtype), e, wm, wn, nw, wmw, occ, a.q.data_ptr(), a.q.stride(0), a.d.data_ptr(),
-            a.bs.data_ptr(), W.data.data_ptr(), M, W.N, W.K, splits, out.data_ptr(), out.stride(0), N.stream_ptr())
     return out
 
 
@@ -624,7 +552,9 @@ def _qmm_shape(M: int, N_: int, K: int, can_split: bool):
 QMM2 = os.environ.get("MX_QMM2", "0") != "0"
 QMM2_FORCE: tuple | None = None  # (wm, ks, wn, splits) override for tuning (tools/tune_qmm2.py)
 # compiled (wm, ks, wn): wm 32-row MFMA blocks x wn 32-column groups per wave, ks 1 / 2 waves per SIMD
-QMM2_CONFIGS = ((2, 1, 1), (2, 2, 1), (4, 1, 1), (4, 2, 1), (8, 1, 1), (1, 2, 2), (2, 1, 2), (2, 2, 2), (4, 1, 2))
+QMM2_CONFIGS = ((2, 1, 1), (2, 2, 1), (4, 1, 1), (4, 2, 1), (8, 1, 1), (1, 2, 2), (2, 1, 2), (2, 2, 2), (4, 1, 2),
+                # ks | 8: the 8-slot LDS ring (64-row tiles)
+                (2, 9, 1), (2, 10, 1), (1, 10, 2))
 QMM2_QTYPES = (int(QType.Q4_K), int(QType.Q6_K), int(QType.Q3_K), int(QType.Q2_K), int(QType.Q5_K))
 QMM2_ONLY = tuple(int(q) for q in Q.QMM2_ONLY)  # no qmm.hip variant: qmm2 for every M > 4
 QMM2_MIN_M = int(os.environ.get("MX_QMM2_MIN_M", "16"))
@@ -653,7 +583,7 @@ def _gemm_pick(M: int, N_: int, K: int, qtype: int, can_split: bool):
         return ("q3", *_qmm3_shape(M, N_, K, can_split))
     if (QMM2 and M >= QMM2_MIN_M) or qtype in QMM2_ONLY:
         return ("q2", *_qmm2_shape(M, N_, K, can_split))
-    if GEMM_POLICY != "auto" or M < 16 or QMM_FORCE is not None or QMM_WS_FORCE is not None:
+    if GEMM_POLICY != "auto" or M < 16 or QMM_FORCE is not None:
         return None
     nct = -(-N_ // 128)
     wide = N_ >= 16384
@@ -709,38 +639,6 @@ def _qmm2_shape(M: int, N_: int, K: int, can_split: bool):
         while tiles * splits < (3 * CU_COUNT) // 4 and nsb // (splits * 2) >= 2:
             splits *= 2
     return wm, ks, wn, splits
-
-
-# qmm_ws.hip: warp-specialised variant (4 producer waves: LDS-DMA + dequant into an f16 B tile; 4 MFMA-only
-# consumer waves). cfg = CM*10000 + WM*1000 + WN*100 + GP*10 + LEAD: consumer grid CM x (4/CM), wave tile
-# 32WM x 32WN, GP weight groups (32 columns) per producer wave (BN = 128 GP), producers LEAD k-tiles ahead;
-# + AD*100000: A fragments read by the consumers into an AD-deep register ring instead of an LDS tile.
-QMM_WS = os.environ.get("MX_QMM_WS", "0") == "1"
-QMM_WS_FORCE: tuple | None = None  # (cfg, splits) override for tuning (tools/tune_qmm_ws.py)
-QMM_WS_CONFIGS = (22211, 22212, 24211, 22421, 12111, 12112, 12221, 41411, 41412, 441412, 242412, 241821, 422212)
-
-
-def qmm_ws_geom(cfg: int):
-    """-> (BM, BN) of a qmm_ws configuration."""
-    cm, wm, wn = (cfg // 10000) % 10, (cfg // 1000) % 10, (cfg // 100) % 10
-    return 32 * wm * cm, 32 * wn * (4 // cm)
-
-
-def _qmm_ws_shape(M: int, N_: int, K: int, can_split: bool, qtype: int):
-    """(cfg, splits) for the warp-specialised qmm, or None for the monolithic kernel."""
-    if QMM_WS_FORCE is not None:
-        cfg, splits = QMM_WS_FORCE
-        return cfg, (splits if can_split else 1)
-    if not QMM_WS or M < 64:
-        return None
-    cfg = 22212 if M <= 128 else 24211
-    bm, bn = qmm_ws_geom(cfg)
-    tiles = -(-M // bm) * -(-N_ // bn)
-    splits = 1
-    if can_split:
-        while tiles * splits < (3 * CU_COUNT) // 4 and (K // 64) // (splits * 2) >= 8:
-            splits *= 2
-    return cfg, splits
 
 
 def _mfma32_shape(M: int, N_: int, nblk: int, can_split: bool):

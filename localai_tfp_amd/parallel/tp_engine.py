@@ -34,7 +34,7 @@ import torch
 log = logging.getLogger("localai_tfp_amd.tp")
 
 MAGIC = 0x4D585450  # "MXTP"
-K_PLAN, K_STOP, K_CAPTURE, K_PICKLE, K_HEARTBEAT = 1, 2, 3, 4, 5
+K_PLAN, K_STOP, K_CAPTURE, K_PICKLE, K_HEARTBEAT, K_PART = 1, 2, 3, 4, 5, 6
 PLAN_ARRAYS = ("tokens", "positions", "slots", "lidx", "dec_bt", "dec_lens", "pf_bt", "pf_cu", "pf_ctx",
                "pf_tseq", "pf_tq0", "fix_dst", "fix_src")
 EXIT_TP_FAILURE = 75
@@ -175,8 +175,12 @@ class TPLink:
                 try:
                     b = None if body is None else np.ascontiguousarray(body, np.int32)
                     if b is not None and b.nbytes > self.shm.max_body():
-                        self.shm.send(K_PICKLE)  # oversized plan: object over gloo
-                        dist.broadcast_object_list([decode_plan(b)], src=self.src, group=self.cpu_group)
+                        # oversized plan (long prompts, many sequences): raw int32 pieces through the same ring,
+                        # the last one carrying the message kind — no pickling
+                        per = self.shm.max_body() // 4
+                        for o in range(0, b.size - per, per):
+                            self.shm.send(K_PART, b[o:o + per])
+                        self.shm.send(kind, b[(b.size - 1) // per * per:])
                     else:
                         self.shm.send(kind, b)
                         if kind == K_PICKLE:
@@ -206,7 +210,15 @@ class TPLink:
             from .shm_channel import ChannelDead
             try:
                 kind, raw = self.shm.recv()
-                body = np.frombuffer(raw, np.int32).copy() if raw else None
+                parts = []
+                while kind == K_PART:  # pieces of an oversized message (see _send)
+                    parts.append(np.frombuffer(raw, np.int32))
+                    kind, raw = self.shm.recv()
+                if parts:
+                    parts.append(np.frombuffer(raw, np.int32))
+                    body = np.concatenate(parts)
+                else:
+                    body = np.frombuffer(raw, np.int32).copy() if raw else None
                 obj = None
                 if kind == K_PICKLE:
                     buf = [None]

@@ -76,6 +76,24 @@ def main():
     ar.check(block=True)
     ok &= dt < 0.02 and busy
     print(f"rank {rank} nonblocking check {dt * 1e3:.2f} ms (stream busy={busy}) ok={ok}", flush=True)
+    # per-call latency at 16 KB and 1 MB (all ranks issue back to back; on the 1-GPU box the ranks share one GPU,
+    # so this measures the protocol, not xGMI)
+    for nbytes in (16 << 10, 1 << 20):
+        t = torch.ones(nbytes // 2, device=dev, dtype=torch.float16)
+        dist.barrier()
+        for _ in range(5):
+            ar(t)
+        torch.cuda.synchronize()
+        dist.barrier()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(20):
+            ar(t)
+        e1.record()
+        torch.cuda.synchronize()
+        ar.check(block=True)
+        print(f"rank {rank} world {world} allreduce {nbytes >> 10} KB: {e0.elapsed_time(e1) / 20 * 1e3:.1f} us/call",
+              flush=True)
     dist.barrier()
     ar.close()
     dist.destroy_process_group()

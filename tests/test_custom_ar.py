@@ -20,7 +20,7 @@ def _port():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_one_shot_allreduce_multiprocess(world):
     port = _port()
     procs = []
@@ -39,3 +39,6 @@ def test_one_shot_allreduce_multiprocess(world):
         outs.append(out)
     for r, (p, o) in enumerate(zip(procs, outs)):
         assert p.returncode == 0, f"rank {r} rc={p.returncode}\n{o[-3000:]}"
+    for ln in outs[0].splitlines():  # rank 0's latency lines into the test log
+        if "us/call" in ln:
+            print(ln)

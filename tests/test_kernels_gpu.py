@@ -440,7 +440,7 @@ def test_qmm(qt, M, wm, wn, nw, ks, splits, monkeypatch):
     (64, 2, 1, 1, 1), (64, 2, 2, 1, 3), (17, 2, 2, 1, 1), (128, 4, 2, 1, 1), (77, 4, 2, 1, 2), (128, 4, 1, 1, 4),
     (256, 8, 1, 1, 1), (300, 8, 1, 1, 3), (511, 8, 1, 1, 1), (100, 2, 1, 1, 5),
     (64, 1, 2, 2, 1), (40, 1, 2, 2, 3), (128, 2, 1, 2, 1), (200, 2, 2, 2, 2), (256, 4, 1, 2, 1), (300, 4, 1, 2, 3),
-    (511, 4, 1, 2, 2)])
+    (511, 4, 1, 2, 2), (64, 2, 9, 1, 1), (300, 2, 10, 1, 3), (100, 2, 10, 1, 8), (40, 1, 10, 2, 1), (200, 1, 10, 2, 5)])
 def test_qmm2(qt, M, wm, ks, wn, splits, monkeypatch):
     """qmm2.hip for every epilogue and tile / split-K choice, incl. ragged M / N tails (416 columns = 3.25
     workgroup tiles; with wn = 2 a wave's second group may lie past N), split counts that do not divide the

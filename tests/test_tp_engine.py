@@ -223,3 +223,41 @@ def test_vocab_parallel_argmax(world):
     for p in ps:
         p.join(timeout=60)
     assert got == want and got[1] == 7 and got[2] == 0
+
+
+def _big_plan_worker(rank, world, port, q):
+    import numpy as np
+    import torch.distributed as dist
+    link = _link(rank, world, port, heartbeat_s=0)
+    assert link.shm is not None
+    n = link.shm.max_body() // 4 * 2 + 12345  # > 2 ring slots of int32: three raw pieces
+    plan = {"nd": 3, "graph": False, "tokens": np.arange(n, dtype=np.int32), "positions": np.arange(7, dtype=np.int32)}
+    if rank == 0:
+        link.send_plan(plan)
+        link.send_plan({"nd": 1, "graph": False, "tokens": np.array([5], np.int32)})
+        link.send_plan(None)
+        q.put("sent")
+    else:
+        got = link.recv_plan()
+        small = link.recv_plan()
+        stop = link.recv_plan()
+        ok = (got["nd"] == 3 and np.array_equal(got["tokens"], plan["tokens"])
+              and np.array_equal(got["positions"], plan["positions"]) and small["tokens"].tolist() == [5]
+              and stop is None)
+        q.put(("recv", ok))
+    link.close()
+    dist.destroy_process_group()
+
+
+def test_oversized_plan_raw_pieces():
+    """A plan larger than one shared-memory ring slot travels as raw int32 pieces (no pickle fallback)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_big_plan_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(2)]
+    for p in ps:
+        p.join(timeout=60)
+    assert "sent" in res and ("recv", True) in res, res

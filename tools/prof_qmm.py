@@ -22,7 +22,6 @@ def main():
     ap.add_argument("--cfg", default="")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--gemv", action="store_true", help="M <= 4 decode GEMV with the fused RMSNorm / q8 prologue")
-    ap.add_argument("--ws", default="", help="qmm_ws cfg,splits (warp-specialised kernel)")
     ap.add_argument("--q2", default="", help="qmm2 wm,ks,wn,splits")
     ap.add_argument("--qmv1", type=int, default=1, help="0: disable the batch-1 fast-prologue GEMV (qmv1_kernel)")
     ap.add_argument("--q3dbg", default="", help="qmm3 isolation build dbg,wm (Q4_K SwiGLU only)")
@@ -35,8 +34,6 @@ def main():
     qt = a.qt or qt
     W = L.QWeight.from_ggml(random_quantized(np.random.default_rng(1), qt, N, K), qt, N, K, "cuda", t32=True)
     assert W.to_t32()
-    if a.ws:
-        L.QMM_WS_FORCE = tuple(int(v) for v in a.ws.split(","))
     if a.cfg:
         L.QMM_FORCE = tuple(int(v) for v in a.cfg.split(","))
     if a.q2:
