@@ -340,8 +340,12 @@ def main():
         }
         print(json.dumps(out), flush=True)
         if eng.trace is not None:
+            torch.cuda.synchronize() if dev.type == "cuda" else None
+            ev = eng.trace_events[-(args.steps + 50):]
+            # device time of each step (launch marker -> sampler end) and the device idle before the next one
+            gpu = [[a.elapsed_time(b), b.elapsed_time(c)] for (a, b), (c, _) in zip(ev, ev[1:])]
             with open(os.environ["MX_STEP_TRACE"], "w") as f:
-                json.dump(eng.trace, f)
+                json.dump({"host": eng.trace, "gpu_ms": gpu}, f)
         if os.environ.get("MX_TUNE_REPORT"):
             from localai_tfp_amd.ops import autotune
             with open(os.environ["MX_TUNE_REPORT"], "w") as f:

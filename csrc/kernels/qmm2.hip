@@ -41,7 +41,7 @@ extern "C" int mxk_qmm2_dbg(int dbg, int wm, int ks, int wn, const uint16_t* A, 
     return qmm2_dbg_q4k(dbg, wm, ks, wn, A, lda, W, M, N, K, C, ldc, st);
 }
 
-// A f16 [M, K] (lda % 8 == 0, 16-B aligned), W t32 Q4_K / Q5_K / Q6_K / Q3_K / Q2_K [N, K] (N % 32 == 0, K % 256 == 0).
+// A f16 [M, K] (lda % 8 == 0, 16-B aligned), W t32 Q4_K / Q5_K / Q6_K / Q3_K / Q2_K / Q8_0 / MX4F / MX5F [N, K] (N % 32 == 0, K % 256 == 0).
 // epi: 0 fp32 store, 1 f16 store, 2 fp32 accumulate (split-K via atomics when splits > 1), 3/4 SwiGLU /
 // GeGLU over 16-row interleaved gate|up -> f16 [M, N/2]. wm: 32-row MFMA blocks per wave; wn: 32-column groups
 // per wave (BM = 32 wm wn); ks: 1 (4 waves) or 2 (8 waves, k-steps split per wave pair). splits: K split in
@@ -57,6 +57,9 @@ extern "C" int mxk_qmm2(int qtype, int epi, int wm, int ks, int wn, const uint16
         case MXQ_Q6_K: return qmm2_run_q6k(epi, wm, ks, wn, A, lda, W, M, N, K, splits, C, ldc, st);
         case MXQ_Q3_K: return qmm2_run_q3k(epi, wm, ks, wn, A, lda, W, M, N, K, splits, C, ldc, st);
         case MXQ_Q2_K: return qmm2_run_q2k(epi, wm, ks, wn, A, lda, W, M, N, K, splits, C, ldc, st);
+        case MXQ_Q8_0: return qmm2_run_q80(epi, wm, ks, wn, A, lda, W, M, N, K, splits, C, ldc, st);
+        case MXQ_MX4F: return qmm2_run_mx4(epi, wm, ks, wn, A, lda, W, M, N, K, splits, C, ldc, st);
+        case MXQ_MX5F: return qmm2_run_mx5(epi, wm, ks, wn, A, lda, W, M, N, K, splits, C, ldc, st);
     }
     return (int)hipErrorInvalidValue;
 }

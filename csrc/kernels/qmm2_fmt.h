@@ -50,6 +50,26 @@ struct Q2F<MXQ_Q2_K> {
     static constexpr int qoff(int jq) { return 640 + (jq >> 1) * 1024; }
 };
 
+// MX4F / MX5F t32 unit (Q4_0 / Q4_1 / Q5_0 / Q5_1 carried exactly at 4 / 5 bits): [hdr: 2 halves x 32 x 16 B {f16 s[4],
+// m[4]}, k-tiles 0-1 read half 0, 2-3 half 1][k-tile jq: 2 x (32 x 16 B codes) (+ MX5F: 32 x 8 B high bits)]
+template <>
+struct Q2F<MXQ_MX4F> {
+    static constexpr int UNIT = 5120, HB = 1024, QB = 1024, QI = 1, HI = 1;
+    static constexpr int qoff(int jq) { return 1024 + jq * 1024; }
+};
+template <>
+struct Q2F<MXQ_MX5F> {
+    static constexpr int UNIT = 6144, HB = 1024, QB = 1280, QI = 2, HI = 1;
+    static constexpr int qoff(int jq) { return 1024 + jq * 1280; }
+};
+// Q8_0 t32 unit per 64-k tile: [d: 32 x {f16 d0, f16 d1}][4 k-steps x (32 x 16 B int8 codes)] (2176 B); a "super-block"
+// here is 4 such tiles, and each tile's scales travel with its codes (no header)
+template <>
+struct Q2F<MXQ_Q8_0> {
+    static constexpr int UNIT = 4 * 2176, HB = 0, QB = 2176, QI = 3, HI = 0;
+    static constexpr int qoff(int jq) { return jq * 2176; }
+};
+
 template <int QT>
 struct Q2B;
 
@@ -302,5 +322,138 @@ struct Q2B<MXQ_Q2_K> {
         return r;
     }
 };
+
+// MX4F / MX5F: weight = s * code + m per 32 (f16 s, m); code = nibble (| bit 4 from the k-tile's high-bit word)
+template <bool FIVE>
+struct Q2BMX {
+    u32x4 h0, h1;        // header halves (k-tiles 0-1 / 2-3): {s[4], m[4]} of the half's 4 blocks of 32
+    u32x2 v0, v1;
+    uint32_t vh0, vh1;   // high-bit words of this lane's k, pre-shifted by 8 h
+    f16x2 s2[2], m2[2];
+    MX_DEV void load_hdr(const char* hb, int col, int) {
+        h0 = *(const u32x4*)(hb + col * 16);
+        h1 = *(const u32x4*)(hb + 512 + col * 16);
+    }
+    MX_DEV void load_q(const char* qb, int col, int h) {
+        v0 = *(const u32x2*)(qb + col * 16 + 8 * h);
+        v1 = *(const u32x2*)(qb + 512 + col * 16 + 8 * h);
+        if constexpr (FIVE) {
+            const u32x2 w = *(const u32x2*)(qb + 1024 + col * 8);
+            vh0 = w[0] >> (8 * h);
+            vh1 = w[1] >> (8 * h);
+        }
+    }
+    template <int JQ>
+    MX_DEV void prep() {
+        // blocks 2 (JQ & 1), + 1 of the half: word JQ & 1 of the scale pairs, word 2 + (JQ & 1) of the offsets
+        const u32x4 hh = (JQ >> 1) ? h1 : h0;
+        const uint32_t sw = hh[JQ & 1], mw = hh[2 + (JQ & 1)];
+        const f16x2 sv = __builtin_bit_cast(f16x2, sw), mv = __builtin_bit_cast(f16x2, mw);
+        s2[0] = (f16x2){sv[0], sv[0]};
+        s2[1] = (f16x2){sv[1], sv[1]};
+        m2[0] = (f16x2){mv[0], mv[0]};
+        m2[1] = (f16x2){mv[1], mv[1]};
+    }
+    template <int JQ, int S>
+    MX_DEV f16x8 frag() const {
+        const u32x2 src = (S & 1) ? v1 : v0;
+        constexpr int sh = 4 * (S >> 1);
+        uint32_t t0 = (src[0] >> sh) & 0x0F0F0F0Fu, t1 = (src[1] >> sh) & 0x0F0F0F0Fu;
+        if constexpr (FIVE) {
+            const uint32_t hw = ((S >> 1) ? vh1 : vh0) >> (16 * (S & 1));
+            t0 |= mx_spread4(hw) << 4;
+            t1 |= mx_spread4(hw >> 4) << 4;
+        }
+        const f16x2 k = {(_Float16)1024.f, (_Float16)1024.f};
+        f16x2 p[4];
+        magic4(t0, p[0], p[1]);
+        magic4(t1, p[2], p[3]);
+        f16x8 r;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const f16x2 v = (p[i] - k) * s2[S >> 1] + m2[S >> 1];
+            r[2 * i] = v[0];
+            r[2 * i + 1] = v[1];
+        }
+        return r;
+    }
+};
+template <>
+struct Q2B<MXQ_MX4F> : Q2BMX<false> {};
+template <>
+struct Q2B<MXQ_MX5F> : Q2BMX<true> {};
+
+// Q8_0: weight = d * int8 code per 32; k-step S of a tile reads codes chunk S, block S >> 1's scale
+template <>
+struct Q2B<MXQ_Q8_0> {
+    u32x2 qv[4];
+    uint32_t dw;
+    f16x2 s2[2];
+    MX_DEV void load_hdr(const char*, int, int) {}
+    MX_DEV void load_q(const char* qb, int col, int h) {
+        dw = *(const uint32_t*)(qb + col * 4);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) qv[s] = *(const u32x2*)(qb + 128 + (s * 32 + col) * 16 + 8 * h);
+    }
+    template <int JQ>
+    MX_DEV void prep() {
+        const f16x2 dd = __builtin_bit_cast(f16x2, dw);
+        s2[0] = (f16x2){dd[0], dd[0]};
+        s2[1] = (f16x2){dd[1], dd[1]};
+    }
+    template <int JQ, int S>
+    MX_DEV f16x8 frag() const {
+        const uint32_t t0 = qv[S][0] ^ 0x80808080u, t1 = qv[S][1] ^ 0x80808080u;  // int8 -> u8 + 128
+        const f16x2 k = {(_Float16)1152.f, (_Float16)1152.f};                     // 1024 magic + 128
+        f16x2 p[4];
+        magic4(t0, p[0], p[1]);
+        magic4(t1, p[2], p[3]);
+        f16x8 r;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const f16x2 v = (p[i] - k) * s2[S >> 1];
+            r[2 * i] = v[0];
+            r[2 * i + 1] = v[1];
+        }
+        return r;
+    }
+};
+
+// LDS-DMA of one 32-column group's weight bytes for k-tile JQ of a super-block (unit `u`): the tile's quant bytes
+// (F::QB: whole 1 KB pieces plus one partial piece, F::QI instructions) into `qd` and, with the super-block's first
+// tile, its header (F::HB bytes in the format's layout, F::HI instructions) into `hd`.
+template <int QT, int JQ>
+MX_DEV void q2_stage_weights(const uint8_t* u, char* qd, char* hd, int lane) {
+    using F = Q2F<QT>;
+    const uint8_t* qs = u + F::qoff(JQ);
+    constexpr int NF = F::QB / 1024, REM = F::QB % 1024;
+    static_assert(NF + (REM ? 1 : 0) == F::QI && REM % 16 == 0, "quant piece count");
+#pragma unroll
+    for (int i = 0; i < NF; ++i)
+        __builtin_amdgcn_global_load_lds((const void*)(qs + i * 1024 + lane * 16), (MX_LDS void*)(qd + i * 1024), 16, 0,
+                                         0);
+    if constexpr (REM > 0) {
+        if (lane < REM / 16)
+            __builtin_amdgcn_global_load_lds((const void*)(qs + NF * 1024 + lane * 16), (MX_LDS void*)(qd + NF * 1024),
+                                             16, 0, 0);
+    }
+    if constexpr (JQ == 0) {
+        if constexpr (QT == MXQ_Q3_K) {  // hdr (512 B) + hmask (1 KB): one full and one half instruction
+            __builtin_amdgcn_global_load_lds((const void*)(u + lane * 16), (MX_LDS void*)hd, 16, 0, 0);
+            if (lane < 32)
+                __builtin_amdgcn_global_load_lds((const void*)(u + 1024 + lane * 16), (MX_LDS void*)(hd + 1024), 16, 0, 0);
+        } else if constexpr (QT == MXQ_MX4F || QT == MXQ_MX5F) {  // both header halves (1 KB)
+            __builtin_amdgcn_global_load_lds((const void*)(u + lane * 16), (MX_LDS void*)hd, 16, 0, 0);
+        } else if constexpr (F::HB > 0) {
+            if (lane < 32) __builtin_amdgcn_global_load_lds((const void*)(u + lane * 16), (MX_LDS void*)hd, 16, 0, 0);
+            if constexpr (QT == MXQ_Q6_K || QT == MXQ_Q2_K) {  // + the 32 x 4 B d (/ dmin) words
+                if (lane < 32)
+                    __builtin_amdgcn_global_load_lds((const void*)(u + 512 + lane * 4), (MX_LDS void*)(hd + 512), 4, 0, 0);
+            }
+            if constexpr (QT == MXQ_Q5_K)  // + the qh chunks (fifth bits of the whole super-block)
+                __builtin_amdgcn_global_load_lds((const void*)(u + F::QH + lane * 16), (MX_LDS void*)(hd + 512), 16, 0, 0);
+        }
+    }
+}
 
 }  // namespace

@@ -130,33 +130,7 @@ __global__ __launch_bounds__(256 * KS) void qmm2_kernel(const uint16_t* __restri
                                              16, 0, 0);
         if constexpr (decltype(wl_c)::value && QII > 0) {
             const uint8_t* u = wg + (size_t)sbw * F::UNIT;
-            const uint8_t* qs = u + F::qoff(JQ);
-            char* qd = sb + A_BYTES + cg * F::QB;
-            __builtin_amdgcn_global_load_lds((const void*)(qs + lane * 16), (MX_LDS void*)qd, 16, 0, 0);
-            if constexpr (QT == MXQ_Q6_K) {
-                if (lane < 32)
-                    __builtin_amdgcn_global_load_lds((const void*)(qs + 1024 + lane * 16), (MX_LDS void*)(qd + 1024), 16,
-                                                     0, 0);
-            }
-            if constexpr (JQ == 0) {
-                char* hd = hdr_lds + hslot * G::HSZ + cg * F::HB;
-                if constexpr (QT == MXQ_Q3_K) {  // hdr (512 B) + hmask (1 KB): one full and one half instruction
-                    __builtin_amdgcn_global_load_lds((const void*)(u + lane * 16), (MX_LDS void*)hd, 16, 0, 0);
-                    if (lane < 32)
-                        __builtin_amdgcn_global_load_lds((const void*)(u + 1024 + lane * 16), (MX_LDS void*)(hd + 1024),
-                                                         16, 0, 0);
-                } else {
-                    if (lane < 32) __builtin_amdgcn_global_load_lds((const void*)(u + lane * 16), (MX_LDS void*)hd, 16, 0, 0);
-                    if constexpr (QT == MXQ_Q6_K || QT == MXQ_Q2_K) {  // + the 32 x 4 B d (/ dmin) words
-                        if (lane < 32)
-                            __builtin_amdgcn_global_load_lds((const void*)(u + 512 + lane * 4), (MX_LDS void*)(hd + 512), 4,
-                                                             0, 0);
-                    }
-                    if constexpr (QT == MXQ_Q5_K)  // + the qh chunks (fifth bits of the whole super-block)
-                        __builtin_amdgcn_global_load_lds((const void*)(u + F::QH + lane * 16), (MX_LDS void*)(hd + 512), 16,
-                                                         0, 0);
-                }
-            }
+            q2_stage_weights<QT, JQ>(u, sb + A_BYTES + cg * F::QB, hdr_lds + hslot * G::HSZ + cg * F::HB, lane);
         }
     };
 
@@ -417,12 +391,15 @@ static int launch_qmm2(const uint16_t* A, int lda, const uint8_t* W, int M, int 
 template <int QT, int EPI>
 static int dispatch_qmm2(int wm, int ks, int wn, const uint16_t* A, int lda, const uint8_t* W, int M, int N, int K,
                          int splits, void* C, int ldc, hipStream_t st) {
-#define Q2_CASE(WM_, KS_, WN_)                 \
-    if (wm == WM_ && ks == KS_ && wn == WN_) \
-        return launch_qmm2<QT, WM_, KS_, WN_, EPI>(A, lda, W, M, N, K, splits, C, ldc, st);
-#define Q2_DEEP(WM_, KS_, WN_)                     \
-    if (wm == WM_ && ks == (KS_ | 8) && wn == WN_) \
-        return launch_qmm2<QT, WM_, KS_, WN_, EPI, 8>(A, lda, W, M, N, K, splits, C, ldc, st);
+// (configurations whose ring does not fit the LDS for this format — 256-row tiles of Q8_0 — are not compiled)
+#define Q2_CASE(WM_, KS_, WN_)                                                                \
+    if constexpr (Q2Geom<QT, WM_, KS_, WN_, 4>::LDS <= 160 * 1024)                            \
+        if (wm == WM_ && ks == KS_ && wn == WN_)                                              \
+            return launch_qmm2<QT, WM_, KS_, WN_, EPI>(A, lda, W, M, N, K, splits, C, ldc, st);
+#define Q2_DEEP(WM_, KS_, WN_)                                                                   \
+    if constexpr (Q2Geom<QT, WM_, KS_, WN_, 8>::LDS <= 160 * 1024)                               \
+        if (wm == WM_ && ks == (KS_ | 8) && wn == WN_)                                           \
+            return launch_qmm2<QT, WM_, KS_, WN_, EPI, 8>(A, lda, W, M, N, K, splits, C, ldc, st);
     // (8, 2, 1) / (4, 2, 2) (256-row tiles with 8 waves) exceed the 256 registers a wave has at 2 waves / SIMD
     Q2_CASE(2, 1, 1) Q2_CASE(2, 2, 1) Q2_CASE(4, 1, 1) Q2_CASE(4, 2, 1) Q2_CASE(8, 1, 1)
     Q2_CASE(1, 2, 2) Q2_CASE(2, 1, 2) Q2_CASE(2, 2, 2) Q2_CASE(4, 1, 2)
@@ -470,4 +447,7 @@ int qmm2_run_q5k(int epi, int wm, int ks, int wn, const uint16_t* A, int lda, co
 int qmm2_run_q6k(int epi, int wm, int ks, int wn, const uint16_t* A, int lda, const uint8_t* W, int M, int N, int K, int splits, void* C, int ldc, hipStream_t st);
 int qmm2_run_q3k(int epi, int wm, int ks, int wn, const uint16_t* A, int lda, const uint8_t* W, int M, int N, int K, int splits, void* C, int ldc, hipStream_t st);
 int qmm2_run_q2k(int epi, int wm, int ks, int wn, const uint16_t* A, int lda, const uint8_t* W, int M, int N, int K, int splits, void* C, int ldc, hipStream_t st);
+int qmm2_run_q80(int epi, int wm, int ks, int wn, const uint16_t* A, int lda, const uint8_t* W, int M, int N, int K, int splits, void* C, int ldc, hipStream_t st);
+int qmm2_run_mx4(int epi, int wm, int ks, int wn, const uint16_t* A, int lda, const uint8_t* W, int M, int N, int K, int splits, void* C, int ldc, hipStream_t st);
+int qmm2_run_mx5(int epi, int wm, int ks, int wn, const uint16_t* A, int lda, const uint8_t* W, int M, int N, int K, int splits, void* C, int ldc, hipStream_t st);
 int qmm2_dbg_q4k(int dbg, int wm, int ks, int wn, const uint16_t* A, int lda, const uint8_t* W, int M, int N, int K, void* C, int ldc, hipStream_t st);

@@ -26,7 +26,7 @@ extern "C" int mxk_qmm3_dbg(int dbg, int wm, const uint16_t* A, int lda, const u
     return qmm3_dbg_q4k(dbg, wm, A, lda, W, M, N, K, C, ldc, st);
 }
 
-// A f16 [M, K] (lda % 8 == 0, 16-B aligned), W t32 Q4_K / Q5_K / Q6_K / Q3_K / Q2_K [N, K] (N % 32 == 0, K % 256 == 0).
+// A f16 [M, K] (lda % 8 == 0, 16-B aligned), W t32 Q4_K / Q5_K / Q6_K / Q3_K / Q2_K / Q8_0 / MX4F / MX5F [N, K] (N % 32 == 0, K % 256 == 0).
 // epi as mxk_qmm2 (split-K only with epi 2). wm: 32-row MFMA blocks per consumer wave, BM = 64 wm (1, 2, 4).
 extern "C" int mxk_qmm3(int qtype, int epi, int wm, const uint16_t* A, int lda, const uint8_t* W, int M, int N, int K,
                         int splits, void* C, int ldc, hipStream_t st) {
@@ -39,6 +39,9 @@ extern "C" int mxk_qmm3(int qtype, int epi, int wm, const uint16_t* A, int lda, 
         case MXQ_Q6_K: return qmm3_run_q6k(epi, wm, A, lda, W, M, N, K, splits, C, ldc, st);
         case MXQ_Q3_K: return qmm3_run_q3k(epi, wm, A, lda, W, M, N, K, splits, C, ldc, st);
         case MXQ_Q2_K: return qmm3_run_q2k(epi, wm, A, lda, W, M, N, K, splits, C, ldc, st);
+        case MXQ_Q8_0: return qmm3_run_q80(epi, wm, A, lda, W, M, N, K, splits, C, ldc, st);
+        case MXQ_MX4F: return qmm3_run_mx4(epi, wm, A, lda, W, M, N, K, splits, C, ldc, st);
+        case MXQ_MX5F: return qmm3_run_mx5(epi, wm, A, lda, W, M, N, K, splits, C, ldc, st);
     }
     return (int)hipErrorInvalidValue;
 }

@@ -84,33 +84,8 @@ __global__ __launch_bounds__(512) void qmm3_kernel(const uint16_t* __restrict__ 
             }
             if constexpr (DBG & 8) return;
             const uint8_t* u = wg + (size_t)sb * F::UNIT;
-            const uint8_t* qs = u + F::qoff(JQ);
-            char* qd = smem + G::OFF_Q + slot * G::QSZ + p * F::QB;
-            __builtin_amdgcn_global_load_lds((const void*)(qs + lane * 16), (MX_LDS void*)qd, 16, 0, 0);
-            if constexpr (QT == MXQ_Q6_K) {
-                if (lane < 32)
-                    __builtin_amdgcn_global_load_lds((const void*)(qs + 1024 + lane * 16), (MX_LDS void*)(qd + 1024), 16,
-                                                     0, 0);
-            }
-            if constexpr (JQ == 0) {
-                char* hd = smem + G::OFF_H + ((t >> 2) & 1) * G::HSZ + p * F::HB;
-                if constexpr (QT == MXQ_Q3_K) {
-                    __builtin_amdgcn_global_load_lds((const void*)(u + lane * 16), (MX_LDS void*)hd, 16, 0, 0);
-                    if (lane < 32)
-                        __builtin_amdgcn_global_load_lds((const void*)(u + 1024 + lane * 16), (MX_LDS void*)(hd + 1024),
-                                                         16, 0, 0);
-                } else {
-                    if (lane < 32) __builtin_amdgcn_global_load_lds((const void*)(u + lane * 16), (MX_LDS void*)hd, 16, 0, 0);
-                    if constexpr (QT == MXQ_Q6_K || QT == MXQ_Q2_K) {
-                        if (lane < 32)
-                            __builtin_amdgcn_global_load_lds((const void*)(u + 512 + lane * 4), (MX_LDS void*)(hd + 512), 4,
-                                                             0, 0);
-                    }
-                    if constexpr (QT == MXQ_Q5_K)  // + the qh chunks (fifth bits of the whole super-block)
-                        __builtin_amdgcn_global_load_lds((const void*)(u + F::QH + lane * 16), (MX_LDS void*)(hd + 512), 16,
-                                                         0, 0);
-                }
-            }
+            q2_stage_weights<QT, JQ>(u, smem + G::OFF_Q + slot * G::QSZ + p * F::QB,
+                                     smem + G::OFF_H + ((t >> 2) & 1) * G::HSZ + p * F::HB, lane);
         };
         // dequant of tile t (its bytes landed) into f16 B buffer t & 1
         Q2B<QT> bq;
@@ -366,4 +341,7 @@ int qmm3_run_q5k(int epi, int wm, const uint16_t* A, int lda, const uint8_t* W, 
 int qmm3_run_q6k(int epi, int wm, const uint16_t* A, int lda, const uint8_t* W, int M, int N, int K, int splits, void* C, int ldc, hipStream_t st);
 int qmm3_run_q3k(int epi, int wm, const uint16_t* A, int lda, const uint8_t* W, int M, int N, int K, int splits, void* C, int ldc, hipStream_t st);
 int qmm3_run_q2k(int epi, int wm, const uint16_t* A, int lda, const uint8_t* W, int M, int N, int K, int splits, void* C, int ldc, hipStream_t st);
+int qmm3_run_q80(int epi, int wm, const uint16_t* A, int lda, const uint8_t* W, int M, int N, int K, int splits, void* C, int ldc, hipStream_t st);
+int qmm3_run_mx4(int epi, int wm, const uint16_t* A, int lda, const uint8_t* W, int M, int N, int K, int splits, void* C, int ldc, hipStream_t st);
+int qmm3_run_mx5(int epi, int wm, const uint16_t* A, int lda, const uint8_t* W, int M, int N, int K, int splits, void* C, int ldc, hipStream_t st);
 int qmm3_dbg_q4k(int dbg, int wm, const uint16_t* A, int lda, const uint8_t* W, int M, int N, int K, void* C, int ldc, hipStream_t st);

@@ -36,7 +36,6 @@ KERNEL_SIGS = {
     "mxk_qgemm_mfma": [I, I, I, I, P, I, P, P, I, I, I, I, P, I, P],
     "mxk_qgemm16": [I, I, I, I, P, I, P, P, I, I, I, I, P, I, P],
     "mxk_qgemm32": [I, I, I, I, P, I, P, P, I, I, I, I, P, I, P],
-    "mxk_qmm": [I, I, I, I, I, I, P, I, P, P, I, I, I, I, P, I, P],
     "mxk_qmm2": [I, I, I, I, I, P, I, P, I, I, I, I, P, I, P],
     "mxk_qmm2_dbg": [I, I, I, I, P, I, P, I, I, I, P, I, P],
     "mxk_qmm2_set_rot": [I],

@@ -396,6 +396,7 @@ class LLMEngine:
         # per-step host timeline (t0, scheduled, launched, sampler launched, committed, wait s, done, graph, nd,
         # prefill tokens, sampled rows) when MX_STEP_TRACE is set
         self.trace = [] if os.environ.get("MX_STEP_TRACE") else None
+        self.trace_events = []  # (before launch, after sampler) device events per traced step
         self._trace_wait = 0.0
         self.on_step = None  # optional hook called with the step index before each loop step (bench)
         self.batch_sink: BatchedSink | None = None
@@ -692,6 +693,9 @@ class LLMEngine:
             self.tp.send_plan(plan)
         if roctx.ENABLED:
             roctx.push("launch graph" if plan["graph"] else "launch eager")
+        if self.trace is not None and self.device.type == "cuda":
+            ev0 = torch.cuda.Event(enable_timing=True)
+            ev0.record()
         logits, am = self._execute(plan)
         t_exec = time.perf_counter()
         tok_dev, lp_dev = None, None
@@ -739,6 +743,10 @@ class LLMEngine:
         if roctx.ENABLED:
             roctx.pop()
         t_samp = t2 = time.perf_counter()
+        if self.trace is not None and self.device.type == "cuda":
+            ev1 = torch.cuda.Event(enable_timing=True)
+            ev1.record()
+            self.trace_events.append((ev0, ev1))
         self.sched.commit(so)
         if new is not None:
             self._inflight.append(new)

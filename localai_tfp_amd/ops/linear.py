@@ -345,7 +345,7 @@ def run_plan(plan: tuple, W: QWeight, x: torch.Tensor, epi: int, out: torch.Tens
 
 
 def _qmatmul_t32(W: QWeight, x, epi: int, out, xq, xds, M: int, out_zeroed: bool):
-    """t32 tiled weights: qmv (q8 activations, M <= 4) or qmm (f16 activations, any M)."""
+    """t32 tiled weights: qmv (q8 activations, M <= 4) or qmm2 / qmm3 (f16 activations, any M; tuned plan)."""
     if M <= 4 and xq is not None:
         if epi in (EPI_BF16, *GLU_EPIS):
             N.ensure_act(out.dtype)
@@ -363,24 +363,14 @@ def _qmatmul_t32(W: QWeight, x, epi: int, out, xq, xds, M: int, out_zeroed: bool
     can_split = epi == EPI_ADD_F32 or (epi == EPI_F32 and out_zeroed)
     if W.bf16_cache is not None and M >= dense_min_m(x.dtype, epi, can_split) and W.bf16_cache.dtype == x.dtype:
         return _dense_cached(W, x, epi, out, M)
-    forced = QMM2 or QMM3 or QMM2_FORCE is not None or QMM3_FORCE is not None or QMM_FORCE is not None
+    forced = QMM2 or QMM3 or QMM2_FORCE is not None or QMM3_FORCE is not None
     plan = _AT.lookup(W.N, W.K, int(W.qtype), epi, can_split, M) if (_AT.TUNED and not forced) else None
     if plan is None:
         if len(row_chunks(M)) > 1:
             plan = ("rows", ROW_CHUNK)
         else:
             plan = _gemm_pick(M, W.N, W.K, int(W.qtype), can_split)
-    if plan is not None:
-        return run_plan(plan, W, x, epi, out, out_zeroed)
-    wm, wn, nw, ks, splits = _qmm_shape(M, W.N, W.K, can_split)
-    e = EPI_ADD_F32 if (epi == EPI_F32 and splits > 1) else epi
-    if e in (EPI_BF16, *GLU_EPIS):
-        if out.dtype != x.dtype:
-            raise ValueError(f"qmatmul: {out.dtype} output with {x.dtype} activations")
-        N.ensure_act(out.dtype)
-    N.kcall("mxk_qmm", int(W.qtype), e, wm, wn, nw, ks, x.data_ptr(), x.stride(0), W.data.data_ptr(), None,
-            M, W.N, W.K, splits, out.data_ptr(), out.stride(0), N.stream_ptr())
-    return out
+    return run_plan(plan, W, x, epi, out, out_zeroed)
 
 
 QMV_FUSE = os.environ.get("MX_QMV_FUSE", "1") != "0"
@@ -485,85 +475,21 @@ DENSE_MIN_M_SPLIT = int(os.environ.get("MX_DENSE_MIN_M_SPLIT", "192"))
 
 Q32_MIN_M = int(os.environ.get("MX_Q32_MIN_M", "48"))
 Q32_FORCE: tuple | None = None  # (wm, wn, splits) override for tuning (tools/tune_qgemm32.py)
-# qmm.hip (LDS-DMA ring, counted vmcnt) runs every f16 GEMM on t32-tiled weights
-QMM_FORCE: tuple | None = None  # (wm, wn, nw, ks, splits) override for tuning (tools/tune_qmm.py)
-# tile configurations compiled into qmm.hip (wm, wn, nw, ks)
-# ks field: bits 0-3 k-step split KS, bit 4 half-LDS ring (two workgroups per CU), bits 5-6 WMW - 1 (waves
-# splitting the rows of a column group: wave tile 32*wm x 32*wn, workgroup tile 32*wm*WMW x 32*wn*nw)
-def qmm_ks(ks: int = 1, occ2: bool = False, wmw: int = 1) -> int:
-    return ks | (16 if occ2 else 0) | ((wmw - 1) << 5)
-
-
-QMM_CONFIGS = ((1, 1, 4, 1), (2, 1, 4, 1), (4, 1, 4, 1), (1, 2, 4, 1), (2, 2, 4, 1), (4, 2, 4, 1), (2, 1, 8, 1),
-               (4, 1, 8, 1), (2, 2, 8, 1), (4, 2, 8, 1), (2, 1, 4, 2), (4, 1, 4, 2), (2, 2, 4, 2),
-               # ks | 16: half-LDS ring, two workgroups per CU
-               (2, 1, 4, 17), (4, 1, 4, 17), (2, 2, 4, 17), (2, 1, 4, 18),
-               # row-split wave grids
-               (2, 2, 2, 33), (4, 2, 2, 33), (2, 2, 2, 34), (2, 1, 4, 33), (4, 1, 4, 33), (2, 2, 4, 33),
-               (4, 2, 4, 33), (1, 2, 4, 33), (2, 2, 2, 49), (1, 2, 2, 97), (2, 2, 2, 97))
-
-
-def qmm_geom(wm: int, wn: int, nw: int, ks: int):
-    """-> (BM, BN, waves) of a qmm configuration."""
-    wmw = 1 + ((ks >> 5) & 3)
-    return 32 * wm * wmw, 32 * wn * nw, nw * (ks & 15) * wmw
-
-
-QMM_OCC = os.environ.get("MX_QMM_OCC", "1") != "0"  # A/B switch for the two-workgroups-per-CU tiles
-
-
-def _qmm_shape(M: int, N_: int, K: int, can_split: bool):
-    """qmm tile choice -> (wm, wn, nw, ks, splits): 32*wm-row x 32*wn*nw-column workgroup tiles with
-    nw*ks waves (ks waves per column group split each k-tile's k-steps; 8 waves = two per SIMD, which
-    overlap each other's dequant / LDS phases with MFMAs), K splits (fp32 atomics, split-able outputs
-    only) until the grid holds >= 2 workgroups per CU, keeping >= 8 k-tiles (512 k) per split. Fitted
-    to the tools/tune_qmm.py sweep (Llama-3-8B shapes, M 64..2048)."""
-    if QMM_FORCE is not None:
-        wm, wn, nw, ks, splits = QMM_FORCE
-        return wm, wn, nw, ks, (splits if can_split else 1)
-    # profiles/r2_qmm_tune_ks.jsonl (MI355X, Llama-3-8B projections): up to M = 512 the 4-column-group
-    # tiles with the k-steps split over two waves per group win; beyond, 8 column groups (BN 256/512)
-    # amortise the A-tile reads better. Split-K until ~3/4 of the CUs hold a workgroup.
-    if M <= 64 and QMM_OCC:
-        # two workgroups per CU (half-LDS ring, ks | 16): profiles/r2_qmm_tune_occ.jsonl M=64 — gate_up 37.6 vs
-        # 44.2 us, qkv 16.0 vs 16.8, wo 13.5 vs 14.2, down 24.6 vs 25.7
-        wm, wn, nw, ks = 2, 1, 4, 18
-    elif M <= 128 and QMM_OCC and can_split and N_ <= 6144 and K <= 4096:
-        # qkv 22.6 vs 23.8 us, o_proj 17.9 vs 18.3 at M=128 (same sweep)
-        wm, wn, nw, ks = 2, 1, 4, 18
-    elif M <= 512 and (can_split or M <= 128):
-        wm = 2 if (can_split and N_ <= 4096 and K <= 4096 and M <= 256) else 4
-        wn, nw, ks = 1, 4, 2
-    else:
-        wm, wn, nw, ks = 4, (2 if (M > 256 and N_ >= 6144) else 1), 8, 1
-    bm, bn, _ = qmm_geom(wm, wn, nw, ks)
-    mt = -(-M // bm)
-    cols = -(-N_ // bn)
-    splits = 1
-    if can_split:
-        while cols * mt * splits < (3 * CU_COUNT) // 4 and (K // 64) // (splits * 2) >= 8:
-            splits *= 2
-    return wm, wn, nw, ks, splits
 
 
 # qmm2.hip: second-generation quantised GEMM (wave tile = all BM rows x one 32-column group, super-block
 # unrolled k loop, 4-slot LDS-DMA ring) for the Q4_K_M formats. (wm, ks): BM = 32 wm rows, ks = 1 (4 waves)
 # or 2 (8 waves splitting each k-tile's k-steps); 128 columns per workgroup; K split in whole super-blocks.
 QMM2 = os.environ.get("MX_QMM2", "0") != "0"
-QMM2_FORCE: tuple | None = None  # (wm, ks, wn, splits) override for tuning (tools/tune_qmm2.py)
+QMM2_FORCE: tuple | None = None  # (wm, ks, wn, splits) override (tests, tools/prof_qmm.py)
 # compiled (wm, ks, wn): wm 32-row MFMA blocks x wn 32-column groups per wave, ks 1 / 2 waves per SIMD
 QMM2_CONFIGS = ((2, 1, 1), (2, 2, 1), (4, 1, 1), (4, 2, 1), (8, 1, 1), (1, 2, 2), (2, 1, 2), (2, 2, 2), (4, 1, 2),
                 # ks | 8: the 8-slot LDS ring (64-row tiles)
                 (2, 9, 1), (2, 10, 1), (1, 10, 2))
-QMM2_QTYPES = (int(QType.Q4_K), int(QType.Q6_K), int(QType.Q3_K), int(QType.Q2_K), int(QType.Q5_K))
-QMM2_ONLY = tuple(int(q) for q in Q.QMM2_ONLY)  # no qmm.hip variant: qmm2 for every M > 4
+# every t32 block format runs on qmm2 / qmm3 (qmm2_fmt.h decoders)
+QMM2_QTYPES = (int(QType.Q4_K), int(QType.Q6_K), int(QType.Q3_K), int(QType.Q2_K), int(QType.Q5_K), int(QType.Q8_0),
+               int(QType.MX4F), int(QType.MX5F))
 QMM2_MIN_M = int(os.environ.get("MX_QMM2_MIN_M", "16"))
-
-
-# K-quant GEMM choice (MX_GEMM_POLICY=auto): per (M bucket, shape class) the kernel / tile that won the round-4
-# sweep on the Llama-3-8B projections (profiles/r4_qmm_tune.md): qmm2 (one role per wave) for M <= 128 except the
-# narrow o_proj, qmm3 (warp-specialised) above; "r3" keeps the round-3 qmm.hip / qmm_ws path.
-GEMM_POLICY = os.environ.get("MX_GEMM_POLICY", "auto")
 
 
 def _split_for(tiles: int, K: int, can_split: bool) -> int:
@@ -576,27 +502,23 @@ def _split_for(tiles: int, K: int, can_split: bool) -> int:
 
 
 def _gemm_pick(M: int, N_: int, K: int, qtype: int, can_split: bool):
-    """("q3", wm, splits) | ("q2", wm, ks, wn, splits) | None (round-3 kernels) for a t32 K-quant GEMM."""
-    if qtype not in QMM2_QTYPES:
-        return None
+    """Untuned fallback plan ("q3", wm, splits) | ("q2", wm, ks, wn, splits) for a t32 GEMM — shapes the load-time
+    autotuner (ops/autotune.py) did not time. The rule follows the tuned Llama-3-8B table
+    (profiles/r5_gemm_autotune.md): 64-row 8-wave qmm2 tiles for the narrow projections, 128-row tiles for the
+    wide ones, qmm3 for the gated FFN at 129-256 rows."""
     if QMM3 and M >= QMM3_MIN_M:  # explicit overrides (tests, tuning)
         return ("q3", *_qmm3_shape(M, N_, K, can_split))
-    if (QMM2 and M >= QMM2_MIN_M) or qtype in QMM2_ONLY:
+    if QMM2 and M >= QMM2_MIN_M:
         return ("q2", *_qmm2_shape(M, N_, K, can_split))
-    if GEMM_POLICY != "auto" or M < 16 or QMM_FORCE is not None:
-        return None
     nct = -(-N_ // 128)
     wide = N_ >= 16384
-    if M <= 64:
+    if M <= 64 or (not wide and K < 8192 and M <= 256):
         return ("q2", 2, 2, 1, _split_for(-(-M // 64) * nct, K, can_split))
-    if M <= 128:
-        if not wide and K < 8192 and N_ <= 4096:  # o_proj
-            return ("q3", 1, _split_for(-(-M // 64) * nct, K, can_split))
-        if not wide and K >= 8192:  # down
-            return ("q2", 2, 1, 1, _split_for(-(-M // 64) * nct, K, can_split))
-        return ("q2", 4, 2, 1, _split_for(-(-M // 128) * nct, K, can_split))
-    wm = 4 if wide else (1 if (N_ <= 4096 and K < 8192 and M <= 256) else 2)
-    return ("q3", wm, _split_for(-(-M // (64 * wm)) * nct, K, can_split))
+    if wide and 128 < M <= 256:
+        return ("q3", 4, 1)
+    if not wide and M > 256 and K < 8192:
+        return ("q2", 4, 2, 1, 1)
+    return ("q2", 4, 2, 1, _split_for(-(-M // 128) * nct, K, can_split))
 
 
 # qmm3.hip: warp-specialised (4 DMA / dequant waves + 4 MFMA waves per workgroup), BM = 64 wm rows

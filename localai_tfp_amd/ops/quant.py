@@ -586,8 +586,6 @@ GPU_NATIVE = (QType.Q4_K, QType.Q6_K, QType.Q8_0, QType.Q5_K, QType.MX4F, QType.
 # that cannot be tiled (N % 32, expert stacks) is carried on the Q8_0 kernels instead (QWeight.ensure_kernel_layout;
 # Q3_K exactly, Q2_K re-quantised)
 T32_ONLY = (QType.Q5_K, QType.MX4F, QType.MX5F, QType.Q3_K, QType.Q2_K)
-# formats whose M > 4 GEMM is qmm2.hip only (no qmm.hip variant)
-QMM2_ONLY = (QType.Q3_K, QType.Q2_K, QType.Q5_K)
 
 # Block formats without a dedicated kernel layout yet, carried on the Q8_0 kernels (qmm / qmv) instead of
 # a dense 16-bit copy: the integer code of every weight is kept EXACTLY where the format is "scale x

@@ -392,50 +392,7 @@ def test_qgemm32(qt, M, wm, wn, splits, monkeypatch):
     assert rel(sw, ref_sw) < 1e-2
 
 
-@pytest.mark.parametrize("qt", [QType.Q4_K, QType.Q6_K, QType.Q8_0])
-@pytest.mark.parametrize("M,wm,wn,nw,ks,splits", [
-    (64, 2, 1, 4, 1, 1), (77, 4, 2, 4, 1, 2), (128, 4, 1, 4, 1, 1), (128, 2, 2, 4, 1, 4), (200, 4, 2, 4, 1, 3),
-    (300, 4, 1, 4, 1, 2), (7, 1, 1, 4, 1, 2), (33, 1, 2, 4, 1, 1), (100, 2, 1, 8, 1, 2), (300, 4, 2, 8, 1, 1),
-    (129, 4, 1, 8, 1, 3), (64, 2, 2, 8, 1, 1), (128, 4, 1, 4, 2, 1), (77, 2, 1, 4, 2, 2), (200, 2, 2, 4, 2, 3),
-    (5, 4, 1, 4, 2, 1),
-    # ks | 16: half-LDS ring, two workgroups per CU
-    (128, 2, 1, 4, 17, 1), (77, 4, 1, 4, 17, 2), (200, 2, 2, 4, 17, 3), (130, 2, 1, 4, 18, 2), (64, 4, 1, 4, 17, 1)])
-def test_qmm(qt, M, wm, wn, nw, ks, splits, monkeypatch):
-    """qmm.hip (LDS-DMA ring GEMM) for every epilogue and tile / split-K choice, incl. ragged M / N
-    tails, split counts that do not divide the k-tiles, the in-workgroup k-step split (ks = 2) and the
-    two-workgroups-per-CU ring (ks | 16)."""
-    from localai_tfp_amd.ops import linear as L
-    if ks >= 16 and wm == 4 and qt == QType.Q6_K:
-        pytest.skip("a Q6_K 128-row stage does not fit a half-LDS ring of 3 k-tiles")
-    monkeypatch.setattr(L, "QMM_FORCE", (wm, wn, nw, ks, splits))
-    monkeypatch.setattr(L, "QMM2", False)
-    n, k = 416, 2304  # 416 = 3.25 x 128 columns: partial column tiles (multiple of 32 for the GLU)
-    raw, dense = make_w(qt, n, k, seed=M + 7 * wm + 3 * wn)
-    W = QWeight.from_ggml(raw, qt, n, k, DEV, t32=True)
-    assert W.to_t32() and W.layout == "t32"
-    x = torch.randn(M, k, device=DEV).half()
-    ref = x.float().cpu() @ dense.t()
-    out = torch.empty(M, n, device=DEV)
-    qmatmul(W, x, EPI_F32, out)
-    assert rel(out, ref) < 5e-3
-    z = torch.zeros(M, n, device=DEV)
-    qmatmul(W, x, EPI_F32, z, out_zeroed=True)
-    assert rel(z, ref) < 5e-3
-    acc = torch.randn(M, n, device=DEV)
-    acc0 = acc.clone()
-    qmatmul(W, x, EPI_ADD_F32, acc)
-    assert rel(acc - acc0, ref) < 5e-3
-    ob = torch.empty(M, n, dtype=torch.float16, device=DEV)
-    qmatmul(W, x, EPI_BF16, ob)
-    assert rel(ob, ref) < 5e-3
-    sw = torch.empty(M, n // 2, dtype=torch.float16, device=DEV)
-    qmatmul(W, x, EPI_SWIGLU, sw)
-    g = ref.reshape(M, n // 32, 2, 16)
-    ref_sw = torch.nn.functional.silu(g[:, :, 0].reshape(M, -1)) * g[:, :, 1].reshape(M, -1)
-    assert rel(sw, ref_sw) < 1e-2
-
-
-@pytest.mark.parametrize("qt", [QType.Q4_K, QType.Q6_K, QType.Q3_K, QType.Q2_K, QType.Q5_K])
+@pytest.mark.parametrize("qt", [QType.Q4_K, QType.Q6_K, QType.Q3_K, QType.Q2_K, QType.Q5_K, QType.Q8_0])
 @pytest.mark.parametrize("M,wm,ks,wn,splits", [
     (64, 2, 1, 1, 1), (64, 2, 2, 1, 3), (17, 2, 2, 1, 1), (128, 4, 2, 1, 1), (77, 4, 2, 1, 2), (128, 4, 1, 1, 4),
     (256, 8, 1, 1, 1), (300, 8, 1, 1, 3), (511, 8, 1, 1, 1), (100, 2, 1, 1, 5),
@@ -475,7 +432,7 @@ def test_qmm2(qt, M, wm, ks, wn, splits, monkeypatch):
     assert rel(sw, ref_sw) < 1e-2
 
 
-@pytest.mark.parametrize("qt", [QType.Q4_K, QType.Q6_K, QType.Q3_K, QType.Q2_K, QType.Q5_K])
+@pytest.mark.parametrize("qt", [QType.Q4_K, QType.Q6_K, QType.Q3_K, QType.Q2_K, QType.Q5_K, QType.Q8_0])
 @pytest.mark.parametrize("M,wm,splits", [
     (64, 1, 1), (40, 1, 3), (128, 2, 1), (77, 2, 2), (200, 2, 5), (256, 4, 1), (300, 4, 3), (511, 4, 2), (17, 1, 1)])
 def test_qmm3(qt, M, wm, splits, monkeypatch):

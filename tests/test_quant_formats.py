@@ -173,9 +173,10 @@ def test_mxf_kernels_gpu(qt, monkeypatch):
         assert L.qmv_fused(W, r32, EPI_F32, o3, norm=nw, eps=1e-5)
         y = (r32 * torch.rsqrt(r32.pow(2).mean(-1, keepdim=True) + 1e-5) * nw).cpu()
         assert rel(o3, y @ dense.t()) < 2e-2
-    for M, cfg in ((40, None), (200, None), (77, (4, 2, 4, 1, 2)), (130, (2, 1, 4, 17, 2)), (96, (2, 2, 4, 2, 1)),
-                   (256, (2, 2, 2, 33, 1))):
-        monkeypatch.setattr(L, "QMM_FORCE", cfg)
+    for M, cfg in ((40, None), (200, None), (77, (4, 2, 1, 2)), (130, (2, 10, 1, 2)), (96, (2, 1, 2, 1)),
+                   (256, (4, 1, 2, 1)), (300, (8, 1, 1, 3))):
+        monkeypatch.setattr(L, "QMM2", cfg is not None)
+        monkeypatch.setattr(L, "QMM2_FORCE", cfg)
         x = torch.randn(M, k, generator=g).half()
         ref = x.float() @ dense.t()
         out = torch.zeros(M, n, device="cuda")

@@ -6,7 +6,8 @@
 #                                                    concurrency CONC (default 128): per-kernel table per step
 #   bash tools/gpu_profile.sh pmc SHAPE M CFG          counter passes (MFMA / VALU / LDS / waits) of one qmm2
 #                                                    configuration "wm,ks,wn,splits" on a Llama-3-8B projection
-#   bash tools/gpu_profile.sh gemm [MS] [SHAPES]       qmm2 vs round-3 qmm vs hipBLASLt-on-dense sweep (JSONL)
+#   bash tools/gpu_profile.sh gemm [MS] [SHAPES]       default (untuned-rule) GEMM dispatch against M, one-launch vs
+#                                                    256-row chunks (JSONL; the tuned plans: MX_TUNE_REPORT)
 #
 # Every GPU step runs under its own timeout; counter passes stay within the per-block slot limits (8 SQ).
 set -o pipefail
@@ -38,9 +39,9 @@ case "$mode" in
     cat "$R/pmc_${shape}_${M}_${t}.md"
     ;;
   gemm)
-    MS=${1:-128,256,512} SHAPES=${2:-gate_up,qkv,wo,down,down_q6} FULL=${FULL:-0} \
-      timeout -k 10 600 python -u tools/tune_qmm2.py > "$R/tune_qmm2.jsonl" || exit 1
-    cat "$R/tune_qmm2.jsonl"
+    MS=${1:-128,192,256,320,384,512} SHAPES=${2:-gate_up,qkv,wo,down,down_q6} \
+      timeout -k 10 600 python -u tools/gemm_curve.py > "$R/gemm_curve.jsonl" || exit 1
+    cat "$R/gemm_curve.jsonl"
     ;;
   *)
     sed -n 2,12p "$0"; exit 2 ;;

@@ -19,7 +19,6 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--shape", default="gate_up")
     ap.add_argument("--M", type=int, default=2048)
-    ap.add_argument("--cfg", default="")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--gemv", action="store_true", help="M <= 4 decode GEMV with the fused RMSNorm / q8 prologue")
     ap.add_argument("--q2", default="", help="qmm2 wm,ks,wn,splits")
@@ -34,8 +33,6 @@ def main():
     qt = a.qt or qt
     W = L.QWeight.from_ggml(random_quantized(np.random.default_rng(1), qt, N, K), qt, N, K, "cuda", t32=True)
     assert W.to_t32()
-    if a.cfg:
-        L.QMM_FORCE = tuple(int(v) for v in a.cfg.split(","))
     if a.q2:
         L.QMM2, L.QMM2_FORCE = True, tuple(int(v) for v in a.q2.split(","))
     from localai_tfp_amd import _native as Nq
@@ -79,7 +76,7 @@ def main():
     torch.cuda.synchronize()
     us = e0.elapsed_time(e1) / a.iters * 1e3
     cfg = ("qmv_fused" if a.gemv else f"q2dbg {a.q2dbg}" if a.q2dbg else f"q3dbg {a.q3dbg}" if a.q3dbg else
-           f"qmm2 {L._qmm2_shape(a.M, N, K, epi in (0, 2))}" if a.q2 else L._qmm_shape(a.M, N, K, epi in (0, 2)))
+           f"qmm2 {L._qmm2_shape(a.M, N, K, epi in (0, 2))}" if a.q2 else L._gemm_pick(a.M, N, K, qt, epi in (0, 2)))
     print(f"{a.shape} qt={int(W.qtype)} M={a.M} cfg={cfg} {us:.1f} us {2*a.M*N*K/us/1e6:.0f} TF {W.data.numel() / us / 1e6:.2f} TB/s weights")
 
 
