@@ -83,8 +83,11 @@ def _build_lib(name: str, srcs, headers, compiler, cflags, ldflags, verbose=Fals
     LIB.mkdir(parents=True, exist_ok=True)
     BUILD.mkdir(parents=True, exist_ok=True)
     out = LIB / name
-    stamp = BUILD / (name + ".stamp")
-    key = _hash(list(srcs) + list(headers)) + "|" + " ".join(cflags) + "|" + ARCH + "|" + repr(sorted(FILE_FLAGS.items()))
+    # the stamp lives next to the library (both travel with the tree to a GPU box); its key is independent of the
+    # checkout location, so an up-to-date library is not rebuilt wherever the tree lands
+    stamp = LIB / (name + ".stamp")
+    portable = [f for f in cflags if not f.startswith(str(ROOT))]
+    key = _hash(list(srcs) + list(headers)) + "|" + " ".join(portable) + "|" + ARCH + "|" + repr(sorted(FILE_FLAGS.items()))
     if out.exists() and stamp.exists() and stamp.read_text() == key:
         return out
     objs = []

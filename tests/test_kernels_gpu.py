@@ -404,6 +404,8 @@ def test_qmm2(qt, M, wm, ks, wn, splits, monkeypatch):
     super-blocks, the 8-wave k-step split (ks = 2) and the 2-group wave tiles (wn = 2), against the fp32
     product of the dequantised weight."""
     from localai_tfp_amd.ops import linear as L
+    if qt == QType.Q8_0 and 32 * wm * wn == 256:
+        pytest.skip("a 256-row Q8_0 stage ring exceeds the LDS (not compiled)")
     monkeypatch.setattr(L, "QMM2", True)
     monkeypatch.setattr(L, "QMM2_FORCE", (wm, ks, wn, splits))
     n, k = 416, 2304
