@@ -17,18 +17,20 @@
 
 #define LOG2E_D 1.4426950408889634f
 
+// K image: row p holds D/8 16-byte chunks; chunk c lives at c ^ f(p) (f < 16: 16 consecutive rows, one chunk
+// column, land in 16 different banks). D = 512 uses the D = 128 swizzle (its rows are 4 x as wide, same banking).
 template <int D>
 MX_DEV int kd_lds_off(int p, int c) {
     const int r = p & 15;
     int f;
-    if constexpr (D == 128) f = r ^ (((r + 4) >> 3) & 1);
+    if constexpr (D >= 128) f = r ^ (((r + 4) >> 3) & 1);
     else f = ((r >> 1) & 7) ^ (((r + 4) >> 3) & 1);
     return p * (D * 2) + ((c ^ (f & (D / 8 - 1))) << 4);
 }
 template <int D>
 MX_DEV int vd_lds_off(int p, int nt) {
     int sv;
-    if constexpr (D == 128) sv = (p & 3) | (((p >> 3) & 1) << 2);
+    if constexpr (D >= 128) sv = (p & 3) | (((p >> 3) & 1) << 2);
     else sv = ((p >> 1) & 1) | (((p >> 3) & 1) << 1);
     return p * (D * 2) + ((nt ^ sv) << 5);
 }
@@ -51,7 +53,8 @@ __global__ __launch_bounds__(256) void attn_dense_kernel(const uint16_t* __restr
                                                          int Hq, int Hkv, const int* __restrict__ qlen_b,
                                                          const int* __restrict__ klen_b, int causal, float scale,
                                                          int kv_rows, const float* __restrict__ rbias, int rb_ld) {
-    constexpr int KT = 64;
+    // key tile: 64 keys (D <= 128) or 32 (D = 512: the VAE mid-block's single 512-wide head; K + V tiles 64 KB)
+    constexpr int KT = D > 128 ? 32 : 64;
     constexpr int KBYTES = KT * D * 2;
     constexpr int PSTRIDE = (KT + 8) * 2;
     __shared__ __attribute__((aligned(16))) char smem[2 * KBYTES + 4 * 16 * PSTRIDE];
@@ -103,9 +106,10 @@ __global__ __launch_bounds__(256) void attn_dense_kernel(const uint16_t* __restr
             *(uint4*)(v_lds + vd_lds_off<D>(p, c >> 1) + 16 * (c & 1)) = vv;
         }
         __syncthreads();
-        f32x4 sacc[4];
+        constexpr int NT16 = KT / 16;
+        f32x4 sacc[NT16];
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
+        for (int t = 0; t < NT16; ++t) {
             sacc[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int ks = 0; ks < D / 32; ++ks) {
@@ -119,7 +123,7 @@ __global__ __launch_bounds__(256) void attn_dense_kernel(const uint16_t* __restr
             const int qi = row_q0 + 4 * g + i;
             float mx = -INFINITY;
 #pragma unroll
-            for (int t = 0; t < 4; ++t) {
+            for (int t = 0; t < NT16; ++t) {
                 const int kp = kt0 + 16 * t + col;
                 float s = sacc[t][i] * qs;
                 if (kp >= kv_end || qi >= qlen || (causal && kp > qi + shift)) s = -INFINITY;
@@ -136,7 +140,7 @@ __global__ __launch_bounds__(256) void attn_dense_kernel(const uint16_t* __restr
             alpha[i] = mn == -INFINITY ? 1.f : exp2f(mrow[i] - mn);
             float rs = 0.f;
 #pragma unroll
-            for (int t = 0; t < 4; ++t) {
+            for (int t = 0; t < NT16; ++t) {
                 const float pv = mn == -INFINITY ? 0.f : exp2f(sacc[t][i] - mn);
                 sacc[t][i] = pv;
                 rs += pv;
@@ -150,14 +154,14 @@ __global__ __launch_bounds__(256) void attn_dense_kernel(const uint16_t* __restr
 #pragma unroll
             for (int i = 0; i < 4; ++i) oacc[nt][i] *= alpha[i];
 #pragma unroll
-        for (int t = 0; t < 4; ++t)
+        for (int t = 0; t < NT16; ++t)
 #pragma unroll
             for (int i = 0; i < 4; ++i)
                 *(uint16_t*)(pw + (4 * g + i) * PSTRIDE + (16 * t + col) * 2) = f32_to_act<F16>(sacc[t][i]);
         __builtin_amdgcn_s_waitcnt(0xc07f);
         __builtin_amdgcn_wave_barrier();
 #pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
+        for (int ks = 0; ks < KT / 32; ++ks) {
             const u32x4 pa = *(const u32x4*)(pw + col * PSTRIDE + (32 * ks + 8 * g) * 2);
             const int r0 = 32 * ks + 8 * g;
             const int q4 = col >> 2, p4 = col & 3;
@@ -186,7 +190,7 @@ __global__ __launch_bounds__(256) void attn_dense_kernel(const uint16_t* __restr
 }
 
 // q/k/v/o: 16-bit (act16 mode) token-major with row strides in elements; B batches of Sq queries /
-// Sk keys; Hq query heads, Hkv key/value heads (Hq % Hkv == 0); D in {64, 128}. K/V rows of batch b
+// Sk keys; Hq query heads, Hkv key/value heads (Hq % Hkv == 0); D in {64, 128, 512}. K/V rows of batch b
 // start at row b * kv_rows (kv_rows = 0 -> Sk): a fixed-capacity KV cache [B, cap, H*D] is read in
 // place with Sk = valid length (causal offset Sk - Sq) or Sk = cap with per-batch klen.
 extern "C" int mxk_attn_dense(const uint16_t* q, int q_stride, const uint16_t* k, int k_stride, const uint16_t* v,
@@ -195,11 +199,14 @@ extern "C" int mxk_attn_dense(const uint16_t* q, int q_stride, const uint16_t* k
                               const float* rbias, int rb_ld, hipStream_t st) {
     if (B <= 0 || Sq <= 0) return 0;
     if (kv_rows <= 0) kv_rows = Sk;
-    if (Hq % Hkv || (D != 64 && D != 128)) return (int)hipErrorInvalidValue;
+    if (Hq % Hkv || (D != 64 && D != 128 && D != 512)) return (int)hipErrorInvalidValue;
     if ((q_stride | k_stride | v_stride) & 7) return (int)hipErrorInvalidValue;
     dim3 grid((Sq + 63) / 64, Hq, B);
     MX_ACT_DISPATCH({
-        if (D == 128)
+        if (D == 512)
+            attn_dense_kernel<512, F16><<<grid, 256, 0, st>>>(q, q_stride, k, k_stride, v, v_stride, o, o_stride, Sq, Sk,
+                                                             Hq, Hkv, qlen, klen, causal, scale, kv_rows, rbias, rb_ld);
+        else if (D == 128)
             attn_dense_kernel<128, F16><<<grid, 256, 0, st>>>(q, q_stride, k, k_stride, v, v_stride, o, o_stride, Sq, Sk,
                                                              Hq, Hkv, qlen, klen, causal, scale, kv_rows, rbias, rb_ld);
         else

@@ -170,14 +170,16 @@ extern "C" int mxk_wavenet_gate(const float* x, float* out, int B, int H, int T,
 // slice; the direction's workgroups then meet at a grid barrier: agent-scope release + relaxed counter
 // ticket, relaxed polling + agent-scope acquire (placement independent, any XCD). The 2 x NB workgroups are
 // far below one per CU, so all are co-resident; every spin is bounded (err flag, no hang).
-// gx: [2][T][4H] (direction 1 in original time order), whh: [2][4H][H], hbuf: [2][2][H] (parity 0 = h0),
-// out: [T][2H] (forward | backward halves), cnt: [2] zeroed counters; all fp32 except cnt / err.
+// gx: [ND][T][4H] (direction 1 in original time order), whh: [ND][4H][H], hbuf: [ND][2][H] (parity 0 = h0),
+// out: [T][ND H] (forward | backward halves), cnt: [ND] zeroed counters; all fp32 except cnt / err. ND = 1 runs a
+// unidirectional layer (EnCodec's decoder LSTM, H = 512: 128 W_hh columns per thread in registers).
 template <int H>
 __global__ __launch_bounds__(256) void lstm_bidir_coop_kernel(const float* __restrict__ gx, const float* __restrict__ whh,
                                                               float* hbuf, float* __restrict__ out, unsigned* cnt,
                                                               int* err, int T) {
     constexpr int NB = H / 16, NC = H / 4;  // workgroups per direction, columns per thread
     const int dir = blockIdx.x / NB, wb = blockIdx.x % NB;
+    const int od = (int)(gridDim.x / NB) * H;  // output row stride: ND x H
     const int tid = threadIdx.x, row = tid >> 2, q = tid & 3;
     const int grow = (row >> 4) * H + wb * 16 + (row & 15);  // gate (row >> 4), unit (row & 15)
     __shared__ float sg[64];
@@ -217,7 +219,7 @@ __global__ __launch_bounds__(256) void lstm_bidir_coop_kernel(const float* __res
             c = fg * c + ig * gg;
             const float h = og * tanh_f(c);
             hbuf[(size_t)(dir * 2 + ((s + 1) & 1)) * H + wb * 16 + tid] = h;
-            out[(size_t)t * 2 * H + dir * H + wb * 16 + tid] = h;
+            out[(size_t)t * od + dir * H + wb * 16 + tid] = h;
         }
         if (s + 1 == T) break;
         // grid barrier of this direction's NB workgroups (release -> ticket; poll -> acquire)
@@ -243,12 +245,22 @@ __global__ __launch_bounds__(256) void lstm_bidir_coop_kernel(const float* __res
     }
 }
 
+// LSTM scan of ndir = 1 (unidirectional) or 2 (bidirectional) directions, H in {128, 256, 512}; the caller zeroes
+// cnt / err and fills hbuf parity 0 with h0.
+extern "C" int mxk_lstm_coop(const float* gx, const float* whh, float* hbuf, float* out, unsigned* cnt, int* err, int T,
+                             int H, int ndir, hipStream_t st) {
+    if (T <= 0) return 0;
+    if (ndir != 1 && ndir != 2) return (int)hipErrorInvalidValue;
+    if (H == 512) lstm_bidir_coop_kernel<512><<<ndir * (512 / 16), 256, 0, st>>>(gx, whh, hbuf, out, cnt, err, T);
+    else if (H == 256) lstm_bidir_coop_kernel<256><<<ndir * (256 / 16), 256, 0, st>>>(gx, whh, hbuf, out, cnt, err, T);
+    else if (H == 128) lstm_bidir_coop_kernel<128><<<ndir * (128 / 16), 256, 0, st>>>(gx, whh, hbuf, out, cnt, err, T);
+    else return (int)hipErrorInvalidValue;
+    return (int)hipGetLastError();
+}
+
 // Bidirectional LSTM scan (H in {128, 256}); the caller zeroes cnt / err and fills hbuf parity 0 with h0.
 extern "C" int mxk_lstm_bidir(const float* gx, const float* whh, float* hbuf, float* out, unsigned* cnt, int* err, int T,
                               int H, hipStream_t st) {
-    if (T <= 0) return 0;
-    if (H == 256) lstm_bidir_coop_kernel<256><<<2 * (256 / 16), 256, 0, st>>>(gx, whh, hbuf, out, cnt, err, T);
-    else if (H == 128) lstm_bidir_coop_kernel<128><<<2 * (128 / 16), 256, 0, st>>>(gx, whh, hbuf, out, cnt, err, T);
-    else return (int)hipErrorInvalidValue;
-    return (int)hipGetLastError();
+    if (H != 128 && H != 256) return (int)hipErrorInvalidValue;
+    return mxk_lstm_coop(gx, whh, hbuf, out, cnt, err, T, H, 2, st);
 }

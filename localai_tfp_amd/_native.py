@@ -78,6 +78,7 @@ KERNEL_SIGS = {
     "mxk_select_rows_f32": [P, I, P, I, I, P, I, P],
     "mxk_lstm_scan": [P, P, P, P, P, F, P, I, I, I, P],
     "mxk_lstm_bidir": [P, P, P, P, P, P, I, I, P],
+    "mxk_lstm_coop": [P, P, P, P, P, P, I, I, I, P],
     "mxk_wavenet_gate": [P, P, I, I, I, P],
     # xz, ldxz, w, bias, state, kc, slots, positions, slot_div, n_dec, pf_cu, n_pf, xc, xc16, ldo16, Di, stream
     "mxk_ssm_conv": [P, I, P, P, P, I, P, P, I, I, P, I, P, P, I, I, P],

@@ -13,6 +13,18 @@ from ..ops.sampling import SamplingParams
 _ids = itertools.count(1)
 
 
+def _utf8_incomplete_tail(b: bytes) -> int:
+    """Number of trailing bytes that start a UTF-8 character not yet complete (0 if the tail is complete)."""
+    n = len(b)
+    for k in range(1, min(4, n) + 1):
+        c = b[n - k]
+        if c & 0xC0 == 0x80:
+            continue  # continuation byte: look further back for the lead byte
+        need = 2 if c & 0xE0 == 0xC0 else 3 if c & 0xF0 == 0xE0 else 4 if c & 0xF8 == 0xF0 else 1
+        return k if need > k else 0
+    return 0
+
+
 class Status(enum.Enum):
     WAITING = 0
     RUNNING = 1
@@ -83,6 +95,7 @@ class Sequence:
         self._prefix_off = 0
         self._read_off = 0
         self._held = ""
+        self._pbytes = b""  # byte-level detokenisation: bytes of an incomplete trailing UTF-8 character
         self.emitted_text = ""
         self._pending_ids: list[int] = []
         self._pending_lp: list[float] = []
@@ -128,6 +141,9 @@ class Sequence:
             self._pending_lp.append(float(logprob))
 
     def _decode_new(self) -> str:
+        sb = getattr(self.tok, "stream_bytes", None)
+        if sb is not None:
+            return self._decode_bytes(sb())
         ids = self.output_ids
         prefix = self.tok.decode(ids[self._prefix_off:self._read_off])
         full = self.tok.decode(ids[self._prefix_off:])
@@ -139,6 +155,20 @@ class Sequence:
         if self._prefix_off > self._read_off:
             self._prefix_off = self._read_off
         return new
+
+    def _decode_bytes(self, table: list) -> str:
+        """Byte-level streaming detokenisation: append each new token's bytes, emit the longest valid UTF-8 prefix
+        and hold back an incomplete trailing character (grpc-server.cpp:1069-1190 partial-UTF-8 check)."""
+        ids = self.output_ids
+        new = ids[self._read_off:]
+        self._read_off = len(ids)
+        if not new:
+            return ""
+        n = len(table)
+        buf = self._pbytes + b"".join([table[i] if 0 <= i < n else b"" for i in new])
+        k = _utf8_incomplete_tail(buf)
+        self._pbytes = buf[len(buf) - k:] if k else b""
+        return (buf[:len(buf) - k] if k else buf).decode("utf-8", errors="replace")
 
     def flush_text(self, final: bool = False) -> tuple[str, bool]:
         """Returns (text to emit, stop_string_hit)."""

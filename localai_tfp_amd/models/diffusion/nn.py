@@ -104,7 +104,7 @@ def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, B: int, Sq: int
               scale: float | None = None, causal: bool = False, klen=None) -> torch.Tensor:
     """q: [B*Sq, H*D] rows (any row stride), k/v: [B*Sk, H*D] -> [B*Sq, H*D] (q dtype)."""
     scale = scale if scale is not None else 1.0 / math.sqrt(D)
-    if q.is_cuda and D <= 128:
+    if q.is_cuda and D in (64, 128, 512):  # D = 512: the VAE mid-block's single head
         out = torch.empty(B * Sq, H * D, dtype=q.dtype, device=q.device)
         return K.attn_dense(q, k, v, out, B, Sq, Sk, H, H, D, scale, causal, klen=klen)
     qh = q.reshape(B, Sq, H, D).transpose(1, 2)

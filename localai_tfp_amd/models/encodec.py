@@ -187,6 +187,8 @@ class EncodecDecoder:
             for name, prm in lstm.named_parameters():
                 prm.copy_(sd[lp + name].float())
         self.lstm = lstm.to(dev).eval()
+        from ..ops.rnn import LSTMStack
+        self.lstm_scan = LSTMStack(self.lstm)  # the recurrence on the repo's cooperative scan kernel (audio.hip)
         self.plan.append(("lstm", None))
         li += 1
         for ratio in cfg.upsampling_ratios:
@@ -222,7 +224,7 @@ class EncodecDecoder:
                 x = mod(x)
             elif kind == "lstm":
                 xf = x.float().transpose(0, 1)  # [T, B, C]
-                y = self.lstm(xf)[0] + xf
+                y = self.lstm_scan(xf) + xf
                 x = y.transpose(0, 1).to(self.dtype).contiguous()
             elif kind == "convt":
                 x = mod(F.elu(x))

@@ -36,9 +36,10 @@ from ..formats.gguf import QType
 from ..ops import core as K
 from ..ops import quant as Q
 from ..ops.linear import (ACT_DTYPE, EPI_ADD_F32, EPI_BF16, EPI_F32, EPI_GEGLU, EPI_SWIGLU, QWeight, concat_rows,
-                          _fp32_out_ok, dense_min_m, interleave_gate_up, qmatmul, qmv_fusable, qmv_rope_ok,
+                          _fp32_out_ok, dense_min_m, interleave_gate_up, glu_interleaved, qmatmul, qmv_fusable, qmv_rope_ok,
                           qmv_fused, qmv_rope_fused)
 from ..ops.moe import MoEWeights, moe_ffn
+from . import lora_runtime as LR
 from .config import LlamaConfig
 
 GEMV_MAX_M = 4
@@ -78,6 +79,7 @@ class LlamaLayer:
     window: int = 0  # sliding-window attention (0 = full)
     rope: tuple | None = None  # (inv_freq, attn_factor) of windowed layers with their own RoPE base
     qkv_dense: torch.Tensor | None = None  # dense 16-bit Q|K|V (large-M path) when the parts' quant types differ
+    lora: "object | None" = None  # runtime LoRA of this layer (models/lora_runtime.LayerLora)
 
 
 @dataclass
@@ -597,8 +599,10 @@ class LlamaModel:
             q = ws.q[:T]
             inv_freq, attn_factor = L.rope or (self.inv_freq, self.attn_factor)
             # batch 1: RoPE + KV append in each qkv part's GEMV epilogue (no rope_kv launch); every part or none
+            lo = L.lora
+            lo_qkv = lo.qkv if lo is not None else None
             rope_fused = (fuse_qkv and T == 1 and off == 0 and not cfg.neox and cfg.rope_dim == D
-                          and L.q_norm is None and self.tp_size == 1)
+                          and L.q_norm is None and self.tp_size == 1 and lo_qkv is None)
             if rope_fused:
                 # every part is checked before any launches: parts may mix block formats
                 o2 = 0
@@ -622,6 +626,10 @@ class LlamaModel:
                 else:
                     qmatmul(w, xb, EPI_F32, sl, out_zeroed=True)
                 off += w.N
+            if lo_qkv is not None:  # runtime LoRA: q|k|v += B (A x) on the normed rows
+                if gemv:
+                    K.rmsnorm(h, L.attn_norm, eps, out_bf16=xb)
+                LR.add_qkv(lo_qkv, xb, qkv)
             if not rope_fused:
                 K.rope_kv(qkv, L.bqkv, fb.positions, fb.slots, inv_freq, attn_factor, Hq, Hkv, D,
                           cfg.rope_dim, cfg.neox, q.view(T, Hq, D), kc, vc, kv.block_size,
@@ -645,6 +653,8 @@ class LlamaModel:
                 else:
                     aq = ads = None
                 self._residual_proj(L.wo, attn, aq, ads, h, L.post_attn_norm, ws, T, eps)
+            if lo is not None and lo.o is not None:
+                LR.add_residual(lo.o, attn, h)
             # ---- FFN block ----
             if L.moe is not None:
                 K.rmsnorm(h, L.ffn_norm, eps, out_bf16=xb)
@@ -658,6 +668,15 @@ class LlamaModel:
                     moe_ffn(L.moe, xb, h)
                 continue
             act = ws.act[:T]
+            if lo is not None and lo.gate_up is not None:
+                # runtime LoRA on gate / up: the update lands on the pre-activation rows, so the gated activation
+                # runs after it instead of in the GEMM epilogue
+                K.rmsnorm(h, L.ffn_norm, eps, out_bf16=xb)
+                self._lora_ffn_in(L, lo.gate_up, xb, act, T)
+                self._residual_proj(L.wd, act, None, None, h, L.post_ffn_norm, ws, T, eps)
+                if lo.down is not None:
+                    LR.add_residual(lo.down, act, h)
+                continue
             fuse_gu = fuse_in and L.wgu is not None and qmv_fusable(L.wgu, T, self.glu_epi)
             if fuse_gu:
                 pass
@@ -682,6 +701,8 @@ class LlamaModel:
                 K.glu(g_out, u_out, act, cfg.ffn_act)
             if fuse_in and L.post_ffn_norm is None and self.tp_size == 1 and qmv_fusable(L.wd, T, EPI_ADD_F32):
                 qmv_fused(L.wd, act, EPI_ADD_F32, h)
+                if lo is not None and lo.down is not None:
+                    LR.add_residual(lo.down, act, h)
                 continue
             if gemv:
                 aq, ads = ws.q8(T, F)
@@ -689,6 +710,8 @@ class LlamaModel:
             else:
                 aq = ads = None
             self._residual_proj(L.wd, act, aq, ads, h, L.post_ffn_norm, ws, T, eps)
+            if lo is not None and lo.down is not None:
+                LR.add_residual(lo.down, act, h)
         if self.stage or fb.stop_layer is not None:
             return h
         if self.remote is not None:  # remote layer ranges (parallel/pp_rpc.py), in place on h
@@ -811,6 +834,23 @@ class LlamaModel:
                 break
             out[:, lo:min(V, lo + vl)] = g[r * S:(r + 1) * S, :min(V, lo + vl) - lo]
         return out
+
+    def _lora_ffn_in(self, L, lp, xb: torch.Tensor, act: torch.Tensor, T: int):
+        """Gated FFN input with a runtime LoRA on gate / up: 16-bit pre-activations, + the low-rank update, then the
+        gated activation (fused gate|up weights: one GEMM on the interleaved rows; separate gate / up otherwise)."""
+        F = act.shape[1]
+        if L.wgu is not None:
+            y = torch.empty((T, 2 * F), dtype=xb.dtype if xb.is_cuda else torch.float32, device=xb.device)
+            qmatmul(L.wgu, xb, EPI_BF16, y)
+            LR.add_gate_up(lp, xb, y, F)
+            glu_interleaved(y, self.glu_epi, act)
+            return
+        g = torch.empty((T, F), dtype=act.dtype, device=act.device)
+        u = torch.empty((T, F), dtype=act.dtype, device=act.device)
+        qmatmul(L.wg, xb, EPI_BF16, g)
+        qmatmul(L.wu, xb, EPI_BF16, u)
+        LR.add_parts(lp, xb, {"ffn_gate": g, "ffn_up": u})
+        K.glu(g, u, act, self.cfg.ffn_act)
 
     def _residual_proj(self, W: QWeight, x, xq, xds, h: torch.Tensor, post_norm, ws: Workspace, T: int, eps: float):
         """h += x W^T — or, with a Gemma post-norm, h += rmsnorm(x W^T) * post_norm. Under tensor

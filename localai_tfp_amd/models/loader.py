@@ -50,8 +50,8 @@ def load_llm(model: str, device="cpu", tp_rank: int = 0, tp_size: int = 1, tp_gr
         import copy
         cfg = copy.deepcopy(cfg)
         _apply_overrides(cfg, ov)
-        src = _lora_source(synthetic_source(cfg, "Q4_K_M", seed=1), ov, cfg)
-        m = LlamaModel.load(cfg, src, device, tp_rank, tp_size, tp_group)
+        src = _lora_source(synthetic_source(cfg, "Q4_K_M", seed=1), ov, cfg, tp_size)
+        m = _lora_attach(LlamaModel.load(cfg, src, device, tp_rank, tp_size, tp_group), ov, cfg, tp_size)
         return m, ByteTokenizer(cfg.vocab), cfg, {}
     from .hf import QUANTS, hf_source, is_hf_dir
     if is_hf_dir(model):  # vllm / transformers backends: HF safetensors directory (models/hf.py)
@@ -63,7 +63,8 @@ def load_llm(model: str, device="cpu", tp_rank: int = 0, tp_size: int = 1, tp_gr
             q = "bf16"
         cfg, get = hf_source(model, q)
         _apply_overrides(cfg, ov)
-        m = LlamaModel.load(cfg, _lora_source(get, ov, cfg), device, tp_rank, tp_size, tp_group)
+        m = _lora_attach(LlamaModel.load(cfg, _lora_source(get, ov, cfg, tp_size), device, tp_rank, tp_size, tp_group),
+                         ov, cfg, tp_size)
         try:
             from ..tokenizer import from_hf_dir
             tok = from_hf_dir(model)
@@ -84,7 +85,8 @@ def load_llm(model: str, device="cpu", tp_rank: int = 0, tp_size: int = 1, tp_gr
         ti = r.tensors["rope_freqs.weight"]
         cfg.extra["rope_freqs"] = dequantize(r.tensor_bytes("rope_freqs.weight"), ti.qtype, ti.shape).tolist()
     _apply_overrides(cfg, ov)
-    m = LlamaModel.load(cfg, _lora_source(gguf_source(r), ov, cfg), device, tp_rank, tp_size, tp_group)
+    m = _lora_attach(LlamaModel.load(cfg, _lora_source(gguf_source(r), ov, cfg, tp_size), device, tp_rank, tp_size,
+                                     tp_group), ov, cfg, tp_size)
     try:
         tok = from_gguf(md)
     except Exception as ex:
@@ -93,15 +95,39 @@ def load_llm(model: str, device="cpu", tp_rank: int = 0, tp_size: int = 1, tp_gr
     return m, tok, cfg, md
 
 
-def _lora_source(get_tensor, ov: dict, cfg: LlamaConfig):
-    """overrides["lora"] = [(adapter path, scale), ...] -> a source yielding LoRA-merged weights."""
-    if not ov.get("lora"):
+def _lora_mode(ov: dict, tp_size: int, cfg: LlamaConfig | None = None) -> str:
+    """`lora_requant`: runtime (default: adapters kept beside the untouched base weights, as llama.cpp applies them)
+    | q8_0 | same | f32 (merged into the weights at load). Tensor parallelism merges (shards are cut after it), and
+    so do post-norm (Gemma 2/3) blocks, whose o / down outputs are normalised before the residual add."""
+    m = str(ov.get("lora_requant") or "runtime").lower()
+    if m == "runtime" and (tp_size > 1 or (cfg is not None and cfg.post_norms)):
+        log.info("LoRA: %s load merges the adapters (Q8_0)", "tensor parallel" if tp_size > 1 else "post-norm model")
+        m = "q8_0"
+    return m
+
+
+def _lora_source(get_tensor, ov: dict, cfg: LlamaConfig, tp_size: int = 1):
+    """overrides["lora"] = [(adapter path, scale), ...] -> a source yielding LoRA-merged weights (merge modes),
+    or the base source unchanged (runtime mode: _lora_attach after the load)."""
+    if not ov.get("lora") or _lora_mode(ov, tp_size, cfg) == "runtime":
         return get_tensor
     from .lora import load_adapter, with_adapters
     ads = [load_adapter(p, s, cfg) for p, s in ov["lora"]]
-    src = with_adapters(get_tensor, ads, ov.get("lora_requant") or "q8_0")
+    src = with_adapters(get_tensor, ads, _lora_mode(ov, tp_size, cfg))
     log.info("LoRA: %d adapter(s), %d weight tensors merged", len(ads), src.lora_targets)
     return src
+
+
+def _lora_attach(m, ov: dict, cfg: LlamaConfig, tp_size: int = 1, l0: int = 0):
+    """Runtime LoRA: the adapters beside the loaded base weights (models/lora_runtime.py)."""
+    if not ov.get("lora") or _lora_mode(ov, tp_size, cfg) != "runtime":
+        return m
+    from .lora import load_adapter
+    from .lora_runtime import build
+    ads = [load_adapter(p, s, cfg) for p, s in ov["lora"]]
+    n = build(m, ads, l0)
+    log.info("LoRA: %d adapter(s) applied at runtime to %d projections (base weights unchanged)", len(ads), n)
+    return m
 
 
 def _apply_overrides(cfg: LlamaConfig, ov: dict):

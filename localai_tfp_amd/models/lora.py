@@ -6,10 +6,10 @@ Reference: the llama-cpp backend passes `LoraAdapter` (relative to the model dir
 `adapter.lora.alpha`, tensors `<base name>.lora_a` [r, K] / `.lora_b` [N, r]) and scales each
 adapter by `scale * alpha / r`.
 
-MI355X design: instead of two extra skinny GEMMs per projection per token (rank-16 GEMMs are
-pure launch + HBM-latency overhead on the decode path), every adapter is folded into the base
-weight once at load — `W' = W + sum_i scale_i * alpha_i / r_i * B_i @ A_i` — and re-quantised.
-Default `requant="q8_0"`: merged K-quant tensors are stored as Q8_0 (a second 4-bit rounding would
+Two modes (model option `lora_requant`): `runtime` (default, models/lora_runtime.py) keeps the adapters beside
+the untouched base weights as llama.cpp does; the merge modes fold every adapter into the base weight once at
+load — `W' = W + sum_i scale_i * alpha_i / r_i * B_i @ A_i` — and re-quantise (no extra launches per token).
+Merge `requant="q8_0"`: merged K-quant tensors are stored as Q8_0 (a second 4-bit rounding would
 cost more accuracy than the adapter adds; Q8_0 stays on the native MFMA GEMM / GEMV kernels and only
 the adapted tensors grow). `requant="same"` keeps the base block format (Q4_K / Q6_K / Q8_0 — same
 bytes and kernels as without LoRA, like llama.cpp's `export-lora`). F32/F16/BF16 and formats without
@@ -119,6 +119,8 @@ def merged_tensor(raw, qtype: int, shape, deltas: list[np.ndarray], requant: str
     # requant "q8_0" (default): every block-quantised base (Q4_K, Q5_K, Q4_0, IQ*, ...) comes back as
     # Q8_0 when K allows it, never as 4-byte F32; "same": keep the base type where it can be re-encoded
     dense = qt in (QType.F32, QType.F16, QType.BF16)
+    if requant == "f32":  # exact merge, dense fp32 (the runtime path's numerics oracle)
+        return np.ascontiguousarray(w).view(np.uint8).reshape(N_, -1), int(QType.F32), shape
     if requant != "same" and not dense and K_ % 32 == 0:
         qt = QType.Q8_0
     if qt in _REQUANT and K_ % (32 if qt == QType.Q8_0 else 256) == 0:

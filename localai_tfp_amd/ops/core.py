@@ -451,7 +451,7 @@ def attn_dense(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, out: torch.Ten
 
     q/out: [B*Sq, >= Hq*D] (row stride = .stride(0)); k/v: [B*kv_rows, >= Hkv*D] of which the first
     Sk rows per batch are read (kv_rows = 0 -> Sk; a fixed-capacity KV cache passes its capacity).
-    Head dims other than 64/128 are zero-padded to the next supported size (exact: padded dims add
+    Head dims other than 64/128/512 are zero-padded to the next supported size (exact: padded dims add
     0 to q.k and produce 0 output columns that are dropped). klen/qlen: optional int32 [B] valid
     lengths (padding). rbias: optional fp32 [Hq, Sq + Sk - 1] additive bias by key-minus-query offset
     (index j - i + Sq - 1; T5's relative position bias), added to the scaled logits."""
@@ -483,7 +483,9 @@ def attn_dense(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, out: torch.Ten
                 o[b * Sq + int(qlen[b]):(b + 1) * Sq] = 0
         out[:, :Hq * D].copy_(o)
         return out
-    Dp = 64 if D <= 64 else 128
+    Dp = 64 if D <= 64 else 128 if D <= 128 else 512 if D <= 512 else 0
+    if not Dp:
+        raise ValueError(f"attn_dense: head dim {D} > 512")
     if Dp != D:
         def pad(t, H):
             x = t[:, :H * D].reshape(t.shape[0], H, D)

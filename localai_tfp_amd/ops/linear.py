@@ -637,6 +637,17 @@ def _apply_epi_dense(y: torch.Tensor, epi: int, out: torch.Tensor):
     return out
 
 
+def glu_interleaved(y: torch.Tensor, epi: int, out: torch.Tensor) -> torch.Tensor:
+    """Gated activation of pre-activation rows in the fused gate|up layout (16-row groups: interleave_gate_up):
+    y [M, 2F] -> out [M, F] = act(gate) * up (the qmm GLU epilogue as its own step)."""
+    if y.is_cuda:
+        N.ensure_act(out.dtype)
+        N.kcall("mxk_swiglu_il16", y.data_ptr(), y.stride(0), out.data_ptr(), out.stride(0), y.shape[0],
+                y.shape[1] // 2, int(epi == EPI_GEGLU), N.stream_ptr())
+        return out
+    return _apply_epi_dense(y.float(), epi, out)
+
+
 def _qmatmul_ref(W: QWeight, x: torch.Tensor, epi: int, out: torch.Tensor):
     y = x.float() @ W.dense_f32().t()
     return _apply_epi_dense(y, epi, out)

@@ -57,3 +57,47 @@ def lstm_bidir(x: torch.Tensor, p: dict, name: str, cache: dict | None = None) -
         log.warning("lstm_bidir %s: cooperative kernel barrier timed out (T=%d, H=%d); reference LSTM used", name, T, H)
         return _ref(x, p, name)
     return out
+
+
+class LSTMStack:
+    """Unidirectional multi-layer LSTM (torch.nn.LSTM parameter names / gate order, batch 1 per launch) on the
+    cooperative scan kernel (mxk_lstm_coop, ND = 1): per layer one GEMM for the input gates of all time steps,
+    then the recurrence. H in {128, 256, 512}; other sizes and CPU tensors run torch.nn.LSTM (the test oracle).
+    Reference parity: EnCodec's decoder SLSTM (backend/python/bark, transformers MusicGen audio decoder)."""
+
+    def __init__(self, lstm: torch.nn.LSTM):
+        self.ref = lstm
+        self.H, self.L = lstm.hidden_size, lstm.num_layers
+        p = dict(lstm.named_parameters())
+        self.layers = []
+        for i in range(self.L):
+            wih = p[f"weight_ih_l{i}"].detach().float().contiguous()
+            whh = p[f"weight_hh_l{i}"].detach().float().contiguous()
+            b = (p[f"bias_ih_l{i}"] + p[f"bias_hh_l{i}"]).detach().float().contiguous()
+            self.layers.append((wih, whh, b))
+
+    def native_ok(self, x: torch.Tensor) -> bool:
+        return x.is_cuda and self.H in (128, 256, 512) and not self.ref.bidirectional and self.ref.batch_first is False
+
+    def __call__(self, x: torch.Tensor) -> torch.Tensor:
+        """x [T, B, C] fp32 -> [T, B, H] (the last layer's hidden states)."""
+        if not self.native_ok(x):
+            return self.ref(x)[0]
+        T, B, _ = x.shape
+        H = self.H
+        outs = []
+        for bi in range(B):
+            y = x[:, bi].contiguous()
+            for wih, whh, b in self.layers:
+                gx = torch.addmm(b, y, wih.t()).contiguous()  # [T, 4H]
+                hbuf = torch.zeros(2, H, dtype=torch.float32, device=x.device)
+                cnt = torch.zeros(2, dtype=torch.int32, device=x.device)  # direction counter + the error flag
+                out = torch.empty(T, H, dtype=torch.float32, device=x.device)
+                N.kcall("mxk_lstm_coop", gx.data_ptr(), whh.data_ptr(), hbuf.data_ptr(), out.data_ptr(), cnt.data_ptr(),
+                        cnt[1:].data_ptr(), T, H, 1, N.stream_ptr())
+                if int(cnt[1].item()):
+                    log.warning("LSTMStack: cooperative kernel barrier timed out (T=%d, H=%d); reference LSTM used", T, H)
+                    return self.ref(x)[0]
+                y = out
+            outs.append(y)
+        return torch.stack(outs, 1)

@@ -78,7 +78,7 @@ class _Stage:
     def __init__(self, req: dict, device):
         from ..engine.kv_cache import KVCache
         from ..models.llama import Workspace
-        from ..models.loader import _apply_overrides, _lora_source, gguf_source, SYNTHETIC
+        from ..models.loader import _apply_overrides, _lora_attach, _lora_source, gguf_source, SYNTHETIC
         from ..models.llama import LlamaModel
         from ..engine.engine import kv_torch_dtype
         model = req["model"]
@@ -96,9 +96,10 @@ class _Stage:
             cfg = LlamaConfig.from_gguf_metadata(dict(r.metadata))
             _apply_overrides(cfg, req.get("overrides") or {})
             src = gguf_source(r)
-        # LoRA adapters merge on every stage (adapter paths must resolve on the stage's host)
-        src = _lora_source(src, req.get("overrides") or {}, cfg)
-        self.model = LlamaModel.load(cfg, src, device, layer_range=(l0, l1), stage=True)
+        # LoRA adapters apply on every stage (adapter paths must resolve on the stage's host)
+        ov = req.get("overrides") or {}
+        self.model = _lora_attach(LlamaModel.load(cfg, _lora_source(src, ov, cfg), device, layer_range=(l0, l1),
+                                                  stage=True), ov, cfg, 1, l0)
         self.cfg = cfg
         self.device = torch.device(device)
         self.kv = KVCache(l1 - l0, int(req["num_blocks"]), self.model.n_kv, int(req["block_size"]), cfg.head_dim,
@@ -268,7 +269,7 @@ def split_layers(n_layers: int, n_parts: int, weights: list[float] | None = None
 def load_split(model_ref: str, servers: list[str], device, tensor_split: list[float] | None = None, overrides=None):
     """-> (leader LlamaModel holding the first range + embedding/head, tokenizer, cfg, metadata).
     `servers`: "host:port" stages, in pipeline order (LLAMACPP_GRPC_SERVERS)."""
-    from ..models.loader import _apply_overrides, _lora_source, gguf_source, SYNTHETIC
+    from ..models.loader import _apply_overrides, _lora_attach, _lora_source, gguf_source, SYNTHETIC
     from ..models.llama import LlamaModel
     from ..tokenizer import ByteTokenizer, from_gguf
     md = {}
@@ -292,7 +293,9 @@ def load_split(model_ref: str, servers: list[str], device, tensor_split: list[fl
         except Exception:
             tok = ByteTokenizer(cfg.vocab)
     ranges = split_layers(cfg.n_layers, 1 + len(servers), tensor_split)
-    m = LlamaModel.load(cfg, _lora_source(src, overrides or {}, cfg), device, layer_range=ranges[0])
+    ov = overrides or {}
+    m = _lora_attach(LlamaModel.load(cfg, _lora_source(src, ov, cfg), device, layer_range=ranges[0]), ov, cfg, 1,
+                     ranges[0][0])
     m.remote = RemoteStages(model_ref, servers, ranges[1:], overrides)
     log.info("layer split: local %s, remote %s", ranges[0], list(zip(servers, ranges[1:])))
     return m, tok, cfg, md

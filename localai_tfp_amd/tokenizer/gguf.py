@@ -116,6 +116,16 @@ class BPETokenizer(_Base):
     def decode(self, ids, skip_special: bool = True) -> str:
         return self._tk.decode([int(i) for i in ids], skip_special_tokens=skip_special)
 
+    def stream_bytes(self) -> list[bytes]:
+        """Bytes each id contributes to decode(ids, skip_special=True) (b"" for the special / added tokens it
+        skips): byte-level BPE text is the concatenation of these, so streamed detokenisation can append bytes
+        per token instead of re-decoding a window (engine/sequence.py)."""
+        if getattr(self, "_sb", None) is None:
+            skip = set(self._special_set)
+            self._sb = [b"" if (i in skip or self.token_type[i] in (TT_CONTROL, TT_UNKNOWN, TT_UNUSED))
+                        else self._piece_bytes(i) for i in range(self.vocab_size)]
+        return self._sb
+
     def _piece_bytes(self, i: int) -> bytes:
         t = self.tokens[i]
         if self.token_type[i] == TT_USER:

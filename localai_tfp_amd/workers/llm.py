@@ -212,7 +212,7 @@ class LLMServicer(BackendServicer):
                     self.device = "cpu"
             ov = {"rope_freq_base": request.RopeFreqBase, "rope_freq_scale": request.RopeFreqScale,
                   "rope_scaling": request.RopeScaling, "rms_norm_eps": request.RMSNormEps,
-                  "lora": _lora_list(request, path), "lora_requant": opts.get("lora_requant", "q8_0"),
+                  "lora": _lora_list(request, path), "lora_requant": opts.get("lora_requant", "runtime"),
                   # HF safetensors checkpoints (vllm / transformers backends): load-time block format
                   "hf_quant": opts.get("quant") or request.Quantization or "bf16"}
             ec = EngineConfig()

@@ -599,9 +599,10 @@ def test_attn_outputs_act16(dt):
 
 
 @pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
-@pytest.mark.parametrize("D,Hq,Hkv", [(64, 8, 8), (128, 8, 2), (40, 8, 8), (80, 4, 4)])
+@pytest.mark.parametrize("D,Hq,Hkv", [(64, 8, 8), (128, 8, 2), (40, 8, 8), (80, 4, 4), (512, 1, 1), (320, 2, 2)])
 @pytest.mark.parametrize("causal", [False, True])
 def test_attn_dense(dt, D, Hq, Hkv, causal):
+    """(D = 512: the SD VAE mid-block's single head; 320 pads to it.)"""
     B, Sq, Sk = 2, 77, 150 if not causal else 77
     g = torch.Generator().manual_seed(D + Hq)
     q = torch.randn(B * Sq, Hq * D, generator=g).to(dt)

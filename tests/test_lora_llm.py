@@ -1,8 +1,10 @@
 """LLM LoRA adapters (reference: backend/cpp/llama/grpc-server.cpp:2402-2410 — LoraAdapter relative to
 the model directory, LoraScale default 1.0, handed to llama.cpp which scales by scale*alpha/rank).
 
-Adapters are merged into the GGUF weights at load and re-quantised (Q8_0 by default, or the base block
-format). Checked:
+Runtime mode (the default, as llama.cpp): adapters stay beside the untouched quantised base weights and
+`B (A x)` is added to every adapted projection's output (models/lora_runtime.py); the merge modes fold them into
+the GGUF weights at load (Q8_0, the base block format, or exact fp32). Checked:
+runtime logits == exact-fp32-merge logits, every projection adapted, prefill + decode, CPU and GPU;
 merged tensor == quantise(dequantise(W) + scale*alpha/r * B@A) byte for byte (Q4_K, Q6_K, Q8_0, F32);
 llama.cpp adapter GGUF and HF PEFT safetensors name mapping (incl. the q/k rotary-row permutation);
 through the gRPC worker an adapter changes the greedy output, deterministically."""
@@ -130,3 +132,61 @@ def test_worker_lora_gpu(tmp_path):
     base = _predict(device="cuda:0")
     a = _predict("q.gguf", 1.0, tmp_path, device="cuda:0")
     assert a != base and a == _predict("q.gguf", 1.0, tmp_path, device="cuda:0")
+
+
+def _all_proj_adapter(path, cfg, rng, r=4, layers=None):
+    dims = {"attn_q": (cfg.hidden, cfg.q_dim), "attn_k": (cfg.hidden, cfg.kv_dim), "attn_v": (cfg.hidden, cfg.kv_dim),
+            "attn_output": (cfg.q_dim, cfg.hidden), "ffn_gate": (cfg.hidden, cfg.ffn), "ffn_up": (cfg.hidden, cfg.ffn),
+            "ffn_down": (cfg.ffn, cfg.hidden)}
+    pairs = {f"blk.{i}.{n}.weight": (rng.standard_normal((r, k)).astype(np.float32) * 0.05,
+                                     rng.standard_normal((nout, r)).astype(np.float32) * 0.05)
+             for i in (layers if layers is not None else range(cfg.n_layers)) for n, (k, nout) in dims.items()}
+    _write_adapter(path, pairs, 2 * r)
+
+
+def _runtime_vs_merged(tmp_path, device, model="synthetic:tiny"):
+    import torch
+    from localai_tfp_amd.models.loader import SYNTHETIC, load_llm
+    from test_model_gpu import _run
+    cfg = SYNTHETIC[model.split(":")[1]]
+    _all_proj_adapter(tmp_path / "a.gguf", cfg, np.random.default_rng(7))
+    _all_proj_adapter(tmp_path / "b.gguf", cfg, np.random.default_rng(8), r=2, layers=[0])
+    ads = [(str(tmp_path / "a.gguf"), 0.7), (str(tmp_path / "b.gguf"), 1.3)]
+    rng = np.random.default_rng(0)
+    prompt, forced = rng.integers(0, cfg.vocab, 19).tolist(), rng.integers(0, cfg.vocab, 3).tolist()
+    outs = {}
+    for mode in ("runtime", "f32", None):
+        ov = {"lora": ads, "lora_requant": mode} if mode else {}
+        m, _, _, _ = load_llm(model, device, overrides=ov)
+        if mode == "runtime":
+            assert all(L.lora is not None and L.lora.any for L in m.layers)
+        outs[mode] = _run(m, torch.device(device), prompt, forced)
+        del m
+    for got, want, base in zip(outs["runtime"], outs["f32"], outs[None]):
+        rel = float((got - want).norm() / want.norm())
+        assert rel < (1e-3 if device == "cpu" else 2e-2), rel  # q-kernel vs dense fp32 rounding
+        assert float((base - want).norm() / want.norm()) > 10 * rel  # the adapters do change the logits
+
+
+def test_runtime_lora_matches_exact_merge(tmp_path):
+    _runtime_vs_merged(tmp_path, "cpu")
+
+
+@pytest.mark.gpu
+def test_runtime_lora_matches_exact_merge_gpu(tmp_path):
+    """GPU: the LoRA GEMMs run beside the quantised qmm/qmv kernels (batch-1 GEMV path, fused prologues off where
+    the update needs the normed rows; prefill path with the gated activation after the update)."""
+    _runtime_vs_merged(tmp_path, "cuda:0")
+
+
+def test_runtime_lora_pipeline_stage(tmp_path):
+    """A pipeline stage holding blocks l0..l1 attaches only its own blocks' adapters, at local indices."""
+    from localai_tfp_amd.models import lora_runtime as LRT
+    from localai_tfp_amd.models.llama import LlamaModel
+    from localai_tfp_amd.models.loader import SYNTHETIC
+    from localai_tfp_amd.models.synthetic import synthetic_source
+    cfg = SYNTHETIC["tiny-4l"]
+    _all_proj_adapter(tmp_path / "a.gguf", cfg, np.random.default_rng(3), layers=[2])
+    m = LlamaModel.load(cfg, synthetic_source(cfg, "Q4_K_M", seed=1), "cpu", layer_range=(1, 3))
+    n = LRT.build(m, [L.load_adapter(str(tmp_path / "a.gguf"), 1.0, cfg)], l0=1)
+    assert n == 7 and m.layers[0].lora is None and m.layers[1].lora.any

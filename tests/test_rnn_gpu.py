@@ -33,3 +33,23 @@ def test_lstm_bidir_matches_torch(C, H, T):
     err = float((got.cpu() - ref).abs().max())
     assert err < 2e-4, err
     assert torch.equal(got, got2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("H,L,T,B", [(512, 2, 45, 1), (256, 1, 9, 2), (128, 2, 1, 1)])
+def test_lstm_stack_matches_torch(H, L, T, B):
+    """Unidirectional multi-layer LSTM on the cooperative scan (EnCodec's decoder SLSTM: H = 512, 2 layers)."""
+    from localai_tfp_amd.ops.rnn import LSTMStack
+    torch.manual_seed(H + T)
+    m = torch.nn.LSTM(H, H, L)
+    with torch.no_grad():
+        for prm in m.parameters():
+            prm.mul_(0.6)
+    x = torch.randn(T, B, H)
+    ref = m(x)[0]
+    st = LSTMStack(m.to(DEV))
+    got = st(x.to(DEV))
+    torch.cuda.synchronize()
+    assert got.shape == (T, B, H)
+    err = float((got.cpu() - ref).abs().max())
+    assert err < 3e-4, err

@@ -14,6 +14,7 @@ def main():
     ap.add_argument("--window-ms", type=float, default=0.0, help="only kernels that start in the last W ms (0: all)")
     ap.add_argument("--steps", type=int, default=0, help="engine steps inside the window (per-step column)")
     ap.add_argument("--top", type=int, default=30)
+    ap.add_argument("--gaps", action="store_true", help="also: idle time between consecutive kernels, by next kernel")
     a = ap.parse_args()
     c = sqlite3.connect(a.db)
     t_end = c.execute("select max(end) from kernels").fetchone()[0]
@@ -36,6 +37,29 @@ def main():
         if a.steps:
             line += f" {ms * 1e3 / a.steps:.1f} |"
         print(line)
+    if a.gaps:
+        ks = c.execute("select name, start, end from kernels where start >= ? order by start", (t0,)).fetchall()
+        by: dict = {}
+        tot = 0.0
+        hist = [0, 0, 0, 0, 0]  # < 1, 1-2, 2-4, 4-8, >= 8 us
+        for (_, _, e0), (nm, s1, _) in zip(ks, ks[1:]):
+            g = max(0.0, (s1 - e0) / 1e3)
+            if g > 1000:  # between steps (host-bound idle), not a launch gap
+                continue
+            tot += g
+            hist[0 if g < 1 else 1 if g < 2 else 2 if g < 4 else 3 if g < 8 else 4] += 1
+            nm = nm.replace("(anonymous namespace)::", "").split("(")[0][:90]
+            t = by.setdefault(nm, [0, 0.0])
+            t[0] += 1
+            t[1] += g
+        print()
+        print(f"inter-kernel gaps (< 1 ms): {tot / 1e3:.2f} ms total" + (f", {tot / 1e3 / a.steps:.3f} ms/step" if a.steps else "")
+              + f"; histogram <1/1-2/2-4/4-8/>=8 us: {hist}")
+        print()
+        print("| next kernel | gaps | total ms | avg us |")
+        print("|---|---|---|---|")
+        for nm, (n, g) in sorted(by.items(), key=lambda kv: -kv[1][1])[: a.top]:
+            print(f"| `{nm}` | {n} | {g / 1e3:.2f} | {g / n:.2f} |")
 
 
 if __name__ == "__main__":
