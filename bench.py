@@ -59,6 +59,11 @@ def parse():
     ap.add_argument("--max-batched-tokens", type=int, default=2048)
     ap.add_argument("--prefill-chunk", type=int, default=0, help="prompt tokens per sequence per step (0: budget)")
     ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--dp-gateway", default="per-rank", choices=["per-rank", "single"],
+                    help="http path under DP: one gateway + load generator per rank, or ONE `local-ai run` gateway "
+                         "(--gateway-workers processes) in front of every rank's worker, as `data_parallel: N` is "
+                         "deployed")
+    ap.add_argument("--gateway-workers", type=int, default=0, help="single gateway's processes (0: one per GPU)")
     ap.add_argument("--kv-dtype", default="bf16", choices=["bf16", "f16", "fp8"],
                     help="paged KV cache element type (llama.cpp cache_type_k/v); fp8 = e4m3")
     ap.add_argument("--profile-steps", type=int, default=0)
@@ -283,13 +288,16 @@ def main():
     p99 = float(np.percentile(ttfts, 99)) if len(ttfts) else float("nan")
     t_max, tok_sum, p50_all, p99_all = t_el, float(tokens), p50, p99
     if dist:
+        single = args.path == "http" and args.dp_gateway == "single" and world > 1
+        if single and rank != 0:
+            p50 = p99 = 0.0  # the client-side latencies are rank 0's load generators'
         tt = torch.tensor([t_el, float(tokens), p50, p99], device=dev, dtype=torch.float64)
         mx = tt.clone()
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
         sm = tt.clone()
         dist.all_reduce(sm, op=dist.ReduceOp.SUM)
         t_max, tok_sum = float(mx[0]), float(sm[1])
-        p50_all, p99_all = float(sm[2] / dp), float(mx[3])
+        p50_all, p99_all = float(sm[2] / (1 if single else dp)), float(mx[3])
     value = tok_sum / t_max
     from localai_tfp_amd.ops.linear import ACT_DTYPE
     # 16-bit MFMA operands (Q4_K_M weights dequantised in-register), fp32 accumulation everywhere
@@ -320,6 +328,9 @@ def main():
                 **({"tp_selfcheck_rel_err": tp_rel} if tp_rel is not None else {}),
                 "path": ("HTTP /v1/chat/completions (SSE) -> FastAPI gateway -> mxstream (batched gRPC-side channel) -> LLM worker engine" if args.path == "http"
                          else "engine in-process (gateway/gRPC excluded)"),
+                **({"dp_gateway": args.dp_gateway if world > 1 else "single",
+                    "gateway_workers": args.gateway_workers or (world if args.dp_gateway == "single" and world > 1 else 1)}
+                   if args.path == "http" else {}),
                 "load_s": round(t_load, 1), "gemm_tune_s": round(getattr(eng, "stats_tune_s", 0.0), 1),
                 "graph_capture_s": round(t_capture, 1), "graphs": n_graphs,
                 "graph_steps": st["graph_steps"], "total_steps": st["steps"],
@@ -417,6 +428,18 @@ def run_http(args, eng, tok, cfg, dev, dist):
     svc.attach(eng, tok)
     eng.start()
     server = AioServer(svc, "127.0.0.1:0", max_workers=16)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    single = args.dp_gateway == "single" and dist is not None and world > 1
+    front = not single or int(os.environ.get("RANK", "0")) == 0
+    if single:
+        # every rank's worker address to rank 0, whose one gateway fronts them all as data-parallel replicas
+        pt = torch.zeros(world, dtype=torch.int64, device=dev)
+        pt[int(os.environ.get("RANK", "0"))] = server.port
+        dist.all_reduce(pt)
+        backends = "|".join(f"127.0.0.1:{int(p)}" for p in pt.tolist())
+        conc, n_gw = args.concurrency * world, args.gateway_workers or world
+    else:
+        backends, conc, n_gw = f"127.0.0.1:{server.port}", args.concurrency, args.gateway_workers or 1
     work = tempfile.mkdtemp(prefix="mxbench")
     models = os.path.join(work, "models")
     os.makedirs(models)
@@ -435,17 +458,20 @@ def run_http(args, eng, tok, cfg, dev, dist):
                            "--address", f"127.0.0.1:{port}", "--disable-webui", "--log-level", "warning",
                            "--localai-config-dir", os.path.join(work, "cfg"),
                            "--generated-content-path", os.path.join(work, "gen"),
-                           "--upload-path", os.path.join(work, "up"),
-                           "--external-grpc-backends", f"llama-cpp:127.0.0.1:{server.port}"],
-                          env=env, cwd=ROOT, stdout=gw_log, stderr=subprocess.STDOUT, start_new_session=True)
+                           "--upload-path", os.path.join(work, "up"), "--gateway-workers", str(n_gw),
+                           "--external-grpc-backends", f"llama-cpp:{backends}"],
+                          env=env, cwd=ROOT, stdout=gw_log, stderr=subprocess.STDOUT,
+                          start_new_session=True) if front else None
     if args.tokenizer == "byte":
         size_args = ["--prompt-chars", str(max(1, args.prompt_len - TEMPLATE_OVERHEAD))]
     else:
         _, n_words = prompt_sizing(tok, args.prompt_len)
         size_args = ["--prompt-words", str(n_words)]
     out = []
+    n_lg = max(1, min(world, 4)) if single else 1  # one asyncio load generator carries ~25k chunks/s
     try:
-        wait_http(f"http://127.0.0.1:{port}/readyz", 120, gw)
+        if front:
+            wait_http(f"http://127.0.0.1:{port}/readyz", 120, gw)
         for pi, phase in enumerate(args.phases.split(",")):
             sp = SAMPLING[phase]
             samp_args = ["--temperature", str(sp["temperature"])]
@@ -458,12 +484,14 @@ def run_http(args, eng, tok, cfg, dev, dist):
             win = Window(eng, args.warmup, args.steps, dev, dist, steady_gate(args),
                          base_finished=eng.stats["finished"])
             eng.on_step = win
-            rec_path = os.path.join(work, f"loadgen_{pi}.json")
-            lg = subprocess.Popen([sys.executable, "-m", "localai_tfp_amd.tools.loadgen",
-                                   "--url", f"http://127.0.0.1:{port}", "--model", "llama-3-8b-instruct",
-                                   "--concurrency", str(args.concurrency), *size_args, *samp_args,
-                                   "--gen-len", str(args.gen_len), "--seed", str(int(os.environ.get("RANK", "0")) + 97 * pi),
-                                   "--stagger", "--out", rec_path], env=env, cwd=ROOT, start_new_session=True)
+            rec_paths = [os.path.join(work, f"loadgen_{pi}_{i}.json") for i in range(n_lg)] if front else []
+            lgs = [subprocess.Popen([sys.executable, "-m", "localai_tfp_amd.tools.loadgen",
+                                     "--url", f"http://127.0.0.1:{port}", "--model", "llama-3-8b-instruct",
+                                     "--concurrency", str(conc // n_lg + (i < conc % n_lg)), *size_args, *samp_args,
+                                     "--gen-len", str(args.gen_len),
+                                     "--seed", str(int(os.environ.get("RANK", "0")) + 97 * pi + 1000 * i),
+                                     "--stagger", "--out", rp], env=env, cwd=ROOT, start_new_session=True)
+                   for i, rp in enumerate(rec_paths)]
             try:
                 t_start = time.time()
                 last = -1
@@ -471,48 +499,56 @@ def run_http(args, eng, tok, cfg, dev, dist):
                     n = eng.stats["steps"]
                     print(f"[bench rank {os.environ.get('RANK', '0')}] phase={phase} steps={n} "
                           f"out_tokens={eng.stats['out_tokens']}", file=sys.stderr, flush=True)
-                    if lg.poll() is not None or gw.poll() is not None:
+                    if any(lg.poll() is not None for lg in lgs) or (gw is not None and gw.poll() is not None):
                         raise RuntimeError("load generator or gateway exited early; see " + work)
                     if time.time() - t_start > args.timeout or (n == last and n > 0):
                         raise TimeoutError(f"window not reached (steps={n}); see {work}")
                     last = n
             finally:
                 eng.on_step = None
-                if lg.poll() is None:
-                    lg.send_signal(signal.SIGTERM)
+                for lg in lgs:
+                    if lg.poll() is None:
+                        lg.send_signal(signal.SIGTERM)
+                for lg in lgs:
                     try:
                         lg.wait(timeout=60)
                     except subprocess.TimeoutExpired:
                         lg.kill()
-            out.append(_http_phase_result(win, rec_path))
+            out.append(_http_phase_result(win, rec_paths))
             # the cancelled streams of this phase must leave the engine before the next phase's gate counts
             t_d = time.time()
             while (eng.sched.running or eng.sched.waiting) and time.time() - t_d < 120:
                 time.sleep(0.1)
     finally:
         eng.on_step = None
+        if single:  # the gateway (rank 0) still holds connections to every rank's worker
+            dist.barrier()
         eng.shutdown()
-        gw.terminate()
-        try:
-            gw.wait(timeout=20)
-        except subprocess.TimeoutExpired:
-            gw.kill()
+        if gw is not None:
+            gw.terminate()
+            try:
+                gw.wait(timeout=20)
+            except subprocess.TimeoutExpired:
+                gw.kill()
         server.stop()
     return out
 
 
-def _http_phase_result(win, rec_path):
+def _http_phase_result(win, rec_paths):
     recs = []
-    try:
-        with open(rec_path) as f:
-            recs = json.load(f)
-    except (OSError, ValueError):
-        pass
+    for rp in rec_paths:
+        try:
+            with open(rp) as f:
+                recs += json.load(f)
+        except (OSError, ValueError):
+            pass
     t0, t1 = win.t0, win.t1
     ttfts = [(r["t_first"] - r["t_send"]) * 1e3 for r in recs if r.get("t_first") and t0 <= r["t_first"] <= t1]
     done = [r for r in recs if r.get("ok") and t0 <= r["t_end"] <= t1]
     client_tps = sum(r["tokens"] for r in done) / (t1 - t0) if done else 0.0
     errors = sum(1 for r in recs if r.get("error") not in (None, "CancelledError"))
+    if not recs:  # a rank behind the single DP gateway: its engine's tokens count, the client side is rank 0's
+        return t1 - t0, win.tok1 - win.tok0, [], {"steady_at_step": win.steady_step}
     # inter-token latency: gaps between consecutive content chunks of one stream, both inside the window
     itl = [(b - a) * 1e3 for r in recs for a, b in zip(r.get("t_chunks", []), r.get("t_chunks", [])[1:])
            if t0 <= a and b <= t1]

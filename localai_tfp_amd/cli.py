@@ -52,6 +52,9 @@ def add_run_args(ap: argparse.ArgumentParser):
     ap.add_argument("--config-file", "--models-config-file", dest="config_file")
     ap.add_argument("--galleries", help="JSON list of galleries")
     ap.add_argument("--autoload-galleries", action="store_true", default=None)
+    ap.add_argument("--gateway-workers", type=int, default=None,
+                    help="gateway processes accepting on the address (SO_REUSEPORT) and sharing the backends "
+                         "(env LOCALAI_GATEWAY_WORKERS; default 1): one Python gateway carries ~20k SSE chunks/s")
     ap.add_argument("--preload-models", help="JSON list of gallery models to apply at start")
     ap.add_argument("--preload-models-config")
     ap.add_argument("--f16", action="store_true", default=None)
@@ -141,10 +144,59 @@ def app_config_from_args(a):
     return c
 
 
+def _listen_socket(host: str, port: int, reuse_port: bool):
+    import socket
+    fam = socket.AF_INET6 if ":" in host else socket.AF_INET
+    s = socket.socket(fam, socket.SOCK_STREAM)
+    s.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+    if reuse_port:
+        s.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEPORT, 1)
+    s.bind((host, port))
+    s.listen(2048)
+    s.set_inheritable(True)
+    return s
+
+
+def _spawn_gateway_followers(a, n: int, registry: str) -> list:
+    """n sibling gateway processes: same arguments, same address (SO_REUSEPORT), backends shared through
+    `registry` (serving/shared_backends.py); gallery preloads and p2p stay with this (primary) process."""
+    import subprocess
+    env = dict(os.environ, LOCALAI_BACKEND_REGISTRY=registry, LOCALAI_GATEWAY_FOLLOWER=str(os.getpid()),
+               LOCALAI_GATEWAY_WORKERS="1")
+    argv = [x for x in a._argv]
+    return [subprocess.Popen([sys.executable, "-m", "localai_tfp_amd", *argv], env=env) for _ in range(n)]
+
+
+def _watch_parent(ppid: int):
+    """A follower gateway ends with its primary (SIGTERM to itself: uvicorn's graceful shutdown)."""
+    import signal
+    import threading
+    import time as _t
+
+    def run():
+        while True:
+            _t.sleep(1.0)
+            if os.getppid() != ppid:
+                os.kill(os.getpid(), signal.SIGTERM)
+                return
+    threading.Thread(target=run, daemon=True, name="gateway-parent-watch").start()
+
+
 def cmd_run(a):
     import uvicorn
     from .gateway.app import create_app
     c = app_config_from_args(a)
+    follower = os.environ.get("LOCALAI_GATEWAY_FOLLOWER", "")
+    nw = a.gateway_workers if a.gateway_workers is not None else int(os.environ.get("LOCALAI_GATEWAY_WORKERS", "1") or 1)
+    followers = []
+    if follower:
+        c.p2p = c.federated = False
+        a.preload_models = a.preload_models_config = None
+        _watch_parent(int(follower))
+    elif nw > 1:
+        import tempfile
+        reg = os.path.join(c.config_dir or tempfile.gettempdir(), f".gateway-backends-{os.getpid()}")
+        os.environ["LOCALAI_BACKEND_REGISTRY"] = reg
     app = create_app(c)
     st = app.state.localai
     if a.preload_models:
@@ -164,8 +216,27 @@ def cmd_run(a):
         st.shutdown()
         return 0
     host, port = c.host_port
-    uvicorn.run(app, host=host, port=port, log_level=a.log_level.lower() if a.log_level else "info",
-                access_log=a.log_level.lower() == "debug", timeout_keep_alive=60)
+    level = a.log_level.lower() if a.log_level else "info"
+    if not follower and nw <= 1:
+        uvicorn.run(app, host=host, port=port, log_level=level, access_log=level == "debug", timeout_keep_alive=60)
+        return 0
+    sock = _listen_socket(host, port, True)
+    if not follower:
+        followers = _spawn_gateway_followers(a, nw - 1, os.environ["LOCALAI_BACKEND_REGISTRY"])
+    try:
+        uvicorn.Server(uvicorn.Config(app, log_level=level, access_log=level == "debug",
+                                      timeout_keep_alive=60)).run(sockets=[sock])
+    finally:
+        for p in followers:
+            p.terminate()
+        for p in followers:
+            try:
+                p.wait(timeout=30)
+            except Exception:
+                p.kill()
+        if not follower:
+            import shutil
+            shutil.rmtree(os.environ.get("LOCALAI_BACKEND_REGISTRY", ""), ignore_errors=True)
     return 0
 
 
@@ -424,6 +495,7 @@ def main(argv=None):
     w.add_argument("kind", help="backend name, e.g. llama-cpp, whisper, bert-embeddings; llama-cpp-rpc = layer-split stage")
     w.add_argument("--addr", default="127.0.0.1:50051")
     a = ap.parse_args(argv)
+    a._argv = list(argv) if argv is not None else sys.argv[1:]
     logging.basicConfig(level=getattr(logging, str(getattr(a, "log_level", "info") or "info").upper(), logging.INFO),
                         format="%(asctime)s %(levelname)s %(name)s: %(message)s")
     fn = {"run": cmd_run, "models": cmd_models, "tts": cmd_tts, "transcript": cmd_transcript,

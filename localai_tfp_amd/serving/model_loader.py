@@ -125,6 +125,8 @@ class LoadedModel:
         self.name, self.backend, self.replicas = name, backend, replicas
         self._rr = 0
         self._lock = threading.Lock()
+        self.shared: dict | None = None  # registry entry this process attached to (another gateway owns it)
+        self._checked = 0.0
 
     def pick(self) -> BackendClient:
         return self.pick_replica().client
@@ -269,6 +271,12 @@ class ModelLoader:
         self.inproc = inproc if inproc is not None else os.environ.get("LOCALAI_INPROC_BACKENDS", "") == "1"
         self.gpus = visible_gpus()
         self._gpu_load: dict[int, int] = {g: 0 for g in self.gpus}
+        # multi-process gateway (cli.py --gateway-workers): backends shared with the sibling gateway processes
+        reg = os.environ.get("LOCALAI_BACKEND_REGISTRY", "")
+        self.shared = None
+        if reg:
+            from .shared_backends import SharedBackends
+            self.shared = SharedBackends(reg)
         self.watchdog: WatchDog | None = None
         if getattr(app, "watchdog_busy", False) or getattr(app, "watchdog_idle", False):
             self.watchdog = WatchDog(self, app.watchdog_busy_timeout_s, app.watchdog_idle_timeout_s,
@@ -279,6 +287,12 @@ class ModelLoader:
     def get(self, name: str) -> LoadedModel | None:
         with self._lock:
             m = self.models.get(name)
+        if m is not None and m.shared is not None and time.time() - m._checked > 1.0:
+            m._checked = time.time()
+            if not self.shared.same(self.shared.read(name), m.shared):
+                log.info("shared backend for %s was unloaded by its owner; detaching", name)
+                self.shutdown_model(name, force=True)
+                return None
         if m is not None and not m.alive():
             log.warning("backend for %s died; removing", name)
             self.shutdown_model(name, force=True)
@@ -312,20 +326,46 @@ class ModelLoader:
             if getattr(self.app, "single_active_backend", False):
                 for other in self.list_loaded():
                     self.shutdown_model(other)
-            cands = [backend or cfg.backend] if (backend or cfg.backend) else guess_backend(cfg, self.app.models_path)
-            errs = []
-            for b in cands:
-                try:
-                    m = self._load_with(cfg, name, b)
-                    break
-                except Exception as ex:
-                    errs.append(f"{b}: {ex}")
-                    log.warning("loading %s with %s failed: %s", name, b, ex)
+            if self.shared is not None:
+                with self.shared.locked(name):
+                    e = self.shared.read(name)
+                    if e is not None and e["owner"] != self.shared.pid:
+                        m = self._attach(name, e)
+                    else:
+                        m = self._load_candidates(cfg, name, backend)
+                        self.shared.publish(name, m.backend, m.replicas)
             else:
-                raise BackendLoadError(f"could not load model {name!r}: " + "; ".join(errs))
+                m = self._load_candidates(cfg, name, backend)
             with self._lock:
                 self.models[name] = m
             return m
+
+    def _attach(self, name: str, e: dict) -> LoadedModel:
+        """Clients to the replicas another gateway process published (it owns and stops them)."""
+        parallel = bool(getattr(self.app, "parallel_backend_requests", True))
+        reps = []
+        for r in e["replicas"]:
+            rep_ = Replica(r["address"], BackendClient(r["address"], parallel=parallel))
+            rep_.mx_path = r["mx_path"] if r["mx_path"] and os.path.exists(r["mx_path"]) else ""
+            reps.append(rep_)
+        m = LoadedModel(name, e["backend"], reps)
+        m.shared, m._checked = e, time.time()
+        log.info("attached %s: %d replica(s) owned by gateway process %d", name, len(reps), e["owner"])
+        return m
+
+    def _load_candidates(self, cfg, name: str, backend: str | None) -> LoadedModel:
+        cands = [backend or cfg.backend] if (backend or cfg.backend) else guess_backend(cfg, self.app.models_path)
+        errs = []
+        for b in cands:
+            try:
+                m = self._load_with(cfg, name, b)
+                break
+            except Exception as ex:
+                errs.append(f"{b}: {ex}")
+                log.warning("loading %s with %s failed: %s", name, b, ex)
+        else:
+            raise BackendLoadError(f"could not load model {name!r}: " + "; ".join(errs))
+        return m
 
     def _assign_gpus(self, n: int) -> list[int]:
         if not self.gpus:
@@ -354,8 +394,10 @@ class ModelLoader:
         replicas: list[Replica] = []
         try:
             if ext and ":" in ext and not os.path.exists(ext):
-                # external backend at a fixed address: no process to manage
-                replicas.append(self._connect(ext, parallel))
+                # external backend at fixed address(es): no process to manage; "host:port|host:port|..." lists
+                # externally started data-parallel replicas of one model
+                for addr in ext.split("|"):
+                    replicas.append(self._connect(addr.strip(), parallel))
             else:
                 for _ in range(dp):
                     gpus = tuple(self._assign_gpus(tp))
@@ -451,6 +493,15 @@ class ModelLoader:
         if m is None:
             return False
         force = force if force is not None else getattr(self.app, "force_backend_shutdown", False)
+        if m.shared is not None:  # attached: the owning gateway process stops the workers
+            for r in m.replicas:
+                try:
+                    r.client.close()
+                except Exception:
+                    pass
+            return True
+        if self.shared is not None:
+            self.shared.withdraw(name)
         for r in m.replicas:
             if self.watchdog:
                 self.watchdog.remove(r.address)

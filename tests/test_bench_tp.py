@@ -52,3 +52,22 @@ def test_bench_world_mismatch_refused(tmp_path):
     p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--path", "engine"], env=env,
                        cwd=str(tmp_path), capture_output=True, text=True, timeout=300)
     assert p.returncode != 0 and "--gpus 2" in p.stderr
+
+
+def test_bench_dp2_single_gateway_http_cpu(tmp_path):
+    """`--dp-gateway single`: ONE `local-ai run` gateway (2 processes sharing the replicas) fronts both ranks'
+    workers as `data_parallel` replicas of one model, as a user deploys DP; every rank's
+    engine serves part of the load and the JSON line sums them."""
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="2")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--path", "http", "--dp-gateway", "single",
+           "--steps", "4", "--warmup", "1", "--concurrency", "4", "--prompt-len", "32", "--gen-len", "8",
+           "--phases", "reference", "--tokenizer", "byte"]
+    p = subprocess.run(cmd, env=env, cwd=str(tmp_path), capture_output=True, text=True, timeout=600)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["config"]["dp_gateway"] == "single" and out["config"]["gateway_workers"] == 2
+    assert out["value"] > 0 and out["p50_ttft_ms"] > 0
