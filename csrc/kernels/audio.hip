@@ -172,15 +172,21 @@ extern "C" int mxk_wavenet_gate(const float* x, float* out, int B, int H, int T,
 // far below one per CU, so all are co-resident; every spin is bounded (err flag, no hang).
 // gx: [ND][T][4H] (direction 1 in original time order), whh: [ND][4H][H], hbuf: [ND][2][H] (parity 0 = h0),
 // out: [T][ND H] (forward | backward halves), cnt: [ND] zeroed counters; all fp32 except cnt / err. ND = 1 runs a
-// unidirectional layer (EnCodec's decoder LSTM, H = 512: 128 W_hh columns per thread in registers).
+// unidirectional layer (EnCodec's decoder LSTM: H = 512 for the 24 kHz codec, 128 W_hh columns per thread in
+// registers; H = 1024 for MusicGen's 32 kHz codec, rows split over QS = 8 threads -> 512-thread workgroups, still
+// 128 columns per thread).
 template <int H>
-__global__ __launch_bounds__(256) void lstm_bidir_coop_kernel(const float* __restrict__ gx, const float* __restrict__ whh,
-                                                              float* hbuf, float* __restrict__ out, unsigned* cnt,
-                                                              int* err, int T) {
-    constexpr int NB = H / 16, NC = H / 4;  // workgroups per direction, columns per thread
+constexpr int lstm_qs() { return H >= 1024 ? 8 : 4; }
+template <int H>
+__global__ __launch_bounds__(64 * lstm_qs<H>()) void lstm_bidir_coop_kernel(const float* __restrict__ gx,
+                                                                            const float* __restrict__ whh, float* hbuf,
+                                                                            float* __restrict__ out, unsigned* cnt,
+                                                                            int* err, int T) {
+    constexpr int QS = lstm_qs<H>();
+    constexpr int NB = H / 16, NC = H / QS;  // workgroups per direction, columns per thread
     const int dir = blockIdx.x / NB, wb = blockIdx.x % NB;
     const int od = (int)(gridDim.x / NB) * H;  // output row stride: ND x H
-    const int tid = threadIdx.x, row = tid >> 2, q = tid & 3;
+    const int tid = threadIdx.x, row = tid / QS, q = tid % QS;
     const int grow = (row >> 4) * H + wb * 16 + (row & 15);  // gate (row >> 4), unit (row & 15)
     __shared__ float sg[64];
     float w[NC];
@@ -211,6 +217,7 @@ __global__ __launch_bounds__(256) void lstm_bidir_coop_kernel(const float* __res
         }
         acc += __shfl_xor(acc, 1, 64);
         acc += __shfl_xor(acc, 2, 64);
+        if constexpr (QS == 8) acc += __shfl_xor(acc, 4, 64);
         if (q == 0) sg[row] = acc;
         __syncthreads();
         if (tid < 16) {  // PyTorch gate order: i, f, g, o
@@ -245,13 +252,14 @@ __global__ __launch_bounds__(256) void lstm_bidir_coop_kernel(const float* __res
     }
 }
 
-// LSTM scan of ndir = 1 (unidirectional) or 2 (bidirectional) directions, H in {128, 256, 512}; the caller zeroes
+// LSTM scan of ndir = 1 (unidirectional) or 2 (bidirectional) directions, H in {128, 256, 512, 1024}; the caller zeroes
 // cnt / err and fills hbuf parity 0 with h0.
 extern "C" int mxk_lstm_coop(const float* gx, const float* whh, float* hbuf, float* out, unsigned* cnt, int* err, int T,
                              int H, int ndir, hipStream_t st) {
     if (T <= 0) return 0;
     if (ndir != 1 && ndir != 2) return (int)hipErrorInvalidValue;
-    if (H == 512) lstm_bidir_coop_kernel<512><<<ndir * (512 / 16), 256, 0, st>>>(gx, whh, hbuf, out, cnt, err, T);
+    if (H == 1024) lstm_bidir_coop_kernel<1024><<<ndir * (1024 / 16), 512, 0, st>>>(gx, whh, hbuf, out, cnt, err, T);
+    else if (H == 512) lstm_bidir_coop_kernel<512><<<ndir * (512 / 16), 256, 0, st>>>(gx, whh, hbuf, out, cnt, err, T);
     else if (H == 256) lstm_bidir_coop_kernel<256><<<ndir * (256 / 16), 256, 0, st>>>(gx, whh, hbuf, out, cnt, err, T);
     else if (H == 128) lstm_bidir_coop_kernel<128><<<ndir * (128 / 16), 256, 0, st>>>(gx, whh, hbuf, out, cnt, err, T);
     else return (int)hipErrorInvalidValue;

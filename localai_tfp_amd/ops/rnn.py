@@ -62,7 +62,7 @@ def lstm_bidir(x: torch.Tensor, p: dict, name: str, cache: dict | None = None) -
 class LSTMStack:
     """Unidirectional multi-layer LSTM (torch.nn.LSTM parameter names / gate order, batch 1 per launch) on the
     cooperative scan kernel (mxk_lstm_coop, ND = 1): per layer one GEMM for the input gates of all time steps,
-    then the recurrence. H in {128, 256, 512}; other sizes and CPU tensors run torch.nn.LSTM (the test oracle).
+    then the recurrence. H in {128, 256, 512, 1024}; other sizes and CPU tensors run torch.nn.LSTM (the test oracle).
     Reference parity: EnCodec's decoder SLSTM (backend/python/bark, transformers MusicGen audio decoder)."""
 
     def __init__(self, lstm: torch.nn.LSTM):
@@ -77,7 +77,7 @@ class LSTMStack:
             self.layers.append((wih, whh, b))
 
     def native_ok(self, x: torch.Tensor) -> bool:
-        return x.is_cuda and self.H in (128, 256, 512) and not self.ref.bidirectional and self.ref.batch_first is False
+        return x.is_cuda and self.H in (128, 256, 512, 1024) and not self.ref.bidirectional and self.ref.batch_first is False
 
     def __call__(self, x: torch.Tensor) -> torch.Tensor:
         """x [T, B, C] fp32 -> [T, B, H] (the last layer's hidden states)."""

@@ -36,7 +36,7 @@ def test_lstm_bidir_matches_torch(C, H, T):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("H,L,T,B", [(512, 2, 45, 1), (256, 1, 9, 2), (128, 2, 1, 1)])
+@pytest.mark.parametrize("H,L,T,B", [(512, 2, 45, 1), (256, 1, 9, 2), (128, 2, 1, 1), (1024, 2, 33, 1)])
 def test_lstm_stack_matches_torch(H, L, T, B):
     """Unidirectional multi-layer LSTM on the cooperative scan (EnCodec's decoder SLSTM: H = 512, 2 layers)."""
     from localai_tfp_amd.ops.rnn import LSTMStack
