@@ -302,6 +302,7 @@ static int dispatch_qmm3(int wm, const uint16_t* A, int lda, const uint8_t* W, i
     if (wm == 1) return launch_qmm3<QT, 1, EPI>(A, lda, W, M, N, K, splits, C, ldc, st);
     if (wm == 2) return launch_qmm3<QT, 2, EPI>(A, lda, W, M, N, K, splits, C, ldc, st);
     if (wm == 4) return launch_qmm3<QT, 4, EPI>(A, lda, W, M, N, K, splits, C, ldc, st);
+    if (wm == 3) return launch_qmm3<QT, 3, EPI>(A, lda, W, M, N, K, splits, C, ldc, st);  // 192-row tiles
     return (int)hipErrorInvalidValue;
 }
 

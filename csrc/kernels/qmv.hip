@@ -470,48 +470,60 @@ struct QRope {
     bf16_t* vc;
 };
 
-template <int QT, int EPI, bool F16, int SRC>
+// NU: weight units per wave (2: K slices <= 16 units, e.g. K = 4096; 4: <= 32 units, the 8192-wide rows of 70B-class
+// models). The activation slice is read in NU / 2 passes of 8 elements per thread (4096 per pass).
+template <int QT, int EPI, bool F16, int SRC, int NU = 2>
 __global__ __launch_bounds__(64 * QMV_WAVES) void qmv1_kernel(const uint8_t* __restrict__ W, int N, int K,
                                                               void* __restrict__ Cv, const void* __restrict__ xsrc,
                                                               const float* __restrict__ nw, float eps, QRope rp) {
     using U = TUnit<QT>;
     constexpr int NT = 64 * QMV_WAVES;
+    constexpr int NP = NU / 2;  // activation passes of 8 elements per thread
     static_assert(SRC == SRC_ACT || SRC == SRC_NORM, "fused prologue only");
+    static_assert(NU == 2 || NU == 4, "units per wave");
     __shared__ float red[QMV_WAVES][32];
     __shared__ float nred[QMV_WAVES];
     extern __shared__ __attribute__((aligned(16))) char qmv1_smem[];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int r = lane & 31, h = lane >> 5;
     const int g = blockIdx.x;
-    const int nunit = K / U::ELEMS;  // K == 4096 (checked by the launcher)
+    const int nunit = K / U::ELEMS;  // SRC_NORM: K == 4096 NU (checked by the launcher)
     const int per = (nunit + gridDim.y - 1) / gridDim.y;
     const int u0 = blockIdx.y * per, u1 = min(nunit, u0 + per);
     const int k0 = u0 * U::ELEMS, klen = max(0, u1 - u0) * U::ELEMS;
     const uint8_t* wg = W + (size_t)g * nunit * U::BYTES;
-    // 1. this workgroup's slice of the activation row (8 elements per thread; SRC_NORM: the whole row, ks = 1)
-    //    and, for the norm, its weights
-    const int er = 8 * threadIdx.x, e = k0 + min(er, max(klen - 8, 0));  // clamped: a valid address
-    float a8[8], w8[8];
-    if constexpr (SRC == SRC_NORM) {
-        const float* xr = (const float*)xsrc + e;
-        const float4 v0 = *(const float4*)xr, v1 = *(const float4*)(xr + 4);
-        const float4 n0 = *(const float4*)(nw + e), n1 = *(const float4*)(nw + e + 4);
-        a8[0] = v0.x; a8[1] = v0.y; a8[2] = v0.z; a8[3] = v0.w; a8[4] = v1.x; a8[5] = v1.y; a8[6] = v1.z; a8[7] = v1.w;
-        w8[0] = n0.x; w8[1] = n0.y; w8[2] = n0.z; w8[3] = n0.w; w8[4] = n1.x; w8[5] = n1.y; w8[6] = n1.z; w8[7] = n1.w;
-    } else {
-        const uint4 raw = *(const uint4*)((const bf16_t*)xsrc + e);
-        unpack_act2<F16>(raw.x, a8[0], a8[1]);
-        unpack_act2<F16>(raw.y, a8[2], a8[3]);
-        unpack_act2<F16>(raw.z, a8[4], a8[5]);
-        unpack_act2<F16>(raw.w, a8[6], a8[7]);
+    // 1. this workgroup's slice of the activation row (8 elements per thread per pass; SRC_NORM: the whole row,
+    //    ks = 1) and, for the norm, its weights
+    float a8[NP][8], w8[NP][8];
+#pragma unroll
+    for (int ps = 0; ps < NP; ++ps) {
+        const int er = 8 * threadIdx.x + 8 * NT * ps, e = k0 + min(er, max(klen - 8, 0));  // clamped: a valid address
+        if constexpr (SRC == SRC_NORM) {
+            const float* xr = (const float*)xsrc + e;
+            const float4 v0 = *(const float4*)xr, v1 = *(const float4*)(xr + 4);
+            const float4 n0 = *(const float4*)(nw + e), n1 = *(const float4*)(nw + e + 4);
+            a8[ps][0] = v0.x; a8[ps][1] = v0.y; a8[ps][2] = v0.z; a8[ps][3] = v0.w;
+            a8[ps][4] = v1.x; a8[ps][5] = v1.y; a8[ps][6] = v1.z; a8[ps][7] = v1.w;
+            w8[ps][0] = n0.x; w8[ps][1] = n0.y; w8[ps][2] = n0.z; w8[ps][3] = n0.w;
+            w8[ps][4] = n1.x; w8[ps][5] = n1.y; w8[ps][6] = n1.z; w8[ps][7] = n1.w;
+        } else {
+            const uint4 raw = *(const uint4*)((const bf16_t*)xsrc + e);
+            unpack_act2<F16>(raw.x, a8[ps][0], a8[ps][1]);
+            unpack_act2<F16>(raw.y, a8[ps][2], a8[ps][3]);
+            unpack_act2<F16>(raw.z, a8[ps][4], a8[ps][5]);
+            unpack_act2<F16>(raw.w, a8[ps][6], a8[ps][7]);
+        }
     }
     asm volatile("" ::: "memory");  // the row reads stay ahead of the weight requests
-    // 2. this wave's (at most) two weight units
-    U a, b;
+    // 2. this wave's (at most) NU weight units: u0 + wave + 8 j
+    U un[NU];
+    bool hv[NU];
     const int u = u0 + wave;
-    const bool ha = u < u1, hb = u + QMV_WAVES < u1;
-    if (ha) a.load(wg + (size_t)u * U::BYTES, r, h);
-    if (hb) b.load(wg + (size_t)(u + QMV_WAVES) * U::BYTES, r, h);
+#pragma unroll
+    for (int j = 0; j < NU; ++j) {
+        hv[j] = u + QMV_WAVES * j < u1;
+        if (hv[j]) un[j].load(wg + (size_t)(u + QMV_WAVES * j) * U::BYTES, r, h);
+    }
     // 3. norm + quantisation of the slice into LDS while the weights stream
     int8_t* sq = (int8_t*)qmv1_smem;
     float2* sd = (float2*)(qmv1_smem + klen);
@@ -519,28 +531,34 @@ __global__ __launch_bounds__(64 * QMV_WAVES) void qmv1_kernel(const uint8_t* __r
     if constexpr (SRC == SRC_NORM) {
         float ss = 0.f;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) ss += a8[j] * a8[j];
+        for (int ps = 0; ps < NP; ++ps)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) ss += a8[ps][j] * a8[ps][j];
         ss = wave_sum(ss);
         if (lane == 0) nred[wave] = ss;
     }
-    if (er < klen) {  // whole 4-lane groups (klen % 256 == 0)
-        float v8[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v8[j] = SRC == SRC_NORM ? a8[j] * w8[j] : a8[j];
-        float am = 0.f;
+    for (int ps = 0; ps < NP; ++ps) {
+        const int er = 8 * threadIdx.x + 8 * NT * ps;
+        if (er < klen) {  // whole 4-lane groups (klen % 256 == 0)
+            float v8[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) am = fmaxf(am, fabsf(v8[j]));
-        am = group_max<4>(am);
-        const float d = am / 127.f, id = d > 0.f ? 1.f / d : 0.f;
-        int q[8], sum = 0;
+            for (int j = 0; j < 8; ++j) v8[j] = SRC == SRC_NORM ? a8[ps][j] * w8[ps][j] : a8[ps][j];
+            float am = 0.f;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) { q[j] = __float2int_rn(v8[j] * id); sum += q[j]; }
-        const float sf = group_sum<4>((float)sum);
-        uint2 pk;
-        pk.x = (q[0] & 0xFF) | ((q[1] & 0xFF) << 8) | ((q[2] & 0xFF) << 16) | ((uint32_t)(q[3] & 0xFF) << 24);
-        pk.y = (q[4] & 0xFF) | ((q[5] & 0xFF) << 8) | ((q[6] & 0xFF) << 16) | ((uint32_t)(q[7] & 0xFF) << 24);
-        *(uint2*)(sq + er) = pk;
-        if ((threadIdx.x & 3) == 0) sd[er / 32] = make_float2(d, d * sf);
+            for (int j = 0; j < 8; ++j) am = fmaxf(am, fabsf(v8[j]));
+            am = group_max<4>(am);
+            const float d = am / 127.f, id = d > 0.f ? 1.f / d : 0.f;
+            int q[8], sum = 0;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) { q[j] = __float2int_rn(v8[j] * id); sum += q[j]; }
+            const float sf = group_sum<4>((float)sum);
+            uint2 pk;
+            pk.x = (q[0] & 0xFF) | ((q[1] & 0xFF) << 8) | ((q[2] & 0xFF) << 16) | ((uint32_t)(q[3] & 0xFF) << 24);
+            pk.y = (q[4] & 0xFF) | ((q[5] & 0xFF) << 8) | ((q[6] & 0xFF) << 16) | ((uint32_t)(q[7] & 0xFF) << 24);
+            *(uint2*)(sq + er) = pk;
+            if ((threadIdx.x & 3) == 0) sd[er / 32] = make_float2(d, d * sf);
+        }
     }
     __syncthreads();
     if constexpr (SRC == SRC_NORM) {
@@ -552,8 +570,11 @@ __global__ __launch_bounds__(64 * QMV_WAVES) void qmv1_kernel(const uint8_t* __r
     // 4. dot products
     float acc = 0.f;
     const int ul = u - u0;
-    if (ha) acc += a.dot(sq + (size_t)ul * U::ELEMS, sd + ul * (U::ELEMS / 32), h);
-    if (hb) acc += b.dot(sq + (size_t)(ul + QMV_WAVES) * U::ELEMS, sd + (ul + QMV_WAVES) * (U::ELEMS / 32), h);
+#pragma unroll
+    for (int j = 0; j < NU; ++j) {
+        const int uj = ul + QMV_WAVES * j;
+        if (hv[j]) acc += un[j].dot(sq + (size_t)uj * U::ELEMS, sd + uj * (U::ELEMS / 32), h);
+    }
     acc *= rs;
     {
         const float v = acc + __shfl_xor(acc, 32);
@@ -721,15 +742,24 @@ static int launch_qmv(const int8_t* xq, const float2* xds, const uint8_t* W, int
         const size_t sl = (size_t)per * TUnit<QT>::ELEMS;
         const size_t lds = MM * (sl + sl / 32 * sizeof(float2));
         if (lds > 64 * 1024) return (int)hipErrorInvalidValue;
-        // qmv1: batch 1, at most two units per wave; the norm needs the whole row in one workgroup (ks = 1)
-        if (MM == 1 && M == 1 && per <= 2 * QMV_WAVES && g_qmv1_on &&
-            (src == SRC_ACT || (K == 4096 && ks == 1))) {
+        // qmv1: batch 1, at most four units per wave; the norm needs the whole row in one workgroup (ks = 1)
+        if (MM == 1 && M == 1 && per <= 4 * QMV_WAVES && g_qmv1_on &&
+            (src == SRC_ACT || ((K == 4096 || K == 8192) && ks == 1 && per == K / TUnit<QT>::ELEMS))) {
+            const bool four = per > 2 * QMV_WAVES;
             if (src == SRC_ACT) {
-                MX_ACT_DISPATCH(qmv1_kernel<QT, EPI, F16, SRC_ACT><<<dim3(N / 32, ks), 64 * QMV_WAVES, lds, st>>>(
-                    W, N, K, C, xsrc, nullptr, 0.f, QRope{}));
+                if (four)
+                    MX_ACT_DISPATCH(qmv1_kernel<QT, EPI, F16, SRC_ACT, 4><<<dim3(N / 32, ks), 64 * QMV_WAVES, lds, st>>>(
+                        W, N, K, C, xsrc, nullptr, 0.f, QRope{}));
+                else
+                    MX_ACT_DISPATCH(qmv1_kernel<QT, EPI, F16, SRC_ACT><<<dim3(N / 32, ks), 64 * QMV_WAVES, lds, st>>>(
+                        W, N, K, C, xsrc, nullptr, 0.f, QRope{}));
             } else {
-                MX_ACT_DISPATCH(qmv1_kernel<QT, EPI, F16, SRC_NORM><<<dim3(N / 32, ks), 64 * QMV_WAVES, lds, st>>>(
-                    W, N, K, C, xsrc, nw, eps, QRope{}));
+                if (four)
+                    MX_ACT_DISPATCH(qmv1_kernel<QT, EPI, F16, SRC_NORM, 4><<<dim3(N / 32, ks), 64 * QMV_WAVES, lds, st>>>(
+                        W, N, K, C, xsrc, nw, eps, QRope{}));
+                else
+                    MX_ACT_DISPATCH(qmv1_kernel<QT, EPI, F16, SRC_NORM><<<dim3(N / 32, ks), 64 * QMV_WAVES, lds, st>>>(
+                        W, N, K, C, xsrc, nw, eps, QRope{}));
             }
             MXK_CHECK_LAUNCH();
         }
@@ -814,17 +844,23 @@ extern "C" int mxk_qmv_x(int qtype, int epi, int src, const void* x, int ldx, co
 }
 
 // Batch-1 qkv GEMV with the input RMSNorm fused in front and RoPE + paged KV append fused behind (EPI_ROPEKV):
-// x fp32 [1, 4096] residual row, W one t32 part (q, k, v or a fused run of them) whose columns start at column
+// x fp32 [1, K] residual row (K = 4096, or 8192: 70B-class hidden size, four units per wave), W one t32 part (q, k, v or a fused run of them) whose columns start at column
 // n_off of the q|k|v row; rotation over whole heads of D (adjacent pairs, rot_dim == D), bf16 q and caches.
 extern "C" int mxk_qmv1_rope(int qtype, const float* x, const float* nw, float eps, const uint8_t* W, int N, int K,
                              int n_off, const int* pos, const int* slots, const float* inv_freq, const float* bias,
                              float attn_factor, int Hq, int Hkv, int D, bf16_t* qo, bf16_t* kc, bf16_t* vc,
                              int block_size, hipStream_t st) {
-    if (K != 4096 || N % 32 || (D != 64 && D != 128) || n_off % 32 || ((uintptr_t)x & 15)) return (int)hipErrorInvalidValue;
+    if ((K != 4096 && K != 8192) || N % 32 || (D != 64 && D != 128) || n_off % 32 || ((uintptr_t)x & 15))
+        return (int)hipErrorInvalidValue;
     const QRope rp{pos, slots, inv_freq, bias, attn_factor, Hq, Hkv, D, n_off, block_size, qo, kc, vc};
     const size_t lds = (size_t)K + K / 32 * sizeof(float2);
-#define QR1(QT_) \
-    qmv1_kernel<QT_, EPI_ROPEKV, true, SRC_NORM><<<dim3(N / 32, 1), 64 * QMV_WAVES, lds, st>>>(W, N, K, nullptr, x, nw, eps, rp)
+#define QR1(QT_)                                                                                                     \
+    if (K == 8192)                                                                                                   \
+        qmv1_kernel<QT_, EPI_ROPEKV, true, SRC_NORM, 4><<<dim3(N / 32, 1), 64 * QMV_WAVES, lds, st>>>(W, N, K, nullptr, x, \
+                                                                                                   nw, eps, rp);     \
+    else                                                                                                             \
+        qmv1_kernel<QT_, EPI_ROPEKV, true, SRC_NORM><<<dim3(N / 32, 1), 64 * QMV_WAVES, lds, st>>>(W, N, K, nullptr, x, nw, \
+                                                                                                eps, rp)
     switch (qtype) {
         case MXQ_Q4_K: QR1(MXQ_Q4_K); break;
         case MXQ_Q5_K: QR1(MXQ_Q5_K); break;

@@ -602,7 +602,7 @@ class LlamaModel:
             lo = L.lora
             lo_qkv = lo.qkv if lo is not None else None
             rope_fused = (fuse_qkv and T == 1 and off == 0 and not cfg.neox and cfg.rope_dim == D
-                          and L.q_norm is None and self.tp_size == 1 and lo_qkv is None)
+                          and L.q_norm is None and lo_qkv is None)
             if rope_fused:
                 # every part is checked before any launches: parts may mix block formats
                 o2 = 0
@@ -646,6 +646,8 @@ class LlamaModel:
                                window=L.window, softcap=cfg.attn_softcap, tiles=fb.pf_tiles)
             if fuse_in and L.post_attn_norm is None and self.tp_size == 1 and qmv_fusable(L.wo, T, EPI_ADD_F32):
                 qmv_fused(L.wo, attn, EPI_ADD_F32, h)  # h += attn W_o^T, q8 quantisation in the prologue
+            elif fuse_in and self.tp_size > 1 and self._tp_fused_proj(L.wo, attn, h, L.post_attn_norm, ws, T, eps):
+                pass  # row-parallel shard: q8 prologue GEMV -> 16-bit partial -> all-reduce + residual
             else:
                 if gemv:
                     aq, ads = ws.q8(T, qd)
@@ -703,6 +705,8 @@ class LlamaModel:
                 qmv_fused(L.wd, act, EPI_ADD_F32, h)
                 if lo is not None and lo.down is not None:
                     LR.add_residual(lo.down, act, h)
+                continue
+            if fuse_in and self.tp_size > 1 and self._tp_fused_proj(L.wd, act, h, L.post_ffn_norm, ws, T, eps):
                 continue
             if gemv:
                 aq, ads = ws.q8(T, F)
@@ -851,6 +855,31 @@ class LlamaModel:
         qmatmul(L.wu, xb, EPI_BF16, u)
         LR.add_parts(lp, xb, {"ffn_gate": g, "ffn_up": u})
         K.glu(g, u, act, self.cfg.ffn_act)
+
+    def _tp_fused_proj(self, W: QWeight, x, h: torch.Tensor, post_norm, ws: Workspace, T: int, eps: float) -> bool:
+        """Tensor-parallel decode (T <= 4) row-parallel projection with the q8 quantisation of `x` in the GEMV
+        prologue (no quant_q8 launch, as on one GPU): the shard's 16-bit partial, then the all-reduce + residual.
+        False (nothing launched) where the fused GEMV does not apply."""
+        y16 = ws.y16[:T]
+        if post_norm is not None or not h.is_contiguous() or not qmv_fused(W, x, EPI_BF16, y16):
+            return False
+        self._reduce_add(y16, h, T)
+        return True
+
+    def _reduce_add(self, y16: torch.Tensor, h: torch.Tensor, T: int):
+        """h += all-reduce(y16): the one-shot IPC kernel's fused add when present, else the collective then the
+        16-bit-into-fp32 add."""
+        ar = getattr(self, "custom_ar", None)
+        if ar is not None:
+            ar.add_into(y16, h)
+            return
+        self._allreduce(y16)
+        if h.is_cuda and y16.is_contiguous():
+            N.ensure_act(y16.dtype)
+            N.kcall("mxk_add_act_into_f32", y16.data_ptr(), y16.stride(0), h.data_ptr(), h.stride(0), T,
+                    h.shape[1], N.stream_ptr())
+        else:
+            h.add_(y16)
 
     def _residual_proj(self, W: QWeight, x, xq, xds, h: torch.Tensor, post_norm, ws: Workspace, T: int, eps: float):
         """h += x W^T — or, with a Gemma post-norm, h += rmsnorm(x W^T) * post_norm. Under tensor

@@ -60,7 +60,7 @@ def candidates(M: int, N: int, K: int, qtype: int, can_split: bool) -> list[tupl
         for s in sp:
             out.append(("q2", wm, ks, wn, s))
     if M >= 32:
-        for wm in (1, 2, 4):
+        for wm in (1, 2, 3, 4):
             if 64 * wm > 2 * max(M, 64):
                 continue
             for s in sp:

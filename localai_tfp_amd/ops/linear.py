@@ -386,7 +386,7 @@ def qmv_fusable(W, M: int, epi: int, out_zeroed: bool = False, norm: bool = Fals
         return 0
     ks = 1
     elem = 64 if int(W.qtype) == int(QType.Q8_0) else 256
-    if norm and M == 1 and W.K == 4096 and QMV1_NORM_KS1:
+    if norm and M == 1 and W.K in (4096, 8192) and QMV1_NORM_KS1:
         return 1  # unsplit: the batch-1 qmv1 kernel reads the row once, ahead of the weights (qmv.hip)
     if epi == EPI_ADD_F32 or (epi == EPI_F32 and out_zeroed):
         units = W.K // elem
@@ -430,7 +430,7 @@ def qmv_rope_ok(W, x: torch.Tensor, q_out: torch.Tensor, k_cache: torch.Tensor, 
     """Does mxk_qmv1_rope apply to this qkv part? Callers fusing several parts check EVERY part first, so a
     model whose parts mix block formats (q|k Q4_K, v Q8_0 / MX4F) takes the unfused path for all of them."""
     return not (not QMV_ROPE_FUSE or not isinstance(W, QWeight) or W.layout != "t32"
-                or int(W.qtype) not in QMV_ROPE_QTYPES or W.K != 4096 or x.shape[0] != 1 or not x.is_cuda
+                or int(W.qtype) not in QMV_ROPE_QTYPES or W.K not in (4096, 8192) or x.shape[0] != 1 or not x.is_cuda
                 or x.dtype != torch.float32 or not x.is_contiguous() or k_cache.dtype != torch.bfloat16
                 or v_cache.dtype != torch.bfloat16 or q_out.dtype != torch.bfloat16 or D not in (64, 128) or n_off % 32)
 
@@ -484,6 +484,8 @@ QMM2 = os.environ.get("MX_QMM2", "0") != "0"
 QMM2_FORCE: tuple | None = None  # (wm, ks, wn, splits) override (tests, tools/prof_qmm.py)
 # compiled (wm, ks, wn): wm 32-row MFMA blocks x wn 32-column groups per wave, ks 1 / 2 waves per SIMD
 QMM2_CONFIGS = ((2, 1, 1), (2, 2, 1), (4, 1, 1), (4, 2, 1), (8, 1, 1), (1, 2, 2), (2, 1, 2), (2, 2, 2), (4, 1, 2),
+                # 192-row tiles (M = 384 as two row tiles)
+                (6, 1, 1), (6, 2, 1), (3, 2, 2),
                 # ks | 8: the 8-slot LDS ring (64-row tiles)
                 (2, 9, 1), (2, 10, 1), (1, 10, 2))
 # every t32 block format runs on qmm2 / qmm3 (qmm2_fmt.h decoders)

@@ -397,7 +397,8 @@ def test_qgemm32(qt, M, wm, wn, splits, monkeypatch):
     (64, 2, 1, 1, 1), (64, 2, 2, 1, 3), (17, 2, 2, 1, 1), (128, 4, 2, 1, 1), (77, 4, 2, 1, 2), (128, 4, 1, 1, 4),
     (256, 8, 1, 1, 1), (300, 8, 1, 1, 3), (511, 8, 1, 1, 1), (100, 2, 1, 1, 5),
     (64, 1, 2, 2, 1), (40, 1, 2, 2, 3), (128, 2, 1, 2, 1), (200, 2, 2, 2, 2), (256, 4, 1, 2, 1), (300, 4, 1, 2, 3),
-    (511, 4, 1, 2, 2), (64, 2, 9, 1, 1), (300, 2, 10, 1, 3), (100, 2, 10, 1, 8), (40, 1, 10, 2, 1), (200, 1, 10, 2, 5)])
+    (511, 4, 1, 2, 2), (64, 2, 9, 1, 1), (300, 2, 10, 1, 3), (100, 2, 10, 1, 8), (40, 1, 10, 2, 1), (200, 1, 10, 2, 5),
+    (384, 6, 1, 1, 1), (250, 6, 2, 1, 2), (400, 3, 2, 2, 3)])
 def test_qmm2(qt, M, wm, ks, wn, splits, monkeypatch):
     """qmm2.hip for every epilogue and tile / split-K choice, incl. ragged M / N tails (416 columns = 3.25
     workgroup tiles; with wn = 2 a wave's second group may lie past N), split counts that do not divide the
@@ -436,7 +437,8 @@ def test_qmm2(qt, M, wm, ks, wn, splits, monkeypatch):
 
 @pytest.mark.parametrize("qt", [QType.Q4_K, QType.Q6_K, QType.Q3_K, QType.Q2_K, QType.Q5_K, QType.Q8_0])
 @pytest.mark.parametrize("M,wm,splits", [
-    (64, 1, 1), (40, 1, 3), (128, 2, 1), (77, 2, 2), (200, 2, 5), (256, 4, 1), (300, 4, 3), (511, 4, 2), (17, 1, 1)])
+    (64, 1, 1), (40, 1, 3), (128, 2, 1), (77, 2, 2), (200, 2, 5), (256, 4, 1), (300, 4, 3), (511, 4, 2), (17, 1, 1),
+    (384, 3, 1), (250, 3, 3)])
 def test_qmm3(qt, M, wm, splits, monkeypatch):
     """qmm3.hip (warp-specialised producer / consumer waves) for every epilogue, row tile and split-K choice,
     incl. ragged M / N tails (416 columns: a consumer's second group past N) and split counts that do not
@@ -919,12 +921,13 @@ def test_argmax_keys_merge(tp):
 @pytest.mark.parametrize("qt", [QType.Q4_K, QType.Q6_K, QType.Q3_K])
 def test_qmv1_batch1(qt):
     """The batch-1 qmv1 kernel (activation slice read before the weights, no unit loop): unsplit RMSNorm input at
-    K = 4096 (fp32 store and the interleaved SwiGLU) and split 16-bit input at K = 14336 (accumulate), against
+    K = 4096 / 8192 (two / four units per wave; fp32 store and the interleaved SwiGLU) and split 16-bit input at
+    K = 14336 (accumulate), against
     the fp32 reference and against the generic kernel (mxk_qmv1_enable(0))."""
     from localai_tfp_amd.ops.linear import qmv_fused
     g = torch.Generator().manual_seed(int(qt))
     eps = 1e-5
-    for k, src in ((4096, "norm"), (14336, "act")):
+    for k, src in ((4096, "norm"), (8192, "norm"), (14336, "act")):
         n = 512
         raw, dense = make_w(qt, n, k, seed=k + int(qt))
         W = QWeight.from_ggml(raw, qt, n, k, DEV)
@@ -961,12 +964,13 @@ def test_qmv1_batch1(qt):
 
 @pytest.mark.parametrize("qt", [QType.Q4_K, QType.Q6_K])
 @pytest.mark.parametrize("bias", [False, True])
-def test_qmv_rope_fused(qt, bias):
+@pytest.mark.parametrize("k", [4096, 8192])
+def test_qmv_rope_fused(qt, bias, k):
     """Batch-1 qkv GEMV with RoPE + paged KV append in the epilogue == the unfused qmv + rope_kv kernels: q rows,
     the K and V cache rows at the slot, and nothing else in the caches touched."""
     from localai_tfp_amd.ops.linear import qmv_fused, qmv_rope_fused
     Hq, Hkv, D, bs, nb = 8, 2, 128, 16, 8
-    n, k = (Hq + 2 * Hkv) * D, 4096
+    n = (Hq + 2 * Hkv) * D
     raw, _ = make_w(qt, n, k, seed=11)
     W = QWeight.from_ggml(raw, qt, n, k, DEV)
     assert W.to_t32()
