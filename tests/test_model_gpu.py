@@ -24,7 +24,7 @@ def _run(model, dev, prompt, forced):
     cfg = model.cfg
     bs = 16
     kv = KVCache(cfg.n_layers, 64, model.n_kv, bs, cfg.head_dim, dev)
-    ws = Workspace(cfg, 256, 8, dev)
+    ws = Workspace(cfg, 256, 8, dev, model.tp_size)
     blocks = list(range(1, 1 + (len(prompt) + len(forced) + bs) // bs + 1))
     bt = torch.tensor([blocks], dtype=torch.int32, device=dev)
     P = len(prompt)
@@ -208,6 +208,26 @@ def test_batch1_rope_fusion_with_mixed_qkv_formats():
     assert len({int(w.qtype) for w in m_gpu.layers[0].qkv_parts}) == 2
     prompt = list(np.random.default_rng(1).integers(0, cfg.vocab, 12))
     forced = [7, 300, 11]
+    a = _run(m_cpu, "cpu", prompt, forced)
+    b = _run(m_gpu, "cuda", prompt, forced)
+    for x, y in zip(a, b):
+        r = float((x - y).norm() / x.norm())
+        assert r < 6e-2, r
+
+
+def test_tp_shard_batch1_fusions_match_cpu():
+    """One rank's shard of a tensor-parallel model (tp 2, no process group: the collectives are no-ops, as in
+    bench.py --tp-rehearsal) with 70B-class 8192-wide rows: the batch-1 decode takes the fused paths — qkv
+    RMSNorm + RoPE + KV append in one GEMV with four weight units per wave (qmv1 K = 8192), the row-parallel
+    o_proj / down shards on the q8-prologue GEMV writing the 16-bit partial — and matches the CPU reference of
+    the same shard."""
+    cfg = tiny_config(hidden=8192, ffn=1024, n_heads=64, n_kv_heads=8, head_dim=128, rope_dim=128, vocab=512,
+                      n_layers=1)
+    src = synthetic_source(cfg, "Q4_K_M", seed=13, shard_gen=True)
+    m_cpu = LlamaModel.load(cfg, src, "cpu", 0, 2, None)
+    m_gpu = LlamaModel.load(cfg, src, "cuda", 0, 2, None)
+    prompt = list(np.random.default_rng(2).integers(0, cfg.vocab, 9))
+    forced = [5, 77, 301]
     a = _run(m_cpu, "cpu", prompt, forced)
     b = _run(m_gpu, "cuda", prompt, forced)
     for x, y in zip(a, b):
