@@ -13,6 +13,8 @@
 //   head) so every K/V tile staged in LDS is reused by all heads of the group. K is stored
 //   XOR-swizzled for conflict-free ds_read_b128 B-fragments; V is read with ds_read_b64_tr_b16
 //   (hardware transpose) from a region-swizzled image; P goes register -> LDS -> A-fragment.
+#include <type_traits>
+
 #include "mx_common.h"
 
 #define LOG2E 1.4426950408889634f
@@ -681,7 +683,7 @@ __global__ __launch_bounds__(512) void attn_prefill_kernel(const bf16_t* __restr
     char* k_lds = smem;
     char* v_lds = smem + KBYTES;
     char* p_lds = smem + KBYTES + VBYTES;
-    const int NT = NW * 64;
+    constexpr int NT_C = NW * 64;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int g = lane >> 4, col = lane & 15;
     const int tile = blockIdx.x;
@@ -720,23 +722,47 @@ __global__ __launch_bounds__(512) void attn_prefill_kernel(const bf16_t* __restr
     for (int i = 0; i < 4; ++i) { mrow[i] = -INFINITY; lrow[i] = 0.f; }
     char* pw = p_lds + wave * 16 * PSTRIDE;
 
-    for (int kt0 = kt_begin; kt0 < kv_end; kt0 += KT) {
-        // ---- stage K and V tiles (64 keys x D) ----
-        constexpr int CH = KT * D / 8;  // 16-byte chunks per tile
-        for (int id = threadIdx.x; id < CH; id += NT) {
+    // K / V tiles are software-pipelined one tile deep: tile t + 1's global loads (block-table entry, then the
+    // 16-byte chunks) are issued right after tile t is staged in LDS, so their latency hides behind tile t's
+    // MFMAs and softmax instead of opening every tile (short prompt chunks run only a few tiles per workgroup)
+    constexpr int CH = KT * D / 8;              // 16-byte chunks per tile
+    constexpr int NCH = (CH + NT_C - 1) / NT_C;  // chunks per thread
+    using KRaw = typename std::conditional<KV8, uint2, uint4>::type;
+    KRaw kr[NCH], vr[NCH];
+    auto load_tile = [&](int kt0) {
+#pragma unroll
+        for (int j = 0; j < NCH; ++j) {
+            const int id = threadIdx.x + j * NT_C;
             const int p = id / (D / 8), c = id % (D / 8);
             const int pos = kt0 + p;
-            uint4 kv = make_uint4(0, 0, 0, 0), vv = make_uint4(0, 0, 0, 0);
-            if (pos < kv_end) {
+            kr[j] = KRaw{};
+            vr[j] = KRaw{};
+            if (id < CH && pos < kv_end) {
                 const int blk = bt[pos / bs], off = pos % bs;
                 const size_t eo = (((size_t)blk * Hkv + kvh) * bs + off) * D + c * 8;
                 if constexpr (KV8) {
-                    kv = fp8x8_to_bf16x8(*(const uint2*)((const uint8_t*)kc + eo));
-                    vv = fp8x8_to_bf16x8(*(const uint2*)((const uint8_t*)vc + eo));
+                    kr[j] = *(const uint2*)((const uint8_t*)kc + eo);
+                    vr[j] = *(const uint2*)((const uint8_t*)vc + eo);
                 } else {
-                    kv = *(const uint4*)((const bf16_t*)kc + eo);
-                    vv = *(const uint4*)((const bf16_t*)vc + eo);
+                    kr[j] = *(const uint4*)((const bf16_t*)kc + eo);
+                    vr[j] = *(const uint4*)((const bf16_t*)vc + eo);
                 }
+            }
+        }
+    };
+    auto store_tile = [&]() {
+#pragma unroll
+        for (int j = 0; j < NCH; ++j) {
+            const int id = threadIdx.x + j * NT_C;
+            if (id >= CH) continue;
+            const int p = id / (D / 8), c = id % (D / 8);
+            uint4 kv, vv;
+            if constexpr (KV8) {
+                kv = fp8x8_to_bf16x8(kr[j]);
+                vv = fp8x8_to_bf16x8(vr[j]);
+            } else {
+                kv = kr[j];
+                vv = vr[j];
             }
             *(uint4*)(k_lds + k_lds_off<D>(p, c)) = kv;
             if constexpr (VT == 0) {
@@ -744,10 +770,16 @@ __global__ __launch_bounds__(512) void attn_prefill_kernel(const bf16_t* __restr
             } else {
                 const uint32_t w[4] = {vv.x, vv.y, vv.z, vv.w};
 #pragma unroll
-                for (int j = 0; j < 8; ++j)
-                    *(bf16_t*)(v_lds + (8 * c + j) * VTSTRIDE + 2 * p) = (bf16_t)(w[j >> 1] >> (16 * (j & 1)));
+                for (int jj = 0; jj < 8; ++jj)
+                    *(bf16_t*)(v_lds + (8 * c + jj) * VTSTRIDE + 2 * p) = (bf16_t)(w[jj >> 1] >> (16 * (jj & 1)));
             }
         }
+    };
+    if (kt_begin < kv_end) load_tile(kt_begin);
+    for (int kt0 = kt_begin; kt0 < kv_end; kt0 += KT) {
+        // ---- stage this K and V tile (64 keys x D), then request the next one ----
+        store_tile();
+        if (kt0 + KT < kv_end) load_tile(kt0 + KT);
         __syncthreads();
         // ---- S = Q K^T : 16 rows x 64 keys ----
         f32x4 sacc[4];

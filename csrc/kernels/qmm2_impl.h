@@ -405,6 +405,8 @@ static int dispatch_qmm2(int wm, int ks, int wn, const uint16_t* A, int lda, con
     Q2_CASE(1, 2, 2) Q2_CASE(2, 1, 2) Q2_CASE(2, 2, 2) Q2_CASE(4, 1, 2)
     // 192-row tiles: M = 384 (a c128 decode batch + a 256-token prompt chunk) in two row tiles, no padding rows
     Q2_CASE(6, 1, 1) Q2_CASE(6, 2, 1) Q2_CASE(3, 2, 2)
+    // 224-row tiles: M in (384, 448] (a decode batch + a prompt chunk a little over 256 tokens) in two row tiles
+    Q2_CASE(7, 1, 1)
     Q2_DEEP(2, 1, 1) Q2_DEEP(2, 2, 1) Q2_DEEP(1, 2, 2)
 #undef Q2_DEEP
 #undef Q2_CASE

@@ -472,10 +472,16 @@ struct QRope {
 
 // NU: weight units per wave (2: K slices <= 16 units, e.g. K = 4096; 4: <= 32 units, the 8192-wide rows of 70B-class
 // models). The activation slice is read in NU / 2 passes of 8 elements per thread (4096 per pass).
+// Split K (gridDim.y > 1) with an epilogue that needs whole sums (RoPE / KV append, SwiGLU, 16-bit store): the
+// workgroups' partial column sums meet in the fp32 workspace `skw` and the last workgroup of each column group
+// (ticket `skc[g]`) runs the epilogue on the total, then re-zeroes its workspace columns and ticket (graph replays
+// start clean). Lets the narrow batch-1 projections (qkv parts of 1024-6144 columns: 32-192 column groups) use
+// every CU. SRC_NORM then reads the whole row once more for the norm's sum of squares.
 template <int QT, int EPI, bool F16, int SRC, int NU = 2>
 __global__ __launch_bounds__(64 * QMV_WAVES) void qmv1_kernel(const uint8_t* __restrict__ W, int N, int K,
                                                               void* __restrict__ Cv, const void* __restrict__ xsrc,
-                                                              const float* __restrict__ nw, float eps, QRope rp) {
+                                                              const float* __restrict__ nw, float eps, QRope rp,
+                                                              float* __restrict__ skw, unsigned* __restrict__ skc) {
     using U = TUnit<QT>;
     constexpr int NT = 64 * QMV_WAVES;
     constexpr int NP = NU / 2;  // activation passes of 8 elements per thread
@@ -530,10 +536,18 @@ __global__ __launch_bounds__(64 * QMV_WAVES) void qmv1_kernel(const uint8_t* __r
     float rs = 1.f;
     if constexpr (SRC == SRC_NORM) {
         float ss = 0.f;
+        if (gridDim.y == 1) {  // the slice is the whole row
 #pragma unroll
-        for (int ps = 0; ps < NP; ++ps)
+            for (int ps = 0; ps < NP; ++ps)
 #pragma unroll
-            for (int j = 0; j < 8; ++j) ss += a8[ps][j] * a8[ps][j];
+                for (int j = 0; j < 8; ++j) ss += a8[ps][j] * a8[ps][j];
+        } else {
+            for (int e = 8 * threadIdx.x; e < K; e += 8 * NT) {
+                const float4 v0 = *(const float4*)((const float*)xsrc + e), v1 = *(const float4*)((const float*)xsrc + e + 4);
+                ss += v0.x * v0.x + v0.y * v0.y + v0.z * v0.z + v0.w * v0.w + v1.x * v1.x + v1.y * v1.y + v1.z * v1.z +
+                      v1.w * v1.w;
+            }
+        }
         ss = wave_sum(ss);
         if (lane == 0) nred[wave] = ss;
     }
@@ -588,6 +602,20 @@ __global__ __launch_bounds__(64 * QMV_WAVES) void qmv1_kernel(const uint8_t* __r
         for (int w = 0; w < QMV_WAVES; ++w) v += red[w][r];
     }
     const int n = g * 32 + r;
+    if (EPI != E16_ADD_F32 && gridDim.y > 1) {
+        if (h == 0) atomicAdd(skw + n, v);
+        __threadfence();  // release: this workgroup's partials before its ticket
+        unsigned last = 0;
+        if (lane == 0) last = atomicAdd(skc + g, 1u) == gridDim.y - 1;
+        last = __shfl(last, 0);
+        if (!last) return;
+        __threadfence();  // acquire: every workgroup's partials
+        if (h == 0) {
+            v = __hip_atomic_load(skw + n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            atomicExch(skw + n, 0.f);
+        }
+        if (lane == 0) atomicExch(skc + g, 0u);
+    }
     if constexpr (EPI == EPI_ROPEKV) {
         if (rp.bias) v += rp.bias[n];
         const float partner = __shfl_xor(v, 1);  // the other element of this adjacent rotation pair
@@ -749,17 +777,17 @@ static int launch_qmv(const int8_t* xq, const float2* xds, const uint8_t* W, int
             if (src == SRC_ACT) {
                 if (four)
                     MX_ACT_DISPATCH(qmv1_kernel<QT, EPI, F16, SRC_ACT, 4><<<dim3(N / 32, ks), 64 * QMV_WAVES, lds, st>>>(
-                        W, N, K, C, xsrc, nullptr, 0.f, QRope{}));
+                        W, N, K, C, xsrc, nullptr, 0.f, QRope{}, nullptr, nullptr));
                 else
                     MX_ACT_DISPATCH(qmv1_kernel<QT, EPI, F16, SRC_ACT><<<dim3(N / 32, ks), 64 * QMV_WAVES, lds, st>>>(
-                        W, N, K, C, xsrc, nullptr, 0.f, QRope{}));
+                        W, N, K, C, xsrc, nullptr, 0.f, QRope{}, nullptr, nullptr));
             } else {
                 if (four)
                     MX_ACT_DISPATCH(qmv1_kernel<QT, EPI, F16, SRC_NORM, 4><<<dim3(N / 32, ks), 64 * QMV_WAVES, lds, st>>>(
-                        W, N, K, C, xsrc, nw, eps, QRope{}));
+                        W, N, K, C, xsrc, nw, eps, QRope{}, nullptr, nullptr));
                 else
                     MX_ACT_DISPATCH(qmv1_kernel<QT, EPI, F16, SRC_NORM><<<dim3(N / 32, ks), 64 * QMV_WAVES, lds, st>>>(
-                        W, N, K, C, xsrc, nw, eps, QRope{}));
+                        W, N, K, C, xsrc, nw, eps, QRope{}, nullptr, nullptr));
             }
             MXK_CHECK_LAUNCH();
         }
@@ -849,18 +877,20 @@ extern "C" int mxk_qmv_x(int qtype, int epi, int src, const void* x, int ldx, co
 extern "C" int mxk_qmv1_rope(int qtype, const float* x, const float* nw, float eps, const uint8_t* W, int N, int K,
                              int n_off, const int* pos, const int* slots, const float* inv_freq, const float* bias,
                              float attn_factor, int Hq, int Hkv, int D, bf16_t* qo, bf16_t* kc, bf16_t* vc,
-                             int block_size, hipStream_t st) {
+                             int block_size, int ks, float* skw, unsigned* skc, hipStream_t st) {
+    // ks > 1: split K over ks workgroups per column group (skw: >= N zeroed floats, skc: >= N / 32 zeroed tickets)
+    if (ks < 1 || (ks > 1 && (!skw || !skc)) || (K / 256) % ks) return (int)hipErrorInvalidValue;
     if ((K != 4096 && K != 8192) || N % 32 || (D != 64 && D != 128) || n_off % 32 || ((uintptr_t)x & 15))
         return (int)hipErrorInvalidValue;
     const QRope rp{pos, slots, inv_freq, bias, attn_factor, Hq, Hkv, D, n_off, block_size, qo, kc, vc};
     const size_t lds = (size_t)K + K / 32 * sizeof(float2);
 #define QR1(QT_)                                                                                                     \
     if (K == 8192)                                                                                                   \
-        qmv1_kernel<QT_, EPI_ROPEKV, true, SRC_NORM, 4><<<dim3(N / 32, 1), 64 * QMV_WAVES, lds, st>>>(W, N, K, nullptr, x, \
-                                                                                                   nw, eps, rp);     \
+        qmv1_kernel<QT_, EPI_ROPEKV, true, SRC_NORM, 4><<<dim3(N / 32, ks), 64 * QMV_WAVES, lds, st>>>(W, N, K, nullptr, x, \
+                                                                                                    nw, eps, rp, skw, skc); \
     else                                                                                                             \
-        qmv1_kernel<QT_, EPI_ROPEKV, true, SRC_NORM><<<dim3(N / 32, 1), 64 * QMV_WAVES, lds, st>>>(W, N, K, nullptr, x, nw, \
-                                                                                                eps, rp)
+        qmv1_kernel<QT_, EPI_ROPEKV, true, SRC_NORM><<<dim3(N / 32, ks), 64 * QMV_WAVES, lds, st>>>(W, N, K, nullptr, x, nw, \
+                                                                                                 eps, rp, skw, skc)
     switch (qtype) {
         case MXQ_Q4_K: QR1(MXQ_Q4_K); break;
         case MXQ_Q5_K: QR1(MXQ_Q5_K); break;

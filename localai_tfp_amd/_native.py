@@ -42,7 +42,7 @@ KERNEL_SIGS = {
     "mxk_qmm3": [I, I, I, P, I, P, I, I, I, I, P, I, P],
     "mxk_sample_trace": [I, P],
     "mxk_qmv1_enable": [I],
-    "mxk_qmv1_rope": [I, P, P, F, P, I, I, I, P, P, P, P, F, I, I, I, P, P, P, I, P],
+    "mxk_qmv1_rope": [I, P, P, F, P, I, I, I, P, P, P, P, F, I, I, I, P, P, P, I, I, P, P, P],
     "mxk_qmm3_dbg": [I, I, P, I, P, I, I, I, P, I, P],
     "mxk_qmm_ws_dbg": [I],
     "mxk_qmv": [I, I, P, P, P, I, I, I, I, P, I, P],

@@ -80,7 +80,7 @@ def gc_tune():
 @dataclass
 class EngineConfig:
     max_num_seqs: int = 256
-    max_batched_tokens: int = 2048
+    max_batched_tokens: int = 512  # tokens per step: llama.cpp's n_batch default (LocalAI `batch: 512`)
     prefill_chunk: int | None = None  # prompt tokens per sequence per step (None: the whole step budget)
     max_model_len: int = 8192
     block_size: int = 16

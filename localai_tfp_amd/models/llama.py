@@ -130,6 +130,10 @@ class Workspace:
         # zero-initialised and kept zero between uses: rope_kv re-zeroes the rows it consumes, so the
         # split-K QKV GEMM (atomic accumulate) never needs a separate fill launch
         self.qkv = torch.zeros((T, qd + 2 * kvd), dtype=torch.float32, device=dev)
+        # split-K workspace of the batch-1 qkv GEMV with the RoPE epilogue (ops/linear.py qmv_rope_fused): zeroed,
+        # and re-zeroed by the kernel after every use
+        self.sk_ws = torch.zeros(qd + 2 * kvd, dtype=torch.float32, device=dev)
+        self.sk_cnt = torch.zeros(-(-(qd + 2 * kvd) // 32), dtype=torch.int32, device=dev)
         self.q = torch.empty((T, qd), dtype=torch.bfloat16, device=dev)
         self.attn = torch.empty((T, qd), dtype=act, device=dev)
         self.act = torch.empty((T, F), dtype=act, device=dev)
@@ -614,7 +618,8 @@ class LlamaModel:
                 for w in L.qkv_parts:
                     b = L.bqkv[o2:o2 + w.N] if L.bqkv is not None else None
                     if not qmv_rope_fused(w, h, L.attn_norm, eps, o2, fb.positions, fb.slots, inv_freq, b, attn_factor,
-                                          Hq, Hkv, D, q.view(T, Hq, D), kc, vc, kv.block_size):
+                                          Hq, Hkv, D, q.view(T, Hq, D), kc, vc, kv.block_size,
+                                          sk=(ws.sk_ws, ws.sk_cnt)):
                         raise RuntimeError("qkv RoPE fusion applied to some parts only")
                     o2 += w.N
             for w in (L.qkv_parts if off == 0 and not rope_fused else ()):

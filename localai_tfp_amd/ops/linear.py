@@ -435,16 +435,35 @@ def qmv_rope_ok(W, x: torch.Tensor, q_out: torch.Tensor, k_cache: torch.Tensor, 
                 or v_cache.dtype != torch.bfloat16 or q_out.dtype != torch.bfloat16 or D not in (64, 128) or n_off % 32)
 
 
+QMV_ROPE_SPLIT = os.environ.get("MX_QMV_ROPE_SPLIT", "1") != "0"
+
+
+def qmv_rope_split(W: QWeight) -> int:
+    """K-split of the batch-1 qkv GEMV: narrow parts (1024-6144 columns = 32-192 column groups) spread over the CUs,
+    keeping at least two 256-element units per workgroup; the last workgroup of a column group runs the epilogue."""
+    if not QMV_ROPE_SPLIT:
+        return 1
+    groups, units = W.N // 32, W.K // 256
+    ks = 1
+    while groups * ks < CU_COUNT and units % (ks * 2) == 0 and units // (ks * 2) >= 2:
+        ks *= 2
+    return ks
+
+
 def qmv_rope_fused(W: QWeight, x: torch.Tensor, norm: torch.Tensor, eps: float, n_off: int, positions, slots,
                    inv_freq: torch.Tensor, bias, attn_factor: float, Hq: int, Hkv: int, D: int, q_out: torch.Tensor,
-                   k_cache: torch.Tensor, v_cache: torch.Tensor, block_size: int) -> bool:
+                   k_cache: torch.Tensor, v_cache: torch.Tensor, block_size: int, sk=None) -> bool:
     """Batch-1 qkv part: RMSNorm -> q8 -> GEMV -> (+bias) -> RoPE (adjacent pairs, whole head) -> q_out or the
-    paged K/V caches at slots[0], one launch (qmv.hip mxk_qmv1_rope). False: not applicable, nothing launched."""
+    paged K/V caches at slots[0], one launch (qmv.hip mxk_qmv1_rope). sk = (fp32 workspace >= N, int32 tickets
+    >= N / 32), both zeroed: the GEMV splits K over several workgroups per column group. False: not applicable,
+    nothing launched."""
     if not qmv_rope_ok(W, x, q_out, k_cache, v_cache, D, n_off):
         return False
+    ks = qmv_rope_split(W) if sk is not None and sk[0].numel() >= W.N and sk[1].numel() >= W.N // 32 else 1
     N.kcall("mxk_qmv1_rope", int(W.qtype), x.data_ptr(), norm.data_ptr(), float(eps), W.data.data_ptr(), W.N, W.K,
             n_off, positions.data_ptr(), slots.data_ptr(), inv_freq.data_ptr(), N.ptr(bias), float(attn_factor), Hq,
-            Hkv, D, q_out.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), block_size, N.stream_ptr())
+            Hkv, D, q_out.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), block_size, ks,
+            sk[0].data_ptr() if ks > 1 else 0, sk[1].data_ptr() if ks > 1 else 0, N.stream_ptr())
     return True
 
 
@@ -484,8 +503,8 @@ QMM2 = os.environ.get("MX_QMM2", "0") != "0"
 QMM2_FORCE: tuple | None = None  # (wm, ks, wn, splits) override (tests, tools/prof_qmm.py)
 # compiled (wm, ks, wn): wm 32-row MFMA blocks x wn 32-column groups per wave, ks 1 / 2 waves per SIMD
 QMM2_CONFIGS = ((2, 1, 1), (2, 2, 1), (4, 1, 1), (4, 2, 1), (8, 1, 1), (1, 2, 2), (2, 1, 2), (2, 2, 2), (4, 1, 2),
-                # 192-row tiles (M = 384 as two row tiles)
-                (6, 1, 1), (6, 2, 1), (3, 2, 2),
+                # 192- / 224-row tiles (M = 384 / 448 as two row tiles)
+                (6, 1, 1), (6, 2, 1), (3, 2, 2), (7, 1, 1),
                 # ks | 8: the 8-slot LDS ring (64-row tiles)
                 (2, 9, 1), (2, 10, 1), (1, 10, 2))
 # every t32 block format runs on qmm2 / qmm3 (qmm2_fmt.h decoders)

@@ -398,7 +398,7 @@ def test_qgemm32(qt, M, wm, wn, splits, monkeypatch):
     (256, 8, 1, 1, 1), (300, 8, 1, 1, 3), (511, 8, 1, 1, 1), (100, 2, 1, 1, 5),
     (64, 1, 2, 2, 1), (40, 1, 2, 2, 3), (128, 2, 1, 2, 1), (200, 2, 2, 2, 2), (256, 4, 1, 2, 1), (300, 4, 1, 2, 3),
     (511, 4, 1, 2, 2), (64, 2, 9, 1, 1), (300, 2, 10, 1, 3), (100, 2, 10, 1, 8), (40, 1, 10, 2, 1), (200, 1, 10, 2, 5),
-    (384, 6, 1, 1, 1), (250, 6, 2, 1, 2), (400, 3, 2, 2, 3)])
+    (384, 6, 1, 1, 1), (250, 6, 2, 1, 2), (400, 3, 2, 2, 3), (448, 7, 1, 1, 1), (300, 7, 1, 1, 3)])
 def test_qmm2(qt, M, wm, ks, wn, splits, monkeypatch):
     """qmm2.hip for every epilogue and tile / split-K choice, incl. ragged M / N tails (416 columns = 3.25
     workgroup tiles; with wn = 2 a wave's second group may lie past N), split counts that do not divide the
@@ -965,9 +965,11 @@ def test_qmv1_batch1(qt):
 @pytest.mark.parametrize("qt", [QType.Q4_K, QType.Q6_K])
 @pytest.mark.parametrize("bias", [False, True])
 @pytest.mark.parametrize("k", [4096, 8192])
-def test_qmv_rope_fused(qt, bias, k):
+@pytest.mark.parametrize("split", [False, True])
+def test_qmv_rope_fused(qt, bias, k, split):
     """Batch-1 qkv GEMV with RoPE + paged KV append in the epilogue == the unfused qmv + rope_kv kernels: q rows,
-    the K and V cache rows at the slot, and nothing else in the caches touched."""
+    the K and V cache rows at the slot, and nothing else in the caches touched. split: K split over several
+    workgroups per column group, the last one running the epilogue; its workspace and tickets end re-zeroed."""
     from localai_tfp_amd.ops.linear import qmv_fused, qmv_rope_fused
     Hq, Hkv, D, bs, nb = 8, 2, 128, 16, 8
     n = (Hq + 2 * Hkv) * D
@@ -992,12 +994,18 @@ def test_qmv_rope_fused(qt, bias, k):
     q = torch.zeros_like(q_ref)
     kc = torch.zeros_like(kc_ref)
     vc = torch.zeros_like(vc_ref)
-    split = (Hq + Hkv) * D
-    for off, rows in ((0, slice(0, split)), (split, slice(split, n))):
+    cut = (Hq + Hkv) * D
+    sk = (torch.zeros(n, device=DEV), torch.zeros(n // 32, dtype=torch.int32, device=DEV)) if split else None
+    for off, rows in ((0, slice(0, cut)), (cut, slice(cut, n))):
         Wp = QWeight.from_ggml(raw.reshape(n, -1)[rows], qt, rows.stop - rows.start, k, DEV)
         assert Wp.to_t32()
+        if split:
+            from localai_tfp_amd.ops.linear import qmv_rope_split
+            assert qmv_rope_split(Wp) > 1
         b = bq[rows] if bq is not None else None
-        assert qmv_rope_fused(Wp, h, nw, 1e-5, off, pos, slots, inv_freq, b, 1.0, Hq, Hkv, D, q, kc, vc, bs)
+        assert qmv_rope_fused(Wp, h, nw, 1e-5, off, pos, slots, inv_freq, b, 1.0, Hq, Hkv, D, q, kc, vc, bs, sk=sk)
+    if split:
+        assert float(sk[0].abs().sum()) == 0.0 and int(sk[1].abs().sum()) == 0
     assert rel(q.float(), q_ref.float()) < 2e-2
     assert rel(kc.float(), kc_ref.float()) < 2e-2 and rel(vc.float(), vc_ref.float()) < 2e-2
     touched = torch.zeros(nb, bs, dtype=torch.bool)
