@@ -594,9 +594,10 @@ static int launch_decode_mfma(const bf16_t* q, int q_stride, const void* kc, con
                               float2* part_ml, float* part_o, int* part_cnt, int kv8, hipStream_t st) {
     dim3 grid(Hkv, B, n_parts);
     static_assert(16 * D * 4 <= dec_wave_lds<D>(), "merge buffer");
-    // 512-key partitions run 16 waves per workgroup (one 32-key tile each), smaller ones 4
+    // 512-key partitions run 16 waves per workgroup (one 32-key tile each), 256-key ones 8, smaller ones 4
     const bool wide = part_size >= 512 && !kv8 && B < 8;  // (large batches keep 4-wave workgroups)
-    const int NWs = wide ? 16 : 4;
+    const bool mid = !wide && part_size >= 256 && !kv8 && B < 8;
+    const int NWs = wide ? 16 : mid ? 8 : 4;
     const size_t lds = NWs * dec_wave_lds<D>() + NWs * 32 * 4;
     MX_ACT_DISPATCH({
         if (kv8)
@@ -612,6 +613,16 @@ static int launch_decode_mfma(const bf16_t* q, int q_stride, const void* kc, con
                 attr = true;
             }
             attn_decode_mfma_kernel<D, F16, false, 16><<<grid, 1024, lds, st>>>(
+                q, q_stride, kc, vc, bt, bt_stride, seq_lens, Hkv, G, bs, scale, window, softcap, part_size, n_parts,
+                out, out_stride, part_ml, part_o, part_cnt);
+        } else if (mid) {
+            static bool attr8 = false;
+            if (!attr8) {
+                (void)hipFuncSetAttribute((const void*)attn_decode_mfma_kernel<D, F16, false, 8>,
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+                attr8 = true;
+            }
+            attn_decode_mfma_kernel<D, F16, false, 8><<<grid, 512, lds, st>>>(
                 q, q_stride, kc, vc, bt, bt_stride, seq_lens, Hkv, G, bs, scale, window, softcap, part_size, n_parts,
                 out, out_stride, part_ml, part_o, part_cnt);
         } else

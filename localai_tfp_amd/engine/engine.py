@@ -375,7 +375,10 @@ class LLMEngine:
         if self.recurrent:
             self.ws = model.make_workspace(max(c.max_batched_tokens, c.max_num_seqs), c.max_num_seqs)
         else:
-            self.ws = Workspace(mc, max(c.max_batched_tokens, c.max_num_seqs), c.max_num_seqs, self.device,
+            # rows: a mixed step's graph bucket pads its decode rows to the decode bucket (<= max_num_seqs) and its
+            # prompt tokens to the next mixed-graph token bucket, so the workspace holds both paddings at once
+            p_max = next((x for x in c.mixed_graph_tokens if x >= c.max_batched_tokens), c.max_batched_tokens)
+            self.ws = Workspace(mc, max(c.max_batched_tokens, c.max_num_seqs + p_max), c.max_num_seqs, self.device,
                                 model.tp_size, max_parts)
         self.sampler = SamplerBatch(self.device)
         self.handles: dict[int, RequestHandle] = {}

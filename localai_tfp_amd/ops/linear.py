@@ -435,7 +435,9 @@ def qmv_rope_ok(W, x: torch.Tensor, q_out: torch.Tensor, k_cache: torch.Tensor, 
                 or v_cache.dtype != torch.bfloat16 or q_out.dtype != torch.bfloat16 or D not in (64, 128) or n_off % 32)
 
 
-QMV_ROPE_SPLIT = os.environ.get("MX_QMV_ROPE_SPLIT", "1") != "0"
+# off by default: the ticket / fence / atomic chain cost more than the extra workgroups bought at batch 1 (8B c1
+# 469 vs 529 tok/s, 70B TP8 shard unchanged; gpurun_out/k12)
+QMV_ROPE_SPLIT = os.environ.get("MX_QMV_ROPE_SPLIT", "0") == "1"
 
 
 def qmv_rope_split(W: QWeight) -> int:

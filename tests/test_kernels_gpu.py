@@ -966,7 +966,7 @@ def test_qmv1_batch1(qt):
 @pytest.mark.parametrize("bias", [False, True])
 @pytest.mark.parametrize("k", [4096, 8192])
 @pytest.mark.parametrize("split", [False, True])
-def test_qmv_rope_fused(qt, bias, k, split):
+def test_qmv_rope_fused(qt, bias, k, split, monkeypatch):
     """Batch-1 qkv GEMV with RoPE + paged KV append in the epilogue == the unfused qmv + rope_kv kernels: q rows,
     the K and V cache rows at the slot, and nothing else in the caches touched. split: K split over several
     workgroups per column group, the last one running the epilogue; its workspace and tickets end re-zeroed."""
@@ -1000,8 +1000,9 @@ def test_qmv_rope_fused(qt, bias, k, split):
         Wp = QWeight.from_ggml(raw.reshape(n, -1)[rows], qt, rows.stop - rows.start, k, DEV)
         assert Wp.to_t32()
         if split:
-            from localai_tfp_amd.ops.linear import qmv_rope_split
-            assert qmv_rope_split(Wp) > 1
+            from localai_tfp_amd.ops import linear as L
+            monkeypatch.setattr(L, "QMV_ROPE_SPLIT", True)
+            assert L.qmv_rope_split(Wp) > 1
         b = bq[rows] if bq is not None else None
         assert qmv_rope_fused(Wp, h, nw, 1e-5, off, pos, slots, inv_freq, b, 1.0, Hq, Hkv, D, q, kc, vc, bs, sk=sk)
     if split:
