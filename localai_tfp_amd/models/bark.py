@@ -65,6 +65,7 @@ class _GPT:
 
     def __init__(self, sd: dict, prefix: str, cfg: dict, device, dtype, causal: bool):
         self.causal = causal
+        self.gelu_approx = cfg.get("gelu_approx", "none")  # "tanh": GPT-2's gelu_new (XTTS, models/xtts.py)
         self.H = cfg["num_heads"]
         self.D = cfg["hidden_size"]
         self.device, self.dtype = torch.device(device), dtype
@@ -106,9 +107,14 @@ class _GPT:
         """x: input embeddings [B, S, D] fp32 (positions pos0..pos0+S) -> logits [B, S, V] fp32.
         Attention runs on the MFMA flash kernel (ops.core.attn_dense): causal masks are bottom-right aligned,
         so a cached chunk at pos0 attends keys 0..pos0+S-1 exactly as the reference's chunk mask."""
+        x = x + self.pos[pos0:pos0 + x.shape[1]][None]
+        return F.linear(self.trunk(x, pos0, cache), self.heads[head]).float()
+
+    def trunk(self, x: torch.Tensor, pos0: int = 0, cache=None) -> torch.Tensor:
+        """The transformer blocks + final LayerNorm over input embeddings x [B, S, D] fp32 (positions already
+        added) -> [B, S, D] 16-bit."""
         B, S, _ = x.shape
         D, hd = self.D, self.D // self.H
-        x = x + self.pos[pos0:pos0 + S][None]
         for li, L in enumerate(self.layers):
             h = self._ln(x, L["ln1"])
             qkv = F.linear(h, L["qkv"], L["qkv_b"]).view(B * S, 3 * D)
@@ -124,16 +130,20 @@ class _GPT:
             attn_dense(q, k, v, a, B, S, Sk, self.H, self.H, hd, hd ** -0.5, causal=self.causal, kv_rows=rows)
             x = x + F.linear(a.view(B, S, D), L["o"], L["o_b"]).float()
             h = self._ln(x, L["ln2"])
-            x = x + F.linear(F.gelu(F.linear(h, L["fc1"], L["fc1_b"])), L["fc2"], L["fc2_b"]).float()
-        h = self._ln(x, self.ln_f)
-        return F.linear(h, self.heads[head]).float()
+            x = x + F.linear(F.gelu(F.linear(h, L["fc1"], L["fc1_b"]), approximate=self.gelu_approx), L["fc2"],
+                             L["fc2_b"]).float()
+        return self._ln(x, self.ln_f)
 
     def decode_step(self, tok: torch.Tensor, pos: torch.Tensor, cache, head: int = 0) -> torch.Tensor:
         """One token (int64 [1], device) at device position pos (int64 [1]) against the cache -> logits [1, V]
         fp32. Shape-static (no host values), so the decode loop replays it as one HIP graph."""
+        x = (self.emb[0].index_select(0, tok).float() + self.pos.index_select(0, pos))[None]  # [1, 1, D]
+        return F.linear(self.decode_trunk(x, pos, cache), self.heads[head]).float()[:, -1]
+
+    def decode_trunk(self, x: torch.Tensor, pos: torch.Tensor, cache) -> torch.Tensor:
+        """The blocks for one token embedding x [1, 1, D] fp32 at device position pos -> [1, 1, D] 16-bit."""
         D, hd = self.D, self.D // self.H
         T = cache[0][0].shape[1]
-        x = (self.emb[0].index_select(0, tok).float() + self.pos.index_select(0, pos))[None]  # [1, 1, D]
         klen = pos.to(torch.int32) + 1
         a = torch.empty(1, D, dtype=self.dtype, device=self.device)
         for li, L in enumerate(self.layers):
@@ -146,9 +156,9 @@ class _GPT:
                        kv_rows=T)
             x = x + F.linear(a.view(1, 1, D), L["o"], L["o_b"]).float()
             h = self._ln(x, L["ln2"])
-            x = x + F.linear(F.gelu(F.linear(h, L["fc1"], L["fc1_b"])), L["fc2"], L["fc2_b"]).float()
-        h = self._ln(x, self.ln_f)
-        return F.linear(h, self.heads[head]).float()[:, -1]
+            x = x + F.linear(F.gelu(F.linear(h, L["fc1"], L["fc1_b"]), approximate=self.gelu_approx), L["fc2"],
+                             L["fc2_b"]).float()
+        return self._ln(x, self.ln_f)
 
     def embed(self, ids: torch.Tensor, table: int = 0) -> torch.Tensor:
         return self.emb[table][ids.to(self.device).long()].float()

@@ -20,7 +20,8 @@ a checkpoint that pickles anything but tensors and plain containers is refused, 
   blank, characters, punctuations), optional BOS/EOS and blank interspersing (`add_blank`).
 * speakers: `voice` is a speaker name from `speakers.json` / `speaker_ids.json` / `speakers.pth` (or
   config `speaker_ids`), or an integer id.
-XTTS (`"model": "xtts"`, a GPT-2 audio-code LM + HiFi-GAN decoder) is not implemented: refused explicitly.
+XTTS (`"model": "xtts"`, a GPT-2 audio-code LM + HiFi-GAN decoder) directories load through models/xtts.py
+(the TTS worker dispatches on config.json before calling load_coqui).
 """
 from __future__ import annotations
 
@@ -284,7 +285,7 @@ def load_coqui(d: str, device="cpu", espeak_data: str = ""):
     cfg = json.load(open(os.path.join(d, "config.json"), encoding="utf-8"))
     kind = str(cfg.get("model", "")).lower()
     if kind == "xtts" or "xtts" in kind:
-        raise ValueError("Coqui XTTS models are not implemented by this MI355X build (Coqui VITS models are)")
+        raise ValueError("a Coqui XTTS directory: load it with models/xtts.load_xtts (load_coqui serves VITS)")
     if kind and kind != "vits":
         raise ValueError(f"Coqui model type {kind!r} is not implemented (Coqui VITS models are)")
     try:

@@ -2,7 +2,9 @@
 backend's VITS / MMS-TTS path behind the TTS RPC, served by the VITS engine (models/tts.py) on the GPU.
 The reference's `coqui` backend (backend/python/coqui/backend.py:26-80) is routed here too: Coqui VITS
 model directories (config.json + model_file.pth, models/coqui.py), found by path or by Coqui model name
-("tts_models/en/vctk/vits") in the models directory or Coqui's local cache; XTTS refuses explicitly.
+("tts_models/en/vctk/vits") in the models directory or Coqui's local cache. Coqui XTTS-v2 directories load
+models/xtts.py: voice cloning from the LoadModel AudioPath clip (speaker_wav) or a named speaker (`voice`,
+speakers_xtts.pth); `language` is required, as the reference requires it for multi-lingual models.
 Bark, Kokoro and MusicGen have workers of their own.
 
 LoadModel: a piper voice (`<voice>.onnx` + `<voice>.onnx.json`, models/piper.py; espeak-ng data from
@@ -41,6 +43,8 @@ class TTSServicer(BackendServicer):
         self.tok = None
         self.opts: dict = {}
         self.speakers: dict = {}
+        self.xtts = None  # models/xtts.Xtts when the model directory holds a Coqui XTTS checkpoint
+        self.xtts_voice = None  # (GPT conditioning latents, speaker embedding) of LoadModel's AudioPath clip
 
     def LoadModel(self, request, context):
         import torch
@@ -68,6 +72,18 @@ class TTSServicer(BackendServicer):
                     path if os.path.isdir(path) else os.path.dirname(path)):
                 cdir = path if os.path.isdir(path) else os.path.dirname(path)
             if cdir is not None and CQ.is_coqui_dir(cdir):
+                from ..models import xtts as XT
+                if XT.is_xtts_dir(cdir):
+                    # Coqui XTTS-v2: voice cloning from AudioPath (speaker_wav) or a named speaker; the reference
+                    # clip is conditioned once here (backend/python/coqui/backend.py:40-47, 77-80)
+                    self.xtts = XT.load_xtts(cdir, self.device)
+                    self.model = self.xtts
+                    if request.AudioPath:
+                        ap = request.AudioPath if os.path.isabs(request.AudioPath) else os.path.join(
+                            request.ModelPath, request.AudioPath)
+                        self.xtts_voice = self.xtts.voice(audio_path=ap)
+                    return pb.Result(message=f"loaded Coqui XTTS {os.path.basename(os.path.normpath(cdir))}",
+                                     success=True)
                 self.model, self.tok, self.speakers = CQ.load_coqui(
                     cdir, self.device, o.get("espeak_data", "") or request.LibrarySearchPath)
                 return pb.Result(message=f"loaded Coqui VITS {os.path.basename(os.path.normpath(cdir))}", success=True)
@@ -101,11 +117,30 @@ class TTSServicer(BackendServicer):
                                      noise_scale_duration=float(nsd) if nsd is not None else None,
                                      seed=int(o.get("seed", 0)))
 
+    def _synth_xtts(self, request) -> np.ndarray:
+        """XTTS: the reference's rules — a multi-lingual model needs `language` (or COQUI_LANGUAGE); a named
+        `voice` wins over the AudioPath clip (backend/python/coqui/backend.py:66-80)."""
+        lang = request.language or os.environ.get("COQUI_LANGUAGE", "")
+        if not lang:
+            raise ValueError("Model is multi-lingual, but no language was provided")
+        if request.voice:
+            voice = self.xtts.voice(speaker=request.voice)
+        elif self.xtts_voice is not None:
+            voice = self.xtts_voice
+        else:
+            raise ValueError("Model is multi-speaker, but no speaker was provided (voice, or AudioPath at load)")
+        mx = self.opts.get("max_new")
+        return self.xtts.synthesize(request.text, lang, voice=voice, seed=int(self.opts.get("seed", 0)),
+                                    max_new=int(mx) if mx else None)
+
     def TTS(self, request, context):
         from ..utils.audio import write_wav
         if self.model is None:
             return pb.Result(message="model not loaded", success=False)
         try:
+            if self.xtts is not None:
+                write_wav(request.dst, self._synth_xtts(request), self.xtts.sample_rate)
+                return pb.Result(message="ok", success=True)
             wav = self._synth(request.text, request.voice)
             write_wav(request.dst, wav, self.model.cfg.sample_rate)
             return pb.Result(message="ok", success=True)

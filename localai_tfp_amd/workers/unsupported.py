@@ -1,6 +1,6 @@
 """Backend names of the reference whose model families this framework does not implement (Bark is served
 by workers/bark.py, MusicGen by workers/musicgen.py, Kokoro by workers/kokoro.py, Coqui VITS by
-workers/tts.py — Coqui XTTS checkpoints are refused by models/coqui.py).
+workers/tts.py, Coqui XTTS-v2 by workers/tts.py + models/xtts.py).
 
 The worker starts and answers Health like any backend (so the process manager's lifecycle is the same),
 but LoadModel fails with an explicit error naming the backend — a request for Bark never silently gets
