@@ -16,8 +16,10 @@ The speaker's transcript is prepended to the text and its words (with their dura
 prefix of the audio section, so the model continues in that voice. v0.2 writes codes as `<|17|>` without
 code_start/code_end. Speakers are outetts JSON profiles ({"text", "words": [{"word", "duration",
 "codes"}]}); the outetts package's bundled default voices are not shipped here (no voice = the model's
-own), and creating a profile from AudioPath needs the WavTokenizer encoder + a word aligner (not
-implemented: LoadModel reports it).
+own). AudioPath creates a profile (`create_speaker`): the clip's codes from the WavTokenizer SEANet encoder
+(models/wavtokenizer.py `WavTokenizerEncoder`), its words from `speaker_text:` or Whisper segments, each
+segment's codes shared over its words by length (outetts uses word timestamps; the boundaries here are an
+approximation, the codes are exact).
 """
 from __future__ import annotations
 
@@ -47,6 +49,36 @@ class Speaker:
         with open(path, encoding="utf-8") as f:
             d = json.load(f)
         return cls(text=d.get("text", ""), words=list(d.get("words", [])))
+
+
+def create_speaker(encoder, audio: np.ndarray, sample_rate: int, fps: float, transcript: str = "",
+                   segments: list | None = None) -> Speaker:
+    """Speaker profile from a reference clip (outetts `create_speaker`): the clip's WavTokenizer codes, cut into
+    words. segments: [(start_s, end_s, text)] (e.g. Whisper's), else the whole clip with `transcript`. Within a
+    segment the codes are shared out over its words in proportion to their length (outetts aligns words with
+    Whisper word timestamps or a CTC aligner, neither of which ships here: the word boundaries are an
+    approximation, the codes themselves are the clip's)."""
+    import torch
+    codes = encoder.encode(torch.from_numpy(np.asarray(audio, np.float32)))
+    items = segments or [(0.0, len(audio) / sample_rate, transcript)]
+    words, texts = [], []
+    for s0, s1, text in items:
+        ws = normalize_words(text or "")
+        if not ws:
+            continue
+        texts.append(text.strip())
+        c0, c1 = int(round(s0 * fps)), min(len(codes), int(round(s1 * fps)))
+        if c1 <= c0:
+            continue
+        wt = np.cumsum([len(w) + 1 for w in ws], dtype=np.float64)
+        bounds = [c0] + [c0 + int(round(x / wt[-1] * (c1 - c0))) for x in wt]
+        for w, a, b in zip(ws, bounds, bounds[1:]):
+            if b > a:
+                wc = [int(v) for v in codes[a:b]]
+                words.append({"word": w, "duration": round(len(wc) / fps, 2), "codes": wc})
+    if not words:
+        raise ValueError("speaker creation: no words (empty transcript, or the clip is shorter than a code frame)")
+    return Speaker(text=" ".join(texts), words=words)
 
 
 class PromptV2:
@@ -129,17 +161,16 @@ class OuteTTS:
 def load_outetts(model: str, device: str, options: dict, audio_path: str = "", model_path: str = "") -> OuteTTS:
     """model: a Hugging Face OuteTTS directory (or `synthetic:outetts-test`); options: version (0.2 / 0.3),
     tokenizer (directory), speaker (an outetts speaker JSON, relative to model_path), wavtokenizer
-    (codec checkpoint; default <model>/wavtokenizer)."""
+    (codec checkpoint; default <model>/wavtokenizer); audio_path (a reference clip: the speaker is created
+    from it, with option speaker_text:<its transcript> or whisper:<model> to transcribe it)."""
     from ..engine.engine import EngineConfig, LLMEngine
     from .loader import load_llm
     from .wavtokenizer import WAVTOKENIZER_TEST, WavTokenizerDecoder, load_wavtokenizer
     version = options.get("version", "0.3")
-    if audio_path:
-        raise NotImplementedError("OuteTTS speaker cloning from AudioPath needs the WavTokenizer encoder and a word "
-                                  "aligner, which this framework does not ship; pass speaker:<profile.json>")
 
     def full(p):
         return p if not p or os.path.isabs(p) or not model_path else os.path.join(model_path, p)
+    wt = ""
     if model.startswith("synthetic:"):
         model_, tok, cfg, _ = load_llm("synthetic:tiny", device)
         codec = WavTokenizerDecoder(WAVTOKENIZER_TEST)
@@ -158,4 +189,34 @@ def load_outetts(model: str, device: str, options: dict, audio_path: str = "", m
         codec = load_wavtokenizer(wt, device, torch.float32)
     eng = LLMEngine(model_, tok, EngineConfig(max_num_seqs=1, max_model_len=min(8192, cfg.ctx_train or 8192)))
     spk = Speaker.load(full(options["speaker"])) if options.get("speaker", "").endswith(".json") else None
+    if audio_path and spk is None:
+        opts = dict(options)
+        if opts.get("whisper") and not opts["whisper"].startswith("synthetic:"):
+            opts["whisper"] = full(opts["whisper"])
+        spk = speaker_from_audio(full(audio_path), codec, wt, opts, device)
     return OuteTTS(eng, tok, codec, version, spk)
+
+
+def speaker_from_audio(path: str, codec, wt_path: str, options: dict, device) -> Speaker:
+    """AudioPath speaker cloning (reference transformers/backend.py:235-241 `interface.create_speaker`): the
+    clip at the codec's rate through the WavTokenizer encoder; the transcript from `speaker_text:` or, with
+    `whisper:<model>`, this framework's Whisper (segment timestamps)."""
+    from ..utils.audio import load_audio
+    from .wavtokenizer import WavTokenizerEncoder, load_wavtokenizer_encoder, synthetic_encoder_state
+    sr = codec.cfg.sample_rate
+    if wt_path:
+        enc = load_wavtokenizer_encoder(wt_path, codec.codebook.detach(), device)
+    else:  # synthetic codec: an encoder of the same geometry
+        enc = WavTokenizerEncoder(synthetic_encoder_state(codec.cfg), codec.codebook.detach(), device)
+    audio = load_audio(path, sr)
+    segments = None
+    text = options.get("speaker_text", "")
+    if not text and options.get("whisper"):
+        from .whisper import Transcriber, load_whisper
+        wm, wtok = load_whisper(options["whisper"], device)
+        _, segs, _ = Transcriber(wm, wtok).transcribe(load_audio(path, 16000))
+        segments = [(sg.start, sg.end, sg.text) for sg in segs]
+    if not text and not segments:
+        raise ValueError("OuteTTS speaker from AudioPath needs its transcript: option speaker_text:<text>, or "
+                         "whisper:<model> to transcribe it")
+    return create_speaker(enc, audio, sr, sr / codec.cfg.hop, text, segments)

@@ -14,6 +14,7 @@ The decoder is a once-per-utterance convolutional pass (T ~ 75 x seconds); it ru
 """
 from __future__ import annotations
 
+import math
 import os
 from dataclasses import dataclass
 
@@ -197,3 +198,141 @@ def load_wavtokenizer(path: str, device="cpu", dtype=torch.float32) -> WavTokeni
     c = config_from_state(sd)
     m = WavTokenizerDecoder(c).load_checkpoint_dict(sd)
     return m.to(device=device, dtype=dtype).eval()
+
+
+# ------------------------------------------------------------------------------------------------ encoder
+
+def _pad_reflect(x: torch.Tensor, left: int, right: int) -> torch.Tensor:
+    """Reflect padding that also works when the input is shorter than the pad (zero-extend first, as EnCodec)."""
+    n = x.shape[-1]
+    m = max(left, right)
+    extra = 0
+    if n <= m:
+        extra = m - n + 1
+        x = F.pad(x, (0, extra))
+    y = F.pad(x, (left, right), mode="reflect")
+    return y[..., : y.shape[-1] - extra]
+
+
+def _sconv(x: torch.Tensor, w: torch.Tensor, b, stride: int = 1, dilation: int = 1) -> torch.Tensor:
+    """EnCodec SConv1d, non-causal: reflect padding split around the input plus the extra right padding that
+    makes the last frame whole."""
+    k = (w.shape[-1] - 1) * dilation + 1
+    pad_total = k - stride
+    L = x.shape[-1]
+    n_frames = (L - k + pad_total) / stride + 1
+    extra = (math.ceil(n_frames) - 1) * stride + (k - pad_total) - L
+    pr = pad_total // 2
+    return F.conv1d(_pad_reflect(x, pad_total - pr, pr + extra), w, b, stride, dilation=dilation)
+
+
+class WavTokenizerEncoder:
+    """WavTokenizer's feature extractor for speaker creation (OuteTTS `create_speaker`): the EnCodec SEANet
+    encoder (`feature_extractor.encodec.encoder.model.*`: conv 7, [residual block (ELU, conv 3, ELU, conv 1, 1x1
+    shortcut), ELU, strided conv 2r] per ratio, 2-layer LSTM with skip, ELU, conv 7 to the feature width) and the
+    nearest entry of the one 4096-code codebook. audio (24 kHz) -> codes at sample_rate / hop per second. The
+    layer list is read from the checkpoint's keys (index kinds: conv / residual block / LSTM; gaps are ELUs), so
+    ratios and widths follow the file."""
+
+    def __init__(self, sd: dict, codebook: torch.Tensor, device="cpu"):
+        from .tts import fold_weight_norm
+        sd = sd.get("state_dict", sd)
+        P = "feature_extractor.encodec.encoder.model."
+        enc = fold_weight_norm({k[len(P):]: v.float() for k, v in sd.items() if k.startswith(P)})
+        if not enc:
+            raise ValueError("WavTokenizer checkpoint: no encoder (feature_extractor.encodec.encoder.model.*)")
+        self.dev = torch.device(device)
+        self.w = {k: v.to(self.dev) for k, v in enc.items()}
+        n = 1 + max(int(k.split(".", 1)[0]) for k in enc)
+        self.layers = []
+        for i in range(n):
+            if f"{i}.conv.conv.weight" in enc:
+                k = enc[f"{i}.conv.conv.weight"].shape[-1]
+                self.layers.append(("conv", f"{i}.conv.conv", k // 2 if k % 2 == 0 else 1))
+            elif f"{i}.block.1.conv.conv.weight" in enc:
+                self.layers.append(("res", f"{i}.", 1))
+            elif f"{i}.lstm.weight_ih_l0" in enc:
+                C = enc[f"{i}.lstm.weight_ih_l0"].shape[1]
+                nl = sum(1 for k in enc if k.startswith(f"{i}.lstm.weight_ih_l"))
+                lstm = torch.nn.LSTM(C, C, nl)
+                with torch.no_grad():
+                    for name, p in lstm.named_parameters():
+                        p.copy_(enc[f"{i}.lstm.{name}"])
+                from ..ops.rnn import LSTMStack
+                lstm = lstm.to(self.dev).eval()
+                self.layers.append(("lstm", (lstm, LSTMStack(lstm)), 1))
+            else:
+                self.layers.append(("elu", None, 1))
+        self.codebook = codebook.float().to(self.dev)
+
+    def _res(self, x, p):
+        w = self.w
+        h = _sconv(F.elu(x), w[p + "block.1.conv.conv.weight"], w.get(p + "block.1.conv.conv.bias"))
+        h = _sconv(F.elu(h), w[p + "block.3.conv.conv.weight"], w.get(p + "block.3.conv.conv.bias"))
+        sc = x if (p + "shortcut.conv.conv.weight") not in w else _sconv(
+            x, w[p + "shortcut.conv.conv.weight"], w.get(p + "shortcut.conv.conv.bias"))
+        return sc + h
+
+    @torch.no_grad()
+    def features(self, audio: torch.Tensor) -> torch.Tensor:
+        x = audio.float().to(self.dev).view(1, 1, -1)
+        for kind, p, stride in self.layers:
+            if kind == "conv":
+                x = _sconv(x, self.w[p + ".weight"], self.w.get(p + ".bias"), stride)
+            elif kind == "res":
+                x = self._res(x, p)
+            elif kind == "lstm":
+                lstm, scan = p
+                xf = x.permute(2, 0, 1).contiguous()  # [T, 1, C]
+                y = scan(xf) if x.is_cuda else lstm(xf)[0]
+                x = (y + xf).permute(1, 2, 0)
+            else:
+                x = F.elu(x)
+        return x[0].t()  # [T, feat]
+
+    @torch.no_grad()
+    def encode(self, audio: torch.Tensor) -> list[int]:
+        f = self.features(audio)
+        cb = self.codebook
+        d = (f * f).sum(1, keepdim=True) - 2 * f @ cb.t() + (cb * cb).sum(1)[None]
+        return d.argmin(1).tolist()
+
+
+def load_wavtokenizer_encoder(path: str, codebook: torch.Tensor, device="cpu") -> WavTokenizerEncoder:
+    if os.path.isdir(path):
+        cands = [f for f in sorted(os.listdir(path)) if f.endswith((".safetensors", ".ckpt", ".pt", ".pth", ".bin"))]
+        path = os.path.join(path, cands[0])
+    if path.endswith(".safetensors"):
+        from safetensors.torch import load_file
+        sd = load_file(path)
+    else:
+        sd = torch.load(path, map_location="cpu", weights_only=True)
+    return WavTokenizerEncoder(sd, codebook, device)
+
+
+def synthetic_encoder_state(c: WavTokenizerConfig, ratios=(2, 2, 2, 2), n_filters: int = 8, seed: int = 0) -> dict:
+    """Random SEANet encoder weights in the checkpoint's names (tests): hop = prod(ratios)."""
+    g = torch.Generator().manual_seed(seed)
+
+    def r(*shape):
+        return torch.randn(*shape, generator=g) * (1.0 / math.sqrt(shape[1] * shape[-1]))
+    P = "feature_extractor.encodec.encoder.model."
+    sd, i, ch = {}, 0, n_filters
+    sd[f"{P}{i}.conv.conv.weight"], sd[f"{P}{i}.conv.conv.bias"] = r(ch, 1, 7), torch.zeros(ch)
+    i += 1
+    for ratio in reversed(ratios):
+        sd[f"{P}{i}.block.1.conv.conv.weight"], sd[f"{P}{i}.block.1.conv.conv.bias"] = r(ch // 2, ch, 3), torch.zeros(ch // 2)
+        sd[f"{P}{i}.block.3.conv.conv.weight"], sd[f"{P}{i}.block.3.conv.conv.bias"] = r(ch, ch // 2, 1), torch.zeros(ch)
+        sd[f"{P}{i}.shortcut.conv.conv.weight"], sd[f"{P}{i}.shortcut.conv.conv.bias"] = r(ch, ch, 1), torch.zeros(ch)
+        i += 2  # residual block, ELU
+        sd[f"{P}{i}.conv.conv.weight"], sd[f"{P}{i}.conv.conv.bias"] = r(2 * ch, ch, 2 * ratio), torch.zeros(2 * ch)
+        ch *= 2
+        i += 1
+    for layer in range(2):
+        for n, shape in (("weight_ih", (4 * ch, ch)), ("weight_hh", (4 * ch, ch))):
+            sd[f"{P}{i}.lstm.{n}_l{layer}"] = r(*shape)
+        sd[f"{P}{i}.lstm.bias_ih_l{layer}"] = torch.zeros(4 * ch)
+        sd[f"{P}{i}.lstm.bias_hh_l{layer}"] = torch.zeros(4 * ch)
+    i += 2  # LSTM, ELU
+    sd[f"{P}{i}.conv.conv.weight"], sd[f"{P}{i}.conv.conv.bias"] = r(c.feat_dim, ch, 7), torch.zeros(c.feat_dim)
+    return sd

@@ -7,6 +7,7 @@ import json
 import numpy as np
 import pytest
 import torch
+import torch.nn.functional as F
 
 from localai_tfp_amd.models import outetts as O
 from localai_tfp_amd.models import wavtokenizer as WT
@@ -100,6 +101,71 @@ def test_outetts_generate_text_on_engine():
     assert isinstance(out, str) and len(out) > 0
 
 
-def test_outetts_audio_path_refused():
-    with pytest.raises(NotImplementedError, match="AudioPath"):
-        O.load_outetts("synthetic:outetts-test", "cpu", {}, audio_path="/x.wav")
+def _encoder(seed=0):
+    sd = WT.synthetic_encoder_state(WT.WAVTOKENIZER_TEST, ratios=(2, 2, 2, 2), seed=seed)
+    return WT.WavTokenizerEncoder({"state_dict": sd}, torch.zeros(64, 32))
+
+
+def test_wavtokenizer_encoder_frames_and_codes():
+    """SEANet encoder: one feature frame per hop (16 = 2*2*2*2 samples), codes = nearest codebook entry. With the
+    codebook built from the clip's own (permuted) features the codes recover the permutation exactly."""
+    enc = _encoder()
+    assert [k for k, _, _ in enc.layers].count("res") == 4 and any(k == "lstm" for k, _, _ in enc.layers)
+    assert [s for k, _, s in enc.layers if k == "conv"] == [1, 2, 2, 2, 2, 1]
+    audio = torch.randn(16 * 20, generator=torch.Generator().manual_seed(1)) * 0.3
+    f = enc.features(audio)
+    assert f.shape == (20, 32) and torch.isfinite(f).all()
+    assert enc.features(audio[:16 * 20 - 5]).shape == (20, 32)  # partial last frame padded, not dropped
+    perm = torch.randperm(20, generator=torch.Generator().manual_seed(2))
+    enc.codebook = torch.cat([f[perm], f[:1] + 100.0])  # + one far-away decoy
+    assert enc.encode(audio) == torch.argsort(perm).tolist()
+
+
+def test_wavtokenizer_encoder_residual_math():
+    """One residual block against the plain formula: shortcut(x) + conv1(elu(conv3(elu(x)))), reflect padding."""
+    enc = _encoder()
+    x = torch.randn(1, 8, 12, generator=torch.Generator().manual_seed(4))
+    w = enc.w
+    p = "1."
+    h = F.conv1d(F.pad(F.elu(x), (1, 1), mode="reflect"), w[p + "block.1.conv.conv.weight"], w[p + "block.1.conv.conv.bias"])
+    h = F.conv1d(F.elu(h), w[p + "block.3.conv.conv.weight"], w[p + "block.3.conv.conv.bias"])
+    ref = F.conv1d(x, w[p + "shortcut.conv.conv.weight"], w[p + "shortcut.conv.conv.bias"]) + h
+    assert torch.allclose(enc._res(x, p), ref, atol=1e-5)
+
+
+def test_create_speaker_word_split():
+    class Enc:
+        def encode(self, a):
+            return list(range(100, 100 + len(a) // 16))
+    audio = np.zeros(16 * 30, np.float32)  # 30 frames at 1500 fps
+    sp = O.create_speaker(Enc(), audio, 24000, 1500.0, "Hi, everybody here!")
+    assert [w["word"] for w in sp.words] == ["hi", "everybody", "here"]
+    codes = [c for w in sp.words for c in w["codes"]]
+    assert codes == list(range(100, 130))  # every code, in order, once
+    lens = [len(w["codes"]) for w in sp.words]
+    assert lens[1] > lens[2] > lens[0]  # proportional to word length
+    assert sp.words[1]["duration"] == round(lens[1] / 1500.0, 2)
+    # segments (Whisper timestamps): each word stays inside its segment
+    sp = O.create_speaker(Enc(), audio, 24000, 1500.0, segments=[(0.0, 0.01, "one two"), (0.01, 0.02, "three")])
+    assert [w["word"] for w in sp.words] == ["one", "two", "three"]
+    assert sp.words[2]["codes"] == list(range(115, 130)) and sp.text == "one two three"
+    with pytest.raises(ValueError, match="no words"):
+        O.create_speaker(Enc(), audio, 24000, 1500.0, "")
+
+
+def test_outetts_speaker_from_audio_path(tmp_path):
+    """LoadModel AudioPath: the clip is encoded by the codec's encoder and becomes the prompt's speaker."""
+    from localai_tfp_amd.utils.audio import write_wav
+    sr = 24000
+    t = np.arange(sr // 10) / sr
+    write_wav(str(tmp_path / "ref.wav"), (0.3 * np.sin(2 * np.pi * 220 * t)).astype(np.float32), sr)
+    with pytest.raises(ValueError, match="transcript"):
+        O.load_outetts("synthetic:outetts-test", "cpu", {}, model_path=str(tmp_path), audio_path="ref.wav")
+    tts = O.load_outetts("synthetic:outetts-test", "cpu", {"speaker_text": "Hello there."},
+                         model_path=str(tmp_path), audio_path="ref.wav")
+    sp = tts.speaker
+    assert sp.text == "Hello there." and [w["word"] for w in sp.words] == ["hello", "there"]
+    codes = [c for w in sp.words for c in w["codes"]]
+    assert len(codes) == sr // 10 // 16 and all(0 <= c < 64 for c in codes)
+    p = O.PromptV2("0.3").completion("Go.", sp)
+    assert "hello<|t_" in p and f"<|c_{codes[0]}|>" in p
