@@ -92,19 +92,39 @@ __global__ __launch_bounds__(256) void attn_dense_kernel(const uint16_t* __restr
     for (int i = 0; i < 4; ++i) { mrow[i] = -INFINITY; lrow[i] = 0.f; }
     char* pw = smem + 2 * KBYTES + wave * 16 * PSTRIDE;
 
-    for (int kt0 = 0; kt0 < kv_end; kt0 += KT) {
-        constexpr int CH = KT * D / 8;
-        for (int id = threadIdx.x; id < CH; id += 256) {
+    // K / V tiles software-pipelined one tile deep: the next tile's 16-byte chunks are requested right after
+    // this tile is staged in LDS, so their latency hides behind this tile's MFMAs and softmax
+    constexpr int CH = KT * D / 8;
+    constexpr int NCH = (CH + 255) / 256;  // chunks per thread
+    uint4 kr[NCH], vr[NCH];
+    auto load_tile = [&](int kt0) {
+#pragma unroll
+        for (int j = 0; j < NCH; ++j) {
+            const int id = threadIdx.x + 256 * j;
             const int p = id / (D / 8), c = id % (D / 8);
             const int pos = kt0 + p;
-            uint4 kv = make_uint4(0, 0, 0, 0), vv = make_uint4(0, 0, 0, 0);
-            if (pos < kv_end) {
-                kv = *(const uint4*)(kb + (size_t)pos * k_stride + c * 8);
-                vv = *(const uint4*)(vb_ + (size_t)pos * v_stride + c * 8);
+            kr[j] = make_uint4(0, 0, 0, 0);
+            vr[j] = make_uint4(0, 0, 0, 0);
+            if (id < CH && pos < kv_end) {
+                kr[j] = *(const uint4*)(kb + (size_t)pos * k_stride + c * 8);
+                vr[j] = *(const uint4*)(vb_ + (size_t)pos * v_stride + c * 8);
             }
-            *(uint4*)(k_lds + kd_lds_off<D>(p, c)) = kv;
-            *(uint4*)(v_lds + vd_lds_off<D>(p, c >> 1) + 16 * (c & 1)) = vv;
         }
+    };
+    // (D = 512: a tile is 8 chunks per thread and per operand; prefetching it would spill, so it loads in place)
+    constexpr bool PF = D <= 128;
+    if (PF && kv_end > 0) load_tile(0);
+    for (int kt0 = 0; kt0 < kv_end; kt0 += KT) {
+        if constexpr (!PF) load_tile(kt0);
+#pragma unroll
+        for (int j = 0; j < NCH; ++j) {
+            const int id = threadIdx.x + 256 * j;
+            if (id >= CH) continue;
+            const int p = id / (D / 8), c = id % (D / 8);
+            *(uint4*)(k_lds + kd_lds_off<D>(p, c)) = kr[j];
+            *(uint4*)(v_lds + vd_lds_off<D>(p, c >> 1) + 16 * (c & 1)) = vr[j];
+        }
+        if (PF && kt0 + KT < kv_end) load_tile(kt0 + KT);
         __syncthreads();
         constexpr int NT16 = KT / 16;
         f32x4 sacc[NT16];
