@@ -29,6 +29,32 @@ RT_SIGS = {
     "mxrt_bm_match_prefix": (I, [P, P, I, P, P]),
     "mxrt_bm_commit": (None, [P, C.c_int32, P, P, P]),
     "mxrt_bm_stats": (None, [P, P]),
+    # scheduler.cpp
+    "mxrt_sched_new": (P, [P, I, I, I, I, I, I]),
+    "mxrt_sched_free": (None, [P]),
+    "mxrt_sched_table": (P, [P]),
+    "mxrt_sched_set_hold": (None, [P, I]),
+    "mxrt_sched_add": (I, [P, P, I, I, I]),
+    "mxrt_sched_push": (None, [P, I, C.c_int32]),
+    "mxrt_sched_pop": (None, [P, I]),
+    "mxrt_sched_push_many": (None, [P, P, I]),
+    "mxrt_sched_schedule": (I, [P, P]),
+    "mxrt_sched_out": (P, [P, I]),
+    "mxrt_sched_out_packed": (I, [P, P, I]),
+    "mxrt_sched_plan_packed": (I, [P, P, I]),
+    "mxrt_sched_add_pending": (None, [P, P, I, I]),
+    "mxrt_sched_plan": (I, [P, P, I, P, I, P]),
+    "mxrt_sched_plan_arr": (P, [P, I]),
+    "mxrt_sched_commit": (None, [P, P, I]),
+    "mxrt_sched_set_prev": (None, [P, P, I]),
+    "mxrt_sched_clear_prev": (None, [P]),
+    "mxrt_sched_finish": (None, [P, I]),
+    "mxrt_sched_abort": (I, [P, I]),
+    "mxrt_sched_release_deferred": (I, [P, P]),
+    "mxrt_sched_release_slot": (None, [P, I]),
+    "mxrt_sched_grow": (I, [P, I, I]),
+    "mxrt_sched_blocks": (I, [P, I, P, I]),
+    "mxrt_sched_queue": (I, [P, I, P, I]),
     # store.cpp
     "mxrt_store_new": (P, []),
     "mxrt_store_free": (None, [P]),

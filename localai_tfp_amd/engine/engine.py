@@ -369,7 +369,12 @@ class LLMEngine:
                 self.cfg.use_graphs = False  # a network hop cannot live inside a hipGraph
             self.kv = KVCache(nl, nb, model.n_kv, c.block_size, mc.head_dim, self.device, self.kv_dtype)
         self.bm = make_block_manager(nb, c.block_size, c.enable_prefix_cache)
-        self.sched = Scheduler(self.bm, c.block_size, c.max_num_seqs, c.max_batched_tokens, c.max_model_len,
+        # scheduler + step planner: native (csrc/runtime/scheduler.cpp) on the native block manager; the Python
+        # Scheduler is the reference implementation (MX_PY_SCHED=1, or no libmxrt)
+        from . import native_scheduler as NS
+        self.native_sched = (os.environ.get("MX_PY_SCHED", "0") != "1" and hasattr(self.bm, "_h") and NS.available())
+        sched_cls = NS.NativeScheduler if self.native_sched else Scheduler
+        self.sched = sched_cls(self.bm, c.block_size, c.max_num_seqs, c.max_batched_tokens, c.max_model_len,
                                prefill_chunk=c.prefill_chunk)
         max_parts = max(1, -(-c.max_model_len // c.attn_part_size))
         if self.recurrent:
@@ -473,7 +478,7 @@ class LLMEngine:
                     req.prompt_ids = ids[:n_keep] + ids[n_keep + erased:]
                 if not req.prompt_ids:
                     req.prompt_ids = [getattr(self.tok, "bos_token_id", 0) or 0]
-                s = Sequence(req, self.tok)
+                s = self.sched.new_sequence(req, self.tok) if self.native_sched else Sequence(req, self.tok)
                 self.seqs[req.rid] = s
                 self.sched.add(s)
             else:
@@ -537,6 +542,8 @@ class LLMEngine:
             except Exception as ex:  # fail every in-flight request loudly, keep the worker alive
                 log.exception("engine step failed")
                 self._inflight, self._prev_dev = collections.deque(), None
+                if self.native_sched:
+                    self.sched.clear_prev()
                 for s in list(self.sched.running) + list(self.sched.waiting):
                     s.n_pending = 0
                     self.sched.abort(s.rid)
@@ -703,8 +710,14 @@ class LLMEngine:
         t_exec = time.perf_counter()
         tok_dev, lp_dev = None, None
         steps = [it.seq.n_generated for it in items]  # sampler step index (seed advance) of each row's sample
-        for it in items:  # this step's samples are in flight from here on (their KV blocks must stay)
-            it.seq.n_pending += 1
+        # this step's samples are in flight from here on (their KV blocks must stay)
+        nslots = None
+        if self.native_sched:
+            nslots = self.sched.item_slots(so, items)
+            self.sched.add_pending(nslots, 1)
+        else:
+            for it in items:
+                it.seq.n_pending += 1
         if items and not self.sched.hold_host_state and any(
                 needs_host_state(it.seq) and it.seq.n_pending > 1 for it in items):
             # a grammar mask / mirostat mu needs the previous step's token: read that step now, while this
@@ -740,7 +753,7 @@ class LLMEngine:
             if self.device.type == "cuda":
                 ev = torch.cuda.Event()
                 ev.record()
-            new = (ev, k, items, lp_dev is not None)
+            new = (ev, k, items, lp_dev is not None, nslots)
         else:
             new = None
         if roctx.ENABLED:
@@ -754,6 +767,8 @@ class LLMEngine:
         if new is not None:
             self._inflight.append(new)
         self._prev_dev = (tok_dev, {it.seq.rid: r for r, it in enumerate(items)}) if items else None
+        if self.native_sched:
+            self.sched.set_prev(items, nslots) if items else self.sched.clear_prev()
         # read back the oldest launched steps, keeping `overlap_depth - 1` of them (plus this one) in
         # flight; a step without samples is a sync point (the next plan cannot gather from it)
         keep = max(0, self.cfg.overlap_depth - 1) if items else 0
@@ -781,7 +796,7 @@ class LLMEngine:
         st["busy_s"] += t3 - t0
 
     def _process_inflight(self, inf):
-        ev, k, items, has_lp = inf
+        ev, k, items, has_lp, nslots = inf
         t0 = time.perf_counter()
         if ev is not None:
             if roctx.ENABLED:
@@ -797,9 +812,12 @@ class LLMEngine:
         toks = self._pin_tok[k][:S].tolist()
         lps = self._pin_lp[k][:S].tolist() if has_lp else None
         now = time.perf_counter()
+        if nslots is not None:
+            self.sched.add_pending(nslots, -1)
         for j, it in enumerate(items):
             s = it.seq
-            s.n_pending -= 1
+            if nslots is None:
+                s.n_pending -= 1
             if s.status == Status.FINISHED:
                 continue  # finished on an earlier token (or aborted): this sample is discarded
             if s.t_first_token is None:
@@ -817,7 +835,7 @@ class LLMEngine:
         """Read every in-flight step; drop sequences that finished on those tokens from the plan."""
         self._drain_inflight()
         if any(it.seq.status == Status.FINISHED for it in so.decode + so.prefill):
-            self.sched.running = [x for x in self.sched.running if x.status != Status.FINISHED]
+            self.sched.drop_finished()
             so = SchedulerOutput([it for it in so.decode if it.seq.status != Status.FINISHED],
                                  [it for it in so.prefill if it.seq.status != Status.FINISHED])
         return None if so.empty else so
@@ -825,6 +843,8 @@ class LLMEngine:
     def _drain_inflight(self):
         q, self._inflight = self._inflight, collections.deque()
         self._prev_dev = None
+        if self.native_sched:
+            self.sched.clear_prev()
         while q:
             self._process_inflight(q.popleft())
 
@@ -896,6 +916,10 @@ class LLMEngine:
         bs = self.cfg.block_size
         dec, pf = so.decode, so.prefill
         nd = len(dec)
+        if self.native_sched:
+            plan = self.sched.plan_arrays(so)
+            plan["nd"], plan["keep_hidden"] = nd, False
+            return self._plan_finish(so, plan)
         T = so.num_tokens
         tokens = np.empty(T, np.int32)
         positions = np.empty(T, np.int32)
@@ -935,16 +959,6 @@ class LLMEngine:
                 "lidx": np.asarray(lidx, np.int32), "keep_hidden": False}
         if fix_dst:
             plan["fix"] = (np.asarray(fix_dst, np.int64), np.asarray(fix_src, np.int64))
-        mm = []
-        row = nd
-        for it in pf:  # multimodal spans intersecting this chunk -> (row in T, embedding rows)
-            for p0, emb in it.seq.req.mm_embeds:
-                lo, hi = max(p0, it.start), min(p0 + emb.shape[0], it.start + it.n)
-                if lo < hi:
-                    mm.append((row + lo - it.start, emb[lo - p0:hi - p0]))
-            row += it.n
-        if mm:
-            plan["mm"] = mm
         if nd:
             maxb = max(len(it.seq.blocks) for it in dec)
             bt = np.zeros((nd, maxb), np.int32)
@@ -963,6 +977,23 @@ class LLMEngine:
                 cu[k + 1] = cu[k] + it.n
                 ctx[k] = it.start + it.n
             plan["pf_bt"], plan["pf_cu"], plan["pf_ctx"] = bt, cu, ctx
+        return self._plan_finish(so, plan)
+
+    def _plan_finish(self, so: SchedulerOutput, plan: dict) -> dict:
+        """The Python-side rest of a plan: multimodal spans, embedding rows, prefill attention tiles, graph bucket."""
+        pf = so.prefill
+        nd = plan["nd"]
+        mm = []
+        row = nd
+        for it in pf:  # multimodal spans intersecting this chunk -> (row in T, embedding rows)
+            for p0, emb in it.seq.req.mm_embeds:
+                lo, hi = max(p0, it.start), min(p0 + emb.shape[0], it.start + it.n)
+                if lo < hi:
+                    mm.append((row + lo - it.start, emb[lo - p0:hi - p0]))
+            row += it.n
+        if mm:
+            plan["mm"] = mm
+        if pf:
             plan["keep_hidden"] = any(it.seq.req.embedding for it in pf if it.sample)
         if pf and self.device.type == "cuda" and hasattr(self.model, "prefill_rows"):
             from ..ops.core import prefill_tiles
@@ -1221,8 +1252,7 @@ class LLMEngine:
             self.stats["out_tokens"] += 1
             if (t in self.eos_ids or t in s.req.stop_token_ids) and not s.params.ignore_eos:
                 reason = "stop"
-                s.output_ids.pop()  # EOS is not part of the visible output
-                s._pending_ids.pop() if s._pending_ids else None
+                s.pop_output()  # EOS is not part of the visible output
             elif len(s.output_ids) >= s.req.max_tokens:
                 reason = "length"
             elif s.known_len >= self.cfg.max_model_len:

@@ -18,7 +18,7 @@ from dataclasses import dataclass, field
 from .sequence import Sequence, Status
 
 
-@dataclass
+@dataclass(slots=True)
 class ScheduledSeq:
     seq: Sequence
     start: int  # first token index computed this step
@@ -221,6 +221,9 @@ class Scheduler:
             self.deferred.append(seq)  # a launched step still writes its KV blocks
         else:
             self.free(seq)
+
+    def drop_finished(self):
+        self.running = [x for x in self.running if x.status != Status.FINISHED]
 
     def release_deferred(self):
         """Free the blocks of finished sequences whose in-flight steps have all been read."""

@@ -140,6 +140,12 @@ class Sequence:
         if logprob is not None:
             self._pending_lp.append(float(logprob))
 
+    def pop_output(self):
+        """Drop the newest output token (an EOS is not part of the visible output)."""
+        self.output_ids.pop()
+        if self._pending_ids:
+            self._pending_ids.pop()
+
     def _decode_new(self) -> str:
         sb = getattr(self.tok, "stream_bytes", None)
         if sb is not None:

@@ -3,7 +3,7 @@
 step plus the device idle before the next one. Answers "where does wall time exceed kernel time": idle is
 attributed to the host phase the next step's launch was waiting on.
 
-    python -m localai_tfp_amd.tools.step_trace_summary trace.json   (or: python tools/step_trace_summary.py ...)
+    python tools/step_trace_summary.py trace.json [last_n_steps]
 """
 from __future__ import annotations
 
@@ -30,8 +30,9 @@ def summarise(path: str, last: int = 0) -> dict:
     samp = (H[1:, 3] - H[1:, 2]) * 1e3
     wait = H[1:, 5] * 1e3
     proc = (H[1:, 6] - H[1:, 4]) * 1e3 - wait
-    graph = H[1:, 7] > 0
-    mixed = H[1:, 9] > 0
+    # gpu row i is host step i (H[:-1]); the idle after it waits on host step i + 1 (H[1:])
+    graph = H[:-1, 7] > 0
+    mixed = H[:-1, 9] > 0
     out = {"steps": int(n), "wall_ms": round(float(wall.mean()), 3), "gpu_busy_ms": round(float(busy.mean()), 3),
            "gpu_idle_ms": round(float(idle.mean()), 3), "graph_frac": round(float(graph.mean()), 3),
            "mixed_frac": round(float(mixed.mean()), 3),
@@ -46,7 +47,7 @@ def summarise(path: str, last: int = 0) -> dict:
                          "process": round(float(proc[m].mean()), 3)}
     big = np.argsort(idle)[-8:][::-1]
     out["largest_idle"] = [{"i": int(i), "idle": round(float(idle[i]), 3), "graph": bool(graph[i]),
-                            "nd": int(H[i + 1, 8]), "npf": int(H[i + 1, 9]),
+                            "nd": int(H[i, 8]), "npf": int(H[i, 9]),
                             "next_sched": round(float(sched[min(i + 1, n - 1)]), 3),
                             "next_launch": round(float(launch[min(i + 1, n - 1)]), 3)} for i in big]
     return out
