@@ -417,6 +417,16 @@ int mxrt_sched_plan_packed(void* h, int32_t* out, int cap) {
     return (int)n;
 }
 
+// every decode slot with a token in flight finds it in the last launched step (engine._pending_on_device)
+int mxrt_sched_pending_ok(void* h, const int32_t* slots, int n) {
+    Sched* m = (Sched*)h;
+    for (int k = 0; k < n; ++k) {
+        const int sl = slots[k];
+        if (m->f(F_NP, sl) && m->s[sl].prev_gen != m->gen) return 0;
+    }
+    return 1;
+}
+
 // n_pending += d for each slot (a launched step's sampled rows: +1; their read-back: -1)
 void mxrt_sched_add_pending(void* h, const int32_t* slots, int n, int d) {
     Sched* m = (Sched*)h;

@@ -43,6 +43,7 @@ RT_SIGS = {
     "mxrt_sched_out_packed": (I, [P, P, I]),
     "mxrt_sched_plan_packed": (I, [P, P, I]),
     "mxrt_sched_add_pending": (None, [P, P, I, I]),
+    "mxrt_sched_pending_ok": (I, [P, P, I]),
     "mxrt_sched_plan": (I, [P, P, I, P, I, P]),
     "mxrt_sched_plan_arr": (P, [P, I]),
     "mxrt_sched_commit": (None, [P, P, I]),

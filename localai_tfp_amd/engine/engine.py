@@ -654,7 +654,10 @@ class LLMEngine:
 
     def _overlap_row_ok(self, it) -> bool:
         s = it.seq
-        if s.req.embedding or not self._overlap_params(s.params):
+        ok = s.overlap_static
+        if ok is None:  # the request's own part of the decision, fixed for its lifetime
+            ok = s.overlap_static = not s.req.embedding and self._overlap_params(s.params)
+        if not ok:
             return False
         # grammar rows: held by the scheduler while a token is in flight, or masked after the late read of that
         # token (_step_overlap), so their mask is current when they are sampled
@@ -828,6 +831,8 @@ class LLMEngine:
 
     def _pending_on_device(self, so: SchedulerOutput) -> bool:
         """Every decode row whose input token is still in flight can gather it from the latest step."""
+        if self.native_sched:
+            return self.sched.pending_on_device(so)
         rows = self._prev_dev[1] if self._prev_dev is not None else {}
         return all(it.seq.rid in rows for it in so.decode if it.seq.n_pending)
 

@@ -365,6 +365,10 @@ class NativeScheduler:
             raise RuntimeError("in-flight sample of a released sequence")
         self.rt.mxrt_sched_add_pending(self._h, slots.ctypes.data, len(slots), d)
 
+    def pending_on_device(self, so: SchedulerOutput) -> bool:
+        dec = np.ascontiguousarray(self._items(so)[0], np.int32)
+        return bool(self.rt.mxrt_sched_pending_ok(self._h, dec.ctypes.data, len(dec)))
+
     def set_prev(self, items, slots: np.ndarray | None = None):
         """Rows of the last launched sampling step (decode inputs in flight are gathered from it)."""
         sl = slots if slots is not None else np.asarray([it.seq._slot for it in items], np.int32)

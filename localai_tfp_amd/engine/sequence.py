@@ -99,6 +99,7 @@ class Sequence:
         self.emitted_text = ""
         self._pending_ids: list[int] = []
         self._pending_lp: list[float] = []
+        self.overlap_static = None  # engine cache: may this request's rows run in the overlap pipeline
 
     # ---------------------------------------------------------------- token bookkeeping
     @property

@@ -15,6 +15,9 @@ def main():
     ap.add_argument("--steps", type=int, default=0, help="engine steps inside the window (per-step column)")
     ap.add_argument("--top", type=int, default=30)
     ap.add_argument("--gaps", action="store_true", help="also: idle time between consecutive kernels, by next kernel")
+    ap.add_argument("--split-steps", default="", help="kernel-name substring that starts each engine step: per-step "
+                    "tables for steps with / without --mixed-marker kernels")
+    ap.add_argument("--mixed-marker", default="attn_prefill", help="kernel-name substring of mixed (prefill) steps")
     a = ap.parse_args()
     c = sqlite3.connect(a.db)
     t_end = c.execute("select max(end) from kernels").fetchone()[0]
@@ -37,6 +40,8 @@ def main():
         if a.steps:
             line += f" {ms * 1e3 / a.steps:.1f} |"
         print(line)
+    if a.split_steps:
+        split_steps(c, t0, a.split_steps, a.mixed_marker, a.top)
     if a.gaps:
         ks = c.execute("select name, start, end from kernels where start >= ? order by start", (t0,)).fetchall()
         by: dict = {}
@@ -60,6 +65,42 @@ def main():
         print("|---|---|---|---|")
         for nm, (n, g) in sorted(by.items(), key=lambda kv: -kv[1][1])[: a.top]:
             print(f"| `{nm}` | {n} | {g / 1e3:.2f} | {g / n:.2f} |")
+
+
+def split_steps(c, t0, marker, mixed_marker, top):
+    """Per engine step (a step starts at each `marker` kernel): wall, kernel sum, and the per-kernel split of
+    decode-only vs mixed steps."""
+    ks = c.execute("select name, start, end from kernels where start >= ? order by start", (t0,)).fetchall()
+    steps, cur = [], None
+    for nm, s0, e0 in ks:
+        if marker in nm:
+            if cur is not None:
+                steps.append(cur)
+            cur = []
+        if cur is not None:
+            cur.append((nm, s0, e0))
+    # the last (possibly partial) step is dropped: its wall is not bounded by a next marker
+    out = {}
+    for st, nxt in zip(steps, steps[1:] + [None]):
+        if nxt is None:
+            break
+        kind = "mixed" if any(mixed_marker in k[0] for k in st) else "decode"
+        d = out.setdefault(kind, {"n": 0, "wall": 0.0, "kern": 0.0, "by": {}})
+        d["n"] += 1
+        d["wall"] += (nxt[0][1] - st[0][1]) / 1e3
+        for nm, s0, e0 in st:
+            d["kern"] += (e0 - s0) / 1e3
+            nm = nm.replace("(anonymous namespace)::", "").split("(")[0][:90]
+            d["by"][nm] = d["by"].get(nm, 0.0) + (e0 - s0) / 1e3
+    for kind, d in out.items():
+        n = d["n"]
+        print()
+        print(f"{kind} steps: {n}, wall {d['wall'] / n / 1e3:.3f} ms/step, kernels {d['kern'] / n / 1e3:.3f} ms/step")
+        print()
+        print("| kernel | us/step |")
+        print("|---|---|")
+        for nm, us in sorted(d["by"].items(), key=lambda kv: -kv[1])[:top]:
+            print(f"| `{nm}` | {us / n:.1f} |")
 
 
 if __name__ == "__main__":
