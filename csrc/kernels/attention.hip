@@ -318,8 +318,10 @@ constexpr int dec_wave_lds() { return 32 * D * 2 + 16 * (32 + 8) * 2; }
 // NW = 16 (1024 threads, one workgroup per CU): the small-batch form — a 512-key partition per workgroup, so a
 // context of <= 512 keys is ONE partition whose workgroup writes the final output (no reduce work for it).
 // TS: debug instantiation writing wall-clock stamps of workgroup (0, 0, 0) wave 0 to ts[0..7] (tools/prof_attn_decode.py)
-template <int D, bool F16, bool KV8, int NW = 4, bool TS = false>
-__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(KV8 ? 2 : 4, KV8 ? 2 : 4))) void attn_decode_mfma_kernel(
+// DPF: the K-prefetch form (below; 2 waves / SIMD for its registers, MX_DECODE_PF=0 selects the 4-wave form)
+template <int D, bool F16, bool KV8, int NW = 4, bool TS = false, bool DPF = false>
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(
+    (KV8 || (DPF && !TS && NW <= 8)) ? 2 : 4, (KV8 || (DPF && !TS && NW <= 8)) ? 2 : 4))) void attn_decode_mfma_kernel(
     const bf16_t* __restrict__ q, int q_stride, const void* __restrict__ kcv, const void* __restrict__ vcv,
     const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ seq_lens, int Hkv, int G, int bs,
     float scale, int window, float softcap, int part_size, int n_parts, bf16_t* __restrict__ out, int out_stride,
@@ -382,32 +384,57 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(KV8 ? 2
     const char* kc = (const char*)kcv;
     const char* vc = (const char*)vcv;
 
-    for (int kt0 = p_start + wave * KT; kt0 < p1; kt0 += NW * KT) {
-        // ---- issue the tile's K fragment loads and V chunk loads ----
-        bf16x8 kf[2][D / 32];
+    // PF (bf16 caches): the next tile's K fragments are requested while this tile computes. Every K load is then
+    // issued unconditionally (keys past the end read a valid row and are zeroed after the load), and V comes
+    // through registers (plain loads, stored to the LDS image after QK^T) instead of LDS-DMA: the explicit vmcnt
+    // waits below count exactly NK K loads and NVC V loads per tile, which holds only for loads that complete in
+    // issue order (LDS-DMA completions are not ordered against plain loads).
+    constexpr bool PF = DPF && !KV8 && !TS && NW <= 8;  // (16-wave form: 128 VGPRs, no room for a second K tile)
+    constexpr int NK = 2 * (D / 32);
+    auto load_k = [&](int kt, bf16x8(&kf_)[2][D / 32]) {
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
-            const int key = kt0 + 16 * t + col;
+            const int key = kt + 16 * t + col;
             const bool ok = key < p1;
-            const size_t eo = ok ? (((size_t)sbt[key / bs - blk0] * Hkv + kvh) * bs + key % bs) * D : 0;
+            const int kk = (PF || ok) ? (ok ? key : kt) : 0;
+            const size_t eo = (PF || ok) ? (((size_t)sbt[kk / bs - blk0] * Hkv + kvh) * bs + kk % bs) * D : 0;
 #pragma unroll
             for (int ks = 0; ks < D / 32; ++ks) {
                 if constexpr (KV8) {
                     const uint2 w = ok ? *(const uint2*)(kc + (eo + 32 * ks + 8 * g)) : make_uint2(0, 0);
-                    kf[t][ks] = __builtin_bit_cast(bf16x8, fp8x8_to_bf16x8(w));
+                    kf_[t][ks] = __builtin_bit_cast(bf16x8, fp8x8_to_bf16x8(w));
+                } else if constexpr (PF) {
+                    const bf16x8 w = *(const bf16x8*)(kc + (eo + 32 * ks + 8 * g) * ES);
+                    kf_[t][ks] = ok ? w : (bf16x8){};
                 } else {
-                    kf[t][ks] = ok ? *(const bf16x8*)(kc + (eo + 32 * ks + 8 * g) * ES) : (bf16x8){};
+                    kf_[t][ks] = ok ? *(const bf16x8*)(kc + (eo + 32 * ks + 8 * g) * ES) : (bf16x8){};
                 }
             }
+        }
+    };
+    [[maybe_unused]] bf16x8 knext[2][D / 32];
+    if constexpr (PF) {
+        if (p_start + wave * KT < p1) load_k(p_start + wave * KT, knext);
+    }
+    for (int kt0 = p_start + wave * KT; kt0 < p1; kt0 += NW * KT) {
+        // ---- the tile's K fragments (PF: requested during the previous tile) and V chunk loads ----
+        bf16x8 kf[2][D / 32];
+        if constexpr (PF) {
+#pragma unroll
+            for (int t = 0; t < 2; ++t)
+#pragma unroll
+                for (int ks = 0; ks < D / 32; ++ks) kf[t][ks] = knext[t][ks];
+        } else {
+            load_k(kt0, kf);
         }
         // V: bf16 caches go HBM -> LDS by DMA (global_load_lds, no VGPR staging): instruction j fills
         // bytes [1024 j, 1024 j + 1024) of the slice linearly by lane, so each lane fetches the chunk
         // that the swizzled V image (v_lds_off) places at its slot; fp8 caches widen in registers.
-        [[maybe_unused]] uint4 vv[KV8 ? NVC : 1];
+        [[maybe_unused]] uint4 vv[(KV8 || PF) ? NVC : 1];
 #pragma unroll
         for (int j = 0; j < NVC; ++j) {
             int p, c;
-            if constexpr (KV8) {
+            if constexpr (KV8 || PF) {
                 const int id = lane + 64 * j;
                 p = id / (D / 8);
                 c = id % (D / 8);
@@ -424,9 +451,20 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(KV8 ? 2
             const size_t eo = (((size_t)sbt[key / bs - blk0] * Hkv + kvh) * bs + key % bs) * D + c * 8;
             if constexpr (KV8) {
                 vv[j] = kt0 + p < p1 ? fp8x8_to_bf16x8(*(const uint2*)(vc + eo)) : make_uint4(0, 0, 0, 0);
+            } else if constexpr (PF) {
+                vv[j] = *(const uint4*)(vc + eo * ES);  // rows past the end: a valid row, P = 0 there
             } else {
                 __builtin_amdgcn_global_load_lds((const void*)(vc + eo * ES), (MX_LDS void*)(v_lds + 1024 * j), 16, 0, 0);
             }
+        }
+        [[maybe_unused]] const bool more = kt0 + NW * KT < p1;  // wave-uniform
+        if constexpr (PF) {
+            __builtin_amdgcn_sched_barrier(0);
+            if (more) load_k(kt0 + NW * KT, knext);
+            __builtin_amdgcn_sched_barrier(0);
+            // this tile's K (issued before its V DMAs and the next tile's K) has landed
+            if (more) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NVC + NK) : "memory");
+            else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NVC) : "memory");
         }
         // ---- S = Q K^T : 16 head rows x 32 keys ----
         f32x4 sacc[2];
@@ -440,7 +478,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(KV8 ? 2
         if constexpr (TS) {
             if (kt0 == p_start) DEC_TS(3)  // the K tile has landed (first tile of wave 0)
         }
-        if constexpr (KV8) {  // V -> this wave's LDS slice (the previous tile's reads have returned)
+        if constexpr (KV8 || PF) {  // V -> this wave's LDS slice (the previous tile's reads have returned)
 #pragma unroll
             for (int j = 0; j < NVC; ++j) {
                 const int id = lane + 64 * j, p = id / (D / 8), c = id % (D / 8);
@@ -482,8 +520,13 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(KV8 ? 2
 #pragma unroll
             for (int i = 0; i < 4; ++i)
                 *(bf16_t*)(pw + (4 * g + i) * PSTRIDE + (16 * t + col) * 2) = f32_to_bf16(sacc[t][i]);
-        // vmcnt(0) + lgkmcnt(0): the V DMA has landed and the P (and fp8 V) writes are visible
-        __builtin_amdgcn_s_waitcnt(0);
+        // the V DMA has landed and the P (and fp8 V) writes are visible (PF: the next tile's K may stay in flight)
+        if constexpr (PF) {
+            if (more) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(NK) : "memory");
+            else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        } else {
+            __builtin_amdgcn_s_waitcnt(0);
+        }
         __builtin_amdgcn_wave_barrier();
         // ---- O += P V ----
         const bf16x8 pa = *(const bf16x8*)(pw + col * PSTRIDE + 8 * g * 2);
@@ -587,6 +630,13 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(KV8 ? 2
     }
 }
 
+static bool decode_pf() {
+    // off by default: at c128 the 2-wave prefetch form measured 1.5 % slower end to end than the 4-wave form
+    // (profiles/r5_step_composition.md); MX_DECODE_PF=1 selects it
+    static const bool on = getenv("MX_DECODE_PF") && atoi(getenv("MX_DECODE_PF")) != 0;
+    return on;
+}
+
 template <int D>
 static int launch_decode_mfma(const bf16_t* q, int q_stride, const void* kc, const void* vc, const int* bt,
                               int bt_stride, const int* seq_lens, int B, int Hkv, int G, int bs, float scale,
@@ -625,7 +675,11 @@ static int launch_decode_mfma(const bf16_t* q, int q_stride, const void* kc, con
             attn_decode_mfma_kernel<D, F16, false, 8><<<grid, 512, lds, st>>>(
                 q, q_stride, kc, vc, bt, bt_stride, seq_lens, Hkv, G, bs, scale, window, softcap, part_size, n_parts,
                 out, out_stride, part_ml, part_o, part_cnt);
-        } else
+        } else if (decode_pf())
+            attn_decode_mfma_kernel<D, F16, false, 4, false, true><<<grid, 256, lds, st>>>(
+                q, q_stride, kc, vc, bt, bt_stride, seq_lens, Hkv, G, bs, scale, window, softcap, part_size, n_parts,
+                out, out_stride, part_ml, part_o, part_cnt);
+        else
             attn_decode_mfma_kernel<D, F16, false><<<grid, 256, lds, st>>>(q, q_stride, kc, vc, bt, bt_stride,
                                                                           seq_lens, Hkv, G, bs, scale, window, softcap,
                                                                           part_size, n_parts, out, out_stride, part_ml,
@@ -672,7 +726,11 @@ extern "C" int mxk_attn_decode_mfma(const bf16_t* q, int q_stride, const void* k
     return (int)hipErrorInvalidValue;
 }
 
-template <int D, int GW, int VT, bool F16, bool KV8>
+// KSP = 2 (key split, GW = 4 only: 8 waves): two groups of GW waves share the workgroup's 16 query rows x GW heads and take alternate
+// 64-key tiles (each group stages its own K / V tile), then merge (m, l, O) through LDS. A short prompt chunk runs
+// only ~n_tiles x Hq / GW workgroups (136 for a 270-token chunk of Llama-3-8B, fewer than the CUs), each walking
+// its causal key range one tile at a time: the split halves the longest walk.
+template <int D, int GW, int VT, bool F16, bool KV8, int KSP = 1>
 __global__ __launch_bounds__(512) void attn_prefill_kernel(const bf16_t* __restrict__ q,
                                                            const void* __restrict__ kc,
                                                            const void* __restrict__ vc,
@@ -683,26 +741,30 @@ __global__ __launch_bounds__(512) void attn_prefill_kernel(const bf16_t* __restr
                                                            const int* __restrict__ ctx_lens, int Hq, int Hkv,
                                                            int G, int bs, float scale, int window, float softcap,
                                                            bf16_t* __restrict__ out) {
-    constexpr int NW = GW >= 3 ? GW : 4;      // waves per workgroup
-    constexpr int RT = NW / GW;               // 16-row query tiles per workgroup
+    static_assert(KSP == 1 || GW == 4, "key split: 2 x 4 waves (the 512-thread launch bound)");
+    constexpr int NWG = GW >= 3 ? GW : 4;     // waves per key group
+    constexpr int NW = NWG * KSP;             // waves per workgroup
+    constexpr int RT = NWG / GW;              // 16-row query tiles per workgroup
     constexpr int KT = 64;                    // keys per tile
     constexpr int KBYTES = KT * D * 2;
     constexpr int PSTRIDE = (KT + 8) * 2;     // bytes per P row (padded)
     constexpr int VTSTRIDE = (KT + 8) * 2;    // VT=1: bytes per transposed V row (one dim)
     constexpr int VBYTES = VT ? D * VTSTRIDE : KBYTES;
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    char* k_lds = smem;
-    char* v_lds = smem + KBYTES;
-    char* p_lds = smem + KBYTES + VBYTES;
-    constexpr int NT_C = NW * 64;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int ksp = KSP > 1 ? wave / NWG : 0;  // key group
+    char* k_lds = smem + ksp * (KBYTES + VBYTES);
+    char* v_lds = k_lds + KBYTES;
+    char* p_lds = smem + KSP * (KBYTES + VBYTES);
+    constexpr int NT_C = NWG * 64;             // threads staging one group's tile
+    const int tid = threadIdx.x - ksp * NT_C;
     const int g = lane >> 4, col = lane & 15;
     const int tile = blockIdx.x;
     const int s = tile_seq[tile], q0 = tile_q0[tile];
     if (s < 0) return;  // padding tile of a graph-captured step (uniform across the workgroup)
     const int hq = blockIdx.y * GW + (wave % GW);
     const int kvh = (blockIdx.y * GW) / G;
-    const int rt = wave / GW;
+    const int rt = KSP > 1 ? 0 : wave / GW;
     const int qbeg = cu_q[s], qlen = cu_q[s + 1] - qbeg;
     const int ctx = ctx_lens[s];
     const int pos_off = ctx - qlen;  // position of query 0
@@ -743,7 +805,7 @@ __global__ __launch_bounds__(512) void attn_prefill_kernel(const bf16_t* __restr
     auto load_tile = [&](int kt0) {
 #pragma unroll
         for (int j = 0; j < NCH; ++j) {
-            const int id = threadIdx.x + j * NT_C;
+            const int id = tid + j * NT_C;
             const int p = id / (D / 8), c = id % (D / 8);
             const int pos = kt0 + p;
             kr[j] = KRaw{};
@@ -764,7 +826,7 @@ __global__ __launch_bounds__(512) void attn_prefill_kernel(const bf16_t* __restr
     auto store_tile = [&]() {
 #pragma unroll
         for (int j = 0; j < NCH; ++j) {
-            const int id = threadIdx.x + j * NT_C;
+            const int id = tid + j * NT_C;
             if (id >= CH) continue;
             const int p = id / (D / 8), c = id % (D / 8);
             uint4 kv, vv;
@@ -786,12 +848,21 @@ __global__ __launch_bounds__(512) void attn_prefill_kernel(const bf16_t* __restr
             }
         }
     };
-    if (kt_begin < kv_end) load_tile(kt_begin);
-    for (int kt0 = kt_begin; kt0 < kv_end; kt0 += KT) {
+    // key group ksp takes tiles kt_begin + KT (ksp + KSP r); every group runs the same number of rounds (the
+    // barriers below are workgroup-wide), a group past the end idles through its last round
+    const int n_rounds = kv_end > kt_begin ? (kv_end - kt_begin + KSP * KT - 1) / (KSP * KT) : 0;
+    if (kt_begin + ksp * KT < kv_end) load_tile(kt_begin + ksp * KT);
+    for (int r = 0; r < n_rounds; ++r) {
+        const int kt0 = kt_begin + (KSP * r + ksp) * KT;
+        const bool live = kt0 < kv_end;
         // ---- stage this K and V tile (64 keys x D), then request the next one ----
-        store_tile();
-        if (kt0 + KT < kv_end) load_tile(kt0 + KT);
+        if (live) store_tile();
+        if (kt0 + KSP * KT < kv_end) load_tile(kt0 + KSP * KT);
         __syncthreads();
+        if (!live) {
+            __syncthreads();
+            continue;
+        }
         // ---- S = Q K^T : 16 rows x 64 keys ----
         f32x4 sacc[4];
 #pragma unroll
@@ -876,6 +947,33 @@ __global__ __launch_bounds__(512) void attn_prefill_kernel(const bf16_t* __restr
         }
         __syncthreads();
     }
+    if constexpr (KSP > 1) {
+        // ---- merge the key groups: group 1 parks (m, l, O) in the freed tile buffers, group 0 combines ----
+        float* mo = (float*)smem + (wave % GW) * (16 * D + 32);  // [16 rows][D] O, then m[16], l[16]
+        if (ksp == 1) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+#pragma unroll
+                for (int nt = 0; nt < D / 16; ++nt) mo[(4 * g + i) * D + 16 * nt + col] = oacc[nt][i];
+                if (col == 0) {
+                    mo[16 * D + 4 * g + i] = mrow[i];
+                    mo[16 * D + 16 + 4 * g + i] = lrow[i];
+                }
+            }
+        }
+        __syncthreads();
+        if (ksp == 1) return;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const float m1 = mo[16 * D + 4 * g + i], l1 = mo[16 * D + 16 + 4 * g + i];
+            const float mn = fmaxf(mrow[i], m1);
+            const float a0 = mn == -INFINITY ? 0.f : exp2f(mrow[i] - mn), a1 = mn == -INFINITY ? 0.f : exp2f(m1 - mn);
+            lrow[i] = lrow[i] * a0 + l1 * a1;
+#pragma unroll
+            for (int nt = 0; nt < D / 16; ++nt)
+                oacc[nt][i] = oacc[nt][i] * a0 + mo[(4 * g + i) * D + 16 * nt + col] * a1;
+        }
+    }
     // ---- write O / l ----
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -888,21 +986,21 @@ __global__ __launch_bounds__(512) void attn_prefill_kernel(const bf16_t* __restr
     }
 }
 
-template <int D, int GW, int VT, bool KV8>
+template <int D, int GW, int VT, bool KV8, int KSP = 1>
 static void launch_prefill_t(dim3 grid, int threads, size_t lds, const bf16_t* q, const void* kc, const void* vc,
                              const int* bt, int bt_stride, const int* tile_seq, const int* tile_q0, const int* cu_q,
                              const int* ctx_lens, int Hq, int Hkv, int bs, float scale, int window, float softcap,
                              bf16_t* out, hipStream_t st) {
     MX_ACT_DISPATCH({
-        if (lds > 65536) {  // D=256 tiles (73-82 KB): opt in to the large LDS allocation once
+        if (lds > 65536) {  // D=256 tiles / key-split tiles (73-82 KB): opt in to the large LDS allocation once
             static bool opted = false;
             if (!opted) {
-                (void)hipFuncSetAttribute((const void*)attn_prefill_kernel<D, GW, VT, F16, KV8>,
+                (void)hipFuncSetAttribute((const void*)attn_prefill_kernel<D, GW, VT, F16, KV8, KSP>,
                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
                 opted = true;
             }
         }
-        attn_prefill_kernel<D, GW, VT, F16, KV8><<<grid, threads, lds, st>>>(
+        attn_prefill_kernel<D, GW, VT, F16, KV8, KSP><<<grid, threads, lds, st>>>(
             q, kc, vc, bt, bt_stride, tile_seq, tile_q0, cu_q, ctx_lens, Hq, Hkv, Hq / Hkv, bs, scale, window,
             softcap, out);
     });
@@ -917,6 +1015,18 @@ static int launch_prefill(const bf16_t* q, const void* kc, const void* vc, const
     dim3 grid(n_tiles, Hq / GW);
     const size_t lds0 = 2 * 64 * D * 2 + NW * 16 * (64 + 8) * 2;
     const size_t lds1 = 64 * D * 2 + D * (64 + 8) * 2 + NW * 16 * (64 + 8) * 2;
+    // key split when the grid leaves most CUs idle (short prompt chunks): bf16 cache, V image, D = 128, one wave
+    // per head and GW = 4 (2 x 4 waves = 512 threads, the kernel's launch bound; the merge buffer, 4 x (16 D + 32)
+    // floats, fits the two tile buffers)
+    if constexpr (D == 128 && GW == 4) {
+        static const bool ks_on = !getenv("MX_PREFILL_KSPLIT") || atoi(getenv("MX_PREFILL_KSPLIT")) != 0;
+        if (ks_on && vmode == 0 && !kv8 && (long)n_tiles * (Hq / GW) < 256) {
+            launch_prefill_t<D, GW, 0, false, 2>(grid, 2 * NW * 64, 2 * (2 * 64 * D * 2) + 2 * NW * 16 * (64 + 8) * 2,
+                                                 q, kc, vc, bt, bt_stride, tile_seq, tile_q0, cu_q, ctx_lens, Hq, Hkv,
+                                                 bs, scale, window, softcap, out, st);
+            MXK_CHECK_LAUNCH();
+        }
+    }
 #define PFL(VT_, K8_)                                                                                          \
     launch_prefill_t<D, GW, VT_, K8_>(grid, NW * 64, VT_ ? lds1 : lds0, q, kc, vc, bt, bt_stride, tile_seq,    \
                                       tile_q0, cu_q, ctx_lens, Hq, Hkv, bs, scale, window, softcap, out, st)

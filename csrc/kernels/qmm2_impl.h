@@ -10,14 +10,19 @@ namespace {
 // stage is only 12-14 KB, and with 4 slots a workgroup keeps ~2 stages (24 KB) in flight: at the ~1.1 us
 // issue -> landed latency of LDS-DMA under load that caps the CU at ~30 GB/s, which is what the narrow
 // projections measured (qkv M = 256: 768 KB per workgroup in 25 us). 8 slots keep 6 stages in flight.
-template <int QT, int WM, int KS, int WN, int NS = 4>
+// NG: 32-column groups per workgroup — 4 (128 columns, 4 KS waves), or 8 (256 columns, 8 waves, KS = 1: "wide"
+// tiles). The A tile is staged once per workgroup and read by every column group, so the A bytes a CU stages per
+// MFMA flop are 1 / (32 NG): the wide tile halves the activation staging that caps large-M GEMMs
+// (tools/lds_stage_bench.hip: ~13-19 TB/s of L2 -> LDS staging for the whole chip).
+template <int QT, int WM, int KS, int WN, int NS = 4, int NG = 4>
 struct Q2Geom {
     using F = Q2F<QT>;
+    static_assert(NG == 4 || (NG == 8 && KS == 1), "wide tiles: 8 waves, one per column group");
     static constexpr int BM = 32 * WM * WN;
-    static constexpr int NT = 4 * KS;                 // waves
+    static constexpr int NT = NG == 8 ? 8 : 4 * KS;   // waves
     static constexpr int A_BYTES = BM * 128;          // one 64-k tile of A
-    static constexpr int STAGE = A_BYTES + 4 * F::QB; // A + the 4 column groups' quant bytes
-    static constexpr int HSZ = 4 * F::HB;             // one super-block header slot (4 groups)
+    static constexpr int STAGE = A_BYTES + NG * F::QB; // A + the column groups' quant bytes
+    static constexpr int HSZ = NG * F::HB;            // one super-block header slot (NG groups)
     static constexpr int NH = NS == 8 ? 3 : 2;         // header slots: super-blocks live at once
     static constexpr int LDS = NS * STAGE + NH * HSZ;
     static constexpr int WA = BM / 8 / NT;            // A LDS-DMA instructions per wave per stage
@@ -51,12 +56,12 @@ constexpr int q2_cnt_run() {
 }
 
 // DBG (isolation builds, tools/prof_qmm.py --q2dbg): 1 no MFMA, 2 no dequant VALU, 4 no A loads, 8 no weight loads
-template <int QT, int WM, int KS, int WN, int EPI, int DBG = 0, int NS = 4>
-__global__ __launch_bounds__(256 * KS) void qmm2_kernel(const uint16_t* __restrict__ A, int lda,
+template <int QT, int WM, int KS, int WN, int EPI, int DBG = 0, int NS = 4, int NG = 4>
+__global__ __launch_bounds__(NG == 8 ? 512 : 256 * KS) void qmm2_kernel(const uint16_t* __restrict__ A, int lda,
                                                         const uint8_t* __restrict__ W, int M, int N, int K,
                                                         int n_mt, int splits, int sbps, void* __restrict__ Cv,
                                                         int ldc, int rot_mul) {
-    using G = Q2Geom<QT, WM, KS, WN, NS>;
+    using G = Q2Geom<QT, WM, KS, WN, NS, NG>;
     using F = Q2F<QT>;
     constexpr int BM = G::BM, WA = G::WA, STAGE = G::STAGE, A_BYTES = G::A_BYTES;
     static_assert(NS == 4 || NS == 8, "ring depth");
@@ -79,8 +84,8 @@ __global__ __launch_bounds__(256 * KS) void qmm2_kernel(const uint16_t* __restri
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int h = lane >> 5, col = lane & 31;
     // cg: the column group this wave DMAs; (mw, nw): its compute tile = rows mw * 32 WM .., groups nw * WN + j
-    const int cg = wave & 3, kh = wave >> 2;
-    constexpr int NW = 4 / WN;
+    const int cg = wave % NG, kh = NG == 8 ? 0 : wave >> 2;
+    constexpr int NW = NG / WN;
     const int nw = cg % NW, mw = cg / NW;
 
     // XCD-aware bijective remap: consecutive logical ids (the row tiles and splits of one column panel)
@@ -98,7 +103,7 @@ __global__ __launch_bounds__(256 * KS) void qmm2_kernel(const uint16_t* __restri
     if (sb0 >= sb1) return;
     const int m_base = mt * BM;
     const int ngrp = N >> 5;
-    const int g = min(ct * 4 + cg, ngrp - 1);  // groups past N re-read the last (never stored)
+    const int g = min(ct * NG + cg, ngrp - 1);  // groups past N re-read the last (never stored)
     const uint8_t* wg = W + (size_t)g * ((size_t)nsb * F::UNIT);
 
     // A LDS-DMA sources: instruction i of this wave fills 8-row block j = wave * WA + i; lane p writes
@@ -307,7 +312,7 @@ __global__ __launch_bounds__(256 * KS) void qmm2_kernel(const uint16_t* __restri
     const int mb = m_base + mw * WM * 32;
 #pragma unroll
     for (int j = 0; j < WN; ++j) {
-        const int nt = (ct * 4 + nw * WN + j) * 32;
+        const int nt = (ct * NG + nw * WN + j) * 32;
         const int n = nt + col;
         if (nt >= N) break;
         if constexpr (EPI == E16_SWIGLU || EPI == E16_GEGLU) {
@@ -365,29 +370,29 @@ __global__ __launch_bounds__(256 * KS) void qmm2_kernel(const uint16_t* __restri
     }
 }
 
-template <int QT, int WM, int KS, int WN, int EPI, int NS = 4>
+template <int QT, int WM, int KS, int WN, int EPI, int NS = 4, int NG = 4>
 static int launch_qmm2(const uint16_t* A, int lda, const uint8_t* W, int M, int N, int K, int splits, void* C, int ldc,
                        hipStream_t st) {
-    using G = Q2Geom<QT, WM, KS, WN, NS>;
+    using G = Q2Geom<QT, WM, KS, WN, NS, NG>;
     const int nsb = K >> 8;
     splits = max(1, min(splits, nsb));
     const int sbps = (nsb + splits - 1) / splits;
     splits = (nsb + sbps - 1) / sbps;  // no empty splits
-    const int n_ct = (N + 127) / 128, n_mt = (M + G::BM - 1) / G::BM;
+    const int n_ct = (N + 32 * NG - 1) / (32 * NG), n_mt = (M + G::BM - 1) / G::BM;
     const long nwg = (long)n_ct * splits * n_mt;
     if (nwg <= 0 || nwg > 0x7fffffff) return (int)hipErrorInvalidValue;
     static bool attr_set = false;
     if (!attr_set) {
-        (void)hipFuncSetAttribute((const void*)qmm2_kernel<QT, WM, KS, WN, EPI, 0, NS>,
+        (void)hipFuncSetAttribute((const void*)qmm2_kernel<QT, WM, KS, WN, EPI, 0, NS, NG>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS);
         attr_set = true;
     }
-    qmm2_kernel<QT, WM, KS, WN, EPI, 0, NS><<<dim3((unsigned)nwg), 256 * KS, G::LDS, st>>>(A, lda, W, M, N, K, n_mt,
-                                                                                           splits, sbps, C, ldc, g_qmm2_rot);
+    qmm2_kernel<QT, WM, KS, WN, EPI, 0, NS, NG><<<dim3((unsigned)nwg), 64 * G::NT, G::LDS, st>>>(
+        A, lda, W, M, N, K, n_mt, splits, sbps, C, ldc, g_qmm2_rot);
     MXK_CHECK_LAUNCH();
 }
 
-// ks: 1 / 2 waves per column group; ks | 8 selects the 8-slot ring (64-row tiles only)
+// ks: 1 / 2 waves per column group; ks | 8 selects the 8-slot ring (64-row tiles only); 17 the wide tiles
 template <int QT, int EPI>
 static int dispatch_qmm2(int wm, int ks, int wn, const uint16_t* A, int lda, const uint8_t* W, int M, int N, int K,
                          int splits, void* C, int ldc, hipStream_t st) {
@@ -408,6 +413,13 @@ static int dispatch_qmm2(int wm, int ks, int wn, const uint16_t* A, int lda, con
     // 224-row tiles: M in (384, 448] (a decode batch + a prompt chunk a little over 256 tokens) in two row tiles
     Q2_CASE(7, 1, 1)
     Q2_DEEP(2, 1, 1) Q2_DEEP(2, 2, 1) Q2_DEEP(1, 2, 2)
+    // ks | 16: wide tiles (8 column groups, 256 columns per workgroup, 8 waves)
+#define Q2_WIDE(WM_, WN_)                                                                      \
+    if constexpr (Q2Geom<QT, WM_, 1, WN_, 4, 8>::LDS <= 160 * 1024)                           \
+        if (wm == WM_ && ks == 17 && wn == WN_)                                                \
+            return launch_qmm2<QT, WM_, 1, WN_, EPI, 4, 8>(A, lda, W, M, N, K, splits, C, ldc, st);
+    Q2_WIDE(2, 1) Q2_WIDE(4, 1) Q2_WIDE(6, 1) Q2_WIDE(3, 2)
+#undef Q2_WIDE
 #undef Q2_DEEP
 #undef Q2_CASE
     return (int)hipErrorInvalidValue;

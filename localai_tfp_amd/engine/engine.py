@@ -91,7 +91,8 @@ class EngineConfig:
     graph_buckets: tuple = (1, 2, 4, 8, 16, 32, 48, 64, 96, 128, 160, 192, 224, 256)
     # mixed steps (decode rows + prompt chunks) replay graphs too: prefill-token buckets, max prompt
     # sequences per graphed step, and a cap on captured graphs (captured lazily, first use of a shape)
-    mixed_graph_tokens: tuple = (64, 128, 256, 384, 512, 768, 1024)
+    mixed_graph_tokens: tuple = tuple(int(x) for x in (__import__("os").environ.get("MX_MIXED_TOKENS") or
+                                                       "64,128,256,384,512,768,1024").split(",") if x.strip())
     mixed_graph_seqs: int = 4
     max_graphs: int = 64
     attn_part_size: int = 256  # must match ops.core.attn_decode's default
@@ -892,6 +893,10 @@ class LLMEngine:
         P = next((x for x in c.mixed_graph_tokens if x >= npf), None)
         if P is None or B + P > self.ws.max_tokens:
             return None
+        # the decode rows of a mixed step: one attention partition per sequence too (no partition-merge launch)
+        if nd and B >= self.SINGLE_PART_B and int(plan["dec_lens"].max()) <= self.SINGLE_PART_CTX and \
+                os.environ.get("MX_MIXED_SINGLE_PART", "1") == "1":
+            return (B, P, c.mixed_graph_seqs, self.SINGLE_PART_CTX)
         return (B, P, c.mixed_graph_seqs, 0)
 
     def _graph_get(self, key, create: bool = True) -> StepGraph | None:
