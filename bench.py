@@ -56,7 +56,8 @@ def parse():
     ap.add_argument("--concurrency", type=int, default=128)
     ap.add_argument("--prompt-len", type=int, default=256)
     ap.add_argument("--gen-len", type=int, default=256)
-    ap.add_argument("--max-batched-tokens", type=int, default=512, help="tokens per engine step (llama.cpp n_batch default)")
+    ap.add_argument("--max-batched-tokens", type=int, default=416,
+                    help="tokens per engine step (the engine default: a c128 decode batch + a 288-token prompt chunk)")
     ap.add_argument("--prefill-chunk", type=int, default=0, help="prompt tokens per sequence per step (0: budget)")
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--dp-gateway", default="per-rank", choices=["per-rank", "single"],

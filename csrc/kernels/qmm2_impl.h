@@ -25,7 +25,9 @@ struct Q2Geom {
     static constexpr int HSZ = NG * F::HB;            // one super-block header slot (NG groups)
     static constexpr int NH = NS == 8 ? 3 : 2;         // header slots: super-blocks live at once
     static constexpr int LDS = NS * STAGE + NH * HSZ;
-    static constexpr int WA = BM / 8 / NT;            // A LDS-DMA instructions per wave per stage
+    // A LDS-DMA instructions per wave per stage (rounded up: with BM / 8 not a multiple of NT the last wave's spare
+    // instructions re-load the tile's last 8-row block into its own slot, identical bytes)
+    static constexpr int WA = (BM / 8 + NT - 1) / NT;
     // LDS-DMA instructions per stage of a weight-loading wave (kh == 0) / an A-only wave, by the stage's
     // position in its super-block (JQ == 0 stages also carry the header)
     template <int JQ, bool WL>
@@ -67,7 +69,7 @@ __global__ __launch_bounds__(NG == 8 ? 512 : 256 * KS) void qmm2_kernel(const ui
     static_assert(NS == 4 || NS == 8, "ring depth");
     static_assert(WN == 1 || WN == 2, "WN");
     static_assert(KS == 1 || 4 * WM * WN * 16 * 64 * 4 <= G::LDS, "KS = 2 partials fit in the ring");
-    static_assert(WA >= 1 && WA * 8 * G::NT == BM, "A tile split");
+    static_assert(WA >= 1 && WA * 8 * G::NT >= BM && (WA - 1) * 8 * G::NT < BM, "A tile split");
     static_assert(G::LDS <= 160 * 1024, "LDS");
     static_assert((NS - 2) * G::template cnt<0, true>() <= 63, "vmcnt range");
     // LDS-DMA instructions per stage as issued (the isolation builds drop some)
@@ -111,7 +113,7 @@ __global__ __launch_bounds__(NG == 8 ? 512 : 256 * KS) void qmm2_kernel(const ui
     uint32_t aoff[WA];
 #pragma unroll
     for (int i = 0; i < WA; ++i) {
-        const int j = wave * WA + i;
+        const int j = min(wave * WA + i, BM / 8 - 1);
         const int s = lane >> 4, r8 = (lane >> 1) & 7, hh = (lane & 1) ^ (j & 1);
         const int row = min(m_base + 8 * j + r8, M - 1);
         aoff[i] = (uint32_t)(row * lda + 16 * s + 8 * hh);
@@ -131,7 +133,8 @@ __global__ __launch_bounds__(NG == 8 ? 512 : 256 * KS) void qmm2_kernel(const ui
         const uint16_t* ak = A + (size_t)kta * 64;
 #pragma unroll
         for (int i = 0; i < WAI; ++i)
-            __builtin_amdgcn_global_load_lds((const void*)(ak + aoff[i]), (MX_LDS void*)(sb + (wave * WA + i) * 1024),
+            __builtin_amdgcn_global_load_lds((const void*)(ak + aoff[i]),
+                                             (MX_LDS void*)(sb + min(wave * WA + i, BM / 8 - 1) * 1024),
                                              16, 0, 0);
         if constexpr (decltype(wl_c)::value && QII > 0) {
             const uint8_t* u = wg + (size_t)sbw * F::UNIT;
@@ -418,7 +421,7 @@ static int dispatch_qmm2(int wm, int ks, int wn, const uint16_t* A, int lda, con
     if constexpr (Q2Geom<QT, WM_, 1, WN_, 4, 8>::LDS <= 160 * 1024)                           \
         if (wm == WM_ && ks == 17 && wn == WN_)                                                \
             return launch_qmm2<QT, WM_, 1, WN_, EPI, 4, 8>(A, lda, W, M, N, K, splits, C, ldc, st);
-    Q2_WIDE(2, 1) Q2_WIDE(4, 1) Q2_WIDE(6, 1) Q2_WIDE(3, 2)
+    Q2_WIDE(2, 1) Q2_WIDE(4, 1) Q2_WIDE(6, 1) Q2_WIDE(3, 2) Q2_WIDE(7, 1)
 #undef Q2_WIDE
 #undef Q2_DEEP
 #undef Q2_CASE
@@ -429,12 +432,18 @@ template <int DBG>
 static int launch_dbg(int wm, int ks, int wn, const uint16_t* A, int lda, const uint8_t* W, int M, int N, int K, void* C, int ldc,
                       hipStream_t st) {
     constexpr int QT = MXQ_Q4_K, EPI = E16_SWIGLU;
-    auto go = [&](auto kern, int bm, int ks, int lds) {
+    auto go = [&](auto kern, int bm, int ks, int lds, int ng = 4) {
         (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-        const int n_ct = (N + 127) / 128, n_mt = (M + bm - 1) / bm;
-        kern<<<dim3(n_ct * n_mt), 256 * ks, lds, st>>>(A, lda, W, M, N, K, n_mt, 1, K >> 8, C, ldc, g_qmm2_rot);
+        const int n_ct = (N + 32 * ng - 1) / (32 * ng), n_mt = (M + bm - 1) / bm;
+        kern<<<dim3(n_ct * n_mt), ng == 8 ? 512 : 256 * ks, lds, st>>>(A, lda, W, M, N, K, n_mt, 1, K >> 8, C, ldc,
+                                                                      g_qmm2_rot);
         return (int)hipGetLastError();
     };
+    // ks 17: the wide tiles (8 column groups)
+    if (wm == 6 && ks == 17 && wn == 1)
+        return go(qmm2_kernel<QT, 6, 1, 1, EPI, DBG, 4, 8>, 192, 1, Q2Geom<QT, 6, 1, 1, 4, 8>::LDS, 8);
+    if (wm == 4 && ks == 17 && wn == 1)
+        return go(qmm2_kernel<QT, 4, 1, 1, EPI, DBG, 4, 8>, 128, 1, Q2Geom<QT, 4, 1, 1, 4, 8>::LDS, 8);
     if (wm == 8 && ks == 1 && wn == 1) return go(qmm2_kernel<QT, 8, 1, 1, EPI, DBG>, 256, 1, Q2Geom<QT, 8, 1, 1>::LDS);
     if (wm == 4 && ks == 2 && wn == 1) return go(qmm2_kernel<QT, 4, 2, 1, EPI, DBG>, 128, 2, Q2Geom<QT, 4, 2, 1>::LDS);
     if (wm == 4 && ks == 1 && wn == 2) return go(qmm2_kernel<QT, 4, 1, 2, EPI, DBG>, 256, 1, Q2Geom<QT, 4, 1, 2>::LDS);

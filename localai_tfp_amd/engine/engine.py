@@ -80,7 +80,10 @@ def gc_tune():
 @dataclass
 class EngineConfig:
     max_num_seqs: int = 256
-    max_batched_tokens: int = 512  # tokens per step: llama.cpp's n_batch default (LocalAI `batch: 512`)
+    # tokens per step (llama.cpp's n_batch; a model's `batch:` overrides it). 416 = a full c128 decode batch plus a
+    # 288-token prompt chunk: the measured best step composition on MI355X (profiles/r5_step_composition.md; 512
+    # packs two prompts' chunks into 512-row steps that the GEMM tiles cover less evenly)
+    max_batched_tokens: int = 416
     prefill_chunk: int | None = None  # prompt tokens per sequence per step (None: the whole step budget)
     max_model_len: int = 8192
     block_size: int = 16
@@ -92,7 +95,8 @@ class EngineConfig:
     # mixed steps (decode rows + prompt chunks) replay graphs too: prefill-token buckets, max prompt
     # sequences per graphed step, and a cap on captured graphs (captured lazily, first use of a shape)
     mixed_graph_tokens: tuple = tuple(int(x) for x in (__import__("os").environ.get("MX_MIXED_TOKENS") or
-                                                       "64,128,256,384,512,768,1024").split(",") if x.strip())
+                                                       "64,128,192,256,288,320,352,384,448,512,768,1024").split(",")
+                              if x.strip())
     mixed_graph_seqs: int = 4
     max_graphs: int = 64
     attn_part_size: int = 256  # must match ops.core.attn_decode's default

@@ -31,7 +31,7 @@ def model_options(c, app=None, model_path: str = "") -> object:
         CLIPSubfolder=d.clip_subfolder, Options=[str(o) for o in c.options], CLIPSkip=int(d.clip_skip),
         ControlNet=d.control_net, ContextSize=int(c.context_size or (app.context_size if app and app.context_size
                                                                      else 4096)),
-        Seed=_seed(c), NBatch=int(c.parameters.batch or 512), NoMulMatQ=c.no_mulmatq, DraftModel=c.draft_model,
+        Seed=_seed(c), NBatch=int(c.parameters.batch or 0), NoMulMatQ=c.no_mulmatq, DraftModel=c.draft_model,
         AudioPath="", Quantization=c.quantization, LoadFormat=c.load_format,
         GPUMemoryUtilization=c.gpu_memory_utilization, TrustRemoteCode=c.trust_remote_code,
         EnforceEager=c.enforce_eager, SwapSpace=c.swap_space, MaxModelLen=c.max_model_len,
