@@ -1028,7 +1028,8 @@ extern "C" int mxk_sample_topk_cap() { return TK_CAP; }
 // greedy argmax over rows (fast path used by the decode graph when every row is greedy)
 __global__ __launch_bounds__(1024) void argmax_kernel(const float* __restrict__ x, int ld, int V,
                                                       int* __restrict__ out, unsigned long long* __restrict__ keys,
-                                                      int off) {
+                                                      int off, const int* __restrict__ gate = nullptr) {
+    if (gate && *gate == 0) return;  // graph-captured head of a step whose rows are all sampled
     __shared__ float rv[16];
     __shared__ int ri[16];
     const float* r = x + (size_t)blockIdx.x * ld;
@@ -1084,6 +1085,14 @@ __global__ __launch_bounds__(1024) void argmax_kernel(const float* __restrict__ 
 extern "C" int mxk_argmax(const float* x, int ld, int B, int V, int* out, hipStream_t st) {
     if (B <= 0) return 0;
     argmax_kernel<<<B, 1024, 0, st>>>(x, ld, V, out, nullptr, 0);
+    MXK_CHECK_LAUNCH();
+}
+
+// the same, skipped on the device when *gate == 0 (a step-graph input: the greedy fast path's argmax runs only on
+// steps that use it)
+extern "C" int mxk_argmax_gated(const float* x, int ld, int B, int V, int* out, const int* gate, hipStream_t st) {
+    if (B <= 0) return 0;
+    argmax_kernel<<<B, 1024, 0, st>>>(x, ld, V, out, nullptr, 0, gate);
     MXK_CHECK_LAUNCH();
 }
 

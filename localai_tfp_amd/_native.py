@@ -65,6 +65,7 @@ KERNEL_SIGS = {
     "mxk_sample_topk_split": [P, I, I, I, P, I, P, P, P, P, I, I, P, P, P, P, P, P, P, P],
     "mxk_sample_params_size": [],
     "mxk_argmax": [P, I, I, I, P, P],
+    "mxk_argmax_gated": [P, I, I, I, P, P, P],
     "mxk_argmax_keys": [P, I, I, I, I, P, P],
     "mxk_argmax_merge": [P, I, I, P, P],
     "mxk_glu": [I, P, P, I, P, I, I, I, P],

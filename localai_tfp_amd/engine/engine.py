@@ -202,7 +202,7 @@ class StepGraph:
         # tokens has one dummy row past T: the in-graph fix-up of decode inputs sampled by the previous
         # (still unread) step scatters into it for the rows that need no fix
         lay = [("tokens", (T + 1,)), ("positions", (T,)), ("slots", (T,)), ("lidx", (self.S,)),
-               ("dec_bt", (Bp, mb)), ("dec_lens", (Bp,)), ("fix_dst", (Bp,)), ("fix_src", (Bp,))]
+               ("dec_bt", (Bp, mb)), ("dec_lens", (Bp,)), ("fix_dst", (Bp,)), ("fix_src", (Bp,)), ("argmax_on", (1,))]
         if P:
             lay += [("pf_bt", (PS, mb)), ("pf_cu", (PS + 1,)), ("pf_ctx", (PS,)), ("pf_tseq", (self.NT,)),
                     ("pf_tq0", (self.NT,))]
@@ -213,7 +213,7 @@ class StepGraph:
         self.n = o
         img = np.zeros(o, np.int32)
         self._default = img
-        for k, v in (("slots", -1), ("dec_lens", 1), ("pf_tseq", -1), ("fix_dst", T)):
+        for k, v in (("slots", -1), ("dec_lens", 1), ("pf_tseq", -1), ("fix_dst", T), ("argmax_on", 1)):
             if k in self.off:
                 self.view(img, k)[...] = v
         self.buf = torch.from_numpy(img.copy()).to(dev)
@@ -260,8 +260,8 @@ class StepGraph:
             if self.vp:
                 engine.model.vocab_argmax(lg, engine.ws, self.argmax)
             else:
-                N.kcall("mxk_argmax", lg.data_ptr(), lg.stride(0), self.S, lg.shape[1], self.argmax.data_ptr(),
-                        N.stream_ptr())
+                N.kcall("mxk_argmax_gated", lg.data_ptr(), lg.stride(0), self.S, lg.shape[1], self.argmax.data_ptr(),
+                        self.v["argmax_on"].data_ptr(), N.stream_ptr())
 
         with torch.cuda.stream(s):
             for _ in range(2):  # warm-up (allocations, lazy init) outside capture
@@ -312,6 +312,8 @@ class StepGraph:
             dst, src = plan["fix"]
             self.view(img, "fix_dst")[:len(dst)] = dst
             self.view(img, "fix_src")[:len(src)] = src
+        if not plan.get("argmax_on", True):
+            self.view(img, "argmax_on")[0] = 0
         return img
 
     def run(self, plan: dict, prev=None):
@@ -705,6 +707,8 @@ class LLMEngine:
             roctx.pop()
         self.stats["plan_s"] += time.perf_counter() - t1
         items = list(so.decode) + [it for it in so.prefill if it.sample]
+        # the graph's greedy argmax head runs only when this step takes its tokens from it
+        plan["argmax_on"] = bool(items) and self._argmax_only(items)
         if self.tp is not None:
             plan["ns"] = len(items)
             plan["gather"] = bool(items) and not self._argmax_only(items)

@@ -47,7 +47,8 @@ def encode_plan(plan: dict) -> np.ndarray:
     """Flat int32 image of a step plan: [nd, flags, graph bucket (B, P, PS, L), ns (rows the leader samples and
     broadcasts on the device: overlap mode), then per PLAN_ARRAYS entry: ndim, *shape, *data]."""
     g = plan.get("graph")
-    flags = int(bool(g)) | (int(bool(plan.get("keep_hidden"))) << 1) | (int(bool(plan.get("gather"))) << 2)
+    flags = int(bool(g)) | (int(bool(plan.get("keep_hidden"))) << 1) | (int(bool(plan.get("gather"))) << 2) | \
+        (int(not plan.get("argmax_on", True)) << 3)
     gk = (tuple(g) + (0, 0, 0, 0))[:4] if g else (0, 0, 0, 0)  # (B, P, PS[, L]) padded to 4
     parts = [np.array([plan["nd"], flags, *gk, int(plan.get("ns", 0))], np.int32)]
     arrays = dict(plan)
@@ -67,7 +68,7 @@ def encode_plan(plan: dict) -> np.ndarray:
 def decode_plan(buf: np.ndarray) -> dict:
     nd, flags = int(buf[0]), int(buf[1])
     plan = {"nd": nd, "graph": tuple(int(x) for x in buf[2:6]) if flags & 1 else False,
-            "keep_hidden": bool(flags & 2), "gather": bool(flags & 4), "ns": int(buf[6])}
+            "keep_hidden": bool(flags & 2), "gather": bool(flags & 4), "ns": int(buf[6]), "argmax_on": not flags & 8}
     i = 7
     for k in PLAN_ARRAYS:
         ndim = int(buf[i])

@@ -147,6 +147,8 @@ def test_plan_codec_roundtrip():
                                         "slots": np.array([19], np.int32), "lidx": np.array([0], np.int32),
                                         "graph": (8, 0, 0, 512)}))
     assert dec_only["graph"] == (8, 0, 0, 512) and "pf_cu" not in dec_only and "fix" not in dec_only
+    assert out["argmax_on"] and dec_only["argmax_on"]  # default: the graph's greedy head runs
+    assert not decode_plan(encode_plan({**plan, "argmax_on": False}))["argmax_on"]
 
 
 def _die_worker(rank, world, port, who):
