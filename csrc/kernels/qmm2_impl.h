@@ -14,12 +14,16 @@ namespace {
 // tiles). The A tile is staged once per workgroup and read by every column group, so the A bytes a CU stages per
 // MFMA flop are 1 / (32 NG): the wide tile halves the activation staging that caps large-M GEMMs
 // (tools/lds_stage_bench.hip: ~13-19 TB/s of L2 -> LDS staging for the whole chip).
-template <int QT, int WM, int KS, int WN, int NS = 4, int NG = 4>
+// GPW: column groups each wave stages (and, with WN = GPW, computes): 1, or 2 for the 4-wave wide form whose
+// waves cover 64 columns each (one wave per SIMD, all of its registers; the A fragments it reads from LDS serve
+// twice the MFMAs)
+template <int QT, int WM, int KS, int WN, int NS = 4, int NG = 4, int GPW = 1>
 struct Q2Geom {
     using F = Q2F<QT>;
     static_assert(NG == 4 || (NG == 8 && KS == 1), "wide tiles: 8 waves, one per column group");
-    static constexpr int BM = 32 * WM * WN;
-    static constexpr int NT = NG == 8 ? 8 : 4 * KS;   // waves
+    static_assert(GPW == 1 || (NG == 8 && WN == 2), "2 groups per wave: the 4-wave wide form");
+    static constexpr int BM = GPW == 2 ? 32 * WM : 32 * WM * WN;
+    static constexpr int NT = NG == 8 ? 8 / GPW : 4 * KS;   // waves
     static constexpr int A_BYTES = BM * 128;          // one 64-k tile of A
     static constexpr int STAGE = A_BYTES + NG * F::QB; // A + the column groups' quant bytes
     static constexpr int HSZ = NG * F::HB;            // one super-block header slot (NG groups)
@@ -31,7 +35,7 @@ struct Q2Geom {
     // LDS-DMA instructions per stage of a weight-loading wave (kh == 0) / an A-only wave, by the stage's
     // position in its super-block (JQ == 0 stages also carry the header)
     template <int JQ, bool WL>
-    static constexpr int cnt() { return WA + (WL ? F::QI + (JQ == 0 ? F::HI : 0) : 0); }
+    static constexpr int cnt() { return WA + (WL ? GPW * (F::QI + (JQ == 0 ? F::HI : 0)) : 0); }
 };
 
 
@@ -58,12 +62,12 @@ constexpr int q2_cnt_run() {
 }
 
 // DBG (isolation builds, tools/prof_qmm.py --q2dbg): 1 no MFMA, 2 no dequant VALU, 4 no A loads, 8 no weight loads
-template <int QT, int WM, int KS, int WN, int EPI, int DBG = 0, int NS = 4, int NG = 4>
-__global__ __launch_bounds__(NG == 8 ? 512 : 256 * KS) void qmm2_kernel(const uint16_t* __restrict__ A, int lda,
+template <int QT, int WM, int KS, int WN, int EPI, int DBG = 0, int NS = 4, int NG = 4, int GPW = 1>
+__global__ __launch_bounds__(NG == 8 ? 512 / GPW : 256 * KS) void qmm2_kernel(const uint16_t* __restrict__ A, int lda,
                                                         const uint8_t* __restrict__ W, int M, int N, int K,
                                                         int n_mt, int splits, int sbps, void* __restrict__ Cv,
                                                         int ldc, int rot_mul) {
-    using G = Q2Geom<QT, WM, KS, WN, NS, NG>;
+    using G = Q2Geom<QT, WM, KS, WN, NS, NG, GPW>;
     using F = Q2F<QT>;
     constexpr int BM = G::BM, WA = G::WA, STAGE = G::STAGE, A_BYTES = G::A_BYTES;
     static_assert(NS == 4 || NS == 8, "ring depth");
@@ -73,7 +77,7 @@ __global__ __launch_bounds__(NG == 8 ? 512 : 256 * KS) void qmm2_kernel(const ui
     static_assert(G::LDS <= 160 * 1024, "LDS");
     static_assert((NS - 2) * G::template cnt<0, true>() <= 63, "vmcnt range");
     // LDS-DMA instructions per stage as issued (the isolation builds drop some)
-    constexpr int WAI = (DBG & 4) ? 0 : WA, QII = (DBG & 8) ? 0 : F::QI, HII = (DBG & 8) ? 0 : F::HI;
+    constexpr int WAI = (DBG & 4) ? 0 : WA, QII = (DBG & 8) ? 0 : GPW * F::QI, HII = (DBG & 8) ? 0 : GPW * F::HI;
     auto cnt = [](auto jq_c, auto wl_c) constexpr {
         return WAI + (decltype(wl_c)::value ? QII + (decltype(jq_c)::value == 0 ? HII : 0) : 0);
     };
@@ -86,7 +90,7 @@ __global__ __launch_bounds__(NG == 8 ? 512 : 256 * KS) void qmm2_kernel(const ui
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int h = lane >> 5, col = lane & 31;
     // cg: the column group this wave DMAs; (mw, nw): its compute tile = rows mw * 32 WM .., groups nw * WN + j
-    const int cg = wave % NG, kh = NG == 8 ? 0 : wave >> 2;
+    const int cg = wave % NG, kh = NG == 8 ? 0 : wave >> 2;  // (GPW 2: cg = wave, staging groups 2 cg, 2 cg + 1)
     constexpr int NW = NG / WN;
     const int nw = cg % NW, mw = cg / NW;
 
@@ -105,8 +109,9 @@ __global__ __launch_bounds__(NG == 8 ? 512 : 256 * KS) void qmm2_kernel(const ui
     if (sb0 >= sb1) return;
     const int m_base = mt * BM;
     const int ngrp = N >> 5;
-    const int g = min(ct * NG + cg, ngrp - 1);  // groups past N re-read the last (never stored)
+    const int g = min(ct * NG + GPW * cg, ngrp - 1);  // groups past N re-read the last (never stored)
     const uint8_t* wg = W + (size_t)g * ((size_t)nsb * F::UNIT);
+    [[maybe_unused]] const uint8_t* wg2 = W + (size_t)min(ct * NG + GPW * cg + 1, ngrp - 1) * ((size_t)nsb * F::UNIT);
 
     // A LDS-DMA sources: instruction i of this wave fills 8-row block j = wave * WA + i; lane p writes
     // image slot (k-step p >> 4, row (p >> 1) & 7, half (p & 1) ^ (j & 1)) from 16 B of that row
@@ -138,7 +143,11 @@ __global__ __launch_bounds__(NG == 8 ? 512 : 256 * KS) void qmm2_kernel(const ui
                                              16, 0, 0);
         if constexpr (decltype(wl_c)::value && QII > 0) {
             const uint8_t* u = wg + (size_t)sbw * F::UNIT;
-            q2_stage_weights<QT, JQ>(u, sb + A_BYTES + cg * F::QB, hdr_lds + hslot * G::HSZ + cg * F::HB, lane);
+            q2_stage_weights<QT, JQ>(u, sb + A_BYTES + GPW * cg * F::QB, hdr_lds + hslot * G::HSZ + GPW * cg * F::HB,
+                                     lane);
+            if constexpr (GPW == 2)
+                q2_stage_weights<QT, JQ>(wg2 + (size_t)sbw * F::UNIT, sb + A_BYTES + (2 * cg + 1) * F::QB,
+                                         hdr_lds + hslot * G::HSZ + (2 * cg + 1) * F::HB, lane);
         }
     };
 
@@ -373,10 +382,10 @@ __global__ __launch_bounds__(NG == 8 ? 512 : 256 * KS) void qmm2_kernel(const ui
     }
 }
 
-template <int QT, int WM, int KS, int WN, int EPI, int NS = 4, int NG = 4>
+template <int QT, int WM, int KS, int WN, int EPI, int NS = 4, int NG = 4, int GPW = 1>
 static int launch_qmm2(const uint16_t* A, int lda, const uint8_t* W, int M, int N, int K, int splits, void* C, int ldc,
                        hipStream_t st) {
-    using G = Q2Geom<QT, WM, KS, WN, NS, NG>;
+    using G = Q2Geom<QT, WM, KS, WN, NS, NG, GPW>;
     const int nsb = K >> 8;
     splits = max(1, min(splits, nsb));
     const int sbps = (nsb + splits - 1) / splits;
@@ -386,11 +395,11 @@ static int launch_qmm2(const uint16_t* A, int lda, const uint8_t* W, int M, int 
     if (nwg <= 0 || nwg > 0x7fffffff) return (int)hipErrorInvalidValue;
     static bool attr_set = false;
     if (!attr_set) {
-        (void)hipFuncSetAttribute((const void*)qmm2_kernel<QT, WM, KS, WN, EPI, 0, NS, NG>,
+        (void)hipFuncSetAttribute((const void*)qmm2_kernel<QT, WM, KS, WN, EPI, 0, NS, NG, GPW>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS);
         attr_set = true;
     }
-    qmm2_kernel<QT, WM, KS, WN, EPI, 0, NS, NG><<<dim3((unsigned)nwg), 64 * G::NT, G::LDS, st>>>(
+    qmm2_kernel<QT, WM, KS, WN, EPI, 0, NS, NG, GPW><<<dim3((unsigned)nwg), 64 * G::NT, G::LDS, st>>>(
         A, lda, W, M, N, K, n_mt, splits, sbps, C, ldc, g_qmm2_rot);
     MXK_CHECK_LAUNCH();
 }
@@ -422,6 +431,13 @@ static int dispatch_qmm2(int wm, int ks, int wn, const uint16_t* A, int lda, con
         if (wm == WM_ && ks == 17 && wn == WN_)                                                \
             return launch_qmm2<QT, WM_, 1, WN_, EPI, 4, 8>(A, lda, W, M, N, K, splits, C, ldc, st);
     Q2_WIDE(2, 1) Q2_WIDE(4, 1) Q2_WIDE(6, 1) Q2_WIDE(3, 2) Q2_WIDE(7, 1)
+    // ks 18: the 4-wave wide form (each wave 64 columns x 32 wm rows)
+#define Q2_WIDE4(WM_)                                                                          \
+    if constexpr (Q2Geom<QT, WM_, 1, 2, 4, 8, 2>::LDS <= 160 * 1024)                          \
+        if (wm == WM_ && ks == 18 && wn == 2)                                                  \
+            return launch_qmm2<QT, WM_, 1, 2, EPI, 4, 8, 2>(A, lda, W, M, N, K, splits, C, ldc, st);
+    Q2_WIDE4(4) Q2_WIDE4(6) Q2_WIDE4(2)
+#undef Q2_WIDE4
 #undef Q2_WIDE
 #undef Q2_DEEP
 #undef Q2_CASE
@@ -444,6 +460,17 @@ static int launch_dbg(int wm, int ks, int wn, const uint16_t* A, int lda, const 
         return go(qmm2_kernel<QT, 6, 1, 1, EPI, DBG, 4, 8>, 192, 1, Q2Geom<QT, 6, 1, 1, 4, 8>::LDS, 8);
     if (wm == 4 && ks == 17 && wn == 1)
         return go(qmm2_kernel<QT, 4, 1, 1, EPI, DBG, 4, 8>, 128, 1, Q2Geom<QT, 4, 1, 1, 4, 8>::LDS, 8);
+    if (wm == 3 && ks == 17 && wn == 2)
+        return go(qmm2_kernel<QT, 3, 1, 2, EPI, DBG, 4, 8>, 192, 1, Q2Geom<QT, 3, 1, 2, 4, 8>::LDS, 8);
+    if (wm == 6 && ks == 18 && wn == 2) {
+        auto k4 = qmm2_kernel<QT, 6, 1, 2, EPI, DBG, 4, 8, 2>;
+        (void)hipFuncSetAttribute((const void*)k4, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  Q2Geom<QT, 6, 1, 2, 4, 8, 2>::LDS);
+        const int n_ct = (N + 255) / 256, n_mt = (M + 191) / 192;
+        k4<<<dim3(n_ct * n_mt), 256, Q2Geom<QT, 6, 1, 2, 4, 8, 2>::LDS, st>>>(A, lda, W, M, N, K, n_mt, 1, K >> 8, C, ldc,
+                                                                            g_qmm2_rot);
+        return (int)hipGetLastError();
+    }
     if (wm == 8 && ks == 1 && wn == 1) return go(qmm2_kernel<QT, 8, 1, 1, EPI, DBG>, 256, 1, Q2Geom<QT, 8, 1, 1>::LDS);
     if (wm == 4 && ks == 2 && wn == 1) return go(qmm2_kernel<QT, 4, 2, 1, EPI, DBG>, 128, 2, Q2Geom<QT, 4, 2, 1>::LDS);
     if (wm == 4 && ks == 1 && wn == 2) return go(qmm2_kernel<QT, 4, 1, 2, EPI, DBG>, 256, 1, Q2Geom<QT, 4, 1, 2>::LDS);

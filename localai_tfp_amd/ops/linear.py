@@ -511,6 +511,10 @@ QMM2_CONFIGS = ((2, 1, 1), (2, 2, 1), (4, 1, 1), (4, 2, 1), (8, 1, 1), (1, 2, 2)
                 (2, 9, 1), (2, 10, 1), (1, 10, 2),
                 # ks 17: wide tiles, 8 column groups (256 columns) per 8-wave workgroup — half the A staging per flop
                 (2, 17, 1), (4, 17, 1), (6, 17, 1), (3, 17, 2), (7, 17, 1))
+# ks 18: 4-wave wide tiles, each wave 64 columns x 32 wm rows (one wave per SIMD); compiled and tested
+# (test_qmm2[*-18-*]), offered to the tuner with MX_QMM2_WIDE4=1
+if os.environ.get("MX_QMM2_WIDE4", "0") == "1":
+    QMM2_CONFIGS = QMM2_CONFIGS + ((2, 18, 2), (4, 18, 2), (6, 18, 2))
 # every t32 block format runs on qmm2 / qmm3 (qmm2_fmt.h decoders)
 QMM2_QTYPES = (int(QType.Q4_K), int(QType.Q6_K), int(QType.Q3_K), int(QType.Q2_K), int(QType.Q5_K), int(QType.Q8_0),
                int(QType.MX4F), int(QType.MX5F))

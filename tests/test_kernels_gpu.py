@@ -401,14 +401,18 @@ def test_qgemm32(qt, M, wm, wn, splits, monkeypatch):
     (384, 6, 1, 1, 1), (250, 6, 2, 1, 2), (400, 3, 2, 2, 3), (448, 7, 1, 1, 1), (300, 7, 1, 1, 3),
     # ks 17: wide tiles (8 column groups per workgroup; 416 columns = 1.625 tiles)
     (128, 4, 17, 1, 1), (300, 4, 17, 1, 3), (384, 6, 17, 1, 1), (250, 6, 17, 1, 2), (400, 3, 17, 2, 1),
-    (64, 2, 17, 1, 2), (100, 2, 17, 1, 1), (448, 7, 17, 1, 1), (300, 7, 17, 1, 2)])
+    (64, 2, 17, 1, 2), (100, 2, 17, 1, 1), (448, 7, 17, 1, 1), (300, 7, 17, 1, 2),
+    # ks 18: 4-wave wide tiles (2 column groups per wave)
+    (384, 6, 18, 2, 1), (250, 6, 18, 2, 2), (128, 4, 18, 2, 1), (77, 2, 18, 2, 3)])
 def test_qmm2(qt, M, wm, ks, wn, splits, monkeypatch):
     """qmm2.hip for every epilogue and tile / split-K choice, incl. ragged M / N tails (416 columns = 3.25
     workgroup tiles; with wn = 2 a wave's second group may lie past N), split counts that do not divide the
     super-blocks, the 8-wave k-step split (ks = 2) and the 2-group wave tiles (wn = 2), against the fp32
     product of the dequantised weight."""
     from localai_tfp_amd.ops import linear as L
-    if qt == QType.Q8_0 and (32 * wm * wn == 256 or (ks == 17 and 32 * wm * wn >= 192)):
+    if ks == 18 and qt == QType.Q8_0 and wm == 6:
+        pytest.skip("the 192-row wide Q8_0 ring exceeds the LDS (not compiled)")
+    if qt == QType.Q8_0 and ks != 18 and (32 * wm * wn == 256 or (ks == 17 and 32 * wm * wn >= 192)):
         pytest.skip("a 256-row (wide: 192-row) Q8_0 stage ring exceeds the LDS (not compiled)")
     if ks == 17 and wm == 7 and qt not in (QType.Q4_K, QType.Q2_K):
         pytest.skip("the 224-row wide ring fits the LDS for Q4_K / Q2_K only (not compiled)")
