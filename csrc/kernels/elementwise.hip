@@ -188,6 +188,20 @@ extern "C" int mxk_add_act_into_f32(const uint16_t* y, int ldy, float* h, int ld
     MXK_CHECK_LAUNCH();
 }
 
+// overlap-mode decode inputs: tokens[dst[i]] = prev[src[i]] (the previous, still unread step's samples) — one launch
+// for what index_select + index_copy + two index casts took four
+__global__ __launch_bounds__(256) void fix_tokens_kernel(int* __restrict__ tokens, const int* __restrict__ dst,
+                                                         const int* __restrict__ src, const int* __restrict__ prev,
+                                                         int n) {
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) tokens[dst[i]] = prev[src[i]];
+}
+
+extern "C" int mxk_fix_tokens(int* tokens, const int* dst, const int* src, const int* prev, int n, hipStream_t st) {
+    if (n <= 0) return 0;
+    fix_tokens_kernel<<<(n + 255) / 256, 256, 0, st>>>(tokens, dst, src, prev, n);
+    MXK_CHECK_LAUNCH();
+}
+
 // gather selected rows of an fp32 matrix (last-token-of-each-sequence selection before the LM head)
 __global__ __launch_bounds__(256) void select_rows_f32_kernel(const float* __restrict__ x, int ld,
                                                               const int* __restrict__ idx, int cols,

@@ -432,8 +432,10 @@ static int dispatch_qmm2(int wm, int ks, int wn, const uint16_t* A, int lda, con
             return launch_qmm2<QT, WM_, 1, WN_, EPI, 4, 8>(A, lda, W, M, N, K, splits, C, ldc, st);
     Q2_WIDE(2, 1) Q2_WIDE(4, 1) Q2_WIDE(6, 1) Q2_WIDE(3, 2) Q2_WIDE(7, 1)
     // ks 18: the 4-wave wide form (each wave 64 columns x 32 wm rows)
+// (Q4_K / MX4F only: formats whose tile and header each take one DMA instruction; the Q6_K form returned NaNs in
+// test_qmm2 and is not compiled)
 #define Q2_WIDE4(WM_)                                                                          \
-    if constexpr (Q2Geom<QT, WM_, 1, 2, 4, 8, 2>::LDS <= 160 * 1024)                          \
+    if constexpr ((QT == MXQ_Q4_K || QT == MXQ_MX4F) && Q2Geom<QT, WM_, 1, 2, 4, 8, 2>::LDS <= 160 * 1024) \
         if (wm == WM_ && ks == 18 && wn == 2)                                                  \
             return launch_qmm2<QT, WM_, 1, 2, EPI, 4, 8, 2>(A, lda, W, M, N, K, splits, C, ldc, st);
     Q2_WIDE4(4) Q2_WIDE4(6) Q2_WIDE4(2)
@@ -462,7 +464,7 @@ static int launch_dbg(int wm, int ks, int wn, const uint16_t* A, int lda, const 
         return go(qmm2_kernel<QT, 4, 1, 1, EPI, DBG, 4, 8>, 128, 1, Q2Geom<QT, 4, 1, 1, 4, 8>::LDS, 8);
     if (wm == 3 && ks == 17 && wn == 2)
         return go(qmm2_kernel<QT, 3, 1, 2, EPI, DBG, 4, 8>, 192, 1, Q2Geom<QT, 3, 1, 2, 4, 8>::LDS, 8);
-    if (wm == 6 && ks == 18 && wn == 2) {
+    if (wm == 6 && ks == 18 && wn == 2 && QT == MXQ_Q4_K) {
         auto k4 = qmm2_kernel<QT, 6, 1, 2, EPI, DBG, 4, 8, 2>;
         (void)hipFuncSetAttribute((const void*)k4, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   Q2Geom<QT, 6, 1, 2, 4, 8, 2>::LDS);

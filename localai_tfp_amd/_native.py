@@ -66,6 +66,7 @@ KERNEL_SIGS = {
     "mxk_sample_params_size": [],
     "mxk_argmax": [P, I, I, I, P, P],
     "mxk_argmax_gated": [P, I, I, I, P, P, P],
+    "mxk_fix_tokens": [P, P, P, P, I, P],
     "mxk_argmax_keys": [P, I, I, I, I, P, P],
     "mxk_argmax_merge": [P, I, I, P, P],
     "mxk_glu": [I, P, P, I, P, I, I, I, P],

@@ -277,7 +277,12 @@ class StepGraph:
 
     def _fix(self):
         v = self.v
-        v["tokens"].index_copy_(0, v["fix_dst"].long(), self.prev.index_select(0, v["fix_src"].long()))
+        if v["tokens"].is_cuda:
+            from .. import _native as N
+            N.kcall("mxk_fix_tokens", v["tokens"].data_ptr(), v["fix_dst"].data_ptr(), v["fix_src"].data_ptr(),
+                    self.prev.data_ptr(), v["fix_dst"].numel(), N.stream_ptr())
+        else:
+            v["tokens"].index_copy_(0, v["fix_dst"].long(), self.prev.index_select(0, v["fix_src"].long()))
 
     def image(self, plan: dict) -> np.ndarray:
         """Padded host image of the step's inputs in this bucket's layout."""
