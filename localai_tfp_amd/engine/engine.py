@@ -506,9 +506,27 @@ class LLMEngine:
         if self.tp is not None and self.tp.is_leader:
             self.tp.send_plan("capture")  # followers capture the same buckets in the same order
         n = 0
-        for b in self.cfg.graph_buckets:
-            if b <= self.cfg.max_num_seqs and self._graph_for(b) is not None:  # decode-only buckets
+        c = self.cfg
+        for b in c.graph_buckets:
+            if b <= c.max_num_seqs and self._graph_for(b) is not None:  # decode-only buckets
                 n += 1
+        # the full-batch steps of a saturated server: the single-partition decode form and every mixed (decode + prompt
+        # chunk) bucket the step budget allows, so no capture (~10-50 ms) stalls serving or lands in a timed window
+        top = max((b for b in c.graph_buckets if b <= c.max_num_seqs), default=0)
+        if top and not self.recurrent and hasattr(self.model, "prefill_rows") and \
+                os.environ.get("MX_PRECAPTURE_MIXED", "1") == "1":
+            keys = [(top, 0, 0, self.SINGLE_PART_CTX)] if top >= self.SINGLE_PART_B else []
+            for p in c.mixed_graph_tokens:
+                if p > c.max_batched_tokens or top + p > self.ws.max_tokens:
+                    continue
+                keys.append((top, p, c.mixed_graph_seqs, 0))
+                if top >= self.SINGLE_PART_B:
+                    keys.append((top, p, c.mixed_graph_seqs, self.SINGLE_PART_CTX))
+            for k in keys:
+                if len(self.graphs) >= c.max_graphs:
+                    break
+                if self._graph_get(k) is not None:
+                    n += 1
         gc_tune()
         return n
 
