@@ -513,7 +513,8 @@ class LLMEngine:
         # the full-batch steps of a saturated server: the single-partition decode form and every mixed (decode + prompt
         # chunk) bucket the step budget allows, so no capture (~10-50 ms) stalls serving or lands in a timed window
         top = max((b for b in c.graph_buckets if b <= c.max_num_seqs), default=0)
-        if top and not self.recurrent and hasattr(self.model, "prefill_rows") and \
+        # (single-rank engines only: tensor-parallel ranks keep to the decode buckets they have always shared)
+        if top and self.tp is None and not self.recurrent and hasattr(self.model, "prefill_rows") and \
                 os.environ.get("MX_PRECAPTURE_MIXED", "1") == "1":
             keys = [(top, 0, 0, self.SINGLE_PART_CTX)] if top >= self.SINGLE_PART_B else []
             for p in c.mixed_graph_tokens:
