@@ -19,6 +19,7 @@ void* mxrt_bm_new(int num_blocks, int block_size, int prefix_cache) {
     return new BM(num_blocks, block_size, prefix_cache != 0);
 }
 void mxrt_bm_free(void* h) { delete (BM*)h; }
+void mxrt_bm_set_lifo(void* h, int on) { ((BM*)h)->lifo = on != 0; }
 int mxrt_bm_num_free(void* h) { return ((BM*)h)->num_free(); }
 
 // allocate n blocks into out; returns 0 on success, -1 if not enough (nothing allocated)

@@ -45,6 +45,9 @@ struct BM {
     std::vector<std::list<int32_t>::iterator> lru_it;
     std::vector<uint8_t> in_lru;
     int64_t hits = 0, queries = 0;
+    // LIFO reuse: a released block is handed out again first, so the live KV working set stays in a compact range of
+    // the pool (fewer distinct pages for the attention kernels' TLBs) instead of drifting through it
+    bool lifo = false;
 
     BM(int nb, int bs, bool pc) : num_blocks(nb), block_size(bs), prefix(pc), ref(nb, 0), hash_of(nb),
                                    has_hash(nb, 0), toks_of(nb), lru_it(nb), in_lru(nb, 0) {
@@ -110,7 +113,8 @@ struct BM {
                 } else {
                     has_hash[b] = 0;
                     toks_of[b].clear();
-                    free_list.push_back(b);
+                    if (lifo) free_list.push_front(b);
+                    else free_list.push_back(b);
                 }
             }
         }

@@ -23,6 +23,7 @@ RT_SIGS = {
     # block_manager.cpp
     "mxrt_bm_new": (P, [I, I, I]),
     "mxrt_bm_free": (None, [P]),
+    "mxrt_bm_set_lifo": (None, [P, I]),
     "mxrt_bm_num_free": (I, [P]),
     "mxrt_bm_allocate": (I, [P, I, P]),
     "mxrt_bm_release": (None, [P, P, I]),

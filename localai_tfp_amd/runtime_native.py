@@ -25,6 +25,8 @@ class NativeBlockManager:
         self.num_blocks, self.block_size = num_blocks, block_size
         self.enable_prefix_cache = enable_prefix_cache
         self._h = _rt().mxrt_bm_new(num_blocks, block_size, int(enable_prefix_cache))
+        if os.environ.get("MX_KV_LIFO", "0") == "1":  # A/B: reuse released blocks first (KV locality)
+            _rt().mxrt_bm_set_lifo(self._h, 1)
 
     def __del__(self):
         try:
