@@ -69,7 +69,7 @@ def parse():
                     help="paged KV cache element type (llama.cpp cache_type_k/v); fp8 = e4m3")
     ap.add_argument("--profile-steps", type=int, default=0)
     ap.add_argument("--steady-finished", type=int, default=-1,
-                    help="completed requests before the warmup count starts (-1: concurrency/2)")
+                    help="completed requests before the warmup count starts (-1: 2 x concurrency)")
     ap.add_argument("--timeout", type=float, default=900.0, help="abort if the window is not reached")
     ap.add_argument("--tp", type=int, default=1,
                     help="tensor-parallel ranks per serving replica (BASELINE config #3: --model llama3-70b "
@@ -414,7 +414,11 @@ class Window:
 
 def steady_gate(args) -> int:
     """Completed requests after which the serving mix is stationary (see Window)."""
-    return args.steady_finished if args.steady_finished >= 0 else max(1, args.concurrency // 2)
+    # two full generations of the concurrency: every request that was running at the load's start has been replaced
+    # and the replacements' ages are spread evenly, so a small driver W no longer times the ramp (with the round-4
+    # gate of half a generation, the phase after a first one ran 2-3 % faster than that first phase on the same box;
+    # with W = 800 the two agreed — profiles/r5_step_composition.md)
+    return args.steady_finished if args.steady_finished >= 0 else max(1, 2 * args.concurrency)
 
 
 def run_http(args, eng, tok, cfg, dev, dist):
