@@ -163,3 +163,60 @@ def test_grammar_mask_batch_matches_rows():
             allowed = np.flatnonzero(np.unpackbits(out[i].view(np.uint8), bitorder="little")[:V])
             if len(allowed):
                 assert m.accept(int(rng.choice(allowed)))
+
+
+def _mask_rows_ok(ms, V, steps, seed):
+    from localai_tfp_amd.runtime_native import GrammarMatcher
+    rng = np.random.default_rng(seed)
+    W = (V + 31) // 32
+    for _ in range(steps):
+        out = np.zeros((len(ms), W), np.uint32)
+        GrammarMatcher.masks_into(ms, out, list(range(len(ms))))
+        for i, m in enumerate(ms):
+            if not (out[i] == m.allowed_mask(V)).all():
+                return False
+            allowed = np.flatnonzero(np.unpackbits(out[i].view(np.uint8), bitorder="little")[:V])
+            if len(allowed):
+                m.accept(int(rng.choice(allowed)))
+    return True
+
+
+def _fork_child(q):
+    from localai_tfp_amd import functions as F
+    from localai_tfp_amd.runtime_native import GrammarMatcher, NativeGrammar, NativeVocab
+    tb = [bytes([i]) for i in range(256)] + [b'{"', b'":', b"true", b", "]
+    g = NativeGrammar(F.JSON_BNF)
+    vocab = NativeVocab(tb)
+    q.put(_mask_rows_ok([GrammarMatcher(g, vocab, tb, -1) for _ in range(6)], len(tb), 5, 1))
+
+
+def test_grammar_mask_pool_concurrent_callers_and_fork():
+    """The batched mask runs on a persistent worker pool (csrc/runtime/grammar.cpp MaskPool): concurrent callers are
+    serialised, grammars freed between calls do not leak stale transition tables into later grammars, and a forked
+    child (whose parent's workers do not exist) builds its own pool."""
+    import multiprocessing as mp
+    import threading
+    from localai_tfp_amd import functions as F
+    from localai_tfp_amd.runtime_native import GrammarMatcher, NativeGrammar, NativeVocab
+    tb = [bytes([i]) for i in range(256)] + [b"{", b"}", b'"', b'":', b", ", b"true", b"12", b" "]
+    V = len(tb)
+    vocab = NativeVocab(tb)
+    res = []
+
+    def caller(seed):
+        for k in range(4):  # a fresh grammar (new serial) each round, the old one freed
+            g = NativeGrammar(F.JSON_BNF)
+            res.append(_mask_rows_ok([GrammarMatcher(g, vocab, tb, -1) for _ in range(8)], V, 6, seed + k))
+
+    ths = [threading.Thread(target=caller, args=(s,)) for s in (10, 20, 30)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join(timeout=120)
+    assert len(res) == 12 and all(res)
+    ctx = mp.get_context("fork")
+    q = ctx.Queue()
+    p = ctx.Process(target=_fork_child, args=(q,))
+    p.start()
+    p.join(timeout=120)
+    assert p.exitcode == 0 and q.get(timeout=5) is True
