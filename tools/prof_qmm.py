@@ -11,7 +11,7 @@ import numpy as np
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-SHAPES = {"qkv": (6144, 4096, 12, 0), "wo": (4096, 4096, 12, 2), "gate_up": (28672, 4096, 12, 3),
+SHAPES = {"qkv": (6144, 4096, 12, 0), "wo": (4096, 4096, 12, 2), "gate_up": (28672, 4096, 12, 3), "gate_up_f32": (28672, 4096, 12, 2),
           "down": (4096, 14336, 12, 2), "down_q6": (4096, 14336, 14, 2), "lm_head": (128256, 4096, 14, 0)}
 
 
