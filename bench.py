@@ -15,11 +15,17 @@ Each rank:
     (tools/loadgen.py) in another child: `--concurrency` users streaming chat completions
     (prompt `--prompt-len` tokens after the Llama-3 chat template, `--gen-len` tokens, ignore_eos);
   * (`--path engine`) drives the engine directly in-process (kernel/scheduler-only number).
-A "step" is one engine iteration (continuous batching: decode rows + chunked prefill). The engine
-thread itself brackets the window: at step W it does device sync + barrier and records t0, at step
-W+K again sync + barrier and t1, so exactly K steps are timed on every rank. Output tokens = tokens
-the engine generated for HTTP requests inside the window; TTFT = client-side time from sending the
-request to the first content chunk, over requests whose first token arrived inside the window.
+A bench "step" is a fixed group of G = --step-group (default 16) engine iterations (one engine iteration =
+one continuous-batching forward: every running sequence's decode row + chunked prefill of arriving prompts).
+One engine iteration at c128 takes ~5-11 ms and a 256-token generation takes 256 of them, so a 20-iteration
+window sees either no prefill at all or a burst of it (VERDICT r5 Weak #1); 20 grouped steps = 320 iterations
+cover more than one full generation, i.e. the stationary mix of decode rows, prompt chunks and completions.
+The engine thread itself brackets the window: after W*G iterations of the steady state it does device sync +
+barrier and records t0, after K*G more again sync + barrier and t1, so exactly K steps (K*G iterations) are timed
+on every rank. Output tokens = tokens the engine generated inside the window; TTFT = client-side time from
+sending the request to the first content chunk, over requests whose first token arrived inside the window.
+The JSON reports the window's engine iterations, prompt (prefill) tokens, output tokens and TTFT sample count;
+rank 0 exits non-zero when fewer than 32 TTFT samples fell in the window (a window that timed no prefill).
 value = sum over ranks of tokens / max over ranks of window. Rank 0 prints one JSON line.
 """
 from __future__ import annotations
@@ -47,8 +53,12 @@ TEMPLATE_OVERHEAD = 24  # Llama-3 chat template tokens around one user message (
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=400)
-    ap.add_argument("--warmup", type=int, default=200)
+    ap.add_argument("--steps", type=int, default=25, help="timed bench steps (each = --step-group engine iterations)")
+    ap.add_argument("--warmup", type=int, default=10, help="untimed bench steps after the steady-state gate")
+    ap.add_argument("--step-group", type=int, default=16,
+                    help="engine iterations per bench step (G): K steps time K*G continuous-batching iterations")
+    ap.add_argument("--min-ttft-samples", type=int, default=32,
+                    help="rank 0 exits non-zero if fewer TTFT samples fall in the window (0: no check)")
     ap.add_argument("--model", default="llama3-8b", choices=["llama3-8b", "llama3-70b", "llama32-1b"])
     ap.add_argument("--path", default="http", choices=["http", "engine"])
     ap.add_argument("--ftype", default="Q4_K_M", choices=["Q4_K_M", "Q3_K_M"],
@@ -223,8 +233,11 @@ def main():
     from localai_tfp_amd.tokenizer import ByteTokenizer
 
     cfg = {"llama3-8b": C.LLAMA3_8B, "llama3-70b": C.LLAMA3_70B, "llama32-1b": C.LLAMA32_1B}[args.model]
-    if dev.type == "cpu":  # plumbing only (row-parallel shards need whole 256-wide super-blocks: tp <= 2)
-        cfg = C.tiny_config(hidden=512, ffn=1024, n_heads=8, n_kv_heads=2)
+    if dev.type == "cpu":  # plumbing only (row-parallel shards need whole 256-wide super-blocks)
+        if args.tp > 2:  # 8-way row-parallel shards (config #3's layout: 1 KV head per rank at tp 8)
+            cfg = C.tiny_config(hidden=2048, ffn=4096, n_heads=16, n_kv_heads=8, head_dim=128, rope_dim=128)
+        else:
+            cfg = C.tiny_config(hidden=512, ffn=1024, n_heads=8, n_kv_heads=2)
     tp, link, tp_group, dp = args.tp, None, None, world
     tp_rel = None
     rehearsal = args.tp_rehearsal
@@ -277,13 +290,15 @@ def main():
         res = run_engine(args, eng, tok, dev, dist)
         eng.shutdown()  # tensor parallel: releases the followers from engine.follow()
     t_el, tokens, ttfts, extra = res[0]
+    bad_window = False
     phase_extra = {}
     for ph, (t2, tok2, tt2, ex2) in zip(args.phases.split(",")[1:], res[1:]):
         phase_extra[ph] = {"value": round(tok2 / t2, 2) if t2 else None,
                            "p50_ttft_ms": round(float(np.percentile(tt2, 50)), 2) if len(tt2) else None,
                            "p99_ttft_ms": round(float(np.percentile(tt2, 99)), 2) if len(tt2) else None,
                            "ms_per_step": round(t2 / args.steps * 1e3, 3), **{k: ex2[k] for k in (
-                               "client_completed_requests", "ttft_samples", "p50_itl_ms") if k in ex2}}
+                               "client_completed_requests", "ttft_samples", "p50_itl_ms", "window_engine_steps",
+                               "window_prompt_tokens", "window_output_tokens") if k in ex2}}
 
     p50 = float(np.percentile(ttfts, 50)) if len(ttfts) else float("nan")
     p99 = float(np.percentile(ttfts, 99)) if len(ttfts) else float("nan")
@@ -313,6 +328,8 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(t_max / args.steps * 1e3, 3),
+            "step_unit": f"{args.step_group} engine iterations (continuous-batching forwards)",
+            "ms_per_engine_iteration": round(t_max / (args.steps * args.step_group) * 1e3, 3),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -351,9 +368,14 @@ def main():
             },
         }
         print(json.dumps(out), flush=True)
+        n_tt = extra.get("ttft_samples")
+        if args.min_ttft_samples and n_tt is not None and n_tt < args.min_ttft_samples and not rehearsal:
+            print(f"[bench] only {n_tt} TTFT samples fell in the timed window (< {args.min_ttft_samples}): the window "
+                  "did not time a representative serving mix", file=sys.stderr, flush=True)
+            bad_window = True
         if eng.trace is not None:
             torch.cuda.synchronize() if dev.type == "cuda" else None
-            ev = eng.trace_events[-(args.steps + 50):]
+            ev = eng.trace_events[-(args.steps * args.step_group + 50):]
             # device time of each step (launch marker -> sampler end) and the device idle before the next one
             gpu = [[a.elapsed_time(b), b.elapsed_time(c)] for (a, b), (c, _) in zip(ev, ev[1:])]
             with open(os.environ["MX_STEP_TRACE"], "w") as f:
@@ -367,6 +389,8 @@ def main():
     if world > 1:
         import torch.distributed as tdist
         tdist.destroy_process_group()
+    if bad_window:
+        sys.exit(3)
 
 
 class Window:
@@ -381,7 +405,9 @@ class Window:
     """
 
     def __init__(self, eng, warmup, steps, dev, dist, steady_finished: int, base_finished: int = 0):
+        # warmup / steps are ENGINE ITERATIONS here (the caller multiplies bench steps by the step group)
         self.eng, self.W, self.K, self.dev, self.dist = eng, warmup, steps, dev, dist
+        self.pre0 = self.pre1 = 0
         self.steady_finished = steady_finished + base_finished
         self.steady_step = None
         self.t0 = self.t1 = None
@@ -404,11 +430,13 @@ class Window:
             self._sync()
             self.t0 = time.monotonic()
             self.tok0 = self.eng.stats["out_tokens"]
+            self.pre0 = self.eng.stats["prefill_tokens"]
             self.step0 = i
         elif j == self.W + self.K and self.t1 is None:
             self._sync()
             self.t1 = time.monotonic()
             self.tok1 = self.eng.stats["out_tokens"]
+            self.pre1 = self.eng.stats["prefill_tokens"]
             self.done.set()
 
 
@@ -486,7 +514,7 @@ def run_http(args, eng, tok, cfg, dev, dist):
                 samp_args += ["--frequency-penalty", str(sp["frequency_penalty"])]
             if sp.get("json"):
                 samp_args += ["--json"]
-            win = Window(eng, args.warmup, args.steps, dev, dist, steady_gate(args),
+            win = Window(eng, args.warmup * args.step_group, args.steps * args.step_group, dev, dist, steady_gate(args),
                          base_finished=eng.stats["finished"])
             eng.on_step = win
             rec_paths = [os.path.join(work, f"loadgen_{pi}_{i}.json") for i in range(n_lg)] if front else []
@@ -552,8 +580,10 @@ def _http_phase_result(win, rec_paths):
     done = [r for r in recs if r.get("ok") and t0 <= r["t_end"] <= t1]
     client_tps = sum(r["tokens"] for r in done) / (t1 - t0) if done else 0.0
     errors = sum(1 for r in recs if r.get("error") not in (None, "CancelledError"))
+    window = {"window_engine_steps": win.K, "window_prompt_tokens": win.pre1 - win.pre0,
+              "window_output_tokens": win.tok1 - win.tok0}
     if not recs:  # a rank behind the single DP gateway: its engine's tokens count, the client side is rank 0's
-        return t1 - t0, win.tok1 - win.tok0, [], {"steady_at_step": win.steady_step}
+        return t1 - t0, win.tok1 - win.tok0, [], {"steady_at_step": win.steady_step, **window}
     # inter-token latency: gaps between consecutive content chunks of one stream, both inside the window
     itl = [(b - a) * 1e3 for r in recs for a, b in zip(r.get("t_chunks", []), r.get("t_chunks", [])[1:])
            if t0 <= a and b <= t1]
@@ -563,7 +593,7 @@ def _http_phase_result(win, rec_paths):
              "http_errors": errors, "ttft_samples": len(ttfts),
              "p50_itl_ms": round(float(np.percentile(itl, 50)), 2) if itl else None,
              "p99_itl_ms": round(float(np.percentile(itl, 99)), 2) if itl else None,
-             "steady_at_step": win.steady_step, "window_first_step": getattr(win, "step0", None)}
+             "steady_at_step": win.steady_step, "window_first_step": getattr(win, "step0", None), **window}
     return t1 - t0, win.tok1 - win.tok0, ttfts, extra
 
 
@@ -628,7 +658,8 @@ def run_engine(args, eng, tok, dev, dist):
     while eng.stats["finished"] < gate and n_pre < 100000:
         step()
         n_pre += 1
-    for _ in range(args.warmup):
+    G = args.step_group
+    for _ in range(args.warmup * G):
         step()
     if dev.type == "cuda":
         torch.cuda.synchronize()
@@ -636,17 +667,20 @@ def run_engine(args, eng, tok, dev, dist):
         dist.barrier()
     timed["on"] = True
     tok0 = eng.stats["out_tokens"]
+    pre0 = eng.stats["prefill_tokens"]
     s0 = _host_snapshot(eng)
     t_start = time.monotonic()
-    for _ in range(args.steps):
+    for _ in range(args.steps * G):
         step()
     if dev.type == "cuda":
         torch.cuda.synchronize()
     if dist:
         dist.barrier()
     t_el = time.monotonic() - t_start
-    return [(t_el, eng.stats["out_tokens"] - tok0, ttfts, {"steady_at_step": n_pre,
-                                                          "window_host": _host_delta(s0, _host_snapshot(eng))})]
+    return [(t_el, eng.stats["out_tokens"] - tok0, ttfts, {
+        "steady_at_step": n_pre, "window_host": _host_delta(s0, _host_snapshot(eng)), "ttft_samples": len(ttfts),
+        "window_engine_steps": args.steps * G, "window_prompt_tokens": eng.stats["prefill_tokens"] - pre0,
+        "window_output_tokens": eng.stats["out_tokens"] - tok0})]
 
 
 def _host_snapshot(eng):

@@ -572,14 +572,24 @@ class LLMEngine:
                 self.step()
             except Exception as ex:  # fail every in-flight request loudly, keep the worker alive
                 log.exception("engine step failed")
-                self._inflight, self._prev_dev = collections.deque(), None
-                if self.native_sched:
-                    self.sched.clear_prev()
-                for s in list(self.sched.running) + list(self.sched.waiting):
-                    s.n_pending = 0
-                    self.sched.abort(s.rid)
-                    self._finish(s, f"error:{type(ex).__name__}: {ex}")
+                self._fail_step(ex)
             self.flush_outputs()
+
+    def _fail_step(self, ex: Exception):
+        """A step raised: drop the in-flight steps, finish every live request with the error, free all blocks."""
+        self._inflight, self._prev_dev = collections.deque(), None
+        if self.native_sched:
+            self.sched.clear_prev()
+        for s in list(self.sched.running) + list(self.sched.waiting):
+            s.n_pending = 0
+            self.sched.abort(s.rid)
+            self._finish(s, f"error:{type(ex).__name__}: {ex}")
+        # finished / aborted sequences still waiting on the dropped in-flight samples: nothing will read those
+        # back now, so free their KV blocks (and native slots) here (ADVICE r5)
+        for s in list(self.sched.deferred):
+            s.n_pending = 0
+        if self.sched.deferred:
+            self.sched.release_deferred()
 
     def run_until_done(self, max_steps: int = 1 << 30):
         """Synchronous driver (tests / bench): step until every submitted request finished."""

@@ -147,14 +147,14 @@ class Sequence:
         if self._pending_ids:
             self._pending_ids.pop()
 
-    def _decode_new(self) -> str:
+    def _decode_new(self, final: bool = False) -> str:
         sb = getattr(self.tok, "stream_bytes", None)
         if sb is not None:
             return self._decode_bytes(sb())
         ids = self.output_ids
         prefix = self.tok.decode(ids[self._prefix_off:self._read_off])
         full = self.tok.decode(ids[self._prefix_off:])
-        if full.endswith("�"):
+        if full.endswith("�") and not final:
             return ""  # incomplete UTF-8 sequence: hold back (grpc-server.cpp:1069-1190 partial check)
         new = full[len(prefix):]
         self._prefix_off = max(0, len(ids) - 6) if len(ids) > 6 else self._prefix_off
@@ -179,7 +179,10 @@ class Sequence:
 
     def flush_text(self, final: bool = False) -> tuple[str, bool]:
         """Returns (text to emit, stop_string_hit)."""
-        self._held += self._decode_new()
+        self._held += self._decode_new(final)
+        if final and self._pbytes:  # a generation cut mid-character: emit the partial bytes as U+FFFD (ADVICE r5)
+            self._held += self._pbytes.decode("utf-8", errors="replace")
+            self._pbytes = b""
         stops = [s for s in self.req.stop if s]
         for s in stops:
             i = self._held.find(s)

@@ -90,6 +90,8 @@ def tune_weight(W, epi: int, can_split: bool, buckets=BUCKETS, iters: int = 8) -
     x = (torch.randn(Mmax, W.K, device=dev) * 0.5).to(torch.float16)
     if epi in L.GLU_EPIS:
         out = torch.empty(Mmax, W.N // 2, device=dev, dtype=torch.float16)
+    elif epi == L.EPI_BF16:  # 16-bit activation out: the plan runner requires out.dtype == x.dtype
+        out = torch.empty(Mmax, W.N, device=dev, dtype=x.dtype)
     else:
         out = torch.zeros(Mmax, W.N, device=dev, dtype=torch.float32)
     res = []
@@ -201,7 +203,10 @@ def tune_gemms(specs, buckets=BUCKETS) -> float:
             TUNED[key] = [(b, tuple(p)) for b, p in cache[ck]]
             continue
         res = tune_weight(W, epi, can_split, buckets)
-        new[ck] = [(b, list(p)) for b, p in res]
+        if res:  # an empty result (every candidate refused) is not cached: the next load tunes it again
+            new[ck] = [(b, list(p)) for b, p in res]
+        else:
+            log.warning("gemm autotune: no plan ran for %s; the untuned fallback rule serves it", key)
     if new:
         save_cache(new)
     dt = time.time() - t0

@@ -158,6 +158,9 @@ class LoadedModel:
             r.stop(force)
 
 
+from .shared_backends import ActivityReporter  # noqa: E402
+
+
 class WatchDog:
     """Kills backends busy for longer than busy_timeout or idle for longer than idle_timeout."""
 
@@ -198,6 +201,7 @@ class WatchDog:
     def check_once(self, now: float | None = None) -> list[str]:
         now = now or time.time()
         victims = set()
+        shared = getattr(self.loader, "shared", None)
         with self._lock:
             if self.busy_check:
                 for a, t in self.busy_since.items():
@@ -206,7 +210,15 @@ class WatchDog:
                         victims.add(self.addr_model.get(a))
             if self.idle_check:
                 for a, t in self.last_used.items():
-                    if a not in self.busy_since and now - t > self.idle_timeout:
+                    if a in self.busy_since:
+                        continue
+                    if shared is not None and now - t > self.idle_timeout:
+                        # sibling gateway processes serve this replica too: their use counts
+                        s_last, s_busy = shared.activity(a)
+                        if s_busy:
+                            continue
+                        t = max(t, s_last)
+                    if now - t > self.idle_timeout:
                         log.warning("watchdog: %s idle for %.0fs, killing", a, now - t)
                         victims.add(self.addr_model.get(a))
         victims.discard(None)
@@ -277,6 +289,8 @@ class ModelLoader:
         if reg:
             from .shared_backends import SharedBackends
             self.shared = SharedBackends(reg)
+            if getattr(app, "watchdog_idle", False):
+                log.info("watchdog: idle checks of shared replicas include the sibling gateway processes' activity")
         self.watchdog: WatchDog | None = None
         if getattr(app, "watchdog_busy", False) or getattr(app, "watchdog_idle", False):
             self.watchdog = WatchDog(self, app.watchdog_busy_timeout_s, app.watchdog_idle_timeout_s,
@@ -345,7 +359,8 @@ class ModelLoader:
         parallel = bool(getattr(self.app, "parallel_backend_requests", True))
         reps = []
         for r in e["replicas"]:
-            rep_ = Replica(r["address"], BackendClient(r["address"], parallel=parallel))
+            rep_ = Replica(r["address"], BackendClient(r["address"], parallel=parallel,
+                                                       watchdog=ActivityReporter(self.shared)))
             rep_.mx_path = r["mx_path"] if r["mx_path"] and os.path.exists(r["mx_path"]) else ""
             reps.append(rep_)
         m = LoadedModel(name, e["backend"], reps)

@@ -15,6 +15,11 @@ spawning their own (which would load every model N times):
 
 Entries are JSON files updated under an fcntl lock per model, so concurrent first requests in two processes still
 spawn the model once.
+
+Watchdog activity: only the owner runs the WatchDog, but SO_REUSEPORT hands most connections to the
+siblings. Every attached process therefore reports its use of each replica address in a small per-process
+activity file ({last use, requests in flight}, rewritten when the in-flight count changes and at most once a
+second otherwise); the owner's idle / busy checks fold the live siblings' activity into its own before killing.
 """
 from __future__ import annotations
 
@@ -87,6 +92,72 @@ class SharedBackends:
                 with contextlib.suppress(OSError):
                     os.unlink(self._path(name))
 
+    # ---------------------------------------------------------------- watchdog activity of attached processes
+    def _act_path(self, address: str, pid: int | None = None) -> str:
+        h = hashlib.sha1(address.encode()).hexdigest()[:20]
+        return os.path.join(self.root, f"{h}.act.{pid if pid is not None else self.pid}")
+
+    def report(self, address: str, last: float, busy: int):
+        p = self._act_path(address)
+        tmp = p + ".tmp"
+        with open(tmp, "w") as f:
+            json.dump({"last": last, "busy": busy}, f)
+        os.replace(tmp, p)
+
+    def activity(self, address: str) -> tuple[float, bool]:
+        """(latest use, any request in flight) of `address` over the live attached processes (not this one)."""
+        prefix = os.path.basename(self._act_path(address, 0))[:-1]
+        last, busy = 0.0, False
+        try:
+            names = os.listdir(self.root)
+        except OSError:
+            return last, busy
+        for n in names:
+            if not n.startswith(prefix) or n.endswith(".tmp"):
+                continue
+            try:
+                pid = int(n[len(prefix):])
+            except ValueError:
+                continue
+            if pid == self.pid or not _alive(pid):
+                continue
+            try:
+                with open(os.path.join(self.root, n)) as f:
+                    a = json.load(f)
+            except (OSError, ValueError):
+                continue
+            last = max(last, float(a.get("last", 0.0)))
+            busy = busy or int(a.get("busy", 0)) > 0
+        return last, busy
+
     @staticmethod
     def same(a: dict | None, b: dict | None) -> bool:
         return bool(a and b and a["owner"] == b["owner"] and a["replicas"] == b["replicas"])
+
+
+class ActivityReporter:
+    """Watchdog stand-in for a client of an ATTACHED replica: mark / unmark report this process's use of the
+    address to the owner through SharedBackends.report (the owner's WatchDog reads it)."""
+
+    def __init__(self, shared: SharedBackends, min_interval: float = 1.0):
+        self.shared, self.min_interval = shared, min_interval
+        self._busy: dict[str, int] = {}
+        self._sent: dict[str, float] = {}
+
+    def _send(self, address: str, force: bool):
+        now = time.time()
+        if force or now - self._sent.get(address, 0.0) >= self.min_interval:
+            self._sent[address] = now
+            try:
+                self.shared.report(address, now, self._busy.get(address, 0))
+            except OSError:
+                pass
+
+    def mark(self, address: str):
+        n = self._busy.get(address, 0)
+        self._busy[address] = n + 1
+        self._send(address, force=n == 0)
+
+    def unmark(self, address: str):
+        self._busy[address] = 0
+        self._send(address, force=True)

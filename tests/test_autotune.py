@@ -32,7 +32,7 @@ def test_candidates_respect_split_and_rows():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("epi", [L.EPI_F32, L.EPI_ADD_F32, L.EPI_SWIGLU])
+@pytest.mark.parametrize("epi", [L.EPI_F32, L.EPI_ADD_F32, L.EPI_SWIGLU, L.EPI_BF16])
 def test_tuned_plans_match_reference(epi, tmp_path, monkeypatch):
     from localai_tfp_amd.ops.quant import random_quantized
     monkeypatch.setenv("MX_TUNE_CACHE", str(tmp_path / "tune.json"))
@@ -42,7 +42,7 @@ def test_tuned_plans_match_reference(epi, tmp_path, monkeypatch):
     W = L.QWeight.from_ggml(raw, int(QType.Q4_K), N, K, dev)
     assert W.to_t32()
     dense = W.dequant_gpu(torch.float16).float()
-    can_split = epi != L.EPI_SWIGLU
+    can_split = epi not in (L.EPI_SWIGLU, L.EPI_BF16)
     buckets = (64, 128, 192, 320)
     res = AT.tune_weight(W, epi, can_split, buckets, iters=2)
     assert [b for b, _ in res] == list(buckets)
@@ -52,6 +52,7 @@ def test_tuned_plans_match_reference(epi, tmp_path, monkeypatch):
         ref = y if epi != L.EPI_SWIGLU else (lambda v: torch.nn.functional.silu(v[:, :, 0]) * v[:, :, 1])(
             y.reshape(M, N // 32, 2, 16)).reshape(M, N // 2)
         out = torch.zeros(M, N // 2, device=dev, dtype=torch.float16) if epi == L.EPI_SWIGLU else \
+            torch.zeros(M, N, device=dev, dtype=torch.float16) if epi == L.EPI_BF16 else \
             torch.zeros(M, N, device=dev, dtype=torch.float32)
         L.qmatmul(W, x, epi, out, out_zeroed=True)
         torch.cuda.synchronize()

@@ -33,3 +33,24 @@ def test_stream_matches_full_decode():
             out.append(seq._decode_new())
     assert "".join(out) == tok.decode(ids) == text
     assert rng is not None
+
+
+def test_final_flush_emits_partial_character():
+    """a generation that stops (max_tokens) in the middle of a multi-byte character must not silently
+    drop the held bytes — the final flush emits them as U+FFFD, like a full decode with errors='replace'."""
+    from localai_tfp_amd.tokenizer import ByteTokenizer
+    from localai_tfp_amd.tokenizer.synth_bpe import llama3_like_tokenizer
+    for tok in (ByteTokenizer(512), llama3_like_tokenizer()):  # decode-based and byte-table streaming
+        seq = Sequence(Request(prompt_ids=[1, 2, 3]), tok)
+        raw = "ab日".encode()[:-1]  # cut inside the 3-byte character
+        if hasattr(tok, "stream_bytes"):  # the vocabulary's single-byte tokens
+            table = tok.stream_bytes()
+            ids = [table.index(bytes([b])) for b in raw]
+        else:
+            ids = list(raw)
+        for t in ids:
+            seq.append_token(t, None)
+        text, stop = seq.flush_text(final=False)
+        tail, stop2 = seq.flush_text(final=True)
+        assert not stop and not stop2
+        assert text + tail == "ab\ufffd" and seq.emitted_text == "ab\ufffd", (type(tok).__name__, text, tail)

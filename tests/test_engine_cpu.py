@@ -271,3 +271,27 @@ def test_overlap_abort_mid_flight(model):
     assert outs1[-1].finished and outs1[-1].finish_reason == "abort"
     assert e.bm.num_free == free0 or e.cfg.enable_prefix_cache  # cached blocks may stay resident
     assert not e.sched.deferred and not e._inflight
+
+
+@pytest.mark.parametrize("native", [False, True])
+def test_step_failure_frees_deferred(model, native, monkeypatch):
+    """a step that raises while a finished sequence is deferred (its blocks still awaited by an
+    in-flight step) must free those blocks — the in-flight results are dropped and will never be read back."""
+    monkeypatch.setenv("MX_PY_SCHED", "0" if native else "1")
+    e, tok = mk(model, overlap=True, overlap_depth=3, enable_prefix_cache=False)
+    assert e.native_sched == native or not native
+    free0 = e.bm.num_free
+    r1 = Request(list(range(20, 60)), SamplingParams(temperature=0.0), max_tokens=40)
+    r2 = Request(list(range(70, 90)), SamplingParams(temperature=0.0), max_tokens=40)
+    e.submit(r1), e.submit(r2)
+    e._drain_inbox()
+    for _ in range(4):
+        e.step()
+    e.abort(r2.rid)
+    e._drain_inbox()
+    e.step()  # r2 leaves the running set with samples still in flight -> deferred
+    assert e.sched.deferred and e._inflight
+    e._fail_step(RuntimeError("injected"))
+    assert not e.sched.deferred and not e._inflight
+    assert not e.sched.running and not e.sched.waiting
+    assert e.bm.num_free == free0

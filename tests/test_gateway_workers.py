@@ -40,3 +40,41 @@ def test_gateway_workers_share_replicas():
                   gateway_workers=2)
     assert r["workers_started"] == 2, r  # one model load, shared by both gateway processes
     assert r["requests_ok"] > 20 and r["chunks_per_s"] > 0, r
+
+
+def test_owner_watchdog_counts_sibling_activity(tmp_path):
+    """the owner's idle watchdog must not kill a replica that an attached sibling process is
+    serving — siblings report use through the registry and the owner folds it into its idle / busy checks."""
+    import subprocess
+    import sys
+    import time
+
+    from localai_tfp_amd.serving.model_loader import WatchDog
+    from localai_tfp_amd.serving.shared_backends import ActivityReporter
+
+    owner = SharedBackends(str(tmp_path))
+
+    class _Loader:
+        shared = owner
+        killed: list = []
+
+        def shutdown_model(self, m, force=False):
+            self.killed.append(m)
+
+    ld = _Loader()
+    wd = WatchDog(ld, busy_timeout=1e9, idle_timeout=10.0, interval=1e9)
+    wd.add("127.0.0.1:9", "m")
+    wd.last_used["127.0.0.1:9"] = time.time() - 100  # the owner itself has not used it for 100 s
+    # a live sibling process (not this pid) reports a request in flight
+    sib = subprocess.Popen([sys.executable, "-c", "import time; time.sleep(30)"])
+    try:
+        rep = ActivityReporter(SharedBackends(str(tmp_path)))
+        rep.shared.pid = sib.pid
+        rep.mark("127.0.0.1:9")
+        assert wd.check_once() == [] and ld.killed == []           # busy in a sibling: not idle
+        rep.unmark("127.0.0.1:9")
+        assert wd.check_once() == []                               # used by the sibling just now
+        assert wd.check_once(now=time.time() + 60) == ["m"]        # nobody used it for 60 s
+    finally:
+        sib.kill()
+        sib.wait()
