@@ -24,6 +24,21 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 #define MX_DEV __device__ __forceinline__
 #define MX_LDS __attribute__((address_space(3)))
 
+// LDS-DMA (global_load_lds) issued from inline asm. hipcc's waitcnt pass counts a compiler-visible LDS-DMA as an
+// LGKM event that completes out of order with ds_read, so in any loop that has one it waits lgkmcnt(0) before
+// every use of an LDS read — a k-step's fragment reads can then never run ahead of its MFMAs
+// (profiles/r6_lgkm_lds_dma.md). Issued from asm the DMA is invisible to that pass: the kernel waits for the DMA
+// itself (an explicit `s_waitcnt vmcnt(N)` before the barrier that publishes the slot) and the compiler keeps
+// counted lgkmcnt waits for its own ds_reads. M0 = the wave-uniform LDS destination (lane l writes M0 + 16 l).
+MX_DEV void mx_lds_dma16(const void* g, const MX_LDS void* lds) {
+    const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)lds);
+    asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "{m0}"(m0) : "memory");
+}
+MX_DEV void mx_lds_dma4(const void* g, const MX_LDS void* lds) {
+    const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)lds);
+    asm volatile("s_nop 0\n\tglobal_load_lds_dword %0, off" ::"v"(g), "{m0}"(m0) : "memory");
+}
+
 MX_DEV float bf16_to_f32(bf16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
 
 // round-to-nearest-even; NaN stays NaN (the plain cast lowers to v_cvt_pk_bf16_f32 on gfx950).

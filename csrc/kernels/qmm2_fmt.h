@@ -7,6 +7,21 @@
 
 namespace {
 
+// Q2_ASM_DMA: issue the ring's LDS-DMA from inline asm (mx_common.h mx_lds_dma16), so the compiler's lgkmcnt
+// waits for the fragment reads are counted instead of lgkmcnt(0) (the explicit vmcnt waits below cover the DMA)
+#ifndef Q2_ASM_DMA
+#define Q2_ASM_DMA 1
+#endif
+MX_DEV void q2_dma(const void* g, MX_LDS void* lds, int sz) {
+#if Q2_ASM_DMA
+    if (sz == 16) mx_lds_dma16(g, lds);
+    else mx_lds_dma4(g, lds);
+#else
+    if (sz == 16) __builtin_amdgcn_global_load_lds(g, lds, 16, 0, 0);
+    else __builtin_amdgcn_global_load_lds(g, lds, 4, 0, 0);
+#endif
+}
+
 template <int N_>
 MX_DEV void q2_wait_barrier() {
     asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N_) : "memory");
@@ -430,28 +445,26 @@ MX_DEV void q2_stage_weights(const uint8_t* u, char* qd, char* hd, int lane) {
     static_assert(NF + (REM ? 1 : 0) == F::QI && REM % 16 == 0, "quant piece count");
 #pragma unroll
     for (int i = 0; i < NF; ++i)
-        __builtin_amdgcn_global_load_lds((const void*)(qs + i * 1024 + lane * 16), (MX_LDS void*)(qd + i * 1024), 16, 0,
-                                         0);
+        q2_dma((const void*)(qs + i * 1024 + lane * 16), (MX_LDS void*)(qd + i * 1024), 16);
     if constexpr (REM > 0) {
         if (lane < REM / 16)
-            __builtin_amdgcn_global_load_lds((const void*)(qs + NF * 1024 + lane * 16), (MX_LDS void*)(qd + NF * 1024),
-                                             16, 0, 0);
+            q2_dma((const void*)(qs + NF * 1024 + lane * 16), (MX_LDS void*)(qd + NF * 1024), 16);
     }
     if constexpr (JQ == 0) {
         if constexpr (QT == MXQ_Q3_K) {  // hdr (512 B) + hmask (1 KB): one full and one half instruction
-            __builtin_amdgcn_global_load_lds((const void*)(u + lane * 16), (MX_LDS void*)hd, 16, 0, 0);
+            q2_dma((const void*)(u + lane * 16), (MX_LDS void*)(hd), 16);
             if (lane < 32)
-                __builtin_amdgcn_global_load_lds((const void*)(u + 1024 + lane * 16), (MX_LDS void*)(hd + 1024), 16, 0, 0);
+                q2_dma((const void*)(u + 1024 + lane * 16), (MX_LDS void*)(hd + 1024), 16);
         } else if constexpr (QT == MXQ_MX4F || QT == MXQ_MX5F) {  // both header halves (1 KB)
-            __builtin_amdgcn_global_load_lds((const void*)(u + lane * 16), (MX_LDS void*)hd, 16, 0, 0);
+            q2_dma((const void*)(u + lane * 16), (MX_LDS void*)(hd), 16);
         } else if constexpr (F::HB > 0) {
-            if (lane < 32) __builtin_amdgcn_global_load_lds((const void*)(u + lane * 16), (MX_LDS void*)hd, 16, 0, 0);
+            if (lane < 32) q2_dma((const void*)(u + lane * 16), (MX_LDS void*)(hd), 16);
             if constexpr (QT == MXQ_Q6_K || QT == MXQ_Q2_K) {  // + the 32 x 4 B d (/ dmin) words
                 if (lane < 32)
-                    __builtin_amdgcn_global_load_lds((const void*)(u + 512 + lane * 4), (MX_LDS void*)(hd + 512), 4, 0, 0);
+                    q2_dma((const void*)(u + 512 + lane * 4), (MX_LDS void*)(hd + 512), 4);
             }
             if constexpr (QT == MXQ_Q5_K)  // + the qh chunks (fifth bits of the whole super-block)
-                __builtin_amdgcn_global_load_lds((const void*)(u + F::QH + lane * 16), (MX_LDS void*)(hd + 512), 16, 0, 0);
+                q2_dma((const void*)(u + F::QH + lane * 16), (MX_LDS void*)(hd + 512), 16);
         }
     }
 }

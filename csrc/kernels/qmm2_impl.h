@@ -52,6 +52,22 @@ MX_DEV void q2_interleave() {
     }
 }
 
+// Q2_AEARLY 1: the next k-step's A fragments are read at the TOP of a k-step (all WM reads back to back, then the
+// k-step's MFMAs with the dequant VALU in their shadows) instead of one read after each MFMA (0, default). Same-box
+// A/B with the asm LDS-DMA (counted lgkmcnt waits either way): within 1 % on every projection, and 0 needs 20
+// fewer VGPRs (profiles/r6_qmm2_asm_dma.md)
+#ifndef Q2_AEARLY
+#define Q2_AEARLY 0
+#endif
+template <int I, int NM, int NV>
+MX_DEV void q2_interleave_mfma() {
+    if constexpr (I < NM) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, NV, 0);
+        q2_interleave_mfma<I + 1, NM, NV>();
+    }
+}
+
 // outstanding LDS-DMA instructions of NN consecutive stages from super-block position J0 (a stage: WAI A pieces,
 // plus QII quant pieces and, at position 0, HII header pieces for a weight-loading wave)
 template <int WAI, int QII, int HII, bool WL, int J0, int NN>
@@ -138,9 +154,7 @@ __global__ __launch_bounds__(NG == 8 ? 512 / GPW : 256 * KS) void qmm2_kernel(co
         const uint16_t* ak = A + (size_t)kta * 64;
 #pragma unroll
         for (int i = 0; i < WAI; ++i)
-            __builtin_amdgcn_global_load_lds((const void*)(ak + aoff[i]),
-                                             (MX_LDS void*)(sb + min(wave * WA + i, BM / 8 - 1) * 1024),
-                                             16, 0, 0);
+            q2_dma((const void*)(ak + aoff[i]), (MX_LDS void*)(sb + min(wave * WA + i, BM / 8 - 1) * 1024), 16);
         if constexpr (decltype(wl_c)::value && QII > 0) {
             const uint8_t* u = wg + (size_t)sbw * F::UNIT;
             q2_stage_weights<QT, JQ>(u, sb + A_BYTES + GPW * cg * F::QB, hdr_lds + hslot * G::HSZ + GPW * cg * F::HB,
@@ -275,7 +289,14 @@ __global__ __launch_bounds__(NG == 8 ? 512 / GPW : 256 * KS) void qmm2_kernel(co
                         if constexpr (DBG & 1) asm volatile("" ::"v"(af[cur][i]), "v"(bfc[j]));
                         else acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[cur][i], bfc[j], acc[i][j], 0, 0, 0);
                     }
-                if constexpr (!(DBG & 1)) q2_interleave<0, WM * WN, WM, Q2_VPM>();
+                if constexpr (!(DBG & 1)) {
+                    if constexpr (Q2_AEARLY) {
+                        __builtin_amdgcn_sched_group_barrier(0x100, WM, 0);  // the next k-step's A reads first
+                        q2_interleave_mfma<0, WM * WN, Q2_VPM>();
+                    } else {
+                        q2_interleave<0, WM * WN, WM, Q2_VPM>();
+                    }
+                }
 #pragma unroll
                 for (int j = 0; j < WN; ++j) bfc[j] = bfn[j];
             }

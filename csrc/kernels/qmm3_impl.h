@@ -79,8 +79,7 @@ __global__ __launch_bounds__(512) void qmm3_kernel(const uint16_t* __restrict__ 
             if constexpr (!(DBG & 4)) {
 #pragma unroll
                 for (int i = 0; i < WA; ++i)
-                    __builtin_amdgcn_global_load_lds((const void*)(ak + aoff[i]),
-                                                     (MX_LDS void*)(as + (p * WA + i) * 1024), 16, 0, 0);
+                    q2_dma((const void*)(ak + aoff[i]), (MX_LDS void*)(as + (p * WA + i) * 1024), 16);
             }
             if constexpr (DBG & 8) return;
             const uint8_t* u = wg + (size_t)sb * F::UNIT;

@@ -113,7 +113,7 @@ class NativeError(RuntimeError):
 
 
 def _load(name: str):
-    path = _LIBDIR / name
+    path = kernel_lib_path() if name == "libmxk.so" else _LIBDIR / name
     if not path.exists():
         raise NativeError(
             f"{path} is missing: build it with `python -m localai_tfp_amd._build` "
@@ -122,7 +122,9 @@ def _load(name: str):
 
 
 def kernel_lib_path():
-    return _LIBDIR / "libmxk.so"
+    # MX_KERNEL_LIB: an alternative build of the kernel library (same-box A/B runs of kernel variants)
+    alt = os.environ.get("MX_KERNEL_LIB")
+    return Path(alt) if alt else _LIBDIR / "libmxk.so"
 
 
 def kernels():
