@@ -17,14 +17,9 @@
 //                  atomics on the residual stream).
 #include "mx_common.h"
 
+// one wave routes one token: softmax over the row's E logits, k rounds of arg-max, optional renormalisation
 template <int VPL>
-__global__ __launch_bounds__(256) void moe_route_kernel(const float* __restrict__ logits, int ldl, int T, int E,
-                                                        int k, int renorm, int* __restrict__ ids,
-                                                        float* __restrict__ wts) {
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int t = blockIdx.x * 4 + wave;
-    if (t >= T) return;
-    const float* row = logits + (size_t)t * ldl;
+MX_DEV void route_row(const float* row, int E, int k, int renorm, int* ids, float* wts, int lane) {
     float v[VPL];
     float mx = -INFINITY;
 #pragma unroll
@@ -75,9 +70,94 @@ __global__ __launch_bounds__(256) void moe_route_kernel(const float* __restrict_
         }
     }
     if (lane < k) {
-        ids[(size_t)t * k + lane] = my_id;
-        wts[(size_t)t * k + lane] = renorm ? my_p / picked : my_p;
+        ids[lane] = my_id;
+        wts[lane] = renorm ? my_p / picked : my_p;
     }
+}
+
+template <int VPL>
+__global__ __launch_bounds__(256) void moe_route_kernel(const float* __restrict__ logits, int ldl, int T, int E,
+                                                        int k, int renorm, int* __restrict__ ids,
+                                                        float* __restrict__ wts) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int t = blockIdx.x * 4 + wave;
+    if (t >= T) return;
+    route_row<VPL>(logits + (size_t)t * ldl, E, k, renorm, ids + (size_t)t * k, wts + (size_t)t * k, lane);
+}
+
+// Router GEMV + routing in one launch: TT tokens per workgroup, their 16-bit hidden rows staged in LDS, each wave
+// takes every 4th expert (fp32 router row read once per TT tokens, coalesced float4 per lane), the logits land in
+// LDS and each wave then routes TT / 4 of the tokens (route_row). Replaces the fp32 hipBLASLt matmul + route launch.
+template <int VPL, int TT, bool F16>
+__global__ __launch_bounds__(256) void moe_router_kernel(const bf16_t* __restrict__ x, int ldx,
+                                                         const float* __restrict__ wr, int T, int H, int E, int k,
+                                                         int renorm, int* __restrict__ ids, float* __restrict__ wts) {
+    extern __shared__ __attribute__((aligned(16))) char rsm[];
+    bf16_t* xs = (bf16_t*)rsm;                         // [TT][H]
+    float* lg = (float*)(rsm + (size_t)TT * H * 2);    // [TT][E]
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int t0 = blockIdx.x * TT, nt = min(TT, T - t0);
+    for (int i = threadIdx.x * 8; i < TT * H; i += 256 * 8) {
+        const int t = i / H, c = i % H;
+        *(uint4*)(xs + i) = t < nt ? *(const uint4*)(x + (size_t)(t0 + t) * ldx + c) : make_uint4(0, 0, 0, 0);
+    }
+    __syncthreads();
+    for (int e = wave; e < E; e += 4) {
+        float acc[TT];
+#pragma unroll
+        for (int t = 0; t < TT; ++t) acc[t] = 0.f;
+        const float* w = wr + (size_t)e * H;
+        for (int c = lane * 4; c < H; c += 256) {
+            const float4 w4 = *(const float4*)(w + c);
+#pragma unroll
+            for (int t = 0; t < TT; ++t) {
+                const uint2 raw = *(const uint2*)(xs + t * H + c);
+                float a0, a1, a2, a3;
+                unpack_act2<F16>(raw.x, a0, a1);
+                unpack_act2<F16>(raw.y, a2, a3);
+                acc[t] += w4.x * a0 + w4.y * a1 + w4.z * a2 + w4.w * a3;
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < TT; ++t) {
+            const float s = wave_sum(acc[t]);
+            if (lane == 0) lg[t * E + e] = s;
+        }
+    }
+    __syncthreads();
+    for (int t = wave; t < nt; t += 4)
+        route_row<VPL>(lg + t * E, E, k, renorm, ids + (size_t)(t0 + t) * k, wts + (size_t)(t0 + t) * k, lane);
+}
+
+// x 16-bit [T, H] (the normed hidden state), wr fp32 [E, H] -> ids / wts [T, k]; H % 256 == 0
+extern "C" int mxk_moe_router(const void* x, int ldx, const float* wr, int T, int H, int E, int k, int renorm, int* ids,
+                              float* wts, hipStream_t st) {
+    if (T <= 0) return 0;
+    if (k < 1 || k > 64 || k > E || H % 256 || ldx % 8 || ((uintptr_t)x & 15) || ((uintptr_t)wr & 15))
+        return (int)hipErrorInvalidValue;
+    constexpr int TT = 8;
+    const size_t lds = (size_t)TT * H * 2 + (size_t)TT * E * 4;
+    if (lds > 160 * 1024) return (int)hipErrorInvalidValue;
+    const int blocks = (T + TT - 1) / TT;
+#define MRR(V)                                                                                                   \
+    {                                                                                                            \
+        auto kern = moe_router_kernel<V, TT, F16>;                                                               \
+        (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);      \
+        kern<<<blocks, 256, lds, st>>>((const bf16_t*)x, ldx, wr, T, H, E, k, renorm, ids, wts);                 \
+    }
+    if (E <= 64) {
+        MX_ACT_DISPATCH(MRR(1));
+    } else if (E <= 128) {
+        MX_ACT_DISPATCH(MRR(2));
+    } else if (E <= 256) {
+        MX_ACT_DISPATCH(MRR(4));
+    } else if (E <= 512) {
+        MX_ACT_DISPATCH(MRR(8));
+    } else {
+        return (int)hipErrorInvalidValue;
+    }
+#undef MRR
+    MXK_CHECK_LAUNCH();
 }
 
 extern "C" int mxk_moe_route(const float* logits, int ldl, int T, int E, int k, int renorm, int* ids, float* wts,
@@ -133,7 +213,8 @@ extern "C" int mxk_moe_sort(const int* ids, int P, int k, int E, int BM, int* of
     MXK_CHECK_LAUNCH();
 }
 
-// h[t, :] (+)= sum_j w[t, j] * Y[inv_pos[t*k + j], :]   (fp32; `accumulate` adds into h)
+// h[t, :] (+)= sum_j w[t, j] * Y[inv_pos[t*k + j], :]   (fp32; `accumulate` adds into h; inv_pos null: Y rows in
+// pair order t*k + j, as the grouped decode GEMV writes them)
 __global__ __launch_bounds__(256) void moe_combine_kernel(const float* __restrict__ Y, int ldy,
                                                           const int* __restrict__ inv_pos,
                                                           const float* __restrict__ wts, int k, int H,
@@ -143,7 +224,8 @@ __global__ __launch_bounds__(256) void moe_combine_kernel(const float* __restric
         float4 acc = accumulate ? *(const float4*)(h + (size_t)t * ldh + c) : (float4){0.f, 0.f, 0.f, 0.f};
         for (int j = 0; j < k; ++j) {
             const float w = wts[(size_t)t * k + j];
-            const float4 y = *(const float4*)(Y + (size_t)inv_pos[(size_t)t * k + j] * ldy + c);
+            const size_t row = inv_pos ? (size_t)inv_pos[(size_t)t * k + j] : (size_t)t * k + j;
+            const float4 y = *(const float4*)(Y + row * ldy + c);
             acc.x = fmaf(w, y.x, acc.x);
             acc.y = fmaf(w, y.y, acc.y);
             acc.z = fmaf(w, y.z, acc.z);

@@ -77,12 +77,25 @@ constexpr int q2_cnt_run() {
     return c;
 }
 
+// Grouped (mixture-of-experts) mode, GR = true: the rows are token-expert pairs sorted by expert (ops/moe.py,
+// moe.hip moe_sort: off[e] .. off[e + 1] are expert e's rows, tiles[e] its first row tile of BM rows), W holds the
+// experts' [N, K] t32 matrices back to back (expert e = column groups e N / 32 ..), and A row r is A[stok[r]] (the
+// token's normed hidden state; stok == nullptr: A[r], the gate|up activations of pair r for the down projection).
+// Output row r is pair r's. The grid covers the maximum row-tile count (P / BM + E, independent of the routing, so a
+// captured graph replays any routing); workgroups past tiles[E] exit at once.
+struct Q2Group {
+    const int* tiles;
+    const int* off;
+    const int* stok;
+    int E;
+};
+
 // DBG (isolation builds, tools/prof_qmm.py --q2dbg): 1 no MFMA, 2 no dequant VALU, 4 no A loads, 8 no weight loads
-template <int QT, int WM, int KS, int WN, int EPI, int DBG = 0, int NS = 4, int NG = 4, int GPW = 1>
+template <int QT, int WM, int KS, int WN, int EPI, int DBG = 0, int NS = 4, int NG = 4, int GPW = 1, bool GR = false>
 __global__ __launch_bounds__(NG == 8 ? 512 / GPW : 256 * KS) void qmm2_kernel(const uint16_t* __restrict__ A, int lda,
                                                         const uint8_t* __restrict__ W, int M, int N, int K,
                                                         int n_mt, int splits, int sbps, void* __restrict__ Cv,
-                                                        int ldc, int rot_mul) {
+                                                        int ldc, int rot_mul, Q2Group grp) {
     using G = Q2Geom<QT, WM, KS, WN, NS, NG, GPW>;
     using F = Q2F<QT>;
     constexpr int BM = G::BM, WA = G::WA, STAGE = G::STAGE, A_BYTES = G::A_BYTES;
@@ -123,11 +136,26 @@ __global__ __launch_bounds__(NG == 8 ? 512 / GPW : 256 * KS) void qmm2_kernel(co
     const int nsb = K >> 8;
     const int sb0 = split * sbps, sb1 = min(sb0 + sbps, nsb);
     if (sb0 >= sb1) return;
-    const int m_base = mt * BM;
+    int m_base = mt * BM;
     const int ngrp = N >> 5;
+    size_t g_base = 0;  // grouped: the expert's first column group
+    if constexpr (GR) {
+        const int tot = grp.tiles[grp.E];
+        if (mt >= tot) return;
+        int lo = 0, hi = grp.E - 1;  // the expert e with tiles[e] <= mt < tiles[e + 1]
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (grp.tiles[mid] <= mt) lo = mid;
+            else hi = mid - 1;
+        }
+        m_base = grp.off[lo] + (mt - grp.tiles[lo]) * BM;
+        M = grp.off[lo + 1];  // rows of this tile: m_base .. min(m_base + BM, M)
+        g_base = (size_t)lo * ngrp;
+    }
     const int g = min(ct * NG + GPW * cg, ngrp - 1);  // groups past N re-read the last (never stored)
-    const uint8_t* wg = W + (size_t)g * ((size_t)nsb * F::UNIT);
-    [[maybe_unused]] const uint8_t* wg2 = W + (size_t)min(ct * NG + GPW * cg + 1, ngrp - 1) * ((size_t)nsb * F::UNIT);
+    const uint8_t* wg = W + (g_base + g) * ((size_t)nsb * F::UNIT);
+    [[maybe_unused]] const uint8_t* wg2 =
+        W + (g_base + min(ct * NG + GPW * cg + 1, ngrp - 1)) * ((size_t)nsb * F::UNIT);
 
     // A LDS-DMA sources: instruction i of this wave fills 8-row block j = wave * WA + i; lane p writes
     // image slot (k-step p >> 4, row (p >> 1) & 7, half (p & 1) ^ (j & 1)) from 16 B of that row
@@ -136,7 +164,10 @@ __global__ __launch_bounds__(NG == 8 ? 512 / GPW : 256 * KS) void qmm2_kernel(co
     for (int i = 0; i < WA; ++i) {
         const int j = min(wave * WA + i, BM / 8 - 1);
         const int s = lane >> 4, r8 = (lane >> 1) & 7, hh = (lane & 1) ^ (j & 1);
-        const int row = min(m_base + 8 * j + r8, M - 1);
+        int row = min(m_base + 8 * j + r8, M - 1);
+        if constexpr (GR) {
+            if (grp.stok) row = grp.stok[row];
+        }
         aoff[i] = (uint32_t)(row * lda + 16 * s + 8 * hh);
     }
     // per-lane fragment read bases (byte offsets within a stage)
@@ -421,8 +452,39 @@ static int launch_qmm2(const uint16_t* A, int lda, const uint8_t* W, int M, int 
         attr_set = true;
     }
     qmm2_kernel<QT, WM, KS, WN, EPI, 0, NS, NG, GPW><<<dim3((unsigned)nwg), 64 * G::NT, G::LDS, st>>>(
-        A, lda, W, M, N, K, n_mt, splits, sbps, C, ldc, g_qmm2_rot);
+        A, lda, W, M, N, K, n_mt, splits, sbps, C, ldc, g_qmm2_rot, Q2Group{});
     MXK_CHECK_LAUNCH();
+}
+
+// grouped (MoE) launch: P sorted rows, E experts of N columns each, tiles / off from moe_sort with BM = 32 WM
+template <int QT, int WM, int KS, int EPI>
+static int launch_qmm2_grouped(const uint16_t* A, int lda, const int* stok, const uint8_t* W, int P, int E, int N, int K,
+                               const int* tiles, const int* off, void* C, int ldc, hipStream_t st) {
+    using G = Q2Geom<QT, WM, KS, 1>;
+    const int n_ct = (N + 127) / 128, n_mt = (P + G::BM - 1) / G::BM + E;
+    const long nwg = (long)n_ct * n_mt;
+    if (nwg <= 0 || nwg > 0x7fffffff) return (int)hipErrorInvalidValue;
+    static bool attr_set = false;
+    if (!attr_set) {
+        (void)hipFuncSetAttribute((const void*)qmm2_kernel<QT, WM, KS, 1, EPI, 0, 4, 4, 1, true>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS);
+        attr_set = true;
+    }
+    qmm2_kernel<QT, WM, KS, 1, EPI, 0, 4, 4, 1, true><<<dim3((unsigned)nwg), 64 * G::NT, G::LDS, st>>>(
+        A, lda, W, P, N, K, n_mt, 1, K >> 8, C, ldc, 0, Q2Group{tiles, off, stok, E});
+    MXK_CHECK_LAUNCH();
+}
+
+// wm 1 (32-row tiles) or 2 (64); epi F32 (the down projection into the [P, H] buffer) or SwiGLU / GeGLU (gate|up)
+template <int QT>
+static int qmm2_grouped_run(int epi, int wm, const uint16_t* A, int lda, const int* stok, const uint8_t* W, int P, int E,
+                            int N, int K, const int* tiles, const int* off, void* C, int ldc, hipStream_t st) {
+#define Q2G(WM_, EPI_)                                                                                          \
+    if (wm == WM_ && epi == EPI_)                                                                               \
+        return launch_qmm2_grouped<QT, WM_, 2, EPI_>(A, lda, stok, W, P, E, N, K, tiles, off, C, ldc, st);
+    Q2G(1, E16_F32) Q2G(2, E16_F32) Q2G(1, E16_SWIGLU) Q2G(2, E16_SWIGLU) Q2G(1, E16_GEGLU) Q2G(2, E16_GEGLU)
+#undef Q2G
+    return (int)hipErrorInvalidValue;
 }
 
 // ks: 1 / 2 waves per column group; ks | 8 selects the 8-slot ring (64-row tiles only); 17 the wide tiles
@@ -475,7 +537,7 @@ static int launch_dbg(int wm, int ks, int wn, const uint16_t* A, int lda, const 
         (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
         const int n_ct = (N + 32 * ng - 1) / (32 * ng), n_mt = (M + bm - 1) / bm;
         kern<<<dim3(n_ct * n_mt), ng == 8 ? 512 : 256 * ks, lds, st>>>(A, lda, W, M, N, K, n_mt, 1, K >> 8, C, ldc,
-                                                                      g_qmm2_rot);
+                                                                      g_qmm2_rot, Q2Group{});
         return (int)hipGetLastError();
     };
     // ks 17: the wide tiles (8 column groups)
@@ -491,7 +553,7 @@ static int launch_dbg(int wm, int ks, int wn, const uint16_t* A, int lda, const 
                                   Q2Geom<QT, 6, 1, 2, 4, 8, 2>::LDS);
         const int n_ct = (N + 255) / 256, n_mt = (M + 191) / 192;
         k4<<<dim3(n_ct * n_mt), 256, Q2Geom<QT, 6, 1, 2, 4, 8, 2>::LDS, st>>>(A, lda, W, M, N, K, n_mt, 1, K >> 8, C, ldc,
-                                                                            g_qmm2_rot);
+                                                                            g_qmm2_rot, Q2Group{});
         return (int)hipGetLastError();
     }
     if (wm == 8 && ks == 1 && wn == 1) return go(qmm2_kernel<QT, 8, 1, 1, EPI, DBG>, 256, 1, Q2Geom<QT, 8, 1, 1>::LDS);
@@ -525,4 +587,8 @@ int qmm2_run_q2k(int epi, int wm, int ks, int wn, const uint16_t* A, int lda, co
 int qmm2_run_q80(int epi, int wm, int ks, int wn, const uint16_t* A, int lda, const uint8_t* W, int M, int N, int K, int splits, void* C, int ldc, hipStream_t st);
 int qmm2_run_mx4(int epi, int wm, int ks, int wn, const uint16_t* A, int lda, const uint8_t* W, int M, int N, int K, int splits, void* C, int ldc, hipStream_t st);
 int qmm2_run_mx5(int epi, int wm, int ks, int wn, const uint16_t* A, int lda, const uint8_t* W, int M, int N, int K, int splits, void* C, int ldc, hipStream_t st);
+int qmm2_grouped_q4k(int epi, int wm, const uint16_t* A, int lda, const int* stok, const uint8_t* W, int P, int E, int N, int K, const int* tiles, const int* off, void* C, int ldc, hipStream_t st);
+int qmm2_grouped_q5k(int epi, int wm, const uint16_t* A, int lda, const int* stok, const uint8_t* W, int P, int E, int N, int K, const int* tiles, const int* off, void* C, int ldc, hipStream_t st);
+int qmm2_grouped_q6k(int epi, int wm, const uint16_t* A, int lda, const int* stok, const uint8_t* W, int P, int E, int N, int K, const int* tiles, const int* off, void* C, int ldc, hipStream_t st);
+int qmm2_grouped_q80(int epi, int wm, const uint16_t* A, int lda, const int* stok, const uint8_t* W, int P, int E, int N, int K, const int* tiles, const int* off, void* C, int ldc, hipStream_t st);
 int qmm2_dbg_q4k(int dbg, int wm, int ks, int wn, const uint16_t* A, int lda, const uint8_t* W, int M, int N, int K, void* C, int ldc, hipStream_t st);

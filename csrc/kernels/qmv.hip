@@ -908,6 +908,119 @@ extern "C" int mxk_qmv1_enable(int on) {
     return 0;
 }
 
+// Grouped (mixture-of-experts) decode GEMV on t32 expert stacks: one workgroup per (32-column group g of one expert's
+// N, token-expert pair p). Pair p multiplies activation row p / xdiv (xdiv = k: the token's normed hidden state for
+// gate|up; 1: the pair's own gate|up activations for the down projection) by expert ids[p] - e0's columns
+// (W = the experts' [N, K] t32 matrices back to back) and writes output row p (pair order, no sort). Pairs routed to
+// experts outside [e0, e0 + El) (another rank's, expert parallelism) are skipped: their rows stay as the caller
+// initialised them. Every workgroup quantises its whole activation row into LDS (q8 per 32, llama.cpp q8_1
+// numerics as qmv), two weight units in flight per wave. Used at decode batch sizes (P = T k pairs <= 64), where a
+// 32-row grouped GEMM tile would stream each expert through at most a few busy CUs.
+template <int QT, int EPI, bool F16>
+__global__ __launch_bounds__(64 * QMV_WAVES) void qmv_moe_kernel(const uint8_t* __restrict__ W, int N, int K,
+                                                                 const int* __restrict__ ids, int e0, int El,
+                                                                 const bf16_t* __restrict__ x, int ldx, int xdiv,
+                                                                 void* __restrict__ Cv, int ldc) {
+    using U = TUnit<QT>;
+    __shared__ float red[QMV_WAVES][32];
+    extern __shared__ __attribute__((aligned(16))) char qmv_smem[];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int r = lane & 31, h = lane >> 5;
+    const int g = blockIdx.x, p = blockIdx.y;
+    const int e = ids[p] - e0;
+    if (e < 0 || e >= El) return;
+    const int nunit = K / U::ELEMS;
+    const uint8_t* wg = W + ((size_t)e * (N >> 5) + g) * ((size_t)nunit * U::BYTES);
+    U a, b;
+    int u = wave;
+    if (u < nunit) a.load(wg + (size_t)u * U::BYTES, r, h);
+    if (u + QMV_WAVES < nunit) b.load(wg + (size_t)(u + QMV_WAVES) * U::BYTES, r, h);
+    int8_t* sq = (int8_t*)qmv_smem;
+    float2* sd = (float2*)(qmv_smem + K);
+    const bf16_t* xr = x + (size_t)(p / xdiv) * ldx;
+    // 8 consecutive elements per lane, 4 lanes per 32-element block (K % 256 == 0: the 4-lane groups enter and
+    // leave the loop together)
+    for (int e8 = threadIdx.x * 8; e8 < K; e8 += 64 * QMV_WAVES * 8) {
+        float a8[8];
+        const uint4 raw = *(const uint4*)(xr + e8);
+        unpack_act2<F16>(raw.x, a8[0], a8[1]);
+        unpack_act2<F16>(raw.y, a8[2], a8[3]);
+        unpack_act2<F16>(raw.z, a8[4], a8[5]);
+        unpack_act2<F16>(raw.w, a8[6], a8[7]);
+        float am = 0.f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) am = fmaxf(am, fabsf(a8[i]));
+        am = group_max<4>(am);
+        const float d = am / 127.f, id = d > 0.f ? 1.f / d : 0.f;
+        int q[8], sum = 0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) { q[i] = __float2int_rn(a8[i] * id); sum += q[i]; }
+        const float sf = group_sum<4>((float)sum);
+        uint2 pk;
+        pk.x = (q[0] & 0xFF) | ((q[1] & 0xFF) << 8) | ((q[2] & 0xFF) << 16) | ((uint32_t)(q[3] & 0xFF) << 24);
+        pk.y = (q[4] & 0xFF) | ((q[5] & 0xFF) << 8) | ((q[6] & 0xFF) << 16) | ((uint32_t)(q[7] & 0xFF) << 24);
+        *(uint2*)(sq + e8) = pk;
+        if ((threadIdx.x & 3) == 0) sd[e8 / 32] = make_float2(d, d * sf);
+    }
+    __syncthreads();
+    float acc = 0.f;
+    while (u < nunit) {
+        const bool hb = u + QMV_WAVES < nunit;
+        acc += a.dot(sq + (size_t)u * U::ELEMS, sd + u * (U::ELEMS / 32), h);
+        if (hb) acc += b.dot(sq + (size_t)(u + QMV_WAVES) * U::ELEMS, sd + (u + QMV_WAVES) * (U::ELEMS / 32), h);
+        u += 2 * QMV_WAVES;
+        if (u < nunit) a.load(wg + (size_t)u * U::BYTES, r, h);
+        if (u + QMV_WAVES < nunit) b.load(wg + (size_t)(u + QMV_WAVES) * U::BYTES, r, h);
+    }
+    {
+        const float v = acc + __shfl_xor(acc, 32);
+        if (h == 0) red[wave][r] = v;
+    }
+    __syncthreads();
+    if (wave != 0) return;
+    float v = 0.f;
+    if (h == 0) {
+#pragma unroll
+        for (int w = 0; w < QMV_WAVES; ++w) v += red[w][r];
+    }
+    if constexpr (EPI == E16_SWIGLU || EPI == E16_GEGLU) {
+        const float up = __shfl_down(v, 16);
+        if (h == 0 && r < 16) ((uint16_t*)Cv)[(size_t)p * ldc + g * 16 + r] = f32_to_act<F16>(glu_gate_f<EPI>(v) * up);
+    } else if (h == 0) {
+        ((float*)Cv)[(size_t)p * ldc + g * 32 + r] = v;
+    }
+}
+
+// W t32 expert stack [E_local * N, K]; x 16-bit rows (row p / xdiv for pair p); ids [P]; epi 0 fp32 [P, N] or
+// 3 / 4 SwiGLU / GeGLU f16 [P, N / 2]. N % 32 == 0, K % 256 == 0, K <= 16384.
+extern "C" int mxk_qmv_moe(int qtype, int epi, const uint8_t* W, int N, int K, const int* ids, int P, int e0, int El,
+                           const void* x, int ldx, int xdiv, void* C, int ldc, hipStream_t st) {
+    if (P <= 0) return 0;
+    if (K % 256 || N % 32 || K > 16384 || xdiv < 1 || ((uintptr_t)x & 15) || (ldx % 8)) return (int)hipErrorInvalidValue;
+    const size_t lds = (size_t)K + (size_t)K / 32 * sizeof(float2);
+    const dim3 grid(N / 32, P);
+#define QMOE(QT_, EPI_)                                                                                         \
+    MX_ACT_DISPATCH(qmv_moe_kernel<QT_, EPI_, F16><<<grid, 64 * QMV_WAVES, lds, st>>>(                          \
+        W, N, K, ids, e0, El, (const bf16_t*)x, ldx, xdiv, C, ldc));                                            \
+    MXK_CHECK_LAUNCH();
+#define QMOE_EPI(QT_)                                          \
+    switch (epi) {                                             \
+        case E16_F32: { QMOE(QT_, E16_F32) }                   \
+        case E16_SWIGLU: { QMOE(QT_, E16_SWIGLU) }             \
+        case E16_GEGLU: { QMOE(QT_, E16_GEGLU) }               \
+    }                                                          \
+    break;
+    switch (qtype) {
+        case MXQ_Q4_K: QMOE_EPI(MXQ_Q4_K)
+        case MXQ_Q5_K: QMOE_EPI(MXQ_Q5_K)
+        case MXQ_Q6_K: QMOE_EPI(MXQ_Q6_K)
+        case MXQ_Q8_0: QMOE_EPI(MXQ_Q8_0)
+    }
+#undef QMOE_EPI
+#undef QMOE
+    return (int)hipErrorInvalidValue;
+}
+
 extern "C" int mxk_dequant_t32(int qtype, const uint8_t* W, const int* rows, int nrows, int K, uint16_t* ob,
                                float* of, int ldo, hipStream_t st) {
     if (nrows <= 0) return 0;

@@ -95,6 +95,12 @@ KERNEL_SIGS = {
     "mxk_qk_norm_rope_gqa": [P, I, I, I, I, I, I, P, P, P, I, F, P],
     "mxk_ssm_scan": [P, P, I, P, P, P, P, P, I, P, P, P, I, I, P, I, P, I, I, I, I, P],
     "mxk_moe_route": [P, I, I, I, I, I, P, P, P],
+    # x, ldx, wr, T, H, E, k, renorm, ids, wts, stream
+    "mxk_moe_router": [P, I, P, I, I, I, I, I, P, P, P],
+    # qtype, epi, W, N, K, ids, P, e0, El, x, ldx, xdiv, C, ldc, stream
+    "mxk_qmv_moe": [I, I, P, I, I, P, I, I, I, P, I, I, P, I, P],
+    # qtype, epi, wm, A, lda, stok, W, P, E, N, K, tiles, off, C, ldc, stream
+    "mxk_qmm2_grouped": [I, I, I, P, I, P, P, I, I, I, I, P, P, P, I, P],
     "mxk_moe_sort": [P, I, I, I, I, P, P, P, P, P],
     "mxk_moe_combine": [P, I, P, P, I, I, I, P, I, I, P],
     "mxk_moe_qgemm16": [I, I, I, P, I, P, P, P, P, P, I, I, I, I, P, I, P],

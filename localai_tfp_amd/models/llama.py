@@ -370,7 +370,10 @@ class LlamaModel:
     def finalize_layout(self):
         """Re-lay the dense-layer projections (and the LM head) out in the t32 tiled layout the qmm /
         qmv kernels stream (ops/quant.py tile32). After gate|up interleaving and Q|K|V fusion, which
-        work on the row layout; MoE expert stacks keep theirs (moe.py kernels). No-op on CPU / bf16 mode."""
+        work on the row layout. MoE expert stacks (gate|up interleaved per expert, down) and shared experts go t32 too
+        when every expert's rows are whole 32-row groups and K is whole super-blocks: the grouped qmm2 GEMM and the
+        grouped decode GEMV (ops/moe.py) stream them; stacks that do not qualify keep the row layout and the
+        qgemm16 grouped kernel. No-op on CPU / bf16 mode."""
         # the q8-activation decode GEMVs need block-quantised weights: a dense (F16 / BF16) checkpoint runs
         # its small batches through the 16-bit GEMM path instead
         self._gemv_ok = all(not isinstance(w, QWeight) or w.is_quant for L in self.layers
@@ -381,6 +384,8 @@ class LlamaModel:
             for w in (*L.qkv_parts, L.wo, L.wgu, L.wg, L.wu, L.wd):
                 if isinstance(w, QWeight):
                     w.to_t32()
+            if L.moe is not None:
+                L.moe.to_t32()
         if isinstance(self.lm_head, QWeight):
             self.lm_head.to_t32()  # tied embeddings follow (embed() reads either layout)
         if isinstance(self.tok_embd, QWeight) and self.tok_embd is not self.lm_head and \

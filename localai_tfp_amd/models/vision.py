@@ -43,6 +43,13 @@ class ClipVisionConfig:
     std: tuple = (0.26862954, 0.26130258, 0.27577711)
     pad_square: bool = True
     name: str = "clip-vit-l-336"
+    # LLaVA-1.6 "anyres": candidate (width, height) canvases (clip.vision.image_grid_pinpoints); empty = 1.5 single crop
+    grid_pinpoints: tuple = ()
+    # projector (clip.projector_type): "mlp" (LLaVA: CLS token, pre-LN, penultimate-layer features, mlp2x_gelu) or
+    # "gemma3" (SigLIP: no CLS / pre-LN, patch bias, post-LN, then avg-pool to tokens_per_image, RMSNorm, projection)
+    projector: str = "mlp"
+    tokens_per_image: int = 256
+    resample: str = "bicubic"
     extra: dict = field(default_factory=dict)
 
     @property
@@ -61,12 +68,73 @@ class ClipVisionConfig:
                    act="gelu" if md.get("clip.use_gelu", False) else "quick_gelu",
                    mean=tuple(float(x) for x in g("image_mean", cls.mean)),
                    std=tuple(float(x) for x in g("image_std", cls.std)),
-                   name=str(md.get("general.name", "clip")))
+                   name=str(md.get("general.name", "clip")),
+                   grid_pinpoints=_pairs(g("image_grid_pinpoints", ())),
+                   pad_square=not _pairs(g("image_grid_pinpoints", ())) and
+                   str(md.get("clip.projector_type", "mlp")) == "mlp",
+                   projector=str(md.get("clip.projector_type", "mlp")),
+                   resample="bilinear" if str(md.get("clip.projector_type", "mlp")) == "gemma3" else "bicubic")
+
+
+def _pairs(v) -> tuple:
+    """Flattened [w0, h0, w1, h1, ...] -> ((w0, h0), ...); clip.cpp stops at the first 0."""
+    vals = [int(x) for x in (v or ())]
+    out = []
+    for i in range(0, len(vals) - 1, 2):
+        if vals[i] == 0:
+            break
+        out.append((vals[i], vals[i + 1]))
+    return tuple(out)
+
+
+def select_best_resolution(size: tuple, candidates) -> tuple:
+    """clip.cpp select_best_resolution: the (w, h) canvas that keeps the most of the image's pixels after an
+    aspect-preserving downscale, ties broken by the least wasted canvas area."""
+    ow, oh = size
+    best, best_eff, best_waste = None, 0, None
+    for w, h in candidates:
+        scale = min(w / ow, h / oh)
+        dw, dh = int(ow * scale), int(oh * scale)
+        eff = min(dw * dh, ow * oh)
+        waste = w * h - eff
+        if eff > best_eff or (eff == best_eff and (best_waste is None or waste < best_waste)):
+            best, best_eff, best_waste = (w, h), eff, waste
+    return best
+
+
+def resize_and_pad(img, target: tuple):
+    """clip.cpp resize_and_pad_image: aspect-preserving bicubic resize into the (w, h) canvas, centred on black."""
+    from PIL import Image
+    tw, th = target
+    sw, sh = tw / img.width, th / img.height
+    if sw < sh:
+        nw, nh = tw, min(math.ceil(img.height * sw), th)
+    else:
+        nw, nh = min(math.ceil(img.width * sh), tw), th
+    r = img.resize((nw, nh), Image.BICUBIC)
+    out = Image.new("RGB", (tw, th), (0, 0, 0))
+    out.paste(r, ((tw - nw) // 2, (th - nh) // 2))
+    return out
 
 
 CLIP_TEST = ClipVisionConfig(image_size=56, patch=14, hidden=128, ffn=256, heads=4, layers=2, proj_hidden=256,
                              name="clip-test")
-SYNTHETIC = {"clip-vit-l-336": ClipVisionConfig(), "clip-test": CLIP_TEST}
+CLIP_TEST_ANYRES = ClipVisionConfig(image_size=56, patch=14, hidden=128, ffn=256, heads=4, layers=2, proj_hidden=256,
+                                    name="clip-test-anyres", grid_pinpoints=((56, 112), (112, 56), (112, 112)),
+                                    pad_square=False)
+GEMMA3_TEST = ClipVisionConfig(image_size=56, patch=14, hidden=128, ffn=256, heads=4, layers=2, proj_hidden=192,
+                               name="gemma3-test", projector="gemma3", tokens_per_image=4, eps=1e-6, act="gelu_tanh",
+                               mean=(0.5, 0.5, 0.5), std=(0.5, 0.5, 0.5), pad_square=False, resample="bilinear")
+# Gemma-3 mmproj (gemma-3-*-it mmproj): SigLIP-So400m/14 at 896 px, 4x4 average pool -> 256 tokens
+GEMMA3_SIGLIP = ClipVisionConfig(image_size=896, patch=14, hidden=1152, ffn=4304, heads=16, layers=27, proj_hidden=3840,
+                                 name="gemma3-siglip", projector="gemma3", tokens_per_image=256, eps=1e-6,
+                                 act="gelu_tanh", mean=(0.5, 0.5, 0.5), std=(0.5, 0.5, 0.5), pad_square=False,
+                                 resample="bilinear")
+# LLaVA-1.6 (llava-v1.6-*-mmproj): ViT-L/14-336 with the 5 anyres canvases of the published configs
+LLAVA16 = ClipVisionConfig(name="llava-v1.6-clip", pad_square=False,
+                           grid_pinpoints=((336, 672), (672, 336), (672, 672), (1008, 336), (336, 1008)))
+SYNTHETIC = {"clip-vit-l-336": ClipVisionConfig(), "clip-test": CLIP_TEST, "clip-test-anyres": CLIP_TEST_ANYRES,
+             "llava-v1.6-clip": LLAVA16, "gemma3-test": GEMMA3_TEST, "gemma3-siglip": GEMMA3_SIGLIP}
 
 
 def synthetic_clip(cfg: ClipVisionConfig, seed: int = 0) -> dict:
@@ -75,6 +143,19 @@ def synthetic_clip(cfg: ClipVisionConfig, seed: int = 0) -> dict:
 
     def r(*s, std=0.02):
         return torch.randn(*s, generator=g) * std
+    if cfg.projector == "gemma3":
+        sd = {"v.patch_embd.weight": r(H, 3, P, P), "v.patch_embd.bias": r(H),
+              "v.position_embd.weight": r(cfg.n_patches, H), "v.post_ln.weight": 1 + r(H), "v.post_ln.bias": r(H),
+              "mm.soft_emb_norm.weight": 1 + r(H), "mm.input_projection.weight": r(H, cfg.proj_hidden)}
+        for i in range(cfg.layers):
+            p = f"v.blk.{i}."
+            for n in ("attn_q", "attn_k", "attn_v", "attn_out"):
+                sd[p + n + ".weight"], sd[p + n + ".bias"] = r(H, H), r(H)
+            sd[p + "ffn_up.weight"], sd[p + "ffn_up.bias"] = r(Fd, H), r(Fd)  # fc1 (gguf-py naming)
+            sd[p + "ffn_down.weight"], sd[p + "ffn_down.bias"] = r(H, Fd), r(H)
+            for n in ("ln1", "ln2"):
+                sd[p + n + ".weight"], sd[p + n + ".bias"] = 1 + r(H), r(H)
+        return sd
     sd = {"v.patch_embd.weight": r(H, 3, P, P), "v.class_embd": r(H), "v.position_embd.weight": r(cfg.n_patches + 1, H),
           "v.pre_ln.weight": 1 + r(H), "v.pre_ln.bias": r(H),
           "mm.0.weight": r(cfg.proj_hidden, H), "mm.0.bias": r(cfg.proj_hidden),
@@ -103,8 +184,13 @@ def load_mmproj(path: str, device="cpu") -> "ClipVision":
         sd[name] = torch.from_numpy(np.ascontiguousarray(a).reshape(tuple(reversed(ti.shape))).copy()).float()
     n_blocks = len({k.split(".")[2] for k in sd if k.startswith("v.blk.")})
     cfg = ClipVisionConfig.from_gguf_metadata(r.metadata, n_blocks)
-    if str(r.metadata.get("clip.projector_type", "mlp")) != "mlp":
-        raise NotImplementedError(f"projector type {r.metadata.get('clip.projector_type')!r}")
+    if cfg.projector not in ("mlp", "gemma3"):
+        raise NotImplementedError(f"projector type {cfg.projector!r} (supported: mlp / LLaVA-1.5 and -1.6, gemma3)")
+    if cfg.projector == "gemma3":
+        cfg.proj_hidden = int(sd["mm.input_projection.weight"].shape[1])
+        cfg.act = "gelu_tanh"
+        n_tok = int(r.metadata.get("clip.vision.mm_tokens_per_image", 256) or 256)
+        cfg.tokens_per_image = n_tok
     return ClipVision(cfg, sd, device)
 
 
@@ -115,43 +201,78 @@ class ClipVision:
         self.dtype = model_dtype(device)
         dt, dev = self.dtype, self.device
         H, P = cfg.hidden, cfg.patch
-        self.patch = Dense(sd["v.patch_embd.weight"].reshape(H, 3 * P * P), None, dev, dt)
-        self.cls = sd["v.class_embd"].reshape(H).float().to(dev)
+        self.patch = Dense(sd["v.patch_embd.weight"].reshape(H, 3 * P * P), sd.get("v.patch_embd.bias"), dev, dt)
+        self.cls = sd["v.class_embd"].reshape(H).float().to(dev) if "v.class_embd" in sd else None
         self.pos = sd["v.position_embd.weight"].float().to(dev)
 
         def f32(k):
             return sd[k].float().to(dev).contiguous()
-        self.pre_ln = (f32("v.pre_ln.weight"), f32("v.pre_ln.bias"))
+        self.pre_ln = (f32("v.pre_ln.weight"), f32("v.pre_ln.bias")) if "v.pre_ln.weight" in sd else None
+        self.post_ln = (f32("v.post_ln.weight"), f32("v.post_ln.bias")) if "v.post_ln.weight" in sd else None
         self.blocks = []
         for i in range(cfg.layers):
             p = f"v.blk.{i}."
             qkv_w = torch.cat([sd[p + f"attn_{x}.weight"] for x in "qkv"], 0)
             qkv_b = torch.cat([sd[p + f"attn_{x}.bias"] for x in "qkv"], 0)
+            # fc1 (hidden -> ffn) / fc2: the LLaVA surgery scripts stored fc1 as ffn_down, gguf-py as ffn_up; pick by
+            # shape, as clip.cpp does
+            a, b = p + "ffn_down", p + "ffn_up"
+            if sd[a + ".weight"].shape[1] != H:
+                a, b = b, a
             self.blocks.append(dict(
                 ln1=(f32(p + "ln1.weight"), f32(p + "ln1.bias")), ln2=(f32(p + "ln2.weight"), f32(p + "ln2.bias")),
                 qkv=Dense(qkv_w, qkv_b, dev, dt), out=Dense(sd[p + "attn_out.weight"], sd[p + "attn_out.bias"], dev, dt),
-                fc1=Dense(sd[p + "ffn_down.weight"], sd[p + "ffn_down.bias"], dev, dt),
-                fc2=Dense(sd[p + "ffn_up.weight"], sd[p + "ffn_up.bias"], dev, dt)))
-        self.mm0 = Dense(sd["mm.0.weight"], sd["mm.0.bias"], dev, dt)
-        self.mm2 = Dense(sd["mm.2.weight"], sd["mm.2.bias"], dev, dt)
+                fc1=Dense(sd[a + ".weight"], sd[a + ".bias"], dev, dt),
+                fc2=Dense(sd[b + ".weight"], sd[b + ".bias"], dev, dt)))
+        if cfg.projector == "gemma3":
+            self.soft_norm = f32("mm.soft_emb_norm.weight")  # (1 + w) as the gguf converter stores it
+            self.mm_proj = Dense(sd["mm.input_projection.weight"].t().contiguous(), None, dev, dt)
+        else:
+            self.mm0 = Dense(sd["mm.0.weight"], sd["mm.0.bias"], dev, dt)
+            self.mm2 = Dense(sd["mm.2.weight"], sd["mm.2.bias"], dev, dt)
 
     # ---------------------------------------------------------------- preprocessing
-    def preprocess(self, img) -> torch.Tensor:
-        """PIL image / encoded bytes / base64 string -> normalised [3, S, S] fp32 (clip_image_preprocess)."""
+    @staticmethod
+    def load_image(img):
         from PIL import Image
         if isinstance(img, str):
             s = img.split(",", 1)[1] if img.startswith("data:") else img
             img = base64.b64decode(s)
         if isinstance(img, (bytes, bytearray)):
             img = Image.open(io.BytesIO(img))
-        img = img.convert("RGB")
+        return img.convert("RGB")
+
+    def normalise(self, img) -> torch.Tensor:
+        c = self.cfg
+        x = torch.from_numpy(np.asarray(img, dtype=np.float32) / 255.0).permute(2, 0, 1)
+        return (x - torch.tensor(c.mean)[:, None, None]) / torch.tensor(c.std)[:, None, None]
+
+    def anyres_crops(self, img) -> tuple[list, tuple]:
+        """LLaVA-1.6 crops (clip.cpp clip_image_preprocess, grid pinpoints): the whole image bicubic-resized to one
+        crop, then the best canvas (select_best_resolution) cut into image_size crops in row-major order.
+        -> ([crops as [3, S, S]], (grid columns, grid rows))."""
+        from PIL import Image
+        img = self.load_image(img)
+        S = self.cfg.image_size
+        w, h = select_best_resolution((img.width, img.height), self.cfg.grid_pinpoints)
+        canvas = resize_and_pad(img, (w, h))
+        crops = [self.normalise(img.resize((S, S), Image.BICUBIC))]
+        for y in range(0, h, S):
+            for x in range(0, w, S):
+                crops.append(self.normalise(canvas.crop((x, y, x + S, y + S))))
+        return crops, (w // S, h // S)
+
+    def preprocess(self, img) -> torch.Tensor:
+        """PIL image / encoded bytes / base64 string -> normalised [3, S, S] fp32 (clip_image_preprocess)."""
+        from PIL import Image
+        img = self.load_image(img)
         c = self.cfg
         if c.pad_square and img.width != img.height:
             side = max(img.width, img.height)
             bg = Image.new("RGB", (side, side), tuple(int(255 * m) for m in c.mean))
             bg.paste(img, ((side - img.width) // 2, (side - img.height) // 2))
             img = bg
-        img = img.resize((c.image_size, c.image_size), Image.BICUBIC)
+        img = img.resize((c.image_size, c.image_size), Image.BILINEAR if c.resample == "bilinear" else Image.BICUBIC)
         x = torch.from_numpy(np.asarray(img, dtype=np.float32) / 255.0).permute(2, 0, 1)
         return (x - torch.tensor(c.mean)[:, None, None]) / torch.tensor(c.std)[:, None, None]
 
@@ -159,6 +280,8 @@ class ClipVision:
     def _act(self, y: torch.Tensor) -> torch.Tensor:
         if self.cfg.act == "quick_gelu":
             return y * torch.sigmoid(1.702 * y)
+        if self.cfg.act == "gelu_tanh":
+            return F.gelu(y, approximate="tanh")
         return F.gelu(y)
 
     @torch.no_grad()
@@ -170,9 +293,12 @@ class ClipVision:
         x = pixels.to(self.device, torch.float32)
         cols = F.unfold(x, P, stride=P).transpose(1, 2).reshape(-1, 3 * P * P)  # [B*np, 3PP]
         pe = self.patch.f32(cols.to(self.dtype)).view(B, c.n_patches, H)
-        h = torch.cat([self.cls.view(1, 1, H).expand(B, 1, H), pe], 1) + self.pos[None]
+        h = (torch.cat([self.cls.view(1, 1, H).expand(B, 1, H), pe], 1) if self.cls is not None else pe) + self.pos[None]
         S = h.shape[1]
-        h = F.layer_norm(h.reshape(B * S, H), (H,), *self.pre_ln, c.eps).contiguous()  # residual stream (fp32)
+        h = h.reshape(B * S, H)
+        if self.pre_ln is not None:
+            h = F.layer_norm(h, (H,), *self.pre_ln, c.eps)
+        h = h.contiguous()  # residual stream (fp32)
         hd = H // c.heads
         xa = torch.empty(B * S, H, dtype=self.dtype, device=self.device)
         attn = torch.empty(B * S, H, dtype=self.dtype, device=self.device)
@@ -184,16 +310,49 @@ class ClipVision:
             blk["out"].acc(attn, h)
             K.layernorm(h, *blk["ln2"], c.eps, xa)
             blk["fc2"].acc(self._act(blk["fc1"](xa)), h)
+        if c.projector == "gemma3":
+            return self._gemma3_project(h, B)
         feats = h.view(B, S, H)[:, 1:].reshape(-1, H).to(self.dtype)
         y = self.mm2.f32(F.gelu(self.mm0(feats)))
         return y.view(B, c.n_patches, c.proj_hidden)
 
+    def _gemma3_project(self, h: torch.Tensor, B: int) -> torch.Tensor:
+        """clip.cpp PROJECTOR_TYPE_GEMMA3: post-LN, [side x side] patch grid average-pooled to tokens_per_image,
+        RMSNorm with the (1 + w) soft-embedding norm, then x @ mm_input_projection (-> LLM hidden)."""
+        c = self.cfg
+        H = c.hidden
+        h = F.layer_norm(h, (H,), *self.post_ln, c.eps)
+        side, ts = c.image_size // c.patch, int(round(c.tokens_per_image ** 0.5))
+        k = side // ts
+        g = h.view(B, side, side, H).permute(0, 3, 1, 2)
+        pooled = F.avg_pool2d(g, k, k).flatten(2).transpose(1, 2).reshape(-1, H)  # [B * tokens, H]
+        normed = pooled * torch.rsqrt(pooled.pow(2).mean(-1, keepdim=True) + c.eps) * self.soft_norm
+        y = self.mm_proj.f32(normed.to(self.dtype))
+        return y.view(B, c.tokens_per_image, c.proj_hidden)
+
+    @property
+    def tokens_per_image(self) -> int:
+        return self.cfg.tokens_per_image if self.cfg.projector == "gemma3" else self.cfg.n_patches
+
     def embed_images(self, images: list) -> list[torch.Tensor]:
         if not images:
             return []
+        if self.cfg.grid_pinpoints:
+            return [self.embed_anyres(im) for im in images]
         px = torch.stack([self.preprocess(im) for im in images])
         out = self.encode(px)
         return [out[i] for i in range(out.shape[0])]
+
+    def embed_anyres(self, img) -> torch.Tensor:
+        """LLaVA-1.6 as llava.cpp clip_llava_handle_patches runs it: the whole-image crop's n_patches embeddings,
+        then the grid crops' embeddings re-ordered into the raster of the whole canvas (grid row, patch row, grid
+        column, patch column) — no unpadding and no image_newline rows (llava.cpp: "append without newline tokens")."""
+        crops, (gw, gh) = self.anyres_crops(img)
+        feats = self.encode(torch.stack(crops))  # [1 + gw gh, n, H]
+        side = self.cfg.image_size // self.cfg.patch
+        Hp = feats.shape[-1]
+        grid = feats[1:].view(gh, gw, side, side, Hp).permute(0, 2, 1, 3, 4).reshape(gh * side * gw * side, Hp)
+        return torch.cat([feats[0], grid], 0)
 
 
 # ------------------------------------------------------------------------------------------------

@@ -4,11 +4,18 @@ Parity target: llama.cpp's build_moe_ffn as the reference's llama-cpp backend ru
 softmax, top-k, optional weight renormalisation, ggml_mul_mat_id over the stacked
 `ffn_{gate,up,down}_exps` tensors, optional shared expert with a sigmoid gate for Qwen2-MoE).
 
-GPU path (all device-side, hipGraph-capturable — csrc/kernels/moe.hip + qgemm16.hip grouped mode):
-    logits = x W_router^T (fp32)  ->  moe_route (softmax + top-k per wave)  ->  moe_sort (counting
-    sort of token-expert pairs, per-expert tile prefix)  ->  grouped SwiGLU GEMM over the stacked,
-    16-row-interleaved gate|up experts (A rows gathered by index)  ->  grouped down GEMM into a
-    [P, H] fp32 buffer  ->  moe_combine (h += sum_j w_j * y_j, fixed order).
+GPU path (all device-side, hipGraph-capturable):
+    moe_router (moe.hip: the router GEMV over 8 tokens per workgroup with the fp32 router rows read once, logits in
+    LDS, softmax + top-k per wave in the same launch) -> then, with the expert stacks in the t32 layout
+    (models/llama.py finalize_layout; 16-row-interleaved gate|up per expert):
+      * decode (P = T k pairs <= GEMV_MAX_PAIRS): qmv_moe (qmv.hip) — one workgroup per (pair, 32 columns of its
+        expert), q8 activations, gate|up SwiGLU into [P, F] then down into [P, H] fp32, rows in pair order;
+      * larger batches: moe_sort (counting sort of the pairs by expert, per-expert tile prefix) -> grouped qmm2
+        (qmm2_impl.h Q2Group: 32- / 64-row MFMA tiles per expert, A rows gathered through the sort) for gate|up
+        SwiGLU and down;
+    -> moe_combine (h += sum_j w_j * y_j, fixed order). Expert stacks that do not fit the t32 layout (a row count
+    per expert or K that is not whole 32-row groups / 256-k super-blocks) keep the row layout and the qgemm16
+    grouped kernel.
 CPU path: the same math with dequantised fp32 expert weights (numerics oracle).
 """
 from __future__ import annotations
@@ -21,6 +28,8 @@ from .. import _native as N
 from .linear import ACT_DTYPE, EPI_F32, EPI_SWIGLU, QWeight, qmatmul
 
 E16_F32, E16_SWIGLU = 0, 3
+MOE_T32 = (12, 13, 14, 8)  # Q4_K, Q5_K, Q6_K, Q8_0: block formats with grouped t32 kernels (qmv_moe, qmm2 grouped)
+GEMV_MAX_PAIRS = 64  # token-expert pairs up to which the grouped decode GEMV runs (above: the grouped qmm2 GEMM)
 
 
 @dataclass
@@ -41,6 +50,7 @@ class MoEWeights:
     sh_inp: torch.Tensor | None = None  # fp32 [H] sigmoid gate of the shared expert
     e0: int = 0  # expert parallelism: this rank holds experts [e0, e0 + n_local) of the n_expert
     n_local: int = 0  # 0 = all
+    t32: bool = False  # gate_up / down re-laid in the t32 layout (grouped qmv / qmm2 kernels)
 
     def nbytes(self) -> int:
         n = self.router.numel() * 4
@@ -49,6 +59,20 @@ class MoEWeights:
             if w is not None:
                 n += w.nbytes()
         return n
+
+    def to_t32(self) -> bool:
+        """Re-lay gate|up and down (and the shared expert) out in the t32 layout when every expert's rows are whole
+        32-row groups and K whole 256-k super-blocks of a format the grouped kernels decode; returns self.t32."""
+        El = self.n_local or self.n_expert
+        gu, d = self.gate_up, self.down
+        if (not self.t32 and gu is not None and gu.is_quant and d.is_quant and gu.data.is_cuda
+                and (2 * self.ffn) % 32 == 0 and d.N % (32 * El) == 0 and gu.K % 256 == 0 and d.K % 256 == 0
+                and ACT_DTYPE == torch.float16 and int(gu.qtype) in MOE_T32 and int(d.qtype) in MOE_T32):
+            self.t32 = gu.to_t32() and d.to_t32()
+        for w in (self.sh_gate_up, self.sh_down, self.sh_gate, self.sh_up):
+            if isinstance(w, QWeight):
+                w.to_t32()
+        return self.t32
 
     def build_bf16_cache(self):
         for w in (self.sh_gate_up, self.sh_down):
@@ -78,13 +102,24 @@ def moe_ffn(W: MoEWeights, x: torch.Tensor, h: torch.Tensor) -> torch.Tensor:
     H = h.shape[1]
     if not x.is_cuda:
         return _moe_ref(W, x.float(), h)
-    logits = x.float() @ W.router.t()
     ids = torch.empty(T, k, dtype=torch.int32, device=x.device)
     wts = torch.empty(T, k, dtype=torch.float32, device=x.device)
     st = N.stream_ptr()
-    N.kcall("mxk_moe_route", logits.data_ptr(), logits.stride(0), T, E, k, int(W.renorm), ids.data_ptr(),
-            wts.data_ptr(), st)
+    if x.dtype in (torch.float16, torch.bfloat16) and H % 256 == 0 and x.stride(1) == 1 and x.stride(0) % 8 == 0 \
+            and W.router.is_contiguous():
+        N.ensure_act(x.dtype)
+        N.kcall("mxk_moe_router", x.data_ptr(), x.stride(0), W.router.data_ptr(), T, H, E, k, int(W.renorm),
+                ids.data_ptr(), wts.data_ptr(), st)
+    else:
+        logits = x.float() @ W.router.t()
+        N.kcall("mxk_moe_route", logits.data_ptr(), logits.stride(0), T, E, k, int(W.renorm), ids.data_ptr(),
+                wts.data_ptr(), st)
     El = W.n_local or E
+    if W.t32:
+        _experts_t32(W, x, h, ids, wts, El)
+        if W.sh_down is not None:
+            _shared(W, x, h)
+        return h
     y_zero = False
     if El != E:
         # expert parallelism: pairs routed to other ranks' experts go to a null bucket El (sorted last,
@@ -119,6 +154,45 @@ def moe_ffn(W: MoEWeights, x: torch.Tensor, h: torch.Tensor) -> torch.Tensor:
     if W.sh_down is not None:
         _shared(W, x, h)
     return h
+
+
+def _experts_t32(W: MoEWeights, x: torch.Tensor, h: torch.Tensor, ids: torch.Tensor, wts: torch.Tensor, El: int):
+    """Routed experts on the t32 stacks: grouped decode GEMV (small P) or grouped qmm2 (sorted pairs)."""
+    T, k, F, E = x.shape[0], W.n_used, W.ffn, W.n_expert
+    H = h.shape[1]
+    P = T * k
+    st = N.stream_ptr()
+    gu, d = W.gate_up, W.down
+    N.ensure_act(x.dtype)
+    act = torch.empty(P, F, dtype=x.dtype, device=x.device)
+    # rows of pairs routed to another rank's experts stay zero (weight 0 in the combine)
+    y = (torch.zeros if El != E else torch.empty)(P, H, dtype=torch.float32, device=x.device)
+    if P <= GEMV_MAX_PAIRS:
+        N.kcall("mxk_qmv_moe", int(gu.qtype), E16_SWIGLU, gu.data.data_ptr(), 2 * F, gu.K, ids.data_ptr(), P, W.e0,
+                El, x.data_ptr(), x.stride(0), k, act.data_ptr(), act.stride(0), st)
+        N.kcall("mxk_qmv_moe", int(d.qtype), E16_F32, d.data.data_ptr(), H, d.K, ids.data_ptr(), P, W.e0, El,
+                act.data_ptr(), act.stride(0), 1, y.data_ptr(), y.stride(0), st)
+        N.kcall("mxk_moe_combine", y.data_ptr(), y.stride(0), None, wts.data_ptr(), T, k, H, h.data_ptr(),
+                h.stride(0), 1, st)
+        return
+    if El != E:  # expert parallelism: other ranks' pairs go to a null bucket El, sorted last, never computed
+        loc = ids - W.e0
+        off_rank = (loc < 0) | (loc >= El)
+        ids = torch.where(off_rank, torch.full_like(loc, El), loc)
+    wm = 1 if P <= 32 * El else 2
+    Eb = El + (1 if El != E else 0)
+    off = torch.empty(Eb + 1, dtype=torch.int32, device=x.device)
+    tiles = torch.empty(Eb + 1, dtype=torch.int32, device=x.device)
+    stok = torch.empty(P, dtype=torch.int32, device=x.device)
+    inv = torch.empty(P, dtype=torch.int32, device=x.device)
+    N.kcall("mxk_moe_sort", ids.data_ptr(), P, k, Eb, 32 * wm, off.data_ptr(), tiles.data_ptr(), stok.data_ptr(),
+            inv.data_ptr(), st)
+    N.kcall("mxk_qmm2_grouped", int(gu.qtype), E16_SWIGLU, wm, x.data_ptr(), x.stride(0), stok.data_ptr(),
+            gu.data.data_ptr(), P, El, 2 * F, gu.K, tiles.data_ptr(), off.data_ptr(), act.data_ptr(), act.stride(0), st)
+    N.kcall("mxk_qmm2_grouped", int(d.qtype), E16_F32, wm, act.data_ptr(), act.stride(0), None, d.data.data_ptr(), P,
+            El, H, d.K, tiles.data_ptr(), off.data_ptr(), y.data_ptr(), y.stride(0), st)
+    N.kcall("mxk_moe_combine", y.data_ptr(), y.stride(0), inv.data_ptr(), wts.data_ptr(), T, k, H, h.data_ptr(),
+            h.stride(0), 1, st)
 
 
 def _shared(W: MoEWeights, x: torch.Tensor, h: torch.Tensor):

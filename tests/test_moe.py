@@ -135,11 +135,15 @@ def _rand_qweight(rng, qt, N, K, dev):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("t32", [True, False])
 @pytest.mark.parametrize("E,k,H,F,qt,renorm", [(8, 2, 512, 512, QType.Q4_K, True),
                                                (128, 8, 256, 768, QType.Q4_K, True),
                                                (16, 4, 256, 256, QType.Q6_K, False),
-                                               (8, 2, 256, 256, QType.Q8_0, True)])
-def test_moe_ffn_gpu_matches_fp32(E, k, H, F, qt, renorm):
+                                               (8, 2, 256, 256, QType.Q8_0, True),
+                                               (16, 4, 512, 256, QType.Q5_K, True)])
+def test_moe_ffn_gpu_matches_fp32(E, k, H, F, qt, renorm, t32):
+    """The GPU MoE layer (fused router + route, then either the t32 kernels — grouped decode GEMV for <= 64 pairs,
+    sorted grouped qmm2 above — or the row-layout qgemm16 grouped kernel) against the fp32 CPU path."""
     from localai_tfp_amd.ops.linear import ACT_DTYPE, interleave_gate_up
     rng = np.random.default_rng(E + k)
     raws = {n: random_quantized(rng, qt, r, c, std=0.05).reshape(r, -1)
@@ -155,7 +159,11 @@ def test_moe_ffn_gpu_matches_fp32(E, k, H, F, qt, renorm):
                              gate_up=interleave_gate_up(g, u) if gpu else None, down=d, n_expert=E, n_used=k,
                              ffn=F, renorm=renorm)
     wc, wg = build("cpu"), build("cuda")
-    for T in (1, 3, 37, 300):
+    if t32:
+        assert wg.to_t32()
+    elif qt == QType.Q5_K:
+        pytest.skip("Q5_K expert stacks run only on the t32 kernels")
+    for T in (1, 3, 16, 37, 300):
         x = torch.randn(T, H).to(ACT_DTYPE)
         h0 = torch.randn(T, H)
         ref = MO.moe_ffn(wc, x.float(), h0.clone())
@@ -193,8 +201,9 @@ def test_moe_model_gpu_matches_cpu_and_engine():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("t32", [True, False])
 @pytest.mark.parametrize("tp", [2, 4])
-def test_moe_expert_parallel_gpu(tp):
+def test_moe_expert_parallel_gpu(tp, t32):
     """Expert parallelism (tensor-parallel MoE layers): every rank's share computed by the GPU kernels
     with the off-rank pairs in the null bucket; the shares sum to the unsharded MoE output."""
     from localai_tfp_amd.ops.linear import ACT_DTYPE, interleave_gate_up
@@ -208,8 +217,11 @@ def test_moe_expert_parallel_gpu(tp):
         g = QWeight.from_ggml(np.ascontiguousarray(raws["g"][e0 * F:(e0 + el) * F]), int(qt), el * F, H, "cuda")
         u = QWeight.from_ggml(np.ascontiguousarray(raws["u"][e0 * F:(e0 + el) * F]), int(qt), el * F, H, "cuda")
         d = QWeight.from_ggml(np.ascontiguousarray(raws["d"][e0 * H:(e0 + el) * H]), int(qt), el * H, F, "cuda")
-        return MO.MoEWeights(router=router.cuda(), gate=None, up=None, gate_up=interleave_gate_up(g, u), down=d,
-                             n_expert=E, n_used=k, ffn=F, renorm=True, e0=e0, n_local=0 if el == E else el)
+        w = MO.MoEWeights(router=router.cuda(), gate=None, up=None, gate_up=interleave_gate_up(g, u), down=d,
+                          n_expert=E, n_used=k, ffn=F, renorm=True, e0=e0, n_local=0 if el == E else el)
+        if t32:
+            assert w.to_t32()
+        return w
     full = build(0, E)
     shards = [build(r * E // tp, E // tp) for r in range(tp)]
     for T in (1, 5, 64):
