@@ -4,9 +4,11 @@ from __future__ import annotations
 from dataclasses import dataclass, field
 
 # llama.cpp rope type per architecture: NORM (adjacent pairs) vs NEOX (half split)
-NEOX_ARCHS = {"qwen2", "qwen2moe", "qwen3", "qwen3moe", "phi2", "phi3", "gemma", "gemma2", "gemma3", "starcoder2",
+NEOX_ARCHS = {"qwen2", "qwen2vl", "qwen2moe", "qwen3", "qwen3moe", "phi2", "phi3", "gemma", "gemma2", "gemma3", "starcoder2",
               "falcon", "gptneox", "stablelm", "olmo2", "bert", "nomic-bert", "jina-bert-v2"}
-BIAS_QKV_ARCHS = {"qwen2", "qwen2moe"}
+# qwen2vl (Qwen2-VL / Qwen2.5-VL text model): M-RoPE, whose three position components coincide for text tokens, so
+# it runs as NEOX RoPE (image embeddings take the next sequential positions, as the reference's llava path decodes them)
+BIAS_QKV_ARCHS = {"qwen2", "qwen2vl", "qwen2moe"}
 
 
 @dataclass

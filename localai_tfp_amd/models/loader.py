@@ -21,7 +21,7 @@ SYNTHETIC = {"llama3-8b": C.LLAMA3_8B, "llama3-70b": C.LLAMA3_70B, "llama32-1b":
              "tiny-draft": C.tiny_config(n_layers=1, name="tiny-draft"),
              "tiny-4l": C.tiny_config(n_layers=4, name="tiny-4l"),  # layer-split tests  # speculative-decoding draft for "tiny"
              "tiny-moe": C.tiny_config(arch="qwen3moe", n_expert=8, n_expert_used=2, expert_ffn=256, qk_norm=True)}
-SUPPORTED_ARCHS = {"llama", "mistral", "qwen2", "qwen3", "qwen2moe", "qwen3moe", "phi3", "gemma", "gemma2", "gemma3", "granite", "internlm2", "deci", "exaone", "olmo", "minicpm",
+SUPPORTED_ARCHS = {"llama", "mistral", "qwen2", "qwen2vl", "qwen3", "qwen2moe", "qwen3moe", "phi3", "gemma", "gemma2", "gemma3", "granite", "internlm2", "deci", "exaone", "olmo", "minicpm",
                    "smollm", "codellama"}
 
 

@@ -122,7 +122,7 @@ CLIP_TEST = ClipVisionConfig(image_size=56, patch=14, hidden=128, ffn=256, heads
 CLIP_TEST_ANYRES = ClipVisionConfig(image_size=56, patch=14, hidden=128, ffn=256, heads=4, layers=2, proj_hidden=256,
                                     name="clip-test-anyres", grid_pinpoints=((56, 112), (112, 56), (112, 112)),
                                     pad_square=False)
-GEMMA3_TEST = ClipVisionConfig(image_size=56, patch=14, hidden=128, ffn=256, heads=4, layers=2, proj_hidden=192,
+GEMMA3_TEST = ClipVisionConfig(image_size=56, patch=14, hidden=128, ffn=256, heads=4, layers=2, proj_hidden=256,
                                name="gemma3-test", projector="gemma3", tokens_per_image=4, eps=1e-6, act="gelu_tanh",
                                mean=(0.5, 0.5, 0.5), std=(0.5, 0.5, 0.5), pad_square=False, resample="bilinear")
 # Gemma-3 mmproj (gemma-3-*-it mmproj): SigLIP-So400m/14 at 896 px, 4x4 average pool -> 256 tokens
@@ -171,13 +171,25 @@ def synthetic_clip(cfg: ClipVisionConfig, seed: int = 0) -> dict:
     return sd
 
 
-def load_mmproj(path: str, device="cpu") -> "ClipVision":
+QWEN_VL_PROJECTORS = ("qwen2vl_merger", "qwen2.5vl_merger", "qwen25vl", "qwen2vl")
+
+
+def load_mmproj(path: str, device="cpu"):
+    """An mmproj GGUF (clip.projector_type mlp / gemma3 -> ClipVision; qwen2vl_merger / qwen2.5vl_merger ->
+    models/qwen_vl.QwenVLVision) or `synthetic:<name>`."""
     if path.startswith("synthetic:"):
-        cfg = SYNTHETIC[path.split(":", 1)[1]]
-        return ClipVision(cfg, synthetic_clip(cfg), device)
+        name = path.split(":", 1)[1]
+        if name.startswith("qwen"):
+            from .qwen_vl import load_qwen_vl
+            return load_qwen_vl(path, device)
+        cfg = SYNTHETIC[name]
+        return ClipVision(cfg, synthetic_clip(cfg, seed=0), device)
     from ..formats.gguf import GGUFReader
     from ..ops.quant import dequantize
     r = GGUFReader(path)
+    if str(r.metadata.get("clip.projector_type", "mlp")) in QWEN_VL_PROJECTORS:
+        from .qwen_vl import load_qwen_vl
+        return load_qwen_vl(path, device)
     sd = {}
     for name, ti in r.tensors.items():
         a = dequantize(r.tensor_bytes(name), ti.qtype, ti.shape)
@@ -331,6 +343,10 @@ class ClipVision:
         return y.view(B, c.tokens_per_image, c.proj_hidden)
 
     @property
+    def proj_hidden(self) -> int:
+        return self.cfg.proj_hidden
+
+    @property
     def tokens_per_image(self) -> int:
         return self.cfg.tokens_per_image if self.cfg.projector == "gemma3" else self.cfg.n_patches
 
@@ -357,6 +373,48 @@ class ClipVision:
 
 # ------------------------------------------------------------------------------------------------
 # prompt splicing (grpc-server.cpp:900-944)
+_MEDIA = None
+
+
+def split_media(prompt: str, n_images: int, n_videos: int) -> list:
+    """Prompt -> text pieces and ("img" | "vid", index) markers: `[img-N]` / `[vid-N]` (llama.cpp worker style) or
+    the Qwen2-VL chat template's `<|image_pad|>` / `<|video_pad|>` (the i-th pad is medium i, the vLLM style).
+    Without any marker the media precede the text (images, then videos)."""
+    import re
+    global _MEDIA
+    if _MEDIA is None:
+        _MEDIA = re.compile(r"\[img-([^\]]*)\]|\[vid-([^\]]*)\]|<\|image_pad\|>|<\|video_pad\|>")
+    out, pos, ni, nv = [], 0, 0, 0
+    for m in _MEDIA.finditer(prompt):
+        out.append(prompt[pos:m.start()])
+        tok = m.group(0)
+        if tok == "<|image_pad|>":
+            kind, idx = "img", ni
+            ni += 1
+        elif tok == "<|video_pad|>":
+            kind, idx = "vid", nv
+            nv += 1
+        else:
+            kind = "img" if tok.startswith("[img") else "vid"
+            try:
+                idx = int(m.group(1) if kind == "img" else m.group(2))
+            except ValueError:
+                raise ValueError(f"Invalid {'image' if kind == 'img' else 'video'} number id in prompt") from None
+        lim = n_images if kind == "img" else n_videos
+        if not 0 <= idx < lim:
+            raise ValueError(f"{'Image' if kind == 'img' else 'Video'} with id: {idx}, not found.")
+        out.append((kind, idx))
+        pos = m.end()
+    out.append(prompt[pos:])
+    if len(out) == 1 and (n_images or n_videos):
+        media = [("img", i) for i in range(n_images)] + [("vid", i) for i in range(n_videos)]
+        out = [""]
+        for md in media:
+            out += [md, ""]
+        out[-1] = prompt
+    return out
+
+
 def split_prompt(prompt: str, n_images: int) -> list:
     """'a [img-0] b [img-1] c' -> ['a ', 0, ' b ', 1, ' c']; ids must be < n_images."""
     out, pos = [], 0

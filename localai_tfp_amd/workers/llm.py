@@ -262,8 +262,8 @@ class LLMServicer(BackendServicer):
                 if not mp.startswith("synthetic:") and not os.path.isabs(mp) and request.ModelPath:
                     mp = os.path.join(request.ModelPath, mp)
                 self.vision = load_mmproj(mp, self.device)
-                if self.vision.cfg.proj_hidden != mcfg.hidden:
-                    raise ValueError(f"mmproj projects to {self.vision.cfg.proj_hidden} but the LLM hidden size is "
+                if self.vision.proj_hidden != mcfg.hidden:
+                    raise ValueError(f"mmproj projects to {self.vision.proj_hidden} but the LLM hidden size is "
                                      f"{mcfg.hidden}; make sure that you use the correct mmproj file")
             draft = None
             if request.DraftModel and self.tp is None:
@@ -317,24 +317,24 @@ class LLMServicer(BackendServicer):
         return self.tok.encode(text, add_special=special)
 
     def _mm_prompt(self, r) -> tuple[list[int], list]:
-        """Images: encode with the CLIP tower + projector and splice the embeddings where the prompt
-        has `[img-N]` (grpc-server.cpp:900-944; without markers the images precede the prompt, as
-        the reference's input_suffix handling does). Placeholder rows use token id 0."""
-        from ..models.vision import split_prompt
+        """Images (and, for a Qwen2-VL-family projector, videos as frame lists: vLLM's multi_modal_data["video"],
+        backend/python/vllm/backend.py:238-252): encode with the vision tower + projector and splice the embeddings
+        where the prompt has `[img-N]` / `[vid-N]` or the Qwen template's image / video pads (grpc-server.cpp:900-944;
+        without markers the media precede the prompt, as the reference's input_suffix handling does). Placeholder
+        rows use token id 0."""
+        from ..models.vision import split_media
         text, special = self._prompt_text(r)
         imgs = list(r.Images)
-        parts = split_prompt(text, len(imgs))
-        if len(parts) == 1 and imgs:  # no markers: images first, then the prompt
-            parts = [""]
-            for i in range(len(imgs)):
-                parts += [i, ""]
-            parts[-1] = text
-        embs = self.vision.embed_images(imgs)
+        vids = list(r.Videos) if hasattr(self.vision, "embed_video") else []
+        parts = split_media(text, len(imgs), len(vids))
+        embs = {("img", i): e for i, e in enumerate(self.vision.embed_images(imgs))}
+        for i, v in enumerate(vids):
+            embs[("vid", i)] = self.vision.embed_video([v])
         ids: list[int] = []
         mm = []
         first = True
         for part in parts:
-            if isinstance(part, int):
+            if isinstance(part, tuple):
                 e = embs[part]
                 mm.append((len(ids), e))
                 ids.extend([0] * e.shape[0])
@@ -366,7 +366,7 @@ class LLMServicer(BackendServicer):
 
     def _request(self, r) -> Request:
         mm = []
-        if len(r.Images) and self.vision is not None:
+        if (len(r.Images) or (len(r.Videos) and hasattr(self.vision, "embed_video"))) and self.vision is not None:
             if self.tp is not None:
                 raise ValueError("images with a tensor-parallel LLM worker are not supported")
             ids, mm = self._mm_prompt(r)
@@ -381,9 +381,11 @@ class LLMServicer(BackendServicer):
         req.n_keep = int(r.NKeep) if r.NKeep > 0 else 0
         if r.Grammar:
             req.grammar = self._grammar(r.Grammar)
-        if (len(r.Images) and self.vision is None) or len(r.Videos) or len(r.Audios):
-            log.warning("ignoring %d images / %d videos / %d audios: this model has no multimodal projector",
-                        len(r.Images), len(r.Videos), len(r.Audios))
+        if (len(r.Images) and self.vision is None) or (len(r.Videos) and not hasattr(self.vision, "embed_video")) \
+                or len(r.Audios):
+            log.warning("ignoring %d images / %d videos / %d audios: this model has no projector for them",
+                        len(r.Images) if self.vision is None else 0,
+                        len(r.Videos) if not hasattr(self.vision, "embed_video") else 0, len(r.Audios))
         return req
 
     @staticmethod

@@ -252,3 +252,146 @@ def test_gemma3_mmproj_gguf_roundtrip(tmp_path):
     px = torch.stack([ref.preprocess(_png(7))])
     assert torch.allclose(vis.encode(px), ref.encode(px), atol=1e-5)
     assert vis.embed_images([_png(2)])[0].shape == (cfg.tokens_per_image, cfg.proj_hidden)
+
+
+# ------------------------------------------------------------------------------------------------ Qwen2.5-VL
+def _qwen_hf(cfg):
+    from transformers.models.qwen2_5_vl.configuration_qwen2_5_vl import Qwen2_5_VLVisionConfig
+    from transformers.models.qwen2_5_vl.modeling_qwen2_5_vl import Qwen2_5_VisionTransformerPretrainedModel
+    vc = Qwen2_5_VLVisionConfig(depth=cfg.depth, hidden_size=cfg.hidden, intermediate_size=cfg.ffn,
+                                num_heads=cfg.heads, out_hidden_size=cfg.out_hidden, window_size=cfg.window,
+                                fullatt_block_indexes=list(cfg.fullatt), patch_size=cfg.patch,
+                                spatial_merge_size=cfg.merge, temporal_patch_size=cfg.temporal, hidden_act="silu")
+    vc._attn_implementation = "eager"
+    torch.manual_seed(0)
+    m = Qwen2_5_VisionTransformerPretrainedModel(vc).eval()
+    with torch.no_grad():
+        for p in m.parameters():
+            p.add_(torch.randn_like(p) * 0.02)
+    return m
+
+
+@pytest.mark.parametrize("size", [(84, 56), (140, 100)])
+def test_qwen25vl_vision_matches_transformers(size):
+    """Qwen2.5-VL image embeddings: patch GEMM, 2-D RoPE, window / full attention blocks, SwiGLU MLP, patch merger
+    and the window-order round trip against transformers' Qwen2_5_VisionTransformerPretrainedModel (same weights,
+    same flattened patches); the preprocessing against Qwen2VLImageProcessor's pixel values and grid."""
+    from PIL import Image
+    from localai_tfp_amd.models import qwen_vl as QV
+    cfg = QV.QWEN25VL_TEST
+    hm = _qwen_hf(cfg)
+    ours = QV.QwenVLVision(cfg, hm.state_dict(), "cpu")
+    rng = np.random.default_rng(size[0])
+    im = Image.fromarray(rng.integers(0, 255, (size[1], size[0], 3), dtype=np.uint8))
+    px, grid = ours.patches([im])
+    try:
+        from transformers import Qwen2VLImageProcessor
+        pr = Qwen2VLImageProcessor(min_pixels=cfg.min_pixels, max_pixels=cfg.max_pixels, patch_size=cfg.patch,
+                                   merge_size=cfg.merge, temporal_patch_size=cfg.temporal)
+        ref_in = pr(images=[im], return_tensors="pt")
+        assert tuple(ref_in["image_grid_thw"][0].tolist()) == grid
+        assert float((ref_in["pixel_values"] - px).abs().max()) < 0.05  # resize implementations differ slightly
+    except ImportError:
+        pass
+    with torch.no_grad():
+        out = hm(px, grid_thw=torch.tensor([grid]))
+    ref = out.pooler_output if hasattr(out, "pooler_output") else out
+    got = ours.encode_patches(px, grid)
+    assert got.shape == ref.shape == (grid[0] * grid[1] * grid[2] // 4, cfg.out_hidden)
+    assert torch.allclose(got, ref, atol=2e-4, rtol=2e-4), float((got - ref).abs().max())
+
+
+def test_qwen25vl_video_frames_and_gguf_names():
+    """A video as a frame list: frame pairs become temporal patches (grid_t = frames / 2), matching transformers on the
+    same patches; and the clip.cpp-style tensor names map onto the same tower."""
+    from PIL import Image
+    from localai_tfp_amd.models import qwen_vl as QV
+    cfg = QV.QWEN25VL_TEST
+    hm = _qwen_hf(cfg)
+    hs = hm.state_dict()
+    ours = QV.QwenVLVision(cfg, hs, "cpu")
+    rng = np.random.default_rng(3)
+    frames = [Image.fromarray(rng.integers(0, 255, (56, 84, 3), dtype=np.uint8)) for _ in range(4)]
+    px, grid = ours.patches(frames)
+    assert grid == (2, 4, 6)
+    with torch.no_grad():
+        out = hm(px, grid_thw=torch.tensor([grid]))
+    ref = out.pooler_output if hasattr(out, "pooler_output") else out
+    assert torch.allclose(ours.embed_video(frames), ref, atol=2e-4, rtol=2e-4)
+    # clip.cpp names: split q / k / v, the Conv3d's two temporal halves, merger as mm.0 / mm.2 + v.post_ln
+    gg = {"v.patch_embd.weight": hs["patch_embed.proj.weight"][:, :, 0], "v.patch_embd.weight.1":
+          hs["patch_embed.proj.weight"][:, :, 1], "v.post_ln.weight": hs["merger.ln_q.weight"],
+          "mm.0.weight": hs["merger.mlp.0.weight"], "mm.0.bias": hs["merger.mlp.0.bias"],
+          "mm.2.weight": hs["merger.mlp.2.weight"], "mm.2.bias": hs["merger.mlp.2.bias"]}
+    H = cfg.hidden
+    for i in range(cfg.depth):
+        p, q = f"v.blk.{i}.", f"blocks.{i}."
+        for j, n in enumerate(("attn_q", "attn_k", "attn_v")):
+            gg[p + n + ".weight"] = hs[q + "attn.qkv.weight"][j * H:(j + 1) * H]
+            gg[p + n + ".bias"] = hs[q + "attn.qkv.bias"][j * H:(j + 1) * H]
+        for a, b in (("attn.proj", "attn_out"), ("mlp.gate_proj", "ffn_gate"), ("mlp.up_proj", "ffn_up"),
+                     ("mlp.down_proj", "ffn_down")):
+            gg[p + b + ".weight"], gg[p + b + ".bias"] = hs[q + a + ".weight"], hs[q + a + ".bias"]
+        gg[p + "ln1.weight"], gg[p + "ln2.weight"] = hs[q + "norm1.weight"], hs[q + "norm2.weight"]
+    o2 = QV.QwenVLVision(cfg, QV.from_gguf_names(gg), "cpu")
+    assert torch.allclose(o2.embed_video(frames), ref, atol=2e-4, rtol=2e-4)
+
+
+def test_split_media_markers():
+    assert V.split_media("a [img-1] b [vid-0] c", 2, 1) == ["a ", ("img", 1), " b ", ("vid", 0), " c"]
+    assert V.split_media("<|vision_start|><|image_pad|><|vision_end|>x<|video_pad|>", 1, 1) == \
+        ["<|vision_start|>", ("img", 0), "<|vision_end|>x", ("vid", 0), ""]
+    assert V.split_media("text", 1, 1) == ["", ("img", 0), "", ("vid", 0), "text"]
+    with pytest.raises(ValueError):
+        V.split_media("[vid-2]", 0, 1)
+
+
+def _gif(n=4, size=(60, 40)):
+    from PIL import Image
+    rng = np.random.default_rng(n)
+    frames = [Image.fromarray(rng.integers(0, 255, (size[1], size[0], 3), dtype=np.uint8)) for _ in range(n)]
+    b = io.BytesIO()
+    frames[0].save(b, "GIF", save_all=True, append_images=frames[1:], duration=40)
+    return base64.b64encode(b.getvalue()).decode()
+
+
+@pytest.mark.parametrize("proj", ["gemma3-test", "qwen25vl-test"])
+def test_worker_predict_with_projectors(proj):
+    """The LLM worker with a Gemma-3 (SigLIP) or Qwen2.5-VL mmproj: images spliced at [img-N] / the Qwen image pad,
+    a video (animated GIF frames, vLLM's multi_modal_data["video"]) at the video pad, generation runs."""
+    import asyncio
+    from localai_tfp_amd.grpc import pb
+    from localai_tfp_amd.workers.llm import LLMServicer
+    s = LLMServicer(device="cpu")
+    r = s.LoadModel(pb.ModelOptions(Model="synthetic:tiny", MMProj=f"synthetic:{proj}", Options=["lazy_graphs"]), None)
+    assert r.success, r.message
+    if proj == "gemma3-test":
+        req = s._request(pb.PredictOptions(Prompt="USER: [img-0] what? ASSISTANT:", Images=[_png(4)], Tokens=3))
+        assert [e.shape[0] for _, e in req.mm_embeds] == [V.GEMMA3_TEST.tokens_per_image]
+        po = pb.PredictOptions(Prompt="[img-0] hi", Images=[_png(4)], Tokens=3)
+    else:
+        prompt = "<|vision_start|><|image_pad|><|vision_end|> and <|vision_start|><|video_pad|><|vision_end|>?"
+        req = s._request(pb.PredictOptions(Prompt=prompt, Images=[_png(4, (70, 50))], Videos=[_gif()], Tokens=3))
+        (p0, e0), (p1, e1) = req.mm_embeds
+        assert p1 > p0 + e0.shape[0] and e1.shape[0] == 2 * 1 * 2  # 2 frame pairs x (28/28) x (56/28) merge groups
+        po = pb.PredictOptions(Prompt=prompt, Images=[_png(4, (70, 50))], Videos=[_gif()], Tokens=3)
+    res = asyncio.run(s.Predict(po, None))
+    assert res.tokens == 3
+    s.engine.shutdown()
+
+
+@pytest.mark.gpu
+def test_projectors_gpu_match_cpu():
+    """Gemma-3 SigLIP + projector, LLaVA-1.6 anyres and Qwen2.5-VL (window attention through attention_dense.hip with
+    per-window lengths) on the GPU against their fp32 CPU path."""
+    from localai_tfp_amd.models import qwen_vl as QV
+    for cfg in (V.GEMMA3_TEST, V.CLIP_TEST_ANYRES):
+        sd = V.synthetic_clip(cfg, 2)
+        c, g = V.ClipVision(cfg, sd, "cpu"), V.ClipVision(cfg, sd, "cuda:0")
+        a = c.embed_images([_png(5, (90, 40))])[0]
+        b = g.embed_images([_png(5, (90, 40))])[0].cpu()
+        assert float((a - b).norm() / a.norm()) < 1e-2, cfg.name
+    sd = QV.synthetic_qwen_vl(QV.QWEN25VL_TEST, 1)
+    c, g = QV.QwenVLVision(QV.QWEN25VL_TEST, sd, "cpu"), QV.QwenVLVision(QV.QWEN25VL_TEST, sd, "cuda:0")
+    a, b = c.embed_images([_png(6, (140, 100))])[0], g.embed_images([_png(6, (140, 100))])[0].cpu()
+    assert float((a - b).norm() / a.norm()) < 1e-2
