@@ -1,7 +1,9 @@
 // attention.hip — paged GQA attention for the LLM worker (K4/K5 of SURVEY §2.6).
 //
 // KV cache layout (written by rope_kv.hip): [num_blocks][Hkv][block_size][D] bf16, or fp8 e4m3
-// (KV8: half the bytes per position; widened to fp32 in registers / to bf16 while staging to LDS).
+// (KV8: half the bytes per position; widened to fp32 in registers / to bf16 while staging to LDS), or rows of the
+// llama.cpp block formats q8_0 / q4_0 / q4_1 / q5_0 / q5_1 / iq4_nl (kvq.h; written by kvq.hip, dequantised to bf16
+// in registers like fp8 — the decode-MFMA and prefill kernels take the format as template KVF).
 //
 // decode  (one query token per sequence): memory-bound split-K over context partitions. A 256-thread
 //   workgroup owns (sequence, kv-head, partition); D/8 lanes cover one cached position with 16-byte
@@ -15,7 +17,7 @@
 //   (hardware transpose) from a region-swizzled image; P goes register -> LDS -> A-fragment.
 #include <type_traits>
 
-#include "mx_common.h"
+#include "kvq.h"
 
 #define LOG2E 1.4426950408889634f
 
@@ -259,6 +261,7 @@ static int launch_decode(const bf16_t* q, int q_stride, const void* kc, const vo
             attn_decode_reduce_kernel<F16><<<B * Hkv * G, 128, 0, st>>>(part_ml, part_o, n_parts, Hkv * G, D, seq_lens,
                                                                         part_size, out, out_stride);
     });
+#undef DQK
     MXK_CHECK_LAUNCH();
 }
 
@@ -267,7 +270,7 @@ extern "C" int mxk_attn_decode(const bf16_t* q, int q_stride, const void* kc, co
                                float scale, int window, float softcap, int part_size, int n_parts, bf16_t* out,
                                int out_stride, float2* part_ml, float* part_o, int kv8, hipStream_t st) {
     if (B <= 0) return 0;
-    if (Hq % Hkv) return (int)hipErrorInvalidValue;
+    if (Hq % Hkv || kv8 > KVF_FP8) return (int)hipErrorInvalidValue;  // block-quantised caches: the MFMA kernel only
     const int G = Hq / Hkv;
     if (n_parts > 1 && (!part_ml || !part_o)) return (int)hipErrorInvalidValue;
     if (bs <= 0 || part_size / bs + 1 > 256) return (int)hipErrorInvalidValue;  // LDS block-id stage
@@ -319,9 +322,16 @@ constexpr int dec_wave_lds() { return 32 * D * 2 + 16 * (32 + 8) * 2; }
 // context of <= 512 keys is ONE partition whose workgroup writes the final output (no reduce work for it).
 // TS: debug instantiation writing wall-clock stamps of workgroup (0, 0, 0) wave 0 to ts[0..7] (tools/prof_attn_decode.py)
 // DPF: the K-prefetch form (below; 2 waves / SIMD for its registers, MX_DECODE_PF=0 selects the 4-wave form)
-template <int D, bool F16, bool KV8, int NW = 4, bool TS = false, bool DPF = false>
+// 8 cached elements at element offset eo widened to bf16 (fp8 / block-quantised caches)
+template <int KVF, int D>
+MX_DEV uint4 kv_widen8(const void* base, size_t eo) {
+    if constexpr (KVF == KVF_FP8) return fp8x8_to_bf16x8(*(const uint2*)((const uint8_t*)base + eo));
+    else return kvq_to_bf16x8<KVF>(kvq_load<KVF, D>(base, eo));
+}
+
+template <int D, bool F16, int KVF, int NW = 4, bool TS = false, bool DPF = false>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(
-    (KV8 || (DPF && !TS && NW <= 8)) ? 2 : 4, (KV8 || (DPF && !TS && NW <= 8)) ? 2 : 4))) void attn_decode_mfma_kernel(
+    (KVF != KVF_BF16 || (DPF && !TS && NW <= 8)) ? 2 : 4, (KVF != KVF_BF16 || (DPF && !TS && NW <= 8)) ? 2 : 4))) void attn_decode_mfma_kernel(
     const bf16_t* __restrict__ q, int q_stride, const void* __restrict__ kcv, const void* __restrict__ vcv,
     const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ seq_lens, int Hkv, int G, int bs,
     float scale, int window, float softcap, int part_size, int n_parts, bf16_t* __restrict__ out, int out_stride,
@@ -339,6 +349,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(
     constexpr int PSTRIDE = (KT + 8) * 2;       // bytes per P row (padded)
     constexpr int WB = dec_wave_lds<D>();
     constexpr int NVC = KT * D / 8 / 64;        // 16-byte V chunks per lane per tile
+    constexpr bool KV8 = KVF != KVF_BF16;       // a cache widened in registers (fp8 or block-quantised)
     constexpr int ES = KV8 ? 1 : 2;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     constexpr int MAXB = 256;
@@ -401,8 +412,8 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(
 #pragma unroll
             for (int ks = 0; ks < D / 32; ++ks) {
                 if constexpr (KV8) {
-                    const uint2 w = ok ? *(const uint2*)(kc + (eo + 32 * ks + 8 * g)) : make_uint2(0, 0);
-                    kf_[t][ks] = __builtin_bit_cast(bf16x8, fp8x8_to_bf16x8(w));
+                    kf_[t][ks] = ok ? __builtin_bit_cast(bf16x8, kv_widen8<KVF, D>(kc, eo + 32 * ks + 8 * g))
+                                    : (bf16x8){};
                 } else if constexpr (PF) {
                     const bf16x8 w = *(const bf16x8*)(kc + (eo + 32 * ks + 8 * g) * ES);
                     kf_[t][ks] = ok ? w : (bf16x8){};
@@ -450,7 +461,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(
             const int key = kt0 + p < p1 ? kt0 + p : kt0;  // past the end: a valid row (P = 0 there)
             const size_t eo = (((size_t)sbt[key / bs - blk0] * Hkv + kvh) * bs + key % bs) * D + c * 8;
             if constexpr (KV8) {
-                vv[j] = kt0 + p < p1 ? fp8x8_to_bf16x8(*(const uint2*)(vc + eo)) : make_uint4(0, 0, 0, 0);
+                vv[j] = kt0 + p < p1 ? kv_widen8<KVF, D>(vc, eo) : make_uint4(0, 0, 0, 0);
             } else if constexpr (PF) {
                 vv[j] = *(const uint4*)(vc + eo * ES);  // rows past the end: a valid row, P = 0 there
             } else {
@@ -649,38 +660,44 @@ static int launch_decode_mfma(const bf16_t* q, int q_stride, const void* kc, con
     const bool mid = !wide && part_size >= 256 && !kv8 && B < 8;
     const int NWs = wide ? 16 : mid ? 8 : 4;
     const size_t lds = NWs * dec_wave_lds<D>() + NWs * 32 * 4;
+#define DQK(F_)                                                                                                   \
+    attn_decode_mfma_kernel<D, F16, F_><<<grid, 256, lds, st>>>(q, q_stride, kc, vc, bt, bt_stride, seq_lens, Hkv, G, \
+                                                               bs, scale, window, softcap, part_size, n_parts, out,   \
+                                                               out_stride, part_ml, part_o, part_cnt)
     MX_ACT_DISPATCH({
-        if (kv8)
-            attn_decode_mfma_kernel<D, F16, true><<<grid, 256, lds, st>>>(q, q_stride, kc, vc, bt, bt_stride, seq_lens,
-                                                                         Hkv, G, bs, scale, window, softcap, part_size,
-                                                                         n_parts, out, out_stride, part_ml, part_o,
-                                                                         part_cnt);
+        if (kv8 == KVF_FP8) DQK(KVF_FP8);
+        else if (kv8 == KVF_Q8_0) DQK(KVF_Q8_0);
+        else if (kv8 == KVF_Q4_0) DQK(KVF_Q4_0);
+        else if (kv8 == KVF_Q4_1) DQK(KVF_Q4_1);
+        else if (kv8 == KVF_Q5_0) DQK(KVF_Q5_0);
+        else if (kv8 == KVF_Q5_1) DQK(KVF_Q5_1);
+        else if (kv8 == KVF_IQ4_NL) DQK(KVF_IQ4_NL);
         else if (wide) {
             static bool attr = false;
             if (!attr) {
-                (void)hipFuncSetAttribute((const void*)attn_decode_mfma_kernel<D, F16, false, 16>,
+                (void)hipFuncSetAttribute((const void*)attn_decode_mfma_kernel<D, F16, KVF_BF16, 16>,
                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
                 attr = true;
             }
-            attn_decode_mfma_kernel<D, F16, false, 16><<<grid, 1024, lds, st>>>(
+            attn_decode_mfma_kernel<D, F16, KVF_BF16, 16><<<grid, 1024, lds, st>>>(
                 q, q_stride, kc, vc, bt, bt_stride, seq_lens, Hkv, G, bs, scale, window, softcap, part_size, n_parts,
                 out, out_stride, part_ml, part_o, part_cnt);
         } else if (mid) {
             static bool attr8 = false;
             if (!attr8) {
-                (void)hipFuncSetAttribute((const void*)attn_decode_mfma_kernel<D, F16, false, 8>,
+                (void)hipFuncSetAttribute((const void*)attn_decode_mfma_kernel<D, F16, KVF_BF16, 8>,
                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
                 attr8 = true;
             }
-            attn_decode_mfma_kernel<D, F16, false, 8><<<grid, 512, lds, st>>>(
+            attn_decode_mfma_kernel<D, F16, KVF_BF16, 8><<<grid, 512, lds, st>>>(
                 q, q_stride, kc, vc, bt, bt_stride, seq_lens, Hkv, G, bs, scale, window, softcap, part_size, n_parts,
                 out, out_stride, part_ml, part_o, part_cnt);
         } else if (decode_pf())
-            attn_decode_mfma_kernel<D, F16, false, 4, false, true><<<grid, 256, lds, st>>>(
+            attn_decode_mfma_kernel<D, F16, KVF_BF16, 4, false, true><<<grid, 256, lds, st>>>(
                 q, q_stride, kc, vc, bt, bt_stride, seq_lens, Hkv, G, bs, scale, window, softcap, part_size, n_parts,
                 out, out_stride, part_ml, part_o, part_cnt);
         else
-            attn_decode_mfma_kernel<D, F16, false><<<grid, 256, lds, st>>>(q, q_stride, kc, vc, bt, bt_stride,
+            attn_decode_mfma_kernel<D, F16, KVF_BF16><<<grid, 256, lds, st>>>(q, q_stride, kc, vc, bt, bt_stride,
                                                                           seq_lens, Hkv, G, bs, scale, window, softcap,
                                                                           part_size, n_parts, out, out_stride, part_ml,
                                                                           part_o, part_cnt);
@@ -700,9 +717,9 @@ extern "C" int mxk_attn_decode_ts(const bf16_t* q, int q_stride, const void* kc,
     if (Hq % Hkv || Hq / Hkv > 16 || part_size < 512 || bs <= 0 || part_size / bs + 1 > 256)
         return (int)hipErrorInvalidValue;
     const size_t lds = 16 * dec_wave_lds<128>() + 16 * 32 * 4;
-    (void)hipFuncSetAttribute((const void*)attn_decode_mfma_kernel<128, false, false, 16, true>,
+    (void)hipFuncSetAttribute((const void*)attn_decode_mfma_kernel<128, false, KVF_BF16, 16, true>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    attn_decode_mfma_kernel<128, false, false, 16, true><<<dim3(Hkv, B, 1), 1024, lds, st>>>(
+    attn_decode_mfma_kernel<128, false, KVF_BF16, 16, true><<<dim3(Hkv, B, 1), 1024, lds, st>>>(
         q, q_stride, kc, vc, bt, bt_stride, seq_lens, Hkv, Hq / Hkv, bs, scale, 0, 0.f, part_size, 1, out, out_stride,
         nullptr, nullptr, nullptr, ts);
     MXK_CHECK_LAUNCH();
@@ -730,7 +747,7 @@ extern "C" int mxk_attn_decode_mfma(const bf16_t* q, int q_stride, const void* k
 // 64-key tiles (each group stages its own K / V tile), then merge (m, l, O) through LDS. A short prompt chunk runs
 // only ~n_tiles x Hq / GW workgroups (136 for a 270-token chunk of Llama-3-8B, fewer than the CUs), each walking
 // its causal key range one tile at a time: the split halves the longest walk.
-template <int D, int GW, int VT, bool F16, bool KV8, int KSP = 1>
+template <int D, int GW, int VT, bool F16, int KVF, int KSP = 1>
 __global__ __launch_bounds__(512) void attn_prefill_kernel(const bf16_t* __restrict__ q,
                                                            const void* __restrict__ kc,
                                                            const void* __restrict__ vc,
@@ -800,7 +817,9 @@ __global__ __launch_bounds__(512) void attn_prefill_kernel(const bf16_t* __restr
     // MFMAs and softmax instead of opening every tile (short prompt chunks run only a few tiles per workgroup)
     constexpr int CH = KT * D / 8;              // 16-byte chunks per tile
     constexpr int NCH = (CH + NT_C - 1) / NT_C;  // chunks per thread
-    using KRaw = typename std::conditional<KV8, uint2, uint4>::type;
+    constexpr bool KV8 = KVF == KVF_FP8;
+    constexpr bool KVQ_ = KVF >= KVF_Q8_0;  // block-quantised rows (kvq.h): raw codes + scales kept in flight
+    using KRaw = typename std::conditional<KVQ_, KVQRaw, typename std::conditional<KV8, uint2, uint4>::type>::type;
     KRaw kr[NCH], vr[NCH];
     auto load_tile = [&](int kt0) {
 #pragma unroll
@@ -813,7 +832,10 @@ __global__ __launch_bounds__(512) void attn_prefill_kernel(const bf16_t* __restr
             if (id < CH && pos < kv_end) {
                 const int blk = bt[pos / bs], off = pos % bs;
                 const size_t eo = (((size_t)blk * Hkv + kvh) * bs + off) * D + c * 8;
-                if constexpr (KV8) {
+                if constexpr (KVQ_) {
+                    kr[j] = kvq_load<KVF, D>(kc, eo);
+                    vr[j] = kvq_load<KVF, D>(vc, eo);
+                } else if constexpr (KV8) {
                     kr[j] = *(const uint2*)((const uint8_t*)kc + eo);
                     vr[j] = *(const uint2*)((const uint8_t*)vc + eo);
                 } else {
@@ -830,7 +852,10 @@ __global__ __launch_bounds__(512) void attn_prefill_kernel(const bf16_t* __restr
             if (id >= CH) continue;
             const int p = id / (D / 8), c = id % (D / 8);
             uint4 kv, vv;
-            if constexpr (KV8) {
+            if constexpr (KVQ_) {
+                kv = kvq_to_bf16x8<KVF>(kr[j]);
+                vv = kvq_to_bf16x8<KVF>(vr[j]);
+            } else if constexpr (KV8) {
                 kv = fp8x8_to_bf16x8(kr[j]);
                 vv = fp8x8_to_bf16x8(vr[j]);
             } else {
@@ -986,7 +1011,7 @@ __global__ __launch_bounds__(512) void attn_prefill_kernel(const bf16_t* __restr
     }
 }
 
-template <int D, int GW, int VT, bool KV8, int KSP = 1>
+template <int D, int GW, int VT, int KVF, int KSP = 1>
 static void launch_prefill_t(dim3 grid, int threads, size_t lds, const bf16_t* q, const void* kc, const void* vc,
                              const int* bt, int bt_stride, const int* tile_seq, const int* tile_q0, const int* cu_q,
                              const int* ctx_lens, int Hq, int Hkv, int bs, float scale, int window, float softcap,
@@ -995,12 +1020,12 @@ static void launch_prefill_t(dim3 grid, int threads, size_t lds, const bf16_t* q
         if (lds > 65536) {  // D=256 tiles / key-split tiles (73-82 KB): opt in to the large LDS allocation once
             static bool opted = false;
             if (!opted) {
-                (void)hipFuncSetAttribute((const void*)attn_prefill_kernel<D, GW, VT, F16, KV8, KSP>,
+                (void)hipFuncSetAttribute((const void*)attn_prefill_kernel<D, GW, VT, F16, KVF, KSP>,
                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
                 opted = true;
             }
         }
-        attn_prefill_kernel<D, GW, VT, F16, KV8, KSP><<<grid, threads, lds, st>>>(
+        attn_prefill_kernel<D, GW, VT, F16, KVF, KSP><<<grid, threads, lds, st>>>(
             q, kc, vc, bt, bt_stride, tile_seq, tile_q0, cu_q, ctx_lens, Hq, Hkv, Hq / Hkv, bs, scale, window,
             softcap, out);
     });
@@ -1021,7 +1046,7 @@ static int launch_prefill(const bf16_t* q, const void* kc, const void* vc, const
     if constexpr (D == 128 && GW == 4) {
         static const bool ks_on = !getenv("MX_PREFILL_KSPLIT") || atoi(getenv("MX_PREFILL_KSPLIT")) != 0;
         if (ks_on && vmode == 0 && !kv8 && (long)n_tiles * (Hq / GW) < 256) {
-            launch_prefill_t<D, GW, 0, false, 2>(grid, 2 * NW * 64, 2 * (2 * 64 * D * 2) + 2 * NW * 16 * (64 + 8) * 2,
+            launch_prefill_t<D, GW, 0, KVF_BF16, 2>(grid, 2 * NW * 64, 2 * (2 * 64 * D * 2) + 2 * NW * 16 * (64 + 8) * 2,
                                                  q, kc, vc, bt, bt_stride, tile_seq, tile_q0, cu_q, ctx_lens, Hq, Hkv,
                                                  bs, scale, window, softcap, out, st);
             MXK_CHECK_LAUNCH();
@@ -1030,8 +1055,19 @@ static int launch_prefill(const bf16_t* q, const void* kc, const void* vc, const
 #define PFL(VT_, K8_)                                                                                          \
     launch_prefill_t<D, GW, VT_, K8_>(grid, NW * 64, VT_ ? lds1 : lds0, q, kc, vc, bt, bt_stride, tile_seq,    \
                                       tile_q0, cu_q, ctx_lens, Hq, Hkv, bs, scale, window, softcap, out, st)
-    if (vmode == 0) { if (kv8) PFL(0, true); else PFL(0, false); }
-    else { if (kv8) PFL(1, true); else PFL(1, false); }
+#define PFK(VT_)                                                                                                \
+    {                                                                                                           \
+        if (kv8 == KVF_FP8) PFL(VT_, KVF_FP8);                                                                  \
+        else if (kv8 == KVF_Q8_0) PFL(VT_, KVF_Q8_0);                                                           \
+        else if (kv8 == KVF_Q4_0) PFL(VT_, KVF_Q4_0);                                                           \
+        else if (kv8 == KVF_Q4_1) PFL(VT_, KVF_Q4_1);                                                           \
+        else if (kv8 == KVF_Q5_0) PFL(VT_, KVF_Q5_0);                                                           \
+        else if (kv8 == KVF_Q5_1) PFL(VT_, KVF_Q5_1);                                                           \
+        else if (kv8 == KVF_IQ4_NL) PFL(VT_, KVF_IQ4_NL);                                                       \
+        else PFL(VT_, KVF_BF16);                                                                                \
+    }
+    if (vmode == 0) PFK(0) else PFK(1)
+#undef PFK
 #undef PFL
     MXK_CHECK_LAUNCH();
 }

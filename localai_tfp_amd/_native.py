@@ -95,6 +95,10 @@ KERNEL_SIGS = {
     "mxk_qk_norm_rope_gqa": [P, I, I, I, I, I, I, P, P, P, I, F, P],
     "mxk_ssm_scan": [P, P, I, P, P, P, P, P, I, P, P, P, I, I, P, I, P, I, I, I, I, P],
     "mxk_moe_route": [P, I, I, I, I, I, P, P, P],
+    # kvf, ks, vs, slots, T, Hkv, D, bs, kc, vc, stream
+    "mxk_kvq_append": [I, P, P, P, I, I, I, I, P, P, P],
+    # kvf, cache, rows, n, D, out, stream
+    "mxk_kvq_dequant_rows": [I, P, P, I, I, P, P],
     # x, ldx, wr, T, H, E, k, renorm, ids, wts, stream
     "mxk_moe_router": [P, I, P, I, I, I, I, I, P, P, P],
     # qtype, epi, W, N, K, ids, P, e0, El, x, ldx, xdiv, C, ldc, stream

@@ -120,15 +120,27 @@ class EngineConfig:
 
 
 def kv_torch_dtype(name: str) -> torch.dtype:
-    """KV cache type names (engine `kv_dtype`, reference `cache_type_k` / `cache_type_v`:
-    f16 / q8_0 / ...) -> storage dtype. 8-bit llama.cpp types map to fp8 e4m3 (the gfx950-native
-    8-bit float), 16-bit types to bf16."""
+    """KV cache type names (engine `kv_dtype`, reference `cache_type_k` / `cache_type_v`: f16 / q8_0 / ...) -> storage
+    dtype: 16-bit types bf16, fp8 e4m3 (the gfx950-native 8-bit float), and the llama.cpp block formats q8_0 / q4_0 /
+    q4_1 / q5_0 / q5_1 / iq4_nl as uint8 rows of real blocks (kv_format, ops/kvq.py)."""
     n = (name or "bf16").lower()
-    if n in ("fp8", "f8", "e4m3", "fp8_e4m3", "q8_0", "q8", "q4_0", "q4_1", "q5_0", "q5_1", "iq4_nl"):
+    if n in ("fp8", "f8", "e4m3", "fp8_e4m3"):
         return torch.float8_e4m3fn
+    if n in ("q8", "q8_0", "q4_0", "q4_1", "q5_0", "q5_1", "iq4_nl"):
+        return torch.uint8
     if n in ("bf16", "f16", "fp16", "f32", "auto", ""):
         return torch.bfloat16
     raise ValueError(f"unknown KV cache type {name!r}")
+
+
+def kv_format_id(name: str) -> int:
+    """ops/kvq.py format id of a KV cache type name (0 bf16, 1 fp8, 2.. llama.cpp block formats)."""
+    from ..ops.kvq import FORMATS
+    n = (name or "bf16").lower()
+    n = "q8_0" if n == "q8" else n
+    if n in FORMATS:
+        return FORMATS[n]
+    return 1 if kv_torch_dtype(n) == torch.float8_e4m3fn else 0
 
 
 class RequestHandle:
@@ -361,7 +373,11 @@ class LLMEngine:
         use_spec = draft is not None and c.n_draft > 0 and tp is None
         frac = c.kv_mem_fraction
         self.kv_dtype = kv_torch_dtype(c.kv_dtype)
+        self.kvf = kv_format_id(c.kv_dtype)
         eb = self.kv_dtype.itemsize
+        if self.kvf >= 2:  # block-quantised rows: llama.cpp's bytes per element (e.g. q4_0 18 / 32)
+            from ..ops.kvq import row_bytes
+            eb = row_bytes(self.kvf, mc.head_dim) / mc.head_dim
         if use_spec:  # the draft's cache shares the block ids: split the pool bytes between the two
             per_t = KVCache.bytes_per_block(mc.n_layers, model.n_kv, c.block_size, mc.head_dim, eb)
             per_d = KVCache.bytes_per_block(draft.cfg.n_layers, draft.n_kv, c.block_size, draft.cfg.head_dim, eb)
@@ -379,7 +395,7 @@ class LLMEngine:
                 nb = model.remote.setup_kv(nb, c.block_size, c.kv_dtype, max(c.max_batched_tokens, c.max_num_seqs),
                                            c.max_num_seqs, max(1, -(-c.max_model_len // c.attn_part_size)))
                 self.cfg.use_graphs = False  # a network hop cannot live inside a hipGraph
-            self.kv = KVCache(nl, nb, model.n_kv, c.block_size, mc.head_dim, self.device, self.kv_dtype)
+            self.kv = KVCache(nl, nb, model.n_kv, c.block_size, mc.head_dim, self.device, self.kv_dtype, kvf=self.kvf)
         self.bm = make_block_manager(nb, c.block_size, c.enable_prefix_cache)
         # scheduler + step planner: native (csrc/runtime/scheduler.cpp) on the native block manager; the Python
         # Scheduler is the reference implementation (MX_PY_SCHED=1, or no libmxrt)

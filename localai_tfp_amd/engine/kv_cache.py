@@ -24,20 +24,32 @@ import torch
 
 
 class KVCache:
+    """Paged K / V caches [n_layers, num_blocks, n_kv, block_size, head_dim] in bf16 / fp8, or, for the llama.cpp
+    block formats (kvf >= 2, ops/kvq.py), uint8 rows [.., block_size, row_bytes] of the quantised head vectors."""
+
     def __init__(self, n_layers: int, num_blocks: int, n_kv: int, block_size: int, head_dim: int, device,
-                 dtype=torch.bfloat16):
+                 dtype=torch.bfloat16, kvf: int = 0):
         self.n_layers, self.num_blocks, self.block_size = n_layers, num_blocks, block_size
         self.n_kv, self.head_dim = n_kv, head_dim
-        shape = (n_layers, num_blocks, n_kv, block_size, head_dim)
+        self.kvf = kvf
+        if kvf >= 2:
+            from ..ops.kvq import row_bytes
+            shape = (n_layers, num_blocks, n_kv, block_size, row_bytes(kvf, head_dim))
+            dtype = torch.uint8
+        else:
+            shape = (n_layers, num_blocks, n_kv, block_size, head_dim)
         self.k = torch.zeros(shape, dtype=dtype, device=device)
         self.v = torch.zeros(shape, dtype=dtype, device=device)
 
     def layer(self, i: int):
-        return self.k[i], self.v[i]
+        k, v = self.k[i], self.v[i]
+        if self.kvf >= 2:
+            k.kvf = v.kvf = self.kvf
+        return k, v
 
     @staticmethod
     def bytes_per_block(n_layers, n_kv, block_size, head_dim, dtype_bytes=2):
-        return 2 * n_layers * n_kv * block_size * head_dim * dtype_bytes
+        return int(2 * n_layers * n_kv * block_size * head_dim * dtype_bytes)
 
     @classmethod
     def auto_num_blocks(cls, n_layers, n_kv, block_size, head_dim, device, fraction: float = 0.85,

@@ -46,7 +46,8 @@ class SpeculativeDecoder:
         self.max_batch = max(1, min(int(max_batch), e.cfg.max_num_seqs))
         c = e.cfg
         nb = e.kv.num_blocks
-        self.kv = KVCache(dc.n_layers, nb, draft.n_kv, c.block_size, dc.head_dim, e.device, e.kv_dtype)
+        self.kv = KVCache(dc.n_layers, nb, draft.n_kv, c.block_size, dc.head_dim, e.device, e.kv_dtype,
+                          kvf=getattr(e, "kvf", 0))
         rows = self.max_batch * (self.k + 1)
         # draft catch-up chunks can be whole prompts: size its workspace like the engine's
         self.dws = Workspace(dc, max(c.max_batched_tokens, rows), max(self.max_batch, 1), e.device, 1,

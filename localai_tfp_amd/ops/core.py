@@ -273,13 +273,37 @@ def rope_kv(qkv: torch.Tensor, bias: torch.Tensor | None, positions: torch.Tenso
 
         q_out.copy_(rot(q).to(q_out.dtype))
         kr = rot(k)
+        kvf = kv_format(k_cache)
+        if kvf >= 2:  # the kernel stages bf16 rows before quantising them: same rounding here
+            from .kvq import quantize_rows
+            kq = torch.from_numpy(quantize_rows(kr.to(torch.bfloat16).float().reshape(-1, D), kvf)).view(T, Hkv, -1)
+            vq = torch.from_numpy(quantize_rows(v.to(torch.bfloat16).float().reshape(-1, D), kvf)).view(T, Hkv, -1)
         for t in range(T):
             s = int(slots[t])
             if s < 0:
                 continue
             blk, off = divmod(s, block_size)
-            k_cache[blk, :, off, :] = _to_cache(kr[t], k_cache.dtype)
-            v_cache[blk, :, off, :] = _to_cache(v[t], v_cache.dtype)
+            if kvf >= 2:
+                k_cache[blk, :, off, :] = kq[t]
+                v_cache[blk, :, off, :] = vq[t]
+            else:
+                k_cache[blk, :, off, :] = _to_cache(kr[t], k_cache.dtype)
+                v_cache[blk, :, off, :] = _to_cache(v[t], v_cache.dtype)
+        return
+    kvf = kv_format(k_cache)
+    if kvf >= 2:
+        # block-quantised cache: the rotated K and V rows go to a bf16 staging buffer [T, Hkv, D] (identity slots,
+        # block size 1), then kvq.hip quantises them into their paged slots (one extra launch per layer)
+        ks = torch.empty(T, Hkv, D, dtype=torch.bfloat16, device=qkv.device)
+        vs = torch.empty_like(ks)
+        ident = torch.arange(T, dtype=torch.int32, device=qkv.device)
+        N.kcall("mxk_rope_kv", qkv.data_ptr(), N.ptr(bias), positions.data_ptr(), ident.data_ptr(),
+                inv_freq.data_ptr(), float(attn_factor), T, Hq, Hkv, D, rot_dim, int(neox), q_out.data_ptr(),
+                ks.data_ptr(), vs.data_ptr(), 1, N.ptr(qk_norm[0]) if qk_norm else None,
+                N.ptr(qk_norm[1]) if qk_norm else None, float(qk_norm[2]) if qk_norm else 0.0, int(zero_after), 0,
+                N.stream_ptr())
+        N.kcall("mxk_kvq_append", kvf, ks.data_ptr(), vs.data_ptr(), slots.data_ptr(), T, Hkv, D, block_size,
+                k_cache.data_ptr(), v_cache.data_ptr(), N.stream_ptr())
         return
     N.kcall("mxk_rope_kv", qkv.data_ptr(), N.ptr(bias), positions.data_ptr(), slots.data_ptr(), inv_freq.data_ptr(),
             float(attn_factor), T, Hq, Hkv, D, rot_dim, int(neox), q_out.data_ptr(), k_cache.data_ptr(),
@@ -287,6 +311,8 @@ def rope_kv(qkv: torch.Tensor, bias: torch.Tensor | None, positions: torch.Tenso
             N.ptr(qk_norm[1]) if qk_norm else None, float(qk_norm[2]) if qk_norm else 0.0, int(zero_after),
             int(is_fp8(k_cache)), N.stream_ptr())
 
+
+from .kvq import kv_format  # noqa: E402  (0 bf16, 1 fp8, 2.. llama.cpp block formats)
 
 FP8_KV = torch.float8_e4m3fn  # OCP e4m3: the gfx950 hardware conversion format
 FP8_MAX = 448.0
@@ -315,8 +341,14 @@ def _attn_ref_one(q, k_cache, v_cache, table, ctx: int, qpos0: int, scale: float
     Hkv = k_cache.shape[1]
     nb = (ctx + block_size - 1) // block_size
     blocks = table[:nb].long()
-    k = k_cache[blocks].permute(1, 0, 2, 3).reshape(Hkv, nb * block_size, D)[:, :ctx].float()
-    v = v_cache[blocks].permute(1, 0, 2, 3).reshape(Hkv, nb * block_size, D)[:, :ctx].float()
+    if kv_format(k_cache) >= 2:  # block-quantised rows: dequantise the blocks this sequence reads
+        from .kvq import dequant_cache
+        kvf = kv_format(k_cache)
+        kb, vb = dequant_cache(k_cache[blocks], kvf, D), dequant_cache(v_cache[blocks], kvf, D)
+    else:
+        kb, vb = k_cache[blocks], v_cache[blocks]
+    k = kb.permute(1, 0, 2, 3).reshape(Hkv, nb * block_size, D)[:, :ctx].float()
+    v = vb.permute(1, 0, 2, 3).reshape(Hkv, nb * block_size, D)[:, :ctx].float()
     G = Hq // Hkv
     k = k.repeat_interleave(G, 0)
     v = v.repeat_interleave(G, 0)
@@ -376,9 +408,12 @@ def attn_decode(q: torch.Tensor, k_cache, v_cache, block_tables: torch.Tensor, s
         ml_t = po = None
     N.ensure_act(out.dtype)
     mfma = (impl or ATTN_DECODE_IMPL) == "mfma" and D in (64, 128) and Hq // Hkv <= 16
+    if kv_format(k_cache) >= 2 and not mfma:
+        raise ValueError(f"block-quantised KV caches need the MFMA decode kernel (head dim 64 / 128, <= 16 q heads per "
+                         f"kv head); got D {D}, {Hq // Hkv} q heads per kv head")
     args = [q.data_ptr(), q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(), block_tables.data_ptr(),
             block_tables.stride(0), seq_lens.data_ptr(), B, Hq, Hkv, D, bs, float(scale), int(window), float(softcap),
-            part_size, n_parts, out.data_ptr(), out.stride(0), N.ptr(ml_t), N.ptr(po), int(is_fp8(k_cache))]
+            part_size, n_parts, out.data_ptr(), out.stride(0), N.ptr(ml_t), N.ptr(po), kv_format(k_cache)]
     if mfma:
         # partition merge inside the attention kernel (zeroed per-(seq, kv head) counters), else a reduce launch
         if cnt is not None and (cnt.numel() < B * Hkv or not FUSED_DECODE_MERGE):
@@ -416,7 +451,7 @@ def attn_prefill(q: torch.Tensor, k_cache, v_cache, block_tables: torch.Tensor, 
         N.kcall("mxk_attn_prefill", q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), block_tables.data_ptr(),
                 block_tables.stride(0), tiles[0].data_ptr(), tiles[1].data_ptr(), int(tiles[0].numel()),
                 cu_q.data_ptr(), ctx_lens.data_ptr(), Hq, Hkv, D, bs, float(scale), int(window), float(softcap),
-                out.data_ptr(), ATTN_VMODE if vmode is None else int(vmode), int(is_fp8(k_cache)), N.stream_ptr())
+                out.data_ptr(), ATTN_VMODE if vmode is None else int(vmode), kv_format(k_cache), N.stream_ptr())
         return out
     Hkv, bs = k_cache.shape[1], k_cache.shape[2]
     cu = cu_q.tolist() if q_lens_host is None else None
@@ -439,7 +474,7 @@ def attn_prefill(q: torch.Tensor, k_cache, v_cache, block_tables: torch.Tensor, 
     N.kcall("mxk_attn_prefill", q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), block_tables.data_ptr(),
             block_tables.stride(0), tiles[0].data_ptr(), tiles[1].data_ptr(), len(seqs), cu_q.data_ptr(),
             ctx_lens.data_ptr(), Hq, Hkv, D, bs, float(scale), int(window), float(softcap), out.data_ptr(),
-            ATTN_VMODE if vmode is None else int(vmode), int(is_fp8(k_cache)), N.stream_ptr())
+            ATTN_VMODE if vmode is None else int(vmode), kv_format(k_cache), N.stream_ptr())
     return out
 
 

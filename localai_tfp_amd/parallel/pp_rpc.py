@@ -80,7 +80,7 @@ class _Stage:
         from ..models.llama import Workspace
         from ..models.loader import _apply_overrides, _lora_attach, _lora_source, gguf_source, SYNTHETIC
         from ..models.llama import LlamaModel
-        from ..engine.engine import kv_torch_dtype
+        from ..engine.engine import kv_format_id, kv_torch_dtype
         model = req["model"]
         l0, l1 = req["layers"]
         if model.startswith("synthetic:"):
@@ -103,7 +103,8 @@ class _Stage:
         self.cfg = cfg
         self.device = torch.device(device)
         self.kv = KVCache(l1 - l0, int(req["num_blocks"]), self.model.n_kv, int(req["block_size"]), cfg.head_dim,
-                          self.device, kv_torch_dtype(req.get("kv_dtype", "bf16")))
+                          self.device, kv_torch_dtype(req.get("kv_dtype", "bf16")),
+                          kvf=kv_format_id(req.get("kv_dtype", "bf16")))
         self.ws = Workspace(cfg, int(req["max_tokens"]), int(req["max_seqs"]), self.device, 1, int(req["max_parts"]))
 
     def forward(self, header: dict, arrays: dict) -> np.ndarray:

@@ -23,7 +23,8 @@ F8 = torch.float8_e4m3fn
 
 
 def test_cache_type_names():
-    assert kv_torch_dtype("q8_0") == F8 and kv_torch_dtype("fp8") == F8
+    # llama.cpp's block formats are stored as real blocks (uint8 rows, tests/test_kv_quant.py); fp8 stays e4m3
+    assert kv_torch_dtype("q8_0") == torch.uint8 and kv_torch_dtype("q4_0") == torch.uint8 and kv_torch_dtype("fp8") == F8
     assert kv_torch_dtype("f16") == torch.bfloat16 and kv_torch_dtype("") == torch.bfloat16
     with pytest.raises(ValueError):
         kv_torch_dtype("int3")
@@ -75,7 +76,7 @@ def test_engine_fp8_kv_cpu():
     m = LlamaModel.load(cfg, synthetic_source(cfg, "Q4_K_M", seed=11), "cpu")
     tok = ByteTokenizer(cfg.vocab)
     e = LLMEngine(m, tok, EngineConfig(num_blocks=128, max_num_seqs=4, max_batched_tokens=64, max_model_len=256,
-                                       kv_dtype="q8_0"))
+                                       kv_dtype="fp8"))
     assert e.kv.k.dtype == F8
     o = e.generate(tok.encode("fp8 cache"), SamplingParams(temperature=0.0, ignore_eos=True), max_tokens=8)
     assert len(o.token_ids) == 8
