@@ -182,6 +182,9 @@ def load_mmproj(path: str, device="cpu"):
         if name.startswith("qwen"):
             from .qwen_vl import load_qwen_vl
             return load_qwen_vl(path, device)
+        if name.startswith("minicpmv"):
+            from .minicpmv import MINICPMV_TEST, MiniCPMVVision, synthetic_minicpmv
+            return MiniCPMVVision(MINICPMV_TEST, synthetic_minicpmv(MINICPMV_TEST), device)
         cfg = SYNTHETIC[name]
         return ClipVision(cfg, synthetic_clip(cfg, seed=0), device)
     from ..formats.gguf import GGUFReader
@@ -196,8 +199,17 @@ def load_mmproj(path: str, device="cpu"):
         sd[name] = torch.from_numpy(np.ascontiguousarray(a).reshape(tuple(reversed(ti.shape))).copy()).float()
     n_blocks = len({k.split(".")[2] for k in sd if k.startswith("v.blk.")})
     cfg = ClipVisionConfig.from_gguf_metadata(r.metadata, n_blocks)
+    if cfg.projector == "resampler":  # MiniCPM-V
+        from .minicpmv import MiniCPMVConfig, MiniCPMVVision
+        qd = sd["resampler.query"].shape
+        cfg.act, cfg.pad_square = "gelu_tanh", False
+        side = int(round(sd["v.position_embd.weight"].shape[0] ** 0.5))
+        mc = MiniCPMVConfig(vision=cfg, embed_dim=int(qd[1]), queries=int(qd[0]), heads=max(1, int(qd[1]) // 128),
+                            scale_resolution=int(r.metadata.get("clip.vision.image_size", 448) or 448), pos_side=side)
+        return MiniCPMVVision(mc, sd, device)
     if cfg.projector not in ("mlp", "gemma3"):
-        raise NotImplementedError(f"projector type {cfg.projector!r} (supported: mlp / LLaVA-1.5 and -1.6, gemma3)")
+        raise NotImplementedError(f"projector type {cfg.projector!r} (supported: mlp / LLaVA-1.5 and -1.6, gemma3, "
+                                  f"resampler / MiniCPM-V, qwen2vl_merger / qwen2.5vl_merger)")
     if cfg.projector == "gemma3":
         cfg.proj_hidden = int(sd["mm.input_projection.weight"].shape[1])
         cfg.act = "gelu_tanh"
@@ -239,9 +251,10 @@ class ClipVision:
         if cfg.projector == "gemma3":
             self.soft_norm = f32("mm.soft_emb_norm.weight")  # (1 + w) as the gguf converter stores it
             self.mm_proj = Dense(sd["mm.input_projection.weight"].t().contiguous(), None, dev, dt)
-        else:
+        elif cfg.projector == "mlp":
             self.mm0 = Dense(sd["mm.0.weight"], sd["mm.0.bias"], dev, dt)
             self.mm2 = Dense(sd["mm.2.weight"], sd["mm.2.bias"], dev, dt)
+        # "resampler" (MiniCPM-V): models/minicpmv.py adds its own projector
 
     # ---------------------------------------------------------------- preprocessing
     @staticmethod

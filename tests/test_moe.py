@@ -170,7 +170,10 @@ def test_moe_ffn_gpu_matches_fp32(E, k, H, F, qt, renorm, t32):
         got = MO.moe_ffn(wg, x.cuda(), h0.cuda().clone()).cpu()
         torch.cuda.synchronize()
         rel = float((got - ref).norm() / (ref - h0).norm())
-        assert rel < 1e-2, (T, rel)
+        # the grouped decode GEMV (t32, <= 64 pairs) runs on q8 activations per 32 (llama.cpp's MMVQ numerics): the
+        # activations are quantised twice (x, then the SwiGLU output), ~1 % more error than the 16-bit GEMM paths
+        tol = 2.5e-2 if (t32 and T * k <= MO.GEMV_MAX_PAIRS) else 1e-2
+        assert rel < tol, (T, rel)
 
 
 @pytest.mark.gpu

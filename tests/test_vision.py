@@ -395,3 +395,87 @@ def test_projectors_gpu_match_cpu():
     c, g = QV.QwenVLVision(QV.QWEN25VL_TEST, sd, "cpu"), QV.QwenVLVision(QV.QWEN25VL_TEST, sd, "cuda:0")
     a, b = c.embed_images([_png(6, (140, 100))])[0], g.embed_images([_png(6, (140, 100))])[0].cpu()
     assert float((a - b).norm() / a.norm()) < 1e-2
+    from localai_tfp_amd.models import minicpmv as MC
+    sd = MC.synthetic_minicpmv(MC.MINICPMV_TEST, 2)
+    c, g = MC.MiniCPMVVision(MC.MINICPMV_TEST, sd, "cpu"), MC.MiniCPMVVision(MC.MINICPMV_TEST, sd, "cuda:0")
+    a, b = c.embed_images([_png(7, (170, 60))])[0], g.embed_images([_png(7, (170, 60))])[0].cpu()
+    assert float((a - b).norm() / a.norm()) < 1e-2
+
+
+# ------------------------------------------------------------------------------------------------ MiniCPM-V
+def test_minicpmv_slicing():
+    """MiniCPM-V's slice grid / refine size (the published processor, as clip.cpp uhd_slice_image): small images are
+    not sliced, wide ones get a log-aspect-matched grid, every piece is a multiple of the patch size."""
+    from PIL import Image
+    from localai_tfp_amd.models import minicpmv as MC
+    assert MC.get_sliced_grid((448, 448), 448, 9) is None
+    assert MC.get_sliced_grid((1344, 448), 448, 9) == [3, 1]
+    assert MC.get_sliced_grid((896, 896), 448, 9) == [2, 2]
+    assert MC.find_best_resize((1000, 500), 448, 14) == (630, 322)
+    cfg = MC.MINICPMV_TEST
+    parts = MC.slice_image(Image.new("RGB", (170, 60)), cfg)
+    assert len(parts) == 1 + 3 and all(p.width % 14 == 0 and p.height % 14 == 0 for p in parts)
+    assert len({p.size for p in parts[1:]}) == 1
+
+
+def test_minicpmv_tower_and_resampler():
+    """Tower at the native slice size == transformers' SiglipVisionModel (bucketed position ids are then the identity);
+    the resampler == a torch.nn.MultiheadAttention re-statement (learned queries, ln_kv / ln_q / ln_post, sin-cos key
+    positions, proj)."""
+    from transformers import SiglipVisionConfig, SiglipVisionModel
+    from localai_tfp_amd.models import minicpmv as MC
+    cfg = MC.MINICPMV_TEST
+    vc = cfg.vision
+    hc = SiglipVisionConfig(hidden_size=vc.hidden, intermediate_size=vc.ffn, num_hidden_layers=vc.layers,
+                            num_attention_heads=vc.heads, image_size=vc.image_size, patch_size=vc.patch,
+                            layer_norm_eps=vc.eps, hidden_act="gelu_pytorch_tanh")
+    torch.manual_seed(0)
+    tower = SiglipVisionModel(hc).eval()
+    with torch.no_grad():
+        for p in tower.parameters():
+            p.add_(torch.randn_like(p) * 0.02)
+    proj = type("P", (), {})()
+    proj.mm_soft_emb_norm = type("N", (), {"weight": torch.zeros(vc.hidden)})()
+    proj.mm_input_projection_weight = torch.zeros(vc.hidden, 4)
+    sd = {k: v for k, v in _gemma3_sd(tower, proj, vc).items() if not k.startswith("mm.")}
+    sd.update({k: v for k, v in MC.synthetic_minicpmv(cfg, 1).items() if k.startswith("resampler.")})
+    ours = MC.MiniCPMVVision(cfg, sd, "cpu")
+    from PIL import Image
+    im = Image.fromarray(np.random.default_rng(2).integers(0, 255, (56, 56, 3), dtype=np.uint8))
+    px = ours.normalise(im)
+    feats, hw = ours._tower(px)
+    with torch.no_grad():
+        ref = tower(pixel_values=px[None]).last_hidden_state[0]
+    assert hw == (4, 4) and torch.allclose(feats, ref, atol=2e-4, rtol=2e-4)
+    # resampler oracle
+    E = cfg.embed_dim
+    mha = torch.nn.MultiheadAttention(E, cfg.heads)
+    with torch.no_grad():
+        mha.in_proj_weight.copy_(torch.cat([sd[f"resampler.attn.{x}.weight"] for x in "qkv"]))
+        mha.in_proj_bias.copy_(torch.cat([sd[f"resampler.attn.{x}.bias"] for x in "qkv"]))
+        mha.out_proj.weight.copy_(sd["resampler.attn.out.weight"])
+        mha.out_proj.bias.copy_(sd["resampler.attn.out.bias"])
+        ln = lambda x, n: torch.nn.functional.layer_norm(x, (E,), sd[f"resampler.ln_{n}.weight"],  # noqa: E731
+                                                        sd[f"resampler.ln_{n}.bias"], 1e-6)
+        x = ln(feats @ sd["resampler.kv.weight"].t(), "kv")
+        q = ln(sd["resampler.query"], "q")
+        pos = MC.sincos_2d(E, 4, 4).reshape(16, E)
+        o = mha(q[:, None], (x + pos)[:, None], x[:, None])[0][:, 0]
+        want = ln(o, "post") @ sd["resampler.proj.weight"]
+    got = ours._resample(feats, hw)
+    assert torch.allclose(got, want, atol=2e-4, rtol=2e-4)
+
+
+def test_worker_predict_with_minicpmv():
+    import asyncio
+    from localai_tfp_amd.grpc import pb
+    from localai_tfp_amd.workers.llm import LLMServicer
+    s = LLMServicer(device="cpu")
+    r = s.LoadModel(pb.ModelOptions(Model="synthetic:tiny", MMProj="synthetic:minicpmv-test", Options=["lazy_graphs"]),
+                    None)
+    assert r.success, r.message
+    req = s._request(pb.PredictOptions(Prompt="[img-0] what?", Images=[_png(4, (170, 60))], Tokens=3))
+    assert req.mm_embeds[0][1].shape == (8 * 4, 256)  # source + 3 slices x 8 queries
+    res = asyncio.run(s.Predict(pb.PredictOptions(Prompt="[img-0] what?", Images=[_png(4, (170, 60))], Tokens=3), None))
+    assert res.tokens == 3
+    s.engine.shutdown()
