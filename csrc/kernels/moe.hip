@@ -85,79 +85,90 @@ __global__ __launch_bounds__(256) void moe_route_kernel(const float* __restrict_
     route_row<VPL>(logits + (size_t)t * ldl, E, k, renorm, ids + (size_t)t * k, wts + (size_t)t * k, lane);
 }
 
-// Router GEMV + routing in one launch: TT tokens per workgroup, their 16-bit hidden rows staged in LDS, each wave
-// takes every 4th expert (fp32 router row read once per TT tokens, coalesced float4 per lane), the logits land in
-// LDS and each wave then routes TT / 4 of the tokens (route_row). Replaces the fp32 hipBLASLt matmul + route launch.
-template <int VPL, int TT, bool F16>
+extern "C" int mxk_moe_route(const float* logits, int ldl, int T, int E, int k, int renorm, int* ids, float* wts,
+                             hipStream_t st);
+
+// Router GEMV: logits[t, e] = x[t] . wr[e] (fp32 router rows, 16-bit hidden rows). Workgroup (token block, expert
+// block): TT tokens' rows staged in LDS, one expert per wave — the wave's fp32 router row (H floats) is requested in
+// full before any FMA, so a decode step's router costs one load latency instead of one per 256 columns (the first
+// form, one workgroup walking every expert, took 177 us per layer at batch 1: profiles/r6_moe_qwen3_30b.md).
+// The top-k routing then runs as moe_route_kernel over the logits.
+template <int TT, bool F16>
 __global__ __launch_bounds__(256) void moe_router_kernel(const bf16_t* __restrict__ x, int ldx,
-                                                         const float* __restrict__ wr, int T, int H, int E, int k,
-                                                         int renorm, int* __restrict__ ids, float* __restrict__ wts) {
+                                                         const float* __restrict__ wr, int T, int H, int E,
+                                                         float* __restrict__ logits) {
     extern __shared__ __attribute__((aligned(16))) char rsm[];
-    bf16_t* xs = (bf16_t*)rsm;                         // [TT][H]
-    float* lg = (float*)(rsm + (size_t)TT * H * 2);    // [TT][E]
+    bf16_t* xs = (bf16_t*)rsm;  // [TT][H]
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int t0 = blockIdx.x * TT, nt = min(TT, T - t0);
+    const int e = blockIdx.y * 4 + wave;
     for (int i = threadIdx.x * 8; i < TT * H; i += 256 * 8) {
         const int t = i / H, c = i % H;
-        *(uint4*)(xs + i) = t < nt ? *(const uint4*)(x + (size_t)(t0 + t) * ldx + c) : make_uint4(0, 0, 0, 0);
+        if (t < nt) *(uint4*)(xs + i) = *(const uint4*)(x + (size_t)(t0 + t) * ldx + c);
     }
     __syncthreads();
-    for (int e = wave; e < E; e += 4) {
-        float acc[TT];
+    if (e >= E) return;
+    float acc[TT];
 #pragma unroll
-        for (int t = 0; t < TT; ++t) acc[t] = 0.f;
-        const float* w = wr + (size_t)e * H;
-        for (int c = lane * 4; c < H; c += 256) {
-            const float4 w4 = *(const float4*)(w + c);
+    for (int t = 0; t < TT; ++t) acc[t] = 0.f;
+    const float* w = wr + (size_t)e * H;
+    for (int c0 = 0; c0 < H; c0 += 256 * 8) {  // up to 8 float4 per lane in flight (H <= 16384 per pass)
+        float4 w4[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int c = c0 + 256 * j + lane * 4;
+            w4[j] = c < H ? *(const float4*)(w + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int c = c0 + 256 * j + lane * 4;
+            if (c >= H) break;
 #pragma unroll
             for (int t = 0; t < TT; ++t) {
-                const uint2 raw = *(const uint2*)(xs + t * H + c);
-                float a0, a1, a2, a3;
-                unpack_act2<F16>(raw.x, a0, a1);
-                unpack_act2<F16>(raw.y, a2, a3);
-                acc[t] += w4.x * a0 + w4.y * a1 + w4.z * a2 + w4.w * a3;
+                if (t < nt) {
+                    const uint2 raw = *(const uint2*)(xs + t * H + c);
+                    float a0, a1, a2, a3;
+                    unpack_act2<F16>(raw.x, a0, a1);
+                    unpack_act2<F16>(raw.y, a2, a3);
+                    acc[t] += w4[j].x * a0 + w4[j].y * a1 + w4[j].z * a2 + w4[j].w * a3;
+                }
             }
         }
+    }
 #pragma unroll
-        for (int t = 0; t < TT; ++t) {
+    for (int t = 0; t < TT; ++t) {
+        if (t < nt) {
             const float s = wave_sum(acc[t]);
-            if (lane == 0) lg[t * E + e] = s;
+            if (lane == 0) logits[(size_t)(t0 + t) * E + e] = s;
         }
     }
-    __syncthreads();
-    for (int t = wave; t < nt; t += 4)
-        route_row<VPL>(lg + t * E, E, k, renorm, ids + (size_t)(t0 + t) * k, wts + (size_t)(t0 + t) * k, lane);
 }
 
-// x 16-bit [T, H] (the normed hidden state), wr fp32 [E, H] -> ids / wts [T, k]; H % 256 == 0
+// x 16-bit [T, H] (the normed hidden state), wr fp32 [E, H] -> logits fp32 [T, E] (workspace) -> ids / wts [T, k];
+// H % 256 == 0
 extern "C" int mxk_moe_router(const void* x, int ldx, const float* wr, int T, int H, int E, int k, int renorm, int* ids,
-                              float* wts, hipStream_t st) {
+                              float* wts, float* logits, hipStream_t st) {
     if (T <= 0) return 0;
-    if (k < 1 || k > 64 || k > E || H % 256 || ldx % 8 || ((uintptr_t)x & 15) || ((uintptr_t)wr & 15))
+    if (k < 1 || k > 64 || k > E || H % 256 || ldx % 8 || ((uintptr_t)x & 15) || ((uintptr_t)wr & 15) || !logits)
         return (int)hipErrorInvalidValue;
     constexpr int TT = 8;
-    const size_t lds = (size_t)TT * H * 2 + (size_t)TT * E * 4;
+    const size_t lds = (size_t)TT * H * 2;
     if (lds > 160 * 1024) return (int)hipErrorInvalidValue;
-    const int blocks = (T + TT - 1) / TT;
-#define MRR(V)                                                                                                   \
-    {                                                                                                            \
-        auto kern = moe_router_kernel<V, TT, F16>;                                                               \
-        (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);      \
-        kern<<<blocks, 256, lds, st>>>((const bf16_t*)x, ldx, wr, T, H, E, k, renorm, ids, wts);                 \
+    const dim3 grid((T + TT - 1) / TT, (E + 3) / 4);
+    MX_ACT_DISPATCH({
+        static bool attr = false;
+        if (!attr && lds > 64 * 1024) {
+            (void)hipFuncSetAttribute((const void*)moe_router_kernel<TT, F16>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            attr = true;
+        }
+        moe_router_kernel<TT, F16><<<grid, 256, lds, st>>>((const bf16_t*)x, ldx, wr, T, H, E, logits);
+    });
+    {
+        const int err = (int)hipGetLastError();
+        if (err) return err;
     }
-    if (E <= 64) {
-        MX_ACT_DISPATCH(MRR(1));
-    } else if (E <= 128) {
-        MX_ACT_DISPATCH(MRR(2));
-    } else if (E <= 256) {
-        MX_ACT_DISPATCH(MRR(4));
-    } else if (E <= 512) {
-        MX_ACT_DISPATCH(MRR(8));
-    } else {
-        return (int)hipErrorInvalidValue;
-    }
-#undef MRR
-    MXK_CHECK_LAUNCH();
+    return mxk_moe_route(logits, E, T, E, k, renorm, ids, wts, st);
 }
 
 extern "C" int mxk_moe_route(const float* logits, int ldl, int T, int E, int k, int renorm, int* ids, float* wts,

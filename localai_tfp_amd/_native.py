@@ -99,8 +99,8 @@ KERNEL_SIGS = {
     "mxk_kvq_append": [I, P, P, P, I, I, I, I, P, P, P],
     # kvf, cache, rows, n, D, out, stream
     "mxk_kvq_dequant_rows": [I, P, P, I, I, P, P],
-    # x, ldx, wr, T, H, E, k, renorm, ids, wts, stream
-    "mxk_moe_router": [P, I, P, I, I, I, I, I, P, P, P],
+    # x, ldx, wr, T, H, E, k, renorm, ids, wts, logits (workspace [T, E] fp32), stream
+    "mxk_moe_router": [P, I, P, I, I, I, I, I, P, P, P, P],
     # qtype, epi, W, N, K, ids, P, e0, El, x, ldx, xdiv, C, ldc, stream
     "mxk_qmv_moe": [I, I, P, I, I, P, I, I, I, P, I, I, P, I, P],
     # qtype, epi, wm, A, lda, stok, W, P, E, N, K, tiles, off, C, ldc, stream

@@ -5,8 +5,8 @@ softmax, top-k, optional weight renormalisation, ggml_mul_mat_id over the stacke
 `ffn_{gate,up,down}_exps` tensors, optional shared expert with a sigmoid gate for Qwen2-MoE).
 
 GPU path (all device-side, hipGraph-capturable):
-    moe_router (moe.hip: the router GEMV over 8 tokens per workgroup with the fp32 router rows read once, logits in
-    LDS, softmax + top-k per wave in the same launch) -> then, with the expert stacks in the t32 layout
+    moe_router (moe.hip: the router GEMV, one expert per wave with its fp32 row requested whole, 8 tokens per
+    workgroup from LDS) -> moe_route (softmax + top-k per wave) -> then, with the expert stacks in the t32 layout
     (models/llama.py finalize_layout; 16-row-interleaved gate|up per expert):
       * decode (P = T k pairs <= GEMV_MAX_PAIRS): qmv_moe (qmv.hip) — one workgroup per (pair, 32 columns of its
         expert), q8 activations, gate|up SwiGLU into [P, F] then down into [P, H] fp32, rows in pair order;
@@ -108,8 +108,9 @@ def moe_ffn(W: MoEWeights, x: torch.Tensor, h: torch.Tensor) -> torch.Tensor:
     if x.dtype in (torch.float16, torch.bfloat16) and H % 256 == 0 and x.stride(1) == 1 and x.stride(0) % 8 == 0 \
             and W.router.is_contiguous():
         N.ensure_act(x.dtype)
+        logits = torch.empty(T, E, dtype=torch.float32, device=x.device)
         N.kcall("mxk_moe_router", x.data_ptr(), x.stride(0), W.router.data_ptr(), T, H, E, k, int(W.renorm),
-                ids.data_ptr(), wts.data_ptr(), st)
+                ids.data_ptr(), wts.data_ptr(), logits.data_ptr(), st)
     else:
         logits = x.float() @ W.router.t()
         N.kcall("mxk_moe_route", logits.data_ptr(), logits.stride(0), T, E, k, int(W.renorm), ids.data_ptr(),
