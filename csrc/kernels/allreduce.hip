@@ -8,8 +8,9 @@
 // xGMI write is seen by the owner's polling loads without any fence); then each rank polls its OWN
 // receive slots until every granule carries this call's tag and sums them in fp32. No separate flag, no
 // barrier: a granule is complete when its tag matches.
-//  * epoch lives in device memory (read at kernel start, bumped by a one-thread kernel after it), so a
-//    captured hipGraph replays correctly; epoch >= 1, the buffers are zeroed at allocation;
+//  * epoch lives in device memory (epoch_ctr[0], read at kernel start) and the last workgroup to finish bumps it
+//    (ticket in epoch_ctr[1]: every workgroup has read the epoch before it takes its ticket), so a captured hipGraph
+//    replays correctly with ONE launch per all-reduce; epoch >= 1, the buffers are zeroed at allocation;
 //  * two parity halves: a rank can only start call e+2 (writing parity e%2 again) after it received
 //    every peer's call-e+1 data, which each peer pushes only after finishing its call-e reads;
 //  * spins are bounded: a peer that never arrives sets *err and the kernel exits (the host raises).
@@ -27,9 +28,9 @@ struct MxArPeers {
 template <bool F16, bool RES>
 __global__ __launch_bounds__(256) void allreduce_1shot_kernel(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
                                                               int ng, int rank, int world, MxArPeers peers,
-                                                              long slot_granules, const uint32_t* epoch_ctr,
+                                                              long slot_granules, uint32_t* epoch_ctr,
                                                               int* err, float2* __restrict__ res) {
-    const uint32_t epoch = *epoch_ctr + 1u;
+    const uint32_t epoch = __hip_atomic_load(epoch_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
     const long par = epoch & 1u;
     const int stride = gridDim.x * blockDim.x;
     // phase 1: push this rank's granules to every rank's slot [par][rank]
@@ -42,7 +43,8 @@ __global__ __launch_bounds__(256) void allreduce_1shot_kernel(const uint32_t* __
     }
     // phase 2: gather every rank's granule i from the local receive buffer, sum in fp32
     unsigned long long* local = peers.recv[rank];
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < ng; i += stride) {
+    bool dead = false;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < ng && !dead; i += stride) {
         float a = 0.f, b = 0.f;
         for (int p = 0; p < world; ++p) {
             unsigned long long* src = local + (par * world + p) * slot_granules + i;
@@ -51,16 +53,19 @@ __global__ __launch_bounds__(256) void allreduce_1shot_kernel(const uint32_t* __
             while ((uint32_t)(g >> 32) != epoch) {
                 if (++spins > (1u << 22)) {  // ~seconds: a dead peer, not a slow one
                     __hip_atomic_fetch_max(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    return;
+                    dead = true;
+                    break;
                 }
                 __builtin_amdgcn_s_sleep(1);
                 g = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             }
+            if (dead) break;
             float lo, hi;
             unpack_act2<F16>((uint32_t)g, lo, hi);
             a += lo;
             b += hi;
         }
+        if (dead) break;
         if constexpr (RES) {
             float2 r = res[i];
             r.x += a;
@@ -70,10 +75,15 @@ __global__ __launch_bounds__(256) void allreduce_1shot_kernel(const uint32_t* __
             out[i] = pack_act2<F16>(a, b);
         }
     }
-}
-
-__global__ void allreduce_epoch_bump_kernel(uint32_t* epoch_ctr) {
-    if (threadIdx.x == 0) epoch_ctr[0] += 1u;
+    // the last workgroup to get here bumps the epoch for the next call and re-arms the ticket
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t t = __hip_atomic_fetch_add(epoch_ctr + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        if (t == gridDim.x - 1) {
+            __hip_atomic_store(epoch_ctr + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(epoch_ctr, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
 }
 
 // ---- host side ----------------------------------------------------------------------------------
@@ -96,7 +106,8 @@ extern "C" int mxk_ar_ipc_close(void* ptr) { return (int)hipIpcCloseMemHandle(pt
 extern "C" int mxk_ar_handle_size() { return (int)sizeof(hipIpcMemHandle_t); }
 
 // in/out: n 16-bit elements (n even, 4-B aligned; out may alias in); peers: world receive-buffer pointers
-// (host array; [rank] = this rank's own buffer); slot_granules >= n / 2; epoch_ctr / err: device words.
+// (host array; [rank] = this rank's own buffer); slot_granules >= n / 2; epoch_ctr: 2 device words {epoch,
+// ticket}, zeroed once; err: device word.
 extern "C" int mxk_allreduce_1shot(const uint16_t* in, uint16_t* out, int n, int rank, int world,
                                    unsigned long long* const* peers, long slot_granules, uint32_t* epoch_ctr,
                                    int* err, hipStream_t st) {
@@ -111,7 +122,6 @@ extern "C" int mxk_allreduce_1shot(const uint16_t* in, uint16_t* out, int n, int
     if (blocks > 128) blocks = 128;
     MX_ACT_DISPATCH((allreduce_1shot_kernel<F16, false><<<blocks, 256, 0, st>>>(
         (const uint32_t*)in, (uint32_t*)out, ng, rank, world, pp, slot_granules, epoch_ctr, err, nullptr)));
-    allreduce_epoch_bump_kernel<<<1, 64, 0, st>>>(epoch_ctr);
     MXK_CHECK_LAUNCH();
 }
 
@@ -130,6 +140,5 @@ extern "C" int mxk_allreduce_1shot_add(const uint16_t* in, float* res, int n, in
     if (blocks > 128) blocks = 128;
     MX_ACT_DISPATCH((allreduce_1shot_kernel<F16, true><<<blocks, 256, 0, st>>>(
         (const uint32_t*)in, nullptr, ng, rank, world, pp, slot_granules, epoch_ctr, err, (float2*)res)));
-    allreduce_epoch_bump_kernel<<<1, 64, 0, st>>>(epoch_ctr);
     MXK_CHECK_LAUNCH();
 }

@@ -1092,8 +1092,15 @@ class LLMEngine:
         t = self._stage_plan(plan, ("tokens", "positions", "slots", "lidx", "dec_bt", "dec_lens", "pf_bt", "pf_cu",
                                     "pf_ctx", "pf_tseq", "pf_tq0"))
         fb = self._build_fb(plan, t)
-        fix = self._fix_tensors(t)
-        if fix is not None:
+        if "fix_dst" in t and fb.tokens.is_cuda:
+            # one kernel (no int64 casts + index_select + index_copy launches)
+            from .. import _native as N
+            prev = self._prev_dev[0]
+            if prev.dtype != torch.int32 or not prev.is_contiguous():
+                prev = prev.to(torch.int32).contiguous()
+            N.kcall("mxk_fix_tokens", fb.tokens.data_ptr(), t["fix_dst"].data_ptr(), t["fix_src"].data_ptr(),
+                    prev.data_ptr(), t["fix_dst"].numel(), N.stream_ptr())
+        elif (fix := self._fix_tensors(t)) is not None:
             dst, src, prev = fix
             fb.tokens.index_copy_(0, dst, prev.index_select(0, src))
         logits = self.model.forward(fb, self.kv, self.ws)

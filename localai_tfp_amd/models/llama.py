@@ -551,10 +551,14 @@ class LlamaModel:
         all-reduces go through the one-shot hipIpc kernel (parallel/custom_ar.py). MX_CUSTOM_AR=0 disables."""
         import os
         import torch.distributed as dist
-        if (self.tp_size <= 1 or self.device.type != "cuda" or os.environ.get("MX_CUSTOM_AR", "1") == "0"
-                or not dist.is_initialized()):  # (single-process shard rehearsal: collectives are no-ops)
+        if self.tp_size <= 1 or self.device.type != "cuda" or os.environ.get("MX_CUSTOM_AR", "1") == "0":
             return None
         from ..parallel.custom_ar import OneShotAllReduce
+        if not dist.is_initialized():
+            # single-process shard rehearsal (bench.py --tp-rehearsal): the same one-launch all-reduce + residual
+            # add over this rank's own slot, so the rehearsal's step has the real path's kernels (minus xGMI)
+            self.custom_ar = OneShotAllReduce(None, self.device, max_bytes, world=1)
+            return self.custom_ar
         self.custom_ar = OneShotAllReduce(self.tp_group, self.device, max_bytes)
         return self.custom_ar
 

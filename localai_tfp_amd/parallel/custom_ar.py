@@ -54,10 +54,14 @@ class OneShotAllReduce:
     MAX_WORLD = 8
 
     def __init__(self, group, device, max_bytes: int = 1 << 20, rank: int | None = None, world: int | None = None):
+        """group None with world 1: a single-rank instance (no process group, no handle exchange) — the same
+        kernel over its own slot only, which the one-GPU tensor-parallel rehearsal runs where the real group's
+        all-reduce + residual add would be (bench.py --tp-rehearsal)."""
         import torch.distributed as dist
+        solo = group is None and world == 1
         self.group = group
-        self.rank = dist.get_rank(group) if rank is None else rank
-        self.world = dist.get_world_size(group) if world is None else world
+        self.rank = 0 if solo else dist.get_rank(group) if rank is None else rank
+        self.world = 1 if solo else dist.get_world_size(group) if world is None else world
         if self.world > self.MAX_WORLD:
             raise ValueError(f"one-shot all-reduce supports up to {self.MAX_WORLD} ranks")
         self.device = torch.device(device)
@@ -68,17 +72,18 @@ class OneShotAllReduce:
         with torch.cuda.device(self.device):
             self.buf = C.c_void_p()
             _ok(lib.mxk_ar_alloc(2 * self.world * self.slot * 8, C.byref(self.buf)), "mxk_ar_alloc")
-            hs = lib.mxk_ar_handle_size()
-            h = (C.c_ubyte * hs)()
-            _ok(lib.mxk_ar_ipc_handle(self.buf, h), "hipIpcGetMemHandle")
-            mine = torch.tensor(bytearray(h), dtype=torch.uint8)
-            # the handle exchange runs on the group's backend: CPU tensors for gloo, device tensors for RCCL
-            on_dev = dist.get_backend(group) == "nccl"
-            src = mine.to(self.device) if on_dev else mine
-            allh = [torch.empty_like(src) for _ in range(self.world)]
-            dist.all_gather(allh, src, group=group)
             self.ptrs = (C.c_void_p * self.world)()
             self._opened = []
+            if not solo:
+                hs = lib.mxk_ar_handle_size()
+                h = (C.c_ubyte * hs)()
+                _ok(lib.mxk_ar_ipc_handle(self.buf, h), "hipIpcGetMemHandle")
+                mine = torch.tensor(bytearray(h), dtype=torch.uint8)
+                # the handle exchange runs on the group's backend: CPU tensors for gloo, device tensors for RCCL
+                on_dev = dist.get_backend(group) == "nccl"
+                src = mine.to(self.device) if on_dev else mine
+                allh = [torch.empty_like(src) for _ in range(self.world)]
+                dist.all_gather(allh, src, group=group)
             for p in range(self.world):
                 if p == self.rank:
                     self.ptrs[p] = self.buf
@@ -88,23 +93,25 @@ class OneShotAllReduce:
                 _ok(lib.mxk_ar_ipc_open(hb, C.byref(ptr)), "hipIpcOpenMemHandle")
                 self.ptrs[p] = ptr
                 self._opened.append(ptr)
-            self.epoch = torch.zeros(1, dtype=torch.int32, device=self.device)
+            self.epoch = torch.zeros(2, dtype=torch.int32, device=self.device)  # {epoch, last-workgroup ticket}
             self.err = torch.zeros(1, dtype=torch.int32, device=self.device)
         # error-flag snapshots: pinned host slots filled by async copies, each with the event that retires it
         self._err_host = torch.zeros(self.SNAP_RING, dtype=torch.int32, pin_memory=self.device.type == "cuda")
         self._snaps: deque = deque()
         self._snap_i = 0
-        dist.barrier(group=group)
+        if not solo:
+            dist.barrier(group=group)
 
     def __call__(self, t: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
         out = t if out is None else out
         n = t.numel()
         if (t.dtype not in (torch.float16, torch.bfloat16) or n * 2 > self.max_bytes or n % 2
                 or not t.is_contiguous() or not out.is_contiguous()):
-            import torch.distributed as dist
             if out is not t:
                 out.copy_(t)
-            dist.all_reduce(out, group=self.group)
+            if self.world > 1:
+                import torch.distributed as dist
+                dist.all_reduce(out, group=self.group)
             return out
         N.ensure_act(t.dtype)
         _ok(self.lib.mxk_allreduce_1shot(t.data_ptr(), out.data_ptr(), n, self.rank, self.world, self.ptrs,

@@ -42,3 +42,42 @@ def test_one_shot_allreduce_multiprocess(world):
     for ln in outs[0].splitlines():  # rank 0's latency lines into the test log
         if "us/call" in ln:
             print(ln)
+
+
+@pytest.mark.gpu
+def test_one_shot_allreduce_single_rank_graph():
+    """World-1 instance (the --tp-rehearsal stand-in): identity all-reduce and residual add, eager and replayed from a
+    hipGraph many times — the in-kernel epoch bump (last workgroup's ticket) must advance once per call."""
+    import torch
+    from localai_tfp_amd.parallel.custom_ar import OneShotAllReduce
+    ar = OneShotAllReduce(None, "cuda", 1 << 20, world=1)
+    g = torch.Generator(device="cuda").manual_seed(0)
+    for n in (2, 4096, 1 << 19):  # 1 .. 128 workgroups
+        t = torch.randn(n, device="cuda", generator=g).to(torch.float16)
+        res = torch.randn(n, device="cuda", generator=g)
+        ref = res + t.float()
+        ar.add_into(t, res)
+        out = torch.empty_like(t)
+        ar(t, out)
+        torch.cuda.synchronize()
+        assert torch.equal(out, t)
+        assert torch.allclose(res, ref, atol=1e-6)
+    e0 = int(ar.epoch[0])
+    assert int(ar.epoch[1]) == 0  # ticket re-armed
+    t = torch.randn(8192, device="cuda", generator=g).to(torch.float16)
+    res = torch.zeros(8192, device="cuda")
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        ar.add_into(t, res)  # warm-up outside capture
+    torch.cuda.current_stream().wait_stream(s)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph, stream=s):
+        ar.add_into(t, res)
+    res.zero_()
+    for _ in range(50):
+        graph.replay()
+    torch.cuda.synchronize()
+    assert torch.allclose(res, 50 * t.float(), atol=1e-3)
+    assert int(ar.epoch[0]) == e0 + 51  # the warm-up call + 50 replays (capture launches nothing)
+    assert int(ar.epoch[1]) == 0

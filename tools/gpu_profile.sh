@@ -21,7 +21,7 @@ case "$mode" in
     conc=${1:-128}; steps=${2:-40}
     cd /tmp && export TMPDIR=/tmp
     timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$R/prof_engine_c$conc" -o run --output-format csv -- \
-      python3 "$ROOT/bench.py" --path engine --concurrency "$conc" --steps "$steps" --warmup 5 --step-group 1 --min-ttft-samples 0 ${MODEL:+--model $MODEL} > "$R/prof_engine_c$conc.log" 2>&1 || exit 1
+      python3 "$ROOT/bench.py" --path engine --concurrency "$conc" --steps "$steps" --warmup 5 --step-group 1 --min-ttft-samples 0 ${MODEL:+--model $MODEL} ${BENCH_ARGS} > "$R/prof_engine_c$conc.log" 2>&1 || exit 1
     cd "$ROOT" && python tools/prof_summary.py "$R/prof_engine_c$conc" --top 40 --steps "$steps" > "$R/prof_engine_c$conc.md"
     tail -45 "$R/prof_engine_c$conc.md"
     ;;
