@@ -20,7 +20,10 @@ model directory (``config.json`` + ``*.safetensors`` [+ ``model.safetensors.inde
   (backend/python/vllm/backend.py:106-107) — are dequantised at load from their packed
   ``qweight / qzeros / scales [/ g_idx]`` tensors, then served like any other checkpoint (bf16 by default,
   or re-blocked with ``quant``). Parity with AutoGPTQ / AutoAWQ kernels is unpinned (not installed here);
-  the formulas are pinned by tests/test_hf_gptq.py's independent packer.
+  the formulas are pinned by tests/test_hf_gptq.py's independent packer;
+* EXL2 (exllamav2, the reference's exllama2 backend: backend/python/exllama2/backend.py:49-56): per-group 2-8-bit
+  codes behind a row permutation (``q_weight / q_scale / q_scale_max / q_groups / q_invperm``), dequantised the
+  same way (:func:`dequant_exl2`; exllamav2 is not importable here, parity unpinned).
 """
 from __future__ import annotations
 
@@ -173,6 +176,70 @@ def dequant_awq(qweight, qzeros, scales, bits: int = 4, group_size: int = 128):
     return np.ascontiguousarray((s[g] * (q - z[g])).T)
 
 
+EXL2_BITS = (2, 3, 4, 5, 6, 8)
+
+
+def _exl2_groupsize(K: int, G: int) -> int:
+    """exllamav2's group size: the smallest power of two whose G groups cover the K input rows."""
+    gs = 1
+    while gs * G < K:
+        gs *= 2
+    return gs
+
+
+def dequant_exl2(q_weight, q_scale, q_scale_max, q_groups, q_invperm):
+    """exllamav2 EXL2 linear -> fp32 weight [N, K] (out, in).
+
+    Layout (exllamav2's QMatrix tensors, reference backend/python/exllama2/backend.py:49-56 loads them):
+      q_groups    int16 [2 G]: per row group (bits b_g, first int32 row of its codes in q_weight); group g covers the
+                  permuted input rows [g gs, (g + 1) gs), gs = _exl2_groupsize(K, G);
+      q_weight    int32 [*, N]: each column's codes of a group as one little-endian bitstream of b_g-bit fields, row
+                  after row (so 32 / b_g rows per word for b in {2, 4, 8}; 16 rows in 3 words at 6 bits, 32 rows in
+                  3 / 5 words at 3 / 5 bits), code value c -> c - 2^(b_g - 1);
+      q_scale     int32 [G, N / 8]: a 4-bit scale code s per (group, column), column n in nibble n % 8;
+      q_scale_max fp16 [G]: the group's scale = ((s + 1) / 16)^2 * q_scale_max[g];
+      q_invperm   int16 [K]: packed row of input feature j (the codes are stored in a permuted row order that sorts the
+                  groups by bit width) — W[:, j] = W_packed[:, q_invperm[j]].
+    exllamav2 is not importable here: the layout is re-stated from its format, parity with its kernels is unpinned
+    (tests/test_hf_gptq.py packs EXL2 tensors independently)."""
+    qw = np.ascontiguousarray(q_weight).view(np.uint32)
+    N = qw.shape[1]
+    qg = np.asarray(q_groups).astype(np.int64) & 0xFFFF
+    G = qg.size // 2
+    bits, start = qg[0::2], qg[1::2]
+    inv = np.asarray(q_invperm).astype(np.int64) & 0xFFFF
+    K = inv.size
+    gs = _exl2_groupsize(K, G)
+    sc = np.ascontiguousarray(q_scale).view(np.uint32)
+    snib = np.empty((G, N), np.float32)
+    for i in range(8):
+        snib[:, i::8] = ((sc >> np.uint32(4 * i)) & 0xF)[:, : (N - i + 7) // 8]
+    scale = ((snib + 1.0) / 16.0) ** 2 * np.asarray(q_scale_max, np.float32).reshape(G, 1)
+    wp = np.empty((K, N), np.float32)  # [packed row, column]
+    g = 0
+    while g < G:  # runs of consecutive groups with one bit width decode as one bitstream
+        b = int(bits[g])
+        if b not in EXL2_BITS:
+            raise ValueError(f"EXL2 group with {b}-bit codes")
+        h = g
+        while h + 1 < G and int(bits[h + 1]) == b and int(start[h + 1]) == int(start[g]) + (h + 1 - g) * gs * b // 32:
+            h += 1
+        r_run0, r_run1 = g * gs, min(K, (h + 1) * gs)
+        for r0 in range(r_run0, r_run1, 1024):  # 1024-row chunks (whole words: 1024 b / 32) bound the bit arrays
+            r1 = min(r_run1, r0 + 1024)
+            w0 = int(start[g]) + (r0 - r_run0) * b // 32
+            words = qw[w0: w0 + -(-(r1 - r0) * b // 32)]  # [words, N]
+            stream = np.unpackbits(np.ascontiguousarray(words.T).view(np.uint8), axis=1, bitorder="little")
+            fields = stream[:, : (r1 - r0) * b].reshape(N, r1 - r0, b)
+            codes = np.zeros((N, r1 - r0), np.int32)
+            for t in range(b):
+                codes |= fields[..., t].astype(np.int32) << t
+            codes -= 1 << (b - 1)
+            wp[r0:r1] = codes.T.astype(np.float32) * scale[np.arange(r0, r1) // gs]
+        g = h + 1
+    return np.ascontiguousarray(wp[inv].T)
+
+
 class _SafetensorsDir:
     """Lazy tensor access over one or more .safetensors shards (fp32 numpy out). With a GPTQ / AWQ
     quantization_config, `<linear>.weight` is served dequantised from `<linear>.qweight / qzeros / scales`."""
@@ -196,17 +263,15 @@ class _SafetensorsDir:
             self.where.update({k: v for k, v in wm.items() if v in self._h})
         self.qcfg = qcfg or {}
         self.qmethod = str(self.qcfg.get("quant_method", "") or "").lower()
-        if self.qmethod == "exl2" or any(k.endswith((".q_invperm", ".q_scale_max", ".q_groups")) for k in self.where):
-            # exllamav2's EXL2 (per-group mixed 2-8-bit codes behind a row permutation): no decoder here —
-            # refused by name instead of failing later on the missing .weight tensors
-            raise ValueError("EXL2 (exllamav2) checkpoints are not supported: convert to GGUF, GPTQ or AWQ "
-                             "(reference backend/python/exllama2/backend.py:45-62)")
-        if self.qmethod and self.qmethod not in ("gptq", "awq"):
-            raise ValueError(f"quantization_config.quant_method {self.qmethod!r} is not supported (gptq / awq)")
+        if any(k.endswith(".q_invperm") for k in self.where):
+            self.qmethod = "exl2"  # exllamav2 EXL2 (per-group mixed 2-8-bit codes behind a row permutation)
+        if self.qmethod and self.qmethod not in ("gptq", "awq", "exl2"):
+            raise ValueError(f"quantization_config.quant_method {self.qmethod!r} is not supported (gptq / awq / exl2)")
 
     def _packed(self, k):
-        return (self.qmethod and k.endswith(".weight") and k not in self.where
-                and k[: -len("weight")] + "qweight" in self.where)
+        if not (self.qmethod and k.endswith(".weight") and k not in self.where):
+            return False
+        return k[: -len("weight")] + ("q_weight" if self.qmethod == "exl2" else "qweight") in self.where
 
     def __contains__(self, k):
         return k in self.where or bool(self._packed(k))
@@ -219,6 +284,9 @@ class _SafetensorsDir:
     def get(self, k) -> np.ndarray:
         if self._packed(k):
             b = k[: -len("weight")]
+            if self.qmethod == "exl2":
+                return dequant_exl2(self.raw(b + "q_weight"), self.raw(b + "q_scale"), self.raw(b + "q_scale_max"),
+                                    self.raw(b + "q_groups"), self.raw(b + "q_invperm"))
             c = self.qcfg
             bits, gs = int(c.get("bits", c.get("w_bit", 4))), int(c.get("group_size", c.get("q_group_size", 128)))
             if self.qmethod == "gptq":

@@ -1,5 +1,6 @@
-"""GPTQ / AWQ HF checkpoints (vLLM `quantization: gptq / awq`, backend/python/vllm/backend.py:106-107; exllama2
-loads GPTQ too): models/hf.py dequantises `qweight / qzeros / scales [/ g_idx]` at load. The packed tensors
+"""GPTQ / AWQ / EXL2 HF checkpoints (vLLM `quantization: gptq / awq`, backend/python/vllm/backend.py:106-107; the
+exllama2 backend's EXL2 and GPTQ, backend/python/exllama2/backend.py:49-56): models/hf.py dequantises `qweight /
+qzeros / scales [/ g_idx]` and EXL2's `q_weight / q_scale / q_scale_max / q_groups / q_invperm` at load. The packed tensors
 here come from an independent packer written in this test (AutoGPTQ v1 zero-point storage, act-order g_idx,
 AWQ's GEMM nibble order); the loaded model's logits match transformers' forward of the same dequantised
 weights. AutoGPTQ / AutoAWQ are not installed: parity with their kernels is unpinned."""
@@ -127,20 +128,111 @@ def test_quantized_hf_dir_matches_transformers(method, tmp_path):
     assert rel < 5e-3, (method, rel)
 
 
-def test_exl2_checkpoint_refused(tmp_path):
-    """exllamav2 EXL2 tensors (q_weight / q_invperm / q_scale_max / q_groups) are refused by name at load."""
-    import json
-    import torch
-    from localai_tfp_amd.models.hf import hf_source
+# ----------------------------------------------------------------------------------------------- EXL2 (exllamav2)
+def exl2_pack(w: np.ndarray, group_bits, gs: int, rng):
+    """Independent EXL2 packer: w [N, K] -> (tensors, dequantised reference [N, K]). Random row permutation, group g
+    of the permuted rows quantised symmetrically at group_bits[g] bits with per-(group, column) 4-bit scale codes
+    against the group's fp16 maximum scale; codes written one Python-int bitstream per column."""
+    N, K = w.shape
+    G = len(group_bits)
+    perm = rng.permutation(K)  # packed row i holds input feature perm[i]
+    wp = w[:, perm]
+    words, groups, qs = [], [], np.zeros((G, N // 8), np.uint32)
+    smax16 = np.zeros(G, np.float16)
+    deq_p = np.zeros((N, K), np.float32)
+    start = 0
+    for g, b in enumerate(group_bits):
+        blk = wp[:, g * gs:(g + 1) * gs]  # [N, rows]
+        need = np.maximum(np.abs(blk).max(1) / (2 ** (b - 1) - 1), 1e-8)
+        smax16[g] = np.float16(need.max())
+        smax = float(smax16[g])
+        s = np.clip(np.ceil(16 * np.sqrt(need / smax)) - 1, 0, 15).astype(np.int64)
+        scale = ((s + 1) / 16.0) ** 2 * smax
+        q = np.clip(np.round(blk / scale[:, None]) + 2 ** (b - 1), 0, 2 ** b - 1).astype(np.int64)
+        deq_p[:, g * gs:(g + 1) * gs] = ((q - 2 ** (b - 1)) * scale[:, None]).astype(np.float32)
+        for n in range(N):
+            qs[g, n // 8] |= np.uint32(s[n] << (4 * (n % 8)))
+        nw = blk.shape[1] * b // 32
+        colw = np.zeros((nw, N), np.uint32)
+        for n in range(N):
+            acc = 0
+            for i, c in enumerate(q[n]):
+                acc |= int(c) << (i * b)
+            for j in range(nw):
+                colw[j, n] = (acc >> (32 * j)) & 0xFFFFFFFF
+        words.append(colw)
+        groups += [b, start]
+        start += nw
+    t = {"q_weight": np.concatenate(words).view(np.int32), "q_scale": qs.view(np.int32), "q_scale_max": smax16,
+         "q_groups": np.array(groups, np.int16), "q_invperm": np.argsort(perm).astype(np.int16)}
+    ref = np.empty_like(deq_p)
+    ref[:, perm] = deq_p
+    return t, ref
+
+
+def test_exl2_dequant_formula():
+    from localai_tfp_amd.models.hf import dequant_exl2
+    rng = np.random.default_rng(0)
+    w = rng.standard_normal((16, 384)).astype(np.float32)
+    bits = [8, 8, 6, 5, 5, 4, 4, 4, 3, 3, 2, 2]  # sorted by width, as exllamav2's permutation leaves them
+    t, ref = exl2_pack(w, bits, 32, rng)
+    got = dequant_exl2(t["q_weight"], t["q_scale"], t["q_scale_max"], t["q_groups"], t["q_invperm"])
+    np.testing.assert_allclose(got, ref, rtol=0, atol=1e-6)
+    assert float(np.abs(got - w).mean()) < 0.3  # a quantisation of w (2-bit groups coarse, 8-bit ones close)
+
+
+def test_exl2_hf_dir_matches_transformers(tmp_path):
+    """A Llama directory with every linear in EXL2 tensors (mixed 8..2-bit groups, quant_method exl2) loads through the
+    vllm / exllama2 path and matches transformers' forward of the same dequantised weights."""
+    torch.manual_seed(0)
+    T = transformers
+    hc = T.LlamaConfig(vocab_size=320, hidden_size=128, intermediate_size=256, num_hidden_layers=2,
+                       num_attention_heads=4, num_key_value_heads=2, max_position_embeddings=512)
+    hc._attn_implementation = "eager"
+    m = T.LlamaForCausalLM(hc).eval()
     d = tmp_path / "exl2"
+    m.save_pretrained(str(d))
+    sd = load_file(str(d / "model.safetensors"))
+    rng = np.random.default_rng(1)
+    deq = {}
+    for k in list(sd):
+        if not any(f".{n}.weight" in k for n in LINEARS):
+            continue
+        w = sd.pop(k).float().numpy()
+        G = w.shape[1] // 32
+        bits = sorted((8, 6, 5, 4)[i % 4] for i in range(G))[::-1]
+        t, ref = exl2_pack(w, bits, 32, rng)
+        base = k[: -len("weight")]
+        for n, a in t.items():
+            sd[base + n] = torch.from_numpy(np.ascontiguousarray(a))
+        deq[k] = torch.from_numpy(ref.copy())
+    (d / "model.safetensors").unlink()
+    save_file(sd, str(d / "model.safetensors"), metadata={"format": "pt"})
+    cj = json.loads((d / "config.json").read_text())
+    cj["quantization_config"] = {"quant_method": "exl2", "version": "0.2.8", "bits": 5.75, "head_bits": 0}
+    (d / "config.json").write_text(json.dumps(cj))
+    with torch.no_grad():
+        sdm = m.state_dict()
+        for k, v in deq.items():
+            sdm[k].copy_(v)
+        prompt = [int(x) for x in np.random.default_rng(3).integers(3, 320, 17)]
+        ref = m(torch.tensor([prompt])).logits[0, -1].float()
+    model, tok, cfg, _ = load_llm(str(d), "cpu", overrides={"hf_quant": "f32"})
+    from test_model_gpu import _run
+    got = _run(model, "cpu", prompt, [])[0][0]
+    rel = float((got - ref).norm() / ref.norm())
+    assert rel < 5e-3, rel
+
+
+def test_unknown_quant_method_refused(tmp_path):
+    from localai_tfp_amd.models.hf import hf_source
+    d = tmp_path / "q"
     d.mkdir()
     cfg = {"architectures": ["LlamaForCausalLM"], "model_type": "llama", "hidden_size": 64, "intermediate_size": 128,
            "num_hidden_layers": 1, "num_attention_heads": 4, "num_key_value_heads": 4, "vocab_size": 32,
-           "rms_norm_eps": 1e-5, "max_position_embeddings": 64}
+           "rms_norm_eps": 1e-5, "max_position_embeddings": 64,
+           "quantization_config": {"quant_method": "hqq"}}
     (d / "config.json").write_text(json.dumps(cfg))
-    sd = {"model.layers.0.self_attn.q_proj.q_weight": torch.zeros(8, 64, dtype=torch.int32),
-          "model.layers.0.self_attn.q_proj.q_invperm": torch.zeros(64, dtype=torch.int16),
-          "model.layers.0.self_attn.q_proj.q_scale_max": torch.zeros(4, dtype=torch.float16)}
-    save_file(sd, str(d / "model.safetensors"), metadata={"format": "pt"})
-    with pytest.raises(ValueError, match="EXL2"):
-        hf_source(str(d), "exl2")
+    save_file({"model.embed_tokens.weight": torch.zeros(32, 64)}, str(d / "model.safetensors"), metadata={"format": "pt"})
+    with pytest.raises(ValueError, match="hqq"):
+        hf_source(str(d), "bf16")
