@@ -75,13 +75,15 @@ __global__ __launch_bounds__(256) void allreduce_1shot_kernel(const uint32_t* __
             out[i] = pack_act2<F16>(a, b);
         }
     }
-    // the last workgroup to get here bumps the epoch for the next call and re-arms the ticket
+    // the last workgroup to get here bumps the epoch for the next call and re-arms the ticket. Relaxed atomics: the
+    // ticket only has to order the epoch reads (every workgroup read it before taking a ticket); no plain data is
+    // published through it, so no release fence (on gfx950 an agent-scope release writes back the whole L2)
     __syncthreads();
     if (threadIdx.x == 0) {
-        const uint32_t t = __hip_atomic_fetch_add(epoch_ctr + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t t = __hip_atomic_fetch_add(epoch_ctr + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (t == gridDim.x - 1) {
             __hip_atomic_store(epoch_ctr + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_fetch_add(epoch_ctr, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(epoch_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
 }

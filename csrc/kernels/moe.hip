@@ -93,31 +93,79 @@ extern "C" int mxk_moe_route(const float* logits, int ldl, int T, int E, int k, 
 // full before any FMA, so a decode step's router costs one load latency instead of one per 256 columns (the first
 // form, one workgroup walking every expert, took 177 us per layer at batch 1: profiles/r6_moe_qwen3_30b.md).
 // The top-k routing then runs as moe_route_kernel over the logits.
-template <int TT, bool F16>
-__global__ __launch_bounds__(256) void moe_router_kernel(const bf16_t* __restrict__ x, int ldx,
+// With `tickets` (one zeroed int per token block): the last expert-block workgroup of a token block to finish runs the
+// top-k routing of its tokens (route_row, one wave per token) — router + route in one launch; it re-arms the ticket.
+// NRM: the FFN RMSNorm fused in front — the workgroup reads its tokens' fp32 residual rows `hs`, normalises them
+// (x = hs / rms(hs) * gamma, rounded to the 16-bit activation type exactly as the norm kernel stores it) into its LDS
+// rows, and the expert-block-0 workgroups also write them to `x` for the expert GEMMs: no separate norm launch.
+template <int TT, bool F16, int VPL, bool NRM>
+__global__ __launch_bounds__(256) void moe_router_kernel(bf16_t* __restrict__ x, int ldx,
                                                          const float* __restrict__ wr, int T, int H, int E,
-                                                         float* __restrict__ logits) {
+                                                         float* __restrict__ logits, int* __restrict__ tickets, int k,
+                                                         int renorm, int* __restrict__ ids, float* __restrict__ wts,
+                                                         const float* __restrict__ hs, int ldh,
+                                                         const float* __restrict__ gamma, float eps) {
     extern __shared__ __attribute__((aligned(16))) char rsm[];
     bf16_t* xs = (bf16_t*)rsm;  // [TT][H]
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int t0 = blockIdx.x * TT, nt = min(TT, T - t0);
     const int e = blockIdx.y * 4 + wave;
-    for (int i = threadIdx.x * 8; i < TT * H; i += 256 * 8) {
-        const int t = i / H, c = i % H;
-        if (t < nt) *(uint4*)(xs + i) = *(const uint4*)(x + (size_t)(t0 + t) * ldx + c);
+    // the wave's router row (first 2048 columns) is requested before the rows are staged / normalised: its load
+    // latency overlaps that work instead of following it
+    const float* w = wr + (size_t)min(e, E - 1) * H;
+    float4 w4[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int c = 256 * j + lane * 4;
+        w4[j] = (c < H && e < E) ? *(const float4*)(w + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    if constexpr (NRM) {
+        __shared__ float s_ss[TT];
+        if (threadIdx.x < TT) s_ss[threadIdx.x] = 0.f;
+        __syncthreads();
+        for (int i = threadIdx.x * 8; i < TT * H; i += 256 * 8) {
+            const int t = i / H, c = i % H;
+            if (t < nt) {
+                const float* r = hs + (size_t)(t0 + t) * ldh + c;
+                const float4 a = *(const float4*)r, b = *(const float4*)(r + 4);
+                atomicAdd(&s_ss[t], a.x * a.x + a.y * a.y + a.z * a.z + a.w * a.w + b.x * b.x + b.y * b.y +
+                                        b.z * b.z + b.w * b.w);
+            }
+        }
+        __syncthreads();
+        for (int i = threadIdx.x * 8; i < TT * H; i += 256 * 8) {
+            const int t = i / H, c = i % H;
+            if (t < nt) {
+                const float rs = rsqrtf(s_ss[t] / (float)H + eps);
+                const float* r = hs + (size_t)(t0 + t) * ldh + c;
+                const float4 a = *(const float4*)r, b = *(const float4*)(r + 4);
+                const float4 ga = *(const float4*)(gamma + c), gb = *(const float4*)(gamma + c + 4);
+                uint4 o;
+                o.x = pack_act2<F16>(a.x * rs * ga.x, a.y * rs * ga.y);
+                o.y = pack_act2<F16>(a.z * rs * ga.z, a.w * rs * ga.w);
+                o.z = pack_act2<F16>(b.x * rs * gb.x, b.y * rs * gb.y);
+                o.w = pack_act2<F16>(b.z * rs * gb.z, b.w * rs * gb.w);
+                *(uint4*)(xs + i) = o;
+                if (blockIdx.y == 0) *(uint4*)(x + (size_t)(t0 + t) * ldx + c) = o;
+            }
+        }
+    } else {
+        for (int i = threadIdx.x * 8; i < TT * H; i += 256 * 8) {
+            const int t = i / H, c = i % H;
+            if (t < nt) *(uint4*)(xs + i) = *(const uint4*)(x + (size_t)(t0 + t) * ldx + c);
+        }
     }
     __syncthreads();
-    if (e >= E) return;
     float acc[TT];
 #pragma unroll
     for (int t = 0; t < TT; ++t) acc[t] = 0.f;
-    const float* w = wr + (size_t)e * H;
-    for (int c0 = 0; c0 < H; c0 += 256 * 8) {  // up to 8 float4 per lane in flight (H <= 16384 per pass)
-        float4 w4[8];
+    for (int c0 = 0; c0 < H && e < E; c0 += 256 * 8) {  // 8 float4 per lane in flight per 2048-column pass
+        if (c0 > 0) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const int c = c0 + 256 * j + lane * 4;
-            w4[j] = c < H ? *(const float4*)(w + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+            for (int j = 0; j < 8; ++j) {
+                const int c = c0 + 256 * j + lane * 4;
+                w4[j] = c < H ? *(const float4*)(w + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
         }
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -139,35 +187,65 @@ __global__ __launch_bounds__(256) void moe_router_kernel(const bf16_t* __restric
     for (int t = 0; t < TT; ++t) {
         if (t < nt) {
             const float s = wave_sum(acc[t]);
-            if (lane == 0) logits[(size_t)(t0 + t) * E + e] = s;
+            if (lane == 0 && e < E) logits[(size_t)(t0 + t) * E + e] = s;
         }
     }
+    if (!tickets) return;
+    __shared__ int s_last;
+    __threadfence();  // release: this workgroup's logits at device scope before its ticket
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const int old = atomicAdd(&tickets[blockIdx.x], 1);
+        s_last = old == (int)gridDim.y - 1;
+        if (s_last) atomicExch(&tickets[blockIdx.x], 0);
+    }
+    __syncthreads();
+    if (!s_last) return;
+    __threadfence();  // acquire: every expert block's logits of these tokens
+    for (int t = wave; t < nt; t += 4)
+        route_row<VPL>(logits + (size_t)(t0 + t) * E, E, k, renorm, ids + (size_t)(t0 + t) * k,
+                       wts + (size_t)(t0 + t) * k, lane);
 }
 
 // x 16-bit [T, H] (the normed hidden state), wr fp32 [E, H] -> logits fp32 [T, E] (workspace) -> ids / wts [T, k];
-// H % 256 == 0
-extern "C" int mxk_moe_router(const void* x, int ldx, const float* wr, int T, int H, int E, int k, int renorm, int* ids,
-                              float* wts, float* logits, hipStream_t st) {
+// H % 256 == 0. tickets: ceil(T / 8) zeroed ints (left zeroed) to route in the same launch, or null (a second launch).
+// hs (fp32 [T, H] residual rows, ldh) + gamma: x is the OUTPUT, hs's RMSNorm (eps) written by the router itself.
+extern "C" int mxk_moe_router(void* x, int ldx, const float* wr, int T, int H, int E, int k, int renorm, int* ids,
+                              float* wts, float* logits, int* tickets, const float* hs, int ldh, const float* gamma,
+                              float eps, hipStream_t st) {
     if (T <= 0) return 0;
     if (k < 1 || k > 64 || k > E || H % 256 || ldx % 8 || ((uintptr_t)x & 15) || ((uintptr_t)wr & 15) || !logits)
         return (int)hipErrorInvalidValue;
+    const bool nrm = hs != nullptr;
+    if (nrm && (!gamma || ldh % 4 || ((uintptr_t)hs & 15) || ((uintptr_t)gamma & 15))) return (int)hipErrorInvalidValue;
     constexpr int TT = 8;
     const size_t lds = (size_t)TT * H * 2;
     if (lds > 160 * 1024) return (int)hipErrorInvalidValue;
     const dim3 grid((T + TT - 1) / TT, (E + 3) / 4);
-    MX_ACT_DISPATCH({
-        static bool attr = false;
-        if (!attr && lds > 64 * 1024) {
-            (void)hipFuncSetAttribute((const void*)moe_router_kernel<TT, F16>,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-            attr = true;
-        }
-        moe_router_kernel<TT, F16><<<grid, 256, lds, st>>>((const bf16_t*)x, ldx, wr, T, H, E, logits);
-    });
+    if (E > 512) return (int)hipErrorInvalidValue;
+#define MRK2(V, N_)                                                                                                  \
+    do {                                                                                                             \
+        static bool attr = false;                                                                                    \
+        if (!attr && lds > 64 * 1024) {                                                                              \
+            (void)hipFuncSetAttribute((const void*)moe_router_kernel<TT, F16, V, N_>,                                \
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                         \
+            attr = true;                                                                                             \
+        }                                                                                                            \
+        moe_router_kernel<TT, F16, V, N_><<<grid, 256, lds, st>>>((bf16_t*)x, ldx, wr, T, H, E, logits, tickets, k,    \
+                                                                  renorm, ids, wts, hs, ldh, gamma, eps);            \
+    } while (0)
+#define MRK(V) MX_ACT_DISPATCH({ if (nrm) MRK2(V, true); else MRK2(V, false); })
+    if (E <= 64) MRK(1);
+    else if (E <= 128) MRK(2);
+    else if (E <= 256) MRK(4);
+    else MRK(8);
+#undef MRK
+#undef MRK2
     {
         const int err = (int)hipGetLastError();
         if (err) return err;
     }
+    if (tickets) return 0;  // routed by the last workgroup of each token block
     return mxk_moe_route(logits, E, T, E, k, renorm, ids, wts, st);
 }
 

@@ -1021,6 +1021,120 @@ extern "C" int mxk_qmv_moe(int qtype, int epi, const uint8_t* W, int N, int K, c
     return (int)hipErrorInvalidValue;
 }
 
+// Token-major grouped down projection with the MoE combine fused: one workgroup per (32-column group of H, token t).
+// The workgroup quantises the token's k pair rows of the SwiGLU activations (act rows t k .. t k + k - 1, q8 per 32)
+// into LDS, then its waves walk the k x (F / 256) weight units of the token's experts (unit i: pair i / nu, unit
+// i % nu), each dot product scaled by the pair's routing weight before the cross-wave reduction, and the workgroup
+// adds the weighted sum into h[t] — no [P, H] buffer, no combine launch, one writer per output (deterministic).
+// Pairs routed outside [e0, e0 + El) (another rank's experts) contribute nothing.
+template <int QT, bool F16>
+__global__ __launch_bounds__(64 * QMV_WAVES) void qmv_moe_down_kernel(const uint8_t* __restrict__ W, int N, int K,
+                                                                      const int* __restrict__ ids,
+                                                                      const float* __restrict__ wts, int k, int e0,
+                                                                      int El, const bf16_t* __restrict__ act, int lda,
+                                                                      float* __restrict__ h, int ldh) {
+    using U = TUnit<QT>;
+    __shared__ float red[QMV_WAVES][32];
+    extern __shared__ __attribute__((aligned(16))) char qmd_smem[];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int r = lane & 31, hh = lane >> 5;
+    const int g = blockIdx.x, t = blockIdx.y;
+    const int nu = K / U::ELEMS, total = k * nu;
+    int8_t* sq = (int8_t*)qmd_smem;                      // [k][K]
+    float2* sd = (float2*)(qmd_smem + (size_t)k * K);    // [k][K / 32]
+    // unit j of this wave: flat index wave + QMV_WAVES j -> (pair, unit); weights requested before the quantisation
+    auto unit_ptr = [&](int i, int& pr, int& ok) -> const uint8_t* {
+        pr = min(i / nu, k - 1);  // (i >= total: a valid pair index, never used)
+        const int e = ids[(size_t)t * k + pr] - e0;
+        ok = i < total && e >= 0 && e < El;
+        return W + ((size_t)(ok ? e : 0) * (N >> 5) + g) * ((size_t)nu * U::BYTES) + (size_t)(i % nu) * U::BYTES;
+    };
+    U a, b;
+    int pa = 0, pb = 0, oka = 0, okb = 0;
+    int i = wave;
+    {
+        const uint8_t* pa_ = unit_ptr(i, pa, oka);
+        if (oka) a.load(pa_, r, hh);
+        const uint8_t* pb_ = unit_ptr(i + QMV_WAVES, pb, okb);
+        if (okb) b.load(pb_, r, hh);
+    }
+    for (int e8 = threadIdx.x * 8; e8 < k * K; e8 += 64 * QMV_WAVES * 8) {
+        const int j = e8 / K, c = e8 % K;
+        float a8[8];
+        const uint4 raw = *(const uint4*)(act + ((size_t)t * k + j) * lda + c);
+        unpack_act2<F16>(raw.x, a8[0], a8[1]);
+        unpack_act2<F16>(raw.y, a8[2], a8[3]);
+        unpack_act2<F16>(raw.z, a8[4], a8[5]);
+        unpack_act2<F16>(raw.w, a8[6], a8[7]);
+        float am = 0.f;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) am = fmaxf(am, fabsf(a8[q]));
+        am = group_max<4>(am);
+        const float d = am / 127.f, id = d > 0.f ? 1.f / d : 0.f;
+        int q8[8], sum = 0;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) { q8[q] = __float2int_rn(a8[q] * id); sum += q8[q]; }
+        const float sf = group_sum<4>((float)sum);
+        uint2 pk;
+        pk.x = (q8[0] & 0xFF) | ((q8[1] & 0xFF) << 8) | ((q8[2] & 0xFF) << 16) | ((uint32_t)(q8[3] & 0xFF) << 24);
+        pk.y = (q8[4] & 0xFF) | ((q8[5] & 0xFF) << 8) | ((q8[6] & 0xFF) << 16) | ((uint32_t)(q8[7] & 0xFF) << 24);
+        *(uint2*)(sq + e8) = pk;
+        if ((threadIdx.x & 3) == 0) sd[e8 / 32] = make_float2(d, d * sf);
+    }
+    __syncthreads();
+    float acc = 0.f;
+    while (i < total) {
+        if (oka) {
+            const int u = i % nu;
+            acc += wts[(size_t)t * k + pa] * a.dot(sq + (size_t)pa * K + (size_t)u * U::ELEMS,
+                                                   sd + (size_t)pa * (K / 32) + u * (U::ELEMS / 32), hh);
+        }
+        if (okb) {
+            const int u = (i + QMV_WAVES) % nu;
+            acc += wts[(size_t)t * k + pb] * b.dot(sq + (size_t)pb * K + (size_t)u * U::ELEMS,
+                                                   sd + (size_t)pb * (K / 32) + u * (U::ELEMS / 32), hh);
+        }
+        i += 2 * QMV_WAVES;
+        const uint8_t* pa_ = unit_ptr(i, pa, oka);
+        if (oka) a.load(pa_, r, hh);
+        const uint8_t* pb_ = unit_ptr(i + QMV_WAVES, pb, okb);
+        if (okb) b.load(pb_, r, hh);
+    }
+    {
+        const float v = acc + __shfl_xor(acc, 32);
+        if (hh == 0) red[wave][r] = v;
+    }
+    __syncthreads();
+    if (wave != 0 || hh != 0) return;
+    float v = 0.f;
+#pragma unroll
+    for (int w = 0; w < QMV_WAVES; ++w) v += red[w][r];
+    h[(size_t)t * ldh + g * 32 + r] += v;
+}
+
+// h [T, N] fp32 += sum_j wts[t, j] * (act[t k + j] . W_{ids[t, j] - e0}^T): W t32 expert stack [El * N, K], act 16-bit
+// [T k, K] (the SwiGLU output rows in pair order). N % 32 == 0, K % 256 == 0, k K + k K / 4 <= 64 KB.
+extern "C" int mxk_qmv_moe_down(int qtype, const uint8_t* W, int N, int K, const int* ids, const float* wts, int T,
+                                int k, int e0, int El, const void* act, int lda, float* h, int ldh, hipStream_t st) {
+    if (T <= 0) return 0;
+    const size_t lds = (size_t)k * K + (size_t)k * K / 32 * sizeof(float2);
+    if (K % 256 || N % 32 || k < 1 || lds > 64 * 1024 || ((uintptr_t)act & 15) || (lda % 8))
+        return (int)hipErrorInvalidValue;
+    const dim3 grid(N / 32, T);
+#define QMD(QT_)                                                                                                  \
+    MX_ACT_DISPATCH(qmv_moe_down_kernel<QT_, F16><<<grid, 64 * QMV_WAVES, lds, st>>>(W, N, K, ids, wts, k, e0, El, \
+                                                                                     (const bf16_t*)act, lda, h, ldh)); \
+    MXK_CHECK_LAUNCH();
+    switch (qtype) {
+        case MXQ_Q4_K: { QMD(MXQ_Q4_K) }
+        case MXQ_Q5_K: { QMD(MXQ_Q5_K) }
+        case MXQ_Q6_K: { QMD(MXQ_Q6_K) }
+        case MXQ_Q8_0: { QMD(MXQ_Q8_0) }
+    }
+#undef QMD
+    return (int)hipErrorInvalidValue;
+}
+
 extern "C" int mxk_dequant_t32(int qtype, const uint8_t* W, const int* rows, int nrows, int K, uint16_t* ob,
                                float* of, int ldo, hipStream_t st) {
     if (nrows <= 0) return 0;

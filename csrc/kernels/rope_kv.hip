@@ -109,16 +109,20 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(float* __restrict__ qkv, c
     }
 }
 
-// Vectorised variant for the common case (rot_dim == D in {64, 128}, no per-head QK norm): each thread owns
-// whole rotation pairs — 4 consecutive dims (NORM: two adjacent pairs) or 4 dims + their partners D/2 away
-// (NEOX) — so every element is loaded once as a float4, written as 8-byte bf16 / 4-byte fp8 runs, and the
-// head / dim split is shifts instead of divisions.
-template <int D, bool NEOX, bool HAS_BIAS, bool ZERO, bool KV8>
+// Vectorised variant for the common case (rot_dim == D in {64, 128}): each thread owns whole rotation pairs — 4
+// consecutive dims (NORM: two adjacent pairs) or 4 dims + their partners D/2 away (NEOX) — so every element is loaded
+// once as a float4, written as 8-byte bf16 / 4-byte fp8 runs, and the head / dim split is shifts instead of
+// divisions. QKN (Qwen3 / Gemma-3 per-head RMSNorm of q and k before the rotation): a head's UPH threads are
+// consecutive lanes of one wave, so its sum of squares is a UPH-lane shuffle reduction of the values already in
+// registers (no LDS pass, no second read of the row).
+template <int D, bool NEOX, bool HAS_BIAS, bool ZERO, bool KV8, bool QKN = false>
 __global__ __launch_bounds__(256) void rope_kv4_kernel(float* __restrict__ qkv, const float* __restrict__ bias,
                                                        const int* __restrict__ pos, const int* __restrict__ slots,
                                                        const float* __restrict__ inv_freq, float attn_factor, int Hq,
                                                        int Hkv, bf16_t* __restrict__ qo, void* __restrict__ kc,
-                                                       void* __restrict__ vc, int block_size) {
+                                                       void* __restrict__ vc, int block_size,
+                                                       const float* __restrict__ qn = nullptr,
+                                                       const float* __restrict__ kn = nullptr, float eps = 0.f) {
     constexpr int HALF = D / 2;
     constexpr int UPH = NEOX ? D / 8 : D / 4;  // work units per head
     constexpr int USH = UPH == 8 ? 3 : UPH == 16 ? 4 : 5;
@@ -180,7 +184,16 @@ __global__ __launch_bounds__(256) void rope_kv4_kernel(float* __restrict__ qkv, 
         const int h = h_lo + (idx >> USH), u = idx & (UPH - 1);
         if constexpr (NEOX) {
             const int d = 4 * u;  // dims d..d+3 and their partners d+HALF..
-            const float4 a = idx == threadIdx.x ? a0 : ld4(h * D + d), b = idx == threadIdx.x ? b0 : ld4(h * D + d + HALF);
+            float4 a = idx == threadIdx.x ? a0 : ld4(h * D + d), b = idx == threadIdx.x ? b0 : ld4(h * D + d + HALF);
+            if constexpr (QKN) {
+                const float ss = group_sum<UPH>(a.x * a.x + a.y * a.y + a.z * a.z + a.w * a.w + b.x * b.x + b.y * b.y +
+                                                b.z * b.z + b.w * b.w);
+                const float rs = rsqrtf(ss / D + eps);
+                const float* nw = h < Hq ? qn : kn;
+                const float4 na = *(const float4*)(nw + d), nb = *(const float4*)(nw + d + HALF);
+                a.x *= rs * na.x; a.y *= rs * na.y; a.z *= rs * na.z; a.w *= rs * na.w;
+                b.x *= rs * nb.x; b.y *= rs * nb.y; b.z *= rs * nb.z; b.w *= rs * nb.w;
+            }
             float4 ya, yb;
             ya.x = a.x * cs[d] - b.x * sn[d];         yb.x = b.x * cs[d] + a.x * sn[d];
             ya.y = a.y * cs[d + 1] - b.y * sn[d + 1]; yb.y = b.y * cs[d + 1] + a.y * sn[d + 1];
@@ -194,7 +207,13 @@ __global__ __launch_bounds__(256) void rope_kv4_kernel(float* __restrict__ qkv, 
             }
         } else {
             const int d = 4 * u, f = 2 * u;  // pairs (d, d+1) and (d+2, d+3): frequencies f, f+1
-            const float4 x = idx == threadIdx.x ? a0 : ld4(h * D + d);
+            float4 x = idx == threadIdx.x ? a0 : ld4(h * D + d);
+            if constexpr (QKN) {
+                const float ss = group_sum<UPH>(x.x * x.x + x.y * x.y + x.z * x.z + x.w * x.w);
+                const float rs = rsqrtf(ss / D + eps);
+                const float4 nw = *(const float4*)((h < Hq ? qn : kn) + d);
+                x.x *= rs * nw.x; x.y *= rs * nw.y; x.z *= rs * nw.z; x.w *= rs * nw.w;
+            }
             float4 y;
             y.x = x.x * cs[f] - x.y * sn[f];
             y.y = x.y * cs[f] + x.x * sn[f];
@@ -238,8 +257,16 @@ extern "C" int mxk_rope_kv(float* qkv, const float* bias, const int* pos, const 
     int ng = (512 + T - 1) / T;
     ng = max(1, min(ng, min(8, Hkv)));
     const dim3 grid(T, ng);
-    if (!qkn && rot_dim == D && (D == 64 || D == 128) && !(((uintptr_t)qkv) & 15) && !(((uintptr_t)bias) & 15)) {
-#define RK4(D_, N_, B_, Z_, K8_) rope_kv4_kernel<D_, N_, B_, Z_, K8_><<<grid, 256, 0, st>>>(qkv, bias, pos, slots, inv_freq, attn_factor, Hq, Hkv, qo, kc, vc, block_size)
+    if (rot_dim == D && (D == 64 || D == 128) && !(((uintptr_t)qkv) & 15) && !(((uintptr_t)bias) & 15) &&
+        (!qkn || (!(((uintptr_t)qn) & 15) && !(((uintptr_t)kn) & 15)))) {
+#define RK4(D_, N_, B_, Z_, K8_)                                                                                         \
+    do {                                                                                                                 \
+        if (qkn) rope_kv4_kernel<D_, N_, B_, Z_, K8_, true><<<grid, 256, 0, st>>>(qkv, bias, pos, slots, inv_freq,       \
+                                                                                  attn_factor, Hq, Hkv, qo, kc, vc,      \
+                                                                                  block_size, qn, kn, eps);              \
+        else rope_kv4_kernel<D_, N_, B_, Z_, K8_><<<grid, 256, 0, st>>>(qkv, bias, pos, slots, inv_freq, attn_factor,    \
+                                                                        Hq, Hkv, qo, kc, vc, block_size);                \
+    } while (0)
 #define RK4Z(D_, N_, B_) { if (zero_after) { if (kv_fp8) RK4(D_, N_, B_, true, true); else RK4(D_, N_, B_, true, false); } \
                            else { if (kv_fp8) RK4(D_, N_, B_, false, true); else RK4(D_, N_, B_, false, false); } }
 #define RK4B(D_, N_) { if (bias) RK4Z(D_, N_, true) else RK4Z(D_, N_, false) }

@@ -673,15 +673,15 @@ class LlamaModel:
                 LR.add_residual(lo.o, attn, h)
             # ---- FFN block ----
             if L.moe is not None:
-                K.rmsnorm(h, L.ffn_norm, eps, out_bf16=xb)
+                # the FFN norm runs inside the MoE router kernel (GPU fast path) or just before it
                 if self.tp_size > 1:  # expert parallel: this rank's experts' share, summed over ranks
                     y = ws.moe_y[:T]
                     y.zero_()
-                    moe_ffn(L.moe, xb, y)
+                    moe_ffn(L.moe, xb, y, norm=(h, L.ffn_norm, eps))
                     self._allreduce(y)
                     h.add_(y)
                 else:
-                    moe_ffn(L.moe, xb, h)
+                    moe_ffn(L.moe, xb, h, norm=(h, L.ffn_norm, eps))
                 continue
             act = ws.act[:T]
             if lo is not None and lo.gate_up is not None:

@@ -6,14 +6,16 @@ softmax, top-k, optional weight renormalisation, ggml_mul_mat_id over the stacke
 
 GPU path (all device-side, hipGraph-capturable):
     moe_router (moe.hip: the router GEMV, one expert per wave with its fp32 row requested whole, 8 tokens per
-    workgroup from LDS) -> moe_route (softmax + top-k per wave) -> then, with the expert stacks in the t32 layout
-    (models/llama.py finalize_layout; 16-row-interleaved gate|up per expert):
+    workgroup from LDS; the last workgroup of each token block runs the softmax + top-k, so router and routing are
+    one launch) -> then, with the expert stacks in the t32 layout (models/llama.py finalize_layout;
+    16-row-interleaved gate|up per expert):
       * decode (P = T k pairs <= GEMV_MAX_PAIRS): qmv_moe (qmv.hip) — one workgroup per (pair, 32 columns of its
-        expert), q8 activations, gate|up SwiGLU into [P, F] then down into [P, H] fp32, rows in pair order;
+        expert), q8 activations, gate|up SwiGLU into [P, F]; then qmv_moe_down — one workgroup per (token, 32
+        columns of H) walks the token's k experts and adds the routing-weighted sum into h (the combine fused: no
+        [P, H] buffer, one writer per output);
       * larger batches: moe_sort (counting sort of the pairs by expert, per-expert tile prefix) -> grouped qmm2
         (qmm2_impl.h Q2Group: 32- / 64-row MFMA tiles per expert, A rows gathered through the sort) for gate|up
-        SwiGLU and down;
-    -> moe_combine (h += sum_j w_j * y_j, fixed order). Expert stacks that do not fit the t32 layout (a row count
+        SwiGLU and down -> moe_combine (h += sum_j w_j * y_j, fixed order). Expert stacks that do not fit the t32 layout (a row count
     per expert or K that is not whole 32-row groups / 256-k super-blocks) keep the row layout and the qgemm16
     grouped kernel.
 CPU path: the same math with dequantised fp32 expert weights (numerics oracle).
@@ -25,6 +27,7 @@ from dataclasses import dataclass
 import torch
 
 from .. import _native as N
+from . import core as K
 from .linear import ACT_DTYPE, EPI_F32, EPI_SWIGLU, QWeight, qmatmul
 
 E16_F32, E16_SWIGLU = 0, 3
@@ -88,29 +91,62 @@ def route_ref(logits: torch.Tensor, k: int, renorm: bool):
     return ids.int(), w
 
 
+_TICKETS: dict = {}
+# top-k in the router launch (last workgroup of a token block, after a device-scope fence): off by default — the
+# fence writes back the L2 on gfx950 and at c64 the fused router took 48 us / layer against 15 + 7 us for two launches
+# (profiles/r6_moe_qwen3_30b.md)
+ROUTE_FUSE = __import__("os").environ.get("MX_MOE_ROUTE_FUSE", "0") == "1"
+# FFN RMSNorm inside the router launch for batches of at most one router token block (8 rows): c1 352 vs 339 tok/s;
+# above, every expert-block workgroup would redo its tokens' norm (c64 7,531 vs 7,668 unfused)
+NORM_FUSE = __import__("os").environ.get("MX_MOE_NORM_FUSE", "1") != "0"
+NORM_FUSE_MAX_T = 8
+
+
+def _router_tickets(dev, n: int) -> torch.Tensor:
+    """Per-device zeroed ints for the router's last-workgroup routing (the kernel leaves them zeroed, so one buffer
+    serves every layer and graph replay). Allocated outside capture by the first (warm-up) forward of a size."""
+    t = _TICKETS.get(dev)
+    if t is None or t.numel() < n:
+        t = torch.zeros(max(n, 8192), dtype=torch.int32, device=dev)  # 64k tokens: never regrown under capture
+        _TICKETS[dev] = t
+    return t
+
+
 def _grouped_wm(P: int, E: int) -> int:
     avg = P / max(1, min(E, P))
     return 1 if avg <= 16 else 2 if avg <= 40 else 4
 
 
-def moe_ffn(W: MoEWeights, x: torch.Tensor, h: torch.Tensor) -> torch.Tensor:
-    """h [T, H] fp32 += MoE(x); x is the normed hidden state in 16-bit (GPU) or fp32 (CPU)."""
+def moe_ffn(W: MoEWeights, x: torch.Tensor, h: torch.Tensor, norm: tuple | None = None) -> torch.Tensor:
+    """h [T, H] fp32 += MoE(x); x is the normed hidden state in 16-bit (GPU) or fp32 (CPU). norm = (src fp32 [T, H],
+    gamma, eps): x is then the OUTPUT buffer of src's RMSNorm — on the GPU fast path the router kernel computes it
+    (no separate norm launch), otherwise the norm kernel runs first."""
     T = x.shape[0]
     if T == 0:
         return h
     E, k, F = W.n_expert, W.n_used, W.ffn
     H = h.shape[1]
     if not x.is_cuda:
+        if norm is not None:
+            K.rmsnorm(norm[0], norm[1], norm[2], out_bf16=x)
         return _moe_ref(W, x.float(), h)
     ids = torch.empty(T, k, dtype=torch.int32, device=x.device)
     wts = torch.empty(T, k, dtype=torch.float32, device=x.device)
     st = N.stream_ptr()
-    if x.dtype in (torch.float16, torch.bfloat16) and H % 256 == 0 and x.stride(1) == 1 and x.stride(0) % 8 == 0 \
-            and W.router.is_contiguous():
+    fast = (x.dtype in (torch.float16, torch.bfloat16) and H % 256 == 0 and x.stride(1) == 1 and x.stride(0) % 8 == 0
+            and W.router.is_contiguous() and E <= 512)
+    fuse_norm = (fast and NORM_FUSE and T <= NORM_FUSE_MAX_T and norm is not None and norm[0].dtype == torch.float32 and norm[0].stride(1) == 1
+                 and norm[0].stride(0) % 4 == 0 and norm[1].dtype == torch.float32 and norm[1].is_contiguous())
+    if norm is not None and not fuse_norm:
+        K.rmsnorm(norm[0], norm[1], norm[2], out_bf16=x)
+    if fast:
         N.ensure_act(x.dtype)
         logits = torch.empty(T, E, dtype=torch.float32, device=x.device)
+        tk = _router_tickets(x.device, (T + 7) // 8) if ROUTE_FUSE else None
+        hs, g, eps = norm if fuse_norm else (None, None, 0.0)
         N.kcall("mxk_moe_router", x.data_ptr(), x.stride(0), W.router.data_ptr(), T, H, E, k, int(W.renorm),
-                ids.data_ptr(), wts.data_ptr(), logits.data_ptr(), st)
+                ids.data_ptr(), wts.data_ptr(), logits.data_ptr(), N.ptr(tk), N.ptr(hs), hs.stride(0) if fuse_norm else 0,
+                N.ptr(g), float(eps), st)
     else:
         logits = x.float() @ W.router.t()
         N.kcall("mxk_moe_route", logits.data_ptr(), logits.stride(0), T, E, k, int(W.renorm), ids.data_ptr(),
@@ -166,16 +202,22 @@ def _experts_t32(W: MoEWeights, x: torch.Tensor, h: torch.Tensor, ids: torch.Ten
     gu, d = W.gate_up, W.down
     N.ensure_act(x.dtype)
     act = torch.empty(P, F, dtype=x.dtype, device=x.device)
-    # rows of pairs routed to another rank's experts stay zero (weight 0 in the combine)
-    y = (torch.zeros if El != E else torch.empty)(P, H, dtype=torch.float32, device=x.device)
     if P <= GEMV_MAX_PAIRS:
         N.kcall("mxk_qmv_moe", int(gu.qtype), E16_SWIGLU, gu.data.data_ptr(), 2 * F, gu.K, ids.data_ptr(), P, W.e0,
                 El, x.data_ptr(), x.stride(0), k, act.data_ptr(), act.stride(0), st)
+        if k * d.K * 5 // 4 <= 64 * 1024 and h.stride(1) == 1:
+            # down + combine in one launch: h[t] += sum_j w_tj (act_tj . W_e(tj)) (off-rank pairs contribute nothing)
+            N.kcall("mxk_qmv_moe_down", int(d.qtype), d.data.data_ptr(), H, d.K, ids.data_ptr(), wts.data_ptr(), T, k,
+                    W.e0, El, act.data_ptr(), act.stride(0), h.data_ptr(), h.stride(0), st)
+            return
+        y = (torch.zeros if El != E else torch.empty)(P, H, dtype=torch.float32, device=x.device)
         N.kcall("mxk_qmv_moe", int(d.qtype), E16_F32, d.data.data_ptr(), H, d.K, ids.data_ptr(), P, W.e0, El,
                 act.data_ptr(), act.stride(0), 1, y.data_ptr(), y.stride(0), st)
         N.kcall("mxk_moe_combine", y.data_ptr(), y.stride(0), None, wts.data_ptr(), T, k, H, h.data_ptr(),
                 h.stride(0), 1, st)
         return
+    # rows of pairs routed to another rank's experts stay zero (weight 0 in the combine)
+    y = (torch.zeros if El != E else torch.empty)(P, H, dtype=torch.float32, device=x.device)
     if El != E:  # expert parallelism: other ranks' pairs go to a null bucket El, sorted last, never computed
         loc = ids - W.e0
         off_rank = (loc < 0) | (loc >= El)

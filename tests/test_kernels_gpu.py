@@ -158,20 +158,30 @@ def _rope_setup(T, Hq, Hkv, D, nb, bs, seed=0):
     return qkv, pos, slots
 
 
+@pytest.mark.parametrize("qkn", [False, True])
 @pytest.mark.parametrize("neox", [False, True])
 @pytest.mark.parametrize("D,rot", [(128, 128), (64, 64), (128, 64)])
-def test_rope_kv(neox, D, rot):
+def test_rope_kv(neox, D, rot, qkn):
+    """RoPE + KV append (the vectorised kernel for rot == D in {64, 128}, incl. the QK-norm form; the general kernel
+    for partial rotation) against the fp32 CPU path."""
     T, Hq, Hkv, nb, bs = 9, 8, 2, 8, 16
     qkv, pos, slots = _rope_setup(T, Hq, Hkv, D, nb, bs)
     bias = torch.randn((Hq + 2 * Hkv) * D) * 0.1
     inv, af = K.rope_inv_freq(rot, 500000.0)
+    g = torch.Generator().manual_seed(5)
+    nq, nk = 1 + 0.3 * torch.randn(D, generator=g), 1 + 0.3 * torch.randn(D, generator=g)
     outs = []
     for dev in ("cpu", DEV):
         q = torch.empty(T, Hq, D, dtype=torch.bfloat16, device=dev)
         kc = torch.zeros(nb, Hkv, bs, D, dtype=torch.bfloat16, device=dev)
         vc = torch.zeros_like(kc)
-        K.rope_kv(qkv.to(dev), bias.to(dev), pos.to(dev), slots.to(dev), inv.to(dev), af, Hq, Hkv, D, rot, neox, q, kc, vc, bs)
+        K.rope_kv(qkv.to(dev), bias.to(dev), pos.to(dev), slots.to(dev), inv.to(dev), af, Hq, Hkv, D, rot, neox, q, kc, vc, bs,
+                  qk_norm=(nq.to(dev), nk.to(dev), 1e-6) if qkn else None)
         outs.append((q.cpu(), kc.cpu(), vc.cpu()))
+    if qkn:
+        for a, b in zip(*outs):
+            assert rel(b, a) < 1e-2
+        return
     for a, b in zip(*outs):
         assert rel(b, a) < 1e-2
     # zero_after: the fp32 QKV rows are handed back zeroed (the next split-K GEMM accumulates into them)

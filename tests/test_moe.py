@@ -177,6 +177,36 @@ def test_moe_ffn_gpu_matches_fp32(E, k, H, F, qt, renorm, t32):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("T", [1, 5, 37, 300])
+def test_moe_router_fused_norm_gpu(T):
+    """moe_ffn(norm=(h, gamma, eps)): the router kernel computes the FFN RMSNorm (and writes the normed rows the expert
+    GEMMs read) — same result as the norm kernel followed by the unfused layer, and the written rows match it."""
+    from localai_tfp_amd.ops import core as K
+    from localai_tfp_amd.ops.linear import ACT_DTYPE, interleave_gate_up
+    E, k, H, F, qt = 128, 8, 256, 768, QType.Q4_K
+    rng = np.random.default_rng(3)
+    raws = {n: random_quantized(rng, qt, r, c, std=0.05).reshape(r, -1)
+            for n, r, c in (("g", E * F, H), ("u", E * F, H), ("d", E * H, F))}
+    g = QWeight.from_ggml(raws["g"], int(qt), E * F, H, "cuda")
+    u = QWeight.from_ggml(raws["u"], int(qt), E * F, H, "cuda")
+    d = QWeight.from_ggml(raws["d"], int(qt), E * H, F, "cuda")
+    w = MO.MoEWeights(router=(torch.randn(E, H) * 0.5).cuda(), gate=None, up=None, gate_up=interleave_gate_up(g, u),
+                      down=d, n_expert=E, n_used=k, ffn=F, renorm=True)
+    assert w.to_t32()
+    h = torch.randn(T, H, device="cuda") * 3
+    gamma = (1 + 0.2 * torch.randn(H)).cuda()
+    xa = torch.empty(T, H, dtype=ACT_DTYPE, device="cuda")
+    K.rmsnorm(h, gamma, 1e-6, out_bf16=xa)
+    ref = MO.moe_ffn(w, xa, h.clone())
+    xb = torch.empty_like(xa)
+    got = MO.moe_ffn(w, xb, h.clone(), norm=(h, gamma, 1e-6))
+    torch.cuda.synchronize()
+    assert float((xb.float() - xa.float()).abs().max()) <= 2e-3 * float(xa.float().abs().max())
+    rel = float((got - ref).norm() / (ref - h).norm())
+    assert rel < 1e-2, rel
+
+
+@pytest.mark.gpu
 def test_moe_model_gpu_matches_cpu_and_engine():
     from localai_tfp_amd.engine.engine import EngineConfig, LLMEngine
     from localai_tfp_amd.ops.sampling import SamplingParams

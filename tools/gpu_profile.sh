@@ -4,6 +4,8 @@
 #
 #   bash tools/gpu_profile.sh engine [CONC] [STEPS]   rocprofv3 kernel trace of the in-process engine bench at
 #                                                    concurrency CONC (default 128): per-kernel table per step
+#   bash tools/gpu_profile.sh window [CONC] [STEPS] [WIN_MS]  the same from a rocpd trace, restricted to the last WIN_MS
+#                                                    of kernels: per-step tables (decode-only / mixed) and launch gaps
 #   bash tools/gpu_profile.sh pmc SHAPE M CFG          counter passes (MFMA / VALU / LDS / waits) of one qmm2
 #                                                    configuration "wm,ks,wn,splits" on a Llama-3-8B projection
 #   bash tools/gpu_profile.sh gemm [MS] [SHAPES]       default (untuned-rule) GEMM dispatch against M, one-launch vs
@@ -24,6 +26,18 @@ case "$mode" in
       python3 "$ROOT/bench.py" --path engine --concurrency "$conc" --steps "$steps" --warmup 5 --step-group 1 --min-ttft-samples 0 ${MODEL:+--model $MODEL} ${BENCH_ARGS} > "$R/prof_engine_c$conc.log" 2>&1 || exit 1
     cd "$ROOT" && python tools/prof_summary.py "$R/prof_engine_c$conc" --top 40 --steps "$steps" > "$R/prof_engine_c$conc.md"
     tail -45 "$R/prof_engine_c$conc.md"
+    ;;
+  window)
+    # rocpd trace of the engine bench; table over the last WIN ms (the steady state, after tuning / capture), per-step
+    # split (decode-only vs mixed) by the step's first kernel (the embedding gather) and the inter-kernel gaps
+    conc=${1:-128}; steps=${2:-200}; win=${3:-1000}
+    cd /tmp && export TMPDIR=/tmp
+    timeout -k 10 600 rocprofv3 --kernel-trace -d "$R/profw_c$conc" -o run -- \
+      python3 "$ROOT/bench.py" --path engine --concurrency "$conc" --steps "$steps" --warmup 5 --step-group 1 --min-ttft-samples 0 ${MODEL:+--model $MODEL} ${BENCH_ARGS} > "$R/profw_c$conc.log" 2>&1 || exit 1
+    db=$(find "$R/profw_c$conc" -name '*.db' | head -1)
+    cd "$ROOT" && python tools/rocpd_summary.py "$db" --window-ms "$win" --split-steps dequant_rows --gaps --top 30 > "$R/profw_c$conc.md" || exit 1
+    rm -rf "$R/profw_c$conc"
+    head -40 "$R/profw_c$conc.md"
     ;;
   pmc)
     shape=$1; M=$2; cfg=$3; t=$(echo "$cfg" | tr , _)

@@ -26,6 +26,9 @@ def main():
                      "where start >= ? group by name order by 3 desc", (t0,)).fetchall()
     tot_ms = sum(r[2] for r in rows)
     n = sum(r[1] for r in rows)
+    if not a.steps and a.split_steps:  # steps in the window = marker kernels in it
+        a.steps = c.execute("select count(*) from kernels where start >= ? and name like ?",
+                            (t0, f"%{a.split_steps}%")).fetchone()[0]
     busy = c.execute("select min(start), max(end) from kernels where start >= ?", (t0,)).fetchone()
     span = (busy[1] - busy[0]) / 1e6
     print(f"kernel time {tot_ms:.2f} ms over {n} dispatches in a {span:.2f} ms span"
