@@ -603,8 +603,13 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(
             out[(size_t)b * out_stride + (size_t)hq * D + d] = f32_to_act<F16>(ls > 0.f ? os / ls : 0.f);
         } else {
             const size_t pi = ((size_t)b * Hq + hq) * n_parts + part;
-            if (d == 0) part_ml[pi] = make_float2(mx, ls);
-            part_o[pi * D + d] = os;
+            // sc1 stores (agent-scope relaxed atomics): the fused merge below reads them from another CU / XCD with
+            // sc1 loads, so no L2 write-back fence is needed (MI355X_MICROARCH.md inter-workgroup hand-off, row 1)
+            if (d == 0)
+                __hip_atomic_store((unsigned long long*)(part_ml + pi),
+                                   __builtin_bit_cast(unsigned long long, make_float2(mx, ls)), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(part_o + pi * D + d, os, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
     DEC_TS(7)
@@ -613,29 +618,35 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(
     // fused split-K merge: the last of the (b, kvh) partition workgroups to finish merges all of them,
     // instead of a separate reduce launch (at batch 1 that launch costs as much as the attention itself).
     // The counter is left at zero for the next launch / graph replay.
+    // hand-off without fences: every storing wave waits for its sc1 stores, a barrier, then ONE agent-scope atomic add
+    // per workgroup; the workgroup whose add came last reads the partials with sc1 loads (no buffer_wbl2 / buffer_inv:
+    // an agent fence costs ~3.5 us per workgroup here and made this merge lose to a separate launch in round 5)
     __shared__ int s_last;
     const int np = min(n_parts, (L + part_size - 1) / part_size);  // partitions that did not return early
-    __threadfence();  // release: this workgroup's partials reach device scope (every XCD's L2)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
-        const int old = atomicAdd(&part_cnt[b * Hkv + kvh], 1);
+        const int old = __hip_atomic_fetch_add(&part_cnt[b * Hkv + kvh], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         s_last = old == np - 1;
-        if (old == np - 1) atomicExch(&part_cnt[b * Hkv + kvh], 0);
+        if (old == np - 1) __hip_atomic_store(&part_cnt[b * Hkv + kvh], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();
     if (!s_last) return;
-    __threadfence();  // acquire: the other workgroups' partials
+    auto ml_at = [&](size_t i) {
+        return __builtin_bit_cast(float2, __hip_atomic_load((unsigned long long*)(part_ml + i), __ATOMIC_RELAXED,
+                                                            __HIP_MEMORY_SCOPE_AGENT));
+    };
     for (int idx = threadIdx.x; idx < G * D; idx += 64 * NW) {
         const int h = idx / D, d = idx % D, hq = kvh * G + h;
         const size_t pb = ((size_t)b * Hq + hq) * n_parts;
         float mx = -INFINITY;
-        for (int p = 0; p < np; ++p) mx = fmaxf(mx, part_ml[pb + p].x);
+        for (int p = 0; p < np; ++p) mx = fmaxf(mx, ml_at(pb + p).x);
         float ls = 0.f, os = 0.f;
         for (int p = 0; p < np; ++p) {
-            const float2 pm = part_ml[pb + p];
+            const float2 pm = ml_at(pb + p);
             const float a = mx == -INFINITY ? 0.f : exp2f(pm.x - mx);
             ls += pm.y * a;
-            os += part_o[(pb + p) * D + d] * a;
+            os += __hip_atomic_load(part_o + (pb + p) * D + d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) * a;
         }
         out[(size_t)b * out_stride + (size_t)hq * D + d] = f32_to_act<F16>(ls > 0.f ? os / ls : 0.f);
     }
