@@ -17,15 +17,19 @@
 //                  atomics on the residual stream).
 #include "mx_common.h"
 
-// one wave routes one token: softmax over the row's E logits, k rounds of arg-max, optional renormalisation
-template <int VPL>
+// one wave routes one token: softmax over the row's E logits, k rounds of arg-max, optional renormalisation.
+// SC1: the row was written by other workgroups in this launch — read it with agent-scope (sc1) loads
+template <int VPL, bool SC1 = false>
 MX_DEV void route_row(const float* row, int E, int k, int renorm, int* ids, float* wts, int lane) {
     float v[VPL];
     float mx = -INFINITY;
 #pragma unroll
     for (int i = 0; i < VPL; ++i) {
         const int e = lane + 64 * i;
-        v[i] = e < E ? row[e] : -INFINITY;
+        if constexpr (SC1)
+            v[i] = e < E ? __hip_atomic_load((float*)row + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : -INFINITY;
+        else
+            v[i] = e < E ? row[e] : -INFINITY;
         mx = fmaxf(mx, v[i]);
     }
     mx = wave_max(mx);
@@ -187,24 +191,30 @@ __global__ __launch_bounds__(256) void moe_router_kernel(bf16_t* __restrict__ x,
     for (int t = 0; t < TT; ++t) {
         if (t < nt) {
             const float s = wave_sum(acc[t]);
-            if (lane == 0 && e < E) logits[(size_t)(t0 + t) * E + e] = s;
+            if (lane == 0 && e < E) {
+                if (tickets)  // read by another workgroup of this launch: an sc1 store
+                    __hip_atomic_store(logits + (size_t)(t0 + t) * E + e, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                else
+                    logits[(size_t)(t0 + t) * E + e] = s;
+            }
         }
     }
     if (!tickets) return;
+    // fence-free hand-off (MI355X_MICROARCH.md inter-workgroup visibility, row 1): every wave's sc1 stores complete,
+    // a barrier, ONE agent-scope atomic add per workgroup; the workgroup whose add came last routes with sc1 loads
     __shared__ int s_last;
-    __threadfence();  // release: this workgroup's logits at device scope before its ticket
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
-        const int old = atomicAdd(&tickets[blockIdx.x], 1);
+        const int old = __hip_atomic_fetch_add(&tickets[blockIdx.x], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         s_last = old == (int)gridDim.y - 1;
-        if (s_last) atomicExch(&tickets[blockIdx.x], 0);
+        if (s_last) __hip_atomic_store(&tickets[blockIdx.x], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();
     if (!s_last) return;
-    __threadfence();  // acquire: every expert block's logits of these tokens
     for (int t = wave; t < nt; t += 4)
-        route_row<VPL>(logits + (size_t)(t0 + t) * E, E, k, renorm, ids + (size_t)(t0 + t) * k,
-                       wts + (size_t)(t0 + t) * k, lane);
+        route_row<VPL, true>(logits + (size_t)(t0 + t) * E, E, k, renorm, ids + (size_t)(t0 + t) * k,
+                             wts + (size_t)(t0 + t) * k, lane);
 }
 
 // x 16-bit [T, H] (the normed hidden state), wr fp32 [E, H] -> logits fp32 [T, E] (workspace) -> ids / wts [T, k];

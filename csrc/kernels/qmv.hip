@@ -603,13 +603,14 @@ __global__ __launch_bounds__(64 * QMV_WAVES) void qmv1_kernel(const uint8_t* __r
     }
     const int n = g * 32 + r;
     if (EPI != E16_ADD_F32 && gridDim.y > 1) {
+        // hand-off without agent fences (each is an L2 write-back / invalidate, ~3.5 us): the partials are agent-scope
+        // atomics, completed (vmcnt) before the ticket; the last workgroup reads them with agent-scope (sc1) loads
         if (h == 0) atomicAdd(skw + n, v);
-        __threadfence();  // release: this workgroup's partials before its ticket
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         unsigned last = 0;
-        if (lane == 0) last = atomicAdd(skc + g, 1u) == gridDim.y - 1;
+        if (lane == 0) last = __hip_atomic_fetch_add(skc + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.y - 1;
         last = __shfl(last, 0);
         if (!last) return;
-        __threadfence();  // acquire: every workgroup's partials
         if (h == 0) {
             v = __hip_atomic_load(skw + n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             atomicExch(skw + n, 0.f);

@@ -207,6 +207,32 @@ def test_moe_router_fused_norm_gpu(T):
 
 
 @pytest.mark.gpu
+def test_moe_router_route_fused_gpu(monkeypatch):
+    """MX_MOE_ROUTE_FUSE: the top-k routing inside the router launch (last workgroup of each token block, fence-free
+    hand-off of the logits) selects the same experts and weights as the separate routing launch."""
+    from localai_tfp_amd.ops.linear import ACT_DTYPE
+    E, k, H = 128, 8, 512
+    router = (torch.randn(E, H) * 0.5).cuda()
+    for T in (1, 9, 64, 300):
+        x = torch.randn(T, H).to(ACT_DTYPE).cuda()
+        res = []
+        for fuse in (False, True):
+            monkeypatch.setattr(MO, "ROUTE_FUSE", fuse)
+            ids = torch.empty(T, k, dtype=torch.int32, device="cuda")
+            wts = torch.empty(T, k, dtype=torch.float32, device="cuda")
+            logits = torch.empty(T, E, dtype=torch.float32, device="cuda")
+            tk = MO._router_tickets(x.device, (T + 7) // 8) if fuse else None
+            from localai_tfp_amd import _native as N
+            N.ensure_act(x.dtype)
+            N.kcall("mxk_moe_router", x.data_ptr(), x.stride(0), router.data_ptr(), T, H, E, k, 1, ids.data_ptr(),
+                    wts.data_ptr(), logits.data_ptr(), N.ptr(tk), None, 0, None, 0.0, N.stream_ptr())
+            torch.cuda.synchronize()
+            res.append((ids.cpu(), wts.cpu()))
+        assert torch.equal(res[0][0], res[1][0]), T
+        assert torch.allclose(res[0][1], res[1][1], atol=1e-6), T
+
+
+@pytest.mark.gpu
 def test_moe_model_gpu_matches_cpu_and_engine():
     from localai_tfp_amd.engine.engine import EngineConfig, LLMEngine
     from localai_tfp_amd.ops.sampling import SamplingParams
