@@ -27,7 +27,7 @@ struct Q2Geom {
     static constexpr int A_BYTES = BM * 128;          // one 64-k tile of A
     static constexpr int STAGE = A_BYTES + NG * F::QB; // A + the column groups' quant bytes
     static constexpr int HSZ = NG * F::HB;            // one super-block header slot (NG groups)
-    static constexpr int NH = NS == 8 ? 3 : 2;         // header slots: super-blocks live at once
+    static constexpr int NH = NS >= 6 ? 3 : 2;         // header slots: super-blocks live at once (stages kt .. kt+NS-1)
     static constexpr int LDS = NS * STAGE + NH * HSZ;
     // A LDS-DMA instructions per wave per stage (rounded up: with BM / 8 not a multiple of NT the last wave's spare
     // instructions re-load the tile's last 8-row block into its own slot, identical bytes)
@@ -99,7 +99,7 @@ __global__ __launch_bounds__(NG == 8 ? 512 / GPW : 256 * KS) void qmm2_kernel(co
     using G = Q2Geom<QT, WM, KS, WN, NS, NG, GPW>;
     using F = Q2F<QT>;
     constexpr int BM = G::BM, WA = G::WA, STAGE = G::STAGE, A_BYTES = G::A_BYTES;
-    static_assert(NS == 4 || NS == 8, "ring depth");
+    static_assert(NS >= 4 && NS <= 8, "ring depth");
     static_assert(WN == 1 || WN == 2, "WN");
     static_assert(KS == 1 || 4 * WM * WN * 16 * 64 * 4 <= G::LDS, "KS = 2 partials fit in the ring");
     static_assert(WA >= 1 && WA * 8 * G::NT >= BM && (WA - 1) * 8 * G::NT < BM, "A tile split");
@@ -113,7 +113,7 @@ __global__ __launch_bounds__(NG == 8 ? 512 / GPW : 256 * KS) void qmm2_kernel(co
     extern __shared__ __attribute__((aligned(16))) char smem[];
     char* const hdr_lds = smem + NS * STAGE;
     // ring slot of k-tile ki = ki % NS; header slot of super-block v = v % NH
-    auto hslot_of = [](int v) { return NS == 8 ? v % 3 : v & 1; };
+    auto hslot_of = [](int v) { return G::NH == 3 ? v % 3 : v & 1; };
 
     // wave index as a scalar: every LDS-DMA destination (M0) and weight pointer below is then SGPR math
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -234,12 +234,10 @@ __global__ __launch_bounds__(NG == 8 ? 512 / GPW : 256 * KS) void qmm2_kernel(co
         issue_stage(0, I0{});
         issue_stage(1, I1{});
         issue_stage(2, I2{});
-        if constexpr (NS == 8) {
-            issue_stage(3, I3{});
-            issue_stage(4, I0{});
-            issue_stage(5, I1{});
-            issue_stage(6, I2{});
-        }
+        if constexpr (NS >= 5) issue_stage(3, I3{});
+        if constexpr (NS >= 6) issue_stage(4, I0{});
+        if constexpr (NS >= 7) issue_stage(5, I1{});
+        if constexpr (NS >= 8) issue_stage(6, I2{});
         q2_wait_barrier<q2_cnt_run<WAI, QII, HII, WL, 1, NS - 2>()>();
 
         // fragment producers (S is a compile-time constant after unrolling)
@@ -508,6 +506,14 @@ static int dispatch_qmm2(int wm, int ks, int wn, const uint16_t* A, int lda, con
     // 224-row tiles: M in (384, 448] (a decode batch + a prompt chunk a little over 256 tokens) in two row tiles
     Q2_CASE(7, 1, 1)
     Q2_DEEP(2, 1, 1) Q2_DEEP(2, 2, 1) Q2_DEEP(1, 2, 2)
+    // ks | 32: a 6-slot ring for the 128-row decode tiles (5 stages in flight instead of 3: the LDS-DMA issue ->
+    // landed latency, not the MFMA rate, bounds a one-workgroup-per-CU M = 128 GEMM at ~30 GB/s per CU with 4 slots)
+#define Q2_R6(WM_, KS_, WN_)                                                                     \
+    if constexpr (Q2Geom<QT, WM_, KS_, WN_, 6>::LDS <= 160 * 1024)                               \
+        if (wm == WM_ && ks == (KS_ | 32) && wn == WN_)                                          \
+            return launch_qmm2<QT, WM_, KS_, WN_, EPI, 6>(A, lda, W, M, N, K, splits, C, ldc, st);
+    Q2_R6(4, 1, 1) Q2_R6(4, 2, 1) Q2_R6(2, 2, 2) Q2_R6(2, 1, 2)
+#undef Q2_R6
     // ks | 16: wide tiles (8 column groups, 256 columns per workgroup, 8 waves)
 #define Q2_WIDE(WM_, WN_)                                                                      \
     if constexpr (Q2Geom<QT, WM_, 1, WN_, 4, 8>::LDS <= 160 * 1024)                           \

@@ -510,7 +510,11 @@ QMM2_CONFIGS = ((2, 1, 1), (2, 2, 1), (4, 1, 1), (4, 2, 1), (8, 1, 1), (1, 2, 2)
                 # ks | 8: the 8-slot LDS ring (64-row tiles)
                 (2, 9, 1), (2, 10, 1), (1, 10, 2),
                 # ks 17: wide tiles, 8 column groups (256 columns) per 8-wave workgroup — half the A staging per flop
-                (2, 17, 1), (4, 17, 1), (6, 17, 1), (3, 17, 2), (7, 17, 1))
+                (2, 17, 1), (4, 17, 1), (6, 17, 1), (3, 17, 2), (7, 17, 1),
+                # ks | 32: 6-slot LDS-DMA ring for the 128-row tiles, offered to the tuner with MX_QMM2_R6=1: five stages
+                # in flight instead of three changed nothing at M = 128-256 (gate_up M=128 42.1 vs 41.9 us,
+                # profiles/r6_qmm2_ring6.md) — the DMA latency is not what bounds the decode tiles
+                *(((4, 33, 1), (4, 34, 1), (2, 34, 2), (2, 33, 2)) if os.environ.get("MX_QMM2_R6", "0") == "1" else ()))
 # ks 18: 4-wave wide tiles, each wave 64 columns x 32 wm rows (one wave per SIMD); compiled and tested
 # (test_qmm2[*-18-*]), offered to the tuner with MX_QMM2_WIDE4=1
 if os.environ.get("MX_QMM2_WIDE4", "0") == "1":

@@ -413,7 +413,9 @@ def test_qgemm32(qt, M, wm, wn, splits, monkeypatch):
     (128, 4, 17, 1, 1), (300, 4, 17, 1, 3), (384, 6, 17, 1, 1), (250, 6, 17, 1, 2), (400, 3, 17, 2, 1),
     (64, 2, 17, 1, 2), (100, 2, 17, 1, 1), (448, 7, 17, 1, 1), (300, 7, 17, 1, 2),
     # ks 18: 4-wave wide tiles (2 column groups per wave)
-    (384, 6, 18, 2, 1), (250, 6, 18, 2, 2), (128, 4, 18, 2, 1), (77, 2, 18, 2, 3)])
+    (384, 6, 18, 2, 1), (250, 6, 18, 2, 2), (128, 4, 18, 2, 1), (77, 2, 18, 2, 3),
+    # ks | 32: 6-slot ring (128-row tiles)
+    (128, 4, 34, 1, 1), (77, 4, 34, 1, 3), (128, 4, 33, 1, 2), (300, 4, 33, 1, 1), (128, 2, 34, 2, 1), (200, 2, 33, 2, 2)])
 def test_qmm2(qt, M, wm, ks, wn, splits, monkeypatch):
     """qmm2.hip for every epilogue and tile / split-K choice, incl. ragged M / N tails (416 columns = 3.25
     workgroup tiles; with wn = 2 a wave's second group may lie past N), split counts that do not divide the
