@@ -90,6 +90,17 @@ def _build_lib(name: str, srcs, headers, compiler, cflags, ldflags, verbose=Fals
     key = _hash(list(srcs) + list(headers)) + "|" + " ".join(portable) + "|" + ARCH + "|" + repr(sorted(FILE_FLAGS.items()))
     if out.exists() and stamp.exists() and stamp.read_text() == key:
         return out
+    # several ranks of one job (torchrun, 8 per node) may find the library stale at once: one builds under an
+    # exclusive file lock, the others wait and then see its stamp
+    import fcntl
+    with open(LIB / (name + ".lock"), "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        if out.exists() and stamp.exists() and stamp.read_text() == key:
+            return out
+        return _build_locked(name, out, stamp, key, srcs, headers, compiler, cflags, ldflags, verbose)
+
+
+def _build_locked(name, out, stamp, key, srcs, headers, compiler, cflags, ldflags, verbose) -> Path:
     objs = []
 
     def compile_one(src: Path):
