@@ -59,7 +59,7 @@ def parse():
                     help="engine iterations per bench step (G): K steps time K*G continuous-batching iterations")
     ap.add_argument("--min-ttft-samples", type=int, default=32,
                     help="rank 0 exits non-zero if fewer TTFT samples fall in the window (0: no check)")
-    ap.add_argument("--model", default="llama3-8b", choices=["llama3-8b", "llama3-70b", "llama32-1b", "qwen3-30b-a3b"],
+    ap.add_argument("--model", default="llama3-8b", choices=["llama3-8b", "llama3-70b", "llama32-1b", "qwen3-30b-a3b", "qwen3-8b"],
                     help="qwen3-30b-a3b: the gallery's first entry (128 experts, 8 active) on the MoE path")
     ap.add_argument("--path", default="http", choices=["http", "engine"])
     ap.add_argument("--ftype", default="Q4_K_M", choices=["Q4_K_M", "Q3_K_M"],
@@ -234,7 +234,7 @@ def main():
     from localai_tfp_amd.tokenizer import ByteTokenizer
 
     cfg = {"llama3-8b": C.LLAMA3_8B, "llama3-70b": C.LLAMA3_70B, "llama32-1b": C.LLAMA32_1B,
-           "qwen3-30b-a3b": C.QWEN3_30B_A3B}[args.model]
+           "qwen3-30b-a3b": C.QWEN3_30B_A3B, "qwen3-8b": C.QWEN3_8B}[args.model]
     if dev.type == "cpu":  # plumbing only (row-parallel shards need whole 256-wide super-blocks)
         if args.tp > 2:  # 8-way row-parallel shards (config #3's layout: 1 KV head per rank at tp 8)
             cfg = C.tiny_config(hidden=2048, ffn=4096, n_heads=16, n_kv_heads=8, head_dim=128, rope_dim=128)

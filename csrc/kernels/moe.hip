@@ -255,7 +255,7 @@ extern "C" int mxk_moe_router(void* x, int ldx, const float* wr, int T, int H, i
         const int err = (int)hipGetLastError();
         if (err) return err;
     }
-    if (tickets) return 0;  // routed by the last workgroup of each token block
+    if (tickets || !ids) return 0;  // routed by the last workgroup of each token block / logits only (route_sort)
     return mxk_moe_route(logits, E, T, E, k, renorm, ids, wts, st);
 }
 
@@ -309,6 +309,69 @@ extern "C" int mxk_moe_sort(const int* ids, int P, int k, int E, int BM, int* of
                             int* inv_pos, hipStream_t st) {
     if (E <= 0 || E > 4096 || BM <= 0) return (int)hipErrorInvalidValue;
     moe_sort_kernel<<<1, 1024, 2 * E * sizeof(int), st>>>(ids, P, k, E, BM, off, tile_start, sorted_tok, inv_pos);
+    MXK_CHECK_LAUNCH();
+}
+
+// Decode-sized batches (T <= 64): routing and the counting sort in ONE workgroup — each of the 16 waves routes tokens
+// wave, wave + 16, .. (route_row), the pairs' experts stay in LDS, then the same histogram / scan / scatter as
+// moe_sort_kernel. One launch instead of two per MoE layer.
+template <int VPL>
+__global__ __launch_bounds__(1024) void moe_route_sort_kernel(const float* __restrict__ logits, int ldl, int T, int E,
+                                                              int k, int renorm, int* __restrict__ ids,
+                                                              float* __restrict__ wts, int BM, int* __restrict__ off,
+                                                              int* __restrict__ tile_start,
+                                                              int* __restrict__ sorted_tok, int* __restrict__ inv_pos) {
+    extern __shared__ int rs_sm[];
+    int* cnt = rs_sm;            // [E]
+    int* cur = rs_sm + E;        // [E]
+    int* sid = rs_sm + 2 * E;    // [T k] routed experts
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (int e = threadIdx.x; e < E; e += 1024) cnt[e] = 0;
+    for (int t = wave; t < T; t += 16) {
+        route_row<VPL>(logits + (size_t)t * ldl, E, k, renorm, ids + (size_t)t * k, wts + (size_t)t * k, lane);
+    }
+    __syncthreads();
+    // the routed ids as this workgroup wrote them (same workgroup: visible after the barrier; first touch of the lines)
+    const int P = T * k;
+    for (int p = threadIdx.x; p < P; p += 1024) {
+        const int e = min(max(__hip_atomic_load(ids + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP), 0), E - 1);
+        sid[p] = e;
+        atomicAdd(&cnt[e], 1);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int o = 0, ts = 0;
+        for (int e = 0; e < E; ++e) {
+            const int c = cnt[e];
+            off[e] = o;
+            tile_start[e] = ts;
+            cur[e] = o;
+            o += c;
+            ts += (c + BM - 1) / BM;
+        }
+        off[E] = o;
+        tile_start[E] = ts;
+    }
+    __syncthreads();
+    for (int p = threadIdx.x; p < P; p += 1024) {
+        const int pos = atomicAdd(&cur[sid[p]], 1);
+        sorted_tok[pos] = p / k;
+        inv_pos[p] = pos;
+    }
+}
+
+extern "C" int mxk_moe_route_sort(const float* logits, int ldl, int T, int E, int k, int renorm, int* ids, float* wts,
+                                  int BM, int* off, int* tile_start, int* sorted_tok, int* inv_pos, hipStream_t st) {
+    if (T <= 0) return 0;
+    if (k < 1 || k > 64 || k > E || E > 512 || BM <= 0 || T * k > 8192) return (int)hipErrorInvalidValue;
+    const size_t lds = (size_t)(2 * E + T * k) * sizeof(int);
+#define MRS(V) moe_route_sort_kernel<V><<<1, 1024, lds, st>>>(logits, ldl, T, E, k, renorm, ids, wts, BM, off, tile_start, \
+                                                             sorted_tok, inv_pos)
+    if (E <= 64) MRS(1);
+    else if (E <= 128) MRS(2);
+    else if (E <= 256) MRS(4);
+    else MRS(8);
+#undef MRS
     MXK_CHECK_LAUNCH();
 }
 

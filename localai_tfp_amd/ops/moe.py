@@ -100,6 +100,10 @@ ROUTE_FUSE = __import__("os").environ.get("MX_MOE_ROUTE_FUSE", "0") == "1"
 # above, every expert-block workgroup would redo its tokens' norm (c64 7,531 vs 7,668 unfused)
 NORM_FUSE = __import__("os").environ.get("MX_MOE_NORM_FUSE", "1") != "0"
 NORM_FUSE_MAX_T = 8
+# routing inside the single-workgroup counting sort for grouped batches of at most this many tokens: opt-in
+# (MX_MOE_ROUTE_SORT=1) — one workgroup routing 64 tokens is a serial tail, c64 7,032 vs 7,552 tok/s with two launches
+ROUTE_SORT = __import__("os").environ.get("MX_MOE_ROUTE_SORT", "0") == "1"
+ROUTE_SORT_MAX_T = 64
 
 
 def _router_tickets(dev, n: int) -> torch.Tensor:
@@ -135,6 +139,9 @@ def moe_ffn(W: MoEWeights, x: torch.Tensor, h: torch.Tensor, norm: tuple | None 
     st = N.stream_ptr()
     fast = (x.dtype in (torch.float16, torch.bfloat16) and H % 256 == 0 and x.stride(1) == 1 and x.stride(0) % 8 == 0
             and W.router.is_contiguous() and E <= 512)
+    El = W.n_local or E
+    # decode-sized grouped batches: the routing runs inside the sort's single workgroup (moe_route_sort)
+    route_in_sort = (fast and W.t32 and El == E and ROUTE_SORT and GEMV_MAX_PAIRS < T * k and T <= ROUTE_SORT_MAX_T)
     fuse_norm = (fast and NORM_FUSE and T <= NORM_FUSE_MAX_T and norm is not None and norm[0].dtype == torch.float32 and norm[0].stride(1) == 1
                  and norm[0].stride(0) % 4 == 0 and norm[1].dtype == torch.float32 and norm[1].is_contiguous())
     if norm is not None and not fuse_norm:
@@ -142,18 +149,17 @@ def moe_ffn(W: MoEWeights, x: torch.Tensor, h: torch.Tensor, norm: tuple | None 
     if fast:
         N.ensure_act(x.dtype)
         logits = torch.empty(T, E, dtype=torch.float32, device=x.device)
-        tk = _router_tickets(x.device, (T + 7) // 8) if ROUTE_FUSE else None
+        tk = _router_tickets(x.device, (T + 7) // 8) if (ROUTE_FUSE and not route_in_sort) else None
         hs, g, eps = norm if fuse_norm else (None, None, 0.0)
         N.kcall("mxk_moe_router", x.data_ptr(), x.stride(0), W.router.data_ptr(), T, H, E, k, int(W.renorm),
-                ids.data_ptr(), wts.data_ptr(), logits.data_ptr(), N.ptr(tk), N.ptr(hs), hs.stride(0) if fuse_norm else 0,
-                N.ptr(g), float(eps), st)
+                None if route_in_sort else ids.data_ptr(), wts.data_ptr(), logits.data_ptr(), N.ptr(tk), N.ptr(hs),
+                hs.stride(0) if fuse_norm else 0, N.ptr(g), float(eps), st)
     else:
         logits = x.float() @ W.router.t()
         N.kcall("mxk_moe_route", logits.data_ptr(), logits.stride(0), T, E, k, int(W.renorm), ids.data_ptr(),
                 wts.data_ptr(), st)
-    El = W.n_local or E
     if W.t32:
-        _experts_t32(W, x, h, ids, wts, El)
+        _experts_t32(W, x, h, ids, wts, El, logits if route_in_sort else None)
         if W.sh_down is not None:
             _shared(W, x, h)
         return h
@@ -193,8 +199,10 @@ def moe_ffn(W: MoEWeights, x: torch.Tensor, h: torch.Tensor, norm: tuple | None 
     return h
 
 
-def _experts_t32(W: MoEWeights, x: torch.Tensor, h: torch.Tensor, ids: torch.Tensor, wts: torch.Tensor, El: int):
-    """Routed experts on the t32 stacks: grouped decode GEMV (small P) or grouped qmm2 (sorted pairs)."""
+def _experts_t32(W: MoEWeights, x: torch.Tensor, h: torch.Tensor, ids: torch.Tensor, wts: torch.Tensor, El: int,
+                 logits: torch.Tensor | None = None):
+    """Routed experts on the t32 stacks: grouped decode GEMV (small P) or grouped qmm2 (sorted pairs). logits: the
+    routing is still to do and runs inside the sort launch (moe_route_sort)."""
     T, k, F, E = x.shape[0], W.n_used, W.ffn, W.n_expert
     H = h.shape[1]
     P = T * k
@@ -228,8 +236,12 @@ def _experts_t32(W: MoEWeights, x: torch.Tensor, h: torch.Tensor, ids: torch.Ten
     tiles = torch.empty(Eb + 1, dtype=torch.int32, device=x.device)
     stok = torch.empty(P, dtype=torch.int32, device=x.device)
     inv = torch.empty(P, dtype=torch.int32, device=x.device)
-    N.kcall("mxk_moe_sort", ids.data_ptr(), P, k, Eb, 32 * wm, off.data_ptr(), tiles.data_ptr(), stok.data_ptr(),
-            inv.data_ptr(), st)
+    if logits is not None:
+        N.kcall("mxk_moe_route_sort", logits.data_ptr(), logits.stride(0), T, E, k, int(W.renorm), ids.data_ptr(),
+                wts.data_ptr(), 32 * wm, off.data_ptr(), tiles.data_ptr(), stok.data_ptr(), inv.data_ptr(), st)
+    else:
+        N.kcall("mxk_moe_sort", ids.data_ptr(), P, k, Eb, 32 * wm, off.data_ptr(), tiles.data_ptr(), stok.data_ptr(),
+                inv.data_ptr(), st)
     N.kcall("mxk_qmm2_grouped", int(gu.qtype), E16_SWIGLU, wm, x.data_ptr(), x.stride(0), stok.data_ptr(),
             gu.data.data_ptr(), P, El, 2 * F, gu.K, tiles.data_ptr(), off.data_ptr(), act.data_ptr(), act.stride(0), st)
     N.kcall("mxk_qmm2_grouped", int(d.qtype), E16_F32, wm, act.data_ptr(), act.stride(0), None, d.data.data_ptr(), P,
