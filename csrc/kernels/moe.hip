@@ -276,7 +276,8 @@ extern "C" int mxk_moe_route(const float* logits, int ldl, int T, int E, int k, 
 
 __global__ __launch_bounds__(1024) void moe_sort_kernel(const int* __restrict__ ids, int P, int k, int E, int BM,
                                                         int* __restrict__ off, int* __restrict__ tile_start,
-                                                        int* __restrict__ sorted_tok, int* __restrict__ inv_pos) {
+                                                        int* __restrict__ sorted_tok, int* __restrict__ inv_pos,
+                                                        const float* __restrict__ wts, float* __restrict__ sorted_wt) {
     extern __shared__ int sm[];
     int* cnt = sm;         // [E]
     int* cur = sm + E;     // [E]
@@ -302,13 +303,15 @@ __global__ __launch_bounds__(1024) void moe_sort_kernel(const int* __restrict__ 
         const int pos = atomicAdd(&cur[min(max(ids[p], 0), E - 1)], 1);
         sorted_tok[pos] = p / k;
         inv_pos[p] = pos;
+        if (sorted_wt) sorted_wt[pos] = wts[p];
     }
 }
 
 extern "C" int mxk_moe_sort(const int* ids, int P, int k, int E, int BM, int* off, int* tile_start, int* sorted_tok,
-                            int* inv_pos, hipStream_t st) {
-    if (E <= 0 || E > 4096 || BM <= 0) return (int)hipErrorInvalidValue;
-    moe_sort_kernel<<<1, 1024, 2 * E * sizeof(int), st>>>(ids, P, k, E, BM, off, tile_start, sorted_tok, inv_pos);
+                            int* inv_pos, const float* wts, float* sorted_wt, hipStream_t st) {
+    if (E <= 0 || E > 4096 || BM <= 0 || (sorted_wt && !wts)) return (int)hipErrorInvalidValue;
+    moe_sort_kernel<<<1, 1024, 2 * E * sizeof(int), st>>>(ids, P, k, E, BM, off, tile_start, sorted_tok, inv_pos, wts,
+                                                          sorted_wt);
     MXK_CHECK_LAUNCH();
 }
 
@@ -320,7 +323,8 @@ __global__ __launch_bounds__(1024) void moe_route_sort_kernel(const float* __res
                                                               int k, int renorm, int* __restrict__ ids,
                                                               float* __restrict__ wts, int BM, int* __restrict__ off,
                                                               int* __restrict__ tile_start,
-                                                              int* __restrict__ sorted_tok, int* __restrict__ inv_pos) {
+                                                              int* __restrict__ sorted_tok, int* __restrict__ inv_pos,
+                                                              float* __restrict__ sorted_wt) {
     extern __shared__ int rs_sm[];
     int* cnt = rs_sm;            // [E]
     int* cur = rs_sm + E;        // [E]
@@ -357,16 +361,18 @@ __global__ __launch_bounds__(1024) void moe_route_sort_kernel(const float* __res
         const int pos = atomicAdd(&cur[sid[p]], 1);
         sorted_tok[pos] = p / k;
         inv_pos[p] = pos;
+        if (sorted_wt) sorted_wt[pos] = __hip_atomic_load(wts + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
 }
 
 extern "C" int mxk_moe_route_sort(const float* logits, int ldl, int T, int E, int k, int renorm, int* ids, float* wts,
-                                  int BM, int* off, int* tile_start, int* sorted_tok, int* inv_pos, hipStream_t st) {
+                                  int BM, int* off, int* tile_start, int* sorted_tok, int* inv_pos, float* sorted_wt,
+                                  hipStream_t st) {
     if (T <= 0) return 0;
     if (k < 1 || k > 64 || k > E || E > 512 || BM <= 0 || T * k > 8192) return (int)hipErrorInvalidValue;
     const size_t lds = (size_t)(2 * E + T * k) * sizeof(int);
 #define MRS(V) moe_route_sort_kernel<V><<<1, 1024, lds, st>>>(logits, ldl, T, E, k, renorm, ids, wts, BM, off, tile_start, \
-                                                             sorted_tok, inv_pos)
+                                                             sorted_tok, inv_pos, sorted_wt)
     if (E <= 64) MRS(1);
     else if (E <= 128) MRS(2);
     else if (E <= 256) MRS(4);

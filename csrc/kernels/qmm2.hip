@@ -69,15 +69,15 @@ extern "C" int mxk_qmm2(int qtype, int epi, int wm, int ks, int wn, const uint16
 // mxk_moe_sort with BM = 32 wm; C row r = sorted pair r. epi: 0 fp32 store [P, N], 3 / 4 SwiGLU / GeGLU f16 [P, N/2].
 extern "C" int mxk_qmm2_grouped(int qtype, int epi, int wm, const uint16_t* A, int lda, const int* stok, const uint8_t* W,
                                 int P, int E, int N, int K, const int* tiles, const int* off, void* C, int ldc,
-                                hipStream_t st) {
+                                const int* otok, const float* owt, hipStream_t st) {
     if (P <= 0) return 0;
     if (K % 256 || (lda & 7) || ((uintptr_t)A & 15) || ((uintptr_t)W & 15) || (N & 31) || E <= 0)
         return (int)hipErrorInvalidValue;
     switch (qtype) {
-        case MXQ_Q4_K: return qmm2_grouped_q4k(epi, wm, A, lda, stok, W, P, E, N, K, tiles, off, C, ldc, st);
-        case MXQ_Q5_K: return qmm2_grouped_q5k(epi, wm, A, lda, stok, W, P, E, N, K, tiles, off, C, ldc, st);
-        case MXQ_Q6_K: return qmm2_grouped_q6k(epi, wm, A, lda, stok, W, P, E, N, K, tiles, off, C, ldc, st);
-        case MXQ_Q8_0: return qmm2_grouped_q80(epi, wm, A, lda, stok, W, P, E, N, K, tiles, off, C, ldc, st);
+        case MXQ_Q4_K: return qmm2_grouped_q4k(epi, wm, A, lda, stok, W, P, E, N, K, tiles, off, C, ldc, otok, owt, st);
+        case MXQ_Q5_K: return qmm2_grouped_q5k(epi, wm, A, lda, stok, W, P, E, N, K, tiles, off, C, ldc, otok, owt, st);
+        case MXQ_Q6_K: return qmm2_grouped_q6k(epi, wm, A, lda, stok, W, P, E, N, K, tiles, off, C, ldc, otok, owt, st);
+        case MXQ_Q8_0: return qmm2_grouped_q80(epi, wm, A, lda, stok, W, P, E, N, K, tiles, off, C, ldc, otok, owt, st);
     }
     return (int)hipErrorInvalidValue;
 }

@@ -88,6 +88,11 @@ struct Q2Group {
     const int* off;
     const int* stok;
     int E;
+    // E16_ADD_F32 in grouped mode (the down projection with the MoE combine fused): sorted row r adds
+    // owt[r] * its output row into C row otok[r] (the token's residual), fp32 atomics (rows of one token come from
+    // different experts' tiles)
+    const int* otok = nullptr;
+    const float* owt = nullptr;
 };
 
 // DBG (isolation builds, tools/prof_qmm.py --q2dbg): 1 no MFMA, 2 no dequant VALU, 4 no A loads, 8 no weight loads
@@ -377,6 +382,16 @@ __global__ __launch_bounds__(NG == 8 ? 512 / GPW : 256 * KS) void qmm2_kernel(co
         const int nt = (ct * NG + nw * WN + j) * 32;
         const int n = nt + col;
         if (nt >= N) break;
+        if constexpr (GR && EPI == E16_ADD_F32) {
+#pragma unroll
+            for (int i = 0; i < WM; ++i)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int m = mb + i * 32 + 8 * (r >> 2) + 4 * h + (r & 3);
+                    if (m < M) atomicAdd((float*)Cv + (size_t)grp.otok[m] * ldc + n, grp.owt[m] * acc[i][j][r]);
+                }
+            continue;
+        }
         if constexpr (EPI == E16_SWIGLU || EPI == E16_GEGLU) {
             // W rows interleaved in 16-row groups: tile columns 0..15 gate, 16..31 up of the same features
 #pragma unroll
@@ -457,7 +472,9 @@ static int launch_qmm2(const uint16_t* A, int lda, const uint8_t* W, int M, int 
 // grouped (MoE) launch: P sorted rows, E experts of N columns each, tiles / off from moe_sort with BM = 32 WM
 template <int QT, int WM, int KS, int EPI>
 static int launch_qmm2_grouped(const uint16_t* A, int lda, const int* stok, const uint8_t* W, int P, int E, int N, int K,
-                               const int* tiles, const int* off, void* C, int ldc, hipStream_t st) {
+                               const int* tiles, const int* off, void* C, int ldc, const int* otok, const float* owt,
+                               hipStream_t st) {
+    if (EPI == E16_ADD_F32 && (!otok || !owt)) return (int)hipErrorInvalidValue;
     using G = Q2Geom<QT, WM, KS, 1>;
     const int n_ct = (N + 127) / 128, n_mt = (P + G::BM - 1) / G::BM + E;
     const long nwg = (long)n_ct * n_mt;
@@ -469,18 +486,21 @@ static int launch_qmm2_grouped(const uint16_t* A, int lda, const int* stok, cons
         attr_set = true;
     }
     qmm2_kernel<QT, WM, KS, 1, EPI, 0, 4, 4, 1, true><<<dim3((unsigned)nwg), 64 * G::NT, G::LDS, st>>>(
-        A, lda, W, P, N, K, n_mt, 1, K >> 8, C, ldc, 0, Q2Group{tiles, off, stok, E});
+        A, lda, W, P, N, K, n_mt, 1, K >> 8, C, ldc, 0, Q2Group{tiles, off, stok, E, otok, owt});
     MXK_CHECK_LAUNCH();
 }
 
-// wm 1 (32-row tiles) or 2 (64); epi F32 (the down projection into the [P, H] buffer) or SwiGLU / GeGLU (gate|up)
+// wm 1 (32-row tiles) or 2 (64); epi F32 (the down projection into the [P, H] buffer), ADD_F32 (the down projection
+// with the combine fused: weighted atomic adds into the tokens' rows, otok / owt) or SwiGLU / GeGLU (gate|up)
 template <int QT>
 static int qmm2_grouped_run(int epi, int wm, const uint16_t* A, int lda, const int* stok, const uint8_t* W, int P, int E,
-                            int N, int K, const int* tiles, const int* off, void* C, int ldc, hipStream_t st) {
+                            int N, int K, const int* tiles, const int* off, void* C, int ldc, const int* otok,
+                            const float* owt, hipStream_t st) {
 #define Q2G(WM_, EPI_)                                                                                          \
     if (wm == WM_ && epi == EPI_)                                                                               \
-        return launch_qmm2_grouped<QT, WM_, 2, EPI_>(A, lda, stok, W, P, E, N, K, tiles, off, C, ldc, st);
-    Q2G(1, E16_F32) Q2G(2, E16_F32) Q2G(1, E16_SWIGLU) Q2G(2, E16_SWIGLU) Q2G(1, E16_GEGLU) Q2G(2, E16_GEGLU)
+        return launch_qmm2_grouped<QT, WM_, 2, EPI_>(A, lda, stok, W, P, E, N, K, tiles, off, C, ldc, otok, owt, st);
+    Q2G(1, E16_F32) Q2G(2, E16_F32) Q2G(1, E16_ADD_F32) Q2G(2, E16_ADD_F32) Q2G(1, E16_SWIGLU) Q2G(2, E16_SWIGLU)
+    Q2G(1, E16_GEGLU) Q2G(2, E16_GEGLU)
 #undef Q2G
     return (int)hipErrorInvalidValue;
 }
@@ -593,8 +613,8 @@ int qmm2_run_q2k(int epi, int wm, int ks, int wn, const uint16_t* A, int lda, co
 int qmm2_run_q80(int epi, int wm, int ks, int wn, const uint16_t* A, int lda, const uint8_t* W, int M, int N, int K, int splits, void* C, int ldc, hipStream_t st);
 int qmm2_run_mx4(int epi, int wm, int ks, int wn, const uint16_t* A, int lda, const uint8_t* W, int M, int N, int K, int splits, void* C, int ldc, hipStream_t st);
 int qmm2_run_mx5(int epi, int wm, int ks, int wn, const uint16_t* A, int lda, const uint8_t* W, int M, int N, int K, int splits, void* C, int ldc, hipStream_t st);
-int qmm2_grouped_q4k(int epi, int wm, const uint16_t* A, int lda, const int* stok, const uint8_t* W, int P, int E, int N, int K, const int* tiles, const int* off, void* C, int ldc, hipStream_t st);
-int qmm2_grouped_q5k(int epi, int wm, const uint16_t* A, int lda, const int* stok, const uint8_t* W, int P, int E, int N, int K, const int* tiles, const int* off, void* C, int ldc, hipStream_t st);
-int qmm2_grouped_q6k(int epi, int wm, const uint16_t* A, int lda, const int* stok, const uint8_t* W, int P, int E, int N, int K, const int* tiles, const int* off, void* C, int ldc, hipStream_t st);
-int qmm2_grouped_q80(int epi, int wm, const uint16_t* A, int lda, const int* stok, const uint8_t* W, int P, int E, int N, int K, const int* tiles, const int* off, void* C, int ldc, hipStream_t st);
+int qmm2_grouped_q4k(int epi, int wm, const uint16_t* A, int lda, const int* stok, const uint8_t* W, int P, int E, int N, int K, const int* tiles, const int* off, void* C, int ldc, const int* otok, const float* owt, hipStream_t st);
+int qmm2_grouped_q5k(int epi, int wm, const uint16_t* A, int lda, const int* stok, const uint8_t* W, int P, int E, int N, int K, const int* tiles, const int* off, void* C, int ldc, const int* otok, const float* owt, hipStream_t st);
+int qmm2_grouped_q6k(int epi, int wm, const uint16_t* A, int lda, const int* stok, const uint8_t* W, int P, int E, int N, int K, const int* tiles, const int* off, void* C, int ldc, const int* otok, const float* owt, hipStream_t st);
+int qmm2_grouped_q80(int epi, int wm, const uint16_t* A, int lda, const int* stok, const uint8_t* W, int P, int E, int N, int K, const int* tiles, const int* off, void* C, int ldc, const int* otok, const float* owt, hipStream_t st);
 int qmm2_dbg_q4k(int dbg, int wm, int ks, int wn, const uint16_t* A, int lda, const uint8_t* W, int M, int N, int K, void* C, int ldc, hipStream_t st);

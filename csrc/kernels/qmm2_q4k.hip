@@ -22,6 +22,7 @@ int qmm2_dbg_q4k(int dbg, int wm, int ks, int wn, const uint16_t* A, int lda, co
 }
 
 int qmm2_grouped_q4k(int epi, int wm, const uint16_t* A, int lda, const int* stok, const uint8_t* W, int P, int E, int N,
-                     int K, const int* tiles, const int* off, void* C, int ldc, hipStream_t st) {
-    return qmm2_grouped_run<MXQ_Q4_K>(epi, wm, A, lda, stok, W, P, E, N, K, tiles, off, C, ldc, st);
+                     int K, const int* tiles, const int* off, void* C, int ldc, const int* otok, const float* owt,
+                     hipStream_t st) {
+    return qmm2_grouped_run<MXQ_Q4_K>(epi, wm, A, lda, stok, W, P, E, N, K, tiles, off, C, ldc, otok, owt, st);
 }

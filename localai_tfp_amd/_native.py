@@ -103,11 +103,11 @@ KERNEL_SIGS = {
     "mxk_moe_router": [P, I, P, I, I, I, I, I, P, P, P, P, P, I, P, F, P],
     # qtype, epi, W, N, K, ids, P, e0, El, x, ldx, xdiv, C, ldc, stream
     "mxk_qmv_moe": [I, I, P, I, I, P, I, I, I, P, I, I, P, I, P],
-    "mxk_moe_route_sort": [P, I, I, I, I, I, P, P, I, P, P, P, P, P],
+    "mxk_moe_route_sort": [P, I, I, I, I, I, P, P, I, P, P, P, P, P, P],
     "mxk_qmv_moe_down": [I, P, I, I, P, P, I, I, I, I, P, I, P, I, P],
     # qtype, epi, wm, A, lda, stok, W, P, E, N, K, tiles, off, C, ldc, stream
-    "mxk_qmm2_grouped": [I, I, I, P, I, P, P, I, I, I, I, P, P, P, I, P],
-    "mxk_moe_sort": [P, I, I, I, I, P, P, P, P, P],
+    "mxk_qmm2_grouped": [I, I, I, P, I, P, P, I, I, I, I, P, P, P, I, P, P, P],
+    "mxk_moe_sort": [P, I, I, I, I, P, P, P, P, P, P, P],
     "mxk_moe_combine": [P, I, P, P, I, I, I, P, I, I, P],
     "mxk_moe_qgemm16": [I, I, I, P, I, P, P, P, P, P, I, I, I, I, P, I, P],
     # x, Nb, H, W, Cp, w, Cout, KH, KW, Kp, stride, dil, pad_h, pad_w, up, Ho, Wo, bias, tadd, ldt, res, ldr, y,

@@ -30,7 +30,7 @@ from .. import _native as N
 from . import core as K
 from .linear import ACT_DTYPE, EPI_F32, EPI_SWIGLU, QWeight, qmatmul
 
-E16_F32, E16_SWIGLU = 0, 3
+E16_F32, E16_ADD_F32, E16_SWIGLU = 0, 2, 3
 MOE_T32 = (12, 13, 14, 8)  # Q4_K, Q5_K, Q6_K, Q8_0: block formats with grouped t32 kernels (qmv_moe, qmm2 grouped)
 GEMV_MAX_PAIRS = 64  # token-expert pairs up to which the grouped decode GEMV runs (above: the grouped qmm2 GEMM)
 
@@ -104,6 +104,10 @@ NORM_FUSE_MAX_T = 8
 # (MX_MOE_ROUTE_SORT=1) — one workgroup routing 64 tokens is a serial tail, c64 7,032 vs 7,552 tok/s with two launches
 ROUTE_SORT = __import__("os").environ.get("MX_MOE_ROUTE_SORT", "0") == "1"
 ROUTE_SORT_MAX_T = 64
+# grouped (sorted) path: the down projection adds routing-weighted rows straight into the residual (fp32 atomics: the
+# k rows of a token come from different experts' tiles, so the sum order is not fixed) instead of a [P, H] buffer + a
+# combine launch; MX_MOE_GROUPED_COMBINE=0 keeps the deterministic combine
+GROUPED_COMBINE_FUSE = __import__("os").environ.get("MX_MOE_GROUPED_COMBINE", "1") != "0"
 
 
 def _router_tickets(dev, n: int) -> torch.Tensor:
@@ -180,7 +184,7 @@ def moe_ffn(W: MoEWeights, x: torch.Tensor, h: torch.Tensor, norm: tuple | None 
     stok = torch.empty(P, dtype=torch.int32, device=x.device)
     inv = torch.empty(P, dtype=torch.int32, device=x.device)
     N.kcall("mxk_moe_sort", ids.data_ptr(), P, k, Eb, 16 * wm, off.data_ptr(), tiles.data_ptr(), stok.data_ptr(),
-            inv.data_ptr(), st)
+            inv.data_ptr(), None, None, st)
     E = El
     act = torch.empty(P, F, dtype=x.dtype, device=x.device)
     N.ensure_act(x.dtype)
@@ -224,8 +228,6 @@ def _experts_t32(W: MoEWeights, x: torch.Tensor, h: torch.Tensor, ids: torch.Ten
         N.kcall("mxk_moe_combine", y.data_ptr(), y.stride(0), None, wts.data_ptr(), T, k, H, h.data_ptr(),
                 h.stride(0), 1, st)
         return
-    # rows of pairs routed to another rank's experts stay zero (weight 0 in the combine)
-    y = (torch.zeros if El != E else torch.empty)(P, H, dtype=torch.float32, device=x.device)
     if El != E:  # expert parallelism: other ranks' pairs go to a null bucket El, sorted last, never computed
         loc = ids - W.e0
         off_rank = (loc < 0) | (loc >= El)
@@ -236,16 +238,28 @@ def _experts_t32(W: MoEWeights, x: torch.Tensor, h: torch.Tensor, ids: torch.Ten
     tiles = torch.empty(Eb + 1, dtype=torch.int32, device=x.device)
     stok = torch.empty(P, dtype=torch.int32, device=x.device)
     inv = torch.empty(P, dtype=torch.int32, device=x.device)
+    fuse = GROUPED_COMBINE_FUSE and h.stride(1) == 1
+    swt = torch.empty(P, dtype=torch.float32, device=x.device) if fuse else None
     if logits is not None:
         N.kcall("mxk_moe_route_sort", logits.data_ptr(), logits.stride(0), T, E, k, int(W.renorm), ids.data_ptr(),
-                wts.data_ptr(), 32 * wm, off.data_ptr(), tiles.data_ptr(), stok.data_ptr(), inv.data_ptr(), st)
+                wts.data_ptr(), 32 * wm, off.data_ptr(), tiles.data_ptr(), stok.data_ptr(), inv.data_ptr(), N.ptr(swt),
+                st)
     else:
         N.kcall("mxk_moe_sort", ids.data_ptr(), P, k, Eb, 32 * wm, off.data_ptr(), tiles.data_ptr(), stok.data_ptr(),
-                inv.data_ptr(), st)
+                inv.data_ptr(), wts.data_ptr(), N.ptr(swt), st)
     N.kcall("mxk_qmm2_grouped", int(gu.qtype), E16_SWIGLU, wm, x.data_ptr(), x.stride(0), stok.data_ptr(),
-            gu.data.data_ptr(), P, El, 2 * F, gu.K, tiles.data_ptr(), off.data_ptr(), act.data_ptr(), act.stride(0), st)
+            gu.data.data_ptr(), P, El, 2 * F, gu.K, tiles.data_ptr(), off.data_ptr(), act.data_ptr(), act.stride(0),
+            None, None, st)
+    if fuse:
+        # down + combine: each sorted row's output, scaled by its routing weight, added into its token's residual row
+        N.kcall("mxk_qmm2_grouped", int(d.qtype), E16_ADD_F32, wm, act.data_ptr(), act.stride(0), None,
+                d.data.data_ptr(), P, El, H, d.K, tiles.data_ptr(), off.data_ptr(), h.data_ptr(), h.stride(0),
+                stok.data_ptr(), swt.data_ptr(), st)
+        return
+    # rows of pairs routed to another rank's experts stay zero (weight 0 in the combine)
+    y = (torch.zeros if El != E else torch.empty)(P, H, dtype=torch.float32, device=x.device)
     N.kcall("mxk_qmm2_grouped", int(d.qtype), E16_F32, wm, act.data_ptr(), act.stride(0), None, d.data.data_ptr(), P,
-            El, H, d.K, tiles.data_ptr(), off.data_ptr(), y.data_ptr(), y.stride(0), st)
+            El, H, d.K, tiles.data_ptr(), off.data_ptr(), y.data_ptr(), y.stride(0), None, None, st)
     N.kcall("mxk_moe_combine", y.data_ptr(), y.stride(0), inv.data_ptr(), wts.data_ptr(), T, k, H, h.data_ptr(),
             h.stride(0), 1, st)
 
