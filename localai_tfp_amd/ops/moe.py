@@ -6,8 +6,9 @@ softmax, top-k, optional weight renormalisation, ggml_mul_mat_id over the stacke
 
 GPU path (all device-side, hipGraph-capturable):
     moe_router (moe.hip: the router GEMV, one expert per wave with its fp32 row requested whole, 8 tokens per
-    workgroup from LDS; the last workgroup of each token block runs the softmax + top-k, so router and routing are
-    one launch) -> then, with the expert stacks in the t32 layout (models/llama.py finalize_layout;
+    workgroup from LDS; for <= 8 rows it also computes the FFN RMSNorm) -> moe_route (softmax + top-k, one wave per
+    token; in-launch variants are opt-in: profiles/r6_fence_free_handoffs.md) -> then, with the expert stacks in the
+    t32 layout (models/llama.py finalize_layout;
     16-row-interleaved gate|up per expert):
       * decode (P = T k pairs <= GEMV_MAX_PAIRS): qmv_moe (qmv.hip) — one workgroup per (pair, 32 columns of its
         expert), q8 activations, gate|up SwiGLU into [P, F]; then qmv_moe_down — one workgroup per (token, 32
@@ -15,7 +16,9 @@ GPU path (all device-side, hipGraph-capturable):
         [P, H] buffer, one writer per output);
       * larger batches: moe_sort (counting sort of the pairs by expert, per-expert tile prefix) -> grouped qmm2
         (qmm2_impl.h Q2Group: 32- / 64-row MFMA tiles per expert, A rows gathered through the sort) for gate|up
-        SwiGLU and down -> moe_combine (h += sum_j w_j * y_j, fixed order). Expert stacks that do not fit the t32 layout (a row count
+        SwiGLU and down, the down epilogue adding each sorted row times its routing weight into the token's
+        residual row (fp32 atomics; MX_MOE_GROUPED_COMBINE=0: [P, H] buffer + moe_combine in fixed order).
+    Expert stacks that do not fit the t32 layout (a row count
     per expert or K that is not whole 32-row groups / 256-k super-blocks) keep the row layout and the qgemm16
     grouped kernel.
 CPU path: the same math with dequantised fp32 expert weights (numerics oracle).
