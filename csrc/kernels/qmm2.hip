@@ -46,22 +46,54 @@ extern "C" int mxk_qmm2_dbg(int dbg, int wm, int ks, int wn, const uint16_t* A, 
 // GeGLU over 16-row interleaved gate|up -> f16 [M, N/2]. wm: 32-row MFMA blocks per wave; wn: 32-column groups
 // per wave (BM = 32 wm wn); ks: 1 (4 waves) or 2 (8 waves, k-steps split per wave pair). splits: K split in
 // whole super-blocks.
-extern "C" int mxk_qmm2(int qtype, int epi, int wm, int ks, int wn, const uint16_t* A, int lda, const uint8_t* W, int M,
-                        int N, int K, int splits, void* C, int ldc, hipStream_t st) {
+static int qmm2_go(int qtype, int epi, int wm, int ks, int wn, const uint16_t* A, int lda, const uint8_t* W, int M, int N,
+                   int K, int splits, void* C, int ldc, hipStream_t st, const Q2Fuse& fu) {
     if (M <= 0) return 0;
     if (K % 256 || (lda & 7) || ((uintptr_t)A & 15) || ((uintptr_t)W & 15) || (N & 31)) return (int)hipErrorInvalidValue;
     if (epi != E16_ADD_F32 && splits != 1) return (int)hipErrorInvalidValue;
     switch (qtype) {
-        case MXQ_Q4_K: return qmm2_run_q4k(epi, wm, ks, wn, A, lda, W, M, N, K, splits, C, ldc, st);
-        case MXQ_Q5_K: return qmm2_run_q5k(epi, wm, ks, wn, A, lda, W, M, N, K, splits, C, ldc, st);
-        case MXQ_Q6_K: return qmm2_run_q6k(epi, wm, ks, wn, A, lda, W, M, N, K, splits, C, ldc, st);
-        case MXQ_Q3_K: return qmm2_run_q3k(epi, wm, ks, wn, A, lda, W, M, N, K, splits, C, ldc, st);
-        case MXQ_Q2_K: return qmm2_run_q2k(epi, wm, ks, wn, A, lda, W, M, N, K, splits, C, ldc, st);
-        case MXQ_Q8_0: return qmm2_run_q80(epi, wm, ks, wn, A, lda, W, M, N, K, splits, C, ldc, st);
-        case MXQ_MX4F: return qmm2_run_mx4(epi, wm, ks, wn, A, lda, W, M, N, K, splits, C, ldc, st);
-        case MXQ_MX5F: return qmm2_run_mx5(epi, wm, ks, wn, A, lda, W, M, N, K, splits, C, ldc, st);
+        case MXQ_Q4_K: return qmm2_run_q4k(epi, wm, ks, wn, A, lda, W, M, N, K, splits, C, ldc, st, fu);
+        case MXQ_Q5_K: return qmm2_run_q5k(epi, wm, ks, wn, A, lda, W, M, N, K, splits, C, ldc, st, fu);
+        case MXQ_Q6_K: return qmm2_run_q6k(epi, wm, ks, wn, A, lda, W, M, N, K, splits, C, ldc, st, fu);
+        case MXQ_Q3_K: return qmm2_run_q3k(epi, wm, ks, wn, A, lda, W, M, N, K, splits, C, ldc, st, fu);
+        case MXQ_Q2_K: return qmm2_run_q2k(epi, wm, ks, wn, A, lda, W, M, N, K, splits, C, ldc, st, fu);
+        case MXQ_Q8_0: return qmm2_run_q80(epi, wm, ks, wn, A, lda, W, M, N, K, splits, C, ldc, st, fu);
+        case MXQ_MX4F: return qmm2_run_mx4(epi, wm, ks, wn, A, lda, W, M, N, K, splits, C, ldc, st, fu);
+        case MXQ_MX5F: return qmm2_run_mx5(epi, wm, ks, wn, A, lda, W, M, N, K, splits, C, ldc, st, fu);
     }
     return (int)hipErrorInvalidValue;
+}
+
+extern "C" int mxk_qmm2(int qtype, int epi, int wm, int ks, int wn, const uint16_t* A, int lda, const uint8_t* W, int M,
+                        int N, int K, int splits, void* C, int ldc, hipStream_t st) {
+    return qmm2_go(qtype, epi, wm, ks, wn, A, lda, W, M, N, K, splits, C, ldc, st, Q2Fuse{});
+}
+
+// mxk_qmm2 with the RMSNorm split across two GEMMs (Q2Fuse in qmm2_impl.h).
+// mode 1 (producer; epi must be 2 = fp32 accumulate into the residual C): ss_out / ss_zero rows of 32 floats
+// (ss_zero may be null), gamma [N], xn f16 [M, ldxn] (null: only re-zero ss_zero), tick >= ceil(M / 32) * N / 32
+// zeroed counters (left zeroed).
+// mode 2 (consumer; any epi): rows scaled by rsqrt(ss_in[32 m] * inv_h + eps) before the epilogue.
+extern "C" int mxk_qmm2_fused(int qtype, int epi, int wm, int ks, int wn, const uint16_t* A, int lda, const uint8_t* W,
+                              int M, int N, int K, int splits, void* C, int ldc, int mode, float* ss_out, float* ss_zero,
+                              const float* gamma, uint16_t* xn, int ldxn, unsigned* tick, const float* ss_in,
+                              float inv_h, float eps, hipStream_t st) {
+    if (mode == 1 && (epi != E16_ADD_F32 || (xn && (!gamma || !ss_out || !tick || (ldxn < N)))))
+        return (int)hipErrorInvalidValue;
+    if (mode == 2 && !ss_in) return (int)hipErrorInvalidValue;
+    if (mode < 0 || mode > 2) return (int)hipErrorInvalidValue;
+    Q2Fuse fu;
+    fu.mode = mode;
+    fu.ss_out = ss_out;
+    fu.ss_zero = ss_zero;
+    fu.gamma = gamma;
+    fu.xn = xn;
+    fu.ldxn = ldxn;
+    fu.tick = tick;
+    fu.ss_in = ss_in;
+    fu.inv_h = inv_h;
+    fu.eps = eps;
+    return qmm2_go(qtype, epi, wm, ks, wn, A, lda, W, M, N, K, splits, C, ldc, st, fu);
 }
 
 // Grouped MoE GEMM on t32 expert stacks (see Q2Group in qmm2_impl.h): A f16 token rows gathered through stok (or the

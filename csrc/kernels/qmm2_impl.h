@@ -4,6 +4,29 @@
 
 extern int g_qmm2_rot;  // k-order rotation multiplier per column tile (0: natural order), mxk_qmm2_set_rot
 
+// RMSNorm fused across two GEMMs (M > 4 dense layers: o_proj -> gate|up, down -> next qkv). rmsnorm(x) W^T =
+// diag(1 / rms(x)) ((x * g) W^T), so the norm splits into
+//   mode 1, the producer (E16_ADD_F32 into the fp32 residual): once a 32-row x 32-column block of the residual is
+//     final (splits == 1, or the last of its K splits by a relaxed per-block ticket), its wave writes
+//     xn = f16(x * g) (the next GEMM's A operand) and adds the rows' partial sums of squares into ss_out
+//     (one 128-byte line per row); workgroup 0 re-zeroes ss_zero (the buffer the previous consumer read);
+//   mode 2, the consumer (any epilogue): scales its fp32 accumulators by rsqrt(ss_in[m] * inv_h + eps) per row
+//     before the epilogue (SwiGLU's gate and up alike: the scale is linear in both).
+// That removes the standalone rmsnorm launches between them (profiles/r6_norm_fusion.md).
+struct Q2Fuse {
+    int mode = 0;
+    float* ss_out = nullptr;
+    float* ss_zero = nullptr;
+    const float* gamma = nullptr;
+    uint16_t* xn = nullptr;
+    int ldxn = 0;
+    unsigned* tick = nullptr;
+    const float* ss_in = nullptr;
+    float inv_h = 0.f;
+    float eps = 0.f;
+};
+constexpr int Q2F_SS_STRIDE = 32;  // floats between rows of ss_out / ss_in
+
 namespace {
 
 // NS: ring slots (k-tiles of 64): 4, or 8 for the 64-row tiles ("deep ring", ks | 8 in mxk_qmm2) — a 64-row
@@ -95,12 +118,14 @@ struct Q2Group {
     const float* owt = nullptr;
 };
 
+
 // DBG (isolation builds, tools/prof_qmm.py --q2dbg): 1 no MFMA, 2 no dequant VALU, 4 no A loads, 8 no weight loads
-template <int QT, int WM, int KS, int WN, int EPI, int DBG = 0, int NS = 4, int NG = 4, int GPW = 1, bool GR = false>
+template <int QT, int WM, int KS, int WN, int EPI, int DBG = 0, int NS = 4, int NG = 4, int GPW = 1, bool GR = false,
+          bool FU = false>
 __global__ __launch_bounds__(NG == 8 ? 512 / GPW : 256 * KS) void qmm2_kernel(const uint16_t* __restrict__ A, int lda,
                                                         const uint8_t* __restrict__ W, int M, int N, int K,
                                                         int n_mt, int splits, int sbps, void* __restrict__ Cv,
-                                                        int ldc, int rot_mul, Q2Group grp) {
+                                                        int ldc, int rot_mul, Q2Group grp, Q2Fuse fu = Q2Fuse{}) {
     using G = Q2Geom<QT, WM, KS, WN, NS, NG, GPW>;
     using F = Q2F<QT>;
     constexpr int BM = G::BM, WA = G::WA, STAGE = G::STAGE, A_BYTES = G::A_BYTES;
@@ -377,6 +402,24 @@ __global__ __launch_bounds__(NG == 8 ? 512 / GPW : 256 * KS) void qmm2_kernel(co
 
     // ---- epilogue: 32x32 C/D layout: col = lane & 31, row = 8*(r>>2) + 4*(lane>>5) + (r&3) ----
     const int mb = m_base + mw * WM * 32;
+    if constexpr (FU && !GR) {
+        if (fu.mode == 2) {  // fused RMSNorm, consumer side: the rows' 1 / rms
+            // one row per lane (row mb + 32 i + lane % 32), handed to the C/D layout's rows by lane shuffles: one
+            // load per 32 rows keeps the register footprint at the kernel's own
+#pragma unroll
+            for (int i = 0; i < WM; ++i) {
+                const int mr = mb + i * 32 + col;
+                const float s = mr < M ? fu.ss_in[(size_t)mr * Q2F_SS_STRIDE] : 0.f;
+                const float rsl = rsqrtf(s * fu.inv_h + fu.eps);
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const float rs = __shfl(rsl, 8 * (r >> 2) + 4 * h + (r & 3));
+#pragma unroll
+                    for (int j = 0; j < WN; ++j) acc[i][j][r] *= rs;
+                }
+            }
+        }
+    }
 #pragma unroll
     for (int j = 0; j < WN; ++j) {
         const int nt = (ct * NG + nw * WN + j) * 32;
@@ -445,11 +488,75 @@ __global__ __launch_bounds__(NG == 8 ? 512 / GPW : 256 * KS) void qmm2_kernel(co
             }
         }
     }
+    if constexpr (FU && EPI == E16_ADD_F32 && !GR) {
+        if (fu.mode == 1) {  // fused RMSNorm, producer side
+            if (fu.ss_zero && bid == 0 && wave == 0)
+                for (int m = lane; m < M; m += 64) fu.ss_zero[(size_t)m * Q2F_SS_STRIDE] = 0.f;
+            if (!fu.xn) return;
+            // this wave's block is final once every K split has added into it: the adds complete (vmcnt) before a
+            // relaxed agent-scope ticket; the last split reads the block with agent-scope loads (no fence: see
+            // profiles/r6_fence_free_handoffs.md)
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const int n0 = (ct * NG + nw * WN) * 32;
+            if (n0 >= N || mb >= M) return;
+            if (splits > 1) {
+                const int tk = (mb >> 5) * ngrp + (n0 >> 5);
+                unsigned last = 0;
+                if (lane == 0)
+                    last = __hip_atomic_fetch_add(fu.tick + tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                           (unsigned)(splits - 1);
+                last = __shfl(last, 0);
+                if (!last) return;
+                if (lane == 0) __hip_atomic_store(fu.tick + tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            // lane = one column, one 32-row block at a time: x * g -> xn, the row's sum of squares over this wave's
+            // 32 WN columns -> one atomic per row
+            for (int i = 0; i < WM; ++i) {
+                const int mr = mb + i * 32;
+                if (mr >= M) break;
+                float ssr = 0.f;  // sum for row mr + (lane % 32) after the transposing shuffles below
+#pragma unroll
+                for (int j = 0; j < WN; ++j) {
+                    const int n = n0 + j * 32 + col;
+                    if (n0 + j * 32 >= N) break;
+                    const float g = fu.gamma[n];
+                    float sq[16];
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const int m = mr + 8 * (r >> 2) + 4 * h + (r & 3);
+                        float x = 0.f;
+                        if (m < M) {
+                            x = __hip_atomic_load((float*)Cv + (size_t)m * ldc + n, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
+                            fu.xn[(size_t)m * fu.ldxn + n] = f32_to_act<true>(fminf(fmaxf(x * g, -65504.f), 65504.f));
+                        }
+                        sq[r] = x * x;
+                    }
+                    // reduce each row's 32 columns (the lanes of this half)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        float v = sq[r];
+                        v += __shfl_xor(v, 1);
+                        v += __shfl_xor(v, 2);
+                        v += __shfl_xor(v, 4);
+                        v += __shfl_xor(v, 8);
+                        v += __shfl_xor(v, 16);
+                        // lane c of the block's row c: row 8 (r >> 2) + 4 h + (r & 3) lives in half h
+                        const int rr = 8 * (r >> 2) + (r & 3);
+                        const float v0 = __shfl(v, 0), v1 = __shfl(v, 32);  // the two halves' rows rr and rr + 4
+                        if (col == rr) ssr += v0;
+                        if (col == rr + 4) ssr += v1;
+                    }
+                }
+                if (lane < 32 && mr + col < M) atomicAdd(fu.ss_out + (size_t)(mr + col) * Q2F_SS_STRIDE, ssr);
+            }
+        }
+    }
 }
 
-template <int QT, int WM, int KS, int WN, int EPI, int NS = 4, int NG = 4, int GPW = 1>
+template <int QT, int WM, int KS, int WN, int EPI, int NS = 4, int NG = 4, int GPW = 1, bool FU = false>
 static int launch_qmm2(const uint16_t* A, int lda, const uint8_t* W, int M, int N, int K, int splits, void* C, int ldc,
-                       hipStream_t st) {
+                       hipStream_t st, const Q2Fuse& fu) {
     using G = Q2Geom<QT, WM, KS, WN, NS, NG, GPW>;
     const int nsb = K >> 8;
     splits = max(1, min(splits, nsb));
@@ -460,12 +567,12 @@ static int launch_qmm2(const uint16_t* A, int lda, const uint8_t* W, int M, int 
     if (nwg <= 0 || nwg > 0x7fffffff) return (int)hipErrorInvalidValue;
     static bool attr_set = false;
     if (!attr_set) {
-        (void)hipFuncSetAttribute((const void*)qmm2_kernel<QT, WM, KS, WN, EPI, 0, NS, NG, GPW>,
+        (void)hipFuncSetAttribute((const void*)qmm2_kernel<QT, WM, KS, WN, EPI, 0, NS, NG, GPW, false, FU>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS);
         attr_set = true;
     }
-    qmm2_kernel<QT, WM, KS, WN, EPI, 0, NS, NG, GPW><<<dim3((unsigned)nwg), 64 * G::NT, G::LDS, st>>>(
-        A, lda, W, M, N, K, n_mt, splits, sbps, C, ldc, g_qmm2_rot, Q2Group{});
+    qmm2_kernel<QT, WM, KS, WN, EPI, 0, NS, NG, GPW, false, FU><<<dim3((unsigned)nwg), 64 * G::NT, G::LDS, st>>>(
+        A, lda, W, M, N, K, n_mt, splits, sbps, C, ldc, g_qmm2_rot, Q2Group{}, fu);
     MXK_CHECK_LAUNCH();
 }
 
@@ -486,7 +593,7 @@ static int launch_qmm2_grouped(const uint16_t* A, int lda, const int* stok, cons
         attr_set = true;
     }
     qmm2_kernel<QT, WM, KS, 1, EPI, 0, 4, 4, 1, true><<<dim3((unsigned)nwg), 64 * G::NT, G::LDS, st>>>(
-        A, lda, W, P, N, K, n_mt, 1, K >> 8, C, ldc, 0, Q2Group{tiles, off, stok, E, otok, owt});
+        A, lda, W, P, N, K, n_mt, 1, K >> 8, C, ldc, 0, Q2Group{tiles, off, stok, E, otok, owt}, Q2Fuse{});
     MXK_CHECK_LAUNCH();
 }
 
@@ -506,18 +613,18 @@ static int qmm2_grouped_run(int epi, int wm, const uint16_t* A, int lda, const i
 }
 
 // ks: 1 / 2 waves per column group; ks | 8 selects the 8-slot ring (64-row tiles only); 17 the wide tiles
-template <int QT, int EPI>
+template <int QT, int EPI, bool FU = false>
 static int dispatch_qmm2(int wm, int ks, int wn, const uint16_t* A, int lda, const uint8_t* W, int M, int N, int K,
-                         int splits, void* C, int ldc, hipStream_t st) {
+                         int splits, void* C, int ldc, hipStream_t st, const Q2Fuse& fu) {
 // (configurations whose ring does not fit the LDS for this format — 256-row tiles of Q8_0 — are not compiled)
 #define Q2_CASE(WM_, KS_, WN_)                                                                \
     if constexpr (Q2Geom<QT, WM_, KS_, WN_, 4>::LDS <= 160 * 1024)                            \
         if (wm == WM_ && ks == KS_ && wn == WN_)                                              \
-            return launch_qmm2<QT, WM_, KS_, WN_, EPI>(A, lda, W, M, N, K, splits, C, ldc, st);
+            return launch_qmm2<QT, WM_, KS_, WN_, EPI, 4, 4, 1, FU>(A, lda, W, M, N, K, splits, C, ldc, st, fu);
 #define Q2_DEEP(WM_, KS_, WN_)                                                                   \
     if constexpr (Q2Geom<QT, WM_, KS_, WN_, 8>::LDS <= 160 * 1024)                               \
         if (wm == WM_ && ks == (KS_ | 8) && wn == WN_)                                           \
-            return launch_qmm2<QT, WM_, KS_, WN_, EPI, 8>(A, lda, W, M, N, K, splits, C, ldc, st);
+            return launch_qmm2<QT, WM_, KS_, WN_, EPI, 8, 4, 1, FU>(A, lda, W, M, N, K, splits, C, ldc, st, fu);
     // (8, 2, 1) / (4, 2, 2) (256-row tiles with 8 waves) exceed the 256 registers a wave has at 2 waves / SIMD
     Q2_CASE(2, 1, 1) Q2_CASE(2, 2, 1) Q2_CASE(4, 1, 1) Q2_CASE(4, 2, 1) Q2_CASE(8, 1, 1)
     Q2_CASE(1, 2, 2) Q2_CASE(2, 1, 2) Q2_CASE(2, 2, 2) Q2_CASE(4, 1, 2)
@@ -531,14 +638,14 @@ static int dispatch_qmm2(int wm, int ks, int wn, const uint16_t* A, int lda, con
 #define Q2_R6(WM_, KS_, WN_)                                                                     \
     if constexpr (Q2Geom<QT, WM_, KS_, WN_, 6>::LDS <= 160 * 1024)                               \
         if (wm == WM_ && ks == (KS_ | 32) && wn == WN_)                                          \
-            return launch_qmm2<QT, WM_, KS_, WN_, EPI, 6>(A, lda, W, M, N, K, splits, C, ldc, st);
+            return launch_qmm2<QT, WM_, KS_, WN_, EPI, 6, 4, 1, FU>(A, lda, W, M, N, K, splits, C, ldc, st, fu);
     Q2_R6(4, 1, 1) Q2_R6(4, 2, 1) Q2_R6(2, 2, 2) Q2_R6(2, 1, 2)
 #undef Q2_R6
     // ks | 16: wide tiles (8 column groups, 256 columns per workgroup, 8 waves)
 #define Q2_WIDE(WM_, WN_)                                                                      \
     if constexpr (Q2Geom<QT, WM_, 1, WN_, 4, 8>::LDS <= 160 * 1024)                           \
         if (wm == WM_ && ks == 17 && wn == WN_)                                                \
-            return launch_qmm2<QT, WM_, 1, WN_, EPI, 4, 8>(A, lda, W, M, N, K, splits, C, ldc, st);
+            return launch_qmm2<QT, WM_, 1, WN_, EPI, 4, 8, 1, FU>(A, lda, W, M, N, K, splits, C, ldc, st, fu);
     Q2_WIDE(2, 1) Q2_WIDE(4, 1) Q2_WIDE(6, 1) Q2_WIDE(3, 2) Q2_WIDE(7, 1)
     // ks 18: the 4-wave wide form (each wave 64 columns x 32 wm rows)
 // (Q4_K / MX4F only: formats whose tile and header each take one DMA instruction; the Q6_K form returned NaNs in
@@ -546,7 +653,7 @@ static int dispatch_qmm2(int wm, int ks, int wn, const uint16_t* A, int lda, con
 #define Q2_WIDE4(WM_)                                                                          \
     if constexpr ((QT == MXQ_Q4_K || QT == MXQ_MX4F) && Q2Geom<QT, WM_, 1, 2, 4, 8, 2>::LDS <= 160 * 1024) \
         if (wm == WM_ && ks == 18 && wn == 2)                                                  \
-            return launch_qmm2<QT, WM_, 1, 2, EPI, 4, 8, 2>(A, lda, W, M, N, K, splits, C, ldc, st);
+            return launch_qmm2<QT, WM_, 1, 2, EPI, 4, 8, 2, FU>(A, lda, W, M, N, K, splits, C, ldc, st, fu);
     Q2_WIDE4(4) Q2_WIDE4(6) Q2_WIDE4(2)
 #undef Q2_WIDE4
 #undef Q2_WIDE
@@ -563,7 +670,7 @@ static int launch_dbg(int wm, int ks, int wn, const uint16_t* A, int lda, const 
         (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
         const int n_ct = (N + 32 * ng - 1) / (32 * ng), n_mt = (M + bm - 1) / bm;
         kern<<<dim3(n_ct * n_mt), ng == 8 ? 512 : 256 * ks, lds, st>>>(A, lda, W, M, N, K, n_mt, 1, K >> 8, C, ldc,
-                                                                      g_qmm2_rot, Q2Group{});
+                                                                      g_qmm2_rot, Q2Group{}, Q2Fuse{});
         return (int)hipGetLastError();
     };
     // ks 17: the wide tiles (8 column groups)
@@ -579,7 +686,7 @@ static int launch_dbg(int wm, int ks, int wn, const uint16_t* A, int lda, const 
                                   Q2Geom<QT, 6, 1, 2, 4, 8, 2>::LDS);
         const int n_ct = (N + 255) / 256, n_mt = (M + 191) / 192;
         k4<<<dim3(n_ct * n_mt), 256, Q2Geom<QT, 6, 1, 2, 4, 8, 2>::LDS, st>>>(A, lda, W, M, N, K, n_mt, 1, K >> 8, C, ldc,
-                                                                            g_qmm2_rot, Q2Group{});
+                                                                            g_qmm2_rot, Q2Group{}, Q2Fuse{});
         return (int)hipGetLastError();
     }
     if (wm == 8 && ks == 1 && wn == 1) return go(qmm2_kernel<QT, 8, 1, 1, EPI, DBG>, 256, 1, Q2Geom<QT, 8, 1, 1>::LDS);
@@ -592,27 +699,40 @@ static int launch_dbg(int wm, int ks, int wn, const uint16_t* A, int lda, const 
 
 // all epilogues of one block format (each format's instances live in their own translation unit, qmm2_q*.hip)
 template <int QT>
-static int qmm2_run(int epi, int wm, int ks, int wn, const uint16_t* A, int lda, const uint8_t* W, int M, int N, int K, int splits, void* C, int ldc, hipStream_t st) {
+static int qmm2_run(int epi, int wm, int ks, int wn, const uint16_t* A, int lda, const uint8_t* W, int M, int N, int K, int splits, void* C, int ldc, hipStream_t st, const Q2Fuse& fu) {
+    if (fu.mode != 0) {
+        // the fused-RMSNorm forms (separate instances: the plain ones keep their register allocation): the
+        // residual-add producer, the fp32 (split-K qkv) and SwiGLU consumers, for the K-quant formats of the
+        // Q4_K_M / Q5_K_M / Q6_K / Q8_0 files
+        if constexpr (QT == MXQ_Q4_K || QT == MXQ_Q5_K || QT == MXQ_Q6_K || QT == MXQ_Q8_0) {
+            switch (epi) {
+                case E16_F32: return dispatch_qmm2<QT, E16_F32, true>(wm, ks, wn, A, lda, W, M, N, K, splits, C, ldc, st, fu);
+                case E16_ADD_F32: return dispatch_qmm2<QT, E16_ADD_F32, true>(wm, ks, wn, A, lda, W, M, N, K, splits, C, ldc, st, fu);
+                case E16_SWIGLU: return dispatch_qmm2<QT, E16_SWIGLU, true>(wm, ks, wn, A, lda, W, M, N, K, splits, C, ldc, st, fu);
+            }
+        }
+        return (int)hipErrorNotSupported;
+    }
     switch (epi) {
-        case E16_F32: return dispatch_qmm2<QT, E16_F32>(wm, ks, wn, A, lda, W, M, N, K, splits, C, ldc, st);
-        case E16_ACT: return dispatch_qmm2<QT, E16_ACT>(wm, ks, wn, A, lda, W, M, N, K, splits, C, ldc, st);
-        case E16_ADD_F32: return dispatch_qmm2<QT, E16_ADD_F32>(wm, ks, wn, A, lda, W, M, N, K, splits, C, ldc, st);
-        case E16_SWIGLU: return dispatch_qmm2<QT, E16_SWIGLU>(wm, ks, wn, A, lda, W, M, N, K, splits, C, ldc, st);
-        case E16_GEGLU: return dispatch_qmm2<QT, E16_GEGLU>(wm, ks, wn, A, lda, W, M, N, K, splits, C, ldc, st);
+        case E16_F32: return dispatch_qmm2<QT, E16_F32>(wm, ks, wn, A, lda, W, M, N, K, splits, C, ldc, st, fu);
+        case E16_ACT: return dispatch_qmm2<QT, E16_ACT>(wm, ks, wn, A, lda, W, M, N, K, splits, C, ldc, st, fu);
+        case E16_ADD_F32: return dispatch_qmm2<QT, E16_ADD_F32>(wm, ks, wn, A, lda, W, M, N, K, splits, C, ldc, st, fu);
+        case E16_SWIGLU: return dispatch_qmm2<QT, E16_SWIGLU>(wm, ks, wn, A, lda, W, M, N, K, splits, C, ldc, st, fu);
+        case E16_GEGLU: return dispatch_qmm2<QT, E16_GEGLU>(wm, ks, wn, A, lda, W, M, N, K, splits, C, ldc, st, fu);
     }
     return (int)hipErrorInvalidValue;
 }
 
 }  // namespace
 
-int qmm2_run_q4k(int epi, int wm, int ks, int wn, const uint16_t* A, int lda, const uint8_t* W, int M, int N, int K, int splits, void* C, int ldc, hipStream_t st);
-int qmm2_run_q5k(int epi, int wm, int ks, int wn, const uint16_t* A, int lda, const uint8_t* W, int M, int N, int K, int splits, void* C, int ldc, hipStream_t st);
-int qmm2_run_q6k(int epi, int wm, int ks, int wn, const uint16_t* A, int lda, const uint8_t* W, int M, int N, int K, int splits, void* C, int ldc, hipStream_t st);
-int qmm2_run_q3k(int epi, int wm, int ks, int wn, const uint16_t* A, int lda, const uint8_t* W, int M, int N, int K, int splits, void* C, int ldc, hipStream_t st);
-int qmm2_run_q2k(int epi, int wm, int ks, int wn, const uint16_t* A, int lda, const uint8_t* W, int M, int N, int K, int splits, void* C, int ldc, hipStream_t st);
-int qmm2_run_q80(int epi, int wm, int ks, int wn, const uint16_t* A, int lda, const uint8_t* W, int M, int N, int K, int splits, void* C, int ldc, hipStream_t st);
-int qmm2_run_mx4(int epi, int wm, int ks, int wn, const uint16_t* A, int lda, const uint8_t* W, int M, int N, int K, int splits, void* C, int ldc, hipStream_t st);
-int qmm2_run_mx5(int epi, int wm, int ks, int wn, const uint16_t* A, int lda, const uint8_t* W, int M, int N, int K, int splits, void* C, int ldc, hipStream_t st);
+int qmm2_run_q4k(int epi, int wm, int ks, int wn, const uint16_t* A, int lda, const uint8_t* W, int M, int N, int K, int splits, void* C, int ldc, hipStream_t st, const Q2Fuse& fu);
+int qmm2_run_q5k(int epi, int wm, int ks, int wn, const uint16_t* A, int lda, const uint8_t* W, int M, int N, int K, int splits, void* C, int ldc, hipStream_t st, const Q2Fuse& fu);
+int qmm2_run_q6k(int epi, int wm, int ks, int wn, const uint16_t* A, int lda, const uint8_t* W, int M, int N, int K, int splits, void* C, int ldc, hipStream_t st, const Q2Fuse& fu);
+int qmm2_run_q3k(int epi, int wm, int ks, int wn, const uint16_t* A, int lda, const uint8_t* W, int M, int N, int K, int splits, void* C, int ldc, hipStream_t st, const Q2Fuse& fu);
+int qmm2_run_q2k(int epi, int wm, int ks, int wn, const uint16_t* A, int lda, const uint8_t* W, int M, int N, int K, int splits, void* C, int ldc, hipStream_t st, const Q2Fuse& fu);
+int qmm2_run_q80(int epi, int wm, int ks, int wn, const uint16_t* A, int lda, const uint8_t* W, int M, int N, int K, int splits, void* C, int ldc, hipStream_t st, const Q2Fuse& fu);
+int qmm2_run_mx4(int epi, int wm, int ks, int wn, const uint16_t* A, int lda, const uint8_t* W, int M, int N, int K, int splits, void* C, int ldc, hipStream_t st, const Q2Fuse& fu);
+int qmm2_run_mx5(int epi, int wm, int ks, int wn, const uint16_t* A, int lda, const uint8_t* W, int M, int N, int K, int splits, void* C, int ldc, hipStream_t st, const Q2Fuse& fu);
 int qmm2_grouped_q4k(int epi, int wm, const uint16_t* A, int lda, const int* stok, const uint8_t* W, int P, int E, int N, int K, const int* tiles, const int* off, void* C, int ldc, const int* otok, const float* owt, hipStream_t st);
 int qmm2_grouped_q5k(int epi, int wm, const uint16_t* A, int lda, const int* stok, const uint8_t* W, int P, int E, int N, int K, const int* tiles, const int* off, void* C, int ldc, const int* otok, const float* owt, hipStream_t st);
 int qmm2_grouped_q6k(int epi, int wm, const uint16_t* A, int lda, const int* stok, const uint8_t* W, int P, int E, int N, int K, const int* tiles, const int* off, void* C, int ldc, const int* otok, const float* owt, hipStream_t st);

@@ -2,8 +2,8 @@
 // the instances compile in parallel).
 #include "qmm2_impl.h"
 
-int qmm2_run_q4k(int epi, int wm, int ks, int wn, const uint16_t* A, int lda, const uint8_t* W, int M, int N, int K, int splits, void* C, int ldc, hipStream_t st) {
-    return qmm2_run<MXQ_Q4_K>(epi, wm, ks, wn, A, lda, W, M, N, K, splits, C, ldc, st);
+int qmm2_run_q4k(int epi, int wm, int ks, int wn, const uint16_t* A, int lda, const uint8_t* W, int M, int N, int K, int splits, void* C, int ldc, hipStream_t st, const Q2Fuse& fu) {
+    return qmm2_run<MXQ_Q4_K>(epi, wm, ks, wn, A, lda, W, M, N, K, splits, C, ldc, st, fu);
 }
 
 int qmm2_dbg_q4k(int dbg, int wm, int ks, int wn, const uint16_t* A, int lda, const uint8_t* W, int M, int N, int K, void* C,

@@ -37,7 +37,8 @@ from ..ops import core as K
 from ..ops import quant as Q
 from ..ops.linear import (ACT_DTYPE, EPI_ADD_F32, EPI_BF16, EPI_F32, EPI_GEGLU, EPI_SWIGLU, QWeight, concat_rows,
                           _fp32_out_ok, dense_min_m, interleave_gate_up, glu_interleaved, qmatmul, qmv_fusable, qmv_rope_ok,
-                          qmv_fused, qmv_rope_fused)
+                          qmv_fused, qmv_rope_fused, NormFuse, norm_fusable)
+from ..ops import autotune as _AT
 from ..ops.moe import MoEWeights, moe_ffn
 from . import lora_runtime as LR
 from .config import LlamaConfig
@@ -53,6 +54,9 @@ DECODE_PART_SMALL_B = int(__import__("os").environ.get("MX_DECODE_PART_SMALL_B",
 # SRC_NORM / SRC_ACT). Every workgroup of the GEMV redoes the row statistics, so the fusion pays only at
 # batch 1 (profiles/r2_qmv_fuse_fuse{0,1}_c{1,4}.json: c1 387 -> 442 tok/s, c4 961 -> 861)
 QMV_FUSE_MAX_M = int(__import__("os").environ.get("MX_QMV_FUSE_MAX_M", "1"))
+# timing-only switch (WRONG outputs): skip the M > 4 path's standalone "norm" / "rope" / "attn" launches to bound
+# what fusing them away could save (profiles/r6_fusion_bound.md)
+_DBG_SKIP = frozenset(__import__("os").environ.get("MX_DBG_SKIP", "").split(","))
 
 
 def vocab_shard(V: int, tp: int) -> int:
@@ -158,6 +162,11 @@ class Workspace:
         self.part_o = torch.empty((max_seqs * nh * max_parts, cfg.head_dim), dtype=torch.float32, device=dev)
         # per-(sequence, kv head) arrival counters of the decode kernel's fused partition merge (self-resetting)
         self.part_cnt = torch.zeros(max_seqs * max(1, cfg.n_kv_heads // tp_size), dtype=torch.int32, device=dev)
+        # RMSNorm split across the GEMMs at M > 4 (ops/linear.py NormFuse): per-row sums of squares (one 128-byte line
+        # per row) in two buffers that alternate between producers, and the producers' per-block split tickets; both
+        # are zero between uses (each producer re-zeroes the buffer the previous consumer read, tickets self-reset)
+        self.norm_ss = torch.zeros((2, T, 32), dtype=torch.float32, device=dev)
+        self.norm_tick = torch.zeros(-(-T // 32) * -(-H // 32), dtype=torch.int32, device=dev)
 
     def decode_part_size(self, B: int, Hq: int, max_len: int) -> int:
         """Split-K partition length of the paged decode attention: small batches split the context
@@ -567,6 +576,31 @@ class LlamaModel:
         from .. import _native as N
         return int(N.kernels().mxk_attn_prefill_rows(self.n_heads, self.n_kv))
 
+    def _norm_fuse_on(self, T: int, gemv: bool, fb, ws: Workspace) -> bool:
+        """Whether this M = T forward splits each layer's RMSNorms across the GEMMs around them (ops/linear.py
+        NormFuse): dense SwiGLU layers, no LoRA / post-norms / dense qkv copy, one rank, every o_proj / down / qkv /
+        gate|up GEMM on a qmm2 plan with a fused instance. Cached per (T, tuned-plan count)."""
+        if gemv or self.tp_size != 1 or self.device.type != "cuda" or fb.stop_layer is not None or not self.layers:
+            return False
+        key = (T, len(_AT.TUNED))
+        c = self.__dict__.setdefault("_nf_cache", {})
+        ok = c.get(key)
+        if ok is None:
+            H = self.cfg.hidden
+            ok = (self.glu_epi == EPI_SWIGLU and T <= ws.norm_ss.shape[1]
+                  and -(-T // 32) * -(-H // 32) <= ws.norm_tick.numel() and ws.xb.dtype == torch.float16)
+            for L in self.layers if ok else ():
+                if (L.moe is not None or L.lora is not None or L.post_attn_norm is not None
+                        or L.post_ffn_norm is not None or L.qkv_dense is not None or L.wgu is None
+                        or L.attn_norm.dtype != torch.float32 or L.ffn_norm.dtype != torch.float32
+                        or not norm_fusable(L.wo, T, EPI_ADD_F32) or not norm_fusable(L.wd, T, EPI_ADD_F32)
+                        or not norm_fusable(L.wgu, T, EPI_SWIGLU)
+                        or not all(norm_fusable(w, T, EPI_F32, True) for w in L.qkv_parts)):
+                    ok = False
+                    break
+            c[key] = ok
+        return ok
+
     def forward(self, fb: ForwardBatch, kv, ws: Workspace) -> torch.Tensor:
         cfg = self.cfg
         T = fb.T
@@ -585,9 +619,14 @@ class LlamaModel:
                 for r0, e in fb.embed_rows:
                     h[r0:r0 + e.shape[0]].copy_(e)
         xb = ws.xb[:T, :H]
+        # M > 4: each layer's RMSNorms split across the GEMMs (o_proj -> gate|up, down -> next qkv), no norm launches
+        nf = self._norm_fuse_on(T, gemv, fb, ws)
+        nl = len(self.layers)
         for li, L in enumerate(self.layers):
             if fb.stop_layer is not None and li >= fb.stop_layer:
                 break
+            # consumer side of the fused norms (this layer's qkv reads xb = f16(h * attn_norm) from the previous down)
+            nf_qkv = NormFuse(2, ss_in=ws.norm_ss[1], eps=eps) if nf and li > 0 else None
             kc, vc = kv.layer(li)
             # ---- attention block ----
             qkv = ws.qkv[:T]
@@ -600,7 +639,8 @@ class LlamaModel:
                 xq, xds = ws.q8(T, H)
                 K.rmsnorm(h, L.attn_norm, eps, out_q8=(xq, xds))
             else:
-                K.rmsnorm(h, L.attn_norm, eps, out_bf16=xb)
+                if nf_qkv is None and "norm" not in _DBG_SKIP:
+                    K.rmsnorm(h, L.attn_norm, eps, out_bf16=xb)
                 xq = xds = None
             if not gemv and not qkv.is_cuda:
                 qkv.zero_()
@@ -638,18 +678,18 @@ class LlamaModel:
                 elif gemv:
                     qmatmul(w, None, EPI_F32, sl, xq=xq, xds=xds, out_zeroed=qkv.is_cuda)
                 else:
-                    qmatmul(w, xb, EPI_F32, sl, out_zeroed=True)
+                    qmatmul(w, xb, EPI_F32, sl, out_zeroed=True, fuse=nf_qkv)
                 off += w.N
             if lo_qkv is not None:  # runtime LoRA: q|k|v += B (A x) on the normed rows
                 if gemv:
                     K.rmsnorm(h, L.attn_norm, eps, out_bf16=xb)
                 LR.add_qkv(lo_qkv, xb, qkv)
-            if not rope_fused:
+            if not rope_fused and ("rope" not in _DBG_SKIP or gemv):
                 K.rope_kv(qkv, L.bqkv, fb.positions, fb.slots, inv_freq, attn_factor, Hq, Hkv, D,
                           cfg.rope_dim, cfg.neox, q.view(T, Hq, D), kc, vc, kv.block_size,
                           qk_norm=(L.q_norm, L.k_norm, eps) if L.q_norm is not None else None, zero_after=True)
             attn = ws.attn[:T]
-            if nd:
+            if nd and ("attn" not in _DBG_SKIP or gemv):
                 K.attn_decode(q[:nd].view(nd, Hq, D), kc, vc, fb.dec_block_tables, fb.dec_seq_lens, self.scale,
                               attn[:nd].view(nd, Hq, D), max_seq_len=fb.dec_max_len or None,
                               workspace=(ws.part_ml, ws.part_o, ws.part_cnt), window=L.window, softcap=cfg.attn_softcap,
@@ -668,7 +708,10 @@ class LlamaModel:
                     K.quant_q8(attn, aq, ads)
                 else:
                     aq = ads = None
-                self._residual_proj(L.wo, attn, aq, ads, h, L.post_attn_norm, ws, T, eps)
+                # producer: h += attn W_o^T, then xb = f16(h * ffn_norm) and the rows' sums of squares -> norm_ss[0]
+                self._residual_proj(L.wo, attn, aq, ads, h, L.post_attn_norm, ws, T, eps,
+                                    fuse=NormFuse(1, ss_out=ws.norm_ss[0], ss_zero=ws.norm_ss[1], gamma=L.ffn_norm,
+                                                  xn=xb, tick=ws.norm_tick) if nf else None)
             if lo is not None and lo.o is not None:
                 LR.add_residual(lo.o, attn, h)
             # ---- FFN block ----
@@ -699,7 +742,7 @@ class LlamaModel:
             elif gemv:
                 xq, xds = ws.q8(T, H)
                 K.rmsnorm(h, L.ffn_norm, eps, out_q8=(xq, xds))
-            else:
+            elif not nf and "norm" not in _DBG_SKIP:
                 K.rmsnorm(h, L.ffn_norm, eps, out_bf16=xb)
             if L.wgu is not None:
                 if fuse_gu:
@@ -707,7 +750,8 @@ class LlamaModel:
                 elif gemv:
                     qmatmul(L.wgu, None, self.glu_epi, act, xq=xq, xds=xds)
                 else:
-                    qmatmul(L.wgu, xb, self.glu_epi, act)
+                    qmatmul(L.wgu, xb, self.glu_epi, act,
+                            fuse=NormFuse(2, ss_in=ws.norm_ss[0], eps=eps) if nf else None)
             else:
                 g_out = torch.empty((T, F), dtype=ACT_DTYPE, device=h.device)
                 u_out = torch.empty((T, F), dtype=ACT_DTYPE, device=h.device)
@@ -727,7 +771,13 @@ class LlamaModel:
                 K.quant_q8(act, aq, ads)
             else:
                 aq = ads = None
-            self._residual_proj(L.wd, act, aq, ads, h, L.post_ffn_norm, ws, T, eps)
+            nf_down = None
+            if nf:  # producer for the next layer's qkv (the last layer's down only re-zeroes norm_ss[0])
+                last = li + 1 >= nl
+                nf_down = NormFuse(1, ss_out=None if last else ws.norm_ss[1], ss_zero=ws.norm_ss[0],
+                                   gamma=None if last else self.layers[li + 1].attn_norm, xn=None if last else xb,
+                                   tick=ws.norm_tick)
+            self._residual_proj(L.wd, act, aq, ads, h, L.post_ffn_norm, ws, T, eps, fuse=nf_down)
             if lo is not None and lo.down is not None:
                 LR.add_residual(lo.down, act, h)
         if self.stage or fb.stop_layer is not None:
@@ -895,7 +945,8 @@ class LlamaModel:
         else:
             h.add_(y16)
 
-    def _residual_proj(self, W: QWeight, x, xq, xds, h: torch.Tensor, post_norm, ws: Workspace, T: int, eps: float):
+    def _residual_proj(self, W: QWeight, x, xq, xds, h: torch.Tensor, post_norm, ws: Workspace, T: int, eps: float,
+                       fuse: NormFuse | None = None):
         """h += x W^T — or, with a Gemma post-norm, h += rmsnorm(x W^T) * post_norm. Under tensor
         parallelism each rank's partial projection is all-reduced in 16 bits (half the fp32 residual's
         bytes; one message per row-parallel projection) and added to the replicated residual."""
@@ -932,9 +983,11 @@ class LlamaModel:
             if gemv:
                 mm(W, None, EPI_ADD_F32, h, xq=xq, xds=xds)
             else:
-                mm(W, x, EPI_ADD_F32, h)
+                mm(W, x, EPI_ADD_F32, h, fuse=fuse)
             self._allreduce(h)
             return
+        if fuse is not None:
+            raise ValueError("norm fusion with a post-norm")
         y = ws.y[:T]
         if gemv:
             mm(W, None, EPI_F32, y, xq=xq, xds=xds)

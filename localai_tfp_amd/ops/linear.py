@@ -232,13 +232,14 @@ def _mfma_shape(M: int, N_: int, nblk: int, can_split: bool, qtype: int):
 
 
 def qmatmul(W: QWeight, x: torch.Tensor | None, epi: int, out: torch.Tensor, *, xq: torch.Tensor | None = None,
-            xds: torch.Tensor | None = None, out_zeroed: bool = False):
+            xds: torch.Tensor | None = None, out_zeroed: bool = False, fuse: "NormFuse | None" = None):
     """out (+)= x @ W^T with the given epilogue.
 
     x:   bf16 [M, K] (MFMA / dense path) — may be None when (xq, xds) given and M <= 4
     epi: EPI_F32 (store fp32) | EPI_BF16 | EPI_ADD_F32 (out += ; fp32) | EPI_SWIGLU / EPI_GEGLU
          (silu- / gelu-gated, 16-bit [M, N/2])
     out_zeroed: for EPI_F32, caller guarantees `out` is zero so split-K may accumulate atomically.
+    fuse: the RMSNorm split across this GEMM and its neighbour (NormFuse; only where norm_fusable() said so).
     """
     M = (x if x is not None else xq).shape[0]
     if M == 0:
@@ -250,7 +251,9 @@ def qmatmul(W: QWeight, x: torch.Tensor | None, epi: int, out: torch.Tensor, *, 
         y = torch.matmul(x, W.data.t()) if x.dtype == W.data.dtype else torch.matmul(x.to(W.data.dtype), W.data.t())
         return _apply_epi_dense(y, epi, out)
     if W.layout == "t32":
-        return _qmatmul_t32(W, x, epi, out, xq, xds, M, out_zeroed)
+        return _qmatmul_t32(W, x, epi, out, xq, xds, M, out_zeroed, fuse)
+    if fuse is not None:
+        raise ValueError("qmatmul: norm fusion needs t32 weights")
     if M <= 4 and xq is not None:
         if epi in (EPI_BF16, *GLU_EPIS):
             N.ensure_act(out.dtype)
@@ -319,10 +322,13 @@ def row_chunks(M: int, chunk: int | None = None) -> list[tuple[int, int]]:
     return [(r, min(r + c, M)) for r in range(0, M, c)]
 
 
-def run_plan(plan: tuple, W: QWeight, x: torch.Tensor, epi: int, out: torch.Tensor, out_zeroed: bool):
+def run_plan(plan: tuple, W: QWeight, x: torch.Tensor, epi: int, out: torch.Tensor, out_zeroed: bool,
+             fuse: "NormFuse | None" = None):
     """Launch one GEMM plan (ops/autotune.py): ("q3", wm, splits) | ("q2", wm, ks, wn, splits) | ("rows", chunk)."""
     M = x.shape[0]
     kind = plan[0]
+    if fuse is not None and kind != "q2":
+        raise ValueError(f"norm fusion needs a qmm2 plan, not {plan}")
     if kind == "rows":
         for r0, r1 in row_chunks(M, plan[1]):
             _qmatmul_t32(W, x[r0:r1], epi, out[r0:r1], None, None, r1 - r0, out_zeroed)
@@ -336,6 +342,12 @@ def run_plan(plan: tuple, W: QWeight, x: torch.Tensor, epi: int, out: torch.Tens
     if kind == "q3":
         N.kcall("mxk_qmm3", int(W.qtype), e, plan[1], x.data_ptr(), x.stride(0), W.data.data_ptr(), M, W.N, W.K,
                 splits, out.data_ptr(), out.stride(0), N.stream_ptr())
+    elif kind == "q2" and fuse is not None:
+        f = fuse
+        N.kcall("mxk_qmm2_fused", int(W.qtype), e, plan[1], plan[2], plan[3], x.data_ptr(), x.stride(0),
+                W.data.data_ptr(), M, W.N, W.K, splits, out.data_ptr(), out.stride(0), f.mode, N.ptr(f.ss_out),
+                N.ptr(f.ss_zero), N.ptr(f.gamma), N.ptr(f.xn), f.xn.stride(0) if f.xn is not None else 0,
+                N.ptr(f.tick), N.ptr(f.ss_in), 1.0 / W.K if f.mode == 2 else 1.0 / W.N, f.eps, N.stream_ptr())
     elif kind == "q2":
         N.kcall("mxk_qmm2", int(W.qtype), e, plan[1], plan[2], plan[3], x.data_ptr(), x.stride(0), W.data.data_ptr(),
                 M, W.N, W.K, splits, out.data_ptr(), out.stride(0), N.stream_ptr())
@@ -344,8 +356,60 @@ def run_plan(plan: tuple, W: QWeight, x: torch.Tensor, epi: int, out: torch.Tens
     return out
 
 
-def _qmatmul_t32(W: QWeight, x, epi: int, out, xq, xds, M: int, out_zeroed: bool):
+def _t32_plan(W: QWeight, M: int, epi: int, out_zeroed: bool, dtype=torch.float16):
+    """The plan _qmatmul_t32 runs for an M-row f16 GEMM on t32 weights, or None where it takes the dense copy."""
+    can_split = epi == EPI_ADD_F32 or (epi == EPI_F32 and out_zeroed)
+    if W.bf16_cache is not None and M >= dense_min_m(dtype, epi, can_split) and W.bf16_cache.dtype == dtype:
+        return None
+    forced = QMM2 or QMM3 or QMM2_FORCE is not None or QMM3_FORCE is not None
+    plan = _AT.lookup(W.N, W.K, int(W.qtype), epi, can_split, M) if (_AT.TUNED and not forced) else None
+    if plan is None:
+        if len(row_chunks(M)) > 1:
+            plan = ("rows", ROW_CHUNK)
+        else:
+            plan = _gemm_pick(M, W.N, W.K, int(W.qtype), can_split)
+    return plan
+
+
+class NormFuse:
+    """The RMSNorm between two K-quant GEMMs, split across them (qmm2_impl.h Q2Fuse): the producer (the residual-add
+    o_proj / down GEMM, mode 1) writes xn = f16(h * gamma) and the rows' sums of squares into ss_out as its output
+    blocks become final, and re-zeroes ss_zero; the consumer (qkv / gate|up, mode 2) scales its rows by
+    rsqrt(ss_in / K + eps). ss buffers: [rows, 32] fp32 (one 128-byte line per row), tick: zeroed int32 counters."""
+    __slots__ = ("mode", "ss_out", "ss_zero", "gamma", "xn", "tick", "ss_in", "eps")
+
+    def __init__(self, mode: int, *, ss_out=None, ss_zero=None, gamma=None, xn=None, tick=None, ss_in=None,
+                 eps: float = 0.0):
+        self.mode, self.ss_out, self.ss_zero, self.gamma, self.xn = mode, ss_out, ss_zero, gamma, xn
+        self.tick, self.ss_in, self.eps = tick, ss_in, float(eps)
+
+
+NORM_FUSE = os.environ.get("MX_NORM_FUSE", "0") != "0"
+_NORM_FUSE_QT = None
+
+
+def norm_fusable(W, M: int, epi: int, out_zeroed: bool = False) -> bool:
+    """True where an M-row GEMM on W runs a qmm2 plan whose fused-RMSNorm instance exists (Q4_K / Q5_K / Q6_K / Q8_0
+    t32 weights, M > 4, f16 activations; fp32 / residual-add / SwiGLU epilogues)."""
+    global _NORM_FUSE_QT
+    if _NORM_FUSE_QT is None:
+        _NORM_FUSE_QT = {int(QType.Q4_K), int(QType.Q5_K), int(QType.Q6_K), int(QType.Q8_0)}
+    if (not NORM_FUSE or not isinstance(W, QWeight) or W.layout != "t32" or M <= 4 or int(W.qtype) not in _NORM_FUSE_QT
+            or epi not in (EPI_F32, EPI_ADD_F32, EPI_SWIGLU) or W.data.device.type != "cuda"):
+        return False
+    plan = _t32_plan(W, M, epi, out_zeroed)
+    return plan is not None and plan[0] == "q2"
+
+
+def _qmatmul_t32(W: QWeight, x, epi: int, out, xq, xds, M: int, out_zeroed: bool, fuse: "NormFuse | None" = None):
     """t32 tiled weights: qmv (q8 activations, M <= 4) or qmm2 / qmm3 (f16 activations, any M; tuned plan)."""
+    if fuse is not None:
+        if x is None or x.dtype != torch.float16:
+            raise ValueError("qmatmul: norm fusion needs f16 activations")
+        plan = _t32_plan(W, M, epi, out_zeroed)
+        if plan is None:
+            raise ValueError("qmatmul: norm fusion on a dense-copy GEMM")
+        return run_plan(plan, W, x, epi, out, out_zeroed, fuse)
     if M <= 4 and xq is not None:
         if epi in (EPI_BF16, *GLU_EPIS):
             N.ensure_act(out.dtype)
