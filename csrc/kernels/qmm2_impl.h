@@ -24,6 +24,19 @@ struct Q2Fuse {
     const float* ss_in = nullptr;
     float inv_h = 0.f;
     float eps = 0.f;
+    // mode bit 4, the qkv GEMM (E16_F32, or E16_ADD_F32 split-K into the zeroed qkv buffer): RoPE (adjacent pairs,
+    // rot_dim = D) and the paged KV append in the epilogue instead of a rope_kv launch; split-K blocks are summed by
+    // the last split (ticket, as mode 1), which re-zeroes them. Column n_off + n of the q|k|v row is head
+    // (n_off + n) >> dsh.
+    const int* pos = nullptr;
+    const int* slots = nullptr;
+    const float* inv_freq = nullptr;
+    const float* bias = nullptr;
+    uint16_t* qo = nullptr;
+    uint16_t* kc = nullptr;
+    uint16_t* vc = nullptr;
+    float attn_factor = 1.f;
+    int n_off = 0, dsh = 7, hq = 0, hkv = 0, block_size = 16;
 };
 constexpr int Q2F_SS_STRIDE = 32;  // floats between rows of ss_out / ss_in
 
@@ -403,7 +416,7 @@ __global__ __launch_bounds__(NG == 8 ? 512 / GPW : 256 * KS) void qmm2_kernel(co
     // ---- epilogue: 32x32 C/D layout: col = lane & 31, row = 8*(r>>2) + 4*(lane>>5) + (r&3) ----
     const int mb = m_base + mw * WM * 32;
     if constexpr (FU && !GR) {
-        if (fu.mode == 2) {  // fused RMSNorm, consumer side: the rows' 1 / rms
+        if (fu.mode & 2) {  // fused RMSNorm, consumer side: the rows' 1 / rms
             // one row per lane (row mb + 32 i + lane % 32), handed to the C/D layout's rows by lane shuffles: one
             // load per 32 rows keeps the register footprint at the kernel's own
 #pragma unroll
@@ -418,6 +431,86 @@ __global__ __launch_bounds__(NG == 8 ? 512 / GPW : 256 * KS) void qmm2_kernel(co
                     for (int j = 0; j < WN; ++j) acc[i][j][r] *= rs;
                 }
             }
+        }
+    }
+    if constexpr (FU && !GR && (EPI == E16_F32 || EPI == E16_ADD_F32)) {
+        if (fu.mode & 4) {  // RoPE + KV append epilogue (q|k|v GEMM)
+            const int n0 = (ct * NG + nw * WN) * 32;
+            if (n0 >= N || mb >= M) return;
+            if (splits > 1) {  // sum the splits in C, the last one takes the block (as the fused-norm producer)
+#pragma unroll
+                for (int j = 0; j < WN; ++j) {
+                    if (n0 + j * 32 >= N) break;
+#pragma unroll
+                    for (int i = 0; i < WM; ++i)
+#pragma unroll
+                        for (int r = 0; r < 16; ++r) {
+                            const int m = mb + i * 32 + 8 * (r >> 2) + 4 * h + (r & 3);
+                            if (m < M) atomicAdd((float*)Cv + (size_t)m * ldc + n0 + j * 32 + col, acc[i][j][r]);
+                        }
+                }
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                const int tk = (mb >> 5) * ngrp + (n0 >> 5);
+                unsigned last = 0;
+                if (lane == 0)
+                    last = __hip_atomic_fetch_add(fu.tick + tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                           (unsigned)(splits - 1);
+                last = __shfl(last, 0);
+                if (!last) return;
+                if (lane == 0) __hip_atomic_store(fu.tick + tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            const int D = 1 << fu.dsh;
+            for (int i = 0; i < WM; ++i) {
+                const int mr = mb + i * 32;
+                if (mr >= M) break;
+                // one row per lane, handed out by shuffles (as the row scale above)
+                const int pl = mr + col < M ? fu.pos[mr + col] : 0;
+                const int sl = mr + col < M ? fu.slots[mr + col] : -1;
+#pragma unroll
+                for (int j = 0; j < WN; ++j) {
+                    if (n0 + j * 32 >= N) break;
+                    const int n = n0 + j * 32 + col;
+                    const int c = fu.n_off + n, hh = c >> fu.dsh, d = c & (D - 1);
+                    const float bn = fu.bias ? fu.bias[c] : 0.f;
+                    const float fr = fu.inv_freq[d >> 1];
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const int rr = 8 * (r >> 2) + 4 * h + (r & 3), m = mr + rr;
+                        float v;
+                        if (splits > 1) {
+                            float* cp = (float*)Cv + (size_t)min(m, M - 1) * ldc + n;
+                            v = m < M ? __hip_atomic_load(cp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.f;
+                            if (m < M) *cp = 0.f;  // the buffer stays zero for the next split-K accumulation
+                        } else {
+                            v = acc[i][j][r];
+                        }
+                        v += bn;
+                        const float partner = __shfl_xor(v, 1);  // the other element of the adjacent pair
+                        const int p = __shfl(pl, rr), slot = __shfl(sl, rr);
+                        float y = v;
+                        if (hh < fu.hq + fu.hkv) {
+                            float sv, cv;
+                            sincosf((float)p * fr, &sv, &cv);
+                            cv *= fu.attn_factor;
+                            sv *= fu.attn_factor;
+                            y = (d & 1) ? partner * sv + v * cv : v * cv - partner * sv;
+                        }
+                        if (m < M) {
+                            const uint16_t yb = (uint16_t)(pack_bf16x2(y, 0.f) & 0xFFFF);
+                            if (hh < fu.hq) {
+                                fu.qo[((size_t)m * fu.hq + hh) * D + d] = yb;
+                            } else if (slot >= 0) {
+                                const bool isk = hh < fu.hq + fu.hkv;
+                                const int kvh = hh - fu.hq - (isk ? 0 : fu.hkv);
+                                const size_t e = (((size_t)(slot / fu.block_size) * fu.hkv + kvh) * fu.block_size +
+                                                  slot % fu.block_size) * D + d;
+                                (isk ? fu.kc : fu.vc)[e] = yb;
+                            }
+                        }
+                    }
+                }
+            }
+            return;
         }
     }
 #pragma unroll
@@ -489,7 +582,7 @@ __global__ __launch_bounds__(NG == 8 ? 512 / GPW : 256 * KS) void qmm2_kernel(co
         }
     }
     if constexpr (FU && EPI == E16_ADD_F32 && !GR) {
-        if (fu.mode == 1) {  // fused RMSNorm, producer side
+        if (fu.mode & 1) {  // fused RMSNorm, producer side
             if (fu.ss_zero && bid == 0 && wave == 0)
                 for (int m = lane; m < M; m += 64) fu.ss_zero[(size_t)m * Q2F_SS_STRIDE] = 0.f;
             if (!fu.xn) return;

@@ -38,6 +38,7 @@ from ..ops import quant as Q
 from ..ops.linear import (ACT_DTYPE, EPI_ADD_F32, EPI_BF16, EPI_F32, EPI_GEGLU, EPI_SWIGLU, QWeight, concat_rows,
                           _fp32_out_ok, dense_min_m, interleave_gate_up, glu_interleaved, qmatmul, qmv_fusable, qmv_rope_ok,
                           qmv_fused, qmv_rope_fused, NormFuse, norm_fusable)
+from ..ops import linear as _LIN
 from ..ops import autotune as _AT
 from ..ops.moe import MoEWeights, moe_ffn
 from . import lora_runtime as LR
@@ -166,7 +167,7 @@ class Workspace:
         # per row) in two buffers that alternate between producers, and the producers' per-block split tickets; both
         # are zero between uses (each producer re-zeroes the buffer the previous consumer read, tickets self-reset)
         self.norm_ss = torch.zeros((2, T, 32), dtype=torch.float32, device=dev)
-        self.norm_tick = torch.zeros(-(-T // 32) * -(-H // 32), dtype=torch.int32, device=dev)
+        self.norm_tick = torch.zeros(-(-T // 32) * -(-max(H, qd + 2 * kvd) // 32), dtype=torch.int32, device=dev)
 
     def decode_part_size(self, B: int, Hq: int, max_len: int) -> int:
         """Split-K partition length of the paged decode attention: small batches split the context
@@ -601,6 +602,17 @@ class LlamaModel:
             c[key] = ok
         return ok
 
+    def _rope_fuse_on(self, T: int) -> bool:
+        """Every layer's q|k|v GEMM at M = T runs a qmm2 plan with a fused instance (RoPE epilogue, mode bit 4)."""
+        key = ("rope", T, len(_AT.TUNED))
+        c = self.__dict__.setdefault("_nf_cache", {})
+        ok = c.get(key)
+        if ok is None:
+            ok = all(L.qkv_dense is None and all(norm_fusable(w, T, EPI_F32, True, rope=True) for w in L.qkv_parts)
+                     for L in self.layers)
+            c[key] = ok
+        return ok
+
     def forward(self, fb: ForwardBatch, kv, ws: Workspace) -> torch.Tensor:
         cfg = self.cfg
         T = fb.T
@@ -622,6 +634,10 @@ class LlamaModel:
         # M > 4: each layer's RMSNorms split across the GEMMs (o_proj -> gate|up, down -> next qkv), no norm launches
         nf = self._norm_fuse_on(T, gemv, fb, ws)
         nl = len(self.layers)
+        nf_rope = (_LIN.ROPE_FUSE and not gemv and self.tp_size == 1 and self.device.type == "cuda" and not cfg.neox
+                   and cfg.rope_dim == D and D in (64, 128) and fb.stop_layer is None and ws.q.dtype == torch.bfloat16
+                   and -(-T // 32) * -(-(qd + 2 * kvd) // 32) <= ws.norm_tick.numel()
+                   and self._rope_fuse_on(T))
         for li, L in enumerate(self.layers):
             if fb.stop_layer is not None and li >= fb.stop_layer:
                 break
@@ -656,6 +672,9 @@ class LlamaModel:
             lo_qkv = lo.qkv if lo is not None else None
             rope_fused = (fuse_qkv and T == 1 and off == 0 and not cfg.neox and cfg.rope_dim == D
                           and L.q_norm is None and lo_qkv is None)
+            # M > 4: RoPE + KV append in the q|k|v GEMM epilogue (qmm2 mode bit 4) instead of a rope_kv launch
+            rope_ep = (nf_rope and off == 0 and L.q_norm is None and lo_qkv is None and kc.dtype == torch.bfloat16
+                       and vc.dtype == torch.bfloat16)
             if rope_fused:
                 # every part is checked before any launches: parts may mix block formats
                 o2 = 0
@@ -677,6 +696,11 @@ class LlamaModel:
                     qmv_fused(w, h, EPI_F32, sl, norm=L.attn_norm, eps=eps, out_zeroed=True)
                 elif gemv:
                     qmatmul(w, None, EPI_F32, sl, xq=xq, xds=xds, out_zeroed=qkv.is_cuda)
+                elif rope_ep:
+                    qmatmul(w, xb, EPI_F32, sl, out_zeroed=True, fuse=NormFuse(
+                        4 | (2 if nf_qkv is not None else 0), ss_in=ws.norm_ss[1], eps=eps, tick=ws.norm_tick,
+                        rope=(fb.positions, fb.slots, inv_freq, L.bqkv, q, kc, vc, attn_factor, off, D, Hq, Hkv,
+                              kv.block_size)))
                 else:
                     qmatmul(w, xb, EPI_F32, sl, out_zeroed=True, fuse=nf_qkv)
                 off += w.N
@@ -684,7 +708,7 @@ class LlamaModel:
                 if gemv:
                     K.rmsnorm(h, L.attn_norm, eps, out_bf16=xb)
                 LR.add_qkv(lo_qkv, xb, qkv)
-            if not rope_fused and ("rope" not in _DBG_SKIP or gemv):
+            if not rope_fused and not rope_ep and ("rope" not in _DBG_SKIP or gemv):
                 K.rope_kv(qkv, L.bqkv, fb.positions, fb.slots, inv_freq, attn_factor, Hq, Hkv, D,
                           cfg.rope_dim, cfg.neox, q.view(T, Hq, D), kc, vc, kv.block_size,
                           qk_norm=(L.q_norm, L.k_norm, eps) if L.q_norm is not None else None, zero_after=True)

@@ -342,12 +342,20 @@ def run_plan(plan: tuple, W: QWeight, x: torch.Tensor, epi: int, out: torch.Tens
     if kind == "q3":
         N.kcall("mxk_qmm3", int(W.qtype), e, plan[1], x.data_ptr(), x.stride(0), W.data.data_ptr(), M, W.N, W.K,
                 splits, out.data_ptr(), out.stride(0), N.stream_ptr())
+    elif kind == "q2" and fuse is not None and fuse.mode & 4:
+        f = fuse
+        pos, slots, inv_freq, bias, qo, kc, vc, af, n_off, D, hq, hkv, bsz = f.rope
+        N.kcall("mxk_qmm2_rope", int(W.qtype), e, plan[1], plan[2], plan[3], x.data_ptr(), x.stride(0),
+                W.data.data_ptr(), M, W.N, W.K, splits, out.data_ptr(), out.stride(0), f.mode, N.ptr(f.ss_in),
+                1.0 / W.K, f.eps, N.ptr(f.tick), pos.data_ptr(), slots.data_ptr(), inv_freq.data_ptr(), N.ptr(bias),
+                qo.data_ptr(), kc.data_ptr(), vc.data_ptr(), float(af), int(n_off), int(D).bit_length() - 1, int(hq),
+                int(hkv), int(bsz), N.stream_ptr())
     elif kind == "q2" and fuse is not None:
         f = fuse
         N.kcall("mxk_qmm2_fused", int(W.qtype), e, plan[1], plan[2], plan[3], x.data_ptr(), x.stride(0),
                 W.data.data_ptr(), M, W.N, W.K, splits, out.data_ptr(), out.stride(0), f.mode, N.ptr(f.ss_out),
                 N.ptr(f.ss_zero), N.ptr(f.gamma), N.ptr(f.xn), f.xn.stride(0) if f.xn is not None else 0,
-                N.ptr(f.tick), N.ptr(f.ss_in), 1.0 / W.K if f.mode == 2 else 1.0 / W.N, f.eps, N.stream_ptr())
+                N.ptr(f.tick), N.ptr(f.ss_in), 1.0 / W.K, f.eps, N.stream_ptr())
     elif kind == "q2":
         N.kcall("mxk_qmm2", int(W.qtype), e, plan[1], plan[2], plan[3], x.data_ptr(), x.stride(0), W.data.data_ptr(),
                 M, W.N, W.K, splits, out.data_ptr(), out.stride(0), N.stream_ptr())
@@ -376,25 +384,29 @@ class NormFuse:
     o_proj / down GEMM, mode 1) writes xn = f16(h * gamma) and the rows' sums of squares into ss_out as its output
     blocks become final, and re-zeroes ss_zero; the consumer (qkv / gate|up, mode 2) scales its rows by
     rsqrt(ss_in / K + eps). ss buffers: [rows, 32] fp32 (one 128-byte line per row), tick: zeroed int32 counters."""
-    __slots__ = ("mode", "ss_out", "ss_zero", "gamma", "xn", "tick", "ss_in", "eps")
+    __slots__ = ("mode", "ss_out", "ss_zero", "gamma", "xn", "tick", "ss_in", "eps", "rope")
 
     def __init__(self, mode: int, *, ss_out=None, ss_zero=None, gamma=None, xn=None, tick=None, ss_in=None,
-                 eps: float = 0.0):
+                 eps: float = 0.0, rope: tuple | None = None):
         self.mode, self.ss_out, self.ss_zero, self.gamma, self.xn = mode, ss_out, ss_zero, gamma, xn
         self.tick, self.ss_in, self.eps = tick, ss_in, float(eps)
+        # mode bit 4 (the q|k|v GEMM): RoPE + paged KV append in the epilogue, rope = (positions, slots, inv_freq,
+        # bias or None, q_out bf16 [T, Hq * D], k_cache, v_cache, attn_factor, column offset, D, Hq, Hkv, block_size)
+        self.rope = rope
 
 
 NORM_FUSE = os.environ.get("MX_NORM_FUSE", "0") != "0"
+ROPE_FUSE = os.environ.get("MX_ROPE_FUSE", "0") != "0"
 _NORM_FUSE_QT = None
 
 
-def norm_fusable(W, M: int, epi: int, out_zeroed: bool = False) -> bool:
+def norm_fusable(W, M: int, epi: int, out_zeroed: bool = False, rope: bool = False) -> bool:
     """True where an M-row GEMM on W runs a qmm2 plan whose fused-RMSNorm instance exists (Q4_K / Q5_K / Q6_K / Q8_0
     t32 weights, M > 4, f16 activations; fp32 / residual-add / SwiGLU epilogues)."""
     global _NORM_FUSE_QT
     if _NORM_FUSE_QT is None:
         _NORM_FUSE_QT = {int(QType.Q4_K), int(QType.Q5_K), int(QType.Q6_K), int(QType.Q8_0)}
-    if (not NORM_FUSE or not isinstance(W, QWeight) or W.layout != "t32" or M <= 4 or int(W.qtype) not in _NORM_FUSE_QT
+    if (not (ROPE_FUSE if rope else NORM_FUSE) or not isinstance(W, QWeight) or W.layout != "t32" or M <= 4 or int(W.qtype) not in _NORM_FUSE_QT
             or epi not in (EPI_F32, EPI_ADD_F32, EPI_SWIGLU) or W.data.device.type != "cuda"):
         return False
     plan = _t32_plan(W, M, epi, out_zeroed)

@@ -69,10 +69,12 @@ def test_norm_fusion_producer_consumer(qt, M, wm, ks, wn, splits, monkeypatch):
 
 
 @pytest.mark.parametrize("P", [40, 200])
-def test_norm_fusion_model_forward(P, monkeypatch):
-    """A Llama-shaped model's M > 4 forward with the norms fused equals the forward with separate norm launches
-    (the buffer ping-pong and re-zeroing over all layers, and over repeated forwards on one workspace), and the
-    fused path is the one taken."""
+@pytest.mark.parametrize("norm,rope", [(True, False), (False, True), (True, True)])
+def test_norm_fusion_model_forward(P, norm, rope, monkeypatch):
+    """A Llama-shaped model's M > 4 forward with the norms split across the GEMMs and / or RoPE + KV append in the
+    q|k|v GEMM epilogue equals the forward with separate norm / rope_kv launches: logits and the paged KV cache,
+    over repeated forwards on one workspace (buffer ping-pong, re-zeroing, self-resetting tickets), and the fused
+    path is the one taken."""
     import numpy as np
     from localai_tfp_amd.engine.kv_cache import KVCache
     from localai_tfp_amd.models.config import tiny_config
@@ -84,8 +86,9 @@ def test_norm_fusion_model_forward(P, monkeypatch):
     prompt = list(np.random.default_rng(0).integers(0, cfg.vocab, P))
     bs = 16
 
-    def run(fused):
-        monkeypatch.setattr(L, "NORM_FUSE", fused)
+    def run(nf, rf):
+        monkeypatch.setattr(L, "NORM_FUSE", nf)
+        monkeypatch.setattr(L, "ROPE_FUSE", rf)
         m.__dict__.pop("_nf_cache", None)
         kv = KVCache(cfg.n_layers, 64, m.n_kv, bs, cfg.head_dim, "cuda")
         ws = Workspace(cfg, 256, 8, "cuda", m.tp_size)
@@ -99,14 +102,22 @@ def test_norm_fusion_model_forward(P, monkeypatch):
                           pf_ctx_lens=torch.tensor([P], dtype=torch.int32, device=DEV), pf_q_lens_host=[P],
                           pf_ctx_lens_host=[P])
         outs = [m.forward(fb, kv, ws).float().cpu().clone() for _ in range(2)]
-        taken = any(m.__dict__.get("_nf_cache", {}).values())
+        cache = torch.cat([kv.layer(li)[j][1:len(blocks) + 1].float().flatten().cpu()
+                           for li in range(cfg.n_layers) for j in (0, 1)])
+        taken = {k: v for k, v in m.__dict__.get("_nf_cache", {}).items() if v}
         assert float(ws.norm_ss.abs().max()) == 0.0 and int(ws.norm_tick.abs().max()) == 0
-        return outs, taken
+        assert float(ws.qkv.abs().max()) == 0.0  # the split-K q|k|v buffer is left zeroed either way
+        return outs, cache, taken
 
-    (f1, f2), taken = run(True)
-    assert taken, "the fused-norm path did not apply"
-    (u1, _), taken_u = run(False)
+    (f1, f2), fc, taken = run(norm, rope)
+    if norm:
+        assert any(isinstance(k[0], int) for k in taken), "the fused-norm path did not apply"
+    if rope:
+        assert any(k[0] == "rope" for k in taken), "the RoPE epilogue did not apply"
+    (u1, _), uc, taken_u = run(False, False)
     assert not taken_u
-    assert float((f1 - f2).abs().max()) == 0.0 or float((f1 - f2).norm() / f1.norm()) < 1e-3
+    assert float((f1 - f2).norm() / f1.norm()) < 1e-3
     r = float((f1 - u1).norm() / u1.norm())
     assert r < 1e-2, r
+    rc = float((fc - uc).norm() / uc.norm())
+    assert rc < 1e-2, rc
