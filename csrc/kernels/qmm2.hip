@@ -96,17 +96,18 @@ extern "C" int mxk_qmm2_fused(int qtype, int epi, int wm, int ks, int wn, const 
     return qmm2_go(qtype, epi, wm, ks, wn, A, lda, W, M, N, K, splits, C, ldc, st, fu);
 }
 
-// mxk_qmm2_fused plus mode bit 4: RoPE (adjacent pairs over the whole head, D = 1 << dsh in {64, 128}) and the paged
+// mxk_qmm2_fused plus mode bit 4: RoPE (adjacent pairs over the whole head, D = 1 << dsh in {64, 128}; rot = the
+// step's [M][D / 2] (cos, sin) x attn_factor table) and the paged
 // bf16 KV append in the q|k|v GEMM's epilogue (Q2Fuse in qmm2_impl.h). epi 0 (splits 1) or 2 (split-K into the
 // zeroed fp32 C, left zeroed; tick as mode 1). Columns n_off .. n_off + N of the q|k|v row; qo bf16 [M, hq << dsh];
 // kc / vc [blocks][hkv][block_size][D] bf16.
 extern "C" int mxk_qmm2_rope(int qtype, int epi, int wm, int ks, int wn, const uint16_t* A, int lda, const uint8_t* W,
                              int M, int N, int K, int splits, void* C, int ldc, int mode, const float* ss_in, float inv_h,
-                             float eps, unsigned* tick, const int* pos, const int* slots, const float* inv_freq,
-                             const float* bias, uint16_t* qo, uint16_t* kc, uint16_t* vc, float attn_factor, int n_off,
-                             int dsh, int hq, int hkv, int block_size, hipStream_t st) {
-    if (!(mode & 4) || (mode & 1) || (epi != E16_F32 && epi != E16_ADD_F32) || (dsh != 6 && dsh != 7) || !pos ||
-        !slots || !inv_freq || !qo || !kc || !vc || block_size <= 0 || (splits > 1 && (epi != E16_ADD_F32 || !tick)) ||
+                             float eps, unsigned* tick, const int* slots, const float2* rot, const float* bias,
+                             uint16_t* qo, uint16_t* kc, uint16_t* vc, int n_off, int dsh, int hq, int hkv,
+                             int block_size, hipStream_t st) {
+    if (!(mode & 4) || (mode & 1) || (epi != E16_F32 && epi != E16_ADD_F32) || (dsh != 6 && dsh != 7) || !slots ||
+        !rot || !qo || !kc || !vc || block_size <= 0 || (splits > 1 && (epi != E16_ADD_F32 || !tick)) ||
         ((mode & 2) && !ss_in) || (n_off & 31))
         return (int)hipErrorInvalidValue;
     Q2Fuse fu;
@@ -115,14 +116,12 @@ extern "C" int mxk_qmm2_rope(int qtype, int epi, int wm, int ks, int wn, const u
     fu.inv_h = inv_h;
     fu.eps = eps;
     fu.tick = tick;
-    fu.pos = pos;
     fu.slots = slots;
-    fu.inv_freq = inv_freq;
+    fu.rot = rot;
     fu.bias = bias;
     fu.qo = qo;
     fu.kc = kc;
     fu.vc = vc;
-    fu.attn_factor = attn_factor;
     fu.n_off = n_off;
     fu.dsh = dsh;
     fu.hq = hq;

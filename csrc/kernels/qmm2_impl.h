@@ -28,19 +28,33 @@ struct Q2Fuse {
     // rot_dim = D) and the paged KV append in the epilogue instead of a rope_kv launch; split-K blocks are summed by
     // the last split (ticket, as mode 1), which re-zeroes them. Column n_off + n of the q|k|v row is head
     // (n_off + n) >> dsh.
-    const int* pos = nullptr;
     const int* slots = nullptr;
-    const float* inv_freq = nullptr;
+    const float2* rot = nullptr;  // [M][D / 2] (cos, sin) x attn_factor of each row's position (one table per step)
     const float* bias = nullptr;
     uint16_t* qo = nullptr;
     uint16_t* kc = nullptr;
     uint16_t* vc = nullptr;
-    float attn_factor = 1.f;
     int n_off = 0, dsh = 7, hq = 0, hkv = 0, block_size = 16;
 };
 constexpr int Q2F_SS_STRIDE = 32;  // floats between rows of ss_out / ss_in
 
 namespace {
+
+// 16 agent-coherent (sc1) loads in flight at once and one wait: the relaxed __hip_atomic_load form waits for each
+// load before issuing the next (measured: +10-40 us per GEMM for a 32 x 128 block per wave). Rows past M load row
+// M - 1 (the caller ignores them).
+MX_DEV void q2_ld16_sc1(float (&v)[16], const float* base, size_t ld, int m0, int M) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const float* p = base + (size_t)min(m0 + 8 * (r >> 2) + (r & 3), M - 1) * ld;
+        asm volatile("global_load_dword %0, %1, off sc1" : "=v"(v[r]) : "v"(p) : "memory");
+    }
+    asm volatile("s_waitcnt vmcnt(0)"
+                 : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]), "+v"(v[7]),
+                   "+v"(v[8]), "+v"(v[9]), "+v"(v[10]), "+v"(v[11]), "+v"(v[12]), "+v"(v[13]), "+v"(v[14]), "+v"(v[15])
+                 :
+                 : "memory");
+}
 
 // NS: ring slots (k-tiles of 64): 4, or 8 for the 64-row tiles ("deep ring", ks | 8 in mxk_qmm2) — a 64-row
 // stage is only 12-14 KB, and with 4 slots a workgroup keeps ~2 stages (24 KB) in flight: at the ~1.1 us
@@ -459,12 +473,11 @@ __global__ __launch_bounds__(NG == 8 ? 512 / GPW : 256 * KS) void qmm2_kernel(co
                 if (!last) return;
                 if (lane == 0) __hip_atomic_store(fu.tick + tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
-            const int D = 1 << fu.dsh;
+            const int D = 1 << fu.dsh, HALF = D >> 1;
             for (int i = 0; i < WM; ++i) {
                 const int mr = mb + i * 32;
                 if (mr >= M) break;
                 // one row per lane, handed out by shuffles (as the row scale above)
-                const int pl = mr + col < M ? fu.pos[mr + col] : 0;
                 const int sl = mr + col < M ? fu.slots[mr + col] : -1;
 #pragma unroll
                 for (int j = 0; j < WN; ++j) {
@@ -472,29 +485,34 @@ __global__ __launch_bounds__(NG == 8 ? 512 / GPW : 256 * KS) void qmm2_kernel(co
                     const int n = n0 + j * 32 + col;
                     const int c = fu.n_off + n, hh = c >> fu.dsh, d = c & (D - 1);
                     const float bn = fu.bias ? fu.bias[c] : 0.f;
-                    const float fr = fu.inv_freq[d >> 1];
+                    const bool rotate = hh < fu.hq + fu.hkv;
+                    float v[16];
+                    if (splits > 1) {
+                        float* cp = (float*)Cv + n;
+                        q2_ld16_sc1(v, cp, ldc, mr + 4 * h, M);
+#pragma unroll
+                        for (int r = 0; r < 16; ++r) {
+                            const int m = mr + 8 * (r >> 2) + 4 * h + (r & 3);
+                            if (m < M) cp[(size_t)m * ldc] = 0.f;  // zero again for the next split-K accumulation
+                        }
+                    } else {
+#pragma unroll
+                        for (int r = 0; r < 16; ++r) v[r] = acc[i][j][r];
+                    }
+                    float2 cs[16];
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const int m = min(mr + 8 * (r >> 2) + 4 * h + (r & 3), M - 1);
+                        cs[r] = rotate ? fu.rot[(size_t)m * HALF + (d >> 1)] : make_float2(1.f, 0.f);
+                    }
 #pragma unroll
                     for (int r = 0; r < 16; ++r) {
                         const int rr = 8 * (r >> 2) + 4 * h + (r & 3), m = mr + rr;
-                        float v;
-                        if (splits > 1) {
-                            float* cp = (float*)Cv + (size_t)min(m, M - 1) * ldc + n;
-                            v = m < M ? __hip_atomic_load(cp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.f;
-                            if (m < M) *cp = 0.f;  // the buffer stays zero for the next split-K accumulation
-                        } else {
-                            v = acc[i][j][r];
-                        }
-                        v += bn;
-                        const float partner = __shfl_xor(v, 1);  // the other element of the adjacent pair
-                        const int p = __shfl(pl, rr), slot = __shfl(sl, rr);
-                        float y = v;
-                        if (hh < fu.hq + fu.hkv) {
-                            float sv, cv;
-                            sincosf((float)p * fr, &sv, &cv);
-                            cv *= fu.attn_factor;
-                            sv *= fu.attn_factor;
-                            y = (d & 1) ? partner * sv + v * cv : v * cv - partner * sv;
-                        }
+                        const float x = v[r] + bn;
+                        const float partner = __shfl_xor(x, 1);  // the other element of the adjacent pair
+                        const int slot = __shfl(sl, rr);
+                        const float y = rotate ? ((d & 1) ? partner * cs[r].y + x * cs[r].x : x * cs[r].x - partner * cs[r].y)
+                                               : x;
                         if (m < M) {
                             const uint16_t yb = (uint16_t)(pack_bf16x2(y, 0.f) & 0xFFFF);
                             if (hh < fu.hq) {
@@ -614,15 +632,13 @@ __global__ __launch_bounds__(NG == 8 ? 512 / GPW : 256 * KS) void qmm2_kernel(co
                     if (n0 + j * 32 >= N) break;
                     const float g = fu.gamma[n];
                     float sq[16];
+                    q2_ld16_sc1(sq, (const float*)Cv + n, ldc, mr + 4 * h, M);
 #pragma unroll
                     for (int r = 0; r < 16; ++r) {
                         const int m = mr + 8 * (r >> 2) + 4 * h + (r & 3);
-                        float x = 0.f;
-                        if (m < M) {
-                            x = __hip_atomic_load((float*)Cv + (size_t)m * ldc + n, __ATOMIC_RELAXED,
-                                                  __HIP_MEMORY_SCOPE_AGENT);
+                        const float x = m < M ? sq[r] : 0.f;
+                        if (m < M)
                             fu.xn[(size_t)m * fu.ldxn + n] = f32_to_act<true>(fminf(fmaxf(x * g, -65504.f), 65504.f));
-                        }
                         sq[r] = x * x;
                     }
                     // reduce each row's 32 columns (the lanes of this half)

@@ -38,7 +38,7 @@ KERNEL_SIGS = {
     "mxk_qgemm32": [I, I, I, I, P, I, P, P, I, I, I, I, P, I, P],
     "mxk_qmm2": [I, I, I, I, I, P, I, P, I, I, I, I, P, I, P],
     "mxk_qmm2_fused": [I, I, I, I, I, P, I, P, I, I, I, I, P, I, I, P, P, P, P, I, P, P, F, F, P],
-    "mxk_qmm2_rope": [I, I, I, I, I, P, I, P, I, I, I, I, P, I, I, P, F, F, P, P, P, P, P, P, P, P, F, I, I, I, I, I, P],
+    "mxk_qmm2_rope": [I, I, I, I, I, P, I, P, I, I, I, I, P, I, I, P, F, F, P, P, P, P, P, P, P, I, I, I, I, I, P],
     "mxk_qmm2_dbg": [I, I, I, I, P, I, P, I, I, I, P, I, P],
     "mxk_qmm2_set_rot": [I],
     "mxk_qmm3": [I, I, I, P, I, P, I, I, I, I, P, I, P],

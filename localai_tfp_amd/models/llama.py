@@ -638,6 +638,11 @@ class LlamaModel:
                    and cfg.rope_dim == D and D in (64, 128) and fb.stop_layer is None and ws.q.dtype == torch.bfloat16
                    and -(-T // 32) * -(-(qd + 2 * kvd) // 32) <= ws.norm_tick.numel()
                    and self._rope_fuse_on(T))
+        # the step's RoPE table for the epilogue: (cos, sin) x attn_factor per row position, shared by every layer
+        rot_tab = None
+        if nf_rope:
+            ang = fb.positions[:T].float()[:, None] * self.inv_freq[None, :].float()
+            rot_tab = torch.stack((torch.cos(ang), torch.sin(ang)), -1).mul_(self.attn_factor).contiguous()
         for li, L in enumerate(self.layers):
             if fb.stop_layer is not None and li >= fb.stop_layer:
                 break
@@ -674,7 +679,7 @@ class LlamaModel:
                           and L.q_norm is None and lo_qkv is None)
             # M > 4: RoPE + KV append in the q|k|v GEMM epilogue (qmm2 mode bit 4) instead of a rope_kv launch
             rope_ep = (nf_rope and off == 0 and L.q_norm is None and lo_qkv is None and kc.dtype == torch.bfloat16
-                       and vc.dtype == torch.bfloat16)
+                       and vc.dtype == torch.bfloat16 and L.rope is None)
             if rope_fused:
                 # every part is checked before any launches: parts may mix block formats
                 o2 = 0
@@ -699,8 +704,7 @@ class LlamaModel:
                 elif rope_ep:
                     qmatmul(w, xb, EPI_F32, sl, out_zeroed=True, fuse=NormFuse(
                         4 | (2 if nf_qkv is not None else 0), ss_in=ws.norm_ss[1], eps=eps, tick=ws.norm_tick,
-                        rope=(fb.positions, fb.slots, inv_freq, L.bqkv, q, kc, vc, attn_factor, off, D, Hq, Hkv,
-                              kv.block_size)))
+                        rope=(fb.slots, rot_tab, L.bqkv, q, kc, vc, off, D, Hq, Hkv, kv.block_size)))
                 else:
                     qmatmul(w, xb, EPI_F32, sl, out_zeroed=True, fuse=nf_qkv)
                 off += w.N

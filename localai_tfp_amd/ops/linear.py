@@ -344,12 +344,12 @@ def run_plan(plan: tuple, W: QWeight, x: torch.Tensor, epi: int, out: torch.Tens
                 splits, out.data_ptr(), out.stride(0), N.stream_ptr())
     elif kind == "q2" and fuse is not None and fuse.mode & 4:
         f = fuse
-        pos, slots, inv_freq, bias, qo, kc, vc, af, n_off, D, hq, hkv, bsz = f.rope
+        slots, rot, bias, qo, kc, vc, n_off, D, hq, hkv, bsz = f.rope
         N.kcall("mxk_qmm2_rope", int(W.qtype), e, plan[1], plan[2], plan[3], x.data_ptr(), x.stride(0),
                 W.data.data_ptr(), M, W.N, W.K, splits, out.data_ptr(), out.stride(0), f.mode, N.ptr(f.ss_in),
-                1.0 / W.K, f.eps, N.ptr(f.tick), pos.data_ptr(), slots.data_ptr(), inv_freq.data_ptr(), N.ptr(bias),
-                qo.data_ptr(), kc.data_ptr(), vc.data_ptr(), float(af), int(n_off), int(D).bit_length() - 1, int(hq),
-                int(hkv), int(bsz), N.stream_ptr())
+                1.0 / W.K, f.eps, N.ptr(f.tick), slots.data_ptr(), rot.data_ptr(), N.ptr(bias), qo.data_ptr(),
+                kc.data_ptr(), vc.data_ptr(), int(n_off), int(D).bit_length() - 1, int(hq), int(hkv), int(bsz),
+                N.stream_ptr())
     elif kind == "q2" and fuse is not None:
         f = fuse
         N.kcall("mxk_qmm2_fused", int(W.qtype), e, plan[1], plan[2], plan[3], x.data_ptr(), x.stride(0),
@@ -390,8 +390,9 @@ class NormFuse:
                  eps: float = 0.0, rope: tuple | None = None):
         self.mode, self.ss_out, self.ss_zero, self.gamma, self.xn = mode, ss_out, ss_zero, gamma, xn
         self.tick, self.ss_in, self.eps = tick, ss_in, float(eps)
-        # mode bit 4 (the q|k|v GEMM): RoPE + paged KV append in the epilogue, rope = (positions, slots, inv_freq,
-        # bias or None, q_out bf16 [T, Hq * D], k_cache, v_cache, attn_factor, column offset, D, Hq, Hkv, block_size)
+        # mode bit 4 (the q|k|v GEMM): RoPE + paged KV append in the epilogue, rope = (slots, rot = the step's
+        # [T, D / 2, 2] (cos, sin) x attn_factor table, bias or None, q_out bf16 [T, Hq * D], k_cache, v_cache, column
+        # offset, D, Hq, Hkv, block_size)
         self.rope = rope
 
 
