@@ -55,9 +55,6 @@ DECODE_PART_SMALL_B = int(__import__("os").environ.get("MX_DECODE_PART_SMALL_B",
 # SRC_NORM / SRC_ACT). Every workgroup of the GEMV redoes the row statistics, so the fusion pays only at
 # batch 1 (profiles/r2_qmv_fuse_fuse{0,1}_c{1,4}.json: c1 387 -> 442 tok/s, c4 961 -> 861)
 QMV_FUSE_MAX_M = int(__import__("os").environ.get("MX_QMV_FUSE_MAX_M", "1"))
-# timing-only switch (WRONG outputs): skip the M > 4 path's standalone "norm" / "rope" / "attn" launches to bound
-# what fusing them away could save (profiles/r6_fusion_bound.md)
-_DBG_SKIP = frozenset(__import__("os").environ.get("MX_DBG_SKIP", "").split(","))
 
 
 def vocab_shard(V: int, tp: int) -> int:
@@ -660,7 +657,7 @@ class LlamaModel:
                 xq, xds = ws.q8(T, H)
                 K.rmsnorm(h, L.attn_norm, eps, out_q8=(xq, xds))
             else:
-                if nf_qkv is None and "norm" not in _DBG_SKIP:
+                if nf_qkv is None:
                     K.rmsnorm(h, L.attn_norm, eps, out_bf16=xb)
                 xq = xds = None
             if not gemv and not qkv.is_cuda:
@@ -712,12 +709,12 @@ class LlamaModel:
                 if gemv:
                     K.rmsnorm(h, L.attn_norm, eps, out_bf16=xb)
                 LR.add_qkv(lo_qkv, xb, qkv)
-            if not rope_fused and not rope_ep and ("rope" not in _DBG_SKIP or gemv):
+            if not rope_fused and not rope_ep:
                 K.rope_kv(qkv, L.bqkv, fb.positions, fb.slots, inv_freq, attn_factor, Hq, Hkv, D,
                           cfg.rope_dim, cfg.neox, q.view(T, Hq, D), kc, vc, kv.block_size,
                           qk_norm=(L.q_norm, L.k_norm, eps) if L.q_norm is not None else None, zero_after=True)
             attn = ws.attn[:T]
-            if nd and ("attn" not in _DBG_SKIP or gemv):
+            if nd:
                 K.attn_decode(q[:nd].view(nd, Hq, D), kc, vc, fb.dec_block_tables, fb.dec_seq_lens, self.scale,
                               attn[:nd].view(nd, Hq, D), max_seq_len=fb.dec_max_len or None,
                               workspace=(ws.part_ml, ws.part_o, ws.part_cnt), window=L.window, softcap=cfg.attn_softcap,
@@ -770,7 +767,7 @@ class LlamaModel:
             elif gemv:
                 xq, xds = ws.q8(T, H)
                 K.rmsnorm(h, L.ffn_norm, eps, out_q8=(xq, xds))
-            elif not nf and "norm" not in _DBG_SKIP:
+            elif not nf:
                 K.rmsnorm(h, L.ffn_norm, eps, out_bf16=xb)
             if L.wgu is not None:
                 if fuse_gu:
