@@ -437,16 +437,9 @@ def _qmatmul_t32(W: QWeight, x, epi: int, out, xq, xds, M: int, out_zeroed: bool
         return out
     if x is None or x.dtype != torch.float16:
         raise ValueError("qmatmul: t32 weights need f16 activations (or q8 activations with M <= 4)")
-    can_split = epi == EPI_ADD_F32 or (epi == EPI_F32 and out_zeroed)
-    if W.bf16_cache is not None and M >= dense_min_m(x.dtype, epi, can_split) and W.bf16_cache.dtype == x.dtype:
-        return _dense_cached(W, x, epi, out, M)
-    forced = QMM2 or QMM3 or QMM2_FORCE is not None or QMM3_FORCE is not None
-    plan = _AT.lookup(W.N, W.K, int(W.qtype), epi, can_split, M) if (_AT.TUNED and not forced) else None
+    plan = _t32_plan(W, M, epi, out_zeroed, x.dtype)
     if plan is None:
-        if len(row_chunks(M)) > 1:
-            plan = ("rows", ROW_CHUNK)
-        else:
-            plan = _gemm_pick(M, W.N, W.K, int(W.qtype), can_split)
+        return _dense_cached(W, x, epi, out, M)
     return run_plan(plan, W, x, epi, out, out_zeroed)
 
 
