@@ -72,6 +72,8 @@ def add_run_args(ap: argparse.ArgumentParser):
     ap.add_argument("--disable-metrics-endpoint", action="store_true", default=None)
     ap.add_argument("--p2p", action="store_true", default=None)
     ap.add_argument("--p2ptoken")
+    ap.add_argument("--p2p-dht-interval", type=int)
+    ap.add_argument("--p2p-otp-interval", type=int)
     ap.add_argument("--parallel-requests", action="store_true", default=None)
     ap.add_argument("--single-active-backend", action="store_true", default=None)
     ap.add_argument("--preload-backend-only", action="store_true", default=None)
@@ -97,6 +99,7 @@ def app_config_from_args(a):
               "localai_config_dir": "config_dir", "config_file": "config_file", "threads": "threads",
               "context_size": "context_size", "cors_allow_origins": "cors_allow_origins",
               "upload_limit": "upload_limit_mb", "machine_tag": "machine_tag", "p2ptoken": "p2p_token",
+              "p2p_dht_interval": "p2p_dht_interval", "p2p_otp_interval": "p2p_otp_interval",
               "gpus": "gpus"}
     for src, dst in simple.items():
         v = getattr(a, src, None)

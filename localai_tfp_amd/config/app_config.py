@@ -64,6 +64,9 @@ class ApplicationConfig:
     p2p: bool = field(default_factory=lambda: _env(["LOCALAI_P2P", "P2P"], False, bool))
     p2p_token: str = field(default_factory=lambda: _env(["LOCALAI_P2P_TOKEN", "P2P_TOKEN", "TOKEN"], ""))
     p2p_network_id: str = field(default_factory=lambda: _env(["LOCALAI_P2P_NETWORK_ID", "P2P_NETWORK_ID"], ""))
+    # intervals written into a generated token (core/cli/run.go:57-58)
+    p2p_dht_interval: int = field(default_factory=lambda: _env(["LOCALAI_P2P_DHT_INTERVAL", "P2P_DHT_INTERVAL"], 360, int))
+    p2p_otp_interval: int = field(default_factory=lambda: _env(["LOCALAI_P2P_OTP_INTERVAL", "P2P_OTP_INTERVAL"], 9000, int))
     # federator / peer URLs this instance announces itself to (libp2p discovery replacement)
     p2p_peers: list = field(default_factory=lambda: _env(["LOCALAI_P2P_PEERS", "P2P_PEERS"], [], list))
     # LAN discovery beacons (the reference's libp2p mDNS, on by default with p2p); unicast targets for

@@ -69,7 +69,7 @@ class Application:
         if c.p2p:
             from .. import p2p as P
             if not c.p2p_token:
-                c.p2p_token = P.generate_token()
+                c.p2p_token = P.generate_token(c.p2p_dht_interval, c.p2p_otp_interval)
                 log.info("p2p enabled without a token; generated network token: %s", c.p2p_token)
             me = P.self_node(c.address, P.FEDERATED_ID if c.federated else P.WORKER_ID)
             self.p2p = P.P2PNode(c.p2p_token, c.p2p_network_id, list(c.p2p_peers), me,

@@ -23,7 +23,7 @@ import struct
 import threading
 import time
 
-from . import NodeData, Registry
+from . import NodeData, Registry, token_secret
 
 log = logging.getLogger("localai_tfp_amd.p2p.discovery")
 
@@ -32,7 +32,7 @@ VERSION = 1
 
 
 def _mac(token: str, payload: bytes) -> str:
-    return hmac.new(token.encode(), payload, hashlib.sha256).hexdigest()
+    return hmac.new(token_secret(token).encode(), payload, hashlib.sha256).hexdigest()
 
 
 def encode_beacon(node: NodeData, token: str, network: str, now: float | None = None) -> bytes:

@@ -138,3 +138,57 @@ def test_explorer_db_discovery_and_routes(tmp_path):
     finally:
         loop.call_soon_threadsafe(srv.close)
         backend.shutdown()
+
+
+def test_token_has_the_reference_edgevpn_shape():
+    """generate_token mirrors core/p2p/p2p.go:33-66: base64 of the edgevpn connection YAML with 43-letter names and
+    OTP keys, DHT / crypto intervals (defaults 360 / 9000, overridable like --p2p-dht-interval / --p2p-otp-interval)
+    and the 20 MB message cap."""
+    import base64
+    import re
+
+    import yaml
+    cfg = yaml.safe_load(base64.b64decode(P.generate_token()))
+    assert cfg["max_message_size"] == 20 << 20
+    for k in ("room", "rendezvous", "mdns"):
+        assert re.fullmatch(r"[A-Za-z]{43}", cfg[k])
+    assert cfg["otp"]["dht"]["interval"] == 360 and cfg["otp"]["crypto"]["interval"] == 9000
+    for o in ("dht", "crypto"):
+        assert re.fullmatch(r"[A-Za-z]{43}", cfg["otp"][o]["key"]) and cfg["otp"][o]["length"] == 43
+    c2 = P.parse_token(P.generate_token(100, 200))
+    assert c2["otp"]["dht"]["interval"] == 100 and c2["otp"]["crypto"]["interval"] == 200
+    assert P.generate_token() != P.generate_token()
+
+
+def test_reference_token_parses_and_keys_the_network():
+    """A token written the way the reference writes one (Go yaml of node.YAMLConnectionConfig, standard base64) is
+    accepted: its crypto OTP key + room are the network secret, so two nodes holding it authenticate each other's
+    beacons and a node with another token does not. Opaque tokens keep working as their own secret."""
+    import base64
+
+    from localai_tfp_amd.p2p import discovery as D
+    go_yaml = ("otp:\n  dht:\n    interval: 360\n    key: " + "A" * 43 + "\n    length: 43\n"
+               "  crypto:\n    interval: 9000\n    key: " + "B" * 43 + "\n    length: 43\n"
+               "room: " + "C" * 43 + "\nrendezvous: " + "D" * 43 + "\nmdns: " + "E" * 43 + "\n"
+               "max_message_size: 20971520\n")
+    tok = base64.b64encode(go_yaml.encode()).decode()
+    cfg = P.parse_token(tok)
+    assert cfg is not None and cfg["room"] == "C" * 43
+    assert P.token_secret(tok) == "B" * 43 + ":" + "C" * 43
+    assert P.parse_token("tok") is None and P.token_secret("tok") == "tok"
+    assert P.parse_token(base64.b64encode(b"just: text").decode()) is None
+    node = P.NodeData(id="n1", address="127.0.0.1:9", service="worker")
+    beacon = D.encode_beacon(node, tok, "net")
+    assert D.decode_beacon(beacon, tok, "net").id == "n1"
+    assert D.decode_beacon(beacon, P.generate_token(), "net") is None
+
+
+def test_cli_p2p_intervals_reach_the_config():
+    import argparse
+
+    from localai_tfp_amd.cli import add_run_args, app_config_from_args
+    ap = argparse.ArgumentParser()
+    add_run_args(ap)
+    a = ap.parse_args(["--p2p-dht-interval", "120", "--p2p-otp-interval", "600"])
+    c = app_config_from_args(a)
+    assert c.p2p_dht_interval == 120 and c.p2p_otp_interval == 600
